@@ -1,0 +1,147 @@
+#!/usr/bin/env python3
+"""Headline benchmark: sparse-LR training throughput on the MI355X parameter server.
+
+Metric (BASELINE.json): training samples/sec for the whole node, 1B-feature
+sparse logistic regression, at 1/2/4/8 MI355X.
+
+Each rank is a colocated worker + server shard (one process per GPU):
+  * its table shard holds 1/N of the 1B-feature space (AdaGrad, 16-byte slots);
+  * its worker trains on its own synthetic CTR stream (B samples x 39 fields
+    per step, generated on-device inside the timed step);
+  * pull/push rounds route keys over RCCL alltoallv (xGMI) for N > 1.
+
+Weak scaling: the per-GPU batch is fixed, the global batch is N*B.
+
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B]
+        (N > 1 via: python -m torch.distributed.run --nproc-per-node N
+         --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+METRIC = "training samples/sec (whole node), 1B-feature sparse LR at 1/2/4/8 MI355X"
+BASELINE_SAMPLES_PER_SEC = None  # reference publishes no number
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=65536, help="samples per GPU per step")
+    ap.add_argument("--fields", type=int, default=39)
+    ap.add_argument("--features", type=int, default=1_000_000_000)
+    ap.add_argument("--load", type=float, default=0.7, help="table load factor at full feature space")
+    ap.add_argument("--tail", type=float, default=0.1)
+    ap.add_argument("--optimizer", default="adagrad")
+    ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--verbose", action="store_true")
+    a = ap.parse_args(argv)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        if world == 1 and a.gpus > 1:
+            print("bench.py: --gpus > 1 must be launched with torch.distributed.run", file=sys.stderr)
+            return 2
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.parallel.transport import LoopbackTransport, RcclTransport
+
+    if world > 1:
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        store = dist.distributed_c10d._get_default_store()
+        transport = RcclTransport(rank, world, dev, store=store)
+    else:
+        transport = LoopbackTransport()
+
+    data = CtrSynth(batch_size=a.batch, num_fields=a.fields, num_features=a.features,
+                    tail_frac=a.tail)
+    opt = Optimizer(a.optimizer, lr=a.lr)
+    table = make_lr_table(a.features, world, optimizer=opt, load=a.load, device=dev)
+    engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev)
+    worker = SparseLRWorker(engine, data, rank=rank, world=world)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        worker.step()
+    torch.cuda.synchronize()
+    table.check()
+    first_loss = worker.mean_loss()
+
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        worker.step()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    table.check()
+    last_loss = worker.mean_loss()
+    keys_in_table = torch.tensor([table.size()], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(keys_in_table)
+
+    samples = a.batch * world * a.steps
+    value = samples / elapsed
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(1000.0 * elapsed / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / BASELINE_SAMPLES_PER_SEC, 2)
+                            if BASELINE_SAMPLES_PER_SEC else None),
+            "dtype": "fp32",
+            "data": "synthetic (on-device CTR generator, 39 fields, Zipf ids over 1B features)",
+            "config": {
+                "model": f"sparse_lr_{a.features // 1_000_000}M_features",
+                "global_batch": a.batch * world,
+                "seq_len": a.fields,
+                "parallelism": f"ps{world} (colocated worker+server shard per GPU, RCCL alltoallv)",
+                "optimizer": a.optimizer,
+                "keys_per_step_per_gpu": a.batch * a.fields,
+                "table_keys": int(keys_in_table.item()),
+                "loss_first": round(first_loss, 5),
+                "loss_last": round(last_loss, 5),
+            },
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

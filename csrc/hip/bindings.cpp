@@ -1,0 +1,183 @@
+// bindings.cpp — pybind11 module `_ss_hip`: the gfx950 kernels and the RCCL
+// communicator.  Pointers and streams cross the boundary as integers
+// (torch.Tensor.data_ptr(), torch.cuda.Stream.cuda_stream) so the module does
+// not compile against torch headers and loads next to whatever torch build is
+// present; memory is owned by torch's caching allocator on the Python side.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "comm.h"
+#include "ss_launch.h"
+
+namespace py = pybind11;
+using namespace ss;
+
+static hipStream_t S(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+template <class T>
+static T* P(uintptr_t p) {
+  return reinterpret_cast<T*>(p);
+}
+
+static SegList make_seglist(const std::vector<long long>& offs, const std::vector<long long>& cnts) {
+  if (offs.size() != cnts.size() || offs.empty() || offs.size() > (size_t)kMaxSeg)
+    throw std::runtime_error("SegList: need 1..64 (offset, count) pairs");
+  SegList sl{};
+  sl.nseg = (int)offs.size();
+  sl.dev_count = nullptr;
+  sl.prefix[0] = 0;
+  for (int i = 0; i < sl.nseg; ++i) {
+    if (cnts[i] < 0) throw std::runtime_error("SegList: negative count");
+    sl.off[i] = offs[i];
+    sl.prefix[i + 1] = sl.prefix[i] + cnts[i];
+  }
+  return sl;
+}
+
+static SegList make_seglist_dev(uintptr_t dev_count) {
+  SegList sl{};
+  sl.nseg = 1;
+  sl.dev_count = P<const long long>(dev_count);
+  sl.off[0] = 0;
+  sl.prefix[0] = 0;
+  sl.prefix[1] = 0;
+  return sl;
+}
+
+static long long seglist_total(const SegList& s) { return s.dev_count ? -1 : s.prefix[s.nseg]; }
+
+PYBIND11_MODULE(_ss_hip, m) {
+  m.doc() = "SwiftSnails-AMD gfx950 kernels + RCCL communicator";
+
+  py::class_<DevTable>(m, "DevTable")
+      .def(py::init([](uintptr_t base, unsigned long long cap, uint32_t stride, uint32_t key_off,
+                       uint32_t dim, uint32_t width) {
+             return DevTable{P<char>(base), cap, stride, key_off, dim, width};
+           }),
+           py::arg("base"), py::arg("cap"), py::arg("stride"), py::arg("key_off"), py::arg("dim"),
+           py::arg("width"))
+      .def_readonly("cap", &DevTable::cap)
+      .def_readonly("stride", &DevTable::stride)
+      .def_readonly("key_off", &DevTable::key_off)
+      .def_readonly("dim", &DevTable::dim)
+      .def_readonly("width", &DevTable::width);
+
+  py::class_<InitParams>(m, "InitParams")
+      .def(py::init([](int kind, float scale, float state_init, uint64_t seed) {
+             return InitParams{kind, scale, state_init, seed};
+           }),
+           py::arg("kind") = 0, py::arg("scale") = 0.f, py::arg("state_init") = 0.f,
+           py::arg("seed") = 0);
+
+  py::class_<OptParams>(m, "OptParams")
+      .def(py::init([](int kind, float lr, float l1, float l2, float eps, float beta1, float beta2,
+                       float bc1, float bc2, float alpha, float beta, float grad_scale,
+                       float clip) {
+             return OptParams{kind, lr, l1, l2, eps, beta1, beta2, bc1, bc2, alpha, beta,
+                              grad_scale, clip};
+           }),
+           py::arg("kind") = 1, py::arg("lr") = 0.05f, py::arg("l1") = 0.f, py::arg("l2") = 0.f,
+           py::arg("eps") = 1e-8f, py::arg("beta1") = 0.9f, py::arg("beta2") = 0.999f,
+           py::arg("bc1") = 1.f, py::arg("bc2") = 1.f, py::arg("alpha") = 0.05f,
+           py::arg("beta") = 1.f, py::arg("grad_scale") = 1.f, py::arg("clip") = 0.f);
+
+  py::class_<SegList>(m, "SegList")
+      .def_static("from_host", &make_seglist)
+      .def_static("from_device", &make_seglist_dev)
+      .def_property_readonly("total", &seglist_total)
+      .def_readonly("nseg", &SegList::nseg);
+
+  m.def("opt_state_width", &opt_state_width);
+
+  // ---- table (K3/K4/K5/K8)
+  m.def("probe", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
+                    uintptr_t slots, const InitParams& ip, int insert, uintptr_t size_ctr,
+                    uintptr_t err, int G, uintptr_t st) {
+    launch_probe(t, P<const uint64_t>(keys), sl, max_n, P<long long>(slots), ip, insert,
+                 P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
+  });
+  m.def("gather", [](const DevTable& t, uintptr_t slots, const SegList& sl, long long max_n,
+                     uintptr_t out, int G, uintptr_t st) {
+    launch_gather(t, P<const long long>(slots), sl, max_n, P<float>(out), G, S(st));
+  });
+  m.def("pull_unique", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
+                          uintptr_t slots, uintptr_t out, const InitParams& ip, uintptr_t size_ctr,
+                          uintptr_t err, int G, uintptr_t st) {
+    launch_pull_unique(t, P<const uint64_t>(keys), sl, max_n, P<long long>(slots), P<float>(out),
+                       ip, P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
+  });
+  m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
+                    long long max_n, const OptParams& op, int G, uintptr_t st) {
+    launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st));
+  });
+  m.def("assign", [](const DevTable& t, uintptr_t keys, uintptr_t rows, long long n,
+                     uintptr_t size_ctr, uintptr_t err, int G, uintptr_t st) {
+    launch_assign(t, P<const uint64_t>(keys), P<const float>(rows), n,
+                  P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
+  });
+  m.def("export_slots", [](const DevTable& t, unsigned long long s0, long long n, uintptr_t keys,
+                           uintptr_t rows, uintptr_t cursor, uintptr_t st) {
+    launch_export(t, s0, n, P<uint64_t>(keys), P<float>(rows), P<unsigned long long>(cursor),
+                  S(st));
+  });
+
+  // ---- dedup / route (K1/K2/K6/K7)
+  m.def("dedup_route", [](uintptr_t keys, long long n, uintptr_t skeys, uintptr_t suid,
+                          unsigned long long scap, uintptr_t slot_of, uintptr_t frag_map,
+                          int frag_num, int nranks, long long ucap, uintptr_t ucount,
+                          uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t st) {
+    RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
+    launch_dedup_route(P<const uint64_t>(keys), n, P<uint64_t>(skeys), P<uint32_t>(suid), scap,
+                       P<uint32_t>(slot_of), rs, ucap, P<unsigned long long>(ucount),
+                       P<uint64_t>(ukeys), P<float>(ugrad), gdim, S(st));
+  });
+  m.def("dedup_inverse", [](uintptr_t slot_of, uintptr_t suid, long long n, uintptr_t inv,
+                            uintptr_t st) {
+    launch_dedup_inverse(P<const uint32_t>(slot_of), P<const uint32_t>(suid), n, P<uint32_t>(inv),
+                         S(st));
+  });
+  m.def("route_keys", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num,
+                         int nranks, uintptr_t dest, uintptr_t st) {
+    RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
+    launch_route_keys(P<const uint64_t>(keys), n, rs, P<int>(dest), S(st));
+  });
+  m.def("gather_rows", [](uintptr_t src, uintptr_t idx, long long n, int dim, uintptr_t out,
+                          uintptr_t st) {
+    launch_gather_rows(P<const float>(src), P<const uint32_t>(idx), n, dim, P<float>(out), S(st));
+  });
+  m.def("scatter_add_rows", [](uintptr_t src, uintptr_t idx, long long n, int dim, uintptr_t out,
+                               uintptr_t st) {
+    launch_scatter_add_rows(P<const float>(src), P<const uint32_t>(idx), n, dim, P<float>(out),
+                            S(st));
+  });
+
+  // ---- models
+  m.def("gen_ctr", [](uint64_t seed, long long sample_base, int B, int F, long long V,
+                      float tail_frac, float truth_scale, float truth_bias, uintptr_t keys,
+                      uintptr_t labels, uintptr_t st) {
+    launch_gen_ctr(seed, sample_base, B, F, V, tail_frac, truth_scale, truth_bias,
+                   P<uint64_t>(keys), P<float>(labels), S(st));
+  });
+  m.def("lr_fwd_bwd", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
+                         uintptr_t uvals, uintptr_t ugrad, uintptr_t loss_sum, uintptr_t pred,
+                         uintptr_t st) {
+    launch_lr_fwd_bwd(P<const uint32_t>(inv), P<const float>(xval), P<const float>(labels), B, F,
+                      P<const float>(uvals), P<float>(ugrad), P<float>(loss_sum), P<float>(pred),
+                      S(st));
+  });
+
+  // ---- RCCL
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](int rank, int nranks, py::bytes uid, int device) {
+             return new RcclComm(rank, nranks, std::string(uid), device);
+           }),
+           py::arg("rank"), py::arg("nranks"), py::arg("uid"), py::arg("device"))
+      .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("nranks", &RcclComm::nranks)
+      .def("alltoallv", &RcclComm::alltoallv, py::call_guard<py::gil_scoped_release>())
+      .def("alltoall", &RcclComm::alltoall, py::call_guard<py::gil_scoped_release>())
+      .def("allreduce", &RcclComm::allreduce, py::call_guard<py::gil_scoped_release>())
+      .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())
+      .def("allgather", &RcclComm::allgather, py::call_guard<py::gil_scoped_release>())
+      .def("abort", &RcclComm::abort);
+}

@@ -1,0 +1,144 @@
+// models.hip — fused model kernels for the sparse-LR workload (gfx950).
+//
+// The reference ships no application code (its scripts name the absent
+// src/apps/logistic_regression, /root/reference/src/tools/hadoop-server.sh:7);
+// its `train()` hot loop would be a per-sample sparse dot + sigmoid + grad
+// scatter over the pulled GlobalParamCache (global_param_cache.h:28-118,
+// Vec math in utils/vec1.h:97-104).  Here that loop is one kernel:
+//
+//   K6+K7  gather w through the dedup inverse index, per-sample dot (LDS
+//          segmented sum), sigmoid + logloss, and scatter the per-key
+//          gradient (p - y) * x into the unique-key gradient rows that the
+//          push round ships to the servers.
+//
+// Synthetic CTR data is generated on device each step (counter-based RNG), so
+// the timed step includes producing its input batch.
+#include "ss_device.h"
+#include "ss_launch.h"
+
+namespace ss {
+
+static constexpr uint32_t kInvalidU = 0xFFFFFFFFu;
+
+// Samples handled by one 256-thread block when a sample has F features.
+__host__ __device__ inline int samples_per_block(int F) { return F >= 256 ? 1 : 256 / F; }
+
+// Per-key ground-truth weight of the synthetic generator (labels are drawn
+// from a true sparse-LR model so convergence is measurable).
+__device__ __forceinline__ float truth_weight(uint64_t key, float scale) {
+  return (u01(splitmix64(key ^ 0x5DEECE66Dull)) - 0.5f) * scale;
+}
+
+// Keys: field f owns [f*V, (f+1)*V); ids are log-uniform (Zipf-like head, as
+// in CTR data) with a `tail_frac` share drawn uniformly over the field (long
+// tail that keeps inserting new keys into the table).
+__global__ __launch_bounds__(256) void k_gen_ctr(uint64_t seed, long long sample_base, int B,
+                                                 int F, long long V, double logV, float tail_frac,
+                                                 float truth_scale, float truth_bias,
+                                                 uint64_t* __restrict__ keys,
+                                                 float* __restrict__ labels) {
+  __shared__ float sdot[256];
+  const int spb = samples_per_block(F);
+  const int t = threadIdx.x;
+  const int ls = t / F, f = t - (t / F) * F;
+  const long long s0 = (long long)blockIdx.x * spb;
+  if (t < spb) sdot[t] = 0.f;
+  __syncthreads();
+  if (ls < spb && s0 + ls < B && F <= 256) {
+    const long long s = s0 + ls;
+    const uint64_t gs = (uint64_t)(sample_base + s);
+    const uint64_t r = splitmix64(seed ^ (gs * 0xA24BAED4963EE407ull) ^ ((uint64_t)f << 40));
+    const uint64_t r2 = splitmix64(r);
+    uint64_t id;
+    if (u01(r2) < tail_frac) {
+      id = fastrange64(splitmix64(r2 ^ 0x632BE59BD9B4E019ull), (uint64_t)V);
+    } else {
+      const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+      long long v = (long long)exp(u * logV) - 1;
+      id = (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
+    }
+    const uint64_t key = (uint64_t)f * (uint64_t)V + id;
+    keys[s * F + f] = key;
+    atomicAdd(&sdot[ls], truth_weight(key, truth_scale));
+  }
+  __syncthreads();
+  if (t < spb && s0 + t < B) {
+    const float z = sdot[t] + truth_bias;
+    const float p = 1.f / (1.f + __expf(-z));
+    const uint64_t gs = (uint64_t)(sample_base + s0 + t);
+    labels[s0 + t] = u01(splitmix64(seed ^ 0xBEEF ^ (gs * 0x9E3779B97F4A7C15ull))) < p ? 1.f : 0.f;
+  }
+}
+
+// Fused LR forward/backward over B samples x F features (CTR-style fixed
+// field count).  inv[j] indexes the pulled unique-key value/gradient rows.
+__global__ __launch_bounds__(256) void k_lr_fwd_bwd(const uint32_t* __restrict__ inv,
+                                                    const float* __restrict__ xval,
+                                                    const float* __restrict__ labels, int B, int F,
+                                                    const float* __restrict__ uvals,
+                                                    float* __restrict__ ugrad,
+                                                    float* __restrict__ loss_sum,
+                                                    float* __restrict__ pred) {
+  __shared__ float sdot[256];
+  __shared__ float sg[256];
+  __shared__ float sloss[4];
+  const int spb = samples_per_block(F);
+  const int t = threadIdx.x;
+  const int ls = t / F;
+  const long long s0 = (long long)blockIdx.x * spb;
+  if (t < spb) sdot[t] = 0.f;
+  __syncthreads();
+  const bool active = ls < spb && s0 + ls < B;
+  const long long j = s0 * F + t;
+  uint32_t u = kInvalidU;
+  float x = 0.f;
+  if (active) {
+    u = inv[j];
+    x = xval ? xval[j] : 1.f;
+    if (u != kInvalidU) atomicAdd(&sdot[ls], uvals[u] * x);
+  }
+  __syncthreads();
+  float l = 0.f;
+  if (t < spb && s0 + t < B) {
+    const float z = sdot[t];
+    const float y = labels[s0 + t];
+    const float p = 1.f / (1.f + __expf(-z));
+    sg[t] = p - y;
+    if (pred) pred[s0 + t] = p;
+    // numerically stable logloss: softplus(z) - y*z
+    l = fmaxf(z, 0.f) + __logf(1.f + __expf(-fabsf(z))) - y * z;
+  }
+  // block loss reduce (wave shuffle + LDS)
+  for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, 64);
+  if ((t & 63) == 0) sloss[t >> 6] = l;
+  __syncthreads();
+  if (t == 0 && loss_sum) atomicAdd(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
+  if (active && u != kInvalidU) atomicAdd(ugrad + u, sg[ls] * x);
+}
+
+void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long long vocab_per_field,
+                    float tail_frac, float truth_scale, float truth_bias, uint64_t* keys,
+                    float* labels, hipStream_t st) {
+  if (B <= 0) return;
+  if (F < 1 || F > 256) throw_error("gen_ctr: F must be in [1,256]");
+  const int spb = samples_per_block(F);
+  const int blocks = (B + spb - 1) / spb;
+  hipLaunchKernelGGL(k_gen_ctr, dim3(blocks), dim3(256), 0, st, seed, sample_base, B, F,
+                     vocab_per_field, log((double)vocab_per_field + 1.0), tail_frac, truth_scale,
+                     truth_bias, keys, labels);
+  check_launch("k_gen_ctr");
+}
+
+void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
+                       const float* uvals, float* ugrad, float* loss_sum, float* pred,
+                       hipStream_t st) {
+  if (B <= 0) return;
+  if (F < 1 || F > 256) throw_error("lr_fwd_bwd: F must be in [1,256]");
+  const int spb = samples_per_block(F);
+  const int blocks = (B + spb - 1) / spb;
+  hipLaunchKernelGGL(k_lr_fwd_bwd, dim3(blocks), dim3(256), 0, st, inv, xval, labels, B, F, uvals,
+                     ugrad, loss_sum, pred);
+  check_launch("k_lr_fwd_bwd");
+}
+
+}  // namespace ss

@@ -1,0 +1,65 @@
+// ss_launch.h — host-side launch helpers and the launcher declarations that the
+// pybind11 module (bindings.cpp) calls.  Kernels never allocate or synchronise:
+// every launcher only enqueues on the caller's stream (hipGraph-capturable).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include "ss_device.h"
+
+namespace ss {
+
+[[noreturn]] inline void throw_error(const std::string& msg) { throw std::runtime_error(msg); }
+
+inline void check_hip(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+inline void check_launch(const char* what) { check_hip(hipGetLastError(), what); }
+
+// --- table.hip
+void launch_probe(const DevTable& t, const uint64_t* keys, const SegList& sl, long long max_n,
+                  long long* slots, const InitParams& ip, int insert,
+                  unsigned long long* size_ctr, int* err, int G, hipStream_t st);
+void launch_gather(const DevTable& t, const long long* slots, const SegList& sl, long long max_n,
+                   float* out, int G, hipStream_t st);
+void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& sl,
+                        long long max_n, long long* slots, float* out, const InitParams& ip,
+                        unsigned long long* size_ctr, int* err, int G, hipStream_t st);
+void launch_apply(const DevTable& t, const long long* slots, const float* grads,
+                  const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st);
+void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, long long n,
+                   unsigned long long* size_ctr, int* err, int G, hipStream_t st);
+void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,
+                   float* rows_out, unsigned long long* cursor, hipStream_t st);
+
+// --- dedup.hip
+struct RouteSpec {
+  const int* frag_map;  // frag -> destination rank (device)
+  int frag_num;
+  int nranks;
+};
+void launch_dedup_route(const uint64_t* keys, long long n, uint64_t* scratch_keys,
+                        uint32_t* scratch_uid, unsigned long long scratch_cap,
+                        uint32_t* slot_of, RouteSpec rs, long long ucap,
+                        unsigned long long* ucount, uint64_t* ukeys, float* ugrad, int gdim,
+                        hipStream_t st);
+void launch_dedup_inverse(const uint32_t* slot_of, const uint32_t* scratch_uid, long long n,
+                          uint32_t* inv, hipStream_t st);
+void launch_route_keys(const uint64_t* keys, long long n, RouteSpec rs, int* dest,
+                       hipStream_t st);
+void launch_gather_rows(const float* src, const uint32_t* idx, long long n, int dim, float* out,
+                        hipStream_t st);
+void launch_scatter_add_rows(const float* src, const uint32_t* idx, long long n, int dim,
+                             float* out, hipStream_t st);
+
+// --- models.hip
+void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long long vocab_per_field,
+                    float tail_frac, float truth_scale, float truth_bias, uint64_t* keys,
+                    float* labels, hipStream_t st);
+void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
+                       const float* uvals, float* ugrad, float* loss_sum, float* pred,
+                       hipStream_t st);
+
+}  // namespace ss

@@ -1,0 +1,320 @@
+// table.hip — HBM open-addressed parameter table kernels (gfx950).
+//
+// Replaces, per SURVEY §2.9.1:
+//   K3  server lookup-or-init  (PullAccessAgent::get_pull_value,
+//       /root/reference/src/core/parameter/sparsetable.h:142-149)
+//   K4  row gather for the pull response (server/init.h:61-68)
+//   K5  server push apply      (PushAccessAgent::apply_push_value,
+//       sparsetable.h:181-192; server/init.h:119-125)
+//   K8  occupied-slot compaction for the text/binary dump
+//       (SparseTableShard operator<<, sparsetable.h:49-56)
+//
+// Work decomposition: a *group* of G lanes (G in {1,4,16,64}) owns one key.
+// The group leader walks the probe sequence (one 8-byte key load per step,
+// the row sits in the same slot so the following gather is a sequential read
+// of the same/adjacent lines); the slot is broadcast with a width-G shuffle
+// and the G lanes sweep the row.  G=1 for sparse-LR rows (width 2 = 8 B),
+// G=16/64 for embedding rows (word2vec / FM), so a 64-wide wavefront always
+// has all lanes busy on HBM traffic.
+#include "ss_device.h"
+#include "ss_launch.h"
+
+namespace ss {
+
+__device__ __forceinline__ long long probe_slot(const DevTable& t, uint64_t key, bool insert,
+                                                bool* inserted) {
+  uint64_t s = fastrange64(table_hash(key), t.cap);
+  for (uint64_t n = 0; n < t.cap; ++n) {
+    uint64_t* kp = slot_key(t, s);
+    // A slot's key only ever changes EMPTY -> key inside a launch, so a stale
+    // plain load can only read EMPTY; the CAS below then returns the truth.
+    uint64_t k = *kp;
+    if (k == key) return (long long)s;
+    if (k == kEmptyKey) {
+      if (!insert) return -1;
+      unsigned long long prev =
+          atomicCAS(reinterpret_cast<unsigned long long*>(kp), kEmptyKey, key);
+      if (prev == kEmptyKey) {
+        *inserted = true;
+        return (long long)s;
+      }
+      if (prev == key) return (long long)s;
+    }
+    s = (s + 1 == t.cap) ? 0 : s + 1;
+  }
+  return -1;
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_down(v, o, 64);
+  return v;
+}
+
+template <int G>
+__device__ __forceinline__ void init_row(const DevTable& t, const InitParams& ip, float* row,
+                                         uint64_t key, int lg) {
+  for (uint32_t j = lg; j < t.width; j += G)
+    row[j] = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
+}
+
+// K3: lookup-or-init (insert=1) or lookup-only (insert=0). slots_out[pos] = slot | -1.
+template <int G>
+__global__ __launch_bounds__(256) void k_probe(DevTable t, const uint64_t* __restrict__ keys,
+                                               SegList sl, long long* __restrict__ slots_out,
+                                               InitParams ip, int insert,
+                                               unsigned long long* size_ctr, int* err) {
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x % G;
+  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
+  unsigned long long ins = 0;
+  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
+       g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    const uint64_t key = keys[pos];
+    long long slot = -1;
+    int inserted = 0;
+    if (lg == 0) {
+      bool b = false;
+      if (key != kEmptyKey) slot = probe_slot(t, key, insert != 0, &b);
+      inserted = b;
+      if (slot < 0 && insert) atomicOr(err, key == kEmptyKey ? 2 : 1);
+      slots_out[pos] = slot;
+    }
+    if (G > 1) {
+      slot = __shfl(slot, 0, G);
+      inserted = __shfl(inserted, 0, G);
+    }
+    if (inserted) init_row<G>(t, ip, slot_row(t, slot), key, lg);
+    ins += (lg == 0 && inserted);
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+}
+
+// K4: gather parameter rows (dim floats) for resolved slots; missing -> 0.
+template <int G>
+__global__ __launch_bounds__(256) void k_gather(DevTable t, const long long* __restrict__ slots,
+                                                SegList sl, float* __restrict__ out) {
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x % G;
+  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
+  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
+       g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    const long long slot = slots[pos];
+    float* o = out + pos * (long long)t.dim;
+    if (slot < 0) {
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
+    } else {
+      const float* row = slot_row(t, slot);
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
+    }
+  }
+}
+
+// K3+K4 fused, for key lists known to be unique within the launch (the
+// worker's dedup output on the colocated 1-GPU path): probe, init if new,
+// and emit the row without a second pass.
+template <int G>
+__global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t* __restrict__ keys,
+                                                     SegList sl, long long* __restrict__ slots_out,
+                                                     float* __restrict__ out, InitParams ip,
+                                                     unsigned long long* size_ctr, int* err) {
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x % G;
+  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
+  unsigned long long ins = 0;
+  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
+       g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    const uint64_t key = keys[pos];
+    long long slot = -1;
+    int inserted = 0;
+    if (lg == 0) {
+      bool b = false;
+      if (key != kEmptyKey) slot = probe_slot(t, key, true, &b);
+      inserted = b;
+      if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
+      if (slots_out) slots_out[pos] = slot;
+    }
+    if (G > 1) {
+      slot = __shfl(slot, 0, G);
+      inserted = __shfl(inserted, 0, G);
+    }
+    float* o = out + pos * (long long)t.dim;
+    if (slot < 0) {
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
+    } else {
+      float* row = slot_row(t, slot);
+      if (inserted) {
+        for (uint32_t j = lg; j < t.width; j += G) {
+          const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
+          row[j] = v;
+          if (j < t.dim) o[j] = v;
+        }
+      } else {
+        for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
+      }
+    }
+    ins += (lg == 0 && inserted);
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+}
+
+// K5: fused optimizer update on resolved slots. Keys inside one launch must be
+// unique (the host launches one segment per source rank, in rank order, so
+// duplicate keys from different workers are applied sequentially — no lost
+// updates, deterministic, and no float atomics on the hot path).
+template <int G>
+__global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __restrict__ slots,
+                                               const float* __restrict__ grads, SegList sl,
+                                               OptParams op) {
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x % G;
+  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
+  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
+       g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    const long long slot = slots[pos];
+    if (slot < 0) continue;
+    float* row = slot_row(t, slot);
+    const float* gr = grads + pos * (long long)t.dim;
+    for (uint32_t j = lg; j < t.dim; j += G) opt_apply(op, row, row + t.dim, t.dim, j, gr[j]);
+  }
+}
+
+// Assign full rows (params + state) for keys, inserting when missing
+// (checkpoint load / rehash).  `rows` has `width` floats per key.
+template <int G>
+__global__ __launch_bounds__(256) void k_assign(DevTable t, const uint64_t* __restrict__ keys,
+                                                const float* __restrict__ rows, long long n,
+                                                unsigned long long* size_ctr, int* err) {
+  const int lg = threadIdx.x % G;
+  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
+  unsigned long long ins = 0;
+  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < n;
+       g += ngroups) {
+    const uint64_t key = keys[g];
+    long long slot = -1;
+    int inserted = 0;
+    if (lg == 0) {
+      bool b = false;
+      if (key != kEmptyKey) slot = probe_slot(t, key, true, &b);
+      inserted = b;
+      if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
+    }
+    if (G > 1) {
+      slot = __shfl(slot, 0, G);
+      inserted = __shfl(inserted, 0, G);
+    }
+    if (slot >= 0) {
+      float* row = slot_row(t, slot);
+      const float* src = rows + g * (long long)t.width;
+      for (uint32_t j = lg; j < t.width; j += G) row[j] = src[j];
+    }
+    ins += (lg == 0 && inserted);
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+}
+
+// K8: compact occupied slots of [s0, s0+n) into (keys_out, rows_out[width]).
+// Wave ballot + one atomic per wave for the output cursor.
+__global__ __launch_bounds__(256) void k_export(DevTable t, unsigned long long s0, long long n,
+                                                uint64_t* __restrict__ keys_out,
+                                                float* __restrict__ rows_out,
+                                                unsigned long long* cursor) {
+  const int lane = threadIdx.x & 63;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long base = (long long)blockIdx.x * blockDim.x; base < n; base += stride) {
+    const long long i = base + threadIdx.x;
+    uint64_t key = kEmptyKey;
+    if (i < n) key = *slot_key(t, s0 + i);
+    const bool occ = key != kEmptyKey;
+    const unsigned long long mask = __ballot(occ);
+    unsigned long long wbase = 0;
+    if (lane == 0 && mask) wbase = atomicAdd(cursor, (unsigned long long)__popcll(mask));
+    wbase = __shfl(wbase, 0, 64);
+    if (occ) {
+      const unsigned long long o = wbase + __popcll(mask & ((1ull << lane) - 1));
+      keys_out[o] = key;
+      const float* row = slot_row(t, s0 + i);
+      for (uint32_t j = 0; j < t.width; ++j) rows_out[o * t.width + j] = row[j];
+    }
+  }
+}
+
+// ---------------------------------------------------------------- launchers
+static inline int grid_for(long long groups, int G, int cap_blocks = 16384) {
+  long long threads = groups * G;
+  long long b = (threads + 255) / 256;
+  if (b < 1) b = 1;
+  if (b > cap_blocks) b = cap_blocks;
+  return (int)b;
+}
+
+#define SS_DISPATCH_G(G, ...)                   \
+  switch (G) {                                  \
+    case 1: { constexpr int kG = 1; __VA_ARGS__; } break;   \
+    case 4: { constexpr int kG = 4; __VA_ARGS__; } break;   \
+    case 16: { constexpr int kG = 16; __VA_ARGS__; } break; \
+    case 64: { constexpr int kG = 64; __VA_ARGS__; } break; \
+    default: throw_error("unsupported lane-group size");    \
+  }
+
+void launch_probe(const DevTable& t, const uint64_t* keys, const SegList& sl, long long max_n,
+                  long long* slots, const InitParams& ip, int insert,
+                  unsigned long long* size_ctr, int* err, int G, hipStream_t st) {
+  if (max_n <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_probe<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0, st, t,
+                                      keys, sl, slots, ip, insert, size_ctr, err));
+  check_launch("k_probe");
+}
+
+void launch_gather(const DevTable& t, const long long* slots, const SegList& sl, long long max_n,
+                   float* out, int G, hipStream_t st) {
+  if (max_n <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_gather<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0, st,
+                                      t, slots, sl, out));
+  check_launch("k_gather");
+}
+
+void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& sl,
+                        long long max_n, long long* slots, float* out, const InitParams& ip,
+                        unsigned long long* size_ctr, int* err, int G, hipStream_t st) {
+  if (max_n <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
+                                      st, t, keys, sl, slots, out, ip, size_ctr, err));
+  check_launch("k_pull_unique");
+}
+
+void launch_apply(const DevTable& t, const long long* slots, const float* grads,
+                  const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st) {
+  if (max_n <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0, st, t,
+                                      slots, grads, sl, op));
+  check_launch("k_apply");
+}
+
+void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, long long n,
+                   unsigned long long* size_ctr, int* err, int G, hipStream_t st) {
+  if (n <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_assign<kG>, dim3(grid_for(n, kG)), dim3(256), 0, st, t,
+                                      keys, rows, n, size_ctr, err));
+  check_launch("k_assign");
+}
+
+void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,
+                   float* rows_out, unsigned long long* cursor, hipStream_t st) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_export, dim3(grid_for(n, 1, 8192)), dim3(256), 0, st, t, s0, n, keys_out,
+                     rows_out, cursor);
+  check_launch("k_export");
+}
+
+}  // namespace ss

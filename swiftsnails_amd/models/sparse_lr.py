@@ -1,0 +1,88 @@
+"""Sparse logistic regression on the parameter server (BASELINE headline model).
+
+The reference names a ``logistic_regression`` app that is absent from the
+snapshot (/root/reference/src/tools/hadoop-server.sh:7, distribute.sh:8); its
+worker would ``pull_with_barrier`` the batch's keys, compute per-sample
+sigmoid(w·x) and push the per-key gradients (SwiftWorker/BaseAlgorithm::train,
+/root/reference/src/core/framework/SwiftWorker.h:19-30).  This module is that
+worker on MI355X:
+
+    step:  gen batch (device)  ->  pull (dedup/route/[a2av]/probe-init-gather)
+           ->  fused LR fwd/bwd kernel  ->  push (AdaGrad apply on the servers)
+
+Synthetic CTR data (``CtrSynth``): ``num_fields`` categorical fields, field f
+owning key range [f*V, (f+1)*V) of a ``num_features``-wide feature space
+(1B in the headline config), log-uniform (Zipf-like) ids with a uniform tail,
+labels drawn from a hidden ground-truth sparse LR model so loss goes down.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from .._native import hip
+from ..ops.optim import InitConfig, Optimizer
+from ..ops.table import HbmTable
+
+
+@dataclass
+class CtrSynth:
+    batch_size: int = 65536
+    num_fields: int = 39
+    num_features: int = 1_000_000_000
+    tail_frac: float = 0.1
+    truth_scale: float = 1.0
+    truth_bias: float = -1.0
+    seed: int = 20150404
+
+    @property
+    def vocab_per_field(self) -> int:
+        return max(1, self.num_features // self.num_fields)
+
+    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, labels: torch.Tensor,
+                 stream=None):
+        B, F = self.batch_size, self.num_fields
+        base = (step * world + rank) * B
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        hip().gen_ctr(self.seed, base, B, F, self.vocab_per_field, self.tail_frac,
+                      self.truth_scale, self.truth_bias, keys.data_ptr(), labels.data_ptr(), st)
+
+
+class SparseLRWorker:
+    """Trains sparse LR through a ``PSEngine`` (one per rank)."""
+
+    def __init__(self, engine, data: CtrSynth, rank: int = 0, world: int = 1):
+        self.engine, self.data, self.rank, self.world = engine, data, rank, world
+        dev = engine.device
+        B, F = data.batch_size, data.num_fields
+        self.keys = torch.empty(B * F, dtype=torch.int64, device=dev)
+        self.labels = torch.empty(B, dtype=torch.float32, device=dev)
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_idx = 0
+
+    def step(self, step: Optional[int] = None) -> torch.Tensor:
+        """One training step. Returns the summed batch logloss (device tensor)."""
+        d = self.data
+        s = self.step_idx if step is None else step
+        d.generate(s, self.rank, self.world, self.keys, self.labels)
+        rnd = self.engine.pull(self.keys)
+        self.loss_sum.zero_()
+        hip().lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels.data_ptr(), d.batch_size,
+                         d.num_fields, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
+                         self.loss_sum.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
+        self.engine.push(rnd)
+        self.step_idx += 1
+        return self.loss_sum
+
+    def mean_loss(self) -> float:
+        return float(self.loss_sum.item()) / self.data.batch_size
+
+
+def make_lr_table(num_features: int, world: int = 1, optimizer: Optional[Optimizer] = None,
+                  load: float = 0.7, device=None, capacity: Optional[int] = None) -> HbmTable:
+    """Shard sized for the whole feature space split over `world` servers."""
+    opt = optimizer or Optimizer("adagrad", lr=0.05, eps=1e-8)
+    cap = capacity or int(num_features / world / load) + 1024
+    return HbmTable(1, cap, optimizer=opt, init=InitConfig("zero"), device=device)

@@ -1,0 +1,116 @@
+"""Worker-side key dedup + routing (K1/K2) with preallocated scratch.
+
+Replaces the caller-side ``std::unordered_set`` and ``arrange_local_vals``
+grouping of ``pull_with_barrier``/``push_with_barrier``
+(/root/reference/src/core/parameter/global_pull_access.h:40-72,
+global_push_access.h:80-99).  Output layout is the alltoallv send layout:
+
+* ``ukeys[nranks * ucap]``: unique keys, destination ``r`` owns
+  ``[r*ucap, r*ucap + ucount[r])``;
+* ``inv[n]``: occurrence -> unique id (index into rows laid out the same way);
+* ``ugrad[nranks * ucap, gdim]``: zeroed gradient rows for the unique keys.
+
+``dedup_reference`` is the host implementation used on CPU and by the tests.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..utils.hashing import fmix64
+from .table import _stream_ptr
+
+INVALID = 0xFFFFFFFF
+
+
+def _next_pow2(x: int) -> int:
+    return 1 << max(4, (int(x) - 1).bit_length())
+
+
+@dataclass
+class DedupResult:
+    ukeys: torch.Tensor       # int64 [nranks*ucap]
+    ucount: torch.Tensor      # int64 [nranks] (device)
+    inv: torch.Tensor         # int32 [n] (uint32 bit pattern; INVALID for bad keys)
+    ugrad: Optional[torch.Tensor]
+    ucap: int
+    nranks: int
+    n: int
+
+
+class Deduper:
+    """Device dedup/route with scratch sized for up to ``max_n`` keys per call."""
+
+    def __init__(self, max_n: int, nranks: int = 1, frag_map: Optional[torch.Tensor] = None,
+                 gdim: int = 1, device=None, with_grad: bool = True):
+        from .._native import hip
+
+        self.h = hip()
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.max_n = int(max_n)
+        self.nranks = int(nranks)
+        self.gdim = int(gdim)
+        self.ucap = self.max_n
+        self.scap = _next_pow2(2 * self.max_n)
+        d = self.device
+        if frag_map is None:
+            frag_map = torch.zeros(1, dtype=torch.int32)
+        self.frag_map = frag_map.to(d, torch.int32).contiguous()
+        self.skeys = torch.empty(self.scap, dtype=torch.int64, device=d)
+        self.suid = torch.empty(self.scap, dtype=torch.int32, device=d)
+        self.slot_of = torch.empty(self.max_n, dtype=torch.int32, device=d)
+        self.inv = torch.empty(self.max_n, dtype=torch.int32, device=d)
+        self.ukeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64, device=d)
+        self.ucount = torch.zeros(self.nranks, dtype=torch.int64, device=d)
+        self.ugrad = (torch.empty((self.nranks * self.ucap, self.gdim), dtype=torch.float32,
+                                  device=d) if with_grad else None)
+
+    def __call__(self, keys: torch.Tensor, stream=None) -> DedupResult:
+        n = keys.numel()
+        if n > self.max_n:
+            raise ValueError(f"dedup: {n} keys > capacity {self.max_n}")
+        st = _stream_ptr(stream)
+        # scratch reset (memset nodes; hipGraph-capturable)
+        self.skeys.fill_(-1)
+        self.ucount.zero_()
+        self.h.dedup_route(keys.data_ptr(), n, self.skeys.data_ptr(), self.suid.data_ptr(),
+                           self.scap, self.slot_of.data_ptr(), self.frag_map.data_ptr(),
+                           self.frag_map.numel(), self.nranks, self.ucap, self.ucount.data_ptr(),
+                           self.ukeys.data_ptr(),
+                           self.ugrad.data_ptr() if self.ugrad is not None else 0, self.gdim, st)
+        self.h.dedup_inverse(self.slot_of.data_ptr(), self.suid.data_ptr(), n, self.inv.data_ptr(),
+                             st)
+        return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
+                           self.nranks, n)
+
+
+def dedup_reference(keys, nranks: int = 1, frag_map: Optional[np.ndarray] = None,
+                    ucap: Optional[int] = None):
+    """Host reference: returns (ukeys [nranks*ucap] u64, ucount [nranks], inv [n]).
+
+    Unique keys inside a destination segment are sorted ascending (the device
+    kernel's order is arbitrary; compare as sets + inverse consistency)."""
+    k = np.asarray(keys).view(np.uint64) if np.asarray(keys).dtype == np.int64 else np.asarray(
+        keys, dtype=np.uint64)
+    n = len(k)
+    ucap = ucap or max(n, 1)
+    uniq, inv0 = np.unique(k, return_inverse=True)
+    if nranks == 1 or frag_map is None:
+        dest = np.zeros(len(uniq), dtype=np.int64)
+    else:
+        dest = frag_map[(fmix64(uniq) % np.uint64(len(frag_map))).astype(np.int64)].astype(
+            np.int64)
+    ukeys = np.full(nranks * ucap, np.uint64(0xFFFFFFFFFFFFFFFF), dtype=np.uint64)
+    ucount = np.zeros(nranks, dtype=np.int64)
+    uid = np.empty(len(uniq), dtype=np.int64)
+    for r in range(nranks):
+        idx = np.nonzero(dest == r)[0]
+        ucount[r] = len(idx)
+        ukeys[r * ucap:r * ucap + len(idx)] = uniq[idx]
+        uid[idx] = r * ucap + np.arange(len(idx))
+    inv = uid[inv0] if n else np.zeros(0, dtype=np.int64)
+    return ukeys, ucount, inv

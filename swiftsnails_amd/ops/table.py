@@ -1,0 +1,258 @@
+"""HBM-resident sparse parameter table (one shard per GPU).
+
+Replaces ``SparseTable``/``SparseTableShard`` (google dense_hash_map + pthread
+RW lock per shard, /root/reference/src/core/parameter/sparsetable.h:5-121) and
+the server halves of ``PullAccessAgent``/``PushAccessAgent``
+(sparsetable.h:123-222) with an open-addressed table in HBM driven by the
+HIP kernels of ``csrc/hip/table.hip``:
+
+* ``pull``  = lookup-or-init + row gather (K3/K4); missing keys are created
+  with the configured initialiser, exactly like ``get_pull_value``.
+* ``push``  = fused probe/update (K5) with the configured optimizer.
+* ``export``/``assign`` = slot compaction / bulk insert (K8) used by the text
+  and binary checkpoints and by ``resize``.
+
+Slot layout: ``[row: width fp32 | pad | key u64]`` (see ss_device.h).
+Sizing: ``HbmTable.plan(n_keys, dim, optimizer, load=0.7)`` gives the bytes a
+shard needs; a 1B-key sparse-LR table (AdaGrad) is 1B/0.7 * 16 B ≈ 23 GB, so
+it fits a single MI355X's 288 GB with room to spare.
+"""
+from __future__ import annotations
+
+import math
+from typing import Iterator, Optional
+
+import numpy as np
+import torch
+
+from .._native import hip
+from .optim import InitConfig, Optimizer
+
+EMPTY_I64 = -1  # u64 0xFFFF_FFFF_FFFF_FFFF
+
+
+def _align(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+def slot_layout(width: int) -> tuple[int, int]:
+    """(stride_bytes, key_offset_bytes) of one slot."""
+    key_off = _align(4 * width, 8)
+    stride = key_off + 8
+    if width >= 4:
+        stride = _align(stride, 16)
+    return stride, key_off
+
+
+def default_lane_group(width: int) -> int:
+    if width <= 2:
+        return 1
+    if width <= 16:
+        return 4
+    if width <= 64:
+        return 16
+    return 64
+
+
+def _stream_ptr(stream) -> int:
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+class TableFullError(RuntimeError):
+    pass
+
+
+class HbmTable:
+    """One GPU shard of the sparse parameter table."""
+
+    def __init__(self, dim: int, capacity: int, optimizer: Optional[Optimizer] = None,
+                 init: Optional[InitConfig] = None, device=None, lane_group: Optional[int] = None,
+                 max_load: float = 0.85):
+        if dim < 1:
+            raise ValueError("dim must be >= 1")
+        if capacity < 1:
+            raise ValueError("capacity must be >= 1")
+        self.device = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        self.dim = int(dim)
+        self.opt = optimizer or Optimizer()
+        self.init_cfg = init or InitConfig()
+        self.width = self.dim + self.opt.state_width(self.dim)
+        self.stride, self.key_off = slot_layout(self.width)
+        self.G = lane_group or default_lane_group(self.width)
+        self.max_load = max_load
+        self._alloc(int(capacity))
+        self._init_native = self.init_cfg.native()
+
+    # -- storage ------------------------------------------------------------
+    def _alloc(self, cap: int):
+        self.capacity = cap
+        self.storage = torch.empty(cap * self.stride, dtype=torch.uint8, device=self.device)
+        self.storage.fill_(255)  # every key word = EMPTY
+        self.size_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.dt = hip().DevTable(self.storage.data_ptr(), cap, self.stride, self.key_off, self.dim,
+                                 self.width)
+
+    @staticmethod
+    def plan(n_keys: int, dim: int, optimizer: Optional[Optimizer] = None,
+             load: float = 0.7) -> dict:
+        opt = optimizer or Optimizer()
+        width = dim + opt.state_width(dim)
+        stride, _ = slot_layout(width)
+        cap = int(math.ceil(n_keys / load))
+        return {"capacity": cap, "stride": stride, "bytes": cap * stride, "width": width}
+
+    @classmethod
+    def for_keys(cls, n_keys: int, dim: int, load: float = 0.7, **kw) -> "HbmTable":
+        return cls(dim, max(16, int(math.ceil(n_keys / load))), **kw)
+
+    @property
+    def nbytes(self) -> int:
+        return self.capacity * self.stride
+
+    def set_optimizer(self, opt: Optimizer):
+        if opt.state_width(self.dim) != self.width - self.dim:
+            raise ValueError("optimizer state width differs from the table layout")
+        self.opt = opt
+
+    # -- hot path -----------------------------------------------------------
+    def _seg(self, n: int):
+        return hip().SegList.from_host([0], [int(n)])
+
+    @staticmethod
+    def segs(offsets, counts):
+        """Segment list over one buffer: (offset, count) pairs in rows."""
+        return hip().SegList.from_host([int(o) for o in offsets], [int(c) for c in counts])
+
+    @staticmethod
+    def dev_segs(count: torch.Tensor):
+        """Single segment at offset 0 whose length is ``count[0]`` on the device."""
+        return hip().SegList.from_device(count.data_ptr())
+
+    def pull(self, keys: torch.Tensor, insert: bool = True, unique: bool = False,
+             out: Optional[torch.Tensor] = None, slots: Optional[torch.Tensor] = None,
+             segs=None, max_n: Optional[int] = None, stream=None):
+        """Lookup-or-init (insert=True) + gather. Returns (vals[n, dim], slots[n])."""
+        n = keys.numel() if max_n is None else max_n
+        st = _stream_ptr(stream)
+        h = hip()
+        if out is None:
+            out = torch.empty((keys.numel(), self.dim), dtype=torch.float32, device=self.device)
+        if slots is None:
+            slots = torch.empty(keys.numel(), dtype=torch.int64, device=self.device)
+        sl = segs if segs is not None else self._seg(keys.numel())
+        if unique and insert:
+            h.pull_unique(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), out.data_ptr(),
+                          self._init_native, self.size_ctr.data_ptr(), self.err.data_ptr(), self.G,
+                          st)
+        else:
+            h.probe(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), self._init_native,
+                    int(insert), self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, st)
+            h.gather(self.dt, slots.data_ptr(), sl, n, out.data_ptr(), self.G, st)
+        return out, slots
+
+    def lookup_slots(self, keys: torch.Tensor, insert: bool = False, segs=None,
+                     max_n: Optional[int] = None, stream=None) -> torch.Tensor:
+        slots = torch.empty(keys.numel(), dtype=torch.int64, device=self.device)
+        sl = segs if segs is not None else self._seg(keys.numel())
+        hip().probe(self.dt, keys.data_ptr(), sl, keys.numel() if max_n is None else max_n,
+                    slots.data_ptr(), self._init_native, int(insert), self.size_ctr.data_ptr(),
+                    self.err.data_ptr(), self.G, _stream_ptr(stream))
+        return slots
+
+    def push_slots(self, slots: torch.Tensor, grads: torch.Tensor, segs=None,
+                   max_n: Optional[int] = None, stream=None):
+        """Apply the optimizer at resolved slots (keys in one call must be unique)."""
+        sl = segs if segs is not None else self._seg(slots.numel())
+        hip().apply(self.dt, slots.data_ptr(), grads.data_ptr(), sl,
+                    slots.numel() if max_n is None else max_n, self.opt.native(), self.G,
+                    _stream_ptr(stream))
+
+    def push(self, keys: torch.Tensor, grads: torch.Tensor, stream=None):
+        """push by key: keys missing from the table are created first (the
+        reference CHECK-fails instead, sparsetable.h:184)."""
+        slots = self.lookup_slots(keys, insert=True, stream=stream)
+        self.push_slots(slots, grads.reshape(-1, self.dim).contiguous(), stream=stream)
+
+    def next_round(self):
+        """Advance per-round optimizer state (Adam bias correction)."""
+        self.opt.step += 1
+
+    # -- maintenance --------------------------------------------------------
+    def size(self) -> int:
+        return int(self.size_ctr.item())
+
+    def load_factor(self) -> float:
+        return self.size() / self.capacity
+
+    def check(self):
+        e = int(self.err.item())
+        if e & 1:
+            raise TableFullError(f"table full: capacity {self.capacity}, size {self.size()}")
+        if e & 2:
+            raise ValueError("key 0xFFFFFFFFFFFFFFFF is reserved (empty-slot sentinel)")
+
+    def assign(self, keys: torch.Tensor, rows: torch.Tensor, stream=None):
+        """Insert-or-overwrite full rows (params + optimizer state)."""
+        keys = keys.to(self.device, torch.int64).contiguous()
+        rows = rows.to(self.device, torch.float32).reshape(-1, self.width).contiguous()
+        if rows.shape[0] != keys.numel():
+            raise ValueError("rows/keys length mismatch")
+        hip().assign(self.dt, keys.data_ptr(), rows.data_ptr(), keys.numel(),
+                     self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, _stream_ptr(stream))
+
+    def export(self, chunk_slots: int = 1 << 24, to_host: bool = True
+               ) -> Iterator[tuple[torch.Tensor, torch.Tensor]]:
+        """Yield (keys int64, rows float32 [m, width]) for all occupied slots."""
+        h = hip()
+        st = _stream_ptr(None)
+        cursor = torch.zeros(1, dtype=torch.int64, device=self.device)
+        kbuf = torch.empty(min(chunk_slots, self.capacity), dtype=torch.int64, device=self.device)
+        rbuf = torch.empty((min(chunk_slots, self.capacity), self.width), dtype=torch.float32,
+                           device=self.device)
+        for s0 in range(0, self.capacity, chunk_slots):
+            n = min(chunk_slots, self.capacity - s0)
+            cursor.zero_()
+            h.export_slots(self.dt, s0, n, kbuf.data_ptr(), rbuf.data_ptr(), cursor.data_ptr(), st)
+            m = int(cursor.item())
+            if m:
+                k, r = kbuf[:m], rbuf[:m]
+                yield (k.cpu(), r.cpu()) if to_host else (k.clone(), r.clone())
+
+    def resize(self, new_capacity: int):
+        """Rehash into a new allocation (capacity planning / growth)."""
+        if new_capacity < self.size():
+            raise ValueError("new capacity smaller than the number of keys")
+        chunks = list(self.export(to_host=False))
+        old = self.storage
+        self._alloc(int(new_capacity))
+        del old
+        for k, r in chunks:
+            self.assign(k, r)
+        self.check()
+
+    def maybe_grow(self, incoming: int = 0, factor: float = 2.0) -> bool:
+        if self.size() + incoming > self.max_load * self.capacity:
+            self.resize(int(max(self.capacity * factor, (self.size() + incoming) / 0.5)))
+            return True
+        return False
+
+    # -- dense views (tests / small tables) --------------------------------
+    def to_dict(self, with_state: bool = False) -> dict[int, np.ndarray]:
+        out = {}
+        for k, r in self.export():
+            kn = k.numpy().view(np.uint64)
+            rn = r.numpy()
+            for i in range(len(kn)):
+                out[int(kn[i])] = rn[i] if with_state else rn[i, :self.dim]
+        return out
+
+    def __len__(self):
+        return self.size()
+
+    def __repr__(self):
+        return (f"HbmTable(dim={self.dim}, width={self.width}, capacity={self.capacity}, "
+                f"stride={self.stride}B, opt={self.opt.kind}, device={self.device})")

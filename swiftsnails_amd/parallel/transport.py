@@ -1,0 +1,194 @@
+"""Data-plane transports for the collective round engine.
+
+The reference's transport is ZeroMQ PUSH/PULL over TCP with a per-message RPC
+(/root/reference/src/core/transfer/transfer.h:75-225).  Here one pull or push
+*round* is a small set of alltoallv exchanges between all ranks:
+
+* ``RcclTransport``   — native RCCL communicator (``csrc/hip/comm.cpp``) over
+  xGMI: grouped ncclSend/ncclRecv with per-peer displacements on a HIP stream.
+  Bootstrapped with an ``ncclUniqueId`` broadcast through the torch.distributed
+  store.  This is the MI355X data plane.
+* ``TorchDistTransport`` — ``torch.distributed.all_to_all_single`` (gloo on
+  CPU for the multi-process tests; also works over the nccl=RCCL backend).
+* ``LoopbackTransport`` — world size 1 (device copies only).
+
+All transports speak in *rows*: a buffer is a flat tensor of rows of
+``row_elems`` elements; counts and displacements are in rows.
+"""
+from __future__ import annotations
+
+from abc import ABC, abstractmethod
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+class Transport(ABC):
+    rank: int = 0
+    world: int = 1
+
+    @abstractmethod
+    def exchange_counts(self, send_counts: torch.Tensor) -> tuple[np.ndarray, np.ndarray]:
+        """All-to-all of one int64 per peer. Returns host (send_counts, recv_counts)."""
+
+    @abstractmethod
+    def alltoallv(self, send: torch.Tensor, scounts: Sequence[int], sdispls: Sequence[int],
+                  recv: torch.Tensor, rcounts: Sequence[int], rdispls: Sequence[int],
+                  row_elems: int = 1) -> None:
+        ...
+
+    @abstractmethod
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        ...
+
+    @abstractmethod
+    def barrier(self) -> None:
+        ...
+
+    def close(self) -> None:
+        pass
+
+
+class LoopbackTransport(Transport):
+    def __init__(self):
+        self.rank, self.world = 0, 1
+
+    def exchange_counts(self, send_counts):
+        c = send_counts.detach().cpu().numpy().astype(np.int64)
+        return c, c.copy()
+
+    def alltoallv(self, send, scounts, sdispls, recv, rcounts, rdispls, row_elems=1):
+        n = int(scounts[0]) * row_elems
+        if n and (send.data_ptr() != recv.data_ptr() or sdispls[0] != rdispls[0]):
+            s0, r0 = int(sdispls[0]) * row_elems, int(rdispls[0]) * row_elems
+            recv.view(-1)[r0:r0 + n].copy_(send.view(-1)[s0:s0 + n])
+
+    def allreduce_(self, t, op="sum"):
+        return t
+
+    def barrier(self):
+        pass
+
+
+class TorchDistTransport(Transport):
+    """torch.distributed-based transport (gloo on CPU, or nccl on GPU)."""
+
+    def __init__(self, group=None):
+        self.group = group
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        self.backend = dist.get_backend(group)
+
+    def _dev(self, t: torch.Tensor):
+        return t if self.backend != "gloo" else t.cpu()
+
+    def exchange_counts(self, send_counts):
+        s = self._dev(send_counts.to(torch.int64).contiguous())
+        r = torch.empty_like(s)
+        dist.all_to_all_single(r, s, group=self.group)
+        return s.cpu().numpy(), r.cpu().numpy()
+
+    def alltoallv(self, send, scounts, sdispls, recv, rcounts, rdispls, row_elems=1):
+        sflat, rflat = send.view(-1), recv.view(-1)
+        parts = [sflat[int(d) * row_elems:(int(d) + int(c)) * row_elems]
+                 for c, d in zip(scounts, sdispls)]
+        sbuf = self._dev(torch.cat(parts) if parts else sflat[:0])
+        rtotal = int(sum(rcounts)) * row_elems
+        rbuf = torch.empty(rtotal, dtype=sbuf.dtype, device=sbuf.device)
+        dist.all_to_all_single(rbuf, sbuf, [int(c) * row_elems for c in rcounts],
+                               [int(c) * row_elems for c in scounts], group=self.group)
+        rbuf = rbuf.to(recv.device)
+        o = 0
+        for c, d in zip(rcounts, rdispls):
+            n = int(c) * row_elems
+            if n:
+                rflat[int(d) * row_elems:int(d) * row_elems + n].copy_(rbuf[o:o + n])
+            o += n
+
+    def allreduce_(self, t, op="sum"):
+        o = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op]
+        if self.backend == "gloo" and t.device.type != "cpu":
+            c = t.cpu()
+            dist.all_reduce(c, o, group=self.group)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, o, group=self.group)
+        return t
+
+    def barrier(self):
+        dist.barrier(group=self.group)
+
+
+class RcclTransport(Transport):
+    """Native RCCL communicator on a dedicated (or the current) HIP stream."""
+
+    _DT = {torch.float32: 0, torch.float64: 1, torch.int32: 2, torch.int64: 3}
+
+    def __init__(self, rank: int, world: int, device: torch.device, store=None,
+                 uid: Optional[bytes] = None, prefix: str = "ss_rccl"):
+        from .._native import hip
+
+        h = hip()
+        self.rank, self.world, self.device = rank, world, torch.device(device)
+        if uid is None:
+            if store is None:
+                raise ValueError("RcclTransport needs a store (or an explicit unique id)")
+            key = f"{prefix}_uid"
+            if rank == 0:
+                uid = h.RcclComm.unique_id()
+                store.set(key, uid)
+            else:
+                store.wait([key])
+                uid = store.get(key)
+        self.comm = h.RcclComm(rank, world, uid, self.device.index or 0)
+        self._pin = torch.empty(2 * world, dtype=torch.int64, pin_memory=True)
+        self._cnt_recv = torch.empty(world, dtype=torch.int64, device=self.device)
+
+    @staticmethod
+    def _st():
+        return torch.cuda.current_stream().cuda_stream
+
+    def exchange_counts(self, send_counts):
+        s = send_counts.to(torch.int64).contiguous()
+        self.comm.alltoall(s.data_ptr(), self._cnt_recv.data_ptr(), 1, 8, self._st())
+        self._pin[:self.world].copy_(s, non_blocking=True)
+        self._pin[self.world:].copy_(self._cnt_recv, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        p = self._pin.numpy()
+        return p[:self.world].copy(), p[self.world:].copy()
+
+    def alltoallv(self, send, scounts, sdispls, recv, rcounts, rdispls, row_elems=1):
+        eb = send.element_size() * row_elems
+        self.comm.alltoallv(send.data_ptr(), [int(x) for x in scounts],
+                            [int(x) for x in sdispls], recv.data_ptr(),
+                            [int(x) for x in rcounts], [int(x) for x in rdispls], eb, self._st())
+
+    def allreduce_(self, t, op="sum"):
+        self.comm.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._DT[t.dtype],
+                            {"sum": 0, "max": 1, "min": 2}[op], self._st())
+        return t
+
+    def barrier(self):
+        x = torch.zeros(1, dtype=torch.float32, device=self.device)
+        self.allreduce_(x)
+        torch.cuda.current_stream().synchronize()
+
+    def close(self):
+        self.comm = None
+
+
+def make_transport(kind: str = "auto", device=None, store=None) -> Transport:
+    """auto: loopback for world 1; rccl on GPU; torch.distributed otherwise."""
+    if not dist.is_available() or not dist.is_initialized():
+        return LoopbackTransport()
+    world = dist.get_world_size()
+    if world == 1 and kind == "auto":
+        return LoopbackTransport()
+    dev = torch.device(device) if device is not None else None
+    if kind == "rccl" or (kind == "auto" and dev is not None and dev.type == "cuda"):
+        if store is None:
+            store = dist.distributed_c10d._get_default_store()
+        return RcclTransport(dist.get_rank(), world, dev, store=store)
+    return TorchDistTransport()

@@ -1,0 +1,237 @@
+"""HIP kernel numerics vs fp32 host references (run on MI355X: -m gpu)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    from swiftsnails_amd._native import hip
+
+    hip()  # loud failure if the extension is missing on a GPU box
+    return torch.device("cuda", 0)
+
+
+def _keys(n, seed=0, hi=1 << 40):
+    rng = np.random.default_rng(seed)
+    return rng.integers(0, hi, size=n, dtype=np.int64)
+
+
+def test_table_pull_inits_and_is_stable(dev):
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer, init_reference
+    from swiftsnails_amd.ops.table import HbmTable
+
+    init = InitConfig("uniform", scale=0.25, state_init=0.1, seed=7)
+    t = HbmTable(8, 4096, optimizer=Optimizer("adagrad"), init=init, device=dev)
+    k = np.unique(_keys(1000, 1))
+    kt = torch.from_numpy(k).to(dev)
+    v1, s1 = t.pull(kt)
+    v2, s2 = t.pull(kt)
+    torch.cuda.synchronize()
+    t.check()
+    assert t.size() == len(k)
+    ref = init_reference(init, k, 8, t.width)
+    np.testing.assert_array_equal(v1.cpu().numpy(), ref[:, :8])
+    np.testing.assert_array_equal(v2.cpu().numpy(), v1.cpu().numpy())
+    assert torch.equal(s1, s2)
+    d = t.to_dict(with_state=True)
+    row = d[int(k[3])]
+    np.testing.assert_allclose(row[8:], 0.1)
+
+
+@pytest.mark.parametrize("G", [1, 4, 16, 64])
+def test_probe_duplicates_same_slot(dev, G):
+    from swiftsnails_amd.ops.table import HbmTable
+
+    t = HbmTable(4, 1 << 12, device=dev, lane_group=G)
+    base = _keys(300, 2)
+    k = np.concatenate([base, base[::-1], base[:50]])
+    kt = torch.from_numpy(k).to(dev)
+    v, s = t.pull(kt, unique=False)
+    torch.cuda.synchronize()
+    t.check()
+    assert t.size() == len(np.unique(base))
+    sn = s.cpu().numpy()
+    for key in np.unique(base)[:50]:
+        idx = np.nonzero(k == key)[0]
+        assert len(set(sn[idx].tolist())) == 1
+
+
+@pytest.mark.parametrize("kind", ["sgd", "adagrad", "ftrl", "adam"])
+@pytest.mark.parametrize("dim", [1, 8, 33])
+def test_apply_matches_reference(dev, kind, dim):
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer, apply_reference
+    from swiftsnails_amd.ops.table import HbmTable
+
+    opt = Optimizer(kind, lr=0.1, l1=0.01, l2=0.001, grad_scale=0.5, clip=5.0)
+    opt.step = 1
+    t = HbmTable(dim, 4096, optimizer=opt, init=InitConfig("uniform", 0.5, 0.05), device=dev)
+    k = np.unique(_keys(700, 3))
+    kt = torch.from_numpy(k).to(dev)
+    t.pull(kt)
+    before = t.to_dict(with_state=True)
+    rows0 = np.stack([before[int(x)] for x in k.view(np.uint64)])
+    g = np.random.default_rng(4).standard_normal((len(k), dim)).astype(np.float32)
+    t.push(kt, torch.from_numpy(g).to(dev))
+    torch.cuda.synchronize()
+    after = t.to_dict(with_state=True)
+    rows1 = np.stack([after[int(x)] for x in k.view(np.uint64)])
+    ref = apply_reference(opt, rows0, g, dim)
+    np.testing.assert_allclose(rows1, ref, rtol=2e-5, atol=2e-6)
+
+
+def test_export_assign_resize_roundtrip(dev):
+    from swiftsnails_amd.ops.optim import InitConfig
+    from swiftsnails_amd.ops.table import HbmTable
+
+    t = HbmTable(3, 1000, init=InitConfig("normal", 0.1), device=dev)
+    k = np.unique(_keys(600, 5))
+    t.pull(torch.from_numpy(k).to(dev))
+    d0 = t.to_dict(with_state=True)
+    t.resize(5000)
+    assert t.capacity == 5000 and t.size() == len(k)
+    d1 = t.to_dict(with_state=True)
+    assert d0.keys() == d1.keys()
+    for kk in d0:
+        np.testing.assert_array_equal(d0[kk], d1[kk])
+
+
+def test_table_full_raises(dev):
+    from swiftsnails_amd.ops.table import HbmTable, TableFullError
+
+    t = HbmTable(1, 64, device=dev)
+    t.pull(torch.from_numpy(_keys(100, 6)).to(dev))
+    torch.cuda.synchronize()
+    with pytest.raises(TableFullError):
+        t.check()
+
+
+@pytest.mark.parametrize("nranks", [1, 3, 8])
+def test_dedup_route_matches_reference(dev, nranks):
+    from swiftsnails_amd.ops.dedup import Deduper, dedup_reference
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    rng = np.random.default_rng(nranks)
+    k = rng.integers(0, 5000, size=20000, dtype=np.int64)  # heavy duplication
+    hf = HashFrag(nranks, 97)
+    fm = hf.rank_map()
+    d = Deduper(25000, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=2,
+                device=dev)
+    r = d(torch.from_numpy(k).to(dev))
+    torch.cuda.synchronize()
+    uk_ref, uc_ref, _ = dedup_reference(k, nranks, fm, ucap=d.ucap)
+    uc = r.ucount.cpu().numpy()
+    np.testing.assert_array_equal(uc, uc_ref)
+    uk = r.ukeys.cpu().numpy()
+    for q in range(nranks):
+        seg = np.sort(uk[q * d.ucap:q * d.ucap + uc[q]])
+        np.testing.assert_array_equal(seg, np.sort(uk_ref[q * d.ucap:q * d.ucap + uc_ref[q]]
+                                                   .view(np.int64)))
+    inv = r.inv.cpu().numpy().view(np.uint32).astype(np.int64)
+    np.testing.assert_array_equal(uk[inv], k)  # ukeys[inv] reproduces the batch
+    g = r.ugrad.cpu().numpy()
+    for q in range(nranks):
+        assert not g[q * d.ucap:q * d.ucap + uc[q]].any()
+    # reference routing parity: dest segment of each key == map[fmix64 % frag]
+    dest = inv // d.ucap
+    np.testing.assert_array_equal(dest, hf.rank_map()[hf.frag_of(k)])
+
+
+def test_lr_fwd_bwd_matches_torch(dev):
+    from swiftsnails_amd._native import hip
+
+    B, F, U = 3000, 39, 5000
+    rng = np.random.default_rng(9)
+    inv = rng.integers(0, U, size=B * F).astype(np.int32)
+    x = rng.standard_normal(B * F).astype(np.float32)
+    y = (rng.random(B) < 0.3).astype(np.float32)
+    w = (rng.standard_normal(U) * 0.1).astype(np.float32)
+    tinv, tx, ty, tw = (torch.from_numpy(a).to(dev) for a in (inv, x, y, w))
+    g = torch.zeros(U, device=dev)
+    loss = torch.zeros(1, device=dev)
+    pred = torch.empty(B, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    hip().lr_fwd_bwd(tinv.data_ptr(), tx.data_ptr(), ty.data_ptr(), B, F, tw.data_ptr(),
+                     g.data_ptr(), loss.data_ptr(), pred.data_ptr(), st)
+    torch.cuda.synchronize()
+    # fp32 torch reference
+    W = torch.from_numpy(w).double()
+    z = (W[torch.from_numpy(inv).long()] * torch.from_numpy(x).double()).view(B, F).sum(1)
+    p = torch.sigmoid(z)
+    Y = torch.from_numpy(y).double()
+    ref_loss = torch.nn.functional.binary_cross_entropy_with_logits(z, Y, reduction="sum")
+    gs = (p - Y).repeat_interleave(F) * torch.from_numpy(x).double()
+    ref_g = torch.zeros(U, dtype=torch.float64).index_add_(0, torch.from_numpy(inv).long(), gs)
+    np.testing.assert_allclose(pred.cpu().numpy(), p.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(loss.item(), ref_loss.item(), rtol=1e-4)
+    np.testing.assert_allclose(g.cpu().numpy(), ref_g.numpy(), rtol=1e-3, atol=1e-4)
+
+
+def test_gen_ctr_ranges(dev):
+    from swiftsnails_amd.models.sparse_lr import CtrSynth
+
+    d = CtrSynth(batch_size=4096, num_fields=39, num_features=10_000_000)
+    keys = torch.empty(4096 * 39, dtype=torch.int64, device=dev)
+    labels = torch.empty(4096, device=dev)
+    d.generate(0, 0, 1, keys, labels)
+    torch.cuda.synchronize()
+    k = keys.cpu().numpy().reshape(4096, 39)
+    V = d.vocab_per_field
+    f = k // V
+    assert (f == np.arange(39)[None, :]).all()
+    lab = labels.cpu().numpy()
+    assert set(np.unique(lab)) <= {0.0, 1.0} and 0.05 < lab.mean() < 0.95
+    k2 = torch.empty_like(keys)
+    d.generate(0, 0, 1, k2, labels)
+    assert torch.equal(keys, k2)  # deterministic
+
+
+def test_sparse_lr_trains_world1(dev):
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    data = CtrSynth(batch_size=8192, num_fields=16, num_features=200_000, tail_frac=0.0)
+    table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
+    eng = PSEngine(table, None, max_keys=8192 * 16, dim=1, device=dev)
+    w = SparseLRWorker(eng, data)
+    losses = []
+    for i in range(60):
+        w.step()
+        losses.append(w.mean_loss())
+    table.check()
+    assert np.mean(losses[-5:]) < np.mean(losses[:3]) - 0.02, losses
+    assert 0 < table.size() <= data.num_features
+
+
+def test_engine_pull_push_keys_world1(dev):
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    t = HbmTable(4, 1 << 14, optimizer=Optimizer("sgd", lr=1.0), init=InitConfig("zero"),
+                 device=dev)
+    eng = PSEngine(t, None, max_keys=1000, dim=4, device=dev)
+    k = torch.tensor([5, 7, 5, 9, 7, 5], dtype=torch.int64, device=dev)
+    g = torch.ones(6, 4, device=dev)
+    eng.push_keys(k, g)
+    vals = eng.pull_dense(k)
+    torch.cuda.synchronize()
+    v = vals.cpu().numpy()[:, 0]
+    np.testing.assert_allclose(v, [-3, -2, -3, -1, -2, -3])  # SGD lr=1, merged grads
+
+
+def test_rccl_comm_world1(dev):
+    from swiftsnails_amd._native import hip
+
+    h = hip()
+    c = h.RcclComm(0, 1, h.RcclComm.unique_id(), 0)
+    a = torch.arange(10, dtype=torch.float32, device=dev)
+    b = torch.zeros(10, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    c.alltoallv(a.data_ptr(), [4], [2], b.data_ptr(), [4], [5], 4, st)
+    c.allreduce(a.data_ptr(), a.data_ptr(), 10, 0, 0, st)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(b.cpu().numpy()[5:9], [2, 3, 4, 5])

@@ -1,0 +1,40 @@
+#!/usr/bin/env bash
+# One GPU-box session: smoke -> gpu tests -> bench -> rocprofv3 kernel stats.
+# Stops at the first fault/abort/timeout (exit 124/134/137/139 or signal);
+# an ordinary test failure (pytest exit 1) does not stop the session.
+set -u
+OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+STEPS=${STEPS:-smoke,tests,bench,prof}
+BENCH_ARGS=${BENCH_ARGS:-"--steps 30 --warmup 5"}
+
+fatal() {  # exit code -> is it a fault we must not continue after?
+  case "$1" in
+    0|1|2|5) return 1 ;;
+    *) return 0 ;;
+  esac
+}
+
+run() {  # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "=== $name: $*" | tee -a "$OUT/session.log"
+  local t0=$(date +%s)
+  timeout -k 10 "$to" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc ($(( $(date +%s) - t0 ))s)" | tee -a "$OUT/session.log"
+  tail -n 15 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL in $name (rc=$rc): stopping session" | tee -a "$OUT/session.log"; exit $rc; fi
+  return 0
+}
+
+for s in ${STEPS//,/ }; do
+  case $s in
+    smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    bench) run bench 600 python bench.py $BENCH_ARGS ;;
+    prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
+    *) run custom 600 bash -c "$s" ;;
+  esac
+done
+echo "session done"
