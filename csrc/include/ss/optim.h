@@ -1,0 +1,112 @@
+// ss/optim.h — parameter initialisers and per-coordinate update rules shared
+// bit-for-bit (modulo libm rounding) by the gfx950 table kernels and the host
+// CPU table, so a CPU server and an MI355X server apply identical semantics.
+//
+// These replace the user-subclassed PullAccessMethod::init_param and
+// PushAccessMethod::apply_push_value of the reference
+// (/root/reference/src/core/parameter/sparse_access_method.h:10-48) with a
+// fixed, compiled menu.
+#pragma once
+#include <cmath>
+#include <cstdint>
+
+#include "ss/hash.h"
+
+namespace ss {
+
+enum InitKind : int { kInitZero = 0, kInitUniform = 1, kInitNormal = 2 };
+enum OptKind : int { kOptSGD = 0, kOptAdaGrad = 1, kOptFTRL = 2, kOptAdam = 3 };
+
+struct InitParams {
+  int kind;
+  float scale;       // uniform: (u - 0.5) * scale ; normal: N(0,1) * scale
+  float state_init;  // initial value of every optimizer-state float
+  uint64_t seed;
+};
+
+struct OptParams {
+  int kind;
+  float lr;
+  float l1, l2;
+  float eps;
+  float beta1, beta2;  // Adam
+  float bc1, bc2;      // Adam bias corrections 1/(1-b^t), host-computed per round
+  float ftrl_alpha, ftrl_beta;
+  float grad_scale;    // multiplies incoming gradients
+  float clip;          // |g| clip, 0 = off
+};
+
+SS_HD int opt_state_width(int kind, int dim) {
+  return kind == kOptAdaGrad ? dim : ((kind == kOptFTRL || kind == kOptAdam) ? 2 * dim : 0);
+}
+
+#if defined(__HIP_DEVICE_COMPILE__)
+#define SS_RSQRT(x) __frsqrt_rn(x)
+#define SS_LOGF(x) __logf(x)
+#define SS_COSF(x) __cosf(x)
+#else
+#define SS_RSQRT(x) (1.0f / std::sqrt(x))
+#define SS_LOGF(x) std::log(x)
+#define SS_COSF(x) std::cos(x)
+#endif
+
+// Deterministic per-(key, j) initial value: independent of the inserting lane,
+// the shard layout and the world size, so checkpoints are reproducible.
+SS_HD float init_value(const InitParams& ip, uint64_t key, uint32_t j, uint32_t dim) {
+  (void)dim;
+  if (ip.kind == kInitZero) return 0.0f;
+  const uint64_t r =
+      splitmix64(ip.seed ^ (key * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)j << 48) ^ (uint64_t)j);
+  if (ip.kind == kInitUniform) {
+    // reference word2vec convention: (rand/RAND_MAX - 0.5) / size  (vec1.h:223-226)
+    return (u01(r) - 0.5f) * ip.scale;
+  }
+  float u1 = u01(r);
+  u1 = u1 < 1e-7f ? 1e-7f : u1;
+  const float u2 = u01(splitmix64(r));
+  return std::sqrt(-2.0f * SS_LOGF(u1)) * SS_COSF(6.2831853f * u2) * ip.scale;
+}
+
+// One coordinate of an optimizer step. `row` = params, `st` = state base.
+SS_HD void opt_apply(const OptParams& op, float* row, float* st, uint32_t dim, uint32_t j,
+                     float g) {
+  g *= op.grad_scale;
+  if (op.clip > 0.f) g = g < -op.clip ? -op.clip : (g > op.clip ? op.clip : g);
+  const float w = row[j];
+  switch (op.kind) {
+    case kOptSGD: {
+      g += op.l2 * w;
+      row[j] = w - op.lr * g;
+    } break;
+    case kOptAdaGrad: {
+      g += op.l2 * w;
+      const float h = st[j] + g * g;
+      st[j] = h;
+      row[j] = w - op.lr * g * SS_RSQRT(h + op.eps);
+    } break;
+    case kOptFTRL: {
+      // FTRL-Proximal (per-coordinate); w is kept materialised in the row.
+      float z = st[j];
+      const float n = st[dim + j];
+      const float n2 = n + g * g;
+      const float sigma = (std::sqrt(n2) - std::sqrt(n)) / op.ftrl_alpha;
+      z += g - sigma * w;
+      st[j] = z;
+      st[dim + j] = n2;
+      const float az = std::fabs(z);
+      row[j] = az <= op.l1 ? 0.0f
+                           : -(z - std::copysign(op.l1, z)) /
+                                 ((op.ftrl_beta + std::sqrt(n2)) / op.ftrl_alpha + op.l2);
+    } break;
+    case kOptAdam: {
+      g += op.l2 * w;
+      const float m = op.beta1 * st[j] + (1.f - op.beta1) * g;
+      const float v = op.beta2 * st[dim + j] + (1.f - op.beta2) * g * g;
+      st[j] = m;
+      st[dim + j] = v;
+      row[j] = w - op.lr * (m * op.bc1) / (std::sqrt(v * op.bc2) + op.eps);
+    } break;
+  }
+}
+
+}  // namespace ss

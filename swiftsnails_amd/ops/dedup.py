@@ -88,14 +88,36 @@ class Deduper:
                            self.nranks, n)
 
 
+class CpuDeduper:
+    """Host implementation with the same output layout (CPU engine / tests)."""
+
+    def __init__(self, max_n: int, nranks: int = 1, frag_map: Optional[torch.Tensor] = None,
+                 gdim: int = 1, device=None, with_grad: bool = True):
+        self.max_n, self.nranks, self.gdim = int(max_n), int(nranks), int(gdim)
+        self.ucap = self.max_n
+        self.frag_map = (frag_map.cpu().numpy().astype(np.int64) if frag_map is not None
+                         else np.zeros(1, dtype=np.int64))
+        self.with_grad = with_grad
+
+    def __call__(self, keys: torch.Tensor, stream=None) -> DedupResult:
+        n = keys.numel()
+        if n > self.max_n:
+            raise ValueError(f"dedup: {n} keys > capacity {self.max_n}")
+        uk, uc, inv = dedup_reference(keys.cpu().numpy(), self.nranks, self.frag_map, self.ucap)
+        ug = (torch.zeros((self.nranks * self.ucap, self.gdim), dtype=torch.float32)
+              if self.with_grad else None)
+        return DedupResult(torch.from_numpy(uk.view(np.int64)), torch.from_numpy(uc),
+                           torch.from_numpy(inv.astype(np.int32)), ug, self.ucap, self.nranks, n)
+
+
 def dedup_reference(keys, nranks: int = 1, frag_map: Optional[np.ndarray] = None,
                     ucap: Optional[int] = None):
     """Host reference: returns (ukeys [nranks*ucap] u64, ucount [nranks], inv [n]).
 
     Unique keys inside a destination segment are sorted ascending (the device
     kernel's order is arbitrary; compare as sets + inverse consistency)."""
-    k = np.asarray(keys).view(np.uint64) if np.asarray(keys).dtype == np.int64 else np.asarray(
-        keys, dtype=np.uint64)
+    k = np.asarray(keys)
+    k = k.view(np.uint64) if k.dtype == np.int64 else k.astype(np.uint64)
     n = len(k)
     ucap = ucap or max(n, 1)
     uniq, inv0 = np.unique(k, return_inverse=True)

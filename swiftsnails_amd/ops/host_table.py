@@ -1,0 +1,96 @@
+"""CPU sparse parameter table (C++ ``ss::HostTable`` behind a Python facade).
+
+Same semantics as the HBM table (lookup-or-init pull, optimizer push, text
+checkpoint) using the same ``ss/optim.h`` init/update code; used by CPU
+clusters (reference-style master/server/worker over TCP), by the CPU
+multi-process tests of the collective engine, and as the reference-semantics
+CPU baseline (BASELINE config 1).  Reference: SparseTable
+(/root/reference/src/core/parameter/sparsetable.h:69-121).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .._native import host
+from .optim import INIT_KINDS, OPT_KINDS, InitConfig, Optimizer
+
+
+def _host_init(c: InitConfig):
+    return host().InitParams(INIT_KINDS[c.kind], float(c.scale), float(c.state_init),
+                             int(c.seed) & ((1 << 64) - 1))
+
+
+def _host_opt(o: Optimizer):
+    bc1, bc2 = o.bias_corrections()
+    return host().OptParams(OPT_KINDS[o.kind], o.lr, o.l1, o.l2, o.eps, o.beta1, o.beta2, bc1, bc2,
+                            o.ftrl_alpha, o.ftrl_beta, o.grad_scale, o.clip)
+
+
+def _u64(keys) -> np.ndarray:
+    if isinstance(keys, torch.Tensor):
+        keys = keys.detach().cpu().numpy()
+    a = np.ascontiguousarray(keys)
+    return a.view(np.uint64) if a.dtype == np.int64 else a.astype(np.uint64)
+
+
+class HostTable:
+    device = torch.device("cpu")
+
+    def __init__(self, dim: int, shard_num: int = 8, optimizer: Optional[Optimizer] = None,
+                 init: Optional[InitConfig] = None, nthreads: int = 0):
+        self.dim = int(dim)
+        self.opt = optimizer or Optimizer()
+        self.init_cfg = init or InitConfig()
+        self._t = host().HostTable(self.dim, shard_num, _host_init(self.init_cfg),
+                                   _host_opt(self.opt), nthreads)
+        self.width = self._t.width
+
+    # same surface as HbmTable where it makes sense
+    def pull_keys(self, keys) -> torch.Tensor:
+        return torch.from_numpy(self._t.pull(_u64(keys)))
+
+    def push_keys(self, keys, grads):
+        g = grads.detach().cpu().numpy() if isinstance(grads, torch.Tensor) else np.asarray(grads)
+        self._t.set_opt(_host_opt(self.opt))
+        self._t.push(_u64(keys), np.ascontiguousarray(g, dtype=np.float32).reshape(-1))
+
+    def next_round(self):
+        self.opt.step += 1
+
+    def assign(self, keys, rows):
+        r = rows.detach().cpu().numpy() if isinstance(rows, torch.Tensor) else np.asarray(rows)
+        self._t.assign(_u64(keys), np.ascontiguousarray(r, dtype=np.float32).reshape(-1))
+
+    def export(self, chunk_slots: int = 0, to_host: bool = True):
+        k, r = self._t.export()
+        if len(k):
+            yield torch.from_numpy(k.view(np.int64)), torch.from_numpy(r)
+
+    def size(self) -> int:
+        return self._t.size()
+
+    def check(self):
+        pass
+
+    def write_text(self, path: str, precision: int = 9, with_state: bool = False) -> int:
+        return self._t.write_text(path, precision, with_state)
+
+    def load_text(self, path: str) -> int:
+        return self._t.load_text(path)
+
+    def to_dict(self, with_state: bool = False):
+        out = {}
+        for k, r in self.export():
+            kn, rn = k.numpy().view(np.uint64), r.numpy()
+            for i in range(len(kn)):
+                out[int(kn[i])] = rn[i] if with_state else rn[i, :self.dim]
+        return out
+
+    def __len__(self):
+        return self.size()
+
+    def __repr__(self):
+        return f"HostTable(dim={self.dim}, width={self.width}, opt={self.opt.kind})"
