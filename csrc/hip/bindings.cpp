@@ -48,7 +48,7 @@ static long long seglist_total(const SegList& s) { return s.dev_count ? -1 : s.p
 PYBIND11_MODULE(_ss_hip, m) {
   m.doc() = "SwiftSnails-AMD gfx950 kernels + RCCL communicator";
 
-  py::class_<DevTable>(m, "DevTable")
+  py::class_<DevTable>(m, "DevTable", py::module_local())
       .def(py::init([](uintptr_t base, unsigned long long cap, uint32_t stride, uint32_t key_off,
                        uint32_t dim, uint32_t width) {
              return DevTable{P<char>(base), cap, stride, key_off, dim, width};
@@ -61,14 +61,14 @@ PYBIND11_MODULE(_ss_hip, m) {
       .def_readonly("dim", &DevTable::dim)
       .def_readonly("width", &DevTable::width);
 
-  py::class_<InitParams>(m, "InitParams")
+  py::class_<InitParams>(m, "InitParams", py::module_local())
       .def(py::init([](int kind, float scale, float state_init, uint64_t seed) {
              return InitParams{kind, scale, state_init, seed};
            }),
            py::arg("kind") = 0, py::arg("scale") = 0.f, py::arg("state_init") = 0.f,
            py::arg("seed") = 0);
 
-  py::class_<OptParams>(m, "OptParams")
+  py::class_<OptParams>(m, "OptParams", py::module_local())
       .def(py::init([](int kind, float lr, float l1, float l2, float eps, float beta1, float beta2,
                        float bc1, float bc2, float alpha, float beta, float grad_scale,
                        float clip) {
@@ -80,7 +80,7 @@ PYBIND11_MODULE(_ss_hip, m) {
            py::arg("bc1") = 1.f, py::arg("bc2") = 1.f, py::arg("alpha") = 0.05f,
            py::arg("beta") = 1.f, py::arg("grad_scale") = 1.f, py::arg("clip") = 0.f);
 
-  py::class_<SegList>(m, "SegList")
+  py::class_<SegList>(m, "SegList", py::module_local())
       .def_static("from_host", &make_seglist)
       .def_static("from_device", &make_seglist_dev)
       .def_property_readonly("total", &seglist_total)
@@ -166,7 +166,7 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
 
   // ---- RCCL
-  py::class_<RcclComm>(m, "RcclComm")
+  py::class_<RcclComm>(m, "RcclComm", py::module_local())
       .def(py::init([](int rank, int nranks, py::bytes uid, int device) {
              return new RcclComm(rank, nranks, std::string(uid), device);
            }),

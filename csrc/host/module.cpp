@@ -52,7 +52,7 @@ PYBIND11_MODULE(_ss_host, m) {
   m.def("startswith", &startswith);
 
   // ---- config
-  py::class_<ConfigParser>(m, "ConfigParser")
+  py::class_<ConfigParser>(m, "ConfigParser", py::module_local())
       .def(py::init<>())
       .def(py::init<std::string>())
       .def("load_conf", &ConfigParser::load_conf)
@@ -76,7 +76,7 @@ PYBIND11_MODULE(_ss_host, m) {
   m.def("global_config", &global_config, py::return_value_policy::reference);
 
   // ---- binary codec
-  py::class_<BinaryBuffer>(m, "BinaryBuffer")
+  py::class_<BinaryBuffer>(m, "BinaryBuffer", py::module_local())
       .def(py::init<>())
       .def(py::init([](py::bytes b) { return BinaryBuffer(std::string(b)); }))
       .def("put_i32", [](BinaryBuffer& b, int32_t v) { b << v; })
@@ -99,7 +99,7 @@ PYBIND11_MODULE(_ss_host, m) {
       .def("bytes", [](const BinaryBuffer& b) { return py::bytes(b.str()); });
 
   // ---- router
-  py::class_<HashFrag>(m, "HashFrag")
+  py::class_<HashFrag>(m, "HashFrag", py::module_local())
       .def(py::init<>())
       .def(py::init<int, int>())
       .def("init", &HashFrag::init)
@@ -118,10 +118,10 @@ PYBIND11_MODULE(_ss_host, m) {
       .def_property_readonly("num_frags", &HashFrag::num_frags);
 
   // ---- optimizer params (shared layout with the device module)
-  py::class_<InitParams>(m, "InitParams")
+  py::class_<InitParams>(m, "InitParams", py::module_local())
       .def(py::init(&mk_init), py::arg("kind") = 0, py::arg("scale") = 0.f,
            py::arg("state_init") = 0.f, py::arg("seed") = 0);
-  py::class_<OptParams>(m, "OptParams")
+  py::class_<OptParams>(m, "OptParams", py::module_local())
       .def(py::init(&mk_opt), py::arg("kind") = 1, py::arg("lr") = 0.05f, py::arg("l1") = 0.f,
            py::arg("l2") = 0.f, py::arg("eps") = 1e-8f, py::arg("beta1") = 0.9f,
            py::arg("beta2") = 0.999f, py::arg("bc1") = 1.f, py::arg("bc2") = 1.f,
@@ -129,7 +129,7 @@ PYBIND11_MODULE(_ss_host, m) {
            py::arg("clip") = 0.f);
 
   // ---- CPU table
-  py::class_<HostTable>(m, "HostTable")
+  py::class_<HostTable>(m, "HostTable", py::module_local())
       .def(py::init<int, int, InitParams, OptParams, int, size_t>(), py::arg("dim"),
            py::arg("shard_num"), py::arg("init"), py::arg("opt"), py::arg("nthreads") = 0,
            py::arg("cap_per_shard") = 1024)
@@ -187,7 +187,7 @@ PYBIND11_MODULE(_ss_host, m) {
       .def("is_response", &Request::is_response)
       .def_property("payload", [](const Request& r) { return py::bytes(r.cont.str()); },
                     [](Request& r, py::bytes b) { r.cont = BinaryBuffer(std::string(b)); });
-  py::class_<Transfer>(m, "Transfer")
+  py::class_<Transfer>(m, "Transfer", py::module_local())
       .def(py::init<>())
       .def("listen", &Transfer::listen, py::arg("addr") = "")
       .def("service_start", &Transfer::service_start, py::arg("async_threads") = 4)
@@ -240,7 +240,7 @@ PYBIND11_MODULE(_ss_host, m) {
   m.def("get_local_ip", &get_local_ip);
 
   // ---- cluster roles
-  py::class_<Master>(m, "Master")
+  py::class_<Master>(m, "Master", py::module_local())
       .def(py::init<const ConfigParser&>(), py::keep_alive<1, 2>())
       .def_property_readonly("addr", &Master::addr)
       .def("init", &Master::init, py::call_guard<py::gil_scoped_release>())
@@ -248,7 +248,7 @@ PYBIND11_MODULE(_ss_host, m) {
       .def("run", &Master::run, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("server_num", &Master::server_num)
       .def_property_readonly("worker_num", &Master::worker_num);
-  py::class_<Server>(m, "Server")
+  py::class_<Server>(m, "Server", py::module_local())
       .def(py::init<const ConfigParser&, int>(), py::keep_alive<1, 2>())
       .def("connect", &Server::connect, py::call_guard<py::gil_scoped_release>())
       .def("wait_terminate", &Server::wait_terminate, py::arg("timeout") = 1e9,
@@ -257,7 +257,7 @@ PYBIND11_MODULE(_ss_host, m) {
       .def("backup", &Server::backup)
       .def_property_readonly("push_count", &Server::push_count)
       .def_property_readonly("client_id", &Server::client_id);
-  py::class_<WorkerClient>(m, "WorkerClient")
+  py::class_<WorkerClient>(m, "WorkerClient", py::module_local())
       .def(py::init<const ConfigParser&>(), py::keep_alive<1, 2>())
       .def("connect", &WorkerClient::connect, py::call_guard<py::gil_scoped_release>())
       .def("pull", [](WorkerClient& w, u64arr k) {
@@ -283,7 +283,7 @@ PYBIND11_MODULE(_ss_host, m) {
       .def("hashfrag", [](WorkerClient& w) { return w.hashfrag(); });
 
   // ---- concurrency primitives (exposed for tests / apps)
-  py::class_<ThreadPool>(m, "ThreadPool")
+  py::class_<ThreadPool>(m, "ThreadPool", py::module_local())
       .def(py::init<int>())
       .def("parallel_for", [](ThreadPool& p, int n, std::function<void(int)> f) {
         py::gil_scoped_release rel;
