@@ -63,11 +63,22 @@ def main(argv=None):
     from swiftsnails_amd.parallel.engine import PSEngine
     from swiftsnails_amd.parallel.transport import LoopbackTransport, RcclTransport
 
+    ctrans = None
     if world > 1:
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
         store = dist.distributed_c10d._get_default_store()
-        transport = RcclTransport(rank, world, dev, store=store)
+        try:
+            # two native RCCL communicators: data plane (main stream) and the
+            # route-stage count exchange (route stream)
+            transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
+            ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts")
+        except Exception as e:  # pragma: no cover - hardware dependent
+            from swiftsnails_amd.parallel.transport import TorchDistTransport
+
+            print(f"bench.py: native RCCL communicator failed ({e}); "
+                  "falling back to torch.distributed(nccl=RCCL)", file=sys.stderr)
+            transport = TorchDistTransport(dist.new_group(backend="nccl"))
     else:
         transport = LoopbackTransport()
 
@@ -75,7 +86,8 @@ def main(argv=None):
                     tail_frac=a.tail)
     opt = Optimizer(a.optimizer, lr=a.lr)
     table = make_lr_table(a.features, world, optimizer=opt, load=a.load, device=dev)
-    engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev)
+    engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev,
+                      count_transport=ctrans)
     worker = SparseLRWorker(engine, data, rank=rank, world=world)
 
     def barrier():

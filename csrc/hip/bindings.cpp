@@ -105,6 +105,12 @@ PYBIND11_MODULE(_ss_hip, m) {
     launch_pull_unique(t, P<const uint64_t>(keys), sl, max_n, P<long long>(slots), P<float>(out),
                        ip, P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
   });
+  m.def("pull_claim", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
+                         uintptr_t slots, uintptr_t out, const InitParams& ip, uintptr_t size_ctr,
+                         uintptr_t err, int G, uintptr_t st) {
+    launch_pull_claim(t, P<const uint64_t>(keys), sl, max_n, P<long long>(slots), P<float>(out),
+                      ip, P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
+  });
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
                     long long max_n, const OptParams& op, int G, uintptr_t st) {
     launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st));

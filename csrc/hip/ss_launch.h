@@ -27,6 +27,9 @@ void launch_gather(const DevTable& t, const long long* slots, const SegList& sl,
 void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& sl,
                         long long max_n, long long* slots, float* out, const InitParams& ip,
                         unsigned long long* size_ctr, int* err, int G, hipStream_t st);
+void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
+                       long long max_n, long long* slots, float* out, const InitParams& ip,
+                       unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st);
 void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, long long n,

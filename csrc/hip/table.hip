@@ -165,6 +165,121 @@ __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t*
   if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
 }
 
+// ---------------------------------------------------------------------------
+// CAS-free insert for key lists that are unique within the launch.
+//
+// Measured on MI355X: every device-scope atomic executes at the memory side
+// (the 8 XCD L2s are not coherent), so a 64-bit CAS per new key made the
+// fused pull_unique atomic-throughput bound (1.3M CAS ≈ 320 µs/step).  Here a
+// new key is claimed OPTIMISTICALLY with a plain 8-byte store into the first
+// empty slot of its probe sequence (pass 1); after the kernel boundary, pass 2
+// re-reads the slot: the key that is there owns it (an aligned 8-byte store is
+// single-copy atomic, so a slot holds exactly one of the racing keys), the
+// rare losers finish with the CAS probe (continuing at their slot).  Correct
+// because (a) keys are unique, so a loser's key is nowhere else in the table,
+// (b) slots only ever go EMPTY -> key, so a present key is always met before
+// the first empty slot of its sequence, and (c) pass 2 never plain-stores.
+static constexpr long long kPending = 1ll << 62;
+
+template <int G>
+__global__ __launch_bounds__(256) void k_pull_claim(DevTable t, const uint64_t* __restrict__ keys,
+                                                    SegList sl, long long* __restrict__ slots_out,
+                                                    float* __restrict__ out, int* err) {
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x % G;
+  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
+  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
+       g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    const uint64_t key = keys[pos];
+    long long slot = -1;
+    if (lg == 0) {
+      if (key == kEmptyKey) {
+        atomicOr(err, 2);
+      } else {
+        uint64_t s = fastrange64(table_hash(key), t.cap);
+        for (uint64_t n = 0; n < t.cap; ++n) {
+          uint64_t* kp = slot_key(t, s);
+          const uint64_t k = *kp;
+          if (k == key) {
+            slot = (long long)s;
+            break;
+          }
+          if (k == kEmptyKey) {
+            *kp = key;  // optimistic claim, verified after the kernel boundary
+            slot = (long long)s | kPending;
+            break;
+          }
+          s = (s + 1 == t.cap) ? 0 : s + 1;
+        }
+        if (slot < 0) atomicOr(err, 1);
+      }
+      slots_out[pos] = slot;
+    }
+    if (G > 1) slot = __shfl(slot, 0, G);
+    if (slot >= 0 && !(slot & kPending)) {  // present: gather now
+      const float* row = slot_row(t, slot);
+      float* o = out + pos * (long long)t.dim;
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
+    }
+  }
+}
+
+template <int G>
+__global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t* __restrict__ keys,
+                                                     SegList sl, long long* __restrict__ slots_out,
+                                                     float* __restrict__ out, InitParams ip,
+                                                     unsigned long long* size_ctr, int* err) {
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x % G;
+  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
+  unsigned long long ins = 0;
+  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
+       g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    long long slot = slots_out[pos];
+    if (slot < 0 || !(slot & kPending)) continue;  // group-uniform: same pos per group
+    const uint64_t key = keys[pos];
+    int inserted = 0;
+    if (lg == 0) {
+      slot &= ~kPending;
+      if (*slot_key(t, (uint64_t)slot) == key) {
+        inserted = 1;  // our optimistic claim stood
+      } else {
+        bool b = false;
+        slot = probe_slot(t, key, true, &b);  // lost the race: CAS from here on
+        inserted = b;
+        if (slot < 0) atomicOr(err, 1);
+      }
+      slots_out[pos] = slot;
+    }
+    if (G > 1) {
+      slot = __shfl(slot, 0, G);
+      inserted = __shfl(inserted, 0, G);
+    }
+    float* o = out + pos * (long long)t.dim;
+    if (slot < 0) {
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
+      continue;
+    }
+    float* row = slot_row(t, slot);
+    if (inserted) {
+      for (uint32_t j = lg; j < t.width; j += G) {
+        const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
+        row[j] = v;
+        if (j < t.dim) o[j] = v;
+      }
+    } else {
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
+    }
+    ins += (lg == 0 && inserted);
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+}
+
 // K5: fused optimizer update on resolved slots. Keys inside one launch must be
 // unique (the host launches one segment per source rank, in rank order, so
 // duplicate keys from different workers are applied sequentially — no lost
@@ -291,6 +406,18 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
                                       st, t, keys, sl, slots, out, ip, size_ctr, err));
   check_launch("k_pull_unique");
+}
+
+void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
+                       long long max_n, long long* slots, float* out, const InitParams& ip,
+                       unsigned long long* size_ctr, int* err, int G, hipStream_t st) {
+  if (max_n <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_claim<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
+                                      st, t, keys, sl, slots, out, err));
+  check_launch("k_pull_claim");
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_verify<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
+                                      st, t, keys, sl, slots, out, ip, size_ctr, err));
+  check_launch("k_pull_verify");
 }
 
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,

@@ -20,6 +20,7 @@ it fits a single MI355X's 288 GB with room to spare.
 from __future__ import annotations
 
 import math
+import os
 from typing import Iterator, Optional
 
 import numpy as np
@@ -83,6 +84,9 @@ class HbmTable:
         self.stride, self.key_off = slot_layout(self.width)
         self.G = lane_group or default_lane_group(self.width)
         self.max_load = max_load
+        # unique-key insert: "claim" = optimistic plain-store claim + verify
+        # pass (no device-scope atomics on the hot path); "cas" = 64-bit CAS.
+        self.insert_mode = os.environ.get("SS_TABLE_INSERT", "claim")
         self._alloc(int(capacity))
         self._init_native = self.init_cfg.native()
 
@@ -145,9 +149,9 @@ class HbmTable:
             slots = torch.empty(keys.numel(), dtype=torch.int64, device=self.device)
         sl = segs if segs is not None else self._seg(keys.numel())
         if unique and insert:
-            h.pull_unique(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), out.data_ptr(),
-                          self._init_native, self.size_ctr.data_ptr(), self.err.data_ptr(), self.G,
-                          st)
+            fn = h.pull_unique if self.insert_mode == "cas" else h.pull_claim
+            fn(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), out.data_ptr(),
+               self._init_native, self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, st)
         else:
             h.probe(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), self._init_native,
                     int(insert), self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, st)

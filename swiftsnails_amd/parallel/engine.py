@@ -11,19 +11,27 @@ Reference call stacks being replaced:
 * ``GlobalPushAccess::push_with_barrier`` (global_push_access.h:36-149):
   group (key, grad) per server, server ``apply_push_value`` (server/init.h:115-149).
 
-Here a round is lockstep across ranks:
+A round is lockstep across ranks and split in three stages:
 
-    pull:  dedup+route (1 kernel + inverse) -> [N>1] counts a2a -> keys a2av
-           -> server probe/init/gather -> values a2av back
-    push:  grads a2av -> server apply, one launch per source rank in rank order
+    route (route stream): dedup + route keys into per-rank segments (1 kernel
+                          + inverse); [N>1] counts all-to-all + async D2H
+    pull  (main stream) : [N>1] wait counts; keys a2av -> server
+                          probe/init/gather -> values a2av back
+    push  (main stream) : grads a2av -> server apply, one launch per source
+                          rank in rank order (duplicate keys never race)
 
-On one GPU (world 1) the round needs no host synchronisation at all: the
-unique-key count stays on the device and every kernel reads it there.
+``route`` of step i+1 is enqueued before ``pull`` of step i, on its own HIP
+stream and its own RCCL communicator, so key generation, dedup and the count
+exchange overlap the previous step's compute, and the one host
+synchronisation per round (the counts RCCL needs on the host) is already
+satisfied when ``pull`` asks for it.  Route buffers are a ring of depth 2.
+On one GPU (world 1) no host synchronisation happens at all: the unique-key
+count stays on the device and every kernel reads it there.
 
 Split roles (S servers + W workers) fall out of the same code: non-server
 ranks own no table and receive nothing (the router never maps to them);
-non-worker ranks call ``pull``/``push`` with an empty key set — every rank
-still enters the collective, which is what makes the round lockstep.
+non-worker ranks route an empty key set — every rank still enters the
+collectives, which is what makes the round lockstep.
 
 The same engine runs on CPU (``HostTable`` shards, host dedup, gloo
 transport) — that is how the multi-rank logic is tested without GPUs.
@@ -38,13 +46,23 @@ import torch
 
 from ..ops.dedup import CpuDeduper, DedupResult, Deduper
 from .router import HashFrag
-from .transport import LoopbackTransport, Transport
+from .transport import CountsHandle, LoopbackTransport, Transport
+
+
+@dataclass
+class Routed:
+    """A batch whose keys are deduplicated and routed (stage 1 of a round)."""
+    dd: DedupResult
+    slot: int                               # ring slot of the route buffers
+    counts: Optional[CountsHandle] = None   # N>1: host counts (async)
+    ready: Optional[torch.cuda.Event] = None  # route-stream completion (GPU)
 
 
 @dataclass
 class Round:
     dd: DedupResult
     uvals: torch.Tensor                   # [N*ucap, dim] pulled rows, unique-key order
+    slot: int = 0
     slots: Optional[torch.Tensor] = None  # GPU world-1 path: table slots of ukeys
     scounts: Optional[np.ndarray] = None  # keys this rank sent to each server
     rcounts: Optional[np.ndarray] = None  # keys this rank received from each worker
@@ -73,18 +91,24 @@ def _stream():
 class PSEngine:
     """Worker+server round engine for one rank.
 
-    table         : this rank's shard (``HbmTable``/``HostTable``) or None when not a server
-    transport     : data-plane transport (RCCL on MI355X)
-    max_keys      : max key occurrences per pull on this rank
-    server_ranks  : ranks that host a shard (default: all — colocated mode)
-    frag_num      : number of hash fragments (reference config ``frag_num``)
+    table           : this rank's shard (``HbmTable``/``HostTable``) or None when not a server
+    transport       : data-plane transport (RCCL on MI355X)
+    count_transport : transport for the route-stage count exchange (a second
+                      RCCL communicator on GPU; defaults to ``transport``)
+    max_keys        : max key occurrences per pull on this rank
+    server_ranks    : ranks that host a shard (default: all — colocated mode)
+    frag_num        : number of hash fragments (reference config ``frag_num``)
+    depth           : route-buffer ring depth (2 = one batch of lookahead)
 
-    A ``Round`` aliases engine-owned buffers: it is valid until the next pull.
+    A ``Round`` aliases engine-owned buffers of its ring slot: it is valid
+    until that slot is routed again (``depth`` routes later).
     """
 
     def __init__(self, table, transport: Optional[Transport], max_keys: int, dim: int,
-                 frag_num: int = 0, server_ranks: Optional[Sequence[int]] = None, device=None):
+                 frag_num: int = 0, server_ranks: Optional[Sequence[int]] = None, device=None,
+                 count_transport: Optional[Transport] = None, depth: int = 2):
         self.t = transport or LoopbackTransport()
+        self.ct = count_transport or self.t
         self.rank, self.world = self.t.rank, self.t.world
         self.table = table
         self.dim = int(dim)
@@ -102,42 +126,112 @@ class PSEngine:
         self.router = HashFrag(len(self.server_ranks), frag_num)
         self.frag_map = self.router.rank_map(self.server_ranks)
         self.max_keys = int(max_keys)
+        self.depth = max(1, int(depth))
         dd_cls = Deduper if self.gpu else CpuDeduper
-        self.dedup = dd_cls(self.max_keys, nranks=self.world,
-                            frag_map=torch.from_numpy(self.frag_map.astype(np.int32)),
-                            gdim=self.dim, device=self.device)
+        fm = torch.from_numpy(self.frag_map.astype(np.int32))
+        self.dedupers = [dd_cls(self.max_keys, nranks=self.world, frag_map=fm, gdim=self.dim,
+                                device=self.device) for _ in range(self.depth)]
         N, cap, d = self.world, self.max_keys, self.dim
         dev = self.device
-        self.uvals = torch.empty((N * cap, d), dtype=torch.float32, device=dev)
+        self.uvals = [torch.empty((N * cap, d), dtype=torch.float32, device=dev)
+                      for _ in range(self.depth)]
         self.fast1 = self.gpu and self.world == 1
         if self.fast1:
-            self.slots = torch.empty(cap, dtype=torch.int64, device=dev)
+            self.slots = [torch.empty(cap, dtype=torch.int64, device=dev)
+                          for _ in range(self.depth)]
         else:
-            # server-side receive buffers: one fixed segment per source rank
+            # server-side receive buffers: one fixed segment per source rank.
+            # rslots must survive from pull to push of the same round -> ring.
             self.rkeys = torch.empty(N * cap, dtype=torch.int64, device=dev)
             self.rvals = torch.zeros((N * cap, d), dtype=torch.float32, device=dev)
             self.rgrads = torch.empty((N * cap, d), dtype=torch.float32, device=dev)
             if self.gpu:
-                self.rslots = torch.empty(N * cap, dtype=torch.int64, device=dev)
+                self.rslots = [torch.empty(N * cap, dtype=torch.int64, device=dev)
+                               for _ in range(self.depth)]
+        if self.gpu:
+            self.route_stream = torch.cuda.Stream(device=dev)
+            self._free = [None] * self.depth  # main-stream event: slot buffers released
+            self._pins = [torch.zeros(2 * N, dtype=torch.int64, pin_memory=True)
+                          for _ in range(self.depth)]
         self.displs = [r * cap for r in range(N)]
         self.rounds = 0
+        self._next_slot = 0
 
-    # ----------------------------------------------------------- server side
-    def _server_pull(self, rcounts: np.ndarray) -> None:
+    # ------------------------------------------------------------ stage 1
+    def route(self, keys: Optional[torch.Tensor] = None, produce=None) -> Routed:
+        """Dedup + route a batch on the route stream (non-blocking on GPU).
+
+        Either pass ``keys`` (produced on the current stream), or a
+        ``produce(stream)`` callable that writes and returns the keys on the
+        route stream (e.g. the synthetic data generator)."""
+        slot = self._next_slot
+        self._next_slot = (slot + 1) % self.depth
+        dd_fn = self.dedupers[slot]
+        if not self.gpu:
+            if produce is not None:
+                keys = produce(None)
+            keys = keys.reshape(-1).to(self.device)
+            dd = dd_fn(keys)
+            counts = None if self.world == 1 and self.fast1 else self.ct.exchange_counts_async(
+                dd.ucount)
+            return Routed(dd, slot, counts)
+        rs = self.route_stream
+        main = torch.cuda.current_stream()
+        if self._free[slot] is not None:
+            rs.wait_event(self._free[slot])  # previous user of this slot is done
+        if keys is not None:
+            rs.wait_stream(main)             # keys were produced on the main stream
+        with torch.cuda.stream(rs):
+            if produce is not None:
+                keys = produce(rs)
+            keys = keys.reshape(-1)
+            if keys.device != self.device:
+                keys = keys.to(self.device)
+            dd = dd_fn(keys, stream=rs)
+            counts = None
+            if not self.fast1:
+                counts = self.ct.exchange_counts_async(dd.ucount, pinned=self._pins[slot],
+                                                       stream=rs)
+            ev = torch.cuda.Event()
+            ev.record(rs)
+        return Routed(dd, slot, counts, ev)
+
+    # ------------------------------------------------------------ stage 2
+    def _server_pull(self, rcounts: np.ndarray, slot: int) -> None:
         tab, D = self.table, self.displs
         nrecv = int(rcounts.sum())
         if tab is None or nrecv == 0:
             return
         if self.gpu:
-            tab.pull(self.rkeys, insert=True, unique=False, out=self.rvals, slots=self.rslots,
-                     segs=tab.segs(D, rcounts), max_n=nrecv)
+            tab.pull(self.rkeys, insert=True, unique=False, out=self.rvals,
+                     slots=self.rslots[slot], segs=tab.segs(D, rcounts), max_n=nrecv)
         else:
             for s in range(self.world):
                 c = int(rcounts[s])
                 if c:
                     self.rvals[D[s]:D[s] + c] = tab.pull_keys(self.rkeys[D[s]:D[s] + c])
 
-    def _server_apply(self, rcounts: np.ndarray, resolved: bool) -> None:
+    def pull(self, keys_or_routed) -> Round:
+        r = keys_or_routed if isinstance(keys_or_routed, Routed) else self.route(keys_or_routed)
+        dd, slot = r.dd, r.slot
+        if self.gpu:
+            torch.cuda.current_stream().wait_event(r.ready)
+        tab = self.table
+        uv = self.uvals[slot]
+        if self.fast1:
+            tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
+                     segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
+            return Round(dd, uv, slot, slots=self.slots[slot])
+        scounts, rcounts = r.counts.wait()
+        D = self.displs
+        self.t.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
+        self._server_pull(rcounts, slot)
+        self.t.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
+        return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
+                     stats={"sent": int(scounts.sum()), "recv": int(rcounts.sum())})
+
+    # ------------------------------------------------------------ stage 3
+    def _server_apply(self, rcounts: np.ndarray, slot: int, resolved: bool) -> None:
         """Apply received grads, one source rank at a time in rank order, so
         duplicate keys from different workers never race (no lost updates)."""
         tab, D = self.table, self.displs
@@ -149,36 +243,22 @@ class PSEngine:
                 continue
             if self.gpu:
                 sl = tab.segs([D[s]], [c])
+                rsl = self.rslots[slot]
                 if not resolved:
-                    h = _hip()
-                    h.probe(tab.dt, self.rkeys.data_ptr(), sl, c, self.rslots.data_ptr(),
-                            tab._init_native, 1, tab.size_ctr.data_ptr(), tab.err.data_ptr(),
-                            tab.G, _stream())
-                tab.push_slots(self.rslots, self.rgrads, segs=sl, max_n=c)
+                    _hip().probe(tab.dt, self.rkeys.data_ptr(), sl, c, rsl.data_ptr(),
+                                 tab._init_native, 1, tab.size_ctr.data_ptr(),
+                                 tab.err.data_ptr(), tab.G, _stream())
+                tab.push_slots(rsl, self.rgrads, segs=sl, max_n=c)
             else:
                 tab.push_keys(self.rkeys[D[s]:D[s] + c], self.rgrads[D[s]:D[s] + c])
         tab.next_round()
 
-    # ------------------------------------------------------------------ pull
-    def pull(self, keys: torch.Tensor) -> Round:
-        keys = keys.reshape(-1)
-        if keys.device != self.device:
-            keys = keys.to(self.device)
-        dd = self.dedup(keys)
-        tab = self.table
-        if self.fast1:
-            tab.pull(dd.ukeys, insert=True, unique=True, out=self.uvals, slots=self.slots,
-                     segs=tab.dev_segs(dd.ucount), max_n=max(1, min(keys.numel(), dd.ucap)))
-            return Round(dd, self.uvals, slots=self.slots)
-        scounts, rcounts = self.t.exchange_counts(dd.ucount)
-        D = self.displs
-        self.t.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
-        self._server_pull(rcounts)
-        self.t.alltoallv(self.rvals, rcounts, D, self.uvals, scounts, D, self.dim)
-        return Round(dd, self.uvals, scounts=scounts, rcounts=rcounts,
-                     stats={"sent": int(scounts.sum()), "recv": int(rcounts.sum())})
+    def _release(self, slot: int):
+        if self.gpu:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())
+            self._free[slot] = ev
 
-    # ------------------------------------------------------------------ push
     def push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
         g = rnd.ugrad if grads is None else grads
         tab = self.table
@@ -189,7 +269,8 @@ class PSEngine:
         else:
             D = self.displs
             self.t.alltoallv(g, rnd.scounts, D, self.rgrads, rnd.rcounts, D, self.dim)
-            self._server_apply(rnd.rcounts, resolved=True)
+            self._server_apply(rnd.rcounts, rnd.slot, resolved=True)
+        self._release(rnd.slot)
         rnd.pushed = True
         self.rounds += 1
 
@@ -217,7 +298,9 @@ class PSEngine:
     def pull_dense(self, keys: torch.Tensor) -> torch.Tensor:
         """pull_with_barrier in occurrence order: rows for `keys` ([n, dim])."""
         rnd = self.pull(keys)
-        return self.gather(rnd, keys.numel())
+        out = self.gather(rnd, keys.numel())
+        self._release(rnd.slot)
+        return out
 
     def push_keys(self, keys: torch.Tensor, grads: torch.Tensor) -> None:
         """Stand-alone push of per-occurrence gradients (no pull this round).
@@ -226,27 +309,28 @@ class PSEngine:
         to the server are created with the initialiser before the update (the
         reference CHECK-fails, sparsetable.h:184)."""
         keys = keys.reshape(-1)
-        if keys.device != self.device:
-            keys = keys.to(self.device)
-        grads = grads.to(self.device)
-        dd = self.dedup(keys)
-        rnd = Round(dd, self.uvals)
-        self.accumulate(rnd, grads)
+        r = self.route(keys)
+        if self.gpu:
+            torch.cuda.current_stream().wait_event(r.ready)
+        dd = r.dd
+        rnd = Round(dd, self.uvals[r.slot], r.slot)
+        self.accumulate(rnd, grads.to(self.device))
         tab = self.table
         if self.fast1:
             sl = tab.dev_segs(dd.ucount)
-            n = max(1, min(keys.numel(), dd.ucap))
-            _hip().probe(tab.dt, dd.ukeys.data_ptr(), sl, n, self.slots.data_ptr(),
-                         tab._init_native, 1, tab.size_ctr.data_ptr(), tab.err.data_ptr(), tab.G,
-                         _stream())
-            tab.push_slots(self.slots, dd.ugrad, segs=sl, max_n=n)
+            n = max(1, min(dd.n, dd.ucap))
+            s = self.slots[r.slot]
+            _hip().probe(tab.dt, dd.ukeys.data_ptr(), sl, n, s.data_ptr(), tab._init_native, 1,
+                         tab.size_ctr.data_ptr(), tab.err.data_ptr(), tab.G, _stream())
+            tab.push_slots(s, dd.ugrad, segs=sl, max_n=n)
             tab.next_round()
         else:
-            scounts, rcounts = self.t.exchange_counts(dd.ucount)
+            scounts, rcounts = r.counts.wait()
             D = self.displs
             self.t.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
             self.t.alltoallv(dd.ugrad, scounts, D, self.rgrads, rcounts, D, self.dim)
-            self._server_apply(rcounts, resolved=False)
+            self._server_apply(rcounts, r.slot, resolved=False)
+        self._release(r.slot)
         self.rounds += 1
 
     def barrier(self):

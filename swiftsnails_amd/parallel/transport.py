@@ -25,6 +25,21 @@ import torch
 import torch.distributed as dist
 
 
+class CountsHandle:
+    """Result of an (possibly asynchronous) count exchange."""
+
+    def __init__(self, s: Optional[np.ndarray] = None, r: Optional[np.ndarray] = None,
+                 event=None, pinned: Optional[torch.Tensor] = None, world: int = 1):
+        self._s, self._r, self.event, self.pinned, self.world = s, r, event, pinned, world
+
+    def wait(self) -> tuple[np.ndarray, np.ndarray]:
+        if self._s is None:
+            self.event.synchronize()
+            p = self.pinned.numpy()
+            self._s, self._r = p[:self.world].copy(), p[self.world:2 * self.world].copy()
+        return self._s, self._r
+
+
 class Transport(ABC):
     rank: int = 0
     world: int = 1
@@ -32,6 +47,13 @@ class Transport(ABC):
     @abstractmethod
     def exchange_counts(self, send_counts: torch.Tensor) -> tuple[np.ndarray, np.ndarray]:
         """All-to-all of one int64 per peer. Returns host (send_counts, recv_counts)."""
+
+    def exchange_counts_async(self, send_counts: torch.Tensor, pinned: Optional[torch.Tensor] = None,
+                              stream=None) -> CountsHandle:
+        """Enqueue the count exchange; ``.wait()`` returns host counts.  The
+        default implementation is synchronous."""
+        s, r = self.exchange_counts(send_counts)
+        return CountsHandle(s, r)
 
     @abstractmethod
     def alltoallv(self, send: torch.Tensor, scounts: Sequence[int], sdispls: Sequence[int],
@@ -151,13 +173,23 @@ class RcclTransport(Transport):
         return torch.cuda.current_stream().cuda_stream
 
     def exchange_counts(self, send_counts):
-        s = send_counts.to(torch.int64).contiguous()
-        self.comm.alltoall(s.data_ptr(), self._cnt_recv.data_ptr(), 1, 8, self._st())
-        self._pin[:self.world].copy_(s, non_blocking=True)
-        self._pin[self.world:].copy_(self._cnt_recv, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
-        p = self._pin.numpy()
-        return p[:self.world].copy(), p[self.world:].copy()
+        return self.exchange_counts_async(send_counts).wait()
+
+    def exchange_counts_async(self, send_counts, pinned=None, stream=None):
+        """Counts all-to-all + D2H into pinned memory on `stream`; the host
+        only blocks in ``wait()`` (on an event), so the exchange overlaps with
+        whatever the other streams are running."""
+        st = stream or torch.cuda.current_stream()
+        pin = pinned if pinned is not None else self._pin
+        with torch.cuda.stream(st):
+            s = send_counts.to(torch.int64).contiguous()
+            recv = torch.empty(self.world, dtype=torch.int64, device=self.device)
+            self.comm.alltoall(s.data_ptr(), recv.data_ptr(), 1, 8, st.cuda_stream)
+            pin[:self.world].copy_(s, non_blocking=True)
+            pin[self.world:2 * self.world].copy_(recv, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        return CountsHandle(event=ev, pinned=pin, world=self.world)
 
     def alltoallv(self, send, scounts, sdispls, recv, rcounts, rdispls, row_elems=1):
         eb = send.element_size() * row_elems

@@ -235,3 +235,33 @@ def test_rccl_comm_world1(dev):
     c.allreduce(a.data_ptr(), a.data_ptr(), 10, 0, 0, st)
     torch.cuda.synchronize()
     np.testing.assert_array_equal(b.cpu().numpy()[5:9], [2, 3, 4, 5])
+
+
+@pytest.mark.parametrize("mode", ["claim", "cas"])
+@pytest.mark.parametrize("G,load", [(1, 0.9), (4, 0.5), (64, 0.95)])
+def test_pull_unique_insert_modes(dev, mode, G, load):
+    """Unique-key pull: optimistic claim+verify (and CAS) under heavy collisions."""
+    from swiftsnails_amd.ops.optim import InitConfig, init_reference
+    from swiftsnails_amd.ops.table import HbmTable
+
+    init = InitConfig("uniform", 1.0, 0.0, seed=11)
+    n = 20000
+    t = HbmTable(2, int(n / load) + 1, init=init, device=dev, lane_group=G)
+    t.insert_mode = mode
+    k = np.unique(_keys(n + 500, 12))[:n]
+    rng = np.random.default_rng(13)
+    # two overlapping rounds: half old keys, half new keys in round 2
+    k1 = k[: n // 2]
+    k2 = np.concatenate([k[n // 4: n // 2], k[n // 2:]])
+    rng.shuffle(k2)
+    v1, s1 = t.pull(torch.from_numpy(k1).to(dev), unique=True)
+    v2, s2 = t.pull(torch.from_numpy(k2).to(dev), unique=True)
+    torch.cuda.synchronize()
+    t.check()
+    assert t.size() == n
+    np.testing.assert_array_equal(v1.cpu().numpy(), init_reference(init, k1, 2, 2)[:, :2])
+    np.testing.assert_array_equal(v2.cpu().numpy(), init_reference(init, k2, 2, 2)[:, :2])
+    s2n = s2.cpu().numpy()
+    assert (s2n >= 0).all() and len(np.unique(s2n)) == len(k2)
+    d = t.to_dict()
+    assert len(d) == n and set(d) == set(int(x) for x in k.view(np.uint64))
