@@ -62,11 +62,11 @@ PYBIND11_MODULE(_ss_hip, m) {
       .def_readonly("width", &DevTable::width);
 
   py::class_<InitParams>(m, "InitParams", py::module_local())
-      .def(py::init([](int kind, float scale, float state_init, uint64_t seed) {
-             return InitParams{kind, scale, state_init, seed};
+      .def(py::init([](int kind, float scale, float state_init, uint64_t seed, int zero_bit) {
+             return InitParams{kind, scale, state_init, seed, zero_bit};
            }),
            py::arg("kind") = 0, py::arg("scale") = 0.f, py::arg("state_init") = 0.f,
-           py::arg("seed") = 0);
+           py::arg("seed") = 0, py::arg("zero_bit") = -1);
 
   py::class_<OptParams>(m, "OptParams", py::module_local())
       .def(py::init([](int kind, float lr, float l1, float l2, float eps, float beta1, float beta2,
@@ -170,6 +170,24 @@ PYBIND11_MODULE(_ss_hip, m) {
                       P<const float>(uvals), P<float>(ugrad), P<float>(loss_sum), P<float>(pred),
                       S(st));
   });
+
+  m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
+                         uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {
+    launch_fm_fwd_bwd(P<const uint32_t>(inv), P<const float>(labels), B, F, dim,
+                      P<const float>(uvals), P<float>(ugrad), P<float>(loss), P<float>(pred),
+                      S(st));
+  });
+  m.def("w2v_sgns", [](uintptr_t inv_c, uintptr_t inv_x, uintptr_t inv_n, int B, int C, int D,
+                       float neg_scale, uintptr_t uvals, uintptr_t ugrad, uintptr_t loss,
+                       uintptr_t st) {
+    launch_w2v_sgns(P<const uint32_t>(inv_c), P<const uint32_t>(inv_x), P<const uint32_t>(inv_n), B,
+                    C, D, neg_scale, P<const float>(uvals), P<float>(ugrad), P<float>(loss), S(st));
+  });
+  m.def("w2v_gen", [](uint64_t seed, long long base, int B, int C, int W, long long nneg,
+                      long long V, float noise, uintptr_t keys, uintptr_t st) {
+    launch_w2v_gen(seed, base, B, C, W, nneg, V, noise, P<uint64_t>(keys), S(st));
+  });
+  m.def("w2v_smem_bytes", &w2v_smem_bytes);
 
   // ---- RCCL
   py::class_<RcclComm>(m, "RcclComm", py::module_local())

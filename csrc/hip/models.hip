@@ -116,6 +116,96 @@ __global__ __launch_bounds__(256) void k_lr_fwd_bwd(const uint32_t* __restrict__
   if (active && u != kInvalidU) atomicAdd(ugrad + u, sg[ls] * x);
 }
 
+// Factorization machine (binary features) fused forward/backward.
+// Row of a key = [w | v_0..v_{K-1}] (dim = 1 + K).  Per sample
+//   z = sum_i w_i + 1/2 * sum_f [(sum_i v_if)^2 - sum_i v_if^2]
+//   dz/dw_i = 1, dz/dv_if = s_f - v_if  with s_f = sum_i v_if
+// One lane per (sample, field) occurrence; per-sample sums in LDS; the
+// per-key gradient rows (dim contiguous floats) leave as row atomics.
+template <int DIM>
+__global__ __launch_bounds__(256) void k_fm_fwd_bwd(const uint32_t* __restrict__ inv,
+                                                    const float* __restrict__ labels, int B, int F,
+                                                    const float* __restrict__ uvals,
+                                                    float* __restrict__ ugrad,
+                                                    float* __restrict__ loss_sum,
+                                                    float* __restrict__ pred) {
+  constexpr int K = DIM - 1;
+  __shared__ float ssum[256 / 2][K > 0 ? K : 1];  // spb <= 128 (F >= 2)
+  __shared__ float sz[128];
+  __shared__ float sg[128];
+  __shared__ float sloss[4];
+  const int spb = samples_per_block(F);
+  const int t = threadIdx.x, ls = t / F;
+  const long long s0 = (long long)blockIdx.x * spb;
+  for (int e = t; e < spb * K; e += 256) ssum[e / K][e % K] = 0.f;
+  if (t < spb) sz[t] = 0.f;
+  __syncthreads();
+  const bool active = ls < spb && s0 + ls < B;
+  const long long j = s0 * F + t;
+  uint32_t u = kInvalidU;
+  float row[DIM];
+  if (active) u = inv[j];
+  if (active && u != kInvalidU) {
+    const float* r = uvals + (long long)u * DIM;
+#pragma unroll
+    for (int d = 0; d < DIM; ++d) row[d] = r[d];
+    float sq = 0.f;
+#pragma unroll
+    for (int f = 0; f < K; ++f) {
+      atomicAdd(&ssum[ls][f], row[1 + f]);
+      sq += row[1 + f] * row[1 + f];
+    }
+    atomicAdd(&sz[ls], row[0] - 0.5f * sq);
+  }
+  __syncthreads();
+  float l = 0.f;
+  if (t < spb && s0 + t < B) {
+    float z = sz[t];
+#pragma unroll
+    for (int f = 0; f < K; ++f) z += 0.5f * ssum[t][f] * ssum[t][f];
+    const float y = labels[s0 + t];
+    const float p = 1.f / (1.f + __expf(-z));
+    sg[t] = p - y;
+    if (pred) pred[s0 + t] = p;
+    l = fmaxf(z, 0.f) + __logf(1.f + __expf(-fabsf(z))) - y * z;
+  }
+  for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, 64);
+  if ((t & 63) == 0) sloss[t >> 6] = l;
+  __syncthreads();
+  if (t == 0 && loss_sum) atomicAdd(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
+  if (active && u != kInvalidU) {
+    const float g = sg[ls];
+    float* gr = ugrad + (long long)u * DIM;
+    atomicAdd(gr, g);
+#pragma unroll
+    for (int f = 0; f < K; ++f) atomicAdd(gr + 1 + f, g * (ssum[ls][f] - row[1 + f]));
+  }
+}
+
+void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, int dim,
+                       const float* uvals, float* ugrad, float* loss_sum, float* pred,
+                       hipStream_t st) {
+  if (B <= 0) return;
+  if (F < 2 || F > 256) throw_error("fm_fwd_bwd: F must be in [2,256]");
+  const int spb = samples_per_block(F);
+  const int blocks = (B + spb - 1) / spb;
+  switch (dim) {
+#define SS_FM_CASE(DD)                                                                       \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL(k_fm_fwd_bwd<DD>, dim3(blocks), dim3(256), 0, st, inv, labels, B, F, uvals, \
+                       ugrad, loss_sum, pred);                                               \
+    break;
+    SS_FM_CASE(2)
+    SS_FM_CASE(5)
+    SS_FM_CASE(9)
+    SS_FM_CASE(17)
+#undef SS_FM_CASE
+    default:
+      throw_error("fm_fwd_bwd: dim must be 1+K with K in {1,4,8,16}");
+  }
+  check_launch("k_fm_fwd_bwd");
+}
+
 void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long long vocab_per_field,
                     float tail_frac, float truth_scale, float truth_bias, uint64_t* keys,
                     float* labels, hipStream_t st) {

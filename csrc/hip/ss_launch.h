@@ -65,4 +65,16 @@ void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labe
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
                        hipStream_t st);
 
+void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, int dim,
+                       const float* uvals, float* ugrad, float* loss_sum, float* pred,
+                       hipStream_t st);
+
+// --- w2v.hip
+size_t w2v_smem_bytes(int D);
+void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
+                     int C, int D, float neg_scale, const float* uvals, float* ugrad,
+                     float* loss_sum, hipStream_t st);
+void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,
+                    long long V, float noise, uint64_t* keys, hipStream_t st);
+
 }  // namespace ss

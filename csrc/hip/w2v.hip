@@ -1,0 +1,224 @@
+// w2v.hip — word2vec skip-gram with negative sampling on the parameter server.
+//
+// The reference names a word2vec app as its default binary but does not ship
+// it (/root/reference/src/tools/copy_exec.sh:4-9, distribute.sh:9); its test
+// corpus generator is src/tools/gen-word2vec-data.py and its dense helper is
+// utils/vec1.h (Vec::dot, randInit (rand/RAND_MAX-0.5)/size).  This is that
+// workload designed for CDNA4:
+//
+//   * keys: center words in the input namespace (syn0 = word id), context
+//     and negative words in the output namespace (syn1neg = id | 1<<40,
+//     zero-initialised through InitParams.zero_bit);
+//   * one 256-thread workgroup = a tile of T=64 centers, each with C context
+//     words, plus S=64 negatives SHARED by the tile ("shared negative
+//     sampling"): the negative part becomes three small GEMMs —
+//         S  = V·Nᵀ   (64×64, K=D)      scores
+//         gV = G·N    (64×D,  K=64)     center grads
+//         gN = Gᵀ·V   (64×D,  K=64)     negative grads
+//     run on the f32-input MFMA (v_mfma_f32_32x32x2_f32, exact fp32) out of
+//     LDS (rows padded by one float: conflict-free column reads);
+//   * positive (center, context) pairs are row dot products (wave shuffle
+//     reduce), context-row gradients go out as coalesced row atomics;
+//   * all gradient rows leave the kernel as float atomics shaped as whole
+//     128-B row segments (the full-rate atomic shape on MI355X).
+#include "ss_device.h"
+#include "ss_launch.h"
+
+namespace ss {
+
+static constexpr uint32_t kInv = 0xFFFFFFFFu;
+static constexpr int kT = 64;  // centers per tile
+static constexpr int kS = 64;  // shared negatives per tile
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float softplus(float x) {
+  return fmaxf(x, 0.f) + __logf(1.f + __expf(-fabsf(x)));
+}
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// 32x32 C/D map of v_mfma_f32_32x32x* (cdna_hip_programming.md §3):
+// col = lane&31, row = (r&3) + 8*(r>>2) + 4*(lane>>5)
+__device__ __forceinline__ int mrow(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
+
+template <int D>
+__global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ inv_c,
+                                                  const uint32_t* __restrict__ inv_x,
+                                                  const uint32_t* __restrict__ inv_n, int B, int C,
+                                                  float neg_scale, const float* __restrict__ uvals,
+                                                  float* __restrict__ ugrad,
+                                                  float* __restrict__ loss_sum) {
+  constexpr int P = D + 1;  // padded LDS row
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Vs = smem;              // [T][P] center rows
+  float* Ns = Vs + kT * P;       // [S][P] negative rows
+  float* Gv = Ns + kS * P;       // [T][P] positive-part center grads
+  float* Gs = Gv + kT * P;       // [T][S+1] negative score grads
+  float* red = Gs + kT * (kS + 1);  // [4] loss partials
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long t0 = (long long)blockIdx.x * kT;
+  __shared__ uint32_t rc[kT], rn[kS];
+  if (tid < kT) rc[tid] = (t0 + tid < B) ? inv_c[t0 + tid] : kInv;
+  else if (tid < kT + kS) rn[tid - kT] = inv_n[(long long)blockIdx.x * kS + (tid - kT)];
+  __syncthreads();
+  // gather center / negative rows into LDS, zero the positive-grad tile
+  for (int e = tid; e < kT * D; e += 256) {
+    const int r = e / D, d = e - r * D;
+    Vs[r * P + d] = rc[r] == kInv ? 0.f : uvals[(long long)rc[r] * D + d];
+    Ns[r * P + d] = rn[r] == kInv ? 0.f : uvals[(long long)rn[r] * D + d];
+    Gv[r * P + d] = 0.f;
+  }
+  __syncthreads();
+
+  float loss = 0.f;
+  // ---- negative scores S = V·Nᵀ: wave w owns quadrant (w>>1, w&1)
+  {
+    const int i0 = (w >> 1) * 32, j0 = (w & 1) * 32;
+    f32x16 acc = {};
+    const int ar = i0 + (lane & 31), kk = lane >> 5;
+#pragma unroll 8
+    for (int k0 = 0; k0 < D; k0 += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Vs[ar * P + k0 + kk], Ns[(j0 + (lane & 31)) * P + k0 + kk],
+                                                 acc, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = i0 + mrow(r, lane), col = j0 + (lane & 31);
+      const bool ok = rc[row] != kInv && rn[col] != kInv;
+      const float s = acc[r];
+      Gs[row * (kS + 1) + col] = ok ? neg_scale * sigm(s) : 0.f;  // d/ds softplus(s)
+      if (ok) loss += neg_scale * softplus(s);
+    }
+  }
+  // ---- positive pairs: wave w owns centers [16w, 16w+16)
+  for (int t = w * 16; t < w * 16 + 16; ++t) {
+    if (rc[t] == kInv) continue;  // wave-uniform
+    for (int j = 0; j < C; ++j) {
+      const uint32_t x = inv_x[(t0 + t) * (long long)C + j];
+      if (x == kInv) continue;
+      const float* u = uvals + (long long)x * D;
+      float part = 0.f;
+      for (int d = lane; d < D; d += 64) part += Vs[t * P + d] * u[d];
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+      const float g = sigm(part) - 1.f;  // d/ds softplus(-s)
+      if (lane == 0) loss += softplus(-part);
+      float* gu = ugrad + (long long)x * D;
+      for (int d = lane; d < D; d += 64) {
+        atomicAdd(gu + d, g * Vs[t * P + d]);
+        Gv[t * P + d] += g * u[d];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- gV = G·N (+ positive part) and gN = Gᵀ·V: (2 x D/32) tiles each
+  constexpr int NT = 2 * (D / 32);
+  for (int tt = w; tt < 2 * NT; tt += 4) {
+    const bool center = tt < NT;
+    const int q = center ? tt : tt - NT;
+    const int ti = q / (D / 32), tj = q % (D / 32);
+    f32x16 acc = {};
+    const int kk = lane >> 5, li = lane & 31;
+    if (center) {
+#pragma unroll 8
+      for (int k0 = 0; k0 < kS; k0 += 2)  // A[i][k]=G[ti*32+i][k], B[k][j]=N[k][tj*32+j]
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Gs[(ti * 32 + li) * (kS + 1) + k0 + kk],
+                                                   Ns[(k0 + kk) * P + tj * 32 + li], acc, 0, 0, 0);
+    } else {
+#pragma unroll 8
+      for (int k0 = 0; k0 < kT; k0 += 2)  // A[i][k]=G[k][ti*32+i], B[k][j]=V[k][tj*32+j]
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Gs[(k0 + kk) * (kS + 1) + ti * 32 + li],
+                                                   Vs[(k0 + kk) * P + tj * 32 + li], acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = ti * 32 + mrow(r, lane), col = tj * 32 + li;
+      const uint32_t dst = center ? rc[row] : rn[row];
+      if (dst == kInv) continue;
+      const float v = acc[r] + (center ? Gv[row * P + col] : 0.f);
+      atomicAdd(ugrad + (long long)dst * D + col, v);  // lanes 0-31 / 32-63: two 128-B rows
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) loss += __shfl_down(loss, o, 64);
+  if (lane == 0) red[w] = loss;
+  __syncthreads();
+  if (tid == 0 && loss_sum) atomicAdd(loss_sum, red[0] + red[1] + red[2] + red[3]);
+}
+
+// Synthetic skip-gram batches. Centers are Zipf-like (log-uniform) over V
+// words; a context sits within +-W ids of its center (words with nearby ids
+// co-occur: learnable structure) except with probability `noise`; negatives
+// are drawn from the same unigram-like distribution.  keys = [centers B]
+// [contexts B*C][negatives ntile*S], contexts/negatives in namespace 1<<40.
+__global__ __launch_bounds__(256) void k_w2v_gen(uint64_t seed, long long base, int B, int C, int W,
+                                                 long long nneg, long long V, double logV,
+                                                 float noise, uint64_t* __restrict__ keys) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long n = (long long)B + (long long)B * C + nneg;
+  if (i >= n) return;
+  auto zipf = [&](uint64_t r) -> uint64_t {
+    const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+    long long v = (long long)exp(u * logV) - 1;
+    return (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
+  };
+  const uint64_t kOut = 1ull << 40;
+  if (i < B) {
+    keys[i] = zipf(splitmix64(seed ^ ((uint64_t)(base + i) * 0xA24BAED4963EE407ull)));
+  } else if (i < B + (long long)B * C) {
+    const long long p = i - B, b = p / C;
+    const uint64_t c = zipf(splitmix64(seed ^ ((uint64_t)(base + b) * 0xA24BAED4963EE407ull)));
+    const uint64_t r = splitmix64(seed ^ 0xC0FFEEull ^ ((uint64_t)(base * C + p) * 0x9E3779B97F4A7C15ull));
+    uint64_t x;
+    if (u01(r) < noise) {
+      x = zipf(splitmix64(r));
+    } else {
+      const long long off = 1 + (long long)(splitmix64(r ^ 1) % (uint64_t)W);
+      const long long s = (r >> 7) & 1 ? off : -off;
+      x = (uint64_t)((((long long)c + s) % V + V) % V);
+    }
+    keys[i] = x | kOut;
+  } else {
+    const long long q = i - B - (long long)B * C;
+    keys[i] = zipf(splitmix64(seed ^ 0xBADC0DEull ^ ((uint64_t)(base + q) * 0xD1B54A32D192ED03ull))) | kOut;
+  }
+}
+
+size_t w2v_smem_bytes(int D) {
+  const int P = D + 1;
+  return sizeof(float) * ((size_t)3 * kT * P + (size_t)kT * (kS + 1) + 4);
+}
+
+void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
+                     int C, int D, float neg_scale, const float* uvals, float* ugrad,
+                     float* loss_sum, hipStream_t st) {
+  if (B <= 0) return;
+  const int tiles = (B + kT - 1) / kT;
+  const size_t sm = w2v_smem_bytes(D);
+  switch (D) {
+#define SS_W2V_CASE(DD)                                                                     \
+  case DD:                                                                                  \
+    check_hip(hipFuncSetAttribute((const void*)k_w2v_sgns<DD>,                               \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm),    \
+              "w2v smem attr");                                                             \
+    hipLaunchKernelGGL(k_w2v_sgns<DD>, dim3(tiles), dim3(256), sm, st, inv_c, inv_x, inv_n, B, C, \
+                       neg_scale, uvals, ugrad, loss_sum);                                  \
+    break;
+    SS_W2V_CASE(32)
+    SS_W2V_CASE(64)
+    SS_W2V_CASE(128)
+#undef SS_W2V_CASE
+    default:
+      throw_error("w2v_sgns: D must be 32, 64 or 128");
+  }
+  check_launch("k_w2v_sgns");
+}
+
+void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,
+                    long long V, float noise, uint64_t* keys, hipStream_t st) {
+  const long long n = (long long)B + (long long)B * C + nneg;
+  if (n <= 0) return;
+  if (W < 1) throw_error("w2v_gen: window must be >= 1");
+  hipLaunchKernelGGL(k_w2v_gen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed, base, B,
+                     C, W, nneg, V, log((double)V + 1.0), noise, keys);
+  check_launch("k_w2v_gen");
+}
+
+}  // namespace ss

@@ -70,7 +70,7 @@ struct RouteTable {
 
 inline InitParams init_from_config(const ConfigParser& c) {
   const std::string k = c.get("param_init", "zero");
-  InitParams ip{kInitZero, 0.f, 0.f, 2015};
+  InitParams ip{kInitZero, 0.f, 0.f, 2015, -1};
   ip.kind = k == "uniform" ? kInitUniform : (k == "normal" ? kInitNormal : kInitZero);
   ip.scale = std::stof(c.get("param_init_scale", "0"));
   ip.state_init = std::stof(c.get("optimizer_state_init", "0"));

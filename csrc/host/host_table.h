@@ -61,7 +61,7 @@ class HostShard : NonCopyable {
     return nullptr;
   }
   void assign(uint64_t key, const float* row) {
-    float* r = find_or_insert(key, InitParams{kInitZero, 0.f, 0.f, 0}, nullptr);
+    float* r = find_or_insert(key, InitParams{kInitZero, 0.f, 0.f, 0, -1}, nullptr);
     std::copy(row, row + width_, r);
   }
   template <class F>

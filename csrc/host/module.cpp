@@ -22,8 +22,8 @@ using namespace ss;
 using u64arr = py::array_t<uint64_t, py::array::c_style | py::array::forcecast>;
 using f32arr = py::array_t<float, py::array::c_style | py::array::forcecast>;
 
-static InitParams mk_init(int kind, float scale, float state_init, uint64_t seed) {
-  return InitParams{kind, scale, state_init, seed};
+static InitParams mk_init(int kind, float scale, float state_init, uint64_t seed, int zero_bit) {
+  return InitParams{kind, scale, state_init, seed, zero_bit};
 }
 static OptParams mk_opt(int kind, float lr, float l1, float l2, float eps, float beta1, float beta2,
                         float bc1, float bc2, float alpha, float beta, float grad_scale,
@@ -120,7 +120,7 @@ PYBIND11_MODULE(_ss_host, m) {
   // ---- optimizer params (shared layout with the device module)
   py::class_<InitParams>(m, "InitParams", py::module_local())
       .def(py::init(&mk_init), py::arg("kind") = 0, py::arg("scale") = 0.f,
-           py::arg("state_init") = 0.f, py::arg("seed") = 0);
+           py::arg("state_init") = 0.f, py::arg("seed") = 0, py::arg("zero_bit") = -1);
   py::class_<OptParams>(m, "OptParams", py::module_local())
       .def(py::init(&mk_opt), py::arg("kind") = 1, py::arg("lr") = 0.05f, py::arg("l1") = 0.f,
            py::arg("l2") = 0.f, py::arg("eps") = 1e-8f, py::arg("beta1") = 0.9f,

@@ -22,6 +22,8 @@ struct InitParams {
   float scale;       // uniform: (u - 0.5) * scale ; normal: N(0,1) * scale
   float state_init;  // initial value of every optimizer-state float
   uint64_t seed;
+  int zero_bit;      // keys with this bit set start at zero (-1: none) — e.g. the
+                     // word2vec output-embedding namespace (syn1neg starts at 0)
 };
 
 struct OptParams {
@@ -55,6 +57,7 @@ SS_HD int opt_state_width(int kind, int dim) {
 SS_HD float init_value(const InitParams& ip, uint64_t key, uint32_t j, uint32_t dim) {
   (void)dim;
   if (ip.kind == kInitZero) return 0.0f;
+  if (ip.zero_bit >= 0 && ((key >> ip.zero_bit) & 1ull)) return 0.0f;
   const uint64_t r =
       splitmix64(ip.seed ^ (key * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)j << 48) ^ (uint64_t)j);
   if (ip.kind == kInitUniform) {

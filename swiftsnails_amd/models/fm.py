@@ -1,0 +1,95 @@
+"""Factorization machine on a wide embedding table (BASELINE config 5:
+FM-style wide table, 10B keys sharded across 8x288 GB HBM, async AdaGrad).
+
+Each key's row is ``[w | v_0..v_{K-1}]`` (dim = 1 + K) — the second-order FM
+of Rendle (2010) with binary features:
+
+    z = sum_i w_i + 1/2 * sum_f [(sum_i v_if)^2 - sum_i v_if^2]
+
+Sizing (``HbmTable.plan``): 10B keys, K=8, AdaGrad -> width 18 floats,
+80-byte slots; 10e9/8 shards/0.7 load = 1.79e9 slots = 143 GB per MI355X,
+well inside 288 GB (``plan_fm_table`` reports this).  "Async" here means the
+reference's Hogwild semantics carried over: workers never wait for each
+other beyond the lockstep collective round.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .._native import hip
+from ..ops.optim import InitConfig, Optimizer
+from ..ops.table import HbmTable
+from .sparse_lr import CtrSynth
+
+
+def fm_table_args(k: int, optimizer: Optional[Optimizer] = None):
+    opt = optimizer or Optimizer("adagrad", lr=0.05)
+    init = InitConfig("normal", scale=0.01, state_init=0.0)
+    return opt, init
+
+
+def plan_fm_table(n_keys: int, k: int = 8, shards: int = 8, load: float = 0.7) -> dict:
+    p = HbmTable.plan(n_keys // shards, 1 + k, Optimizer("adagrad"), load)
+    p["GB_per_shard"] = round(p["bytes"] / 1e9, 1)
+    return p
+
+
+class FMWorker:
+    def __init__(self, engine, data: CtrSynth, rank: int = 0, world: int = 1):
+        if engine.dim not in (2, 5, 9, 17):
+            raise ValueError("FMWorker: dim must be 1+K with K in {1,4,8,16}")
+        self.engine, self.data, self.rank, self.world = engine, data, rank, world
+        dev = engine.device
+        B, F = data.batch_size, data.num_fields
+        self.keys = [torch.empty(B * F, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
+        self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_idx = 0
+        self._next = None
+
+    def _route(self, step: int):
+        slot = self.engine._next_slot
+
+        def produce(stream):
+            self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
+                               stream=stream.cuda_stream if stream is not None else None)
+            return self.keys[slot]
+
+        return self.engine.route(produce=produce)
+
+    def step(self) -> torch.Tensor:
+        d = self.data
+        r = self._next if self._next is not None else self._route(self.step_idx)
+        self._next = self._route(self.step_idx + 1)
+        rnd = self.engine.pull(r)
+        self.loss_sum.zero_()
+        hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[r.slot].data_ptr(), d.batch_size,
+                         d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
+                         rnd.ugrad.data_ptr(), self.loss_sum.data_ptr(), 0,
+                         torch.cuda.current_stream().cuda_stream)
+        self.engine.push(rnd)
+        self.step_idx += 1
+        return self.loss_sum
+
+    def mean_loss(self) -> float:
+        return float(self.loss_sum.item()) / self.data.batch_size
+
+
+def fm_reference(rows: np.ndarray, labels: np.ndarray):
+    """fp64 reference for one batch. rows [B, F, dim] (occurrence rows).
+    Returns (loss_sum, pred [B], grad rows [B, F, dim])."""
+    R = rows.astype(np.float64)
+    w, v = R[..., 0], R[..., 1:]
+    s = v.sum(1)                                   # [B, K]
+    z = w.sum(1) + 0.5 * ((s ** 2).sum(1) - (v ** 2).sum((1, 2)))
+    p = 1.0 / (1.0 + np.exp(-z))
+    y = labels.astype(np.float64)
+    loss = float(np.sum(np.maximum(z, 0) + np.log1p(np.exp(-np.abs(z))) - y * z))
+    g = (p - y)[:, None, None]
+    grad = np.empty_like(R)
+    grad[..., 0] = g[..., 0]
+    grad[..., 1:] = g * (s[:, None, :] - v)
+    return loss, p, grad

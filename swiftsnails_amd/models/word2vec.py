@@ -1,0 +1,128 @@
+"""word2vec skip-gram with (shared) negative sampling on the parameter server.
+
+BASELINE config 3: 1M-vocab synthetic corpus, 4 servers + 4 workers on 4
+MI355X.  The reference's word2vec app is absent from the snapshot (named by
+/root/reference/src/tools/copy_exec.sh:4-9); its corpus generator
+(src/tools/gen-word2vec-data.py: lines of 6-15 random word ids) is mirrored by
+``W2VSynth`` at scale, and the dense-vector math of utils/vec1.h (dot, scaled
+add, random init (u-0.5)/size) lives in the fused ``k_w2v_sgns`` kernel
+(csrc/hip/w2v.hip) which runs the shared-negative GEMMs on MFMA.
+
+Parameters: one table of ``dim``-float rows.  Input vectors (syn0) are keyed
+by the word id, output vectors (syn1neg) by ``id | 1<<40``; the output
+namespace starts at zero (``InitConfig.zero_key_bit=40``), the input one at
+``(u-0.5)/dim`` like the reference's Vec::randInit.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .._native import hip
+from ..ops.optim import InitConfig, Optimizer
+
+OUT_BIT = 40
+TILE = 64      # centers per workgroup tile
+NEG_TILE = 64  # shared negatives per tile
+
+
+@dataclass
+class W2VSynth:
+    batch_size: int = 16384        # centers per step per worker (multiple of 64)
+    window: int = 5                # contexts per center = 2*window
+    vocab: int = 1_000_000
+    noise: float = 0.1
+    negatives: int = 5             # K negatives per positive pair (sets the shared-negative weight)
+    seed: int = 1234
+
+    @property
+    def contexts(self) -> int:
+        return 2 * self.window
+
+    @property
+    def tiles(self) -> int:
+        return (self.batch_size + TILE - 1) // TILE
+
+    @property
+    def n_keys(self) -> int:
+        return self.batch_size * (1 + self.contexts) + self.tiles * NEG_TILE
+
+    @property
+    def neg_scale(self) -> float:
+        return self.contexts * self.negatives / NEG_TILE
+
+    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None):
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        base = (step * world + rank) * self.batch_size
+        hip().w2v_gen(self.seed, base, self.batch_size, self.contexts, self.window,
+                      self.tiles * NEG_TILE, self.vocab, self.noise, keys.data_ptr(), st)
+
+
+def make_w2v_table_args(dim: int, optimizer: Optional[Optimizer] = None):
+    opt = optimizer or Optimizer("adagrad", lr=0.05)
+    init = InitConfig("uniform", scale=1.0 / dim, state_init=0.0, zero_key_bit=OUT_BIT)
+    return opt, init
+
+
+class Word2VecWorker:
+    """Trains skip-gram embeddings through a ``PSEngine`` (dim = embedding size)."""
+
+    def __init__(self, engine, data: W2VSynth, rank: int = 0, world: int = 1):
+        if engine.dim not in (32, 64, 128):
+            raise ValueError("Word2VecWorker: dim must be 32, 64 or 128")
+        self.engine, self.data, self.rank, self.world = engine, data, rank, world
+        dev = engine.device
+        self.keys = [torch.empty(data.n_keys, dtype=torch.int64, device=dev)
+                     for _ in range(engine.depth)]
+        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
+        self.step_idx = 0
+        self._next = None
+
+    def _route(self, step: int):
+        slot = self.engine._next_slot
+
+        def produce(stream):
+            self.data.generate(step, self.rank, self.world, self.keys[slot],
+                               stream=stream.cuda_stream if stream is not None else None)
+            return self.keys[slot]
+
+        return self.engine.route(produce=produce)
+
+    def step(self) -> torch.Tensor:
+        d = self.data
+        r = self._next if self._next is not None else self._route(self.step_idx)
+        self._next = self._route(self.step_idx + 1)
+        rnd = self.engine.pull(r)
+        self.loss_sum.zero_()
+        inv = rnd.inv
+        B, C = d.batch_size, d.contexts
+        ptr, es = inv.data_ptr(), inv.element_size()
+        hip().w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
+                       d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
+                       self.loss_sum.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        self.engine.push(rnd)
+        self.step_idx += 1
+        return self.loss_sum
+
+    def mean_loss(self) -> float:
+        return float(self.loss_sum.item()) / (self.data.batch_size * self.data.contexts)
+
+
+def sgns_reference(V: np.ndarray, X: np.ndarray, N: np.ndarray, neg_scale: float):
+    """fp64 reference of one tile.  V [T,D] centers, X [T,C,D] contexts,
+    N [S,D] shared negatives.  Returns (loss, gV [T,D], gX [T,C,D], gN [S,D])."""
+    V, X, N = (a.astype(np.float64) for a in (V, X, N))
+    sig = lambda z: 1.0 / (1.0 + np.exp(-z))  # noqa: E731
+    sp = lambda z: np.maximum(z, 0) + np.log1p(np.exp(-np.abs(z)))  # noqa: E731
+    S = V @ N.T
+    G = neg_scale * sig(S)
+    pos = np.einsum("td,tcd->tc", V, X)
+    gp = sig(pos) - 1.0
+    loss = neg_scale * sp(S).sum() + sp(-pos).sum()
+    gV = G @ N + np.einsum("tc,tcd->td", gp, X)
+    gX = gp[:, :, None] * V[:, None, :]
+    gN = G.T @ V
+    return loss, gV, gX, gN

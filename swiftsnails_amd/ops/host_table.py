@@ -20,7 +20,7 @@ from .optim import INIT_KINDS, OPT_KINDS, InitConfig, Optimizer
 
 def _host_init(c: InitConfig):
     return host().InitParams(INIT_KINDS[c.kind], float(c.scale), float(c.state_init),
-                             int(c.seed) & ((1 << 64) - 1))
+                             int(c.seed) & ((1 << 64) - 1), int(c.zero_key_bit))
 
 
 def _host_opt(o: Optimizer):

@@ -36,12 +36,13 @@ class InitConfig:
     scale: float = 0.0
     state_init: float = 0.0  # initial optimizer-state value (e.g. AdaGrad accumulator)
     seed: int = 2015
+    zero_key_bit: int = -1  # keys with this bit set start at zero (namespaced tables)
 
     def native(self):
         from .._native import hip
 
         return hip().InitParams(INIT_KINDS[self.kind], float(self.scale), float(self.state_init),
-                                int(self.seed) & ((1 << 64) - 1))
+                                int(self.seed) & ((1 << 64) - 1), int(self.zero_key_bit))
 
 
 @dataclass
@@ -97,6 +98,9 @@ def init_reference(init: InitConfig, keys: np.ndarray, dim: int, width: int) -> 
     out[:, dim:] = np.float32(init.state_init)
     if init.kind == "zero" or dim == 0:
         return out
+    zmask = None
+    if init.zero_key_bit >= 0:
+        zmask = ((keys >> np.uint64(init.zero_key_bit)) & np.uint64(1)).astype(bool)
     seed = np.uint64(int(init.seed) & ((1 << 64) - 1))
     with np.errstate(over="ignore"):
         kk = keys * np.uint64(0x9E3779B97F4A7C15)
@@ -112,6 +116,8 @@ def init_reference(init: InitConfig, keys: np.ndarray, dim: int, width: int) -> 
                 u2 = (r2 >> np.uint64(40)).astype(np.float32) * np.float32(1.0 / 16777216.0)
                 out[:, j] = (np.sqrt(-2.0 * np.log(u1)) * np.cos(6.2831853 * u2) *
                              init.scale).astype(np.float32)
+    if zmask is not None:
+        out[zmask, :dim] = 0.0
     return out
 
 
