@@ -14,6 +14,7 @@
 #pragma once
 #include <algorithm>
 #include <cstring>
+#include <thread>
 #include <cstdio>
 #include <fstream>
 #include <memory>
@@ -102,6 +103,77 @@ class HostShard : NonCopyable {
   std::vector<float> rows_;
   std::mutex mu_;
 };
+
+// Text checkpoint codec shared by the CPU table and the HBM table dump path
+// (K8 host half: device compaction -> pinned D2H -> these formatters).
+// Line format: "key\tv0 v1 ... v{dim-1}[ | s0 s1 ...]\n" (sparsetable.h:49-56;
+// the optional " | state" tail makes a dump resumable).
+inline void format_rows_into(std::string& o, const uint64_t* keys, const float* rows, size_t n,
+                             int dim, int width, bool with_state, int precision) {
+  char buf[64];
+  const int w = with_state ? width : dim;
+  for (size_t i = 0; i < n; ++i) {
+    o += std::to_string(keys[i]);
+    o += '\t';
+    const float* r = rows + i * (size_t)width;
+    for (int j = 0; j < w; ++j) {
+      if (j) o += (with_state && j == dim) ? " | " : " ";
+      const int len = std::snprintf(buf, sizeof(buf), "%.*g", precision, (double)r[j]);
+      o.append(buf, (size_t)len);
+    }
+    o += '\n';
+  }
+}
+
+inline std::string format_rows(const uint64_t* keys, const float* rows, size_t n, int dim,
+                               int width, bool with_state, int precision, int nthreads = 8) {
+  nthreads = std::max(1, std::min(nthreads, (int)(n / 4096) + 1));
+  std::vector<std::string> parts((size_t)nthreads);
+  std::vector<std::thread> th;
+  const size_t per = (n + nthreads - 1) / nthreads;
+  for (int t = 0; t < nthreads; ++t)
+    th.emplace_back([&, t] {
+      const size_t a = std::min(n, per * t), b = std::min(n, per * (t + 1));
+      parts[t].reserve((b - a) * (size_t)(12 + 12 * (with_state ? width : dim)));
+      format_rows_into(parts[t], keys + a, rows + a * (size_t)width, b - a, dim, width,
+                       with_state, precision);
+    });
+  for (auto& x : th) x.join();
+  std::string out;
+  size_t tot = 0;
+  for (auto& p : parts) tot += p.size();
+  out.reserve(tot);
+  for (auto& p : parts) out += p;
+  return out;
+}
+
+// Parses one checkpoint line into (key, row[width]); missing state floats
+// are left as given in `row` (caller pre-fills state_init).
+inline bool parse_row_line(const char* p, int dim, int width, uint64_t* key, float* row) {
+  char* e = nullptr;
+  *key = std::strtoull(p, &e, 10);
+  if (e == p || *e != '\t') return false;
+  p = e + 1;
+  if (std::strncmp(p, "Vec:", 4) == 0) p += 4;
+  int j = 0;
+  bool in_state = false;
+  while (*p) {
+    while (*p == ' ' || *p == '\t') ++p;
+    if (!*p || *p == '\n') break;
+    if (*p == '|') {
+      in_state = true;
+      j = dim;
+      ++p;
+      continue;
+    }
+    const float v = std::strtof(p, &e);
+    if (e == p) return false;
+    if (j < width && (in_state || j < dim)) row[j] = v;
+    ++j;
+    p = e;
+  }
+  return true;
+}
 
 class HostTable : NonCopyable {
  public:

@@ -177,6 +177,77 @@ PYBIND11_MODULE(_ss_host, m) {
            py::arg("with_state") = false, py::call_guard<py::gil_scoped_release>())
       .def("load_text", &HostTable::load_text, py::call_guard<py::gil_scoped_release>());
 
+  // ---- text checkpoint codec (host half of K8)
+  m.def("format_rows", [](u64arr keys, f32arr rows, int dim, int width, bool with_state,
+                          int precision, int nthreads) {
+    SS_CHECK_MSG((size_t)rows.size() == (size_t)keys.size() * width, "rows must be [n, width]");
+    std::string s;
+    {
+      py::gil_scoped_release rel;
+      s = format_rows(keys.data(), rows.data(), (size_t)keys.size(), dim, width, with_state,
+                      precision, nthreads);
+    }
+    return py::bytes(s);
+  }, py::arg("keys"), py::arg("rows"), py::arg("dim"), py::arg("width"),
+     py::arg("with_state") = false, py::arg("precision") = 9, py::arg("nthreads") = 8);
+  m.def("parse_rows", [](py::bytes data, int dim, int width, float state_init, int nthreads) {
+    std::string buf = data;
+    std::vector<std::pair<size_t, size_t>> chunks;
+    {
+      const size_t n = buf.size();
+      const size_t per = std::max<size_t>(1, n / (size_t)std::max(1, nthreads));
+      size_t a = 0;
+      while (a < n) {
+        size_t b = std::min(n, a + per);
+        while (b < n && buf[b - 1] != '\n') ++b;
+        chunks.push_back({a, b});
+        a = b;
+      }
+    }
+    std::vector<std::vector<uint64_t>> ks(chunks.size());
+    std::vector<std::vector<float>> rs(chunks.size());
+    std::vector<int> bad(chunks.size(), 0);
+    {
+      py::gil_scoped_release rel;
+      std::vector<std::thread> th;
+      for (size_t c = 0; c < chunks.size(); ++c)
+        th.emplace_back([&, c] {
+          size_t p = chunks[c].first;
+          std::vector<float> row((size_t)width);
+          while (p < chunks[c].second) {
+            size_t e = buf.find('\n', p);
+            if (e == std::string::npos || e > chunks[c].second) e = chunks[c].second;
+            if (e > p) {
+              std::string line = buf.substr(p, e - p);
+              for (int j = 0; j < width; ++j) row[j] = j < dim ? 0.f : state_init;
+              uint64_t k;
+              if (parse_row_line(line.c_str(), dim, width, &k, row.data())) {
+                ks[c].push_back(k);
+                rs[c].insert(rs[c].end(), row.begin(), row.end());
+              } else {
+                bad[c]++;
+              }
+            }
+            p = e + 1;
+          }
+        });
+      for (auto& t : th) t.join();
+    }
+    size_t n = 0;
+    for (auto& k : ks) n += k.size();
+    for (int b : bad) SS_CHECK_MSG(b == 0, "malformed checkpoint line(s)");
+    py::array_t<uint64_t> ka((py::ssize_t)n);
+    py::array_t<float> ra({(py::ssize_t)n, (py::ssize_t)width});
+    size_t o = 0;
+    for (size_t c = 0; c < ks.size(); ++c) {
+      std::memcpy(ka.mutable_data() + o, ks[c].data(), ks[c].size() * 8);
+      std::memcpy(ra.mutable_data() + o * width, rs[c].data(), rs[c].size() * 4);
+      o += ks[c].size();
+    }
+    return py::make_tuple(ka, ra);
+  }, py::arg("data"), py::arg("dim"), py::arg("width"), py::arg("state_init") = 0.f,
+     py::arg("nthreads") = 8);
+
   // ---- TCP RPC
   py::class_<Request, std::shared_ptr<Request>>(m, "Request")
       .def(py::init<>())

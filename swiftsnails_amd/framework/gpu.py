@@ -1,0 +1,220 @@
+"""MI355X collective mode: one process per GPU, HBM shards, RCCL rounds.
+
+This is the GPU-native counterpart of the reference's three roles
+(/root/reference/src/core/framework/Swift{Master,Server,Worker}.h):
+
+* master   -> rank 0 + the torch.distributed TCPStore: rendezvous,
+              RCCL unique-id broadcast, the role table, termination barrier
+              (replaces registration/route/hashfrag messages, S3-S5, S8);
+* server   -> the ranks in ``server_ranks``: an ``HbmTable`` shard each;
+* worker   -> the ranks in ``worker_ranks``: a model worker each.
+Colocated (every rank both) is the default; "4 servers + 4 workers" is
+``server_ranks: 0,1,2,3`` / ``worker_ranks: 4,5,6,7``.
+
+``PSContext`` owns the per-rank pieces (process group, two RCCL
+communicators, table, round engine) and the reference's periodic backup /
+final dump behaviour (``param_backup_period``/``param_backup_root`` counted
+in rounds, ``param_output`` at the end), plus resume (``resume_from``), which
+the reference lacks.  ``run_training`` drives a model from a config.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..ops.optim import InitConfig, Optimizer
+from ..ops.table import HbmTable
+from ..parallel.engine import PSEngine
+from ..parallel.transport import LoopbackTransport, RcclTransport, TorchDistTransport
+from ..utils import checkpoint as ck
+from ..utils.config import Config
+from ..utils.logging import get_logger
+from ..utils.tracing import Tracer
+
+log = get_logger("swiftsnails.gpu")
+
+
+def _ranks(spec, world: int) -> list[int]:
+    if spec is None or str(spec).strip() in ("", "all"):
+        return list(range(world))
+    out = sorted({int(x) for x in str(spec).replace(";", ",").split(",") if x.strip()})
+    if not out or out[-1] >= world or out[0] < 0:
+        raise ValueError(f"bad rank list {spec!r} for world {world}")
+    return out
+
+
+class PSContext:
+    def __init__(self, cfg: Config, dim: int, optimizer: Optimizer, init: InitConfig,
+                 max_keys: int, capacity: int):
+        self.cfg = cfg
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(self.local_rank)
+        self.device = torch.device("cuda", self.local_rank)
+        self.servers = _ranks(cfg.get("server_ranks"), self.world)
+        self.workers = _ranks(cfg.get("worker_ranks"), self.world)
+        self.is_server = self.rank in self.servers
+        self.is_worker = self.rank in self.workers
+        ct = None
+        if self.world > 1:
+            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+            if not dist.is_initialized():
+                timeout = float(cfg.get("init_timeout", 600))
+                import datetime
+
+                dist.init_process_group("gloo", rank=self.rank, world_size=self.world,
+                                        timeout=datetime.timedelta(seconds=timeout))
+            store = dist.distributed_c10d._get_default_store()
+            kind = cfg.get("transport", "rccl")
+            if kind == "rccl":
+                tr = RcclTransport(self.rank, self.world, self.device, store=store,
+                                   prefix="ss_data")
+                ct = RcclTransport(self.rank, self.world, self.device, store=store,
+                                   prefix="ss_counts")
+            else:
+                tr = TorchDistTransport()
+        else:
+            tr = LoopbackTransport()
+        self.transport = tr
+        self.table = (HbmTable(dim, capacity, optimizer=optimizer, init=init, device=self.device)
+                      if self.is_server else None)
+        self.engine = PSEngine(self.table, tr, max_keys=max_keys, dim=dim,
+                               frag_num=int(cfg.get("frag_num", 0) or 0),
+                               server_ranks=self.servers, device=self.device,
+                               count_transport=ct)
+        self.backup_period = int(cfg.get("param_backup_period", 0) or 0)
+        self.backup_root = cfg.get("param_backup_root", ".")
+        self.ckpt_format = cfg.get("checkpoint_format", "bin")
+        self.tracer = Tracer(enabled=str(cfg.get("trace", "0")) not in ("0", "false"))
+        resume = cfg.get("resume_from")
+        if resume:
+            self.resume(resume)
+
+    # ------------------------------------------------------------ ckpt
+    def _owner(self):
+        return ck.owner_filter(self.engine.frag_map, self.rank)
+
+    def save(self, prefix: str, fmt: Optional[str] = None) -> Optional[str]:
+        torch.cuda.synchronize()
+        p = None
+        if self.table is not None:
+            p = ck.save_sharded(self.table, prefix, self.servers.index(self.rank),
+                                len(self.servers), fmt or self.ckpt_format)
+        self.barrier()
+        return p
+
+    def resume(self, prefix: str) -> int:
+        n = 0
+        if self.table is not None:
+            n = ck.load_sharded(self.table, prefix, owner_fn=self._owner())
+            log.info("rank %d resumed %d keys from %s", self.rank, n, prefix)
+        self.barrier()
+        return n
+
+    def maybe_backup(self, round_idx: int) -> None:
+        """Reference: every param_backup_period pushes -> param-<n>.txt."""
+        if self.backup_period > 0 and round_idx > 0 and round_idx % self.backup_period == 0:
+            self.save(os.path.join(self.backup_root, f"param-{round_idx}"))
+
+    def barrier(self):
+        if self.world > 1:
+            dist.barrier()
+
+    def finish(self):
+        out = self.cfg.get("param_output")
+        if out:
+            self.save(out, fmt=self.cfg.get("param_output_format", "text"))
+        if self.table is not None:
+            self.table.check()
+        self.barrier()
+
+    def close(self):
+        if self.world > 1 and dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def build_worker(cfg: Config):
+    """(ctx, worker) for the configured model."""
+    from ..models.fm import FMWorker, fm_table_args
+    from ..models.sparse_lr import CtrSynth, SparseLRWorker
+    from ..models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
+
+    model = cfg.get("model", "sparse_lr")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    nserv = len(_ranks(cfg.get("server_ranks"), world))
+    load = float(cfg.get("table_load", 0.7))
+    opt = Optimizer(cfg.get("optimizer", "adagrad"), lr=float(cfg.get("learning_rate", 0.05)),
+                    l1=float(cfg.get("l1", 0.0)), l2=float(cfg.get("l2", 0.0)))
+    if model in ("sparse_lr", "fm"):
+        data = CtrSynth(batch_size=int(cfg.get("batch_size", 65536)),
+                        num_fields=int(cfg.get("num_fields", 39)),
+                        num_features=int(float(cfg.get("num_features", 1e9))),
+                        tail_frac=float(cfg.get("tail_frac", 0.1)))
+        dim = 1 if model == "sparse_lr" else int(cfg.get("dim", 9))
+        init = InitConfig("zero") if model == "sparse_lr" else fm_table_args(dim - 1, opt)[1]
+        cap = int(cfg.get("table_capacity", 0) or data.num_features / nserv / load + 1024)
+        ctx = PSContext(cfg, dim, opt, init, data.batch_size * data.num_fields, cap)
+        cls = SparseLRWorker if model == "sparse_lr" else FMWorker
+        w = cls(ctx.engine, data, rank=ctx.rank, world=world, active=ctx.is_worker)
+    elif model == "word2vec":
+        data = W2VSynth(batch_size=int(cfg.get("batch_size", 16384)),
+                        window=int(cfg.get("window", 5)),
+                        vocab=int(float(cfg.get("vocab", 1e6))),
+                        negatives=int(cfg.get("negatives", 5)))
+        dim = int(cfg.get("dim", 128))
+        opt, init = make_w2v_table_args(dim, opt)
+        cap = int(cfg.get("table_capacity", 0) or 2 * data.vocab / nserv / load + 1024)
+        ctx = PSContext(cfg, dim, opt, init, data.n_keys, cap)
+        w = Word2VecWorker(ctx.engine, data, rank=ctx.rank, world=world, active=ctx.is_worker)
+    else:
+        raise ValueError(f"unknown model {model!r}")
+    return ctx, w
+
+
+def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
+                 log_every: int = 0) -> dict:
+    """Train `steps` rounds (config num_iters) and return throughput stats."""
+    ctx, w = build_worker(cfg)
+    steps = int(steps if steps is not None else cfg.get("num_iters", 100))
+    log_every = log_every or int(cfg.get("log_every", 0) or 0)
+    for _ in range(warmup):
+        w.step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        with ctx.tracer.range(f"step{i}"):
+            w.step()
+        ctx.maybe_backup(w.step_idx)
+        if log_every and (i + 1) % log_every == 0 and ctx.rank == 0:
+            log.warning("step %d loss %.5f", i + 1, w.mean_loss())
+    torch.cuda.synchronize()
+    ctx.barrier()
+    el = time.perf_counter() - t0
+    t = torch.tensor([el], dtype=torch.float64)
+    if ctx.world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    n = torch.tensor([w.samples_per_step()], dtype=torch.int64)
+    if ctx.world > 1:
+        dist.all_reduce(n)
+    stats = {"model": cfg.get("model", "sparse_lr"), "world": ctx.world,
+             "servers": len(ctx.servers), "workers": len(ctx.workers), "steps": steps,
+             "seconds": el, "ms_per_step": 1000 * el / max(1, steps),
+             "samples_per_s": int(n.item()) * steps / el if el > 0 else 0.0,
+             "loss": w.mean_loss() if ctx.is_worker else None}
+    ctx.finish()
+    ctx.close()
+    return stats
+
+
+if __name__ == "__main__":  # pragma: no cover
+    print("use: python -m swiftsnails_amd.launch --config <file>", file=sys.stderr)
+    np.zeros(0)

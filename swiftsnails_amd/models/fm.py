@@ -22,6 +22,7 @@ import torch
 from .._native import hip
 from ..ops.optim import InitConfig, Optimizer
 from ..ops.table import HbmTable
+from .base import PipelinedWorker
 from .sparse_lr import CtrSynth
 
 
@@ -37,45 +38,31 @@ def plan_fm_table(n_keys: int, k: int = 8, shards: int = 8, load: float = 0.7) -
     return p
 
 
-class FMWorker:
-    def __init__(self, engine, data: CtrSynth, rank: int = 0, world: int = 1):
+class FMWorker(PipelinedWorker):
+    def __init__(self, engine, data: CtrSynth, rank: int = 0, world: int = 1,
+                 active: bool = True):
         if engine.dim not in (2, 5, 9, 17):
             raise ValueError("FMWorker: dim must be 1+K with K in {1,4,8,16}")
-        self.engine, self.data, self.rank, self.world = engine, data, rank, world
+        super().__init__(engine, rank, world, active)
+        self.data = data
         dev = engine.device
         B, F = data.batch_size, data.num_fields
         self.keys = [torch.empty(B * F, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
         self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
-        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.step_idx = 0
-        self._next = None
 
-    def _route(self, step: int):
-        slot = self.engine._next_slot
+    def _produce(self, step, slot, stream):
+        self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
+                           stream=stream)
+        return self.keys[slot]
 
-        def produce(stream):
-            self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
-                               stream=stream.cuda_stream if stream is not None else None)
-            return self.keys[slot]
-
-        return self.engine.route(produce=produce)
-
-    def step(self) -> torch.Tensor:
+    def _compute(self, rnd, slot, st):
         d = self.data
-        r = self._next if self._next is not None else self._route(self.step_idx)
-        self._next = self._route(self.step_idx + 1)
-        rnd = self.engine.pull(r)
-        self.loss_sum.zero_()
-        hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[r.slot].data_ptr(), d.batch_size,
+        hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
-                         rnd.ugrad.data_ptr(), self.loss_sum.data_ptr(), 0,
-                         torch.cuda.current_stream().cuda_stream)
-        self.engine.push(rnd)
-        self.step_idx += 1
-        return self.loss_sum
+                         rnd.ugrad.data_ptr(), self.loss_sum.data_ptr(), 0, st)
 
-    def mean_loss(self) -> float:
-        return float(self.loss_sum.item()) / self.data.batch_size
+    def samples_per_step(self) -> int:
+        return self.data.batch_size if self.active else 0
 
 
 def fm_reference(rows: np.ndarray, labels: np.ndarray):

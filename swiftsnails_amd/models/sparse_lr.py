@@ -25,6 +25,7 @@ import torch
 from .._native import hip
 from ..ops.optim import InitConfig, Optimizer
 from ..ops.table import HbmTable
+from .base import PipelinedWorker
 
 
 @dataclass
@@ -50,50 +51,35 @@ class CtrSynth:
                       self.truth_scale, self.truth_bias, keys.data_ptr(), labels.data_ptr(), st)
 
 
-class SparseLRWorker:
+class SparseLRWorker(PipelinedWorker):
     """Trains sparse LR through a ``PSEngine`` (one per rank).
 
     The batch of step i+1 is generated, deduplicated and routed on the
     engine's route stream while step i computes (one batch of lookahead; no
     parameter staleness — routing does not read parameters)."""
 
-    def __init__(self, engine, data: CtrSynth, rank: int = 0, world: int = 1):
-        self.engine, self.data, self.rank, self.world = engine, data, rank, world
+    def __init__(self, engine, data: CtrSynth, rank: int = 0, world: int = 1,
+                 active: bool = True):
+        super().__init__(engine, rank, world, active)
+        self.data = data
         dev = engine.device
         B, F = data.batch_size, data.num_fields
-        D = engine.depth
-        self.keys = [torch.empty(B * F, dtype=torch.int64, device=dev) for _ in range(D)]
-        self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(D)]
-        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.step_idx = 0
-        self._next = None
+        self.keys = [torch.empty(B * F, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
+        self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
 
-    def _route(self, step: int):
-        slot = self.engine._next_slot
+    def _produce(self, step, slot, stream):
+        self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
+                           stream=stream)
+        return self.keys[slot]
 
-        def produce(stream):
-            self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
-                               stream=stream.cuda_stream if stream is not None else None)
-            return self.keys[slot]
-
-        return self.engine.route(produce=produce)
-
-    def step(self) -> torch.Tensor:
-        """One training step. Returns the summed batch logloss (device tensor)."""
+    def _compute(self, rnd, slot, st):
         d = self.data
-        r = self._next if self._next is not None else self._route(self.step_idx)
-        self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
-        rnd = self.engine.pull(r)
-        self.loss_sum.zero_()
-        hip().lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels[r.slot].data_ptr(), d.batch_size,
+        hip().lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
-                         self.loss_sum.data_ptr(), 0, torch.cuda.current_stream().cuda_stream)
-        self.engine.push(rnd)
-        self.step_idx += 1
-        return self.loss_sum
+                         self.loss_sum.data_ptr(), 0, st)
 
-    def mean_loss(self) -> float:
-        return float(self.loss_sum.item()) / self.data.batch_size
+    def samples_per_step(self) -> int:
+        return self.data.batch_size if self.active else 0
 
 
 def make_lr_table(num_features: int, world: int = 1, optimizer: Optional[Optimizer] = None,

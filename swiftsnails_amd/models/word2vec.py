@@ -23,6 +23,7 @@ import torch
 
 from .._native import hip
 from ..ops.optim import InitConfig, Optimizer
+from .base import PipelinedWorker
 
 OUT_BIT = 40
 TILE = 64      # centers per workgroup tile
@@ -67,48 +68,34 @@ def make_w2v_table_args(dim: int, optimizer: Optional[Optimizer] = None):
     return opt, init
 
 
-class Word2VecWorker:
+class Word2VecWorker(PipelinedWorker):
     """Trains skip-gram embeddings through a ``PSEngine`` (dim = embedding size)."""
 
-    def __init__(self, engine, data: W2VSynth, rank: int = 0, world: int = 1):
+    def __init__(self, engine, data: W2VSynth, rank: int = 0, world: int = 1,
+                 active: bool = True):
         if engine.dim not in (32, 64, 128):
             raise ValueError("Word2VecWorker: dim must be 32, 64 or 128")
-        self.engine, self.data, self.rank, self.world = engine, data, rank, world
-        dev = engine.device
-        self.keys = [torch.empty(data.n_keys, dtype=torch.int64, device=dev)
+        super().__init__(engine, rank, world, active)
+        self.data = data
+        self.keys = [torch.empty(data.n_keys, dtype=torch.int64, device=engine.device)
                      for _ in range(engine.depth)]
-        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.step_idx = 0
-        self._next = None
 
-    def _route(self, step: int):
-        slot = self.engine._next_slot
+    def _produce(self, step, slot, stream):
+        self.data.generate(step, self.rank, self.world, self.keys[slot], stream=stream)
+        return self.keys[slot]
 
-        def produce(stream):
-            self.data.generate(step, self.rank, self.world, self.keys[slot],
-                               stream=stream.cuda_stream if stream is not None else None)
-            return self.keys[slot]
-
-        return self.engine.route(produce=produce)
-
-    def step(self) -> torch.Tensor:
+    def _compute(self, rnd, slot, st):
         d = self.data
-        r = self._next if self._next is not None else self._route(self.step_idx)
-        self._next = self._route(self.step_idx + 1)
-        rnd = self.engine.pull(r)
-        self.loss_sum.zero_()
         inv = rnd.inv
         B, C = d.batch_size, d.contexts
         ptr, es = inv.data_ptr(), inv.element_size()
         hip().w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
                        d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
-                       self.loss_sum.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        self.engine.push(rnd)
-        self.step_idx += 1
-        return self.loss_sum
+                       self.loss_sum.data_ptr(), st)
 
-    def mean_loss(self) -> float:
-        return float(self.loss_sum.item()) / (self.data.batch_size * self.data.contexts)
+    def samples_per_step(self) -> int:
+        """Positive (center, context) pairs per step ("words/s" numerator)."""
+        return self.data.batch_size * self.data.contexts if self.active else 0
 
 
 def sgns_reference(V: np.ndarray, X: np.ndarray, N: np.ndarray, neg_scale: float):

@@ -1,0 +1,80 @@
+"""Checkpoint formats (reference text format + binary) and resharded resume."""
+import numpy as np
+import pytest
+
+from swiftsnails_amd.ops.host_table import HostTable
+from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+from swiftsnails_amd.parallel.router import HashFrag
+from swiftsnails_amd.utils import checkpoint as ck
+
+
+def _table(dim=4, opt="adagrad", seed=0):
+    t = HostTable(dim, 3, Optimizer(opt, lr=0.1), InitConfig("normal", 0.5, 0.01, seed=seed))
+    keys = np.random.default_rng(seed).integers(0, 1 << 50, 2000).astype(np.int64)
+    t.pull_keys(keys)
+    t.push_keys(np.unique(keys), np.ones((len(np.unique(keys)), dim), np.float32))
+    return t
+
+
+def test_text_format_matches_reference_layout(tmp_path):
+    t = _table(dim=1)
+    p = str(tmp_path / "param-10.txt")
+    n = ck.save_text(t, p, precision=6)
+    lines = open(p).read().splitlines()
+    assert n == len(lines) == t.size()
+    k, v = lines[0].split("\t")  # "key\tvalue" (sparsetable.h:49-56)
+    assert k.isdigit() and len(v.split()) == 1
+
+
+@pytest.mark.parametrize("fmt", ["text", "bin"])
+def test_roundtrip_exact_with_state(tmp_path, fmt):
+    t = _table()
+    p = str(tmp_path / ("c.txt" if fmt == "text" else "c.bin"))
+    if fmt == "text":
+        ck.save_text(t, p, precision=9, with_state=True)
+    else:
+        ck.save_binary(t, p)
+    t2 = HostTable(4, 5, Optimizer("adagrad", lr=0.1), InitConfig("zero", 0, 0.01))
+    (ck.load_text if fmt == "text" else ck.load_binary)(t2, p)
+    a, b = t.to_dict(True), t2.to_dict(True)
+    assert a.keys() == b.keys()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+
+
+def test_reference_vec_prefix_and_params_only(tmp_path):
+    p = tmp_path / "ref.txt"
+    p.write_text("17\tVec:\t0.5 -1.25 2 \n99\t3 4 5\n")
+    t = HostTable(3, 2, Optimizer("adagrad"), InitConfig("zero", 0, 0.1))
+    assert ck.load_text(t, str(p)) == 2
+    d = t.to_dict(True)
+    np.testing.assert_allclose(d[17], [0.5, -1.25, 2, 0.1, 0.1, 0.1])
+    np.testing.assert_allclose(d[99], [3, 4, 5, 0.1, 0.1, 0.1])
+
+
+def test_sharded_resume_on_different_world_size(tmp_path):
+    src = _table(dim=2, seed=3)
+    keys = np.array(list(src.to_dict().keys()), dtype=np.uint64)
+    # split into 3 "server" shards by the world-3 router, save them
+    hf3 = HashFrag(3, 64)
+    m3 = hf3.rank_map()
+    all_rows = src.to_dict(True)
+    prefix = str(tmp_path / "ckpt" / "model")
+    for r in range(3):
+        t = HostTable(2, 2, Optimizer("adagrad", lr=0.1))
+        mine = keys[ck.owner_filter(m3, r)(keys)]
+        t.assign(mine.view(np.int64), np.stack([all_rows[int(k)] for k in mine]))
+        ck.save_sharded(t, prefix, r, 3, fmt="bin" if r != 1 else "text")
+    # resume on world 2
+    hf2 = HashFrag(2, 64)
+    m2 = hf2.rank_map()
+    merged = {}
+    for r in range(2):
+        t = HostTable(2, 2, Optimizer("adagrad", lr=0.1))
+        ck.load_sharded(t, prefix, owner_fn=ck.owner_filter(m2, r))
+        d = t.to_dict(True)
+        assert not (set(d) & set(merged))
+        merged.update(d)
+    assert set(merged) == set(all_rows)
+    for k in all_rows:
+        np.testing.assert_array_equal(merged[k], all_rows[k])

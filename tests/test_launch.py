@@ -1,0 +1,64 @@
+"""End-to-end CLI: reference-style role processes over TCP loopback (CPU) and
+the MI355X collective mode (GPU, world 1) with backup + resume."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def test_cli_master_server_worker_processes(tmp_path):
+    port = _port()
+    out = tmp_path / "final.txt"
+    sets = ["--set", f"listen_addr=tcp://127.0.0.1:{port}",
+            "--set", f"master_addr=tcp://127.0.0.1:{port}",
+            "--set", f"param_output={out}", "--set", "num_iters=30"]
+    base = [sys.executable, "-m", "swiftsnails_amd.launch", "--config",
+            os.path.join(ROOT, "configs", "dense_lr_cpu.conf")] + sets
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    procs = [subprocess.Popen(base + ["--role", r], cwd=ROOT, env=env, stdout=subprocess.PIPE,
+                              stderr=subprocess.PIPE) for r in ("master", "server", "worker")]
+    for p in procs:
+        try:
+            p.wait(120)
+        except subprocess.TimeoutExpired:
+            p.kill()
+            raise
+    for p in procs:
+        assert p.returncode == 0, p.stderr.read().decode()[-2000:]
+    lines = out.read_text().splitlines()
+    assert len(lines) == 64  # dense_dim weights, one "key\tvalue" line each
+    assert sorted(int(x.split("\t")[0]) for x in lines) == list(range(64))
+
+
+@pytest.mark.gpu
+def test_cli_gpu_sparse_lr_backup_and_resume(tmp_path):
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    common = [sys.executable, "-m", "swiftsnails_amd.launch", "--config",
+              os.path.join(ROOT, "configs", "sparse_lr_10m.conf"),
+              "--set", "batch_size=4096", "--set", "num_features=1000000",
+              "--set", f"param_backup_root={tmp_path}", "--set", "param_backup_period=5"]
+    r = subprocess.run(common + ["--steps", "10", "--set", f"param_output={tmp_path}/final"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    stats = json.loads(r.stdout.strip().splitlines()[-1])
+    assert stats["samples_per_s"] > 0 and stats["steps"] == 10
+    assert (tmp_path / "param-5.shard0-of-1.bin").exists()
+    assert (tmp_path / "param-10.shard0-of-1.bin").exists()
+    txt = tmp_path / "final.shard0-of-1.txt"
+    assert txt.exists() and txt.read_text().count("\n") > 1000
+    r2 = subprocess.run(common + ["--steps", "2", "--set", f"resume_from={tmp_path}/param-10"],
+                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r2.returncode == 0, r2.stderr[-3000:]

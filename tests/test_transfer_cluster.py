@@ -151,6 +151,26 @@ def test_cluster_master_servers_workers(tmp_path):
     assert list(tmp_path.glob("param-*.txt"))
 
 
+def test_dense_lr_one_worker_one_server_loopback(tmp_path):
+    """BASELINE config 1: dense LR, 1 worker + 1 server on CPU over TCP loopback."""
+    from swiftsnails_amd.framework.cluster import SwiftMaster, SwiftServer, SwiftWorker
+    from swiftsnails_amd.models.dense_lr import DenseLR, DenseLRData
+
+    port = _free_port()
+    cfg = lambda: _cluster_cfg(port, str(tmp_path), "", S=1, W=1,  # noqa: E731
+                               extra={"optimizer": "adagrad", "learning_rate": 0.2,
+                                      "param_backup_period": 0})
+    alg = DenseLR(DenseLRData(dim=32), steps=60, batch=256)
+    m, s, w = SwiftMaster(cfg()), SwiftServer(cfg(), dim=1), SwiftWorker(cfg(), alg, dim=1)
+    ths = [threading.Thread(target=x.run) for x in (m, s, w)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join(60)
+    assert all(not t.is_alive() for t in ths)
+    assert np.mean(alg.losses[-5:]) < alg.losses[0] - 0.1, alg.losses
+
+
 def test_local_train_mode():
     from swiftsnails_amd.framework.cluster import BaseAlgorithm, SwiftWorker
 
