@@ -127,20 +127,19 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
 
   // ---- dedup / route (K1/K2/K6/K7)
-  m.def("dedup_route", [](uintptr_t keys, long long n, uintptr_t skeys, uintptr_t suid,
+  m.def("dedup_route", [](uintptr_t keys, long long n, uintptr_t skeys, uintptr_t stag,
                           unsigned long long scap, uintptr_t slot_of, uintptr_t frag_map,
                           int frag_num, int nranks, long long ucap, uintptr_t ucount,
-                          uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t st) {
+                          uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t blk_cnt,
+                          uintptr_t inv, uintptr_t st) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
-    launch_dedup_route(P<const uint64_t>(keys), n, P<uint64_t>(skeys), P<uint32_t>(suid), scap,
+    launch_dedup_route(P<const uint64_t>(keys), n, P<uint64_t>(skeys), P<uint32_t>(stag), scap,
                        P<uint32_t>(slot_of), rs, ucap, P<unsigned long long>(ucount),
-                       P<uint64_t>(ukeys), P<float>(ugrad), gdim, S(st));
+                       P<uint64_t>(ukeys), P<float>(ugrad), gdim, P<uint32_t>(blk_cnt),
+                       P<uint32_t>(inv), S(st));
   });
-  m.def("dedup_inverse", [](uintptr_t slot_of, uintptr_t suid, long long n, uintptr_t inv,
-                            uintptr_t st) {
-    launch_dedup_inverse(P<const uint32_t>(slot_of), P<const uint32_t>(suid), n, P<uint32_t>(inv),
-                         S(st));
-  });
+  m.def("dedup_blocks", &dedup_blocks);
+  m.attr("CTR_SHARDS") = kCtrShards;
   m.def("route_keys", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num,
                          int nranks, uintptr_t dest, uintptr_t st) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};

@@ -12,44 +12,51 @@
 //       written straight into per-destination segments at fixed displacement
 //       dest*ucap, which is exactly the alltoallv send layout.
 //
-// One pass: every occurrence CASes its key into a power-of-two scratch table
-// (load <= 0.5, scratch is memset to 0xFF once per round).  The lane that wins
-// the CAS is the unique representative: it routes the key, takes a position
-// inside its destination segment (LDS counter per destination, one global
-// atomic per block and destination), writes the key and zeroes the gradient
-// row the model will accumulate into.  A second tiny pass turns each
-// occurrence's scratch slot into its unique id (the `inverse` index the model
-// kernels gather/scatter through).
+// Three kernels, and no same-address atomics (measured on MI355X: one
+// atomic per wave onto a single counter serialises at ~12 ns each — 23K of
+// them cost 285 us, more than the whole dedup):
+//   1. insert:  every occurrence CASes its key into a power-of-two scratch
+//      table (load <= 0.5).  The CAS winner is the key's representative: it
+//      routes the key and takes a block-local offset in its destination from
+//      an LDS counter; the block writes its per-destination counts with plain
+//      stores, and the winner parks (block, dest, offset) in the slot's tag.
+//   2. scan:    one workgroup per destination turns the per-block counts into
+//      per-block bases (exclusive prefix sum) and the destination total.
+//   3. finish:  every occurrence resolves its unique id from its slot's tag;
+//      the winner also writes the key into the send segment and zeroes the
+//      gradient row.  (`inverse` is what the model kernels gather through.)
 #include "ss_device.h"
 #include "ss_launch.h"
 
 namespace ss {
 
 static constexpr uint32_t kInvalid = 0xFFFFFFFFu;
+static constexpr uint32_t kWinBit = 0x80000000u;  // slot_of[i] flag: occurrence i won its key
+// tag = (block << 15) | (dest << 9) | local_offset
+__device__ __forceinline__ uint32_t mk_tag(uint32_t b, uint32_t d, uint32_t o) {
+  return (b << 15) | (d << 9) | o;
+}
 
-__global__ __launch_bounds__(256) void k_dedup_route(
-    const uint64_t* __restrict__ keys, long long n, uint64_t* __restrict__ skeys,
-    uint32_t* __restrict__ suid, unsigned long long smask, uint32_t* __restrict__ slot_of,
-    RouteSpec rs, long long ucap, unsigned long long* __restrict__ ucount,
-    uint64_t* __restrict__ ukeys, float* __restrict__ ugrad, int gdim) {
+__global__ __launch_bounds__(256) void k_dedup_insert(const uint64_t* __restrict__ keys, long long n,
+                                                      uint64_t* __restrict__ skeys,
+                                                      uint32_t* __restrict__ stag,
+                                                      unsigned long long smask,
+                                                      uint32_t* __restrict__ slot_of, RouteSpec rs,
+                                                      uint32_t* __restrict__ blk_cnt, int nblocks) {
   __shared__ unsigned int lcnt[kMaxSeg];
-  __shared__ unsigned long long lbase[kMaxSeg];
   for (int r = threadIdx.x; r < rs.nranks; r += blockDim.x) lcnt[r] = 0;
   __syncthreads();
-
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   bool won = false;
   int dest = 0;
-  unsigned int loff = 0;
-  uint64_t key = kEmptyKey;
   unsigned long long s = 0;
   if (i < n) {
-    key = keys[i];
+    const uint64_t key = keys[i];
     if (key == kEmptyKey) {
       slot_of[i] = kInvalid;
     } else {
       s = dedup_hash(key) & smask;
-      for (;;) {  // terminates: scratch holds >= 2n slots, at most n distinct keys
+      for (;;) {  // terminates: scratch holds > n slots
         const uint64_t k = skeys[s];
         if (k == key) break;
         if (k == kEmptyKey) {
@@ -63,33 +70,79 @@ __global__ __launch_bounds__(256) void k_dedup_route(
         }
         s = (s + 1) & smask;
       }
-      slot_of[i] = (uint32_t)s;
-      if (won) {
-        dest = rs.nranks == 1 ? 0 : rs.frag_map[fmix64(key) % (uint64_t)rs.frag_num];
-        loff = atomicAdd(&lcnt[dest], 1u);
-      }
+      slot_of[i] = (uint32_t)s | (won ? kWinBit : 0u);
+      if (won) dest = rs.nranks == 1 ? 0 : rs.frag_map[fmix64(key) % (uint64_t)rs.frag_num];
     }
   }
+  unsigned int loff = 0;
+  if (won) loff = atomicAdd(&lcnt[dest], 1u);  // LDS atomic (cheap)
+  if (won) stag[s] = mk_tag(blockIdx.x, (uint32_t)dest, loff);
   __syncthreads();
   for (int r = threadIdx.x; r < rs.nranks; r += blockDim.x)
-    lbase[r] = lcnt[r] ? atomicAdd(&ucount[r], (unsigned long long)lcnt[r]) : 0ull;
-  __syncthreads();
-  if (won) {
-    const unsigned long long uid = (unsigned long long)dest * ucap + lbase[dest] + loff;
-    ukeys[uid] = key;
-    suid[s] = (uint32_t)uid;
-    if (ugrad)
-      for (int j = 0; j < gdim; ++j) ugrad[uid * gdim + j] = 0.f;
-  }
+    blk_cnt[(long long)r * nblocks + blockIdx.x] = lcnt[r];
 }
 
-__global__ __launch_bounds__(256) void k_dedup_inverse(const uint32_t* __restrict__ slot_of,
-                                                       const uint32_t* __restrict__ suid,
-                                                       long long n, uint32_t* __restrict__ inv) {
+// One workgroup per destination: exclusive scan of blk_cnt[dest][*].
+__global__ __launch_bounds__(1024) void k_dedup_scan(uint32_t* __restrict__ blk_cnt, int nblocks,
+                                                     unsigned long long* __restrict__ ucount) {
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned int carry;
+  const int dest = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
+  uint32_t* c = blk_cnt + (long long)dest * nblocks;
+  if (t == 0) carry = 0;
+  __syncthreads();
+  for (int base = 0; base < nblocks; base += 1024) {
+    const int idx = base + t;
+    const unsigned int v = idx < nblocks ? c[idx] : 0u;
+    unsigned int x = v;  // inclusive wave scan
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+      unsigned int ws = lane < 16 ? wsum[lane] : 0u;
+      for (int o = 1; o < 16; o <<= 1) {
+        const unsigned int y = __shfl_up(ws, o, 64);
+        if (lane >= o) ws += y;
+      }
+      if (lane < 16) wsum[lane] = ws;  // inclusive over waves
+    }
+    __syncthreads();
+    const unsigned int excl = carry + (w ? wsum[w - 1] : 0u) + x - v;
+    if (idx < nblocks) c[idx] = excl;
+    __syncthreads();
+    if (t == 0) carry += wsum[15];
+    __syncthreads();
+  }
+  if (t == 0) ucount[dest] = carry;
+}
+
+__global__ __launch_bounds__(256) void k_dedup_finish(const uint64_t* __restrict__ keys, long long n,
+                                                      const uint32_t* __restrict__ slot_of,
+                                                      const uint32_t* __restrict__ stag,
+                                                      const uint32_t* __restrict__ blk_base,
+                                                      int nblocks, long long ucap,
+                                                      uint32_t* __restrict__ inv,
+                                                      uint64_t* __restrict__ ukeys,
+                                                      float* __restrict__ ugrad, int gdim) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) {
-    const uint32_t s = slot_of[i];
-    inv[i] = s == kInvalid ? kInvalid : suid[s];
+  if (i >= n) return;
+  const uint32_t so = slot_of[i];
+  if (so == kInvalid) {
+    inv[i] = kInvalid;
+    return;
+  }
+  const uint32_t tag = stag[so & ~kWinBit];
+  const uint32_t b = tag >> 15, d = (tag >> 9) & 63u, o = tag & 511u;
+  const unsigned long long uid =
+      (unsigned long long)d * ucap + blk_base[(long long)d * nblocks + b] + o;
+  inv[i] = (uint32_t)uid;
+  if (so & kWinBit) {
+    ukeys[uid] = keys[i];
+    if (ugrad)
+      for (int j = 0; j < gdim; ++j) ugrad[uid * gdim + j] = 0.f;
   }
 }
 
@@ -134,29 +187,34 @@ static inline int blocks_for(long long n, int cap = 1 << 30) {
   return (int)(b > cap ? cap : b);
 }
 
+int dedup_blocks(long long n) { return blocks_for(n); }
+
 void launch_dedup_route(const uint64_t* keys, long long n, uint64_t* scratch_keys,
-                        uint32_t* scratch_uid, unsigned long long scratch_cap,
-                        uint32_t* slot_of, RouteSpec rs, long long ucap,
-                        unsigned long long* ucount, uint64_t* ukeys, float* ugrad, int gdim,
+                        uint32_t* scratch_tag, unsigned long long scratch_cap, uint32_t* slot_of,
+                        RouteSpec rs, long long ucap, unsigned long long* ucount, uint64_t* ukeys,
+                        float* ugrad, int gdim, uint32_t* blk_cnt, uint32_t* inv,
                         hipStream_t st) {
-  if (n <= 0) return;
-  if ((scratch_cap & (scratch_cap - 1)) != 0 || scratch_cap < 2ull * (unsigned long long)n)
-    throw_error("dedup scratch capacity must be a power of two >= 2n");
+  if (n <= 0) {
+    check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
+    return;
+  }
+  if ((scratch_cap & (scratch_cap - 1)) != 0 || scratch_cap <= (unsigned long long)n)
+    throw_error("dedup scratch capacity must be a power of two > n");
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("dedup: bad nranks");
   if (ucap < n) throw_error("dedup: per-destination capacity must be >= n");
-  if ((unsigned long long)rs.nranks * (unsigned long long)ucap >= 0xFFFFFFFFull)
-    throw_error("dedup: nranks*ucap overflows 32-bit unique ids");
-  hipLaunchKernelGGL(k_dedup_route, dim3(blocks_for(n)), dim3(256), 0, st, keys, n, scratch_keys,
-                     scratch_uid, scratch_cap - 1, slot_of, rs, ucap, ucount, ukeys, ugrad, gdim);
-  check_launch("k_dedup_route");
-}
-
-void launch_dedup_inverse(const uint32_t* slot_of, const uint32_t* scratch_uid, long long n,
-                          uint32_t* inv, hipStream_t st) {
-  if (n <= 0) return;
-  hipLaunchKernelGGL(k_dedup_inverse, dim3(blocks_for(n)), dim3(256), 0, st, slot_of, scratch_uid,
-                     n, inv);
-  check_launch("k_dedup_inverse");
+  if ((unsigned long long)rs.nranks * (unsigned long long)ucap >= 0x7FFFFFFFull)
+    throw_error("dedup: nranks*ucap overflows 31-bit unique ids");
+  if (scratch_cap > 0x80000000ull) throw_error("dedup: scratch too large for 31-bit slots");
+  const int nb = blocks_for(n);
+  if (nb >= (1 << 17)) throw_error("dedup: too many keys per call (max 33M)");
+  hipLaunchKernelGGL(k_dedup_insert, dim3(nb), dim3(256), 0, st, keys, n, scratch_keys, scratch_tag,
+                     scratch_cap - 1, slot_of, rs, blk_cnt, nb);
+  check_launch("k_dedup_insert");
+  hipLaunchKernelGGL(k_dedup_scan, dim3(rs.nranks), dim3(1024), 0, st, blk_cnt, nb, ucount);
+  check_launch("k_dedup_scan");
+  hipLaunchKernelGGL(k_dedup_finish, dim3(nb), dim3(256), 0, st, keys, n, slot_of, scratch_tag,
+                     blk_cnt, nb, ucap, inv, ukeys, ugrad, gdim);
+  check_launch("k_dedup_finish");
 }
 
 void launch_route_keys(const uint64_t* keys, long long n, RouteSpec rs, int* dest,

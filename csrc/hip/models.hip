@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_bwd(const uint32_t* __restrict__
   for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, 64);
   if ((t & 63) == 0) sloss[t >> 6] = l;
   __syncthreads();
-  if (t == 0 && loss_sum) atomicAdd(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
+  if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
   if (active && u != kInvalidU) atomicAdd(ugrad + u, sg[ls] * x);
 }
 
@@ -172,7 +172,7 @@ __global__ __launch_bounds__(256) void k_fm_fwd_bwd(const uint32_t* __restrict__
   for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, 64);
   if ((t & 63) == 0) sloss[t >> 6] = l;
   __syncthreads();
-  if (t == 0 && loss_sum) atomicAdd(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
+  if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
   if (active && u != kInvalidU) {
     const float g = sg[ls];
     float* gr = ugrad + (long long)u * DIM;

@@ -24,6 +24,19 @@ namespace ss {
 
 static constexpr int kMaxSeg = 64;
 
+// Sharded counters.  Measured on MI355X: one atomic per wave onto a single
+// address serialises at ~12 ns (23K wave atomics = 285 us), while the same
+// adds spread over 256 cache-line-separated shards cost nothing measurable.
+// Every accumulate-only counter (table size, loss sums) is a [256 x 128 B]
+// array; readers sum the shards.
+static constexpr int kCtrShards = 256;
+__device__ __forceinline__ void ctr_add(unsigned long long* base, unsigned long long v) {
+  atomicAdd(base + 16 * (blockIdx.x & (kCtrShards - 1)), v);
+}
+__device__ __forceinline__ void ctr_addf(float* base, float v) {
+  atomicAdd(base + 32 * (blockIdx.x & (kCtrShards - 1)), v);
+}
+
 struct DevTable {
   char* base;         // cap * stride bytes
   uint64_t cap;       // number of slots

@@ -43,13 +43,12 @@ struct RouteSpec {
   int frag_num;
   int nranks;
 };
+int dedup_blocks(long long n);
 void launch_dedup_route(const uint64_t* keys, long long n, uint64_t* scratch_keys,
-                        uint32_t* scratch_uid, unsigned long long scratch_cap,
-                        uint32_t* slot_of, RouteSpec rs, long long ucap,
-                        unsigned long long* ucount, uint64_t* ukeys, float* ugrad, int gdim,
+                        uint32_t* scratch_tag, unsigned long long scratch_cap, uint32_t* slot_of,
+                        RouteSpec rs, long long ucap, unsigned long long* ucount, uint64_t* ukeys,
+                        float* ugrad, int gdim, uint32_t* blk_cnt, uint32_t* inv,
                         hipStream_t st);
-void launch_dedup_inverse(const uint32_t* slot_of, const uint32_t* scratch_uid, long long n,
-                          uint32_t* inv, hipStream_t st);
 void launch_route_keys(const uint64_t* keys, long long n, RouteSpec rs, int* dest,
                        hipStream_t st);
 void launch_gather_rows(const float* src, const uint32_t* idx, long long n, int dim, float* out,

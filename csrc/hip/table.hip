@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void k_probe(DevTable t, const uint64_t* __res
     ins += (lg == 0 && inserted);
   }
   ins = wave_sum_u64(ins);
-  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
 
 // K4: gather parameter rows (dim floats) for resolved slots; missing -> 0.
@@ -162,7 +162,7 @@ __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t*
     ins += (lg == 0 && inserted);
   }
   ins = wave_sum_u64(ins);
-  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
 
 // ---------------------------------------------------------------------------
@@ -277,7 +277,7 @@ __global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t*
     ins += (lg == 0 && inserted);
   }
   ins = wave_sum_u64(ins);
-  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
 
 // K5: fused optimizer update on resolved slots. Keys inside one launch must be
@@ -335,7 +335,7 @@ __global__ __launch_bounds__(256) void k_assign(DevTable t, const uint64_t* __re
     ins += (lg == 0 && inserted);
   }
   ins = wave_sum_u64(ins);
-  if ((threadIdx.x & 63) == 0 && ins) atomicAdd(size_ctr, ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
 
 // K8: compact occupied slots of [s0, s0+n) into (keys_out, rows_out[width]).

@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
   for (int o = 32; o > 0; o >>= 1) loss += __shfl_down(loss, o, 64);
   if (lane == 0) red[w] = loss;
   __syncthreads();
-  if (tid == 0 && loss_sum) atomicAdd(loss_sum, red[0] + red[1] + red[2] + red[3]);
+  if (tid == 0 && loss_sum) ctr_addf(loss_sum, red[0] + red[1] + red[2] + red[3]);
 }
 
 // Synthetic skip-gram batches. Centers are Zipf-like (log-uniform) over V

@@ -18,7 +18,9 @@ import torch
 class PipelinedWorker:
     def __init__(self, engine, rank: int = 0, world: int = 1, active: bool = True):
         self.engine, self.rank, self.world, self.active = engine, rank, world, active
-        self.loss_sum = torch.zeros(1, dtype=torch.float32, device=engine.device)
+        from ..ops.table import loss_buffer
+
+        self.loss_sum = loss_buffer(engine.device)
         self.step_idx = 0
         self._next = None
         self._empty = torch.empty(0, dtype=torch.int64, device=engine.device)
@@ -57,4 +59,4 @@ class PipelinedWorker:
 
     def mean_loss(self) -> float:
         n = self.samples_per_step()
-        return float(self.loss_sum.item()) / n if n else 0.0
+        return float(self.loss_sum.sum().item()) / n if n else 0.0

@@ -55,13 +55,16 @@ class Deduper:
         self.nranks = int(nranks)
         self.gdim = int(gdim)
         self.ucap = self.max_n
-        self.scap = _next_pow2(2 * self.max_n)
+        # load <= 0.67 even if every key is unique; ~0.35 for CTR batches
+        self.scap = _next_pow2(self.max_n + self.max_n // 2 + 1)
+        self.nblocks = self.h.dedup_blocks(max(1, self.max_n))
         d = self.device
         if frag_map is None:
             frag_map = torch.zeros(1, dtype=torch.int32)
         self.frag_map = frag_map.to(d, torch.int32).contiguous()
         self.skeys = torch.empty(self.scap, dtype=torch.int64, device=d)
-        self.suid = torch.empty(self.scap, dtype=torch.int32, device=d)
+        self.stag = torch.empty(self.scap, dtype=torch.int32, device=d)
+        self.blk_cnt = torch.empty(self.nranks * self.nblocks, dtype=torch.int32, device=d)
         self.slot_of = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.inv = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.ukeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64, device=d)
@@ -76,14 +79,12 @@ class Deduper:
         st = _stream_ptr(stream)
         # scratch reset (memset nodes; hipGraph-capturable)
         self.skeys.fill_(-1)
-        self.ucount.zero_()
-        self.h.dedup_route(keys.data_ptr(), n, self.skeys.data_ptr(), self.suid.data_ptr(),
+        self.h.dedup_route(keys.data_ptr(), n, self.skeys.data_ptr(), self.stag.data_ptr(),
                            self.scap, self.slot_of.data_ptr(), self.frag_map.data_ptr(),
                            self.frag_map.numel(), self.nranks, self.ucap, self.ucount.data_ptr(),
                            self.ukeys.data_ptr(),
-                           self.ugrad.data_ptr() if self.ugrad is not None else 0, self.gdim, st)
-        self.h.dedup_inverse(self.slot_of.data_ptr(), self.suid.data_ptr(), n, self.inv.data_ptr(),
-                             st)
+                           self.ugrad.data_ptr() if self.ugrad is not None else 0, self.gdim,
+                           self.blk_cnt.data_ptr(), self.inv.data_ptr(), st)
         return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                            self.nranks, n)
 

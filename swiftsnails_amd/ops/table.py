@@ -30,6 +30,13 @@ from .._native import hip
 from .optim import InitConfig, Optimizer
 
 EMPTY_I64 = -1  # u64 0xFFFF_FFFF_FFFF_FFFF
+CTR_SHARDS = 256  # == ss::kCtrShards
+
+
+def loss_buffer(device) -> torch.Tensor:
+    """Sharded fp32 accumulator the fused model kernels add their loss into
+    (256 shards x 128 B, ss::ctr_addf); read it with ``.sum()``."""
+    return torch.zeros(CTR_SHARDS * 32, dtype=torch.float32, device=device)
 
 
 def _align(x: int, a: int) -> int:
@@ -97,7 +104,8 @@ class HbmTable:
         self.capacity = cap
         self.storage = torch.empty(cap * self.stride, dtype=torch.uint8, device=self.device)
         self.storage.fill_(255)  # every key word = EMPTY
-        self.size_ctr = torch.zeros(1, dtype=torch.int64, device=self.device)
+        # sharded counter: 256 shards x 128 B (see ss_device.h ctr_add)
+        self.size_ctr = torch.zeros(CTR_SHARDS * 16, dtype=torch.int64, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.dt = hip().DevTable(self.storage.data_ptr(), cap, self.stride, self.key_off, self.dim,
                                  self.width)
@@ -189,7 +197,7 @@ class HbmTable:
 
     # -- maintenance --------------------------------------------------------
     def size(self) -> int:
-        return int(self.size_ctr.item())
+        return int(self.size_ctr.sum().item())
 
     def load_factor(self) -> float:
         return self.size() / self.capacity

@@ -150,7 +150,7 @@ def test_lr_fwd_bwd_matches_torch(dev):
     w = (rng.standard_normal(U) * 0.1).astype(np.float32)
     tinv, tx, ty, tw = (torch.from_numpy(a).to(dev) for a in (inv, x, y, w))
     g = torch.zeros(U, device=dev)
-    loss = torch.zeros(1, device=dev)
+    loss = torch.zeros(256 * 32, device=dev)
     pred = torch.empty(B, device=dev)
     st = torch.cuda.current_stream().cuda_stream
     hip().lr_fwd_bwd(tinv.data_ptr(), tx.data_ptr(), ty.data_ptr(), B, F, tw.data_ptr(),
@@ -165,7 +165,7 @@ def test_lr_fwd_bwd_matches_torch(dev):
     gs = (p - Y).repeat_interleave(F) * torch.from_numpy(x).double()
     ref_g = torch.zeros(U, dtype=torch.float64).index_add_(0, torch.from_numpy(inv).long(), gs)
     np.testing.assert_allclose(pred.cpu().numpy(), p.numpy(), rtol=1e-4, atol=1e-5)
-    np.testing.assert_allclose(loss.item(), ref_loss.item(), rtol=1e-4)
+    np.testing.assert_allclose(loss.sum().item(), ref_loss.item(), rtol=1e-4)
     np.testing.assert_allclose(g.cpu().numpy(), ref_g.numpy(), rtol=1e-3, atol=1e-4)
 
 

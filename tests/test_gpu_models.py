@@ -27,7 +27,7 @@ def test_w2v_sgns_tile_matches_reference(dev, D):
     U = (rng.standard_normal((nrows, D)) * 0.3).astype(np.float32)
     inv = np.arange(nrows, dtype=np.int32)
     g = torch.zeros((nrows, D), device=dev)
-    loss = torch.zeros(1, device=dev)
+    loss = torch.zeros(256 * 32, device=dev)
     tu, ti = torch.from_numpy(U).to(dev), torch.from_numpy(inv).to(dev)
     p, es = ti.data_ptr(), 4
     neg_scale = 0.7
@@ -47,7 +47,7 @@ def test_w2v_sgns_tile_matches_reference(dev, D):
                                    rtol=2e-4, atol=2e-5)
         np.testing.assert_allclose(G[T + T * C + t * S:T + T * C + (t + 1) * S], gN, rtol=2e-4,
                                    atol=2e-5)
-    np.testing.assert_allclose(loss.item(), tot, rtol=1e-4)
+    np.testing.assert_allclose(loss.sum().item(), tot, rtol=1e-4)
 
 
 def test_w2v_sgns_duplicate_rows_accumulate(dev):
@@ -89,14 +89,14 @@ def test_fm_fwd_bwd_matches_reference(dev, dim):
     y = (rng.random(B) < 0.4).astype(np.float32)
     tr, ti, ty = (torch.from_numpy(a).to(dev) for a in (rows, inv, y))
     g = torch.zeros((U, dim), device=dev)
-    loss = torch.zeros(1, device=dev)
+    loss = torch.zeros(256 * 32, device=dev)
     pred = torch.empty(B, device=dev)
     hip().fm_fwd_bwd(ti.data_ptr(), ty.data_ptr(), B, F, dim, tr.data_ptr(), g.data_ptr(),
                      loss.data_ptr(), pred.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
     l, p, gr = fm_reference(rows.reshape(B, F, dim), y)
     np.testing.assert_allclose(pred.cpu().numpy(), p, rtol=1e-4, atol=1e-5)
-    np.testing.assert_allclose(loss.item(), l, rtol=1e-4)
+    np.testing.assert_allclose(loss.sum().item(), l, rtol=1e-4)
     np.testing.assert_allclose(g.cpu().numpy().reshape(B, F, dim), gr, rtol=1e-3, atol=1e-5)
 
 
@@ -111,7 +111,7 @@ def test_fm_trains_world1(dev):
     table = HbmTable(9, 200_000, optimizer=opt, init=init, device=dev)
     eng = PSEngine(table, None, max_keys=4096 * 16, dim=9, device=dev)
     w = FMWorker(eng, data)
-    losses = [float(w.step().item()) / 4096 for _ in range(50)]
+    losses = [float(w.step().sum().item()) / 4096 for _ in range(50)]
     table.check()
     assert np.mean(losses[-5:]) < np.mean(losses[:3]) - 0.02, losses
 
