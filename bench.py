@@ -45,6 +45,7 @@ def main(argv=None):
     ap.add_argument("--tail", type=float, default=0.1)
     ap.add_argument("--optimizer", default="adagrad")
     ap.add_argument("--lr", type=float, default=0.05)
+    ap.add_argument("--grad-mode", default="segreduce", choices=["segreduce", "atomic"])
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -88,7 +89,7 @@ def main(argv=None):
     table = make_lr_table(a.features, world, optimizer=opt, load=a.load, device=dev)
     engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev,
                       count_transport=ctrans)
-    worker = SparseLRWorker(engine, data, rank=rank, world=world)
+    worker = SparseLRWorker(engine, data, rank=rank, world=world, grad_mode=a.grad_mode)
 
     def barrier():
         if world > 1:

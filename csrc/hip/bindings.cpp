@@ -170,6 +170,27 @@ PYBIND11_MODULE(_ss_hip, m) {
                       S(st));
   });
 
+  m.def("sr_nbins", &sr_nbins);
+  m.def("sr_nchunks", &sr_nchunks);
+  m.def("sr_plan", [](uintptr_t inv, long long n, uintptr_t ucount, int nranks, long long ucap,
+                      uintptr_t hist, int nbins, uintptr_t pos, uintptr_t st) {
+    launch_sr_plan(P<const uint32_t>(inv), n, P<const unsigned long long>(ucount), nranks, ucap,
+                   P<uint32_t>(hist), nbins, P<uint32_t>(pos), S(st));
+  });
+  m.def("sr_reduce", [](uintptr_t pairs, uintptr_t hist, int nbins, long long n, uintptr_t ucount,
+                        int nranks, long long ucap, uintptr_t ugrad, uintptr_t st) {
+    launch_sr_reduce(P<const void>(pairs), P<const uint32_t>(hist), nbins, n,
+                     P<const unsigned long long>(ucount), nranks, ucap, P<float>(ugrad), S(st));
+  });
+  m.def("lr_fwd_pairs", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
+                           uintptr_t uvals, uintptr_t ucount, int nranks, long long ucap,
+                           uintptr_t pos, uintptr_t pairs, uintptr_t loss, uintptr_t pred,
+                           uintptr_t st) {
+    launch_lr_fwd_pairs(P<const uint32_t>(inv), P<const float>(xval), P<const float>(labels), B, F,
+                        P<const float>(uvals), P<const unsigned long long>(ucount), nranks, ucap,
+                        P<const uint32_t>(pos), P<void>(pairs), P<float>(loss), P<float>(pred),
+                        S(st));
+  });
   m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
                          uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {
     launch_fm_fwd_bwd(P<const uint32_t>(inv), P<const float>(labels), B, F, dim,

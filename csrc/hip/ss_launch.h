@@ -68,6 +68,20 @@ void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, i
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
                        hipStream_t st);
 
+// --- segreduce.hip
+int sr_nbins(long long max_unique);
+int sr_nchunks(long long n);
+void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* ucount,
+                    int nranks, long long ucap, uint32_t* hist, int nbins, uint32_t* pos,
+                    hipStream_t st);
+void launch_sr_reduce(const void* pairs, const uint32_t* hist, int nbins, long long n,
+                      const unsigned long long* ucount, int nranks, long long ucap, float* ugrad,
+                      hipStream_t st);
+void launch_lr_fwd_pairs(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
+                         const float* uvals, const unsigned long long* ucount, int nranks,
+                         long long ucap, const uint32_t* pos, void* pairs, float* loss_sum,
+                         float* pred, hipStream_t st);
+
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,

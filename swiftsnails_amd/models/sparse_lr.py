@@ -59,13 +59,40 @@ class SparseLRWorker(PipelinedWorker):
     parameter staleness — routing does not read parameters)."""
 
     def __init__(self, engine, data: CtrSynth, rank: int = 0, world: int = 1,
-                 active: bool = True):
+                 active: bool = True, grad_mode: str = "segreduce"):
         super().__init__(engine, rank, world, active)
         self.data = data
         dev = engine.device
         B, F = data.batch_size, data.num_fields
-        self.keys = [torch.empty(B * F, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
+        n = B * F
+        self.keys = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
         self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
+        # grad_mode "segreduce": atomic-free duplicate merge (segreduce.hip) —
+        # bin plan on the route stream, (key, grad) pairs + LDS reduce on main;
+        # "atomic": one float atomicAdd per occurrence (the first design).
+        self.grad_mode = grad_mode
+        if grad_mode == "segreduce":
+            h = hip()
+            self.nbins = h.sr_nbins(n)
+            nch = h.sr_nchunks(n)
+            self.hist = [torch.empty(self.nbins * nch + 1, dtype=torch.int32, device=dev)
+                         for _ in range(engine.depth)]
+            self.pos = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(engine.depth)]
+            self.pairs = torch.empty(n, dtype=torch.int64, device=dev)
+            for dd in engine.dedupers:
+                dd.zero_grad = False  # the reduce writes every unique row
+
+    def _post(self, dd, slot, st):
+        hip().sr_plan(dd.inv.data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks, dd.ucap,
+                      self.hist[slot].data_ptr(), self.nbins, self.pos[slot].data_ptr(), st)
+
+    def _route(self, step: int):
+        if self.grad_mode != "segreduce" or not self.active:
+            return super()._route(step)
+        slot = self.engine._next_slot
+        return self.engine.route(produce=lambda stream: self._produce(step, slot,
+                                                                      stream.cuda_stream),
+                                 post=self._post)
 
     def _produce(self, step, slot, stream):
         self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
@@ -74,7 +101,17 @@ class SparseLRWorker(PipelinedWorker):
 
     def _compute(self, rnd, slot, st):
         d = self.data
-        hip().lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
+        h = hip()
+        if self.grad_mode == "segreduce":
+            dd = rnd.dd
+            h.lr_fwd_pairs(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
+                           d.num_fields, rnd.uvals.data_ptr(), dd.ucount.data_ptr(), dd.nranks,
+                           dd.ucap, self.pos[slot].data_ptr(), self.pairs.data_ptr(),
+                           self.loss_sum.data_ptr(), 0, st)
+            h.sr_reduce(self.pairs.data_ptr(), self.hist[slot].data_ptr(), self.nbins, dd.n,
+                        dd.ucount.data_ptr(), dd.nranks, dd.ucap, rnd.ugrad.data_ptr(), st)
+        else:
+            h.lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
                          self.loss_sum.data_ptr(), 0, st)
 

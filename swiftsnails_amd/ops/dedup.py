@@ -45,8 +45,12 @@ class Deduper:
     """Device dedup/route with scratch sized for up to ``max_n`` keys per call."""
 
     def __init__(self, max_n: int, nranks: int = 1, frag_map: Optional[torch.Tensor] = None,
-                 gdim: int = 1, device=None, with_grad: bool = True):
+                 gdim: int = 1, device=None, with_grad: bool = True, zero_grad: bool = True):
         from .._native import hip
+
+        # zero_grad=False: the model's backward writes every unique row itself
+        # (e.g. the segmented reduction of segreduce.hip), skip zeroing here.
+        self.zero_grad = zero_grad
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -83,7 +87,8 @@ class Deduper:
                            self.scap, self.slot_of.data_ptr(), self.frag_map.data_ptr(),
                            self.frag_map.numel(), self.nranks, self.ucap, self.ucount.data_ptr(),
                            self.ukeys.data_ptr(),
-                           self.ugrad.data_ptr() if self.ugrad is not None else 0, self.gdim,
+                           self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0,
+                           self.gdim,
                            self.blk_cnt.data_ptr(), self.inv.data_ptr(), st)
         return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                            self.nranks, n)
@@ -93,7 +98,7 @@ class CpuDeduper:
     """Host implementation with the same output layout (CPU engine / tests)."""
 
     def __init__(self, max_n: int, nranks: int = 1, frag_map: Optional[torch.Tensor] = None,
-                 gdim: int = 1, device=None, with_grad: bool = True):
+                 gdim: int = 1, device=None, with_grad: bool = True, zero_grad: bool = True):
         self.max_n, self.nranks, self.gdim = int(max_n), int(nranks), int(gdim)
         self.ucap = self.max_n
         self.frag_map = (frag_map.cpu().numpy().astype(np.int64) if frag_map is not None

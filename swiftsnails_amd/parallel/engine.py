@@ -106,7 +106,8 @@ class PSEngine:
 
     def __init__(self, table, transport: Optional[Transport], max_keys: int, dim: int,
                  frag_num: int = 0, server_ranks: Optional[Sequence[int]] = None, device=None,
-                 count_transport: Optional[Transport] = None, depth: int = 2):
+                 count_transport: Optional[Transport] = None, depth: int = 2,
+                 zero_grad: bool = True):
         self.t = transport or LoopbackTransport()
         self.ct = count_transport or self.t
         self.rank, self.world = self.t.rank, self.t.world
@@ -130,7 +131,7 @@ class PSEngine:
         dd_cls = Deduper if self.gpu else CpuDeduper
         fm = torch.from_numpy(self.frag_map.astype(np.int32))
         self.dedupers = [dd_cls(self.max_keys, nranks=self.world, frag_map=fm, gdim=self.dim,
-                                device=self.device) for _ in range(self.depth)]
+                                device=self.device, zero_grad=zero_grad) for _ in range(self.depth)]
         N, cap, d = self.world, self.max_keys, self.dim
         dev = self.device
         self.uvals = [torch.empty((N * cap, d), dtype=torch.float32, device=dev)
@@ -158,12 +159,14 @@ class PSEngine:
         self._next_slot = 0
 
     # ------------------------------------------------------------ stage 1
-    def route(self, keys: Optional[torch.Tensor] = None, produce=None) -> Routed:
+    def route(self, keys: Optional[torch.Tensor] = None, produce=None, post=None) -> Routed:
         """Dedup + route a batch on the route stream (non-blocking on GPU).
 
         Either pass ``keys`` (produced on the current stream), or a
         ``produce(stream)`` callable that writes and returns the keys on the
-        route stream (e.g. the synthetic data generator)."""
+        route stream (e.g. the synthetic data generator).  ``post(dd, slot,
+        stream_ptr)`` runs right after dedup on the route stream (model-side
+        planning that only depends on the key layout)."""
         slot = self._next_slot
         self._next_slot = (slot + 1) % self.depth
         dd_fn = self.dedupers[slot]
@@ -188,6 +191,8 @@ class PSEngine:
             if keys.device != self.device:
                 keys = keys.to(self.device)
             dd = dd_fn(keys, stream=rs)
+            if post is not None:
+                post(dd, slot, rs.cuda_stream)
             counts = None
             if not self.fast1:
                 counts = self.ct.exchange_counts_async(dd.ucount, pinned=self._pins[slot],

@@ -169,6 +169,56 @@ def test_lr_fwd_bwd_matches_torch(dev):
     np.testing.assert_allclose(g.cpu().numpy(), ref_g.numpy(), rtol=1e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_segreduce_lr_matches_atomic_path(dev, nranks):
+    """Atomic-free bin-partition reduction == per-occurrence atomics (and torch)."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.dedup import Deduper
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    h = hip()
+    B, F = 20000, 13
+    n = B * F
+    rng = np.random.default_rng(21 + nranks)
+    keys = (rng.zipf(1.3, n) % 300000).astype(np.int64)  # heavy duplication + long tail
+    fm = HashFrag(nranks, 64).rank_map()
+    d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=1,
+                device=dev)
+    r = d(torch.from_numpy(keys).to(dev))
+    st = torch.cuda.current_stream().cuda_stream
+    U = nranks * d.ucap
+    uvals = (torch.randn(U, device=dev) * 0.1)
+    y = torch.from_numpy((rng.random(B) < 0.3).astype(np.float32)).to(dev)
+    # atomic reference path
+    g_at = torch.zeros(U, device=dev)
+    l_at = torch.zeros(256 * 32, device=dev)
+    h.lr_fwd_bwd(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), g_at.data_ptr(),
+                 l_at.data_ptr(), 0, st)
+    # segmented path
+    nbins, nch = h.sr_nbins(n), h.sr_nchunks(n)
+    hist = torch.empty(nbins * nch + 1, dtype=torch.int32, device=dev)
+    pos = torch.empty(n, dtype=torch.int32, device=dev)
+    pairs = torch.empty(n, dtype=torch.int64, device=dev)
+    g_sr = torch.full((U,), 12345.0, device=dev)
+    l_sr = torch.zeros(256 * 32, device=dev)
+    h.sr_plan(r.inv.data_ptr(), n, r.ucount.data_ptr(), nranks, d.ucap, hist.data_ptr(), nbins,
+              pos.data_ptr(), st)
+    h.lr_fwd_pairs(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), r.ucount.data_ptr(),
+                   nranks, d.ucap, pos.data_ptr(), pairs.data_ptr(), l_sr.data_ptr(), 0, st)
+    h.sr_reduce(pairs.data_ptr(), hist.data_ptr(), nbins, n, r.ucount.data_ptr(), nranks, d.ucap,
+                g_sr.data_ptr(), st)
+    torch.cuda.synchronize()
+    uc = r.ucount.cpu().numpy()
+    assert int(hist[-1].item()) == n  # every valid occurrence placed exactly once
+    ps = np.sort(pos.cpu().numpy().view(np.uint32))
+    np.testing.assert_array_equal(ps, np.arange(n, dtype=np.uint32))
+    for q in range(nranks):
+        a, b = q * d.ucap, q * d.ucap + uc[q]
+        np.testing.assert_allclose(g_sr[a:b].cpu().numpy(), g_at[a:b].cpu().numpy(), rtol=1e-4,
+                                   atol=1e-4)
+    np.testing.assert_allclose(l_sr.sum().item(), l_at.sum().item(), rtol=1e-5)
+
+
 def test_gen_ctr_ranges(dev):
     from swiftsnails_amd.models.sparse_lr import CtrSynth
 
