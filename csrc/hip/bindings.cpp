@@ -172,14 +172,18 @@ PYBIND11_MODULE(_ss_hip, m) {
 
   m.def("sr_nbins", &sr_nbins);
   m.def("sr_nchunks", &sr_nchunks);
+  m.def("sr_max_items", &sr_max_items);
   m.def("sr_plan", [](uintptr_t inv, long long n, uintptr_t ucount, int nranks, long long ucap,
-                      uintptr_t hist, int nbins, uintptr_t pos, uintptr_t st) {
+                      uintptr_t hist, int nbins, uintptr_t pos, uintptr_t items, uintptr_t nitems,
+                      uintptr_t st) {
     launch_sr_plan(P<const uint32_t>(inv), n, P<const unsigned long long>(ucount), nranks, ucap,
-                   P<uint32_t>(hist), nbins, P<uint32_t>(pos), S(st));
+                   P<uint32_t>(hist), nbins, P<uint32_t>(pos), P<void>(items), P<uint32_t>(nitems),
+                   S(st));
   });
-  m.def("sr_reduce", [](uintptr_t pairs, uintptr_t hist, int nbins, long long n, uintptr_t ucount,
-                        int nranks, long long ucap, uintptr_t ugrad, uintptr_t st) {
-    launch_sr_reduce(P<const void>(pairs), P<const uint32_t>(hist), nbins, n,
+  m.def("sr_reduce", [](uintptr_t pairs, uintptr_t items, uintptr_t nitems, long long n,
+                        uintptr_t ucount, int nranks, long long ucap, uintptr_t ugrad,
+                        uintptr_t st) {
+    launch_sr_reduce(P<const void>(pairs), P<const void>(items), P<const uint32_t>(nitems), n,
                      P<const unsigned long long>(ucount), nranks, ucap, P<float>(ugrad), S(st));
   });
   m.def("lr_fwd_pairs", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,

@@ -1,4 +1,4 @@
-// segreduce.hip — atomic-free duplicate-key gradient reduction (K7) for
+// segreduce.hip — atomic-light duplicate-key gradient reduction (K7) for
 // scalar-per-key models (sparse LR).
 //
 // The reference merges duplicate-key gradients on the worker
@@ -6,20 +6,23 @@
 // global_param_cache.h:14-15; PushAccessMethod::merge_push_value,
 // sparse_access_method.h:39-40).  The first version here scattered one float
 // atomicAdd per key occurrence: 2.56M atomics = 164 us/step, because on
-// MI355X every device-scope atomic executes at the memory side (~18 G/s).
+// MI355X every device-scope atomic executes at the memory side (~18 G/s for
+// one-lane-per-address adds, tools/mb_atomics.hip).
 //
-// Replacement = one radix-partition pass + an LDS accumulation:
+// Replacement = one radix-partition pass + LDS accumulation:
 //   route stream (off the critical path, right after dedup):
-//     count      per chunk of 8192 occurrences, histogram of bin(cu) in LDS,
-//                where cu = compact unique id and bin = cu >> 13
-//     scan       exclusive scan over [bin][chunk] (one workgroup)
+//     count      per 8192-occurrence chunk, histogram of bin(cu) in LDS
+//                (cu = compact unique id, bin = cu >> 13)
+//     scan       exclusive scan over [bin][chunk] through LDS tiles, then a
+//                work list: each bin cut into <= 8192-pair items, so a bin
+//                holding the batch's hot keys (dedup numbers them first) is
+//                spread over many workgroups instead of serialising one
 //     positions  every occurrence gets its slot in the bin-ordered pair array
-//                (LDS cursor per bin, no global atomics)
 //   main stream:
 //     the model's forward kernel writes (cu & 8191, grad) at that slot
-//     reduce     one workgroup per bin: LDS atomics into 8192 accumulators,
-//                then ONE coalesced store per unique key (also zero-fills the
-//                keys with no contribution, so dedup need not zero grads)
+//     reduce     one workgroup per work item: LDS atomics into 8192
+//                accumulators, then one coalesced row-shaped atomicAdd per
+//                touched unique key (full-rate atomic shape, ~10 MB/step)
 #include "ss_device.h"
 #include "ss_launch.h"
 
@@ -29,7 +32,9 @@ static constexpr uint32_t kInvS = 0xFFFFFFFFu;
 static constexpr int kBinShift = 13;
 static constexpr int kBinW = 1 << kBinShift;  // unique ids per bin (LDS floats)
 static constexpr int kChunk = 8192;           // occurrences per count/positions block
+static constexpr int kItem = 8192;            // pairs per reduce work item
 static constexpr int kMaxBins = 4096;
+static constexpr int kPer = kChunk / 1024;    // occurrences per thread (1024-thread blocks)
 
 // compact id <-> layout id: uid = d*ucap + local, cu = prefix[d] + local
 struct CuMap {
@@ -38,114 +43,179 @@ struct CuMap {
   long long ucap;
 };
 
-__device__ __forceinline__ void load_prefix(const CuMap& m, unsigned long long* pre) {
+__device__ __forceinline__ void load_prefix(const CuMap& m, unsigned int* pre) {
   if (threadIdx.x == 0) {
-    unsigned long long a = 0;
+    unsigned int a = 0;
     for (int d = 0; d < m.nranks; ++d) {
       pre[d] = a;
-      a += m.ucount[d];
+      a += (unsigned int)m.ucount[d];
     }
     pre[m.nranks] = a;
   }
   __syncthreads();
 }
-__device__ __forceinline__ unsigned long long cu_of(const CuMap& m, const unsigned long long* pre,
-                                                    uint32_t uid) {
-  const unsigned long long d = uid / (unsigned long long)m.ucap;
-  return pre[d] + (uid - d * (unsigned long long)m.ucap);
+__device__ __forceinline__ unsigned int cu_of(const CuMap& m, const unsigned int* pre, uint32_t uid) {
+  if (m.nranks == 1) return uid;
+  const uint32_t d = uid / (uint32_t)m.ucap;  // uid < 2^31: 32-bit divide
+  return pre[d] + (uid - d * (uint32_t)m.ucap);
 }
 
-__global__ __launch_bounds__(256) void k_sr_count(const uint32_t* __restrict__ inv, long long n,
-                                                  CuMap m, uint32_t* __restrict__ hist, int nbins,
-                                                  int nchunks) {
-  __shared__ unsigned long long pre[kMaxSeg + 1];
+__global__ __launch_bounds__(1024) void k_sr_count(const uint32_t* __restrict__ inv, long long n,
+                                                   CuMap m, uint32_t* __restrict__ hist, int nbins,
+                                                   int nchunks) {
+  __shared__ unsigned int pre[kMaxSeg + 1];
   __shared__ unsigned int h[kMaxBins];
-  for (int b = threadIdx.x; b < nbins; b += 256) h[b] = 0;
+  for (int b = threadIdx.x; b < nbins; b += 1024) h[b] = 0;
   load_prefix(m, pre);
-  const long long a = (long long)blockIdx.x * kChunk;
-  const long long e = a + kChunk < n ? a + kChunk : n;
-  for (long long j = a + threadIdx.x; j < e; j += 256) {
-    const uint32_t u = inv[j];
-    if (u != kInvS) atomicAdd(&h[cu_of(m, pre, u) >> kBinShift], 1u);
-  }
+  const long long a = (long long)blockIdx.x * kChunk + threadIdx.x;
+  uint32_t u[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) u[k] = a + k * 1024 < n ? inv[a + k * 1024] : kInvS;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+    if (u[k] != kInvS) atomicAdd(&h[cu_of(m, pre, u[k]) >> kBinShift], 1u);
   __syncthreads();
-  for (int b = threadIdx.x; b < nbins; b += 256) hist[(long long)b * nchunks + blockIdx.x] = h[b];
+  for (int b = threadIdx.x; b < nbins; b += 1024) hist[(long long)b * nchunks + blockIdx.x] = h[b];
 }
 
-// In-place exclusive scan of len values (single workgroup); total -> data[len].
-__global__ __launch_bounds__(1024) void k_scan_flat(uint32_t* __restrict__ data, long long len) {
+// Exclusive scan of data[0, len) in place (single workgroup, LDS tiles of
+// 32K values, coalesced loads); total -> data[len].  Then the reduce work
+// list: items[k] = (bin, first pair, end pair), <= kItem pairs each.
+__global__ __launch_bounds__(1024) void k_sr_scan(uint32_t* __restrict__ data, int nbins,
+                                                  int nchunks, uint4* __restrict__ items,
+                                                  uint32_t* __restrict__ nitems) {
+  constexpr int kTile = 32768, kPT = kTile / 1024;
+  __shared__ unsigned int tile[kTile];
   __shared__ unsigned int wsum[16];
+  __shared__ unsigned int carry;
+  const long long len = (long long)nbins * nchunks;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  const long long per = (len + 1023) / 1024;
-  const long long a = t * per, e = a + per < len ? a + per : len;
-  unsigned int s = 0;
-  for (long long i = a; i < e; ++i) s += data[i];
-  unsigned int x = s;
-  for (int o = 1; o < 64; o <<= 1) {
-    const unsigned int y = __shfl_up(x, o, 64);
-    if (lane >= o) x += y;
-  }
-  if (lane == 63) wsum[w] = x;
+  if (t == 0) carry = 0;
   __syncthreads();
-  if (w == 0) {
-    unsigned int ws = lane < 16 ? wsum[lane] : 0u;
-    for (int o = 1; o < 16; o <<= 1) {
-      const unsigned int y = __shfl_up(ws, o, 64);
-      if (lane >= o) ws += y;
+  for (long long base = 0; base < len; base += kTile) {
+    for (int k = 0; k < kPT; ++k) {
+      const long long i = base + k * 1024 + t;
+      tile[k * 1024 + t] = i < len ? data[i] : 0u;
     }
-    if (lane < 16) wsum[lane] = ws;
+    __syncthreads();
+    unsigned int s = 0;
+#pragma unroll
+    for (int k = 0; k < kPT; ++k) s += tile[t * kPT + k];
+    unsigned int x = s;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+      unsigned int ws = lane < 16 ? wsum[lane] : 0u;
+      for (int o = 1; o < 16; o <<= 1) {
+        const unsigned int y = __shfl_up(ws, o, 64);
+        if (lane >= o) ws += y;
+      }
+      if (lane < 16) wsum[lane] = ws;
+    }
+    __syncthreads();
+    unsigned int run = carry + (w ? wsum[w - 1] : 0u) + x - s;
+#pragma unroll
+    for (int k = 0; k < kPT; ++k) {
+      const unsigned int v = tile[t * kPT + k];
+      tile[t * kPT + k] = run;
+      run += v;
+    }
+    __syncthreads();
+    for (int k = 0; k < kPT; ++k) {
+      const long long i = base + k * 1024 + t;
+      if (i < len) data[i] = tile[k * 1024 + t];
+    }
+    if (t == 0) carry += wsum[15];
+    __syncthreads();
   }
+  if (t == 0) data[len] = carry;
   __syncthreads();
-  unsigned int run = (w ? wsum[w - 1] : 0u) + x - s;
-  for (long long i = a; i < e; ++i) {
-    const unsigned int v = data[i];
-    data[i] = run;
-    run += v;
+  // ---- work list: per bin ceil(pairs / kItem) items; block scan over bins
+  unsigned int off = 0;
+  for (int b0 = 0; b0 < nbins; b0 += 1024) {
+    const int b = b0 + t;
+    unsigned int st = 0, en = 0, cnt = 0;
+    if (b < nbins) {
+      st = data[(long long)b * nchunks];
+      en = b + 1 < nbins ? data[(long long)(b + 1) * nchunks] : data[len];
+      cnt = (en - st + kItem - 1) / kItem;
+    }
+    unsigned int x = cnt;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    if (w == 0) {
+      unsigned int ws = lane < 16 ? wsum[lane] : 0u;
+      for (int o = 1; o < 16; o <<= 1) {
+        const unsigned int y = __shfl_up(ws, o, 64);
+        if (lane >= o) ws += y;
+      }
+      if (lane < 16) wsum[lane] = ws;
+    }
+    __syncthreads();
+    unsigned int k0 = off + (w ? wsum[w - 1] : 0u) + x - cnt;
+    for (unsigned int q = 0; q < cnt; ++q) {
+      const unsigned int a = st + q * kItem;
+      items[k0 + q] = make_uint4((unsigned)b, a, a + kItem < en ? a + kItem : en, 0u);
+    }
+    off += wsum[15];
+    __syncthreads();
   }
-  if (t == 1023) data[len] = wsum[15];
+  if (t == 0) *nitems = off;
 }
 
-__global__ __launch_bounds__(256) void k_sr_positions(const uint32_t* __restrict__ inv, long long n,
-                                                      CuMap m, const uint32_t* __restrict__ hist,
-                                                      int nbins, int nchunks,
-                                                      uint32_t* __restrict__ pos) {
-  __shared__ unsigned long long pre[kMaxSeg + 1];
+__global__ __launch_bounds__(1024) void k_sr_positions(const uint32_t* __restrict__ inv, long long n,
+                                                       CuMap m, const uint32_t* __restrict__ hist,
+                                                       int nbins, int nchunks,
+                                                       uint32_t* __restrict__ pos) {
+  __shared__ unsigned int pre[kMaxSeg + 1];
   __shared__ unsigned int cur[kMaxBins];
-  for (int b = threadIdx.x; b < nbins; b += 256)
+  for (int b = threadIdx.x; b < nbins; b += 1024)
     cur[b] = hist[(long long)b * nchunks + blockIdx.x];
   load_prefix(m, pre);
-  const long long a = (long long)blockIdx.x * kChunk;
-  const long long e = a + kChunk < n ? a + kChunk : n;
-  for (long long j = a + threadIdx.x; j < e; j += 256) {
-    const uint32_t u = inv[j];
-    pos[j] = u == kInvS ? kInvS : atomicAdd(&cur[cu_of(m, pre, u) >> kBinShift], 1u);
+  const long long a = (long long)blockIdx.x * kChunk + threadIdx.x;
+  uint32_t u[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) u[k] = a + k * 1024 < n ? inv[a + k * 1024] : kInvS;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const long long j = a + k * 1024;
+    if (j < n) pos[j] = u[k] == kInvS ? kInvS : atomicAdd(&cur[cu_of(m, pre, u[k]) >> kBinShift], 1u);
   }
 }
 
-// One workgroup per bin. pairs[i] = (cu & (kBinW-1), grad bits).
+// One workgroup per work item. pairs[i] = (cu & (kBinW-1), grad bits).
+// ugrad must be zeroed for the round's unique keys (dedup does it).
 __global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pairs,
-                                                    const uint32_t* __restrict__ hist, int nbins,
-                                                    int nchunks, CuMap m,
+                                                    const uint4* __restrict__ items,
+                                                    const uint32_t* __restrict__ nitems, CuMap m,
                                                     float* __restrict__ ugrad) {
-  __shared__ unsigned long long pre[kMaxSeg + 1];
+  __shared__ unsigned int pre[kMaxSeg + 1];
   __shared__ float acc[kBinW];
-  const int bin = blockIdx.x;
-  for (int c = threadIdx.x; c < kBinW; c += blockDim.x) acc[c] = 0.f;
+  if (blockIdx.x >= *nitems) return;  // block-uniform
+  const uint4 it = items[blockIdx.x];
+  for (int c = threadIdx.x; c < kBinW; c += 1024) acc[c] = 0.f;
   load_prefix(m, pre);
-  const uint32_t a = hist[(long long)bin * nchunks];
-  const uint32_t e = hist[(long long)(bin + 1) * nchunks];  // bin+1 == nbins -> total slot
-  for (uint32_t p = a + threadIdx.x; p < e; p += blockDim.x) {
+  for (uint32_t p = it.y + threadIdx.x; p < it.z; p += 1024) {
     const uint2 pr = pairs[p];
     atomicAdd(&acc[pr.x], __uint_as_float(pr.y));
   }
   __syncthreads();
-  const unsigned long long total = pre[m.nranks];
-  for (int c = threadIdx.x; c < kBinW; c += blockDim.x) {
-    const unsigned long long cu = ((unsigned long long)bin << kBinShift) + c;
-    if (cu >= total) break;
+  const unsigned int total = pre[m.nranks];
+  for (int c = threadIdx.x; c < kBinW; c += 1024) {
+    const unsigned int cu = (it.x << kBinShift) + (unsigned)c;
+    const float v = acc[c];
+    if (cu >= total || v == 0.f) continue;
     int d = 0;
     while (d + 1 < m.nranks && cu >= pre[d + 1]) ++d;
-    ugrad[(unsigned long long)d * m.ucap + (cu - pre[d])] = acc[c];
+    atomicAdd(ugrad + (unsigned long long)d * m.ucap + (cu - pre[d]), v);
   }
 }
 
@@ -158,7 +228,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_pairs(const uint32_t* __restrict
                                                       uint2* __restrict__ pairs,
                                                       float* __restrict__ loss_sum,
                                                       float* __restrict__ pred) {
-  __shared__ unsigned long long pre[kMaxSeg + 1];
+  __shared__ unsigned int pre[kMaxSeg + 1];
   __shared__ float sdot[256];
   __shared__ float sg[256];
   __shared__ float sloss[4];
@@ -191,38 +261,46 @@ __global__ __launch_bounds__(256) void k_lr_fwd_pairs(const uint32_t* __restrict
   __syncthreads();
   if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
   if (active && u != kInvS) {
-    const unsigned long long cu = cu_of(m, pre, u);
-    pairs[pos[j]] = make_uint2((uint32_t)(cu & (kBinW - 1)), __float_as_uint(sg[ls] * x));
+    const unsigned int cu = cu_of(m, pre, u);
+    pairs[pos[j]] = make_uint2(cu & (kBinW - 1), __float_as_uint(sg[ls] * x));
   }
 }
 
 // -------------------------------------------------------------- launchers
 int sr_nbins(long long max_unique) { return (int)((max_unique + kBinW - 1) >> kBinShift); }
 int sr_nchunks(long long n) { return (int)((n + kChunk - 1) / kChunk); }
+int sr_max_items(long long n) { return sr_nbins(n) + sr_nchunks(n) + 1; }
 
 void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* ucount,
                     int nranks, long long ucap, uint32_t* hist, int nbins, uint32_t* pos,
-                    hipStream_t st) {
-  if (n <= 0) return;
+                    void* items, uint32_t* nitems, hipStream_t st) {
+  if (n <= 0) {
+    check_hip(hipMemsetAsync(nitems, 0, 4, st), "nitems");
+    return;
+  }
   if (nbins > kMaxBins || nbins < 1) throw_error("segreduce: too many unique keys per call");
+  if ((unsigned long long)nranks * (unsigned long long)ucap >= 0x80000000ull)
+    throw_error("segreduce: unique-id space exceeds 31 bits");
   const int nch = sr_nchunks(n);
   CuMap m{ucount, nranks, ucap};
-  hipLaunchKernelGGL(k_sr_count, dim3(nch), dim3(256), 0, st, inv, n, m, hist, nbins, nch);
+  hipLaunchKernelGGL(k_sr_count, dim3(nch), dim3(1024), 0, st, inv, n, m, hist, nbins, nch);
   check_launch("k_sr_count");
-  hipLaunchKernelGGL(k_scan_flat, dim3(1), dim3(1024), 0, st, hist, (long long)nbins * nch);
-  check_launch("k_scan_flat");
-  hipLaunchKernelGGL(k_sr_positions, dim3(nch), dim3(256), 0, st, inv, n, m, hist, nbins, nch,
+  hipLaunchKernelGGL(k_sr_scan, dim3(1), dim3(1024), 0, st, hist, nbins, nch,
+                     reinterpret_cast<uint4*>(items), nitems);
+  check_launch("k_sr_scan");
+  hipLaunchKernelGGL(k_sr_positions, dim3(nch), dim3(1024), 0, st, inv, n, m, hist, nbins, nch,
                      pos);
   check_launch("k_sr_positions");
 }
 
-void launch_sr_reduce(const void* pairs, const uint32_t* hist, int nbins, long long n,
+void launch_sr_reduce(const void* pairs, const void* items, const uint32_t* nitems, long long n,
                       const unsigned long long* ucount, int nranks, long long ucap, float* ugrad,
                       hipStream_t st) {
   if (n <= 0) return;
   CuMap m{ucount, nranks, ucap};
-  hipLaunchKernelGGL(k_sr_reduce, dim3(nbins), dim3(1024), 0, st,
-                     reinterpret_cast<const uint2*>(pairs), hist, nbins, sr_nchunks(n), m, ugrad);
+  hipLaunchKernelGGL(k_sr_reduce, dim3(sr_max_items(n)), dim3(1024), 0, st,
+                     reinterpret_cast<const uint2*>(pairs), reinterpret_cast<const uint4*>(items),
+                     nitems, m, ugrad);
   check_launch("k_sr_reduce");
 }
 

@@ -71,10 +71,11 @@ void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, i
 // --- segreduce.hip
 int sr_nbins(long long max_unique);
 int sr_nchunks(long long n);
+int sr_max_items(long long n);
 void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* ucount,
                     int nranks, long long ucap, uint32_t* hist, int nbins, uint32_t* pos,
-                    hipStream_t st);
-void launch_sr_reduce(const void* pairs, const uint32_t* hist, int nbins, long long n,
+                    void* items, uint32_t* nitems, hipStream_t st);
+void launch_sr_reduce(const void* pairs, const void* items, const uint32_t* nitems, long long n,
                       const unsigned long long* ucount, int nranks, long long ucap, float* ugrad,
                       hipStream_t st);
 void launch_lr_fwd_pairs(const uint32_t* inv, const float* xval, const float* labels, int B, int F,

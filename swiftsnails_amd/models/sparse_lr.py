@@ -78,13 +78,17 @@ class SparseLRWorker(PipelinedWorker):
             self.hist = [torch.empty(self.nbins * nch + 1, dtype=torch.int32, device=dev)
                          for _ in range(engine.depth)]
             self.pos = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(engine.depth)]
+            mi = h.sr_max_items(n)
+            self.items = [torch.empty(4 * mi, dtype=torch.int32, device=dev)
+                          for _ in range(engine.depth)]
+            self.nitems = [torch.zeros(1, dtype=torch.int32, device=dev)
+                           for _ in range(engine.depth)]
             self.pairs = torch.empty(n, dtype=torch.int64, device=dev)
-            for dd in engine.dedupers:
-                dd.zero_grad = False  # the reduce writes every unique row
 
     def _post(self, dd, slot, st):
         hip().sr_plan(dd.inv.data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks, dd.ucap,
-                      self.hist[slot].data_ptr(), self.nbins, self.pos[slot].data_ptr(), st)
+                      self.hist[slot].data_ptr(), self.nbins, self.pos[slot].data_ptr(),
+                      self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), st)
 
     def _route(self, step: int):
         if self.grad_mode != "segreduce" or not self.active:
@@ -108,8 +112,9 @@ class SparseLRWorker(PipelinedWorker):
                            d.num_fields, rnd.uvals.data_ptr(), dd.ucount.data_ptr(), dd.nranks,
                            dd.ucap, self.pos[slot].data_ptr(), self.pairs.data_ptr(),
                            self.loss_sum.data_ptr(), 0, st)
-            h.sr_reduce(self.pairs.data_ptr(), self.hist[slot].data_ptr(), self.nbins, dd.n,
-                        dd.ucount.data_ptr(), dd.nranks, dd.ucap, rnd.ugrad.data_ptr(), st)
+            h.sr_reduce(self.pairs.data_ptr(), self.items[slot].data_ptr(),
+                        self.nitems[slot].data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks,
+                        dd.ucap, rnd.ugrad.data_ptr(), st)
         else:
             h.lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),

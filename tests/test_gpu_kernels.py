@@ -199,14 +199,16 @@ def test_segreduce_lr_matches_atomic_path(dev, nranks):
     hist = torch.empty(nbins * nch + 1, dtype=torch.int32, device=dev)
     pos = torch.empty(n, dtype=torch.int32, device=dev)
     pairs = torch.empty(n, dtype=torch.int64, device=dev)
-    g_sr = torch.full((U,), 12345.0, device=dev)
+    items = torch.empty(4 * h.sr_max_items(n), dtype=torch.int32, device=dev)
+    nitems = torch.zeros(1, dtype=torch.int32, device=dev)
+    g_sr = torch.zeros(U, device=dev)  # dedup zeroes the round's rows
     l_sr = torch.zeros(256 * 32, device=dev)
     h.sr_plan(r.inv.data_ptr(), n, r.ucount.data_ptr(), nranks, d.ucap, hist.data_ptr(), nbins,
-              pos.data_ptr(), st)
+              pos.data_ptr(), items.data_ptr(), nitems.data_ptr(), st)
     h.lr_fwd_pairs(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), r.ucount.data_ptr(),
                    nranks, d.ucap, pos.data_ptr(), pairs.data_ptr(), l_sr.data_ptr(), 0, st)
-    h.sr_reduce(pairs.data_ptr(), hist.data_ptr(), nbins, n, r.ucount.data_ptr(), nranks, d.ucap,
-                g_sr.data_ptr(), st)
+    h.sr_reduce(pairs.data_ptr(), items.data_ptr(), nitems.data_ptr(), n, r.ucount.data_ptr(),
+                nranks, d.ucap, g_sr.data_ptr(), st)
     torch.cuda.synchronize()
     uc = r.ucount.cpu().numpy()
     assert int(hist[-1].item()) == n  # every valid occurrence placed exactly once
