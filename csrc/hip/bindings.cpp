@@ -173,6 +173,8 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("sr_nbins", &sr_nbins);
   m.def("sr_nchunks", &sr_nchunks);
   m.def("sr_max_items", &sr_max_items);
+  m.def("sr_hist_words", &sr_hist_words);
+  m.def("dedup_cnt_words", &dedup_cnt_words);
   m.def("sr_plan", [](uintptr_t inv, long long n, uintptr_t ucount, int nranks, long long ucap,
                       uintptr_t hist, int nbins, uintptr_t pos, uintptr_t items, uintptr_t nitems,
                       uintptr_t st) {

@@ -12,19 +12,21 @@
 //       written straight into per-destination segments at fixed displacement
 //       dest*ucap, which is exactly the alltoallv send layout.
 //
-// Three kernels, and no same-address atomics (measured on MI355X: one
+// Four kernels, and no same-address atomics (measured on MI355X: one
 // atomic per wave onto a single counter serialises at ~12 ns each — 23K of
 // them cost 285 us, more than the whole dedup):
 //   1. insert:  every occurrence CASes its key into a power-of-two scratch
-//      table (load <= 0.5).  The CAS winner is the key's representative: it
+//      table (load <= 0.67).  The CAS winner is the key's representative: it
 //      routes the key and takes a block-local offset in its destination from
 //      an LDS counter; the block writes its per-destination counts with plain
 //      stores, and the winner parks (block, dest, offset) in the slot's tag.
-//   2. scan:    one workgroup per destination turns the per-block counts into
-//      per-block bases (exclusive prefix sum) and the destination total.
-//   3. finish:  every occurrence resolves its unique id from its slot's tag;
-//      the winner also writes the key into the send segment and zeroes the
-//      gradient row.  (`inverse` is what the model kernels gather through.)
+//   2+3. scan:  two parallel phases (scan.h) turn the per-block counts into
+//      per-block bases and the per-destination totals.
+//   4. finish:  every occurrence resolves its unique id from its slot's tag;
+//      the winner also writes the key into the send segment, zeroes the
+//      gradient row and resets its scratch slot to EMPTY — so the scratch
+//      never needs a full memset between rounds.
+#include "scan.h"
 #include "ss_device.h"
 #include "ss_launch.h"
 
@@ -82,48 +84,13 @@ __global__ __launch_bounds__(256) void k_dedup_insert(const uint64_t* __restrict
     blk_cnt[(long long)r * nblocks + blockIdx.x] = lcnt[r];
 }
 
-// One workgroup per destination: exclusive scan of blk_cnt[dest][*].
-__global__ __launch_bounds__(1024) void k_dedup_scan(uint32_t* __restrict__ blk_cnt, int nblocks,
-                                                     unsigned long long* __restrict__ ucount) {
-  __shared__ unsigned int wsum[16];
-  __shared__ unsigned int carry;
-  const int dest = blockIdx.x, t = threadIdx.x, lane = t & 63, w = t >> 6;
-  uint32_t* c = blk_cnt + (long long)dest * nblocks;
-  if (t == 0) carry = 0;
-  __syncthreads();
-  for (int base = 0; base < nblocks; base += 1024) {
-    const int idx = base + t;
-    const unsigned int v = idx < nblocks ? c[idx] : 0u;
-    unsigned int x = v;  // inclusive wave scan
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned int y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    if (w == 0) {
-      unsigned int ws = lane < 16 ? wsum[lane] : 0u;
-      for (int o = 1; o < 16; o <<= 1) {
-        const unsigned int y = __shfl_up(ws, o, 64);
-        if (lane >= o) ws += y;
-      }
-      if (lane < 16) wsum[lane] = ws;  // inclusive over waves
-    }
-    __syncthreads();
-    const unsigned int excl = carry + (w ? wsum[w - 1] : 0u) + x - v;
-    if (idx < nblocks) c[idx] = excl;
-    __syncthreads();
-    if (t == 0) carry += wsum[15];
-    __syncthreads();
-  }
-  if (t == 0) ucount[dest] = carry;
-}
-
 __global__ __launch_bounds__(256) void k_dedup_finish(const uint64_t* __restrict__ keys, long long n,
                                                       const uint32_t* __restrict__ slot_of,
                                                       const uint32_t* __restrict__ stag,
+                                                      uint64_t* __restrict__ skeys,
                                                       const uint32_t* __restrict__ blk_base,
-                                                      int nblocks, long long ucap,
+                                                      const uint32_t* __restrict__ grp_base,
+                                                      int nblocks, int ngroups, long long ucap,
                                                       uint32_t* __restrict__ inv,
                                                       uint64_t* __restrict__ ukeys,
                                                       float* __restrict__ ugrad, int gdim) {
@@ -134,13 +101,16 @@ __global__ __launch_bounds__(256) void k_dedup_finish(const uint64_t* __restrict
     inv[i] = kInvalid;
     return;
   }
-  const uint32_t tag = stag[so & ~kWinBit];
+  const uint32_t s = so & ~kWinBit;
+  const uint32_t tag = stag[s];
   const uint32_t b = tag >> 15, d = (tag >> 9) & 63u, o = tag & 511u;
-  const unsigned long long uid =
-      (unsigned long long)d * ucap + blk_base[(long long)d * nblocks + b] + o;
+  const unsigned long long uid = (unsigned long long)d * ucap +
+                                 blk_base[(long long)d * nblocks + b] +
+                                 grp_base[(long long)d * ngroups + b / kScanGroup] + o;
   inv[i] = (uint32_t)uid;
   if (so & kWinBit) {
     ukeys[uid] = keys[i];
+    skeys[s] = kEmptyKey;  // only this round's winners dirtied the scratch
     if (ugrad)
       for (int j = 0; j < gdim; ++j) ugrad[uid * gdim + j] = 0.f;
   }
@@ -188,6 +158,11 @@ static inline int blocks_for(long long n, int cap = 1 << 30) {
 }
 
 int dedup_blocks(long long n) { return blocks_for(n); }
+// blk_cnt buffer: [nranks][nblocks] counts followed by [nranks][ngroups] group bases
+long long dedup_cnt_words(long long n, int nranks) {
+  const int nb = blocks_for(n);
+  return (long long)nranks * ((long long)nb + scan_groups(nb));
+}
 
 void launch_dedup_route(const uint64_t* keys, long long n, uint64_t* scratch_keys,
                         uint32_t* scratch_tag, unsigned long long scratch_cap, uint32_t* slot_of,
@@ -210,10 +185,12 @@ void launch_dedup_route(const uint64_t* keys, long long n, uint64_t* scratch_key
   hipLaunchKernelGGL(k_dedup_insert, dim3(nb), dim3(256), 0, st, keys, n, scratch_keys, scratch_tag,
                      scratch_cap - 1, slot_of, rs, blk_cnt, nb);
   check_launch("k_dedup_insert");
-  hipLaunchKernelGGL(k_dedup_scan, dim3(rs.nranks), dim3(1024), 0, st, blk_cnt, nb, ucount);
-  check_launch("k_dedup_scan");
+  uint32_t* grp = blk_cnt + (long long)rs.nranks * nb;
+  launch_rowscan(blk_cnt, rs.nranks, nb, grp, nullptr, ucount, st);
+  check_launch("dedup rowscan");
   hipLaunchKernelGGL(k_dedup_finish, dim3(nb), dim3(256), 0, st, keys, n, slot_of, scratch_tag,
-                     blk_cnt, nb, ucap, inv, ukeys, ugrad, gdim);
+                     scratch_keys, blk_cnt, grp, nb, scan_groups(nb), ucap, inv, ukeys, ugrad,
+                     gdim);
   check_launch("k_dedup_finish");
 }
 

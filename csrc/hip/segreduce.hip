@@ -23,6 +23,7 @@
 //     reduce     one workgroup per work item: LDS atomics into 8192
 //                accumulators, then one coalesced row-shaped atomicAdd per
 //                touched unique key (full-rate atomic shape, ~10 MB/step)
+#include "scan.h"
 #include "ss_device.h"
 #include "ss_launch.h"
 
@@ -78,61 +79,25 @@ __global__ __launch_bounds__(1024) void k_sr_count(const uint32_t* __restrict__ 
   for (int b = threadIdx.x; b < nbins; b += 1024) hist[(long long)b * nchunks + blockIdx.x] = h[b];
 }
 
-// Exclusive scan of data[0, len) in place (single workgroup, LDS tiles of
-// 32K values, coalesced loads); total -> data[len].  Then the reduce work
-// list: items[k] = (bin, first pair, end pair), <= kItem pairs each.
-__global__ __launch_bounds__(1024) void k_sr_scan(uint32_t* __restrict__ data, int nbins,
-                                                  int nchunks, uint4* __restrict__ items,
+// Bin starts (exclusive scan of the per-bin totals from the row scan, single
+// workgroup over <= 4096 values) and the reduce work list:
+// items[k] = (bin, first pair, end pair), <= kItem pairs each.
+__global__ __launch_bounds__(1024) void k_sr_scan(const uint32_t* __restrict__ btot, int nbins,
+                                                  uint32_t* __restrict__ bstart,
+                                                  uint4* __restrict__ items,
                                                   uint32_t* __restrict__ nitems) {
-  constexpr int kTile = 32768, kPT = kTile / 1024;
-  __shared__ unsigned int tile[kTile];
   __shared__ unsigned int wsum[16];
-  __shared__ unsigned int carry;
-  const long long len = (long long)nbins * nchunks;
+  __shared__ unsigned int tot;
   const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-  if (t == 0) carry = 0;
-  __syncthreads();
-  for (long long base = 0; base < len; base += kTile) {
-    for (int k = 0; k < kPT; ++k) {
-      const long long i = base + k * 1024 + t;
-      tile[k * 1024 + t] = i < len ? data[i] : 0u;
-    }
-    __syncthreads();
-    unsigned int s = 0;
-#pragma unroll
-    for (int k = 0; k < kPT; ++k) s += tile[t * kPT + k];
-    unsigned int x = s;
-    for (int o = 1; o < 64; o <<= 1) {
-      const unsigned int y = __shfl_up(x, o, 64);
-      if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    if (w == 0) {
-      unsigned int ws = lane < 16 ? wsum[lane] : 0u;
-      for (int o = 1; o < 16; o <<= 1) {
-        const unsigned int y = __shfl_up(ws, o, 64);
-        if (lane >= o) ws += y;
-      }
-      if (lane < 16) wsum[lane] = ws;
-    }
-    __syncthreads();
-    unsigned int run = carry + (w ? wsum[w - 1] : 0u) + x - s;
-#pragma unroll
-    for (int k = 0; k < kPT; ++k) {
-      const unsigned int v = tile[t * kPT + k];
-      tile[t * kPT + k] = run;
-      run += v;
-    }
-    __syncthreads();
-    for (int k = 0; k < kPT; ++k) {
-      const long long i = base + k * 1024 + t;
-      if (i < len) data[i] = tile[k * 1024 + t];
-    }
-    if (t == 0) carry += wsum[15];
-    __syncthreads();
+  unsigned int carry = 0;
+  for (int b0 = 0; b0 < nbins; b0 += 1024) {
+    const int b = b0 + t;
+    const unsigned int v = b < nbins ? btot[b] : 0u;
+    const unsigned int e = block_excl_scan_1024(v, wsum, &tot);
+    if (b < nbins) bstart[b] = carry + e;
+    carry += tot;
   }
-  if (t == 0) data[len] = carry;
+  if (t == 0) bstart[nbins] = carry;
   __syncthreads();
   // ---- work list: per bin ceil(pairs / kItem) items; block scan over bins
   unsigned int off = 0;
@@ -140,8 +105,8 @@ __global__ __launch_bounds__(1024) void k_sr_scan(uint32_t* __restrict__ data, i
     const int b = b0 + t;
     unsigned int st = 0, en = 0, cnt = 0;
     if (b < nbins) {
-      st = data[(long long)b * nchunks];
-      en = b + 1 < nbins ? data[(long long)(b + 1) * nchunks] : data[len];
+      st = bstart[b];
+      en = bstart[b + 1];
       cnt = (en - st + kItem - 1) / kItem;
     }
     unsigned int x = cnt;
@@ -173,12 +138,15 @@ __global__ __launch_bounds__(1024) void k_sr_scan(uint32_t* __restrict__ data, i
 
 __global__ __launch_bounds__(1024) void k_sr_positions(const uint32_t* __restrict__ inv, long long n,
                                                        CuMap m, const uint32_t* __restrict__ hist,
+                                                       const uint32_t* __restrict__ grp,
+                                                       const uint32_t* __restrict__ bstart,
                                                        int nbins, int nchunks,
                                                        uint32_t* __restrict__ pos) {
   __shared__ unsigned int pre[kMaxSeg + 1];
   __shared__ unsigned int cur[kMaxBins];
+  const int ng = scan_groups(nchunks), g = blockIdx.x / kScanGroup;
   for (int b = threadIdx.x; b < nbins; b += 1024)
-    cur[b] = hist[(long long)b * nchunks + blockIdx.x];
+    cur[b] = bstart[b] + hist[(long long)b * nchunks + blockIdx.x] + grp[(long long)b * ng + g];
   load_prefix(m, pre);
   const long long a = (long long)blockIdx.x * kChunk + threadIdx.x;
   uint32_t u[kPer];
@@ -270,6 +238,12 @@ __global__ __launch_bounds__(256) void k_lr_fwd_pairs(const uint32_t* __restrict
 int sr_nbins(long long max_unique) { return (int)((max_unique + kBinW - 1) >> kBinShift); }
 int sr_nchunks(long long n) { return (int)((n + kChunk - 1) / kChunk); }
 int sr_max_items(long long n) { return sr_nbins(n) + sr_nchunks(n) + 1; }
+// hist buffer: [nbins][nchunks] counts | [nbins][ngroups] group bases |
+//              btot[nbins] | bstart[nbins + 1]
+long long sr_hist_words(long long n) {
+  const long long nb = sr_nbins(n), nch = sr_nchunks(n);
+  return nb * nch + nb * scan_groups((int)nch) + 2 * nb + 1;
+}
 
 void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* ucount,
                     int nranks, long long ucap, uint32_t* hist, int nbins, uint32_t* pos,
@@ -281,15 +255,20 @@ void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* 
   if (nbins > kMaxBins || nbins < 1) throw_error("segreduce: too many unique keys per call");
   if ((unsigned long long)nranks * (unsigned long long)ucap >= 0x80000000ull)
     throw_error("segreduce: unique-id space exceeds 31 bits");
-  const int nch = sr_nchunks(n);
+  const int nch = sr_nchunks(n), ng = scan_groups(nch);
+  uint32_t* grp = hist + (long long)nbins * nch;
+  uint32_t* btot = grp + (long long)nbins * ng;
+  uint32_t* bstart = btot + nbins;
   CuMap m{ucount, nranks, ucap};
   hipLaunchKernelGGL(k_sr_count, dim3(nch), dim3(1024), 0, st, inv, n, m, hist, nbins, nch);
   check_launch("k_sr_count");
-  hipLaunchKernelGGL(k_sr_scan, dim3(1), dim3(1024), 0, st, hist, nbins, nch,
+  launch_rowscan(hist, nbins, nch, grp, btot, nullptr, st);
+  check_launch("sr rowscan");
+  hipLaunchKernelGGL(k_sr_scan, dim3(1), dim3(1024), 0, st, btot, nbins, bstart,
                      reinterpret_cast<uint4*>(items), nitems);
   check_launch("k_sr_scan");
-  hipLaunchKernelGGL(k_sr_positions, dim3(nch), dim3(1024), 0, st, inv, n, m, hist, nbins, nch,
-                     pos);
+  hipLaunchKernelGGL(k_sr_positions, dim3(nch), dim3(1024), 0, st, inv, n, m, hist, grp, bstart,
+                     nbins, nch, pos);
   check_launch("k_sr_positions");
 }
 

@@ -72,6 +72,8 @@ void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, i
 int sr_nbins(long long max_unique);
 int sr_nchunks(long long n);
 int sr_max_items(long long n);
+long long sr_hist_words(long long n);
+long long dedup_cnt_words(long long n, int nranks);
 void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* ucount,
                     int nranks, long long ucap, uint32_t* hist, int nbins, uint32_t* pos,
                     void* items, uint32_t* nitems, hipStream_t st);

@@ -74,8 +74,7 @@ class SparseLRWorker(PipelinedWorker):
         if grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
-            nch = h.sr_nchunks(n)
-            self.hist = [torch.empty(self.nbins * nch + 1, dtype=torch.int32, device=dev)
+            self.hist = [torch.empty(h.sr_hist_words(n), dtype=torch.int32, device=dev)
                          for _ in range(engine.depth)]
             self.pos = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(engine.depth)]
             mi = h.sr_max_items(n)

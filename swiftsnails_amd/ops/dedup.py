@@ -67,8 +67,10 @@ class Deduper:
             frag_map = torch.zeros(1, dtype=torch.int32)
         self.frag_map = frag_map.to(d, torch.int32).contiguous()
         self.skeys = torch.empty(self.scap, dtype=torch.int64, device=d)
+        self._dirty = True
         self.stag = torch.empty(self.scap, dtype=torch.int32, device=d)
-        self.blk_cnt = torch.empty(self.nranks * self.nblocks, dtype=torch.int32, device=d)
+        self.blk_cnt = torch.empty(self.h.dedup_cnt_words(max(1, self.max_n), self.nranks),
+                                   dtype=torch.int32, device=d)
         self.slot_of = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.inv = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.ukeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64, device=d)
@@ -81,8 +83,11 @@ class Deduper:
         if n > self.max_n:
             raise ValueError(f"dedup: {n} keys > capacity {self.max_n}")
         st = _stream_ptr(stream)
-        # scratch reset (memset nodes; hipGraph-capturable)
-        self.skeys.fill_(-1)
+        # the scratch is all-EMPTY between calls: the finish kernel resets the
+        # slots its winners claimed, so no per-round 0xFF memset is needed
+        if self._dirty:
+            self.skeys.fill_(-1)
+            self._dirty = False
         self.h.dedup_route(keys.data_ptr(), n, self.skeys.data_ptr(), self.stag.data_ptr(),
                            self.scap, self.slot_of.data_ptr(), self.frag_map.data_ptr(),
                            self.frag_map.numel(), self.nranks, self.ucap, self.ucount.data_ptr(),

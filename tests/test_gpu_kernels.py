@@ -137,6 +137,16 @@ def test_dedup_route_matches_reference(dev, nranks):
     # reference routing parity: dest segment of each key == map[fmix64 % frag]
     dest = inv // d.ucap
     np.testing.assert_array_equal(dest, hf.rank_map()[hf.frag_of(k)])
+    # the scratch cleans itself (no per-call memset): later calls stay exact
+    for rep in range(3):
+        k2 = rng.integers(0, 7000 + rep, size=15000 + rep, dtype=np.int64)
+        r2 = d(torch.from_numpy(k2).to(dev))
+        torch.cuda.synchronize()
+        uk2 = r2.ukeys.cpu().numpy()
+        inv2 = r2.inv.cpu().numpy().view(np.uint32).astype(np.int64)
+        np.testing.assert_array_equal(uk2[inv2], k2)
+        assert int(r2.ucount.sum().item()) == len(np.unique(k2))
+    assert (d.skeys.cpu().numpy() == -1).all()
 
 
 def test_lr_fwd_bwd_matches_torch(dev):
@@ -196,7 +206,7 @@ def test_segreduce_lr_matches_atomic_path(dev, nranks):
                  l_at.data_ptr(), 0, st)
     # segmented path
     nbins, nch = h.sr_nbins(n), h.sr_nchunks(n)
-    hist = torch.empty(nbins * nch + 1, dtype=torch.int32, device=dev)
+    hist = torch.empty(h.sr_hist_words(n), dtype=torch.int32, device=dev)
     pos = torch.empty(n, dtype=torch.int32, device=dev)
     pairs = torch.empty(n, dtype=torch.int64, device=dev)
     items = torch.empty(4 * h.sr_max_items(n), dtype=torch.int32, device=dev)
