@@ -176,26 +176,24 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("sr_hist_words", &sr_hist_words);
   m.def("dedup_cnt_words", &dedup_cnt_words);
   m.def("sr_plan", [](uintptr_t inv, long long n, uintptr_t ucount, int nranks, long long ucap,
-                      uintptr_t hist, int nbins, uintptr_t pos, uintptr_t items, uintptr_t nitems,
+                      uintptr_t hist, int nbins, uintptr_t plan, uintptr_t items, uintptr_t nitems,
                       uintptr_t st) {
     launch_sr_plan(P<const uint32_t>(inv), n, P<const unsigned long long>(ucount), nranks, ucap,
-                   P<uint32_t>(hist), nbins, P<uint32_t>(pos), P<void>(items), P<uint32_t>(nitems),
+                   P<uint32_t>(hist), nbins, P<void>(plan), P<void>(items), P<uint32_t>(nitems),
                    S(st));
   });
-  m.def("sr_reduce", [](uintptr_t pairs, uintptr_t items, uintptr_t nitems, long long n,
-                        uintptr_t ucount, int nranks, long long ucap, uintptr_t ugrad,
+  m.def("sr_reduce", [](uintptr_t plan, uintptr_t gocc, uintptr_t items, uintptr_t nitems,
+                        long long n, uintptr_t ucount, int nranks, long long ucap, uintptr_t ugrad,
                         uintptr_t st) {
-    launch_sr_reduce(P<const void>(pairs), P<const void>(items), P<const uint32_t>(nitems), n,
-                     P<const unsigned long long>(ucount), nranks, ucap, P<float>(ugrad), S(st));
+    launch_sr_reduce(P<const void>(plan), P<const float>(gocc), P<const void>(items),
+                     P<const uint32_t>(nitems), n, P<const unsigned long long>(ucount), nranks,
+                     ucap, P<float>(ugrad), S(st));
   });
-  m.def("lr_fwd_pairs", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
-                           uintptr_t uvals, uintptr_t ucount, int nranks, long long ucap,
-                           uintptr_t pos, uintptr_t pairs, uintptr_t loss, uintptr_t pred,
-                           uintptr_t st) {
-    launch_lr_fwd_pairs(P<const uint32_t>(inv), P<const float>(xval), P<const float>(labels), B, F,
-                        P<const float>(uvals), P<const unsigned long long>(ucount), nranks, ucap,
-                        P<const uint32_t>(pos), P<void>(pairs), P<float>(loss), P<float>(pred),
-                        S(st));
+  m.def("lr_fwd_g", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
+                       uintptr_t uvals, uintptr_t gocc, uintptr_t loss, uintptr_t pred,
+                       uintptr_t st) {
+    launch_lr_fwd_g(P<const uint32_t>(inv), P<const float>(xval), P<const float>(labels), B, F,
+                    P<const float>(uvals), P<float>(gocc), P<float>(loss), P<float>(pred), S(st));
   });
   m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
                          uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {

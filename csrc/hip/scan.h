@@ -82,9 +82,41 @@ __host__ __device__ inline int scan_groups(int cols) {
   return (cols + kScanGroup - 1) / kScanGroup;
 }
 
+// Short rows (<= 4 groups of 1024): one 64-thread wave scans a whole row —
+// 1024-thread workgroups would wait for whole free CUs behind the table
+// kernels on the other stream (measured: 83 us for a 313 x 313 scan).
+static __global__ __launch_bounds__(64) void k_rowscan_wave(uint32_t* __restrict__ m, int cols,
+                                                            uint32_t* __restrict__ G, int ngroups,
+                                                            uint32_t* __restrict__ total32,
+                                                            unsigned long long* __restrict__ total64) {
+  const int row = blockIdx.x, lane = threadIdx.x;
+  uint32_t* r = m + (long long)row * cols;
+  unsigned int carry = 0;
+  for (int b = 0; b < cols; b += 64) {
+    const unsigned int v = b + lane < cols ? r[b + lane] : 0u;
+    unsigned int x = v;
+    for (int o = 1; o < 64; o <<= 1) {
+      const unsigned int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (b + lane < cols) r[b + lane] = carry + x - v;
+    carry += __shfl(x, 63, 64);
+  }
+  for (int g = lane; g < ngroups; g += 64) G[(long long)row * ngroups + g] = 0u;
+  if (lane == 0) {
+    if (total32) total32[row] = carry;
+    if (total64) total64[row] = carry;
+  }
+}
+
 inline void launch_rowscan(uint32_t* m, int rows, int cols, uint32_t* G, uint32_t* total32,
                            unsigned long long* total64, hipStream_t st) {
   const int ng = scan_groups(cols);
+  if (cols <= 4 * kScanGroup) {
+    hipLaunchKernelGGL(k_rowscan_wave, dim3(rows), dim3(64), 0, st, m, cols, G, ng, total32,
+                       total64);
+    return;
+  }
   hipLaunchKernelGGL(k_rowscan_p1, dim3(ng, rows), dim3(1024), 0, st, m, cols, G, ng);
   hipLaunchKernelGGL(k_rowscan_p2, dim3(rows), dim3(64), 0, st, G, ng, total32, total64);
 }

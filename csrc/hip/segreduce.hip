@@ -141,7 +141,7 @@ __global__ __launch_bounds__(1024) void k_sr_positions(const uint32_t* __restric
                                                        const uint32_t* __restrict__ grp,
                                                        const uint32_t* __restrict__ bstart,
                                                        int nbins, int nchunks,
-                                                       uint32_t* __restrict__ pos) {
+                                                       uint2* __restrict__ plan) {
   __shared__ unsigned int pre[kMaxSeg + 1];
   __shared__ unsigned int cur[kMaxBins];
   const int ng = scan_groups(nchunks), g = blockIdx.x / kScanGroup;
@@ -155,13 +155,19 @@ __global__ __launch_bounds__(1024) void k_sr_positions(const uint32_t* __restric
 #pragma unroll
   for (int k = 0; k < kPer; ++k) {
     const long long j = a + k * 1024;
-    if (j < n) pos[j] = u[k] == kInvS ? kInvS : atomicAdd(&cur[cu_of(m, pre, u[k]) >> kBinShift], 1u);
+    if (j < n && u[k] != kInvS) {
+      const unsigned int cu = cu_of(m, pre, u[k]);
+      const unsigned int p = atomicAdd(&cur[cu >> kBinShift], 1u);
+      plan[p] = make_uint2((uint32_t)j, cu & (kBinW - 1));  // bin order: (occurrence, cu_lo)
+    }
   }
 }
 
-// One workgroup per work item. pairs[i] = (cu & (kBinW-1), grad bits).
+// One workgroup per work item; plan[p] = (occurrence j, cu & (kBinW-1)), the
+// gradient value is gocc[j] (written coalesced by the model's forward).
 // ugrad must be zeroed for the round's unique keys (dedup does it).
-__global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pairs,
+__global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ plan,
+                                                    const float* __restrict__ gocc,
                                                     const uint4* __restrict__ items,
                                                     const uint32_t* __restrict__ nitems, CuMap m,
                                                     float* __restrict__ ugrad) {
@@ -172,8 +178,8 @@ __global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pa
   for (int c = threadIdx.x; c < kBinW; c += 1024) acc[c] = 0.f;
   load_prefix(m, pre);
   for (uint32_t p = it.y + threadIdx.x; p < it.z; p += 1024) {
-    const uint2 pr = pairs[p];
-    atomicAdd(&acc[pr.x], __uint_as_float(pr.y));
+    const uint2 pr = plan[p];
+    atomicAdd(&acc[pr.y], gocc[pr.x]);
   }
   __syncthreads();
   const unsigned int total = pre[m.nranks];
@@ -187,16 +193,15 @@ __global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pa
   }
 }
 
-// ---- LR forward writing bin-ordered (cu_lo, grad) pairs instead of atomics
-__global__ __launch_bounds__(256) void k_lr_fwd_pairs(const uint32_t* __restrict__ inv,
-                                                      const float* __restrict__ xval,
-                                                      const float* __restrict__ labels, int B, int F,
-                                                      const float* __restrict__ uvals, CuMap m,
-                                                      const uint32_t* __restrict__ pos,
-                                                      uint2* __restrict__ pairs,
-                                                      float* __restrict__ loss_sum,
-                                                      float* __restrict__ pred) {
-  __shared__ unsigned int pre[kMaxSeg + 1];
+// ---- LR forward: per-sample dot/sigmoid/logloss, per-occurrence gradient
+// g*x written COALESCED to gocc[j] (the reduce gathers it in bin order)
+__global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ inv,
+                                                  const float* __restrict__ xval,
+                                                  const float* __restrict__ labels, int B, int F,
+                                                  const float* __restrict__ uvals,
+                                                  float* __restrict__ gocc,
+                                                  float* __restrict__ loss_sum,
+                                                  float* __restrict__ pred) {
   __shared__ float sdot[256];
   __shared__ float sg[256];
   __shared__ float sloss[4];
@@ -204,7 +209,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_pairs(const uint32_t* __restrict
   const int t = threadIdx.x, ls = t / F;
   const long long s0 = (long long)blockIdx.x * spb;
   if (t < spb) sdot[t] = 0.f;
-  load_prefix(m, pre);
+  __syncthreads();
   const bool active = ls < spb && s0 + ls < B;
   const long long j = s0 * F + t;
   uint32_t u = kInvS;
@@ -228,10 +233,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_pairs(const uint32_t* __restrict
   if ((t & 63) == 0) sloss[t >> 6] = l;
   __syncthreads();
   if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
-  if (active && u != kInvS) {
-    const unsigned int cu = cu_of(m, pre, u);
-    pairs[pos[j]] = make_uint2(cu & (kBinW - 1), __float_as_uint(sg[ls] * x));
-  }
+  if (active) gocc[j] = sg[ls] * x;
 }
 
 // -------------------------------------------------------------- launchers
@@ -246,7 +248,7 @@ long long sr_hist_words(long long n) {
 }
 
 void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* ucount,
-                    int nranks, long long ucap, uint32_t* hist, int nbins, uint32_t* pos,
+                    int nranks, long long ucap, uint32_t* hist, int nbins, void* plan,
                     void* items, uint32_t* nitems, hipStream_t st) {
   if (n <= 0) {
     check_hip(hipMemsetAsync(nitems, 0, 4, st), "nitems");
@@ -268,32 +270,30 @@ void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* 
                      reinterpret_cast<uint4*>(items), nitems);
   check_launch("k_sr_scan");
   hipLaunchKernelGGL(k_sr_positions, dim3(nch), dim3(1024), 0, st, inv, n, m, hist, grp, bstart,
-                     nbins, nch, pos);
+                     nbins, nch, reinterpret_cast<uint2*>(plan));
   check_launch("k_sr_positions");
 }
 
-void launch_sr_reduce(const void* pairs, const void* items, const uint32_t* nitems, long long n,
-                      const unsigned long long* ucount, int nranks, long long ucap, float* ugrad,
-                      hipStream_t st) {
+void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
+                      const uint32_t* nitems, long long n, const unsigned long long* ucount,
+                      int nranks, long long ucap, float* ugrad, hipStream_t st) {
   if (n <= 0) return;
   CuMap m{ucount, nranks, ucap};
   hipLaunchKernelGGL(k_sr_reduce, dim3(sr_max_items(n)), dim3(1024), 0, st,
-                     reinterpret_cast<const uint2*>(pairs), reinterpret_cast<const uint4*>(items),
-                     nitems, m, ugrad);
+                     reinterpret_cast<const uint2*>(plan), gocc,
+                     reinterpret_cast<const uint4*>(items), nitems, m, ugrad);
   check_launch("k_sr_reduce");
 }
 
-void launch_lr_fwd_pairs(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
-                         const float* uvals, const unsigned long long* ucount, int nranks,
-                         long long ucap, const uint32_t* pos, void* pairs, float* loss_sum,
-                         float* pred, hipStream_t st) {
+void launch_lr_fwd_g(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
+                     const float* uvals, float* gocc, float* loss_sum, float* pred,
+                     hipStream_t st) {
   if (B <= 0) return;
-  if (F < 1 || F > 256) throw_error("lr_fwd_pairs: F must be in [1,256]");
+  if (F < 1 || F > 256) throw_error("lr_fwd_g: F must be in [1,256]");
   const int spb = F >= 256 ? 1 : 256 / F;
-  CuMap m{ucount, nranks, ucap};
-  hipLaunchKernelGGL(k_lr_fwd_pairs, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, xval, labels,
-                     B, F, uvals, m, pos, reinterpret_cast<uint2*>(pairs), loss_sum, pred);
-  check_launch("k_lr_fwd_pairs");
+  hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, xval, labels, B,
+                     F, uvals, gocc, loss_sum, pred);
+  check_launch("k_lr_fwd_g");
 }
 
 }  // namespace ss

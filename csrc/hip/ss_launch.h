@@ -75,15 +75,14 @@ int sr_max_items(long long n);
 long long sr_hist_words(long long n);
 long long dedup_cnt_words(long long n, int nranks);
 void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* ucount,
-                    int nranks, long long ucap, uint32_t* hist, int nbins, uint32_t* pos,
+                    int nranks, long long ucap, uint32_t* hist, int nbins, void* plan,
                     void* items, uint32_t* nitems, hipStream_t st);
-void launch_sr_reduce(const void* pairs, const void* items, const uint32_t* nitems, long long n,
-                      const unsigned long long* ucount, int nranks, long long ucap, float* ugrad,
-                      hipStream_t st);
-void launch_lr_fwd_pairs(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
-                         const float* uvals, const unsigned long long* ucount, int nranks,
-                         long long ucap, const uint32_t* pos, void* pairs, float* loss_sum,
-                         float* pred, hipStream_t st);
+void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
+                      const uint32_t* nitems, long long n, const unsigned long long* ucount,
+                      int nranks, long long ucap, float* ugrad, hipStream_t st);
+void launch_lr_fwd_g(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
+                     const float* uvals, float* gocc, float* loss_sum, float* pred,
+                     hipStream_t st);
 
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);

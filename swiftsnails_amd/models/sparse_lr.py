@@ -68,7 +68,9 @@ class SparseLRWorker(PipelinedWorker):
         self.keys = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
         self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
         # grad_mode "segreduce": atomic-free duplicate merge (segreduce.hip) —
-        # bin plan on the route stream, (key, grad) pairs + LDS reduce on main;
+        # bin-ordered plan (occurrence, row) on the route stream; the forward
+        # writes per-occurrence g*x coalesced, the reduce gathers it in plan
+        # order and merges duplicates in LDS (main stream);
         # "atomic": one float atomicAdd per occurrence (the first design).
         self.grad_mode = grad_mode
         if grad_mode == "segreduce":
@@ -76,17 +78,18 @@ class SparseLRWorker(PipelinedWorker):
             self.nbins = h.sr_nbins(n)
             self.hist = [torch.empty(h.sr_hist_words(n), dtype=torch.int32, device=dev)
                          for _ in range(engine.depth)]
-            self.pos = [torch.empty(n, dtype=torch.int32, device=dev) for _ in range(engine.depth)]
+            self.plan = [torch.empty(n, dtype=torch.int64, device=dev)
+                         for _ in range(engine.depth)]
             mi = h.sr_max_items(n)
             self.items = [torch.empty(4 * mi, dtype=torch.int32, device=dev)
                           for _ in range(engine.depth)]
             self.nitems = [torch.zeros(1, dtype=torch.int32, device=dev)
                            for _ in range(engine.depth)]
-            self.pairs = torch.empty(n, dtype=torch.int64, device=dev)
+            self.gocc = torch.empty(n, dtype=torch.float32, device=dev)
 
     def _post(self, dd, slot, st):
         hip().sr_plan(dd.inv.data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks, dd.ucap,
-                      self.hist[slot].data_ptr(), self.nbins, self.pos[slot].data_ptr(),
+                      self.hist[slot].data_ptr(), self.nbins, self.plan[slot].data_ptr(),
                       self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), st)
 
     def _route(self, step: int):
@@ -107,11 +110,11 @@ class SparseLRWorker(PipelinedWorker):
         h = hip()
         if self.grad_mode == "segreduce":
             dd = rnd.dd
-            h.lr_fwd_pairs(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
-                           d.num_fields, rnd.uvals.data_ptr(), dd.ucount.data_ptr(), dd.nranks,
-                           dd.ucap, self.pos[slot].data_ptr(), self.pairs.data_ptr(),
-                           self.loss_sum.data_ptr(), 0, st)
-            h.sr_reduce(self.pairs.data_ptr(), self.items[slot].data_ptr(),
+            h.lr_fwd_g(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
+                       d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(),
+                       self.loss_sum.data_ptr(), 0, st)
+            h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
+                        self.items[slot].data_ptr(),
                         self.nitems[slot].data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks,
                         dd.ucap, rnd.ugrad.data_ptr(), st)
         else:

@@ -207,22 +207,22 @@ def test_segreduce_lr_matches_atomic_path(dev, nranks):
     # segmented path
     nbins, nch = h.sr_nbins(n), h.sr_nchunks(n)
     hist = torch.empty(h.sr_hist_words(n), dtype=torch.int32, device=dev)
-    pos = torch.empty(n, dtype=torch.int32, device=dev)
-    pairs = torch.empty(n, dtype=torch.int64, device=dev)
+    plan = torch.empty(n, dtype=torch.int64, device=dev)  # (occurrence j, cu low bits)
+    gocc = torch.empty(n, device=dev)
     items = torch.empty(4 * h.sr_max_items(n), dtype=torch.int32, device=dev)
     nitems = torch.zeros(1, dtype=torch.int32, device=dev)
     g_sr = torch.zeros(U, device=dev)  # dedup zeroes the round's rows
     l_sr = torch.zeros(256 * 32, device=dev)
     h.sr_plan(r.inv.data_ptr(), n, r.ucount.data_ptr(), nranks, d.ucap, hist.data_ptr(), nbins,
-              pos.data_ptr(), items.data_ptr(), nitems.data_ptr(), st)
-    h.lr_fwd_pairs(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), r.ucount.data_ptr(),
-                   nranks, d.ucap, pos.data_ptr(), pairs.data_ptr(), l_sr.data_ptr(), 0, st)
-    h.sr_reduce(pairs.data_ptr(), items.data_ptr(), nitems.data_ptr(), n, r.ucount.data_ptr(),
-                nranks, d.ucap, g_sr.data_ptr(), st)
+              plan.data_ptr(), items.data_ptr(), nitems.data_ptr(), st)
+    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gocc.data_ptr(),
+               l_sr.data_ptr(), 0, st)
+    h.sr_reduce(plan.data_ptr(), gocc.data_ptr(), items.data_ptr(), nitems.data_ptr(), n,
+                r.ucount.data_ptr(), nranks, d.ucap, g_sr.data_ptr(), st)
     torch.cuda.synchronize()
     uc = r.ucount.cpu().numpy()
     assert int(hist[-1].item()) == n  # every valid occurrence placed exactly once
-    ps = np.sort(pos.cpu().numpy().view(np.uint32))
+    ps = np.sort(plan.cpu().numpy().view(np.uint32).reshape(n, 2)[:, 0])
     np.testing.assert_array_equal(ps, np.arange(n, dtype=np.uint32))
     for q in range(nranks):
         a, b = q * d.ucap, q * d.ucap + uc[q]
