@@ -46,6 +46,8 @@ def main(argv=None):
     ap.add_argument("--optimizer", default="adagrad")
     ap.add_argument("--lr", type=float, default=0.05)
     ap.add_argument("--grad-mode", default="segreduce", choices=["segreduce", "atomic"])
+    ap.add_argument("--dedup", default=None, choices=["bucket", "hash"],
+                    help="batch dedup implementation (default: bucket)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -56,6 +58,8 @@ def main(argv=None):
         if world == 1 and a.gpus > 1:
             print("bench.py: --gpus > 1 must be launched with torch.distributed.run", file=sys.stderr)
             return 2
+    if a.dedup:
+        os.environ["SS_DEDUP"] = a.dedup
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
 

@@ -139,6 +139,23 @@ PYBIND11_MODULE(_ss_hip, m) {
                        P<uint32_t>(inv), S(st));
   });
   m.def("dedup_blocks", &dedup_blocks);
+  m.def("bd_scratch_words", &bd_scratch_words);
+  m.def("bd_buckets", &bd_buckets);
+  m.def("bd_dedup", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num, int nranks,
+                       long long ucap, uintptr_t scratch, uintptr_t pkeys, uintptr_t pj,
+                       uintptr_t luid, uintptr_t bkeys, uintptr_t ucount, uintptr_t ukeys,
+                       uintptr_t ugrad, int gdim, uintptr_t inv, uintptr_t st) {
+    RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
+    launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch),
+                    P<uint64_t>(pkeys), P<uint32_t>(pj), P<uint32_t>(luid), P<uint64_t>(bkeys),
+                    P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
+                    P<uint32_t>(inv), S(st));
+  });
+  m.def("bd_reduce", [](long long n, int nranks, long long ucap, uintptr_t scratch, uintptr_t pj,
+                        uintptr_t luid, uintptr_t gocc, uintptr_t ugrad, uintptr_t st) {
+    launch_bd_reduce(n, nranks, ucap, P<const uint32_t>(scratch), P<const uint32_t>(pj),
+                     P<const uint32_t>(luid), P<const float>(gocc), P<float>(ugrad), S(st));
+  });
   m.attr("CTR_SHARDS") = kCtrShards;
   m.def("route_keys", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num,
                          int nranks, uintptr_t dest, uintptr_t st) {

@@ -84,6 +84,17 @@ void launch_lr_fwd_g(const uint32_t* inv, const float* xval, const float* labels
                      const float* uvals, float* gocc, float* loss_sum, float* pred,
                      hipStream_t st);
 
+// --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
+long long bd_scratch_words(long long n, int nranks);
+int bd_buckets(long long n, int nranks);
+void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
+                     uint32_t* scratch, uint64_t* pkeys, uint32_t* pj, uint32_t* luid,
+                     uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys, float* ugrad,
+                     int gdim, uint32_t* inv, hipStream_t st);
+void launch_bd_reduce(long long n, int nranks, long long ucap, const uint32_t* scratch,
+                      const uint32_t* pj, const uint32_t* luid, const float* gocc, float* ugrad,
+                      hipStream_t st);
+
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,

@@ -67,13 +67,22 @@ class SparseLRWorker(PipelinedWorker):
         n = B * F
         self.keys = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
         self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
-        # grad_mode "segreduce": atomic-free duplicate merge (segreduce.hip) —
-        # bin-ordered plan (occurrence, row) on the route stream; the forward
-        # writes per-occurrence g*x coalesced, the reduce gathers it in plan
-        # order and merges duplicates in LDS (main stream);
-        # "atomic": one float atomicAdd per occurrence (the first design).
+        # grad_mode "segreduce": duplicate merge without global atomics.  With
+        # the bucketed deduper (default) the dedup partition is the reduction
+        # plan: the forward writes per-occurrence g*x coalesced and one
+        # workgroup per bucket sums them in LDS and stores each unique row once
+        # (so the deduper need not zero the gradient rows).  With the hash
+        # deduper the separate bin plan of segreduce.hip is built on the route
+        # stream instead.  "atomic": one float atomicAdd per occurrence.
         self.grad_mode = grad_mode
+        self.bucketed = grad_mode == "segreduce" and all(
+            getattr(dd, "mode", None) == "bucket" for dd in engine.dedupers)
         if grad_mode == "segreduce":
+            self.gocc = torch.empty(n, dtype=torch.float32, device=dev)
+        if self.bucketed:
+            for dd in engine.dedupers:
+                dd.zero_grad = False
+        elif grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
             self.hist = [torch.empty(h.sr_hist_words(n), dtype=torch.int32, device=dev)
@@ -85,7 +94,6 @@ class SparseLRWorker(PipelinedWorker):
                           for _ in range(engine.depth)]
             self.nitems = [torch.zeros(1, dtype=torch.int32, device=dev)
                            for _ in range(engine.depth)]
-            self.gocc = torch.empty(n, dtype=torch.float32, device=dev)
 
     def _post(self, dd, slot, st):
         hip().sr_plan(dd.inv.data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks, dd.ucap,
@@ -93,12 +101,13 @@ class SparseLRWorker(PipelinedWorker):
                       self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), st)
 
     def _route(self, step: int):
-        if self.grad_mode != "segreduce" or not self.active:
+        if not self.active:
             return super()._route(step)
         slot = self.engine._next_slot
         return self.engine.route(produce=lambda stream: self._produce(step, slot,
                                                                       stream.cuda_stream),
-                                 post=self._post)
+                                 post=None if (self.bucketed or self.grad_mode != "segreduce")
+                                 else self._post)
 
     def _produce(self, step, slot, stream):
         self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
@@ -108,15 +117,19 @@ class SparseLRWorker(PipelinedWorker):
     def _compute(self, rnd, slot, st):
         d = self.data
         h = hip()
+        dd = rnd.dd
         if self.grad_mode == "segreduce":
-            dd = rnd.dd
             h.lr_fwd_g(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
                        d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(),
                        self.loss_sum.data_ptr(), 0, st)
-            h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
-                        self.items[slot].data_ptr(),
-                        self.nitems[slot].data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks,
-                        dd.ucap, rnd.ugrad.data_ptr(), st)
+            if self.bucketed:
+                h.bd_reduce(dd.n, dd.nranks, dd.ucap, dd.owner.scratch.data_ptr(),
+                            dd.owner.pj.data_ptr(), dd.owner.luid.data_ptr(),
+                            self.gocc.data_ptr(), rnd.ugrad.data_ptr(), st)
+            else:
+                h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
+                            self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,
+                            dd.ucount.data_ptr(), dd.nranks, dd.ucap, rnd.ugrad.data_ptr(), st)
         else:
             h.lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),

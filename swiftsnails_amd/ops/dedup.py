@@ -10,10 +10,19 @@ global_push_access.h:80-99).  Output layout is the alltoallv send layout:
 * ``inv[n]``: occurrence -> unique id (index into rows laid out the same way);
 * ``ugrad[nranks * ucap, gdim]``: zeroed gradient rows for the unique keys.
 
+Two device implementations:
+
+* ``bucket`` (default, bdedup.hip): partition occurrences by hash into
+  ~1024-occurrence buckets whose ids encode the destination, dedup each
+  bucket in LDS — no device-scope atomics; the partition (``pj``, ``luid``)
+  is also the plan of the duplicate-merging gradient reduction (``reduce``);
+* ``hash`` (dedup.hip): one global scratch hash table, a CAS per occurrence.
+
 ``dedup_reference`` is the host implementation used on CPU and by the tests.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -39,15 +48,20 @@ class DedupResult:
     ucap: int
     nranks: int
     n: int
+    owner: object = None      # the Deduper (bucket mode: reduce plan lives there)
 
 
 class Deduper:
     """Device dedup/route with scratch sized for up to ``max_n`` keys per call."""
 
     def __init__(self, max_n: int, nranks: int = 1, frag_map: Optional[torch.Tensor] = None,
-                 gdim: int = 1, device=None, with_grad: bool = True, zero_grad: bool = True):
+                 gdim: int = 1, device=None, with_grad: bool = True, zero_grad: bool = True,
+                 mode: Optional[str] = None):
         from .._native import hip
 
+        self.mode = mode or os.environ.get("SS_DEDUP", "bucket")
+        if self.mode not in ("bucket", "hash"):
+            raise ValueError(f"dedup mode {self.mode!r}")
         # zero_grad=False: the model's backward writes every unique row itself
         # (e.g. the segmented reduction of segreduce.hip), skip zeroing here.
         self.zero_grad = zero_grad
@@ -66,12 +80,22 @@ class Deduper:
         if frag_map is None:
             frag_map = torch.zeros(1, dtype=torch.int32)
         self.frag_map = frag_map.to(d, torch.int32).contiguous()
-        self.skeys = torch.empty(self.scap, dtype=torch.int64, device=d)
-        self._dirty = True
-        self.stag = torch.empty(self.scap, dtype=torch.int32, device=d)
-        self.blk_cnt = torch.empty(self.h.dedup_cnt_words(max(1, self.max_n), self.nranks),
-                                   dtype=torch.int32, device=d)
-        self.slot_of = torch.empty(self.max_n, dtype=torch.int32, device=d)
+        m = max(1, self.max_n)
+        if self.mode == "hash":
+            self.skeys = torch.empty(self.scap, dtype=torch.int64, device=d)
+            self._dirty = True
+            self.stag = torch.empty(self.scap, dtype=torch.int32, device=d)
+            self.blk_cnt = torch.empty(self.h.dedup_cnt_words(m, self.nranks),
+                                       dtype=torch.int32, device=d)
+            self.slot_of = torch.empty(self.max_n, dtype=torch.int32, device=d)
+        else:
+            # word 0 of the scratch is the sticky overflow flag (zeroed once)
+            self.scratch = torch.zeros(self.h.bd_scratch_words(m, self.nranks),
+                                       dtype=torch.int32, device=d)
+            self.pkeys = torch.empty(m, dtype=torch.int64, device=d)
+            self.bkeys = torch.empty(m, dtype=torch.int64, device=d)
+            self.pj = torch.empty(m, dtype=torch.int32, device=d)
+            self.luid = torch.empty(m, dtype=torch.int32, device=d)
         self.inv = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.ukeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64, device=d)
         self.ucount = torch.zeros(self.nranks, dtype=torch.int64, device=d)
@@ -83,6 +107,15 @@ class Deduper:
         if n > self.max_n:
             raise ValueError(f"dedup: {n} keys > capacity {self.max_n}")
         st = _stream_ptr(stream)
+        ug = self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0
+        if self.mode == "bucket":
+            self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
+                            self.nranks, self.ucap, self.scratch.data_ptr(),
+                            self.pkeys.data_ptr(), self.pj.data_ptr(), self.luid.data_ptr(),
+                            self.bkeys.data_ptr(), self.ucount.data_ptr(), self.ukeys.data_ptr(),
+                            ug, self.gdim, self.inv.data_ptr(), st)
+            return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
+                               self.nranks, n, self)
         # the scratch is all-EMPTY between calls: the finish kernel resets the
         # slots its winners claimed, so no per-round 0xFF memset is needed
         if self._dirty:
@@ -91,12 +124,25 @@ class Deduper:
         self.h.dedup_route(keys.data_ptr(), n, self.skeys.data_ptr(), self.stag.data_ptr(),
                            self.scap, self.slot_of.data_ptr(), self.frag_map.data_ptr(),
                            self.frag_map.numel(), self.nranks, self.ucap, self.ucount.data_ptr(),
-                           self.ukeys.data_ptr(),
-                           self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0,
-                           self.gdim,
+                           self.ukeys.data_ptr(), ug, self.gdim,
                            self.blk_cnt.data_ptr(), self.inv.data_ptr(), st)
         return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
-                           self.nranks, n)
+                           self.nranks, n, self)
+
+    def reduce(self, n: int, gocc: torch.Tensor, ugrad: torch.Tensor, stream=None):
+        """K7 for scalar rows: ugrad[uid] = sum of gocc over the occurrences of
+        uid, for the LAST call's partition (bucket mode; no zero-fill needed)."""
+        if self.mode != "bucket" or self.gdim != 1:
+            raise RuntimeError("Deduper.reduce needs mode='bucket' and gdim=1")
+        self.h.bd_reduce(n, self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
+                         self.luid.data_ptr(), gocc.data_ptr(), ugrad.data_ptr(),
+                         _stream_ptr(stream))
+
+    def check(self):
+        """Raise if any bucket overflowed its LDS table (sticky; syncs)."""
+        if self.mode == "bucket" and int(self.scratch[0].item()) != 0:
+            raise RuntimeError("bucketed dedup: an LDS bucket table overflowed "
+                               "(pathological key distribution); use SS_DEDUP=hash")
 
 
 class CpuDeduper:

@@ -108,17 +108,22 @@ def test_table_full_raises(dev):
         t.check()
 
 
-@pytest.mark.parametrize("nranks", [1, 3, 8])
-def test_dedup_route_matches_reference(dev, nranks):
+@pytest.mark.parametrize("mode", ["bucket", "hash"])
+@pytest.mark.parametrize("nranks,n", [(1, 20000), (3, 20000), (8, 20000), (1, 400000),
+                                      (3, 400000)])
+def test_dedup_route_matches_reference(dev, nranks, n, mode):
     from swiftsnails_amd.ops.dedup import Deduper, dedup_reference
     from swiftsnails_amd.parallel.router import HashFrag
 
     rng = np.random.default_rng(nranks)
-    k = rng.integers(0, 5000, size=20000, dtype=np.int64)  # heavy duplication
+    if n <= 20000:
+        k = rng.integers(0, 5000, size=n, dtype=np.int64)  # heavy duplication
+    else:  # many buckets, Zipf hot keys, long tail
+        k = (rng.zipf(1.2, n) * 7919 % 2_000_003).astype(np.int64)
     hf = HashFrag(nranks, 97)
     fm = hf.rank_map()
-    d = Deduper(25000, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=2,
-                device=dev)
+    d = Deduper(n + 5000, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=2,
+                device=dev, mode=mode)
     r = d(torch.from_numpy(k).to(dev))
     torch.cuda.synchronize()
     uk_ref, uc_ref, _ = dedup_reference(k, nranks, fm, ucap=d.ucap)
@@ -146,7 +151,61 @@ def test_dedup_route_matches_reference(dev, nranks):
         inv2 = r2.inv.cpu().numpy().view(np.uint32).astype(np.int64)
         np.testing.assert_array_equal(uk2[inv2], k2)
         assert int(r2.ucount.sum().item()) == len(np.unique(k2))
-    assert (d.skeys.cpu().numpy() == -1).all()
+    if mode == "hash":
+        assert (d.skeys.cpu().numpy() == -1).all()
+    else:
+        d.check()
+    # invalid (EMPTY) keys map to INVALID and are not counted
+    k3 = k[:1000].copy()
+    k3[::7] = -1
+    r3 = d(torch.from_numpy(k3).to(dev))
+    torch.cuda.synchronize()
+    inv3 = r3.inv.cpu().numpy().view(np.uint32)
+    assert (inv3[::7] == 0xFFFFFFFF).all()
+    ok = k3 != -1
+    np.testing.assert_array_equal(r3.ukeys.cpu().numpy()[inv3[ok].astype(np.int64)], k3[ok])
+    assert int(r3.ucount.sum().item()) == len(np.unique(k3[ok]))
+
+
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_bucket_reduce_lr_matches_atomic_path(dev, nranks):
+    """Bucketed dedup's LDS reduction == per-occurrence atomics."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.dedup import Deduper
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    h = hip()
+    B, F = 20000, 13
+    n = B * F
+    rng = np.random.default_rng(5 + nranks)
+    keys = (rng.zipf(1.3, n) % 300000).astype(np.int64)
+    keys[::101] = -1  # a few invalid occurrences
+    fm = HashFrag(nranks, 64).rank_map()
+    d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=1,
+                device=dev, mode="bucket")
+    r = d(torch.from_numpy(keys).to(dev))
+    st = torch.cuda.current_stream().cuda_stream
+    U = nranks * d.ucap
+    uvals = torch.randn(U, device=dev) * 0.1
+    y = torch.from_numpy((rng.random(B) < 0.3).astype(np.float32)).to(dev)
+    g_at = torch.zeros(U, device=dev)
+    l_at = torch.zeros(256 * 32, device=dev)
+    h.lr_fwd_bwd(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), g_at.data_ptr(),
+                 l_at.data_ptr(), 0, st)
+    gocc = torch.empty(n, device=dev)
+    l_b = torch.zeros(256 * 32, device=dev)
+    g_b = torch.full((U,), float("nan"), device=dev)  # reduce must write every unique row
+    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gocc.data_ptr(),
+               l_b.data_ptr(), 0, st)
+    d.reduce(n, gocc, g_b)
+    torch.cuda.synchronize()
+    d.check()
+    uc = r.ucount.cpu().numpy()
+    for q in range(nranks):
+        a, b = q * d.ucap, q * d.ucap + uc[q]
+        np.testing.assert_allclose(g_b[a:b].cpu().numpy(), g_at[a:b].cpu().numpy(), rtol=1e-4,
+                                   atol=1e-4)
+    np.testing.assert_allclose(l_b.sum().item(), l_at.sum().item(), rtol=1e-5)
 
 
 def test_lr_fwd_bwd_matches_torch(dev):
@@ -193,7 +252,7 @@ def test_segreduce_lr_matches_atomic_path(dev, nranks):
     keys = (rng.zipf(1.3, n) % 300000).astype(np.int64)  # heavy duplication + long tail
     fm = HashFrag(nranks, 64).rank_map()
     d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=1,
-                device=dev)
+                device=dev, mode="hash")
     r = d(torch.from_numpy(keys).to(dev))
     st = torch.cuda.current_stream().cuda_stream
     U = nranks * d.ucap
