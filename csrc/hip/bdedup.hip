@@ -17,17 +17,25 @@
 // duplicate-merging gradient reduction (k_bd_reduce), which needs no atomics
 // to global memory at all.
 //
-//   1 count    per 8192-occurrence chunk: LDS histogram over buckets
-//   2 rowscan  (scan.h) per-bucket chunk bases + bucket totals
+//   1 count    per 8192-occurrence chunk: LDS histogram over buckets, stored
+//              chunk-major ([nch][P], coalesced)
+//   2 colscan  per-bucket exclusive scan down the chunks + bucket totals
 //   3 bstart   bucket start offsets (one workgroup)
-//   4 scatter  occurrence -> bucket-ordered (key, j) arrays
-//   5 dedup    one workgroup per bucket: LDS hash insert, compact, local ids
-//   6 rowscan  per-destination scan of bucket unique counts -> ucount[d]
-//   7 finish   unique keys to their send segment, inverse index, zeroed grads
+//   4 scatter  bucket-ordered occurrence list pj[pos] = j, and pos_of[j]
+//   5 dedup    one workgroup per bucket: LDS hash insert, compaction, then a
+//              decoupled look-back over the destination's earlier buckets for
+//              the unique-id base (single pass, no extra scan launch); writes
+//              the send-segment keys, per-position unique ids and ucount[d]
+//   6 inverse  inv[j] = luid[pos_of[j]] (coalesced writes, gathered reads)
+//
+// Measured (profiles/): random 4-12 B stores cost ~5x their bytes in write
+// requests (partial 64 B lines from 8 L2s), so the design stores every
+// permuted array with as few random stores as possible (only pj) and turns the
+// rest into coalesced stores plus gathered loads.
 //
 // Bucket b = d * Pd + fastrange32(dedup_hash(key) >> 32, Pd) with
 // d = map[fmix64(key) % frag_num] (hashfrag.h:48-53).  Pd is chosen so a
-// bucket holds ~1024 occurrences; its unique count is then far below the
+// bucket holds ~2048 occurrences; its unique count is then far below the
 // 4096-slot LDS table (overflow is detected and reported, never silent).
 #include "scan.h"
 #include "ss_device.h"
@@ -38,20 +46,22 @@ namespace ss {
 static constexpr uint32_t kBdInvalid = 0xFFFFFFFFu;
 static constexpr int kBdChunk = 8192;   // occurrences per count/scatter workgroup
 static constexpr int kBdPer = kBdChunk / 1024;
-static constexpr int kBdTarget = 1024;  // target occurrences per bucket
+static constexpr int kBdTarget = 2048;  // target occurrences per bucket
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
+static constexpr int kBdRegs = 4;       // occurrences per thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
 
 __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs, uint32_t Pd) {
-  const uint32_t d = rs.nranks == 1 ? 0u : (uint32_t)rs.frag_map[fmix64(key) % (uint64_t)rs.frag_num];
+  const uint32_t d =
+      rs.nranks == 1 ? 0u : (uint32_t)rs.frag_map[fmix64(key) % (uint64_t)rs.frag_num];
   const uint32_t h = (uint32_t)(dedup_hash(key) >> 32);
   return d * Pd + __umulhi(h, Pd);
 }
 
 // ---- layout of the int scratch (u32 words), a function of (n, nranks) only
 struct BdLayout {
-  int P, Pd, nch, ng, ngd;
-  long long hist, grp, btot, bstart, ucnt, unum, ugrp, err, total;
+  int P, Pd, nch;
+  long long hist, btot, bstart, ubase, unum, total;
 };
 
 static BdLayout bd_layout(long long n, int nranks) {
@@ -64,45 +74,77 @@ static BdLayout bd_layout(long long n, int nranks) {
   L.P = (int)(pd * nranks);
   L.nch = (int)((n + kBdChunk - 1) / kBdChunk);
   if (L.nch < 1) L.nch = 1;
-  L.ng = scan_groups(L.nch);
-  L.ngd = scan_groups(L.Pd);
   long long o = 1;  // word 0: sticky error flag (fixed position for any n)
-  L.err = 0;
   L.hist = o; o += (long long)L.P * L.nch;
-  L.grp = o; o += (long long)L.P * L.ng;
   L.btot = o; o += L.P;
   L.bstart = o; o += L.P + 1;
-  L.ucnt = o; o += L.P;
+  L.ubase = o; o += L.P;
   L.unum = o; o += L.P;
-  L.ugrp = o; o += (long long)nranks * L.ngd;
   L.total = o;
   return L;
 }
 
-long long bd_scratch_words(long long n, int nranks) { return bd_layout(n < 1 ? 1 : n, nranks).total; }
+long long bd_scratch_words(long long n, int nranks) {
+  return bd_layout(n < 1 ? 1 : n, nranks).total;
+}
 int bd_buckets(long long n, int nranks) { return bd_layout(n < 1 ? 1 : n, nranks).P; }
+long long bd_ubase_offset(long long n, int nranks) {
+  return bd_layout(n < 1 ? 1 : n, nranks).ubase;
+}
 
-// 1. per-chunk bucket histogram (dynamic LDS: P words)
+// 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output
 __global__ __launch_bounds__(1024) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
                                                    RouteSpec rs, int Pd, int P,
-                                                   uint32_t* __restrict__ hist, int nch) {
+                                                   uint32_t* __restrict__ hist) {
   extern __shared__ unsigned int h[];
   for (int b = threadIdx.x; b < P; b += 1024) h[b] = 0u;
   __syncthreads();
   const long long base = (long long)blockIdx.x * kBdChunk + threadIdx.x;
+  uint64_t k[kBdPer];
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
     const long long j = base + e * 1024;
-    if (j < n) {
-      const uint64_t key = keys[j];
-      if (key != kEmptyKey) atomicAdd(&h[bd_bucket(key, rs, (uint32_t)Pd)], 1u);
-    }
+    k[e] = j < n ? keys[j] : kEmptyKey;
   }
+#pragma unroll
+  for (int e = 0; e < kBdPer; ++e)
+    if (k[e] != kEmptyKey) atomicAdd(&h[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
   __syncthreads();
-  for (int b = threadIdx.x; b < P; b += 1024) hist[(long long)b * nch + blockIdx.x] = h[b];
+  uint32_t* row = hist + (long long)blockIdx.x * P;
+  for (int b = threadIdx.x; b < P; b += 1024) row[b] = h[b];
 }
 
-// 3. exclusive scan of bucket totals -> bucket start offsets (P <= 16384)
+// 2. column scan of the [nch][P] histogram: 64 buckets x 16 chunk segments
+//    per workgroup; two passes of independent loads, no serial chain
+__global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist, int nch, int P,
+                                                     uint32_t* __restrict__ btot) {
+  __shared__ unsigned int ss[16][64];
+  const int col = threadIdx.x & 63, seg = threadIdx.x >> 6;
+  const int b = blockIdx.x * 64 + col;
+  const int R = (nch + 15) / 16;
+  const int c0 = seg * R, c1 = min(nch, c0 + R);
+  unsigned int s = 0;
+  if (b < P) {
+#pragma unroll 8
+    for (int c = c0; c < c1; ++c) s += hist[(long long)c * P + b];
+  }
+  ss[seg][col] = s;
+  __syncthreads();
+  unsigned int off = 0;
+  for (int q = 0; q < seg; ++q) off += ss[q][col];
+  if (b < P) {
+#pragma unroll 8
+    for (int c = c0; c < c1; ++c) {
+      const long long i = (long long)c * P + b;
+      const unsigned int v = hist[i];
+      hist[i] = off;
+      off += v;
+    }
+    if (seg == 15) btot[b] = off;
+  }
+}
+
+// 3. exclusive scan of bucket totals -> bucket start offsets (P <= ~16K)
 __global__ __launch_bounds__(1024) void k_bd_bstart(const uint32_t* __restrict__ btot, int P,
                                                     uint32_t* __restrict__ bstart) {
   __shared__ unsigned int wsum[16];
@@ -121,74 +163,109 @@ __global__ __launch_bounds__(1024) void k_bd_bstart(const uint32_t* __restrict__
   if (threadIdx.x == 0) bstart[P] = tot;
 }
 
-// 4. scatter occurrences into bucket order (dynamic LDS: P words)
+// 4. bucket-ordered occurrence list (dynamic LDS: P words)
 __global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict__ keys, long long n,
                                                      RouteSpec rs, int Pd, int P,
                                                      const uint32_t* __restrict__ hist,
-                                                     const uint32_t* __restrict__ grp, int nch,
-                                                     int ng, const uint32_t* __restrict__ bstart,
-                                                     uint64_t* __restrict__ pkeys,
+                                                     const uint32_t* __restrict__ bstart,
                                                      uint32_t* __restrict__ pj,
-                                                     uint32_t* __restrict__ inv) {
+                                                     uint32_t* __restrict__ pos_of) {
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
-  for (int b = threadIdx.x; b < P; b += 1024)
-    cur[b] = bstart[b] + hist[(long long)b * nch + c] + grp[(long long)b * ng + c / kScanGroup];
-  __syncthreads();
+  const uint32_t* row = hist + (long long)c * P;
+  for (int b = threadIdx.x; b < P; b += 1024) cur[b] = bstart[b] + row[b];
   const long long base = (long long)c * kBdChunk + threadIdx.x;
+  uint64_t k[kBdPer];
+#pragma unroll
+  for (int e = 0; e < kBdPer; ++e) {
+    const long long j = base + e * 1024;
+    k[e] = j < n ? keys[j] : kEmptyKey;
+  }
+  __syncthreads();
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
     const long long j = base + e * 1024;
     if (j < n) {
-      const uint64_t key = keys[j];
-      if (key == kEmptyKey) {
-        inv[j] = kBdInvalid;
-      } else {
-        const uint32_t pos = atomicAdd(&cur[bd_bucket(key, rs, (uint32_t)Pd)], 1u);
-        pkeys[pos] = key;
+      uint32_t pos = kBdInvalid;
+      if (k[e] != kEmptyKey) {
+        pos = atomicAdd(&cur[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
         pj[pos] = (uint32_t)j;
       }
+      pos_of[j] = pos;
     }
   }
 }
 
-// 5. one workgroup per bucket: LDS hash dedup, compaction, local unique ids
-__global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ pkeys,
-                                                   const uint32_t* __restrict__ bstart,
-                                                   uint32_t* __restrict__ luid,
-                                                   uint64_t* __restrict__ bkeys,
-                                                   uint32_t* __restrict__ ucnt,
-                                                   uint32_t* __restrict__ unum,
-                                                   uint32_t* __restrict__ err) {
+// look-back flag word: [epoch:30][state:2][value:32]; state 1 = bucket
+// aggregate, 2 = inclusive prefix within the destination
+__device__ __forceinline__ unsigned long long bd_flag(uint32_t epoch, uint32_t st, uint32_t v) {
+  return ((unsigned long long)(epoch & 0x3FFFFFFFu) << 34) | ((unsigned long long)st << 32) | v;
+}
+
+struct BdOut {
+  uint64_t* ukeys;
+  uint32_t* luid;
+  uint32_t* ubase;
+  uint32_t* unum;
+  unsigned long long* ucount;
+  float* ugrad;
+  int gdim;
+  long long ucap;
+};
+
+// 5. one workgroup per bucket (taken in start order from a ticket counter so
+//    the look-back only ever waits on workgroups that are already running)
+__global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ keys,
+                                                   const uint32_t* __restrict__ pj,
+                                                   const uint32_t* __restrict__ bstart, int P,
+                                                   int Pd, uint32_t epoch,
+                                                   unsigned long long* __restrict__ flags,
+                                                   unsigned long long* __restrict__ ticket,
+                                                   BdOut out, uint32_t* __restrict__ err) {
   __shared__ unsigned long long tab[kBdTS];
   __shared__ unsigned int lid[kBdTS];
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
+  __shared__ int sb;
+  __shared__ unsigned int sbase;
   __shared__ int bad;
-  const int b = blockIdx.x, t = threadIdx.x;
+  const int t = threadIdx.x;
+  if (t == 0) {
+    const unsigned long long tk = atomicAdd(ticket, 1ull);
+    if (tk == (unsigned long long)P - 1) atomicExch(ticket, 0ull);  // every ticket taken
+    sb = (int)tk;
+    bad = 0;
+  }
   for (int s = t; s < kBdTS; s += 1024) tab[s] = kEmptyKey;
-  if (t == 0) bad = 0;
   __syncthreads();
+  const int b = sb;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
-  for (uint32_t p = p0 + t; p < p1; p += 1024) {
-    const uint64_t key = pkeys[p];
+  // insert: the first kBdRegs occurrences of each thread keep their slot in
+  // registers; a hot bucket's excess parks it in luid[] (rewritten below)
+  uint32_t slot[kBdRegs];
+  uint64_t kk[kBdRegs];
+#pragma unroll
+  for (int r = 0; r < kBdRegs; ++r) {
+    const uint32_t p = p0 + t + r * 1024;
+    kk[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
+  }
+  auto insert = [&](uint64_t key) -> uint32_t {
     uint32_t s = (uint32_t)dedup_hash(key) & (kBdTS - 1);
-    int k = 0;
-    for (; k < kBdTS; ++k) {
+    for (int k = 0; k < kBdTS; ++k) {
       const unsigned long long v = tab[s];
-      if (v == key) break;
+      if (v == key) return s;
       if (v == kEmptyKey) {
         const unsigned long long prev = atomicCAS(&tab[s], kEmptyKey, (unsigned long long)key);
-        if (prev == kEmptyKey || prev == key) break;
+        if (prev == kEmptyKey || prev == key) return s;
       }
       s = (s + 1) & (kBdTS - 1);
     }
-    if (k == kBdTS) {
-      bad = 1;
-      s = kBdInvalid;
-    }
-    luid[p] = s;  // slot for now; rewritten to the local id below
-  }
+    bad = 1;
+    return kBdInvalid;
+  };
+#pragma unroll
+  for (int r = 0; r < kBdRegs; ++r) slot[r] = kk[r] != kEmptyKey ? insert(kk[r]) : kBdInvalid;
+  for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) out.luid[p] = insert(keys[pj[p]]);
   __syncthreads();
   // compaction in slot order: thread t owns slots [4t, 4t+4)
   constexpr int kPerT = kBdTS / 1024;
@@ -199,85 +276,105 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
     const int s = t * kPerT + k;
-    const unsigned long long v = tab[s];
-    if (v != kEmptyKey) {
-      lid[s] = o;
-      bkeys[p0 + o] = v;  // bucket's unique keys, staged in its occurrence range
-      ++o;
-    }
+    if (tab[s] != kEmptyKey) lid[s] = o++;
   }
-  __syncthreads();
-  for (uint32_t p = p0 + t; p < p1; p += 1024) {
-    const uint32_t s = luid[p];
-    luid[p] = s == kBdInvalid ? kBdInvalid : lid[s];
-  }
+  // decoupled look-back within the destination's buckets
   if (t == 0) {
-    ucnt[b] = tot;
-    unum[b] = tot;
+    const int d = b / Pd, first = d * Pd;
+    unsigned int excl = 0;
+    if (b == first) {
+      __hip_atomic_store(&flags[b], bd_flag(epoch, 2, tot), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      __hip_atomic_store(&flags[b], bd_flag(epoch, 1, tot), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+      for (int q = b - 1; q >= first; --q) {
+        unsigned long long f;
+        for (;;) {
+          f = __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((uint32_t)(f >> 34) == (epoch & 0x3FFFFFFFu) && ((f >> 32) & 3u) != 0) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+        excl += (uint32_t)f;
+        if (((f >> 32) & 3u) == 2u) break;
+      }
+      __hip_atomic_store(&flags[b], bd_flag(epoch, 2, excl + tot), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const unsigned int base = (unsigned int)((long long)d * out.ucap + excl);
+    sbase = base;
+    out.ubase[b] = base;
+    out.unum[b] = tot;
+    if (b == first + Pd - 1) out.ucount[d] = excl + tot;
     if (bad) atomicOr(err, 1u);
   }
-}
-
-struct BdView {  // where a bucket's unique ids start
-  const uint32_t* ucnt;
-  const uint32_t* ugrp;
-  int Pd, ngd;
-  long long ucap;
-  __device__ __forceinline__ unsigned long long base(int b) const {
-    const int d = b / Pd, c = b - d * Pd;
-    return (unsigned long long)d * ucap + ucnt[b] + ugrp[(long long)d * ngd + c / kScanGroup];
+  __syncthreads();
+  const unsigned int base = sbase;
+#pragma unroll
+  for (int k = 0; k < kPerT; ++k) {
+    const int s = t * kPerT + k;
+    const unsigned long long v = tab[s];
+    if (v != kEmptyKey) out.ukeys[base + lid[s]] = v;
   }
-};
-
-// 7. unique keys -> send segments, inverse index, zeroed gradient rows
-__global__ __launch_bounds__(256) void k_bd_finish(BdView v, const uint32_t* __restrict__ unum,
-                                                   const uint32_t* __restrict__ bstart,
-                                                   const uint64_t* __restrict__ bkeys,
-                                                   const uint32_t* __restrict__ pj,
-                                                   const uint32_t* __restrict__ luid,
-                                                   uint64_t* __restrict__ ukeys,
-                                                   float* __restrict__ ugrad, int gdim,
-                                                   uint32_t* __restrict__ inv) {
-  const int b = blockIdx.x;
-  const unsigned long long base = v.base(b);
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
-  for (uint32_t l = threadIdx.x; l < nu; l += 256) ukeys[base + l] = bkeys[p0 + l];
-  if (ugrad)
-    for (uint32_t e = threadIdx.x; e < nu * (uint32_t)gdim; e += 256) ugrad[base * gdim + e] = 0.f;
-  for (uint32_t p = p0 + threadIdx.x; p < p1; p += 256) {
-    const uint32_t l = luid[p];
-    inv[pj[p]] = l == kBdInvalid ? kBdInvalid : (uint32_t)(base + l);
+  if (out.ugrad)
+    for (uint32_t e = t; e < tot * (uint32_t)out.gdim; e += 1024)
+      out.ugrad[(unsigned long long)base * out.gdim + e] = 0.f;
+#pragma unroll
+  for (int r = 0; r < kBdRegs; ++r) {
+    const uint32_t p = p0 + t + r * 1024;
+    if (p < p1) out.luid[p] = slot[r] == kBdInvalid ? kBdInvalid : base + lid[slot[r]];
+  }
+  for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) {
+    const uint32_t s = out.luid[p];
+    out.luid[p] = s == kBdInvalid ? kBdInvalid : base + lid[s];
   }
 }
 
-// K7 for scalar rows (sparse LR): one workgroup per bucket sums the
-// per-occurrence gradients of its unique keys in LDS, then stores each row
-// once — no zero-fill, no global atomics.
-__global__ __launch_bounds__(1024) void k_bd_reduce(BdView v, const uint32_t* __restrict__ unum,
-                                                    const uint32_t* __restrict__ bstart,
+// 6. inverse index in occurrence order
+__global__ __launch_bounds__(256) void k_bd_inv(const uint32_t* __restrict__ pos_of, long long n,
+                                                const uint32_t* __restrict__ luid,
+                                                uint32_t* __restrict__ inv) {
+  const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (j < n) {
+    const uint32_t p = pos_of[j];
+    inv[j] = p == kBdInvalid ? kBdInvalid : luid[p];
+  }
+}
+
+// K7 for scalar rows (sparse LR): one workgroup per bucket sums the gradients
+// of its unique keys in LDS — per-occurrence g = gs[j / F] * x[j] gathered
+// from the per-sample gradient (L2-resident) — and stores each row once:
+// no zero-fill, no global atomics.
+__global__ __launch_bounds__(1024) void k_bd_reduce(const uint32_t* __restrict__ bstart,
+                                                    const uint32_t* __restrict__ ubase,
+                                                    const uint32_t* __restrict__ unum,
                                                     const uint32_t* __restrict__ pj,
                                                     const uint32_t* __restrict__ luid,
-                                                    const float* __restrict__ gocc,
+                                                    const float* __restrict__ gs,
+                                                    const float* __restrict__ xval, int F,
                                                     float* __restrict__ ugrad) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
   for (uint32_t l = threadIdx.x; l < nu; l += 1024) acc[l] = 0.f;
   __syncthreads();
   for (uint32_t p = p0 + threadIdx.x; p < p1; p += 1024) {
-    const uint32_t l = luid[p];
-    if (l != kBdInvalid) atomicAdd(&acc[l], gocc[pj[p]]);
+    const uint32_t u = luid[p];
+    if (u != kBdInvalid) {
+      const uint32_t j = pj[p];
+      const float g = gs[j / (uint32_t)F];
+      atomicAdd(&acc[u - base], xval ? g * xval[j] : g);
+    }
   }
   __syncthreads();
-  const unsigned long long base = v.base(b);
   for (uint32_t l = threadIdx.x; l < nu; l += 1024) ugrad[base + l] = acc[l];
 }
 
 // ------------------------------------------------------------- launchers
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
-                     uint32_t* scratch, uint64_t* pkeys, uint32_t* pj, uint32_t* luid,
-                     uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys, float* ugrad,
-                     int gdim, uint32_t* inv, hipStream_t st) {
+                     uint32_t* scratch, unsigned long long* sync, uint32_t epoch, uint32_t* pj,
+                     uint32_t* pos_of, uint32_t* luid, unsigned long long* ucount,
+                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   if (n <= 0) {
     check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
@@ -287,41 +384,43 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   if ((unsigned long long)rs.nranks * (unsigned long long)ucap >= 0x7FFFFFFFull)
     throw_error("bdedup: nranks*ucap overflows 31-bit unique ids");
   const BdLayout L = bd_layout(n, rs.nranks);
-  if (L.P > kBdMaxBuckets * 2 || (long long)L.P * L.nch > (1ll << 31))
-    throw_error("bdedup: too many keys per call");
-  if (n > (long long)kBdMaxBuckets * 2800) throw_error("bdedup: too many keys per call (max 45M)");
+  if (L.P > kBdMaxBuckets + kMaxSeg || n > (long long)kBdMaxBuckets * 2800)
+    throw_error("bdedup: too many keys per call (max ~45M)");
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
   hipLaunchKernelGGL(k_bd_count, dim3(L.nch), dim3(1024), lds, st, keys, n, rs, L.Pd, L.P,
-                     S + L.hist, L.nch);
+                     S + L.hist);
   check_launch("k_bd_count");
-  launch_rowscan(S + L.hist, L.P, L.nch, S + L.grp, S + L.btot, nullptr, st);
-  check_launch("bd rowscan");
+  hipLaunchKernelGGL(k_bd_colscan, dim3((L.P + 63) / 64), dim3(1024), 0, st, S + L.hist, L.nch,
+                     L.P, S + L.btot);
+  check_launch("k_bd_colscan");
   hipLaunchKernelGGL(k_bd_bstart, dim3(1), dim3(1024), 0, st, S + L.btot, L.P, S + L.bstart);
   check_launch("k_bd_bstart");
   hipLaunchKernelGGL(k_bd_scatter, dim3(L.nch), dim3(1024), lds, st, keys, n, rs, L.Pd, L.P,
-                     S + L.hist, S + L.grp, L.nch, L.ng, S + L.bstart, pkeys, pj, inv);
+                     S + L.hist, S + L.bstart, pj, pos_of);
   check_launch("k_bd_scatter");
-  hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(1024), 0, st, pkeys, S + L.bstart, luid, bkeys,
-                     S + L.ucnt, S + L.unum, S + L.err);
+  BdOut o{ukeys, luid, S + L.ubase, S + L.unum, ucount, ugrad, gdim, ucap};
+  hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(1024), 0, st, keys, pj, S + L.bstart, L.P, L.Pd,
+                     epoch, sync, sync + kBdMaxBuckets + kMaxSeg, o, S);
   check_launch("k_bd_dedup");
-  launch_rowscan(S + L.ucnt, rs.nranks, L.Pd, S + L.ugrp, nullptr, ucount, st);
-  check_launch("bd uscan");
-  BdView v{S + L.ucnt, S + L.ugrp, L.Pd, L.ngd, ucap};
-  hipLaunchKernelGGL(k_bd_finish, dim3(L.P), dim3(256), 0, st, v, S + L.unum, S + L.bstart, bkeys,
-                     pj, luid, ukeys, ugrad, gdim, inv);
-  check_launch("k_bd_finish");
+  if (inv) {
+    hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos_of, n,
+                       luid, inv);
+    check_launch("k_bd_inv");
+  }
 }
 
-void launch_bd_reduce(long long n, int nranks, long long ucap, const uint32_t* scratch,
-                      const uint32_t* pj, const uint32_t* luid, const float* gocc, float* ugrad,
-                      hipStream_t st) {
+long long bd_sync_words() { return (long long)kBdMaxBuckets + kMaxSeg + 1; }
+
+void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
+                      const uint32_t* luid, const float* gs, const float* xval, int F,
+                      float* ugrad, hipStream_t st) {
   if (n <= 0) return;
+  if (F < 1) throw_error("bd_reduce: F must be >= 1");
   const BdLayout L = bd_layout(n, nranks);
   const uint32_t* S = scratch;
-  BdView v{S + L.ucnt, S + L.ugrp, L.Pd, L.ngd, ucap};
-  hipLaunchKernelGGL(k_bd_reduce, dim3(L.P), dim3(1024), 0, st, v, S + L.unum, S + L.bstart, pj,
-                     luid, gocc, ugrad);
+  hipLaunchKernelGGL(k_bd_reduce, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
+                     S + L.unum, pj, luid, gs, xval, F, ugrad);
   check_launch("k_bd_reduce");
 }
 

@@ -140,23 +140,24 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("dedup_blocks", &dedup_blocks);
   m.def("bd_scratch_words", &bd_scratch_words);
+  m.def("bd_sync_words", &bd_sync_words);
   m.def("bd_buckets", &bd_buckets);
   m.def("bd_dedup", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num, int nranks,
-                       long long ucap, uintptr_t scratch, uintptr_t pkeys, uintptr_t pj,
-                       uintptr_t luid, uintptr_t bkeys, uintptr_t ucount, uintptr_t ukeys,
-                       uintptr_t ugrad, int gdim, uintptr_t inv, uintptr_t st) {
+                       long long ucap, uintptr_t scratch, uintptr_t sync, uint32_t epoch,
+                       uintptr_t pj, uintptr_t pos_of, uintptr_t luid, uintptr_t ucount,
+                       uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, uintptr_t st) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch),
-                    P<uint64_t>(pkeys), P<uint32_t>(pj), P<uint32_t>(luid), P<uint64_t>(bkeys),
-                    P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
-                    P<uint32_t>(inv), S(st));
+                    P<unsigned long long>(sync), epoch, P<uint32_t>(pj), P<uint32_t>(pos_of),
+                    P<uint32_t>(luid), P<unsigned long long>(ucount), P<uint64_t>(ukeys),
+                    P<float>(ugrad), gdim, P<uint32_t>(inv), S(st));
   });
-  m.def("bd_reduce", [](long long n, int nranks, long long ucap, uintptr_t scratch, uintptr_t pj,
-                        uintptr_t luid, uintptr_t gocc, uintptr_t ugrad, uintptr_t st) {
-    launch_bd_reduce(n, nranks, ucap, P<const uint32_t>(scratch), P<const uint32_t>(pj),
-                     P<const uint32_t>(luid), P<const float>(gocc), P<float>(ugrad), S(st));
+  m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
+                        uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st) {
+    launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
+                     P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
+                     P<float>(ugrad), S(st));
   });
-  m.attr("CTR_SHARDS") = kCtrShards;
   m.def("route_keys", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num,
                          int nranks, uintptr_t dest, uintptr_t st) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
@@ -207,10 +208,11 @@ PYBIND11_MODULE(_ss_hip, m) {
                      ucap, P<float>(ugrad), S(st));
   });
   m.def("lr_fwd_g", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
-                       uintptr_t uvals, uintptr_t gocc, uintptr_t loss, uintptr_t pred,
-                       uintptr_t st) {
+                       uintptr_t uvals, uintptr_t g, int per_sample, uintptr_t loss,
+                       uintptr_t pred, uintptr_t st) {
     launch_lr_fwd_g(P<const uint32_t>(inv), P<const float>(xval), P<const float>(labels), B, F,
-                    P<const float>(uvals), P<float>(gocc), P<float>(loss), P<float>(pred), S(st));
+                    P<const float>(uvals), P<float>(g), per_sample, P<float>(loss),
+                    P<float>(pred), S(st));
   });
   m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
                          uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {

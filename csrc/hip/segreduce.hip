@@ -193,13 +193,15 @@ __global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pl
   }
 }
 
-// ---- LR forward: per-sample dot/sigmoid/logloss, per-occurrence gradient
-// g*x written COALESCED to gocc[j] (the reduce gathers it in bin order)
+// ---- LR forward: per-sample dot/sigmoid/logloss; the gradient is written
+// either per occurrence (g*x COALESCED to g[j], the bin-plan reduce gathers
+// it) or per sample (g[s] = p - y, 4 B per sample; the bucketed reduce of
+// bdedup.hip gathers it L2-resident and multiplies by x itself)
 __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ inv,
                                                   const float* __restrict__ xval,
                                                   const float* __restrict__ labels, int B, int F,
                                                   const float* __restrict__ uvals,
-                                                  float* __restrict__ gocc,
+                                                  float* __restrict__ gocc, int per_sample,
                                                   float* __restrict__ loss_sum,
                                                   float* __restrict__ pred) {
   __shared__ float sdot[256];
@@ -226,6 +228,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ i
     const float y = labels[s0 + t];
     const float p = 1.f / (1.f + __expf(-z));
     sg[t] = p - y;
+    if (per_sample) gocc[s0 + t] = p - y;
     if (pred) pred[s0 + t] = p;
     l = fmaxf(z, 0.f) + __logf(1.f + __expf(-fabsf(z))) - y * z;
   }
@@ -233,7 +236,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ i
   if ((t & 63) == 0) sloss[t >> 6] = l;
   __syncthreads();
   if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
-  if (active) gocc[j] = sg[ls] * x;
+  if (active && !per_sample) gocc[j] = sg[ls] * x;
 }
 
 // -------------------------------------------------------------- launchers
@@ -286,13 +289,13 @@ void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
 }
 
 void launch_lr_fwd_g(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
-                     const float* uvals, float* gocc, float* loss_sum, float* pred,
-                     hipStream_t st) {
+                     const float* uvals, float* gocc, int per_sample, float* loss_sum,
+                     float* pred, hipStream_t st) {
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("lr_fwd_g: F must be in [1,256]");
   const int spb = F >= 256 ? 1 : 256 / F;
   hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, xval, labels, B,
-                     F, uvals, gocc, loss_sum, pred);
+                     F, uvals, gocc, per_sample, loss_sum, pred);
   check_launch("k_lr_fwd_g");
 }
 

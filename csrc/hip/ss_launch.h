@@ -81,19 +81,20 @@ void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
                       const uint32_t* nitems, long long n, const unsigned long long* ucount,
                       int nranks, long long ucap, float* ugrad, hipStream_t st);
 void launch_lr_fwd_g(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
-                     const float* uvals, float* gocc, float* loss_sum, float* pred,
+                     const float* uvals, float* g, int per_sample, float* loss_sum, float* pred,
                      hipStream_t st);
 
 // --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
 long long bd_scratch_words(long long n, int nranks);
+long long bd_sync_words();
 int bd_buckets(long long n, int nranks);
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
-                     uint32_t* scratch, uint64_t* pkeys, uint32_t* pj, uint32_t* luid,
-                     uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys, float* ugrad,
-                     int gdim, uint32_t* inv, hipStream_t st);
-void launch_bd_reduce(long long n, int nranks, long long ucap, const uint32_t* scratch,
-                      const uint32_t* pj, const uint32_t* luid, const float* gocc, float* ugrad,
-                      hipStream_t st);
+                     uint32_t* scratch, unsigned long long* sync, uint32_t epoch, uint32_t* pj,
+                     uint32_t* pos_of, uint32_t* luid, unsigned long long* ucount,
+                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st);
+void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
+                      const uint32_t* luid, const float* gs, const float* xval, int F,
+                      float* ugrad, hipStream_t st);
 
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);

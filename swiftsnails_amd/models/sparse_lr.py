@@ -78,7 +78,8 @@ class SparseLRWorker(PipelinedWorker):
         self.bucketed = grad_mode == "segreduce" and all(
             getattr(dd, "mode", None) == "bucket" for dd in engine.dedupers)
         if grad_mode == "segreduce":
-            self.gocc = torch.empty(n, dtype=torch.float32, device=dev)
+            # per-sample gradients (bucketed) or per-occurrence g*x (bin plan)
+            self.gocc = torch.empty(B if self.bucketed else n, dtype=torch.float32, device=dev)
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False
@@ -121,11 +122,12 @@ class SparseLRWorker(PipelinedWorker):
         if self.grad_mode == "segreduce":
             h.lr_fwd_g(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
                        d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(),
-                       self.loss_sum.data_ptr(), 0, st)
+                       int(self.bucketed), self.loss_sum.data_ptr(), 0, st)
             if self.bucketed:
-                h.bd_reduce(dd.n, dd.nranks, dd.ucap, dd.owner.scratch.data_ptr(),
-                            dd.owner.pj.data_ptr(), dd.owner.luid.data_ptr(),
-                            self.gocc.data_ptr(), rnd.ugrad.data_ptr(), st)
+                o = dd.owner
+                h.bd_reduce(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
+                            o.luid.data_ptr(), self.gocc.data_ptr(), 0, d.num_fields,
+                            rnd.ugrad.data_ptr(), st)
             else:
                 h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
                             self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,

@@ -92,9 +92,11 @@ class Deduper:
             # word 0 of the scratch is the sticky overflow flag (zeroed once)
             self.scratch = torch.zeros(self.h.bd_scratch_words(m, self.nranks),
                                        dtype=torch.int32, device=d)
-            self.pkeys = torch.empty(m, dtype=torch.int64, device=d)
-            self.bkeys = torch.empty(m, dtype=torch.int64, device=d)
+            # look-back flags + ticket; flags carry a per-call epoch (no reset)
+            self.sync = torch.zeros(self.h.bd_sync_words(), dtype=torch.int64, device=d)
+            self.epoch = 0
             self.pj = torch.empty(m, dtype=torch.int32, device=d)
+            self.pos_of = torch.empty(m, dtype=torch.int32, device=d)
             self.luid = torch.empty(m, dtype=torch.int32, device=d)
         self.inv = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.ukeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64, device=d)
@@ -109,11 +111,12 @@ class Deduper:
         st = _stream_ptr(stream)
         ug = self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0
         if self.mode == "bucket":
+            self.epoch = self.epoch % 0x3FFFFFFF + 1
             self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
                             self.nranks, self.ucap, self.scratch.data_ptr(),
-                            self.pkeys.data_ptr(), self.pj.data_ptr(), self.luid.data_ptr(),
-                            self.bkeys.data_ptr(), self.ucount.data_ptr(), self.ukeys.data_ptr(),
-                            ug, self.gdim, self.inv.data_ptr(), st)
+                            self.sync.data_ptr(), self.epoch, self.pj.data_ptr(),
+                            self.pos_of.data_ptr(), self.luid.data_ptr(), self.ucount.data_ptr(),
+                            self.ukeys.data_ptr(), ug, self.gdim, self.inv.data_ptr(), st)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self)
         # the scratch is all-EMPTY between calls: the finish kernel resets the
@@ -129,13 +132,16 @@ class Deduper:
         return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                            self.nranks, n, self)
 
-    def reduce(self, n: int, gocc: torch.Tensor, ugrad: torch.Tensor, stream=None):
-        """K7 for scalar rows: ugrad[uid] = sum of gocc over the occurrences of
-        uid, for the LAST call's partition (bucket mode; no zero-fill needed)."""
+    def reduce(self, n: int, gs: torch.Tensor, F: int, ugrad: torch.Tensor,
+                xval: Optional[torch.Tensor] = None, stream=None):
+        """K7 for scalar rows, for the LAST call's partition (bucket mode):
+        ugrad[uid] = sum over occurrences j of uid of gs[j // F] * xval[j]
+        (per-sample gradient times feature value; no zero-fill needed)."""
         if self.mode != "bucket" or self.gdim != 1:
             raise RuntimeError("Deduper.reduce needs mode='bucket' and gdim=1")
-        self.h.bd_reduce(n, self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
-                         self.luid.data_ptr(), gocc.data_ptr(), ugrad.data_ptr(),
+        self.h.bd_reduce(n, self.nranks, self.scratch.data_ptr(), self.pj.data_ptr(),
+                         self.luid.data_ptr(), gs.data_ptr(),
+                         xval.data_ptr() if xval is not None else 0, F, ugrad.data_ptr(),
                          _stream_ptr(stream))
 
     def check(self):

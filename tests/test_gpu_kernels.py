@@ -192,12 +192,12 @@ def test_bucket_reduce_lr_matches_atomic_path(dev, nranks):
     l_at = torch.zeros(256 * 32, device=dev)
     h.lr_fwd_bwd(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), g_at.data_ptr(),
                  l_at.data_ptr(), 0, st)
-    gocc = torch.empty(n, device=dev)
+    gs = torch.empty(B, device=dev)
     l_b = torch.zeros(256 * 32, device=dev)
     g_b = torch.full((U,), float("nan"), device=dev)  # reduce must write every unique row
-    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gocc.data_ptr(),
+    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gs.data_ptr(), 1,
                l_b.data_ptr(), 0, st)
-    d.reduce(n, gocc, g_b)
+    d.reduce(n, gs, F, g_b)
     torch.cuda.synchronize()
     d.check()
     uc = r.ucount.cpu().numpy()
@@ -274,7 +274,7 @@ def test_segreduce_lr_matches_atomic_path(dev, nranks):
     l_sr = torch.zeros(256 * 32, device=dev)
     h.sr_plan(r.inv.data_ptr(), n, r.ucount.data_ptr(), nranks, d.ucap, hist.data_ptr(), nbins,
               plan.data_ptr(), items.data_ptr(), nitems.data_ptr(), st)
-    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gocc.data_ptr(),
+    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gocc.data_ptr(), 0,
                l_sr.data_ptr(), 0, st)
     h.sr_reduce(plan.data_ptr(), gocc.data_ptr(), items.data_ptr(), nitems.data_ptr(), n,
                 r.ucount.data_ptr(), nranks, d.ucap, g_sr.data_ptr(), st)

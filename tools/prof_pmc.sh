@@ -6,9 +6,9 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 ARGS=${ARGS:-"--steps 4 --warmup 2"}
 i=0
-for set in "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum" \
-           "SQ_WAVES SQ_INSTS_VALU SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM" \
-           "FETCH_SIZE" "WRITE_SIZE TCC_EA0_WRREQ_sum"; do
+SETS=${SETS:-"TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum|SQ_WAVES SQ_INSTS_VALU SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_INSTS_VMEM|FETCH_SIZE|WRITE_SIZE TCC_EA0_WRREQ_sum|SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"}
+IFS='|' read -ra SETARR <<< "$SETS"
+for set in "${SETARR[@]}"; do
   i=$((i+1))
   echo "=== pass $i: $set"
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --pmc $set --output-format csv -d "$OUT/p$i" -o run -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
