@@ -17,7 +17,7 @@
 // duplicate-merging gradient reduction (k_bd_reduce), which needs no atomics
 // to global memory at all.
 //
-//   1 count    per 8192-occurrence chunk: LDS histogram over buckets, stored
+//   1 count    per <=8192-occurrence chunk: LDS histogram over buckets, stored
 //              chunk-major ([nch][P], coalesced)
 //   2 colscan  per-bucket exclusive scan down the chunks + bucket totals
 //   3 bstart   bucket start offsets (one workgroup)
@@ -44,8 +44,8 @@
 namespace ss {
 
 static constexpr uint32_t kBdInvalid = 0xFFFFFFFFu;
-static constexpr int kBdChunk = 8192;   // occurrences per count/scatter workgroup
-static constexpr int kBdPer = kBdChunk / 1024;
+static constexpr int kBdMaxChunk = 8192;  // occurrences per count/scatter workgroup
+static constexpr int kBdPer = kBdMaxChunk / 1024;
 static constexpr int kBdTarget = 2048;  // target occurrences per bucket
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
 static constexpr int kBdRegs = 4;       // occurrences per thread kept in registers
@@ -60,7 +60,7 @@ __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs,
 
 // ---- layout of the int scratch (u32 words), a function of (n, nranks) only
 struct BdLayout {
-  int P, Pd, nch;
+  int P, Pd, nch, chunk;
   long long hist, btot, bstart, ubase, unum, total;
 };
 
@@ -72,7 +72,11 @@ static BdLayout bd_layout(long long n, int nranks) {
   if (pd < 1) pd = 1;
   L.Pd = (int)pd;
   L.P = (int)(pd * nranks);
-  L.nch = (int)((n + kBdChunk - 1) / kBdChunk);
+  // chunk count a multiple of the 256 CUs (balanced waves), chunk <= 8192
+  const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
+  const long long per = (n + 256 * waves - 1) / (256 * waves);
+  L.chunk = (int)(((per + 1023) / 1024) * 1024);
+  L.nch = (int)((n + L.chunk - 1) / L.chunk);
   if (L.nch < 1) L.nch = 1;
   long long o = 1;  // word 0: sticky error flag (fixed position for any n)
   L.hist = o; o += (long long)L.P * L.nch;
@@ -94,17 +98,18 @@ long long bd_ubase_offset(long long n, int nranks) {
 
 // 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output
 __global__ __launch_bounds__(1024) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
-                                                   RouteSpec rs, int Pd, int P,
+                                                   RouteSpec rs, int Pd, int P, int chunk,
                                                    uint32_t* __restrict__ hist) {
   extern __shared__ unsigned int h[];
   for (int b = threadIdx.x; b < P; b += 1024) h[b] = 0u;
   __syncthreads();
-  const long long base = (long long)blockIdx.x * kBdChunk + threadIdx.x;
+  const long long base = (long long)blockIdx.x * chunk + threadIdx.x;
+  const int per = chunk >> 10;
   uint64_t k[kBdPer];
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
     const long long j = base + e * 1024;
-    k[e] = j < n ? keys[j] : kEmptyKey;
+    k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
   }
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e)
@@ -165,7 +170,7 @@ __global__ __launch_bounds__(1024) void k_bd_bstart(const uint32_t* __restrict__
 
 // 4. bucket-ordered occurrence list (dynamic LDS: P words)
 __global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict__ keys, long long n,
-                                                     RouteSpec rs, int Pd, int P,
+                                                     RouteSpec rs, int Pd, int P, int chunk,
                                                      const uint32_t* __restrict__ hist,
                                                      const uint32_t* __restrict__ bstart,
                                                      uint32_t* __restrict__ pj,
@@ -174,18 +179,19 @@ __global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict_
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
   for (int b = threadIdx.x; b < P; b += 1024) cur[b] = bstart[b] + row[b];
-  const long long base = (long long)c * kBdChunk + threadIdx.x;
+  const long long base = (long long)c * chunk + threadIdx.x;
+  const int per = chunk >> 10;
   uint64_t k[kBdPer];
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
     const long long j = base + e * 1024;
-    k[e] = j < n ? keys[j] : kEmptyKey;
+    k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
   }
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
     const long long j = base + e * 1024;
-    if (j < n) {
+    if (e < per && j < n) {
       uint32_t pos = kBdInvalid;
       if (k[e] != kEmptyKey) {
         pos = atomicAdd(&cur[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
@@ -278,35 +284,49 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
     const int s = t * kPerT + k;
     if (tab[s] != kEmptyKey) lid[s] = o++;
   }
-  // decoupled look-back within the destination's buckets
-  if (t == 0) {
+  // decoupled look-back within the destination's buckets, 64 predecessors
+  // per step (one flag per lane of wave 0)
+  __syncthreads();
+  if (t < 64) {
     const int d = b / Pd, first = d * Pd;
+    const uint32_t ep = epoch & 0x3FFFFFFFu;
+    if (t == 0)
+      __hip_atomic_store(&flags[b], bd_flag(epoch, b == first ? 2u : 1u, tot), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     unsigned int excl = 0;
-    if (b == first) {
-      __hip_atomic_store(&flags[b], bd_flag(epoch, 2, tot), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      __hip_atomic_store(&flags[b], bd_flag(epoch, 1, tot), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-      for (int q = b - 1; q >= first; --q) {
-        unsigned long long f;
+    int hi = b - 1;  // next predecessor to examine
+    while (hi >= first) {
+      const int q = hi - t;
+      unsigned long long f = 0;
+      uint32_t stt = 2;  // lanes past the destination start act as "inclusive 0"
+      if (q >= first) {
         for (;;) {
           f = __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if ((uint32_t)(f >> 34) == (epoch & 0x3FFFFFFFu) && ((f >> 32) & 3u) != 0) break;
+          stt = (uint32_t)(f >> 32) & 3u;
+          if ((uint32_t)(f >> 34) == ep && stt != 0) break;
           __builtin_amdgcn_s_sleep(1);
         }
-        excl += (uint32_t)f;
-        if (((f >> 32) & 3u) == 2u) break;
       }
-      __hip_atomic_store(&flags[b], bd_flag(epoch, 2, excl + tot), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      // closest predecessor holding an inclusive prefix
+      const unsigned long long incl = __ballot(stt == 2u);
+      const int stop = incl ? __builtin_ctzll(incl) : 64;
+      unsigned int v = (t <= stop && q >= first) ? (uint32_t)f : 0u;
+      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+      excl += v;
+      if (incl) break;
+      hi -= 64;
     }
-    const unsigned int base = (unsigned int)((long long)d * out.ucap + excl);
-    sbase = base;
-    out.ubase[b] = base;
-    out.unum[b] = tot;
-    if (b == first + Pd - 1) out.ucount[d] = excl + tot;
-    if (bad) atomicOr(err, 1u);
+    if (t == 0) {
+      if (b != first)
+        __hip_atomic_store(&flags[b], bd_flag(epoch, 2, excl + tot), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned int base = (unsigned int)((long long)d * out.ucap + excl);
+      sbase = base;
+      out.ubase[b] = base;
+      out.unum[b] = tot;
+      if (b == first + Pd - 1) out.ucount[d] = excl + tot;
+      if (bad) atomicOr(err, 1u);
+    }
   }
   __syncthreads();
   const unsigned int base = sbase;
@@ -389,7 +409,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
   hipLaunchKernelGGL(k_bd_count, dim3(L.nch), dim3(1024), lds, st, keys, n, rs, L.Pd, L.P,
-                     S + L.hist);
+                     L.chunk, S + L.hist);
   check_launch("k_bd_count");
   hipLaunchKernelGGL(k_bd_colscan, dim3((L.P + 63) / 64), dim3(1024), 0, st, S + L.hist, L.nch,
                      L.P, S + L.btot);
@@ -397,7 +417,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   hipLaunchKernelGGL(k_bd_bstart, dim3(1), dim3(1024), 0, st, S + L.btot, L.P, S + L.bstart);
   check_launch("k_bd_bstart");
   hipLaunchKernelGGL(k_bd_scatter, dim3(L.nch), dim3(1024), lds, st, keys, n, rs, L.Pd, L.P,
-                     S + L.hist, S + L.bstart, pj, pos_of);
+                     L.chunk, S + L.hist, S + L.bstart, pj, pos_of);
   check_launch("k_bd_scatter");
   BdOut o{ukeys, luid, S + L.ubase, S + L.unum, ucount, ugrad, gdim, ucap};
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(1024), 0, st, keys, pj, S + L.bstart, L.P, L.Pd,
