@@ -227,7 +227,11 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
                                                    int Pd, uint32_t epoch,
                                                    unsigned long long* __restrict__ flags,
                                                    unsigned long long* __restrict__ ticket,
-                                                   BdOut out, uint32_t* __restrict__ err) {
+                                                   BdOut out, uint32_t* __restrict__ err,
+                                                   unsigned long long* __restrict__ dbg) {
+  // dbg (optional): per bucket 8 wall-clock stamps of the phases (profiling)
+#define BD_STAMP(i) \
+  if (dbg && t == 0) dbg[(long long)sb * 8 + (i)] = wall_clock64();
   __shared__ unsigned long long tab[kBdTS];
   __shared__ unsigned int lid[kBdTS];
   __shared__ unsigned int wsum[16];
@@ -244,6 +248,7 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   }
   for (int s = t; s < kBdTS; s += 1024) tab[s] = kEmptyKey;
   __syncthreads();
+  BD_STAMP(0)
   const int b = sb;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   // insert: the first kBdRegs occurrences of each thread keep their slot in
@@ -255,6 +260,7 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
     const uint32_t p = p0 + t + r * 1024;
     kk[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
   }
+  if (dbg && t == 0) dbg[(long long)sb * 8 + 1] = wall_clock64() + (kk[0] & 0);
   auto insert = [&](uint64_t key) -> uint32_t {
     uint32_t s = (uint32_t)dedup_hash(key) & (kBdTS - 1);
     for (int k = 0; k < kBdTS; ++k) {
@@ -273,6 +279,7 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   for (int r = 0; r < kBdRegs; ++r) slot[r] = kk[r] != kEmptyKey ? insert(kk[r]) : kBdInvalid;
   for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) out.luid[p] = insert(keys[pj[p]]);
   __syncthreads();
+  BD_STAMP(2)
   // compaction in slot order: thread t owns slots [4t, 4t+4)
   constexpr int kPerT = kBdTS / 1024;
   unsigned int occ = 0;
@@ -287,6 +294,7 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   // decoupled look-back within the destination's buckets, 64 predecessors
   // per step (one flag per lane of wave 0)
   __syncthreads();
+  BD_STAMP(3)
   if (t < 64) {
     const int d = b / Pd, first = d * Pd;
     const uint32_t ep = epoch & 0x3FFFFFFFu;
@@ -329,6 +337,7 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
     }
   }
   __syncthreads();
+  BD_STAMP(4)
   const unsigned int base = sbase;
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
@@ -348,6 +357,9 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
     const uint32_t s = out.luid[p];
     out.luid[p] = s == kBdInvalid ? kBdInvalid : base + lid[s];
   }
+  __syncthreads();
+  BD_STAMP(5)
+#undef BD_STAMP
 }
 
 // 6. inverse index in occurrence order
@@ -394,7 +406,8 @@ __global__ __launch_bounds__(1024) void k_bd_reduce(const uint32_t* __restrict__
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                      uint32_t* scratch, unsigned long long* sync, uint32_t epoch, uint32_t* pj,
                      uint32_t* pos_of, uint32_t* luid, unsigned long long* ucount,
-                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st) {
+                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
+                     unsigned long long* dbg) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   if (n <= 0) {
     check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
@@ -421,7 +434,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   check_launch("k_bd_scatter");
   BdOut o{ukeys, luid, S + L.ubase, S + L.unum, ucount, ugrad, gdim, ucap};
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(1024), 0, st, keys, pj, S + L.bstart, L.P, L.Pd,
-                     epoch, sync, sync + kBdMaxBuckets + kMaxSeg, o, S);
+                     epoch, sync, sync + kBdMaxBuckets + kMaxSeg, o, S, dbg);
   check_launch("k_bd_dedup");
   if (inv) {
     hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos_of, n,

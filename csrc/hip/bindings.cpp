@@ -145,13 +145,18 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("bd_dedup", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num, int nranks,
                        long long ucap, uintptr_t scratch, uintptr_t sync, uint32_t epoch,
                        uintptr_t pj, uintptr_t pos_of, uintptr_t luid, uintptr_t ucount,
-                       uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, uintptr_t st) {
+                       uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, uintptr_t st,
+                       uintptr_t dbg) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch),
                     P<unsigned long long>(sync), epoch, P<uint32_t>(pj), P<uint32_t>(pos_of),
                     P<uint32_t>(luid), P<unsigned long long>(ucount), P<uint64_t>(ukeys),
-                    P<float>(ugrad), gdim, P<uint32_t>(inv), S(st));
-  });
+                    P<float>(ugrad), gdim, P<uint32_t>(inv), S(st),
+                    P<unsigned long long>(dbg));
+  }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
+     py::arg("ucap"), py::arg("scratch"), py::arg("sync"), py::arg("epoch"), py::arg("pj"),
+     py::arg("pos_of"), py::arg("luid"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
+     py::arg("gdim"), py::arg("inv"), py::arg("st"), py::arg("dbg") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),

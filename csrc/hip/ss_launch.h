@@ -91,7 +91,8 @@ int bd_buckets(long long n, int nranks);
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                      uint32_t* scratch, unsigned long long* sync, uint32_t epoch, uint32_t* pj,
                      uint32_t* pos_of, uint32_t* luid, unsigned long long* ucount,
-                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st);
+                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
+                     unsigned long long* dbg = nullptr);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st);

@@ -98,6 +98,9 @@ class Deduper:
             self.pj = torch.empty(m, dtype=torch.int32, device=d)
             self.pos_of = torch.empty(m, dtype=torch.int32, device=d)
             self.luid = torch.empty(m, dtype=torch.int32, device=d)
+            # SS_BD_DEBUG=1: per-bucket phase timestamps of the dedup kernel
+            self.dbg = (torch.zeros(8 * self.h.bd_buckets(m, self.nranks), dtype=torch.int64,
+                                    device=d) if os.environ.get("SS_BD_DEBUG") else None)
         self.inv = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.ukeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64, device=d)
         self.ucount = torch.zeros(self.nranks, dtype=torch.int64, device=d)
@@ -116,7 +119,8 @@ class Deduper:
                             self.nranks, self.ucap, self.scratch.data_ptr(),
                             self.sync.data_ptr(), self.epoch, self.pj.data_ptr(),
                             self.pos_of.data_ptr(), self.luid.data_ptr(), self.ucount.data_ptr(),
-                            self.ukeys.data_ptr(), ug, self.gdim, self.inv.data_ptr(), st)
+                            self.ukeys.data_ptr(), ug, self.gdim, self.inv.data_ptr(), st,
+                            self.dbg.data_ptr() if self.dbg is not None else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self)
         # the scratch is all-EMPTY between calls: the finish kernel resets the
