@@ -270,7 +270,7 @@ class Server : public Node {
       if (backup_period_ > 0 && c % backup_period_ == 0) backup(c);
     });
     tr_.add_handler(SERVER_TOLD_TO_TERMINATE, [this](std::shared_ptr<Request>, Request& rsp) {
-      if (!output_.empty()) table_->write_text(output_);
+      if (!output_.empty()) table_->write_text(shard_path(output_));
       rsp.cont << (int32_t)1;
       terminated_.set_state_valid();
     });
@@ -283,9 +283,16 @@ class Server : public Node {
   HostTable& table() { return *table_; }
   int push_count() const { return push_counter_.load(); }
   std::string backup(int c) {
-    const std::string path = backup_root_ + "/param-" + std::to_string(c) + ".txt";
+    const std::string path = shard_path(backup_root_ + "/param-" + std::to_string(c) + ".txt");
     table_->write_text(path);
     return path;
+  }
+  // With several servers every one writes its own shard file (`<path>.s<id>`;
+  // the reference's servers each dumped to their own reducer stdout); a single
+  // server and "-" (stdout) keep the plain name.
+  std::string shard_path(const std::string& path) const {
+    if (path == "-" || route_.server_ids.size() <= 1) return path;
+    return path + ".s" + std::to_string(client_id());
   }
 
  private:

@@ -10,6 +10,7 @@
 #include "channel.h"
 #include "cluster.h"
 #include "config.h"
+#include "dataio.h"
 #include "hashfrag.h"
 #include "host_table.h"
 #include "ss/hash.h"
@@ -365,6 +366,52 @@ PYBIND11_MODULE(_ss_host, m) {
       })
       .def("size", &ThreadPool::size)
       .def("stop", &ThreadPool::stop);
+  // ---- data input (dataio.h)
+  py::class_<SparseDataset>(m, "SparseDataset", py::module_local())
+      .def(py::init<const std::string&, const std::string&, int, int, int>(), py::arg("path"),
+           py::arg("format") = "libsvm", py::arg("nthreads") = 8, py::arg("shard") = 0,
+           py::arg("nshards") = 1, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rows", &SparseDataset::rows)
+      .def_property_readonly("nnz", &SparseDataset::nnz)
+      .def_property_readonly("max_nnz", &SparseDataset::max_nnz)
+      .def_property_readonly("has_values", &SparseDataset::has_values)
+      .def("labels", [](const SparseDataset& d) {
+        return py::array_t<float>(d.labels().size(), d.labels().data());
+      })
+      .def("keys", [](const SparseDataset& d) {
+        return py::array_t<uint64_t>(d.keys().size(), d.keys().data());
+      })
+      .def("vals", [](const SparseDataset& d) {
+        return py::array_t<float>(d.vals().size(), d.vals().data());
+      })
+      .def("offsets", [](const SparseDataset& d) {
+        return py::array_t<uint64_t>(d.offsets().size(), d.offsets().data());
+      })
+      .def("fill", [](const SparseDataset& d, uint64_t cursor, int B, int F, uintptr_t keys,
+                      uintptr_t vals, uintptr_t labels, int nthreads) {
+             return d.fill(cursor, B, F, reinterpret_cast<uint64_t*>(keys),
+                           reinterpret_cast<float*>(vals), reinterpret_cast<float*>(labels),
+                           nthreads);
+           }, py::arg("cursor"), py::arg("B"), py::arg("F"), py::arg("keys"), py::arg("vals"),
+           py::arg("labels"), py::arg("nthreads") = 4, py::call_guard<py::gil_scoped_release>());
+
+  py::class_<Corpus>(m, "Corpus", py::module_local())
+      .def(py::init<const std::string&, int, int, int, int, double>(), py::arg("path"),
+           py::arg("nthreads") = 8, py::arg("shard") = 0, py::arg("nshards") = 1,
+           py::arg("min_count") = 1, py::arg("sample") = 0.0,
+           py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("size", &Corpus::size)
+      .def_property_readonly("sentences", &Corpus::sentences)
+      .def_property_readonly("vocab_size", &Corpus::vocab_size)
+      .def("vocab", &Corpus::vocab)
+      .def("fill_skipgram", [](const Corpus& c, uint64_t seed, uint64_t step, int B, int C, int W,
+                               long long nneg, uintptr_t keys, int nthreads) {
+             c.fill_skipgram(seed, step, B, C, W, nneg, reinterpret_cast<uint64_t*>(keys),
+                             nthreads);
+           }, py::arg("seed"), py::arg("step"), py::arg("B"), py::arg("C"), py::arg("W"),
+           py::arg("nneg"), py::arg("keys"), py::arg("nthreads") = 4,
+           py::call_guard<py::gil_scoped_release>());
+
   m.def("channel_selftest", [](int producers, int items) {
     // MPMC stress: every produced item is consumed exactly once, close drains
     Channel<long> ch(64);

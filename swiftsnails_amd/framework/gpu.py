@@ -152,11 +152,16 @@ def build_worker(cfg: Config):
     load = float(cfg.get("table_load", 0.7))
     opt = Optimizer(cfg.get("optimizer", "adagrad"), lr=float(cfg.get("learning_rate", 0.05)),
                     l1=float(cfg.get("l1", 0.0)), l2=float(cfg.get("l2", 0.0)))
+    rank = int(os.environ.get("RANK", "0"))
     if model in ("sparse_lr", "fm"):
-        data = CtrSynth(batch_size=int(cfg.get("batch_size", 65536)),
-                        num_fields=int(cfg.get("num_fields", 39)),
-                        num_features=int(float(cfg.get("num_features", 1e9))),
-                        tail_frac=float(cfg.get("tail_frac", 0.1)))
+        if cfg.get("data_path", ""):
+            from ..utils.dataio import make_ctr_source
+            data = make_ctr_source(cfg, rank, world)
+        else:
+            data = CtrSynth(batch_size=int(cfg.get("batch_size", 65536)),
+                            num_fields=int(cfg.get("num_fields", 39)),
+                            num_features=int(float(cfg.get("num_features", 1e9))),
+                            tail_frac=float(cfg.get("tail_frac", 0.1)))
         dim = 1 if model == "sparse_lr" else int(cfg.get("dim", 9))
         init = InitConfig("zero") if model == "sparse_lr" else fm_table_args(dim - 1, opt)[1]
         cap = int(cfg.get("table_capacity", 0) or data.num_features / nserv / load + 1024)
@@ -164,10 +169,14 @@ def build_worker(cfg: Config):
         cls = SparseLRWorker if model == "sparse_lr" else FMWorker
         w = cls(ctx.engine, data, rank=ctx.rank, world=world, active=ctx.is_worker)
     elif model == "word2vec":
-        data = W2VSynth(batch_size=int(cfg.get("batch_size", 16384)),
-                        window=int(cfg.get("window", 5)),
-                        vocab=int(float(cfg.get("vocab", 1e6))),
-                        negatives=int(cfg.get("negatives", 5)))
+        if cfg.get("data_path", ""):
+            from ..utils.dataio import make_corpus_source
+            data = make_corpus_source(cfg, rank, world)
+        else:
+            data = W2VSynth(batch_size=int(cfg.get("batch_size", 16384)),
+                            window=int(cfg.get("window", 5)),
+                            vocab=int(float(cfg.get("vocab", 1e6))),
+                            negatives=int(cfg.get("negatives", 5)))
         dim = int(cfg.get("dim", 128))
         opt, init = make_w2v_table_args(dim, opt)
         cap = int(cfg.get("table_capacity", 0) or 2 * data.vocab / nserv / load + 1024)

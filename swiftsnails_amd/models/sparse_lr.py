@@ -67,6 +67,9 @@ class SparseLRWorker(PipelinedWorker):
         n = B * F
         self.keys = [torch.empty(n, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
         self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
+        # feature values (file data with idx:val entries); synthetic data is binary
+        self.xval = ([torch.empty(n, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
+                     if getattr(data, "has_values", False) else None)
         # grad_mode "segreduce": duplicate merge without global atomics.  With
         # the bucketed deduper (default) the dedup partition is the reduction
         # plan: the forward writes per-occurrence g*x coalesced and one
@@ -111,29 +114,34 @@ class SparseLRWorker(PipelinedWorker):
                                  else self._post)
 
     def _produce(self, step, slot, stream):
-        self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
-                           stream=stream)
+        if self.xval is not None:
+            self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
+                               stream=stream, xval=self.xval[slot])
+        else:
+            self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
+                               stream=stream)
         return self.keys[slot]
 
     def _compute(self, rnd, slot, st):
         d = self.data
         h = hip()
         dd = rnd.dd
+        xp = self.xval[slot].data_ptr() if self.xval is not None else 0
         if self.grad_mode == "segreduce":
-            h.lr_fwd_g(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
+            h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
                        d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(),
                        int(self.bucketed), self.loss_sum.data_ptr(), 0, st)
             if self.bucketed:
                 o = dd.owner
                 h.bd_reduce(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
-                            o.luid.data_ptr(), self.gocc.data_ptr(), 0, d.num_fields,
+                            o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
                             rnd.ugrad.data_ptr(), st)
             else:
                 h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
                             self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,
                             dd.ucount.data_ptr(), dd.nranks, dd.ucap, rnd.ugrad.data_ptr(), st)
         else:
-            h.lr_fwd_bwd(rnd.inv.data_ptr(), 0, self.labels[slot].data_ptr(), d.batch_size,
+            h.lr_fwd_bwd(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
                          self.loss_sum.data_ptr(), 0, st)
 

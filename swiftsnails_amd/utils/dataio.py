@@ -1,0 +1,216 @@
+"""File-backed training data with native parsing and asynchronous prefetch.
+
+The reference apps read text data through ``scan_file_by_line`` /
+``LineFileReader`` and the ``BaseAlgorithm::parse_record(line)`` hook
+(/root/reference/src/utils/file.h:14-33, utils/string.h:89-114,
+core/framework/SwiftWorker.h:19-30); the word2vec corpus format is the one
+written by src/tools/gen-word2vec-data.py.  Here parsing and batch assembly
+are native (``csrc/host/dataio.h``: memory-mapped file, per-thread line
+ranges, GIL released) and Python only keeps a ring of pinned host buffers in
+flight:
+
+    fill (C++ threads) -> pinned host buffer -> async H2D copy on the caller's
+    (route) stream -> event -> buffer reused ``prefetch`` steps later
+
+Both sources are drop-in replacements for the synthetic generators
+(``CtrSynth`` / ``W2VSynth``): same attributes the workers read and the same
+``generate(step, rank, world, ...)`` call.  Rank ``r`` of a ``world``-rank job
+reads its own 1/world of the file (data parallelism).
+"""
+from __future__ import annotations
+
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, Optional
+
+import torch
+
+from .._native import host
+
+NEG_TILE = 64
+TILE = 64
+
+
+class _PinnedRing:
+    """Ring of pinned host buffer sets, each refilled by a native fill job once
+    the H2D copy that last read it has completed."""
+
+    def __init__(self, depth: int, shapes: Dict[str, tuple], pin: bool):
+        self.depth = depth
+        self.bufs = [{k: torch.empty(n, dtype=dt, pin_memory=pin) for k, (n, dt) in shapes.items()}
+                     for _ in range(depth)]
+        self.events = [None] * depth
+        self.futures: Dict[int, object] = {}
+        self.pool = ThreadPoolExecutor(max_workers=1, thread_name_prefix="ss-data")
+
+    def submit(self, step: int, fill):
+        if step in self.futures:
+            return
+        slot = step % self.depth
+        ev = self.events[slot]
+
+        def job():
+            if ev is not None:
+                ev.synchronize()  # the previous H2D copy out of this slot is done
+            fill(step, self.bufs[slot])
+            return slot
+
+        self.events[slot] = None
+        self.futures[step] = self.pool.submit(job)
+
+    def take(self, step: int, fill):
+        self.submit(step, fill)
+        slot = self.futures.pop(step).result()
+        for s in range(step + 1, step + self.depth):  # keep the other slots busy
+            self.submit(s, fill)
+        return slot, self.bufs[slot]
+
+    def mark_copied(self, slot: int, stream):
+        if torch.cuda.is_available() and stream is not None:
+            ev = torch.cuda.Event()
+            ev.record(stream)
+            self.events[slot] = ev
+
+    def close(self):
+        self.pool.shutdown(wait=True)
+
+
+def _ext_stream(stream):
+    if stream is None or not torch.cuda.is_available():
+        return None
+    if isinstance(stream, int):
+        return torch.cuda.ExternalStream(stream)
+    return stream
+
+
+class FileCtrSource:
+    """Sparse CTR batches from a libsvm (``label idx[:val] ...``) or categorical
+    TSV (``label<TAB>tok<TAB>tok...``) file, padded to ``num_fields`` keys per
+    sample (short rows padded with the EMPTY key, which the dedup skips)."""
+
+    def __init__(self, path: str, fmt: str = "libsvm", batch_size: int = 65536,
+                 num_fields: Optional[int] = None, rank: int = 0, world: int = 1,
+                 nthreads: int = 8, prefetch: int = 3, pin: Optional[bool] = None):
+        self.ds = host().SparseDataset(path, fmt, nthreads, rank, world)
+        if self.ds.rows == 0:
+            raise ValueError(f"{path}: no rows for shard {rank}/{world}")
+        self.batch_size = int(batch_size)
+        self.num_fields = int(num_fields or self.ds.max_nnz)
+        self.has_values = bool(self.ds.has_values)
+        self.nthreads = nthreads
+        n = self.batch_size * self.num_fields
+        shapes = {"keys": (n, torch.int64), "labels": (self.batch_size, torch.float32)}
+        if self.has_values:
+            shapes["vals"] = (n, torch.float32)
+        pin = torch.cuda.is_available() if pin is None else pin
+        self.ring = _PinnedRing(max(1, prefetch), shapes, pin)
+        # a synthetic-compatible attribute (table sizing when no capacity is set)
+        self.num_features = max(1, self.ds.nnz)
+
+    @property
+    def rows(self) -> int:
+        return self.ds.rows
+
+    def _fill(self, step: int, buf):
+        cursor = (step * self.batch_size) % self.ds.rows
+        self.ds.fill(cursor, self.batch_size, self.num_fields, buf["keys"].data_ptr(),
+                     buf["vals"].data_ptr() if "vals" in buf else 0, buf["labels"].data_ptr(),
+                     self.nthreads)
+
+    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor,
+                 labels: torch.Tensor, stream=None, xval: Optional[torch.Tensor] = None):
+        slot, buf = self.ring.take(step, self._fill)
+        st = _ext_stream(stream)
+        ctx = torch.cuda.stream(st) if st is not None else _null()
+        with ctx:
+            nb = keys.is_cuda
+            keys.copy_(buf["keys"], non_blocking=nb)
+            labels.copy_(buf["labels"], non_blocking=nb)
+            if xval is not None:
+                if "vals" in buf:
+                    xval.copy_(buf["vals"], non_blocking=nb)
+                else:
+                    xval.fill_(1.0)
+        self.ring.mark_copied(slot, st if st is not None else (
+            torch.cuda.current_stream() if keys.is_cuda else None))
+
+    def close(self):
+        self.ring.close()
+
+
+class FileCorpusSource:
+    """Skip-gram batches from a text corpus (one sentence per line; integer
+    tokens are word ids, other tokens are hashed), in the ``W2VSynth`` key
+    layout: [centers | contexts | shared negatives]."""
+
+    def __init__(self, path: str, batch_size: int = 16384, window: int = 5, negatives: int = 5,
+                 rank: int = 0, world: int = 1, min_count: int = 1, sample: float = 0.0,
+                 seed: int = 1234, nthreads: int = 8, prefetch: int = 3,
+                 pin: Optional[bool] = None):
+        self.corpus = host().Corpus(path, nthreads, rank, world, min_count, sample)
+        self.batch_size = int(batch_size)
+        self.window = int(window)
+        self.negatives = int(negatives)
+        self.seed = int(seed) + 7919 * rank
+        self.nthreads = nthreads
+        self.vocab = max(1, self.corpus.vocab_size)
+        pin = torch.cuda.is_available() if pin is None else pin
+        self.ring = _PinnedRing(max(1, prefetch), {"keys": (self.n_keys, torch.int64)}, pin)
+
+    @property
+    def contexts(self) -> int:
+        return 2 * self.window
+
+    @property
+    def tiles(self) -> int:
+        return (self.batch_size + TILE - 1) // TILE
+
+    @property
+    def n_keys(self) -> int:
+        return self.batch_size * (1 + self.contexts) + self.tiles * NEG_TILE
+
+    @property
+    def neg_scale(self) -> float:
+        return self.contexts * self.negatives / NEG_TILE
+
+    def _fill(self, step: int, buf):
+        self.corpus.fill_skipgram(self.seed, step, self.batch_size, self.contexts, self.window,
+                                  self.tiles * NEG_TILE, buf["keys"].data_ptr(), self.nthreads)
+
+    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None):
+        slot, buf = self.ring.take(step, self._fill)
+        st = _ext_stream(stream)
+        ctx = torch.cuda.stream(st) if st is not None else _null()
+        with ctx:
+            keys.copy_(buf["keys"], non_blocking=keys.is_cuda)
+        self.ring.mark_copied(slot, st if st is not None else (
+            torch.cuda.current_stream() if keys.is_cuda else None))
+
+    def close(self):
+        self.ring.close()
+
+
+class _null:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
+def make_ctr_source(cfg, rank: int = 0, world: int = 1):
+    """Config keys: data_path, data_format (libsvm|ctr), batch_size, num_fields."""
+    return FileCtrSource(cfg.get("data_path"), cfg.get("data_format", "libsvm"),
+                         batch_size=int(cfg.get("batch_size", 65536)),
+                         num_fields=int(cfg.get("num_fields", 0) or 0) or None,
+                         rank=rank, world=world,
+                         nthreads=int(cfg.get("data_threads", 8)))
+
+
+def make_corpus_source(cfg, rank: int = 0, world: int = 1):
+    """Config keys: data_path, batch_size, window, negatives, min_count, sample."""
+    return FileCorpusSource(cfg.get("data_path"), batch_size=int(cfg.get("batch_size", 16384)),
+                            window=int(cfg.get("window", 5)),
+                            negatives=int(cfg.get("negatives", 5)), rank=rank, world=world,
+                            min_count=int(cfg.get("min_count", 1)),
+                            sample=float(cfg.get("sample", 0.0)),
+                            nthreads=int(cfg.get("data_threads", 8)))

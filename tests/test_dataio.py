@@ -1,0 +1,225 @@
+"""Native data input (csrc/host/dataio.h): parsing parity with a Python reader,
+sharding, batch padding, corpus sampling, and the pinned prefetch ring."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _host():
+    from swiftsnails_amd._native import host
+    return host()
+
+
+def _write_libsvm(path, rows=997, seed=0):
+    rng = np.random.default_rng(seed)
+    ref = []
+    with open(path, "w") as f:
+        for i in range(rows):
+            n = int(rng.integers(0, 9))
+            idx = rng.integers(0, 10**12, n)
+            val = np.round(rng.standard_normal(n), 3)
+            lab = int(rng.integers(0, 2)) * 2 - 1 if i % 3 else int(rng.integers(0, 2))
+            toks = [f"{a}:{b}" if j % 2 else f"{a}" for j, (a, b) in enumerate(zip(idx, val))]
+            f.write(f"{lab} " + " ".join(toks) + ("\r\n" if i % 7 == 0 else "\n"))
+            vals = [float(b) if j % 2 else 1.0 for j, b in enumerate(val)]
+            ref.append((1.0 if lab > 0 else 0.0, [int(a) for a in idx], vals))
+    return ref
+
+
+def test_libsvm_parse_matches_python(tmp_path):
+    p = str(tmp_path / "a.svm")
+    ref = _write_libsvm(p)
+    for nthreads in (1, 3, 8):
+        ds = _host().SparseDataset(p, "libsvm", nthreads, 0, 1)
+        assert ds.rows == len(ref)
+        offs = ds.offsets()
+        keys, vals, labels = ds.keys(), ds.vals(), ds.labels()
+        for r, (lab, idx, val) in enumerate(ref):
+            a, b = int(offs[r]), int(offs[r + 1])
+            assert labels[r] == lab
+            assert keys[a:b].tolist() == idx
+            np.testing.assert_allclose(vals[a:b], val, rtol=1e-6)
+        assert ds.has_values
+        assert ds.max_nnz == max(len(x[1]) for x in ref)
+
+
+def test_shards_partition_rows(tmp_path):
+    p = str(tmp_path / "a.svm")
+    ref = _write_libsvm(p, rows=501, seed=3)
+    for world in (2, 3, 5):
+        got = []
+        for r in range(world):
+            ds = _host().SparseDataset(p, "libsvm", 2, r, world)
+            offs, keys = ds.offsets(), ds.keys()
+            got += [keys[int(offs[i]):int(offs[i + 1])].tolist() for i in range(ds.rows)]
+        assert got == [x[1] for x in ref]  # contiguous shards, in file order
+
+
+def test_ctr_tsv_fields_and_hashing(tmp_path):
+    from swiftsnails_amd.utils.hashing import fmix64  # noqa: F401 (module import check)
+    p = str(tmp_path / "a.tsv")
+    lines = ["1\ta\tb\t\tc", "0\t\tx\ty\t", "1\tq"]
+    with open(p, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    ds = _host().SparseDataset(p, "ctr", 2, 0, 1)
+    assert ds.rows == 3
+    assert ds.labels().tolist() == [1.0, 0.0, 1.0]
+    offs, keys = ds.offsets(), ds.keys()
+    fields = [[int(k) >> 48 for k in keys[int(offs[i]):int(offs[i + 1])]] for i in range(3)]
+    assert fields == [[0, 1, 3], [1, 2], [0]]
+    # same token in the same field -> same key; different field -> different key
+    k0 = keys[int(offs[0]):int(offs[1])]
+    assert len(set(int(k) & ((1 << 48) - 1) for k in k0)) == 3
+    assert not ds.has_values
+
+
+def test_fill_pads_truncates_and_wraps(tmp_path):
+    p = str(tmp_path / "a.svm")
+    ref = _write_libsvm(p, rows=37, seed=5)
+    ds = _host().SparseDataset(p, "libsvm", 4, 0, 1)
+    B, F = 50, 4
+    keys = np.empty(B * F, dtype=np.uint64)
+    vals = np.empty(B * F, dtype=np.float32)
+    labels = np.empty(B, dtype=np.float32)
+    nxt = ds.fill(30, B, F, keys.ctypes.data, vals.ctypes.data, labels.ctypes.data, 3)
+    assert nxt == (30 + B) % 37
+    for b in range(B):
+        lab, idx, val = ref[(30 + b) % 37]
+        row = keys[b * F:(b + 1) * F]
+        m = min(F, len(idx))
+        assert row[:m].tolist() == idx[:m]
+        assert (row[m:] == np.uint64(0xFFFFFFFFFFFFFFFF)).all()
+        np.testing.assert_allclose(vals[b * F:b * F + m], val[:m], rtol=1e-6)
+        assert (vals[b * F + m:(b + 1) * F] == 0).all()
+        assert labels[b] == lab
+
+
+def test_file_ctr_source_prefetch_cpu(tmp_path):
+    from swiftsnails_amd.utils.dataio import FileCtrSource
+    p = str(tmp_path / "a.svm")
+    _write_libsvm(p, rows=123, seed=9)
+    src = FileCtrSource(p, "libsvm", batch_size=16, num_fields=5, pin=False, prefetch=3)
+    ds = _host().SparseDataset(p, "libsvm", 1, 0, 1)
+    keys = torch.empty(16 * 5, dtype=torch.int64)
+    labels = torch.empty(16)
+    xval = torch.empty(16 * 5)
+    for step in range(12):
+        src.generate(step, 0, 1, keys, labels, xval=xval)
+        ek = np.empty(80, dtype=np.uint64)
+        ev = np.empty(80, dtype=np.float32)
+        el = np.empty(16, dtype=np.float32)
+        ds.fill((step * 16) % 123, 16, 5, ek.ctypes.data, ev.ctypes.data, el.ctypes.data, 1)
+        assert keys.numpy().view(np.uint64).tolist() == ek.tolist()
+        assert labels.numpy().tolist() == el.tolist()
+        assert xval.numpy().tolist() == ev.tolist()
+    src.close()
+
+
+def test_corpus_and_skipgram_sampling(tmp_path):
+    p = str(tmp_path / "w2v.txt")
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_word2vec_data.py"), p,
+                           "--lines", "500", "--seed", "1"])
+    sents = [list(map(int, ln.split())) for ln in open(p)]
+    c = _host().Corpus(p, 4, 0, 1, 1, 0.0)
+    assert c.size == sum(len(s) for s in sents)
+    assert c.sentences == len(sents)
+    vocab = dict(c.vocab())
+    assert sum(vocab.values()) == c.size
+    assert max(vocab) <= 300
+    B, W = 256, 3
+    C = 2 * W
+    nneg = 64
+    keys = np.empty(B + B * C + nneg, dtype=np.uint64)
+    c.fill_skipgram(7, 0, B, C, W, nneg, keys.ctypes.data, 4)
+    out = np.uint64(1 << 40)
+    centers, ctx, neg = keys[:B], keys[B:B + B * C], keys[B + B * C:]
+    assert (ctx & out).all() and (neg & out).all() and not (centers & out).any()
+    assert set((neg & ~out).tolist()) <= set(vocab)
+    # every context is within +-W of SOME occurrence of the center in one sentence
+    for b in range(0, B, 17):
+        cw = int(centers[b])
+        ok_ctx = set()
+        for s in sents:
+            for i, w in enumerate(s):
+                if w == cw:
+                    ok_ctx |= set(s[max(0, i - W):i] + s[i + 1:i + 1 + W])
+        for x in ctx[b * C:(b + 1) * C]:
+            assert int(x & ~out) in ok_ctx
+    # deterministic per (seed, step)
+    k2 = np.empty_like(keys)
+    c.fill_skipgram(7, 0, B, C, W, nneg, k2.ctypes.data, 2)
+    np.testing.assert_array_equal(keys, k2)
+
+
+def test_corpus_hashes_words_and_min_count(tmp_path):
+    p = str(tmp_path / "t.txt")
+    with open(p, "w") as f:
+        f.write("the cat sat\nthe dog\nrare the\n")
+    c = _host().Corpus(p, 2, 0, 1, 2, 0.0)  # min_count 2 keeps only "the"
+    assert c.vocab_size == 1
+    assert c.size == 3
+
+
+@pytest.mark.gpu
+def test_sparse_lr_trains_from_libsvm_file(tmp_path):
+    from swiftsnails_amd.models.sparse_lr import SparseLRWorker, make_lr_table
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.parallel.transport import LoopbackTransport
+    from swiftsnails_amd.utils.dataio import FileCtrSource
+
+    rng = np.random.default_rng(0)
+    w = rng.standard_normal(5000)
+    p = str(tmp_path / "train.svm")
+    with open(p, "w") as f:
+        for _ in range(20000):
+            idx = rng.choice(5000, 8, replace=False)
+            z = w[idx].sum() * 0.5
+            y = int(rng.random() < 1 / (1 + np.exp(-z)))
+            f.write(f"{y} " + " ".join(f"{i}:0.5" for i in idx) + "\n")
+    dev = torch.device("cuda", 0)
+    src = FileCtrSource(p, "libsvm", batch_size=1024, num_fields=8)
+    assert src.has_values
+    table = make_lr_table(10000, device=dev)
+    eng = PSEngine(table, LoopbackTransport(), max_keys=1024 * 8, dim=1, device=dev)
+    wk = SparseLRWorker(eng, src)
+    losses = []
+    for i in range(60):
+        wk.step()
+        if i % 10 == 9:
+            losses.append(wk.mean_loss())
+    torch.cuda.synchronize()
+    assert losses[-1] < losses[0] - 0.02, losses
+    src.close()
+
+
+@pytest.mark.gpu
+def test_word2vec_trains_from_corpus_file(tmp_path):
+    from swiftsnails_amd.models.word2vec import Word2VecWorker, make_w2v_table_args
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.parallel.transport import LoopbackTransport
+    from swiftsnails_amd.utils.dataio import FileCorpusSource
+
+    p = str(tmp_path / "w2v.txt")
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_word2vec_data.py"), p,
+                           "--lines", "5000", "--zipf", "1.3", "--vocab", "2000"])
+    dev = torch.device("cuda", 0)
+    src = FileCorpusSource(p, batch_size=1024, window=2, negatives=5)
+    opt, init = make_w2v_table_args(32)
+    table = HbmTable(capacity=16384, dim=32, optimizer=opt, init=init, device=dev)
+    eng = PSEngine(table, LoopbackTransport(), max_keys=src.n_keys, dim=32, device=dev)
+    wk = Word2VecWorker(eng, src)
+    first = None
+    for i in range(40):
+        wk.step()
+        if i == 4:
+            first = wk.mean_loss()
+    torch.cuda.synchronize()
+    assert wk.mean_loss() < first, (first, wk.mean_loss())
+    src.close()

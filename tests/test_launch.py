@@ -62,3 +62,19 @@ def test_cli_gpu_sparse_lr_backup_and_resume(tmp_path):
     r2 = subprocess.run(common + ["--steps", "2", "--set", f"resume_from={tmp_path}/param-10"],
                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r2.returncode == 0, r2.stderr[-3000:]
+
+
+def test_cluster_script_two_servers_two_workers(tmp_path):
+    """tools/cluster_test.sh: master + 2 servers + 2 workers as processes; each
+    server dumps its own shard, together covering every key exactly once."""
+    out = tmp_path / "final.txt"
+    env = dict(os.environ, PYTHONPATH=ROOT, SERVERS="2", WORKERS="2", LOG_DIR=str(tmp_path))
+    r = subprocess.run(["bash", os.path.join(ROOT, "tools", "cluster_test.sh"),
+                        os.path.join(ROOT, "configs", "dense_lr_cpu.conf"),
+                        "--set", "num_iters=15", "--set", f"param_output={out}"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-2000:]
+    shards = sorted(tmp_path.glob("final.txt.s*"))
+    assert len(shards) == 2
+    keys = [int(ln.split("\t")[0]) for f in shards for ln in f.read_text().splitlines()]
+    assert sorted(keys) == list(range(64))
