@@ -137,8 +137,8 @@ def test_cluster_master_servers_workers(tmp_path):
     assert all(not t.is_alive() for t in ths)
     # 2 workers x 2 pushes x (-lr * 1) on SGD, lr 0.5 => -2.0 after all pushes
     final = {}
-    for i in range(2):
-        for line in open(f"{out_base}_{1 + i}.txt"):
+    for i, sv in enumerate(servers):  # >1 server: each dumps <path>.s<id>
+        for line in open(f"{out_base}_{1 + i}.txt.s{sv.client_id}"):
             k, v = line.rstrip("\n").split("\t")
             final[int(k)] = [float(x) for x in v.split()]
     assert sorted(final) == sorted([1, 2, 3, 1000, 77777, 2**40 + 5])
@@ -148,7 +148,7 @@ def test_cluster_master_servers_workers(tmp_path):
     assert sorted(s.client_id for s in servers) == [1, 2]
     assert sorted(w.client_id for w in workers) == [2**31 - 3, 2**31 - 2]
     # periodic backup every 2 push requests (server/init.h:126-149)
-    assert list(tmp_path.glob("param-*.txt"))
+    assert list(tmp_path.glob("param-*.txt.s*"))
 
 
 def test_dense_lr_one_worker_one_server_loopback(tmp_path):
