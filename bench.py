@@ -95,12 +95,22 @@ def main(argv=None):
                       count_transport=ctrans)
     worker = SparseLRWorker(engine, data, rank=rank, world=world, grad_mode=a.grad_mode)
 
+    # a wedged collective ends the job (exit 3) instead of hanging the node
+    from swiftsnails_amd.parallel.watchdog import FailureHandler, Watchdog
+
+    failure = FailureHandler()
+    for t in (transport, ctrans):
+        if hasattr(t, "abort"):
+            failure.add_hook(t.abort)
+    wd = Watchdog(float(os.environ.get("SS_BENCH_ROUND_TIMEOUT", "300")), failure, name="bench")
+
     def barrier():
         if world > 1:
             dist.barrier()
 
-    for _ in range(a.warmup):
+    for i in range(a.warmup):
         worker.step()
+        wd.beat(i)
     torch.cuda.synchronize()
     table.check()
     first_loss = worker.mean_loss()
@@ -113,6 +123,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    wd.beat("timed")
 
     t = torch.tensor([elapsed], dtype=torch.float64)
     if world > 1:
@@ -154,6 +165,7 @@ def main(argv=None):
             },
         }
         print(json.dumps(out), flush=True)
+    wd.stop()
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

@@ -32,6 +32,7 @@ from ..ops.optim import InitConfig, Optimizer
 from ..ops.table import HbmTable
 from ..parallel.engine import PSEngine
 from ..parallel.transport import LoopbackTransport, RcclTransport, TorchDistTransport
+from ..parallel.watchdog import FailureHandler, FaultInjector, Heartbeat, Watchdog
 from ..utils import checkpoint as ck
 from ..utils.config import Config
 from ..utils.logging import get_logger
@@ -63,6 +64,7 @@ class PSContext:
         self.is_server = self.rank in self.servers
         self.is_worker = self.rank in self.workers
         ct = None
+        store = None
         if self.world > 1:
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
             if not dist.is_initialized():
@@ -93,6 +95,19 @@ class PSContext:
         self.backup_root = cfg.get("param_backup_root", ".")
         self.ckpt_format = cfg.get("checkpoint_format", "bin")
         self.tracer = Tracer(enabled=str(cfg.get("trace", "0")) not in ("0", "false"))
+        # failure detection (parallel/watchdog.py): round watchdog + heartbeats
+        self.failure = FailureHandler(exit_process=str(cfg.get("watchdog_exit", "1")) != "0")
+        for t in (tr, ct):
+            if hasattr(t, "abort"):
+                self.failure.add_hook(t.abort)
+        rt = float(cfg.get("round_timeout", 600) or 0)
+        self.watchdog = Watchdog(rt, self.failure) if rt > 0 else None
+        self.heartbeat = None
+        if store is not None and float(cfg.get("peer_timeout", 120) or 0) > 0:
+            self.heartbeat = Heartbeat(store, self.rank, self.world, self.failure,
+                                       interval=float(cfg.get("heartbeat_interval", 2.0)),
+                                       peer_timeout=float(cfg.get("peer_timeout", 120)))
+        self.fault = FaultInjector(rank=self.rank)
         resume = cfg.get("resume_from")
         if resume:
             self.resume(resume)
@@ -121,13 +136,25 @@ class PSContext:
     def maybe_backup(self, round_idx: int) -> None:
         """Reference: every param_backup_period pushes -> param-<n>.txt."""
         if self.backup_period > 0 and round_idx > 0 and round_idx % self.backup_period == 0:
+            if self.watchdog:
+                self.watchdog.pause()
             self.save(os.path.join(self.backup_root, f"param-{round_idx}"))
+            if self.watchdog:
+                self.watchdog.resume()
+
+    def round_done(self, round_idx: int) -> None:
+        """Per-round progress mark for the watchdog (+ fault injection point)."""
+        if self.watchdog:
+            self.watchdog.beat(round_idx)
+        self.fault.maybe(round_idx)
 
     def barrier(self):
         if self.world > 1:
             dist.barrier()
 
     def finish(self):
+        if self.watchdog:
+            self.watchdog.pause()
         out = self.cfg.get("param_output")
         if out:
             self.save(out, fmt=self.cfg.get("param_output_format", "text"))
@@ -136,6 +163,9 @@ class PSContext:
         self.barrier()
 
     def close(self):
+        for x in (self.watchdog, self.heartbeat):
+            if x is not None:
+                x.stop()
         if self.world > 1 and dist.is_initialized():
             dist.destroy_process_group()
 
@@ -201,6 +231,7 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     for i in range(steps):
         with ctx.tracer.range(f"step{i}"):
             w.step()
+        ctx.round_done(w.step_idx)
         ctx.maybe_backup(w.step_idx)
         if log_every and (i + 1) % log_every == 0 and ctx.rank == 0:
             log.warning("step %d loss %.5f", i + 1, w.mean_loss())

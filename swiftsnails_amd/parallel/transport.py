@@ -172,6 +172,11 @@ class RcclTransport(Transport):
     def _st():
         return torch.cuda.current_stream().cuda_stream
 
+    def abort(self) -> None:
+        """ncclCommAbort: stuck collectives return; the communicator is dead
+        afterwards (failure path of parallel/watchdog.py)."""
+        self.comm.abort()
+
     def exchange_counts(self, send_counts):
         return self.exchange_counts_async(send_counts).wait()
 

@@ -10,7 +10,9 @@ expected_node_num, master_time_out, frag_num, shard_num, param_backup_period,
 param_backup_root, num_iters, learning_rate, async_channel_thread_num,
 local_train`` plus the MI355X additions ``optimizer, l1, l2, param_init,
 param_init_scale, param_output, server_ranks, worker_ranks, table_capacity,
-batch_size``.
+batch_size``, data input ``data_path, data_format, data_threads, min_count,
+sample`` and failure detection ``round_timeout, peer_timeout,
+heartbeat_interval, watchdog_exit`` (parallel/watchdog.py).
 """
 from __future__ import annotations
 
