@@ -216,7 +216,8 @@ class Transfer : NonCopyable {
     SS_CHECK_MSG(lfd_ >= 0, "listen() first");
     SS_CHECK(!running_.exchange(true));
     pool_.reset(new ThreadPool(async_threads));
-    accept_thread_ = std::thread([this] { accept_loop(); });
+    const int lfd = lfd_;  // the accept thread never reads the member (service_end resets it)
+    accept_thread_ = std::thread([this, lfd] { accept_loop(lfd); });
   }
 
   void service_end() {
@@ -227,10 +228,10 @@ class Transfer : NonCopyable {
       }
       return;
     }
-    ::shutdown(lfd_, SHUT_RDWR);
+    ::shutdown(lfd_, SHUT_RDWR);  // wakes accept(); close only after the join so the
+    if (accept_thread_.joinable()) accept_thread_.join();  // fd number cannot be reused under it
     ::close(lfd_);
     lfd_ = -1;
-    if (accept_thread_.joinable()) accept_thread_.join();
     {
       std::lock_guard<std::mutex> lk(conn_mu_);
       for (auto& kv : out_) {
@@ -356,11 +357,11 @@ class Transfer : NonCopyable {
                  "send to node " << id << " failed");
   }
 
-  void accept_loop() {
+  void accept_loop(int lfd) {
     while (running_) {
       sockaddr_in sa{};
       socklen_t len = sizeof(sa);
-      const int fd = ::accept(lfd_, (sockaddr*)&sa, &len);
+      const int fd = ::accept(lfd, (sockaddr*)&sa, &len);
       if (fd < 0) {
         if (!running_) break;
         if (errno == EINTR) continue;

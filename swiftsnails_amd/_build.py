@@ -117,6 +117,34 @@ def build_hip(force=False, nproc=8) -> str:
     return _build_module("_ss_hip", srcs, hipcc, cflags, ldflags, inc, force, nproc)
 
 
+TEST_DIR = os.path.join(BUILD_DIR, "tests")
+SANITIZERS = {
+    "plain": [],
+    # host code only (no GPU code in this binary); -O1 keeps reports readable
+    "asan": ["-fsanitize=address,undefined", "-fno-omit-frame-pointer", "-O1"],
+    "tsan": ["-fsanitize=thread", "-O1", "-include",
+             os.path.join(ROOT, "csrc", "tests", "tsan_compat.h")],
+}
+
+
+def build_cpp_tests(variant: str = "plain", force: bool = False) -> str:
+    """Native host unit tests (csrc/tests/test_host.cpp): plain, ASan+UBSan
+    or TSan build -> build/tests/test_host_<variant>."""
+    os.makedirs(TEST_DIR, exist_ok=True)
+    src = os.path.join(ROOT, "csrc", "tests", "test_host.cpp")
+    out = os.path.join(TEST_DIR, f"test_host_{variant}")
+    inc = [os.path.join(ROOT, "csrc", "include"), os.path.join(ROOT, "csrc", "host")]
+    newest = max(os.path.getmtime(src), _newest(_headers(inc)))
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= newest:
+        return out
+    cxx = os.environ.get("CXX", "g++")
+    flags = ["-std=c++17", "-g", "-pthread", "-Wall", "-Wno-unused-function"]
+    flags += SANITIZERS[variant] or ["-O2"]
+    cmd = [cxx] + flags + ["-I" + d for d in inc] + [src, "-o", out]
+    subprocess.run(cmd, check=True)
+    return out
+
+
 def build_all(force=False, only=None, nproc=None) -> list[str]:
     nproc = nproc or min(16, os.cpu_count() or 4)
     outs = []
