@@ -126,6 +126,10 @@ PYBIND11_MODULE(_ss_hip, m) {
                   S(st));
   });
 
+  m.def("probe_hist", [](const DevTable& t, uintptr_t hist, int nbins, uintptr_t st) {
+    launch_probe_hist(t, P<unsigned long long>(hist), nbins, S(st));
+  });
+
   // ---- dedup / route (K1/K2/K6/K7)
   m.def("dedup_route", [](uintptr_t keys, long long n, uintptr_t skeys, uintptr_t stag,
                           unsigned long long scap, uintptr_t slot_of, uintptr_t frag_map,

@@ -36,6 +36,7 @@ void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, l
                    unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,
                    float* rows_out, unsigned long long* cursor, hipStream_t st);
+void launch_probe_hist(const DevTable& t, unsigned long long* hist, int nbins, hipStream_t st);
 
 // --- dedup.hip
 struct RouteSpec {

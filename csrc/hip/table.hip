@@ -364,6 +364,28 @@ __global__ __launch_bounds__(256) void k_export(DevTable t, unsigned long long s
   }
 }
 
+// Probe-length histogram (observability): for every occupied slot
+// the distance from its key's home slot, binned [0, nbins-1] (last bin =
+// ">= nbins-1").  LDS histogram per workgroup, one global add per bin.
+__global__ __launch_bounds__(256) void k_probe_hist(DevTable t, unsigned long long* __restrict__ hist,
+                                                    int nbins) {
+  __shared__ unsigned int h[256];
+  for (int b = threadIdx.x; b < nbins; b += 256) h[b] = 0u;
+  __syncthreads();
+  const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+  for (unsigned long long s = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; s < t.cap;
+       s += stride) {
+    const uint64_t key = *slot_key(t, s);
+    if (key == kEmptyKey) continue;
+    const uint64_t home = fastrange64(table_hash(key), t.cap);
+    const uint64_t d = s >= home ? s - home : s + t.cap - home;
+    atomicAdd(&h[d < (uint64_t)nbins - 1 ? (int)d : nbins - 1], 1u);
+  }
+  __syncthreads();
+  for (int b = threadIdx.x; b < nbins; b += 256)
+    if (h[b]) atomicAdd(hist + b, (unsigned long long)h[b]);
+}
+
 // ---------------------------------------------------------------- launchers
 static inline int grid_for(long long groups, int G, int cap_blocks = 16384) {
   long long threads = groups * G;
@@ -434,6 +456,13 @@ void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, l
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_assign<kG>, dim3(grid_for(n, kG)), dim3(256), 0, st, t,
                                       keys, rows, n, size_ctr, err));
   check_launch("k_assign");
+}
+
+void launch_probe_hist(const DevTable& t, unsigned long long* hist, int nbins, hipStream_t st) {
+  if (nbins < 2 || nbins > 256) throw_error("probe_hist: nbins must be in [2, 256]");
+  check_hip(hipMemsetAsync(hist, 0, sizeof(unsigned long long) * nbins, st), "probe_hist");
+  hipLaunchKernelGGL(k_probe_hist, dim3(4096), dim3(256), 0, st, t, hist, nbins);
+  check_launch("k_probe_hist");
 }
 
 void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,

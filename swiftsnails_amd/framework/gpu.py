@@ -250,6 +250,11 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
              "seconds": el, "ms_per_step": 1000 * el / max(1, steps),
              "samples_per_s": int(n.item()) * steps / el if el > 0 else 0.0,
              "loss": w.mean_loss() if ctx.is_worker else None}
+    m = ctx.engine.metrics.counters
+    if m:
+        stats["rank0_engine"] = {k: int(v) for k, v in m.items()}
+    if ctx.table is not None and str(cfg.get("table_stats", "1")) != "0":
+        stats["rank0_table"] = ctx.table.stats()
     ctx.finish()
     ctx.close()
     return stats

@@ -202,6 +202,27 @@ class HbmTable:
     def load_factor(self) -> float:
         return self.size() / self.capacity
 
+    def probe_histogram(self, nbins: int = 32):
+        """Distance of every stored key from its home slot (linear probing),
+        binned; the last bin counts ``>= nbins-1``.  Scans the whole shard."""
+        hist = torch.empty(nbins, dtype=torch.int64, device=self.device)
+        hip().probe_hist(self.dt, hist.data_ptr(), nbins, _stream_ptr(None))
+        return hist.cpu().numpy()
+
+    def stats(self) -> dict:
+        """Observability snapshot: size, load factor, mean/max probe length."""
+        import numpy as np
+
+        h = self.probe_histogram(64)
+        n = int(h.sum())
+        d = np.arange(len(h))
+        return {"size": self.size(), "capacity": self.capacity,
+                "load_factor": self.size() / self.capacity,
+                "probe_mean": float((h * d).sum() / n) if n else 0.0,
+                "probe_p99": int(np.searchsorted(np.cumsum(h), 0.99 * n)) if n else 0,
+                "probe_max_bin": int(np.nonzero(h)[0].max()) if n else 0,
+                "hbm_bytes": int(self.storage.numel() * self.storage.element_size())}
+
     def check(self):
         e = int(self.err.item())
         if e & 1:

@@ -136,6 +136,12 @@ class PSEngine:
         dev = self.device
         self.uvals = [torch.empty((N * cap, d), dtype=torch.float32, device=dev)
                       for _ in range(self.depth)]
+        # observability: occurrences routed, unique keys exchanged,
+        # alltoallv payload bytes (host-known counts; world-1 keeps counts on
+        # the device and only counts occurrences)
+        from ..utils.tracing import Metrics
+
+        self.metrics = Metrics()
         self.fast1 = self.gpu and self.world == 1
         if self.fast1:
             self.slots = [torch.empty(cap, dtype=torch.int64, device=dev)
@@ -226,14 +232,19 @@ class PSEngine:
         if self.fast1:
             tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                      segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
+            self.metrics.add(occurrences=dd.n)
             return Round(dd, uv, slot, slots=self.slots[slot])
         scounts, rcounts = r.counts.wait()
         D = self.displs
         self.t.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
         self._server_pull(rcounts, slot)
         self.t.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
+        sent, recv = int(scounts.sum()), int(rcounts.sum())
+        # pull: keys out + rows back; push (next): grad rows out
+        self.metrics.add(occurrences=dd.n, unique_sent=sent, unique_recv=recv,
+                         a2a_bytes=8 * (sent + recv) + 4 * self.dim * (2 * sent + 2 * recv))
         return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
-                     stats={"sent": int(scounts.sum()), "recv": int(rcounts.sum())})
+                     stats={"sent": sent, "recv": recv})
 
     # ------------------------------------------------------------ stage 3
     def _server_apply(self, rcounts: np.ndarray, slot: int, resolved: bool) -> None:

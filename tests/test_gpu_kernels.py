@@ -386,3 +386,17 @@ def test_pull_unique_insert_modes(dev, mode, G, load):
     assert (s2n >= 0).all() and len(np.unique(s2n)) == len(k2)
     d = t.to_dict()
     assert len(d) == n and set(d) == set(int(x) for x in k.view(np.uint64))
+
+
+def test_probe_histogram_and_stats(dev):
+    from swiftsnails_amd.ops.table import HbmTable
+
+    t = HbmTable(1, 5000, device=dev)
+    keys = torch.arange(3500, dtype=torch.int64, device=dev) * 7919 + 11
+    t.pull(keys, insert=True)
+    h = t.probe_histogram(16)
+    assert int(h.sum()) == 3500 == t.size()
+    assert h[0] > 1000  # most keys sit at their home slot at load 0.7
+    st = t.stats()
+    assert abs(st["load_factor"] - 3500 / t.capacity) < 1e-9
+    assert 0 <= st["probe_mean"] < 5
