@@ -218,11 +218,13 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("lr_fwd_g", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
                        uintptr_t uvals, uintptr_t g, int per_sample, uintptr_t loss,
-                       uintptr_t pred, uintptr_t st) {
-    launch_lr_fwd_g(P<const uint32_t>(inv), P<const float>(xval), P<const float>(labels), B, F,
-                    P<const float>(uvals), P<float>(g), per_sample, P<float>(loss),
-                    P<float>(pred), S(st));
-  });
+                       uintptr_t pred, uintptr_t st, uintptr_t pos_of, uintptr_t luid) {
+    launch_lr_fwd_g(P<const uint32_t>(inv), P<const uint32_t>(pos_of), P<const uint32_t>(luid),
+                    P<const float>(xval), P<const float>(labels), B, F, P<const float>(uvals),
+                    P<float>(g), per_sample, P<float>(loss), P<float>(pred), S(st));
+  }, py::arg("inv"), py::arg("xval"), py::arg("labels"), py::arg("B"), py::arg("F"),
+     py::arg("uvals"), py::arg("g"), py::arg("per_sample"), py::arg("loss"), py::arg("pred"),
+     py::arg("st"), py::arg("pos_of") = 0, py::arg("luid") = 0);
   m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
                          uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {
     launch_fm_fwd_bwd(P<const uint32_t>(inv), P<const float>(labels), B, F, dim,

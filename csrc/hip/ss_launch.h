@@ -81,9 +81,9 @@ void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* 
 void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
                       const uint32_t* nitems, long long n, const unsigned long long* ucount,
                       int nranks, long long ucap, float* ugrad, hipStream_t st);
-void launch_lr_fwd_g(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
-                     const float* uvals, float* g, int per_sample, float* loss_sum, float* pred,
-                     hipStream_t st);
+void launch_lr_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t* luid,
+                     const float* xval, const float* labels, int B, int F, const float* uvals,
+                     float* g, int per_sample, float* loss_sum, float* pred, hipStream_t st);
 
 // --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
 long long bd_scratch_words(long long n, int nranks);

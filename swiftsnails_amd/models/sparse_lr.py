@@ -85,7 +85,8 @@ class SparseLRWorker(PipelinedWorker):
             self.gocc = torch.empty(B if self.bucketed else n, dtype=torch.float32, device=dev)
         if self.bucketed:
             for dd in engine.dedupers:
-                dd.zero_grad = False
+                dd.zero_grad = False        # the LDS reduce stores every unique row
+                dd.materialize_inv = False  # the forward reads luid[pos_of[j]] itself
         elif grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
@@ -128,11 +129,17 @@ class SparseLRWorker(PipelinedWorker):
         dd = rnd.dd
         xp = self.xval[slot].data_ptr() if self.xval is not None else 0
         if self.grad_mode == "segreduce":
-            h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
-                       d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(),
-                       int(self.bucketed), self.loss_sum.data_ptr(), 0, st)
+            o = dd.owner
             if self.bucketed:
-                o = dd.owner
+                h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
+                           rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
+                           self.loss_sum.data_ptr(), 0, st, o.pos_of.data_ptr(),
+                           o.luid.data_ptr())
+            else:
+                h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
+                           d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 0,
+                           self.loss_sum.data_ptr(), 0, st)
+            if self.bucketed:
                 h.bd_reduce(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                             o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
                             rnd.ugrad.data_ptr(), st)

@@ -65,6 +65,9 @@ class Deduper:
         # zero_grad=False: the model's backward writes every unique row itself
         # (e.g. the segmented reduction of segreduce.hip), skip zeroing here.
         self.zero_grad = zero_grad
+        # bucket mode: False skips the inverse-index pass; consumers then read
+        # luid[pos_of[j]] themselves (the LR forward does, fused)
+        self.materialize_inv = True
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -119,7 +122,8 @@ class Deduper:
                             self.nranks, self.ucap, self.scratch.data_ptr(),
                             self.sync.data_ptr(), self.epoch, self.pj.data_ptr(),
                             self.pos_of.data_ptr(), self.luid.data_ptr(), self.ucount.data_ptr(),
-                            self.ukeys.data_ptr(), ug, self.gdim, self.inv.data_ptr(), st,
+                            self.ukeys.data_ptr(), ug, self.gdim,
+                            self.inv.data_ptr() if self.materialize_inv else 0, st,
                             self.dbg.data_ptr() if self.dbg is not None else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self)
