@@ -13,6 +13,7 @@
 //
 // Synthetic CTR data is generated on device each step (counter-based RNG), so
 // the timed step includes producing its input batch.
+#include "sample_group.h"
 #include "ss_device.h"
 #include "ss_launch.h"
 
@@ -32,11 +33,50 @@ __device__ __forceinline__ float truth_weight(uint64_t key, float scale) {
 // Keys: field f owns [f*V, (f+1)*V); ids are log-uniform (Zipf-like head, as
 // in CTR data) with a `tail_frac` share drawn uniformly over the field (long
 // tail that keeps inserting new keys into the table).
+__device__ __forceinline__ uint64_t gen_ctr_key(uint64_t seed, uint64_t gs, int f, long long V,
+                                                double logV, float tail_frac) {
+  const uint64_t r = splitmix64(seed ^ (gs * 0xA24BAED4963EE407ull) ^ ((uint64_t)f << 40));
+  const uint64_t r2 = splitmix64(r);
+  uint64_t id;
+  if (u01(r2) < tail_frac) {
+    id = fastrange64(splitmix64(r2 ^ 0x632BE59BD9B4E019ull), (uint64_t)V);
+  } else {
+    const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+    long long v = (long long)exp(u * logV) - 1;
+    id = (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
+  }
+  return (uint64_t)f * (uint64_t)V + id;
+}
+
+__device__ __forceinline__ float gen_ctr_label(uint64_t seed, uint64_t gs, float z) {
+  const float p = 1.f / (1.f + __expf(-z));
+  return u01(splitmix64(seed ^ 0xBEEF ^ (gs * 0x9E3779B97F4A7C15ull))) < p ? 1.f : 0.f;
+}
+
+// one sample per lane group (F <= 64)
 __global__ __launch_bounds__(256) void k_gen_ctr(uint64_t seed, long long sample_base, int B,
-                                                 int F, long long V, double logV, float tail_frac,
-                                                 float truth_scale, float truth_bias,
-                                                 uint64_t* __restrict__ keys,
+                                                 int F, int L, long long V, double logV,
+                                                 float tail_frac, float truth_scale,
+                                                 float truth_bias, uint64_t* __restrict__ keys,
                                                  float* __restrict__ labels) {
+  const int t = threadIdx.x, f = t & (L - 1);
+  const long long s = (long long)blockIdx.x * (256 / L) + t / L;
+  float w = 0.f;
+  if (f < F && s < B) {
+    const uint64_t key = gen_ctr_key(seed, (uint64_t)(sample_base + s), f, V, logV, tail_frac);
+    keys[s * F + f] = key;
+    w = truth_weight(key, truth_scale);
+  }
+  const float z = group_sum(w, L) + truth_bias;
+  if (f == 0 && s < B) labels[s] = gen_ctr_label(seed, (uint64_t)(sample_base + s), z);
+}
+
+// packed layout with an LDS per-sample sum (F > 64)
+__global__ __launch_bounds__(256) void k_gen_ctr_lds(uint64_t seed, long long sample_base, int B,
+                                                     int F, long long V, double logV,
+                                                     float tail_frac, float truth_scale,
+                                                     float truth_bias, uint64_t* __restrict__ keys,
+                                                     float* __restrict__ labels) {
   __shared__ float sdot[256];
   const int spb = samples_per_block(F);
   const int t = threadIdx.x;
@@ -45,34 +85,19 @@ __global__ __launch_bounds__(256) void k_gen_ctr(uint64_t seed, long long sample
   if (t < spb) sdot[t] = 0.f;
   __syncthreads();
   if (ls < spb && s0 + ls < B && F <= 256) {
-    const long long s = s0 + ls;
-    const uint64_t gs = (uint64_t)(sample_base + s);
-    const uint64_t r = splitmix64(seed ^ (gs * 0xA24BAED4963EE407ull) ^ ((uint64_t)f << 40));
-    const uint64_t r2 = splitmix64(r);
-    uint64_t id;
-    if (u01(r2) < tail_frac) {
-      id = fastrange64(splitmix64(r2 ^ 0x632BE59BD9B4E019ull), (uint64_t)V);
-    } else {
-      const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
-      long long v = (long long)exp(u * logV) - 1;
-      id = (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
-    }
-    const uint64_t key = (uint64_t)f * (uint64_t)V + id;
-    keys[s * F + f] = key;
+    const uint64_t key =
+        gen_ctr_key(seed, (uint64_t)(sample_base + s0 + ls), f, V, logV, tail_frac);
+    keys[(s0 + ls) * F + f] = key;
     atomicAdd(&sdot[ls], truth_weight(key, truth_scale));
   }
   __syncthreads();
-  if (t < spb && s0 + t < B) {
-    const float z = sdot[t] + truth_bias;
-    const float p = 1.f / (1.f + __expf(-z));
-    const uint64_t gs = (uint64_t)(sample_base + s0 + t);
-    labels[s0 + t] = u01(splitmix64(seed ^ 0xBEEF ^ (gs * 0x9E3779B97F4A7C15ull))) < p ? 1.f : 0.f;
-  }
+  if (t < spb && s0 + t < B)
+    labels[s0 + t] = gen_ctr_label(seed, (uint64_t)(sample_base + s0 + t), sdot[t] + truth_bias);
 }
 
 // Fused LR forward/backward over B samples x F features (CTR-style fixed
 // field count).  inv[j] indexes the pulled unique-key value/gradient rows.
-__global__ __launch_bounds__(256) void k_lr_fwd_bwd(const uint32_t* __restrict__ inv,
+__global__ __launch_bounds__(256) void k_lr_fwd_bwd_lds(const uint32_t* __restrict__ inv,
                                                     const float* __restrict__ xval,
                                                     const float* __restrict__ labels, int B, int F,
                                                     const float* __restrict__ uvals,
@@ -114,6 +139,42 @@ __global__ __launch_bounds__(256) void k_lr_fwd_bwd(const uint32_t* __restrict__
   __syncthreads();
   if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
   if (active && u != kInvalidU) atomicAdd(ugrad + u, sg[ls] * x);
+}
+
+// Same, one sample per lane group (F <= 64).
+__global__ __launch_bounds__(256) void k_lr_fwd_bwd(const uint32_t* __restrict__ inv,
+                                                    const float* __restrict__ xval,
+                                                    const float* __restrict__ labels, int B, int F,
+                                                    int L, const float* __restrict__ uvals,
+                                                    float* __restrict__ ugrad,
+                                                    float* __restrict__ loss_sum,
+                                                    float* __restrict__ pred) {
+  __shared__ float sloss[4];
+  const int t = threadIdx.x, f = t & (L - 1);
+  const long long s = (long long)blockIdx.x * (256 / L) + t / L;
+  const bool active = f < F && s < B;
+  const long long j = s * F + f;
+  uint32_t u = kInvalidU;
+  float x = 0.f, v = 0.f;
+  if (active) {
+    u = inv[j];
+    x = xval ? xval[j] : 1.f;
+    if (u != kInvalidU) v = uvals[u] * x;
+  }
+  const float z = group_sum(v, L);
+  float l = 0.f, g = 0.f;
+  if (s < B) {
+    const float y = labels[s];
+    const float p = 1.f / (1.f + __expf(-z));
+    g = p - y;
+    if (f == 0) {
+      if (pred) pred[s] = p;
+      l = fmaxf(z, 0.f) + __logf(1.f + __expf(-fabsf(z))) - y * z;
+    }
+  }
+  const float bl = block_sum_256(l, sloss);
+  if (t == 0 && loss_sum) ctr_addf(loss_sum, bl);
+  if (active && u != kInvalidU) atomicAdd(ugrad + u, g * x);
 }
 
 // Factorization machine (binary features) fused forward/backward.
@@ -211,12 +272,20 @@ void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long lon
                     float* labels, hipStream_t st) {
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("gen_ctr: F must be in [1,256]");
+  const double logV = log((double)vocab_per_field + 1.0);
+  if (F <= kGroupMaxF) {
+    const int L = group_lanes(F), spb = 256 / L;
+    hipLaunchKernelGGL(k_gen_ctr, dim3((B + spb - 1) / spb), dim3(256), 0, st, seed, sample_base,
+                       B, F, L, vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys,
+                       labels);
+    check_launch("k_gen_ctr");
+    return;
+  }
   const int spb = samples_per_block(F);
   const int blocks = (B + spb - 1) / spb;
-  hipLaunchKernelGGL(k_gen_ctr, dim3(blocks), dim3(256), 0, st, seed, sample_base, B, F,
-                     vocab_per_field, log((double)vocab_per_field + 1.0), tail_frac, truth_scale,
-                     truth_bias, keys, labels);
-  check_launch("k_gen_ctr");
+  hipLaunchKernelGGL(k_gen_ctr_lds, dim3(blocks), dim3(256), 0, st, seed, sample_base, B, F,
+                     vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels);
+  check_launch("k_gen_ctr_lds");
 }
 
 void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
@@ -224,11 +293,18 @@ void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labe
                        hipStream_t st) {
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("lr_fwd_bwd: F must be in [1,256]");
+  if (F <= kGroupMaxF) {
+    const int L = group_lanes(F), spb = 256 / L;
+    hipLaunchKernelGGL(k_lr_fwd_bwd, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, xval,
+                       labels, B, F, L, uvals, ugrad, loss_sum, pred);
+    check_launch("k_lr_fwd_bwd");
+    return;
+  }
   const int spb = samples_per_block(F);
   const int blocks = (B + spb - 1) / spb;
-  hipLaunchKernelGGL(k_lr_fwd_bwd, dim3(blocks), dim3(256), 0, st, inv, xval, labels, B, F, uvals,
-                     ugrad, loss_sum, pred);
-  check_launch("k_lr_fwd_bwd");
+  hipLaunchKernelGGL(k_lr_fwd_bwd_lds, dim3(blocks), dim3(256), 0, st, inv, xval, labels, B, F,
+                     uvals, ugrad, loss_sum, pred);
+  check_launch("k_lr_fwd_bwd_lds");
 }
 
 }  // namespace ss

@@ -23,6 +23,7 @@
 //     reduce     one workgroup per work item: LDS atomics into 8192
 //                accumulators, then one coalesced row-shaped atomicAdd per
 //                touched unique key (full-rate atomic shape, ~10 MB/step)
+#include "sample_group.h"
 #include "scan.h"
 #include "ss_device.h"
 #include "ss_launch.h"
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pl
 // either per occurrence (g*x COALESCED to g[j], the bin-plan reduce gathers
 // it) or per sample (g[s] = p - y, 4 B per sample; the bucketed reduce of
 // bdedup.hip gathers it L2-resident and multiplies by x itself)
-__global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ inv,
+__global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict__ inv,
                                                   const uint32_t* __restrict__ pos_of,
                                                   const uint32_t* __restrict__ luid,
                                                   const float* __restrict__ xval,
@@ -244,6 +245,50 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ i
   __syncthreads();
   if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
   if (active && !per_sample) gocc[j] = sg[ls] * x;
+}
+
+// Same contract, one sample per lane group (F <= 64, sample_group.h).
+__global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ inv,
+                                                  const uint32_t* __restrict__ pos_of,
+                                                  const uint32_t* __restrict__ luid,
+                                                  const float* __restrict__ xval,
+                                                  const float* __restrict__ labels, int B, int F,
+                                                  int L, const float* __restrict__ uvals,
+                                                  float* __restrict__ gocc, int per_sample,
+                                                  float* __restrict__ loss_sum,
+                                                  float* __restrict__ pred) {
+  __shared__ float sloss[4];
+  const int t = threadIdx.x, f = t & (L - 1);
+  const long long s = (long long)blockIdx.x * (256 / L) + t / L;
+  const bool active = f < F && s < B;
+  const long long j = s * F + f;
+  uint32_t u = kInvS;
+  float x = 0.f, v = 0.f;
+  if (active) {
+    if (pos_of) {  // bucketed dedup without a materialised inverse index
+      const uint32_t p = pos_of[j];
+      u = p == kInvS ? kInvS : luid[p];
+    } else {
+      u = inv[j];
+    }
+    x = xval ? xval[j] : 1.f;
+    if (u != kInvS) v = uvals[u] * x;
+  }
+  const float z = group_sum(v, L);
+  float l = 0.f, g = 0.f;
+  if (s < B) {
+    const float y = labels[s];
+    const float p = 1.f / (1.f + __expf(-z));
+    g = p - y;
+    if (f == 0) {
+      if (per_sample) gocc[s] = g;
+      if (pred) pred[s] = p;
+      l = fmaxf(z, 0.f) + __logf(1.f + __expf(-fabsf(z))) - y * z;
+    }
+  }
+  const float bl = block_sum_256(l, sloss);
+  if (t == 0 && loss_sum) ctr_addf(loss_sum, bl);
+  if (active && !per_sample) gocc[j] = g * x;
 }
 
 // -------------------------------------------------------------- launchers
@@ -301,11 +346,17 @@ void launch_lr_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t
   if (!inv && !(pos_of && luid)) throw_error("lr_fwd_g: need inv or (pos_of, luid)");
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("lr_fwd_g: F must be in [1,256]");
+  if (F <= kGroupMaxF) {
+    const int L = group_lanes(F), spb = 256 / L;
+    hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, pos_of, luid,
+                       xval, labels, B, F, L, uvals, gocc, per_sample, loss_sum, pred);
+    check_launch("k_lr_fwd_g");
+    return;
+  }
   const int spb = F >= 256 ? 1 : 256 / F;
-  hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, pos_of, luid,
-                     xval, labels, B,
-                     F, uvals, gocc, per_sample, loss_sum, pred);
-  check_launch("k_lr_fwd_g");
+  hipLaunchKernelGGL(k_lr_fwd_g_lds, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, pos_of,
+                     luid, xval, labels, B, F, uvals, gocc, per_sample, loss_sum, pred);
+  check_launch("k_lr_fwd_g_lds");
 }
 
 }  // namespace ss

@@ -208,10 +208,11 @@ def test_bucket_reduce_lr_matches_atomic_path(dev, nranks):
     np.testing.assert_allclose(l_b.sum().item(), l_at.sum().item(), rtol=1e-5)
 
 
-def test_lr_fwd_bwd_matches_torch(dev):
+@pytest.mark.parametrize("F", [39, 7, 64, 100])  # lane-group layout (<=64) and LDS fallback
+def test_lr_fwd_bwd_matches_torch(dev, F):
     from swiftsnails_amd._native import hip
 
-    B, F, U = 3000, 39, 5000
+    B, U = 3000, 5000
     rng = np.random.default_rng(9)
     inv = rng.integers(0, U, size=B * F).astype(np.int32)
     x = rng.standard_normal(B * F).astype(np.float32)
@@ -307,6 +308,23 @@ def test_gen_ctr_ranges(dev):
     k2 = torch.empty_like(keys)
     d.generate(0, 0, 1, k2, labels)
     assert torch.equal(keys, k2)  # deterministic
+
+
+@pytest.mark.parametrize("F", [39, 100])  # lane-group kernel and the LDS fallback
+def test_gen_ctr_matches_numpy_generator(dev, F):
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.models.ctr_data import gen_ctr_np
+
+    B, V = 2000, 1_000_003
+    keys = torch.empty(B * F, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, device=dev)
+    hip().gen_ctr(7, 12345, B, F, V, 0.1, 1.0, -1.0, keys.data_ptr(), labels.data_ptr(),
+                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    rk, rl = gen_ctr_np(7, 12345, B, F, V, 0.1, 1.0, -1.0)
+    # ids use fp64 exp on both sides: allow a rare last-ulp floor difference
+    assert (keys.cpu().numpy() == rk).mean() > 0.9999
+    assert (labels.cpu().numpy() == rl).mean() > 0.995  # sums differ in float order only
 
 
 def test_sparse_lr_trains_world1(dev):
