@@ -402,6 +402,56 @@ __global__ __launch_bounds__(1024) void k_bd_reduce(const uint32_t* __restrict__
   for (uint32_t l = threadIdx.x; l < nu; l += 1024) ugrad[base + l] = acc[l];
 }
 
+// K7 for FM rows [w | v_1..v_K]: per unique key u with occurrences in samples
+// S(u):  grad = [G0, G_f - v_uf * G0],  G0 = sum gs[s],  G_f = sum gss[s][f].
+// Columns are accumulated in LDS a few at a time (kFmCols per pass over the
+// bucket's occurrences, which are L2-resident), so any unique count up to the
+// 4096-slot table fits; each row is then stored once.
+static constexpr int kFmCols = 3;
+template <int DIM>
+__global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restrict__ bstart,
+                                                       const uint32_t* __restrict__ ubase,
+                                                       const uint32_t* __restrict__ unum,
+                                                       const uint32_t* __restrict__ pj,
+                                                       const uint32_t* __restrict__ luid,
+                                                       const float* __restrict__ gs,
+                                                       const float* __restrict__ gss, int F,
+                                                       const float* __restrict__ uvals,
+                                                       float* __restrict__ ugrad) {
+  constexpr int K = DIM - 1;
+  __shared__ float g0[kBdTS];
+  __shared__ float acc[kFmCols][kBdTS];
+  const int b = blockIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
+  for (int c0 = 0; c0 < K; c0 += kFmCols) {
+    for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
+      if (c0 == 0) g0[l] = 0.f;
+#pragma unroll
+      for (int c = 0; c < kFmCols; ++c) acc[c][l] = 0.f;
+    }
+    __syncthreads();
+    for (uint32_t p = p0 + threadIdx.x; p < p1; p += 1024) {
+      const uint32_t u = luid[p];
+      if (u == kBdInvalid) continue;
+      const uint32_t l = u - base, s = pj[p] / (uint32_t)F;
+      if (c0 == 0) atomicAdd(&g0[l], gs[s]);
+#pragma unroll
+      for (int c = 0; c < kFmCols; ++c)
+        if (c0 + c < K) atomicAdd(&acc[c][l], gss[(size_t)s * K + c0 + c]);
+    }
+    __syncthreads();
+    for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
+      const size_t r = (size_t)(base + l) * DIM;
+      const float G0 = g0[l];
+      if (c0 == 0) ugrad[r] = G0;
+#pragma unroll
+      for (int c = 0; c < kFmCols; ++c)
+        if (c0 + c < K) ugrad[r + 1 + c0 + c] = acc[c][l] - uvals[r + 1 + c0 + c] * G0;
+    }
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------- launchers
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                      uint32_t* scratch, unsigned long long* sync, uint32_t epoch, uint32_t* pj,
@@ -455,6 +505,29 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   hipLaunchKernelGGL(k_bd_reduce, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
                      S + L.unum, pj, luid, gs, xval, F, ugrad);
   check_launch("k_bd_reduce");
+}
+
+void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
+                         const uint32_t* luid, const float* gs, const float* gss, int F, int dim,
+                         const float* uvals, float* ugrad, hipStream_t st) {
+  if (n <= 0) return;
+  const BdLayout L = bd_layout(n, nranks);
+  const uint32_t* S = scratch;
+  switch (dim) {
+#define SS_BDFM_CASE(DD)                                                                       \
+  case DD:                                                                                     \
+    hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,          \
+                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);           \
+    break;
+    SS_BDFM_CASE(2)
+    SS_BDFM_CASE(5)
+    SS_BDFM_CASE(9)
+    SS_BDFM_CASE(17)
+#undef SS_BDFM_CASE
+    default:
+      throw_error("bd_reduce_fm: dim must be 1+K with K in {1,4,8,16}");
+  }
+  check_launch("k_bd_reduce_fm");
 }
 
 }  // namespace ss

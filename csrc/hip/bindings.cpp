@@ -225,6 +225,20 @@ PYBIND11_MODULE(_ss_hip, m) {
   }, py::arg("inv"), py::arg("xval"), py::arg("labels"), py::arg("B"), py::arg("F"),
      py::arg("uvals"), py::arg("g"), py::arg("per_sample"), py::arg("loss"), py::arg("pred"),
      py::arg("st"), py::arg("pos_of") = 0, py::arg("luid") = 0);
+  m.def("fm_fwd_g", [](uintptr_t inv, uintptr_t pos_of, uintptr_t luid, uintptr_t labels, int B,
+                       int F, int dim, uintptr_t uvals, uintptr_t gs, uintptr_t gss,
+                       uintptr_t loss, uintptr_t pred, uintptr_t st) {
+    launch_fm_fwd_g(P<const uint32_t>(inv), P<const uint32_t>(pos_of), P<const uint32_t>(luid),
+                    P<const float>(labels), B, F, dim, P<const float>(uvals), P<float>(gs),
+                    P<float>(gss), P<float>(loss), P<float>(pred), S(st));
+  });
+  m.def("bd_reduce_fm", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj,
+                           uintptr_t luid, uintptr_t gs, uintptr_t gss, int F, int dim,
+                           uintptr_t uvals, uintptr_t ugrad, uintptr_t st) {
+    launch_bd_reduce_fm(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
+                        P<const uint32_t>(luid), P<const float>(gs), P<const float>(gss), F, dim,
+                        P<const float>(uvals), P<float>(ugrad), S(st));
+  });
   m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
                          uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {
     launch_fm_fwd_bwd(P<const uint32_t>(inv), P<const float>(labels), B, F, dim,

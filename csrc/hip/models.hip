@@ -229,6 +229,97 @@ __global__ __launch_bounds__(256) void k_fm_fwd_bwd(const uint32_t* __restrict__
   }
 }
 
+// FM forward, one sample per lane group (F <= 64), no atomics: emits the
+// per-sample gradient factors instead of per-occurrence rows —
+//   gs[s] = p - y,  gss[s][f] = gs[s] * sum_i v_if
+// from which the per-key gradient is  [sum gs,  sum gss_f - v_f * sum gs]
+// summed over the key's occurrences (k_bd_reduce_fm in bdedup.hip does that
+// per dedup bucket in LDS and stores each unique row once).
+template <int DIM>
+__global__ __launch_bounds__(256) void k_fm_fwd_g(const uint32_t* __restrict__ inv,
+                                                  const uint32_t* __restrict__ pos_of,
+                                                  const uint32_t* __restrict__ luid,
+                                                  const float* __restrict__ labels, int B, int F,
+                                                  int L, const float* __restrict__ uvals,
+                                                  float* __restrict__ gs, float* __restrict__ gss,
+                                                  float* __restrict__ loss_sum,
+                                                  float* __restrict__ pred) {
+  constexpr int K = DIM - 1;
+  __shared__ float sloss[4];
+  const int t = threadIdx.x, f = t & (L - 1);
+  const long long s = (long long)blockIdx.x * (256 / L) + t / L;
+  const long long j = s * F + f;
+  float row[DIM];
+#pragma unroll
+  for (int d = 0; d < DIM; ++d) row[d] = 0.f;
+  if (f < F && s < B) {
+    uint32_t u;
+    if (pos_of) {
+      const uint32_t p = pos_of[j];
+      u = p == kInvalidU ? kInvalidU : luid[p];
+    } else {
+      u = inv[j];
+    }
+    if (u != kInvalidU) {
+      const float* r = uvals + (long long)u * DIM;
+#pragma unroll
+      for (int d = 0; d < DIM; ++d) row[d] = r[d];
+    }
+  }
+  float sq = 0.f;
+#pragma unroll
+  for (int k = 0; k < K; ++k) sq += row[1 + k] * row[1 + k];
+  float z = group_sum(row[0] - 0.5f * sq, L);
+  float ssum[K > 0 ? K : 1];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    ssum[k] = group_sum(row[1 + k], L);
+    z += 0.5f * ssum[k] * ssum[k];
+  }
+  float l = 0.f;
+  if (s < B) {
+    const float y = labels[s];
+    const float p = 1.f / (1.f + __expf(-z));
+    const float g = p - y;
+    if (f == 0) {
+      gs[s] = g;
+      if (pred) pred[s] = p;
+      l = fmaxf(z, 0.f) + __logf(1.f + __expf(-fabsf(z))) - y * z;
+    }
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (f == k) gss[s * K + k] = g * ssum[k];
+  }
+  const float bl = block_sum_256(l, sloss);
+  if (t == 0 && loss_sum) ctr_addf(loss_sum, bl);
+}
+
+void launch_fm_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t* luid,
+                     const float* labels, int B, int F, int dim, const float* uvals, float* gs,
+                     float* gss, float* loss_sum, float* pred, hipStream_t st) {
+  if (B <= 0) return;
+  if (F < 2 || F > kGroupMaxF) throw_error("fm_fwd_g: F must be in [2,64]");
+  if (!inv && !(pos_of && luid)) throw_error("fm_fwd_g: need inv or (pos_of, luid)");
+  const int L = group_lanes(F), spb = 256 / L;
+  if (L < dim - 1) throw_error("fm_fwd_g: needs F >= K lanes per sample");
+  const int blocks = (B + spb - 1) / spb;
+  switch (dim) {
+#define SS_FMG_CASE(DD)                                                                      \
+  case DD:                                                                                   \
+    hipLaunchKernelGGL(k_fm_fwd_g<DD>, dim3(blocks), dim3(256), 0, st, inv, pos_of, luid,     \
+                       labels, B, F, L, uvals, gs, gss, loss_sum, pred);                     \
+    break;
+    SS_FMG_CASE(2)
+    SS_FMG_CASE(5)
+    SS_FMG_CASE(9)
+    SS_FMG_CASE(17)
+#undef SS_FMG_CASE
+    default:
+      throw_error("fm_fwd_g: dim must be 1+K with K in {1,4,8,16}");
+  }
+  check_launch("k_fm_fwd_g");
+}
+
 void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, int dim,
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
                        hipStream_t st) {

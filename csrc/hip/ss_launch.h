@@ -65,6 +65,9 @@ void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labe
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
                        hipStream_t st);
 
+void launch_fm_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t* luid,
+                     const float* labels, int B, int F, int dim, const float* uvals, float* gs,
+                     float* gss, float* loss_sum, float* pred, hipStream_t st);
 void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, int dim,
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
                        hipStream_t st);
@@ -97,6 +100,10 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st);
+
+void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
+                         const uint32_t* luid, const float* gs, const float* gss, int F, int dim,
+                         const float* uvals, float* ugrad, hipStream_t st);
 
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);

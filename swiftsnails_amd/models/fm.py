@@ -49,6 +49,20 @@ class FMWorker(PipelinedWorker):
         B, F = data.batch_size, data.num_fields
         self.keys = [torch.empty(B * F, dtype=torch.int64, device=dev) for _ in range(engine.depth)]
         self.labels = [torch.empty(B, dtype=torch.float32, device=dev) for _ in range(engine.depth)]
+        # Atomic-free path (bucketed dedup, F <= 64): the forward emits per-sample
+        # factors (gs, gs * sum v) and one workgroup per dedup bucket builds each
+        # unique key's gradient row in LDS (bdedup.hip k_bd_reduce_fm).  Otherwise
+        # the fused kernel adds per-occurrence rows with float atomics.
+        K = engine.dim - 1
+        lanes = 1 << max(0, (F - 1).bit_length())
+        self.bucketed = (F <= 64 and lanes >= K and
+                         all(getattr(dd, "mode", None) == "bucket" for dd in engine.dedupers))
+        if self.bucketed:
+            for dd in engine.dedupers:
+                dd.zero_grad = False
+                dd.materialize_inv = False
+            self.gs = torch.empty(B, dtype=torch.float32, device=dev)
+            self.gss = torch.empty(B * K, dtype=torch.float32, device=dev)
 
     def _produce(self, step, slot, stream):
         self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
@@ -57,6 +71,16 @@ class FMWorker(PipelinedWorker):
 
     def _compute(self, rnd, slot, st):
         d = self.data
+        if self.bucketed:
+            h, o, dd = hip(), rnd.dd.owner, rnd.dd
+            h.fm_fwd_g(0, o.pos_of.data_ptr(), o.luid.data_ptr(), self.labels[slot].data_ptr(),
+                       d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
+                       self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
+            h.bd_reduce_fm(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
+                           o.luid.data_ptr(), self.gs.data_ptr(), self.gss.data_ptr(),
+                           d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
+                           rnd.ugrad.data_ptr(), st)
+            return
         hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                          rnd.ugrad.data_ptr(), self.loss_sum.data_ptr(), 0, st)

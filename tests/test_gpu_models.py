@@ -100,6 +100,48 @@ def test_fm_fwd_bwd_matches_reference(dev, dim):
     np.testing.assert_allclose(g.cpu().numpy().reshape(B, F, dim), gr, rtol=1e-3, atol=1e-5)
 
 
+@pytest.mark.parametrize("dim,nranks", [(9, 1), (5, 3), (17, 1)])
+def test_fm_bucket_reduce_matches_atomic_path(dev, dim, nranks):
+    """Atomic-free FM (lane-group forward + per-bucket LDS row reduction) ==
+    the per-occurrence atomic kernel, with heavy key duplication."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.dedup import Deduper
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    h = hip()
+    B, F = 6000, 20
+    n = B * F
+    rng = np.random.default_rng(dim + nranks)
+    keys = (rng.zipf(1.3, n) % 50000).astype(np.int64)
+    fm = HashFrag(nranks, 64).rank_map()
+    d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=dim,
+                device=dev, mode="bucket")
+    r = d(torch.from_numpy(keys).to(dev))
+    st = torch.cuda.current_stream().cuda_stream
+    U = nranks * d.ucap
+    uvals = torch.randn(U, dim, device=dev) * 0.1
+    y = torch.from_numpy((rng.random(B) < 0.4).astype(np.float32)).to(dev)
+    g_at = torch.zeros(U, dim, device=dev)
+    l_at = torch.zeros(256 * 32, device=dev)
+    h.fm_fwd_bwd(r.inv.data_ptr(), y.data_ptr(), B, F, dim, uvals.data_ptr(), g_at.data_ptr(),
+                 l_at.data_ptr(), 0, st)
+    gs = torch.empty(B, device=dev)
+    gss = torch.empty(B * (dim - 1), device=dev)
+    g_b = torch.full((U, dim), float("nan"), device=dev)
+    l_b = torch.zeros(256 * 32, device=dev)
+    h.fm_fwd_g(0, d.pos_of.data_ptr(), d.luid.data_ptr(), y.data_ptr(), B, F, dim,
+               uvals.data_ptr(), gs.data_ptr(), gss.data_ptr(), l_b.data_ptr(), 0, st)
+    h.bd_reduce_fm(n, nranks, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
+                   gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_b.data_ptr(), st)
+    torch.cuda.synchronize()
+    uc = r.ucount.cpu().numpy()
+    for q in range(nranks):
+        a, b = q * d.ucap, q * d.ucap + uc[q]
+        np.testing.assert_allclose(g_b[a:b].cpu().numpy(), g_at[a:b].cpu().numpy(), rtol=2e-3,
+                                   atol=2e-4)
+    np.testing.assert_allclose(l_b.sum().item(), l_at.sum().item(), rtol=1e-4)
+
+
 def test_fm_trains_world1(dev):
     from swiftsnails_amd.models.fm import FMWorker, fm_table_args
     from swiftsnails_amd.models.sparse_lr import CtrSynth
