@@ -21,22 +21,27 @@
 //              chunk-major ([nch][P], coalesced)
 //   2 colscan  per-bucket exclusive scan down the chunks + bucket totals
 //   3 bstart   bucket start offsets (one workgroup)
-//   4 scatter  bucket-ordered occurrence list pj[pos] = j, and pos_of[j]
-//   5 dedup    one workgroup per bucket: LDS hash insert, compaction, then a
-//              decoupled look-back over the destination's earlier buckets for
-//              the unique-id base (single pass, no extra scan launch); writes
-//              the send-segment keys, per-position unique ids and ucount[d]
-//   6 inverse  inv[j] = luid[pos_of[j]] (coalesced writes, gathered reads)
+//   4 scatter  bucket-ordered occurrence list pj[pos] = j; pos_of[j] and the
+//              bucket bkt[j] (both coalesced)
+//   5 dedup    one workgroup per bucket: LDS hash insert + compaction; writes
+//              bucket-local ids luid[pos], the bucket's keys (staged in its own
+//              occurrence range) and its unique count
+//   6 place    one workgroup per bucket: unique-id base = sum of the earlier
+//              buckets of the same destination (L2-resident, no serial scan,
+//              no inter-workgroup waiting), keys -> send segment, ucount[d]
+//   7 inverse  (optional) inv[j] = ubase[bkt[j]] + luid[pos_of[j]]; consumers
+//              that only need uid(j) read it through BdIndex instead
 //
 // Measured (profiles/): random 4-12 B stores cost ~5x their bytes in write
-// requests (partial 64 B lines from 8 L2s), so the design stores every
-// permuted array with as few random stores as possible (only pj) and turns the
-// rest into coalesced stores plus gathered loads.
+// requests (partial 64 B lines from 8 L2s), so only pj is stored permuted;
+// an earlier single-pass variant with a decoupled look-back for the unique-id
+// bases spent ~40% of each dedup workgroup's life waiting on predecessors.
 //
 // Bucket b = d * Pd + fastrange32(dedup_hash(key) >> 32, Pd) with
 // d = map[fmix64(key) % frag_num] (hashfrag.h:48-53).  Pd is chosen so a
 // bucket holds ~2048 occurrences; its unique count is then far below the
 // 4096-slot LDS table (overflow is detected and reported, never silent).
+#include "bdindex.h"
 #include "scan.h"
 #include "ss_device.h"
 #include "ss_launch.h"
@@ -174,7 +179,8 @@ __global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict_
                                                      const uint32_t* __restrict__ hist,
                                                      const uint32_t* __restrict__ bstart,
                                                      uint32_t* __restrict__ pj,
-                                                     uint32_t* __restrict__ pos_of) {
+                                                     uint32_t* __restrict__ pos_of,
+                                                     uint32_t* __restrict__ bkt) {
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
@@ -192,66 +198,40 @@ __global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict_
   for (int e = 0; e < kBdPer; ++e) {
     const long long j = base + e * 1024;
     if (e < per && j < n) {
-      uint32_t pos = kBdInvalid;
+      uint32_t pos = kBdInvalid, b = kBdInvalid;
       if (k[e] != kEmptyKey) {
-        pos = atomicAdd(&cur[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
+        b = bd_bucket(k[e], rs, (uint32_t)Pd);
+        pos = atomicAdd(&cur[b], 1u);
         pj[pos] = (uint32_t)j;
       }
       pos_of[j] = pos;
+      bkt[j] = b;
     }
   }
 }
 
-// look-back flag word: [epoch:30][state:2][value:32]; state 1 = bucket
-// aggregate, 2 = inclusive prefix within the destination
-__device__ __forceinline__ unsigned long long bd_flag(uint32_t epoch, uint32_t st, uint32_t v) {
-  return ((unsigned long long)(epoch & 0x3FFFFFFFu) << 34) | ((unsigned long long)st << 32) | v;
-}
-
-struct BdOut {
-  uint64_t* ukeys;
-  uint32_t* luid;
-  uint32_t* ubase;
-  uint32_t* unum;
-  unsigned long long* ucount;
-  float* ugrad;
-  int gdim;
-  long long ucap;
-};
-
-// 5. one workgroup per bucket (taken in start order from a ticket counter so
-//    the look-back only ever waits on workgroups that are already running)
+// 5. one workgroup per bucket: LDS hash dedup -> bucket-local unique ids
 __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ keys,
                                                    const uint32_t* __restrict__ pj,
-                                                   const uint32_t* __restrict__ bstart, int P,
-                                                   int Pd, uint32_t epoch,
-                                                   unsigned long long* __restrict__ flags,
-                                                   unsigned long long* __restrict__ ticket,
-                                                   BdOut out, uint32_t* __restrict__ err,
+                                                   const uint32_t* __restrict__ bstart,
+                                                   uint32_t* __restrict__ luid,
+                                                   uint64_t* __restrict__ bkeys,
+                                                   uint32_t* __restrict__ unum,
+                                                   uint32_t* __restrict__ err,
                                                    unsigned long long* __restrict__ dbg) {
-  // dbg (optional): per bucket 8 wall-clock stamps of the phases (profiling)
+  // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
-  if (dbg && t == 0) dbg[(long long)sb * 8 + (i)] = wall_clock64();
+  if (dbg && t == 0) dbg[(long long)b * 8 + (i)] = wall_clock64();
   __shared__ unsigned long long tab[kBdTS];
   __shared__ unsigned int lid[kBdTS];
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
-  __shared__ int sb;
-  __shared__ unsigned int sbase;
   __shared__ int bad;
-  const int t = threadIdx.x;
-  if (t == 0) {
-    const unsigned long long tk = atomicAdd(ticket, 1ull);
-    if (tk == (unsigned long long)P - 1) atomicExch(ticket, 0ull);  // every ticket taken
-    sb = (int)tk;
-    bad = 0;
-  }
+  const int t = threadIdx.x, b = blockIdx.x;
+  if (t == 0) bad = 0;
   for (int s = t; s < kBdTS; s += 1024) tab[s] = kEmptyKey;
-  __syncthreads();
-  BD_STAMP(0)
-  const int b = sb;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
-  // insert: the first kBdRegs occurrences of each thread keep their slot in
+  // the first kBdRegs occurrences of each thread keep their slot in
   // registers; a hot bucket's excess parks it in luid[] (rewritten below)
   uint32_t slot[kBdRegs];
   uint64_t kk[kBdRegs];
@@ -260,7 +240,8 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
     const uint32_t p = p0 + t + r * 1024;
     kk[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
   }
-  if (dbg && t == 0) dbg[(long long)sb * 8 + 1] = wall_clock64() + (kk[0] & 0);
+  __syncthreads();
+  BD_STAMP(0)
   auto insert = [&](uint64_t key) -> uint32_t {
     uint32_t s = (uint32_t)dedup_hash(key) & (kBdTS - 1);
     for (int k = 0; k < kBdTS; ++k) {
@@ -277,9 +258,9 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   };
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) slot[r] = kk[r] != kEmptyKey ? insert(kk[r]) : kBdInvalid;
-  for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) out.luid[p] = insert(keys[pj[p]]);
+  for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) luid[p] = insert(keys[pj[p]]);
   __syncthreads();
-  BD_STAMP(2)
+  BD_STAMP(1)
   // compaction in slot order: thread t owns slots [4t, 4t+4)
   constexpr int kPerT = kBdTS / 1024;
   unsigned int occ = 0;
@@ -289,88 +270,69 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
     const int s = t * kPerT + k;
-    if (tab[s] != kEmptyKey) lid[s] = o++;
-  }
-  // decoupled look-back within the destination's buckets, 64 predecessors
-  // per step (one flag per lane of wave 0)
-  __syncthreads();
-  BD_STAMP(3)
-  if (t < 64) {
-    const int d = b / Pd, first = d * Pd;
-    const uint32_t ep = epoch & 0x3FFFFFFFu;
-    if (t == 0)
-      __hip_atomic_store(&flags[b], bd_flag(epoch, b == first ? 2u : 1u, tot), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    unsigned int excl = 0;
-    int hi = b - 1;  // next predecessor to examine
-    while (hi >= first) {
-      const int q = hi - t;
-      unsigned long long f = 0;
-      uint32_t stt = 2;  // lanes past the destination start act as "inclusive 0"
-      if (q >= first) {
-        for (;;) {
-          f = __hip_atomic_load(&flags[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          stt = (uint32_t)(f >> 32) & 3u;
-          if ((uint32_t)(f >> 34) == ep && stt != 0) break;
-          __builtin_amdgcn_s_sleep(1);
-        }
-      }
-      // closest predecessor holding an inclusive prefix
-      const unsigned long long incl = __ballot(stt == 2u);
-      const int stop = incl ? __builtin_ctzll(incl) : 64;
-      unsigned int v = (t <= stop && q >= first) ? (uint32_t)f : 0u;
-      for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-      excl += v;
-      if (incl) break;
-      hi -= 64;
-    }
-    if (t == 0) {
-      if (b != first)
-        __hip_atomic_store(&flags[b], bd_flag(epoch, 2, excl + tot), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned int base = (unsigned int)((long long)d * out.ucap + excl);
-      sbase = base;
-      out.ubase[b] = base;
-      out.unum[b] = tot;
-      if (b == first + Pd - 1) out.ucount[d] = excl + tot;
-      if (bad) atomicOr(err, 1u);
-    }
-  }
-  __syncthreads();
-  BD_STAMP(4)
-  const unsigned int base = sbase;
-#pragma unroll
-  for (int k = 0; k < kPerT; ++k) {
-    const int s = t * kPerT + k;
     const unsigned long long v = tab[s];
-    if (v != kEmptyKey) out.ukeys[base + lid[s]] = v;
+    if (v != kEmptyKey) {
+      lid[s] = o;
+      bkeys[p0 + o] = v;  // staged in the bucket's own occurrence range
+      ++o;
+    }
   }
-  if (out.ugrad)
-    for (uint32_t e = t; e < tot * (uint32_t)out.gdim; e += 1024)
-      out.ugrad[(unsigned long long)base * out.gdim + e] = 0.f;
+  if (t == 0) {
+    unum[b] = tot;
+    if (bad) atomicOr(err, 1u);
+  }
+  __syncthreads();
+  BD_STAMP(2)
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
     const uint32_t p = p0 + t + r * 1024;
-    if (p < p1) out.luid[p] = slot[r] == kBdInvalid ? kBdInvalid : base + lid[slot[r]];
+    if (p < p1) luid[p] = slot[r] == kBdInvalid ? kBdInvalid : lid[slot[r]];
   }
   for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) {
-    const uint32_t s = out.luid[p];
-    out.luid[p] = s == kBdInvalid ? kBdInvalid : base + lid[s];
+    const uint32_t s = luid[p];
+    luid[p] = s == kBdInvalid ? kBdInvalid : lid[s];
   }
   __syncthreads();
-  BD_STAMP(5)
+  BD_STAMP(3)
 #undef BD_STAMP
 }
 
-// 6. inverse index in occurrence order
-__global__ __launch_bounds__(256) void k_bd_inv(const uint32_t* __restrict__ pos_of, long long n,
-                                                const uint32_t* __restrict__ luid,
+// 6. unique-id bases, send-segment keys, per-destination counts
+__global__ __launch_bounds__(256) void k_bd_place(const uint32_t* __restrict__ unum,
+                                                  const uint32_t* __restrict__ bstart, int Pd,
+                                                  long long ucap,
+                                                  const uint64_t* __restrict__ bkeys,
+                                                  uint64_t* __restrict__ ukeys,
+                                                  uint32_t* __restrict__ ubase,
+                                                  unsigned long long* __restrict__ ucount,
+                                                  float* __restrict__ ugrad, int gdim) {
+  __shared__ unsigned int ws[4];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const int d = b / Pd, first = d * Pd;
+  // base = sum of unum over [first, b): independent L2 loads, block reduce
+  unsigned int part = 0;
+  for (int q = first + t; q < b; q += 256) part += unum[q];
+  for (int o = 32; o > 0; o >>= 1) part += __shfl_down(part, o, 64);
+  if ((t & 63) == 0) ws[t >> 6] = part;
+  __syncthreads();
+  const unsigned int excl = ws[0] + ws[1] + ws[2] + ws[3];
+  const unsigned int nu = unum[b];
+  const unsigned long long base = (unsigned long long)d * ucap + excl;
+  if (t == 0) {
+    ubase[b] = (uint32_t)base;
+    if (b == first + Pd - 1) ucount[d] = excl + nu;
+  }
+  const uint32_t p0 = bstart[b];
+  for (uint32_t l = t; l < nu; l += 256) ukeys[base + l] = bkeys[p0 + l];
+  if (ugrad)
+    for (uint32_t e = t; e < nu * (uint32_t)gdim; e += 256) ugrad[base * gdim + e] = 0.f;
+}
+
+// 7. inverse index in occurrence order
+__global__ __launch_bounds__(256) void k_bd_inv(BdIndex ix, long long n,
                                                 uint32_t* __restrict__ inv) {
   const long long j = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (j < n) {
-    const uint32_t p = pos_of[j];
-    inv[j] = p == kBdInvalid ? kBdInvalid : luid[p];
-  }
+  if (j < n) inv[j] = ix.uid(j);
 }
 
 // K7 for scalar rows (sparse LR): one workgroup per bucket sums the gradients
@@ -391,11 +353,11 @@ __global__ __launch_bounds__(1024) void k_bd_reduce(const uint32_t* __restrict__
   for (uint32_t l = threadIdx.x; l < nu; l += 1024) acc[l] = 0.f;
   __syncthreads();
   for (uint32_t p = p0 + threadIdx.x; p < p1; p += 1024) {
-    const uint32_t u = luid[p];
-    if (u != kBdInvalid) {
+    const uint32_t l = luid[p];  // bucket-local unique id
+    if (l != kBdInvalid) {
       const uint32_t j = pj[p];
       const float g = gs[j / (uint32_t)F];
-      atomicAdd(&acc[u - base], xval ? g * xval[j] : g);
+      atomicAdd(&acc[l], xval ? g * xval[j] : g);
     }
   }
   __syncthreads();
@@ -431,9 +393,9 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
     }
     __syncthreads();
     for (uint32_t p = p0 + threadIdx.x; p < p1; p += 1024) {
-      const uint32_t u = luid[p];
-      if (u == kBdInvalid) continue;
-      const uint32_t l = u - base, s = pj[p] / (uint32_t)F;
+      const uint32_t l = luid[p];  // bucket-local unique id
+      if (l == kBdInvalid) continue;
+      const uint32_t s = pj[p] / (uint32_t)F;
       if (c0 == 0) atomicAdd(&g0[l], gs[s]);
 #pragma unroll
       for (int c = 0; c < kFmCols; ++c)
@@ -454,9 +416,9 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
 
 // ------------------------------------------------------------- launchers
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
-                     uint32_t* scratch, unsigned long long* sync, uint32_t epoch, uint32_t* pj,
-                     uint32_t* pos_of, uint32_t* luid, unsigned long long* ucount,
-                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
+                     uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
+                     uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
+                     float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
                      unsigned long long* dbg) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   if (n <= 0) {
@@ -480,20 +442,20 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   hipLaunchKernelGGL(k_bd_bstart, dim3(1), dim3(1024), 0, st, S + L.btot, L.P, S + L.bstart);
   check_launch("k_bd_bstart");
   hipLaunchKernelGGL(k_bd_scatter, dim3(L.nch), dim3(1024), lds, st, keys, n, rs, L.Pd, L.P,
-                     L.chunk, S + L.hist, S + L.bstart, pj, pos_of);
+                     L.chunk, S + L.hist, S + L.bstart, pj, pos_of, bkt);
   check_launch("k_bd_scatter");
-  BdOut o{ukeys, luid, S + L.ubase, S + L.unum, ucount, ugrad, gdim, ucap};
-  hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(1024), 0, st, keys, pj, S + L.bstart, L.P, L.Pd,
-                     epoch, sync, sync + kBdMaxBuckets + kMaxSeg, o, S, dbg);
+  hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(1024), 0, st, keys, pj, S + L.bstart, luid,
+                     bkeys, S + L.unum, S, dbg);
   check_launch("k_bd_dedup");
+  hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart, L.Pd,
+                     ucap, bkeys, ukeys, S + L.ubase, ucount, ugrad, gdim);
+  check_launch("k_bd_place");
   if (inv) {
-    hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, pos_of, n,
-                       luid, inv);
+    BdIndex ix{pos_of, luid, bkt, S + L.ubase};
+    hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, n, inv);
     check_launch("k_bd_inv");
   }
 }
-
-long long bd_sync_words() { return (long long)kBdMaxBuckets + kMaxSeg + 1; }
 
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,

@@ -45,6 +45,13 @@ static SegList make_seglist_dev(uintptr_t dev_count) {
 
 static long long seglist_total(const SegList& s) { return s.dev_count ? -1 : s.prefix[s.nseg]; }
 
+static BdIndex make_bdindex(const std::vector<uintptr_t>& v) {
+  if (v.empty()) return BdIndex{nullptr, nullptr, nullptr, nullptr};
+  if (v.size() != 4) throw std::runtime_error("BdIndex: need (pos_of, luid, bkt, ubase)");
+  return BdIndex{P<const uint32_t>(v[0]), P<const uint32_t>(v[1]), P<const uint32_t>(v[2]),
+                 P<const uint32_t>(v[3])};
+}
+
 PYBIND11_MODULE(_ss_hip, m) {
   m.doc() = "SwiftSnails-AMD gfx950 kernels + RCCL communicator";
 
@@ -144,22 +151,21 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("dedup_blocks", &dedup_blocks);
   m.def("bd_scratch_words", &bd_scratch_words);
-  m.def("bd_sync_words", &bd_sync_words);
+  m.def("bd_ubase_offset", &bd_ubase_offset);
   m.def("bd_buckets", &bd_buckets);
   m.def("bd_dedup", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num, int nranks,
-                       long long ucap, uintptr_t scratch, uintptr_t sync, uint32_t epoch,
-                       uintptr_t pj, uintptr_t pos_of, uintptr_t luid, uintptr_t ucount,
+                       long long ucap, uintptr_t scratch, uintptr_t pj, uintptr_t pos_of,
+                       uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, uintptr_t st,
                        uintptr_t dbg) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
-    launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch),
-                    P<unsigned long long>(sync), epoch, P<uint32_t>(pj), P<uint32_t>(pos_of),
-                    P<uint32_t>(luid), P<unsigned long long>(ucount), P<uint64_t>(ukeys),
-                    P<float>(ugrad), gdim, P<uint32_t>(inv), S(st),
-                    P<unsigned long long>(dbg));
+    launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
+                    P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
+                    P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
+                    P<uint32_t>(inv), S(st), P<unsigned long long>(dbg));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
-     py::arg("ucap"), py::arg("scratch"), py::arg("sync"), py::arg("epoch"), py::arg("pj"),
-     py::arg("pos_of"), py::arg("luid"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
+     py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
+     py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("st"), py::arg("dbg") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st) {
@@ -216,21 +222,22 @@ PYBIND11_MODULE(_ss_hip, m) {
                      P<const uint32_t>(nitems), n, P<const unsigned long long>(ucount), nranks,
                      ucap, P<float>(ugrad), S(st));
   });
+  // ix = (pos_of, luid, bkt, ubase) pointers of a bucketed dedup, or () with inv
   m.def("lr_fwd_g", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
                        uintptr_t uvals, uintptr_t g, int per_sample, uintptr_t loss,
-                       uintptr_t pred, uintptr_t st, uintptr_t pos_of, uintptr_t luid) {
-    launch_lr_fwd_g(P<const uint32_t>(inv), P<const uint32_t>(pos_of), P<const uint32_t>(luid),
-                    P<const float>(xval), P<const float>(labels), B, F, P<const float>(uvals),
-                    P<float>(g), per_sample, P<float>(loss), P<float>(pred), S(st));
+                       uintptr_t pred, uintptr_t st, std::vector<uintptr_t> ix) {
+    launch_lr_fwd_g(P<const uint32_t>(inv), make_bdindex(ix), P<const float>(xval),
+                    P<const float>(labels), B, F, P<const float>(uvals), P<float>(g), per_sample,
+                    P<float>(loss), P<float>(pred), S(st));
   }, py::arg("inv"), py::arg("xval"), py::arg("labels"), py::arg("B"), py::arg("F"),
      py::arg("uvals"), py::arg("g"), py::arg("per_sample"), py::arg("loss"), py::arg("pred"),
-     py::arg("st"), py::arg("pos_of") = 0, py::arg("luid") = 0);
-  m.def("fm_fwd_g", [](uintptr_t inv, uintptr_t pos_of, uintptr_t luid, uintptr_t labels, int B,
+     py::arg("st"), py::arg("ix") = std::vector<uintptr_t>{});
+  m.def("fm_fwd_g", [](uintptr_t inv, std::vector<uintptr_t> ix, uintptr_t labels, int B,
                        int F, int dim, uintptr_t uvals, uintptr_t gs, uintptr_t gss,
                        uintptr_t loss, uintptr_t pred, uintptr_t st) {
-    launch_fm_fwd_g(P<const uint32_t>(inv), P<const uint32_t>(pos_of), P<const uint32_t>(luid),
-                    P<const float>(labels), B, F, dim, P<const float>(uvals), P<float>(gs),
-                    P<float>(gss), P<float>(loss), P<float>(pred), S(st));
+    launch_fm_fwd_g(P<const uint32_t>(inv), make_bdindex(ix), P<const float>(labels), B, F, dim,
+                    P<const float>(uvals), P<float>(gs), P<float>(gss), P<float>(loss),
+                    P<float>(pred), S(st));
   });
   m.def("bd_reduce_fm", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj,
                            uintptr_t luid, uintptr_t gs, uintptr_t gss, int F, int dim,

@@ -236,9 +236,7 @@ __global__ __launch_bounds__(256) void k_fm_fwd_bwd(const uint32_t* __restrict__
 // summed over the key's occurrences (k_bd_reduce_fm in bdedup.hip does that
 // per dedup bucket in LDS and stores each unique row once).
 template <int DIM>
-__global__ __launch_bounds__(256) void k_fm_fwd_g(const uint32_t* __restrict__ inv,
-                                                  const uint32_t* __restrict__ pos_of,
-                                                  const uint32_t* __restrict__ luid,
+__global__ __launch_bounds__(256) void k_fm_fwd_g(const uint32_t* __restrict__ inv, BdIndex ix,
                                                   const float* __restrict__ labels, int B, int F,
                                                   int L, const float* __restrict__ uvals,
                                                   float* __restrict__ gs, float* __restrict__ gss,
@@ -253,13 +251,7 @@ __global__ __launch_bounds__(256) void k_fm_fwd_g(const uint32_t* __restrict__ i
 #pragma unroll
   for (int d = 0; d < DIM; ++d) row[d] = 0.f;
   if (f < F && s < B) {
-    uint32_t u;
-    if (pos_of) {
-      const uint32_t p = pos_of[j];
-      u = p == kInvalidU ? kInvalidU : luid[p];
-    } else {
-      u = inv[j];
-    }
+    const uint32_t u = inv ? inv[j] : ix.uid(j);
     if (u != kInvalidU) {
       const float* r = uvals + (long long)u * DIM;
 #pragma unroll
@@ -294,20 +286,21 @@ __global__ __launch_bounds__(256) void k_fm_fwd_g(const uint32_t* __restrict__ i
   if (t == 0 && loss_sum) ctr_addf(loss_sum, bl);
 }
 
-void launch_fm_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t* luid,
-                     const float* labels, int B, int F, int dim, const float* uvals, float* gs,
-                     float* gss, float* loss_sum, float* pred, hipStream_t st) {
+void launch_fm_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* labels, int B, int F,
+                     int dim, const float* uvals, float* gs, float* gss, float* loss_sum,
+                     float* pred, hipStream_t st) {
   if (B <= 0) return;
   if (F < 2 || F > kGroupMaxF) throw_error("fm_fwd_g: F must be in [2,64]");
-  if (!inv && !(pos_of && luid)) throw_error("fm_fwd_g: need inv or (pos_of, luid)");
+  if (!inv && !(ix.pos_of && ix.luid && ix.bkt && ix.ubase))
+    throw_error("fm_fwd_g: need inv or a complete BdIndex");
   const int L = group_lanes(F), spb = 256 / L;
   if (L < dim - 1) throw_error("fm_fwd_g: needs F >= K lanes per sample");
   const int blocks = (B + spb - 1) / spb;
   switch (dim) {
 #define SS_FMG_CASE(DD)                                                                      \
   case DD:                                                                                   \
-    hipLaunchKernelGGL(k_fm_fwd_g<DD>, dim3(blocks), dim3(256), 0, st, inv, pos_of, luid,     \
-                       labels, B, F, L, uvals, gs, gss, loss_sum, pred);                     \
+    hipLaunchKernelGGL(k_fm_fwd_g<DD>, dim3(blocks), dim3(256), 0, st, inv, ix, labels, B, F, \
+                       L, uvals, gs, gss, loss_sum, pred);                                   \
     break;
     SS_FMG_CASE(2)
     SS_FMG_CASE(5)

@@ -199,8 +199,7 @@ __global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pl
 // it) or per sample (g[s] = p - y, 4 B per sample; the bucketed reduce of
 // bdedup.hip gathers it L2-resident and multiplies by x itself)
 __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict__ inv,
-                                                  const uint32_t* __restrict__ pos_of,
-                                                  const uint32_t* __restrict__ luid,
+                                                  BdIndex ix,
                                                   const float* __restrict__ xval,
                                                   const float* __restrict__ labels, int B, int F,
                                                   const float* __restrict__ uvals,
@@ -220,12 +219,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict
   uint32_t u = kInvS;
   float x = 0.f;
   if (active) {
-    if (pos_of) {  // bucketed dedup without a materialised inverse index
-      const uint32_t p = pos_of[j];
-      u = p == kInvS ? kInvS : luid[p];
-    } else {
-      u = inv[j];
-    }
+    u = inv ? inv[j] : ix.uid(j);  // bucketed dedup: no materialised inverse index
     x = xval ? xval[j] : 1.f;
     if (u != kInvS) atomicAdd(&sdot[ls], uvals[u] * x);
   }
@@ -249,8 +243,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict
 
 // Same contract, one sample per lane group (F <= 64, sample_group.h).
 __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ inv,
-                                                  const uint32_t* __restrict__ pos_of,
-                                                  const uint32_t* __restrict__ luid,
+                                                  BdIndex ix,
                                                   const float* __restrict__ xval,
                                                   const float* __restrict__ labels, int B, int F,
                                                   int L, const float* __restrict__ uvals,
@@ -265,12 +258,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ i
   uint32_t u = kInvS;
   float x = 0.f, v = 0.f;
   if (active) {
-    if (pos_of) {  // bucketed dedup without a materialised inverse index
-      const uint32_t p = pos_of[j];
-      u = p == kInvS ? kInvS : luid[p];
-    } else {
-      u = inv[j];
-    }
+    u = inv ? inv[j] : ix.uid(j);  // bucketed dedup: no materialised inverse index
     x = xval ? xval[j] : 1.f;
     if (u != kInvS) v = uvals[u] * x;
   }
@@ -340,22 +328,23 @@ void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
   check_launch("k_sr_reduce");
 }
 
-void launch_lr_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t* luid,
-                     const float* xval, const float* labels, int B, int F, const float* uvals,
-                     float* gocc, int per_sample, float* loss_sum, float* pred, hipStream_t st) {
-  if (!inv && !(pos_of && luid)) throw_error("lr_fwd_g: need inv or (pos_of, luid)");
+void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
+                     const float* labels, int B, int F, const float* uvals, float* gocc,
+                     int per_sample, float* loss_sum, float* pred, hipStream_t st) {
+  if (!inv && !(ix.pos_of && ix.luid && ix.bkt && ix.ubase))
+    throw_error("lr_fwd_g: need inv or a complete BdIndex");
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("lr_fwd_g: F must be in [1,256]");
   if (F <= kGroupMaxF) {
     const int L = group_lanes(F), spb = 256 / L;
-    hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, pos_of, luid,
-                       xval, labels, B, F, L, uvals, gocc, per_sample, loss_sum, pred);
+    hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, ix, xval,
+                       labels, B, F, L, uvals, gocc, per_sample, loss_sum, pred);
     check_launch("k_lr_fwd_g");
     return;
   }
   const int spb = F >= 256 ? 1 : 256 / F;
-  hipLaunchKernelGGL(k_lr_fwd_g_lds, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, pos_of,
-                     luid, xval, labels, B, F, uvals, gocc, per_sample, loss_sum, pred);
+  hipLaunchKernelGGL(k_lr_fwd_g_lds, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, ix, xval,
+                     labels, B, F, uvals, gocc, per_sample, loss_sum, pred);
   check_launch("k_lr_fwd_g_lds");
 }
 

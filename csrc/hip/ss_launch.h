@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include "bdindex.h"
 #include "ss_device.h"
 
 namespace ss {
@@ -65,8 +66,7 @@ void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labe
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
                        hipStream_t st);
 
-void launch_fm_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t* luid,
-                     const float* labels, int B, int F, int dim, const float* uvals, float* gs,
+void launch_fm_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* labels, int B, int F, int dim, const float* uvals, float* gs,
                      float* gss, float* loss_sum, float* pred, hipStream_t st);
 void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, int dim,
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
@@ -84,18 +84,17 @@ void launch_sr_plan(const uint32_t* inv, long long n, const unsigned long long* 
 void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
                       const uint32_t* nitems, long long n, const unsigned long long* ucount,
                       int nranks, long long ucap, float* ugrad, hipStream_t st);
-void launch_lr_fwd_g(const uint32_t* inv, const uint32_t* pos_of, const uint32_t* luid,
-                     const float* xval, const float* labels, int B, int F, const float* uvals,
+void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval, const float* labels, int B, int F, const float* uvals,
                      float* g, int per_sample, float* loss_sum, float* pred, hipStream_t st);
 
 // --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
 long long bd_scratch_words(long long n, int nranks);
-long long bd_sync_words();
+long long bd_ubase_offset(long long n, int nranks);
 int bd_buckets(long long n, int nranks);
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
-                     uint32_t* scratch, unsigned long long* sync, uint32_t epoch, uint32_t* pj,
-                     uint32_t* pos_of, uint32_t* luid, unsigned long long* ucount,
-                     uint64_t* ukeys, float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
+                     uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
+                     uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
+                     float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
                      unsigned long long* dbg = nullptr);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,

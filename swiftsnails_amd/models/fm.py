@@ -73,7 +73,7 @@ class FMWorker(PipelinedWorker):
         d = self.data
         if self.bucketed:
             h, o, dd = hip(), rnd.dd.owner, rnd.dd
-            h.fm_fwd_g(0, o.pos_of.data_ptr(), o.luid.data_ptr(), self.labels[slot].data_ptr(),
+            h.fm_fwd_g(0, o.index_ptrs(dd.n), self.labels[slot].data_ptr(),
                        d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                        self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
             h.bd_reduce_fm(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),

@@ -86,7 +86,7 @@ class SparseLRWorker(PipelinedWorker):
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False        # the LDS reduce stores every unique row
-                dd.materialize_inv = False  # the forward reads luid[pos_of[j]] itself
+                dd.materialize_inv = False  # the forward resolves uid(j) itself (BdIndex)
         elif grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
@@ -133,8 +133,7 @@ class SparseLRWorker(PipelinedWorker):
             if self.bucketed:
                 h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
                            rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
-                           self.loss_sum.data_ptr(), 0, st, o.pos_of.data_ptr(),
-                           o.luid.data_ptr())
+                           self.loss_sum.data_ptr(), 0, st, o.index_ptrs(dd.n))
             else:
                 h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
                            d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 0,

@@ -95,12 +95,12 @@ class Deduper:
             # word 0 of the scratch is the sticky overflow flag (zeroed once)
             self.scratch = torch.zeros(self.h.bd_scratch_words(m, self.nranks),
                                        dtype=torch.int32, device=d)
-            # look-back flags + ticket; flags carry a per-call epoch (no reset)
-            self.sync = torch.zeros(self.h.bd_sync_words(), dtype=torch.int64, device=d)
-            self.epoch = 0
-            self.pj = torch.empty(m, dtype=torch.int32, device=d)
-            self.pos_of = torch.empty(m, dtype=torch.int32, device=d)
-            self.luid = torch.empty(m, dtype=torch.int32, device=d)
+            self.pj = torch.empty(m, dtype=torch.int32, device=d)      # bucket order -> j
+            self.pos_of = torch.empty(m, dtype=torch.int32, device=d)  # j -> bucket order
+            self.bkt = torch.empty(m, dtype=torch.int32, device=d)     # j -> bucket
+            self.luid = torch.empty(m, dtype=torch.int32, device=d)    # bucket-local ids
+            self.bkeys = torch.empty(m, dtype=torch.int64, device=d)   # staged unique keys
+            self._last_n = 0
             # SS_BD_DEBUG=1: per-bucket phase timestamps of the dedup kernel
             self.dbg = (torch.zeros(8 * self.h.bd_buckets(m, self.nranks), dtype=torch.int64,
                                     device=d) if os.environ.get("SS_BD_DEBUG") else None)
@@ -117,11 +117,11 @@ class Deduper:
         st = _stream_ptr(stream)
         ug = self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0
         if self.mode == "bucket":
-            self.epoch = self.epoch % 0x3FFFFFFF + 1
+            self._last_n = n
             self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
-                            self.nranks, self.ucap, self.scratch.data_ptr(),
-                            self.sync.data_ptr(), self.epoch, self.pj.data_ptr(),
-                            self.pos_of.data_ptr(), self.luid.data_ptr(), self.ucount.data_ptr(),
+                            self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
+                            self.pos_of.data_ptr(), self.bkt.data_ptr(), self.luid.data_ptr(),
+                            self.bkeys.data_ptr(), self.ucount.data_ptr(),
                             self.ukeys.data_ptr(), ug, self.gdim,
                             self.inv.data_ptr() if self.materialize_inv else 0, st,
                             self.dbg.data_ptr() if self.dbg is not None else 0)
@@ -151,6 +151,15 @@ class Deduper:
                          self.luid.data_ptr(), gs.data_ptr(),
                          xval.data_ptr() if xval is not None else 0, F, ugrad.data_ptr(),
                          _stream_ptr(stream))
+
+    def index_ptrs(self, n: Optional[int] = None):
+        """(pos_of, luid, bkt, ubase) device pointers of the last call: the
+        kernels' BdIndex, uid(j) = ubase[bkt[j]] + luid[pos_of[j]]."""
+        if self.mode != "bucket":
+            raise RuntimeError("index_ptrs needs mode='bucket'")
+        n = self._last_n if n is None else n
+        ub = self.scratch.data_ptr() + 4 * self.h.bd_ubase_offset(max(1, n), self.nranks)
+        return [self.pos_of.data_ptr(), self.luid.data_ptr(), self.bkt.data_ptr(), ub]
 
     def check(self):
         """Raise if any bucket overflowed its LDS table (sticky; syncs)."""

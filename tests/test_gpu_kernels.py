@@ -198,7 +198,12 @@ def test_bucket_reduce_lr_matches_atomic_path(dev, nranks):
     h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gs.data_ptr(), 1,
                l_b.data_ptr(), 0, st)
     d.reduce(n, gs, F, g_b)
+    # the same forward through the BdIndex (no inverse index) gives the same gradients
+    gs2 = torch.empty(B, device=dev)
+    h.lr_fwd_g(0, 0, y.data_ptr(), B, F, uvals.data_ptr(), gs2.data_ptr(), 1, 0, 0, st,
+               d.index_ptrs(n))
     torch.cuda.synchronize()
+    assert torch.equal(gs, gs2)
     d.check()
     uc = r.ucount.cpu().numpy()
     for q in range(nranks):

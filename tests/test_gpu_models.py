@@ -129,7 +129,7 @@ def test_fm_bucket_reduce_matches_atomic_path(dev, dim, nranks):
     gss = torch.empty(B * (dim - 1), device=dev)
     g_b = torch.full((U, dim), float("nan"), device=dev)
     l_b = torch.zeros(256 * 32, device=dev)
-    h.fm_fwd_g(0, d.pos_of.data_ptr(), d.luid.data_ptr(), y.data_ptr(), B, F, dim,
+    h.fm_fwd_g(0, d.index_ptrs(n), y.data_ptr(), B, F, dim,
                uvals.data_ptr(), gs.data_ptr(), gss.data_ptr(), l_b.data_ptr(), 0, st)
     h.bd_reduce_fm(n, nranks, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
                    gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_b.data_ptr(), st)

@@ -69,14 +69,14 @@ def main():
             if mode == "bucket" and d.dbg is not None:
                 d(k)
                 torch.cuda.synchronize()
-                ts = d.dbg.view(-1, 8)[:, :6].cpu().numpy().astype(np.float64) * 0.01  # 100 MHz
+                ts = d.dbg.view(-1, 8)[:, :4].cpu().numpy().astype(np.float64) * 0.01  # 100 MHz
                 t0 = ts[:, 0].min()
                 ph = np.diff(ts, axis=1)
                 print("   phases us (mean/p50/max): " + "  ".join(
                     f"{nm}={ph[:, i].mean():.1f}/{np.median(ph[:, i]):.1f}/{ph[:, i].max():.1f}"
-                    for i, nm in enumerate(["load", "insert", "compact", "lookback", "write"])))
+                    for i, nm in enumerate(["insert", "compact", "write"])))
                 st = ts[:, 0] - t0
-                en = ts[:, 5] - t0
+                en = ts[:, 3] - t0
                 print(f"   block start spread: {st.min():.1f}..{st.max():.1f} us, "
                       f"end max {en.max():.1f} us, mean lifetime {(en - st).mean():.1f} us")
 
