@@ -41,6 +41,8 @@
 // d = map[fmix64(key) % frag_num] (hashfrag.h:48-53).  Pd is chosen so a
 // bucket holds ~2048 occurrences; its unique count is then far below the
 // 4096-slot LDS table (overflow is detected and reported, never silent).
+#include <algorithm>
+
 #include "bdindex.h"
 #include "scan.h"
 #include "ss_device.h"
@@ -71,7 +73,9 @@ struct BdLayout {
 
 static BdLayout bd_layout(long long n, int nranks) {
   BdLayout L{};
-  long long target = kBdTarget;
+  // ~2048 occurrences per bucket, but at least ~1024 buckets for small calls
+  // (>= 4 workgroups per CU; a word2vec step of 196K keys got only 96 buckets)
+  long long target = std::min<long long>(kBdTarget, std::max<long long>(128, n / 1024));
   if (n > (long long)kBdMaxBuckets * kBdTarget) target = (n + kBdMaxBuckets - 1) / kBdMaxBuckets;
   long long pd = (n + (long long)nranks * target - 1) / ((long long)nranks * target);
   if (pd < 1) pd = 1;
@@ -258,7 +262,21 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   };
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) slot[r] = kk[r] != kEmptyKey ? insert(kk[r]) : kBdInvalid;
-  for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) luid[p] = insert(keys[pj[p]]);
+  // hot buckets (Zipf heads): the excess in rounds of kBdRegs occurrences per
+  // thread, all loads of a round in flight together; slots park in luid[]
+  for (uint32_t q = p0 + t + kBdRegs * 1024; q < p1; q += kBdRegs * 1024) {
+    uint64_t k2[kBdRegs];
+#pragma unroll
+    for (int r = 0; r < kBdRegs; ++r) {
+      const uint32_t p = q + r * 1024;
+      k2[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
+    }
+#pragma unroll
+    for (int r = 0; r < kBdRegs; ++r) {
+      const uint32_t p = q + r * 1024;
+      if (p < p1) luid[p] = k2[r] != kEmptyKey ? insert(k2[r]) : kBdInvalid;
+    }
+  }
   __syncthreads();
   BD_STAMP(1)
   // compaction in slot order: thread t owns slots [4t, 4t+4)

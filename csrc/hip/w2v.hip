@@ -29,6 +29,7 @@ namespace ss {
 static constexpr uint32_t kInv = 0xFFFFFFFFu;
 static constexpr int kT = 64;  // centers per tile
 static constexpr int kS = 64;  // shared negatives per tile
+static constexpr int kMaxC = 16;  // contexts per center held in registers (window <= 8)
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float softplus(float x) {
@@ -89,22 +90,56 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
       if (ok) loss += neg_scale * softplus(s);
     }
   }
-  // ---- positive pairs: wave w owns centers [16w, 16w+16)
-  for (int t = w * 16; t < w * 16 + 16; ++t) {
-    if (rc[t] == kInv) continue;  // wave-uniform
-    for (int j = 0; j < C; ++j) {
-      const uint32_t x = inv_x[(t0 + t) * (long long)C + j];
-      if (x == kInv) continue;
-      const float* u = uvals + (long long)x * D;
-      float part = 0.f;
-      for (int d = lane; d < D; d += 64) part += Vs[t * P + d] * u[d];
-      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-      const float g = sigm(part) - 1.f;  // d/ds softplus(-s)
-      if (lane == 0) loss += softplus(-part);
-      float* gu = ugrad + (long long)x * D;
-      for (int d = lane; d < D; d += 64) {
-        atomicAdd(gu + d, g * Vs[t * P + d]);
-        Gv[t * P + d] += g * u[d];
+  // ---- positive pairs: wave w owns centers [16w, 16w+16).  All C context
+  // rows of a center are loaded before any is used (one memory round trip
+  // per center instead of one per pair: the first version's per-pair loads
+  // made this loop the kernel's latency chain, 160 dependent loads per wave).
+  {
+    constexpr int R = (D + 63) / 64;  // row floats per lane
+    for (int t = w * 16; t < w * 16 + 16; ++t) {
+      if (rc[t] == kInv) continue;  // wave-uniform
+      const uint32_t xid = lane < C ? inv_x[(t0 + t) * (long long)C + lane] : kInv;
+      float u[kMaxC][R];
+#pragma unroll
+      for (int j = 0; j < kMaxC; ++j) {
+        const uint32_t x = __shfl(xid, j, 64);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          u[j][r] = (j < C && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
+        }
+      }
+      float v[R], gv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        v[r] = d < D ? Vs[t * P + d] : 0.f;
+        gv[r] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kMaxC; ++j) {
+        const uint32_t x = __shfl(xid, j, 64);
+        if (j >= C || x == kInv) continue;  // wave-uniform
+        float part = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) part += v[r] * u[j][r];
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        const float g = sigm(part) - 1.f;  // d/ds softplus(-s)
+        if (lane == 0) loss += softplus(-part);
+        float* gu = ugrad + (long long)x * D;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          if (d < D) {
+            atomicAdd(gu + d, g * v[r]);
+            gv[r] += g * u[j][r];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        if (d < D) Gv[t * P + d] += gv[r];
       }
     }
   }
@@ -190,6 +225,7 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
                      float* loss_sum, hipStream_t st) {
   if (B <= 0) return;
+  if (C < 1 || C > kMaxC) throw_error("w2v_sgns: contexts per center must be in [1,16]");
   const int tiles = (B + kT - 1) / kT;
   const size_t sm = w2v_smem_bytes(D);
   switch (D) {
