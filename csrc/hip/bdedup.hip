@@ -52,10 +52,12 @@ namespace ss {
 
 static constexpr uint32_t kBdInvalid = 0xFFFFFFFFu;
 static constexpr int kBdMaxChunk = 8192;  // occurrences per count/scatter workgroup
-static constexpr int kBdPer = kBdMaxChunk / 1024;
+static constexpr int kBdCT = 256;         // count/scatter workgroup size
+static constexpr int kBdPer = kBdMaxChunk / kBdCT;
+static constexpr int kBdDT = 512;         // dedup workgroup size
 static constexpr int kBdTarget = 2048;  // target occurrences per bucket
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
-static constexpr int kBdRegs = 4;       // occurrences per thread kept in registers
+static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
 
 __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs, uint32_t Pd) {
@@ -68,7 +70,7 @@ __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs,
 // ---- layout of the int scratch (u32 words), a function of (n, nranks) only
 struct BdLayout {
   int P, Pd, nch, chunk;
-  long long hist, btot, bstart, ubase, unum, total;
+  long long hist, btot, bstart, ubase, unum, ctr, total;
 };
 
 static BdLayout bd_layout(long long n, int nranks) {
@@ -84,10 +86,14 @@ static BdLayout bd_layout(long long n, int nranks) {
   // chunk count a multiple of the 256 CUs (balanced waves), chunk <= 8192
   const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
   const long long per = (n + 256 * waves - 1) / (256 * waves);
-  L.chunk = (int)(((per + 1023) / 1024) * 1024);
+  L.chunk = (int)(((per + kBdCT - 1) / kBdCT) * kBdCT);
   L.nch = (int)((n + L.chunk - 1) / L.chunk);
   if (L.nch < 1) L.nch = 1;
-  long long o = 1;  // word 0: sticky error flag (fixed position for any n)
+  // words 0, 1: sticky error flag and the colscan arrival counter, at fixed
+  // positions for any n (the scratch is sized for the largest call and
+  // zeroed once; every other word is rewritten by each call)
+  long long o = 2;
+  L.ctr = 1;
   L.hist = o; o += (long long)L.P * L.nch;
   L.btot = o; o += L.P;
   L.bstart = o; o += L.P + 1;
@@ -105,19 +111,21 @@ long long bd_ubase_offset(long long n, int nranks) {
   return bd_layout(n < 1 ? 1 : n, nranks).ubase;
 }
 
-// 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output
-__global__ __launch_bounds__(1024) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
-                                                   RouteSpec rs, int Pd, int P, int chunk,
-                                                   uint32_t* __restrict__ hist) {
+// 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output.
+// 256-thread workgroups: the route stream runs beside the compute stream's
+// kernels, and small workgroups find free CU slots where 1024-thread ones wait
+__global__ __launch_bounds__(kBdCT) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
+                                                    RouteSpec rs, int Pd, int P, int chunk,
+                                                    uint32_t* __restrict__ hist) {
   extern __shared__ unsigned int h[];
-  for (int b = threadIdx.x; b < P; b += 1024) h[b] = 0u;
+  for (int b = threadIdx.x; b < P; b += kBdCT) h[b] = 0u;
   __syncthreads();
   const long long base = (long long)blockIdx.x * chunk + threadIdx.x;
-  const int per = chunk >> 10;
+  const int per = chunk / kBdCT;
   uint64_t k[kBdPer];
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
-    const long long j = base + e * 1024;
+    const long long j = base + e * kBdCT;
     k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
   }
 #pragma unroll
@@ -125,14 +133,21 @@ __global__ __launch_bounds__(1024) void k_bd_count(const uint64_t* __restrict__ 
     if (k[e] != kEmptyKey) atomicAdd(&h[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
   __syncthreads();
   uint32_t* row = hist + (long long)blockIdx.x * P;
-  for (int b = threadIdx.x; b < P; b += 1024) row[b] = h[b];
+  for (int b = threadIdx.x; b < P; b += kBdCT) row[b] = h[b];
 }
 
-// 2. column scan of the [nch][P] histogram: 64 buckets x 16 chunk segments
-//    per workgroup; two passes of independent loads, no serial chain
+// 2+3. column scan of the [nch][P] histogram (64 buckets x 16 chunk segments
+//    per workgroup, two passes of independent loads, no serial chain); the
+//    LAST workgroup to finish (arrival counter) also scans the bucket totals
+//    into bucket start offsets — no separate single-workgroup launch
 __global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist, int nch, int P,
-                                                     uint32_t* __restrict__ btot) {
+                                                     uint32_t* __restrict__ btot,
+                                                     uint32_t* __restrict__ bstart,
+                                                     unsigned int* __restrict__ ctr) {
   __shared__ unsigned int ss[16][64];
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned int tot;
+  __shared__ bool last;
   const int col = threadIdx.x & 63, seg = threadIdx.x >> 6;
   const int b = blockIdx.x * 64 + col;
   const int R = (nch + 15) / 16;
@@ -156,29 +171,33 @@ __global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist
     }
     if (seg == 15) btot[b] = off;
   }
-}
-
-// 3. exclusive scan of bucket totals -> bucket start offsets (P <= ~16K)
-__global__ __launch_bounds__(1024) void k_bd_bstart(const uint32_t* __restrict__ btot, int P,
-                                                    uint32_t* __restrict__ bstart) {
-  __shared__ unsigned int wsum[16];
-  __shared__ unsigned int tot;
+  // publish btot (release), count arrivals; the last arriver acquires and scans
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;  // workgroup-uniform
+  __threadfence();
   const int per = (P + 1023) / 1024;
   const int b0 = threadIdx.x * per;
-  unsigned int s = 0;
+  unsigned int sum = 0;
   for (int k = 0; k < per; ++k)
-    if (b0 + k < P) s += btot[b0 + k];
-  unsigned int e = block_excl_scan_1024(s, wsum, &tot);
+    if (b0 + k < P)
+      sum += __hip_atomic_load(&btot[b0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned int e = block_excl_scan<16>(sum, wsum, &tot);
   for (int k = 0; k < per; ++k)
     if (b0 + k < P) {
       bstart[b0 + k] = e;
-      e += btot[b0 + k];
+      e += __hip_atomic_load(&btot[b0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  if (threadIdx.x == 0) bstart[P] = tot;
+  if (threadIdx.x == 0) {
+    bstart[P] = tot;
+    *ctr = 0u;  // ready for the next call (stream-ordered)
+  }
 }
 
 // 4. bucket-ordered occurrence list (dynamic LDS: P words)
-__global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict__ keys, long long n,
+__global__ __launch_bounds__(kBdCT) void k_bd_scatter(const uint64_t* __restrict__ keys, long long n,
                                                      RouteSpec rs, int Pd, int P, int chunk,
                                                      const uint32_t* __restrict__ hist,
                                                      const uint32_t* __restrict__ bstart,
@@ -188,19 +207,19 @@ __global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict_
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
-  for (int b = threadIdx.x; b < P; b += 1024) cur[b] = bstart[b] + row[b];
+  for (int b = threadIdx.x; b < P; b += kBdCT) cur[b] = bstart[b] + row[b];
   const long long base = (long long)c * chunk + threadIdx.x;
-  const int per = chunk >> 10;
+  const int per = chunk / kBdCT;
   uint64_t k[kBdPer];
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
-    const long long j = base + e * 1024;
+    const long long j = base + e * kBdCT;
     k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
   }
   __syncthreads();
 #pragma unroll
   for (int e = 0; e < kBdPer; ++e) {
-    const long long j = base + e * 1024;
+    const long long j = base + e * kBdCT;
     if (e < per && j < n) {
       uint32_t pos = kBdInvalid, b = kBdInvalid;
       if (k[e] != kEmptyKey) {
@@ -215,7 +234,7 @@ __global__ __launch_bounds__(1024) void k_bd_scatter(const uint64_t* __restrict_
 }
 
 // 5. one workgroup per bucket: LDS hash dedup -> bucket-local unique ids
-__global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ keys,
+__global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__ keys,
                                                    const uint32_t* __restrict__ pj,
                                                    const uint32_t* __restrict__ bstart,
                                                    uint32_t* __restrict__ luid,
@@ -233,7 +252,7 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   __shared__ int bad;
   const int t = threadIdx.x, b = blockIdx.x;
   if (t == 0) bad = 0;
-  for (int s = t; s < kBdTS; s += 1024) tab[s] = kEmptyKey;
+  for (int s = t; s < kBdTS; s += kBdDT) tab[s] = kEmptyKey;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   // the first kBdRegs occurrences of each thread keep their slot in
   // registers; a hot bucket's excess parks it in luid[] (rewritten below)
@@ -241,7 +260,7 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   uint64_t kk[kBdRegs];
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
-    const uint32_t p = p0 + t + r * 1024;
+    const uint32_t p = p0 + t + r * kBdDT;
     kk[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
   }
   __syncthreads();
@@ -264,27 +283,27 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   for (int r = 0; r < kBdRegs; ++r) slot[r] = kk[r] != kEmptyKey ? insert(kk[r]) : kBdInvalid;
   // hot buckets (Zipf heads): the excess in rounds of kBdRegs occurrences per
   // thread, all loads of a round in flight together; slots park in luid[]
-  for (uint32_t q = p0 + t + kBdRegs * 1024; q < p1; q += kBdRegs * 1024) {
+  for (uint32_t q = p0 + t + kBdRegs * kBdDT; q < p1; q += kBdRegs * kBdDT) {
     uint64_t k2[kBdRegs];
 #pragma unroll
     for (int r = 0; r < kBdRegs; ++r) {
-      const uint32_t p = q + r * 1024;
+      const uint32_t p = q + r * kBdDT;
       k2[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
     }
 #pragma unroll
     for (int r = 0; r < kBdRegs; ++r) {
-      const uint32_t p = q + r * 1024;
+      const uint32_t p = q + r * kBdDT;
       if (p < p1) luid[p] = k2[r] != kEmptyKey ? insert(k2[r]) : kBdInvalid;
     }
   }
   __syncthreads();
   BD_STAMP(1)
-  // compaction in slot order: thread t owns slots [4t, 4t+4)
-  constexpr int kPerT = kBdTS / 1024;
+  // compaction in slot order: thread t owns slots [kPerT*t, kPerT*(t+1))
+  constexpr int kPerT = kBdTS / kBdDT;
   unsigned int occ = 0;
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) occ += tab[t * kPerT + k] != kEmptyKey;
-  unsigned int o = block_excl_scan_1024(occ, wsum, &tot);
+  unsigned int o = block_excl_scan<kBdDT / 64>(occ, wsum, &tot);
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
     const int s = t * kPerT + k;
@@ -303,10 +322,10 @@ __global__ __launch_bounds__(1024) void k_bd_dedup(const uint64_t* __restrict__ 
   BD_STAMP(2)
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
-    const uint32_t p = p0 + t + r * 1024;
+    const uint32_t p = p0 + t + r * kBdDT;
     if (p < p1) luid[p] = slot[r] == kBdInvalid ? kBdInvalid : lid[slot[r]];
   }
-  for (uint32_t p = p0 + t + kBdRegs * 1024; p < p1; p += 1024) {
+  for (uint32_t p = p0 + t + kBdRegs * kBdDT; p < p1; p += kBdDT) {
     const uint32_t s = luid[p];
     luid[p] = s == kBdInvalid ? kBdInvalid : lid[s];
   }
@@ -451,18 +470,16 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     throw_error("bdedup: too many keys per call (max ~45M)");
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
-  hipLaunchKernelGGL(k_bd_count, dim3(L.nch), dim3(1024), lds, st, keys, n, rs, L.Pd, L.P,
+  hipLaunchKernelGGL(k_bd_count, dim3(L.nch), dim3(kBdCT), lds, st, keys, n, rs, L.Pd, L.P,
                      L.chunk, S + L.hist);
   check_launch("k_bd_count");
   hipLaunchKernelGGL(k_bd_colscan, dim3((L.P + 63) / 64), dim3(1024), 0, st, S + L.hist, L.nch,
-                     L.P, S + L.btot);
+                     L.P, S + L.btot, S + L.bstart, S + L.ctr);
   check_launch("k_bd_colscan");
-  hipLaunchKernelGGL(k_bd_bstart, dim3(1), dim3(1024), 0, st, S + L.btot, L.P, S + L.bstart);
-  check_launch("k_bd_bstart");
-  hipLaunchKernelGGL(k_bd_scatter, dim3(L.nch), dim3(1024), lds, st, keys, n, rs, L.Pd, L.P,
+  hipLaunchKernelGGL(k_bd_scatter, dim3(L.nch), dim3(kBdCT), lds, st, keys, n, rs, L.Pd, L.P,
                      L.chunk, S + L.hist, S + L.bstart, pj, pos_of, bkt);
   check_launch("k_bd_scatter");
-  hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(1024), 0, st, keys, pj, S + L.bstart, luid,
+  hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                      bkeys, S + L.unum, S, dbg);
   check_launch("k_bd_dedup");
   hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart, L.Pd,

@@ -43,6 +43,33 @@ __device__ __forceinline__ unsigned int block_excl_scan_1024(unsigned int v, uns
   return r;
 }
 
+// Exclusive scan across a workgroup of NW waves (NW <= 16); *total = sum.
+template <int NW>
+__device__ __forceinline__ unsigned int block_excl_scan(unsigned int v, unsigned int* wsum,
+                                                        unsigned int* total) {
+  const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+  unsigned int x = v;
+  for (int o = 1; o < 64; o <<= 1) {
+    const unsigned int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) wsum[w] = x;
+  __syncthreads();
+  if (w == 0) {
+    unsigned int ws = lane < NW ? wsum[lane] : 0u;
+    for (int o = 1; o < NW; o <<= 1) {
+      const unsigned int y = __shfl_up(ws, o, 64);
+      if (lane >= o) ws += y;
+    }
+    if (lane < NW) wsum[lane] = ws;
+  }
+  __syncthreads();
+  const unsigned int r = (w ? wsum[w - 1] : 0u) + x - v;
+  if (total) *total = wsum[NW - 1];
+  __syncthreads();
+  return r;
+}
+
 static __global__ __launch_bounds__(1024) void k_rowscan_p1(uint32_t* __restrict__ m, int cols,
                                                      uint32_t* __restrict__ G, int ngroups) {
   __shared__ unsigned int wsum[16];
