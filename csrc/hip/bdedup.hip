@@ -26,9 +26,10 @@
 //   5 dedup    one workgroup per bucket: LDS hash insert + compaction; writes
 //              bucket-local ids luid[pos], the bucket's keys (staged in its own
 //              occurrence range) and its unique count
-//   6 place    one workgroup per bucket: unique-id base = sum of the earlier
-//              buckets of the same destination (L2-resident, no serial scan,
-//              no inter-workgroup waiting), keys -> send segment, ucount[d]
+//              the LAST dedup workgroup to finish (arrival counter) scans the
+//              unique counts into unique-id bases and ucount[d] — no
+//              inter-workgroup waiting, no extra single-workgroup launch
+//   6 place    one workgroup per bucket: keys -> send segment (+ zeroed grads)
 //   7 inverse  (optional) inv[j] = ubase[bkt[j]] + luid[pos_of[j]]; consumers
 //              that only need uid(j) read it through BdIndex instead
 //
@@ -52,7 +53,7 @@ namespace ss {
 
 static constexpr uint32_t kBdInvalid = 0xFFFFFFFFu;
 static constexpr int kBdMaxChunk = 8192;  // occurrences per count/scatter workgroup
-static constexpr int kBdCT = 256;         // count/scatter workgroup size
+static constexpr int kBdCT = 1024;        // count/scatter workgroup size (256: slower)
 static constexpr int kBdPer = kBdMaxChunk / kBdCT;
 static constexpr int kBdDT = 512;         // dedup workgroup size
 static constexpr int kBdTarget = 2048;  // target occurrences per bucket
@@ -111,9 +112,7 @@ long long bd_ubase_offset(long long n, int nranks) {
   return bd_layout(n < 1 ? 1 : n, nranks).ubase;
 }
 
-// 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output.
-// 256-thread workgroups: the route stream runs beside the compute stream's
-// kernels, and small workgroups find free CU slots where 1024-thread ones wait
+// 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output
 __global__ __launch_bounds__(kBdCT) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
                                                     RouteSpec rs, int Pd, int P, int chunk,
                                                     uint32_t* __restrict__ hist) {
@@ -171,13 +170,16 @@ __global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist
     }
     if (seg == 15) btot[b] = off;
   }
-  // publish btot (release), count arrivals; the last arriver acquires and scans
-  __threadfence();
+  // publish btot (barrier, then ONE agent-scope release by one lane — not a
+  // fence per thread), count arrivals; the last arriver acquires and scans
   __syncthreads();
-  if (threadIdx.x == 0) last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+  if (threadIdx.x == 0) {
+    __threadfence();
+    last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+    if (last) __threadfence();
+  }
   __syncthreads();
   if (!last) return;  // workgroup-uniform
-  __threadfence();
   const int per = (P + 1023) / 1024;
   const int b0 = threadIdx.x * per;
   unsigned int sum = 0;
@@ -241,6 +243,10 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    uint64_t* __restrict__ bkeys,
                                                    uint32_t* __restrict__ unum,
                                                    uint32_t* __restrict__ err,
+                                                   unsigned int* __restrict__ ctr, int Pd,
+                                                   int nranks, long long ucap,
+                                                   uint32_t* __restrict__ ubase,
+                                                   unsigned long long* __restrict__ ucount,
                                                    unsigned long long* __restrict__ dbg) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
@@ -332,33 +338,45 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   __syncthreads();
   BD_STAMP(3)
 #undef BD_STAMP
+  // the LAST workgroup to finish turns the bucket unique counts into unique-id
+  // bases (exclusive scan within each destination) and ucount[d]; one lane
+  // releases per workgroup, the last arriver acquires (cdna guide G16)
+  __shared__ bool last;
+  if (t == 0) {
+    __threadfence();
+    last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+    if (last) __threadfence();
+  }
+  __syncthreads();
+  if (!last) return;  // workgroup-uniform
+  const int per = (Pd + kBdDT - 1) / kBdDT;
+  for (int d = 0; d < nranks; ++d) {
+    const int q0 = d * Pd + t * per;
+    unsigned int sum = 0;
+    for (int k = 0; k < per; ++k)
+      if (t * per + k < Pd)
+        sum += __hip_atomic_load(&unum[q0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned int e = block_excl_scan<kBdDT / 64>(sum, wsum, &tot);
+    for (int k = 0; k < per; ++k)
+      if (t * per + k < Pd) {
+        ubase[q0 + k] = (uint32_t)((long long)d * ucap + e);
+        e += __hip_atomic_load(&unum[q0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    if (t == 0) ucount[d] = tot;
+  }
+  if (t == 0) *ctr = 0u;  // ready for the next call (stream-ordered)
 }
 
 // 6. unique-id bases, send-segment keys, per-destination counts
 __global__ __launch_bounds__(256) void k_bd_place(const uint32_t* __restrict__ unum,
-                                                  const uint32_t* __restrict__ bstart, int Pd,
-                                                  long long ucap,
+                                                  const uint32_t* __restrict__ bstart,
+                                                  const uint32_t* __restrict__ ubase,
                                                   const uint64_t* __restrict__ bkeys,
                                                   uint64_t* __restrict__ ukeys,
-                                                  uint32_t* __restrict__ ubase,
-                                                  unsigned long long* __restrict__ ucount,
                                                   float* __restrict__ ugrad, int gdim) {
-  __shared__ unsigned int ws[4];
   const int b = blockIdx.x, t = threadIdx.x;
-  const int d = b / Pd, first = d * Pd;
-  // base = sum of unum over [first, b): independent L2 loads, block reduce
-  unsigned int part = 0;
-  for (int q = first + t; q < b; q += 256) part += unum[q];
-  for (int o = 32; o > 0; o >>= 1) part += __shfl_down(part, o, 64);
-  if ((t & 63) == 0) ws[t >> 6] = part;
-  __syncthreads();
-  const unsigned int excl = ws[0] + ws[1] + ws[2] + ws[3];
   const unsigned int nu = unum[b];
-  const unsigned long long base = (unsigned long long)d * ucap + excl;
-  if (t == 0) {
-    ubase[b] = (uint32_t)base;
-    if (b == first + Pd - 1) ucount[d] = excl + nu;
-  }
+  const unsigned long long base = ubase[b];
   const uint32_t p0 = bstart[b];
   for (uint32_t l = t; l < nu; l += 256) ukeys[base + l] = bkeys[p0 + l];
   if (ugrad)
@@ -480,10 +498,11 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      L.chunk, S + L.hist, S + L.bstart, pj, pos_of, bkt);
   check_launch("k_bd_scatter");
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
-                     bkeys, S + L.unum, S, dbg);
+                     bkeys, S + L.unum, S, S + L.ctr, L.Pd, rs.nranks, ucap, S + L.ubase, ucount,
+                     dbg);
   check_launch("k_bd_dedup");
-  hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart, L.Pd,
-                     ucap, bkeys, ukeys, S + L.ubase, ucount, ugrad, gdim);
+  hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart,
+                     S + L.ubase, bkeys, ukeys, ugrad, gdim);
   check_launch("k_bd_place");
   if (inv) {
     BdIndex ix{pos_of, luid, bkt, S + L.ubase};
