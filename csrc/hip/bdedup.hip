@@ -108,6 +108,11 @@ long long bd_scratch_words(long long n, int nranks) {
   return bd_layout(n < 1 ? 1 : n, nranks).total;
 }
 int bd_buckets(long long n, int nranks) { return bd_layout(n < 1 ? 1 : n, nranks).P; }
+// (P, bstart, unum, ubase) word offsets into the scratch for a call of n keys
+std::vector<long long> bd_offsets(long long n, int nranks) {
+  const BdLayout L = bd_layout(n < 1 ? 1 : n, nranks);
+  return {L.P, L.bstart, L.unum, L.ubase};
+}
 long long bd_ubase_offset(long long n, int nranks) {
   return bd_layout(n < 1 ? 1 : n, nranks).ubase;
 }
@@ -168,16 +173,13 @@ __global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist
       hist[i] = off;
       off += v;
     }
-    if (seg == 15) btot[b] = off;
+    if (seg == 15) __hip_atomic_store(&btot[b], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // publish btot (barrier, then ONE agent-scope release by one lane — not a
-  // fence per thread), count arrivals; the last arriver acquires and scans
+  // publish btot: write-through stores drained by every wave, barrier, then
+  // one arrival add; the last arriver reads btot write-through (guide G16 R1)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (threadIdx.x == 0) {
-    __threadfence();
-    last = atomicAdd(ctr, 1u) == gridDim.x - 1;
-    if (last) __threadfence();
-  }
+  if (threadIdx.x == 0) last = atomicAdd(ctr, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;  // workgroup-uniform
   const int per = (P + 1023) / 1024;
@@ -321,7 +323,8 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
     }
   }
   if (t == 0) {
-    unum[b] = tot;
+    // write-through (agent-scope) store: read by the last workgroup below
+    __hip_atomic_store(&unum[b], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (bad) atomicOr(err, 1u);
   }
   __syncthreads();
@@ -339,13 +342,15 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   BD_STAMP(3)
 #undef BD_STAMP
   // the LAST workgroup to finish turns the bucket unique counts into unique-id
-  // bases (exclusive scan within each destination) and ucount[d]; one lane
-  // releases per workgroup, the last arriver acquires (cdna guide G16)
+  // bases (exclusive scan within each destination) and ucount[d].  Hand-off
+  // without fences (a per-workgroup release fence writes back the whole L2 —
+  // it made this kernel 3x slower): unum went out as a write-through store,
+  // drained before the arrival add; the last arriver reads it write-through
+  // (cdna guide G16, R1)
   __shared__ bool last;
   if (t == 0) {
-    __threadfence();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     last = atomicAdd(ctr, 1u) == gridDim.x - 1;
-    if (last) __threadfence();
   }
   __syncthreads();
   if (!last) return;  // workgroup-uniform
@@ -473,7 +478,7 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
-                     float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
+                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                      unsigned long long* dbg) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   if (n <= 0) {
@@ -501,9 +506,11 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      bkeys, S + L.unum, S, S + L.ctr, L.Pd, rs.nranks, ucap, S + L.ubase, ucount,
                      dbg);
   check_launch("k_bd_dedup");
-  hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart,
-                     S + L.ubase, bkeys, ukeys, ugrad, gdim);
-  check_launch("k_bd_place");
+  if (place) {  // send-segment keys (+ zeroed gradient rows)
+    hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart,
+                       S + L.ubase, bkeys, ukeys, ugrad, gdim);
+    check_launch("k_bd_place");
+  }
   if (inv) {
     BdIndex ix{pos_of, luid, bkt, S + L.ubase};
     hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, n, inv);

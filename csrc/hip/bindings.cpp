@@ -112,6 +112,15 @@ PYBIND11_MODULE(_ss_hip, m) {
     launch_pull_unique(t, P<const uint64_t>(keys), sl, max_n, P<long long>(slots), P<float>(out),
                        ip, P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
   });
+  m.def("pull_unique_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
+                             uintptr_t ubase, int P_, uintptr_t slots, uintptr_t out,
+                             const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
+                             uintptr_t st) {
+    launch_pull_unique_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
+                          P<const uint32_t>(unum), P<const uint32_t>(ubase), P_,
+                          P<long long>(slots), P<float>(out), ip, P<unsigned long long>(size_ctr),
+                          P<int>(err), G, S(st));
+  });
   m.def("pull_claim", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
                          uintptr_t slots, uintptr_t out, const InitParams& ip, uintptr_t size_ctr,
                          uintptr_t err, int G, uintptr_t st) {
@@ -152,21 +161,22 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("dedup_blocks", &dedup_blocks);
   m.def("bd_scratch_words", &bd_scratch_words);
   m.def("bd_ubase_offset", &bd_ubase_offset);
+  m.def("bd_offsets", &bd_offsets);
   m.def("bd_buckets", &bd_buckets);
   m.def("bd_dedup", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num, int nranks,
                        long long ucap, uintptr_t scratch, uintptr_t pj, uintptr_t pos_of,
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
-                       uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, uintptr_t st,
-                       uintptr_t dbg) {
+                       uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
+                       uintptr_t st, uintptr_t dbg) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
                     P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
                     P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
-                    P<uint32_t>(inv), S(st), P<unsigned long long>(dbg));
+                    P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
-     py::arg("gdim"), py::arg("inv"), py::arg("st"), py::arg("dbg") = 0);
+     py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),

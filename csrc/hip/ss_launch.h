@@ -6,6 +6,7 @@
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <vector>
 #include "bdindex.h"
 #include "ss_device.h"
 
@@ -28,6 +29,10 @@ void launch_gather(const DevTable& t, const long long* slots, const SegList& sl,
 void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& sl,
                         long long max_n, long long* slots, float* out, const InitParams& ip,
                         unsigned long long* size_ctr, int* err, int G, hipStream_t st);
+void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                           const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
+                           float* out, const InitParams& ip, unsigned long long* size_ctr,
+                           int* err, int G, hipStream_t st);
 void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
                        long long max_n, long long* slots, float* out, const InitParams& ip,
                        unsigned long long* size_ctr, int* err, int G, hipStream_t st);
@@ -90,11 +95,12 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval, 
 // --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
 long long bd_scratch_words(long long n, int nranks);
 long long bd_ubase_offset(long long n, int nranks);
+std::vector<long long> bd_offsets(long long n, int nranks);
 int bd_buckets(long long n, int nranks);
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
-                     float* ugrad, int gdim, uint32_t* inv, hipStream_t st,
+                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                      unsigned long long* dbg = nullptr);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,

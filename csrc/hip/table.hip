@@ -117,6 +117,44 @@ __global__ __launch_bounds__(256) void k_gather(DevTable t, const long long* __r
 // K3+K4 fused, for key lists known to be unique within the launch (the
 // worker's dedup output on the colocated 1-GPU path): probe, init if new,
 // and emit the row without a second pass.
+// one key of a unique-key pull: probe (insert if new) by the group leader,
+// init the row if it was inserted, emit the row to out[pos]
+template <int G>
+__device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long long pos,
+                                         long long* __restrict__ slots_out, float* __restrict__ out,
+                                         const InitParams& ip, int* err, int lg,
+                                         unsigned long long& ins) {
+  long long slot = -1;
+  int inserted = 0;
+  if (lg == 0) {
+    bool b = false;
+    if (key != kEmptyKey) slot = probe_slot(t, key, true, &b);
+    inserted = b;
+    if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
+    if (slots_out) slots_out[pos] = slot;
+  }
+  if (G > 1) {
+    slot = __shfl(slot, 0, G);
+    inserted = __shfl(inserted, 0, G);
+  }
+  float* o = out + pos * (long long)t.dim;
+  if (slot < 0) {
+    for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
+  } else {
+    float* row = slot_row(t, slot);
+    if (inserted) {
+      for (uint32_t j = lg; j < t.width; j += G) {
+        const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
+        row[j] = v;
+        if (j < t.dim) o[j] = v;
+      }
+    } else {
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
+    }
+  }
+  ins += (lg == 0 && inserted);
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t* __restrict__ keys,
                                                      SegList sl, long long* __restrict__ slots_out,
@@ -130,37 +168,29 @@ __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t*
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    const uint64_t key = keys[pos];
-    long long slot = -1;
-    int inserted = 0;
-    if (lg == 0) {
-      bool b = false;
-      if (key != kEmptyKey) slot = probe_slot(t, key, true, &b);
-      inserted = b;
-      if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
-      if (slots_out) slots_out[pos] = slot;
-    }
-    if (G > 1) {
-      slot = __shfl(slot, 0, G);
-      inserted = __shfl(inserted, 0, G);
-    }
-    float* o = out + pos * (long long)t.dim;
-    if (slot < 0) {
-      for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
-    } else {
-      float* row = slot_row(t, slot);
-      if (inserted) {
-        for (uint32_t j = lg; j < t.width; j += G) {
-          const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
-          row[j] = v;
-          if (j < t.dim) o[j] = v;
-        }
-      } else {
-        for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
-      }
-    }
-    ins += (lg == 0 && inserted);
+    pull_one<G>(t, keys[pos], pos, slots_out, out, ip, err, lg, ins);
   }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
+}
+
+// Same, straight from the bucketed dedup's per-bucket staging (bdedup.hip):
+// workgroup b pulls bucket b's unique keys bkeys[bstart[b] + l] to unique id
+// ubase[b] + l — the colocated 1-GPU path needs no send-segment copy.
+template <int G>
+__global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64_t* __restrict__ bkeys,
+                                                        const uint32_t* __restrict__ bstart,
+                                                        const uint32_t* __restrict__ unum,
+                                                        const uint32_t* __restrict__ ubase,
+                                                        long long* __restrict__ slots_out,
+                                                        float* __restrict__ out, InitParams ip,
+                                                        unsigned long long* size_ctr, int* err) {
+  const int b = blockIdx.x, lg = threadIdx.x % G;
+  const uint32_t nu = unum[b], base = ubase[b];
+  const uint64_t* src = bkeys + bstart[b];
+  unsigned long long ins = 0;
+  for (uint32_t l = threadIdx.x / G; l < nu; l += 256 / G)
+    pull_one<G>(t, src[l], (long long)base + l, slots_out, out, ip, err, lg, ins);
   ins = wave_sum_u64(ins);
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
@@ -428,6 +458,16 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
                                       st, t, keys, sl, slots, out, ip, size_ctr, err));
   check_launch("k_pull_unique");
+}
+
+void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                           const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
+                           float* out, const InitParams& ip, unsigned long long* size_ctr,
+                           int* err, int G, hipStream_t st) {
+  if (P <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique_bk<kG>, dim3(P), dim3(256), 0, st, t, bkeys,
+                                      bstart, unum, ubase, slots, out, ip, size_ctr, err));
+  check_launch("k_pull_unique_bk");
 }
 
 void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,

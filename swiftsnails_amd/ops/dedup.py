@@ -68,6 +68,9 @@ class Deduper:
         # bucket mode: False skips the inverse-index pass; consumers then read
         # luid[pos_of[j]] themselves (the LR forward does, fused)
         self.materialize_inv = True
+        # bucket mode: False skips writing the contiguous send segment (ukeys)
+        # when nothing reads it (the colocated 1-GPU engine pulls per bucket)
+        self.need_ukeys = True
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -123,7 +126,8 @@ class Deduper:
                             self.pos_of.data_ptr(), self.bkt.data_ptr(), self.luid.data_ptr(),
                             self.bkeys.data_ptr(), self.ucount.data_ptr(),
                             self.ukeys.data_ptr(), ug, self.gdim,
-                            self.inv.data_ptr() if self.materialize_inv else 0, st,
+                            self.inv.data_ptr() if self.materialize_inv else 0,
+                            int(self.need_ukeys or bool(ug)), st,
                             self.dbg.data_ptr() if self.dbg is not None else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self)
@@ -160,6 +164,17 @@ class Deduper:
         n = self._last_n if n is None else n
         ub = self.scratch.data_ptr() + 4 * self.h.bd_ubase_offset(max(1, n), self.nranks)
         return [self.pos_of.data_ptr(), self.luid.data_ptr(), self.bkt.data_ptr(), ub]
+
+    def bucket_view(self, n: Optional[int] = None):
+        """(bkeys, bstart, unum, ubase, P) of the last call: bucket b's unique
+        keys are bkeys[bstart[b] : bstart[b] + unum[b]] with unique ids from
+        ubase[b] (device pointers; bucket mode)."""
+        if self.mode != "bucket":
+            raise RuntimeError("bucket_view needs mode='bucket'")
+        n = self._last_n if n is None else n
+        P, o_bs, o_un, o_ub = self.h.bd_offsets(max(1, n), self.nranks)
+        b0 = self.scratch.data_ptr()
+        return (self.bkeys.data_ptr(), b0 + 4 * o_bs, b0 + 4 * o_un, b0 + 4 * o_ub, P)
 
     def check(self):
         """Raise if any bucket overflowed its LDS table (sticky; syncs)."""

@@ -169,6 +169,15 @@ class HbmTable:
             h.gather(self.dt, slots.data_ptr(), sl, n, out.data_ptr(), self.G, st)
         return out, slots
 
+    def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None):
+        """Unique-key lookup-or-init + gather straight from a bucketed dedup
+        (``Deduper.bucket_view()``): rows land at their unique ids."""
+        bkeys, bstart, unum, ubase, P = view
+        hip().pull_unique_bk(self.dt, bkeys, bstart, unum, ubase, P, slots.data_ptr(),
+                             out.data_ptr(), self._init_native, self.size_ctr.data_ptr(),
+                             self.err.data_ptr(), self.G, _stream_ptr(stream))
+        return out, slots
+
     def lookup_slots(self, keys: torch.Tensor, insert: bool = False, segs=None,
                      max_n: Optional[int] = None, stream=None) -> torch.Tensor:
         slots = torch.empty(keys.numel(), dtype=torch.int64, device=self.device)

@@ -148,6 +148,11 @@ class PSEngine:
         if self.fast1:
             self.slots = [torch.empty(cap, dtype=torch.int64, device=dev)
                           for _ in range(self.depth)]
+            # the colocated pull reads the bucketed dedup's staging directly:
+            # no contiguous send segment is needed
+            if table is not None and table.insert_mode == "cas":
+                for dd in self.dedupers:
+                    dd.need_ukeys = False
         else:
             # server-side receive buffers: one fixed segment per source rank.
             # rslots must survive from pull to push of the same round -> ring.
@@ -235,8 +240,12 @@ class PSEngine:
         tab = self.table
         uv = self.uvals[slot]
         if self.fast1:
-            tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
-                     segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
+            own = dd.owner
+            if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
+                tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot])
+            else:
+                tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
+                         segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
             self.metrics.add(occurrences=dd.n)
             return Round(dd, uv, slot, slots=self.slots[slot])
         scounts, rcounts = r.counts.wait()
@@ -330,7 +339,15 @@ class PSEngine:
         to the server are created with the initialiser before the update (the
         reference CHECK-fails, sparsetable.h:184)."""
         keys = keys.reshape(-1)
-        r = self.route(keys)
+        # this path merges into zeroed rows and probes the send segment: force
+        # both on the deduper that routes it (a model may have switched them off)
+        own = self.dedupers[self._next_slot]
+        saved = (getattr(own, "zero_grad", True), getattr(own, "need_ukeys", True))
+        own.zero_grad, own.need_ukeys = True, True
+        try:
+            r = self.route(keys)
+        finally:
+            own.zero_grad, own.need_ukeys = saved
         if self.gpu:
             torch.cuda.current_stream().wait_event(r.ready)
         dd = r.dd
