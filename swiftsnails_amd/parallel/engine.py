@@ -108,7 +108,7 @@ class PSEngine:
 
     def __init__(self, table, transport: Optional[Transport], max_keys: int, dim: int,
                  frag_num: int = 0, server_ranks: Optional[Sequence[int]] = None, device=None,
-                 count_transport: Optional[Transport] = None, depth: int = 2,
+                 count_transport: Optional[Transport] = None, depth: Optional[int] = None,
                  zero_grad: bool = True):
         self.t = transport or LoopbackTransport()
         self.ct = count_transport or self.t
@@ -129,7 +129,11 @@ class PSEngine:
         self.router = HashFrag(len(self.server_ranks), frag_num)
         self.frag_map = self.router.rank_map(self.server_ranks)
         self.max_keys = int(max_keys)
-        self.depth = max(1, int(depth))
+        # ring depth 3 by default: with one batch of lookahead, routing round
+        # i+1 then reuses the buffers of round i-2 (long pushed) instead of
+        # waiting on round i-1's push (a cross-queue event on the critical path)
+        self.depth = max(1, int(depth if depth is not None else
+                                os.environ.get("SS_ENGINE_DEPTH", "3")))
         dd_cls = Deduper if self.gpu else CpuDeduper
         fm = torch.from_numpy(self.frag_map.astype(np.int32))
         self.dedupers = [dd_cls(self.max_keys, nranks=self.world, frag_map=fm, gdim=self.dim,
