@@ -23,6 +23,7 @@ class PipelinedWorker:
         self.loss_sum = loss_buffer(engine.device)
         self.step_idx = 0
         self._next = None
+        self._cur = None
         self._empty = torch.empty(0, dtype=torch.int64, device=engine.device)
 
     # -- subclass hooks
@@ -47,6 +48,9 @@ class PipelinedWorker:
         return self.engine.route(produce=produce)
 
     def step(self) -> torch.Tensor:
+        eng = self.engine
+        if getattr(eng, "pull_ahead", False):
+            return self._step_pull_ahead()
         r = self._next if self._next is not None else self._route(self.step_idx)
         self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
         rnd = self.engine.pull(r)
@@ -54,6 +58,25 @@ class PipelinedWorker:
         if self.active:
             self._compute(rnd, r.slot, torch.cuda.current_stream().cuda_stream)
         self.engine.push(rnd)
+        self.step_idx += 1
+        return self.loss_sum
+
+    def _step_pull_ahead(self) -> torch.Tensor:
+        """N>1: round i computes/pushes on the main stream while round i+1 is
+        pulled and round i+2 routed on the route stream (staleness 1)."""
+        eng = self.engine
+        if self._cur is None:  # bootstrap the pipeline
+            r = self._next if self._next is not None else self._route(self.step_idx)
+            self._cur = eng.pull_ahead_round(r)
+            self._next = self._route(self.step_idx + 1)
+        rnd = self._cur
+        eng.begin(rnd)
+        self.loss_sum.zero_()
+        if self.active:
+            self._compute(rnd, rnd.slot, torch.cuda.current_stream().cuda_stream)
+        eng.push(rnd)
+        self._cur = eng.pull_ahead_round(self._next)
+        self._next = self._route(self.step_idx + 2)
         self.step_idx += 1
         return self.loss_sum
 

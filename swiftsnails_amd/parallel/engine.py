@@ -70,6 +70,7 @@ class Round:
     rcounts: Optional[np.ndarray] = None  # keys this rank received from each worker
     pushed: bool = False
     stats: dict = field(default_factory=dict)
+    ready: Optional[object] = None        # pull-ahead: route-stream event of the pulled rows
 
     @property
     def inv(self) -> torch.Tensor:
@@ -177,6 +178,13 @@ class PSEngine:
         self.displs = [r * cap for r in range(N)]
         self.rounds = 0
         self._next_slot = 0
+        # pull-ahead (N>1 on GPU): round i+1's pull (keys a2av, server lookup,
+        # rows a2av) runs on the route stream with the count communicator
+        # while round i computes and pushes on the main stream — bounded
+        # staleness 1, the asynchronous-PS semantics of the reference
+        # (SURVEY X3).  Needs ring depth >= 3 (rounds i, i+1, i+2 in flight).
+        self.pull_ahead = (self.gpu and not self.fast1 and self.depth >= 3 and
+                           os.environ.get("SS_PULL_AHEAD", "1") != "0")
 
     # ------------------------------------------------------------ stage 1
     def route(self, keys: Optional[torch.Tensor] = None, produce=None, post=None) -> Routed:
@@ -263,6 +271,29 @@ class PSEngine:
                          a2a_bytes=8 * (sent + recv) + 4 * self.dim * (2 * sent + 2 * recv))
         return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
                      stats={"sent": sent, "recv": recv})
+
+    def pull_ahead_round(self, r: Routed) -> Round:
+        """Stage 2 of a round on the route stream (pull-ahead mode): returns a
+        Round whose rows are ready at ``rnd.ready``; ``begin(rnd)`` makes the
+        current (main) stream wait for them."""
+        dd, slot = r.dd, r.slot
+        scounts, rcounts = r.counts.wait()  # host: the route stage enqueued earlier
+        rs, D, uv = self.route_stream, self.displs, self.uvals[slot]
+        with torch.cuda.stream(rs):
+            self.ct.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
+            self._server_pull(rcounts, slot)
+            self.ct.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
+            ev = torch.cuda.Event()
+            ev.record(rs)
+        sent, recv = int(scounts.sum()), int(rcounts.sum())
+        self.metrics.add(occurrences=dd.n, unique_sent=sent, unique_recv=recv,
+                         a2a_bytes=8 * (sent + recv) + 4 * self.dim * (2 * sent + 2 * recv))
+        return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
+                     stats={"sent": sent, "recv": recv}, ready=ev)
+
+    def begin(self, rnd: Round) -> None:
+        if rnd.ready is not None:
+            torch.cuda.current_stream().wait_event(rnd.ready)
 
     # ------------------------------------------------------------ stage 3
     def _server_apply(self, rcounts: np.ndarray, slot: int, resolved: bool) -> None:

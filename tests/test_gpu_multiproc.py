@@ -119,3 +119,61 @@ def test_engine_gpu_gloo(world, servers, workers, opt):
 
 def test_engine_gpu_rccl_same_device():
     _run(2, [0, 1], [0, 1], "adagrad", "rccl")
+
+
+def _run_lr_rank(rank, world, port, pull_ahead, grad_mode, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    os.environ["SS_PULL_AHEAD"] = "1" if pull_ahead else "0"
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+        from swiftsnails_amd.parallel.engine import PSEngine
+        from swiftsnails_amd.parallel.transport import TorchDistTransport
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        data = CtrSynth(batch_size=2048, num_fields=13, num_features=200_000, tail_frac=0.0)
+        table = make_lr_table(data.num_features, world, device=dev)
+        eng = PSEngine(table, TorchDistTransport(), max_keys=2048 * 13, dim=1, device=dev)
+        assert eng.pull_ahead == pull_ahead
+        w = SparseLRWorker(eng, data, rank=rank, world=world, grad_mode=grad_mode)
+        losses = []
+        for _ in range(40):
+            w.step()
+            losses.append(w.mean_loss())
+        torch.cuda.synchronize()
+        table.check()
+        q.put((rank, losses, table.size()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("grad_mode", ["segreduce", "atomic"])
+def test_lr_worker_world2_pull_ahead(grad_mode):
+    """Worker pipeline with N>1: pull-ahead (staleness 1, round i+1 pulled on
+    the route stream while round i computes) trains like the synchronous
+    pipeline."""
+    ctx = mp.get_context("spawn")
+    out = {}
+    for pa in (False, True):
+        q = ctx.Queue()
+        port = _free_port()
+        procs = [ctx.Process(target=_run_lr_rank, args=(r, 2, port, pa, grad_mode, q))
+                 for r in range(2)]
+        for p in procs:
+            p.start()
+        res = [q.get(timeout=240) for _ in range(2)]
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+        out[pa] = {r: (l, n) for r, l, n in res}
+    for pa, per_rank in out.items():
+        for r, (losses, n) in per_rank.items():
+            assert np.isfinite(losses).all()
+            assert np.mean(losses[-5:]) < np.mean(losses[:3]) - 0.01, (pa, r, losses)
+            assert n > 0
+    sync_last = np.mean([np.mean(l[-5:]) for l, _ in out[False].values()])
+    ahead_last = np.mean([np.mean(l[-5:]) for l, _ in out[True].values()])
+    assert abs(ahead_last - sync_last) < 0.03, (sync_last, ahead_last)
