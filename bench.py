@@ -48,6 +48,8 @@ def main(argv=None):
     ap.add_argument("--grad-mode", default="segreduce", choices=["segreduce", "atomic"])
     ap.add_argument("--dedup", default=None, choices=["bucket", "hash"],
                     help="batch dedup implementation (default: bucket)")
+    ap.add_argument("--transport", default="rccl", choices=["rccl", "gloo"],
+                    help="N>1 data plane; gloo is a host-staged rehearsal transport (tests)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -60,8 +62,11 @@ def main(argv=None):
             return 2
     if a.dedup:
         os.environ["SS_DEDUP"] = a.dedup
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    # SS_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal
+    # of this script on a 1-GPU box (with --transport gloo)
+    dev_idx = int(os.environ.get("SS_BENCH_DEVICE", local_rank))
+    torch.cuda.set_device(dev_idx)
+    dev = torch.device("cuda", dev_idx)
 
     from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
     from swiftsnails_amd.ops.optim import Optimizer
@@ -74,10 +79,15 @@ def main(argv=None):
         dist.init_process_group("gloo", rank=rank, world_size=world)
         store = dist.distributed_c10d._get_default_store()
         try:
-            # two native RCCL communicators: data plane (main stream) and the
-            # route-stage count exchange (route stream)
-            transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
-            ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts")
+            if a.transport == "gloo":
+                from swiftsnails_amd.parallel.transport import TorchDistTransport
+
+                transport = TorchDistTransport()
+            else:
+                # two native RCCL communicators: data plane (main stream) and
+                # the route stage + pull-ahead (route stream)
+                transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
+                ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts")
         except Exception as e:  # pragma: no cover - hardware dependent
             from swiftsnails_amd.parallel.transport import TorchDistTransport
 
@@ -156,7 +166,10 @@ def main(argv=None):
                 "model": f"sparse_lr_{a.features // 1_000_000}M_features",
                 "global_batch": a.batch * world,
                 "seq_len": a.fields,
-                "parallelism": f"ps{world} (colocated worker+server shard per GPU, RCCL alltoallv)",
+                "parallelism": (f"ps{world} (colocated worker+server shard per GPU, "
+                                f"{'RCCL' if a.transport == 'rccl' else 'gloo'} alltoallv"
+                                + (", pull-ahead staleness 1)" if getattr(engine, "pull_ahead", False)
+                                   else ")")),
                 "optimizer": a.optimizer,
                 "keys_per_step_per_gpu": a.batch * a.fields,
                 "table_keys": int(keys_in_table.item()),
