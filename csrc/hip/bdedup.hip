@@ -43,6 +43,7 @@
 // bucket holds ~2048 occurrences; its unique count is then far below the
 // 4096-slot LDS table (overflow is detected and reported, never silent).
 #include <algorithm>
+#include <cstdlib>
 
 #include "bdindex.h"
 #include "scan.h"
@@ -53,8 +54,7 @@ namespace ss {
 
 static constexpr uint32_t kBdInvalid = 0xFFFFFFFFu;
 static constexpr int kBdMaxChunk = 8192;  // occurrences per count/scatter workgroup
-static constexpr int kBdCT = 1024;        // count/scatter workgroup size (256: slower)
-static constexpr int kBdPer = kBdMaxChunk / kBdCT;
+static constexpr int kBdChunkLanes = 1024;  // chunk granularity (any CT below divides it)
 static constexpr int kBdDT = 512;         // dedup workgroup size
 static constexpr int kBdTarget = 2048;  // target occurrences per bucket
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
@@ -87,7 +87,7 @@ static BdLayout bd_layout(long long n, int nranks) {
   // chunk count a multiple of the 256 CUs (balanced waves), chunk <= 8192
   const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
   const long long per = (n + 256 * waves - 1) / (256 * waves);
-  L.chunk = (int)(((per + kBdCT - 1) / kBdCT) * kBdCT);
+  L.chunk = (int)(((per + kBdChunkLanes - 1) / kBdChunkLanes) * kBdChunkLanes);
   L.nch = (int)((n + L.chunk - 1) / L.chunk);
   if (L.nch < 1) L.nch = 1;
   // words 0, 1: sticky error flag and the colscan arrival counter, at fixed
@@ -118,26 +118,27 @@ long long bd_ubase_offset(long long n, int nranks) {
 }
 
 // 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output
-__global__ __launch_bounds__(kBdCT) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
+template <int CT>
+__global__ __launch_bounds__(CT) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
                                                     RouteSpec rs, int Pd, int P, int chunk,
                                                     uint32_t* __restrict__ hist) {
   extern __shared__ unsigned int h[];
-  for (int b = threadIdx.x; b < P; b += kBdCT) h[b] = 0u;
+  for (int b = threadIdx.x; b < P; b += CT) h[b] = 0u;
   __syncthreads();
   const long long base = (long long)blockIdx.x * chunk + threadIdx.x;
-  const int per = chunk / kBdCT;
-  uint64_t k[kBdPer];
+  const int per = chunk / CT;
+  uint64_t k[(kBdMaxChunk / CT)];
 #pragma unroll
-  for (int e = 0; e < kBdPer; ++e) {
-    const long long j = base + e * kBdCT;
+  for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
+    const long long j = base + e * CT;
     k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
   }
 #pragma unroll
-  for (int e = 0; e < kBdPer; ++e)
+  for (int e = 0; e < (kBdMaxChunk / CT); ++e)
     if (k[e] != kEmptyKey) atomicAdd(&h[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
   __syncthreads();
   uint32_t* row = hist + (long long)blockIdx.x * P;
-  for (int b = threadIdx.x; b < P; b += kBdCT) row[b] = h[b];
+  for (int b = threadIdx.x; b < P; b += CT) row[b] = h[b];
 }
 
 // 2+3. column scan of the [nch][P] histogram (64 buckets x 16 chunk segments
@@ -201,7 +202,8 @@ __global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist
 }
 
 // 4. bucket-ordered occurrence list (dynamic LDS: P words)
-__global__ __launch_bounds__(kBdCT) void k_bd_scatter(const uint64_t* __restrict__ keys, long long n,
+template <int CT>
+__global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ keys, long long n,
                                                      RouteSpec rs, int Pd, int P, int chunk,
                                                      const uint32_t* __restrict__ hist,
                                                      const uint32_t* __restrict__ bstart,
@@ -211,19 +213,19 @@ __global__ __launch_bounds__(kBdCT) void k_bd_scatter(const uint64_t* __restrict
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
-  for (int b = threadIdx.x; b < P; b += kBdCT) cur[b] = bstart[b] + row[b];
+  for (int b = threadIdx.x; b < P; b += CT) cur[b] = bstart[b] + row[b];
   const long long base = (long long)c * chunk + threadIdx.x;
-  const int per = chunk / kBdCT;
-  uint64_t k[kBdPer];
+  const int per = chunk / CT;
+  uint64_t k[(kBdMaxChunk / CT)];
 #pragma unroll
-  for (int e = 0; e < kBdPer; ++e) {
-    const long long j = base + e * kBdCT;
+  for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
+    const long long j = base + e * CT;
     k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
   }
   __syncthreads();
 #pragma unroll
-  for (int e = 0; e < kBdPer; ++e) {
-    const long long j = base + e * kBdCT;
+  for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
+    const long long j = base + e * CT;
     if (e < per && j < n) {
       uint32_t pos = kBdInvalid, b = kBdInvalid;
       if (k[e] != kEmptyKey) {
@@ -493,14 +495,26 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     throw_error("bdedup: too many keys per call (max ~45M)");
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
-  hipLaunchKernelGGL(k_bd_count, dim3(L.nch), dim3(kBdCT), lds, st, keys, n, rs, L.Pd, L.P,
-                     L.chunk, S + L.hist);
+  // count/scatter workgroup size (SS_BD_CT: 256/512/1024; experiments)
+  static const int ct = [] {
+    const char* e = std::getenv("SS_BD_CT");
+    const int v = e ? std::atoi(e) : 1024;
+    return (v == 256 || v == 512) ? v : 1024;
+  }();
+#define SS_BD_CT_DISPATCH(KERNEL, ...)                                                        \
+  switch (ct) {                                                                               \
+    case 256: hipLaunchKernelGGL(KERNEL<256>, dim3(L.nch), dim3(256), lds, st, __VA_ARGS__); break; \
+    case 512: hipLaunchKernelGGL(KERNEL<512>, dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KERNEL<1024>, dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
+  }
+  SS_BD_CT_DISPATCH(k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist);
   check_launch("k_bd_count");
   hipLaunchKernelGGL(k_bd_colscan, dim3((L.P + 63) / 64), dim3(1024), 0, st, S + L.hist, L.nch,
                      L.P, S + L.btot, S + L.bstart, S + L.ctr);
   check_launch("k_bd_colscan");
-  hipLaunchKernelGGL(k_bd_scatter, dim3(L.nch), dim3(kBdCT), lds, st, keys, n, rs, L.Pd, L.P,
-                     L.chunk, S + L.hist, S + L.bstart, pj, pos_of, bkt);
+  SS_BD_CT_DISPATCH(k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pj,
+                    pos_of, bkt);
+#undef SS_BD_CT_DISPATCH
   check_launch("k_bd_scatter");
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                      bkeys, S + L.unum, S, S + L.ctr, L.Pd, rs.nranks, ucap, S + L.ubase, ucount,
