@@ -21,6 +21,9 @@
 
 namespace ss {
 
+static constexpr int kApplyRegs = 4;  // row coordinates per lane held in registers
+
+
 __device__ __forceinline__ long long probe_slot(const DevTable& t, uint64_t key, bool insert,
                                                 bool* inserted) {
   uint64_t s = fastrange64(table_hash(key), t.cap);
@@ -147,6 +150,20 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
         const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
         row[j] = v;
         if (j < t.dim) o[j] = v;
+      }
+    } else if (t.dim <= (uint32_t)G * kApplyRegs) {
+      // every load before the first store: the compiler cannot prove `o` and
+      // `row` disjoint, so a copy loop would be one round trip per coordinate
+      float v[kApplyRegs];
+#pragma unroll
+      for (int r = 0; r < kApplyRegs; ++r) {
+        const uint32_t j = lg + r * G;
+        if (j < t.dim) v[r] = row[j];
+      }
+#pragma unroll
+      for (int r = 0; r < kApplyRegs; ++r) {
+        const uint32_t j = lg + r * G;
+        if (j < t.dim) o[j] = v[r];
       }
     } else {
       for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
@@ -329,7 +346,35 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
     if (slot < 0) continue;
     float* row = slot_row(t, slot);
     const float* gr = grads + pos * (long long)t.dim;
-    for (uint32_t j = lg; j < t.dim; j += G) opt_apply(op, row, row + t.dim, t.dim, j, gr[j]);
+    if (t.dim <= (uint32_t)G * kApplyRegs) {
+      // all of this lane's coordinates loaded first, updated in registers,
+      // stored after: one memory round trip per row (a load-update-store loop
+      // per coordinate serialised dim/G round trips: FM rows took 3)
+      const int ns = opt_state_per_coord(op.kind);
+      float w[kApplyRegs], s1[kApplyRegs], s2[kApplyRegs], g[kApplyRegs];
+#pragma unroll
+      for (int r = 0; r < kApplyRegs; ++r) {
+        const uint32_t j = lg + r * G;
+        if (j < t.dim) {
+          w[r] = row[j];
+          g[r] = gr[j];
+          s1[r] = ns > 0 ? row[t.dim + j] : 0.f;
+          s2[r] = ns > 1 ? row[2 * t.dim + j] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < kApplyRegs; ++r) {
+        const uint32_t j = lg + r * G;
+        if (j < t.dim) {
+          opt_update(op, w[r], s1[r], s2[r], g[r]);
+          row[j] = w[r];
+          if (ns > 0) row[t.dim + j] = s1[r];
+          if (ns > 1) row[2 * t.dim + j] = s2[r];
+        }
+      }
+    } else {
+      for (uint32_t j = lg; j < t.dim; j += G) opt_apply(op, row, row + t.dim, t.dim, j, gr[j]);
+    }
   }
 }
 

@@ -71,45 +71,56 @@ SS_HD float init_value(const InitParams& ip, uint64_t key, uint32_t j, uint32_t 
 }
 
 // One coordinate of an optimizer step. `row` = params, `st` = state base.
-SS_HD void opt_apply(const OptParams& op, float* row, float* st, uint32_t dim, uint32_t j,
-                     float g) {
+// Register form: w = parameter, s1/s2 = the optimizer state slots of this
+// coordinate (AdaGrad: s1 = sum g^2; FTRL: s1 = z, s2 = n; Adam: s1 = m,
+// s2 = v).  Kernels load a row's coordinates first, update in registers and
+// store after (no load behind a store of the same row).
+SS_HD void opt_update(const OptParams& op, float& w, float& s1, float& s2, float g) {
   g *= op.grad_scale;
   if (op.clip > 0.f) g = g < -op.clip ? -op.clip : (g > op.clip ? op.clip : g);
-  const float w = row[j];
   switch (op.kind) {
     case kOptSGD: {
       g += op.l2 * w;
-      row[j] = w - op.lr * g;
+      w = w - op.lr * g;
     } break;
     case kOptAdaGrad: {
       g += op.l2 * w;
-      const float h = st[j] + g * g;
-      st[j] = h;
-      row[j] = w - op.lr * g * SS_RSQRT(h + op.eps);
+      s1 = s1 + g * g;
+      w = w - op.lr * g * SS_RSQRT(s1 + op.eps);
     } break;
     case kOptFTRL: {
       // FTRL-Proximal (per-coordinate); w is kept materialised in the row.
-      float z = st[j];
-      const float n = st[dim + j];
-      const float n2 = n + g * g;
-      const float sigma = (std::sqrt(n2) - std::sqrt(n)) / op.ftrl_alpha;
-      z += g - sigma * w;
-      st[j] = z;
-      st[dim + j] = n2;
-      const float az = std::fabs(z);
-      row[j] = az <= op.l1 ? 0.0f
-                           : -(z - std::copysign(op.l1, z)) /
-                                 ((op.ftrl_beta + std::sqrt(n2)) / op.ftrl_alpha + op.l2);
+      const float n2 = s2 + g * g;
+      const float sigma = (std::sqrt(n2) - std::sqrt(s2)) / op.ftrl_alpha;
+      s1 += g - sigma * w;
+      s2 = n2;
+      const float az = std::fabs(s1);
+      w = az <= op.l1 ? 0.0f
+                      : -(s1 - std::copysign(op.l1, s1)) /
+                            ((op.ftrl_beta + std::sqrt(n2)) / op.ftrl_alpha + op.l2);
     } break;
     case kOptAdam: {
       g += op.l2 * w;
-      const float m = op.beta1 * st[j] + (1.f - op.beta1) * g;
-      const float v = op.beta2 * st[dim + j] + (1.f - op.beta2) * g * g;
-      st[j] = m;
-      st[dim + j] = v;
-      row[j] = w - op.lr * (m * op.bc1) / (std::sqrt(v * op.bc2) + op.eps);
+      s1 = op.beta1 * s1 + (1.f - op.beta1) * g;
+      s2 = op.beta2 * s2 + (1.f - op.beta2) * g * g;
+      w = w - op.lr * (s1 * op.bc1) / (std::sqrt(s2 * op.bc2) + op.eps);
     } break;
   }
+}
+
+// number of state floats per coordinate
+SS_HD int opt_state_per_coord(int kind) {
+  return kind == kOptSGD ? 0 : (kind == kOptAdaGrad ? 1 : 2);
+}
+
+SS_HD void opt_apply(const OptParams& op, float* row, float* st, uint32_t dim, uint32_t j,
+                     float g) {
+  const int ns = opt_state_per_coord(op.kind);
+  float w = row[j], s1 = ns > 0 ? st[j] : 0.f, s2 = ns > 1 ? st[dim + j] : 0.f;
+  opt_update(op, w, s1, s2, g);
+  row[j] = w;
+  if (ns > 0) st[j] = s1;
+  if (ns > 1) st[dim + j] = s2;
 }
 
 }  // namespace ss
