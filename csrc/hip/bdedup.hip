@@ -19,8 +19,8 @@
 //
 //   1 count    per <=8192-occurrence chunk: LDS histogram over buckets, stored
 //              chunk-major ([nch][P], coalesced)
-//   2 colscan  per-bucket exclusive scan down the chunks + bucket totals
-//   3 bstart   bucket start offsets (one workgroup)
+//   2 colscan  per-bucket exclusive scan down the chunks + bucket totals; the
+//              last workgroup to finish scans those into bucket start offsets
 //   4 scatter  bucket-ordered occurrence list pj[pos] = j; pos_of[j] and the
 //              bucket bkt[j] (both coalesced)
 //   5 dedup    one workgroup per bucket: LDS hash insert + compaction; writes
@@ -401,7 +401,8 @@ __global__ __launch_bounds__(256) void k_bd_inv(BdIndex ix, long long n,
 // of its unique keys in LDS — per-occurrence g = gs[j / F] * x[j] gathered
 // from the per-sample gradient (L2-resident) — and stores each row once:
 // no zero-fill, no global atomics.
-__global__ __launch_bounds__(1024) void k_bd_reduce(const uint32_t* __restrict__ bstart,
+template <int RT>
+__global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ bstart,
                                                     const uint32_t* __restrict__ ubase,
                                                     const uint32_t* __restrict__ unum,
                                                     const uint32_t* __restrict__ pj,
@@ -412,9 +413,9 @@ __global__ __launch_bounds__(1024) void k_bd_reduce(const uint32_t* __restrict__
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
-  for (uint32_t l = threadIdx.x; l < nu; l += 1024) acc[l] = 0.f;
+  for (uint32_t l = threadIdx.x; l < nu; l += RT) acc[l] = 0.f;
   __syncthreads();
-  for (uint32_t p = p0 + threadIdx.x; p < p1; p += 1024) {
+  for (uint32_t p = p0 + threadIdx.x; p < p1; p += RT) {
     const uint32_t l = luid[p];  // bucket-local unique id
     if (l != kBdInvalid) {
       const uint32_t j = pj[p];
@@ -423,7 +424,7 @@ __global__ __launch_bounds__(1024) void k_bd_reduce(const uint32_t* __restrict__
     }
   }
   __syncthreads();
-  for (uint32_t l = threadIdx.x; l < nu; l += 1024) ugrad[base + l] = acc[l];
+  for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];
 }
 
 // K7 for FM rows [w | v_1..v_K]: per unique key u with occurrences in samples
@@ -539,7 +540,19 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
   const BdLayout L = bd_layout(n, nranks);
   const uint32_t* S = scratch;
-  hipLaunchKernelGGL(k_bd_reduce, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
+  // workgroup size (SS_BD_RT experiment knob): measured 1024 >= 512 >= 256
+  static const int rt = [] {
+    const char* e = std::getenv("SS_BD_RT");
+    return e ? std::atoi(e) : 1024;
+  }();
+  if (rt == 1024)
+    hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
+                       S + L.unum, pj, luid, gs, xval, F, ugrad);
+  else if (rt == 512)
+    hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
+                       S + L.unum, pj, luid, gs, xval, F, ugrad);
+  else
+    hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
                      S + L.unum, pj, luid, gs, xval, F, ugrad);
   check_launch("k_bd_reduce");
 }
