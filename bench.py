@@ -76,7 +76,7 @@ def main(argv=None):
     from swiftsnails_amd.parallel.engine import PSEngine
     from swiftsnails_amd.parallel.transport import LoopbackTransport, RcclTransport
 
-    ctrans = None
+    ctrans = ptrans = None
     if world > 1:
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -91,6 +91,7 @@ def main(argv=None):
                 # the route stage + pull-ahead (route stream)
                 transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
                 ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts")
+                ptrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_pull")
         except Exception as e:  # pragma: no cover - hardware dependent
             from swiftsnails_amd.parallel.transport import TorchDistTransport
 
@@ -105,14 +106,14 @@ def main(argv=None):
     opt = Optimizer(a.optimizer, lr=a.lr)
     table = make_lr_table(a.features, world, optimizer=opt, load=a.load, device=dev)
     engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev,
-                      count_transport=ctrans)
+                      count_transport=ctrans, pull_transport=ptrans)
     worker = SparseLRWorker(engine, data, rank=rank, world=world, grad_mode=a.grad_mode)
 
     # a wedged collective ends the job (exit 3) instead of hanging the node
     from swiftsnails_amd.parallel.watchdog import FailureHandler, Watchdog
 
     failure = FailureHandler()
-    for t in (transport, ctrans):
+    for t in (transport, ctrans, ptrans):
         if hasattr(t, "abort"):
             failure.add_hook(t.abort)
     wd = Watchdog(float(os.environ.get("SS_BENCH_ROUND_TIMEOUT", "300")), failure, name="bench")

@@ -63,7 +63,7 @@ class PSContext:
         self.workers = _ranks(cfg.get("worker_ranks"), self.world)
         self.is_server = self.rank in self.servers
         self.is_worker = self.rank in self.workers
-        ct = None
+        ct = pt = None
         store = None
         if self.world > 1:
             os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
@@ -80,6 +80,8 @@ class PSContext:
                                    prefix="ss_data")
                 ct = RcclTransport(self.rank, self.world, self.device, store=store,
                                    prefix="ss_counts")
+                pt = RcclTransport(self.rank, self.world, self.device, store=store,
+                                   prefix="ss_pull")
             else:
                 tr = TorchDistTransport()
         else:
@@ -90,14 +92,14 @@ class PSContext:
         self.engine = PSEngine(self.table, tr, max_keys=max_keys, dim=dim,
                                frag_num=int(cfg.get("frag_num", 0) or 0),
                                server_ranks=self.servers, device=self.device,
-                               count_transport=ct)
+                               count_transport=ct, pull_transport=pt)
         self.backup_period = int(cfg.get("param_backup_period", 0) or 0)
         self.backup_root = cfg.get("param_backup_root", ".")
         self.ckpt_format = cfg.get("checkpoint_format", "bin")
         self.tracer = Tracer(enabled=str(cfg.get("trace", "0")) not in ("0", "false"))
         # failure detection (parallel/watchdog.py): round watchdog + heartbeats
         self.failure = FailureHandler(exit_process=str(cfg.get("watchdog_exit", "1")) != "0")
-        for t in (tr, ct):
+        for t in (tr, ct, pt):
             if hasattr(t, "abort"):
                 self.failure.add_hook(t.abort)
         rt = float(cfg.get("round_timeout", 600) or 0)

@@ -110,9 +110,14 @@ class PSEngine:
     def __init__(self, table, transport: Optional[Transport], max_keys: int, dim: int,
                  frag_num: int = 0, server_ranks: Optional[Sequence[int]] = None, device=None,
                  count_transport: Optional[Transport] = None, depth: Optional[int] = None,
+                 pull_transport: Optional[Transport] = None,
                  zero_grad: bool = True):
         self.t = transport or LoopbackTransport()
         self.ct = count_transport or self.t
+        # pull-ahead collectives get their own communicator (one stream per
+        # communicator: RCCL operations of one communicator must not run
+        # concurrently on two streams)
+        self.pt = pull_transport or self.ct
         self.rank, self.world = self.t.rank, self.t.world
         self.table = table
         self.dim = int(dim)
@@ -185,6 +190,10 @@ class PSEngine:
         # (SURVEY X3).  Needs ring depth >= 3 (rounds i, i+1, i+2 in flight).
         self.pull_ahead = (self.gpu and not self.fast1 and self.depth >= 3 and
                            os.environ.get("SS_PULL_AHEAD", "1") != "0")
+        # a third stream for the pulled-ahead round: its collectives wait on the
+        # network while the route stream dedups and the main stream computes
+        self.pull_stream = (torch.cuda.Stream(device=self.device)
+                            if self.pull_ahead and self.pt is not self.ct else None)
 
     # ------------------------------------------------------------ stage 1
     def route(self, keys: Optional[torch.Tensor] = None, produce=None, post=None) -> Routed:
@@ -278,13 +287,16 @@ class PSEngine:
         current (main) stream wait for them."""
         dd, slot = r.dd, r.slot
         scounts, rcounts = r.counts.wait()  # host: the route stage enqueued earlier
-        rs, D, uv = self.route_stream, self.displs, self.uvals[slot]
-        with torch.cuda.stream(rs):
-            self.ct.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
+        D, uv = self.displs, self.uvals[slot]
+        ps = self.pull_stream or self.route_stream
+        if ps is not self.route_stream:
+            ps.wait_event(r.ready)
+        with torch.cuda.stream(ps):
+            self.pt.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
             self._server_pull(rcounts, slot)
-            self.ct.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
+            self.pt.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
             ev = torch.cuda.Event()
-            ev.record(rs)
+            ev.record(ps)
         sent, recv = int(scounts.sum()), int(rcounts.sum())
         self.metrics.add(occurrences=dd.n, unique_sent=sent, unique_recv=recv,
                          a2a_bytes=8 * (sent + recv) + 4 * self.dim * (2 * sent + 2 * recv))
