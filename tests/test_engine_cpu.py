@@ -94,6 +94,8 @@ def _free_port():
     (3, [0, 1, 2], [0, 1, 2], "sgd"),
     (3, [0], [1, 2], "adagrad"),      # split: 1 server + 2 workers
     (3, [1, 2], [0], "ftrl"),         # split: 2 servers + 1 worker
+    (4, [0, 1], [2, 3], "adam"),      # split: 2 servers + 2 workers (BASELINE config 3 shape)
+    (8, list(range(8)), list(range(8)), "adagrad"),  # the 8-rank colocated layout of the bench
 ])
 def test_engine_multiprocess_gloo(world, servers, workers, opt):
     ctx = mp.get_context("spawn")
