@@ -62,8 +62,7 @@ static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in 
 static constexpr int kBdMaxBuckets = 16384;
 
 __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs, uint32_t Pd) {
-  const uint32_t d =
-      rs.nranks == 1 ? 0u : (uint32_t)rs.frag_map[fmix64(key) % (uint64_t)rs.frag_num];
+  const uint32_t d = rs.dest_of(key);
   const uint32_t h = (uint32_t)(dedup_hash(key) >> 32);
   return d * Pd + __umulhi(h, Pd);
 }

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void k_dedup_insert(const uint64_t* __restrict
         s = (s + 1) & smask;
       }
       slot_of[i] = (uint32_t)s | (won ? kWinBit : 0u);
-      if (won) dest = rs.nranks == 1 ? 0 : rs.frag_map[fmix64(key) % (uint64_t)rs.frag_num];
+      if (won) dest = (int)rs.dest_of(key);
     }
   }
   unsigned int loff = 0;
@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void k_dedup_finish(const uint64_t* __restrict
 __global__ __launch_bounds__(256) void k_route_keys(const uint64_t* __restrict__ keys, long long n,
                                                     RouteSpec rs, int* __restrict__ dest) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) dest[i] = rs.frag_map[fmix64(keys[i]) % (uint64_t)rs.frag_num];
+  if (i < n) dest[i] = rs.frag_map[rs.frag_of(fmix64(keys[i]))];
 }
 
 // Row gather through an index (model side of K6): out[i] = src[idx[i]].

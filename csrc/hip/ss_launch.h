@@ -49,6 +49,16 @@ struct RouteSpec {
   const int* frag_map;  // frag -> destination rank (device)
   int frag_num;
   int nranks;
+  // fragment of a key = fmix64(key) % frag_num (reference hashfrag.h:48-53);
+  // a 64-bit modulo is a long software sequence on the GPU, so power-of-two
+  // fragment counts (the default 1024) take the mask instead — same result
+  __host__ __device__ __forceinline__ uint32_t frag_of(uint64_t h) const {
+    return (frag_num & (frag_num - 1)) == 0 ? (uint32_t)(h & (uint64_t)(frag_num - 1))
+                                            : (uint32_t)(h % (uint64_t)frag_num);
+  }
+  __device__ __forceinline__ uint32_t dest_of(uint64_t key) const {
+    return nranks == 1 ? 0u : (uint32_t)frag_map[frag_of(fmix64(key))];
+  }
 };
 int dedup_blocks(long long n);
 void launch_dedup_route(const uint64_t* keys, long long n, uint64_t* scratch_keys,

@@ -109,9 +109,10 @@ def test_table_full_raises(dev):
 
 
 @pytest.mark.parametrize("mode", ["bucket", "hash"])
-@pytest.mark.parametrize("nranks,n", [(1, 20000), (3, 20000), (8, 20000), (1, 400000),
-                                      (3, 400000)])
-def test_dedup_route_matches_reference(dev, nranks, n, mode):
+@pytest.mark.parametrize("nranks,n,frags", [(1, 20000, 97), (3, 20000, 97), (8, 20000, 97),
+                                            (8, 20000, 128), (1, 400000, 97),
+                                            (3, 400000, 1024)])
+def test_dedup_route_matches_reference(dev, nranks, n, frags, mode):
     from swiftsnails_amd.ops.dedup import Deduper, dedup_reference
     from swiftsnails_amd.parallel.router import HashFrag
 
@@ -120,7 +121,7 @@ def test_dedup_route_matches_reference(dev, nranks, n, mode):
         k = rng.integers(0, 5000, size=n, dtype=np.int64)  # heavy duplication
     else:  # many buckets, Zipf hot keys, long tail
         k = (rng.zipf(1.2, n) * 7919 % 2_000_003).astype(np.int64)
-    hf = HashFrag(nranks, 97)
+    hf = HashFrag(nranks, frags)  # 97: modulo routing; powers of two: masked routing
     fm = hf.rank_map()
     d = Deduper(n + 5000, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=2,
                 device=dev, mode=mode)
