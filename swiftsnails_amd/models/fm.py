@@ -45,6 +45,9 @@ class FMWorker(PipelinedWorker):
             raise ValueError("FMWorker: dim must be 1+K with K in {1,4,8,16}")
         super().__init__(engine, rank, world, active)
         self.data = data
+        # the route stream is the light one for this model: pull the next
+        # round's rows behind its dedup (bounded staleness 1)
+        engine.enable_pull_ahead()
         dev = engine.device
         B, F = data.batch_size, data.num_fields
         self.keys = [torch.empty(B * F, dtype=torch.int64, device=dev) for _ in range(engine.depth)]

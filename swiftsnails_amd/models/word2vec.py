@@ -77,6 +77,9 @@ class Word2VecWorker(PipelinedWorker):
             raise ValueError("Word2VecWorker: dim must be 32, 64 or 128")
         super().__init__(engine, rank, world, active)
         self.data = data
+        # the route stream is the light one for this model: pull the next
+        # round's rows behind its dedup (bounded staleness 1)
+        engine.enable_pull_ahead()
         self.keys = [torch.empty(data.n_keys, dtype=torch.int64, device=engine.device)
                      for _ in range(engine.depth)]
 

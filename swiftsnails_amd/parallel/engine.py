@@ -190,6 +190,10 @@ class PSEngine:
         # (SURVEY X3).  Needs ring depth >= 3 (rounds i, i+1, i+2 in flight).
         self.pull_ahead = (self.gpu and not self.fast1 and self.depth >= 3 and
                            os.environ.get("SS_PULL_AHEAD", "1") != "0")
+        # on one GPU pull-ahead moves the table lookup onto the route stream;
+        # a model whose route stream is light (FM, word2vec) opts in with
+        # enable_pull_ahead(), sparse LR (route stream already the longer one)
+        # does not
         # a third stream for the pulled-ahead round: its collectives wait on the
         # network while the route stream dedups and the main stream computes
         self.pull_stream = (torch.cuda.Stream(device=self.device)
@@ -286,6 +290,19 @@ class PSEngine:
         Round whose rows are ready at ``rnd.ready``; ``begin(rnd)`` makes the
         current (main) stream wait for them."""
         dd, slot = r.dd, r.slot
+        if self.fast1:  # one GPU: pull right behind the dedup on the route stream
+            rs, uv, tab = self.route_stream, self.uvals[slot], self.table
+            with torch.cuda.stream(rs):
+                own = dd.owner
+                if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
+                    tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot])
+                else:
+                    tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
+                             segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
+                ev = torch.cuda.Event()
+                ev.record(rs)
+            self.metrics.add(occurrences=dd.n)
+            return Round(dd, uv, slot, slots=self.slots[slot], ready=ev)
         scounts, rcounts = r.counts.wait()  # host: the route stage enqueued earlier
         D, uv = self.displs, self.uvals[slot]
         ps = self.pull_stream or self.route_stream
@@ -302,6 +319,15 @@ class PSEngine:
                          a2a_bytes=8 * (sent + recv) + 4 * self.dim * (2 * sent + 2 * recv))
         return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
                      stats={"sent": sent, "recv": recv}, ready=ev)
+
+    def enable_pull_ahead(self, on: bool = True) -> bool:
+        """Opt into pull-ahead (staleness 1) where the engine supports it."""
+        if on and self.gpu and self.depth >= 3 and \
+                os.environ.get("SS_PULL_AHEAD", "1") != "0":
+            self.pull_ahead = True
+        elif not on:
+            self.pull_ahead = False
+        return self.pull_ahead
 
     def begin(self, rnd: Round) -> None:
         if rnd.ready is not None:
