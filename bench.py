@@ -100,6 +100,10 @@ def main(argv=None):
             transport = TorchDistTransport(dist.new_group(backend="nccl"))
     else:
         transport = LoopbackTransport()
+        if os.environ.get("SS_ENGINE_GENERAL", "0") != "0":
+            # the N>1 engine path on one GPU: one loopback per stream, as the
+            # three RCCL communicators of a multi-GPU run
+            ctrans, ptrans = LoopbackTransport(), LoopbackTransport()
 
     data = CtrSynth(batch_size=a.batch, num_fields=a.fields, num_features=a.features,
                     tail_frac=a.tail)
@@ -145,6 +149,8 @@ def main(argv=None):
     elapsed = float(t.item())
     table.check()
     last_loss = worker.mean_loss()
+    # unique keys per step this rank routed (mean over the ring slots)
+    uniq = sum(int(dd.ucount.sum()) for dd in engine.dedupers) // len(engine.dedupers)
     keys_in_table = torch.tensor([table.size()], dtype=torch.int64)
     if world > 1:
         dist.all_reduce(keys_in_table)
@@ -176,6 +182,7 @@ def main(argv=None):
                                    else ")")),
                 "optimizer": a.optimizer,
                 "keys_per_step_per_gpu": a.batch * a.fields,
+                "unique_keys_per_step_per_gpu": uniq,
                 "table_keys": int(keys_in_table.item()),
                 "loss_first": round(first_loss, 5),
                 "loss_last": round(last_loss, 5),

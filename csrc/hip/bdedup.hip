@@ -67,6 +67,16 @@ __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs,
   return d * Pd + __umulhi(h, Pd);
 }
 
+// upper bound on count/scatter chunks (SS_BD_NCH experiment knob, 2 per CU)
+static long long bd_max_chunks() {
+  static const long long v = [] {
+    const char* e = std::getenv("SS_BD_NCH");
+    const long long x = e ? std::atoll(e) : 512;
+    return x < 64 ? 64 : x;
+  }();
+  return v;
+}
+
 // ---- layout of the int scratch (u32 words), a function of (n, nranks) only
 struct BdLayout {
   int P, Pd, nch, chunk;
@@ -83,10 +93,17 @@ static BdLayout bd_layout(long long n, int nranks) {
   if (pd < 1) pd = 1;
   L.Pd = (int)pd;
   L.P = (int)(pd * nranks);
-  // chunk count a multiple of the 256 CUs (balanced waves), chunk <= 8192
+  // chunk count a multiple of the 256 CUs (balanced waves), chunk <= 8192 ...
   const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
   const long long per = (n + 256 * waves - 1) / (256 * waves);
-  L.chunk = (int)(((per + kBdChunkLanes - 1) / kBdChunkLanes) * kBdChunkLanes);
+  long long chunk = ((per + kBdChunkLanes - 1) / kBdChunkLanes) * kBdChunkLanes;
+  // ... but at most bd_max_chunks() chunks: the [nch][P] histogram grows as
+  // n^2 (P ~ n/2048 buckets per chunk row), 25 MB at n = 10M with 8192-key
+  // chunks; bigger chunks loop over 8192-key register tiles instead
+  const long long cmax = bd_max_chunks();
+  if ((n + chunk - 1) / chunk > cmax)
+    chunk = (((n + cmax - 1) / cmax + kBdChunkLanes - 1) / kBdChunkLanes) * kBdChunkLanes;
+  L.chunk = (int)chunk;
   L.nch = (int)((n + L.chunk - 1) / L.chunk);
   if (L.nch < 1) L.nch = 1;
   // words 0, 1: sticky error flag and the colscan arrival counter, at fixed
@@ -103,8 +120,19 @@ static BdLayout bd_layout(long long n, int nranks) {
   return L;
 }
 
+// words for ANY call of up to n keys: the layout is not monotonic in n (the
+// bucket target grows with n below 2M keys, the chunk count jumps with the
+// wave count), so bound P and nch over all m <= n instead of sizing for n
 long long bd_scratch_words(long long n, int nranks) {
-  return bd_layout(n < 1 ? 1 : n, nranks).total;
+  if (n < 1) n = 1;
+  long long pmax = std::max<long long>(1056, (n + kBdTarget - 1) / kBdTarget);
+  pmax = std::min<long long>(pmax, kBdMaxBuckets) + 2 * nranks;
+  const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
+  long long nchmax = std::min<long long>(256 * waves, bd_max_chunks());
+  nchmax = std::min<long long>(nchmax, (n + kBdChunkLanes - 1) / kBdChunkLanes);
+  nchmax = std::max<long long>(nchmax, 1);
+  const long long bound = 2 + pmax * nchmax + 4 * pmax + 1;
+  return std::max(bound, bd_layout(n, nranks).total);
 }
 int bd_buckets(long long n, int nranks) { return bd_layout(n < 1 ? 1 : n, nranks).P; }
 // (P, bstart, unum, ubase) word offsets into the scratch for a call of n keys
@@ -124,17 +152,21 @@ __global__ __launch_bounds__(CT) void k_bd_count(const uint64_t* __restrict__ ke
   extern __shared__ unsigned int h[];
   for (int b = threadIdx.x; b < P; b += CT) h[b] = 0u;
   __syncthreads();
-  const long long base = (long long)blockIdx.x * chunk + threadIdx.x;
-  const int per = chunk / CT;
-  uint64_t k[(kBdMaxChunk / CT)];
+  // the chunk in register tiles of <= kBdMaxChunk keys (all loads of a tile
+  // in flight together)
+  for (int t0 = 0; t0 < chunk; t0 += kBdMaxChunk) {
+    const long long base = (long long)blockIdx.x * chunk + t0 + threadIdx.x;
+    const int per = min(chunk - t0, kBdMaxChunk) / CT;
+    uint64_t k[(kBdMaxChunk / CT)];
 #pragma unroll
-  for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
-    const long long j = base + e * CT;
-    k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
+    for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
+      const long long j = base + e * CT;
+      k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
+    }
+#pragma unroll
+    for (int e = 0; e < (kBdMaxChunk / CT); ++e)
+      if (k[e] != kEmptyKey) atomicAdd(&h[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
   }
-#pragma unroll
-  for (int e = 0; e < (kBdMaxChunk / CT); ++e)
-    if (k[e] != kEmptyKey) atomicAdd(&h[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
   __syncthreads();
   uint32_t* row = hist + (long long)blockIdx.x * P;
   for (int b = threadIdx.x; b < P; b += CT) row[b] = h[b];
@@ -213,27 +245,29 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
   for (int b = threadIdx.x; b < P; b += CT) cur[b] = bstart[b] + row[b];
-  const long long base = (long long)c * chunk + threadIdx.x;
-  const int per = chunk / CT;
-  uint64_t k[(kBdMaxChunk / CT)];
+  for (int t0 = 0; t0 < chunk; t0 += kBdMaxChunk) {
+    const long long base = (long long)c * chunk + t0 + threadIdx.x;
+    const int per = min(chunk - t0, kBdMaxChunk) / CT;
+    uint64_t k[(kBdMaxChunk / CT)];
 #pragma unroll
-  for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
-    const long long j = base + e * CT;
-    k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
-  }
-  __syncthreads();
+    for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
+      const long long j = base + e * CT;
+      k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
+    }
+    __syncthreads();  // first tile: cursors initialised
 #pragma unroll
-  for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
-    const long long j = base + e * CT;
-    if (e < per && j < n) {
-      uint32_t pos = kBdInvalid, b = kBdInvalid;
-      if (k[e] != kEmptyKey) {
-        b = bd_bucket(k[e], rs, (uint32_t)Pd);
-        pos = atomicAdd(&cur[b], 1u);
-        pj[pos] = (uint32_t)j;
+    for (int e = 0; e < (kBdMaxChunk / CT); ++e) {
+      const long long j = base + e * CT;
+      if (e < per && j < n) {
+        uint32_t pos = kBdInvalid, b = kBdInvalid;
+        if (k[e] != kEmptyKey) {
+          b = bd_bucket(k[e], rs, (uint32_t)Pd);
+          pos = atomicAdd(&cur[b], 1u);
+          pj[pos] = (uint32_t)j;
+        }
+        pos_of[j] = pos;
+        bkt[j] = b;
       }
-      pos_of[j] = pos;
-      bkt[j] = b;
     }
   }
 }

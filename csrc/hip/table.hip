@@ -117,9 +117,20 @@ __global__ __launch_bounds__(256) void k_gather(DevTable t, const long long* __r
   }
 }
 
-// K3+K4 fused, for key lists known to be unique within the launch (the
-// worker's dedup output on the colocated 1-GPU path): probe, init if new,
-// and emit the row without a second pass.
+// A row read by a lane that FOUND its key may belong to a key another lane of
+// the same launch is inserting right now (duplicate keys: the server side of
+// an N>1 pull receives the same key from several workers).  Empty slots hold
+// the 0xFF fill, so a coordinate still reading 0xFFFFFFFF has not been
+// initialised yet: substitute the deterministic initial value the inserting
+// lane is writing (init_value depends on (key, j) only).  No arithmetic NaN
+// has this bit pattern.
+__device__ __forceinline__ float fresh_or(float v, const InitParams& ip, uint64_t key, uint32_t j,
+                                          uint32_t dim) {
+  return __float_as_uint(v) == 0xFFFFFFFFu ? init_value(ip, key, j, dim) : v;
+}
+
+// K3+K4 fused: probe, init if new, and emit the row without a second pass.
+// Duplicate keys within the launch are safe (CAS claim + fresh_or above).
 // one key of a unique-key pull: probe (insert if new) by the group leader,
 // init the row if it was inserted, emit the row to out[pos]
 template <int G>
@@ -163,10 +174,10 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
 #pragma unroll
       for (int r = 0; r < kApplyRegs; ++r) {
         const uint32_t j = lg + r * G;
-        if (j < t.dim) o[j] = v[r];
+        if (j < t.dim) o[j] = fresh_or(v[r], ip, key, j, t.dim);
       }
     } else {
-      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = fresh_or(row[j], ip, key, j, t.dim);
     }
   }
   ins += (lg == 0 && inserted);

@@ -159,7 +159,10 @@ class HbmTable:
         if slots is None:
             slots = torch.empty(keys.numel(), dtype=torch.int64, device=self.device)
         sl = segs if segs is not None else self._seg(keys.numel())
-        if unique and insert:
+        # the CAS-insert fused kernel is also correct for duplicate keys (a
+        # lane reading a row another lane is initialising substitutes the
+        # deterministic init value); the claim insert needs unique keys
+        if insert and (unique or self.insert_mode == "cas"):
             fn = h.pull_unique if self.insert_mode == "cas" else h.pull_claim
             fn(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), out.data_ptr(),
                self._init_native, self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, st)

@@ -154,7 +154,11 @@ class PSEngine:
         from ..utils.tracing import Metrics
 
         self.metrics = Metrics()
-        self.fast1 = self.gpu and self.world == 1
+        # SS_ENGINE_GENERAL=1 runs a 1-GPU job through the N>1 code path
+        # (send segments, count exchange, server-side segment pull/apply): the
+        # per-rank cost of the multi-GPU pipeline without the network
+        self.fast1 = (self.gpu and self.world == 1 and
+                      os.environ.get("SS_ENGINE_GENERAL", "0") == "0")
         if self.fast1:
             self.slots = [torch.empty(cap, dtype=torch.int64, device=dev)
                           for _ in range(self.depth)]

@@ -81,6 +81,18 @@ class LoopbackTransport(Transport):
         c = send_counts.detach().cpu().numpy().astype(np.int64)
         return c, c.copy()
 
+    def exchange_counts_async(self, send_counts, pinned=None, stream=None):
+        if send_counts.device.type != "cuda" or pinned is None:
+            return super().exchange_counts_async(send_counts, pinned, stream)
+        # GPU: D2H into pinned memory on `stream`, the host waits in wait()
+        st = stream or torch.cuda.current_stream()
+        with torch.cuda.stream(st):
+            pinned[:1].copy_(send_counts.to(torch.int64)[:1], non_blocking=True)
+            pinned[1:2].copy_(send_counts.to(torch.int64)[:1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(st)
+        return CountsHandle(event=ev, pinned=pinned, world=1)
+
     def alltoallv(self, send, scounts, sdispls, recv, rcounts, rdispls, row_elems=1):
         n = int(scounts[0]) * row_elems
         if n and (send.data_ptr() != recv.data_ptr() or sdispls[0] != rdispls[0]):

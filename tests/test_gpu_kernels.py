@@ -59,6 +59,36 @@ def test_probe_duplicates_same_slot(dev, G):
         assert len(set(sn[idx].tolist())) == 1
 
 
+@pytest.mark.parametrize("G,dim", [(1, 1), (4, 8), (16, 16), (64, 33)])
+def test_pull_duplicates_see_initialised_rows(dev, G, dim):
+    """Non-unique fused pull (the N>1 server side gets a key from several
+    workers): every occurrence of a key created in this launch must read the
+    initial row, never the 0xFF fill of the empty slot."""
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer, init_reference
+    from swiftsnails_amd.ops.table import HbmTable
+
+    init = InitConfig("uniform", scale=0.5, seed=11)
+    t = HbmTable(dim, 1 << 15, optimizer=Optimizer("adagrad"), init=init, device=dev,
+                 lane_group=G)
+    base = np.unique(_keys(4000, 5))
+    rng = np.random.default_rng(3)
+    # every key 1-8 times, shuffled: duplicates land in the same wavefront
+    k = np.repeat(base, rng.integers(1, 9, size=len(base)))
+    rng.shuffle(k)
+    old = base[:500]  # a third of the keys exist before the launch
+    t.pull(torch.from_numpy(old).to(dev), unique=True)
+    v, s = t.pull(torch.from_numpy(k).to(dev), unique=False)
+    torch.cuda.synchronize()
+    t.check()
+    assert t.size() == len(base)
+    ref = init_reference(init, k, dim, t.width)[:, :dim]
+    np.testing.assert_array_equal(v.cpu().numpy(), ref)
+    sn = s.cpu().numpy()
+    first = {}
+    for key, sl in zip(k.tolist(), sn.tolist()):
+        assert first.setdefault(key, sl) == sl
+
+
 @pytest.mark.parametrize("kind", ["sgd", "adagrad", "ftrl", "adam"])
 @pytest.mark.parametrize("dim", [1, 8, 33])
 def test_apply_matches_reference(dev, kind, dim):

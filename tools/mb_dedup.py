@@ -52,13 +52,8 @@ def main():
                 # bstart follows hist [nch*P] and btot [P] in the scratch (see bdedup.hip)
                 sizes = None
                 try:
-                    import math
-                    waves = math.ceil(n / (256 * 8192))
-                    per = math.ceil(n / (256 * waves))
-                    chunk = ((per + 1023) // 1024) * 1024
-                    nch = math.ceil(n / chunk)
-                    off = 1 + nch * P + P
-                    bs = d.scratch[off:off + P + 1].cpu().numpy().astype(np.int64)
+                    _, o_bs, _, _ = h.bd_offsets(n, 1)
+                    bs = d.scratch[o_bs:o_bs + P + 1].cpu().numpy().astype(np.int64)
                     sizes = np.diff(bs)
                 except Exception as ex:  # layout drift: skip the stats
                     line += f" (no stats: {ex})"
