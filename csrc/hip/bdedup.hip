@@ -462,10 +462,14 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
 
 // K7 for FM rows [w | v_1..v_K]: per unique key u with occurrences in samples
 // S(u):  grad = [G0, G_f - v_uf * G0],  G0 = sum gs[s],  G_f = sum gss[s][f].
-// Columns are accumulated in LDS a few at a time (kFmCols per pass over the
-// bucket's occurrences, which are L2-resident), so any unique count up to the
-// 4096-slot table fits; each row is then stored once.
-static constexpr int kFmCols = 3;
+// Columns are accumulated in LDS, as many per pass over the bucket's
+// occurrences (L2-resident) as fit next to G0 in 160 KB: every column in one
+// pass up to K = 8 (9 x 16 KB), so the occurrence list is read once; then
+// each row is stored once.
+template <int K>
+struct FmCols {
+  static constexpr int v = (K + 1) * kBdTS * 4 <= 150 * 1024 ? K : 8;
+};
 template <int DIM>
 __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ ubase,
@@ -477,15 +481,16 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
                                                        const float* __restrict__ uvals,
                                                        float* __restrict__ ugrad) {
   constexpr int K = DIM - 1;
+  constexpr int NC = FmCols<K>::v;
   __shared__ float g0[kBdTS];
-  __shared__ float acc[kFmCols][kBdTS];
+  __shared__ float acc[NC][kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
-  for (int c0 = 0; c0 < K; c0 += kFmCols) {
+  for (int c0 = 0; c0 < K; c0 += NC) {
     for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
       if (c0 == 0) g0[l] = 0.f;
 #pragma unroll
-      for (int c = 0; c < kFmCols; ++c) acc[c][l] = 0.f;
+      for (int c = 0; c < NC; ++c) acc[c][l] = 0.f;
     }
     __syncthreads();
     for (uint32_t p = p0 + threadIdx.x; p < p1; p += 1024) {
@@ -493,9 +498,12 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
       if (l == kBdInvalid) continue;
       const uint32_t s = pj[p] / (uint32_t)F;
       if (c0 == 0) atomicAdd(&g0[l], gs[s]);
+      float v[NC];  // the sample's factor-gradient columns, loaded together
 #pragma unroll
-      for (int c = 0; c < kFmCols; ++c)
-        if (c0 + c < K) atomicAdd(&acc[c][l], gss[(size_t)s * K + c0 + c]);
+      for (int c = 0; c < NC; ++c) v[c] = c0 + c < K ? gss[(size_t)s * K + c0 + c] : 0.f;
+#pragma unroll
+      for (int c = 0; c < NC; ++c)
+        if (c0 + c < K) atomicAdd(&acc[c][l], v[c]);
     }
     __syncthreads();
     for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
@@ -503,7 +511,7 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
       const float G0 = g0[l];
       if (c0 == 0) ugrad[r] = G0;
 #pragma unroll
-      for (int c = 0; c < kFmCols; ++c)
+      for (int c = 0; c < NC; ++c)
         if (c0 + c < K) ugrad[r + 1 + c0 + c] = acc[c][l] - uvals[r + 1 + c0 + c] * G0;
     }
     __syncthreads();

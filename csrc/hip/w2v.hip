@@ -30,6 +30,12 @@ static constexpr uint32_t kInv = 0xFFFFFFFFu;
 static constexpr int kT = 64;  // centers per tile
 static constexpr int kS = 64;  // shared negatives per tile
 static constexpr int kMaxC = 16;  // contexts per center held in registers (window <= 8)
+// 8 waves per workgroup: the LDS tiles (~116 KB at D = 128) allow one
+// workgroup per CU, and the positive-pair loop is a per-wave latency chain
+// (one context-row round trip per center), so 8 waves halve it per wave and
+// double the loads in flight per CU (4 waves: 223 us per 16K-center step)
+static constexpr int kNW = 8;
+static constexpr int kWG = 64 * kNW;
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ float softplus(float x) {
@@ -42,7 +48,7 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x))
 __device__ __forceinline__ int mrow(int r, int lane) { return (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5); }
 
 template <int D>
-__global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ inv_c,
+__global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ inv_c,
                                                   const uint32_t* __restrict__ inv_x,
                                                   const uint32_t* __restrict__ inv_n, int B, int C,
                                                   float neg_scale, const float* __restrict__ uvals,
@@ -54,7 +60,7 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
   float* Ns = Vs + kT * P;       // [S][P] negative rows
   float* Gv = Ns + kS * P;       // [T][P] positive-part center grads
   float* Gs = Gv + kT * P;       // [T][S+1] negative score grads
-  float* red = Gs + kT * (kS + 1);  // [4] loss partials
+  float* red = Gs + kT * (kS + 1);  // [kNW] loss partials
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long long t0 = (long long)blockIdx.x * kT;
@@ -63,7 +69,7 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
   else if (tid < kT + kS) rn[tid - kT] = inv_n[(long long)blockIdx.x * kS + (tid - kT)];
   __syncthreads();
   // gather center / negative rows into LDS, zero the positive-grad tile
-  for (int e = tid; e < kT * D; e += 256) {
+  for (int e = tid; e < kT * D; e += kWG) {
     const int r = e / D, d = e - r * D;
     Vs[r * P + d] = rc[r] == kInv ? 0.f : uvals[(long long)rc[r] * D + d];
     Ns[r * P + d] = rn[r] == kInv ? 0.f : uvals[(long long)rn[r] * D + d];
@@ -72,8 +78,8 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
   __syncthreads();
 
   float loss = 0.f;
-  // ---- negative scores S = V·Nᵀ: wave w owns quadrant (w>>1, w&1)
-  {
+  // ---- negative scores S = V·Nᵀ: wave w < 4 owns quadrant (w>>1, w&1)
+  if (w < 4) {
     const int i0 = (w >> 1) * 32, j0 = (w & 1) * 32;
     f32x16 acc = {};
     const int ar = i0 + (lane & 31), kk = lane >> 5;
@@ -90,13 +96,14 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
       if (ok) loss += neg_scale * softplus(s);
     }
   }
-  // ---- positive pairs: wave w owns centers [16w, 16w+16).  All C context
+  // ---- positive pairs: wave w owns centers [kT/kNW * w, kT/kNW * (w+1)).  All C context
   // rows of a center are loaded before any is used (one memory round trip
   // per center instead of one per pair: the first version's per-pair loads
   // made this loop the kernel's latency chain, 160 dependent loads per wave).
   {
     constexpr int R = (D + 63) / 64;  // row floats per lane
-    for (int t = w * 16; t < w * 16 + 16; ++t) {
+    constexpr int TW = kT / kNW;
+    for (int t = w * TW; t < w * TW + TW; ++t) {
       if (rc[t] == kInv) continue;  // wave-uniform
       const uint32_t xid = lane < C ? inv_x[(t0 + t) * (long long)C + lane] : kInv;
       float u[kMaxC][R];
@@ -146,7 +153,7 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
   __syncthreads();
   // ---- gV = G·N (+ positive part) and gN = Gᵀ·V: (2 x D/32) tiles each
   constexpr int NT = 2 * (D / 32);
-  for (int tt = w; tt < 2 * NT; tt += 4) {
+  for (int tt = w; tt < 2 * NT; tt += kNW) {
     const bool center = tt < NT;
     const int q = center ? tt : tt - NT;
     const int ti = q / (D / 32), tj = q % (D / 32);
@@ -175,7 +182,12 @@ __global__ __launch_bounds__(256) void k_w2v_sgns(const uint32_t* __restrict__ i
   for (int o = 32; o > 0; o >>= 1) loss += __shfl_down(loss, o, 64);
   if (lane == 0) red[w] = loss;
   __syncthreads();
-  if (tid == 0 && loss_sum) ctr_addf(loss_sum, red[0] + red[1] + red[2] + red[3]);
+  if (tid == 0 && loss_sum) {
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kNW; ++i) tot += red[i];
+    ctr_addf(loss_sum, tot);
+  }
 }
 
 // Synthetic skip-gram batches. Centers are Zipf-like (log-uniform) over V
@@ -218,7 +230,7 @@ __global__ __launch_bounds__(256) void k_w2v_gen(uint64_t seed, long long base, 
 
 size_t w2v_smem_bytes(int D) {
   const int P = D + 1;
-  return sizeof(float) * ((size_t)3 * kT * P + (size_t)kT * (kS + 1) + 4);
+  return sizeof(float) * ((size_t)3 * kT * P + (size_t)kT * (kS + 1) + kNW);
 }
 
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
@@ -234,7 +246,7 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
     check_hip(hipFuncSetAttribute((const void*)k_w2v_sgns<DD>,                               \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm),    \
               "w2v smem attr");                                                             \
-    hipLaunchKernelGGL(k_w2v_sgns<DD>, dim3(tiles), dim3(256), sm, st, inv_c, inv_x, inv_n, B, C, \
+    hipLaunchKernelGGL(k_w2v_sgns<DD>, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, \
                        neg_scale, uvals, ugrad, loss_sum);                                  \
     break;
     SS_W2V_CASE(32)

@@ -5,8 +5,8 @@ OUT=${GRAFT_REPO_ROOT:-$(pwd)}/gpurun_out
 export TMPDIR=/tmp
 prof() {
   local name=$1; shift
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_$name" -o run \
-    -- python3 -m swiftsnails_amd.launch "$@" > "$OUT/prof_$name.log" 2>&1
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_${name}${SUFFIX:-}" -o run \
+    -- python3 -m swiftsnails_amd.launch "$@" > "$OUT/prof_${name}${SUFFIX:-}.log" 2>&1
   local rc=$?
   echo "$name rc=$rc"
   case $rc in 0|1|2) ;; *) exit $rc;; esac
