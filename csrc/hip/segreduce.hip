@@ -23,8 +23,12 @@
 //     reduce     one workgroup per work item: LDS atomics into 8192
 //                accumulators, then one coalesced row-shaped atomicAdd per
 //                touched unique key (full-rate atomic shape, ~10 MB/step)
+#include <cstdlib>
+#include <string>
+
 #include "sample_group.h"
 #include "scan.h"
+
 #include "ss_device.h"
 #include "ss_launch.h"
 
@@ -335,7 +339,17 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
     throw_error("lr_fwd_g: need inv or a complete BdIndex");
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("lr_fwd_g: F must be in [1,256]");
-  if (F <= kGroupMaxF) {
+  // layout: one sample per lane group unless that leaves over a quarter of
+  // the lanes idle (F = 39 -> 64-lane groups, 61% busy), then the packed one
+  // (256/F samples per workgroup, 91% busy at F = 39: 192 vs 202 us per 10.2M
+  // keys).  SS_LR_FWD=packed|group forces one (experiment knob).
+  static const int force = [] {
+    const char* e = std::getenv("SS_LR_FWD");
+    if (!e) return 0;
+    return std::string(e) == "packed" ? 1 : (std::string(e) == "group" ? 2 : 0);
+  }();
+  const bool packed = force == 1 || (force == 0 && 4 * F < 3 * group_lanes(F));
+  if (F <= kGroupMaxF && !packed) {
     const int L = group_lanes(F), spb = 256 / L;
     hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, ix, xval,
                        labels, B, F, L, uvals, gocc, per_sample, loss_sum, pred);
