@@ -27,6 +27,7 @@
 #include "host_table.h"
 #include "string_util.h"
 #include "transfer.h"
+#include "vec.h"
 
 namespace {
 
@@ -64,6 +65,55 @@ std::string tmpfile(const std::string& name, const std::string& body) {
 }  // namespace
 
 using namespace ss;
+
+// ---------------------------------------------------------------- Vec
+// (reference utils/vec1.h; its vec1_test.h only prints)
+TEST(vec_arithmetic_codec_text) {
+  Vec a{1, 2, 3}, b{4, 5, 6};
+  EXPECT(a.dot(b) == 32);
+  EXPECT((a + b) == (Vec{5, 7, 9}));
+  EXPECT((b - a) == (Vec{3, 3, 3}));
+  EXPECT((a * b) == (Vec{4, 10, 18}));
+  EXPECT((b / a) == (Vec{4, 2.5, 2}));
+  EXPECT((2.0 * a) == (Vec{2, 4, 6}));
+  EXPECT((a * 2.0) == (Vec{2, 4, 6}));
+  EXPECT((a + 1.0) == (Vec{2, 3, 4}));
+  EXPECT((1.0 - a) == (Vec{0, -1, -2}));
+  EXPECT((6.0 / a) == (Vec{6, 3, 2}));
+  EXPECT(sqrt(Vec{4, 9}) == (Vec{2, 3}));
+  Vec c = a;
+  c.axpy(-0.5, b);
+  EXPECT(c == (Vec{-1, -0.5, 0}));
+  auto o = outer(Vec{1, 2}, Vec{3, 4, 5});
+  EXPECT(o.size() == 2 && o[1] == (Vec{6, 8, 10}));
+  bool threw = false;
+  try {
+    a += Vec{1, 2};
+  } catch (const std::exception&) {
+    threw = true;
+  }
+  EXPECT(threw);
+  // random init: word2vec convention, |x| <= 0.5 / size, deterministic by seed
+  Vec r(64), r2(64);
+  r.rand_init(0.5, 7);
+  r2.rand_init(0.5, 7);
+  EXPECT(r == r2);
+  bool in_range = true;
+  for (size_t i = 0; i < r.size(); ++i) in_range &= std::fabs(r[i]) <= 0.5 / 64;
+  EXPECT(in_range);
+  r.reset();
+  EXPECT(r.size() == 64 && r.norm2() == 0);
+  // codec + text round trips (checkpoint line value part)
+  BinaryBuffer bb;
+  bb << a << Vec{} << b;
+  Vec x, y, z;
+  bb >> x >> y >> z;
+  EXPECT(x == a && y.empty() && z == b);
+  EXPECT(Vec::parse(Vec{0.25, -3, 1e-3}.to_string()) == (Vec{0.25, -3, 1e-3}));
+  std::ostringstream os;
+  os << Vec{1, 2.5};
+  EXPECT(os.str() == "1 2.5");
+}
 
 // ---------------------------------------------------------------- codec
 struct Apple {  // user struct with its own codec (Buffer_test.h:47-62)
