@@ -240,7 +240,8 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      const uint32_t* __restrict__ bstart,
                                                      uint32_t* __restrict__ pj,
                                                      uint32_t* __restrict__ pos_of,
-                                                     uint32_t* __restrict__ bkt) {
+                                                     uint32_t* __restrict__ bkt,
+                                                     uint32_t* __restrict__ osi_inv) {
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
@@ -264,9 +265,12 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
           b = bd_bucket(k[e], rs, (uint32_t)Pd);
           pos = atomicAdd(&cur[b], 1u);
           pj[pos] = (uint32_t)j;
+        } else if (osi_inv) {
+          osi_inv[j] = kBdInvalid;  // never reaches a bucket
         }
-        pos_of[j] = pos;
-        bkt[j] = b;
+        // the BdIndex (j -> bucket position, bucket) only for its consumers
+        if (pos_of) pos_of[j] = pos;
+        if (bkt) bkt[j] = b;
       }
     }
   }
@@ -284,6 +288,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    int nranks, long long ucap,
                                                    uint32_t* __restrict__ ubase,
                                                    unsigned long long* __restrict__ ucount,
+                                                   uint32_t* __restrict__ osi_inv,
                                                    unsigned long long* __restrict__ dbg) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
@@ -299,12 +304,13 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   // the first kBdRegs occurrences of each thread keep their slot in
   // registers; a hot bucket's excess parks it in luid[] (rewritten below)
-  uint32_t slot[kBdRegs];
+  uint32_t slot[kBdRegs], jr[kBdRegs];
   uint64_t kk[kBdRegs];
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
     const uint32_t p = p0 + t + r * kBdDT;
-    kk[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
+    jr[r] = p < p1 ? pj[p] : 0u;
+    kk[r] = p < p1 ? keys[jr[r]] : kEmptyKey;
   }
   __syncthreads();
   BD_STAMP(0)
@@ -364,14 +370,25 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   }
   __syncthreads();
   BD_STAMP(2)
+  // osi_inv: the inverse index in OCCURRENCE-SPACE ids (unique key l of
+  // bucket b -> bstart[b] + l, known here without the global scan): one
+  // random 4-B store per occurrence, which the LR forward then reads
+  // coalesced instead of gathering luid[pos_of[j]] (a 64-B line per
+  // occurrence; stores move 32-B sectors, measured FETCH/WRITE_SIZE)
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
     const uint32_t p = p0 + t + r * kBdDT;
-    if (p < p1) luid[p] = slot[r] == kBdInvalid ? kBdInvalid : lid[slot[r]];
+    if (p < p1) {
+      const uint32_t l = slot[r] == kBdInvalid ? kBdInvalid : lid[slot[r]];
+      luid[p] = l;
+      if (osi_inv) osi_inv[jr[r]] = l == kBdInvalid ? kBdInvalid : p0 + l;
+    }
   }
   for (uint32_t p = p0 + t + kBdRegs * kBdDT; p < p1; p += kBdDT) {
     const uint32_t s = luid[p];
-    luid[p] = s == kBdInvalid ? kBdInvalid : lid[s];
+    const uint32_t l = s == kBdInvalid ? kBdInvalid : lid[s];
+    luid[p] = l;
+    if (osi_inv) osi_inv[pj[p]] = l == kBdInvalid ? kBdInvalid : p0 + l;
   }
   __syncthreads();
   BD_STAMP(3)
@@ -442,10 +459,11 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     const uint32_t* __restrict__ luid,
                                                     const float* __restrict__ gs,
                                                     const float* __restrict__ xval, int F,
-                                                    float* __restrict__ ugrad) {
+                                                    float* __restrict__ ugrad, int osi) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
+  const uint32_t base = osi ? p0 : ubase[b];  // rows in occurrence space or compact
   for (uint32_t l = threadIdx.x; l < nu; l += RT) acc[l] = 0.f;
   __syncthreads();
   for (uint32_t p = p0 + threadIdx.x; p < p1; p += RT) {
@@ -518,12 +536,27 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
   }
 }
 
+// compact unique rows (ubase[b] + l, the alltoallv layout) -> occurrence-space
+// rows (bstart[b] + l): the N>1 pull returns rows compact, the osi consumers
+// (LR forward through osi_inv) read them in occurrence space
+__global__ __launch_bounds__(256) void k_bd_unplace(const uint32_t* __restrict__ bstart,
+                                                    const uint32_t* __restrict__ unum,
+                                                    const uint32_t* __restrict__ ubase,
+                                                    const float* __restrict__ src,
+                                                    float* __restrict__ dst, int dim) {
+  const int b = blockIdx.x;
+  const unsigned int n = unum[b] * (unsigned int)dim;
+  const float* s = src + (size_t)ubase[b] * dim;
+  float* d = dst + (size_t)bstart[b] * dim;
+  for (unsigned int e = threadIdx.x; e < n; e += 256) d[e] = s[e];
+}
+
 // ------------------------------------------------------------- launchers
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg) {
+                     unsigned long long* dbg, uint32_t* osi_inv) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   if (n <= 0) {
     check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
@@ -555,12 +588,12 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      L.P, S + L.btot, S + L.bstart, S + L.ctr);
   check_launch("k_bd_colscan");
   SS_BD_CT_DISPATCH(k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pj,
-                    pos_of, bkt);
+                    pos_of, bkt, osi_inv);
 #undef SS_BD_CT_DISPATCH
   check_launch("k_bd_scatter");
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                      bkeys, S + L.unum, S, S + L.ctr, L.Pd, rs.nranks, ucap, S + L.ubase, ucount,
-                     dbg);
+                     osi_inv, dbg);
   check_launch("k_bd_dedup");
   if (place) {  // send-segment keys (+ zeroed gradient rows)
     hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart,
@@ -568,15 +601,25 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     check_launch("k_bd_place");
   }
   if (inv) {
+    if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");
     BdIndex ix{pos_of, luid, bkt, S + L.ubase};
     hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, n, inv);
     check_launch("k_bd_inv");
   }
 }
 
+void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,
+                       float* dst, int dim, hipStream_t st) {
+  if (n <= 0) return;
+  const BdLayout L = bd_layout(n, nranks);
+  hipLaunchKernelGGL(k_bd_unplace, dim3(L.P), dim3(256), 0, st, scratch + L.bstart,
+                     scratch + L.unum, scratch + L.ubase, src, dst, dim);
+  check_launch("k_bd_unplace");
+}
+
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
-                      float* ugrad, hipStream_t st) {
+                      float* ugrad, hipStream_t st, int osi) {
   if (n <= 0) return;
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
   const BdLayout L = bd_layout(n, nranks);
@@ -588,13 +631,13 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   }();
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi);
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi);
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
-                     S + L.unum, pj, luid, gs, xval, F, ugrad);
+                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi);
   check_launch("k_bd_reduce");
 }
 

@@ -115,12 +115,14 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("pull_unique_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
                              uintptr_t ubase, int P_, uintptr_t slots, uintptr_t out,
                              const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
-                             uintptr_t st) {
+                             uintptr_t st, int osi) {
     launch_pull_unique_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
                           P<const uint32_t>(unum), P<const uint32_t>(ubase), P_,
                           P<long long>(slots), P<float>(out), ip, P<unsigned long long>(size_ctr),
-                          P<int>(err), G, S(st));
-  });
+                          P<int>(err), G, osi, S(st));
+  }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
+     py::arg("P"), py::arg("slots"), py::arg("out"), py::arg("ip"), py::arg("size_ctr"),
+     py::arg("err"), py::arg("G"), py::arg("st"), py::arg("osi") = 0);
   m.def("pull_claim", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
                          uintptr_t slots, uintptr_t out, const InitParams& ip, uintptr_t size_ctr,
                          uintptr_t err, int G, uintptr_t st) {
@@ -130,6 +132,11 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
                     long long max_n, const OptParams& op, int G, uintptr_t st) {
     launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st));
+  });
+  m.def("apply_bk", [](const DevTable& t, uintptr_t slots, uintptr_t grads, uintptr_t bstart,
+                       uintptr_t unum, int P_, const OptParams& op, int G, uintptr_t st) {
+    launch_apply_bk(t, P<const long long>(slots), P<const float>(grads), P<const uint32_t>(bstart),
+                    P<const uint32_t>(unum), P_, op, G, S(st));
   });
   m.def("assign", [](const DevTable& t, uintptr_t keys, uintptr_t rows, long long n,
                      uintptr_t size_ctr, uintptr_t err, int G, uintptr_t st) {
@@ -167,21 +174,31 @@ PYBIND11_MODULE(_ss_hip, m) {
                        long long ucap, uintptr_t scratch, uintptr_t pj, uintptr_t pos_of,
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
-                       uintptr_t st, uintptr_t dbg) {
+                       uintptr_t st, uintptr_t dbg, uintptr_t osi_inv) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
                     P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
                     P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
-                    P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg));
+                    P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg),
+                    P<uint32_t>(osi_inv));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
-     py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0);
+     py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
+     py::arg("osi_inv") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
-                        uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st) {
+                        uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
+                        int osi) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                      P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
-                     P<float>(ugrad), S(st));
+                     P<float>(ugrad), S(st), osi);
+  }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
+     py::arg("gs"), py::arg("xval"), py::arg("F"), py::arg("ugrad"), py::arg("st"),
+     py::arg("osi") = 0);
+  m.def("bd_unplace", [](long long n, int nranks, uintptr_t scratch, uintptr_t src, uintptr_t dst,
+                         int dim, uintptr_t st) {
+    launch_bd_unplace(n, nranks, P<const uint32_t>(scratch), P<const float>(src), P<float>(dst),
+                      dim, S(st));
   });
   m.def("route_keys", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num,
                          int nranks, uintptr_t dest, uintptr_t st) {

@@ -32,12 +32,15 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, hipStream_t st);
+                           int* err, int G, int osi, hipStream_t st);
 void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
                        long long max_n, long long* slots, float* out, const InitParams& ip,
                        unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st);
+void launch_apply_bk(const DevTable& t, const long long* slots, const float* grads,
+                     const uint32_t* bstart, const uint32_t* unum, int P, const OptParams& op,
+                     int G, hipStream_t st);
 void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, long long n,
                    unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,
@@ -111,10 +114,12 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg = nullptr);
+                     unsigned long long* dbg = nullptr, uint32_t* osi_inv = nullptr);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
-                      float* ugrad, hipStream_t st);
+                      float* ugrad, hipStream_t st, int osi = 0);
+void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,
+                       float* dst, int dim, hipStream_t st);
 
 void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                          const uint32_t* luid, const float* gs, const float* gss, int F, int dim,

@@ -204,7 +204,8 @@ __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t*
 
 // Same, straight from the bucketed dedup's per-bucket staging (bdedup.hip):
 // workgroup b pulls bucket b's unique keys bkeys[bstart[b] + l] to unique id
-// ubase[b] + l — the colocated 1-GPU path needs no send-segment copy.
+// ubase[b] + l (or bstart[b] + l, osi) — the colocated 1-GPU path needs no
+// send-segment copy.
 template <int G>
 __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64_t* __restrict__ bkeys,
                                                         const uint32_t* __restrict__ bstart,
@@ -212,9 +213,12 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
                                                         const uint32_t* __restrict__ ubase,
                                                         long long* __restrict__ slots_out,
                                                         float* __restrict__ out, InitParams ip,
-                                                        unsigned long long* size_ctr, int* err) {
+                                                        unsigned long long* size_ctr, int* err,
+                                                        int osi) {
   const int b = blockIdx.x, lg = threadIdx.x % G;
-  const uint32_t nu = unum[b], base = ubase[b];
+  // osi: rows at occurrence-space ids bstart[b] + l (bdedup.hip), else at the
+  // compact unique ids ubase[b] + l
+  const uint32_t nu = unum[b], base = osi ? bstart[b] : ubase[b];
   const uint64_t* src = bkeys + bstart[b];
   unsigned long long ins = 0;
   for (uint32_t l = threadIdx.x / G; l < nu; l += 256 / G)
@@ -342,6 +346,44 @@ __global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t*
 // unique (the host launches one segment per source rank, in rank order, so
 // duplicate keys from different workers are applied sequentially — no lost
 // updates, deterministic, and no float atomics on the hot path).
+// one row of K5: lane lg of a G-lane group updates its coordinates
+template <int G>
+__device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
+                                          const float* __restrict__ gr, const OptParams& op,
+                                          int lg) {
+  if (slot < 0) return;
+  float* row = slot_row(t, slot);
+  if (t.dim <= (uint32_t)G * kApplyRegs) {
+    // all of this lane's coordinates loaded first, updated in registers,
+    // stored after: one memory round trip per row (a load-update-store loop
+    // per coordinate serialised dim/G round trips: FM rows took 3)
+    const int ns = opt_state_per_coord(op.kind);
+    float w[kApplyRegs], s1[kApplyRegs], s2[kApplyRegs], g[kApplyRegs];
+#pragma unroll
+    for (int r = 0; r < kApplyRegs; ++r) {
+      const uint32_t j = lg + r * G;
+      if (j < t.dim) {
+        w[r] = row[j];
+        g[r] = gr[j];
+        s1[r] = ns > 0 ? row[t.dim + j] : 0.f;
+        s2[r] = ns > 1 ? row[2 * t.dim + j] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kApplyRegs; ++r) {
+      const uint32_t j = lg + r * G;
+      if (j < t.dim) {
+        opt_update(op, w[r], s1[r], s2[r], g[r]);
+        row[j] = w[r];
+        if (ns > 0) row[t.dim + j] = s1[r];
+        if (ns > 1) row[2 * t.dim + j] = s2[r];
+      }
+    }
+  } else {
+    for (uint32_t j = lg; j < t.dim; j += G) opt_apply(op, row, row + t.dim, t.dim, j, gr[j]);
+  }
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __restrict__ slots,
                                                const float* __restrict__ grads, SegList sl,
@@ -353,39 +395,23 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    const long long slot = slots[pos];
-    if (slot < 0) continue;
-    float* row = slot_row(t, slot);
-    const float* gr = grads + pos * (long long)t.dim;
-    if (t.dim <= (uint32_t)G * kApplyRegs) {
-      // all of this lane's coordinates loaded first, updated in registers,
-      // stored after: one memory round trip per row (a load-update-store loop
-      // per coordinate serialised dim/G round trips: FM rows took 3)
-      const int ns = opt_state_per_coord(op.kind);
-      float w[kApplyRegs], s1[kApplyRegs], s2[kApplyRegs], g[kApplyRegs];
-#pragma unroll
-      for (int r = 0; r < kApplyRegs; ++r) {
-        const uint32_t j = lg + r * G;
-        if (j < t.dim) {
-          w[r] = row[j];
-          g[r] = gr[j];
-          s1[r] = ns > 0 ? row[t.dim + j] : 0.f;
-          s2[r] = ns > 1 ? row[2 * t.dim + j] : 0.f;
-        }
-      }
-#pragma unroll
-      for (int r = 0; r < kApplyRegs; ++r) {
-        const uint32_t j = lg + r * G;
-        if (j < t.dim) {
-          opt_update(op, w[r], s1[r], s2[r], g[r]);
-          row[j] = w[r];
-          if (ns > 0) row[t.dim + j] = s1[r];
-          if (ns > 1) row[2 * t.dim + j] = s2[r];
-        }
-      }
-    } else {
-      for (uint32_t j = lg; j < t.dim; j += G) opt_apply(op, row, row + t.dim, t.dim, j, gr[j]);
-    }
+    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg);
+  }
+}
+
+// K5 over a bucketed dedup's rows in OCCURRENCE-SPACE layout (unique key l of
+// bucket b at row bstart[b] + l; see bdedup.hip): one workgroup per bucket
+template <int G>
+__global__ __launch_bounds__(256) void k_apply_bk(DevTable t, const long long* __restrict__ slots,
+                                                  const float* __restrict__ grads,
+                                                  const uint32_t* __restrict__ bstart,
+                                                  const uint32_t* __restrict__ unum,
+                                                  OptParams op) {
+  const int b = blockIdx.x, lg = threadIdx.x % G;
+  const uint32_t nu = unum[b], p0 = bstart[b];
+  for (uint32_t l = threadIdx.x / G; l < nu; l += 256 / G) {
+    const long long pos = (long long)p0 + l;
+    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg);
   }
 }
 
@@ -519,10 +545,10 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, hipStream_t st) {
+                           int* err, int G, int osi, hipStream_t st) {
   if (P <= 0) return;
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique_bk<kG>, dim3(P), dim3(256), 0, st, t, bkeys,
-                                      bstart, unum, ubase, slots, out, ip, size_ctr, err));
+                                      bstart, unum, ubase, slots, out, ip, size_ctr, err, osi));
   check_launch("k_pull_unique_bk");
 }
 
@@ -536,6 +562,15 @@ void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& s
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_verify<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
                                       st, t, keys, sl, slots, out, ip, size_ctr, err));
   check_launch("k_pull_verify");
+}
+
+void launch_apply_bk(const DevTable& t, const long long* slots, const float* grads,
+                     const uint32_t* bstart, const uint32_t* unum, int P, const OptParams& op,
+                     int G, hipStream_t st) {
+  if (P <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_bk<kG>, dim3(P), dim3(256), 0, st, t, slots, grads,
+                                      bstart, unum, op));
+  check_launch("k_apply_bk");
 }
 
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,

@@ -84,10 +84,16 @@ class SparseLRWorker(PipelinedWorker):
         if grad_mode == "segreduce":
             # per-sample gradients (bucketed) or per-occurrence g*x (bin plan)
             self.gocc = torch.empty(B if self.bucketed else n, dtype=torch.float32, device=dev)
+        self.osi = False
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False        # the LDS reduce stores every unique row
                 dd.materialize_inv = False  # the forward resolves uid(j) itself (BdIndex)
+            # occurrence-space unique ids (SS_OSI=1, off by default: measured
+            # slower, see PSEngine.enable_osi): the dedup kernel writes inv[j]
+            # itself and the forward reads it coalesced instead of gathering
+            # luid[pos_of[j]]
+            self.osi = engine.enable_osi()
         elif grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
@@ -131,7 +137,11 @@ class SparseLRWorker(PipelinedWorker):
         xp = self.xval[slot].data_ptr() if self.xval is not None else 0
         if self.grad_mode == "segreduce":
             o = dd.owner
-            if self.bucketed:
+            if self.osi:
+                h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
+                           d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
+                           self.loss_sum.data_ptr(), 0, st)
+            elif self.bucketed:
                 h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
                            rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
                            self.loss_sum.data_ptr(), 0, st, o.index_ptrs(dd.n))
@@ -140,9 +150,11 @@ class SparseLRWorker(PipelinedWorker):
                            d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 0,
                            self.loss_sum.data_ptr(), 0, st)
             if self.bucketed:
+                # one GPU + osi: gradient rows in occurrence space (apply_bk);
+                # N>1: compact, the alltoallv layout
                 h.bd_reduce(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                             o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
-                            rnd.ugrad.data_ptr(), st)
+                            rnd.ugrad.data_ptr(), st, int(self.osi and self.engine.fast1))
             else:
                 h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
                             self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,

@@ -71,6 +71,12 @@ class Deduper:
         # bucket mode: False skips writing the contiguous send segment (ukeys)
         # when nothing reads it (the colocated 1-GPU engine pulls per bucket)
         self.need_ukeys = True
+        # bucket mode: occurrence-space unique ids.  ``inv[j]`` is then
+        # bstart[b] + l (unique key l of bucket b), written by the dedup kernel
+        # itself; rows indexed by it live at those positions of an n-row
+        # buffer (pull_buckets/push_buckets with osi, bd_unplace for N>1), and
+        # no BdIndex (pos_of / bkt) is written
+        self.osi = False
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -121,14 +127,17 @@ class Deduper:
         ug = self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0
         if self.mode == "bucket":
             self._last_n = n
+            osi = self.osi
             self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
                             self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
-                            self.pos_of.data_ptr(), self.bkt.data_ptr(), self.luid.data_ptr(),
+                            0 if osi else self.pos_of.data_ptr(),
+                            0 if osi else self.bkt.data_ptr(), self.luid.data_ptr(),
                             self.bkeys.data_ptr(), self.ucount.data_ptr(),
                             self.ukeys.data_ptr(), ug, self.gdim,
-                            self.inv.data_ptr() if self.materialize_inv else 0,
+                            self.inv.data_ptr() if (self.materialize_inv and not osi) else 0,
                             int(self.need_ukeys or bool(ug)), st,
-                            self.dbg.data_ptr() if self.dbg is not None else 0)
+                            self.dbg.data_ptr() if self.dbg is not None else 0,
+                            self.inv.data_ptr() if osi else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self)
         # the scratch is all-EMPTY between calls: the finish kernel resets the
@@ -145,22 +154,32 @@ class Deduper:
                            self.nranks, n, self)
 
     def reduce(self, n: int, gs: torch.Tensor, F: int, ugrad: torch.Tensor,
-                xval: Optional[torch.Tensor] = None, stream=None):
+                xval: Optional[torch.Tensor] = None, stream=None, osi: bool = False):
         """K7 for scalar rows, for the LAST call's partition (bucket mode):
         ugrad[uid] = sum over occurrences j of uid of gs[j // F] * xval[j]
-        (per-sample gradient times feature value; no zero-fill needed)."""
+        (per-sample gradient times feature value; no zero-fill needed).
+        ``osi``: rows at occurrence-space ids, else at the compact ids."""
         if self.mode != "bucket" or self.gdim != 1:
             raise RuntimeError("Deduper.reduce needs mode='bucket' and gdim=1")
         self.h.bd_reduce(n, self.nranks, self.scratch.data_ptr(), self.pj.data_ptr(),
                          self.luid.data_ptr(), gs.data_ptr(),
                          xval.data_ptr() if xval is not None else 0, F, ugrad.data_ptr(),
-                         _stream_ptr(stream))
+                         _stream_ptr(stream), int(osi))
+
+    def unplace(self, n: int, src: torch.Tensor, dst: torch.Tensor, stream=None):
+        """Rows of the LAST call from compact unique ids (``src``, the
+        alltoallv layout) to occurrence-space ids (``dst``, n rows)."""
+        if self.mode != "bucket":
+            raise RuntimeError("unplace needs mode='bucket'")
+        self.h.bd_unplace(n, self.nranks, self.scratch.data_ptr(), src.data_ptr(),
+                          dst.data_ptr(), src.shape[-1] if src.dim() > 1 else 1,
+                          _stream_ptr(stream))
 
     def index_ptrs(self, n: Optional[int] = None):
         """(pos_of, luid, bkt, ubase) device pointers of the last call: the
         kernels' BdIndex, uid(j) = ubase[bkt[j]] + luid[pos_of[j]]."""
-        if self.mode != "bucket":
-            raise RuntimeError("index_ptrs needs mode='bucket'")
+        if self.mode != "bucket" or self.osi:
+            raise RuntimeError("index_ptrs needs mode='bucket' without osi")
         n = self._last_n if n is None else n
         ub = self.scratch.data_ptr() + 4 * self.h.bd_ubase_offset(max(1, n), self.nranks)
         return [self.pos_of.data_ptr(), self.luid.data_ptr(), self.bkt.data_ptr(), ub]

@@ -172,14 +172,23 @@ class HbmTable:
             h.gather(self.dt, slots.data_ptr(), sl, n, out.data_ptr(), self.G, st)
         return out, slots
 
-    def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None):
+    def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None,
+                     osi: bool = False):
         """Unique-key lookup-or-init + gather straight from a bucketed dedup
-        (``Deduper.bucket_view()``): rows land at their unique ids."""
+        (``Deduper.bucket_view()``): rows land at their unique ids (compact,
+        or occurrence-space with ``osi``)."""
         bkeys, bstart, unum, ubase, P = view
         hip().pull_unique_bk(self.dt, bkeys, bstart, unum, ubase, P, slots.data_ptr(),
                              out.data_ptr(), self._init_native, self.size_ctr.data_ptr(),
-                             self.err.data_ptr(), self.G, _stream_ptr(stream))
+                             self.err.data_ptr(), self.G, _stream_ptr(stream), int(osi))
         return out, slots
+
+    def push_buckets(self, view, slots: torch.Tensor, grads: torch.Tensor, stream=None):
+        """Optimizer update for a bucketed dedup's unique keys whose slots and
+        gradient rows sit at occurrence-space ids (``pull_buckets(osi=True)``)."""
+        _, bstart, unum, _, P = view
+        hip().apply_bk(self.dt, slots.data_ptr(), grads.data_ptr(), bstart, unum, P,
+                       self.opt.native(), self.G, _stream_ptr(stream))
 
     def lookup_slots(self, keys: torch.Tensor, insert: bool = False, segs=None,
                      max_n: Optional[int] = None, stream=None) -> torch.Tensor:

@@ -202,6 +202,40 @@ class PSEngine:
         # network while the route stream dedups and the main stream computes
         self.pull_stream = (torch.cuda.Stream(device=self.device)
                             if self.pull_ahead and self.pt is not self.ct else None)
+        # occurrence-space unique ids (enable_osi): the model indexes rows
+        # with the dedup's own inverse (bstart[b] + l), see ops/dedup.py
+        self.osi = False
+
+    def enable_osi(self) -> bool:
+        """Switch the dedupers to occurrence-space unique ids (bucketed dedup
+        with CAS inserts on GPU only): the dedup kernel writes the inverse
+        index itself and the model's rows live at bstart[b] + l — in the
+        pulled buffer on one GPU, in a per-slot buffer the received rows are
+        unplaced into for N>1.  Returns whether it is on.
+
+        Off unless SS_OSI=1: measured on MI355X (sparse LR, 10.2M keys/step)
+        the forward gets 192 -> 123 us, but the dedup's random 4-B inverse
+        stores cost more (217 -> 350 us): 1.26 vs 1.18 ms/step."""
+        ok = (self.gpu and all(getattr(d, "mode", None) == "bucket" for d in self.dedupers)
+              and (self.table is None or self.table.insert_mode == "cas")
+              and os.environ.get("SS_OSI", "0") != "0")
+        if not ok:
+            return False
+        for d in self.dedupers:
+            d.osi = True
+        if not self.fast1:
+            self.uvals_osi = [torch.empty((self.max_keys, self.dim), dtype=torch.float32,
+                                          device=self.device) for _ in range(self.depth)]
+        self.osi = True
+        return True
+
+    def _rows_for_model(self, dd: DedupResult, uv: torch.Tensor, slot: int) -> torch.Tensor:
+        """N>1 with osi: compact received rows -> occurrence-space rows."""
+        if not self.osi or self.fast1:
+            return uv
+        out = self.uvals_osi[slot]
+        dd.owner.unplace(dd.n, uv, out)
+        return out
 
     # ------------------------------------------------------------ stage 1
     def route(self, keys: Optional[torch.Tensor] = None, produce=None, post=None) -> Routed:
@@ -271,7 +305,7 @@ class PSEngine:
         if self.fast1:
             own = dd.owner
             if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
-                tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot])
+                tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi)
             else:
                 tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                          segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
@@ -282,6 +316,7 @@ class PSEngine:
         self.t.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
         self._server_pull(rcounts, slot)
         self.t.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
+        uv = self._rows_for_model(dd, uv, slot)
         sent, recv = int(scounts.sum()), int(rcounts.sum())
         # pull: keys out + rows back; push (next): grad rows out
         self.metrics.add(occurrences=dd.n, unique_sent=sent, unique_recv=recv,
@@ -299,7 +334,7 @@ class PSEngine:
             with torch.cuda.stream(rs):
                 own = dd.owner
                 if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
-                    tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot])
+                    tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi)
                 else:
                     tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                              segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
@@ -316,6 +351,7 @@ class PSEngine:
             self.pt.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
             self._server_pull(rcounts, slot)
             self.pt.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
+            uv = self._rows_for_model(dd, uv, slot)
             ev = torch.cuda.Event()
             ev.record(ps)
         sent, recv = int(scounts.sum()), int(rcounts.sum())
@@ -370,8 +406,11 @@ class PSEngine:
         g = rnd.ugrad if grads is None else grads
         tab = self.table
         if self.fast1:
-            tab.push_slots(rnd.slots, g, segs=tab.dev_segs(rnd.dd.ucount),
-                           max_n=max(1, min(rnd.dd.n, rnd.dd.ucap)))
+            if self.osi:
+                tab.push_buckets(rnd.dd.owner.bucket_view(rnd.dd.n), rnd.slots, g)
+            else:
+                tab.push_slots(rnd.slots, g, segs=tab.dev_segs(rnd.dd.ucount),
+                               max_n=max(1, min(rnd.dd.n, rnd.dd.ucap)))
             tab.next_round()
         else:
             D = self.displs
@@ -396,6 +435,9 @@ class PSEngine:
         """Add per-occurrence gradients into the round's unique-key rows
         (the reference's merge_push_value, sparse_access_method.h:39-40)."""
         grads = grads.reshape(rnd.dd.n, self.dim).contiguous()
+        if self.osi and not self.fast1:
+            # the push sends compact rows; osi ids index occurrence space
+            raise NotImplementedError("accumulate() with occurrence-space ids needs world 1")
         if self.gpu:
             _hip().scatter_add_rows(grads.data_ptr(), rnd.inv.data_ptr(), rnd.dd.n, self.dim,
                                     rnd.ugrad.data_ptr(), _stream())
@@ -419,12 +461,17 @@ class PSEngine:
         # this path merges into zeroed rows and probes the send segment: force
         # both on the deduper that routes it (a model may have switched them off)
         own = self.dedupers[self._next_slot]
-        saved = (getattr(own, "zero_grad", True), getattr(own, "need_ukeys", True))
+        saved = (getattr(own, "zero_grad", True), getattr(own, "need_ukeys", True),
+                 getattr(own, "osi", False))
         own.zero_grad, own.need_ukeys = True, True
+        if hasattr(own, "osi"):
+            own.osi = False  # compact ids: the merge + probe below use the send segment
         try:
             r = self.route(keys)
         finally:
-            own.zero_grad, own.need_ukeys = saved
+            own.zero_grad, own.need_ukeys = saved[:2]
+            if hasattr(own, "osi"):
+                own.osi = saved[2]
         if self.gpu:
             torch.cuda.current_stream().wait_event(r.ready)
         dd = r.dd

@@ -244,6 +244,72 @@ def test_bucket_reduce_lr_matches_atomic_path(dev, nranks):
     np.testing.assert_allclose(l_b.sum().item(), l_at.sum().item(), rtol=1e-5)
 
 
+@pytest.mark.parametrize("nranks", [1, 3])
+def test_bucket_dedup_occurrence_space_ids(dev, nranks):
+    """osi mode: the dedup kernel's own inverse indexes the staged unique keys
+    (bkeys[inv[j]] == keys[j]); unplace maps compact rows onto those ids; the
+    LDS reduce in occurrence space equals per-occurrence atomics."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.dedup import INVALID, Deduper
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    h = hip()
+    B, F = 20000, 13
+    n = B * F
+    rng = np.random.default_rng(11 + nranks)
+    keys = (rng.zipf(1.3, n) % 300000).astype(np.int64)
+    keys[::97] = -1  # EMPTY: never reaches a bucket, inverse must be INVALID
+    fm = HashFrag(nranks, 64).rank_map()
+    d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=1,
+                device=dev, mode="bucket", zero_grad=False)
+    d.osi = True
+    d.inv.fill_(123)  # every entry must be rewritten
+    r = d(torch.from_numpy(keys).to(dev))
+    torch.cuda.synchronize()
+    d.check()
+    inv = r.inv.cpu().numpy().view(np.uint32).astype(np.int64)
+    bk = d.bkeys.cpu().numpy()
+    bad = keys == -1
+    assert (inv[bad] == INVALID).all()
+    ok = ~bad
+    np.testing.assert_array_equal(bk[inv[ok]], keys[ok])
+    # one id per distinct key
+    ids = {}
+    for k, i in zip(keys[ok][:50000].tolist(), inv[ok][:50000].tolist()):
+        assert ids.setdefault(k, i) == i
+    assert len(set(ids.values())) == len(ids)
+    assert int(r.ucount.sum()) == len(np.unique(keys[ok]))
+    # unplace: compact unique id ubase[b]+l -> occurrence-space id bstart[b]+l
+    P, o_bs, o_un, o_ub = h.bd_offsets(n, nranks)
+    sc = d.scratch.cpu().numpy().view(np.uint32).astype(np.int64)
+    bstart, unum, ubase = sc[o_bs:o_bs + P + 1], sc[o_un:o_un + P], sc[o_ub:o_ub + P]
+    U = nranks * d.ucap
+    src = torch.randn(U, device=dev)
+    dst = torch.full((n,), float("nan"), device=dev)
+    d.unplace(n, src, dst)
+    torch.cuda.synchronize()
+    s_np, d_np = src.cpu().numpy(), dst.cpu().numpy()
+    for b in range(0, P, 7):
+        np.testing.assert_array_equal(d_np[bstart[b]:bstart[b] + unum[b]],
+                                      s_np[ubase[b]:ubase[b] + unum[b]])
+    # reduce in occurrence space == per-occurrence atomics through the osi inverse
+    st = torch.cuda.current_stream().cuda_stream
+    uvals = torch.randn(n, device=dev) * 0.1
+    y = torch.from_numpy((rng.random(B) < 0.3).astype(np.float32)).to(dev)
+    g_at = torch.zeros(n, device=dev)
+    h.lr_fwd_bwd(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), g_at.data_ptr(),
+                 0, 0, st)
+    gs = torch.empty(B, device=dev)
+    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gs.data_ptr(), 1,
+               0, 0, st)
+    g_b = torch.full((n,), float("nan"), device=dev)
+    d.reduce(n, gs, F, g_b, osi=True)
+    torch.cuda.synchronize()
+    live = np.concatenate([np.arange(bstart[b], bstart[b] + unum[b]) for b in range(P)])
+    np.testing.assert_allclose(g_b.cpu().numpy()[live], g_at.cpu().numpy()[live], rtol=1e-4,
+                               atol=1e-4)
+
+
 @pytest.mark.parametrize("F", [39, 7, 64, 100])  # lane-group layout (<=64) and LDS fallback
 def test_lr_fwd_bwd_matches_torch(dev, F):
     from swiftsnails_amd._native import hip
@@ -454,3 +520,30 @@ def test_probe_histogram_and_stats(dev):
     st = t.stats()
     assert abs(st["load_factor"] - 3500 / t.capacity) < 1e-9
     assert 0 <= st["probe_mean"] < 5
+
+
+def test_sparse_lr_osi_matches_compact_ids(dev, monkeypatch):
+    """The LR worker with occurrence-space ids (default) trains the same
+    model as with compact ids + BdIndex (SS_OSI=0), step for step."""
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    out = {}
+    for osi in ("1", "0"):
+        monkeypatch.setenv("SS_OSI", osi)
+        data = CtrSynth(batch_size=4096, num_fields=13, num_features=300_000, tail_frac=0.2)
+        table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
+        eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
+        w = SparseLRWorker(eng, data)
+        assert w.osi == (osi == "1")
+        losses = [float(w.step().sum().item()) for _ in range(12)]
+        torch.cuda.synchronize()
+        table.check()
+        out[osi] = (losses, table.to_dict(with_state=True))
+    (l1, t1), (l0, t0) = out["1"], out["0"]
+    np.testing.assert_allclose(l1, l0, rtol=1e-4)
+    assert t1.keys() == t0.keys()
+    ks = list(t1.keys())[:20000]
+    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
+                               rtol=1e-4, atol=1e-6)
