@@ -44,6 +44,10 @@ struct DevTable {
   uint32_t key_off;   // byte offset of the key inside a slot
   uint32_t dim;       // parameter floats per row (what pull returns)
   uint32_t width;     // dim + optimizer-state floats
+  // 1: every EMPTY slot's row already holds the initial row (key-independent
+  // init, filled at allocation), so an insert is the key CAS alone — no
+  // second write to the freshly claimed line
+  uint32_t prefilled;
 };
 
 __device__ __forceinline__ uint64_t* slot_key(const DevTable& t, uint64_t s) {

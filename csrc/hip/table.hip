@@ -56,6 +56,7 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 template <int G>
 __device__ __forceinline__ void init_row(const DevTable& t, const InitParams& ip, float* row,
                                          uint64_t key, int lg) {
+  if (t.prefilled) return;
   for (uint32_t j = lg; j < t.width; j += G)
     row[j] = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
 }
@@ -159,7 +160,7 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
     if (inserted) {
       for (uint32_t j = lg; j < t.width; j += G) {
         const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
-        row[j] = v;
+        if (!t.prefilled) row[j] = v;
         if (j < t.dim) o[j] = v;
       }
     } else if (t.dim <= (uint32_t)G * kApplyRegs) {
@@ -330,7 +331,7 @@ __global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t*
     if (inserted) {
       for (uint32_t j = lg; j < t.width; j += G) {
         const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
-        row[j] = v;
+        if (!t.prefilled) row[j] = v;
         if (j < t.dim) o[j] = v;
       }
     } else {

@@ -104,12 +104,24 @@ class HbmTable:
     def _alloc(self, cap: int):
         self.capacity = cap
         self.storage = torch.empty(cap * self.stride, dtype=torch.uint8, device=self.device)
-        self.storage.fill_(255)  # every key word = EMPTY
+        # key-independent init (zero): fill every row with the initial row up
+        # front, so an insert is the key CAS alone (SS_TABLE_PREFILL=0: off)
+        self.prefilled = (self.init_cfg.kind == "zero" and
+                          os.environ.get("SS_TABLE_PREFILL", "1") != "0")
+        if self.prefilled:
+            self.storage.zero_()
+            slots = self.storage.view(cap, self.stride)
+            slots[:, self.key_off:self.key_off + 8].fill_(255)  # every key word = EMPTY
+            if self.width > self.dim and float(self.init_cfg.state_init) != 0.0:
+                rows = self.storage.view(torch.float32).view(cap, self.stride // 4)
+                rows[:, self.dim:self.width].fill_(float(self.init_cfg.state_init))
+        else:
+            self.storage.fill_(255)  # every key word = EMPTY (rows: the 0xFF sentinel)
         # sharded counter: 256 shards x 128 B (see ss_device.h ctr_add)
         self.size_ctr = torch.zeros(CTR_SHARDS * 16, dtype=torch.int64, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.dt = hip().DevTable(self.storage.data_ptr(), cap, self.stride, self.key_off, self.dim,
-                                 self.width)
+                                 self.width, int(self.prefilled))
 
     @staticmethod
     def plan(n_keys: int, dim: int, optimizer: Optional[Optimizer] = None,

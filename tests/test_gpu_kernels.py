@@ -547,3 +547,34 @@ def test_sparse_lr_osi_matches_compact_ids(dev, monkeypatch):
     ks = list(t1.keys())[:20000]
     np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
                                rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("prefill", ["1", "0"])
+def test_zero_init_prefilled_rows(dev, monkeypatch, prefill):
+    """Zero-init tables are allocated with the initial row in every empty
+    slot (insert = key CAS only); pulled rows, state and a following update
+    are the same as with per-insert row writes."""
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+
+    monkeypatch.setenv("SS_TABLE_PREFILL", prefill)
+    t = HbmTable(3, 1 << 14, optimizer=Optimizer("adagrad", lr=0.5),
+                 init=InitConfig("zero", state_init=0.1), device=dev)
+    assert t.prefilled == (prefill == "1")
+    base = np.unique(_keys(3000, 9))
+    k = np.concatenate([base, base[:700]])  # duplicates in one launch
+    v, s = t.pull(torch.from_numpy(k).to(dev), unique=False)
+    torch.cuda.synchronize()
+    t.check()
+    assert t.size() == len(base)
+    assert torch.count_nonzero(v).item() == 0
+    d = t.to_dict(with_state=True)
+    np.testing.assert_allclose(np.stack([d[int(x)] for x in base[:100]]),
+                               np.tile([0, 0, 0, 0.1, 0.1, 0.1], (100, 1)), rtol=1e-6)
+    g = torch.ones((len(base), 3), device=dev)
+    t.push(torch.from_numpy(base).to(dev), g)
+    torch.cuda.synchronize()
+    d = t.to_dict(with_state=True)
+    row = d[int(base[5])]
+    np.testing.assert_allclose(row[3:], 1.1, rtol=1e-6)
+    np.testing.assert_allclose(row[:3], -0.5 / np.sqrt(1.1), rtol=1e-4)
