@@ -172,21 +172,26 @@ __global__ __launch_bounds__(CT) void k_bd_count(const uint64_t* __restrict__ ke
   for (int b = threadIdx.x; b < P; b += CT) row[b] = h[b];
 }
 
-// 2+3. column scan of the [nch][P] histogram (64 buckets x 16 chunk segments
-//    per workgroup, two passes of independent loads, no serial chain); the
-//    LAST workgroup to finish (arrival counter) also scans the bucket totals
-//    into bucket start offsets — no separate single-workgroup launch
-__global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist, int nch, int P,
-                                                     uint32_t* __restrict__ btot,
-                                                     uint32_t* __restrict__ bstart,
-                                                     unsigned int* __restrict__ ctr) {
-  __shared__ unsigned int ss[16][64];
+// 2+3. column scan of the [nch][P] histogram (64 buckets x CS/64 chunk
+//    segments per workgroup, two passes of independent loads, no serial
+//    chain); the LAST workgroup to finish (arrival counter) also scans the
+//    bucket totals into bucket start offsets — no separate single-workgroup
+//    launch.  CS = workgroup size (small workgroups are not starved by the
+//    other stream's kernels: 1024-thread ones waited ~200 us for a CU with 16
+//    free wave slots beside the pull)
+template <int CS>
+__global__ __launch_bounds__(CS) void k_bd_colscan(uint32_t* __restrict__ hist, int nch, int P,
+                                                   uint32_t* __restrict__ btot,
+                                                   uint32_t* __restrict__ bstart,
+                                                   unsigned int* __restrict__ ctr) {
+  constexpr int NS = CS / 64;  // chunk segments per column
+  __shared__ unsigned int ss[NS][64];
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
   __shared__ bool last;
   const int col = threadIdx.x & 63, seg = threadIdx.x >> 6;
   const int b = blockIdx.x * 64 + col;
-  const int R = (nch + 15) / 16;
+  const int R = (nch + NS - 1) / NS;
   const int c0 = seg * R, c1 = min(nch, c0 + R);
   unsigned int s = 0;
   if (b < P) {
@@ -205,7 +210,7 @@ __global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist
       hist[i] = off;
       off += v;
     }
-    if (seg == 15) __hip_atomic_store(&btot[b], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (seg == NS - 1) __hip_atomic_store(&btot[b], off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   // publish btot: write-through stores drained by every wave, barrier, then
   // one arrival add; the last arriver reads btot write-through (guide G16 R1)
@@ -214,13 +219,13 @@ __global__ __launch_bounds__(1024) void k_bd_colscan(uint32_t* __restrict__ hist
   if (threadIdx.x == 0) last = atomicAdd(ctr, 1u) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;  // workgroup-uniform
-  const int per = (P + 1023) / 1024;
+  const int per = (P + CS - 1) / CS;
   const int b0 = threadIdx.x * per;
   unsigned int sum = 0;
   for (int k = 0; k < per; ++k)
     if (b0 + k < P)
       sum += __hip_atomic_load(&btot[b0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned int e = block_excl_scan<16>(sum, wsum, &tot);
+  unsigned int e = block_excl_scan<NS>(sum, wsum, &tot);
   for (int k = 0; k < per; ++k)
     if (b0 + k < P) {
       bstart[b0 + k] = e;
@@ -570,24 +575,38 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     throw_error("bdedup: too many keys per call (max ~45M)");
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
-  // count/scatter workgroup size (SS_BD_CT: 256/512/1024; experiments)
-  static const int ct = [] {
-    const char* e = std::getenv("SS_BD_CT");
-    const int v = e ? std::atoi(e) : 1024;
-    return (v == 256 || v == 512) ? v : 1024;
-  }();
-#define SS_BD_CT_DISPATCH(KERNEL, ...)                                                        \
+  // workgroup sizes (256/512/1024): count (SS_BD_CNT), column scan
+  // (SS_BD_CS), scatter (SS_BD_CT).  Measured in the pipelined bench, where
+  // the route stream shares the chip with the pull/forward kernels
+  auto wg_env = [](const char* name, int def) {
+    const char* e = std::getenv(name);
+    const int v = e ? std::atoi(e) : def;
+    return (v == 256 || v == 512 || v == 1024) ? v : def;
+  };
+  static const int ct = wg_env("SS_BD_CT", 1024);
+  static const int cnt = wg_env("SS_BD_CNT", 1024);
+  static const int cs = wg_env("SS_BD_CS", 1024);
+#define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \
     case 256: hipLaunchKernelGGL(KERNEL<256>, dim3(L.nch), dim3(256), lds, st, __VA_ARGS__); break; \
     case 512: hipLaunchKernelGGL(KERNEL<512>, dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
     default: hipLaunchKernelGGL(KERNEL<1024>, dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
   }
-  SS_BD_CT_DISPATCH(k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist);
+  SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist);
   check_launch("k_bd_count");
-  hipLaunchKernelGGL(k_bd_colscan, dim3((L.P + 63) / 64), dim3(1024), 0, st, S + L.hist, L.nch,
-                     L.P, S + L.btot, S + L.bstart, S + L.ctr);
+  switch (cs) {
+#define SS_BD_CS_CASE(CS)                                                                      \
+  case CS:                                                                                     \
+    hipLaunchKernelGGL(k_bd_colscan<CS>, dim3((L.P + 63) / 64), dim3(CS), 0, st, S + L.hist,   \
+                       L.nch, L.P, S + L.btot, S + L.bstart, S + L.ctr);                       \
+    break;
+    SS_BD_CS_CASE(256)
+    SS_BD_CS_CASE(512)
+    SS_BD_CS_CASE(1024)
+#undef SS_BD_CS_CASE
+  }
   check_launch("k_bd_colscan");
-  SS_BD_CT_DISPATCH(k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pj,
+  SS_BD_CT_DISPATCH(ct, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pj,
                     pos_of, bkt, osi_inv);
 #undef SS_BD_CT_DISPATCH
   check_launch("k_bd_scatter");
