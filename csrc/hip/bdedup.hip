@@ -471,13 +471,24 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
   const uint32_t base = osi ? p0 : ubase[b];  // rows in occurrence space or compact
   for (uint32_t l = threadIdx.x; l < nu; l += RT) acc[l] = 0.f;
   __syncthreads();
-  for (uint32_t p = p0 + threadIdx.x; p < p1; p += RT) {
-    const uint32_t l = luid[p];  // bucket-local unique id
-    if (l != kBdInvalid) {
-      const uint32_t j = pj[p];
-      const float g = gs[j / (uint32_t)F];
-      atomicAdd(&acc[l], xval ? g * xval[j] : g);
+  // two occurrences per thread in flight (loads before the LDS atomics)
+  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 2 * RT) {
+    uint32_t l[2], j[2];
+    float g[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t p = pb + r * RT;
+      l[r] = p < p1 ? luid[p] : kBdInvalid;  // bucket-local unique id
+      j[r] = p < p1 ? pj[p] : 0u;
     }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      g[r] = l[r] != kBdInvalid ? gs[j[r] / (uint32_t)F] : 0.f;
+      if (xval && l[r] != kBdInvalid) g[r] *= xval[j[r]];
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+      if (l[r] != kBdInvalid) atomicAdd(&acc[l[r]], g[r]);
   }
   __syncthreads();
   for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];
@@ -516,26 +527,64 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
       for (int c = 0; c < NC; ++c) acc[c][l] = 0.f;
     }
     __syncthreads();
-    for (uint32_t p = p0 + threadIdx.x; p < p1; p += 1024) {
-      const uint32_t l = luid[p];  // bucket-local unique id
-      if (l == kBdInvalid) continue;
-      const uint32_t s = pj[p] / (uint32_t)F;
-      if (c0 == 0) atomicAdd(&g0[l], gs[s]);
-      float v[NC];  // the sample's factor-gradient columns, loaded together
+    // two occurrences per thread in flight: every load of both issued before
+    // the first LDS atomic (the loop is a latency chain otherwise)
+    constexpr int RB = 2;
+    for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 1024 * RB) {
+      uint32_t l[RB], sm[RB];
 #pragma unroll
-      for (int c = 0; c < NC; ++c) v[c] = c0 + c < K ? gss[(size_t)s * K + c0 + c] : 0.f;
+      for (int r = 0; r < RB; ++r) {
+        const uint32_t p = pb + r * 1024;
+        l[r] = p < p1 ? luid[p] : kBdInvalid;  // bucket-local unique id
+        sm[r] = p < p1 ? pj[p] : 0u;
+      }
+      float g[RB], v[RB][NC];
 #pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (c0 + c < K) atomicAdd(&acc[c][l], v[c]);
+      for (int r = 0; r < RB; ++r) {
+        const uint32_t s = sm[r] / (uint32_t)F;
+        g[r] = (c0 == 0 && l[r] != kBdInvalid) ? gs[s] : 0.f;
+        if constexpr (NC == K && K % 4 == 0) {
+          // whole 32-B-aligned row of the sample: 16-B vector loads
+          const float4* g4 = reinterpret_cast<const float4*>(gss + (size_t)s * K);
+#pragma unroll
+          for (int q = 0; q < K / 4; ++q) {
+            const float4 x = l[r] != kBdInvalid ? g4[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+            v[r][4 * q] = x.x, v[r][4 * q + 1] = x.y, v[r][4 * q + 2] = x.z, v[r][4 * q + 3] = x.w;
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < NC; ++c)
+            v[r][c] = (l[r] != kBdInvalid && c0 + c < K) ? gss[(size_t)s * K + c0 + c] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < RB; ++r) {
+        if (l[r] == kBdInvalid) continue;
+        if (c0 == 0) atomicAdd(&g0[l[r]], g[r]);
+#pragma unroll
+        for (int c = 0; c < NC; ++c)
+          if (c0 + c < K) atomicAdd(&acc[c][l[r]], v[r][c]);
+      }
     }
     __syncthreads();
-    for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
-      const size_t r = (size_t)(base + l) * DIM;
-      const float G0 = g0[l];
-      if (c0 == 0) ugrad[r] = G0;
-#pragma unroll
-      for (int c = 0; c < NC; ++c)
-        if (c0 + c < K) ugrad[r + 1 + c0 + c] = acc[c][l] - uvals[r + 1 + c0 + c] * G0;
+    // rows out element-major (consecutive lanes -> consecutive floats of the
+    // bucket's contiguous [nu][DIM] block): coalesced uvals reads / ugrad stores
+    const uint32_t ncol = c0 == 0 ? 1u + (uint32_t)min(NC, K - c0) : (uint32_t)min(NC, K - c0);
+    const uint32_t col0 = c0 == 0 ? 0u : 1u + (uint32_t)c0;
+    if (ncol == (uint32_t)DIM) {
+      const size_t r0 = (size_t)base * DIM;
+      for (uint32_t e = threadIdx.x; e < nu * (uint32_t)DIM; e += 1024) {
+        const uint32_t l = e / (uint32_t)DIM, c = e - l * (uint32_t)DIM;
+        const float G0 = g0[l];
+        ugrad[r0 + e] = c == 0 ? G0 : acc[c - 1][l] - uvals[r0 + e] * G0;
+      }
+    } else {
+      for (uint32_t e = threadIdx.x; e < nu * ncol; e += 1024) {
+        const uint32_t l = e / ncol, c = col0 + (e - l * ncol);
+        const size_t r = (size_t)(base + l) * DIM + c;
+        const float G0 = g0[l];
+        ugrad[r] = c == 0 ? G0 : acc[c - 1 - c0][l] - uvals[r] * G0;
+      }
     }
     __syncthreads();
   }
