@@ -57,8 +57,11 @@ class PSContext:
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-        torch.cuda.set_device(self.local_rank)
-        self.device = torch.device("cuda", self.local_rank)
+        # SS_DEVICE pins every rank to one device: multi-rank rehearsals on a
+        # 1-GPU box (with transport: gloo — RCCL refuses two ranks per GPU)
+        dev_idx = int(os.environ.get("SS_DEVICE", self.local_rank))
+        torch.cuda.set_device(dev_idx)
+        self.device = torch.device("cuda", dev_idx)
         self.servers = _ranks(cfg.get("server_ranks"), self.world)
         self.workers = _ranks(cfg.get("worker_ranks"), self.world)
         self.is_server = self.rank in self.servers
