@@ -53,6 +53,10 @@ def main(argv=None):
                     help="batch dedup implementation (default: bucket)")
     ap.add_argument("--transport", default="rccl", choices=["rccl", "gloo"],
                     help="N>1 data plane; gloo is a host-staged rehearsal transport (tests)")
+    # hipGraph replays: neutral at the default batch (GPU-bound), 74 -> 54
+    # us/step at batch 1024 where host launch work bounds the step
+    ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
+                    help="replay the step as hipGraphs (1 GPU; auto = on for N=1)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -129,6 +133,13 @@ def main(argv=None):
     for i in range(a.warmup):
         worker.step()
         wd.beat(i)
+    # hipGraph replays of the whole step (captured here, outside the timed
+    # region; the data generator then reads its step from a device counter)
+    graphed = False
+    if a.graph == "on" or (a.graph == "auto" and world == 1):
+        graphed = worker.enable_graph()
+        for i in range(2 * engine.depth):  # warm every phase's graph
+            worker.step()
     torch.cuda.synchronize()
     table.check()
     first_loss = worker.mean_loss()
@@ -181,6 +192,7 @@ def main(argv=None):
                                 + (", pull-ahead staleness 1)" if getattr(engine, "pull_ahead", False)
                                    else ")")),
                 "optimizer": a.optimizer,
+                "hipgraph": graphed,
                 "keys_per_step_per_gpu": a.batch * a.fields,
                 "unique_keys_per_step_per_gpu": uniq,
                 "table_keys": int(keys_in_table.item()),

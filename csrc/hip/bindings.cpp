@@ -219,10 +219,15 @@ PYBIND11_MODULE(_ss_hip, m) {
   // ---- models
   m.def("gen_ctr", [](uint64_t seed, long long sample_base, int B, int F, long long V,
                       float tail_frac, float truth_scale, float truth_bias, uintptr_t keys,
-                      uintptr_t labels, uintptr_t st) {
+                      uintptr_t labels, uintptr_t st, uintptr_t step_dev, long long step_mul,
+                      long long step_add) {
     launch_gen_ctr(seed, sample_base, B, F, V, tail_frac, truth_scale, truth_bias,
-                   P<uint64_t>(keys), P<float>(labels), S(st));
-  });
+                   P<uint64_t>(keys), P<float>(labels), S(st), P<const long long>(step_dev),
+                   step_mul, step_add);
+  }, py::arg("seed"), py::arg("sample_base"), py::arg("B"), py::arg("F"), py::arg("V"),
+     py::arg("tail_frac"), py::arg("truth_scale"), py::arg("truth_bias"), py::arg("keys"),
+     py::arg("labels"), py::arg("st"), py::arg("step_dev") = 0, py::arg("step_mul") = 0,
+     py::arg("step_add") = 0);
   m.def("lr_fwd_bwd", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
                          uintptr_t uvals, uintptr_t ugrad, uintptr_t loss_sum, uintptr_t pred,
                          uintptr_t st) {
@@ -287,9 +292,13 @@ PYBIND11_MODULE(_ss_hip, m) {
                     C, D, neg_scale, P<const float>(uvals), P<float>(ugrad), P<float>(loss), S(st));
   });
   m.def("w2v_gen", [](uint64_t seed, long long base, int B, int C, int W, long long nneg,
-                      long long V, float noise, uintptr_t keys, uintptr_t st) {
-    launch_w2v_gen(seed, base, B, C, W, nneg, V, noise, P<uint64_t>(keys), S(st));
-  });
+                      long long V, float noise, uintptr_t keys, uintptr_t st, uintptr_t step_dev,
+                      long long step_mul, long long step_add) {
+    launch_w2v_gen(seed, base, B, C, W, nneg, V, noise, P<uint64_t>(keys), S(st),
+                   P<const long long>(step_dev), step_mul, step_add);
+  }, py::arg("seed"), py::arg("base"), py::arg("B"), py::arg("C"), py::arg("W"),
+     py::arg("nneg"), py::arg("V"), py::arg("noise"), py::arg("keys"), py::arg("st"),
+     py::arg("step_dev") = 0, py::arg("step_mul") = 0, py::arg("step_add") = 0);
   m.def("w2v_smem_bytes", &w2v_smem_bytes);
 
   // ---- RCCL

@@ -58,11 +58,17 @@ __device__ __forceinline__ float gen_ctr_label(uint64_t seed, uint64_t gs, float
 // what counts: measured on MI355X the packed layout (91% of lanes busy at
 // F = 39) beat the one-sample-per-lane-group layout of the LR forward (61%),
 // 55 vs 69 us per 2.56M keys.
+// sample_base: first global sample id of the batch; with step_dev (hipGraph
+// replays, where kernel arguments are frozen) it is *step_dev * step_mul +
+// step_add instead, so every replay generates the next batch
 __global__ __launch_bounds__(256) void k_gen_ctr(uint64_t seed, long long sample_base, int B,
                                                      int F, long long V, double logV,
                                                      float tail_frac, float truth_scale,
                                                      float truth_bias, uint64_t* __restrict__ keys,
-                                                     float* __restrict__ labels) {
+                                                     float* __restrict__ labels,
+                                                     const long long* __restrict__ step_dev,
+                                                     long long step_mul, long long step_add) {
+  if (step_dev) sample_base = *step_dev * step_mul + step_add;
   __shared__ float sdot[256];
   const int spb = samples_per_block(F);
   const int t = threadIdx.x;
@@ -339,14 +345,16 @@ void launch_fm_fwd_bwd(const uint32_t* inv, const float* labels, int B, int F, i
 
 void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long long vocab_per_field,
                     float tail_frac, float truth_scale, float truth_bias, uint64_t* keys,
-                    float* labels, hipStream_t st) {
+                    float* labels, hipStream_t st, const long long* step_dev, long long step_mul,
+                    long long step_add) {
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("gen_ctr: F must be in [1,256]");
   const double logV = log((double)vocab_per_field + 1.0);
   const int spb = samples_per_block(F);
   const int blocks = (B + spb - 1) / spb;
   hipLaunchKernelGGL(k_gen_ctr, dim3(blocks), dim3(256), 0, st, seed, sample_base, B, F,
-                     vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels);
+                     vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels,
+                     step_dev, step_mul, step_add);
   check_launch("k_gen_ctr");
 }
 

@@ -79,7 +79,8 @@ void launch_scatter_add_rows(const float* src, const uint32_t* idx, long long n,
 // --- models.hip
 void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long long vocab_per_field,
                     float tail_frac, float truth_scale, float truth_bias, uint64_t* keys,
-                    float* labels, hipStream_t st);
+                    float* labels, hipStream_t st, const long long* step_dev = nullptr,
+                    long long step_mul = 0, long long step_add = 0);
 void launch_lr_fwd_bwd(const uint32_t* inv, const float* xval, const float* labels, int B, int F,
                        const float* uvals, float* ugrad, float* loss_sum, float* pred,
                        hipStream_t st);
@@ -131,6 +132,8 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
                      float* loss_sum, hipStream_t st);
 void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,
-                    long long V, float noise, uint64_t* keys, hipStream_t st);
+                    long long V, float noise, uint64_t* keys, hipStream_t st,
+                    const long long* step_dev = nullptr, long long step_mul = 0,
+                    long long step_add = 0);
 
 }  // namespace ss

@@ -197,7 +197,10 @@ __global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ i
 // [contexts B*C][negatives ntile*S], contexts/negatives in namespace 1<<40.
 __global__ __launch_bounds__(256) void k_w2v_gen(uint64_t seed, long long base, int B, int C, int W,
                                                  long long nneg, long long V, double logV,
-                                                 float noise, uint64_t* __restrict__ keys) {
+                                                 float noise, uint64_t* __restrict__ keys,
+                                                 const long long* __restrict__ step_dev,
+                                                 long long step_mul, long long step_add) {
+  if (step_dev) base = *step_dev * step_mul + step_add;  // hipGraph replays (models.hip k_gen_ctr)
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long n = (long long)B + (long long)B * C + nneg;
   if (i >= n) return;
@@ -260,12 +263,14 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
 }
 
 void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,
-                    long long V, float noise, uint64_t* keys, hipStream_t st) {
+                    long long V, float noise, uint64_t* keys, hipStream_t st,
+                    const long long* step_dev, long long step_mul, long long step_add) {
   const long long n = (long long)B + (long long)B * C + nneg;
   if (n <= 0) return;
   if (W < 1) throw_error("w2v_gen: window must be >= 1");
   hipLaunchKernelGGL(k_w2v_gen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed, base, B,
-                     C, W, nneg, V, log((double)V + 1.0), noise, keys);
+                     C, W, nneg, V, log((double)V + 1.0), noise, keys, step_dev, step_mul,
+                     step_add);
   check_launch("k_w2v_gen");
 }
 

@@ -69,7 +69,7 @@ class FMWorker(PipelinedWorker):
 
     def _produce(self, step, slot, stream):
         self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
-                           stream=stream)
+                           stream=stream, **self._gen_kwargs(step))
         return self.keys[slot]
 
     def _compute(self, rnd, slot, st):

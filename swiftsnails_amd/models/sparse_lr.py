@@ -43,13 +43,19 @@ class CtrSynth:
     def vocab_per_field(self) -> int:
         return max(1, self.num_features // self.num_fields)
 
+    graph_capturable = True  # generate() can take its step from device memory
+
     def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, labels: torch.Tensor,
-                 stream=None):
+                 stream=None, step_dev: int = 0, step_delta: int = 0):
+        """Batch of global step ``step`` (samples [(step*world+rank)*B, +B)).
+        With ``step_dev`` (a device int64 pointer; hipGraph replays) the step
+        is ``*step_dev + step_delta`` instead, read by the kernel."""
         B, F = self.batch_size, self.num_fields
         base = (step * world + rank) * B
         st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         hip().gen_ctr(self.seed, base, B, F, self.vocab_per_field, self.tail_frac,
-                      self.truth_scale, self.truth_bias, keys.data_ptr(), labels.data_ptr(), st)
+                      self.truth_scale, self.truth_bias, keys.data_ptr(), labels.data_ptr(), st,
+                      step_dev, world * B, (step_delta * world + rank) * B)
 
 
 class SparseLRWorker(PipelinedWorker):
@@ -127,7 +133,7 @@ class SparseLRWorker(PipelinedWorker):
                                stream=stream, xval=self.xval[slot])
         else:
             self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
-                               stream=stream)
+                               stream=stream, **self._gen_kwargs(step))
         return self.keys[slot]
 
     def _compute(self, rnd, slot, st):

@@ -55,11 +55,16 @@ class W2VSynth:
     def neg_scale(self) -> float:
         return self.contexts * self.negatives / NEG_TILE
 
-    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None):
+    graph_capturable = True  # generate() can take its step from device memory
+
+    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None,
+                 step_dev: int = 0, step_delta: int = 0):
         st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
-        base = (step * world + rank) * self.batch_size
-        hip().w2v_gen(self.seed, base, self.batch_size, self.contexts, self.window,
-                      self.tiles * NEG_TILE, self.vocab, self.noise, keys.data_ptr(), st)
+        B = self.batch_size
+        base = (step * world + rank) * B
+        hip().w2v_gen(self.seed, base, B, self.contexts, self.window,
+                      self.tiles * NEG_TILE, self.vocab, self.noise, keys.data_ptr(), st,
+                      step_dev, world * B, (step_delta * world + rank) * B)
 
 
 def make_w2v_table_args(dim: int, optimizer: Optional[Optimizer] = None):
@@ -84,7 +89,8 @@ class Word2VecWorker(PipelinedWorker):
                      for _ in range(engine.depth)]
 
     def _produce(self, step, slot, stream):
-        self.data.generate(step, self.rank, self.world, self.keys[slot], stream=stream)
+        self.data.generate(step, self.rank, self.world, self.keys[slot], stream=stream,
+                           **self._gen_kwargs(step))
         return self.keys[slot]
 
     def _compute(self, rnd, slot, st):

@@ -58,6 +58,7 @@ class Routed:
     slot: int                               # ring slot of the route buffers
     counts: Optional[CountsHandle] = None   # N>1: host counts (async)
     ready: Optional[torch.cuda.Event] = None  # route-stream completion (GPU)
+    tag: Optional[int] = None               # hipGraph capture the event belongs to
 
 
 @dataclass
@@ -71,6 +72,7 @@ class Round:
     pushed: bool = False
     stats: dict = field(default_factory=dict)
     ready: Optional[object] = None        # pull-ahead: route-stream event of the pulled rows
+    tag: Optional[int] = None             # hipGraph capture of `ready`
 
     @property
     def inv(self) -> torch.Tensor:
@@ -182,6 +184,7 @@ class PSEngine:
             prio = -1 if os.environ.get("SS_ROUTE_PRIORITY", "0") != "0" else 0
             self.route_stream = torch.cuda.Stream(device=dev, priority=prio)
             self._free = [None] * self.depth  # main-stream event: slot buffers released
+            self._free_tag = [None] * self.depth
             self._pins = [torch.zeros(2 * N, dtype=torch.int64, pin_memory=True)
                           for _ in range(self.depth)]
         self.displs = [r * cap for r in range(N)]
@@ -205,6 +208,15 @@ class PSEngine:
         # occurrence-space unique ids (enable_osi): the model indexes rows
         # with the dedup's own inverse (bstart[b] + l), see ops/dedup.py
         self.osi = False
+        # hipGraph capture in progress (models/base.py enable_graph): an id
+        # per captured step.  Inside a capture the route stream forks from the
+        # capturing stream, and events of other captures are not waited on —
+        # graph replays run one after the other, so what they order is done
+        self.capture_tag: Optional[int] = None
+
+    def _wait(self, stream, ev, tag) -> None:
+        if ev is not None and tag == self.capture_tag:
+            stream.wait_event(ev)
 
     def enable_osi(self) -> bool:
         """Switch the dedupers to occurrence-space unique ids (bucketed dedup
@@ -259,9 +271,11 @@ class PSEngine:
             return Routed(dd, slot, counts)
         rs = self.route_stream
         main = torch.cuda.current_stream()
+        # previous user of this slot is done (inside a capture only if it ran
+        # in the same capture: an earlier replay has completed anyway)
         if self._free[slot] is not None:
-            rs.wait_event(self._free[slot])  # previous user of this slot is done
-        if keys is not None:
+            self._wait(rs, self._free[slot], self._free_tag[slot])
+        if keys is not None and self.capture_tag is None:
             rs.wait_stream(main)             # keys were produced on the main stream
         with torch.cuda.stream(rs):
             if produce is not None:
@@ -278,7 +292,7 @@ class PSEngine:
                                                        stream=rs)
             ev = torch.cuda.Event()
             ev.record(rs)
-        return Routed(dd, slot, counts, ev)
+        return Routed(dd, slot, counts, ev, self.capture_tag)
 
     # ------------------------------------------------------------ stage 2
     def _server_pull(self, rcounts: np.ndarray, slot: int) -> None:
@@ -299,7 +313,7 @@ class PSEngine:
         r = keys_or_routed if isinstance(keys_or_routed, Routed) else self.route(keys_or_routed)
         dd, slot = r.dd, r.slot
         if self.gpu:
-            torch.cuda.current_stream().wait_event(r.ready)
+            self._wait(torch.cuda.current_stream(), r.ready, r.tag)
         tab = self.table
         uv = self.uvals[slot]
         if self.fast1:
@@ -341,12 +355,12 @@ class PSEngine:
                 ev = torch.cuda.Event()
                 ev.record(rs)
             self.metrics.add(occurrences=dd.n)
-            return Round(dd, uv, slot, slots=self.slots[slot], ready=ev)
+            return Round(dd, uv, slot, slots=self.slots[slot], ready=ev, tag=self.capture_tag)
         scounts, rcounts = r.counts.wait()  # host: the route stage enqueued earlier
         D, uv = self.displs, self.uvals[slot]
         ps = self.pull_stream or self.route_stream
         if ps is not self.route_stream:
-            ps.wait_event(r.ready)
+            self._wait(ps, r.ready, r.tag)
         with torch.cuda.stream(ps):
             self.pt.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
             self._server_pull(rcounts, slot)
@@ -358,7 +372,7 @@ class PSEngine:
         self.metrics.add(occurrences=dd.n, unique_sent=sent, unique_recv=recv,
                          a2a_bytes=8 * (sent + recv) + 4 * self.dim * (2 * sent + 2 * recv))
         return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
-                     stats={"sent": sent, "recv": recv}, ready=ev)
+                     stats={"sent": sent, "recv": recv}, ready=ev, tag=self.capture_tag)
 
     def enable_pull_ahead(self, on: bool = True) -> bool:
         """Opt into pull-ahead (staleness 1) where the engine supports it."""
@@ -371,7 +385,7 @@ class PSEngine:
 
     def begin(self, rnd: Round) -> None:
         if rnd.ready is not None:
-            torch.cuda.current_stream().wait_event(rnd.ready)
+            self._wait(torch.cuda.current_stream(), rnd.ready, rnd.tag)
 
     # ------------------------------------------------------------ stage 3
     def _server_apply(self, rcounts: np.ndarray, slot: int, resolved: bool) -> None:
@@ -401,6 +415,7 @@ class PSEngine:
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream())
             self._free[slot] = ev
+            self._free_tag[slot] = self.capture_tag
 
     def push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
         g = rnd.ugrad if grads is None else grads
@@ -473,7 +488,7 @@ class PSEngine:
             if hasattr(own, "osi"):
                 own.osi = saved[2]
         if self.gpu:
-            torch.cuda.current_stream().wait_event(r.ready)
+            self._wait(torch.cuda.current_stream(), r.ready, r.tag)
         dd = r.dd
         rnd = Round(dd, self.uvals[r.slot], r.slot)
         self.accumulate(rnd, grads.to(self.device))

@@ -1,5 +1,7 @@
 """Model kernels on MI355X vs fp64/fp32 host references: word2vec SGNS, FM,
 plus short end-to-end training runs through the PS engine."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -175,3 +177,73 @@ def test_word2vec_trains_world1(dev):
     table.check()
     assert np.isfinite(losses).all()
     assert np.mean(losses[-5:]) < 0.8 * np.mean(losses[:3]), losses
+
+
+def _graph_worker(model, dev):
+    from swiftsnails_amd.models.fm import FMWorker, fm_table_args
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    if model == "lr":
+        data = CtrSynth(batch_size=4096, num_fields=13, num_features=1_000_000, tail_frac=0.1)
+        table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
+        eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
+        return SparseLRWorker(eng, data), table
+    if model == "fm":
+        data = CtrSynth(batch_size=2048, num_fields=16, num_features=100_000, tail_frac=0.1)
+        opt, init = fm_table_args(8)
+        table = HbmTable(9, 200_000, optimizer=opt, init=init, device=dev)
+        eng = PSEngine(table, None, max_keys=2048 * 16, dim=9, device=dev)
+        return FMWorker(eng, data), table
+    data = W2VSynth(batch_size=1024, window=3, vocab=5000, noise=0.05)
+    opt, init = make_w2v_table_args(64, None)
+    table = HbmTable(64, 40000, optimizer=opt, init=init, device=dev)
+    eng = PSEngine(table, None, max_keys=data.n_keys, dim=64, device=dev)
+    return Word2VecWorker(eng, data), table
+
+
+@pytest.mark.parametrize("model", ["lr", "fm", "w2v"])
+def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
+    """hipGraph replays (one graph per ring phase, device step counter for
+    the generator) train exactly like eager steps: same per-step losses and
+    the same table (up to float-atomic summation order).  Pull-ahead is off
+    here: with it, which of round i's updates round i+1 reads depends on
+    timing (staleness 1), in eager mode as much as in graphs."""
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    per = 1 if os.environ.get("SS_GRAPH_STEPS", "") == "1" else 3
+    n = 1 + 3 * 3
+    wa, ta = _graph_worker(model, dev)
+    la = [float(wa.step().sum().item()) for _ in range(n)]
+    wb, tb = _graph_worker(model, dev)
+    lb = [float(wb.step().sum().item())]
+    assert wb.enable_graph()
+    lb += [float(wb.step().sum().item()) for _ in range(n - 1)]
+    torch.cuda.synchronize()
+    ta.check()
+    tb.check()
+    # a multi-step graph (SS_GRAPH_STEPS) leaves the loss of its last step
+    idx = [0] + [k for k in range(1, n) if (k - 1) % per == per - 1]
+    np.testing.assert_allclose(np.array(lb)[idx], np.array(la)[idx], rtol=2e-4, atol=1e-3)
+    da, db = ta.to_dict(), tb.to_dict()
+    assert da.keys() == db.keys()
+    ks = list(da.keys())[:5000]
+    np.testing.assert_allclose(np.stack([db[k] for k in ks]), np.stack([da[k] for k in ks]),
+                               rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("model", ["fm", "w2v"])
+def test_hipgraph_pull_ahead_trains(dev, model):
+    """Graph replays of the pull-ahead pipeline (rows of round i+1 pulled on
+    the route stream while round i computes) keep training."""
+    w, t = _graph_worker(model, dev)
+    assert w.engine.pull_ahead
+    first = [float(w.step().sum().item()) for _ in range(3)]
+    assert w.enable_graph()
+    last = [float(w.step().sum().item()) for _ in range(30)]
+    torch.cuda.synchronize()
+    t.check()
+    assert np.isfinite(last).all()
+    assert np.mean(last[-5:]) < np.mean(first), (first, last[-5:])
