@@ -230,6 +230,9 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     log_every = log_every or int(cfg.get("log_every", 0) or 0)
     for _ in range(warmup):
         w.step()
+    # config `graph: 1`: replay the step as hipGraphs (1 GPU, synthetic data;
+    # a no-op where unsupported — see PipelinedWorker.enable_graph)
+    graphed = str(cfg.get("graph", "0")) not in ("0", "false", "") and w.enable_graph()
     torch.cuda.synchronize()
     ctx.barrier()
     t0 = time.perf_counter()
@@ -254,7 +257,7 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
              "servers": len(ctx.servers), "workers": len(ctx.workers), "steps": steps,
              "seconds": el, "ms_per_step": 1000 * el / max(1, steps),
              "samples_per_s": int(n.item()) * steps / el if el > 0 else 0.0,
-             "loss": w.mean_loss() if ctx.is_worker else None}
+             "loss": w.mean_loss() if ctx.is_worker else None, "hipgraph": bool(graphed)}
     m = ctx.engine.metrics.counters
     if m:
         stats["rank0_engine"] = {k: int(v) for k, v in m.items()}
