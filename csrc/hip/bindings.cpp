@@ -287,9 +287,20 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("w2v_sgns", [](uintptr_t inv_c, uintptr_t inv_x, uintptr_t inv_n, int B, int C, int D,
                        float neg_scale, uintptr_t uvals, uintptr_t ugrad, uintptr_t loss,
-                       uintptr_t st) {
+                       uintptr_t st, uintptr_t gpos) {
     launch_w2v_sgns(P<const uint32_t>(inv_c), P<const uint32_t>(inv_x), P<const uint32_t>(inv_n), B,
-                    C, D, neg_scale, P<const float>(uvals), P<float>(ugrad), P<float>(loss), S(st));
+                    C, D, neg_scale, P<const float>(uvals), P<float>(ugrad), P<float>(loss), S(st),
+                    P<float>(gpos));
+  }, py::arg("inv_c"), py::arg("inv_x"), py::arg("inv_n"), py::arg("B"), py::arg("C"),
+     py::arg("D"), py::arg("neg_scale"), py::arg("uvals"), py::arg("ugrad"), py::arg("loss"),
+     py::arg("st"), py::arg("gpos") = 0);
+  m.def("w2v_ctx_reduce", [](int P_, uintptr_t bstart, uintptr_t unum, uintptr_t ubase,
+                             uintptr_t pj, uintptr_t luid, uintptr_t inv_c, uintptr_t gpos, int B,
+                             int C, int D, uintptr_t uvals, uintptr_t ugrad, uintptr_t st) {
+    launch_w2v_ctx_reduce(P_, P<const uint32_t>(bstart), P<const uint32_t>(unum),
+                          P<const uint32_t>(ubase), P<const uint32_t>(pj), P<const uint32_t>(luid),
+                          P<const uint32_t>(inv_c), P<const float>(gpos), B, C, D,
+                          P<const float>(uvals), P<float>(ugrad), S(st));
   });
   m.def("w2v_gen", [](uint64_t seed, long long base, int B, int C, int W, long long nneg,
                       long long V, float noise, uintptr_t keys, uintptr_t st, uintptr_t step_dev,

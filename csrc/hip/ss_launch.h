@@ -130,7 +130,11 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
 size_t w2v_smem_bytes(int D);
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
-                     float* loss_sum, hipStream_t st);
+                     float* loss_sum, hipStream_t st, float* gpos = nullptr);
+void launch_w2v_ctx_reduce(int P, const uint32_t* bstart, const uint32_t* unum,
+                           const uint32_t* ubase, const uint32_t* pj, const uint32_t* luid,
+                           const uint32_t* inv_c, const float* gpos, int B, int C, int D,
+                           const float* uvals, float* ugrad, hipStream_t st);
 void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,
                     long long V, float noise, uint64_t* keys, hipStream_t st,
                     const long long* step_dev = nullptr, long long step_mul = 0,

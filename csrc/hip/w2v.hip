@@ -53,7 +53,8 @@ __global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ i
                                                   const uint32_t* __restrict__ inv_n, int B, int C,
                                                   float neg_scale, const float* __restrict__ uvals,
                                                   float* __restrict__ ugrad,
-                                                  float* __restrict__ loss_sum) {
+                                                  float* __restrict__ loss_sum,
+                                                  float* __restrict__ gpos) {
   constexpr int P = D + 1;  // padded LDS row
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Vs = smem;              // [T][P] center rows
@@ -133,13 +134,22 @@ __global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ i
         for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
         const float g = sigm(part) - 1.f;  // d/ds softplus(-s)
         if (lane == 0) loss += softplus(-part);
-        float* gu = ugrad + (long long)x * D;
+        if (gpos) {
+          // the context row's gradient g * v goes out as one scalar per pair;
+          // k_w2v_ctx_reduce sums g * v per unique context key (plain loads)
+          if (lane == 0) gpos[(t0 + t) * (long long)C + j] = g;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int d = lane + 64 * r;
-          if (d < D) {
-            atomicAdd(gu + d, g * v[r]);
-            gv[r] += g * u[j][r];
+          for (int r = 0; r < R; ++r)
+            if (lane + 64 * r < D) gv[r] += g * u[j][r];
+        } else {
+          float* gu = ugrad + (long long)x * D;
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int d = lane + 64 * r;
+            if (d < D) {
+              atomicAdd(gu + d, g * v[r]);
+              gv[r] += g * u[j][r];
+            }
           }
         }
       }
@@ -187,6 +197,106 @@ __global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ i
 #pragma unroll
     for (int i = 0; i < kNW; ++i) tot += red[i];
     ctr_addf(loss_sum, tot);
+  }
+}
+
+// Context-row gradients without global atomics (the sgns kernel's positive
+// pairs otherwise issue one 256-B row of float atomics per pair: 84 MB per
+// 16K-center step at the memory-side atomic rate, ~1.3 TB/s, which also
+// stalls every other stream's memory traffic).  One workgroup per bucket of
+// the bucketed dedup: its context occurrences p (key index j in [B, B+B*C))
+// add gpos[pair] * (center row of the pair) into LDS rows of the bucket's
+// unique keys, a window of kCW keys per pass; each row is then added to its
+// gradient row once (plain read-modify-write: the sgns kernel, whose atomics
+// cover the negative-sample part of the same rows, ran before on the stream).
+static constexpr int kCW = 64;  // unique keys per LDS window
+template <int D>
+__global__ __launch_bounds__(256) void k_w2v_ctx_reduce(const uint32_t* __restrict__ bstart,
+                                                        const uint32_t* __restrict__ unum,
+                                                        const uint32_t* __restrict__ ubase,
+                                                        const uint32_t* __restrict__ pj,
+                                                        const uint32_t* __restrict__ luid,
+                                                        const uint32_t* __restrict__ inv_c,
+                                                        const float* __restrict__ gpos, int B,
+                                                        int C, const float* __restrict__ uvals,
+                                                        float* __restrict__ ugrad) {
+  constexpr int R = (D + 63) / 64;
+  __shared__ float acc[kCW][D];
+  __shared__ uint32_t hit;
+  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
+  const long long jc0 = B, jc1 = (long long)B + (long long)B * C;
+  for (uint32_t l0 = 0; l0 < nu; l0 += kCW) {
+    for (int e = threadIdx.x; e < kCW * D; e += 256) (&acc[0][0])[e] = 0.f;
+    if (threadIdx.x == 0) hit = 0;
+    __syncthreads();
+    // wave w loads the metadata of 64 occurrences at once (lane i: p = pb + i),
+    // then walks the ones that hit this window, 4 rows in flight at a time;
+    // lanes sweep the row
+    for (uint32_t pb = p0 + 64 * w; pb < p1; pb += 256) {
+      const uint32_t p = pb + lane;
+      uint32_t l = kInv, c = kInv;
+      float g = 0.f;
+      if (p < p1) {
+        l = luid[p];
+        if (l != kInv && l >= l0 && l < l0 + kCW) {
+          const long long j = pj[p];
+          if (j >= jc0 && j < jc1) {  // a context occurrence (not a center / negative)
+            const long long pair = j - jc0;
+            c = inv_c[pair / C];
+            g = gpos[pair];
+          }
+        }
+      }
+      unsigned long long m = __ballot(c != kInv);
+      if (m && lane == 0) hit = 1;
+      while (m) {
+        int k[4];
+        int nk = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          k[q] = m ? __builtin_ctzll(m) : -1;
+          if (m) {
+            m &= m - 1;
+            ++nk;
+          }
+        }
+        float v[4][R];
+        uint32_t lk[4];
+        float gk[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int src = k[q] < 0 ? 0 : k[q];
+          const uint32_t cq = __shfl(c, src, 64);
+          lk[q] = __shfl(l, src, 64);
+          gk[q] = __shfl(g, src, 64);
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int d = lane + 64 * r;
+            v[q][r] = (q < nk && d < D) ? uvals[(size_t)cq * D + d] : 0.f;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q >= nk) break;  // wave-uniform
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+            const int d = lane + 64 * r;
+            if (d < D) atomicAdd(&acc[lk[q] - l0][d], gk[q] * v[q][r]);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (hit) {
+      const uint32_t n = min((uint32_t)kCW, nu - l0);
+      for (uint32_t e = threadIdx.x; e < n * D; e += 256) {
+        const uint32_t l = e / D, d = e - l * D;
+        float* gr = ugrad + (size_t)(base + l0 + l) * D + d;
+        *gr += acc[l][d];
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -238,7 +348,7 @@ size_t w2v_smem_bytes(int D) {
 
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
-                     float* loss_sum, hipStream_t st) {
+                     float* loss_sum, hipStream_t st, float* gpos) {
   if (B <= 0) return;
   if (C < 1 || C > kMaxC) throw_error("w2v_sgns: contexts per center must be in [1,16]");
   const int tiles = (B + kT - 1) / kT;
@@ -250,7 +360,7 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm),    \
               "w2v smem attr");                                                             \
     hipLaunchKernelGGL(k_w2v_sgns<DD>, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, \
-                       neg_scale, uvals, ugrad, loss_sum);                                  \
+                       neg_scale, uvals, ugrad, loss_sum, gpos);                            \
     break;
     SS_W2V_CASE(32)
     SS_W2V_CASE(64)
@@ -260,6 +370,27 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
       throw_error("w2v_sgns: D must be 32, 64 or 128");
   }
   check_launch("k_w2v_sgns");
+}
+
+void launch_w2v_ctx_reduce(int P, const uint32_t* bstart, const uint32_t* unum,
+                           const uint32_t* ubase, const uint32_t* pj, const uint32_t* luid,
+                           const uint32_t* inv_c, const float* gpos, int B, int C, int D,
+                           const float* uvals, float* ugrad, hipStream_t st) {
+  if (P <= 0 || B <= 0) return;
+  switch (D) {
+#define SS_W2VR_CASE(DD)                                                                    \
+  case DD:                                                                                  \
+    hipLaunchKernelGGL(k_w2v_ctx_reduce<DD>, dim3(P), dim3(256), 0, st, bstart, unum, ubase, pj, \
+                       luid, inv_c, gpos, B, C, uvals, ugrad);                              \
+    break;
+    SS_W2VR_CASE(32)
+    SS_W2VR_CASE(64)
+    SS_W2VR_CASE(128)
+#undef SS_W2VR_CASE
+    default:
+      throw_error("w2v_ctx_reduce: D must be 32, 64 or 128");
+  }
+  check_launch("k_w2v_ctx_reduce");
 }
 
 void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,

@@ -15,6 +15,7 @@ namespace starts at zero (``InitConfig.zero_key_bit=40``), the input one at
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -87,6 +88,16 @@ class Word2VecWorker(PipelinedWorker):
         engine.enable_pull_ahead()
         self.keys = [torch.empty(data.n_keys, dtype=torch.int64, device=engine.device)
                      for _ in range(engine.depth)]
+        # SS_W2V_CTX=reduce: context-row gradients as one scalar per (center,
+        # context) pair, summed per unique context key over the bucketed
+        # dedup's partition (k_w2v_ctx_reduce) instead of a row of float
+        # atomics per pair.  Measured slower (0.32 -> 0.81 ms/step): the sgns
+        # kernel drops 204 -> 105 us, but a Zipf-head context key puts
+        # thousands of row loads into one bucket's workgroup (587 us tail)
+        self.ctx_reduce = (os.environ.get("SS_W2V_CTX", "atomic") == "reduce" and
+                           all(getattr(d, "mode", None) == "bucket" for d in engine.dedupers))
+        self.gpos = (torch.empty(data.batch_size * data.contexts, dtype=torch.float32,
+                                 device=engine.device) if self.ctx_reduce else None)
 
     def _produce(self, step, slot, stream):
         self.data.generate(step, self.rank, self.world, self.keys[slot], stream=stream,
@@ -98,9 +109,16 @@ class Word2VecWorker(PipelinedWorker):
         inv = rnd.inv
         B, C = d.batch_size, d.contexts
         ptr, es = inv.data_ptr(), inv.element_size()
-        hip().w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
-                       d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
-                       self.loss_sum.data_ptr(), st)
+        h = hip()
+        h.w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
+                   d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
+                   self.loss_sum.data_ptr(), st, self.gpos.data_ptr() if self.ctx_reduce else 0)
+        if self.ctx_reduce:
+            o = rnd.dd.owner
+            _, bstart, unum, ubase, P = o.bucket_view(rnd.dd.n)
+            h.w2v_ctx_reduce(P, bstart, unum, ubase, o.pj.data_ptr(), o.luid.data_ptr(), ptr,
+                             self.gpos.data_ptr(), B, C, self.engine.dim, rnd.uvals.data_ptr(),
+                             rnd.ugrad.data_ptr(), st)
 
     def samples_per_step(self) -> int:
         """Positive (center, context) pairs per step ("words/s" numerator)."""

@@ -247,3 +247,26 @@ def test_hipgraph_pull_ahead_trains(dev, model):
     t.check()
     assert np.isfinite(last).all()
     assert np.mean(last[-5:]) < np.mean(first), (first, last[-5:])
+
+
+def test_word2vec_context_reduce_matches_atomics(dev, monkeypatch):
+    """Context-row gradients summed per unique key over the dedup buckets
+    (k_w2v_ctx_reduce) == one row of float atomics per (center, context)."""
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    out = {}
+    for mode in ("reduce", "atomic"):
+        monkeypatch.setenv("SS_W2V_CTX", mode)  # (atomic is the default)
+        w, t = _graph_worker("w2v", dev)
+        assert w.ctx_reduce == (mode == "reduce")
+        losses = [float(w.step().sum().item()) for _ in range(6)]
+        torch.cuda.synchronize()
+        t.check()
+        out[mode] = (losses, t.to_dict(with_state=True))
+    (lr, tr), (la, ta) = out["reduce"], out["atomic"]
+    np.testing.assert_allclose(lr, la, rtol=1e-4)
+    assert tr.keys() == ta.keys()
+    ks = list(tr.keys())
+    # summation order differs (LDS vs memory-side atomics); AdaGrad divides by
+    # a still-small accumulator in the first steps, so allow a few 1e-4
+    np.testing.assert_allclose(np.stack([tr[k] for k in ks]), np.stack([ta[k] for k in ks]),
+                               rtol=1e-3, atol=5e-4)
