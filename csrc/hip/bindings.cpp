@@ -57,11 +57,12 @@ PYBIND11_MODULE(_ss_hip, m) {
 
   py::class_<DevTable>(m, "DevTable", py::module_local())
       .def(py::init([](uintptr_t base, unsigned long long cap, uint32_t stride, uint32_t key_off,
-                       uint32_t dim, uint32_t width, uint32_t prefilled) {
-             return DevTable{P<char>(base), cap, stride, key_off, dim, width, prefilled};
+                       uint32_t dim, uint32_t width, uint32_t prefilled, uint32_t row_off) {
+             return DevTable{P<char>(base), cap, stride, key_off, dim, width, prefilled, row_off};
            }),
            py::arg("base"), py::arg("cap"), py::arg("stride"), py::arg("key_off"), py::arg("dim"),
-           py::arg("width"), py::arg("prefilled") = 0)
+           py::arg("width"), py::arg("prefilled") = 0, py::arg("row_off") = 0)
+      .def_readonly("row_off", &DevTable::row_off)
       .def_readonly("prefilled", &DevTable::prefilled)
       .def_readonly("cap", &DevTable::cap)
       .def_readonly("stride", &DevTable::stride)

@@ -48,13 +48,14 @@ struct DevTable {
   // init, filled at allocation), so an insert is the key CAS alone — no
   // second write to the freshly claimed line
   uint32_t prefilled;
+  uint32_t row_off;   // byte offset of the row (params, then optimizer state)
 };
 
 __device__ __forceinline__ uint64_t* slot_key(const DevTable& t, uint64_t s) {
   return reinterpret_cast<uint64_t*>(t.base + s * (uint64_t)t.stride + t.key_off);
 }
 __device__ __forceinline__ float* slot_row(const DevTable& t, uint64_t s) {
-  return reinterpret_cast<float*>(t.base + s * (uint64_t)t.stride);
+  return reinterpret_cast<float*>(t.base + s * (uint64_t)t.stride + t.row_off);
 }
 
 // A list of (offset, count) segments inside one buffer.  The collective

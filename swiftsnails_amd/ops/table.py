@@ -43,13 +43,27 @@ def _align(x: int, a: int) -> int:
     return (x + a - 1) // a * a
 
 
-def slot_layout(width: int) -> tuple[int, int]:
-    """(stride_bytes, key_offset_bytes) of one slot."""
-    key_off = _align(4 * width, 8)
-    stride = key_off + 8
-    if width >= 4:
-        stride = _align(stride, 16)
-    return stride, key_off
+def slot_layout(width: int, layout: Optional[str] = None) -> tuple[int, int, int]:
+    """(stride_bytes, key_offset_bytes, row_offset_bytes) of one slot.
+
+    ``rowfirst``: [row | key] (scalar rows: LR's 16-byte [w, h, key] slot).
+    ``keyfirst``: [key | row], so the key and the parameters a pull reads sit
+    together at the slot's start.  ``keyfirst_line``: the same, stride padded
+    to whole 64-byte lines (a pull of key + params touches one line)."""
+    layout = layout or os.environ.get("SS_TABLE_LAYOUT", "") or (
+        "rowfirst" if width <= 2 else "keyfirst")
+    if layout == "rowfirst":
+        key_off = _align(4 * width, 8)
+        stride = key_off + 8
+        if width >= 4:
+            stride = _align(stride, 16)
+        return stride, key_off, 0
+    if layout not in ("keyfirst", "keyfirst_line"):
+        raise ValueError(f"slot layout {layout!r}")
+    stride = _align(8 + 4 * width, 16 if width >= 2 else 8)
+    if layout == "keyfirst_line":
+        stride = _align(stride, 64)
+    return stride, 0, 8
 
 
 def default_lane_group(width: int) -> int:
@@ -88,7 +102,7 @@ class HbmTable:
         self.opt = optimizer or Optimizer()
         self.init_cfg = init or InitConfig()
         self.width = self.dim + self.opt.state_width(self.dim)
-        self.stride, self.key_off = slot_layout(self.width)
+        self.stride, self.key_off, self.row_off = slot_layout(self.width)
         self.G = lane_group or int(os.environ.get("SS_TABLE_G", "0")) or \
             default_lane_group(self.width)
         self.max_load = max_load
@@ -114,21 +128,22 @@ class HbmTable:
             slots[:, self.key_off:self.key_off + 8].fill_(255)  # every key word = EMPTY
             if self.width > self.dim and float(self.init_cfg.state_init) != 0.0:
                 rows = self.storage.view(torch.float32).view(cap, self.stride // 4)
-                rows[:, self.dim:self.width].fill_(float(self.init_cfg.state_init))
+                r0 = self.row_off // 4
+                rows[:, r0 + self.dim:r0 + self.width].fill_(float(self.init_cfg.state_init))
         else:
             self.storage.fill_(255)  # every key word = EMPTY (rows: the 0xFF sentinel)
         # sharded counter: 256 shards x 128 B (see ss_device.h ctr_add)
         self.size_ctr = torch.zeros(CTR_SHARDS * 16, dtype=torch.int64, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.dt = hip().DevTable(self.storage.data_ptr(), cap, self.stride, self.key_off, self.dim,
-                                 self.width, int(self.prefilled))
+                                 self.width, int(self.prefilled), self.row_off)
 
     @staticmethod
     def plan(n_keys: int, dim: int, optimizer: Optional[Optimizer] = None,
              load: float = 0.7) -> dict:
         opt = optimizer or Optimizer()
         width = dim + opt.state_width(dim)
-        stride, _ = slot_layout(width)
+        stride, _, _ = slot_layout(width)
         cap = int(math.ceil(n_keys / load))
         return {"capacity": cap, "stride": stride, "bytes": cap * stride, "width": width}
 
