@@ -504,7 +504,7 @@ template <int K>
 struct FmCols {
   static constexpr int v = (K + 1) * kBdTS * 4 <= 150 * 1024 ? K : 8;
 };
-template <int DIM>
+template <int DIM, int NCOLS = 0>
 __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ ubase,
                                                        const uint32_t* __restrict__ unum,
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
                                                        const float* __restrict__ uvals,
                                                        float* __restrict__ ugrad) {
   constexpr int K = DIM - 1;
-  constexpr int NC = FmCols<K>::v;
+  constexpr int NC = NCOLS > 0 ? (NCOLS < K ? NCOLS : K) : FmCols<K>::v;
   __shared__ float g0[kBdTS];
   __shared__ float acc[NC][kBdTS];
   const int b = blockIdx.x;
@@ -715,11 +715,24 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
   if (n <= 0) return;
   const BdLayout L = bd_layout(n, nranks);
   const uint32_t* S = scratch;
+  // SS_FM_NC: factor columns accumulated per pass (default: all that fit in
+  // LDS; 4 -> 80 KB, two workgroups per CU) — experiment knob
+  static const int nc = [] {
+    const char* e = std::getenv("SS_FM_NC");
+    return e ? std::atoi(e) : 0;
+  }();
   switch (dim) {
 #define SS_BDFM_CASE(DD)                                                                       \
   case DD:                                                                                     \
-    hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,          \
-                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);           \
+    if (nc == 4)                                                                               \
+      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 4>), dim3(L.P), dim3(1024), 0, st, S + L.bstart,  \
+                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);         \
+    else if (nc == 2)                                                                          \
+      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 2>), dim3(L.P), dim3(1024), 0, st, S + L.bstart,  \
+                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);         \
+    else                                                                                       \
+      hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,        \
+                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);         \
     break;
     SS_BDFM_CASE(2)
     SS_BDFM_CASE(5)
