@@ -44,6 +44,7 @@
 // 4096-slot LDS table (overflow is detected and reported, never silent).
 #include <algorithm>
 #include <cstdlib>
+#include <string>
 
 #include "bdindex.h"
 #include "scan.h"
@@ -513,16 +514,25 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
                                                        const float* __restrict__ gs,
                                                        const float* __restrict__ gss, int F,
                                                        const float* __restrict__ uvals,
-                                                       float* __restrict__ ugrad) {
+                                                       float* __restrict__ ugrad,
+                                                       const uint32_t* __restrict__ blist) {
   constexpr int K = DIM - 1;
   constexpr int NC = NCOLS > 0 ? (NCOLS < K ? NCOLS : K) : FmCols<K>::v;
   __shared__ float g0[kBdTS];
   __shared__ float acc[NC][kBdTS];
-  const int b = blockIdx.x;
+  // blist: only the buckets listed there ({count, b...}, the sorted kernel's
+  // overflow list), one per workgroup
+  if (blist && blockIdx.x >= blist[0]) return;
+  const int b = blist ? (int)blist[1 + blockIdx.x] : (int)blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
-  for (int c0 = 0; c0 < K; c0 += NC) {
+  // gridDim.y > 1: workgroup y of the bucket takes column group y alone (the
+  // bucket's column passes run on different CUs); each accumulates G0 itself
+  const int cstart = gridDim.y > 1 ? (int)blockIdx.y * NC : 0;
+  const int cend = gridDim.y > 1 ? min(K, cstart + NC) : K;
+  for (int c0 = cstart; c0 < cend; c0 += NC) {
+    const bool first = c0 == cstart;
     for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
-      if (c0 == 0) g0[l] = 0.f;
+      if (first) g0[l] = 0.f;
 #pragma unroll
       for (int c = 0; c < NC; ++c) acc[c][l] = 0.f;
     }
@@ -542,7 +552,7 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         const uint32_t s = sm[r] / (uint32_t)F;
-        g[r] = (c0 == 0 && l[r] != kBdInvalid) ? gs[s] : 0.f;
+        g[r] = (first && l[r] != kBdInvalid) ? gs[s] : 0.f;
         if constexpr (NC == K && K % 4 == 0) {
           // whole 32-B-aligned row of the sample: 16-B vector loads
           const float4* g4 = reinterpret_cast<const float4*>(gss + (size_t)s * K);
@@ -560,7 +570,7 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
 #pragma unroll
       for (int r = 0; r < RB; ++r) {
         if (l[r] == kBdInvalid) continue;
-        if (c0 == 0) atomicAdd(&g0[l[r]], g[r]);
+        if (first) atomicAdd(&g0[l[r]], g[r]);
 #pragma unroll
         for (int c = 0; c < NC; ++c)
           if (c0 + c < K) atomicAdd(&acc[c][l[r]], v[r][c]);
@@ -603,6 +613,123 @@ __global__ __launch_bounds__(256) void k_bd_unplace(const uint32_t* __restrict__
   const float* s = src + (size_t)ubase[b] * dim;
   float* d = dst + (size_t)bstart[b] * dim;
   for (unsigned int e = threadIdx.x; e < n; e += 256) d[e] = s[e];
+}
+
+// K7 for FM rows without float atomics.  Measured: the LDS form above is
+// bound by its 1 + K ds_add_f32 per occurrence (212 us per 2.56M keys at
+// K = 8; 63 us with plain stores in their place).  Here each bucket's
+// occurrences are grouped by unique id with a counting sort in LDS (two
+// integer LDS atomics per occurrence), then every unique key's occurrence
+// list is summed in registers — one thread per short list, one wave per list
+// longer than kFmLong (Zipf heads: thousands of occurrences) — and its row
+// is stored once.  Buckets with more than kFmOcc occurrences are listed in
+// `ovf` for the LDS-atomic kernel above.
+static constexpr int kFmOcc = 10240;  // occurrences sorted in LDS per bucket (76 KB: 2 per CU)
+static constexpr int kFmLong = 16;    // longer lists: one wave each
+template <int DIM>
+__global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
+    const uint32_t* __restrict__ bstart, const uint32_t* __restrict__ ubase,
+    const uint32_t* __restrict__ unum, const uint32_t* __restrict__ pj,
+    const uint32_t* __restrict__ luid, const float* __restrict__ gs,
+    const float* __restrict__ gss, int F, const float* __restrict__ uvals,
+    float* __restrict__ ugrad, uint32_t* __restrict__ ovf) {
+  constexpr int K = DIM - 1;
+  __shared__ uint32_t cnt[kBdTS];      // counts, then placement cursors
+  __shared__ uint32_t seg[kBdTS + 1];  // list starts (exclusive scan of the counts)
+  __shared__ uint32_t ord[kFmOcc];     // sample index of each occurrence, grouped by id
+  __shared__ uint32_t longl[kFmOcc / (kFmLong + 1) + 1];
+  __shared__ uint32_t nlong;
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned int tot;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
+  if (p1 - p0 > (uint32_t)kFmOcc) {  // workgroup-uniform
+    if (tid == 0) ovf[1 + atomicAdd(&ovf[0], 1u)] = (uint32_t)b;
+    return;
+  }
+  for (uint32_t l = tid; l < nu; l += 1024) cnt[l] = 0u;
+  if (tid == 0) nlong = 0u;
+  __syncthreads();
+  for (uint32_t p = p0 + tid; p < p1; p += 1024) {
+    const uint32_t l = luid[p];
+    if (l != kBdInvalid) atomicAdd(&cnt[l], 1u);
+  }
+  __syncthreads();
+  // exclusive scan of the nu <= 4096 counts, 4 per thread
+  uint32_t c4[4], sum = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t l = 4 * tid + k;
+    c4[k] = l < nu ? cnt[l] : 0u;
+    sum += c4[k];
+  }
+  uint32_t e = block_excl_scan<16>(sum, wsum, &tot);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t l = 4 * tid + k;
+    if (l < nu) {
+      seg[l] = e;
+      cnt[l] = e;
+      if (c4[k] > (uint32_t)kFmLong) longl[atomicAdd(&nlong, 1u)] = l;
+    }
+    e += c4[k];
+  }
+  if (tid == 0) seg[nu] = tot;
+  __syncthreads();
+  for (uint32_t p = p0 + tid; p < p1; p += 1024) {
+    const uint32_t l = luid[p];
+    if (l != kBdInvalid) ord[atomicAdd(&cnt[l], 1u)] = pj[p] / (uint32_t)F;
+  }
+  __syncthreads();
+  // one unique key's sums over sample rows [q0, q1) of its list, step `st`
+  auto accumulate = [&](uint32_t q0, uint32_t q1, uint32_t st, float& g0, float* a) {
+    for (uint32_t q = q0; q < q1; q += st) {
+      const uint32_t sm = ord[q];
+      g0 += gs[sm];
+      if constexpr (K % 4 == 0) {
+        const float4* g4 = reinterpret_cast<const float4*>(gss + (size_t)sm * K);
+#pragma unroll
+        for (int k = 0; k < K / 4; ++k) {
+          const float4 x = g4[k];
+          a[4 * k] += x.x, a[4 * k + 1] += x.y, a[4 * k + 2] += x.z, a[4 * k + 3] += x.w;
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < K; ++k) a[k] += gss[(size_t)sm * K + k];
+      }
+    }
+  };
+  auto store_row = [&](uint32_t l, float g0, const float* a) {
+    const size_t r = (size_t)(base + l) * DIM;
+    ugrad[r] = g0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) ugrad[r + 1 + k] = a[k] - uvals[r + 1 + k] * g0;
+  };
+  // short lists: a thread per unique key
+  for (uint32_t l = tid; l < nu; l += 1024) {
+    const uint32_t q0 = seg[l], q1 = seg[l + 1];
+    if (q1 - q0 > (uint32_t)kFmLong) continue;
+    float g0 = 0.f, a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.f;
+    accumulate(q0, q1, 1u, g0, a);
+    store_row(l, g0, a);
+  }
+  // long lists: a wave per unique key, lanes stride the list, wave-reduced
+  const int lane = tid & 63, w = tid >> 6;
+  for (uint32_t i = w; i < nlong; i += 16) {
+    const uint32_t l = longl[i];
+    float g0 = 0.f, a[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) a[k] = 0.f;
+    accumulate(seg[l] + lane, seg[l + 1], 64u, g0, a);
+    for (int o = 32; o > 0; o >>= 1) {
+      g0 += __shfl_xor(g0, o, 64);
+#pragma unroll
+      for (int k = 0; k < K; ++k) a[k] += __shfl_xor(a[k], o, 64);
+    }
+    if (lane == 0) store_row(l, g0, a);
+  }
 }
 
 // ------------------------------------------------------------- launchers
@@ -709,30 +836,66 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   check_launch("k_bd_reduce");
 }
 
+long long bd_fm_ovf_words(long long n) { return n / kFmOcc + 2; }
+
 void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                          const uint32_t* luid, const float* gs, const float* gss, int F, int dim,
-                         const float* uvals, float* ugrad, hipStream_t st) {
+                         const float* uvals, float* ugrad, hipStream_t st, uint32_t* ovf) {
   if (n <= 0) return;
   const BdLayout L = bd_layout(n, nranks);
   const uint32_t* S = scratch;
+  // default: sorted lists (no float atomics) + LDS-atomic form for overflow
+  // buckets; ovf = {count, bucket ids} scratch of bd_fm_ovf_words(n) words
+  static const bool sorted = [] {
+    const char* e = std::getenv("SS_FM_REDUCE");
+    return !(e && std::string(e) == "atomic");
+  }();
+  if (ovf && sorted) {
+    const int novf = (int)(n / kFmOcc) + 1;  // an overflow bucket holds > kFmOcc keys
+    check_hip(hipMemsetAsync(ovf, 0, sizeof(uint32_t), st), "fm ovf count");
+    switch (dim) {
+#define SS_BDFMS_CASE(DD)                                                                      \
+  case DD:                                                                                     \
+    hipLaunchKernelGGL(k_bd_reduce_fm_sorted<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,  \
+                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, ovf);      \
+    hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(novf), dim3(1024), 0, st, S + L.bstart,         \
+                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, ovf);      \
+    break;
+      SS_BDFMS_CASE(2)
+      SS_BDFMS_CASE(5)
+      SS_BDFMS_CASE(9)
+      SS_BDFMS_CASE(17)
+#undef SS_BDFMS_CASE
+      default:
+        throw_error("bd_reduce_fm: dim must be 1+K with K in {1,4,8,16}");
+    }
+    check_launch("k_bd_reduce_fm_sorted");
+    return;
+  }
   // SS_FM_NC: factor columns accumulated per pass (default: all that fit in
   // LDS; 4 -> 80 KB, two workgroups per CU) — experiment knob
   static const int nc = [] {
     const char* e = std::getenv("SS_FM_NC");
     return e ? std::atoi(e) : 0;
   }();
+  static const bool split = [] {
+    const char* e = std::getenv("SS_FM_SPLIT");
+    return e && std::atoi(e) != 0;
+  }();
   switch (dim) {
 #define SS_BDFM_CASE(DD)                                                                       \
   case DD:                                                                                     \
     if (nc == 4)                                                                               \
-      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 4>), dim3(L.P), dim3(1024), 0, st, S + L.bstart,  \
-                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);         \
+      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 4>), dim3(L.P, split ? (DD + 2) / 4 : 1),        \
+                         dim3(1024), 0, st, S + L.bstart,                                      \
+                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, nullptr);   \
     else if (nc == 2)                                                                          \
-      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 2>), dim3(L.P), dim3(1024), 0, st, S + L.bstart,  \
-                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);         \
+      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 2>), dim3(L.P, split ? DD / 2 : 1), dim3(1024), 0, \
+                         st, S + L.bstart,                                                     \
+                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, nullptr);   \
     else                                                                                       \
       hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,        \
-                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad);         \
+                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, nullptr);   \
     break;
     SS_BDFM_CASE(2)
     SS_BDFM_CASE(5)

@@ -66,6 +66,9 @@ class FMWorker(PipelinedWorker):
                 dd.materialize_inv = False
             self.gs = torch.empty(B, dtype=torch.float32, device=dev)
             self.gss = torch.empty(B * K, dtype=torch.float32, device=dev)
+            # overflow-bucket list of the sorted reduce (buckets too large to
+            # sort in LDS go to the LDS-atomic form)
+            self.ovf = torch.zeros(hip().bd_fm_ovf_words(B * F), dtype=torch.int32, device=dev)
 
     def _produce(self, step, slot, stream):
         self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
@@ -82,7 +85,7 @@ class FMWorker(PipelinedWorker):
             h.bd_reduce_fm(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                            o.luid.data_ptr(), self.gs.data_ptr(), self.gss.data_ptr(),
                            d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
-                           rnd.ugrad.data_ptr(), st)
+                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr())
             return
         hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),

@@ -135,13 +135,60 @@ def test_fm_bucket_reduce_matches_atomic_path(dev, dim, nranks):
                uvals.data_ptr(), gs.data_ptr(), gss.data_ptr(), l_b.data_ptr(), 0, st)
     h.bd_reduce_fm(n, nranks, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
                    gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_b.data_ptr(), st)
+    # the sorted-list form (default with an overflow list)
+    ovf = torch.zeros(h.bd_fm_ovf_words(n), dtype=torch.int32, device=dev)
+    g_s = torch.full((U, dim), float("nan"), device=dev)
+    h.bd_reduce_fm(n, nranks, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
+                   gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_s.data_ptr(), st,
+                   ovf.data_ptr())
     torch.cuda.synchronize()
     uc = r.ucount.cpu().numpy()
     for q in range(nranks):
         a, b = q * d.ucap, q * d.ucap + uc[q]
         np.testing.assert_allclose(g_b[a:b].cpu().numpy(), g_at[a:b].cpu().numpy(), rtol=2e-3,
                                    atol=2e-4)
+        np.testing.assert_allclose(g_s[a:b].cpu().numpy(), g_at[a:b].cpu().numpy(), rtol=2e-3,
+                                   atol=2e-4)
     np.testing.assert_allclose(l_b.sum().item(), l_at.sum().item(), rtol=1e-4)
+
+
+@pytest.mark.parametrize("dim", [5, 9])
+def test_fm_sorted_reduce_overflow_buckets(dev, dim):
+    """Sorted-list FM reduce with buckets too large to sort in LDS (a key
+    with 30K occurrences): those go to the LDS-atomic form; both == the
+    per-occurrence atomic kernel."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.dedup import Deduper
+
+    h = hip()
+    B, F = 16000, 8
+    n = B * F
+    rng = np.random.default_rng(17)
+    keys = rng.integers(0, 1 << 40, size=n).astype(np.int64)
+    keys[rng.random(n) < 0.25] = 12345  # ~32K occurrences of one key
+    d = Deduper(n, nranks=1, gdim=dim, device=dev, mode="bucket")
+    r = d(torch.from_numpy(keys).to(dev))
+    st = torch.cuda.current_stream().cuda_stream
+    U = d.ucap
+    uvals = torch.randn(U, dim, device=dev) * 0.1
+    y = torch.from_numpy((rng.random(B) < 0.4).astype(np.float32)).to(dev)
+    g_at = torch.zeros(U, dim, device=dev)
+    h.fm_fwd_bwd(r.inv.data_ptr(), y.data_ptr(), B, F, dim, uvals.data_ptr(), g_at.data_ptr(),
+                 0, 0, st)
+    gs = torch.empty(B, device=dev)
+    gss = torch.empty(B * (dim - 1), device=dev)
+    h.fm_fwd_g(0, d.index_ptrs(n), y.data_ptr(), B, F, dim,
+               uvals.data_ptr(), gs.data_ptr(), gss.data_ptr(), 0, 0, st)
+    ovf = torch.zeros(h.bd_fm_ovf_words(n), dtype=torch.int32, device=dev)
+    g_s = torch.full((U, dim), float("nan"), device=dev)
+    h.bd_reduce_fm(n, 1, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
+                   gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_s.data_ptr(), st,
+                   ovf.data_ptr())
+    torch.cuda.synchronize()
+    assert int(ovf[0]) >= 1  # the hot key's bucket overflowed
+    u = int(r.ucount[0])
+    np.testing.assert_allclose(g_s[:u].cpu().numpy(), g_at[:u].cpu().numpy(), rtol=2e-3,
+                               atol=5e-3)
 
 
 def test_fm_trains_world1(dev):

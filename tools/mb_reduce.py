@@ -60,6 +60,14 @@ def main():
         t_fm = time_calls(lambda: h.bd_reduce_fm(n, 1, d.scratch.data_ptr(), d.pj.data_ptr(),
                                                  d.luid.data_ptr(), gs.data_ptr(), gss.data_ptr(),
                                                  F, D, uvals.data_ptr(), ug.data_ptr(), st))
+        ovf = torch.zeros(h.bd_fm_ovf_words(n), dtype=torch.int32, device=dev)
+        ug2 = torch.empty(n, D, device=dev)
+        t_fms = time_calls(lambda: h.bd_reduce_fm(n, 1, d.scratch.data_ptr(), d.pj.data_ptr(),
+                                                  d.luid.data_ptr(), gs.data_ptr(), gss.data_ptr(),
+                                                  F, D, uvals.data_ptr(), ug2.data_ptr(), st,
+                                                  ovf.data_ptr()))
+        torch.cuda.synchronize()
+        err = (ug2[:U] - ug[:U]).abs().max().item()  # compact rows [0, U) at world 1
         P, o_bs, o_un, _ = h.bd_offsets(n, 1)
         sc = d.scratch.cpu().numpy().view(np.uint32).astype(np.int64)
         occ = np.diff(sc[o_bs:o_bs + P + 1])
@@ -72,7 +80,9 @@ def main():
             top = max(top, int(np.bincount(seg[seg < 4096]).max()) if len(seg) else 0)
         print(f"{name:8s} n={n} U={U} P={P} occ/bucket mean={occ.mean():.0f} p99={np.percentile(occ, 99):.0f} "
               f"max={occ.max()} uniq/bucket mean={un.mean():.0f} max={un.max()} hottest key in a "
-              f"big bucket={top}  reduce_lr={t_lr:.1f} us reduce_fm<{D}>={t_fm:.1f} us", flush=True)
+              f"big bucket={top}  reduce_lr={t_lr:.1f} us reduce_fm<{D}>={t_fm:.1f} us "
+              f"sorted={t_fms:.1f} us (overflow buckets {int(ovf[0])}, max |diff| {err:.2e})",
+              flush=True)
 
 
 if __name__ == "__main__":
