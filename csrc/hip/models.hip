@@ -69,20 +69,20 @@ __global__ __launch_bounds__(256) void k_gen_ctr(uint64_t seed, long long sample
                                                      const long long* __restrict__ step_dev,
                                                      long long step_mul, long long step_add) {
   if (step_dev) sample_base = *step_dev * step_mul + step_add;
+  __shared__ float sval[256];
   __shared__ float sdot[256];
   const int spb = samples_per_block(F);
   const int t = threadIdx.x;
   const int ls = t / F, f = t - (t / F) * F;
   const long long s0 = (long long)blockIdx.x * spb;
-  if (t < spb) sdot[t] = 0.f;
-  __syncthreads();
+  float wv = 0.f;
   if (ls < spb && s0 + ls < B && F <= 256) {
     const uint64_t key =
         gen_ctr_key(seed, (uint64_t)(sample_base + s0 + ls), f, V, logV, tail_frac);
     keys[(s0 + ls) * F + f] = key;
-    atomicAdd(&sdot[ls], truth_weight(key, truth_scale));
+    wv = truth_weight(key, truth_scale);
   }
-  __syncthreads();
+  packed_sample_sums(wv, F, spb, sval, sdot);  // per-sample sums, no LDS atomics
   if (t < spb && s0 + t < B)
     labels[s0 + t] = gen_ctr_label(seed, (uint64_t)(sample_base + s0 + t), sdot[t] + truth_bias);
 }

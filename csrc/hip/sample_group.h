@@ -26,6 +26,28 @@ __device__ __forceinline__ float group_sum(float v, int L) {
   return v;
 }
 
+// Per-sample sums in the PACKED layout (256/F samples per 256-thread block,
+// sample ls on threads [ls*F, ls*F+F)) without LDS atomics: every thread
+// stores its value, then TPS threads per sample add a strided share and
+// reduce with shuffles (F lanes adding into one LDS word with atomics
+// serialise F-way).  vals: 256 floats of LDS; sums: spb floats of LDS.
+// Every thread of the block must call it (two barriers).
+__device__ __forceinline__ void packed_sample_sums(float v, int F, int spb, float* vals,
+                                                   float* sums) {
+  const int t = threadIdx.x;
+  vals[t] = v;
+  __syncthreads();
+  int tps = 8;  // threads per sample: 8, or fewer when samples are many
+  while (tps > 1 && tps * spb > 256) tps >>= 1;
+  const int gi = t / tps, k = t - gi * tps;
+  float s = 0.f;
+  if (gi < spb)
+    for (int f = k; f < F; f += tps) s += vals[gi * F + f];
+  for (int o = tps >> 1; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (gi < spb && k == 0) sums[gi] = s;
+  __syncthreads();
+}
+
 // block-wide sum of one float per thread (256 threads), added to a sharded
 // counter by thread 0
 __device__ __forceinline__ float block_sum_256(float v, float* s4) {

@@ -210,24 +210,23 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict
                                                   float* __restrict__ gocc, int per_sample,
                                                   float* __restrict__ loss_sum,
                                                   float* __restrict__ pred) {
+  __shared__ float sval[256];
   __shared__ float sdot[256];
   __shared__ float sg[256];
   __shared__ float sloss[4];
   const int spb = F >= 256 ? 1 : 256 / F;
   const int t = threadIdx.x, ls = t / F;
   const long long s0 = (long long)blockIdx.x * spb;
-  if (t < spb) sdot[t] = 0.f;
-  __syncthreads();
   const bool active = ls < spb && s0 + ls < B;
   const long long j = s0 * F + t;
   uint32_t u = kInvS;
-  float x = 0.f;
+  float x = 0.f, wx = 0.f;
   if (active) {
     u = inv ? inv[j] : ix.uid(j);  // bucketed dedup: no materialised inverse index
     x = xval ? xval[j] : 1.f;
-    if (u != kInvS) atomicAdd(&sdot[ls], uvals[u] * x);
+    if (u != kInvS) wx = uvals[u] * x;
   }
-  __syncthreads();
+  packed_sample_sums(wx, F, spb, sval, sdot);  // per-sample dots, no LDS atomics
   float l = 0.f;
   if (t < spb && s0 + t < B) {
     const float z = sdot[t];
