@@ -25,11 +25,13 @@
 //              bucket bkt[j] (both coalesced)
 //   5 dedup    one workgroup per bucket: LDS hash insert + compaction; writes
 //              bucket-local ids luid[pos], the bucket's keys (staged in its own
-//              occurrence range) and its unique count
-//              the LAST dedup workgroup to finish (arrival counter) scans the
-//              unique counts into unique-id bases and ucount[d] — no
-//              inter-workgroup waiting, no extra single-workgroup launch
-//   6 place    one workgroup per bucket: keys -> send segment (+ zeroed grads)
+//              occurrence range, and — N>1 — straight into the destination's
+//              send segment, + zeroed gradient rows) and its unique count;
+//              the bucket's unique-id base is reserved with ONE device-scope
+//              add per bucket on ucount[d] (zeroed by the count kernel): no
+//              scan over buckets, no placement kernel (an arrival-counter
+//              scan + a placement launch before; the placement stretched to
+//              ~150 us beside the main stream)
 //   7 inverse  (optional) inv[j] = ubase[bkt[j]] + luid[pos_of[j]]; consumers
 //              that only need uid(j) read it through BdIndex instead
 //
@@ -149,8 +151,11 @@ long long bd_ubase_offset(long long n, int nranks) {
 template <int CT>
 __global__ __launch_bounds__(CT) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
                                                     RouteSpec rs, int Pd, int P, int chunk,
-                                                    uint32_t* __restrict__ hist) {
+                                                    uint32_t* __restrict__ hist,
+                                                    unsigned long long* __restrict__ ucount) {
   extern __shared__ unsigned int h[];
+  // the dedup's per-destination unique counters start from zero (stream order)
+  if (blockIdx.x == 0 && threadIdx.x < (unsigned)rs.nranks) ucount[threadIdx.x] = 0ull;
   for (int b = threadIdx.x; b < P; b += CT) h[b] = 0u;
   __syncthreads();
   // the chunk in register tiles of <= kBdMaxChunk keys (all loads of a tile
@@ -289,13 +294,14 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    uint32_t* __restrict__ luid,
                                                    uint64_t* __restrict__ bkeys,
                                                    uint32_t* __restrict__ unum,
-                                                   uint32_t* __restrict__ err,
-                                                   unsigned int* __restrict__ ctr, int Pd,
-                                                   int nranks, long long ucap,
+                                                   uint32_t* __restrict__ err, int Pd,
+                                                   long long ucap,
                                                    uint32_t* __restrict__ ubase,
                                                    unsigned long long* __restrict__ ucount,
                                                    uint32_t* __restrict__ osi_inv,
-                                                   unsigned long long* __restrict__ dbg) {
+                                                   unsigned long long* __restrict__ dbg,
+                                                   uint64_t* __restrict__ ukeys,
+                                                   float* __restrict__ ugrad, int gdim) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
   if (dbg && t == 0) dbg[(long long)b * 8 + (i)] = wall_clock64();
@@ -359,21 +365,34 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) occ += tab[t * kPerT + k] != kEmptyKey;
   unsigned int o = block_excl_scan<kBdDT / 64>(occ, wsum, &tot);
+  // the bucket's unique ids: one device-scope add per bucket reserves them in
+  // its destination's segment (ucount[d], zeroed by k_bd_count) — no scan
+  // over the buckets, and the keys go straight to the alltoallv send layout
+  const int d = b / Pd;
+  __shared__ unsigned long long sbase;
+  if (t == 0) {
+    const unsigned long long base = atomicAdd(&ucount[d], (unsigned long long)tot);
+    sbase = (unsigned long long)d * (unsigned long long)ucap + base;
+    ubase[b] = (uint32_t)sbase;
+    unum[b] = tot;
+    if (bad) atomicOr(err, 1u);
+  }
+  __syncthreads();
+  const unsigned long long ub = sbase;
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
     const int s = t * kPerT + k;
     const unsigned long long v = tab[s];
     if (v != kEmptyKey) {
       lid[s] = o;
-      bkeys[p0 + o] = v;  // staged in the bucket's own occurrence range
+      if (bkeys) bkeys[p0 + o] = v;  // staged in the bucket's own occurrence range
+      if (ukeys) ukeys[ub + o] = v;
       ++o;
     }
   }
-  if (t == 0) {
-    // write-through (agent-scope) store: read by the last workgroup below
-    __hip_atomic_store(&unum[b], tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (bad) atomicOr(err, 1u);
-  }
+  if (ugrad)  // zeroed gradient rows for consumers that scatter-add into them
+    for (unsigned int e = t; e < tot * (unsigned int)gdim; e += kBdDT)
+      ugrad[ub * (unsigned long long)gdim + e] = 0.f;
   __syncthreads();
   BD_STAMP(2)
   // osi_inv: the inverse index in OCCURRENCE-SPACE ids (unique key l of
@@ -399,51 +418,6 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   __syncthreads();
   BD_STAMP(3)
 #undef BD_STAMP
-  // the LAST workgroup to finish turns the bucket unique counts into unique-id
-  // bases (exclusive scan within each destination) and ucount[d].  Hand-off
-  // without fences (a per-workgroup release fence writes back the whole L2 —
-  // it made this kernel 3x slower): unum went out as a write-through store,
-  // drained before the arrival add; the last arriver reads it write-through
-  // (cdna guide G16, R1)
-  __shared__ bool last;
-  if (t == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = atomicAdd(ctr, 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (!last) return;  // workgroup-uniform
-  const int per = (Pd + kBdDT - 1) / kBdDT;
-  for (int d = 0; d < nranks; ++d) {
-    const int q0 = d * Pd + t * per;
-    unsigned int sum = 0;
-    for (int k = 0; k < per; ++k)
-      if (t * per + k < Pd)
-        sum += __hip_atomic_load(&unum[q0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    unsigned int e = block_excl_scan<kBdDT / 64>(sum, wsum, &tot);
-    for (int k = 0; k < per; ++k)
-      if (t * per + k < Pd) {
-        ubase[q0 + k] = (uint32_t)((long long)d * ucap + e);
-        e += __hip_atomic_load(&unum[q0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-    if (t == 0) ucount[d] = tot;
-  }
-  if (t == 0) *ctr = 0u;  // ready for the next call (stream-ordered)
-}
-
-// 6. unique-id bases, send-segment keys, per-destination counts
-__global__ __launch_bounds__(256) void k_bd_place(const uint32_t* __restrict__ unum,
-                                                  const uint32_t* __restrict__ bstart,
-                                                  const uint32_t* __restrict__ ubase,
-                                                  const uint64_t* __restrict__ bkeys,
-                                                  uint64_t* __restrict__ ukeys,
-                                                  float* __restrict__ ugrad, int gdim) {
-  const int b = blockIdx.x, t = threadIdx.x;
-  const unsigned int nu = unum[b];
-  const unsigned long long base = ubase[b];
-  const uint32_t p0 = bstart[b];
-  for (uint32_t l = t; l < nu; l += 256) ukeys[base + l] = bkeys[p0 + l];
-  if (ugrad)
-    for (uint32_t e = t; e < nu * (uint32_t)gdim; e += 256) ugrad[base * gdim + e] = 0.f;
 }
 
 // 7. inverse index in occurrence order
@@ -768,7 +742,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     case 512: hipLaunchKernelGGL(KERNEL<512>, dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
     default: hipLaunchKernelGGL(KERNEL<1024>, dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
   }
-  SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist);
+  SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, ucount);
   check_launch("k_bd_count");
   switch (cs) {
 #define SS_BD_CS_CASE(CS)                                                                      \
@@ -786,15 +760,12 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                     pos_of, bkt, osi_inv);
 #undef SS_BD_CT_DISPATCH
   check_launch("k_bd_scatter");
+  // place: unique keys straight into the per-destination send segments
+  // (+ zeroed gradient rows), reserved with one atomic per bucket
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
-                     bkeys, S + L.unum, S, S + L.ctr, L.Pd, rs.nranks, ucap, S + L.ubase, ucount,
-                     osi_inv, dbg);
+                     bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount, osi_inv, dbg,
+                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim);
   check_launch("k_bd_dedup");
-  if (place) {  // send-segment keys (+ zeroed gradient rows)
-    hipLaunchKernelGGL(k_bd_place, dim3(L.P), dim3(256), 0, st, S + L.unum, S + L.bstart,
-                       S + L.ubase, bkeys, ukeys, ugrad, gdim);
-    check_launch("k_bd_place");
-  }
   if (inv) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");
     BdIndex ix{pos_of, luid, bkt, S + L.ubase};
