@@ -301,18 +301,23 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    uint32_t* __restrict__ osi_inv,
                                                    unsigned long long* __restrict__ dbg,
                                                    uint64_t* __restrict__ ukeys,
-                                                   float* __restrict__ ugrad, int gdim) {
+                                                   float* __restrict__ ugrad, int gdim,
+                                                   uint8_t* __restrict__ usingle) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
   if (dbg && t == 0) dbg[(long long)b * 8 + (i)] = wall_clock64();
   __shared__ unsigned long long tab[kBdTS];
   __shared__ unsigned int lid[kBdTS];
+  __shared__ uint8_t dupf[kBdTS];
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
   __shared__ int bad;
   const int t = threadIdx.x, b = blockIdx.x;
   if (t == 0) bad = 0;
-  for (int s = t; s < kBdTS; s += kBdDT) tab[s] = kEmptyKey;
+  for (int s = t; s < kBdTS; s += kBdDT) {
+    tab[s] = kEmptyKey;
+    dupf[s] = 0;
+  }
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   // the first kBdRegs occurrences of each thread keep their slot in
   // registers; a hot bucket's excess parks it in luid[] (rewritten below)
@@ -326,14 +331,23 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   }
   __syncthreads();
   BD_STAMP(0)
+  // dupf[s]: the key of slot s occurs more than once in the bucket (set by
+  // every occurrence but the inserting one: a plain, idempotent LDS store)
   auto insert = [&](uint64_t key) -> uint32_t {
     uint32_t s = (uint32_t)dedup_hash(key) & (kBdTS - 1);
     for (int k = 0; k < kBdTS; ++k) {
       const unsigned long long v = tab[s];
-      if (v == key) return s;
+      if (v == key) {
+        dupf[s] = 1;
+        return s;
+      }
       if (v == kEmptyKey) {
         const unsigned long long prev = atomicCAS(&tab[s], kEmptyKey, (unsigned long long)key);
-        if (prev == kEmptyKey || prev == key) return s;
+        if (prev == kEmptyKey) return s;
+        if (prev == key) {
+          dupf[s] = 1;
+          return s;
+        }
       }
       s = (s + 1) & (kBdTS - 1);
     }
@@ -387,6 +401,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
       lid[s] = o;
       if (bkeys) bkeys[p0 + o] = v;  // staged in the bucket's own occurrence range
       if (ukeys) ukeys[ub + o] = v;
+      if (usingle) usingle[ub + o] = dupf[s] ? 0 : 1;  // one occurrence in the batch
       ++o;
     }
   }
@@ -439,7 +454,8 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     const uint32_t* __restrict__ luid,
                                                     const float* __restrict__ gs,
                                                     const float* __restrict__ xval, int F,
-                                                    float* __restrict__ ugrad, int osi) {
+                                                    float* __restrict__ ugrad, int osi,
+                                                    const uint8_t* __restrict__ usingle) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
@@ -461,9 +477,16 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
       g[r] = l[r] != kBdInvalid ? gs[j[r] / (uint32_t)F] : 0.f;
       if (xval && l[r] != kBdInvalid) g[r] *= xval[j[r]];
     }
+    // keys occurring once in the batch (usingle, from the dedup): a plain
+    // LDS store — LDS float atomics are this kernel's cost (~6 us per 1M)
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
-      if (l[r] != kBdInvalid) atomicAdd(&acc[l[r]], g[r]);
+    for (int r = 0; r < 2; ++r) {
+      if (l[r] == kBdInvalid) continue;
+      if (usingle && usingle[ubase[b] + l[r]])
+        acc[l[r]] = g[r];
+      else
+        atomicAdd(&acc[l[r]], g[r]);
+    }
   }
   __syncthreads();
   for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];
@@ -711,7 +734,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg, uint32_t* osi_inv) {
+                     unsigned long long* dbg, uint32_t* osi_inv, uint8_t* usingle) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   if (n <= 0) {
     check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
@@ -764,7 +787,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   // (+ zeroed gradient rows), reserved with one atomic per bucket
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                      bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount, osi_inv, dbg,
-                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim);
+                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle);
   check_launch("k_bd_dedup");
   if (inv) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");
@@ -785,7 +808,7 @@ void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const f
 
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
-                      float* ugrad, hipStream_t st, int osi) {
+                      float* ugrad, hipStream_t st, int osi, const uint8_t* usingle) {
   if (n <= 0) return;
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
   const BdLayout L = bd_layout(n, nranks);
@@ -797,13 +820,13 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   }();
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle);
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle);
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
-                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi);
+                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle);
   check_launch("k_bd_reduce");
 }
 

@@ -176,27 +176,27 @@ PYBIND11_MODULE(_ss_hip, m) {
                        long long ucap, uintptr_t scratch, uintptr_t pj, uintptr_t pos_of,
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
-                       uintptr_t st, uintptr_t dbg, uintptr_t osi_inv) {
+                       uintptr_t st, uintptr_t dbg, uintptr_t osi_inv, uintptr_t usingle) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
                     P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
                     P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
                     P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg),
-                    P<uint32_t>(osi_inv));
+                    P<uint32_t>(osi_inv), P<uint8_t>(usingle));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
-     py::arg("osi_inv") = 0);
+     py::arg("osi_inv") = 0, py::arg("usingle") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
-                        int osi) {
+                        int osi, uintptr_t usingle) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                      P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
-                     P<float>(ugrad), S(st), osi);
+                     P<float>(ugrad), S(st), osi, P<const uint8_t>(usingle));
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("xval"), py::arg("F"), py::arg("ugrad"), py::arg("st"),
-     py::arg("osi") = 0);
+     py::arg("osi") = 0, py::arg("usingle") = 0);
   m.def("bd_unplace", [](long long n, int nranks, uintptr_t scratch, uintptr_t src, uintptr_t dst,
                          int dim, uintptr_t st) {
     launch_bd_unplace(n, nranks, P<const uint32_t>(scratch), P<const float>(src), P<float>(dst),

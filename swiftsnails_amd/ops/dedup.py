@@ -77,6 +77,10 @@ class Deduper:
         # buffer (pull_buckets/push_buckets with osi, bd_unplace for N>1), and
         # no BdIndex (pos_of / bkt) is written
         self.osi = False
+        # bucket mode: per unique key, whether it occurs once in the batch
+        # (``usingle``, compact unique ids) — lets the LR reduce store instead
+        # of accumulate with LDS atomics.  Allocated by track_singletons().
+        self.usingle = None
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -137,7 +141,8 @@ class Deduper:
                             self.inv.data_ptr() if (self.materialize_inv and not osi) else 0,
                             int(self.need_ukeys or bool(ug)), st,
                             self.dbg.data_ptr() if self.dbg is not None else 0,
-                            self.inv.data_ptr() if osi else 0)
+                            self.inv.data_ptr() if osi else 0,
+                            self.usingle.data_ptr() if self.usingle is not None else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self)
         # the scratch is all-EMPTY between calls: the finish kernel resets the
@@ -153,6 +158,12 @@ class Deduper:
         return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                            self.nranks, n, self)
 
+    def track_singletons(self) -> None:
+        """Have the dedup flag the unique keys that occur once (bucket mode)."""
+        if self.mode == "bucket" and self.usingle is None:
+            self.usingle = torch.zeros(self.nranks * self.ucap, dtype=torch.uint8,
+                                       device=self.device)
+
     def reduce(self, n: int, gs: torch.Tensor, F: int, ugrad: torch.Tensor,
                 xval: Optional[torch.Tensor] = None, stream=None, osi: bool = False):
         """K7 for scalar rows, for the LAST call's partition (bucket mode):
@@ -164,7 +175,8 @@ class Deduper:
         self.h.bd_reduce(n, self.nranks, self.scratch.data_ptr(), self.pj.data_ptr(),
                          self.luid.data_ptr(), gs.data_ptr(),
                          xval.data_ptr() if xval is not None else 0, F, ugrad.data_ptr(),
-                         _stream_ptr(stream), int(osi))
+                         _stream_ptr(stream), int(osi),
+                         self.usingle.data_ptr() if self.usingle is not None else 0)
 
     def unplace(self, n: int, src: torch.Tensor, dst: torch.Tensor, stream=None):
         """Rows of the LAST call from compact unique ids (``src``, the

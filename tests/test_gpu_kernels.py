@@ -199,8 +199,10 @@ def test_dedup_route_matches_reference(dev, nranks, n, frags, mode):
 
 
 @pytest.mark.parametrize("nranks", [1, 3])
-def test_bucket_reduce_lr_matches_atomic_path(dev, nranks):
-    """Bucketed dedup's LDS reduction == per-occurrence atomics."""
+@pytest.mark.parametrize("singles", [False, True])
+def test_bucket_reduce_lr_matches_atomic_path(dev, nranks, singles):
+    """Bucketed dedup's LDS reduction == per-occurrence atomics (also with
+    the dedup's singleton flags: keys seen once are stored, not added)."""
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.ops.dedup import Deduper
     from swiftsnails_amd.parallel.router import HashFrag
@@ -214,9 +216,20 @@ def test_bucket_reduce_lr_matches_atomic_path(dev, nranks):
     fm = HashFrag(nranks, 64).rank_map()
     d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=1,
                 device=dev, mode="bucket")
+    if singles:
+        d.track_singletons()
     r = d(torch.from_numpy(keys).to(dev))
     st = torch.cuda.current_stream().cuda_stream
     U = nranks * d.ucap
+    if singles:  # the flags match the key multiplicities
+        kv = keys[keys != -1]
+        uk, cnt = np.unique(kv, return_counts=True)
+        once = dict(zip(uk.tolist(), (cnt == 1).tolist()))
+        uc0 = r.ucount.cpu().numpy()
+        us, ukd = d.usingle.cpu().numpy(), r.ukeys.cpu().numpy()
+        for q in range(nranks):
+            for i in range(q * d.ucap, q * d.ucap + int(uc0[q]), 97):
+                assert bool(us[i]) == once[int(ukd[i])]
     uvals = torch.randn(U, device=dev) * 0.1
     y = torch.from_numpy((rng.random(B) < 0.3).astype(np.float32)).to(dev)
     g_at = torch.zeros(U, device=dev)
