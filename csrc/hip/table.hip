@@ -16,6 +16,8 @@
 // and the G lanes sweep the row.  G=1 for sparse-LR rows (width 2 = 8 B),
 // G=16/64 for embedding rows (word2vec / FM), so a 64-wide wavefront always
 // has all lanes busy on HBM traffic.
+#include <cstdlib>
+
 #include "ss_device.h"
 #include "ss_launch.h"
 
@@ -351,9 +353,19 @@ __global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t*
 template <int G>
 __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
                                           const float* __restrict__ gr, const OptParams& op,
-                                          int lg) {
+                                          int lg, bool vec = true) {
   if (slot < 0) return;
   float* row = slot_row(t, slot);
+  if (G == 1 && t.dim == 1 && op.kind == kOptAdaGrad && vec &&
+      t.row_off % 8 == 0 && t.stride % 8 == 0) {
+    // scalar-row AdaGrad (sparse LR): the (w, h) pair as one 8-byte load and
+    // one 8-byte store instead of two of each
+    float2 wh = *reinterpret_cast<const float2*>(row);
+    float s2 = 0.f;
+    opt_update(op, wh.x, wh.y, s2, gr[0]);
+    *reinterpret_cast<float2*>(row) = wh;
+    return;
+  }
   if (t.dim <= (uint32_t)G * kApplyRegs) {
     // all of this lane's coordinates loaded first, updated in registers,
     // stored after: one memory round trip per row (a load-update-store loop
@@ -388,7 +400,7 @@ __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
 template <int G>
 __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __restrict__ slots,
                                                const float* __restrict__ grads, SegList sl,
-                                               OptParams op) {
+                                               OptParams op, int vec) {
   const long long total = seg_total(sl);
   const int lg = threadIdx.x % G;
   const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
@@ -396,7 +408,7 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg);
+    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg, vec != 0);
   }
 }
 
@@ -577,8 +589,16 @@ void launch_apply_bk(const DevTable& t, const long long* slots, const float* gra
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st) {
   if (max_n <= 0) return;
-  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0, st, t,
-                                      slots, grads, sl, op));
+  // SS_APPLY_VEC=0: the previous form (experiment knob).  Default: one
+  // group per key (no grid-stride rounds: a second round is a second
+  // random-access latency chain for those lanes) and 8-byte (w, h) accesses
+  static const int vec = [] {
+    const char* e = std::getenv("SS_APPLY_VEC");
+    return e ? std::atoi(e) : 1;
+  }();
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>,
+                                      dim3(grid_for(max_n, kG, vec ? (1 << 22) : 16384)),
+                                      dim3(256), 0, st, t, slots, grads, sl, op, vec));
   check_launch("k_apply");
 }
 
