@@ -569,11 +569,14 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   // lane probes about once; measured 1.19 -> 1.13-1.17 ms/step vs 1 (the
   // kernel alone barely changes: smaller workgroups interleave better with
   // the route stream's kernels)
-  static const int ny = [] {
+  // (scalar rows only: FM / word2vec, whose pull runs on the lighter route
+  // stream, measured neutral)
+  static const int env_ny = [] {
     const char* e = std::getenv("SS_PULL_BK_Y");
-    const int v = e ? std::atoi(e) : 4;
-    return v < 1 ? 1 : (v > 16 ? 16 : v);
+    const int v = e ? std::atoi(e) : 0;
+    return v < 0 ? 0 : (v > 16 ? 16 : v);
   }();
+  const int ny = env_ny ? env_ny : (G == 1 ? 4 : 1);
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique_bk<kG>, dim3(P, ny), dim3(256), 0, st, t,
                                       bkeys, bstart, unum, ubase, slots, out, ip, size_ctr, err,
                                       osi));
