@@ -14,7 +14,9 @@ Here (works for ``HbmTable`` and ``HostTable``):
   tail (optimizer state) makes a dump resumable bit-exactly (precision 9).
   Device compaction (K8 ``export``) -> D2H -> multi-threaded C++ formatter.
 * ``save_binary`` / ``load_binary`` — header + ``u64 keys[n]`` + ``f32
-  rows[n, width]``, the fast default for large tables.
+  rows[n, width]``, the fast default for large tables.  Both stream: host
+  memory is one export / load chunk regardless of the shard size (a 288 GB
+  HBM shard does not have to fit in host RAM).
 * sharded checkpoints: one file per server rank
   (``<prefix>.shard<r>-of-<N>.<ext>``); ``load_sharded`` re-routes every key
   through the current router, so a job can resume on a different world size.
@@ -77,60 +79,130 @@ def _assign(table, keys: np.ndarray, rows: np.ndarray, chunk: int = 1 << 22):
         table.assign(k, r)
 
 
+def iter_text(path: str, dim: int, width: int, state_init: float = 0.0,
+              block_bytes: int = 64 << 20):
+    """Parse a text dump in ~``block_bytes`` blocks cut at line ends."""
+    h = host()
+    with open(path, "rb") as f:
+        tail = b""
+        while True:
+            b = f.read(block_bytes)
+            if not b:
+                break
+            b = tail + b
+            cut = b.rfind(b"\n")
+            if cut < 0:
+                tail = b
+                continue
+            tail = b[cut + 1:]
+            yield h.parse_rows(b[:cut + 1], dim, width, state_init)
+        if tail.strip():
+            yield h.parse_rows(tail, dim, width, state_init)
+
+
 def load_text(table, path: str, key_filter=None) -> int:
-    keys, rows = read_text(path, table.dim, table.width, table.init_cfg.state_init)
-    if key_filter is not None:
-        m = key_filter(keys)
-        keys, rows = keys[m], rows[m]
-    _assign(table, keys, rows)
+    n = 0
+    for keys, rows in iter_text(path, table.dim, table.width, table.init_cfg.state_init):
+        if key_filter is not None:
+            m = key_filter(keys)
+            keys, rows = keys[m], rows[m]
+        if len(keys):
+            _assign(table, keys, rows)
+            n += len(keys)
     table.check()
-    return len(keys)
+    return n
 
 
-def save_binary(table, path: str, meta: Optional[dict] = None) -> int:
-    parts_k, parts_r = [], []
-    for k, r in _iter_export(table):
-        parts_k.append(np.ascontiguousarray(k))
-        parts_r.append(np.ascontiguousarray(r, dtype=np.float32))
-    keys = np.concatenate(parts_k) if parts_k else np.zeros(0, np.uint64)
-    rows = np.concatenate(parts_r) if parts_r else np.zeros((0, table.width), np.float32)
-    hdr = json.dumps({"dim": table.dim, "width": table.width, "n": int(len(keys)),
-                      "optimizer": table.opt.kind, "opt_step": table.opt.step,
-                      **(meta or {})}).encode()
-    tmp = path + ".tmp"
-    with open(tmp, "wb") as f:
-        f.write(MAGIC + struct.pack("<I", len(hdr)) + hdr)
-        f.write(keys.astype("<u8").tobytes())
-        f.write(rows.astype("<f4").tobytes())
-    os.replace(tmp, path)
-    return len(keys)
-
-
-def read_binary(path: str):
+def _header(path: str):
     with open(path, "rb") as f:
         if f.read(8) != MAGIC:
             raise ValueError(f"{path}: not a swiftsnails_amd binary checkpoint")
         (hl,) = struct.unpack("<I", f.read(4))
         hdr = json.loads(f.read(hl))
-        n, w = hdr["n"], hdr["width"]
-        off = 12 + hl
+    return hdr, 12 + hl
+
+
+def save_binary(table, path: str, meta: Optional[dict] = None) -> int:
+    """Stream the table to ``path`` chunk by chunk.
+
+    Host memory stays at one export chunk (keys + rows of ``chunk_slots``
+    table slots) whatever the shard size: ``n`` comes from ``table.size()``,
+    so the key block and the row block are each written at their final
+    offset with ``os.pwrite`` as chunks arrive.  Written to ``path.tmp`` and
+    renamed, so a crash never leaves a truncated checkpoint under ``path``.
+    """
+    n = int(table.size())
+    w = table.width
+    hdr = json.dumps({"dim": table.dim, "width": w, "n": n,
+                      "optimizer": table.opt.kind, "opt_step": table.opt.step,
+                      **(meta or {})}).encode()
+    off = 12 + len(hdr)
+    tmp = path + ".tmp"
+    fd = os.open(tmp, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o644)
+    try:
+        os.pwrite(fd, MAGIC + struct.pack("<I", len(hdr)) + hdr, 0)
+        m = 0
+        for k, r in _iter_export(table):
+            c = len(k)
+            if m + c > n:
+                raise RuntimeError(f"{path}: table grew while saving ({m + c} > {n} keys)")
+            kb = np.ascontiguousarray(k).astype("<u8", copy=False).tobytes()
+            rb = np.ascontiguousarray(r, dtype="<f4").tobytes()
+            os.pwrite(fd, kb, off + 8 * m)
+            os.pwrite(fd, rb, off + 8 * n + 4 * w * m)
+            m += c
+        if m != n:
+            raise RuntimeError(f"{path}: exported {m} keys, table.size() said {n}")
+        os.fsync(fd)
+    except BaseException:
+        os.close(fd)
+        os.unlink(tmp)
+        raise
+    os.close(fd)
+    os.replace(tmp, path)
+    return n
+
+
+def iter_binary(path: str, chunk: int = 1 << 22):
+    """Yield ``(keys u64 [c], rows f32 [c, width])`` chunks of a binary
+    checkpoint without reading the whole file."""
+    hdr, off = _header(path)
+    n, w = hdr["n"], hdr["width"]
+    for a in range(0, n, chunk):
+        c = min(chunk, n - a)
+        keys = np.fromfile(path, dtype="<u8", count=c, offset=off + 8 * a)
+        rows = np.fromfile(path, dtype="<f4", count=c * w,
+                           offset=off + 8 * n + 4 * w * a).reshape(c, w)
+        yield keys, rows
+
+
+def read_binary(path: str):
+    """Whole-file read (small tables / tests); ``iter_binary`` streams."""
+    hdr, off = _header(path)
+    n, w = hdr["n"], hdr["width"]
     keys = np.fromfile(path, dtype="<u8", count=n, offset=off)
     rows = np.fromfile(path, dtype="<f4", count=n * w, offset=off + 8 * n).reshape(n, w)
     return hdr, keys, rows
 
 
-def load_binary(table, path: str, key_filter=None) -> int:
-    hdr, keys, rows = read_binary(path)
+def load_binary(table, path: str, key_filter=None, chunk: int = 1 << 22) -> int:
+    """Stream a binary checkpoint into ``table`` (``chunk`` keys at a time),
+    keeping the keys ``key_filter`` selects."""
+    hdr, _ = _header(path)
     if hdr["width"] != table.width or hdr["dim"] != table.dim:
         raise ValueError(f"checkpoint layout dim={hdr['dim']} width={hdr['width']} != table "
                          f"dim={table.dim} width={table.width}")
-    if key_filter is not None:
-        m = key_filter(keys)
-        keys, rows = keys[m], rows[m]
-    _assign(table, keys, rows)
+    n = 0
+    for keys, rows in iter_binary(path, chunk):
+        if key_filter is not None:
+            m = key_filter(keys)
+            keys, rows = keys[m], rows[m]
+        if len(keys):
+            _assign(table, keys, rows, chunk)
+            n += len(keys)
     table.opt.step = max(table.opt.step, int(hdr.get("opt_step", 0)))
     table.check()
-    return len(keys)
+    return n
 
 
 # ----------------------------------------------------------------- sharded
@@ -171,5 +243,5 @@ def owner_filter(frag_rank_map: np.ndarray, rank: int):
     return lambda keys: route_keys_np(keys, frag_rank_map) == rank
 
 
-__all__ = ["save_text", "load_text", "read_text", "save_binary", "load_binary", "read_binary",
-           "save_sharded", "load_sharded", "shard_path", "owner_filter", "io"]
+__all__ = ["save_text", "load_text", "read_text", "iter_text", "save_binary", "load_binary",
+           "read_binary", "iter_binary", "save_sharded", "load_sharded", "shard_path", "owner_filter", "io"]

@@ -78,3 +78,51 @@ def test_sharded_resume_on_different_world_size(tmp_path):
     assert set(merged) == set(all_rows)
     for k in all_rows:
         np.testing.assert_array_equal(merged[k], all_rows[k])
+
+
+class _Chunked:
+    """Wraps a table so export() yields many small chunks (as HbmTable does)."""
+
+    def __init__(self, t, c):
+        self.t, self.c = t, c
+
+    def __getattr__(self, a):
+        return getattr(self.t, a)
+
+    def export(self, *a, **k):
+        for kk, rr in self.t.export():
+            for i in range(0, len(kk), self.c):
+                yield kk[i:i + self.c], rr[i:i + self.c]
+
+
+def test_streaming_binary_and_text_chunks(tmp_path):
+    t = _table(dim=3, seed=5)
+    p = str(tmp_path / "s.bin")
+    assert ck.save_binary(_Chunked(t, 97), p) == t.size()
+    hdr, keys, rows = ck.read_binary(p)
+    chunks = list(ck.iter_binary(p, chunk=101))
+    assert len(chunks) == -(-t.size() // 101)
+    np.testing.assert_array_equal(np.concatenate([c[0] for c in chunks]), keys)
+    np.testing.assert_array_equal(np.concatenate([c[1] for c in chunks]), rows)
+    t2 = HostTable(3, 5, Optimizer("adagrad", lr=0.1), InitConfig("zero", 0, 0.01))
+    assert ck.load_binary(t2, p, chunk=64) == t.size()
+    a, b = t.to_dict(True), t2.to_dict(True)
+    assert a.keys() == b.keys() and all(np.array_equal(a[k], b[k]) for k in a)
+    # text: blocks much smaller than the file, cut at line ends
+    pt = str(tmp_path / "s.txt")
+    ck.save_text(t, pt, with_state=True)
+    got = list(ck.iter_text(pt, 3, 5, block_bytes=1000))
+    assert len(got) > 10
+    assert sum(len(k) for k, _ in got) == t.size()
+
+
+def test_binary_save_detects_size_mismatch(tmp_path):
+    t = _table(dim=2)
+
+    class Lying(_Chunked):
+        def size(self):
+            return self.t.size() - 1
+
+    with pytest.raises(RuntimeError):
+        ck.save_binary(Lying(t, 50), str(tmp_path / "x.bin"))
+    assert not (tmp_path / "x.bin").exists() and not (tmp_path / "x.bin.tmp").exists()
