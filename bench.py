@@ -104,7 +104,15 @@ def main(argv=None):
             transport = TorchDistTransport(dist.new_group(backend="nccl"))
     else:
         transport = LoopbackTransport()
-        if os.environ.get("SS_ENGINE_GENERAL", "0") != "0":
+        general = os.environ.get("SS_ENGINE_GENERAL", "0")
+        if general == "rccl":
+            # the N>1 engine path on one GPU through three real (size-1) RCCL
+            # communicators: the multi-GPU call sequence, minus the peers
+            from swiftsnails_amd._native import hip
+
+            transport, ctrans, ptrans = (
+                RcclTransport(0, 1, dev, uid=hip().RcclComm.unique_id()) for _ in range(3))
+        elif general != "0":
             # the N>1 engine path on one GPU: one loopback per stream, as the
             # three RCCL communicators of a multi-GPU run
             ctrans, ptrans = LoopbackTransport(), LoopbackTransport()

@@ -226,7 +226,7 @@ def test_word2vec_trains_world1(dev):
     assert np.mean(losses[-5:]) < 0.8 * np.mean(losses[:3]), losses
 
 
-def _graph_worker(model, dev):
+def _graph_worker(model, dev, **ek):
     from swiftsnails_amd.models.fm import FMWorker, fm_table_args
     from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
     from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
@@ -237,18 +237,20 @@ def _graph_worker(model, dev):
     if model == "lr":
         data = CtrSynth(batch_size=4096, num_fields=13, num_features=1_000_000, tail_frac=0.1)
         table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
-        eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
+        eng = PSEngine(table, ek.pop("transport", None), max_keys=4096 * 13, dim=1, device=dev,
+                       **ek)
         return SparseLRWorker(eng, data), table
     if model == "fm":
         data = CtrSynth(batch_size=2048, num_fields=16, num_features=100_000, tail_frac=0.1)
         opt, init = fm_table_args(8)
         table = HbmTable(9, 200_000, optimizer=opt, init=init, device=dev)
-        eng = PSEngine(table, None, max_keys=2048 * 16, dim=9, device=dev)
+        eng = PSEngine(table, ek.pop("transport", None), max_keys=2048 * 16, dim=9, device=dev,
+                       **ek)
         return FMWorker(eng, data), table
     data = W2VSynth(batch_size=1024, window=3, vocab=5000, noise=0.05)
     opt, init = make_w2v_table_args(64, None)
     table = HbmTable(64, 40000, optimizer=opt, init=init, device=dev)
-    eng = PSEngine(table, None, max_keys=data.n_keys, dim=64, device=dev)
+    eng = PSEngine(table, ek.pop("transport", None), max_keys=data.n_keys, dim=64, device=dev, **ek)
     return Word2VecWorker(eng, data), table
 
 
@@ -317,3 +319,47 @@ def test_word2vec_context_reduce_matches_atomics(dev, monkeypatch):
     # a still-small accumulator in the first steps, so allow a few 1e-4
     np.testing.assert_allclose(np.stack([tr[k] for k in ks]), np.stack([ta[k] for k in ks]),
                                rtol=1e-3, atol=5e-4)
+
+
+@pytest.mark.parametrize("model", ["lr", "fm", "w2v"])
+def test_general_path_rccl_world1_matches_loopback(dev, model, monkeypatch):
+    """The N>1 engine path (send segments, count exchange with pinned D2H,
+    server pull over received segments, per-source apply) on one GPU through
+    three real size-1 RCCL communicators trains exactly like the same path
+    over loopback transports: the multi-GPU RCCL call sequence, minus peers."""
+    monkeypatch.setenv("SS_ENGINE_GENERAL", "1")
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    n = 12
+    wa, ta = _graph_worker(model, dev)
+    assert not wa.engine.fast1
+    la = [float(wa.step().sum().item()) for _ in range(n)]
+    wb, tb = _graph_worker(model, dev, **_rccl1(dev))
+    lb = [float(wb.step().sum().item()) for _ in range(n)]
+    torch.cuda.synchronize()
+    ta.check()
+    tb.check()
+    np.testing.assert_allclose(lb, la, rtol=2e-4, atol=1e-3)
+    assert ta.size() == tb.size()
+
+
+def _rccl1(dev):
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.parallel.transport import RcclTransport
+
+    t, c, p = (RcclTransport(0, 1, dev, uid=hip().RcclComm.unique_id()) for _ in range(3))
+    return {"transport": t, "count_transport": c, "pull_transport": p}
+
+
+@pytest.mark.parametrize("model", ["lr", "fm", "w2v"])
+def test_general_path_rccl_world1_pull_ahead_trains(dev, model, monkeypatch):
+    """The production N>1 pipeline — pull-ahead of round i+1 on a third
+    stream with its own RCCL communicator while round i computes — on one
+    GPU through size-1 RCCL communicators: trains and keeps the table sane."""
+    monkeypatch.setenv("SS_ENGINE_GENERAL", "1")
+    w, t = _graph_worker(model, dev, **_rccl1(dev))
+    assert w.engine.pull_ahead and w.engine.pull_stream is not None
+    losses = [float(w.step().sum().item()) for _ in range(40)]
+    torch.cuda.synchronize()
+    t.check()
+    assert np.isfinite(losses).all()
+    assert np.mean(losses[-5:]) < np.mean(losses[:3]), losses
