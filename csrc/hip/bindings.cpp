@@ -117,14 +117,14 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("pull_unique_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
                              uintptr_t ubase, int P_, uintptr_t slots, uintptr_t out,
                              const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
-                             uintptr_t st, int osi) {
+                             uintptr_t st, int osi, uintptr_t snap) {
     launch_pull_unique_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
                           P<const uint32_t>(unum), P<const uint32_t>(ubase), P_,
                           P<long long>(slots), P<float>(out), ip, P<unsigned long long>(size_ctr),
-                          P<int>(err), G, osi, S(st));
+                          P<int>(err), G, osi, S(st), P<float>(snap));
   }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
      py::arg("P"), py::arg("slots"), py::arg("out"), py::arg("ip"), py::arg("size_ctr"),
-     py::arg("err"), py::arg("G"), py::arg("st"), py::arg("osi") = 0);
+     py::arg("err"), py::arg("G"), py::arg("st"), py::arg("osi") = 0, py::arg("snap") = 0);
   m.def("pull_claim", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
                          uintptr_t slots, uintptr_t out, const InitParams& ip, uintptr_t size_ctr,
                          uintptr_t err, int G, uintptr_t st) {
@@ -132,9 +132,11 @@ PYBIND11_MODULE(_ss_hip, m) {
                       ip, P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
   });
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
-                    long long max_n, const OptParams& op, int G, uintptr_t st) {
-    launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st));
-  });
+                    long long max_n, const OptParams& op, int G, uintptr_t st, uintptr_t snap) {
+    launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st),
+                 P<const float>(snap));
+  }, py::arg("t"), py::arg("slots"), py::arg("grads"), py::arg("sl"), py::arg("max_n"),
+     py::arg("op"), py::arg("G"), py::arg("st"), py::arg("snap") = 0);
   m.def("apply_bk", [](const DevTable& t, uintptr_t slots, uintptr_t grads, uintptr_t bstart,
                        uintptr_t unum, int P_, const OptParams& op, int G, uintptr_t st) {
     launch_apply_bk(t, P<const long long>(slots), P<const float>(grads), P<const uint32_t>(bstart),

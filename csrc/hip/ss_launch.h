@@ -32,12 +32,13 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, int osi, hipStream_t st);
+                           int* err, int G, int osi, hipStream_t st, float* snap = nullptr);
 void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
                        long long max_n, long long* slots, float* out, const InitParams& ip,
                        unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
-                  const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st);
+                  const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
+                  const float* snap = nullptr);
 void launch_apply_bk(const DevTable& t, const long long* slots, const float* grads,
                      const uint32_t* bstart, const uint32_t* unum, int P, const OptParams& op,
                      int G, hipStream_t st);

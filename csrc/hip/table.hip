@@ -17,6 +17,7 @@
 // G=16/64 for embedding rows (word2vec / FM), so a 64-wide wavefront always
 // has all lanes busy on HBM traffic.
 #include <cstdlib>
+#include <stdexcept>
 
 #include "ss_device.h"
 #include "ss_launch.h"
@@ -140,7 +141,8 @@ template <int G>
 __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long long pos,
                                          long long* __restrict__ slots_out, float* __restrict__ out,
                                          const InitParams& ip, int* err, int lg,
-                                         unsigned long long& ins) {
+                                         unsigned long long& ins,
+                                         float2* __restrict__ snap = nullptr) {
   long long slot = -1;
   int inserted = 0;
   if (lg == 0) {
@@ -157,6 +159,20 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
   float* o = out + pos * (long long)t.dim;
   if (slot < 0) {
     for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
+  } else if (G == 1 && snap) {
+    // scalar (w, h) rows, snapshot mode (see k_apply): one 8-byte row read,
+    // w to the model, (w, h) to the snapshot the apply updates from
+    float2 wh;
+    if (inserted) {
+      wh = make_float2(init_value(ip, key, 0, 1), ip.state_init);
+      if (!t.prefilled) *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
+    } else {
+      wh = *reinterpret_cast<const float2*>(slot_row(t, slot));
+      wh.x = fresh_or(wh.x, ip, key, 0, 1);
+      if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
+    }
+    o[0] = wh.x;
+    snap[pos] = wh;
   } else {
     float* row = slot_row(t, slot);
     if (inserted) {
@@ -217,7 +233,7 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
                                                         long long* __restrict__ slots_out,
                                                         float* __restrict__ out, InitParams ip,
                                                         unsigned long long* size_ctr, int* err,
-                                                        int osi) {
+                                                        int osi, float2* __restrict__ snap) {
   const int b = blockIdx.x, lg = threadIdx.x % G;
   // osi: rows at occurrence-space ids bstart[b] + l (bdedup.hip), else at the
   // compact unique ids ubase[b] + l
@@ -227,7 +243,7 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
   // gridDim.y workgroups share a bucket (fewer serial probes per lane)
   for (uint32_t l = blockIdx.y * (256 / G) + threadIdx.x / G; l < nu;
        l += gridDim.y * (256 / G))
-    pull_one<G>(t, src[l], (long long)base + l, slots_out, out, ip, err, lg, ins);
+    pull_one<G>(t, src[l], (long long)base + l, slots_out, out, ip, err, lg, ins, snap);
   ins = wave_sum_u64(ins);
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
@@ -355,14 +371,17 @@ __global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t*
 template <int G>
 __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
                                           const float* __restrict__ gr, const OptParams& op,
-                                          int lg, bool vec = true) {
+                                          int lg, bool vec = true,
+                                          const float2* __restrict__ snap = nullptr) {
   if (slot < 0) return;
   float* row = slot_row(t, slot);
   if (G == 1 && t.dim == 1 && op.kind == kOptAdaGrad && vec &&
       t.row_off % 8 == 0 && t.stride % 8 == 0) {
     // scalar-row AdaGrad (sparse LR): the (w, h) pair as one 8-byte load and
-    // one 8-byte store instead of two of each
-    float2 wh = *reinterpret_cast<const float2*>(row);
+    // one 8-byte store instead of two of each.  With a snapshot (the (w, h)
+    // the pull read, valid when nothing else wrote the row in between) the
+    // random read goes away: a coalesced read and a blind random store.
+    float2 wh = snap ? *snap : *reinterpret_cast<const float2*>(row);
     float s2 = 0.f;
     opt_update(op, wh.x, wh.y, s2, gr[0]);
     *reinterpret_cast<float2*>(row) = wh;
@@ -402,7 +421,8 @@ __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
 template <int G>
 __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __restrict__ slots,
                                                const float* __restrict__ grads, SegList sl,
-                                               OptParams op, int vec) {
+                                               OptParams op, int vec,
+                                               const float2* __restrict__ snap) {
   const long long total = seg_total(sl);
   const int lg = threadIdx.x % G;
   const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
@@ -410,7 +430,8 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg, vec != 0);
+    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg, vec != 0,
+                 snap ? snap + pos : nullptr);
   }
 }
 
@@ -563,8 +584,10 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, int osi, hipStream_t st) {
+                           int* err, int G, int osi, hipStream_t st, float* snap) {
   if (P <= 0) return;
+  if (snap && !(G == 1 && t.dim == 1 && t.width == 2 && t.row_off % 8 == 0 && t.stride % 8 == 0))
+    throw std::invalid_argument("pull snapshot: scalar (w, h) rows with G = 1 only");
   // workgroups per bucket (SS_PULL_BK_Y): 4 — one per ~265 unique keys, so a
   // lane probes about once; measured 1.19 -> 1.13-1.17 ms/step vs 1 (the
   // kernel alone barely changes: smaller workgroups interleave better with
@@ -579,7 +602,7 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   const int ny = env_ny ? env_ny : (G == 1 ? 4 : 1);
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique_bk<kG>, dim3(P, ny), dim3(256), 0, st, t,
                                       bkeys, bstart, unum, ubase, slots, out, ip, size_ctr, err,
-                                      osi));
+                                      osi, reinterpret_cast<float2*>(snap)));
   check_launch("k_pull_unique_bk");
 }
 
@@ -605,7 +628,8 @@ void launch_apply_bk(const DevTable& t, const long long* slots, const float* gra
 }
 
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
-                  const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st) {
+                  const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
+                  const float* snap) {
   if (max_n <= 0) return;
   // SS_APPLY_VEC=0: the previous form (experiment knob).  Default: one
   // group per key (no grid-stride rounds: a second round is a second
@@ -616,7 +640,8 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
   }();
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>,
                                       dim3(grid_for(max_n, kG, vec ? (1 << 22) : 16384)),
-                                      dim3(256), 0, st, t, slots, grads, sl, op, vec));
+                                      dim3(256), 0, st, t, slots, grads, sl, op, vec,
+                                      reinterpret_cast<const float2*>(snap)));
   check_launch("k_apply");
 }
 

@@ -111,12 +111,16 @@ class HbmTable:
         # optimistic plain-store claim + verify pass, no device-scope atomics
         # (its verify pass re-reads freshly claimed lines across XCDs).
         self.insert_mode = os.environ.get("SS_TABLE_INSERT", "cas")
+        # bumped by every row-modifying call: a pull snapshot (pull_buckets
+        # snap=) is valid for a blind-write apply only while it is unchanged
+        self.version = 0
         self._alloc(int(capacity))
         self._init_native = self.init_cfg.native()
 
     # -- storage ------------------------------------------------------------
     def _alloc(self, cap: int):
         self.capacity = cap
+        self.version += 1
         self.storage = torch.empty(cap * self.stride, dtype=torch.uint8, device=self.device)
         # key-independent init (zero): fill every row with the initial row up
         # front, so an insert is the key CAS alone (SS_TABLE_PREFILL=0: off)
@@ -199,21 +203,33 @@ class HbmTable:
             h.gather(self.dt, slots.data_ptr(), sl, n, out.data_ptr(), self.G, st)
         return out, slots
 
+    @property
+    def snapshot_ok(self) -> bool:
+        """Rows are (w, h) scalar AdaGrad pairs the pull can snapshot."""
+        return (self.G == 1 and self.dim == 1 and self.width == 2 and
+                self.opt.kind == "adagrad" and self.stride % 8 == 0 and self.row_off % 8 == 0)
+
     def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None,
-                     osi: bool = False):
+                     osi: bool = False, snap: Optional[torch.Tensor] = None):
         """Unique-key lookup-or-init + gather straight from a bucketed dedup
         (``Deduper.bucket_view()``): rows land at their unique ids (compact,
-        or occurrence-space with ``osi``)."""
+        or occurrence-space with ``osi``).  ``snap`` ([ucap, 2] float32,
+        ``snapshot_ok`` tables): also write each key's (w, h) there, for a
+        ``push_slots(snap=)`` that needs no random row read."""
         bkeys, bstart, unum, ubase, P = view
+        if snap is not None and not self.snapshot_ok:
+            raise ValueError("pull snapshot needs scalar AdaGrad rows (dim 1, G 1)")
         hip().pull_unique_bk(self.dt, bkeys, bstart, unum, ubase, P, slots.data_ptr(),
                              out.data_ptr(), self._init_native, self.size_ctr.data_ptr(),
-                             self.err.data_ptr(), self.G, _stream_ptr(stream), int(osi))
+                             self.err.data_ptr(), self.G, _stream_ptr(stream), int(osi),
+                             0 if snap is None else snap.data_ptr())
         return out, slots
 
     def push_buckets(self, view, slots: torch.Tensor, grads: torch.Tensor, stream=None):
         """Optimizer update for a bucketed dedup's unique keys whose slots and
         gradient rows sit at occurrence-space ids (``pull_buckets(osi=True)``)."""
         _, bstart, unum, _, P = view
+        self.version += 1
         hip().apply_bk(self.dt, slots.data_ptr(), grads.data_ptr(), bstart, unum, P,
                        self.opt.native(), self.G, _stream_ptr(stream))
 
@@ -227,12 +243,17 @@ class HbmTable:
         return slots
 
     def push_slots(self, slots: torch.Tensor, grads: torch.Tensor, segs=None,
-                   max_n: Optional[int] = None, stream=None):
-        """Apply the optimizer at resolved slots (keys in one call must be unique)."""
+                   max_n: Optional[int] = None, stream=None,
+                   snap: Optional[torch.Tensor] = None):
+        """Apply the optimizer at resolved slots (keys in one call must be unique).
+        ``snap``: the (w, h) rows ``pull_buckets(snap=)`` read, updated and
+        stored blind — the caller guarantees no row changed since (same
+        ``version``)."""
         sl = segs if segs is not None else self._seg(slots.numel())
+        self.version += 1
         hip().apply(self.dt, slots.data_ptr(), grads.data_ptr(), sl,
                     slots.numel() if max_n is None else max_n, self.opt.native(), self.G,
-                    _stream_ptr(stream))
+                    _stream_ptr(stream), 0 if snap is None else snap.data_ptr())
 
     def push(self, keys: torch.Tensor, grads: torch.Tensor, stream=None):
         """push by key: keys missing from the table are created first (the
@@ -285,6 +306,7 @@ class HbmTable:
         rows = rows.to(self.device, torch.float32).reshape(-1, self.width).contiguous()
         if rows.shape[0] != keys.numel():
             raise ValueError("rows/keys length mismatch")
+        self.version += 1
         hip().assign(self.dt, keys.data_ptr(), rows.data_ptr(), keys.numel(),
                      self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, _stream_ptr(stream))
 

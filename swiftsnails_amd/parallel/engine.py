@@ -73,6 +73,8 @@ class Round:
     stats: dict = field(default_factory=dict)
     ready: Optional[object] = None        # pull-ahead: route-stream event of the pulled rows
     tag: Optional[int] = None             # hipGraph capture of `ready`
+    snap: Optional[torch.Tensor] = None   # world-1: (w, h) rows as pulled (blind apply)
+    snap_version: int = -1                # table.version the snapshot is valid for
 
     @property
     def inv(self) -> torch.Tensor:
@@ -164,6 +166,13 @@ class PSEngine:
         if self.fast1:
             self.slots = [torch.empty(cap, dtype=torch.int64, device=dev)
                           for _ in range(self.depth)]
+            # pull snapshots for the blind-write apply (scalar AdaGrad rows,
+            # pull and push of a round adjacent in table order: Round.snap);
+            # SS_PULL_SNAPSHOT=0 turns them off
+            self.snapshot = (os.environ.get("SS_PULL_SNAPSHOT", "1") != "0" and
+                             getattr(table, "snapshot_ok", False))
+            self._snaps = [torch.empty((cap, 2), dtype=torch.float32, device=dev)
+                           if self.snapshot else None for _ in range(self.depth)]
             # the colocated pull reads the bucketed dedup's staging directly:
             # no contiguous send segment is needed
             if table is not None and table.insert_mode == "cas":
@@ -318,13 +327,18 @@ class PSEngine:
         uv = self.uvals[slot]
         if self.fast1:
             own = dd.owner
+            snap = None
             if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
-                tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi)
+                if self.snapshot and not self.osi:
+                    snap = self._snaps[slot]
+                tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi,
+                                 snap=snap)
             else:
                 tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                          segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
             self.metrics.add(occurrences=dd.n)
-            return Round(dd, uv, slot, slots=self.slots[slot])
+            return Round(dd, uv, slot, slots=self.slots[slot], snap=snap,
+                         snap_version=tab.version)
         scounts, rcounts = r.counts.wait()
         D = self.displs
         self.t.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
@@ -424,8 +438,12 @@ class PSEngine:
             if self.osi:
                 tab.push_buckets(rnd.dd.owner.bucket_view(rnd.dd.n), rnd.slots, g)
             else:
+                # the pull's (w, h) snapshot replaces the random row read when
+                # no row changed since that pull (this round is the next push)
+                snap = rnd.snap if (rnd.snap is not None and
+                                    rnd.snap_version == tab.version) else None
                 tab.push_slots(rnd.slots, g, segs=tab.dev_segs(rnd.dd.ucount),
-                               max_n=max(1, min(rnd.dd.n, rnd.dd.ucap)))
+                               max_n=max(1, min(rnd.dd.n, rnd.dd.ucap)), snap=snap)
             tab.next_round()
         else:
             D = self.displs

@@ -591,3 +591,69 @@ def test_zero_init_prefilled_rows(dev, monkeypatch, prefill):
     row = d[int(base[5])]
     np.testing.assert_allclose(row[3:], 1.1, rtol=1e-6)
     np.testing.assert_allclose(row[:3], -0.5 / np.sqrt(1.1), rtol=1e-4)
+
+
+@pytest.mark.parametrize("prefill", ["1", "0"])
+def test_sparse_lr_pull_snapshot_matches_row_reads(dev, monkeypatch, prefill):
+    """Blind-write apply from the pull's (w, h) snapshot trains like the
+    read-modify-write apply (SS_PULL_SNAPSHOT=0), up to the float summation
+    order of the gradient merge (LDS atomics)."""
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    monkeypatch.setenv("SS_TABLE_PREFILL", prefill)
+    out = {}
+    for snap in ("1", "0"):
+        monkeypatch.setenv("SS_PULL_SNAPSHOT", snap)
+        data = CtrSynth(batch_size=4096, num_fields=13, num_features=300_000, tail_frac=0.2)
+        table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
+        eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
+        assert eng.snapshot == (snap == "1")
+        w = SparseLRWorker(eng, data)
+        losses = [float(w.step().sum().item()) for _ in range(12)]
+        torch.cuda.synchronize()
+        table.check()
+        out[snap] = (losses, table.to_dict(with_state=True))
+    (l1, t1), (l0, t0) = out["1"], out["0"]
+    np.testing.assert_allclose(l1, l0, rtol=1e-5)
+    assert t1.keys() == t0.keys()
+    ks = list(t1.keys())
+    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
+                               rtol=1e-4, atol=1e-6)
+
+
+def test_engine_snapshot_invalidated_by_interleaved_push(dev, monkeypatch):
+    """pull A, pull B, push A, push B over overlapping keys: B's snapshot is
+    stale after A's push, so B must re-read its rows (no lost update)."""
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    ka = torch.arange(1, 3001, dtype=torch.int64, device=dev)
+    kb = torch.arange(1501, 4501, dtype=torch.int64, device=dev)
+    res = {}
+    for snap in ("1", "0"):
+        monkeypatch.setenv("SS_PULL_SNAPSHOT", snap)
+        t = HbmTable(1, 1 << 16, optimizer=Optimizer("adagrad", lr=0.5),
+                     init=InitConfig("uniform", 0.1, 0.1, seed=3), device=dev)
+        assert t.snapshot_ok
+        eng = PSEngine(t, None, max_keys=4096, dim=1, device=dev)
+        ra = eng.pull(ka)
+        rb = eng.pull(kb)
+        assert (ra.snap is not None) == (snap == "1")
+        eng.accumulate(ra, torch.ones(len(ka), 1, device=dev))
+        eng.push(ra)
+        eng.accumulate(rb, torch.full((len(kb), 1), 2.0, device=dev))
+        eng.push(rb)
+        rc = eng.pull(kb)  # sequential pull -> push: the snapshot is used
+        eng.accumulate(rc, torch.ones(len(kb), 1, device=dev))
+        eng.push(rc)
+        torch.cuda.synchronize()
+        t.check()
+        res[snap] = t.to_dict(with_state=True)
+    assert res["1"].keys() == res["0"].keys()
+    for k in res["0"]:
+        np.testing.assert_array_equal(res["1"][k], res["0"][k])
+    # keys in both A and B saw both updates: h = 0.1 + 1 + 4 + 1
+    np.testing.assert_allclose(res["1"][2000][1], 6.1, rtol=1e-6)
