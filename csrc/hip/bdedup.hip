@@ -455,7 +455,9 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     const float* __restrict__ gs,
                                                     const float* __restrict__ xval, int F,
                                                     float* __restrict__ ugrad, int osi,
-                                                    const uint8_t* __restrict__ usingle) {
+                                                    const uint8_t* __restrict__ usingle,
+                                                    DevTable t, const long long* __restrict__ slots,
+                                                    const float2* __restrict__ snap, OptParams op) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
@@ -489,6 +491,20 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     }
   }
   __syncthreads();
+  if (slots) {
+    // fused K5 (one GPU, scalar AdaGrad rows with a pull snapshot): the
+    // merged gradient goes straight into the optimizer update — the (w, h)
+    // the pull read (coalesced), one blind 8-byte store per key
+    for (uint32_t l = threadIdx.x; l < nu; l += RT) {
+      const long long slot = slots[base + l];
+      if (slot < 0) continue;
+      float2 wh = snap[base + l];
+      float s2 = 0.f;
+      opt_update(op, wh.x, wh.y, s2, acc[l]);
+      *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
+    }
+    return;
+  }
   for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];
 }
 
@@ -808,9 +824,21 @@ void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const f
 
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
-                      float* ugrad, hipStream_t st, int osi, const uint8_t* usingle) {
+                      float* ugrad, hipStream_t st, int osi, const uint8_t* usingle,
+                      const DevTable* t, const long long* slots, const float* snap,
+                      const OptParams* op) {
   if (n <= 0) return;
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
+  DevTable tv{};
+  OptParams opv{};
+  if (slots) {
+    if (!t || !op || !snap || osi || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
+        t->row_off % 8 != 0 || t->stride % 8 != 0)
+      throw_error("bd_reduce: fused apply needs scalar AdaGrad rows, a snapshot and compact ids");
+    tv = *t;
+    opv = *op;
+  }
+  const float2* sn = reinterpret_cast<const float2*>(snap);
   const BdLayout L = bd_layout(n, nranks);
   const uint32_t* S = scratch;
   // workgroup size (SS_BD_RT experiment knob): measured 1024 >= 512 >= 256
@@ -820,13 +848,13 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   }();
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
-                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle);
+                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
   check_launch("k_bd_reduce");
 }
 

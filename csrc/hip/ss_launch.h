@@ -121,7 +121,9 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi = 0,
-                      const uint8_t* usingle = nullptr);
+                      const uint8_t* usingle = nullptr, const DevTable* t = nullptr,
+                      const long long* slots = nullptr, const float* snap = nullptr,
+                      const OptParams* op = nullptr);
 void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,
                        float* dst, int dim, hipStream_t st);
 

@@ -164,10 +164,15 @@ class SparseLRWorker(PipelinedWorker):
             if self.bucketed:
                 # one GPU + osi: gradient rows in occurrence space (apply_bk);
                 # N>1: compact, the alltoallv layout
+                # one GPU: the merge kernel runs the AdaGrad update itself
+                # (engine.fuse_apply: pull snapshot still valid), push() then
+                # only does the bookkeeping
+                fa = self.engine.fuse_apply(rnd) if not self.osi else None
                 h.bd_reduce(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                             o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
                             rnd.ugrad.data_ptr(), st, int(self.osi and self.engine.fast1),
-                            o.usingle.data_ptr() if o.usingle is not None else 0)
+                            o.usingle.data_ptr() if o.usingle is not None else 0,
+                            **(fa or {}))
             else:
                 h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
                             self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,

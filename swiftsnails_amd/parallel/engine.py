@@ -75,6 +75,7 @@ class Round:
     tag: Optional[int] = None             # hipGraph capture of `ready`
     snap: Optional[torch.Tensor] = None   # world-1: (w, h) rows as pulled (blind apply)
     snap_version: int = -1                # table.version the snapshot is valid for
+    applied: bool = False                 # the model's kernel already ran K5 (fuse_apply)
 
     @property
     def inv(self) -> torch.Tensor:
@@ -173,6 +174,9 @@ class PSEngine:
                              getattr(table, "snapshot_ok", False))
             self._snaps = [torch.empty((cap, 2), dtype=torch.float32, device=dev)
                            if self.snapshot else None for _ in range(self.depth)]
+            # SS_FUSE_APPLY=0: the model's merge kernel writes ugrad and
+            # k_apply runs separately even when fuse_apply() could fuse them
+            self.fuse_apply_on = os.environ.get("SS_FUSE_APPLY", "1") != "0"
             # the colocated pull reads the bucketed dedup's staging directly:
             # no contiguous send segment is needed
             if table is not None and table.insert_mode == "cas":
@@ -431,10 +435,26 @@ class PSEngine:
             self._free[slot] = ev
             self._free_tag[slot] = self.capture_tag
 
+    def fuse_apply(self, rnd: Round) -> Optional[dict]:
+        """Arguments that let a model's gradient-merge kernel run the optimizer
+        update itself (``bd_reduce(..., **args)``), or None.  One GPU, scalar
+        AdaGrad rows whose pull snapshot is still valid; the round is marked
+        applied and ``push`` only does the bookkeeping."""
+        tab = self.table
+        if not (self.fast1 and self.fuse_apply_on and not self.osi and rnd.snap is not None
+                and rnd.snap_version == tab.version and not rnd.applied):
+            return None
+        rnd.applied = True
+        tab.version += 1
+        return {"t": tab.dt, "slots": rnd.slots.data_ptr(), "snap": rnd.snap.data_ptr(),
+                "op": tab.opt.native()}
+
     def push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
         g = rnd.ugrad if grads is None else grads
         tab = self.table
-        if self.fast1:
+        if self.fast1 and rnd.applied:
+            tab.next_round()
+        elif self.fast1:
             if self.osi:
                 tab.push_buckets(rnd.dd.owner.bucket_view(rnd.dd.n), rnd.slots, g)
             else:

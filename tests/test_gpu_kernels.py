@@ -604,8 +604,11 @@ def test_sparse_lr_pull_snapshot_matches_row_reads(dev, monkeypatch, prefill):
 
     monkeypatch.setenv("SS_TABLE_PREFILL", prefill)
     out = {}
-    for snap in ("1", "0"):
+    # (snapshot, fused merge+apply): default, snapshot with separate k_apply,
+    # plain read-modify-write apply
+    for snap, fuse in (("1", "1"), ("1", "0"), ("0", "1")):
         monkeypatch.setenv("SS_PULL_SNAPSHOT", snap)
+        monkeypatch.setenv("SS_FUSE_APPLY", fuse)
         data = CtrSynth(batch_size=4096, num_fields=13, num_features=300_000, tail_frac=0.2)
         table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
         eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
@@ -614,13 +617,15 @@ def test_sparse_lr_pull_snapshot_matches_row_reads(dev, monkeypatch, prefill):
         losses = [float(w.step().sum().item()) for _ in range(12)]
         torch.cuda.synchronize()
         table.check()
-        out[snap] = (losses, table.to_dict(with_state=True))
-    (l1, t1), (l0, t0) = out["1"], out["0"]
-    np.testing.assert_allclose(l1, l0, rtol=1e-5)
-    assert t1.keys() == t0.keys()
-    ks = list(t1.keys())
-    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
-                               rtol=1e-4, atol=1e-6)
+        out[snap + fuse] = (losses, table.to_dict(with_state=True))
+    l0, t0 = out["01"]
+    ks = list(t0.keys())
+    for cfg in ("11", "10"):
+        l1, t1 = out[cfg]
+        np.testing.assert_allclose(l1, l0, rtol=1e-5)
+        assert t1.keys() == t0.keys()
+        np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
+                                   rtol=1e-4, atol=1e-6)
 
 
 def test_engine_snapshot_invalidated_by_interleaved_push(dev, monkeypatch):
