@@ -518,6 +518,33 @@ template <int K>
 struct FmCols {
   static constexpr int v = (K + 1) * kBdTS * 4 <= 150 * 1024 ? K : 8;
 };
+// Fused K5 for a DIM-wide row whose merged gradient is in registers: the
+// optimizer update as one read-modify-write of the row (one thread per row;
+// the DIM coordinates and their state stay in registers).  The model kernels
+// below call it instead of storing ugrad when the engine fuses the apply
+// (PSEngine.fuse_apply: one GPU, compact unique ids).
+template <int DIM>
+__device__ __forceinline__ void fused_row_update(const DevTable& t, long long slot,
+                                                 const float (&g)[DIM], const OptParams& op) {
+  if (slot < 0) return;
+  float* row = slot_row(t, slot);
+  const int ns = opt_state_per_coord(op.kind);
+  float w[DIM], s1[DIM], s2[DIM];
+#pragma unroll
+  for (int j = 0; j < DIM; ++j) {
+    w[j] = row[j];
+    s1[j] = ns > 0 ? row[DIM + j] : 0.f;
+    s2[j] = ns > 1 ? row[2 * DIM + j] : 0.f;
+  }
+#pragma unroll
+  for (int j = 0; j < DIM; ++j) {
+    opt_update(op, w[j], s1[j], s2[j], g[j]);
+    row[j] = w[j];
+    if (ns > 0) row[DIM + j] = s1[j];
+    if (ns > 1) row[2 * DIM + j] = s2[j];
+  }
+}
+
 template <int DIM, int NCOLS = 0>
 __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ ubase,
@@ -528,7 +555,10 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
                                                        const float* __restrict__ gss, int F,
                                                        const float* __restrict__ uvals,
                                                        float* __restrict__ ugrad,
-                                                       const uint32_t* __restrict__ blist) {
+                                                       const uint32_t* __restrict__ blist,
+                                                       DevTable t = DevTable{},
+                                                       const long long* __restrict__ slots = nullptr,
+                                                       OptParams op = OptParams{}) {
   constexpr int K = DIM - 1;
   constexpr int NC = NCOLS > 0 ? (NCOLS < K ? NCOLS : K) : FmCols<K>::v;
   __shared__ float g0[kBdTS];
@@ -611,6 +641,16 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm(const uint32_t* __restric
     }
     __syncthreads();
   }
+  if (slots) {
+    // fused K5 (single column pass group, gridDim.y == 1): this workgroup's
+    // rows of ugrad are complete after the barrier above
+    for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
+      float g[DIM];
+#pragma unroll
+      for (int j = 0; j < DIM; ++j) g[j] = ugrad[(size_t)(base + l) * DIM + j];
+      fused_row_update<DIM>(t, slots[base + l], g, op);
+    }
+  }
 }
 
 // compact unique rows (ubase[b] + l, the alltoallv layout) -> occurrence-space
@@ -645,7 +685,8 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
     const uint32_t* __restrict__ unum, const uint32_t* __restrict__ pj,
     const uint32_t* __restrict__ luid, const float* __restrict__ gs,
     const float* __restrict__ gss, int F, const float* __restrict__ uvals,
-    float* __restrict__ ugrad, uint32_t* __restrict__ ovf) {
+    float* __restrict__ ugrad, uint32_t* __restrict__ ovf, DevTable t,
+    const long long* __restrict__ slots, OptParams op) {
   constexpr int K = DIM - 1;
   __shared__ uint32_t cnt[kBdTS];      // counts, then placement cursors
   __shared__ uint32_t seg[kBdTS + 1];  // list starts (exclusive scan of the counts)
@@ -714,6 +755,14 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
   };
   auto store_row = [&](uint32_t l, float g0, const float* a) {
     const size_t r = (size_t)(base + l) * DIM;
+    if (slots) {  // fused K5: the row's update instead of its gradient store
+      float g[DIM];
+      g[0] = g0;
+#pragma unroll
+      for (int k = 0; k < K; ++k) g[1 + k] = a[k] - uvals[r + 1 + k] * g0;
+      fused_row_update<DIM>(t, slots[base + l], g, op);
+      return;
+    }
     ugrad[r] = g0;
 #pragma unroll
     for (int k = 0; k < K; ++k) ugrad[r + 1 + k] = a[k] - uvals[r + 1 + k] * g0;
@@ -862,8 +911,17 @@ long long bd_fm_ovf_words(long long n) { return n / kFmOcc + 2; }
 
 void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                          const uint32_t* luid, const float* gs, const float* gss, int F, int dim,
-                         const float* uvals, float* ugrad, hipStream_t st, uint32_t* ovf) {
+                         const float* uvals, float* ugrad, hipStream_t st, uint32_t* ovf,
+                         const DevTable* t, const long long* slots, const OptParams* op) {
   if (n <= 0) return;
+  DevTable tv{};
+  OptParams opv{};
+  if (slots) {
+    if (!t || !op || !ovf || t->dim != (uint32_t)dim)
+      throw_error("bd_reduce_fm: fused apply needs the table, the optimizer, the sorted path");
+    tv = *t;
+    opv = *op;
+  }
   const BdLayout L = bd_layout(n, nranks);
   const uint32_t* S = scratch;
   // default: sorted lists (no float atomics) + LDS-atomic form for overflow
@@ -872,6 +930,8 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
     const char* e = std::getenv("SS_FM_REDUCE");
     return !(e && std::string(e) == "atomic");
   }();
+  if (slots && !(ovf && sorted))
+    throw_error("bd_reduce_fm: fused apply runs on the sorted path only (SS_FM_REDUCE)");
   if (ovf && sorted) {
     const int novf = (int)(n / kFmOcc) + 1;  // an overflow bucket holds > kFmOcc keys
     check_hip(hipMemsetAsync(ovf, 0, sizeof(uint32_t), st), "fm ovf count");
@@ -879,9 +939,11 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
 #define SS_BDFMS_CASE(DD)                                                                      \
   case DD:                                                                                     \
     hipLaunchKernelGGL(k_bd_reduce_fm_sorted<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,  \
-                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, ovf);      \
+                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, ovf, tv,   \
+                       slots, opv);                                                            \
     hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(novf), dim3(1024), 0, st, S + L.bstart,         \
-                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, ovf);      \
+                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, ovf, tv,   \
+                       slots, opv);                                                            \
     break;
       SS_BDFMS_CASE(2)
       SS_BDFMS_CASE(5)

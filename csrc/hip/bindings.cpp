@@ -282,13 +282,16 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("bd_reduce_fm", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj,
                            uintptr_t luid, uintptr_t gs, uintptr_t gss, int F, int dim,
-                           uintptr_t uvals, uintptr_t ugrad, uintptr_t st, uintptr_t ovf) {
+                           uintptr_t uvals, uintptr_t ugrad, uintptr_t st, uintptr_t ovf,
+                           std::optional<DevTable> t, uintptr_t slots, std::optional<OptParams> op) {
     launch_bd_reduce_fm(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                         P<const uint32_t>(luid), P<const float>(gs), P<const float>(gss), F, dim,
-                        P<const float>(uvals), P<float>(ugrad), S(st), P<uint32_t>(ovf));
+                        P<const float>(uvals), P<float>(ugrad), S(st), P<uint32_t>(ovf),
+                        t ? &*t : nullptr, P<const long long>(slots), op ? &*op : nullptr);
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("gss"), py::arg("F"), py::arg("dim"), py::arg("uvals"),
-     py::arg("ugrad"), py::arg("st"), py::arg("ovf") = 0);
+     py::arg("ugrad"), py::arg("st"), py::arg("ovf") = 0, py::arg("t") = py::none(),
+     py::arg("slots") = 0, py::arg("op") = py::none());
   m.def("bd_fm_ovf_words", &bd_fm_ovf_words);
   m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
                          uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {

@@ -130,7 +130,8 @@ void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const f
 void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                          const uint32_t* luid, const float* gs, const float* gss, int F, int dim,
                          const float* uvals, float* ugrad, hipStream_t st,
-                         uint32_t* ovf = nullptr);
+                         uint32_t* ovf = nullptr, const DevTable* t = nullptr,
+                         const long long* slots = nullptr, const OptParams* op = nullptr);
 long long bd_fm_ovf_words(long long n);
 
 // --- w2v.hip

@@ -14,6 +14,8 @@ other beyond the lockstep collective round.
 """
 from __future__ import annotations
 
+import os
+
 from typing import Optional
 
 import numpy as np
@@ -82,10 +84,17 @@ class FMWorker(PipelinedWorker):
             h.fm_fwd_g(0, o.index_ptrs(dd.n), self.labels[slot].data_ptr(),
                        d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                        self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
+            # SS_FM_FUSE_APPLY=1 (one GPU): the sorted merge runs the optimizer
+            # update itself, one thread per row.  Measured slower (0.62 ->
+            # 1.04 ms/step): a thread's 18 dependent 4-byte accesses to a random
+            # 72-byte row vs k_apply's 4-lane groups, so off by default
+            fa = (self.engine.fuse_apply(rnd, snapshot=False)
+                  if os.environ.get("SS_FM_FUSE_APPLY", "0") == "1"
+                  and os.environ.get("SS_FM_REDUCE", "sorted") != "atomic" else None)
             h.bd_reduce_fm(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                            o.luid.data_ptr(), self.gs.data_ptr(), self.gss.data_ptr(),
                            d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
-                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr())
+                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr(), **(fa or {}))
             return
         hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),

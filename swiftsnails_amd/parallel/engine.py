@@ -435,19 +435,25 @@ class PSEngine:
             self._free[slot] = ev
             self._free_tag[slot] = self.capture_tag
 
-    def fuse_apply(self, rnd: Round) -> Optional[dict]:
+    def fuse_apply(self, rnd: Round, snapshot: bool = True) -> Optional[dict]:
         """Arguments that let a model's gradient-merge kernel run the optimizer
-        update itself (``bd_reduce(..., **args)``), or None.  One GPU, scalar
-        AdaGrad rows whose pull snapshot is still valid; the round is marked
-        applied and ``push`` only does the bookkeeping."""
+        update itself (``bd_reduce(..., **args)`` / ``bd_reduce_fm``), or
+        None.  One GPU, compact unique ids; ``snapshot``: scalar AdaGrad rows
+        updated from the pull's still-valid (w, h) snapshot (blind store),
+        else a read-modify-write of the row.  The round is marked applied and
+        ``push`` only does the bookkeeping."""
         tab = self.table
-        if not (self.fast1 and self.fuse_apply_on and not self.osi and rnd.snap is not None
-                and rnd.snap_version == tab.version and not rnd.applied):
+        if not (self.fast1 and self.fuse_apply_on and not self.osi and not rnd.applied
+                and rnd.slots is not None):
+            return None
+        if snapshot and not (rnd.snap is not None and rnd.snap_version == tab.version):
             return None
         rnd.applied = True
         tab.version += 1
-        return {"t": tab.dt, "slots": rnd.slots.data_ptr(), "snap": rnd.snap.data_ptr(),
-                "op": tab.opt.native()}
+        args = {"t": tab.dt, "slots": rnd.slots.data_ptr(), "op": tab.opt.native()}
+        if snapshot:
+            args["snap"] = rnd.snap.data_ptr()
+        return args
 
     def push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
         g = rnd.ugrad if grads is None else grads

@@ -363,3 +363,75 @@ def test_general_path_rccl_world1_pull_ahead_trains(dev, model, monkeypatch):
     t.check()
     assert np.isfinite(losses).all()
     assert np.mean(losses[-5:]) < np.mean(losses[:3]), losses
+
+
+@pytest.mark.parametrize("dim", [5, 9])
+def test_fm_fused_update_matches_separate_apply(dev, dim):
+    """bd_reduce_fm with the fused optimizer update (sorted lists and the
+    overflow bucket of a 32K-occurrence key) leaves the table exactly as the
+    gradient store followed by k_apply."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.dedup import Deduper
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+
+    h = hip()
+    B, F = 16000, 8
+    n = B * F
+    rng = np.random.default_rng(5)
+    keys = rng.integers(0, 1 << 40, size=n).astype(np.int64)
+    keys[rng.random(n) < 0.25] = 12345
+    d = Deduper(n, nranks=1, gdim=dim, device=dev, mode="bucket")
+    r = d(torch.from_numpy(keys).to(dev))
+    st = torch.cuda.current_stream().cuda_stream
+    u = int(r.ucount[0])
+    uk = r.ukeys[:u].clone()
+    tabs, slots = [], []
+    for _ in range(2):
+        t = HbmTable(dim, 1 << 18, optimizer=Optimizer("adagrad", lr=0.2),
+                     init=InitConfig("uniform", 0.1, 0.1, seed=7), device=dev)
+        v, s = t.pull(uk, unique=True)
+        tabs.append(t)
+        slots.append(s)
+    uvals = torch.zeros(d.ucap, dim, device=dev)
+    uvals[:u] = v
+    y = torch.from_numpy((rng.random(B) < 0.4).astype(np.float32)).to(dev)
+    gs = torch.empty(B, device=dev)
+    gss = torch.empty(B * (dim - 1), device=dev)
+    h.fm_fwd_g(0, d.index_ptrs(n), y.data_ptr(), B, F, dim,
+               uvals.data_ptr(), gs.data_ptr(), gss.data_ptr(), 0, 0, st)
+    ovf = torch.zeros(h.bd_fm_ovf_words(n), dtype=torch.int32, device=dev)
+    g = torch.zeros(d.ucap, dim, device=dev)
+    args = (n, 1, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(), gs.data_ptr(),
+            gss.data_ptr(), F, dim, uvals.data_ptr(), g.data_ptr(), st, ovf.data_ptr())
+    h.bd_reduce_fm(*args)
+    tabs[0].push_slots(slots[0][:u], g[:u].contiguous())
+    h.bd_reduce_fm(*args, t=tabs[1].dt, slots=slots[1].data_ptr(), op=tabs[1].opt.native())
+    torch.cuda.synchronize()
+    assert int(ovf[0]) >= 1
+    a, b = tabs[0].to_dict(with_state=True), tabs[1].to_dict(with_state=True)
+    assert a.keys() == b.keys() and len(a) == u
+    ks = list(a.keys())
+    np.testing.assert_allclose(np.stack([b[k] for k in ks]), np.stack([a[k] for k in ks]),
+                               rtol=1e-5, atol=1e-6)
+
+
+def test_fm_worker_fused_update_matches_separate_apply(dev, monkeypatch):
+    """The FM worker with the update fused into its gradient merge trains
+    like the separate k_apply (pull-ahead off: step-for-step comparable)."""
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    out = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("SS_FM_FUSE_APPLY", fuse)
+        w, t = _graph_worker("fm", dev)
+        losses = [float(w.step().sum().item()) for _ in range(10)]
+        torch.cuda.synchronize()
+        t.check()
+        out[fuse] = (losses, t.to_dict(with_state=True))
+    (l1, t1), (l0, t0) = out["1"], out["0"]
+    np.testing.assert_allclose(l1, l0, rtol=1e-4, atol=1e-3)
+    assert t1.keys() == t0.keys()
+    ks = list(t1.keys())[:5000]
+    # float summation order (LDS counting sort, atomics) over 10 training steps
+    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
+                               rtol=1e-3, atol=1e-3)
