@@ -92,10 +92,15 @@ class SparseLRWorker(PipelinedWorker):
             # per-sample gradients (bucketed) or per-occurrence g*x (bin plan)
             self.gocc = torch.empty(B if self.bucketed else n, dtype=torch.float32, device=dev)
         self.osi = False
+        # SS_LR_INV=1: the route stream materialises inv[j] (k_bd_inv) and the
+        # forward reads it coalesced, instead of resolving uid(j) through the
+        # dedup's bucket index on the main stream.  Measured neutral (forward
+        # 206 -> 123 us, k_bd_inv +109 us on the route stream): off
+        self.use_inv = self.bucketed and os.environ.get("SS_LR_INV", "0") == "1"
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False        # the LDS reduce stores every unique row
-                dd.materialize_inv = False  # the forward resolves uid(j) itself (BdIndex)
+                dd.materialize_inv = self.use_inv  # else the forward resolves uid(j) (BdIndex)
                 # SS_LR_SINGLE=1: the dedup flags keys seen once and the reduce
                 # stores their gradient instead of an LDS atomic add (measured:
                 # reduce 96 -> 90 us, step unchanged — off)
@@ -149,7 +154,7 @@ class SparseLRWorker(PipelinedWorker):
         xp = self.xval[slot].data_ptr() if self.xval is not None else 0
         if self.grad_mode == "segreduce":
             o = dd.owner
-            if self.osi:
+            if self.osi or self.use_inv:
                 h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
                            d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
                            self.loss_sum.data_ptr(), 0, st)
