@@ -179,27 +179,45 @@ def test_lr_worker_world2_pull_ahead(grad_mode):
     assert abs(ahead_last - sync_last) < 0.03, (sync_last, ahead_last)
 
 
+def _bench_torchrun(nproc, extra, env_extra=None):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, GLOO_SOCKET_IFNAME="lo", **(env_extra or {}))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.join(root, "bench.py"),
+           "--gpus", str(nproc)] + extra
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 4])  # N = 8 is the driver's scaling run
+def test_bench_script_multi_gpu_rccl(world):
+    """The driver's scaling run in miniature: bench.py over `world` GPUs with
+    the native RCCL communicators (skipped on boxes with fewer GPUs)."""
+    if torch.cuda.device_count() < world:
+        pytest.skip(f"needs {world} GPUs")
+    j = _bench_torchrun(world, ["--steps", "5", "--warmup", "2", "--batch", "16384",
+                                "--features", "10000000"])
+    assert j["n_gpus"] == world and j["value"] > 0
+    assert j["config"]["parallelism"].startswith(f"ps{world}")
+
+
 def test_bench_script_world2_gloo_rehearsal():
     """bench.py itself at N = 2 under torch.distributed.run (the driver's
     launch), both ranks pinned to cuda:0 with the host-staged gloo data plane
     (RCCL refuses two ranks per device): the whole N>1 script path — table
     sizing per shard, pull-ahead worker, barriers, max-over-ranks timing and
     the one JSON line from rank 0."""
-    import json
-    import subprocess
-    import sys
-
-    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    env = dict(os.environ, SS_BENCH_DEVICE="0", GLOO_SOCKET_IFNAME="lo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "4", "--warmup", "2",
-           "--batch", "4096", "--features", "2000000", "--transport", "gloo"]
-    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0, r.stderr[-3000:]
-    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    j = json.loads(lines[0])
+    j = _bench_torchrun(2, ["--steps", "4", "--warmup", "2", "--batch", "4096",
+                            "--features", "2000000", "--transport", "gloo"],
+                        {"SS_BENCH_DEVICE": "0"})
     assert j["n_gpus"] == 2 and j["steps"] == 4 and j["warmup"] == 2
     assert j["value"] > 0 and j["ms_per_step"] > 0
     assert j["config"]["global_batch"] == 2 * 4096
