@@ -11,7 +11,7 @@ IFS='|' read -ra SETARR <<< "$SETS"
 for set in "${SETARR[@]}"; do
   i=$((i+1))
   echo "=== pass $i: $set"
-  timeout -k 10 300 rocprofv3 --kernel-trace --stats --pmc $set --output-format csv -d "$OUT/p$i" -o run -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
+  timeout -s KILL 60 rocprofv3 --kernel-trace --stats --pmc $set --output-format csv -d "$OUT/p$i" -o run -- python3 bench.py $ARGS > "$OUT/p$i.log" 2>&1
   rc=$?
   echo "rc=$rc"; tail -3 "$OUT/p$i.log"
   case $rc in 0|1|2) ;; *) echo "FATAL"; exit $rc;; esac
