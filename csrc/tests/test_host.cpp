@@ -19,15 +19,7 @@
 #include <thread>
 #include <vector>
 
-#include "buffer.h"
-#include "channel.h"
-#include "config.h"
-#include "dataio.h"
-#include "hashfrag.h"
-#include "host_table.h"
-#include "string_util.h"
-#include "transfer.h"
-#include "vec.h"
+#include "swiftsnails.h"  // the umbrella header: every host-runtime header
 
 namespace {
 

@@ -7,6 +7,6 @@ mkdir -p $OUT/pmc_$MNAME
 i=0
 for set in "SQ_WAVES SQ_INSTS_VALU SQ_WAIT_ANY SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT" "FETCH_SIZE" "WRITE_SIZE TCC_EA0_WRREQ_sum" "TCC_HIT_sum TCC_MISS_sum TCC_EA0_ATOMIC_sum TCC_EA0_RDREQ_sum"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --kernel-trace --stats --pmc $set --output-format csv -d $OUT/pmc_$MNAME/p$i -o run -- python3 -m swiftsnails_amd.launch $MODEL_ARGS > $OUT/pmc_$MNAME/p$i.log 2>&1 || { tail $OUT/pmc_$MNAME/p$i.log; exit 1; }
+  timeout -s KILL 60 rocprofv3 --kernel-trace --stats --pmc $set --output-format csv -d $OUT/pmc_$MNAME/p$i -o run -- python3 -m swiftsnails_amd.launch $MODEL_ARGS > $OUT/pmc_$MNAME/p$i.log 2>&1 || { tail $OUT/pmc_$MNAME/p$i.log; exit 1; }
 done
 python tools/pmc_summary.py $OUT/pmc_$MNAME
