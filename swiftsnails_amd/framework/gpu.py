@@ -20,6 +20,7 @@ the reference lacks.  ``run_training`` drives a model from a config.
 from __future__ import annotations
 
 import os
+import re
 import sys
 import time
 from typing import Optional
@@ -113,9 +114,38 @@ class PSContext:
                                        interval=float(cfg.get("heartbeat_interval", 2.0)),
                                        peer_timeout=float(cfg.get("peer_timeout", 120)))
         self.fault = FaultInjector(rank=self.rank)
+        # resume_from: a checkpoint prefix, or "latest" = the newest complete
+        # periodic backup under param_backup_root (restart-after-failure:
+        # tools/run_gpu.sh MAX_RESTARTS=k relaunches the job, which picks up
+        # where its last backup left off); start_round continues the round
+        # count (data stream position, backup numbering)
+        self.start_round = 0
         resume = cfg.get("resume_from")
-        if resume:
+        if resume == "latest":
+            found = self._agree(ck.latest_checkpoint(self.backup_root), store)
+            if found is not None:
+                self.resume(found[0])
+                self.start_round = found[1]
+            else:
+                log.info("resume_from latest: no complete backup under %s", self.backup_root)
+        elif resume:
             self.resume(resume)
+            m = re.match(r".*param-(\d+)$", str(resume))
+            self.start_round = int(m.group(1)) if m else 0
+
+    def _agree(self, found, store):
+        """Rank 0's choice of checkpoint, for every rank (one filesystem view)."""
+        if self.world == 1 or store is None:
+            return found
+        key = "ss_resume_latest"
+        if self.rank == 0:
+            store.set(key, "" if found is None else f"{found[1]}:{found[0]}")
+        v = store.get(key).decode() if self.rank != 0 else (
+            "" if found is None else f"{found[1]}:{found[0]}")
+        if not v:
+            return None
+        rnd, prefix = v.split(":", 1)
+        return prefix, int(rnd)
 
     # ------------------------------------------------------------ ckpt
     def _owner(self):
@@ -226,6 +256,8 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
                  log_every: int = 0) -> dict:
     """Train `steps` rounds (config num_iters) and return throughput stats."""
     ctx, w = build_worker(cfg)
+    # resumed job: continue the round count where the checkpoint was taken
+    w.step_idx = ctx.start_round
     steps = int(steps if steps is not None else cfg.get("num_iters", 100))
     log_every = log_every or int(cfg.get("log_every", 0) or 0)
     for _ in range(warmup):
@@ -257,7 +289,8 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
              "servers": len(ctx.servers), "workers": len(ctx.workers), "steps": steps,
              "seconds": el, "ms_per_step": 1000 * el / max(1, steps),
              "samples_per_s": int(n.item()) * steps / el if el > 0 else 0.0,
-             "loss": w.mean_loss() if ctx.is_worker else None, "hipgraph": bool(graphed)}
+             "loss": w.mean_loss() if ctx.is_worker else None, "hipgraph": bool(graphed),
+             "start_round": ctx.start_round}
     m = ctx.engine.metrics.counters
     if m:
         stats["rank0_engine"] = {k: int(v) for k, v in m.items()}

@@ -236,6 +236,35 @@ def load_sharded(table, prefix: str, owner_fn=None) -> int:
     return n
 
 
+_SHARD_RE = None
+
+
+def latest_checkpoint(root: str, stem: str = "param-") -> Optional[tuple[str, int]]:
+    """Newest COMPLETE periodic backup under `root`: ``(prefix, round)`` of
+    the highest ``<stem><round>`` whose shard files ``.shard<r>-of-<W>`` exist
+    for every r < W (a job that died while writing a backup leaves an
+    incomplete set, which is skipped; single files are renamed into place
+    only once written, see save_binary).  None if there is none."""
+    import re
+
+    global _SHARD_RE
+    if _SHARD_RE is None:
+        _SHARD_RE = re.compile(r"^(.*?)(\d+)\.shard(\d+)-of-(\d+)\.(bin|txt)$")
+    sets: dict[tuple[str, int, int, str], set] = {}
+    for f in glob.glob(os.path.join(root, glob.escape(stem) + "*.shard*-of-*.*")):
+        m = _SHARD_RE.match(os.path.basename(f))
+        if not m or m.group(1) != stem:
+            continue
+        key = (os.path.join(root, stem + m.group(2)), int(m.group(2)), int(m.group(4)),
+               m.group(5))
+        sets.setdefault(key, set()).add(int(m.group(3)))
+    done = [(rnd, prefix) for (prefix, rnd, w, _), rs in sets.items() if rs == set(range(w))]
+    if not done:
+        return None
+    rnd, prefix = max(done)
+    return prefix, rnd
+
+
 def owner_filter(frag_rank_map: np.ndarray, rank: int):
     """Key mask: keys the router assigns to `rank` (fmix64(key) % frag_num)."""
     from ..parallel.router import route_keys_np
@@ -244,4 +273,4 @@ def owner_filter(frag_rank_map: np.ndarray, rank: int):
 
 
 __all__ = ["save_text", "load_text", "read_text", "iter_text", "save_binary", "load_binary",
-           "read_binary", "iter_binary", "save_sharded", "load_sharded", "shard_path", "owner_filter", "io"]
+           "read_binary", "iter_binary", "latest_checkpoint", "save_sharded", "load_sharded", "shard_path", "owner_filter", "io"]

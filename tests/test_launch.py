@@ -62,6 +62,15 @@ def test_cli_gpu_sparse_lr_backup_and_resume(tmp_path):
     r2 = subprocess.run(common + ["--steps", "2", "--set", f"resume_from={tmp_path}/param-10"],
                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r2.returncode == 0, r2.stderr[-3000:]
+    assert json.loads(r2.stdout.strip().splitlines()[-1])["start_round"] == 10
+    # restart-after-failure: resume_from=latest picks the newest complete
+    # backup and continues the round count (backups numbered from there)
+    (tmp_path / "param-10.shard0-of-1.bin").rename(tmp_path / "param-10.partial")
+    r3 = subprocess.run(common + ["--steps", "5", "--set", "resume_from=latest"],
+                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r3.returncode == 0, r3.stderr[-3000:]
+    assert json.loads(r3.stdout.strip().splitlines()[-1])["start_round"] == 5
+    assert (tmp_path / "param-10.shard0-of-1.bin").exists()  # written again at round 10
 
 
 def test_cluster_script_two_servers_two_workers(tmp_path):
@@ -78,3 +87,15 @@ def test_cluster_script_two_servers_two_workers(tmp_path):
     assert len(shards) == 2
     keys = [int(ln.split("\t")[0]) for f in shards for ln in f.read_text().splitlines()]
     assert sorted(keys) == list(range(64))
+
+
+def test_latest_checkpoint_picks_newest_complete_set(tmp_path):
+    from swiftsnails_amd.utils import checkpoint as ck
+
+    for name in ("param-5.shard0-of-2.bin", "param-5.shard1-of-2.bin",
+                 "param-10.shard0-of-2.txt", "param-10.shard1-of-2.txt",
+                 "param-20.shard1-of-2.bin",  # incomplete: rank 0 never wrote
+                 "param-7.shard0-of-1.bin.tmp", "other-30.shard0-of-1.bin"):
+        (tmp_path / name).write_bytes(b"x")
+    assert ck.latest_checkpoint(str(tmp_path)) == (str(tmp_path / "param-10"), 10)
+    assert ck.latest_checkpoint(str(tmp_path / "missing")) is None
