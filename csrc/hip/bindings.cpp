@@ -301,13 +301,13 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("w2v_sgns", [](uintptr_t inv_c, uintptr_t inv_x, uintptr_t inv_n, int B, int C, int D,
                        float neg_scale, uintptr_t uvals, uintptr_t ugrad, uintptr_t loss,
-                       uintptr_t st, uintptr_t gpos) {
+                       uintptr_t st, uintptr_t gpos, int bf16) {
     launch_w2v_sgns(P<const uint32_t>(inv_c), P<const uint32_t>(inv_x), P<const uint32_t>(inv_n), B,
                     C, D, neg_scale, P<const float>(uvals), P<float>(ugrad), P<float>(loss), S(st),
-                    P<float>(gpos));
+                    P<float>(gpos), bf16);
   }, py::arg("inv_c"), py::arg("inv_x"), py::arg("inv_n"), py::arg("B"), py::arg("C"),
      py::arg("D"), py::arg("neg_scale"), py::arg("uvals"), py::arg("ugrad"), py::arg("loss"),
-     py::arg("st"), py::arg("gpos") = 0);
+     py::arg("st"), py::arg("gpos") = 0, py::arg("bf16") = 0);
   m.def("w2v_ctx_reduce", [](int P_, uintptr_t bstart, uintptr_t unum, uintptr_t ubase,
                              uintptr_t pj, uintptr_t luid, uintptr_t inv_c, uintptr_t gpos, int B,
                              int C, int D, uintptr_t uvals, uintptr_t ugrad, uintptr_t st) {

@@ -138,7 +138,7 @@ long long bd_fm_ovf_words(long long n);
 size_t w2v_smem_bytes(int D);
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
-                     float* loss_sum, hipStream_t st, float* gpos = nullptr);
+                     float* loss_sum, hipStream_t st, float* gpos = nullptr, int bf16 = 0);
 void launch_w2v_ctx_reduce(int P, const uint32_t* bstart, const uint32_t* unum,
                            const uint32_t* ubase, const uint32_t* pj, const uint32_t* luid,
                            const uint32_t* inv_c, const float* gpos, int B, int C, int D,

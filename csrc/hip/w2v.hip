@@ -200,6 +200,188 @@ __global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ i
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same tile on the bf16 MFMA (v_mfma_f32_32x32x16_bf16, fp32 accumulate).
+// What it buys is occupancy, not MFMA rate: the fp32 tile's LDS (116 KB at
+// D = 128) allows one 8-wave workgroup per CU, and the kernel is a memory /
+// atomic latency chain (SQ_WAIT_ANY ~80% of wave cycles).  With the center and
+// negative rows and the score gradients staged as bf16 (rows padded by 16 B:
+// 16-B aligned fragments, rows spread over the banks) the tile needs 77 KB,
+// two workgroups per CU.  The positive pairs stay fp32: each wave reads its
+// centers' rows from global (L2-hot) next to the context rows.
+// Lane map (cdna_hip_programming.md §3): lane l (r = l&31, h = l>>5) holds
+// A[r][8h + j] and B[8h + j][r], j = 0..7; C/D as the fp32 form (mrow).
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ unsigned short f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);  // round to nearest even (finite inputs)
+  return (unsigned short)(u >> 16);
+}
+
+template <int D>
+struct W2vBf16Smem {
+  static constexpr int PB = D + 8;    // bf16 row stride of the V / N tiles
+  static constexpr int GB = kS + 8;   // bf16 row stride of the score-gradient tile
+  static constexpr int P = D + 1;     // fp32 row stride of the positive-grad tile
+  static constexpr size_t bytes = sizeof(unsigned short) * ((size_t)(kT + kS) * PB + (size_t)kT * GB) +
+                                  sizeof(float) * ((size_t)kT * P + kNW);
+};
+
+template <int D>
+__global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
+    const uint32_t* __restrict__ inv_c, const uint32_t* __restrict__ inv_x,
+    const uint32_t* __restrict__ inv_n, int B, int C, float neg_scale,
+    const float* __restrict__ uvals, float* __restrict__ ugrad, float* __restrict__ loss_sum) {
+  using L = W2vBf16Smem<D>;
+  constexpr int PB = L::PB, GB = L::GB, P = L::P;
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
+  unsigned short* Vb = smem16;            // [T][PB] center rows (bf16)
+  unsigned short* Nb = Vb + kT * PB;      // [S][PB] negative rows (bf16)
+  unsigned short* Gb = Nb + kS * PB;      // [T][GB] score gradients (bf16)
+  float* Gv = reinterpret_cast<float*>(Gb + kT * GB);  // [T][P] positive-part center grads
+  float* red = Gv + kT * P;                             // [kNW] loss partials
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long t0 = (long long)blockIdx.x * kT;
+  __shared__ uint32_t rc[kT], rn[kS];
+  if (tid < kT) rc[tid] = (t0 + tid < B) ? inv_c[t0 + tid] : kInv;
+  else if (tid < kT + kS) rn[tid - kT] = inv_n[(long long)blockIdx.x * kS + (tid - kT)];
+  __syncthreads();
+  // rows -> bf16 tiles, 4 coordinates per thread (16-B loads, 8-B LDS stores)
+  for (int e = tid; e < kT * D / 4; e += kWG) {
+    const int r = e / (D / 4), d = 4 * (e - r * (D / 4));
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f), n = v;
+    if (rc[r] != kInv) v = *reinterpret_cast<const float4*>(uvals + (long long)rc[r] * D + d);
+    if (rn[r] != kInv) n = *reinterpret_cast<const float4*>(uvals + (long long)rn[r] * D + d);
+    const uint2 pv = make_uint2(f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+                                f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+    const uint2 pn = make_uint2(f2bf(n.x) | ((uint32_t)f2bf(n.y) << 16),
+                                f2bf(n.z) | ((uint32_t)f2bf(n.w) << 16));
+    *reinterpret_cast<uint2*>(Vb + r * PB + d) = pv;
+    *reinterpret_cast<uint2*>(Nb + r * PB + d) = pn;
+  }
+  for (int e = tid; e < kT * P; e += kWG) Gv[e] = 0.f;
+  __syncthreads();
+
+  float loss = 0.f;
+  const int r32 = lane & 31, h = lane >> 5;
+  // ---- S = V·Nᵀ: wave w < 4 owns quadrant (w>>1, w&1)
+  if (w < 4) {
+    const int i0 = (w >> 1) * 32, j0 = (w & 1) * 32;
+    f32x16 acc = {};
+#pragma unroll
+    for (int k0 = 0; k0 < D; k0 += 16) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Vb + (i0 + r32) * PB + k0 + 8 * h);
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(Nb + (j0 + r32) * PB + k0 + 8 * h);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = i0 + mrow(r, lane), col = j0 + r32;
+      const bool ok = rc[row] != kInv && rn[col] != kInv;
+      const float sc = acc[r];
+      Gb[row * GB + col] = f2bf(ok ? neg_scale * sigm(sc) : 0.f);
+      if (ok) loss += neg_scale * softplus(sc);
+    }
+  }
+  // ---- positive pairs (fp32): wave w owns centers [kT/kNW * w, +kT/kNW); the
+  // center row comes from global with the context rows (one round trip)
+  {
+    constexpr int R = (D + 63) / 64;
+    constexpr int TW = kT / kNW;
+    for (int t = w * TW; t < w * TW + TW; ++t) {
+      if (rc[t] == kInv) continue;  // wave-uniform
+      const uint32_t xid = lane < C ? inv_x[(t0 + t) * (long long)C + lane] : kInv;
+      float u[kMaxC][R], v[R], gv[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        v[r] = d < D ? uvals[(long long)rc[t] * D + d] : 0.f;
+        gv[r] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < kMaxC; ++j) {
+        const uint32_t x = __shfl(xid, j, 64);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          u[j][r] = (j < C && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < kMaxC; ++j) {
+        const uint32_t x = __shfl(xid, j, 64);
+        if (j >= C || x == kInv) continue;  // wave-uniform
+        float part = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) part += v[r] * u[j][r];
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        const float g = sigm(part) - 1.f;
+        if (lane == 0) loss += softplus(-part);
+        float* gu = ugrad + (long long)x * D;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          if (d < D) {
+            atomicAdd(gu + d, g * v[r]);
+            gv[r] += g * u[j][r];
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        if (d < D) Gv[t * P + d] += gv[r];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- gV = G·N (+ positive part) and gN = Gᵀ·V, K = 64 in 4 steps of 16.
+  // Row-major fragments (G's rows for gV's A) are one 16-B LDS read; the
+  // k-strided ones (N for gV's B, G and V for gN) are gathered per element.
+  constexpr int NT = 2 * (D / 32);
+  for (int tt = w; tt < 2 * NT; tt += kNW) {
+    const bool center = tt < NT;
+    const int q = center ? tt : tt - NT;
+    const int ti = q / (D / 32), tj = q % (D / 32);
+    f32x16 acc = {};
+#pragma unroll
+    for (int k0 = 0; k0 < 64; k0 += 16) {
+      bf16x8 a, b;
+      const int kb = k0 + 8 * h;
+      if (center) {  // A[i][k] = G[ti*32+i][k], B[k][j] = N[k][tj*32+j]
+        a = *reinterpret_cast<const bf16x8*>(Gb + (ti * 32 + r32) * GB + kb);
+#pragma unroll
+        for (int j = 0; j < 8; ++j) b[j] = (short)Nb[(kb + j) * PB + tj * 32 + r32];
+      } else {       // A[i][k] = G[k][ti*32+i], B[k][j] = V[k][tj*32+j]
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          a[j] = (short)Gb[(kb + j) * GB + ti * 32 + r32];
+          b[j] = (short)Vb[(kb + j) * PB + tj * 32 + r32];
+        }
+      }
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
+      const uint32_t dst = center ? rc[row] : rn[row];
+      if (dst == kInv) continue;
+      const float v = acc[r] + (center ? Gv[row * P + col] : 0.f);
+      atomicAdd(ugrad + (long long)dst * D + col, v);
+    }
+  }
+  for (int o = 32; o > 0; o >>= 1) loss += __shfl_down(loss, o, 64);
+  if (lane == 0) red[w] = loss;
+  __syncthreads();
+  if (tid == 0 && loss_sum) {
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kNW; ++i) tot += red[i];
+    ctr_addf(loss_sum, tot);
+  }
+}
+
 // Context-row gradients without global atomics (the sgns kernel's positive
 // pairs otherwise issue one 256-B row of float atomics per pair: 84 MB per
 // 16K-center step at the memory-side atomic rate, ~1.3 TB/s, which also
@@ -348,10 +530,32 @@ size_t w2v_smem_bytes(int D) {
 
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
-                     float* loss_sum, hipStream_t st, float* gpos) {
+                     float* loss_sum, hipStream_t st, float* gpos, int bf16) {
   if (B <= 0) return;
   if (C < 1 || C > kMaxC) throw_error("w2v_sgns: contexts per center must be in [1,16]");
   const int tiles = (B + kT - 1) / kT;
+  if (bf16) {
+    if (gpos) throw_error("w2v_sgns: the bf16 tile has no context-reduce output");
+    switch (D) {
+#define SS_W2VB_CASE(DD)                                                                     \
+  case DD:                                                                                   \
+    check_hip(hipFuncSetAttribute((const void*)k_w2v_sgns_bf16<DD>,                           \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,                \
+                                  (int)W2vBf16Smem<DD>::bytes),                              \
+              "w2v bf16 smem attr");                                                         \
+    hipLaunchKernelGGL(k_w2v_sgns_bf16<DD>, dim3(tiles), dim3(kWG), W2vBf16Smem<DD>::bytes, st, \
+                       inv_c, inv_x, inv_n, B, C, neg_scale, uvals, ugrad, loss_sum);        \
+    break;
+      SS_W2VB_CASE(32)
+      SS_W2VB_CASE(64)
+      SS_W2VB_CASE(128)
+#undef SS_W2VB_CASE
+      default:
+        throw_error("w2v_sgns: D must be 32, 64 or 128");
+    }
+    check_launch("k_w2v_sgns_bf16");
+    return;
+  }
   const size_t sm = w2v_smem_bytes(D);
   switch (D) {
 #define SS_W2V_CASE(DD)                                                                     \

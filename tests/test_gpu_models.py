@@ -17,8 +17,10 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("D", [32, 64, 128])
-def test_w2v_sgns_tile_matches_reference(dev, D):
+@pytest.mark.parametrize("D,bf16", [(32, 0), (64, 0), (128, 0), (32, 1), (64, 1), (128, 1)])
+def test_w2v_sgns_tile_matches_reference(dev, D, bf16):
+    """fp32 tile: fp32-exact; bf16 tile (SS_W2V_MFMA=bf16): negative-sample
+    GEMMs from bf16-rounded rows, checked at bf16 tolerance."""
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.models.word2vec import sgns_reference
 
@@ -34,22 +36,26 @@ def test_w2v_sgns_tile_matches_reference(dev, D):
     p, es = ti.data_ptr(), 4
     neg_scale = 0.7
     hip().w2v_sgns(p, p + T * es, p + T * (1 + C) * es, T, C, D, neg_scale, tu.data_ptr(),
-                   g.data_ptr(), loss.data_ptr(), torch.cuda.current_stream().cuda_stream)
+                   g.data_ptr(), loss.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                   0, bf16)
     torch.cuda.synchronize()
     G = g.cpu().numpy()
     tot = 0.0
+    # bf16 tile: rows rounded to 8 mantissa bits -> ~3 significant digits in
+    # the negative-sample terms (the positive pairs and context grads are fp32)
+    rt, at = (2e-4, 2e-5) if not bf16 else (3e-2, 1e-2)
     for t in range(tiles):
         V = U[t * 64:(t + 1) * 64]
         X = U[T:T + T * C].reshape(T, C, D)[t * 64:(t + 1) * 64]
         N = U[T + T * C + t * S:T + T * C + (t + 1) * S]
         l, gV, gX, gN = sgns_reference(V, X, N, neg_scale)
         tot += l
-        np.testing.assert_allclose(G[t * 64:(t + 1) * 64], gV, rtol=2e-4, atol=2e-5)
+        np.testing.assert_allclose(G[t * 64:(t + 1) * 64], gV, rtol=rt, atol=at)
         np.testing.assert_allclose(G[T:T + T * C].reshape(T, C, D)[t * 64:(t + 1) * 64], gX,
                                    rtol=2e-4, atol=2e-5)
-        np.testing.assert_allclose(G[T + T * C + t * S:T + T * C + (t + 1) * S], gN, rtol=2e-4,
-                                   atol=2e-5)
-    np.testing.assert_allclose(loss.sum().item(), tot, rtol=1e-4)
+        np.testing.assert_allclose(G[T + T * C + t * S:T + T * C + (t + 1) * S], gN, rtol=rt,
+                                   atol=at)
+    np.testing.assert_allclose(loss.sum().item(), tot, rtol=1e-4 if not bf16 else 3e-3)
 
 
 def test_w2v_sgns_duplicate_rows_accumulate(dev):
@@ -302,6 +308,7 @@ def test_word2vec_context_reduce_matches_atomics(dev, monkeypatch):
     """Context-row gradients summed per unique key over the dedup buckets
     (k_w2v_ctx_reduce) == one row of float atomics per (center, context)."""
     monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    monkeypatch.setenv("SS_W2V_MFMA", "f32")  # the context-reduce mode runs the fp32 tile
     out = {}
     for mode in ("reduce", "atomic"):
         monkeypatch.setenv("SS_W2V_CTX", mode)  # (atomic is the default)
