@@ -192,7 +192,8 @@ def main(argv=None):
             "vs_baseline": (round(value / BASELINE_SAMPLES_PER_SEC, 2)
                             if BASELINE_SAMPLES_PER_SEC else None),
             "dtype": "fp32",
-            "data": "synthetic (on-device CTR generator, 39 fields, Zipf ids over 1B features)",
+            "data": (f"synthetic (on-device CTR generator, {a.fields} fields, Zipf ids over "
+                     f"{a.features / 1e9:g}B features; random-init (zero) weights)"),
             "config": {
                 "model": f"sparse_lr_{a.features // 1_000_000}M_features",
                 "global_batch": a.batch * world,
