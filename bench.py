@@ -39,8 +39,8 @@ def main(argv=None):
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
     # 262144 x 39 = 10.2M key occurrences per GPU per step: a working set sized
-    # for one MI355X (the step still takes ~1.2 ms), which also amortises the
-    # per-round collective latency when N > 1
+    # for one MI355X (the step takes ~1 ms), which also amortises the per-round
+    # collective latency when N > 1
     ap.add_argument("--batch", type=int, default=262144, help="samples per GPU per step")
     ap.add_argument("--fields", type=int, default=39)
     ap.add_argument("--features", type=int, default=1_000_000_000)
@@ -93,8 +93,9 @@ def main(argv=None):
 
                 transport = TorchDistTransport()
             else:
-                # two native RCCL communicators: data plane (main stream) and
-                # the route stage + pull-ahead (route stream)
+                # three native RCCL communicators, one per stream: data plane
+                # (main: gradients), count exchange (route), pulled-ahead round
+                # (pull: keys + rows)
                 transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
                 ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts")
                 ptrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_pull")
