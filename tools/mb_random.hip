@@ -3,6 +3,7 @@
 //   read8  : load one 8-byte key per row
 //   rmw16  : load 16 B, update, store 16 B (AdaGrad-style slot update)
 //   cas8   : one 64-bit CAS per row (insert of a new key)
+//   store8 : one blind 8-byte store per row (the fused LR update's row write)
 // Usage: mb_random [GiB=23] [rows=1500000]
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -33,6 +34,12 @@ __global__ void k_cas8(unsigned long long* __restrict__ tab, const unsigned long
   if (i < n) out[i] = atomicCAS(tab + idx[i] * 2 + 1, ~0ull, (unsigned long long)i);
 }
 
+__global__ void k_store8(unsigned long long* __restrict__ tab,
+                         const unsigned long long* __restrict__ idx, long long n) {
+  long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) tab[idx[i] * 2] = (unsigned long long)i;
+}
+
 int main(int argc, char** argv) {
   const double gib = argc > 1 ? atof(argv[1]) : 23.0;
   const long long n = argc > 2 ? atoll(argv[2]) : 1500000;
@@ -56,7 +63,7 @@ int main(int argc, char** argv) {
   hipEventCreate(&a);
   hipEventCreate(&b);
   const int bs = 256, gr = (int)((n + bs - 1) / bs);
-  for (int kind = 0; kind < 3; ++kind) {
+  for (int kind = 0; kind < 4; ++kind) {
     float best = 1e9;
     for (int rep = 0; rep < 6; ++rep) {
       if (kind == 2) CK(hipMemset(tab, 0xFF, rows * 16));
@@ -64,13 +71,14 @@ int main(int argc, char** argv) {
       if (kind == 0) hipLaunchKernelGGL(k_read8, gr, bs, 0, 0, tab, idx, n, out);
       if (kind == 1) hipLaunchKernelGGL(k_rmw16, gr, bs, 0, 0, (float4*)tab, idx, g, n);
       if (kind == 2) hipLaunchKernelGGL(k_cas8, gr, bs, 0, 0, tab, idx, n, out);
+      if (kind == 3) hipLaunchKernelGGL(k_store8, gr, bs, 0, 0, tab, idx, n);
       hipEventRecord(b);
       hipEventSynchronize(b);
       float ms;
       hipEventElapsedTime(&ms, a, b);
       if (rep && ms < best) best = ms;
     }
-    const char* nm[3] = {"read8", "rmw16", "cas8"};
+    const char* nm[4] = {"read8", "rmw16", "cas8", "store8"};
     printf("%-6s rows=%lld table=%.1f GiB: %.1f us  %.2f G rows/s\n", nm[kind], n, gib, best * 1e3,
            n / (best * 1e-3) / 1e9);
   }
