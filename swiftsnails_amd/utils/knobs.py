@@ -1,0 +1,117 @@
+"""Registry of the ``SS_*`` environment knobs.
+
+Every environment variable the package, its kernels' launchers or the tools
+read is listed here with its default, where it is read and what measuring it
+showed; ``tests/test_knobs.py`` fails when a new one appears in the sources
+without an entry (or an entry outlives its code).  Defaults are the measured
+best; the experiment knobs keep alternatives that measured slower reachable
+for re-measurement on other hardware.
+
+    python -m swiftsnails_amd.utils.knobs        # print the table
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+
+class Knob(NamedTuple):
+    default: str
+    where: str
+    kind: str  # "ops" | "tuning" | "experiment" | "debug" | "build"
+    what: str
+
+
+KNOBS: dict[str, Knob] = {
+    # -- operation / deployment
+    "SS_DEVICE": Knob("LOCAL_RANK", "framework/gpu.py", "ops",
+                      "pin every rank to one device (multi-rank rehearsal on one GPU, gloo)"),
+    "SS_BENCH_DEVICE": Knob("LOCAL_RANK", "bench.py", "ops", "same, for bench.py"),
+    "SS_BENCH_ROUND_TIMEOUT": Knob("300", "bench.py", "ops",
+                                   "seconds without a finished step before the bench aborts"),
+    "SS_FAULT": Knob("", "parallel/watchdog.py", "ops",
+                     "fault injection: hang|crash|slow:rank=R:step=S"),
+    "SS_LOG_LEVEL": Knob("WARNING", "utils/logging.py, csrc/host/common.h", "ops",
+                         "log level (Python and the native runtime)"),
+    "SS_LOCAL_IP": Knob("auto", "csrc/host/transfer.h", "ops",
+                        "address the host-mode roles advertise"),
+    "SS_GRAPH": Knob("1", "models/base.py", "ops",
+                     "0: enable_graph() declines (replay is requested by config `graph` or "
+                     "bench --graph)"),
+    # -- build
+    "SS_OFFLOAD_ARCH": Knob("gfx950", "_build.py", "build", "HIP offload target"),
+    "SS_NO_AUTOBUILD": Knob("0", "_native.py", "build",
+                            "1: never build on import; a missing extension is an error"),
+    # -- engine / table (defaults are the measured best)
+    "SS_ENGINE_DEPTH": Knob("3", "parallel/engine.py", "tuning",
+                            "route-buffer ring depth (3: routing never waits on the last push)"),
+    "SS_PULL_AHEAD": Knob("1", "parallel/engine.py", "tuning",
+                          "N>1 (and FM / word2vec at N=1): pull round i+1 while round i computes"),
+    "SS_PULL_SNAPSHOT": Knob("1", "parallel/engine.py", "tuning",
+                             "1 GPU, scalar AdaGrad: the pull snapshots (w, h) for a blind-store "
+                             "update (1.126 -> 1.085 ms/step)"),
+    "SS_FUSE_APPLY": Knob("1", "parallel/engine.py", "tuning",
+                          "1 GPU LR: AdaGrad update fused into the gradient merge "
+                          "(1.090 -> 0.985 ms/step)"),
+    "SS_DEDUP": Knob("bucket", "ops/dedup.py", "tuning",
+                     "bucket: LDS dedup per hash bucket; hash: global scratch table"),
+    "SS_TABLE_G": Knob("auto", "ops/table.py", "tuning", "lanes per table row"),
+    "SS_TABLE_LAYOUT": Knob("auto", "ops/table.py", "tuning",
+                            "slot layout: rowfirst (width <= 2) / keyfirst"),
+    "SS_TABLE_INSERT": Knob("cas", "ops/table.py", "tuning",
+                            "cas, or claim (plain-store claim + verify; measured slower)"),
+    "SS_TABLE_PREFILL": Knob("1", "ops/table.py", "tuning",
+                             "zero-init tables pre-filled with the init row (insert = CAS only)"),
+    "SS_PULL_BK_Y": Knob("4 (G=1) / 1", "csrc/hip/table.hip", "tuning",
+                         "workgroups per dedup bucket in the bucketed pull"),
+    "SS_APPLY_VEC": Knob("1", "csrc/hip/table.hip", "tuning",
+                         "one lane group per key + 8-byte (w, h) accesses in k_apply"),
+    "SS_BD_NCH": Knob("512", "csrc/hip/bdedup.hip", "tuning", "max count/scatter chunks"),
+    "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "count workgroup size"),
+    "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
+    "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
+    "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
+    "SS_LR_FWD": Knob("auto", "csrc/hip/segreduce.hip", "tuning",
+                      "LR forward layout: packed | group (auto by lane utilisation)"),
+    "SS_FM_REDUCE": Knob("sorted", "csrc/hip/bdedup.hip, models/fm.py", "tuning",
+                         "FM gradient merge: sorted lists, or atomic (LDS float atomics)"),
+    "SS_W2V_MFMA": Knob("bf16", "models/word2vec.py", "tuning",
+                        "word2vec tile: bf16 MFMA (77 KB LDS) or f32 (116 KB)"),
+    # -- experiments (measured slower or neutral; kept for re-measurement)
+    "SS_ENGINE_GENERAL": Knob("0", "parallel/engine.py, bench.py", "experiment",
+                              "run a 1-GPU job through the N>1 path (1: loopback, rccl: size-1 "
+                              "RCCL communicators)"),
+    "SS_OSI": Knob("0", "parallel/engine.py", "experiment",
+                   "occurrence-space unique ids (forward 192 -> 123 us, dedup 217 -> 350 us)"),
+    "SS_LR_SINGLE": Knob("0", "models/sparse_lr.py", "experiment",
+                         "store instead of add for keys seen once (reduce -6 us, step unchanged)"),
+    "SS_LR_INV": Knob("0", "models/sparse_lr.py", "experiment",
+                      "materialised inverse on the route stream (neutral)"),
+    "SS_FM_FUSE_APPLY": Knob("0", "models/fm.py", "experiment",
+                             "FM update fused into the sorted merge (0.62 -> 1.04 ms/step)"),
+    "SS_FM_NC": Knob("auto", "csrc/hip/bdedup.hip", "experiment",
+                     "FM atomic merge: factor columns per LDS pass"),
+    "SS_FM_SPLIT": Knob("0", "csrc/hip/bdedup.hip", "experiment",
+                        "FM atomic merge: column groups on separate workgroups"),
+    "SS_W2V_CTX": Knob("atomic", "models/word2vec.py", "experiment",
+                       "reduce: context gradients merged per key over the dedup buckets "
+                       "(0.32 -> 0.81 ms/step)"),
+    "SS_ROUTE_PRIORITY": Knob("0", "parallel/engine.py", "experiment",
+                              "high-priority route stream (no gain)"),
+    "SS_GRAPH_STEPS": Knob("depth", "models/base.py", "experiment",
+                           "1: one hipGraph per step instead of per ring period"),
+    # -- debug
+    "SS_BD_DEBUG": Knob("0", "ops/dedup.py", "debug",
+                        "per-bucket dedup phase timestamps"),
+}
+
+
+def table() -> str:
+    rows = ["| knob | default | kind | read in | what |", "|---|---|---|---|---|"]
+    for k in sorted(KNOBS):
+        v = KNOBS[k]
+        rows.append(f"| `{k}` | {v.default} | {v.kind} | `{v.where}` | {v.what} |")
+    return "\n".join(rows)
+
+
+if __name__ == "__main__":  # pragma: no cover
+    print(table())
