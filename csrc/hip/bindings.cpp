@@ -293,6 +293,23 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("ugrad"), py::arg("st"), py::arg("ovf") = 0, py::arg("t") = py::none(),
      py::arg("slots") = 0, py::arg("op") = py::none());
   m.def("bd_fm_ovf_words", &bd_fm_ovf_words);
+  // A stream whose kernels may only occupy `keep` of the device's CUs, spread
+  // evenly over the CU index space (hipExtStreamCreateWithCUMask): limits how
+  // much of the memory system a side stream's kernels can claim.
+  m.def("cu_mask_stream", [](int device, int keep) {
+    check_hip(hipSetDevice(device), "hipSetDevice");
+    hipDeviceProp_t prop;
+    check_hip(hipGetDeviceProperties(&prop, device), "hipGetDeviceProperties");
+    const int n = prop.multiProcessorCount;
+    if (keep < 1 || keep > n) throw std::invalid_argument("cu_mask_stream: keep out of range");
+    std::vector<uint32_t> mask((n + 31) / 32, 0u);
+    for (int i = 0; i < n; ++i)
+      if ((long long)(i + 1) * keep / n > (long long)i * keep / n) mask[i / 32] |= 1u << (i % 32);
+    hipStream_t s;
+    check_hip(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask.size(), mask.data()),
+              "hipExtStreamCreateWithCUMask");
+    return reinterpret_cast<uintptr_t>(s);
+  });
   m.def("fm_fwd_bwd", [](uintptr_t inv, uintptr_t labels, int B, int F, int dim, uintptr_t uvals,
                          uintptr_t ugrad, uintptr_t loss, uintptr_t pred, uintptr_t st) {
     launch_fm_fwd_bwd(P<const uint32_t>(inv), P<const float>(labels), B, F, dim,

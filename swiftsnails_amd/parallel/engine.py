@@ -196,6 +196,14 @@ class PSEngine:
             # dispatch priority; measured no gain on 1 GPU (186 vs 189 M/s), off
             prio = -1 if os.environ.get("SS_ROUTE_PRIORITY", "0") != "0" else 0
             self.route_stream = torch.cuda.Stream(device=dev, priority=prio)
+            # SS_ROUTE_CUS=k: the route stream's kernels may use only k CUs (a
+            # CU-masked stream), leaving the memory system to the main stream's
+            # critical chain while the route stage, which has slack, runs longer.
+            # Measured slower for every k (0.97 -> 1.17-1.20 ms/step): off
+            route_cus = int(os.environ.get("SS_ROUTE_CUS", "0") or 0)
+            if route_cus > 0:
+                ptr = _hip().cu_mask_stream(dev.index or 0, route_cus)
+                self.route_stream = torch.cuda.ExternalStream(ptr, device=dev)
             self._free = [None] * self.depth  # main-stream event: slot buffers released
             self._free_tag = [None] * self.depth
             self._pins = [torch.zeros(2 * N, dtype=torch.int64, pin_memory=True)

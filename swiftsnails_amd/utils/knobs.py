@@ -95,6 +95,9 @@ KNOBS: dict[str, Knob] = {
     "SS_W2V_CTX": Knob("atomic", "models/word2vec.py", "experiment",
                        "reduce: context gradients merged per key over the dedup buckets "
                        "(0.32 -> 0.81 ms/step)"),
+    "SS_ROUTE_CUS": Knob("0 (all)", "parallel/engine.py", "experiment",
+                         "route stream on a CU-masked stream of k CUs (measured 0.97 -> "
+                         "1.17-1.20 ms/step for k = 64..192 of 256)"),
     "SS_ROUTE_PRIORITY": Knob("0", "parallel/engine.py", "experiment",
                               "high-priority route stream (no gain)"),
     "SS_GRAPH_STEPS": Knob("depth", "models/base.py", "experiment",
