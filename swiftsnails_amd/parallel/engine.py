@@ -13,10 +13,11 @@ Reference call stacks being replaced:
 
 A round is lockstep across ranks and split in three stages:
 
-    route (route stream): dedup + route keys into per-rank segments (1 kernel
-                          + inverse); [N>1] counts all-to-all + async D2H
-    pull  (main stream) : [N>1] wait counts; keys a2av -> server
-                          probe/init/gather -> values a2av back
+    route (route stream): dedup + route keys into per-rank segments (bucketed
+                          LDS dedup); [N>1] counts all-to-all + async D2H
+    pull  (main stream, or the pull stream with pull-ahead): [N>1] wait
+                          counts; keys a2av -> server probe/init/gather ->
+                          values a2av back
     push  (main stream) : grads a2av -> server apply, one launch per source
                           rank in rank order (duplicate keys never race)
 
@@ -24,9 +25,13 @@ A round is lockstep across ranks and split in three stages:
 stream and its own RCCL communicator, so key generation, dedup and the count
 exchange overlap the previous step's compute, and the one host
 synchronisation per round (the counts RCCL needs on the host) is already
-satisfied when ``pull`` asks for it.  Route buffers are a ring of depth 2.
+satisfied when ``pull`` asks for it.  With pull-ahead (N>1 default; FM and
+word2vec at N=1) round i+1 is pulled on a third stream and communicator
+while round i computes (staleness 1).  Route buffers are a ring of depth 3.
 On one GPU (world 1) no host synchronisation happens at all: the unique-key
-count stays on the device and every kernel reads it there.
+count stays on the device and every kernel reads it there; scalar AdaGrad
+rows are snapshotted by the pull and updated inside the model's gradient
+merge (``fuse_apply``).
 
 Split roles (S servers + W workers) fall out of the same code: non-server
 ranks own no table and receive nothing (the router never maps to them);
