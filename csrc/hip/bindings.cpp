@@ -8,6 +8,7 @@
 #include <pybind11/stl.h>
 
 #include "comm.h"
+#include "worker.h"
 #include "ss_launch.h"
 
 namespace py = pybind11;
@@ -293,6 +294,27 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("ugrad"), py::arg("st"), py::arg("ovf") = 0, py::arg("t") = py::none(),
      py::arg("slots") = 0, py::arg("op") = py::none());
   m.def("bd_fm_ovf_words", &bd_fm_ovf_words);
+  // ---- native worker API (worker.h): pull / push with async handles
+  py::class_<Handle>(m, "Handle")
+      .def("wait", &Handle::wait, py::call_guard<py::gil_scoped_release>())
+      .def("done", &Handle::done);
+  py::class_<GpuWorker>(m, "GpuWorker")
+      .def(py::init([](const DevTable& t, uintptr_t size_ctr, uintptr_t err, const InitParams& ip,
+                       const OptParams& op, int G, long long max_keys) {
+             return new GpuWorker(t, P<unsigned long long>(size_ctr), P<int>(err), ip, op, G,
+                                  max_keys);
+           }),
+           py::arg("t"), py::arg("size_ctr"), py::arg("err"), py::arg("init"), py::arg("opt"),
+           py::arg("G"), py::arg("max_keys"))
+      .def("pull", [](GpuWorker& w, uintptr_t keys, long long n, uintptr_t vals, uintptr_t st) {
+        return w.pull(P<const uint64_t>(keys), n, P<float>(vals), S(st));
+      })
+      .def("push", [](GpuWorker& w, uintptr_t keys, long long n, uintptr_t grads, uintptr_t st) {
+        return w.push(P<const uint64_t>(keys), n, P<const float>(grads), S(st));
+      })
+      .def("unique_count_ptr",
+           [](const GpuWorker& w) { return reinterpret_cast<uintptr_t>(w.unique_count()); })
+      .def_property_readonly("max_keys", &GpuWorker::max_keys);
   // A stream whose kernels may only occupy `keep` of the device's CUs, spread
   // evenly over the CU index space (hipExtStreamCreateWithCUMask): limits how
   // much of the memory system a side stream's kernels can claim.

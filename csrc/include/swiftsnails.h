@@ -12,8 +12,10 @@
 //   Vec (vec.h), string helpers (string_util.h), data loaders (dataio.h)
 //   ss::fmix64, ss::opt_apply (ss/hash.h, ss/optim.h)  shared with the HIP kernels
 //
-// The GPU data plane (HBM tables, bucketed dedup, RCCL rounds) is driven from
-// Python (swiftsnails_amd.parallel.PSEngine) over the _ss_hip extension.
+// GPU side: csrc/hip/worker.h (ss::GpuWorker: pull / push against one GPU's
+// HBM table with async handles, compiled into _ss_hip with the kernels); the
+// multi-GPU round engine (RCCL all-to-all-v rounds, pull-ahead) is driven from
+// Python (swiftsnails_amd.parallel.PSEngine) over the same kernels.
 #pragma once
 
 #include "ss/hash.h"

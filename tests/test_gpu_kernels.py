@@ -697,3 +697,45 @@ def test_hbm_table_streaming_checkpoint(dev, tmp_path):
     assert a.keys() == b.keys()
     for key in list(a)[:2000]:
         np.testing.assert_array_equal(a[key], b[key])
+
+
+def test_native_gpu_worker_pull_push(dev):
+    """C++ GpuWorker (worker.h): pull returns rows in occurrence order
+    (inserting missing keys), push applies the per-key SUM of duplicate keys'
+    gradients once — the same table as the Python path with merged grads."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+
+    def table():
+        return HbmTable(4, 1 << 15, optimizer=Optimizer("adagrad", lr=0.2),
+                        init=InitConfig("uniform", 0.3, 0.1, seed=9), device=dev)
+
+    t, ref = table(), table()
+    w = hip().GpuWorker(t.dt, t.size_ctr.data_ptr(), t.err.data_ptr(), t._init_native,
+                        t.opt.native(), t.G, 4096)
+    rng = np.random.default_rng(2)
+    keys_np = rng.integers(1, 700, 3000).astype(np.int64)  # heavy duplication
+    keys = torch.from_numpy(keys_np).to(dev)
+    st = torch.cuda.current_stream().cuda_stream
+    vals = torch.empty(len(keys), 4, device=dev)
+    h = w.pull(keys.data_ptr(), len(keys), vals.data_ptr(), st)
+    h.wait()
+    assert h.done()
+    uk = np.unique(keys_np)
+    rv, _ = ref.pull(torch.from_numpy(uk).to(dev), unique=True)
+    torch.cuda.synchronize()
+    row = {int(k): rv[i].cpu().numpy() for i, k in enumerate(uk)}
+    np.testing.assert_array_equal(vals.cpu().numpy(), np.stack([row[int(k)] for k in keys_np]))
+    assert t.size() == len(uk)
+    g_np = rng.standard_normal((len(keys_np), 4)).astype(np.float32)
+    w.push(keys.data_ptr(), len(keys), torch.from_numpy(g_np).to(dev).data_ptr(), st).wait()
+    merged = np.zeros((len(uk), 4), np.float32)
+    np.add.at(merged, np.searchsorted(uk, keys_np), g_np)
+    ref.push(torch.from_numpy(uk).to(dev), torch.from_numpy(merged).to(dev))
+    torch.cuda.synchronize()
+    t.check()
+    a, b = t.to_dict(with_state=True), ref.to_dict(with_state=True)
+    assert a.keys() == b.keys()
+    for k in a:
+        np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6)
