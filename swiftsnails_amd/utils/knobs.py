@@ -43,7 +43,8 @@ KNOBS: dict[str, Knob] = {
                             "1: never build on import; a missing extension is an error"),
     # -- engine / table (defaults are the measured best)
     "SS_ENGINE_DEPTH": Knob("3", "parallel/engine.py", "tuning",
-                            "route-buffer ring depth (3: routing never waits on the last push)"),
+                            "route-buffer ring depth (3: routing never waits on the last push; "
+                            "4 measured 1.008 vs 1.018 ms/step, within box noise)"),
     "SS_PULL_AHEAD": Knob("1", "parallel/engine.py", "tuning",
                           "N>1 (and FM / word2vec at N=1): pull round i+1 while round i computes"),
     "SS_PULL_SNAPSHOT": Knob("1", "parallel/engine.py", "tuning",
