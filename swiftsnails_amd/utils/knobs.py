@@ -42,9 +42,9 @@ KNOBS: dict[str, Knob] = {
     "SS_NO_AUTOBUILD": Knob("0", "_native.py", "build",
                             "1: never build on import; a missing extension is an error"),
     # -- engine / table (defaults are the measured best)
-    "SS_ENGINE_DEPTH": Knob("3", "parallel/engine.py", "tuning",
-                            "route-buffer ring depth (3: routing never waits on the last push; "
-                            "4 measured 1.008 vs 1.018 ms/step, within box noise)"),
+    "SS_ENGINE_DEPTH": Knob("4", "parallel/engine.py", "tuning",
+                            "route-buffer ring depth (>= 3 for pull-ahead; 4 measured 1.008 vs "
+                            "1.018 ms/step for 3, four A/B pairs)"),
     "SS_PULL_AHEAD": Knob("1", "parallel/engine.py", "tuning",
                           "N>1 (and FM / word2vec at N=1): pull round i+1 while round i computes"),
     "SS_PULL_SNAPSHOT": Knob("1", "parallel/engine.py", "tuning",
