@@ -100,6 +100,9 @@ KNOBS: dict[str, Knob] = {
     "SS_ROUTE_CUS": Knob("0 (all)", "parallel/engine.py", "experiment",
                          "route stream on a CU-masked stream of k CUs (measured 0.97 -> "
                          "1.17-1.20 ms/step for k = 64..192 of 256)"),
+    "SS_DATA_AHEAD": Knob("0", "models/sparse_lr.py", "experiment",
+                          "generate batch i+2 on a third stream beside the route of i+1 "
+                          "(neutral: 0.971 vs 0.975 ms/step, three A/B pairs)"),
     "SS_ROUTE_PRIORITY": Knob("0", "parallel/engine.py", "experiment",
                               "high-priority route stream (no gain)"),
     "SS_GRAPH_STEPS": Knob("depth", "models/base.py", "experiment",

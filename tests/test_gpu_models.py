@@ -450,3 +450,19 @@ def test_fm_worker_fused_update_matches_separate_apply(dev, monkeypatch):
     # float summation order (LDS counting sort, atomics) over 10 training steps
     np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
                                rtol=1e-3, atol=1e-3)
+
+
+def test_data_ahead_matches_inline(dev, monkeypatch):
+    """SS_DATA_AHEAD=1 (the batch of step i+2 generated on a third stream)
+    trains exactly like in-line generation on the route stream: the generator
+    is a pure function of the step, so the per-step losses agree."""
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    out = []
+    for ahead in ("0", "1"):
+        monkeypatch.setenv("SS_DATA_AHEAD", ahead)
+        w, t = _graph_worker("lr", dev)
+        assert w._data_ahead == (ahead == "1")
+        out.append([float(w.step().sum().item()) for _ in range(9)])
+        torch.cuda.synchronize()
+        t.check()
+    np.testing.assert_allclose(out[1], out[0], rtol=2e-4, atol=1e-3)
