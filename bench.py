@@ -152,7 +152,7 @@ def main(argv=None):
         for i in range(2 * engine.depth):  # warm every phase's graph
             worker.step()
     torch.cuda.synchronize()
-    table.check()
+    engine.check()
     first_loss = worker.mean_loss()
 
     barrier()
@@ -169,7 +169,7 @@ def main(argv=None):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed = float(t.item())
-    table.check()
+    engine.check()  # table full / dedup overflow: fail instead of reporting
     last_loss = worker.mean_loss()
     # unique keys per step this rank routed (mean over the ring slots)
     uniq = sum(int(dd.ucount.sum()) for dd in engine.dedupers) // len(engine.dedupers)

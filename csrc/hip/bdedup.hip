@@ -42,8 +42,13 @@
 //
 // Bucket b = d * Pd + fastrange32(dedup_hash(key) >> 32, Pd) with
 // d = map[fmix64(key) % frag_num] (hashfrag.h:48-53).  Pd is chosen so a
-// bucket holds ~2048 occurrences; its unique count is then far below the
-// 4096-slot LDS table (overflow is detected and reported, never silent).
+// bucket holds ~2048 occurrences (at most 2800) GIVEN THE DESTINATIONS THAT
+// RECEIVE KEYS: `ndest` is the effective number of servers (frag_num over the
+// largest per-server fragment count), so split roles (1 server in 4 ranks)
+// do not pile 4x the keys into each bucket.  Its unique count is then far
+// below the 4096-slot LDS table; a bucket that still overflows sets the
+// sticky error word (scratch[0]), which Deduper.check() / PSEngine.check()
+// turn into an exception at the engine's check points.
 #include <algorithm>
 #include <cstdlib>
 #include <string>
@@ -86,13 +91,20 @@ struct BdLayout {
   long long hist, btot, bstart, ubase, unum, ctr, total;
 };
 
-static BdLayout bd_layout(long long n, int nranks) {
+static int bd_clamp_ndest(int nranks, int ndest) {
+  return ndest < 1 || ndest > nranks ? nranks : ndest;
+}
+
+static BdLayout bd_layout(long long n, int nranks, int ndest) {
   BdLayout L{};
+  ndest = bd_clamp_ndest(nranks, ndest);
   // ~2048 occurrences per bucket, but at least ~1024 buckets for small calls
   // (>= 4 workgroups per CU; a word2vec step of 196K keys got only 96 buckets)
   long long target = std::min<long long>(kBdTarget, std::max<long long>(128, n / 1024));
   if (n > (long long)kBdMaxBuckets * kBdTarget) target = (n + kBdMaxBuckets - 1) / kBdMaxBuckets;
-  long long pd = (n + (long long)nranks * target - 1) / ((long long)nranks * target);
+  // buckets per destination from the keys one destination receives (n /
+  // ndest), not n / nranks: ranks that host no shard get empty buckets
+  long long pd = (n + (long long)ndest * target - 1) / ((long long)ndest * target);
   if (pd < 1) pd = 1;
   L.Pd = (int)pd;
   L.P = (int)(pd * nranks);
@@ -123,28 +135,37 @@ static BdLayout bd_layout(long long n, int nranks) {
   return L;
 }
 
+// largest call the bucketed dedup takes (~2800 occurrences per bucket at
+// the bucket-count cap); Deduper falls back to the scratch-hash dedup above
+long long bd_max_keys() { return (long long)kBdMaxBuckets * 2800; }
+
 // words for ANY call of up to n keys: the layout is not monotonic in n (the
 // bucket target grows with n below 2M keys, the chunk count jumps with the
 // wave count), so bound P and nch over all m <= n instead of sizing for n
-long long bd_scratch_words(long long n, int nranks) {
+long long bd_scratch_words(long long n, int nranks, int ndest) {
   if (n < 1) n = 1;
-  long long pmax = std::max<long long>(1056, (n + kBdTarget - 1) / kBdTarget);
-  pmax = std::min<long long>(pmax, kBdMaxBuckets) + 2 * nranks;
+  ndest = bd_clamp_ndest(nranks, ndest);
+  // active buckets (those of receiving destinations), then all P = Pd * nranks
+  long long pact = std::max<long long>(1056, (n + kBdTarget - 1) / kBdTarget);
+  pact = std::min<long long>(pact, kBdMaxBuckets) + 2 * ndest;
+  const long long pmax = ((pact + ndest - 1) / ndest + 1) * nranks;
   const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
   long long nchmax = std::min<long long>(256 * waves, bd_max_chunks());
   nchmax = std::min<long long>(nchmax, (n + kBdChunkLanes - 1) / kBdChunkLanes);
   nchmax = std::max<long long>(nchmax, 1);
   const long long bound = 2 + pmax * nchmax + 4 * pmax + 1;
-  return std::max(bound, bd_layout(n, nranks).total);
+  return std::max(bound, bd_layout(n, nranks, ndest).total);
 }
-int bd_buckets(long long n, int nranks) { return bd_layout(n < 1 ? 1 : n, nranks).P; }
+int bd_buckets(long long n, int nranks, int ndest) {
+  return bd_layout(n < 1 ? 1 : n, nranks, ndest).P;
+}
 // (P, bstart, unum, ubase) word offsets into the scratch for a call of n keys
-std::vector<long long> bd_offsets(long long n, int nranks) {
-  const BdLayout L = bd_layout(n < 1 ? 1 : n, nranks);
+std::vector<long long> bd_offsets(long long n, int nranks, int ndest) {
+  const BdLayout L = bd_layout(n < 1 ? 1 : n, nranks, ndest);
   return {L.P, L.bstart, L.unum, L.ubase};
 }
-long long bd_ubase_offset(long long n, int nranks) {
-  return bd_layout(n < 1 ? 1 : n, nranks).ubase;
+long long bd_ubase_offset(long long n, int nranks, int ndest) {
+  return bd_layout(n < 1 ? 1 : n, nranks, ndest).ubase;
 }
 
 // 1. per-chunk bucket histogram (dynamic LDS: P words), chunk-major output
@@ -799,7 +820,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg, uint32_t* osi_inv, uint8_t* usingle) {
+                     unsigned long long* dbg, uint32_t* osi_inv, uint8_t* usingle, int ndest) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   if (n <= 0) {
     check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
@@ -808,8 +829,9 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   if (ucap < n) throw_error("bdedup: per-destination capacity must be >= n");
   if ((unsigned long long)rs.nranks * (unsigned long long)ucap >= 0x7FFFFFFFull)
     throw_error("bdedup: nranks*ucap overflows 31-bit unique ids");
-  const BdLayout L = bd_layout(n, rs.nranks);
-  if (L.P > kBdMaxBuckets + kMaxSeg || n > (long long)kBdMaxBuckets * 2800)
+  const BdLayout L = bd_layout(n, rs.nranks, ndest);
+  if ((long long)L.Pd * bd_clamp_ndest(rs.nranks, ndest) > kBdMaxBuckets + kMaxSeg ||
+      n > bd_max_keys())
     throw_error("bdedup: too many keys per call (max ~45M)");
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
@@ -867,9 +889,9 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
 }
 
 void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,
-                       float* dst, int dim, hipStream_t st) {
+                       float* dst, int dim, hipStream_t st, int ndest) {
   if (n <= 0) return;
-  const BdLayout L = bd_layout(n, nranks);
+  const BdLayout L = bd_layout(n, nranks, ndest);
   hipLaunchKernelGGL(k_bd_unplace, dim3(L.P), dim3(256), 0, st, scratch + L.bstart,
                      scratch + L.unum, scratch + L.ubase, src, dst, dim);
   check_launch("k_bd_unplace");
@@ -879,7 +901,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi, const uint8_t* usingle,
                       const DevTable* t, const long long* slots, const float* snap,
-                      const OptParams* op) {
+                      const OptParams* op, int ndest) {
   if (n <= 0) return;
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
   DevTable tv{};
@@ -892,7 +914,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
     opv = *op;
   }
   const float2* sn = reinterpret_cast<const float2*>(snap);
-  const BdLayout L = bd_layout(n, nranks);
+  const BdLayout L = bd_layout(n, nranks, ndest);
   const uint32_t* S = scratch;
   // workgroup size (SS_BD_RT experiment knob): measured 1024 >= 512 >= 256
   static const int rt = [] {
@@ -916,7 +938,8 @@ long long bd_fm_ovf_words(long long n) { return n / kFmOcc + 2; }
 void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                          const uint32_t* luid, const float* gs, const float* gss, int F, int dim,
                          const float* uvals, float* ugrad, hipStream_t st, uint32_t* ovf,
-                         const DevTable* t, const long long* slots, const OptParams* op) {
+                         const DevTable* t, const long long* slots, const OptParams* op,
+                         int ndest) {
   if (n <= 0) return;
   DevTable tv{};
   OptParams opv{};
@@ -926,7 +949,7 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
     tv = *t;
     opv = *op;
   }
-  const BdLayout L = bd_layout(n, nranks);
+  const BdLayout L = bd_layout(n, nranks, ndest);
   const uint32_t* S = scratch;
   // default: sorted lists (no float atomics) + LDS-atomic form for overflow
   // buckets; ovf = {count, bucket ids} scratch of bd_fm_ovf_words(n) words

@@ -172,44 +172,49 @@ PYBIND11_MODULE(_ss_hip, m) {
                        P<uint32_t>(inv), S(st));
   });
   m.def("dedup_blocks", &dedup_blocks);
-  m.def("bd_scratch_words", &bd_scratch_words);
-  m.def("bd_ubase_offset", &bd_ubase_offset);
-  m.def("bd_offsets", &bd_offsets);
-  m.def("bd_buckets", &bd_buckets);
+  m.def("bd_max_keys", &bd_max_keys);
+  m.def("bd_scratch_words", &bd_scratch_words, py::arg("n"), py::arg("nranks"),
+        py::arg("ndest") = 0);
+  m.def("bd_ubase_offset", &bd_ubase_offset, py::arg("n"), py::arg("nranks"),
+        py::arg("ndest") = 0);
+  m.def("bd_offsets", &bd_offsets, py::arg("n"), py::arg("nranks"), py::arg("ndest") = 0);
+  m.def("bd_buckets", &bd_buckets, py::arg("n"), py::arg("nranks"), py::arg("ndest") = 0);
   m.def("bd_dedup", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num, int nranks,
                        long long ucap, uintptr_t scratch, uintptr_t pj, uintptr_t pos_of,
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
-                       uintptr_t st, uintptr_t dbg, uintptr_t osi_inv, uintptr_t usingle) {
+                       uintptr_t st, uintptr_t dbg, uintptr_t osi_inv, uintptr_t usingle,
+                       int ndest) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
                     P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
                     P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
                     P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg),
-                    P<uint32_t>(osi_inv), P<uint8_t>(usingle));
+                    P<uint32_t>(osi_inv), P<uint8_t>(usingle), ndest);
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
-     py::arg("osi_inv") = 0, py::arg("usingle") = 0);
+     py::arg("osi_inv") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
-                        uintptr_t snap, std::optional<OptParams> op) {
+                        uintptr_t snap, std::optional<OptParams> op, int ndest) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                      P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
                      P<float>(ugrad), S(st), osi, P<const uint8_t>(usingle),
                      t ? &*t : nullptr, P<const long long>(slots), P<const float>(snap),
-                     op ? &*op : nullptr);
+                     op ? &*op : nullptr, ndest);
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("xval"), py::arg("F"), py::arg("ugrad"), py::arg("st"),
      py::arg("osi") = 0, py::arg("usingle") = 0, py::arg("t") = py::none(), py::arg("slots") = 0,
-     py::arg("snap") = 0, py::arg("op") = py::none());
+     py::arg("snap") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0);
   m.def("bd_unplace", [](long long n, int nranks, uintptr_t scratch, uintptr_t src, uintptr_t dst,
-                         int dim, uintptr_t st) {
+                         int dim, uintptr_t st, int ndest) {
     launch_bd_unplace(n, nranks, P<const uint32_t>(scratch), P<const float>(src), P<float>(dst),
-                      dim, S(st));
-  });
+                      dim, S(st), ndest);
+  }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("src"), py::arg("dst"),
+     py::arg("dim"), py::arg("st"), py::arg("ndest") = 0);
   m.def("route_keys", [](uintptr_t keys, long long n, uintptr_t frag_map, int frag_num,
                          int nranks, uintptr_t dest, uintptr_t st) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
@@ -284,15 +289,16 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("bd_reduce_fm", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj,
                            uintptr_t luid, uintptr_t gs, uintptr_t gss, int F, int dim,
                            uintptr_t uvals, uintptr_t ugrad, uintptr_t st, uintptr_t ovf,
-                           std::optional<DevTable> t, uintptr_t slots, std::optional<OptParams> op) {
+                           std::optional<DevTable> t, uintptr_t slots, std::optional<OptParams> op,
+                           int ndest) {
     launch_bd_reduce_fm(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                         P<const uint32_t>(luid), P<const float>(gs), P<const float>(gss), F, dim,
                         P<const float>(uvals), P<float>(ugrad), S(st), P<uint32_t>(ovf),
-                        t ? &*t : nullptr, P<const long long>(slots), op ? &*op : nullptr);
+                        t ? &*t : nullptr, P<const long long>(slots), op ? &*op : nullptr, ndest);
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("gss"), py::arg("F"), py::arg("dim"), py::arg("uvals"),
      py::arg("ugrad"), py::arg("st"), py::arg("ovf") = 0, py::arg("t") = py::none(),
-     py::arg("slots") = 0, py::arg("op") = py::none());
+     py::arg("slots") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0);
   m.def("bd_fm_ovf_words", &bd_fm_ovf_words);
   // ---- native worker API (worker.h): pull / push with async handles
   py::class_<Handle>(m, "Handle")

@@ -108,30 +108,34 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval, 
                      float* g, int per_sample, float* loss_sum, float* pred, hipStream_t st);
 
 // --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
-long long bd_scratch_words(long long n, int nranks);
-long long bd_ubase_offset(long long n, int nranks);
-std::vector<long long> bd_offsets(long long n, int nranks);
-int bd_buckets(long long n, int nranks);
+// ndest: destinations that receive keys (effective server count, <= nranks;
+// 0 = nranks) — sizes the buckets per destination (bdedup.hip bd_layout)
+long long bd_max_keys();
+long long bd_scratch_words(long long n, int nranks, int ndest = 0);
+long long bd_ubase_offset(long long n, int nranks, int ndest = 0);
+std::vector<long long> bd_offsets(long long n, int nranks, int ndest = 0);
+int bd_buckets(long long n, int nranks, int ndest = 0);
 void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                      unsigned long long* dbg = nullptr, uint32_t* osi_inv = nullptr,
-                     uint8_t* usingle = nullptr);
+                     uint8_t* usingle = nullptr, int ndest = 0);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi = 0,
                       const uint8_t* usingle = nullptr, const DevTable* t = nullptr,
                       const long long* slots = nullptr, const float* snap = nullptr,
-                      const OptParams* op = nullptr);
+                      const OptParams* op = nullptr, int ndest = 0);
 void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,
-                       float* dst, int dim, hipStream_t st);
+                       float* dst, int dim, hipStream_t st, int ndest = 0);
 
 void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                          const uint32_t* luid, const float* gs, const float* gss, int F, int dim,
                          const float* uvals, float* ugrad, hipStream_t st,
                          uint32_t* ovf = nullptr, const DevTable* t = nullptr,
-                         const long long* slots = nullptr, const OptParams* op = nullptr);
+                         const long long* slots = nullptr, const OptParams* op = nullptr,
+                         int ndest = 0);
 long long bd_fm_ovf_words(long long n);
 
 // --- w2v.hip

@@ -98,6 +98,7 @@ class PSContext:
                                server_ranks=self.servers, device=self.device,
                                count_transport=ct, pull_transport=pt)
         self.backup_period = int(cfg.get("param_backup_period", 0) or 0)
+        self._last_backup = -1
         self.backup_root = cfg.get("param_backup_root", ".")
         self.ckpt_format = cfg.get("checkpoint_format", "bin")
         self.tracer = Tracer(enabled=str(cfg.get("trace", "0")) not in ("0", "false"))
@@ -124,7 +125,7 @@ class PSContext:
         if resume == "latest":
             found = self._agree(ck.latest_checkpoint(self.backup_root), store)
             if found is not None:
-                self.resume(found[0])
+                self.resume(found[0], world=found[2])
                 self.start_round = found[1]
             else:
                 log.info("resume_from latest: no complete backup under %s", self.backup_root)
@@ -134,18 +135,19 @@ class PSContext:
             self.start_round = int(m.group(1)) if m else 0
 
     def _agree(self, found, store):
-        """Rank 0's choice of checkpoint, for every rank (one filesystem view)."""
+        """Rank 0's choice of checkpoint ``(prefix, round, world)``, for every
+        rank (one filesystem view)."""
         if self.world == 1 or store is None:
             return found
         key = "ss_resume_latest"
+        enc = "" if found is None else f"{found[1]}:{found[2]}:{found[0]}"
         if self.rank == 0:
-            store.set(key, "" if found is None else f"{found[1]}:{found[0]}")
-        v = store.get(key).decode() if self.rank != 0 else (
-            "" if found is None else f"{found[1]}:{found[0]}")
+            store.set(key, enc)
+        v = store.get(key).decode() if self.rank != 0 else enc
         if not v:
             return None
-        rnd, prefix = v.split(":", 1)
-        return prefix, int(rnd)
+        rnd, w, prefix = v.split(":", 2)
+        return prefix, int(rnd), int(w)
 
     # ------------------------------------------------------------ ckpt
     def _owner(self):
@@ -160,19 +162,29 @@ class PSContext:
         self.barrier()
         return p
 
-    def resume(self, prefix: str) -> int:
+    def resume(self, prefix: str, world: Optional[int] = None) -> int:
+        """Load one complete shard set of ``prefix`` (``world``: the set
+        written by that many servers), re-routed to this job's shards."""
         n = 0
         if self.table is not None:
-            n = ck.load_sharded(self.table, prefix, owner_fn=self._owner())
+            n = ck.load_sharded(self.table, prefix, owner_fn=self._owner(), world=world)
             log.info("rank %d resumed %d keys from %s", self.rank, n, prefix)
         self.barrier()
         return n
 
     def maybe_backup(self, round_idx: int) -> None:
-        """Reference: every param_backup_period pushes -> param-<n>.txt."""
-        if self.backup_period > 0 and round_idx > 0 and round_idx % self.backup_period == 0:
+        """Reference: every param_backup_period pushes -> param-<n>.txt.
+
+        ``round_idx`` is the number of rounds the device has applied
+        (``PipelinedWorker.rounds_done``, which runs ahead of the step count
+        under hipGraph replays and then repeats): one backup per label."""
+        if (self.backup_period > 0 and round_idx > 0 and round_idx % self.backup_period == 0
+                and round_idx != self._last_backup):
+            self._last_backup = round_idx
             if self.watchdog:
                 self.watchdog.pause()
+            # never back up rounds whose keys were silently dropped
+            self.engine.check()
             self.save(os.path.join(self.backup_root, f"param-{round_idx}"))
             if self.watchdog:
                 self.watchdog.resume()
@@ -193,8 +205,7 @@ class PSContext:
         out = self.cfg.get("param_output")
         if out:
             self.save(out, fmt=self.cfg.get("param_output_format", "text"))
-        if self.table is not None:
-            self.table.check()
+        self.engine.check()
         self.barrier()
 
     def close(self):
@@ -272,7 +283,7 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
         with ctx.tracer.range(f"step{i}"):
             w.step()
         ctx.round_done(w.step_idx)
-        ctx.maybe_backup(w.step_idx)
+        ctx.maybe_backup(w.rounds_done())
         if log_every and (i + 1) % log_every == 0 and ctx.rank == 0:
             log.warning("step %d loss %.5f", i + 1, w.mean_loss())
     torch.cuda.synchronize()

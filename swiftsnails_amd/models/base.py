@@ -164,6 +164,17 @@ class PipelinedWorker:
         self.step_idx += 1
         return self.loss_sum
 
+    def rounds_done(self) -> int:
+        """Rounds whose pushes have been enqueued on the device.  Eagerly
+        that is ``step_idx``; with hipGraphs a replay runs ``per`` steps on
+        the first step of its period, so the device is up to the end of the
+        current period (a backup taken now holds those rounds and must be
+        labelled with them, or a resume would apply them twice)."""
+        if self._graphs is None:
+            return self.step_idx
+        k = self.step_idx - self._gbase
+        return self._gbase + -(-k // self._gper) * self._gper
+
     def mean_loss(self) -> float:
         n = self.samples_per_step()
         return float(self.loss_sum.sum().item()) / n if n else 0.0

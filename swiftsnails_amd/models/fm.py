@@ -94,7 +94,8 @@ class FMWorker(PipelinedWorker):
             h.bd_reduce_fm(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                            o.luid.data_ptr(), self.gs.data_ptr(), self.gss.data_ptr(),
                            d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
-                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr(), **(fa or {}))
+                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr(), ndest=o.ndest,
+                           **(fa or {}))
             return
         hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),

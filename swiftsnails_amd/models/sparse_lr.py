@@ -210,7 +210,7 @@ class SparseLRWorker(PipelinedWorker):
                             o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
                             rnd.ugrad.data_ptr(), st, int(self.osi and self.engine.fast1),
                             o.usingle.data_ptr() if o.usingle is not None else 0,
-                            **(fa or {}))
+                            ndest=o.ndest, **(fa or {}))
             else:
                 h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
                             self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,

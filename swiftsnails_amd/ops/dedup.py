@@ -30,7 +30,10 @@ import numpy as np
 import torch
 
 from ..utils.hashing import fmix64
+from ..utils.logging import get_logger
 from .table import _stream_ptr
+
+log = get_logger("swiftsnails.dedup")
 
 INVALID = 0xFFFFFFFF
 
@@ -95,8 +98,15 @@ class Deduper:
         d = self.device
         if frag_map is None:
             frag_map = torch.zeros(1, dtype=torch.int32)
+        self.ndest = effective_ndest(frag_map, self.nranks)
         self.frag_map = frag_map.to(d, torch.int32).contiguous()
         m = max(1, self.max_n)
+        if self.mode == "bucket" and m > self.h.bd_max_keys():
+            # above ~45M keys per call the bucket-count cap would push more
+            # than ~2800 occurrences into a bucket's 4096-slot LDS table
+            log.warning("dedup: %d keys per call exceed the bucketed dedup's %d; "
+                        "using the scratch-hash dedup", m, self.h.bd_max_keys())
+            self.mode = "hash"
         if self.mode == "hash":
             self.skeys = torch.empty(self.scap, dtype=torch.int64, device=d)
             self._dirty = True
@@ -106,7 +116,7 @@ class Deduper:
             self.slot_of = torch.empty(self.max_n, dtype=torch.int32, device=d)
         else:
             # word 0 of the scratch is the sticky overflow flag (zeroed once)
-            self.scratch = torch.zeros(self.h.bd_scratch_words(m, self.nranks),
+            self.scratch = torch.zeros(self.h.bd_scratch_words(m, self.nranks, self.ndest),
                                        dtype=torch.int32, device=d)
             self.pj = torch.empty(m, dtype=torch.int32, device=d)      # bucket order -> j
             self.pos_of = torch.empty(m, dtype=torch.int32, device=d)  # j -> bucket order
@@ -115,7 +125,8 @@ class Deduper:
             self.bkeys = torch.empty(m, dtype=torch.int64, device=d)   # staged unique keys
             self._last_n = 0
             # SS_BD_DEBUG=1: per-bucket phase timestamps of the dedup kernel
-            self.dbg = (torch.zeros(8 * self.h.bd_buckets(m, self.nranks), dtype=torch.int64,
+            self.dbg = (torch.zeros(8 * self.h.bd_buckets(m, self.nranks, self.ndest),
+                                    dtype=torch.int64,
                                     device=d) if os.environ.get("SS_BD_DEBUG") else None)
         self.inv = torch.empty(self.max_n, dtype=torch.int32, device=d)
         self.ukeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64, device=d)
@@ -142,7 +153,8 @@ class Deduper:
                             int(self.need_ukeys or bool(ug)), st,
                             self.dbg.data_ptr() if self.dbg is not None else 0,
                             self.inv.data_ptr() if osi else 0,
-                            self.usingle.data_ptr() if self.usingle is not None else 0)
+                            self.usingle.data_ptr() if self.usingle is not None else 0,
+                            self.ndest)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self)
         # the scratch is all-EMPTY between calls: the finish kernel resets the
@@ -176,7 +188,8 @@ class Deduper:
                          self.luid.data_ptr(), gs.data_ptr(),
                          xval.data_ptr() if xval is not None else 0, F, ugrad.data_ptr(),
                          _stream_ptr(stream), int(osi),
-                         self.usingle.data_ptr() if self.usingle is not None else 0)
+                         self.usingle.data_ptr() if self.usingle is not None else 0,
+                         ndest=self.ndest)
 
     def unplace(self, n: int, src: torch.Tensor, dst: torch.Tensor, stream=None):
         """Rows of the LAST call from compact unique ids (``src``, the
@@ -185,7 +198,7 @@ class Deduper:
             raise RuntimeError("unplace needs mode='bucket'")
         self.h.bd_unplace(n, self.nranks, self.scratch.data_ptr(), src.data_ptr(),
                           dst.data_ptr(), src.shape[-1] if src.dim() > 1 else 1,
-                          _stream_ptr(stream))
+                          _stream_ptr(stream), self.ndest)
 
     def index_ptrs(self, n: Optional[int] = None):
         """(pos_of, luid, bkt, ubase) device pointers of the last call: the
@@ -193,7 +206,8 @@ class Deduper:
         if self.mode != "bucket" or self.osi:
             raise RuntimeError("index_ptrs needs mode='bucket' without osi")
         n = self._last_n if n is None else n
-        ub = self.scratch.data_ptr() + 4 * self.h.bd_ubase_offset(max(1, n), self.nranks)
+        ub = self.scratch.data_ptr() + 4 * self.h.bd_ubase_offset(max(1, n), self.nranks,
+                                                                  self.ndest)
         return [self.pos_of.data_ptr(), self.luid.data_ptr(), self.bkt.data_ptr(), ub]
 
     def bucket_view(self, n: Optional[int] = None):
@@ -203,15 +217,36 @@ class Deduper:
         if self.mode != "bucket":
             raise RuntimeError("bucket_view needs mode='bucket'")
         n = self._last_n if n is None else n
-        P, o_bs, o_un, o_ub = self.h.bd_offsets(max(1, n), self.nranks)
+        P, o_bs, o_un, o_ub = self.h.bd_offsets(max(1, n), self.nranks, self.ndest)
         b0 = self.scratch.data_ptr()
         return (self.bkeys.data_ptr(), b0 + 4 * o_bs, b0 + 4 * o_un, b0 + 4 * o_ub, P)
 
     def check(self):
-        """Raise if any bucket overflowed its LDS table (sticky; syncs)."""
+        """Raise if any bucket overflowed its LDS table (sticky; syncs).  The
+        overflowing occurrences got no unique id, so their forward rows and
+        gradients were dropped: the engine calls this at every check point
+        (PSEngine.check: end of bench, backups, PSContext.finish)."""
         if self.mode == "bucket" and int(self.scratch[0].item()) != 0:
-            raise RuntimeError("bucketed dedup: an LDS bucket table overflowed "
-                               "(pathological key distribution); use SS_DEDUP=hash")
+            raise DedupOverflowError("bucketed dedup: an LDS bucket table overflowed "
+                                     "(pathological key distribution); use SS_DEDUP=hash")
+
+
+class DedupOverflowError(RuntimeError):
+    pass
+
+
+def effective_ndest(frag_map, nranks: int) -> int:
+    """Destinations the bucketed dedup sizes its buckets for: the fragment
+    count over the largest per-rank fragment count (ranks hosting no shard,
+    and uneven fragment maps, receive proportionally fewer / more keys),
+    rounded with 5% slack so an even-ish map (1024 fragments over 3 servers)
+    counts all its servers."""
+    fm = np.asarray(frag_map.cpu() if isinstance(frag_map, torch.Tensor) else frag_map,
+                    dtype=np.int64).reshape(-1)
+    if fm.size == 0:
+        return 1
+    biggest = int(np.bincount(fm).max())
+    return max(1, min(int(nranks), int(fm.size * 1.05 / biggest)))
 
 
 class CpuDeduper:

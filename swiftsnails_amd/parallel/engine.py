@@ -148,7 +148,15 @@ class PSEngine:
         # ring depth 4 by default: with one batch of lookahead, routing round
         # i+1 reuses the buffers of round i-3 (long pushed) instead of waiting
         # on round i-1's push (a cross-queue event on the critical path); 3 is
-        # the minimum for pull-ahead, 4 measured 1.008 vs 1.018 ms/step (LR)
+        # the minimum for pull-ahead, 4 measured 1.008 vs 1.018 ms/step (LR,
+        # one GPU).  Every slot holds N*max_keys-row buffers (slot_bytes), so
+        # the default drops to 3 when a fourth slot would take more than 1/8
+        # of the device's memory (wide rows at large N)
+        if depth is None and os.environ.get("SS_ENGINE_DEPTH") is None:
+            depth = 4
+            if self.gpu and 4 * self.slot_bytes(self.world, max_keys, dim) > \
+                    torch.cuda.get_device_properties(self.device).total_memory // 8:
+                depth = 3
         self.depth = max(1, int(depth if depth is not None else
                                 os.environ.get("SS_ENGINE_DEPTH", "4")))
         dd_cls = Deduper if self.gpu else CpuDeduper
@@ -240,6 +248,17 @@ class PSEngine:
         # capturing stream, and events of other captures are not waited on —
         # graph replays run one after the other, so what they order is done
         self.capture_tag: Optional[int] = None
+
+    @staticmethod
+    def slot_bytes(world: int, max_keys: int, dim: int) -> int:
+        """Device bytes of one route-ring slot: pulled rows, the deduper's
+        send keys + gradient rows (+ its ~40 B/key scratch) and, for N>1,
+        the resolved server slots — each sized ``world * max_keys`` rows
+        (a destination segment must hold every unique key of a batch).
+        At N=8 and 10.2M keys per batch: 2.4 GB for LR rows (dim 1), 7.6 GB
+        for FM rows (dim 9)."""
+        rows = world * max_keys
+        return rows * (4 * dim + 8 + 4 * dim + (8 if world > 1 else 0)) + 40 * max_keys
 
     def _wait(self, stream, ev, tag) -> None:
         if ev is not None and tag == self.capture_tag:
@@ -570,3 +589,17 @@ class PSEngine:
 
     def barrier(self):
         self.t.barrier()
+
+    def check(self) -> None:
+        """Raise on a sticky device-side error of this rank (syncs): a dedup
+        bucket whose LDS table overflowed (its occurrences got no unique id,
+        so their rows and gradients were dropped) or a full / misused table.
+        Called at the check points that must not pass silently: the end of
+        bench.py, every periodic backup and PSContext.finish."""
+        for d in self.dedupers:
+            chk = getattr(d, "check", None)
+            if chk is not None:
+                chk()
+        chk = getattr(self.table, "check", None) if self.table is not None else None
+        if chk is not None:
+            chk()

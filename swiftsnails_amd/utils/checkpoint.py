@@ -45,24 +45,40 @@ def _iter_export(table) -> Iterable[tuple[np.ndarray, np.ndarray]]:
 
 
 def save_text(table, path: str, precision: int = 9, with_state: bool = False) -> int:
-    """Write ``key\\tv0 v1 ...`` lines; returns the number of keys written."""
+    """Write ``key\\tv0 v1 ...`` lines; returns the number of keys written.
+
+    A file is written to ``path.tmp``, fsynced and renamed into place, so a
+    crash mid-dump never leaves a truncated shard under ``path`` (which
+    ``latest_checkpoint`` would otherwise count, and ``parse_rows`` would
+    read with its cut-off last line defaulted).  ``path == "-"``: stdout,
+    the reference's final dump (server/terminate.h:36)."""
     n = 0
     h = host()
-    out = open(path, "wb") if path != "-" else None
-    try:
-        for k, r in _iter_export(table):
-            b = h.format_rows(np.ascontiguousarray(k), np.ascontiguousarray(r, dtype=np.float32),
-                              table.dim, table.width, with_state, precision)
-            if out is None:
-                import sys
+    if path == "-":
+        import sys
 
-                sys.stdout.buffer.write(b)
-            else:
-                out.write(b)
+        for k, r in _iter_export(table):
+            sys.stdout.buffer.write(h.format_rows(
+                np.ascontiguousarray(k), np.ascontiguousarray(r, dtype=np.float32),
+                table.dim, table.width, with_state, precision))
             n += len(k)
-    finally:
-        if out is not None:
-            out.close()
+        sys.stdout.buffer.flush()
+        return n
+    tmp = path + ".tmp"
+    try:
+        with open(tmp, "wb") as out:
+            for k, r in _iter_export(table):
+                out.write(h.format_rows(np.ascontiguousarray(k),
+                                        np.ascontiguousarray(r, dtype=np.float32),
+                                        table.dim, table.width, with_state, precision))
+                n += len(k)
+            out.flush()
+            os.fsync(out.fileno())
+    except BaseException:
+        if os.path.exists(tmp):
+            os.unlink(tmp)
+        raise
+    os.replace(tmp, path)
     return n
 
 
@@ -223,46 +239,104 @@ def save_sharded(table, prefix: str, rank: int, world: int, fmt: str = "bin",
     return p
 
 
-def load_sharded(table, prefix: str, owner_fn=None) -> int:
-    """Load every shard file of `prefix`, keeping keys for which
-    ``owner_fn(keys) -> bool mask`` is true (re-sharding on resume)."""
-    files = sorted(glob.glob(prefix + ".shard*-of-*.bin")) + sorted(
-        glob.glob(prefix + ".shard*-of-*.txt"))
-    if not files:
-        raise FileNotFoundError(f"no checkpoint shards for prefix {prefix}")
-    n = 0
-    for f in files:
-        n += (load_binary if f.endswith(".bin") else load_text)(table, f, key_filter=owner_fn)
-    return n
-
-
 _SHARD_RE = None
 
 
-def latest_checkpoint(root: str, stem: str = "param-") -> Optional[tuple[str, int]]:
-    """Newest COMPLETE periodic backup under `root`: ``(prefix, round)`` of
-    the highest ``<stem><round>`` whose shard files ``.shard<r>-of-<W>`` exist
-    for every r < W (a job that died while writing a backup leaves an
-    incomplete set, which is skipped; single files are renamed into place
-    only once written, see save_binary).  None if there is none."""
+def _shard_re():
     import re
 
     global _SHARD_RE
     if _SHARD_RE is None:
-        _SHARD_RE = re.compile(r"^(.*?)(\d+)\.shard(\d+)-of-(\d+)\.(bin|txt)$")
-    sets: dict[tuple[str, int, int, str], set] = {}
-    for f in glob.glob(os.path.join(root, glob.escape(stem) + "*.shard*-of-*.*")):
-        m = _SHARD_RE.match(os.path.basename(f))
-        if not m or m.group(1) != stem:
+        _SHARD_RE = re.compile(r"^(.*)\.shard(\d+)-of-(\d+)\.(bin|txt)$")
+    return _SHARD_RE
+
+
+def shard_sets(prefix: str, fmt: Optional[str] = None) -> dict[int, dict[int, list[str]]]:
+    """Shard files of ``prefix`` grouped by the world size that wrote them:
+    ``{world: {rank: [paths]}}`` (a rank lists two paths when both a ``.bin``
+    and a ``.txt`` exist).  ``fmt`` ("bin" / "text") keeps one format."""
+    ext = None if fmt is None else ("txt" if fmt == "text" else "bin")
+    out: dict[int, dict[int, list[str]]] = {}
+    base = os.path.basename(prefix)
+    for f in sorted(glob.glob(glob.escape(prefix) + ".shard*-of-*.*")):
+        m = _shard_re().match(os.path.basename(f))
+        if not m or m.group(1) != base or (ext is not None and m.group(4) != ext):
             continue
-        key = (os.path.join(root, stem + m.group(2)), int(m.group(2)), int(m.group(4)),
-               m.group(5))
-        sets.setdefault(key, set()).add(int(m.group(3)))
-    done = [(rnd, prefix) for (prefix, rnd, w, _), rs in sets.items() if rs == set(range(w))]
-    if not done:
+        out.setdefault(int(m.group(3)), {}).setdefault(int(m.group(2)), []).append(f)
+    return out
+
+
+def _complete(by_rank: dict[int, list[str]], world: int) -> bool:
+    return set(by_rank) == set(range(world))
+
+
+def select_shards(prefix: str, world: Optional[int] = None, fmt: Optional[str] = None) -> list[str]:
+    """The files of exactly ONE complete shard set of ``prefix``: shards
+    ``0..world-1`` written by one job.  Stale shards of another world size
+    or format next to it are never mixed in (rows loaded later would
+    overwrite newer ones).  Without ``world`` the prefix must hold a single
+    complete set; several are ambiguous and raise ValueError."""
+    sets = shard_sets(prefix, fmt)
+    if world is not None:
+        by = sets.get(int(world), {})
+        if not _complete(by, int(world)):
+            raise FileNotFoundError(f"no complete {world}-shard checkpoint for prefix {prefix}")
+        chosen = int(world)
+    else:
+        complete = [w for w, by in sets.items() if _complete(by, w)]
+        if not complete:
+            raise FileNotFoundError(f"no complete checkpoint shard set for prefix {prefix}")
+        if len(complete) > 1:
+            raise ValueError(f"checkpoint prefix {prefix} holds complete shard sets of world "
+                             f"sizes {sorted(complete)}; pass world= to choose one")
+        chosen = complete[0]
+    files = []
+    for r in range(chosen):
+        paths = sets[chosen][r]
+        if len(paths) > 1:
+            raise ValueError(f"shard {r} of {prefix} exists as {paths}; pass fmt= to choose")
+        files.append(paths[0])
+    return files
+
+
+def load_sharded(table, prefix: str, owner_fn=None, world: Optional[int] = None,
+                 fmt: Optional[str] = None) -> int:
+    """Load the shard set of `prefix` (``select_shards``), keeping keys for
+    which ``owner_fn(keys) -> bool mask`` is true (re-sharding on resume)."""
+    n = 0
+    for f in select_shards(prefix, world, fmt):
+        n += (load_binary if f.endswith(".bin") else load_text)(table, f, key_filter=owner_fn)
+    return n
+
+
+def latest_checkpoint(root: str, stem: str = "param-") -> Optional[tuple[str, int, int]]:
+    """Newest COMPLETE periodic backup under `root`: ``(prefix, round,
+    world)`` of the highest ``<stem><round>`` with a shard set
+    ``.shard<r>-of-<W>`` present for every r < W.  A job that died while
+    writing a backup leaves an incomplete set, which is skipped; shard files
+    are renamed into place only once fully written (save_text /
+    save_binary).  When one round holds complete sets of several world sizes
+    (a re-run at another size), the most recently written wins.  None if
+    there is none."""
+    best = None
+    for f in glob.glob(os.path.join(root, glob.escape(stem) + "*.shard*-of-*.*")):
+        m = _shard_re().match(os.path.basename(f))
+        if not m or not m.group(1).startswith(stem):
+            continue
+        rnd_s = m.group(1)[len(stem):]
+        if not rnd_s.isdigit():
+            continue
+        prefix = os.path.join(root, m.group(1))
+        for w, by in shard_sets(prefix).items():
+            if not _complete(by, w):
+                continue
+            mtime = max(os.path.getmtime(p) for ps in by.values() for p in ps)
+            cand = (int(rnd_s), mtime, prefix, w)
+            if best is None or cand[:2] > best[:2]:
+                best = cand
+    if best is None:
         return None
-    rnd, prefix = max(done)
-    return prefix, rnd
+    return best[2], best[0], best[3]
 
 
 def owner_filter(frag_rank_map: np.ndarray, rank: int):
@@ -273,4 +347,5 @@ def owner_filter(frag_rank_map: np.ndarray, rank: int):
 
 
 __all__ = ["save_text", "load_text", "read_text", "iter_text", "save_binary", "load_binary",
-           "read_binary", "iter_binary", "latest_checkpoint", "save_sharded", "load_sharded", "shard_path", "owner_filter", "io"]
+           "read_binary", "iter_binary", "latest_checkpoint", "save_sharded", "load_sharded",
+           "select_shards", "shard_sets", "shard_path", "owner_filter", "io"]

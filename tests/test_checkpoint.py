@@ -126,3 +126,55 @@ def test_binary_save_detects_size_mismatch(tmp_path):
     with pytest.raises(RuntimeError):
         ck.save_binary(Lying(t, 50), str(tmp_path / "x.bin"))
     assert not (tmp_path / "x.bin").exists() and not (tmp_path / "x.bin.tmp").exists()
+
+
+class _CrashingTable:
+    """Export yields one chunk, then the 'process dies' mid-dump."""
+
+    def __init__(self, t):
+        self.t, self.dim, self.width = t, t.dim, t.width
+
+    def export(self):
+        for i, kr in enumerate(self.t.export()):
+            yield kr
+            raise KeyboardInterrupt("crash while dumping")
+
+
+def test_text_save_is_atomic_and_crash_leaves_no_shard(tmp_path):
+    """a crash during a text backup must not leave a truncated
+    shard under its final name for resume_from=latest to pick up."""
+    t = _table(dim=2)
+    root = tmp_path
+    for r in range(2):  # round 5: a complete text set
+        ck.save_sharded(t, str(root / "param-5"), r, 2, fmt="text")
+    ck.save_sharded(t, str(root / "param-9"), 0, 2, fmt="text")
+    with pytest.raises(KeyboardInterrupt):
+        ck.save_text(_CrashingTable(t), ck.shard_path(str(root / "param-9"), 1, 2, "text"))
+    assert not (root / "param-9.shard1-of-2.txt").exists()
+    assert not list(root.glob("*.tmp"))
+    assert ck.latest_checkpoint(str(root)) == (str(root / "param-5"), 5, 2)
+
+
+def test_load_sharded_uses_one_set_only(tmp_path):
+    """stale shards of another world size (or format) next to the
+    chosen set are never loaded into the table."""
+    new, old = _table(dim=2, seed=1), _table(dim=2, seed=2)
+    prefix = str(tmp_path / "param-7")
+    ck.save_sharded(new, prefix, 0, 1, fmt="bin")          # the newer 1-server set
+    for r in range(2):                                      # a stale 2-server set
+        ck.save_sharded(old, prefix, r, 2, fmt="text")
+    with pytest.raises(ValueError, match="world sizes"):
+        ck.select_shards(prefix)
+    t = HostTable(2, 2, Optimizer("adagrad", lr=0.1))
+    ck.load_sharded(t, prefix, world=1)
+    a, b = new.to_dict(True), t.to_dict(True)
+    assert a.keys() == b.keys()
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+    with pytest.raises(FileNotFoundError):
+        ck.load_sharded(t, prefix, world=3)
+    # both formats of one shard: ambiguous unless fmt is given
+    ck.save_sharded(new, prefix, 0, 1, fmt="text")
+    with pytest.raises(ValueError, match="fmt"):
+        ck.select_shards(prefix, world=1)
+    assert ck.select_shards(prefix, world=1, fmt="bin") == [ck.shard_path(prefix, 0, 1, "bin")]

@@ -133,3 +133,32 @@ def test_engine_world1_cpu_push_keys_and_pull_dense():
     eng.push_keys(k, torch.ones(6, 2))
     v = eng.pull_dense(k).numpy()[:, 0]
     np.testing.assert_allclose(v, [-3, -2, -3, -1, -2, -3])
+
+
+def test_effective_ndest_counts_receiving_servers():
+    """Bucketed dedup sizing: buckets per destination come from
+    the servers that actually receive keys, not the world size."""
+    from swiftsnails_amd.ops.dedup import effective_ndest
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    assert effective_ndest(HashFrag(8, 1024).rank_map(), 8) == 8
+    assert effective_ndest(HashFrag(1, 1024).rank_map([2]), 4) == 1
+    assert effective_ndest(HashFrag(3, 1024).rank_map([0, 1, 2]), 6) == 3  # 342/341/341
+    assert effective_ndest(HashFrag(3, 4).rank_map(), 3) == 2  # one node owns half
+    assert effective_ndest(np.zeros(1, np.int32), 4) == 1
+
+
+def test_rounds_done_under_graph_replays():
+    """A replay of a depth-step graph applies all its rounds at the period's
+    first step: backups are labelled with what the device has applied."""
+    from swiftsnails_amd.models.base import PipelinedWorker
+
+    w = PipelinedWorker.__new__(PipelinedWorker)
+    w._graphs, w.step_idx = None, 7
+    assert w.rounds_done() == 7
+    w._graphs, w._gbase, w._gper = [object()], 10, 4
+    got = []
+    for k in range(10, 19):
+        w.step_idx = k
+        got.append(w.rounds_done())
+    assert got == [10, 14, 14, 14, 14, 18, 18, 18, 18]

@@ -138,6 +138,47 @@ def test_table_full_raises(dev):
         t.check()
 
 
+@pytest.mark.parametrize("servers", [[0], [0, 2]])
+def test_bucket_dedup_split_roles_unique_heavy(dev, servers):
+    """split roles (1 or 2 servers in 4 ranks) with all-unique
+    keys.  Buckets were sized for 4 destinations, so each receiving
+    destination's buckets got 4x (2x) the occurrences and overflowed the
+    4096-slot LDS table, dropping keys silently; now sized by the effective
+    destination count, no overflow and every key gets its id."""
+    from swiftsnails_amd.ops.dedup import Deduper
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    n, nranks = 1 << 21, 4
+    fm = HashFrag(len(servers), 1024).rank_map(servers)
+    d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), device=dev,
+                mode="bucket")
+    assert d.ndest == len(servers)
+    k = np.random.default_rng(5).permutation(np.arange(1, n + 1, dtype=np.int64) * 7919)
+    r = d(torch.from_numpy(k).to(dev))
+    torch.cuda.synchronize()
+    d.check()  # raises DedupOverflowError on an overflowed bucket
+    uc = r.ucount.cpu().numpy()
+    assert int(uc.sum()) == n and all(uc[q] == 0 for q in range(nranks) if q not in servers)
+    inv = r.inv.cpu().numpy().view(np.uint32).astype(np.int64)
+    np.testing.assert_array_equal(r.ukeys.cpu().numpy()[inv], k)
+
+
+def test_dedup_overflow_is_raised_by_engine_check(dev):
+    """The sticky overflow word reaches PSEngine.check (end of bench,
+    backups, finish) instead of being dropped silently."""
+    from swiftsnails_amd.ops.dedup import DedupOverflowError
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    t = HbmTable(1, 1 << 16, optimizer=Optimizer("sgd"), device=dev)
+    eng = PSEngine(t, None, max_keys=1 << 12, dim=1, device=dev)
+    eng.check()
+    eng.dedupers[1].scratch[0] = 1  # what k_bd_dedup sets on a full LDS table
+    with pytest.raises(DedupOverflowError):
+        eng.check()
+
+
 @pytest.mark.parametrize("mode", ["bucket", "hash"])
 @pytest.mark.parametrize("nranks,n,frags", [(1, 20000, 97), (3, 20000, 97), (8, 20000, 97),
                                             (8, 20000, 128), (1, 400000, 97),
@@ -293,7 +334,7 @@ def test_bucket_dedup_occurrence_space_ids(dev, nranks):
     assert len(set(ids.values())) == len(ids)
     assert int(r.ucount.sum()) == len(np.unique(keys[ok]))
     # unplace: compact unique id ubase[b]+l -> occurrence-space id bstart[b]+l
-    P, o_bs, o_un, o_ub = h.bd_offsets(n, nranks)
+    P, o_bs, o_un, o_ub = h.bd_offsets(n, nranks, d.ndest)
     sc = d.scratch.cpu().numpy().view(np.uint32).astype(np.int64)
     bstart, unum, ubase = sc[o_bs:o_bs + P + 1], sc[o_un:o_un + P], sc[o_ub:o_ub + P]
     U = nranks * d.ucap

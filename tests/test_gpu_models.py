@@ -140,13 +140,14 @@ def test_fm_bucket_reduce_matches_atomic_path(dev, dim, nranks):
     h.fm_fwd_g(0, d.index_ptrs(n), y.data_ptr(), B, F, dim,
                uvals.data_ptr(), gs.data_ptr(), gss.data_ptr(), l_b.data_ptr(), 0, st)
     h.bd_reduce_fm(n, nranks, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
-                   gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_b.data_ptr(), st)
+                   gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_b.data_ptr(), st,
+                   ndest=d.ndest)
     # the sorted-list form (default with an overflow list)
     ovf = torch.zeros(h.bd_fm_ovf_words(n), dtype=torch.int32, device=dev)
     g_s = torch.full((U, dim), float("nan"), device=dev)
     h.bd_reduce_fm(n, nranks, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
                    gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_s.data_ptr(), st,
-                   ovf.data_ptr())
+                   ovf.data_ptr(), ndest=d.ndest)
     torch.cuda.synchronize()
     uc = r.ucount.cpu().numpy()
     for q in range(nranks):
@@ -189,7 +190,7 @@ def test_fm_sorted_reduce_overflow_buckets(dev, dim):
     g_s = torch.full((U, dim), float("nan"), device=dev)
     h.bd_reduce_fm(n, 1, d.scratch.data_ptr(), d.pj.data_ptr(), d.luid.data_ptr(),
                    gs.data_ptr(), gss.data_ptr(), F, dim, uvals.data_ptr(), g_s.data_ptr(), st,
-                   ovf.data_ptr())
+                   ovf.data_ptr(), ndest=d.ndest)
     torch.cuda.synchronize()
     assert int(ovf[0]) >= 1  # the hot key's bucket overflowed
     u = int(r.ucount[0])
