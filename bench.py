@@ -111,10 +111,8 @@ def main(argv=None):
         if general == "rccl":
             # the N>1 engine path on one GPU through three real (size-1) RCCL
             # communicators: the multi-GPU call sequence, minus the peers
-            from swiftsnails_amd._native import hip
-
             transport, ctrans, ptrans = (
-                RcclTransport(0, 1, dev, uid=hip().RcclComm.unique_id()) for _ in range(3))
+                RcclTransport(0, 1, dev, uid=RcclTransport.new_unique_id()) for _ in range(3))
         elif general != "0":
             # the N>1 engine path on one GPU: one loopback per stream, as the
             # three RCCL communicators of a multi-GPU run

@@ -17,6 +17,9 @@ All transports speak in *rows*: a buffer is a flat tensor of rows of
 """
 from __future__ import annotations
 
+import contextlib
+import os
+import sys
 from abc import ABC, abstractmethod
 from typing import Optional, Sequence
 
@@ -155,6 +158,26 @@ class TorchDistTransport(Transport):
         dist.barrier(group=self.group)
 
 
+@contextlib.contextmanager
+def _stdout_to_stderr():
+    """Point fd 1 at fd 2 for the duration (native code writing to stdout).
+    C stdio buffers are flushed before fd 1 is restored, so buffered native
+    output lands on stderr too."""
+    import ctypes
+
+    libc = ctypes.CDLL(None)
+    sys.stdout.flush()
+    saved = os.dup(1)
+    try:
+        os.dup2(2, 1)
+        yield
+    finally:
+        libc.fflush(None)
+        sys.stdout.flush()
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 class RcclTransport(Transport):
     """Native RCCL communicator on a dedicated (or the current) HIP stream."""
 
@@ -171,14 +194,26 @@ class RcclTransport(Transport):
                 raise ValueError("RcclTransport needs a store (or an explicit unique id)")
             key = f"{prefix}_uid"
             if rank == 0:
-                uid = h.RcclComm.unique_id()
+                uid = self.new_unique_id()
                 store.set(key, uid)
             else:
                 store.wait([key])
                 uid = store.get(key)
-        self.comm = h.RcclComm(rank, world, uid, self.device.index or 0)
+        # RCCL prints a version banner on fd 1 when it initialises: route it
+        # to stderr so a job's stdout stays the caller's (bench.py's one JSON
+        # line)
+        with _stdout_to_stderr():
+            self.comm = h.RcclComm(rank, world, uid, self.device.index or 0)
         self._pin = torch.empty(2 * world, dtype=torch.int64, pin_memory=True)
         self._cnt_recv = torch.empty(world, dtype=torch.int64, device=self.device)
+
+    @staticmethod
+    def new_unique_id() -> bytes:
+        """A fresh ncclUniqueId (RCCL's init banner goes to stderr)."""
+        from .._native import hip
+
+        with _stdout_to_stderr():
+            return hip().RcclComm.unique_id()
 
     @staticmethod
     def _st():
