@@ -154,8 +154,11 @@ class PSEngine:
         # of the device's memory (wide rows at large N)
         if depth is None and os.environ.get("SS_ENGINE_DEPTH") is None:
             depth = 4
+            # (HIP's total memory: torch's device-property query can read a
+            # device count of 0 off the main thread, where the in-process
+            # rehearsal builds its engines)
             if self.gpu and 4 * self.slot_bytes(self.world, max_keys, dim) > \
-                    torch.cuda.get_device_properties(self.device).total_memory // 8:
+                    torch.cuda.mem_get_info(self.device)[1] // 8:
                 depth = 3
         self.depth = max(1, int(depth if depth is not None else
                                 os.environ.get("SS_ENGINE_DEPTH", "4")))
