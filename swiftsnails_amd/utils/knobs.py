@@ -105,6 +105,9 @@ KNOBS: dict[str, Knob] = {
                           "(neutral: 0.971 vs 0.975 ms/step, three A/B pairs)"),
     "SS_ROUTE_PRIORITY": Knob("0", "parallel/engine.py", "experiment",
                               "high-priority route stream (no gain)"),
+    "SS_ROUTE_FIRST": Knob("0", "models/base.py", "experiment",
+                           "pull-ahead step: route round i+2 before waiting for round i+1's "
+                           "counts (1.18 vs 1.16 ms/step, N>1 path on one GPU)"),
     "SS_GRAPH_STEPS": Knob("depth", "models/base.py", "experiment",
                            "1: one hipGraph per step instead of per ring period"),
     # -- debug
