@@ -463,6 +463,35 @@ __global__ __launch_bounds__(256) void k_bd_inv(BdIndex ix, long long n,
   if (j < n) inv[j] = ix.uid(j);
 }
 
+// occurrence-position parameters for scalar rows: occ[p] = uvals[uid] of the
+// occurrence at bucket position p (0 where it has no unique id).  One
+// workgroup per bucket; luid and occ are streamed, the bucket's unique rows
+// are one contiguous ~4 KB range (L2 hits).  The LR forward then reads one
+// random word per occurrence, occ[pos_of[j]], instead of the dependent pair
+// luid[pos_of[j]] -> uvals[ubase + luid].
+__global__ __launch_bounds__(256) void k_bd_fill_occ(const uint32_t* __restrict__ bstart,
+                                                     const uint32_t* __restrict__ ubase,
+                                                     const uint32_t* __restrict__ luid,
+                                                     const float* __restrict__ uvals,
+                                                     float* __restrict__ occ, int osi) {
+  const int b = blockIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+  const uint32_t base = osi ? p0 : ubase[b];
+  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * 256) {
+    uint32_t l[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t p = pb + r * 256;
+      l[r] = p < p1 ? luid[p] : kBdInvalid;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t p = pb + r * 256;
+      if (p < p1) occ[p] = l[r] == kBdInvalid ? 0.f : uvals[base + l[r]];
+    }
+  }
+}
+
 // K7 for scalar rows (sparse LR): one workgroup per bucket sums the gradients
 // of its unique keys in LDS — per-occurrence g = gs[j / F] * x[j] gathered
 // from the per-sample gradient (L2-resident) — and stores each row once:
@@ -886,6 +915,15 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, n, inv);
     check_launch("k_bd_inv");
   }
+}
+
+void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,
+                        const float* uvals, float* occ, int osi, hipStream_t st, int ndest) {
+  if (n <= 0) return;
+  const BdLayout L = bd_layout(n, nranks, ndest);
+  hipLaunchKernelGGL(k_bd_fill_occ, dim3(L.P), dim3(256), 0, st, scratch + L.bstart,
+                     scratch + L.ubase, luid, uvals, occ, osi);
+  check_launch("k_bd_fill_occ");
 }
 
 void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,

@@ -272,13 +272,19 @@ PYBIND11_MODULE(_ss_hip, m) {
   // ix = (pos_of, luid, bkt, ubase) pointers of a bucketed dedup, or () with inv
   m.def("lr_fwd_g", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
                        uintptr_t uvals, uintptr_t g, int per_sample, uintptr_t loss,
-                       uintptr_t pred, uintptr_t st, std::vector<uintptr_t> ix) {
+                       uintptr_t pred, uintptr_t st, std::vector<uintptr_t> ix, uintptr_t occ) {
     launch_lr_fwd_g(P<const uint32_t>(inv), make_bdindex(ix), P<const float>(xval),
                     P<const float>(labels), B, F, P<const float>(uvals), P<float>(g), per_sample,
-                    P<float>(loss), P<float>(pred), S(st));
+                    P<float>(loss), P<float>(pred), S(st), P<const float>(occ));
   }, py::arg("inv"), py::arg("xval"), py::arg("labels"), py::arg("B"), py::arg("F"),
      py::arg("uvals"), py::arg("g"), py::arg("per_sample"), py::arg("loss"), py::arg("pred"),
-     py::arg("st"), py::arg("ix") = std::vector<uintptr_t>{});
+     py::arg("st"), py::arg("ix") = std::vector<uintptr_t>{}, py::arg("occ") = 0);
+  m.def("bd_fill_occ", [](long long n, int nranks, uintptr_t scratch, uintptr_t luid,
+                          uintptr_t uvals, uintptr_t occ, int osi, uintptr_t st, int ndest) {
+    launch_bd_fill_occ(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(luid),
+                       P<const float>(uvals), P<float>(occ), osi, S(st), ndest);
+  }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("luid"), py::arg("uvals"),
+     py::arg("occ"), py::arg("osi"), py::arg("st"), py::arg("ndest") = 0);
   m.def("fm_fwd_g", [](uintptr_t inv, std::vector<uintptr_t> ix, uintptr_t labels, int B,
                        int F, int dim, uintptr_t uvals, uintptr_t gs, uintptr_t gss,
                        uintptr_t loss, uintptr_t pred, uintptr_t st) {

@@ -201,7 +201,21 @@ __global__ __launch_bounds__(1024) void k_sr_reduce(const uint2* __restrict__ pl
 // ---- LR forward: per-sample dot/sigmoid/logloss; the gradient is written
 // either per occurrence (g*x COALESCED to g[j], the bin-plan reduce gathers
 // it) or per sample (g[s] = p - y, 4 B per sample; the bucketed reduce of
-// bdedup.hip gathers it L2-resident and multiplies by x itself)
+// bdedup.hip gathers it L2-resident and multiplies by x itself).
+// Parameter of occurrence j: uvals[inv[j]], uvals[ix.uid(j)] (two dependent
+// gathers: luid, then the row), or — `occ`, filled per bucket by
+// k_bd_fill_occ — occ[ix.pos_of[j]]: one gather per occurrence
+__device__ __forceinline__ float lr_param(long long j, const uint32_t* __restrict__ inv,
+                                          const BdIndex& ix, const float* __restrict__ occ,
+                                          const float* __restrict__ uvals) {
+  if (occ) {
+    const uint32_t p = ix.pos_of[j];
+    return p == kInvS ? 0.f : occ[p];
+  }
+  const uint32_t u = inv ? inv[j] : ix.uid(j);  // bucketed dedup: no materialised inverse
+  return u == kInvS ? 0.f : uvals[u];
+}
+
 __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict__ inv,
                                                   BdIndex ix,
                                                   const float* __restrict__ xval,
@@ -209,7 +223,8 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict
                                                   const float* __restrict__ uvals,
                                                   float* __restrict__ gocc, int per_sample,
                                                   float* __restrict__ loss_sum,
-                                                  float* __restrict__ pred) {
+                                                  float* __restrict__ pred,
+                                                  const float* __restrict__ occ) {
   __shared__ float sval[256];
   __shared__ float sdot[256];
   __shared__ float sg[256];
@@ -219,12 +234,10 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict
   const long long s0 = (long long)blockIdx.x * spb;
   const bool active = ls < spb && s0 + ls < B;
   const long long j = s0 * F + t;
-  uint32_t u = kInvS;
   float x = 0.f, wx = 0.f;
   if (active) {
-    u = inv ? inv[j] : ix.uid(j);  // bucketed dedup: no materialised inverse index
     x = xval ? xval[j] : 1.f;
-    if (u != kInvS) wx = uvals[u] * x;
+    wx = lr_param(j, inv, ix, occ, uvals) * x;
   }
   packed_sample_sums(wx, F, spb, sval, sdot);  // per-sample dots, no LDS atomics
   float l = 0.f;
@@ -252,18 +265,17 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ i
                                                   int L, const float* __restrict__ uvals,
                                                   float* __restrict__ gocc, int per_sample,
                                                   float* __restrict__ loss_sum,
-                                                  float* __restrict__ pred) {
+                                                  float* __restrict__ pred,
+                                                  const float* __restrict__ occ) {
   __shared__ float sloss[4];
   const int t = threadIdx.x, f = t & (L - 1);
   const long long s = (long long)blockIdx.x * (256 / L) + t / L;
   const bool active = f < F && s < B;
   const long long j = s * F + f;
-  uint32_t u = kInvS;
   float x = 0.f, v = 0.f;
   if (active) {
-    u = inv ? inv[j] : ix.uid(j);  // bucketed dedup: no materialised inverse index
     x = xval ? xval[j] : 1.f;
-    if (u != kInvS) v = uvals[u] * x;
+    v = lr_param(j, inv, ix, occ, uvals) * x;
   }
   const float z = group_sum(v, L);
   float l = 0.f, g = 0.f;
@@ -333,9 +345,10 @@ void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
 
 void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
                      const float* labels, int B, int F, const float* uvals, float* gocc,
-                     int per_sample, float* loss_sum, float* pred, hipStream_t st) {
-  if (!inv && !(ix.pos_of && ix.luid && ix.bkt && ix.ubase))
-    throw_error("lr_fwd_g: need inv or a complete BdIndex");
+                     int per_sample, float* loss_sum, float* pred, hipStream_t st,
+                     const float* occ) {
+  if (occ ? !ix.pos_of : (!inv && !(ix.pos_of && ix.luid && ix.bkt && ix.ubase)))
+    throw_error("lr_fwd_g: need inv, a complete BdIndex, or occ with pos_of");
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("lr_fwd_g: F must be in [1,256]");
   // layout: one sample per lane group unless that leaves over a quarter of
@@ -351,13 +364,13 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
   if (F <= kGroupMaxF && !packed) {
     const int L = group_lanes(F), spb = 256 / L;
     hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, ix, xval,
-                       labels, B, F, L, uvals, gocc, per_sample, loss_sum, pred);
+                       labels, B, F, L, uvals, gocc, per_sample, loss_sum, pred, occ);
     check_launch("k_lr_fwd_g");
     return;
   }
   const int spb = F >= 256 ? 1 : 256 / F;
   hipLaunchKernelGGL(k_lr_fwd_g_lds, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, ix, xval,
-                     labels, B, F, uvals, gocc, per_sample, loss_sum, pred);
+                     labels, B, F, uvals, gocc, per_sample, loss_sum, pred, occ);
   check_launch("k_lr_fwd_g_lds");
 }
 

@@ -105,7 +105,8 @@ void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
                       const uint32_t* nitems, long long n, const unsigned long long* ucount,
                       int nranks, long long ucap, float* ugrad, hipStream_t st);
 void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval, const float* labels, int B, int F, const float* uvals,
-                     float* g, int per_sample, float* loss_sum, float* pred, hipStream_t st);
+                     float* g, int per_sample, float* loss_sum, float* pred, hipStream_t st,
+                     const float* occ = nullptr);
 
 // --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
 // ndest: destinations that receive keys (effective server count, <= nranks;
@@ -127,6 +128,10 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       const uint8_t* usingle = nullptr, const DevTable* t = nullptr,
                       const long long* slots = nullptr, const float* snap = nullptr,
                       const OptParams* op = nullptr, int ndest = 0);
+// occ[p] = uvals[uid of occurrence position p] (scalar rows; 0 where none):
+// one workgroup per dedup bucket, for the LR forward's one-gather mode
+void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,
+                        const float* uvals, float* occ, int osi, hipStream_t st, int ndest);
 void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,
                        float* dst, int dim, hipStream_t st, int ndest = 0);
 

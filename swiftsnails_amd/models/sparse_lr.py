@@ -105,6 +105,15 @@ class SparseLRWorker(PipelinedWorker):
         self._data_ahead = os.environ.get("SS_DATA_AHEAD", "0") != "0"
         self._data_stream = None
         self._ahead = {}
+        # SS_LR_OCC=1 (bucketed, no materialised inverse): parameters are
+        # filled per dedup bucket into occurrence-position order
+        # (k_bd_fill_occ) and the forward reads one word per occurrence,
+        # occ[pos_of[j]], instead of the dependent gathers luid[pos_of[j]] ->
+        # uvals[ubase + luid]; the scatter then skips the bucket-of-occurrence
+        # array
+        self.use_occ = (self.bucketed and not self.use_inv and
+                        os.environ.get("SS_LR_OCC", "1") != "0")
+        self.occ = torch.empty(n, dtype=torch.float32, device=dev) if self.use_occ else None
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False        # the LDS reduce stores every unique row
@@ -119,6 +128,10 @@ class SparseLRWorker(PipelinedWorker):
             # itself and the forward reads it coalesced instead of gathering
             # luid[pos_of[j]]
             self.osi = engine.enable_osi()
+            if self.osi:
+                self.use_occ, self.occ = False, None
+            for dd in engine.dedupers:
+                dd.need_bkt = not self.use_occ
         elif grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
@@ -191,6 +204,12 @@ class SparseLRWorker(PipelinedWorker):
                 h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
                            d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
                            self.loss_sum.data_ptr(), 0, st)
+            elif self.use_occ:
+                o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
+                h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
+                           rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
+                           self.loss_sum.data_ptr(), 0, st, o.index_ptrs(dd.n),
+                           occ=self.occ.data_ptr())
             elif self.bucketed:
                 h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
                            rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,

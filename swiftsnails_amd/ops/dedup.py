@@ -71,6 +71,10 @@ class Deduper:
         # bucket mode: False skips the inverse-index pass; consumers then read
         # luid[pos_of[j]] themselves (the LR forward does, fused)
         self.materialize_inv = True
+        # bucket mode: False skips the scatter's bucket-of-occurrence array
+        # (BdIndex.bkt) when no consumer resolves uid(j) through it (the LR
+        # forward in its one-gather mode reads occ[pos_of[j]] instead)
+        self.need_bkt = True
         # bucket mode: False skips writing the contiguous send segment (ukeys)
         # when nothing reads it (the colocated 1-GPU engine pulls per bucket)
         self.need_ukeys = True
@@ -146,7 +150,8 @@ class Deduper:
             self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
                             self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
                             0 if osi else self.pos_of.data_ptr(),
-                            0 if osi else self.bkt.data_ptr(), self.luid.data_ptr(),
+                            0 if (osi or not self.need_bkt) else self.bkt.data_ptr(),
+                            self.luid.data_ptr(),
                             self.bkeys.data_ptr(), self.ucount.data_ptr(),
                             self.ukeys.data_ptr(), ug, self.gdim,
                             self.inv.data_ptr() if (self.materialize_inv and not osi) else 0,
@@ -190,6 +195,17 @@ class Deduper:
                          _stream_ptr(stream), int(osi),
                          self.usingle.data_ptr() if self.usingle is not None else 0,
                          ndest=self.ndest)
+
+    def fill_occ(self, n: int, uvals: torch.Tensor, occ: torch.Tensor, stream=None,
+                 osi: bool = False):
+        """Scalar rows of the LAST call by occurrence position:
+        ``occ[p] = uvals[uid]`` of the occurrence at bucket position p (0
+        where it has none), so a consumer reads ``occ[pos_of[j]]``."""
+        if self.mode != "bucket":
+            raise RuntimeError("fill_occ needs mode='bucket'")
+        self.h.bd_fill_occ(n, self.nranks, self.scratch.data_ptr(), self.luid.data_ptr(),
+                           uvals.data_ptr(), occ.data_ptr(), int(osi), _stream_ptr(stream),
+                           self.ndest)
 
     def unplace(self, n: int, src: torch.Tensor, dst: torch.Tensor, stream=None):
         """Rows of the LAST call from compact unique ids (``src``, the

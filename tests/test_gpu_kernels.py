@@ -287,8 +287,24 @@ def test_bucket_reduce_lr_matches_atomic_path(dev, nranks, singles):
     gs2 = torch.empty(B, device=dev)
     h.lr_fwd_g(0, 0, y.data_ptr(), B, F, uvals.data_ptr(), gs2.data_ptr(), 1, 0, 0, st,
                d.index_ptrs(n))
+    # ... and through per-bucket occurrence-position parameters (k_bd_fill_occ:
+    # one gather per occurrence); invalid occurrences read 0
+    occ = torch.full((n,), float("nan"), device=dev)
+    d.fill_occ(n, uvals, occ)
+    gs3 = torch.empty(B, device=dev)
+    l_c = torch.zeros(256 * 32, device=dev)
+    h.lr_fwd_g(0, 0, y.data_ptr(), B, F, uvals.data_ptr(), gs3.data_ptr(), 1, l_c.data_ptr(),
+               0, st, d.index_ptrs(n), occ=occ.data_ptr())
     torch.cuda.synchronize()
     assert torch.equal(gs, gs2)
+    assert torch.equal(gs, gs3)
+    np.testing.assert_allclose(l_c.sum().item(), l_b.sum().item(), rtol=1e-6)
+    # occ holds each occurrence's row at its bucket position
+    pos_of = d.pos_of[:n].cpu().numpy().astype(np.int64)
+    inv = r.inv.cpu().numpy().astype(np.int64) & 0xFFFFFFFF
+    ok = inv != 0xFFFFFFFF
+    on = occ.cpu().numpy()
+    np.testing.assert_array_equal(on[pos_of[ok]], uvals.cpu().numpy()[inv[ok]])
     d.check()
     uc = r.ucount.cpu().numpy()
     for q in range(nranks):
