@@ -465,29 +465,36 @@ __global__ __launch_bounds__(256) void k_bd_inv(BdIndex ix, long long n,
 
 // occurrence-position parameters for scalar rows: occ[p] = uvals[uid] of the
 // occurrence at bucket position p (0 where it has no unique id).  One
-// workgroup per bucket; luid and occ are streamed, the bucket's unique rows
-// are one contiguous ~4 KB range (L2 hits).  The LR forward then reads one
+// workgroup per bucket: the bucket's unique rows (one contiguous range of
+// <= 4096 floats) are staged in LDS with coalesced loads, then luid is
+// streamed and occ written in bucket order.  The LR forward then reads one
 // random word per occurrence, occ[pos_of[j]], instead of the dependent pair
 // luid[pos_of[j]] -> uvals[ubase + luid].
-__global__ __launch_bounds__(256) void k_bd_fill_occ(const uint32_t* __restrict__ bstart,
-                                                     const uint32_t* __restrict__ ubase,
-                                                     const uint32_t* __restrict__ luid,
-                                                     const float* __restrict__ uvals,
-                                                     float* __restrict__ occ, int osi) {
+template <int FT>
+__global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__ bstart,
+                                                    const uint32_t* __restrict__ ubase,
+                                                    const uint32_t* __restrict__ unum,
+                                                    const uint32_t* __restrict__ luid,
+                                                    const float* __restrict__ uvals,
+                                                    float* __restrict__ occ, int osi) {
+  __shared__ float sv[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   const uint32_t base = osi ? p0 : ubase[b];
-  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * 256) {
+  const uint32_t nu = min(unum[b], (uint32_t)kBdTS);
+  for (uint32_t l = threadIdx.x; l < nu; l += FT) sv[l] = uvals[base + l];
+  __syncthreads();
+  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * FT) {
     uint32_t l[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t p = pb + r * 256;
+      const uint32_t p = pb + r * FT;
       l[r] = p < p1 ? luid[p] : kBdInvalid;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t p = pb + r * 256;
-      if (p < p1) occ[p] = l[r] == kBdInvalid ? 0.f : uvals[base + l[r]];
+      const uint32_t p = pb + r * FT;
+      if (p < p1) occ[p] = l[r] < nu ? sv[l[r]] : 0.f;
     }
   }
 }
@@ -921,8 +928,8 @@ void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const 
                         const float* uvals, float* occ, int osi, hipStream_t st, int ndest) {
   if (n <= 0) return;
   const BdLayout L = bd_layout(n, nranks, ndest);
-  hipLaunchKernelGGL(k_bd_fill_occ, dim3(L.P), dim3(256), 0, st, scratch + L.bstart,
-                     scratch + L.ubase, luid, uvals, occ, osi);
+  hipLaunchKernelGGL(k_bd_fill_occ<512>, dim3(L.P), dim3(512), 0, st, scratch + L.bstart,
+                     scratch + L.ubase, scratch + L.unum, luid, uvals, occ, osi);
   check_launch("k_bd_fill_occ");
 }
 
