@@ -137,12 +137,69 @@ __device__ __forceinline__ float fresh_or(float v, const InitParams& ip, uint64_
 // Duplicate keys within the launch are safe (CAS claim + fresh_or above).
 // one key of a unique-key pull: probe (insert if new) by the group leader,
 // init the row if it was inserted, emit the row to out[pos]
+// Scalar (w, h) rows in 16-byte [w | h | key] slots (sparse LR): each probe
+// step is ONE 16-byte load that brings the key and the row together, so a
+// found key needs no second (dependent) load of its row.  Returns the slot
+// (-1: table full) and the row as it was read; `*inserted` when this lane
+// claimed an EMPTY slot (the row then is the prefilled / initial row).
+__device__ __forceinline__ long long probe_slot16(const DevTable& t, uint64_t key, float2* wh,
+                                                  bool* inserted) {
+  uint64_t s = fastrange64(table_hash(key), t.cap);
+  for (uint64_t n = 0; n < t.cap; ++n) {
+    const uint4 v = *reinterpret_cast<const uint4*>(t.base + s * 16);
+    const uint64_t k = ((uint64_t)v.w << 32) | v.z;
+    if (k == key) {
+      *wh = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+      return (long long)s;
+    }
+    if (k == kEmptyKey) {
+      uint64_t* kp = slot_key(t, s);
+      const unsigned long long prev =
+          atomicCAS(reinterpret_cast<unsigned long long*>(kp), kEmptyKey, key);
+      if (prev == kEmptyKey) {
+        *inserted = true;
+        return (long long)s;
+      }
+      if (prev == key) {  // a duplicate of this key claimed it in this launch
+        *wh = *reinterpret_cast<const float2*>(slot_row(t, s));
+        return (long long)s;
+      }
+    }
+    s = (s + 1 == t.cap) ? 0 : s + 1;
+  }
+  return -1;
+}
+
 template <int G>
 __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long long pos,
                                          long long* __restrict__ slots_out, float* __restrict__ out,
                                          const InitParams& ip, int* err, int lg,
                                          unsigned long long& ins,
-                                         float2* __restrict__ snap = nullptr) {
+                                         float2* __restrict__ snap = nullptr, int one16 = 0) {
+  if (G == 1 && snap && one16) {
+    // snapshot mode on 16-byte slots: one load per probe step (probe_slot16)
+    bool b = false;
+    float2 wh = make_float2(0.f, 0.f);
+    const long long slot = key != kEmptyKey ? probe_slot16(t, key, &wh, &b) : -1;
+    if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
+    if (slots_out) slots_out[pos] = slot;
+    float* o = out + pos * (long long)t.dim;
+    if (slot < 0) {
+      o[0] = 0.f;
+      return;
+    }
+    if (b) {
+      wh = make_float2(init_value(ip, key, 0, 1), ip.state_init);
+      if (!t.prefilled) *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
+    } else {
+      wh.x = fresh_or(wh.x, ip, key, 0, 1);
+      if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
+    }
+    o[0] = wh.x;
+    snap[pos] = wh;
+    ins += b;
+    return;
+  }
   long long slot = -1;
   int inserted = 0;
   if (lg == 0) {
@@ -233,7 +290,8 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
                                                         long long* __restrict__ slots_out,
                                                         float* __restrict__ out, InitParams ip,
                                                         unsigned long long* size_ctr, int* err,
-                                                        int osi, float2* __restrict__ snap) {
+                                                        int osi, float2* __restrict__ snap,
+                                                        int one16) {
   const int b = blockIdx.x, lg = threadIdx.x % G;
   // osi: rows at occurrence-space ids bstart[b] + l (bdedup.hip), else at the
   // compact unique ids ubase[b] + l
@@ -243,7 +301,7 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
   // gridDim.y workgroups share a bucket (fewer serial probes per lane)
   for (uint32_t l = blockIdx.y * (256 / G) + threadIdx.x / G; l < nu;
        l += gridDim.y * (256 / G))
-    pull_one<G>(t, src[l], (long long)base + l, slots_out, out, ip, err, lg, ins, snap);
+    pull_one<G>(t, src[l], (long long)base + l, slots_out, out, ip, err, lg, ins, snap, one16);
   ins = wave_sum_u64(ins);
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
@@ -600,9 +658,16 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
     return v < 0 ? 0 : (v > 16 ? 16 : v);
   }();
   const int ny = env_ny ? env_ny : (G == 1 ? 4 : 1);
+  // snapshot pulls on 16-byte [w | h | key] slots probe with one 16-byte
+  // load per step (probe_slot16); SS_PULL_ONELOAD=0: key load, then row load
+  static const bool oneload_env = [] {
+    const char* e = std::getenv("SS_PULL_ONELOAD");
+    return !(e && std::atoi(e) == 0);
+  }();
+  const int one16 = oneload_env && snap && t.stride == 16 && t.key_off == 8 && t.row_off == 0;
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique_bk<kG>, dim3(P, ny), dim3(256), 0, st, t,
                                       bkeys, bstart, unum, ubase, slots, out, ip, size_ctr, err,
-                                      osi, reinterpret_cast<float2*>(snap)));
+                                      osi, reinterpret_cast<float2*>(snap), one16));
   check_launch("k_pull_unique_bk");
 }
 

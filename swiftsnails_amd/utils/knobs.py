@@ -64,6 +64,9 @@ KNOBS: dict[str, Knob] = {
                              "zero-init tables pre-filled with the init row (insert = CAS only)"),
     "SS_PULL_BK_Y": Knob("4 (G=1) / 1", "csrc/hip/table.hip", "tuning",
                          "workgroups per dedup bucket in the bucketed pull"),
+    "SS_PULL_ONELOAD": Knob("1", "csrc/hip/table.hip", "tuning",
+                            "snapshot pull on 16-byte LR slots: one 16-byte load per probe step "
+                            "(key + row) instead of a key load then a row load"),
     "SS_APPLY_VEC": Knob("1", "csrc/hip/table.hip", "tuning",
                          "one lane group per key + 8-byte (w, h) accesses in k_apply"),
     "SS_BD_NCH": Knob("512", "csrc/hip/bdedup.hip", "tuning", "max count/scatter chunks"),
