@@ -131,13 +131,14 @@ class ThreadPool : NonCopyable {
     std::atomic<int> left{n};
     std::mutex mu;
     std::condition_variable cv;
+    // the count drops under the mutex: the waiter can only see it reach 0
+    // after the last task released the lock, so it never destroys `mu`/`cv`
+    // (this frame) while a task still uses them
     for (int i = 0; i < n; ++i)
       submit([&, i] {
         task(i);
-        if (left.fetch_sub(1) == 1) {
-          std::lock_guard<std::mutex> lk(mu);
-          cv.notify_all();
-        }
+        std::lock_guard<std::mutex> lk(mu);
+        if (left.fetch_sub(1) == 1) cv.notify_all();
       });
     std::unique_lock<std::mutex> lk(mu);
     cv.wait(lk, [&] { return left.load() == 0; });
