@@ -231,6 +231,15 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
 
   // ---- models
+  m.def("csr_batch", [](uintptr_t offs, uintptr_t keys, uintptr_t vals, uintptr_t labels,
+                        long long rows, long long cursor, int B, int F, uintptr_t step_dev,
+                        long long step_add, uintptr_t out_keys, uintptr_t out_vals,
+                        uintptr_t out_labels, uintptr_t st) {
+    launch_csr_batch(P<const uint64_t>(offs), P<const uint64_t>(keys), P<const float>(vals),
+                     P<const float>(labels), rows, cursor, B, F, P<const long long>(step_dev),
+                     step_add, P<uint64_t>(out_keys), P<float>(out_vals), P<float>(out_labels),
+                     S(st));
+  });
   m.def("gen_ctr", [](uint64_t seed, long long sample_base, int B, int F, long long V,
                       float tail_frac, float truth_scale, float truth_bias, uintptr_t keys,
                       uintptr_t labels, uintptr_t st, uintptr_t step_dev, long long step_mul,

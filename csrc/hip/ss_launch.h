@@ -78,6 +78,11 @@ void launch_scatter_add_rows(const float* src, const uint32_t* idx, long long n,
                              float* out, hipStream_t st);
 
 // --- models.hip
+// --- data.hip: batch B x F cut out of an HBM-resident CSR dataset
+void launch_csr_batch(const uint64_t* offs, const uint64_t* keys, const float* vals,
+                      const float* labels, long long rows, long long cursor, int B, int F,
+                      const long long* step_dev, long long step_add, uint64_t* out_keys,
+                      float* out_vals, float* out_labels, hipStream_t st);
 void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long long vocab_per_field,
                     float tail_frac, float truth_scale, float truth_bias, uint64_t* keys,
                     float* labels, hipStream_t st, const long long* step_dev = nullptr,

@@ -229,10 +229,15 @@ def build_worker(cfg: Config):
     opt = Optimizer(cfg.get("optimizer", "adagrad"), lr=float(cfg.get("learning_rate", 0.05)),
                     l1=float(cfg.get("l1", 0.0)), l2=float(cfg.get("l2", 0.0)))
     rank = int(os.environ.get("RANK", "0"))
+    dev = None
+    if torch.cuda.is_available():  # the rank's device before data is uploaded to it
+        dev = torch.device("cuda", int(os.environ.get("SS_DEVICE",
+                                                      os.environ.get("LOCAL_RANK", "0"))))
+        torch.cuda.set_device(dev)
     if model in ("sparse_lr", "fm"):
         if cfg.get("data_path", ""):
             from ..utils.dataio import make_ctr_source
-            data = make_ctr_source(cfg, rank, world)
+            data = make_ctr_source(cfg, rank, world, device=dev)
         else:
             data = CtrSynth(batch_size=int(cfg.get("batch_size", 65536)),
                             num_fields=int(cfg.get("num_fields", 39)),

@@ -187,7 +187,7 @@ class SparseLRWorker(PipelinedWorker):
     def _produce(self, step, slot, stream):
         if self.xval is not None:
             self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
-                               stream=stream, xval=self.xval[slot])
+                               stream=stream, xval=self.xval[slot], **self._gen_kwargs(step))
         else:
             self.data.generate(step, self.rank, self.world, self.keys[slot], self.labels[slot],
                                stream=stream, **self._gen_kwargs(step))

@@ -16,6 +16,13 @@ Both sources are drop-in replacements for the synthetic generators
 (``CtrSynth`` / ``W2VSynth``): same attributes the workers read and the same
 ``generate(step, rank, world, ...)`` call.  Rank ``r`` of a ``world``-rank job
 reads its own 1/world of the file (data parallelism).
+
+``FileCtrSource(resident="hbm")`` (the default on a GPU when the shard fits
+in half of the free HBM) uploads the parsed shard (CSR: offsets, keys,
+values, labels) to the GPU once and cuts each step's padded batch out of it
+with one streaming kernel (``csrc/hip/data.hip``): no per-step host fill and
+no per-step PCIe copy (82 MB for a 262144 x 39 batch), and the step becomes
+hipGraph-capturable (the kernel can read its step from device memory).
 """
 from __future__ import annotations
 
@@ -89,7 +96,8 @@ class FileCtrSource:
 
     def __init__(self, path: str, fmt: str = "libsvm", batch_size: int = 65536,
                  num_fields: Optional[int] = None, rank: int = 0, world: int = 1,
-                 nthreads: int = 8, prefetch: int = 3, pin: Optional[bool] = None):
+                 nthreads: int = 8, prefetch: int = 3, pin: Optional[bool] = None,
+                 resident: Optional[str] = None, device=None):
         self.ds = host().SparseDataset(path, fmt, nthreads, rank, world)
         if self.ds.rows == 0:
             raise ValueError(f"{path}: no rows for shard {rank}/{world}")
@@ -97,14 +105,57 @@ class FileCtrSource:
         self.num_fields = int(num_fields or self.ds.max_nnz)
         self.has_values = bool(self.ds.has_values)
         self.nthreads = nthreads
+        # a synthetic-compatible attribute (table sizing when no capacity is set)
+        self.num_features = max(1, self.ds.nnz)
+        self.resident = self._choose_residency(resident, device)
+        self.ring = None
+        if self.resident == "hbm":
+            self._upload(device)
+            return
         n = self.batch_size * self.num_fields
         shapes = {"keys": (n, torch.int64), "labels": (self.batch_size, torch.float32)}
         if self.has_values:
             shapes["vals"] = (n, torch.float32)
         pin = torch.cuda.is_available() if pin is None else pin
         self.ring = _PinnedRing(max(1, prefetch), shapes, pin)
-        # a synthetic-compatible attribute (table sizing when no capacity is set)
-        self.num_features = max(1, self.ds.nnz)
+
+    def device_bytes(self) -> int:
+        """HBM the resident copy of this shard takes."""
+        ds = self.ds
+        return 8 * (ds.rows + 1) + 8 * ds.nnz + 4 * ds.rows + (4 * ds.nnz if self.has_values else 0)
+
+    def _choose_residency(self, resident, device) -> str:
+        if resident not in (None, "auto", "hbm", "host"):
+            raise ValueError(f"data residency {resident!r}: hbm | host | auto")
+        if resident in ("hbm", "host"):
+            if resident == "hbm" and not torch.cuda.is_available():
+                raise RuntimeError("data_resident: hbm needs a GPU")
+            return resident
+        if not torch.cuda.is_available():
+            return "host"
+        dev = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        free = torch.cuda.mem_get_info(dev)[0]
+        return "hbm" if self.device_bytes() <= free // 2 else "host"
+
+    def _upload(self, device):
+        import numpy as np
+
+        dev = torch.device(device) if device is not None else torch.device(
+            "cuda", torch.cuda.current_device())
+        ds = self.ds
+        self.device = dev
+        self.d_offs = torch.from_numpy(np.asarray(ds.offsets()).view(np.int64)).to(dev)
+        self.d_keys = torch.from_numpy(np.asarray(ds.keys()).view(np.int64)).to(dev)
+        self.d_labels = torch.from_numpy(np.asarray(ds.labels())).to(dev)
+        self.d_vals = (torch.from_numpy(np.asarray(ds.vals())).to(dev) if self.has_values
+                       else None)
+        torch.cuda.synchronize(dev)
+
+    @property
+    def graph_capturable(self) -> bool:
+        """Resident batches read their step from device memory in a replay."""
+        return self.resident == "hbm"
 
     @property
     def rows(self) -> int:
@@ -117,7 +168,32 @@ class FileCtrSource:
                      self.nthreads)
 
     def generate(self, step: int, rank: int, world: int, keys: torch.Tensor,
-                 labels: torch.Tensor, stream=None, xval: Optional[torch.Tensor] = None):
+                 labels: torch.Tensor, stream=None, xval: Optional[torch.Tensor] = None,
+                 step_dev: int = 0, step_delta: int = 0):
+        """Batch of ``step`` (rows [step*B, step*B + B) of this rank's shard,
+        wrapping).  Resident: with ``step_dev`` (a device int64 pointer,
+        hipGraph replays) the step is ``*step_dev + step_delta``."""
+        if self.resident == "hbm":
+            from .._native import hip
+
+            st = stream if stream is not None else torch.cuda.current_stream()
+            st = st.cuda_stream if hasattr(st, "cuda_stream") else int(st)
+            B, F = self.batch_size, self.num_fields
+            if keys.numel() < B * F or labels.numel() < B:
+                raise ValueError("generate: output buffers smaller than the batch")
+            for t in (keys, labels, xval):
+                if t is not None and t.device != self.device:
+                    raise ValueError(f"generate: HBM-resident batches are written on "
+                                     f"{self.device}, got a buffer on {t.device}")
+            hip().csr_batch(self.d_offs.data_ptr(), self.d_keys.data_ptr(),
+                            self.d_vals.data_ptr() if self.d_vals is not None else 0,
+                            self.d_labels.data_ptr(), self.ds.rows,
+                            (step * B) % self.ds.rows, B, F, step_dev, step_delta,
+                            keys.data_ptr(), xval.data_ptr() if xval is not None else 0,
+                            labels.data_ptr(), st)
+            return
+        if step_dev:
+            raise RuntimeError("host-resident file batches cannot be replayed from a graph")
         slot, buf = self.ring.take(step, self._fill)
         st = _ext_stream(stream)
         ctx = torch.cuda.stream(st) if st is not None else _null()
@@ -134,7 +210,8 @@ class FileCtrSource:
             torch.cuda.current_stream() if keys.is_cuda else None))
 
     def close(self):
-        self.ring.close()
+        if self.ring is not None:
+            self.ring.close()
 
 
 class FileCorpusSource:
@@ -197,13 +274,15 @@ class _null:
         return False
 
 
-def make_ctr_source(cfg, rank: int = 0, world: int = 1):
-    """Config keys: data_path, data_format (libsvm|ctr), batch_size, num_fields."""
+def make_ctr_source(cfg, rank: int = 0, world: int = 1, device=None):
+    """Config keys: data_path, data_format (libsvm|ctr), batch_size, num_fields,
+    data_resident (auto|hbm|host)."""
     return FileCtrSource(cfg.get("data_path"), cfg.get("data_format", "libsvm"),
                          batch_size=int(cfg.get("batch_size", 65536)),
                          num_fields=int(cfg.get("num_fields", 0) or 0) or None,
                          rank=rank, world=world,
-                         nthreads=int(cfg.get("data_threads", 8)))
+                         nthreads=int(cfg.get("data_threads", 8)),
+                         resident=cfg.get("data_resident", "auto"), device=device)
 
 
 def make_corpus_source(cfg, rank: int = 0, world: int = 1):

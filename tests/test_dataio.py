@@ -104,7 +104,8 @@ def test_file_ctr_source_prefetch_cpu(tmp_path):
     from swiftsnails_amd.utils.dataio import FileCtrSource
     p = str(tmp_path / "a.svm")
     _write_libsvm(p, rows=123, seed=9)
-    src = FileCtrSource(p, "libsvm", batch_size=16, num_fields=5, pin=False, prefetch=3)
+    src = FileCtrSource(p, "libsvm", batch_size=16, num_fields=5, pin=False, prefetch=3,
+                        resident="host")
     ds = _host().SparseDataset(p, "libsvm", 1, 0, 1)
     keys = torch.empty(16 * 5, dtype=torch.int64)
     labels = torch.empty(16)
@@ -167,7 +168,8 @@ def test_corpus_hashes_words_and_min_count(tmp_path):
 
 
 @pytest.mark.gpu
-def test_sparse_lr_trains_from_libsvm_file(tmp_path):
+@pytest.mark.parametrize("resident", ["hbm", "host"])
+def test_sparse_lr_trains_from_libsvm_file(tmp_path, resident):
     from swiftsnails_amd.models.sparse_lr import SparseLRWorker, make_lr_table
     from swiftsnails_amd.parallel.engine import PSEngine
     from swiftsnails_amd.parallel.transport import LoopbackTransport
@@ -183,7 +185,8 @@ def test_sparse_lr_trains_from_libsvm_file(tmp_path):
             y = int(rng.random() < 1 / (1 + np.exp(-z)))
             f.write(f"{y} " + " ".join(f"{i}:0.5" for i in idx) + "\n")
     dev = torch.device("cuda", 0)
-    src = FileCtrSource(p, "libsvm", batch_size=1024, num_fields=8)
+    src = FileCtrSource(p, "libsvm", batch_size=1024, num_fields=8, resident=resident)
+    assert src.resident == resident
     assert src.has_values
     table = make_lr_table(10000, device=dev)
     eng = PSEngine(table, LoopbackTransport(), max_keys=1024 * 8, dim=1, device=dev)
@@ -223,3 +226,86 @@ def test_word2vec_trains_from_corpus_file(tmp_path):
     torch.cuda.synchronize()
     assert wk.mean_loss() < first, (first, wk.mean_loss())
     src.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fmt", ["libsvm", "ctr"])
+def test_hbm_resident_batches_match_host_fill(tmp_path, fmt):
+    """data_resident: hbm — the batch cut out of the uploaded CSR shard by
+    k_csr_batch equals SparseDataset.fill (padding, truncation, wrap-around,
+    values), also when the kernel reads its step from device memory (the
+    hipGraph replay form)."""
+    from swiftsnails_amd.utils.dataio import FileCtrSource
+
+    p = str(tmp_path / ("a.svm" if fmt == "libsvm" else "a.tsv"))
+    if fmt == "libsvm":
+        _write_libsvm(p, rows=211, seed=11)
+    else:
+        rng = np.random.default_rng(4)
+        with open(p, "w") as f:
+            for i in range(173):
+                cols = ["" if rng.random() < 0.2 else f"t{int(rng.integers(0, 50))}"
+                        for _ in range(int(rng.integers(1, 7)))]
+                f.write(f"{i % 2}\t" + "\t".join(cols) + "\n")
+    dev = torch.device("cuda", 0)
+    B, F = 64, 5
+    src = FileCtrSource(p, fmt, batch_size=B, num_fields=F, resident="hbm", device=dev)
+    assert src.resident == "hbm" and src.graph_capturable
+    ds = _host().SparseDataset(p, fmt, 1, 0, 1)
+    keys = torch.empty(B * F, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, device=dev)
+    xval = torch.empty(B * F, device=dev)
+    step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+    for step in (0, 1, 3, 7):
+        for mode in ("host_step", "device_step"):
+            if mode == "host_step":
+                src.generate(step, 0, 1, keys, labels, xval=xval)
+            else:
+                step_dev.fill_(step - 2)
+                src.generate(999, 0, 1, keys, labels, xval=xval, step_dev=step_dev.data_ptr(),
+                             step_delta=2)
+            torch.cuda.synchronize()
+            ek = np.empty(B * F, dtype=np.uint64)
+            ev = np.empty(B * F, dtype=np.float32)
+            el = np.empty(B, dtype=np.float32)
+            ds.fill((step * B) % ds.rows, B, F, ek.ctypes.data, ev.ctypes.data, el.ctypes.data, 1)
+            assert keys.cpu().numpy().view(np.uint64).tolist() == ek.tolist(), (step, mode)
+            assert labels.cpu().numpy().tolist() == el.tolist()
+            np.testing.assert_array_equal(xval.cpu().numpy(), ev)
+    src.close()
+
+
+@pytest.mark.gpu
+def test_sparse_lr_file_resident_graph_replay(tmp_path):
+    """A file-fed LR job with the shard in HBM replays its step as hipGraphs
+    and trains exactly like the eager steps."""
+    from swiftsnails_amd.models.sparse_lr import SparseLRWorker, make_lr_table
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.utils.dataio import FileCtrSource
+
+    rng = np.random.default_rng(1)
+    w = rng.standard_normal(3000)
+    p = str(tmp_path / "train.svm")
+    with open(p, "w") as f:
+        for _ in range(9000):
+            idx = rng.choice(3000, 6, replace=False)
+            y = int(rng.random() < 1 / (1 + np.exp(-w[idx].sum() * 0.5)))
+            f.write(f"{y} " + " ".join(str(i) for i in idx) + "\n")
+    dev = torch.device("cuda", 0)
+    losses = {}
+    for graph in (False, True):
+        src = FileCtrSource(p, "libsvm", batch_size=512, num_fields=6, resident="hbm", device=dev)
+        table = make_lr_table(6000, device=dev)
+        eng = PSEngine(table, None, max_keys=512 * 6, dim=1, device=dev)
+        wk = SparseLRWorker(eng, src)
+        out = [float(wk.step().sum().item())]
+        if graph:
+            assert wk.enable_graph()
+        out += [float(wk.step().sum().item()) for _ in range(4 * eng.depth)]
+        torch.cuda.synchronize()
+        table.check()
+        losses[graph] = out
+    per = eng.depth
+    idx = [0] + [k for k in range(1, 1 + 4 * per) if (k - 1) % per == per - 1]
+    np.testing.assert_allclose(np.array(losses[True])[idx], np.array(losses[False])[idx],
+                               rtol=2e-4, atol=1e-3)
