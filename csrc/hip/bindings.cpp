@@ -240,6 +240,16 @@ PYBIND11_MODULE(_ss_hip, m) {
                      step_add, P<uint64_t>(out_keys), P<float>(out_vals), P<float>(out_labels),
                      S(st));
   });
+  m.def("w2v_corpus_batch", [](uintptr_t tokens, uintptr_t sent_offs, uintptr_t sent_of,
+                               uintptr_t table, long long table_size, uintptr_t keep, long long N,
+                               uint64_t seed, long long step, uintptr_t step_dev,
+                               long long step_add, int B, int C, int W, long long nneg,
+                               uint64_t out_bit, uintptr_t keys, uintptr_t st) {
+    launch_w2v_corpus_batch(P<const uint64_t>(tokens), P<const uint64_t>(sent_offs),
+                            P<const uint32_t>(sent_of), P<const uint64_t>(table), table_size,
+                            P<const float>(keep), N, seed, step, P<const long long>(step_dev),
+                            step_add, B, C, W, nneg, out_bit, P<uint64_t>(keys), S(st));
+  });
   m.def("gen_ctr", [](uint64_t seed, long long sample_base, int B, int F, long long V,
                       float tail_frac, float truth_scale, float truth_bias, uintptr_t keys,
                       uintptr_t labels, uintptr_t st, uintptr_t step_dev, long long step_mul,

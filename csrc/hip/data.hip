@@ -45,6 +45,74 @@ __global__ __launch_bounds__(256) void k_csr_batch(const uint64_t* __restrict__ 
   if (f == 0) out_labels[b] = labels[r];
 }
 
+// Skip-gram batch of an HBM-resident corpus, bit-identical to the host
+// sampler Corpus::fill_skipgram (csrc/host/dataio.h): keys[0,B) centers drawn
+// uniformly over the shard's tokens (frequent-word sub-sampling by each
+// token's keep probability, up to 16 draws), keys[B, B+B*C) contexts drawn
+// with replacement from the center's sentence within +-W (a one-word
+// sentence draws from the unigram^0.75 noise table), then nneg shared
+// negatives from the noise table; context / negative keys carry the out bit.
+// One lane per center (its C contexts) and one per negative.
+__global__ __launch_bounds__(256) void k_w2v_corpus_batch(
+    const uint64_t* __restrict__ tokens, const uint64_t* __restrict__ sent_offs,
+    const uint32_t* __restrict__ sent_of, const uint64_t* __restrict__ table,
+    unsigned long long table_mask, const float* __restrict__ keep, unsigned long long N,
+    uint64_t seed, unsigned long long step, const long long* __restrict__ step_dev,
+    long long step_add, int B, int C, int W, long long nneg, uint64_t out_bit,
+    uint64_t* __restrict__ keys) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t st = step_dev ? (uint64_t)(*step_dev + step_add) : (uint64_t)step;
+  if (i < B) {
+    const int b = (int)i;
+    uint64_t r = splitmix64(seed ^ (st * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)b << 20));
+    uint64_t pos = 0;
+    for (int tries = 0; tries < 16; ++tries) {
+      r = splitmix64(r);
+      pos = fastrange64(r, N);
+      if (!keep || u01(splitmix64(r ^ 7)) < keep[pos]) break;
+    }
+    keys[b] = tokens[pos];
+    const uint32_t s = sent_of[pos];
+    const long long sb = (long long)sent_offs[s], se = (long long)sent_offs[s + 1];
+    const long long lo = max(sb, (long long)pos - W), hi = min(se - 1, (long long)pos + W);
+    const long long span = hi - lo;
+    for (int c = 0; c < C; ++c) {
+      r = splitmix64(r + (uint64_t)c);
+      uint64_t x;
+      if (span <= 0) {
+        x = table[r & table_mask];
+      } else {
+        long long q = lo + (long long)fastrange64(r, (uint64_t)span);
+        if (q >= (long long)pos) ++q;
+        x = tokens[q];
+      }
+      keys[(long long)B + (long long)b * C + c] = x | out_bit;
+    }
+  } else if (i < (long long)B + nneg) {
+    const long long q = i - B;
+    const uint64_t r = splitmix64(seed ^ 0xBADC0DEull ^ (st * 0xD1B54A32D192ED03ull) ^
+                                  (uint64_t)q * 0x9E37ull);
+    keys[(long long)B + (long long)B * C + q] = table[r & table_mask] | out_bit;
+  }
+}
+
+void launch_w2v_corpus_batch(const uint64_t* tokens, const uint64_t* sent_offs,
+                             const uint32_t* sent_of, const uint64_t* table, long long table_size,
+                             const float* keep, long long N, uint64_t seed, long long step,
+                             const long long* step_dev, long long step_add, int B, int C, int W,
+                             long long nneg, uint64_t out_bit, uint64_t* keys, hipStream_t st) {
+  if (N <= 0) throw_error("w2v_corpus_batch: empty corpus");
+  if (table_size <= 0 || (table_size & (table_size - 1)) != 0)
+    throw_error("w2v_corpus_batch: noise table size must be a power of two");
+  const long long n = (long long)B + nneg;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(k_w2v_corpus_batch, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     tokens, sent_offs, sent_of, table, (unsigned long long)(table_size - 1), keep,
+                     (unsigned long long)N, seed, (unsigned long long)step, step_dev, step_add, B,
+                     C, W, nneg, out_bit, keys);
+  check_launch("k_w2v_corpus_batch");
+}
+
 void launch_csr_batch(const uint64_t* offs, const uint64_t* keys, const float* vals,
                       const float* labels, long long rows, long long cursor, int B, int F,
                       const long long* step_dev, long long step_add, uint64_t* out_keys,

@@ -83,6 +83,11 @@ void launch_csr_batch(const uint64_t* offs, const uint64_t* keys, const float* v
                       const float* labels, long long rows, long long cursor, int B, int F,
                       const long long* step_dev, long long step_add, uint64_t* out_keys,
                       float* out_vals, float* out_labels, hipStream_t st);
+void launch_w2v_corpus_batch(const uint64_t* tokens, const uint64_t* sent_offs,
+                             const uint32_t* sent_of, const uint64_t* table, long long table_size,
+                             const float* keep, long long N, uint64_t seed, long long step,
+                             const long long* step_dev, long long step_add, int B, int C, int W,
+                             long long nneg, uint64_t out_bit, uint64_t* keys, hipStream_t st);
 void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long long vocab_per_field,
                     float tail_frac, float truth_scale, float truth_bias, uint64_t* keys,
                     float* labels, hipStream_t st, const long long* step_dev = nullptr,

@@ -369,6 +369,24 @@ class Corpus : NonCopyable {
 
   size_t size() const { return tokens_.size(); }
   size_t sentences() const { return sent_offs_.size() - 1; }
+  // the sampler's state, for an HBM-resident copy (csrc/hip/data.hip)
+  const std::vector<uint64_t>& tokens() const { return tokens_; }
+  const std::vector<uint64_t>& sent_offsets() const { return sent_offs_; }
+  const std::vector<uint32_t>& sent_of() const { return sent_of_; }
+  const std::vector<uint64_t>& noise_table() const { return table_; }
+  bool subsampled() const { return !keep_.empty(); }
+  // per-token keep probability of the frequent-word sub-sampling (2 = always
+  // kept, as for words without an entry); empty without sub-sampling
+  std::vector<float> keep_per_token() const {
+    std::vector<float> k;
+    if (keep_.empty()) return k;
+    k.resize(tokens_.size(), 2.f);
+    for (size_t i = 0; i < tokens_.size(); ++i) {
+      auto it = keep_.find(tokens_[i]);
+      if (it != keep_.end()) k[i] = it->second;
+    }
+    return k;
+  }
   size_t vocab_size() const { return vocab_.size(); }
   const std::vector<std::pair<uint64_t, uint64_t>>& vocab() const { return vocab_; }
 

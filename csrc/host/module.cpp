@@ -404,6 +404,23 @@ PYBIND11_MODULE(_ss_host, m) {
       .def_property_readonly("sentences", &Corpus::sentences)
       .def_property_readonly("vocab_size", &Corpus::vocab_size)
       .def("vocab", &Corpus::vocab)
+      .def("tokens", [](const Corpus& c) {
+        return py::array_t<uint64_t>(c.tokens().size(), c.tokens().data());
+      })
+      .def("sent_offsets", [](const Corpus& c) {
+        return py::array_t<uint64_t>(c.sent_offsets().size(), c.sent_offsets().data());
+      })
+      .def("sent_of", [](const Corpus& c) {
+        return py::array_t<uint32_t>(c.sent_of().size(), c.sent_of().data());
+      })
+      .def("noise_table", [](const Corpus& c) {
+        return py::array_t<uint64_t>(c.noise_table().size(), c.noise_table().data());
+      })
+      .def_property_readonly("subsampled", &Corpus::subsampled)
+      .def("keep_per_token", [](const Corpus& c) {
+        auto k = c.keep_per_token();
+        return py::array_t<float>(k.size(), k.data());
+      })
       .def("fill_skipgram", [](const Corpus& c, uint64_t seed, uint64_t step, int B, int C, int W,
                                long long nneg, uintptr_t keys, int nthreads) {
              c.fill_skipgram(seed, step, B, C, W, nneg, reinterpret_cast<uint64_t*>(keys),

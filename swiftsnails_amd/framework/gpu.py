@@ -252,7 +252,7 @@ def build_worker(cfg: Config):
     elif model == "word2vec":
         if cfg.get("data_path", ""):
             from ..utils.dataio import make_corpus_source
-            data = make_corpus_source(cfg, rank, world)
+            data = make_corpus_source(cfg, rank, world, device=dev)
         else:
             data = W2VSynth(batch_size=int(cfg.get("batch_size", 16384)),
                             window=int(cfg.get("window", 5)),

@@ -23,6 +23,9 @@ values, labels) to the GPU once and cuts each step's padded batch out of it
 with one streaming kernel (``csrc/hip/data.hip``): no per-step host fill and
 no per-step PCIe copy (82 MB for a 262144 x 39 batch), and the step becomes
 hipGraph-capturable (the kernel can read its step from device memory).
+``FileCorpusSource(resident="hbm")`` does the same for a word2vec corpus: the
+tokens, sentence index, noise table and keep probabilities go to HBM and the
+skip-gram sampler runs on the device, bit-identical to the host sampler.
 """
 from __future__ import annotations
 
@@ -89,6 +92,28 @@ def _ext_stream(stream):
     return stream
 
 
+OUT_BIT = 1 << 40  # word2vec output-embedding key bit (Corpus::kOutBit)
+
+
+def _device(device) -> torch.device:
+    return torch.device(device) if device is not None else torch.device(
+        "cuda", torch.cuda.current_device())
+
+
+def _choose_residency(resident, device, nbytes: int) -> str:
+    """``hbm`` | ``host`` for a data source: ``auto``/None picks ``hbm`` on a
+    GPU when the source's device copy fits in half of the free HBM."""
+    if resident not in (None, "auto", "hbm", "host"):
+        raise ValueError(f"data residency {resident!r}: hbm | host | auto")
+    if resident in ("hbm", "host"):
+        if resident == "hbm" and not torch.cuda.is_available():
+            raise RuntimeError("data_resident: hbm needs a GPU")
+        return resident
+    if not torch.cuda.is_available():
+        return "host"
+    return "hbm" if nbytes <= torch.cuda.mem_get_info(_device(device))[0] // 2 else "host"
+
+
 class FileCtrSource:
     """Sparse CTR batches from a libsvm (``label idx[:val] ...``) or categorical
     TSV (``label<TAB>tok<TAB>tok...``) file, padded to ``num_fields`` keys per
@@ -107,7 +132,7 @@ class FileCtrSource:
         self.nthreads = nthreads
         # a synthetic-compatible attribute (table sizing when no capacity is set)
         self.num_features = max(1, self.ds.nnz)
-        self.resident = self._choose_residency(resident, device)
+        self.resident = _choose_residency(resident, device, self.device_bytes())
         self.ring = None
         if self.resident == "hbm":
             self._upload(device)
@@ -124,25 +149,10 @@ class FileCtrSource:
         ds = self.ds
         return 8 * (ds.rows + 1) + 8 * ds.nnz + 4 * ds.rows + (4 * ds.nnz if self.has_values else 0)
 
-    def _choose_residency(self, resident, device) -> str:
-        if resident not in (None, "auto", "hbm", "host"):
-            raise ValueError(f"data residency {resident!r}: hbm | host | auto")
-        if resident in ("hbm", "host"):
-            if resident == "hbm" and not torch.cuda.is_available():
-                raise RuntimeError("data_resident: hbm needs a GPU")
-            return resident
-        if not torch.cuda.is_available():
-            return "host"
-        dev = torch.device(device) if device is not None else torch.device(
-            "cuda", torch.cuda.current_device())
-        free = torch.cuda.mem_get_info(dev)[0]
-        return "hbm" if self.device_bytes() <= free // 2 else "host"
-
     def _upload(self, device):
         import numpy as np
 
-        dev = torch.device(device) if device is not None else torch.device(
-            "cuda", torch.cuda.current_device())
+        dev = _device(device)
         ds = self.ds
         self.device = dev
         self.d_offs = torch.from_numpy(np.asarray(ds.offsets()).view(np.int64)).to(dev)
@@ -222,7 +232,7 @@ class FileCorpusSource:
     def __init__(self, path: str, batch_size: int = 16384, window: int = 5, negatives: int = 5,
                  rank: int = 0, world: int = 1, min_count: int = 1, sample: float = 0.0,
                  seed: int = 1234, nthreads: int = 8, prefetch: int = 3,
-                 pin: Optional[bool] = None):
+                 pin: Optional[bool] = None, resident: Optional[str] = None, device=None):
         self.corpus = host().Corpus(path, nthreads, rank, world, min_count, sample)
         self.batch_size = int(batch_size)
         self.window = int(window)
@@ -230,8 +240,38 @@ class FileCorpusSource:
         self.seed = int(seed) + 7919 * rank
         self.nthreads = nthreads
         self.vocab = max(1, self.corpus.vocab_size)
+        self.ring = None
+        self.resident = _choose_residency(resident, device, self.device_bytes())
+        if self.resident == "hbm":
+            self._upload(device)
+            return
         pin = torch.cuda.is_available() if pin is None else pin
         self.ring = _PinnedRing(max(1, prefetch), {"keys": (self.n_keys, torch.int64)}, pin)
+
+    def device_bytes(self) -> int:
+        """HBM the resident sampler state takes (tokens, sentence index, noise
+        table, keep probabilities)."""
+        c = self.corpus
+        n = c.size
+        return 8 * n + 4 * n + 8 * (c.sentences + 1) + 8 * (1 << 22) + (4 * n if c.subsampled else 0)
+
+    def _upload(self, device):
+        import numpy as np
+
+        dev = _device(device)
+        c = self.corpus
+        self.device = dev
+        self.d_tokens = torch.from_numpy(np.asarray(c.tokens()).view(np.int64)).to(dev)
+        self.d_soffs = torch.from_numpy(np.asarray(c.sent_offsets()).view(np.int64)).to(dev)
+        self.d_sof = torch.from_numpy(np.asarray(c.sent_of()).view(np.int32)).to(dev)
+        self.d_table = torch.from_numpy(np.asarray(c.noise_table()).view(np.int64)).to(dev)
+        self.d_keep = (torch.from_numpy(np.asarray(c.keep_per_token())).to(dev)
+                       if c.subsampled else None)
+        torch.cuda.synchronize(dev)
+
+    @property
+    def graph_capturable(self) -> bool:
+        return self.resident == "hbm"
 
     @property
     def contexts(self) -> int:
@@ -253,7 +293,25 @@ class FileCorpusSource:
         self.corpus.fill_skipgram(self.seed, step, self.batch_size, self.contexts, self.window,
                                   self.tiles * NEG_TILE, buf["keys"].data_ptr(), self.nthreads)
 
-    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None):
+    def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None,
+                 step_dev: int = 0, step_delta: int = 0):
+        if self.resident == "hbm":
+            from .._native import hip
+
+            if keys.device != self.device or keys.numel() < self.n_keys:
+                raise ValueError("generate: the key buffer must hold n_keys on the corpus' device")
+            st = stream if stream is not None else torch.cuda.current_stream()
+            st = st.cuda_stream if hasattr(st, "cuda_stream") else int(st)
+            hip().w2v_corpus_batch(self.d_tokens.data_ptr(), self.d_soffs.data_ptr(),
+                                   self.d_sof.data_ptr(), self.d_table.data_ptr(),
+                                   self.d_table.numel(),
+                                   self.d_keep.data_ptr() if self.d_keep is not None else 0,
+                                   self.d_tokens.numel(), self.seed, step, step_dev, step_delta,
+                                   self.batch_size, self.contexts, self.window,
+                                   self.tiles * NEG_TILE, OUT_BIT, keys.data_ptr(), st)
+            return
+        if step_dev:
+            raise RuntimeError("host-fed corpus batches cannot be replayed from a graph")
         slot, buf = self.ring.take(step, self._fill)
         st = _ext_stream(stream)
         ctx = torch.cuda.stream(st) if st is not None else _null()
@@ -263,7 +321,8 @@ class FileCorpusSource:
             torch.cuda.current_stream() if keys.is_cuda else None))
 
     def close(self):
-        self.ring.close()
+        if self.ring is not None:
+            self.ring.close()
 
 
 class _null:
@@ -285,11 +344,13 @@ def make_ctr_source(cfg, rank: int = 0, world: int = 1, device=None):
                          resident=cfg.get("data_resident", "auto"), device=device)
 
 
-def make_corpus_source(cfg, rank: int = 0, world: int = 1):
-    """Config keys: data_path, batch_size, window, negatives, min_count, sample."""
+def make_corpus_source(cfg, rank: int = 0, world: int = 1, device=None):
+    """Config keys: data_path, batch_size, window, negatives, min_count, sample,
+    data_resident (auto|hbm|host)."""
     return FileCorpusSource(cfg.get("data_path"), batch_size=int(cfg.get("batch_size", 16384)),
                             window=int(cfg.get("window", 5)),
                             negatives=int(cfg.get("negatives", 5)), rank=rank, world=world,
                             min_count=int(cfg.get("min_count", 1)),
                             sample=float(cfg.get("sample", 0.0)),
-                            nthreads=int(cfg.get("data_threads", 8)))
+                            nthreads=int(cfg.get("data_threads", 8)),
+                            resident=cfg.get("data_resident", "auto"), device=device)

@@ -202,7 +202,41 @@ def test_sparse_lr_trains_from_libsvm_file(tmp_path, resident):
 
 
 @pytest.mark.gpu
-def test_word2vec_trains_from_corpus_file(tmp_path):
+@pytest.mark.parametrize("sample", [0.0, 1e-3])
+def test_hbm_resident_skipgram_matches_host_sampler(tmp_path, sample):
+    """data_resident: hbm for a corpus — the device sampler (k_w2v_corpus_batch)
+    writes the same keys as Corpus.fill_skipgram, with and without frequent-word
+    sub-sampling, from a host step or a device step counter."""
+    from swiftsnails_amd.utils.dataio import FileCorpusSource
+
+    p = str(tmp_path / "w2v.txt")
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_word2vec_data.py"), p,
+                           "--lines", "3000", "--zipf", "1.2", "--vocab", "700"])
+    with open(p, "a") as f:
+        f.write("42\n7 word\n")  # one-word sentences draw noise contexts; a hashed token
+    dev = torch.device("cuda", 0)
+    kw = dict(batch_size=256, window=3, negatives=5, min_count=2, sample=sample, seed=99)
+    dsrc = FileCorpusSource(p, resident="hbm", device=dev, **kw)
+    hsrc = FileCorpusSource(p, resident="host", pin=False, **kw)
+    assert dsrc.resident == "hbm" and dsrc.graph_capturable
+    keys = torch.empty(dsrc.n_keys, dtype=torch.int64, device=dev)
+    hk = torch.empty(hsrc.n_keys, dtype=torch.int64)
+    step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
+    for step in (0, 1, 5):
+        hsrc.generate(step, 0, 1, hk)
+        dsrc.generate(step, 0, 1, keys)
+        torch.cuda.synchronize()
+        assert torch.equal(keys.cpu(), hk), step
+        step_dev.fill_(step + 1)
+        dsrc.generate(0, 0, 1, keys, step_dev=step_dev.data_ptr(), step_delta=-1)
+        torch.cuda.synchronize()
+        assert torch.equal(keys.cpu(), hk), step
+    hsrc.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("resident", ["hbm", "host"])
+def test_word2vec_trains_from_corpus_file(tmp_path, resident):
     from swiftsnails_amd.models.word2vec import Word2VecWorker, make_w2v_table_args
     from swiftsnails_amd.ops.table import HbmTable
     from swiftsnails_amd.parallel.engine import PSEngine
@@ -213,7 +247,8 @@ def test_word2vec_trains_from_corpus_file(tmp_path):
     subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_word2vec_data.py"), p,
                            "--lines", "5000", "--zipf", "1.3", "--vocab", "2000"])
     dev = torch.device("cuda", 0)
-    src = FileCorpusSource(p, batch_size=1024, window=2, negatives=5)
+    src = FileCorpusSource(p, batch_size=1024, window=2, negatives=5, resident=resident)
+    assert src.resident == resident
     opt, init = make_w2v_table_args(32)
     table = HbmTable(capacity=16384, dim=32, optimizer=opt, init=init, device=dev)
     eng = PSEngine(table, LoopbackTransport(), max_keys=src.n_keys, dim=32, device=dev)

@@ -8,6 +8,7 @@ and trains the bench's LR step from it, once with the shard resident in HBM
 (`data_resident: host`, pinned-ring prefetch + H2D copy per step).
 
     python tools/bench_file_data.py --rows 600000 --batch 262144 --steps 20
+    python tools/bench_file_data.py --model word2vec --lines 400000 --vocab 1000000
 
 Prints one JSON line per mode.
 """
@@ -81,6 +82,38 @@ def run(path, resident, a, dev):
     return out
 
 
+def run_w2v(path, resident, a, dev):
+    from swiftsnails_amd.models.word2vec import Word2VecWorker, make_w2v_table_args
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.utils.dataio import FileCorpusSource
+
+    t0 = time.perf_counter()
+    src = FileCorpusSource(path, batch_size=a.w2v_batch, window=5, negatives=5,
+                           resident=resident, device=dev, nthreads=a.threads)
+    load_s = time.perf_counter() - t0
+    opt, init = make_w2v_table_args(128)
+    table = HbmTable(128, int(2 * src.vocab / 0.5) + 1024, optimizer=opt, init=init, device=dev)
+    eng = PSEngine(table, None, max_keys=src.n_keys, dim=128, device=dev)
+    w = Word2VecWorker(eng, src)
+    for _ in range(a.warmup):
+        w.step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        w.step()
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    eng.check()
+    pairs = a.w2v_batch * 10 * a.steps
+    out = {"model": "word2vec", "mode": resident, "tokens": src.corpus.size,
+           "vocab": src.vocab, "batch": a.w2v_batch, "steps": a.steps,
+           "load_s": round(load_s, 2), "ms_per_step": round(1000 * el / a.steps, 3),
+           "pairs_per_s": round(pairs / el, 1), "loss": round(w.mean_loss(), 5)}
+    src.close()
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--rows", type=int, default=600_000)
@@ -91,9 +124,27 @@ def main(argv=None):
     ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--threads", type=int, default=16)
     ap.add_argument("--path", default="/tmp/ss_bench_file.svm")
+    ap.add_argument("--model", default="sparse_lr", choices=["sparse_lr", "word2vec"])
+    ap.add_argument("--lines", type=int, default=400_000, help="word2vec corpus sentences")
+    ap.add_argument("--vocab", type=int, default=1_000_000)
+    ap.add_argument("--w2v-batch", type=int, default=16384)
     a = ap.parse_args(argv)
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
+    if a.model == "word2vec":
+        import subprocess
+
+        path = a.path + ".w2v.txt"
+        t0 = time.perf_counter()
+        subprocess.check_call([sys.executable, os.path.join(os.path.dirname(
+            os.path.abspath(__file__)), "gen_word2vec_data.py"), path, "--lines", str(a.lines),
+            "--vocab", str(a.vocab), "--zipf", "1.1", "--min-len", "8", "--max-len", "40"])
+        print(json.dumps({"file": path, "bytes": os.path.getsize(path),
+                          "write_s": round(time.perf_counter() - t0, 1)}), flush=True)
+        for mode in ("hbm", "host"):
+            print(json.dumps(run_w2v(path, mode, a, dev)), flush=True)
+        os.remove(path)
+        return 0
     wr = write_libsvm(a.path, a.rows, a.fields, a.features, dev)
     print(json.dumps({"file": a.path, "bytes": os.path.getsize(a.path), "write_s": round(wr, 1)}),
           flush=True)
