@@ -75,11 +75,17 @@ __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs,
   return d * Pd + __umulhi(h, Pd);
 }
 
-// upper bound on count/scatter chunks (SS_BD_NCH experiment knob, 2 per CU)
+// upper bound on count/scatter chunks (SS_BD_NCH knob).  128: a chunk of the
+// bench batch (10.2M keys) is 80K keys, looped in 8192-key register tiles,
+// so each (chunk, bucket) run of positions is ~16 long and the scatter's
+// partial-line stores merge better; the route stream also holds fewer CUs
+// beside the main stream.  Measured (bench, 1 GPU, A/B pairs): 512 ->
+// 0.928-0.932 ms/step, 256 -> 0.914, 128 -> 0.886-0.899, 96 -> 0.888-0.894,
+// 64 -> 0.90-0.916; neutral on the N>1 path and at batch 65536
 static long long bd_max_chunks() {
   static const long long v = [] {
     const char* e = std::getenv("SS_BD_NCH");
-    const long long x = e ? std::atoll(e) : 512;
+    const long long x = e ? std::atoll(e) : 128;
     return x < 64 ? 64 : x;
   }();
   return v;
