@@ -4,7 +4,11 @@
 //   rmw16  : load 16 B, update, store 16 B (AdaGrad-style slot update)
 //   cas8   : one 64-bit CAS per row (insert of a new key)
 //   store8 : one blind 8-byte store per row (the fused LR update's row write)
-// Usage: mb_random [GiB=23] [rows=1500000]
+// Usage: mb_random [GiB=23] [rows=1500000] [regions=0]
+//   regions > 0: every run of 1024 consecutive indices (one dedup bucket's
+//   unique keys) falls inside one of `regions` equal slices of the table —
+//   the access pattern of a table whose slot hash keeps a bucket's keys in
+//   one region (TLB / DRAM locality test)
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
@@ -43,6 +47,7 @@ __global__ void k_store8(unsigned long long* __restrict__ tab,
 int main(int argc, char** argv) {
   const double gib = argc > 1 ? atof(argv[1]) : 23.0;
   const long long n = argc > 2 ? atoll(argv[2]) : 1500000;
+  const long long regions = argc > 3 ? atoll(argv[3]) : 0;
   const size_t rows = (size_t)(gib * (1ull << 30) / 16);
   unsigned long long *tab, *idx, *out;
   float* g;
@@ -53,9 +58,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&g, n * 4));
   std::vector<unsigned long long> h(n);
   unsigned long long x = 88172645463325252ull;
+  const size_t rrows = regions > 0 ? rows / (size_t)regions : rows;
+  size_t rbase = 0;
   for (long long i = 0; i < n; ++i) {
     x ^= x << 13; x ^= x >> 7; x ^= x << 17;
-    h[i] = x % rows;
+    if (regions > 0 && i % 1024 == 0) rbase = (x >> 7) % (size_t)regions * rrows;
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    h[i] = regions > 0 ? rbase + x % rrows : x % rows;
   }
   CK(hipMemcpy(idx, h.data(), n * 8, hipMemcpyHostToDevice));
   CK(hipMemset(g, 0, n * 4));
