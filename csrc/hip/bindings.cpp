@@ -127,6 +127,15 @@ PYBIND11_MODULE(_ss_hip, m) {
   }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
      py::arg("P"), py::arg("slots"), py::arg("out"), py::arg("ip"), py::arg("size_ctr"),
      py::arg("err"), py::arg("G"), py::arg("st"), py::arg("osi") = 0, py::arg("snap") = 0);
+  m.def("pull_fill_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
+                           uintptr_t ubase, int P_, uintptr_t slots, uintptr_t out,
+                           const InitParams& ip, uintptr_t size_ctr, uintptr_t err, uintptr_t snap,
+                           uintptr_t luid, uintptr_t occ, uintptr_t st) {
+    launch_pull_fill_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
+                        P<const uint32_t>(unum), P<const uint32_t>(ubase), P_, P<long long>(slots),
+                        P<float>(out), ip, P<unsigned long long>(size_ctr), P<int>(err),
+                        P<float>(snap), P<const uint32_t>(luid), P<float>(occ), S(st));
+  });
   m.def("pull_claim", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
                          uintptr_t slots, uintptr_t out, const InitParams& ip, uintptr_t size_ctr,
                          uintptr_t err, int G, uintptr_t st) {

@@ -33,6 +33,10 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
                            int* err, int G, int osi, hipStream_t st, float* snap = nullptr);
+void launch_pull_fill_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                         const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
+                         float* out, const InitParams& ip, unsigned long long* size_ctr, int* err,
+                         float* snap, const uint32_t* luid, float* occ, hipStream_t st);
 void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
                        long long max_n, long long* slots, float* out, const InitParams& ip,
                        unsigned long long* size_ctr, int* err, int G, hipStream_t st);

@@ -306,6 +306,48 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
 
+// Pull + occurrence fill fused (sparse LR, one GPU, snapshot pull on 16-byte
+// slots): one 1024-thread workgroup per dedup bucket probes the bucket's
+// unique keys (one 16-byte load per probe step), keeps the pulled weights in
+// LDS and then writes every occurrence's parameter in bucket-position order,
+// occ[p] = w[luid[p]] (k_bd_fill_occ's job) — no second pass over the rows
+// and no launch boundary between the two.
+static constexpr int kFillMax = 4096;  // unique keys per bucket (bdedup.hip kBdTS)
+
+__global__ __launch_bounds__(1024) void k_pull_fill_bk(
+    DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
+    const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
+    long long* __restrict__ slots_out, float* __restrict__ out, InitParams ip,
+    unsigned long long* size_ctr, int* err, float2* __restrict__ snap,
+    const uint32_t* __restrict__ luid, float* __restrict__ occ) {
+  __shared__ float sv[kFillMax];
+  const int b = blockIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+  const uint32_t nu = min(unum[b], (uint32_t)kFillMax), base = ubase[b];
+  const uint64_t* src = bkeys + p0;
+  unsigned long long ins = 0;
+  for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
+    pull_one<1>(t, src[l], (long long)base + l, slots_out, out, ip, err, 0, ins, snap, 1);
+    sv[l] = out[base + l];  // this lane's own store: visible to it
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
+  __syncthreads();
+  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 2 * 1024) {
+    uint32_t l[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t p = pb + r * 1024;
+      l[r] = p < p1 ? luid[p] : 0xFFFFFFFFu;
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t p = pb + r * 1024;
+      if (p < p1) occ[p] = l[r] < nu ? sv[l[r]] : 0.f;
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // CAS-free insert for key lists that are unique within the launch.
 //
@@ -637,6 +679,19 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
                                       dim3(256), 0, st, t, keys, sl, slots, out, ip, size_ctr,
                                       err));
   check_launch("k_pull_unique");
+}
+
+void launch_pull_fill_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                         const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
+                         float* out, const InitParams& ip, unsigned long long* size_ctr, int* err,
+                         float* snap, const uint32_t* luid, float* occ, hipStream_t st) {
+  if (P <= 0) return;
+  if (!snap || !luid || !occ || !(t.dim == 1 && t.width == 2 && t.stride == 16 &&
+                                  t.key_off == 8 && t.row_off == 0))
+    throw std::invalid_argument("pull_fill_bk: snapshot pull of 16-byte scalar rows only");
+  hipLaunchKernelGGL(k_pull_fill_bk, dim3(P), dim3(1024), 0, st, t, bkeys, bstart, unum, ubase,
+                     slots, out, ip, size_ctr, err, reinterpret_cast<float2*>(snap), luid, occ);
+  check_launch("k_pull_fill_bk");
 }
 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,

@@ -132,6 +132,13 @@ class SparseLRWorker(PipelinedWorker):
                 self.use_occ, self.occ = False, None
             for dd in engine.dedupers:
                 dd.need_bkt = not self.use_occ
+            # SS_PULL_FILL=1: the 1-GPU snapshot pull writes occ itself
+            # (k_pull_fill_bk: one workgroup per bucket, weights staged in LDS).
+            # Measured slower (0.94 vs 0.86 ms/step, three A/B pairs): one
+            # workgroup per bucket serialises the probes the default pull
+            # spreads over four
+            if self.use_occ and os.environ.get("SS_PULL_FILL", "0") != "0":
+                engine.occ_buf = self.occ
         elif grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
@@ -205,7 +212,8 @@ class SparseLRWorker(PipelinedWorker):
                            d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
                            self.loss_sum.data_ptr(), 0, st)
             elif self.use_occ:
-                o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
+                if not rnd.occ_filled:
+                    o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
                 h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
                            rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
                            self.loss_sum.data_ptr(), 0, st, o.index_ptrs(dd.n),

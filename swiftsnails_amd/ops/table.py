@@ -210,7 +210,8 @@ class HbmTable:
                 self.opt.kind == "adagrad" and self.stride % 8 == 0 and self.row_off % 8 == 0)
 
     def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None,
-                     osi: bool = False, snap: Optional[torch.Tensor] = None):
+                     osi: bool = False, snap: Optional[torch.Tensor] = None,
+                     luid: Optional[torch.Tensor] = None, occ: Optional[torch.Tensor] = None):
         """Unique-key lookup-or-init + gather straight from a bucketed dedup
         (``Deduper.bucket_view()``): rows land at their unique ids (compact,
         or occurrence-space with ``osi``).  ``snap`` ([ucap, 2] float32,
@@ -219,6 +220,16 @@ class HbmTable:
         bkeys, bstart, unum, ubase, P = view
         if snap is not None and not self.snapshot_ok:
             raise ValueError("pull snapshot needs scalar AdaGrad rows (dim 1, G 1)")
+        if occ is not None:
+            # fused with the occurrence fill (``Deduper.fill_occ``): occ[p] =
+            # the pulled weight of the occurrence at bucket position p
+            if snap is None or osi or luid is None or self.stride != 16:
+                raise ValueError("pull_buckets(occ=): snapshot pull of 16-byte rows, compact ids")
+            hip().pull_fill_bk(self.dt, bkeys, bstart, unum, ubase, P, slots.data_ptr(),
+                               out.data_ptr(), self._init_native, self.size_ctr.data_ptr(),
+                               self.err.data_ptr(), snap.data_ptr(), luid.data_ptr(),
+                               occ.data_ptr(), _stream_ptr(stream))
+            return out, slots
         hip().pull_unique_bk(self.dt, bkeys, bstart, unum, ubase, P, slots.data_ptr(),
                              out.data_ptr(), self._init_native, self.size_ctr.data_ptr(),
                              self.err.data_ptr(), self.G, _stream_ptr(stream), int(osi),

@@ -81,6 +81,7 @@ class Round:
     snap: Optional[torch.Tensor] = None   # world-1: (w, h) rows as pulled (blind apply)
     snap_version: int = -1                # table.version the snapshot is valid for
     applied: bool = False                 # the model's kernel already ran K5 (fuse_apply)
+    occ_filled: bool = False              # the pull also wrote the occurrence parameters
 
     @property
     def inv(self) -> torch.Tensor:
@@ -246,6 +247,10 @@ class PSEngine:
         # occurrence-space unique ids (enable_osi): the model indexes rows
         # with the dedup's own inverse (bstart[b] + l), see ops/dedup.py
         self.osi = False
+        # occ_buf (set by a model, one GPU): the bucketed snapshot pull also
+        # writes each occurrence's parameter at its bucket position into it
+        # (table.pull_buckets(occ=), fused with Deduper.fill_occ)
+        self.occ_buf: Optional[torch.Tensor] = None
         # hipGraph capture in progress (models/base.py enable_graph): an id
         # per captured step.  Inside a capture the route stream forks from the
         # capturing stream, and events of other captures are not waited on —
@@ -368,17 +373,20 @@ class PSEngine:
         if self.fast1:
             own = dd.owner
             snap = None
+            occ = None
             if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
                 if self.snapshot and not self.osi:
                     snap = self._snaps[slot]
+                    if self.occ_buf is not None and tab.stride == 16:
+                        occ = self.occ_buf
                 tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi,
-                                 snap=snap)
+                                 snap=snap, luid=own.luid if occ is not None else None, occ=occ)
             else:
                 tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                          segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
             self.metrics.add(occurrences=dd.n)
             return Round(dd, uv, slot, slots=self.slots[slot], snap=snap,
-                         snap_version=tab.version)
+                         snap_version=tab.version, occ_filled=occ is not None)
         scounts, rcounts = r.counts.wait()
         D = self.displs
         self.t.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)

@@ -619,6 +619,41 @@ def test_sparse_lr_osi_matches_compact_ids(dev, monkeypatch):
                                rtol=1e-4, atol=1e-6)
 
 
+@pytest.mark.parametrize("env", [{"SS_PULL_FILL": "1"}, {"SS_LR_OCC": "0"}])
+def test_sparse_lr_occurrence_paths_agree(dev, monkeypatch, env):
+    """The LR forward's parameter paths train the same model: separate fill
+    kernel (default), pull fused with the occurrence fill (SS_PULL_FILL=1),
+    dependent gathers through the dedup index (SS_LR_OCC=0)."""
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    out = {}
+    for name, e in (("default", {}), ("alt", env)):
+        for k in ("SS_PULL_FILL", "SS_LR_OCC"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in e.items():
+            monkeypatch.setenv(k, v)
+        data = CtrSynth(batch_size=4096, num_fields=13, num_features=300_000, tail_frac=0.2)
+        table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
+        eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
+        w = SparseLRWorker(eng, data)
+        if name == "default":
+            assert w.use_occ and eng.occ_buf is None
+        elif "SS_PULL_FILL" in e:
+            assert w.use_occ and eng.occ_buf is not None
+        losses = [float(w.step().sum().item()) for _ in range(12)]
+        torch.cuda.synchronize()
+        table.check()
+        out[name] = (losses, table.to_dict(with_state=True))
+    (l1, t1), (l0, t0) = out["default"], out["alt"]
+    np.testing.assert_allclose(l1, l0, rtol=1e-4)
+    assert t1.keys() == t0.keys()
+    ks = list(t1.keys())[:20000]
+    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
+                               rtol=1e-4, atol=1e-6)
+
+
 @pytest.mark.parametrize("prefill", ["1", "0"])
 def test_zero_init_prefilled_rows(dev, monkeypatch, prefill):
     """Zero-init tables are allocated with the initial row in every empty
