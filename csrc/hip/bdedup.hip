@@ -75,20 +75,23 @@ __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs,
   return d * Pd + __umulhi(h, Pd);
 }
 
-// upper bound on count/scatter chunks (SS_BD_NCH knob).  128: a chunk of the
-// bench batch (10.2M keys) is 80K keys, looped in 8192-key register tiles,
-// so each (chunk, bucket) run of positions is ~16 long and the scatter's
-// partial-line stores merge better; the route stream also holds fewer CUs
-// beside the main stream.  Measured (bench, 1 GPU, A/B pairs): 512 ->
-// 0.928-0.932 ms/step, 256 -> 0.914, 128 -> 0.886-0.899, 96 -> 0.888-0.894,
-// 64 -> 0.90-0.916; neutral on the N>1 path and at batch 65536
-static long long bd_max_chunks() {
-  static const long long v = [] {
+// upper bound on count/scatter chunks (SS_BD_NCH knob; default by path).
+// One rank (the 1-GPU step): 128 — a chunk of the bench batch (10.2M keys)
+// is 80K keys, looped in 8192-key register tiles, so each (chunk, bucket) run
+// of positions is ~16 long and the scatter's partial-line stores merge in L2,
+// and the route stream holds fewer CUs beside the main stream.  Measured
+// (bench, A/B pairs): 512 -> 0.928-0.932 ms/step, 256 -> 0.914, 128 ->
+// 0.886-0.899, 96 -> 0.888-0.894, 64 -> 0.90-0.916.  N>1 ranks: 256 (the
+// route stream is the N>1 step's critical chain and its count kernel must not
+// starve beside the pull and apply streams): 128 -> 1.057-1.062 ms/step,
+// 256 -> 1.032-1.036, 512 -> 1.046-1.049 (N>1 engine path on one GPU).
+static long long bd_max_chunks(int nranks) {
+  static const long long env = [] {
     const char* e = std::getenv("SS_BD_NCH");
-    const long long x = e ? std::atoll(e) : 128;
-    return x < 64 ? 64 : x;
+    return e ? std::atoll(e) : 0ll;
   }();
-  return v;
+  const long long x = env ? env : (nranks > 1 ? 256 : 128);
+  return x < 64 ? 64 : x;
 }
 
 // ---- layout of the int scratch (u32 words), a function of (n, nranks) only
@@ -121,7 +124,7 @@ static BdLayout bd_layout(long long n, int nranks, int ndest) {
   // ... but at most bd_max_chunks() chunks: the [nch][P] histogram grows as
   // n^2 (P ~ n/2048 buckets per chunk row), 25 MB at n = 10M with 8192-key
   // chunks; bigger chunks loop over 8192-key register tiles instead
-  const long long cmax = bd_max_chunks();
+  const long long cmax = bd_max_chunks(nranks);
   if ((n + chunk - 1) / chunk > cmax)
     chunk = (((n + cmax - 1) / cmax + kBdChunkLanes - 1) / kBdChunkLanes) * kBdChunkLanes;
   L.chunk = (int)chunk;
@@ -156,7 +159,7 @@ long long bd_scratch_words(long long n, int nranks, int ndest) {
   pact = std::min<long long>(pact, kBdMaxBuckets) + 2 * ndest;
   const long long pmax = ((pact + ndest - 1) / ndest + 1) * nranks;
   const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
-  long long nchmax = std::min<long long>(256 * waves, bd_max_chunks());
+  long long nchmax = std::min<long long>(256 * waves, bd_max_chunks(nranks));
   nchmax = std::min<long long>(nchmax, (n + kBdChunkLanes - 1) / kBdChunkLanes);
   nchmax = std::max<long long>(nchmax, 1);
   const long long bound = 2 + pmax * nchmax + 4 * pmax + 1;
@@ -892,11 +895,10 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     return (v == 256 || v == 512 || v == 1024) ? v : def;
   };
   static const int ct = wg_env("SS_BD_CT", 1024);
-  // count: 1024 on one GPU; 256 with N>1 ranks, where the route stream shares
-  // the chip with the main and pull streams and a 1024-thread workgroup waits
-  // for 16 free wave slots (measured on the N>1 path: 1.234 -> 1.212 ms/step)
+  // count: 1024 threads (at 256 chunks on the N>1 path: 1.032-1.036 ms/step
+  // vs 1.057-1.062 for 256 threads at 128 chunks; at 512 chunks both equal)
   static const int cnt_env = wg_env("SS_BD_CNT", 0);
-  const int cnt = cnt_env ? cnt_env : (rs.nranks > 1 ? 256 : 1024);
+  const int cnt = cnt_env ? cnt_env : 1024;
   static const int cs = wg_env("SS_BD_CS", 1024);
 #define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \

@@ -69,13 +69,13 @@ KNOBS: dict[str, Knob] = {
                             "(key + row) instead of a key load then a row load"),
     "SS_APPLY_VEC": Knob("1", "csrc/hip/table.hip", "tuning",
                          "one lane group per key + 8-byte (w, h) accesses in k_apply"),
-    "SS_BD_NCH": Knob("128", "csrc/hip/bdedup.hip", "tuning",
-                      "max count/scatter chunks (512 -> 128: 0.93 -> 0.89 ms/step)"),
+    "SS_BD_NCH": Knob("128 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
+                      "max count/scatter chunks (1 GPU 512 -> 128: 0.93 -> 0.89 ms/step; "
+                      "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
     "SS_BD_STAGE": Knob("0", "csrc/hip/bdedup.hip", "experiment",
                         "scatter stages keys in bucket order, dedup reads them coalesced "
                         "(0.949 -> 0.968 ms/step at 128 chunks, three A/B pairs)"),
-    "SS_BD_CNT": Knob("1024 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
-                      "count workgroup size (256 on the N>1 path: 1.234 -> 1.212 ms/step)"),
+    "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "count workgroup size"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
