@@ -7,8 +7,11 @@ Public API (mirrors the reference umbrella header /root/reference/src/swiftsnail
                  collective mode, one process per GPU)
 * parameters   : ``HbmTable`` (GPU shard), ``HostTable`` (CPU shard),
                  ``Optimizer`` / ``InitConfig`` (the Pull/PushAccessMethod menu)
-* access       : ``PSEngine.pull`` / ``push`` / ``pull_dense`` / ``push_keys``
-                 (global_pull_access / global_push_access)
+* access       : ``GlobalParamCache``, ``global_pull_access().pull_with_barrier``,
+                 ``global_push_access().push_with_barrier`` (the reference's calls,
+                 over a GPU engine or a host client); ``PSEngine.pull`` / ``push`` /
+                 ``pull_dense`` / ``push_keys`` (the round engine underneath);
+                 ``HbmTable.set_push_method`` (user-defined update rules)
 * routing      : ``HashFrag`` (key -> fragment -> server)
 * config       : ``Config``, ``global_config`` (``key: value`` files)
 * checkpoints  : ``swiftsnails_amd.utils.checkpoint``
@@ -41,6 +44,10 @@ def __getattr__(name):  # lazy: GPU modules import torch/HIP on first use
         "Word2VecWorker": ("models.word2vec", "Word2VecWorker"),
         "FMWorker": ("models.fm", "FMWorker"),
         "DenseLR": ("models.dense_lr", "DenseLR"),
+        "GlobalParamCache": ("access", "GlobalParamCache"),
+        "global_pull_access": ("access", "global_pull_access"),
+        "global_push_access": ("access", "global_push_access"),
+        "set_global_target": ("access", "set_global_target"),
     }
     if name in lazy:
         import importlib
@@ -52,4 +59,5 @@ def __getattr__(name):  # lazy: GPU modules import torch/HIP on first use
 
 __all__ = ["Config", "global_config", "HashFrag", "InitConfig", "Optimizer", "HbmTable",
            "HostTable", "PSEngine", "SwiftMaster", "SwiftServer", "SwiftWorker", "BaseAlgorithm",
-           "PSContext", "run_training", "SparseLRWorker", "Word2VecWorker", "FMWorker", "DenseLR"]
+           "PSContext", "run_training", "SparseLRWorker", "Word2VecWorker", "FMWorker", "DenseLR",
+           "GlobalParamCache", "global_pull_access", "global_push_access", "set_global_target"]

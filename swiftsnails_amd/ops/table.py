@@ -86,6 +86,14 @@ class TableFullError(RuntimeError):
     pass
 
 
+class _null_ctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class HbmTable:
     """One GPU shard of the sparse parameter table."""
 
@@ -114,6 +122,8 @@ class HbmTable:
         # bumped by every row-modifying call: a pull snapshot (pull_buckets
         # snap=) is valid for a blind-write apply only while it is unchanged
         self.version = 0
+        # user-defined update rule (set_push_method), else the optimizer menu
+        self.push_fn = None
         self._alloc(int(capacity))
         self._init_native = self.init_cfg.native()
 
@@ -206,8 +216,47 @@ class HbmTable:
     @property
     def snapshot_ok(self) -> bool:
         """Rows are (w, h) scalar AdaGrad pairs the pull can snapshot."""
-        return (self.G == 1 and self.dim == 1 and self.width == 2 and
+        return (self.G == 1 and self.dim == 1 and self.width == 2 and self.push_fn is None and
                 self.opt.kind == "adagrad" and self.stride % 8 == 0 and self.row_off % 8 == 0)
+
+    # -- user-defined update rule -------------------------------------------
+    def set_push_method(self, fn) -> None:
+        """Replace the optimizer menu by ``fn(rows, grads) -> new_rows``, the
+        reference's ``PushAccessMethod::apply_push_value`` as tensor code
+        (/root/reference/src/core/parameter/sparse_access_method.h:30-48):
+        ``rows`` [n, width] are the pushed keys' full rows (parameters, then
+        the optimizer state columns of ``optimizer.state_width(dim)``),
+        ``grads`` [n, dim] their merged gradients; the returned rows are
+        stored back.  Runs as torch ops on the gathered rows (two random row
+        passes instead of the fused update kernel).  ``None`` restores the
+        built-in rule."""
+        self.push_fn = fn
+        self.version += 1
+
+    def rows_view(self) -> torch.Tensor:
+        """[capacity, width] float32 view of every slot's row (strided)."""
+        rows = self.storage.view(torch.float32).view(self.capacity, self.stride // 4)
+        r0 = self.row_off // 4
+        return rows[:, r0:r0 + self.width]
+
+    def apply_custom(self, slots: torch.Tensor, grads: torch.Tensor, stream=None) -> None:
+        """Apply ``push_fn`` at resolved ``slots`` (unique; -1 = skipped)."""
+        st = torch.cuda.current_stream() if stream is None else stream
+        with torch.cuda.stream(st) if not isinstance(st, int) else _null_ctx():
+            s = slots.reshape(-1)
+            g = grads.reshape(s.numel(), self.dim)
+            ok = s >= 0
+            s, g = s[ok], g[ok]
+            if s.numel() == 0:
+                return
+            rv = self.rows_view()
+            new = self.push_fn(rv[s].clone(), g.to(torch.float32))
+            new = torch.as_tensor(new, dtype=torch.float32, device=self.device)
+            if new.shape != (s.numel(), self.width):
+                raise ValueError(f"push method returned {tuple(new.shape)}, "
+                                 f"expected {(s.numel(), self.width)}")
+            rv[s] = new
+            self.version += 1
 
     def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None,
                      osi: bool = False, snap: Optional[torch.Tensor] = None,
@@ -260,6 +309,12 @@ class HbmTable:
         ``snap``: the (w, h) rows ``pull_buckets(snap=)`` read, updated and
         stored blind — the caller guarantees no row changed since (same
         ``version``)."""
+        if self.push_fn is not None:
+            if segs is not None:
+                raise ValueError("push_slots with a custom push method takes whole slot lists")
+            n = slots.numel() if max_n is None else max_n
+            self.apply_custom(slots[:n], grads.reshape(-1, self.dim)[:n], stream)
+            return
         sl = segs if segs is not None else self._seg(slots.numel())
         self.version += 1
         hip().apply(self.dt, slots.data_ptr(), grads.data_ptr(), sl,

@@ -467,7 +467,10 @@ class PSEngine:
                     _hip().probe(tab.dt, self.rkeys.data_ptr(), sl, c, rsl.data_ptr(),
                                  tab._init_native, 1, tab.size_ctr.data_ptr(),
                                  tab.err.data_ptr(), tab.G, _stream())
-                tab.push_slots(rsl, self.rgrads, segs=sl, max_n=c)
+                if tab.push_fn is not None:
+                    tab.apply_custom(rsl[D[s]:D[s] + c], self.rgrads[D[s]:D[s] + c])
+                else:
+                    tab.push_slots(rsl, self.rgrads, segs=sl, max_n=c)
             else:
                 tab.push_keys(self.rkeys[D[s]:D[s] + c], self.rgrads[D[s]:D[s] + c])
         tab.next_round()
@@ -488,7 +491,7 @@ class PSEngine:
         ``push`` only does the bookkeeping."""
         tab = self.table
         if not (self.fast1 and self.fuse_apply_on and not self.osi and not rnd.applied
-                and rnd.slots is not None):
+                and rnd.slots is not None and getattr(tab, "push_fn", None) is None):
             return None
         if snapshot and not (rnd.snap is not None and rnd.snap_version == tab.version):
             return None
@@ -503,6 +506,13 @@ class PSEngine:
         g = rnd.ugrad if grads is None else grads
         tab = self.table
         if self.fast1 and rnd.applied:
+            tab.next_round()
+        elif self.fast1 and getattr(tab, "push_fn", None) is not None:
+            # user-defined update rule: compact unique ids 0..ucount-1 (syncs)
+            if self.osi:
+                raise NotImplementedError("a custom push method needs compact unique ids")
+            n = int(rnd.dd.ucount.sum())
+            tab.apply_custom(rnd.slots[:n], g[:n])
             tab.next_round()
         elif self.fast1:
             if self.osi:
@@ -587,7 +597,11 @@ class PSEngine:
             s = self.slots[r.slot]
             _hip().probe(tab.dt, dd.ukeys.data_ptr(), sl, n, s.data_ptr(), tab._init_native, 1,
                          tab.size_ctr.data_ptr(), tab.err.data_ptr(), tab.G, _stream())
-            tab.push_slots(s, dd.ugrad, segs=sl, max_n=n)
+            if tab.push_fn is not None:
+                u = int(dd.ucount.sum())
+                tab.apply_custom(s[:u], dd.ugrad[:u])
+            else:
+                tab.push_slots(s, dd.ugrad, segs=sl, max_n=n)
             tab.next_round()
         else:
             scounts, rcounts = r.counts.wait()
