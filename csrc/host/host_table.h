@@ -18,6 +18,7 @@
 #include <cstdio>
 #include <fstream>
 #include <memory>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -197,18 +198,54 @@ class HostTable : NonCopyable {
   }
   const OptParams& opt() const { return op_; }
 
+  // User-defined access methods, the reference's PullAccessMethod::init_param
+  // and PushAccessMethod::apply_push_value (sparse_access_method.h:10-48):
+  // `init(key, row, dim, width)` fills a new key's row (params, then
+  // `width - dim` optimizer-state floats) after the built-in init rule,
+  // `apply(key, row, grad, dim, width)` updates a row in place.  Both run per
+  // key under the key's shard lock.  Empty functions restore the built-ins.
+  using InitFn = std::function<void(uint64_t key, float* row, int dim, int width)>;
+  using ApplyFn =
+      std::function<void(uint64_t key, float* row, const float* grad, int dim, int width)>;
+  // Batch form for interpreted callers (Python): the rows of a whole push,
+  // gathered to rows[n][width], updated in place, written back.  Runs on the
+  // pushing thread outside the shard locks, so concurrent pushes of the same
+  // key may lose an update (the reference applies without a lock at all,
+  // sparsetable.h:181-192).
+  using BatchApplyFn =
+      std::function<void(const uint64_t* keys, size_t n, float* rows, const float* grads)>;
+  void set_access_methods(InitFn init, ApplyFn apply) {
+    init_fn_ = std::move(init);
+    apply_fn_ = std::move(apply);
+  }
+  void set_batch_apply(BatchApplyFn f) { batch_fn_ = std::move(f); }
+
   // lookup-or-init + gather (reference get_pull_value)
   void pull(const uint64_t* keys, size_t n, float* out) {
     run_sharded(keys, n, [&](HostShard& sh, size_t i) {
-      const float* r = sh.find_or_insert(keys[i], ip_, nullptr);
+      const float* r = row_of(sh, keys[i]);
       std::copy(r, r + dim_, out + i * dim_);
     });
   }
   // apply (reference apply_push_value); missing keys are created first.
   // Duplicate keys in one call are applied sequentially under the shard lock.
   void push(const uint64_t* keys, size_t n, const float* grads) {
+    if (batch_fn_) {
+      std::vector<float> rows(n * (size_t)width_);
+      run_sharded(keys, n, [&](HostShard& sh, size_t i) {
+        const float* r = row_of(sh, keys[i]);
+        std::copy(r, r + width_, rows.data() + i * width_);
+      });
+      batch_fn_(keys, n, rows.data(), grads);
+      assign(keys, n, rows.data());
+      return;
+    }
     run_sharded(keys, n, [&](HostShard& sh, size_t i) {
-      float* r = sh.find_or_insert(keys[i], ip_, nullptr);
+      float* r = row_of(sh, keys[i]);
+      if (apply_fn_) {
+        apply_fn_(keys[i], r, grads + i * dim_, dim_, width_);
+        return;
+      }
       for (int j = 0; j < dim_; ++j) opt_apply(op_, r, r + dim_, dim_, j, grads[i * dim_ + j]);
     });
   }
@@ -333,9 +370,20 @@ class HostTable : NonCopyable {
     }
   }
 
+  // lookup-or-init of one key (shard lock held), with the user init method
+  float* row_of(HostShard& sh, uint64_t key) {
+    bool inserted = false;
+    float* r = sh.find_or_insert(key, ip_, &inserted);
+    if (inserted && init_fn_) init_fn_(key, r, dim_, width_);
+    return r;
+  }
+
   int dim_, width_;
   InitParams ip_;
   OptParams op_;
+  InitFn init_fn_;
+  ApplyFn apply_fn_;
+  BatchApplyFn batch_fn_;
   std::vector<std::unique_ptr<HostShard>> shards_;
   std::unique_ptr<ThreadPool> pool_;
 };

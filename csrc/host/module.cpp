@@ -158,6 +158,30 @@ PYBIND11_MODULE(_ss_host, m) {
         py::gil_scoped_release rel;
         t.assign(k.data(), (size_t)k.size(), r.data());
       })
+      .def("set_batch_apply", [](HostTable& t, py::object fn) {
+        // fn(keys u64[n], rows f32[n, width], grads f32[n, dim]) -> new rows
+        if (fn.is_none()) {
+          t.set_batch_apply(nullptr);
+          return;
+        }
+        auto f = std::make_shared<py::object>(fn);
+        const int dim = t.dim(), width = t.width();
+        t.set_batch_apply([f, dim, width](const uint64_t* keys, size_t n, float* rows,
+                                          const float* grads) {
+          py::gil_scoped_acquire gil;
+          py::array_t<uint64_t> ka((py::ssize_t)n);
+          std::memcpy(ka.mutable_data(), keys, n * 8);
+          py::array_t<float> ra({(py::ssize_t)n, (py::ssize_t)width});
+          std::memcpy(ra.mutable_data(), rows, n * (size_t)width * 4);
+          py::array_t<float> ga({(py::ssize_t)n, (py::ssize_t)dim});
+          std::memcpy(ga.mutable_data(), grads, n * (size_t)dim * 4);
+          auto out = py::array_t<float, py::array::c_style | py::array::forcecast>::ensure(
+              (*f)(ka, ra, ga));
+          SS_CHECK_MSG(out && (size_t)out.size() == n * (size_t)width,
+                       "push method must return rows of shape [n, width]");
+          std::memcpy(rows, out.data(), n * (size_t)width * 4);
+        });
+      }, py::arg("fn"))
       .def("get_rows", [](HostTable& t, u64arr k) {
         py::array_t<float> rows({(py::ssize_t)k.size(), (py::ssize_t)t.width()});
         py::array_t<uint8_t> found((py::ssize_t)k.size());

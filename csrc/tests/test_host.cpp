@@ -271,6 +271,52 @@ TEST(host_table_pull_push_text_roundtrip) {
   std::remove(p.c_str());
 }
 
+// user-defined access methods: the reference's PullAccessMethod::init_param
+// and PushAccessMethod::apply_push_value (sparse_access_method.h:10-48)
+TEST(host_table_user_access_methods) {
+  InitParams ip{0, 0.f, 0.f, 1, -1};
+  OptParams op{1, 0.1f, 0, 0, 1e-8f, 0.9f, 0.999f, 1, 1, 0.05f, 1, 1, 0};  // AdaGrad layout
+  HostTable t(2, 3, ip, op);
+  EXPECT(t.width() == 4);
+  // init: w = key / 10, state = 7; apply: clipped step w -= clamp(g, -1, 1), state counts pushes
+  t.set_access_methods(
+      [](uint64_t key, float* row, int dim, int width) {
+        for (int j = 0; j < dim; ++j) row[j] = (float)key / 10.f;
+        for (int j = dim; j < width; ++j) row[j] = 7.f;
+      },
+      [](uint64_t, float* row, const float* g, int dim, int width) {
+        for (int j = 0; j < dim; ++j) row[j] -= std::max(-1.f, std::min(1.f, g[j]));
+        for (int j = dim; j < width; ++j) row[j] += 1.f;
+      });
+  std::vector<uint64_t> keys = {10, 20, 30};
+  std::vector<float> out(6);
+  t.pull(keys.data(), 3, out.data());
+  EXPECT(out[0] == 1.f && out[3] == 2.f && out[5] == 3.f);
+  std::vector<float> g = {5.f, 0.25f, -3.f, 0.5f, 0.f, 0.f};
+  t.push(keys.data(), 3, g.data());
+  t.pull(keys.data(), 3, out.data());
+  EXPECT(out[0] == 0.f && out[1] == 0.75f && out[2] == 3.f && out[3] == 1.5f && out[4] == 3.f);
+  std::vector<float> rows(12);
+  std::vector<uint8_t> found(3);
+  t.get_rows(keys.data(), 3, rows.data(), found.data());
+  EXPECT(found[0] && rows[2] == 8.f && rows[3] == 8.f);  // 7 + one push
+  // batch form (interpreted callers): whole push at once
+  t.set_batch_apply([](const uint64_t*, size_t n, float* r, const float* gg) {
+    for (size_t i = 0; i < n; ++i) r[i * 4] += 100.f * gg[i * 2];
+  });
+  std::vector<float> g2 = {1.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  t.push(keys.data(), 1, g2.data());
+  t.pull(keys.data(), 1, out.data());
+  EXPECT(out[0] == 100.f);
+  // pushing a key never pulled creates it with the user init first
+  std::vector<uint64_t> k4 = {40};
+  std::vector<float> g4 = {0.f, 0.f};
+  t.set_batch_apply(nullptr);
+  t.push(k4.data(), 1, g4.data());
+  t.pull(k4.data(), 1, out.data());
+  EXPECT(out[0] == 4.f);
+}
+
 // ---------------------------------------------------------------- transfer
 TEST(transfer_loopback_2008_2009) {
   Transfer tr;

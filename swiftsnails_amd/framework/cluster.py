@@ -78,9 +78,16 @@ class SwiftMaster:
 class SwiftServer:
     """A parameter-server shard: pull = lookup-or-init, push = optimizer apply."""
 
-    def __init__(self, config, dim: int = 1):
+    def __init__(self, config, dim: int = 1, push_method=None):
+        """``push_method``: a user-defined update rule ``fn(rows [n, width],
+        grads [n, dim]) -> new rows`` (torch tensors) instead of the
+        configured optimizer (the reference's PushAccessMethod)."""
         self.cfg = _cfg(config)
         self._s = host().Server(self.cfg.native, int(dim))
+        if push_method is not None:
+            from ..ops.host_table import set_table_push_method
+
+            set_table_push_method(self._s.table(), push_method)
 
     def __call__(self, timeout: float = 1e9):
         self._s.connect()

@@ -36,8 +36,26 @@ def _u64(keys) -> np.ndarray:
     return a.view(np.uint64) if a.dtype == np.int64 else a.astype(np.uint64)
 
 
+def set_table_push_method(native_table, fn) -> None:
+    """Install ``fn(rows, grads) -> rows`` (torch tensors) as the batch update
+    rule of a native ``_ss_host.HostTable`` (also the one inside a host-mode
+    server); ``None`` restores the optimizer menu."""
+    if fn is None:
+        native_table.set_batch_apply(None)
+        return
+
+    def batch(keys, rows, grads):
+        out = fn(torch.from_numpy(rows), torch.from_numpy(grads))
+        if isinstance(out, torch.Tensor):
+            out = out.detach().cpu().numpy()
+        return np.ascontiguousarray(out, dtype=np.float32)
+
+    native_table.set_batch_apply(batch)
+
+
 class HostTable:
     device = torch.device("cpu")
+    push_fn = None
 
     def __init__(self, dim: int, shard_num: int = 8, optimizer: Optional[Optimizer] = None,
                  init: Optional[InitConfig] = None, nthreads: int = 0):
@@ -47,6 +65,14 @@ class HostTable:
         self._t = host().HostTable(self.dim, shard_num, _host_init(self.init_cfg),
                                    _host_opt(self.opt), nthreads)
         self.width = self._t.width
+
+    def set_push_method(self, fn) -> None:
+        """User-defined update rule, as ``HbmTable.set_push_method``:
+        ``fn(rows [n, width], grads [n, dim]) -> new rows`` (torch CPU
+        tensors) applied to every push (the reference's
+        ``PushAccessMethod::apply_push_value``, batched per push call)."""
+        self.push_fn = fn
+        set_table_push_method(self._t, fn)
 
     # same surface as HbmTable where it makes sense
     def pull_keys(self, keys) -> torch.Tensor:

@@ -222,3 +222,70 @@ def test_custom_push_method_n2_server_apply():
     assert a.keys() == b.keys()
     for k in a:
         np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6)
+
+
+def test_host_table_push_method_and_cluster_server():
+    """User-defined update rule on the CPU table (batched per push, torch
+    tensors) and on a host-mode server of a real TCP cluster (the
+    reference's PushAccessMethod on its own deployment shape)."""
+    import threading
+
+    from swiftsnails_amd.framework.cluster import BaseAlgorithm, SwiftMaster, SwiftServer, SwiftWorker
+    from swiftsnails_amd.ops.host_table import HostTable
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.utils.config import Config
+    from test_transfer_cluster import _free_port
+
+    def rule(rows, g):  # sign-SGD with a push counter in the state column
+        out = rows.clone()
+        out[:, :2] -= 0.5 * torch.sign(g)
+        out[:, 2:] += 1.0
+        return out
+
+    t = HostTable(2, 3, Optimizer("adagrad"), InitConfig("zero"))
+    t.set_push_method(rule)
+    k = np.array([4, 8, 15])
+    t.push_keys(k, np.array([[1, -1], [0, 2], [-3, 0]], np.float32))
+    d = t.to_dict(with_state=True)
+    np.testing.assert_allclose(d[4], [-0.5, 0.5, 1, 1])
+    np.testing.assert_allclose(d[8], [0, -0.5, 1, 1])
+    np.testing.assert_allclose(d[15], [0.5, 0, 1, 1])
+
+    port = _free_port()
+    cfg = Config.from_dict({
+        "listen_addr": f"tcp://127.0.0.1:{port}", "master_addr": f"tcp://127.0.0.1:{port}",
+        "expected_node_num": 2, "master_time_out": 30, "init_timeout": 30, "frag_num": 16,
+        "shard_num": 2, "async_exec_num": 2, "param_backup_period": 0,
+        "param_output": "", "num_iters": 1, "learning_rate": 0.5, "optimizer": "adagrad",
+        "local_train": 0})
+    got = {}
+
+    class Alg(BaseAlgorithm):
+        def train(self):
+            keys = np.array([1, 2, 3], dtype=np.uint64)
+            self.pull(keys)
+            self.push(keys, np.array([[1, 1], [-1, 0], [0, 2]], np.float32))
+            self.push(keys, np.array([[1, 1], [-1, 0], [0, 2]], np.float32))
+            got["w"] = self.pull(keys)
+
+    master = SwiftMaster(cfg)
+    server = SwiftServer(cfg, dim=2, push_method=rule)
+    worker = SwiftWorker(cfg, Alg(), dim=2)
+    errs = []
+
+    def wrap(f):
+        def g():
+            try:
+                f()
+            except Exception as e:  # pragma: no cover - reported below
+                errs.append(e)
+        return g
+
+    ths = [threading.Thread(target=wrap(x.run)) for x in (master, server, worker)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join(60)
+    assert not errs, errs
+    np.testing.assert_allclose(got["w"], [[-1, -1], [1, 0], [0, -1]])
+    assert server.push_count == 2
