@@ -84,7 +84,9 @@ def main(argv=None):
 
     ctrans = ptrans = None
     if world > 1:
-        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+        from swiftsnails_amd.parallel.transport import default_gloo_ifname
+
+        default_gloo_ifname()
         dist.init_process_group("gloo", rank=rank, world_size=world)
         store = dist.distributed_c10d._get_default_store()
         try:

@@ -70,7 +70,9 @@ class PSContext:
         ct = pt = None
         store = None
         if self.world > 1:
-            os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+            from ..parallel.transport import default_gloo_ifname
+
+            default_gloo_ifname()
             if not dist.is_initialized():
                 timeout = float(cfg.get("init_timeout", 600))
                 import datetime

@@ -158,6 +158,18 @@ class TorchDistTransport(Transport):
         dist.barrier(group=self.group)
 
 
+def default_gloo_ifname() -> None:
+    """Bind the gloo control plane to loopback when the job is single-host
+    (every rank local — torchrun's LOCAL_WORLD_SIZE == WORLD_SIZE — or a
+    loopback MASTER_ADDR), unless the user chose an interface; a multi-host
+    job keeps gloo's own interface choice."""
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    world = os.environ.get("WORLD_SIZE", "1")
+    local = os.environ.get("LOCAL_WORLD_SIZE", world)
+    if local == world or addr in ("localhost", "::1") or addr.startswith("127."):
+        os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+
+
 @contextlib.contextmanager
 def _stdout_to_stderr():
     """Point fd 1 at fd 2 for the duration (native code writing to stdout).
