@@ -86,13 +86,6 @@ class TableFullError(RuntimeError):
     pass
 
 
-class _null_ctx:
-    def __enter__(self):
-        return self
-
-    def __exit__(self, *a):
-        return False
-
 
 class HbmTable:
     """One GPU shard of the sparse parameter table."""
@@ -241,8 +234,13 @@ class HbmTable:
 
     def apply_custom(self, slots: torch.Tensor, grads: torch.Tensor, stream=None) -> None:
         """Apply ``push_fn`` at resolved ``slots`` (unique; -1 = skipped)."""
-        st = torch.cuda.current_stream() if stream is None else stream
-        with torch.cuda.stream(st) if not isinstance(st, int) else _null_ctx():
+        if stream is None:
+            st = torch.cuda.current_stream()
+        elif isinstance(stream, int):
+            st = torch.cuda.ExternalStream(stream, device=self.device)
+        else:
+            st = stream
+        with torch.cuda.stream(st):
             s = slots.reshape(-1)
             g = grads.reshape(s.numel(), self.dim)
             ok = s >= 0
