@@ -24,6 +24,9 @@
 #include "ss_device.h"
 #include "ss_launch.h"
 
+#include <cstdlib>
+#include <string>
+
 namespace ss {
 
 static constexpr uint32_t kInv = 0xFFFFFFFFu;
@@ -218,28 +221,30 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return (unsigned short)(u >> 16);
 }
 
-template <int D>
+// POS = false: the tile's negative part only (the positive pairs run in
+// k_w2v_pos, see there); the positive-grad tile is then not allocated.
+template <int D, bool POS = true>
 struct W2vBf16Smem {
   static constexpr int PB = D + 8;    // bf16 row stride of the V / N tiles
   static constexpr int GB = kS + 8;   // bf16 row stride of the score-gradient tile
   static constexpr int P = D + 1;     // fp32 row stride of the positive-grad tile
   static constexpr size_t bytes = sizeof(unsigned short) * ((size_t)(kT + kS) * PB + (size_t)kT * GB) +
-                                  sizeof(float) * ((size_t)kT * P + kNW);
+                                  sizeof(float) * ((POS ? (size_t)kT * P : 0) + kNW);
 };
 
-template <int D>
+template <int D, bool POS = true>
 __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
     const uint32_t* __restrict__ inv_c, const uint32_t* __restrict__ inv_x,
     const uint32_t* __restrict__ inv_n, int B, int C, float neg_scale,
     const float* __restrict__ uvals, float* __restrict__ ugrad, float* __restrict__ loss_sum) {
-  using L = W2vBf16Smem<D>;
+  using L = W2vBf16Smem<D, POS>;
   constexpr int PB = L::PB, GB = L::GB, P = L::P;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
   unsigned short* Vb = smem16;            // [T][PB] center rows (bf16)
   unsigned short* Nb = Vb + kT * PB;      // [S][PB] negative rows (bf16)
   unsigned short* Gb = Nb + kS * PB;      // [T][GB] score gradients (bf16)
   float* Gv = reinterpret_cast<float*>(Gb + kT * GB);  // [T][P] positive-part center grads
-  float* red = Gv + kT * P;                             // [kNW] loss partials
+  float* red = Gv + (POS ? kT * P : 0);                 // [kNW] loss partials
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long long t0 = (long long)blockIdx.x * kT;
@@ -260,7 +265,8 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
     *reinterpret_cast<uint2*>(Vb + r * PB + d) = pv;
     *reinterpret_cast<uint2*>(Nb + r * PB + d) = pn;
   }
-  for (int e = tid; e < kT * P; e += kWG) Gv[e] = 0.f;
+  if (POS)
+    for (int e = tid; e < kT * P; e += kWG) Gv[e] = 0.f;
   __syncthreads();
 
   float loss = 0.f;
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
   }
   // ---- positive pairs (fp32): wave w owns centers [kT/kNW * w, +kT/kNW); the
   // center row comes from global with the context rows (one round trip)
-  {
+  if (POS) {
     constexpr int R = (D + 63) / 64;
     constexpr int TW = kT / kNW;
     for (int t = w * TW; t < w * TW + TW; ++t) {
@@ -367,7 +373,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
       const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
       const uint32_t dst = center ? rc[row] : rn[row];
       if (dst == kInv) continue;
-      const float v = acc[r] + (center ? Gv[row * P + col] : 0.f);
+      const float v = acc[r] + (POS && center ? Gv[row * P + col] : 0.f);
       atomicAdd(ugrad + (long long)dst * D + col, v);
     }
   }
@@ -380,6 +386,93 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
     for (int i = 0; i < kNW; ++i) tot += red[i];
     ctr_addf(loss_sum, tot);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Positive (center, context) pairs as their own kernel (SS_W2V_POS=split,
+// an experiment: measured slower, see w2v_pos_split): one wave per center.
+// Inside the tile kernel the pairs are a per-wave latency chain (8 centers
+// per wave, each an index load, then C context-row loads, then the row
+// atomics) and a 16K-center step is only 256 tiles, one 8-wave workgroup per
+// CU: 2 waves per SIMD to hide that chain.  Here the same work is 16K waves
+// of ~50 VGPRs (8 per SIMD resident), so the row gathers and the row atomics
+// of many centers are in flight at once.  The center row's gradient goes out
+// as its own row of atomics (the tile kernel then runs with POS = false).
+template <int D>
+__global__ __launch_bounds__(256) void k_w2v_pos(const uint32_t* __restrict__ inv_c,
+                                                 const uint32_t* __restrict__ inv_x, int B, int C,
+                                                 const float* __restrict__ uvals,
+                                                 float* __restrict__ ugrad,
+                                                 float* __restrict__ loss_sum) {
+  constexpr int R = (D + 63) / 64;
+  __shared__ float red[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long t = (long long)blockIdx.x * 4 + w;
+  float loss = 0.f;
+  const uint32_t c = t < B ? inv_c[t] : kInv;
+  if (c != kInv) {  // wave-uniform
+    const uint32_t xid = lane < C ? inv_x[t * C + lane] : kInv;
+    float u[kMaxC][R], v[R], gv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int d = lane + 64 * r;
+      v[r] = d < D ? uvals[(long long)c * D + d] : 0.f;
+      gv[r] = 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxC; ++j) {
+      const uint32_t x = __shfl(xid, j, 64);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        u[j][r] = (j < C && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxC; ++j) {
+      const uint32_t x = __shfl(xid, j, 64);
+      if (j >= C || x == kInv) continue;  // wave-uniform
+      float part = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) part += v[r] * u[j][r];
+      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+      const float g = sigm(part) - 1.f;  // d/ds softplus(-s)
+      if (lane == 0) loss += softplus(-part);
+      float* gu = ugrad + (long long)x * D;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        if (d < D) {
+          atomicAdd(gu + d, g * v[r]);
+          gv[r] += g * u[j][r];
+        }
+      }
+    }
+    float* gc = ugrad + (long long)c * D;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int d = lane + 64 * r;
+      if (d < D) atomicAdd(gc + d, gv[r]);
+    }
+  }
+  if (lane == 0) red[w] = loss;
+  __syncthreads();
+  if (threadIdx.x == 0 && loss_sum) ctr_addf(loss_sum, red[0] + red[1] + red[2] + red[3]);
+}
+
+// SS_W2V_POS: "split" runs the positive pairs in k_w2v_pos and the tile
+// kernel on the negative part only; "fused" (default) keeps them in the tile
+// kernel.  Measured (1M vocab, dim 128, 16K centers): split 0.342-0.346
+// ms/step vs fused 0.307; k_w2v_pos alone takes 142-168 us, as long as the
+// whole fused tile kernel: the pairs are bound by the memory-side rate of
+// their ~92 MB of row atomics (~1.3 TB/s, MI355X_MICROARCH.md "Global float
+// atomics"), not by the tile kernel's occupancy
+static bool w2v_pos_split() {
+  static const bool v = [] {
+    const char* e = std::getenv("SS_W2V_POS");
+    return e && std::string(e) == "split";
+  }();
+  return v;
 }
 
 // Context-row gradients without global atomics (the sgns kernel's positive
@@ -528,6 +621,23 @@ size_t w2v_smem_bytes(int D) {
   return sizeof(float) * ((size_t)3 * kT * P + (size_t)kT * (kS + 1) + kNW);
 }
 
+template <int D>
+static void launch_w2v_bf16(bool split, int tiles, const uint32_t* inv_c, const uint32_t* inv_x,
+                            const uint32_t* inv_n, int B, int C, float neg_scale,
+                            const float* uvals, float* ugrad, float* loss_sum, hipStream_t st) {
+  if (split) {
+    hipLaunchKernelGGL(k_w2v_pos<D>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, inv_c, inv_x,
+                       B, C, uvals, ugrad, loss_sum);
+    check_launch("k_w2v_pos");
+  }
+  auto k = split ? k_w2v_sgns_bf16<D, false> : k_w2v_sgns_bf16<D, true>;
+  const size_t sm = split ? W2vBf16Smem<D, false>::bytes : W2vBf16Smem<D, true>::bytes;
+  check_hip(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm),
+            "w2v bf16 smem attr");
+  hipLaunchKernelGGL(k, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, neg_scale, uvals,
+                     ugrad, loss_sum);
+}
+
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
                      float* loss_sum, hipStream_t st, float* gpos, int bf16) {
@@ -536,15 +646,13 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
   const int tiles = (B + kT - 1) / kT;
   if (bf16) {
     if (gpos) throw_error("w2v_sgns: the bf16 tile has no context-reduce output");
+    // bf16: 1 = positive pairs as SS_W2V_POS says, 2 = split, 3 = fused
+    const bool split = bf16 == 2 ? true : bf16 == 3 ? false : w2v_pos_split();
     switch (D) {
 #define SS_W2VB_CASE(DD)                                                                     \
   case DD:                                                                                   \
-    check_hip(hipFuncSetAttribute((const void*)k_w2v_sgns_bf16<DD>,                           \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,                \
-                                  (int)W2vBf16Smem<DD>::bytes),                              \
-              "w2v bf16 smem attr");                                                         \
-    hipLaunchKernelGGL(k_w2v_sgns_bf16<DD>, dim3(tiles), dim3(kWG), W2vBf16Smem<DD>::bytes, st, \
-                       inv_c, inv_x, inv_n, B, C, neg_scale, uvals, ugrad, loss_sum);        \
+    launch_w2v_bf16<DD>(split, tiles, inv_c, inv_x, inv_n, B, C, neg_scale, uvals, ugrad,    \
+                        loss_sum, st);                                                       \
     break;
       SS_W2VB_CASE(32)
       SS_W2VB_CASE(64)

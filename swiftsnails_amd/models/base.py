@@ -160,6 +160,13 @@ class PipelinedWorker:
         self.loss_sum.zero_()
         if self.active:
             self._compute(rnd, rnd.slot, torch.cuda.current_stream().cuda_stream)
+        if getattr(eng, "push_on_pull", False):
+            # push(i) goes on the pull stream behind pull(i+1) (engine.push_on_pull)
+            self._cur = eng.pull_ahead_round(self._next)
+            eng.push(rnd)
+            self._next = self._route(self.step_idx + 2)
+            self.step_idx += 1
+            return self.loss_sum
         eng.push(rnd)
         if self._route_first:
             # route round i+2 before the host blocks on round i+1's counts

@@ -244,6 +244,18 @@ class PSEngine:
         # network while the route stream dedups and the main stream computes
         self.pull_stream = (torch.cuda.Stream(device=self.device)
                             if self.pull_ahead and self.pt is not self.ct else None)
+        # push on the pull stream (N>1 with a pull stream, SS_PUSH_STREAM=pull):
+        # round i's gradient all-to-all-v and server apply are enqueued on the
+        # pull stream right behind round i+1's pull (the worker calls
+        # pull_ahead_round(i+1) before push(i)).  The main stream is then left
+        # with the model's forward + merge, the pull stream carries lookup +
+        # apply, and pull(i+2) still sees apply(i) (same stream): the same
+        # staleness-1 schedule with the apply off the compute chain.  Measured
+        # (N>1 path on one GPU, three A/B pairs) 1.049-1.053 -> 1.058-1.103
+        # ms/step: every stream shares the chip's memory system, and the route
+        # stream's dedup, which the next pull waits for, stays the chain; off
+        self.push_on_pull = (self.pull_stream is not None and
+                             os.environ.get("SS_PUSH_STREAM", "main") == "pull")
         # occurrence-space unique ids (enable_osi): the model indexes rows
         # with the dedup's own inverse (bstart[b] + l), see ops/dedup.py
         self.osi = False
@@ -525,6 +537,18 @@ class PSEngine:
                 tab.push_slots(rnd.slots, g, segs=tab.dev_segs(rnd.dd.ucount),
                                max_n=max(1, min(rnd.dd.n, rnd.dd.ucap)), snap=snap)
             tab.next_round()
+        elif self.push_on_pull:
+            D, ps = self.displs, self.pull_stream
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream())  # the merged gradients
+            ps.wait_event(ev)
+            with torch.cuda.stream(ps):
+                self.pt.alltoallv(g, rnd.scounts, D, self.rgrads, rnd.rcounts, D, self.dim)
+                self._server_apply(rnd.rcounts, rnd.slot, resolved=True)
+                self._release(rnd.slot)  # the slot is free once the apply has read it
+            rnd.pushed = True
+            self.rounds += 1
+            return
         else:
             D = self.displs
             self.t.alltoallv(g, rnd.scounts, D, self.rgrads, rnd.rcounts, D, self.dim)

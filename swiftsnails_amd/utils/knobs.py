@@ -107,6 +107,13 @@ KNOBS: dict[str, Knob] = {
     "SS_W2V_CTX": Knob("atomic", "models/word2vec.py", "experiment",
                        "reduce: context gradients merged per key over the dedup buckets "
                        "(0.32 -> 0.81 ms/step)"),
+    "SS_PUSH_STREAM": Knob("main", "parallel/engine.py", "experiment",
+                           "pull: N>1 gradient exchange + server apply on the pull stream "
+                           "behind the next round's pull (1.049-1.053 -> 1.058-1.103 ms/step: "
+                           "the route stream's dedup, sharing the chip, stays the chain)"),
+    "SS_W2V_POS": Knob("fused", "csrc/hip/w2v.hip", "experiment",
+                       "split: positive pairs in their own one-wave-per-center kernel "
+                       "(0.307 -> 0.344 ms/step: atomic-rate bound, not occupancy bound)"),
     "SS_ROUTE_CUS": Knob("0 (all)", "parallel/engine.py", "experiment",
                          "route stream on a CU-masked stream of k CUs (measured 0.97 -> "
                          "1.17-1.20 ms/step for k = 64..192 of 256)"),
