@@ -104,6 +104,7 @@ class PSContext:
         self.backup_root = cfg.get("param_backup_root", ".")
         self.ckpt_format = cfg.get("checkpoint_format", "bin")
         self.tracer = Tracer(enabled=str(cfg.get("trace", "0")) not in ("0", "false"))
+        self.engine.tracer = self.tracer  # per-phase ranges: route / pull / compute / push
         # failure detection (parallel/watchdog.py): round watchdog + heartbeats
         self.failure = FailureHandler(exit_process=str(cfg.get("watchdog_exit", "1")) != "0")
         for t in (tr, ct, pt):
@@ -287,7 +288,7 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     ctx.barrier()
     t0 = time.perf_counter()
     for i in range(steps):
-        with ctx.tracer.range(f"step{i}"):
+        with ctx.tracer.range("step"):
             w.step()
         ctx.round_done(w.step_idx)
         ctx.maybe_backup(w.rounds_done())
@@ -312,6 +313,8 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     m = ctx.engine.metrics.counters
     if m:
         stats["rank0_engine"] = {k: int(v) for k, v in m.items()}
+    if ctx.tracer.enabled:
+        stats["trace"] = ctx.tracer.summary()
     if ctx.table is not None and str(cfg.get("table_stats", "1")) != "0":
         stats["rank0_table"] = ctx.table.stats()
     ctx.finish()

@@ -142,7 +142,8 @@ class PipelinedWorker:
         rnd = self.engine.pull(r)
         self.loss_sum.zero_()
         if self.active:
-            self._compute(rnd, r.slot, torch.cuda.current_stream().cuda_stream)
+            with self.engine.trace("compute"):
+                self._compute(rnd, r.slot, torch.cuda.current_stream().cuda_stream)
         self.engine.push(rnd)
         self.step_idx += 1
         return self.loss_sum
@@ -159,7 +160,8 @@ class PipelinedWorker:
         eng.begin(rnd)
         self.loss_sum.zero_()
         if self.active:
-            self._compute(rnd, rnd.slot, torch.cuda.current_stream().cuda_stream)
+            with eng.trace("compute"):
+                self._compute(rnd, rnd.slot, torch.cuda.current_stream().cuda_stream)
         if getattr(eng, "push_on_pull", False):
             # push(i) goes on the pull stream behind pull(i+1) (engine.push_on_pull)
             self._cur = eng.pull_ahead_round(self._next)

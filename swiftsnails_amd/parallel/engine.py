@@ -43,6 +43,7 @@ transport) — that is how the multi-rank logic is tested without GPUs.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 from dataclasses import dataclass, field
@@ -174,9 +175,13 @@ class PSEngine:
         # observability: occurrences routed, unique keys exchanged,
         # alltoallv payload bytes (host-known counts; world-1 keeps counts on
         # the device and only counts occurrences)
-        from ..utils.tracing import Metrics
+        from ..utils.tracing import Metrics, Tracer
 
         self.metrics = Metrics()
+        # per-phase roctx ranges + HIP-event device times (route / pull /
+        # push, and the model's compute); a disabled tracer unless the job
+        # sets `trace: 1` (framework/gpu.py hands its tracer over)
+        self.tracer = Tracer(enabled=False)
         # SS_ENGINE_GENERAL=1 runs a 1-GPU job through the N>1 code path
         # (send segments, count exchange, server-side segment pull/apply): the
         # per-rank cost of the multi-GPU pipeline without the network
@@ -284,6 +289,15 @@ class PSEngine:
         if ev is not None and tag == self.capture_tag:
             stream.wait_event(ev)
 
+    def trace(self, name: str, stream=None):
+        """A phase range of the tracer: roctx + host time, plus the device
+        time between two HIP events on ``stream`` (GPU).  A no-op when the
+        tracer is off and inside a hipGraph capture."""
+        t = self.tracer
+        if not t.enabled or self.capture_tag is not None:
+            return contextlib.nullcontext()
+        return t.gpu_range(name, stream) if self.gpu else t.range(name)
+
     def enable_osi(self) -> bool:
         """Switch the dedupers to occurrence-space unique ids (bucketed dedup
         with CAS inserts on GPU only): the dedup kernel writes the inverse
@@ -328,12 +342,13 @@ class PSEngine:
         self._next_slot = (slot + 1) % self.depth
         dd_fn = self.dedupers[slot]
         if not self.gpu:
-            if produce is not None:
-                keys = produce(None)
-            keys = keys.reshape(-1).to(self.device)
-            dd = dd_fn(keys)
-            counts = None if self.world == 1 and self.fast1 else self.ct.exchange_counts_async(
-                dd.ucount)
+            with self.trace("route"):
+                if produce is not None:
+                    keys = produce(None)
+                keys = keys.reshape(-1).to(self.device)
+                dd = dd_fn(keys)
+                counts = None if self.world == 1 and self.fast1 else \
+                    self.ct.exchange_counts_async(dd.ucount)
             return Routed(dd, slot, counts)
         rs = self.route_stream
         main = torch.cuda.current_stream()
@@ -343,7 +358,7 @@ class PSEngine:
             self._wait(rs, self._free[slot], self._free_tag[slot])
         if keys is not None and self.capture_tag is None:
             rs.wait_stream(main)             # keys were produced on the main stream
-        with torch.cuda.stream(rs):
+        with torch.cuda.stream(rs), self.trace("route", rs):
             if produce is not None:
                 keys = produce(rs)
             keys = keys.reshape(-1)
@@ -377,6 +392,10 @@ class PSEngine:
 
     def pull(self, keys_or_routed) -> Round:
         r = keys_or_routed if isinstance(keys_or_routed, Routed) else self.route(keys_or_routed)
+        with self.trace("pull"):
+            return self._pull(r)
+
+    def _pull(self, r: Routed) -> Round:
         dd, slot = r.dd, r.slot
         if self.gpu:
             self._wait(torch.cuda.current_stream(), r.ready, r.tag)
@@ -419,7 +438,7 @@ class PSEngine:
         dd, slot = r.dd, r.slot
         if self.fast1:  # one GPU: pull right behind the dedup on the route stream
             rs, uv, tab = self.route_stream, self.uvals[slot], self.table
-            with torch.cuda.stream(rs):
+            with torch.cuda.stream(rs), self.trace("pull", rs):
                 own = dd.owner
                 if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
                     tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi)
@@ -435,7 +454,7 @@ class PSEngine:
         ps = self.pull_stream or self.route_stream
         if ps is not self.route_stream:
             self._wait(ps, r.ready, r.tag)
-        with torch.cuda.stream(ps):
+        with torch.cuda.stream(ps), self.trace("pull", ps):
             self.pt.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
             self._server_pull(rcounts, slot)
             self.pt.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
@@ -515,6 +534,10 @@ class PSEngine:
         return args
 
     def push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
+        with self.trace("push", self.pull_stream if self.push_on_pull else None):
+            self._push(rnd, grads)
+
+    def _push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
         g = rnd.ugrad if grads is None else grads
         tab = self.table
         if self.fast1 and rnd.applied:

@@ -135,6 +135,27 @@ def test_engine_world1_cpu_push_keys_and_pull_dense():
     np.testing.assert_allclose(v, [-3, -2, -3, -1, -2, -3])
 
 
+def test_engine_phase_tracing_cpu():
+    """trace: 1 — the engine's route / pull / push phases land in the tracer
+    (roctx ranges + host time; device time on GPU)."""
+    from swiftsnails_amd.ops.host_table import HostTable
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.utils.tracing import Tracer
+
+    t = HostTable(2, 2, Optimizer("sgd", lr=1.0), InitConfig("zero"))
+    eng = PSEngine(t, None, max_keys=100, dim=2, device="cpu")
+    eng.pull_dense(torch.tensor([1, 2, 3]))  # tracer off: nothing recorded, no error
+    eng.tracer = Tracer(enabled=True, roctx=False)
+    k = torch.tensor([5, 7, 5])
+    for _ in range(3):
+        rnd = eng.pull(k)
+        eng.push(rnd)
+    s = eng.tracer.summary()
+    assert s["calls"]["route"] == 3 and s["calls"]["pull"] == 3 and s["calls"]["push"] == 3
+    assert all(s["host_s"][k] >= 0 for k in ("route", "pull", "push"))
+
+
 def test_effective_ndest_counts_receiving_servers():
     """Bucketed dedup sizing: buckets per destination come from
     the servers that actually receive keys, not the world size."""

@@ -73,6 +73,23 @@ def test_cli_gpu_sparse_lr_backup_and_resume(tmp_path):
     assert (tmp_path / "param-10.shard0-of-1.bin").exists()  # written again at round 10
 
 
+@pytest.mark.gpu
+def test_cli_gpu_trace_phases(tmp_path):
+    """`trace: 1`: per-phase device times (route / pull / compute / push, HIP
+    events on the stream each phase runs on) in the job's stats line."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "swiftsnails_amd.launch", "--config",
+                        os.path.join(ROOT, "configs", "sparse_lr_10m.conf"), "--steps", "6",
+                        "--set", "batch_size=4096", "--set", "num_features=1000000",
+                        "--set", "trace=1", "--set", "table_stats=0"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    tr = json.loads(r.stdout.strip().splitlines()[-1])["trace"]
+    for ph in ("route", "pull", "compute", "push"):
+        assert tr["calls"][ph] >= 6 and tr["gpu_s"][ph] > 0, (ph, tr)
+    assert tr["calls"]["step"] == 6
+
+
 def test_cluster_script_two_servers_two_workers(tmp_path):
     """tools/cluster_test.sh: master + 2 servers + 2 workers as processes; each
     server dumps its own shard, together covering every key exactly once."""
