@@ -249,6 +249,16 @@ PYBIND11_MODULE(_ss_hip, m) {
                      step_add, P<uint64_t>(out_keys), P<float>(out_vals), P<float>(out_labels),
                      S(st));
   });
+  m.def("w2v_corpus_window", [](uintptr_t tokens, uintptr_t sent_of, long long nsent,
+                                uintptr_t table, long long table_size, uintptr_t keep, long long N,
+                                uint64_t seed, long long step, uintptr_t step_dev,
+                                long long step_add, int B, int W, long long nneg, uint64_t out_bit,
+                                uintptr_t keys, uintptr_t meta, uintptr_t st) {
+    launch_w2v_corpus_window(P<const uint64_t>(tokens), P<const uint32_t>(sent_of), nsent,
+                             P<const uint64_t>(table), table_size, P<const float>(keep), N, seed,
+                             step, P<const long long>(step_dev), step_add, B, W, nneg, out_bit,
+                             P<uint64_t>(keys), P<int32_t>(meta), S(st));
+  });
   m.def("w2v_corpus_batch", [](uintptr_t tokens, uintptr_t sent_offs, uintptr_t sent_of,
                                uintptr_t table, long long table_size, uintptr_t keep, long long N,
                                uint64_t seed, long long step, uintptr_t step_dev,
@@ -395,6 +405,22 @@ PYBIND11_MODULE(_ss_hip, m) {
                           P<const uint32_t>(inv_c), P<const float>(gpos), B, C, D,
                           P<const float>(uvals), P<float>(ugrad), S(st));
   });
+  m.def("w2v_win", [](uintptr_t inv_c, uintptr_t inv_w, uintptr_t inv_n, uintptr_t meta, int B,
+                      int W, int D, float neg_per_pair, uintptr_t uvals, uintptr_t ugrad,
+                      uintptr_t loss, uintptr_t pairs, uintptr_t st) {
+    launch_w2v_win(P<const uint32_t>(inv_c), P<const uint32_t>(inv_w), P<const uint32_t>(inv_n),
+                   P<const int32_t>(meta), B, W, D, neg_per_pair, P<const float>(uvals),
+                   P<float>(ugrad), P<float>(loss), P<float>(pairs), S(st));
+  });
+  m.def("w2v_stream_gen", [](uint64_t seed, long long base, int B, int W, int L, long long nneg,
+                             long long V, float noise, uintptr_t keys, uintptr_t meta, uintptr_t st,
+                             uintptr_t step_dev, long long step_mul, long long step_add) {
+    launch_w2v_stream_gen(seed, base, B, W, L, nneg, V, noise, P<uint64_t>(keys),
+                          P<int32_t>(meta), S(st), P<const long long>(step_dev), step_mul,
+                          step_add);
+  }, py::arg("seed"), py::arg("base"), py::arg("B"), py::arg("W"), py::arg("L"),
+     py::arg("nneg"), py::arg("V"), py::arg("noise"), py::arg("keys"), py::arg("meta"),
+     py::arg("st"), py::arg("step_dev") = 0, py::arg("step_mul") = 0, py::arg("step_add") = 0);
   m.def("w2v_gen", [](uint64_t seed, long long base, int B, int C, int W, long long nneg,
                       long long V, float noise, uintptr_t keys, uintptr_t st, uintptr_t step_dev,
                       long long step_mul, long long step_add) {

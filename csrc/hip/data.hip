@@ -10,6 +10,7 @@
 // a host fill + 82 MB PCIe copy per step (batch 262144 x 39).
 #include "ss_device.h"
 #include "ss_launch.h"
+#include "ss/w2v_window.h"
 
 namespace ss {
 
@@ -111,6 +112,62 @@ void launch_w2v_corpus_batch(const uint64_t* tokens, const uint64_t* sent_offs,
                      (unsigned long long)N, seed, (unsigned long long)step, step_dev, step_add, B,
                      C, W, nneg, out_bit, keys);
   check_launch("k_w2v_corpus_batch");
+}
+
+// Windowed skip-gram runs from the resident corpus (layout: ss/w2v_window.h).
+// Step `st` of this rank reads the run of B + 2W stream positions starting at
+// st * B - W (mod N: the rank's corpus shard is cycled epoch after epoch, so
+// consecutive steps walk it in order and every token is a center once per
+// epoch).  A position's sentence tag is its sentence index plus the lap's
+// offset (positions of different laps never pair), its reduced window and
+// sub-sampling decision are hashes of its stream position: the host batcher
+// (Corpus::fill_skipgram_window) produces the same batch bit for bit.
+__global__ __launch_bounds__(256) void k_w2v_corpus_window(
+    const uint64_t* __restrict__ tokens, const uint32_t* __restrict__ sent_of,
+    unsigned long long nsent, const uint64_t* __restrict__ table, unsigned long long table_mask,
+    const float* __restrict__ keep, unsigned long long N, uint64_t seed, unsigned long long step,
+    const long long* __restrict__ step_dev, long long step_add, int B, int W, long long nneg,
+    uint64_t out_bit, uint64_t* __restrict__ keys, int32_t* __restrict__ meta) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  const uint64_t st = step_dev ? (uint64_t)(*step_dev + step_add) : (uint64_t)step;
+  const long long R = (long long)B + 2 * W;
+  if (i < R) {
+    const long long x = (long long)((st * (uint64_t)B) % N) - W + i;  // stream position
+    const long long n = (long long)N;
+    const long long lap = x >= 0 ? x / n : -((-x + n - 1) / n);
+    const long long idx = x - lap * n;
+    const uint64_t tok = tokens[idx];
+    int32_t m = w2v_meta((uint64_t)sent_of[idx] + (uint64_t)(lap + 1) * nsent,
+                         w2v_reduced_window(seed, (uint64_t)x, W));
+    if (keep && !w2v_keep(seed, st, (uint64_t)x, keep[idx])) m = -1;
+    keys[B + i] = tok | out_bit;
+    meta[i] = m;
+    if (i >= W && i < W + B) keys[i - W] = tok;
+  } else if (i < R + nneg) {
+    const long long q = i - R;
+    const uint64_t r = splitmix64(seed ^ 0xBADC0DEull ^ (st * 0xD1B54A32D192ED03ull) ^
+                                  (uint64_t)q * 0x9E37ull);
+    keys[B + R + q] = table[r & table_mask] | out_bit;
+  }
+}
+
+void launch_w2v_corpus_window(const uint64_t* tokens, const uint32_t* sent_of, long long nsent,
+                              const uint64_t* table, long long table_size, const float* keep,
+                              long long N, uint64_t seed, long long step,
+                              const long long* step_dev, long long step_add, int B, int W,
+                              long long nneg, uint64_t out_bit, uint64_t* keys, int32_t* meta,
+                              hipStream_t st) {
+  if (N <= 0) throw_error("w2v_corpus_window: empty corpus");
+  if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_corpus_window: window must be in [1, 15]");
+  if (table_size <= 0 || (table_size & (table_size - 1)) != 0)
+    throw_error("w2v_corpus_window: noise table size must be a power of two");
+  const long long n = (long long)B + 2 * W + nneg;
+  if (B <= 0) return;
+  hipLaunchKernelGGL(k_w2v_corpus_window, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     tokens, sent_of, (unsigned long long)nsent, table,
+                     (unsigned long long)(table_size - 1), keep, (unsigned long long)N, seed,
+                     (unsigned long long)step, step_dev, step_add, B, W, nneg, out_bit, keys, meta);
+  check_launch("k_w2v_corpus_window");
 }
 
 void launch_csr_batch(const uint64_t* offs, const uint64_t* keys, const float* vals,

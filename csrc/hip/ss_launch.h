@@ -87,6 +87,20 @@ void launch_csr_batch(const uint64_t* offs, const uint64_t* keys, const float* v
                       const float* labels, long long rows, long long cursor, int B, int F,
                       const long long* step_dev, long long step_add, uint64_t* out_keys,
                       float* out_vals, float* out_labels, hipStream_t st);
+void launch_w2v_corpus_window(const uint64_t* tokens, const uint32_t* sent_of, long long nsent,
+                              const uint64_t* table, long long table_size, const float* keep,
+                              long long N, uint64_t seed, long long step,
+                              const long long* step_dev, long long step_add, int B, int W,
+                              long long nneg, uint64_t out_bit, uint64_t* keys, int32_t* meta,
+                              hipStream_t st);
+void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
+                    const int32_t* meta, int B, int W, int D, float neg_per_pair,
+                    const float* uvals, float* ugrad, float* loss_sum, float* pair_sum,
+                    hipStream_t st);
+void launch_w2v_stream_gen(uint64_t seed, long long base, int B, int W, int L, long long nneg,
+                           long long V, float noise, uint64_t* keys, int32_t* meta,
+                           hipStream_t st, const long long* step_dev, long long step_mul,
+                           long long step_add);
 void launch_w2v_corpus_batch(const uint64_t* tokens, const uint64_t* sent_offs,
                              const uint32_t* sent_of, const uint64_t* table, long long table_size,
                              const float* keep, long long N, uint64_t seed, long long step,

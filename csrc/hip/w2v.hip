@@ -23,7 +23,9 @@
 //     128-B row segments (the full-rate atomic shape on MI355X).
 #include "ss_device.h"
 #include "ss_launch.h"
+#include "ss/w2v_window.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include <string>
 
@@ -575,6 +577,13 @@ __global__ __launch_bounds__(256) void k_w2v_ctx_reduce(const uint32_t* __restri
   }
 }
 
+// log-uniform ("Zipf-like") word id in [0, V) from a 64-bit hash
+__device__ __forceinline__ uint64_t w2v_zipf(uint64_t r, long long V, double logV) {
+  const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+  long long v = (long long)exp(u * logV) - 1;
+  return (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
+}
+
 // Synthetic skip-gram batches. Centers are Zipf-like (log-uniform) over V
 // words; a context sits within +-W ids of its center (words with nearby ids
 // co-occur: learnable structure) except with probability `noise`; negatives
@@ -589,11 +598,7 @@ __global__ __launch_bounds__(256) void k_w2v_gen(uint64_t seed, long long base, 
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const long long n = (long long)B + (long long)B * C + nneg;
   if (i >= n) return;
-  auto zipf = [&](uint64_t r) -> uint64_t {
-    const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
-    long long v = (long long)exp(u * logV) - 1;
-    return (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
-  };
+  auto zipf = [&](uint64_t r) -> uint64_t { return w2v_zipf(r, V, logV); };
   const uint64_t kOut = 1ull << 40;
   if (i < B) {
     keys[i] = zipf(splitmix64(seed ^ ((uint64_t)(base + i) * 0xA24BAED4963EE407ull)));
@@ -616,9 +621,257 @@ __global__ __launch_bounds__(256) void k_w2v_gen(uint64_t seed, long long base, 
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Windowed skip-gram tile: the batch layout of ss/w2v_window.h (a run of
+// B + 2W consecutive stream positions; centers are the middle B, contexts
+// are the neighbouring positions of the run).  One 512-thread workgroup per
+// tile of T = 64 consecutive centers; the tile's window rows are the 64 + 2W
+// run positions around them (padded to kWU = 96), so the positive pairs are a
+// band of the 64 x 96 score matrix and the whole tile is five small GEMMs on
+// the bf16 MFMA (fp32 accumulate):
+//     S+ = V·Uᵀ (64 x 96)   S- = V·Nᵀ (64 x 64)            scores
+//     gV = G+·U + G-·N      gU = G+ᵀ·V (96 x D)   gN = G-ᵀ·V  gradients
+// G+ is σ(s) - 1 on the band's valid pairs (same sentence, |Δ| <= the
+// center's reduced window, both positions unmasked) and 0 elsewhere; G- is
+// σ(s) weighted n_t·K/S for a center with n_t pairs (each pair's K negatives
+// drawn from the tile's S shared ones).  A context row now leaves the tile
+// once (96 row atomics per tile) instead of once per pair (640 at W = 5 in
+// the pairs layout), and the batch carries B + 2W context keys instead of
+// 2W·B: the dedup, pull and apply of a step shrink with it.
+static constexpr int kWU = 96;  // window rows per tile: 64 + 2W (W <= 15), 3 x 32
+
+template <int D>
+struct W2vWinSmem {
+  static constexpr int PB = D + 8;     // bf16 row stride of the V / U / N tiles
+  static constexpr int GPB = kWU + 8;  // bf16 row stride of G+
+  static constexpr int GB = kS + 8;    // bf16 row stride of G-
+  static constexpr size_t bytes =
+      sizeof(unsigned short) * ((size_t)(kT + kWU + kS) * PB + (size_t)kT * GPB + (size_t)kT * GB);
+};
+
+template <int D>
+__global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
+    const uint32_t* __restrict__ inv_c, const uint32_t* __restrict__ inv_w,
+    const uint32_t* __restrict__ inv_n, const int32_t* __restrict__ meta, int B, int W,
+    float neg_per_pair, const float* __restrict__ uvals, float* __restrict__ ugrad,
+    float* __restrict__ loss_sum, float* __restrict__ pair_sum) {
+  using L = W2vWinSmem<D>;
+  constexpr int PB = L::PB, GPB = L::GPB, GB = L::GB, TJ = D / 32;
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
+  unsigned short* Vb = smem16;         // [T][PB]   center rows (syn0), bf16
+  unsigned short* Ub = Vb + kT * PB;   // [kWU][PB] window rows (syn1neg): rows 0.. = run positions t0..
+  unsigned short* Nb = Ub + kWU * PB;  // [S][PB]   shared negatives (syn1neg)
+  unsigned short* Gp = Nb + kS * PB;   // [T][GPB]  G+
+  unsigned short* Gn = Gp + kT * GPB;  // [T][GB]   G-
+  __shared__ uint32_t rc[kT], rw[kWU], rn[kS];
+  __shared__ int32_t mw[kWU];
+  __shared__ int uany[kWU];
+  __shared__ float cwt[kT];  // n_t * K / S
+  __shared__ float red[kNW];
+
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const long long R = (long long)B + 2 * W;
+  const int ntiles = (B + kT - 1) / kT;
+  float loss = 0.f, npairs = 0.f;
+  // a grid smaller than the tile count walks tiles (SS_W2V_WIN_GRID: leaves
+  // CUs to the route stream's kernels)
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long t0 = (long long)tile * kT;  // first center; its run position is t0 + W
+    if (tid < kWU) {  // window row l = run position t0 + l
+      const long long q = t0 + tid;
+      const bool in = tid < kT + 2 * W && q < R;
+      const int32_t m = in ? meta[q] : -1;
+      mw[tid] = m;
+      rw[tid] = m >= 0 ? inv_w[q] : kInv;
+      uany[tid] = 0;
+    } else if (tid < kWU + kS) {
+      rn[tid - kWU] = inv_n[(long long)tile * kS + (tid - kWU)];
+    }
+    __syncthreads();
+    if (tid < kT) {  // center t sits at window row t + W
+      const int32_t mc = mw[tid + W];
+      const bool ok = t0 + tid < B && mc >= 0;
+      int n = 0;
+      if (ok)
+        for (int dq = -W; dq <= W; ++dq) n += w2v_pair_ok(mc, mw[tid + W + dq], dq) ? 1 : 0;
+      rc[tid] = ok && n > 0 ? inv_c[t0 + tid] : kInv;  // a center without pairs does not train
+      cwt[tid] = (float)n * neg_per_pair;
+      npairs += (float)n;
+    }
+    // rows -> bf16 tiles (V, U, N are consecutive rows of stride PB)
+    for (int e = tid; e < (kT + kWU + kS) * (D / 4); e += kWG) {
+      const int r = e / (D / 4), d = 4 * (e - r * (D / 4));
+      uint32_t id;
+      if (r < kT) {
+        const long long c = t0 + r;  // read inv_c directly: rc[] is written by this same phase
+        id = (c < B && mw[r + W] >= 0) ? inv_c[c] : kInv;
+      } else {
+        id = r < kT + kWU ? rw[r - kT] : rn[r - kT - kWU];
+      }
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (id != kInv) v = *reinterpret_cast<const float4*>(uvals + (long long)id * D + d);
+      *reinterpret_cast<uint2*>(smem16 + r * PB + d) =
+          make_uint2(f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16), f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+    }
+    __syncthreads();
+
+    const int r32 = lane & 31, h = lane >> 5;
+    // ---- scores: 6 tiles of S+ (2 x 3) and 4 of S- (2 x 2)
+    for (int k = w; k < 10; k += kNW) {
+      const bool pos = k < 6;
+      const int ti = pos ? k / 3 : (k - 6) >> 1, tj = pos ? k % 3 : (k - 6) & 1;
+      const unsigned short* Bm = pos ? Ub : Nb;
+      f32x16 acc = {};
+#pragma unroll
+      for (int k0 = 0; k0 < D; k0 += 16) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Vb + (ti * 32 + r32) * PB + k0 + 8 * h);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bm + (tj * 32 + r32) * PB + k0 + 8 * h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
+        const float sc = acc[r];
+        if (pos) {
+          const bool ok = rc[row] != kInv && rw[col] != kInv &&
+                          w2v_pair_ok(mw[row + W], mw[col], col - (row + W));
+          Gp[row * GPB + col] = f2bf(ok ? sigm(sc) - 1.f : 0.f);  // d/ds softplus(-s)
+          if (ok) {
+            loss += softplus(-sc);
+            uany[col] = 1;
+          }
+        } else {
+          const bool ok = rc[row] != kInv && rn[col] != kInv;
+          const float cw = cwt[row];
+          Gn[row * GB + col] = f2bf(ok ? cw * sigm(sc) : 0.f);  // d/ds softplus(s), weighted
+          if (ok) loss += cw * softplus(sc);
+        }
+      }
+    }
+    __syncthreads();
+    // ---- gradients: gV (2 x TJ tiles), gU (3 x TJ), gN (2 x TJ)
+    for (int tt = w; tt < 7 * TJ; tt += kNW) {
+      const int kind = tt < 2 * TJ ? 0 : (tt < 5 * TJ ? 1 : 2);
+      const int q = tt - (kind == 0 ? 0 : (kind == 1 ? 2 * TJ : 5 * TJ));
+      const int ti = q / TJ, tj = q % TJ;
+      f32x16 acc = {};
+      if (kind == 0) {  // gV = G+·U (K = window rows) + G-·N (K = negatives)
+#pragma unroll
+        for (int k0 = 0; k0 < kWU; k0 += 16) {
+          const int kb = k0 + 8 * h;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(Gp + (ti * 32 + r32) * GPB + kb);
+          bf16x8 b;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[j] = (short)Ub[(kb + j) * PB + tj * 32 + r32];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k0 = 0; k0 < kS; k0 += 16) {
+          const int kb = k0 + 8 * h;
+          const bf16x8 a = *reinterpret_cast<const bf16x8*>(Gn + (ti * 32 + r32) * GB + kb);
+          bf16x8 b;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[j] = (short)Nb[(kb + j) * PB + tj * 32 + r32];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        }
+      } else {  // gU = G+ᵀ·V, gN = G-ᵀ·V (K = centers)
+        const unsigned short* G = kind == 1 ? Gp : Gn;
+        const int GS = kind == 1 ? GPB : GB;
+#pragma unroll
+        for (int k0 = 0; k0 < kT; k0 += 16) {
+          const int kb = k0 + 8 * h;
+          bf16x8 a, b;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            a[j] = (short)G[(kb + j) * GS + ti * 32 + r32];
+            b[j] = (short)Vb[(kb + j) * PB + tj * 32 + r32];
+          }
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
+        const uint32_t dst = kind == 0 ? rc[row] : (kind == 1 ? (uany[row] ? rw[row] : kInv) : rn[row]);
+        if (dst == kInv) continue;  // lanes 0-31 / 32-63: one 128-B row segment each
+        atomicAdd(ugrad + (long long)dst * D + col, acc[r]);
+      }
+    }
+    __syncthreads();  // the next tile overwrites the LDS tiles
+  }
+  for (int o = 32; o > 0; o >>= 1) loss += __shfl_down(loss, o, 64);
+  if (lane == 0) red[w] = loss;
+  __syncthreads();
+  if (tid == 0 && loss_sum) {
+    float tot = 0.f;
+#pragma unroll
+    for (int i = 0; i < kNW; ++i) tot += red[i];
+    ctr_addf(loss_sum, tot);
+  }
+  if (w == 0 && pair_sum) {  // centers' pair counts live in wave 0 (tid < kT)
+    for (int o = 32; o > 0; o >>= 1) npairs += __shfl_down(npairs, o, 64);
+    if (lane == 0) ctr_addf(pair_sum, npairs);  // valid positive pairs
+  }
+}
+
+// Synthetic token stream in the windowed layout: sentences of L tokens, each
+// around a Zipf-drawn topic word (a token is the topic +- W ids, or with
+// probability `noise` an independent Zipf word), so words with nearby ids
+// co-occur — the learnable structure of k_w2v_gen, as a stream.  Position g
+// of the rank's stream is a pure function of (seed, g): consecutive runs
+// (base = (step * world + rank) * B) overlap by 2W positions consistently.
+// keys = [centers B][run positions B + 2W | 1<<40][negatives nneg | 1<<40].
+__global__ __launch_bounds__(256) void k_w2v_stream_gen(
+    uint64_t seed, long long base, int B, int W, int L, long long nneg, long long V, double logV,
+    float noise, uint64_t* __restrict__ keys, int32_t* __restrict__ meta,
+    const long long* __restrict__ step_dev, long long step_mul, long long step_add) {
+  if (step_dev) base = *step_dev * step_mul + step_add;
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long R = (long long)B + 2 * W;
+  const uint64_t kOut = 1ull << 40;
+  if (i < R) {
+    const long long g = base - W + i;
+    uint64_t tok = 0;
+    int32_t m = -1;
+    if (g >= 0) {
+      const long long s = g / L;
+      const uint64_t c = w2v_zipf(splitmix64(seed ^ ((uint64_t)s * 0xA24BAED4963EE407ull)), V, logV);
+      const uint64_t r = splitmix64(seed ^ 0xC0FFEEull ^ ((uint64_t)g * 0x9E3779B97F4A7C15ull));
+      if (u01(r) < noise) {
+        tok = w2v_zipf(splitmix64(r), V, logV);
+      } else {
+        const long long off = (long long)(splitmix64(r ^ 1) % (uint64_t)(2 * W + 1)) - W;
+        tok = (uint64_t)((((long long)c + off) % V + V) % V);
+      }
+      m = w2v_meta((uint64_t)s, w2v_reduced_window(seed, (uint64_t)g, W));
+    }
+    keys[B + i] = tok | kOut;
+    meta[i] = m;
+    if (i >= W && i < W + B) keys[i - W] = tok;
+  } else if (i < R + nneg) {
+    const long long q = i - R;
+    keys[B + R + q] =
+        w2v_zipf(splitmix64(seed ^ 0xBADC0DEull ^ ((uint64_t)(base + q) * 0xD1B54A32D192ED03ull)), V,
+                 logV) | kOut;
+  }
+}
+
 size_t w2v_smem_bytes(int D) {
   const int P = D + 1;
   return sizeof(float) * ((size_t)3 * kT * P + (size_t)kT * (kS + 1) + kNW);
+}
+
+// Raise a kernel's dynamic-LDS limit once per process (a driver call per
+// launch costs host time on the small-batch path); thread-safe static init.
+template <auto Kernel>
+static void smem_attr_once(size_t bytes) {
+  static const bool done = (check_hip(hipFuncSetAttribute((const void*)Kernel,
+                                                          hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                          (int)bytes),
+                                      "w2v smem attr"),
+                            true);
+  (void)done;
 }
 
 template <int D>
@@ -632,8 +885,10 @@ static void launch_w2v_bf16(bool split, int tiles, const uint32_t* inv_c, const 
   }
   auto k = split ? k_w2v_sgns_bf16<D, false> : k_w2v_sgns_bf16<D, true>;
   const size_t sm = split ? W2vBf16Smem<D, false>::bytes : W2vBf16Smem<D, true>::bytes;
-  check_hip(hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm),
-            "w2v bf16 smem attr");
+  if (split)
+    smem_attr_once<k_w2v_sgns_bf16<D, false>>(sm);
+  else
+    smem_attr_once<k_w2v_sgns_bf16<D, true>>(sm);
   hipLaunchKernelGGL(k, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, neg_scale, uvals,
                      ugrad, loss_sum);
 }
@@ -668,9 +923,7 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
   switch (D) {
 #define SS_W2V_CASE(DD)                                                                     \
   case DD:                                                                                  \
-    check_hip(hipFuncSetAttribute((const void*)k_w2v_sgns<DD>,                               \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm),    \
-              "w2v smem attr");                                                             \
+    smem_attr_once<k_w2v_sgns<DD>>(sm);                                                     \
     hipLaunchKernelGGL(k_w2v_sgns<DD>, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, \
                        neg_scale, uvals, ugrad, loss_sum, gpos);                            \
     break;
@@ -703,6 +956,62 @@ void launch_w2v_ctx_reduce(int P, const uint32_t* bstart, const uint32_t* unum,
       throw_error("w2v_ctx_reduce: D must be 32, 64 or 128");
   }
   check_launch("k_w2v_ctx_reduce");
+}
+
+void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
+                    const int32_t* meta, int B, int W, int D, float neg_per_pair,
+                    const float* uvals, float* ugrad, float* loss_sum, float* pair_sum,
+                    hipStream_t st) {
+  if (B <= 0) return;
+  if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_win: window must be in [1, 15]");
+  const int tiles = (B + kT - 1) / kT;
+  // Default grid: half the CUs, each workgroup walking tiles.  One
+  // workgroup per tile fills every CU with an 85 KB-LDS workgroup for the
+  // kernel's whole run and the route stream's dedup (53 KB LDS) of the next
+  // round then runs 5x slower beside it (11 -> 57 us); with half the CUs
+  // left to it the step measured 0.143 -> 0.123 ms (1M vocab, dim 128, 16K
+  // centers; caps 192 / 128 / 64: 0.124 / 0.123 / 0.148).  SS_W2V_WIN_GRID
+  // overrides (0: one workgroup per tile)
+  static const int grid_cap = [] {
+    const char* e = std::getenv("SS_W2V_WIN_GRID");
+    if (e) return std::atoi(e);
+    int dev = 0, cus = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
+              "CU count");
+    return std::max(1, cus / 2);
+  }();
+  const int grid = grid_cap > 0 ? std::min(tiles, grid_cap) : tiles;
+  switch (D) {
+#define SS_W2VW_CASE(DD)                                                                     \
+  case DD:                                                                                   \
+    smem_attr_once<k_w2v_win_bf16<DD>>(W2vWinSmem<DD>::bytes);                               \
+    hipLaunchKernelGGL(k_w2v_win_bf16<DD>, dim3(grid), dim3(kWG), W2vWinSmem<DD>::bytes, st,  \
+                       inv_c, inv_w, inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum,   \
+                       pair_sum);                                                            \
+    break;
+    SS_W2VW_CASE(32)
+    SS_W2VW_CASE(64)
+    SS_W2VW_CASE(128)
+#undef SS_W2VW_CASE
+    default:
+      throw_error("w2v_win: D must be 32, 64 or 128");
+  }
+  check_launch("k_w2v_win_bf16");
+}
+
+void launch_w2v_stream_gen(uint64_t seed, long long base, int B, int W, int L, long long nneg,
+                           long long V, float noise, uint64_t* keys, int32_t* meta,
+                           hipStream_t st, const long long* step_dev, long long step_mul,
+                           long long step_add) {
+  if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_stream_gen: window must be in [1, 15]");
+  if (L < 1) throw_error("w2v_stream_gen: sentence length must be >= 1");
+  const long long n = (long long)B + 2 * W + nneg;
+  if (B <= 0 || n <= 0) return;
+  hipLaunchKernelGGL(k_w2v_stream_gen, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, seed,
+                     base, B, W, L, nneg, V, log((double)V + 1.0), noise, keys, meta, step_dev,
+                     step_mul, step_add);
+  check_launch("k_w2v_stream_gen");
 }
 
 void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,

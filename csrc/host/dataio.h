@@ -38,6 +38,7 @@
 
 #include "common.h"
 #include "ss/hash.h"
+#include "ss/w2v_window.h"
 
 namespace ss {
 
@@ -395,6 +396,36 @@ class Corpus : NonCopyable {
   // bit).  Contexts are drawn from the center's sentence within +-W (with
   // replacement; a one-word sentence draws a noise word).  Deterministic in
   // (seed, step).
+  // Windowed skip-gram run of `step` (layout: ss/w2v_window.h): keys =
+  // [centers B][run positions B + 2W | out bit][negatives], meta per run
+  // position.  Bit-identical to the resident device batcher
+  // (k_w2v_corpus_window, csrc/hip/data.hip).
+  void fill_skipgram_window(uint64_t seed, uint64_t step, int B, int W, long long nneg,
+                            uint64_t* keys, int32_t* meta) const {
+    const long long n = (long long)tokens_.size(), R = (long long)B + 2 * W;
+    const uint64_t nsent = sent_offs_.empty() ? 0 : sent_offs_.size() - 1;
+    const long long start = (long long)((step * (uint64_t)B) % (uint64_t)n) - W;
+    for (long long i = 0; i < R; ++i) {
+      const long long x = start + i;
+      const long long lap = x >= 0 ? x / n : -((-x + n - 1) / n);
+      const long long idx = x - lap * n;
+      const uint64_t tok = tokens_[idx];
+      int32_t m = w2v_meta((uint64_t)sent_of_[idx] + (uint64_t)(lap + 1) * nsent,
+                           w2v_reduced_window(seed, (uint64_t)x, W));
+      if (!keep_.empty()) {
+        auto it = keep_.find(tok);
+        if (it != keep_.end() && !w2v_keep(seed, step, (uint64_t)x, it->second)) m = -1;
+      }
+      keys[B + i] = tok | kOutBit;
+      meta[i] = m;
+      if (i >= W && i < W + B) keys[i - W] = tok;
+    }
+    for (long long q = 0; q < nneg; ++q) {
+      const uint64_t r = splitmix64(seed ^ 0xBADC0DEull ^ (step * 0xD1B54A32D192ED03ull) ^ (uint64_t)q * 0x9E37ull);
+      keys[(size_t)B + (size_t)R + q] = table_[r & (table_.size() - 1)] | kOutBit;
+    }
+  }
+
   void fill_skipgram(uint64_t seed, uint64_t step, int B, int C, int W, long long nneg,
                      uint64_t* keys, int nthreads) const {
     nthreads = std::max(1, std::min(nthreads, B / 512 + 1));

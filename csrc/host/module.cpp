@@ -445,6 +445,14 @@ PYBIND11_MODULE(_ss_host, m) {
         auto k = c.keep_per_token();
         return py::array_t<float>(k.size(), k.data());
       })
+      .def("fill_skipgram_window", [](const Corpus& c, uint64_t seed, uint64_t step, int B, int W,
+                                      long long nneg, uintptr_t keys, uintptr_t meta) {
+             if (W < 1 || W > kW2vMaxWindow) throw std::invalid_argument("window must be in [1, 15]");
+             if (c.size() == 0) throw std::invalid_argument("empty corpus");
+             c.fill_skipgram_window(seed, step, B, W, nneg, reinterpret_cast<uint64_t*>(keys),
+                                    reinterpret_cast<int32_t*>(meta));
+           }, py::arg("seed"), py::arg("step"), py::arg("B"), py::arg("W"), py::arg("nneg"),
+           py::arg("keys"), py::arg("meta"), py::call_guard<py::gil_scoped_release>())
       .def("fill_skipgram", [](const Corpus& c, uint64_t seed, uint64_t step, int B, int C, int W,
                                long long nneg, uintptr_t keys, int nthreads) {
              c.fill_skipgram(seed, step, B, C, W, nneg, reinterpret_cast<uint64_t*>(keys),

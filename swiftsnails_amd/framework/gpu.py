@@ -260,7 +260,9 @@ def build_worker(cfg: Config):
             data = W2VSynth(batch_size=int(cfg.get("batch_size", 16384)),
                             window=int(cfg.get("window", 5)),
                             vocab=int(float(cfg.get("vocab", 1e6))),
-                            negatives=int(cfg.get("negatives", 5)))
+                            negatives=int(cfg.get("negatives", 5)),
+                            mode=cfg.get("w2v_mode", "window"),
+                            sentence_len=int(cfg.get("sentence_len", 24)))
         dim = int(cfg.get("dim", 128))
         opt, init = make_w2v_table_args(dim, opt)
         cap = int(cfg.get("table_capacity", 0) or 2 * data.vocab / nserv / load + 1024)

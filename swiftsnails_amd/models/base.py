@@ -105,12 +105,15 @@ class PipelinedWorker:
                     eng.capture_tag = p + 1
                     # fork the route stream into the capture at the start (no
                     # ordering: its work overlaps the whole step)
-                    eng.route_stream.wait_stream(torch.cuda.current_stream())
+                    side = [x for x in (eng.route_stream, eng.pull_stream) if x is not None]
+                    for x in side:
+                        x.wait_stream(torch.cuda.current_stream())
                     self._cap_base = self.step_idx  # what the counter holds at replay
                     for _ in range(per):
                         self._step_eager()
                     cur = torch.cuda.current_stream()
-                    cur.wait_stream(eng.route_stream)  # join the forked route stream
+                    for x in side:
+                        cur.wait_stream(x)  # join the forked route / pull streams
                     self._gstep.add_(per)  # after the join: no generator still reads it
                 pool = g.pool()
                 graphs.append(g)
@@ -122,6 +125,10 @@ class PipelinedWorker:
         self.step_idx, self._next, self._cur, eng._next_slot, eng.rounds = saved
         self._graphs, self._gbase = graphs, self.step_idx
         return True
+
+    def _zero_acc(self) -> None:
+        """Zero the per-step device accumulators (the loss) on the current stream."""
+        self.loss_sum.zero_()
 
     def step(self) -> torch.Tensor:
         if self._graphs is not None:
@@ -140,10 +147,10 @@ class PipelinedWorker:
         r = self._next if self._next is not None else self._route(self.step_idx)
         self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
         rnd = self.engine.pull(r)
-        self.loss_sum.zero_()
+        self._zero_acc()
         if self.active:
             with self.engine.trace("compute"):
-                self._compute(rnd, r.slot, torch.cuda.current_stream().cuda_stream)
+                self._compute(rnd, r.slot, self.engine.raw_stream())
         self.engine.push(rnd)
         self.step_idx += 1
         return self.loss_sum
@@ -158,10 +165,10 @@ class PipelinedWorker:
             self._next = self._route(self.step_idx + 1)
         rnd = self._cur
         eng.begin(rnd)
-        self.loss_sum.zero_()
+        self._zero_acc()
         if self.active:
             with eng.trace("compute"):
-                self._compute(rnd, rnd.slot, torch.cuda.current_stream().cuda_stream)
+                self._compute(rnd, rnd.slot, eng.raw_stream())
         if getattr(eng, "push_on_pull", False):
             # push(i) goes on the pull stream behind pull(i+1) (engine.push_on_pull)
             self._cur = eng.pull_ahead_round(self._next)

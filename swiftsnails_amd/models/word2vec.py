@@ -31,14 +31,16 @@ TILE = 64      # centers per workgroup tile
 NEG_TILE = 64  # shared negatives per tile
 
 
-@dataclass
-class W2VSynth:
-    batch_size: int = 16384        # centers per step per worker (multiple of 64)
-    window: int = 5                # contexts per center = 2*window
-    vocab: int = 1_000_000
-    noise: float = 0.1
-    negatives: int = 5             # K negatives per positive pair (sets the shared-negative weight)
-    seed: int = 1234
+class W2VLayout:
+    """Key layout shared by the synthetic and the file-fed sources.
+
+    ``mode="window"`` (default; csrc/include/ss/w2v_window.h): a batch is a
+    run of ``B + 2W`` consecutive stream positions, keys = [B centers | B + 2W
+    run positions (output namespace) | negatives] plus one int32 meta word per
+    run position (sentence tag, reduced window, mask); the contexts of a
+    center are its run neighbours, as in word2vec's sliding window.
+    ``mode="pairs"``: i.i.d. centers with 2W sampled contexts each, keys =
+    [B centers | B x 2W contexts | negatives]."""
 
     @property
     def contexts(self) -> int:
@@ -49,20 +51,62 @@ class W2VSynth:
         return (self.batch_size + TILE - 1) // TILE
 
     @property
+    def run_len(self) -> int:
+        return self.batch_size + 2 * self.window
+
+    @property
     def n_keys(self) -> int:
+        if self.mode == "window":
+            return self.batch_size + self.run_len + self.tiles * NEG_TILE
         return self.batch_size * (1 + self.contexts) + self.tiles * NEG_TILE
 
     @property
     def neg_scale(self) -> float:
+        """pairs layout: weight of each shared negative (2W pairs x K / S)."""
         return self.contexts * self.negatives / NEG_TILE
+
+    @property
+    def neg_per_pair(self) -> float:
+        """window layout: per-pair weight K / S (a center with n pairs weighs
+        its shared negatives n K / S)."""
+        return self.negatives / NEG_TILE
+
+    def _check_mode(self):
+        if self.mode not in ("window", "pairs"):
+            raise ValueError(f"word2vec batch mode must be window or pairs, not {self.mode!r}")
+        if self.mode == "window" and not 1 <= self.window <= 15:
+            raise ValueError("window mode: window must be in [1, 15]")
+
+
+@dataclass
+class W2VSynth(W2VLayout):
+    batch_size: int = 16384        # centers per step per worker (multiple of 64)
+    window: int = 5                # max window (contexts per center: up to 2*window)
+    vocab: int = 1_000_000
+    noise: float = 0.1
+    negatives: int = 5             # K negatives per positive pair (sets the shared-negative weight)
+    seed: int = 1234
+    mode: str = "window"           # window | pairs (see W2VLayout)
+    sentence_len: int = 24         # window mode: tokens per synthetic sentence
+
+    def __post_init__(self):
+        self._check_mode()
 
     graph_capturable = True  # generate() can take its step from device memory
 
     def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None,
-                 step_dev: int = 0, step_delta: int = 0):
+                 step_dev: int = 0, step_delta: int = 0, meta: Optional[torch.Tensor] = None):
         st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         B = self.batch_size
         base = (step * world + rank) * B
+        if self.mode == "window":
+            if meta is None or meta.numel() < self.run_len:
+                raise ValueError("window mode: generate() needs a meta buffer of run_len int32")
+            hip().w2v_stream_gen(self.seed, base, B, self.window, self.sentence_len,
+                                 self.tiles * NEG_TILE, self.vocab, self.noise, keys.data_ptr(),
+                                 meta.data_ptr(), st, step_dev, world * B,
+                                 (step_delta * world + rank) * B)
+            return
         hip().w2v_gen(self.seed, base, B, self.contexts, self.window,
                       self.tiles * NEG_TILE, self.vocab, self.noise, keys.data_ptr(), st,
                       step_dev, world * B, (step_delta * world + rank) * B)
@@ -85,16 +129,25 @@ class Word2VecWorker(PipelinedWorker):
         self.data = data
         # the route stream is the light one for this model: pull the next
         # round's rows behind its dedup (bounded staleness 1)
-        engine.enable_pull_ahead()
+        engine.enable_pull_ahead(pull_stream=True)
         self.keys = [torch.empty(data.n_keys, dtype=torch.int64, device=engine.device)
                      for _ in range(engine.depth)]
+        self.window_mode = getattr(data, "mode", "pairs") == "window"
+        self.meta = ([torch.empty(data.run_len, dtype=torch.int32, device=engine.device)
+                      for _ in range(engine.depth)] if self.window_mode else None)
+        # window layout: positive pairs of the last step (sharded counter),
+        # beside the loss in one buffer: one zero-fill per step for both
+        self._acc = torch.zeros((2, self.loss_sum.numel()), dtype=torch.float32,
+                                device=engine.device)
+        self.loss_sum, self.pair_sum = self._acc[0], self._acc[1]
         # SS_W2V_CTX=reduce: context-row gradients as one scalar per (center,
         # context) pair, summed per unique context key over the bucketed
         # dedup's partition (k_w2v_ctx_reduce) instead of a row of float
         # atomics per pair.  Measured slower (0.32 -> 0.81 ms/step): the sgns
         # kernel drops 204 -> 105 us, but a Zipf-head context key puts
         # thousands of row loads into one bucket's workgroup (587 us tail)
-        self.ctx_reduce = (os.environ.get("SS_W2V_CTX", "atomic") == "reduce" and
+        self.ctx_reduce = (not self.window_mode and
+                           os.environ.get("SS_W2V_CTX", "atomic") == "reduce" and
                            all(getattr(d, "mode", None) == "bucket" for d in engine.dedupers))
         self.gpos = (torch.empty(data.batch_size * data.contexts, dtype=torch.float32,
                                  device=engine.device) if self.ctx_reduce else None)
@@ -105,9 +158,14 @@ class Word2VecWorker(PipelinedWorker):
         # ms/step (1M vocab, dim 128); SS_W2V_MFMA=f32 selects the fp32 tile
         self.mfma_bf16 = (os.environ.get("SS_W2V_MFMA", "bf16") == "bf16" and not self.ctx_reduce)
 
+    def _zero_acc(self) -> None:
+        self._acc.zero_()
+
     def _produce(self, step, slot, stream):
-        self.data.generate(step, self.rank, self.world, self.keys[slot], stream=stream,
-                           **self._gen_kwargs(step))
+        kw = self._gen_kwargs(step)
+        if self.window_mode:
+            kw["meta"] = self.meta[slot]
+        self.data.generate(step, self.rank, self.world, self.keys[slot], stream=stream, **kw)
         return self.keys[slot]
 
     def _compute(self, rnd, slot, st):
@@ -116,6 +174,12 @@ class Word2VecWorker(PipelinedWorker):
         B, C = d.batch_size, d.contexts
         ptr, es = inv.data_ptr(), inv.element_size()
         h = hip()
+        if self.window_mode:
+            h.w2v_win(ptr, ptr + B * es, ptr + (B + d.run_len) * es, self.meta[slot].data_ptr(),
+                      B, d.window, self.engine.dim, d.neg_per_pair, rnd.uvals.data_ptr(),
+                      rnd.ugrad.data_ptr(), self.loss_sum.data_ptr(), self.pair_sum.data_ptr(),
+                      st)
+            return
         h.w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
                    d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
                    self.loss_sum.data_ptr(), st, self.gpos.data_ptr() if self.ctx_reduce else 0,
@@ -128,8 +192,56 @@ class Word2VecWorker(PipelinedWorker):
                              rnd.ugrad.data_ptr(), st)
 
     def samples_per_step(self) -> int:
-        """Positive (center, context) pairs per step ("words/s" numerator)."""
-        return self.data.batch_size * self.data.contexts if self.active else 0
+        """Window layout: centers (words) per step, word2vec's "words/s"
+        numerator; pairs layout: (center, context) pairs per step."""
+        if not self.active:
+            return 0
+        return self.data.batch_size if self.window_mode else \
+            self.data.batch_size * self.data.contexts
+
+    def step_pairs(self) -> float:
+        """Positive pairs trained in the last step (window layout: counted by
+        the tile kernel; pairs layout: B x 2W).  Syncs."""
+        if not self.active:
+            return 0.0
+        if self.window_mode:
+            return float(self.pair_sum.sum().item())
+        return float(self.data.batch_size * self.data.contexts)
+
+    def mean_loss(self) -> float:
+        """Mean SGNS loss per positive pair (incl. its negatives) of the last step."""
+        if not self.window_mode:
+            return super().mean_loss()
+        n = self.step_pairs()
+        return float(self.loss_sum.sum().item()) / n if n else 0.0
+
+
+def window_pairs_reference(meta: np.ndarray, B: int, W: int) -> np.ndarray:
+    """Valid-pair mask [B, B + 2W] of a window-layout run (ss/w2v_window.h):
+    center t (run position t + W) pairs with run position q."""
+    m = meta.astype(np.int64)
+    c = m[W:W + B][:, None]
+    q = m[None, :]
+    d = np.arange(B + 2 * W)[None, :] - (np.arange(B)[:, None] + W)
+    return ((c >= 0) & (q >= 0) & ((c >> 4) == (q >> 4)) & (d != 0) & (np.abs(d) <= (c & 15)))
+
+
+def sgns_window_reference(V: np.ndarray, U: np.ndarray, N: np.ndarray, mask: np.ndarray,
+                          neg_per_pair: float):
+    """fp64 reference of one window tile.  V [T,D] centers, U [Q,D] window
+    rows, N [S,D] shared negatives, mask [T,Q] valid pairs.  Returns (loss,
+    pairs, gV, gU, gN); a center's negatives weigh n_t * neg_per_pair."""
+    V, U, N = (a.astype(np.float64) for a in (V, U, N))
+    sig = lambda z: 1.0 / (1.0 + np.exp(-z))  # noqa: E731
+    sp = lambda z: np.maximum(z, 0) + np.log1p(np.exp(-np.abs(z)))  # noqa: E731
+    n = mask.sum(1).astype(np.float64)
+    Sp = V @ U.T
+    Gp = np.where(mask, sig(Sp) - 1.0, 0.0)
+    Sn = V @ N.T
+    cw = (n * neg_per_pair)[:, None]
+    Gn = cw * sig(Sn)
+    loss = np.where(mask, sp(-Sp), 0.0).sum() + (cw * sp(Sn)).sum()
+    return loss, n.sum(), Gp @ U + Gn @ N, Gp.T @ V, Gn.T @ V
 
 
 def sgns_reference(V: np.ndarray, X: np.ndarray, N: np.ndarray, neg_scale: float):

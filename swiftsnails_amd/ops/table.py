@@ -26,6 +26,7 @@ from typing import Iterator, Optional
 import numpy as np
 import torch
 
+from ..utils.streams import current_raw
 from .._native import hip
 from .optim import InitConfig, Optimizer
 
@@ -78,7 +79,7 @@ def default_lane_group(width: int) -> int:
 
 def _stream_ptr(stream) -> int:
     if stream is None:
-        return torch.cuda.current_stream().cuda_stream
+        return current_raw()
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
 
 

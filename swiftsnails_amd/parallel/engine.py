@@ -53,6 +53,8 @@ import numpy as np
 import torch
 
 from ..ops.dedup import CpuDeduper, DedupResult, Deduper
+from ..utils.streams import current, current_raw, use_stream
+from ..utils.tracing import Tracer
 from .router import HashFrag
 from .transport import CountsHandle, LoopbackTransport, Transport
 
@@ -100,7 +102,7 @@ def _hip():
 
 
 def _stream():
-    return torch.cuda.current_stream().cuda_stream
+    return current_raw()
 
 
 class PSEngine:
@@ -175,7 +177,7 @@ class PSEngine:
         # observability: occurrences routed, unique keys exchanged,
         # alltoallv payload bytes (host-known counts; world-1 keeps counts on
         # the device and only counts occurrences)
-        from ..utils.tracing import Metrics, Tracer
+        from ..utils.tracing import Metrics
 
         self.metrics = Metrics()
         # per-phase roctx ranges + HIP-event device times (route / pull /
@@ -249,6 +251,20 @@ class PSEngine:
         # network while the route stream dedups and the main stream computes
         self.pull_stream = (torch.cuda.Stream(device=self.device)
                             if self.pull_ahead and self.pt is not self.ct else None)
+        # pull-ahead staleness bound (_bound_staleness): a pulled-ahead round
+        # misses at most this many rounds' updates; SS_STALENESS=ring: only the
+        # ring depth bounds it
+        st_env = os.environ.get("SS_STALENESS", "1")
+        self.staleness = 0 if st_env == "ring" else max(1, int(st_env))
+        # device index for the cheap current-stream lookups (utils/streams.py)
+        # and per-slot events, reused round after round (a slot's event is
+        # re-recorded only after the waits on its previous record were enqueued)
+        self._dix = (self.device.index or 0) if self.gpu else -1
+        if self.gpu:
+            self._ev_route = [torch.cuda.Event() for _ in range(self.depth)]
+            self._ev_pull = [torch.cuda.Event() for _ in range(self.depth)]
+            self._ev_free = [torch.cuda.Event() for _ in range(self.depth)]
+            self._ev_grad = [torch.cuda.Event() for _ in range(self.depth)]
         # push on the pull stream (N>1 with a pull stream, SS_PUSH_STREAM=pull):
         # round i's gradient all-to-all-v and server apply are enqueued on the
         # pull stream right behind round i+1's pull (the worker calls
@@ -288,6 +304,14 @@ class PSEngine:
     def _wait(self, stream, ev, tag) -> None:
         if ev is not None and tag == self.capture_tag:
             stream.wait_event(ev)
+
+    def main_stream(self) -> torch.cuda.Stream:
+        """The caller's current stream on this engine's device."""
+        return current(self._dix)
+
+    def raw_stream(self) -> int:
+        """hipStream_t of the caller's current stream on this engine's device."""
+        return current_raw(self._dix)
 
     def trace(self, name: str, stream=None):
         """A phase range of the tracer: roctx + host time, plus the device
@@ -351,14 +375,13 @@ class PSEngine:
                     self.ct.exchange_counts_async(dd.ucount)
             return Routed(dd, slot, counts)
         rs = self.route_stream
-        main = torch.cuda.current_stream()
         # previous user of this slot is done (inside a capture only if it ran
         # in the same capture: an earlier replay has completed anyway)
         if self._free[slot] is not None:
             self._wait(rs, self._free[slot], self._free_tag[slot])
         if keys is not None and self.capture_tag is None:
-            rs.wait_stream(main)             # keys were produced on the main stream
-        with torch.cuda.stream(rs), self.trace("route", rs):
+            rs.wait_stream(self.main_stream())  # keys were produced on the main stream
+        with use_stream(rs), self.trace("route", rs):
             if produce is not None:
                 keys = produce(rs)
             keys = keys.reshape(-1)
@@ -371,7 +394,7 @@ class PSEngine:
             if not self.fast1:
                 counts = self.ct.exchange_counts_async(dd.ucount, pinned=self._pins[slot],
                                                        stream=rs)
-            ev = torch.cuda.Event()
+            ev = self._ev_route[slot]
             ev.record(rs)
         return Routed(dd, slot, counts, ev, self.capture_tag)
 
@@ -398,7 +421,7 @@ class PSEngine:
     def _pull(self, r: Routed) -> Round:
         dd, slot = r.dd, r.slot
         if self.gpu:
-            self._wait(torch.cuda.current_stream(), r.ready, r.tag)
+            self._wait(self.main_stream(), r.ready, r.tag)
         tab = self.table
         uv = self.uvals[slot]
         if self.fast1:
@@ -436,16 +459,25 @@ class PSEngine:
         Round whose rows are ready at ``rnd.ready``; ``begin(rnd)`` makes the
         current (main) stream wait for them."""
         dd, slot = r.dd, r.slot
-        if self.fast1:  # one GPU: pull right behind the dedup on the route stream
-            rs, uv, tab = self.route_stream, self.uvals[slot], self.table
-            with torch.cuda.stream(rs), self.trace("pull", rs):
+        if self.fast1:
+            # one GPU: the pull waits for this round's dedup only, on its own
+            # stream (SS_PULL_STREAM=1), so the route stream goes on with the
+            # next round's dedup meanwhile; or right behind the dedup on the
+            # route stream
+            uv, tab = self.uvals[slot], self.table
+            rs = self.pull_stream or self.route_stream
+            if rs is not self.route_stream:
+                self._wait(rs, r.ready, r.tag)
+            self._bound_staleness(rs, slot)
+            with use_stream(rs), self.trace("pull", rs):
                 own = dd.owner
                 if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
-                    tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi)
+                    tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], osi=self.osi,
+                                     stream=rs)
                 else:
                     tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                              segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
-                ev = torch.cuda.Event()
+                ev = self._ev_pull[slot]
                 ev.record(rs)
             self.metrics.add(occurrences=dd.n)
             return Round(dd, uv, slot, slots=self.slots[slot], ready=ev, tag=self.capture_tag)
@@ -454,12 +486,13 @@ class PSEngine:
         ps = self.pull_stream or self.route_stream
         if ps is not self.route_stream:
             self._wait(ps, r.ready, r.tag)
-        with torch.cuda.stream(ps), self.trace("pull", ps):
+        self._bound_staleness(ps, slot)
+        with use_stream(ps), self.trace("pull", ps):
             self.pt.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
             self._server_pull(rcounts, slot)
             self.pt.alltoallv(self.rvals, rcounts, D, uv, scounts, D, self.dim)
             uv = self._rows_for_model(dd, uv, slot)
-            ev = torch.cuda.Event()
+            ev = self._ev_pull[slot]
             ev.record(ps)
         sent, recv = int(scounts.sum()), int(rcounts.sum())
         self.metrics.add(occurrences=dd.n, unique_sent=sent, unique_recv=recv,
@@ -467,18 +500,42 @@ class PSEngine:
         return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
                      stats={"sent": sent, "recv": recv}, ready=ev, tag=self.capture_tag)
 
-    def enable_pull_ahead(self, on: bool = True) -> bool:
-        """Opt into pull-ahead (staleness 1) where the engine supports it."""
+    def _bound_staleness(self, stream, slot: int) -> None:
+        """Pull-ahead of round i+1 (ring slot ``slot``): wait until round
+        i-1's push has been applied, two slots back in the ring (staleness k:
+        round i-k's).  Round i+1 then reads every update but round i's —
+        staleness exactly 1.  Without
+        the wait a side stream that runs ahead of the main stream (the host
+        enqueues rounds before the device has finished earlier ones) can pull
+        before round i-1 is applied as well: measured on FM (one GPU, pull on
+        its own stream) the loss stuck at 0.69 instead of 0.60."""
+        k = self.staleness
+        if k <= 0 or k + 1 >= self.depth:
+            return  # SS_STALENESS=ring: bounded by the ring depth only
+        prev = (slot - k - 1) % self.depth
+        if self._free[prev] is not None:
+            self._wait(stream, self._free[prev], self._free_tag[prev])
+
+    def enable_pull_ahead(self, on: bool = True, pull_stream: bool = False) -> bool:
+        """Opt into pull-ahead (staleness 1) where the engine supports it.
+        ``pull_stream`` (one GPU; SS_PULL_STREAM=0/1 overrides): run the
+        pulled-ahead lookup on its own stream instead of behind the dedup on
+        the route stream — pays when the lookup would otherwise hold up the
+        next round's dedup (word2vec, 0.128 -> 0.125 ms/step), not when the
+        main stream is the longer one anyway (FM, 0.655 -> 0.685)."""
         if on and self.gpu and self.depth >= 3 and \
                 os.environ.get("SS_PULL_AHEAD", "1") != "0":
             self.pull_ahead = True
+            want = os.environ.get("SS_PULL_STREAM", "1" if pull_stream else "0") != "0"
+            if self.fast1 and self.pull_stream is None and want:
+                self.pull_stream = torch.cuda.Stream(device=self.device)
         elif not on:
             self.pull_ahead = False
         return self.pull_ahead
 
     def begin(self, rnd: Round) -> None:
         if rnd.ready is not None:
-            self._wait(torch.cuda.current_stream(), rnd.ready, rnd.tag)
+            self._wait(self.main_stream(), rnd.ready, rnd.tag)
 
     # ------------------------------------------------------------ stage 3
     def _server_apply(self, rcounts: np.ndarray, slot: int, resolved: bool) -> None:
@@ -508,8 +565,8 @@ class PSEngine:
 
     def _release(self, slot: int):
         if self.gpu:
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())
+            ev = self._ev_free[slot]
+            ev.record(self.main_stream())
             self._free[slot] = ev
             self._free_tag[slot] = self.capture_tag
 
@@ -562,10 +619,10 @@ class PSEngine:
             tab.next_round()
         elif self.push_on_pull:
             D, ps = self.displs, self.pull_stream
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream())  # the merged gradients
+            ev = self._ev_grad[rnd.slot]
+            ev.record(self.main_stream())  # the merged gradients
             ps.wait_event(ev)
-            with torch.cuda.stream(ps):
+            with use_stream(ps):
                 self.pt.alltoallv(g, rnd.scounts, D, self.rgrads, rnd.rcounts, D, self.dim)
                 self._server_apply(rnd.rcounts, rnd.slot, resolved=True)
                 self._release(rnd.slot)  # the slot is free once the apply has read it
@@ -633,7 +690,7 @@ class PSEngine:
             if hasattr(own, "osi"):
                 own.osi = saved[2]
         if self.gpu:
-            self._wait(torch.cuda.current_stream(), r.ready, r.tag)
+            self._wait(self.main_stream(), r.ready, r.tag)
         dd = r.dd
         rnd = Round(dd, self.uvals[r.slot], r.slot)
         self.accumulate(rnd, grads.to(self.device))

@@ -224,19 +224,28 @@ class FileCtrSource:
             self.ring.close()
 
 
-class FileCorpusSource:
+from ..models.word2vec import W2VLayout  # noqa: E402  (key layouts shared with W2VSynth)
+
+
+class FileCorpusSource(W2VLayout):
     """Skip-gram batches from a text corpus (one sentence per line; integer
-    tokens are word ids, other tokens are hashed), in the ``W2VSynth`` key
-    layout: [centers | contexts | shared negatives]."""
+    tokens are word ids, other tokens are hashed) in the ``W2VSynth`` key
+    layouts: ``mode="window"`` (default) walks the rank's corpus shard in
+    order, one run of B + 2W positions per step (every token is a center once
+    per epoch, its contexts are its sentence neighbours within a reduced
+    window); ``mode="pairs"`` samples i.i.d. centers and 2W contexts each."""
 
     def __init__(self, path: str, batch_size: int = 16384, window: int = 5, negatives: int = 5,
                  rank: int = 0, world: int = 1, min_count: int = 1, sample: float = 0.0,
                  seed: int = 1234, nthreads: int = 8, prefetch: int = 3,
-                 pin: Optional[bool] = None, resident: Optional[str] = None, device=None):
+                 pin: Optional[bool] = None, resident: Optional[str] = None, device=None,
+                 mode: str = "window"):
         self.corpus = host().Corpus(path, nthreads, rank, world, min_count, sample)
         self.batch_size = int(batch_size)
         self.window = int(window)
         self.negatives = int(negatives)
+        self.mode = mode
+        self._check_mode()
         self.seed = int(seed) + 7919 * rank
         self.nthreads = nthreads
         self.vocab = max(1, self.corpus.vocab_size)
@@ -246,7 +255,10 @@ class FileCorpusSource:
             self._upload(device)
             return
         pin = torch.cuda.is_available() if pin is None else pin
-        self.ring = _PinnedRing(max(1, prefetch), {"keys": (self.n_keys, torch.int64)}, pin)
+        bufs = {"keys": (self.n_keys, torch.int64)}
+        if self.mode == "window":
+            bufs["meta"] = (self.run_len, torch.int32)
+        self.ring = _PinnedRing(max(1, prefetch), bufs, pin)
 
     def device_bytes(self) -> int:
         """HBM the resident sampler state takes (tokens, sentence index, noise
@@ -273,28 +285,19 @@ class FileCorpusSource:
     def graph_capturable(self) -> bool:
         return self.resident == "hbm"
 
-    @property
-    def contexts(self) -> int:
-        return 2 * self.window
-
-    @property
-    def tiles(self) -> int:
-        return (self.batch_size + TILE - 1) // TILE
-
-    @property
-    def n_keys(self) -> int:
-        return self.batch_size * (1 + self.contexts) + self.tiles * NEG_TILE
-
-    @property
-    def neg_scale(self) -> float:
-        return self.contexts * self.negatives / NEG_TILE
-
     def _fill(self, step: int, buf):
+        if self.mode == "window":
+            self.corpus.fill_skipgram_window(self.seed, step, self.batch_size, self.window,
+                                             self.tiles * NEG_TILE, buf["keys"].data_ptr(),
+                                             buf["meta"].data_ptr())
+            return
         self.corpus.fill_skipgram(self.seed, step, self.batch_size, self.contexts, self.window,
                                   self.tiles * NEG_TILE, buf["keys"].data_ptr(), self.nthreads)
 
     def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None,
-                 step_dev: int = 0, step_delta: int = 0):
+                 step_dev: int = 0, step_delta: int = 0, meta: Optional[torch.Tensor] = None):
+        if self.mode == "window" and (meta is None or meta.numel() < self.run_len):
+            raise ValueError("window mode: generate() needs a meta buffer of run_len int32")
         if self.resident == "hbm":
             from .._native import hip
 
@@ -302,6 +305,18 @@ class FileCorpusSource:
                 raise ValueError("generate: the key buffer must hold n_keys on the corpus' device")
             st = stream if stream is not None else torch.cuda.current_stream()
             st = st.cuda_stream if hasattr(st, "cuda_stream") else int(st)
+            if self.mode == "window":
+                if meta.device != self.device:
+                    raise ValueError("generate: the meta buffer must be on the corpus' device")
+                hip().w2v_corpus_window(self.d_tokens.data_ptr(), self.d_sof.data_ptr(),
+                                        self.corpus.sentences, self.d_table.data_ptr(),
+                                        self.d_table.numel(),
+                                        self.d_keep.data_ptr() if self.d_keep is not None else 0,
+                                        self.d_tokens.numel(), self.seed, step, step_dev,
+                                        step_delta, self.batch_size, self.window,
+                                        self.tiles * NEG_TILE, OUT_BIT, keys.data_ptr(),
+                                        meta.data_ptr(), st)
+                return
             hip().w2v_corpus_batch(self.d_tokens.data_ptr(), self.d_soffs.data_ptr(),
                                    self.d_sof.data_ptr(), self.d_table.data_ptr(),
                                    self.d_table.numel(),
@@ -317,6 +332,8 @@ class FileCorpusSource:
         ctx = torch.cuda.stream(st) if st is not None else _null()
         with ctx:
             keys.copy_(buf["keys"], non_blocking=keys.is_cuda)
+            if self.mode == "window":
+                meta.copy_(buf["meta"], non_blocking=meta.is_cuda)
         self.ring.mark_copied(slot, st if st is not None else (
             torch.cuda.current_stream() if keys.is_cuda else None))
 
@@ -346,11 +363,12 @@ def make_ctr_source(cfg, rank: int = 0, world: int = 1, device=None):
 
 def make_corpus_source(cfg, rank: int = 0, world: int = 1, device=None):
     """Config keys: data_path, batch_size, window, negatives, min_count, sample,
-    data_resident (auto|hbm|host)."""
+    data_resident (auto|hbm|host), w2v_mode (window|pairs)."""
     return FileCorpusSource(cfg.get("data_path"), batch_size=int(cfg.get("batch_size", 16384)),
                             window=int(cfg.get("window", 5)),
                             negatives=int(cfg.get("negatives", 5)), rank=rank, world=world,
                             min_count=int(cfg.get("min_count", 1)),
                             sample=float(cfg.get("sample", 0.0)),
                             nthreads=int(cfg.get("data_threads", 8)),
-                            resident=cfg.get("data_resident", "auto"), device=device)
+                            resident=cfg.get("data_resident", "auto"), device=device,
+                            mode=cfg.get("w2v_mode", "window"))

@@ -107,6 +107,19 @@ KNOBS: dict[str, Knob] = {
     "SS_W2V_CTX": Knob("atomic", "models/word2vec.py", "experiment",
                        "reduce: context gradients merged per key over the dedup buckets "
                        "(0.32 -> 0.81 ms/step)"),
+    "SS_STALENESS": Knob("1", "parallel/engine.py", "ops",
+                         "pull-ahead bound: a round's pull waits until the push of the round "
+                         "k+1 before it is applied (k = 1: staleness 1); ring: bounded by the "
+                         "route-ring depth only (FM 0.655 -> 0.620 ms/step, word2vec 0.125 -> "
+                         "0.118; N>1 LR path unchanged)"),
+    "SS_PULL_STREAM": Knob("model (word2vec 1, FM 0)", "parallel/engine.py", "tuning",
+                           "one GPU with pull-ahead: the pulled-ahead round's table lookup on "
+                           "its own stream, beside the next round's dedup (word2vec 0.128 -> "
+                           "0.125 ms/step; FM 0.655 -> 0.685, so off there)"),
+    "SS_W2V_WIN_GRID": Knob("CUs / 2", "csrc/hip/w2v.hip", "tuning",
+                            "grid of the windowed word2vec tile kernel (workgroups walk tiles; "
+                            "0: one per tile), leaving CUs to the route stream's dedup "
+                            "(0.143 -> 0.123 ms/step)"),
     "SS_PUSH_STREAM": Knob("main", "parallel/engine.py", "experiment",
                            "pull: N>1 gradient exchange + server apply on the pull stream "
                            "behind the next round's pull (1.049-1.053 -> 1.058-1.103 ms/step: "

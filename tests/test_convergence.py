@@ -7,8 +7,6 @@ known: the AUC of the true logits on the held-out batch.  A model trained
 through the parameter server (pull -> gradient -> push with AdaGrad) must
 recover a good fraction of it.
 """
-import os
-import socket
 
 import numpy as np
 import pytest
@@ -74,13 +72,12 @@ def test_sparse_lr_converges_world1_cpu():
     assert ll < np.log(2) - 0.05
 
 
-def _rank_main(rank, world, port, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+def _rank_main(rank, world, init, q):
     import torch.distributed as dist
 
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from _mp import init_gloo
+
+    init_gloo(init, rank, world)
     try:
         from swiftsnails_amd.parallel.transport import TorchDistTransport
 
@@ -94,15 +91,15 @@ def _rank_main(rank, world, port, q):
 def test_sparse_lr_converges_world2_gloo():
     """Two colocated worker+server ranks: each trains on its own data shard,
     the table is split by the router; both ranks see the same model."""
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
+    from _mp import collect, file_init
+
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    init = file_init()
+    ps = [ctx.Process(target=_rank_main, args=(r, 2, init, q)) for r in range(2)]
     for p in ps:
         p.start()
-    res = dict((r, (l, e)) for r, l, e in (q.get(timeout=300) for _ in ps))
+    res = dict((r, (l, e)) for r, l, e in collect(q, ps, 2, 300))
     for p in ps:
         p.join(60)
         assert p.exitcode == 0

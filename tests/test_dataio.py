@@ -158,6 +158,71 @@ def test_corpus_and_skipgram_sampling(tmp_path):
     np.testing.assert_array_equal(keys, k2)
 
 
+def _splitmix64(x: int) -> int:
+    m = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & m
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
+    return x ^ (x >> 31)
+
+
+@pytest.mark.parametrize("step,B", [(0, 64), (3, 64), (0, 5000)])
+def test_corpus_window_runs(tmp_path, step, B):
+    """Windowed skip-gram runs (ss/w2v_window.h): a run is B + 2W consecutive
+    positions of the corpus stream starting at step*B - W (wrapping around the
+    corpus, laps tagged apart), centers are its middle B, meta carries the
+    sentence tag and the reduced window 1 + hash % W (checked against a
+    Python re-implementation of the hash)."""
+    p = str(tmp_path / "w2v.txt")
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_word2vec_data.py"), p,
+                           "--lines", "300", "--seed", "2"])
+    sents = [list(map(int, ln.split())) for ln in open(p)]
+    stream = [w for s in sents for w in s]
+    sid = [i for i, s in enumerate(sents) for _ in s]
+    c = _host().Corpus(p, 2, 0, 1, 1, 0.0)
+    N, S, W, nneg, seed = len(stream), len(sents), 4, 64, 11
+    R = B + 2 * W
+    keys = np.empty(B + R + nneg, dtype=np.uint64)
+    meta = np.empty(R, dtype=np.int32)
+    c.fill_skipgram_window(seed, step, B, W, nneg, keys.ctypes.data, meta.ctypes.data)
+    out = np.uint64(1 << 40)
+    run, neg = keys[B:B + R], keys[B + R:]
+    assert (run & out).all() and (neg & out).all() and not (keys[:B] & out).any()
+    np.testing.assert_array_equal(keys[:B], run[W:W + B] & ~out)
+    m64 = (1 << 64) - 1
+    for i in range(R):
+        x = (step * B) % N - W + i
+        lap, idx = x // N, x % N
+        assert int(run[i] & ~out) == stream[idx]
+        h = _splitmix64(seed ^ 0x5EEDB0A7 ^ ((x & m64) * 0x9E3779B97F4A7C15 & m64))
+        b = 1 + ((h * W) >> 64)
+        tag = (sid[idx] + (lap + 1) * S) & 0x7FFFFFF
+        assert int(meta[i]) == (tag << 4 | b), i
+    k2, m2 = np.empty_like(keys), np.empty_like(meta)
+    c.fill_skipgram_window(seed, step, B, W, nneg, k2.ctypes.data, m2.ctypes.data)
+    np.testing.assert_array_equal(keys, k2)
+    np.testing.assert_array_equal(meta, m2)
+
+
+def test_window_pair_mask_reference():
+    """window_pairs_reference: same sentence, 0 < |d| <= reduced window,
+    masked positions never pair."""
+    from swiftsnails_amd.models.word2vec import window_pairs_reference
+
+    B, W = 6, 2
+    tags = [0, 0, 0, 0, 1, 1, 1, 1, 1, 1]
+    bs = [1, 2, 2, 1, 2, 2, 1, 2, 2, 2]
+    meta = np.array([(t << 4) | b for t, b in zip(tags, bs)], dtype=np.int32)
+    meta[6] = -1
+    m = window_pairs_reference(meta, B, W)
+    # center 0 = run position 2 (b = 2, sentence 0): positions 0, 1, 3
+    assert m[0].nonzero()[0].tolist() == [0, 1, 3]
+    # center 2 = run position 4 (b = 2, sentence 1): 5 (6 is masked)
+    assert m[2].nonzero()[0].tolist() == [5]
+    # center 4 = run position 6 is masked
+    assert not m[4].any()
+
+
 def test_corpus_hashes_words_and_min_count(tmp_path):
     p = str(tmp_path / "t.txt")
     with open(p, "w") as f:
@@ -203,10 +268,12 @@ def test_sparse_lr_trains_from_libsvm_file(tmp_path, resident):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("sample", [0.0, 1e-3])
-def test_hbm_resident_skipgram_matches_host_sampler(tmp_path, sample):
-    """data_resident: hbm for a corpus — the device sampler (k_w2v_corpus_batch)
-    writes the same keys as Corpus.fill_skipgram, with and without frequent-word
-    sub-sampling, from a host step or a device step counter."""
+@pytest.mark.parametrize("mode,batch", [("pairs", 256), ("window", 256), ("window", 40000)])
+def test_hbm_resident_skipgram_matches_host_sampler(tmp_path, sample, mode, batch):
+    """data_resident: hbm for a corpus — the device batchers (k_w2v_corpus_batch,
+    k_w2v_corpus_window) write the same keys (and window meta) as the host
+    ones, with and without frequent-word sub-sampling, from a host step or a
+    device step counter; a 40000-center run wraps the corpus."""
     from swiftsnails_amd.utils.dataio import FileCorpusSource
 
     p = str(tmp_path / "w2v.txt")
@@ -215,28 +282,39 @@ def test_hbm_resident_skipgram_matches_host_sampler(tmp_path, sample):
     with open(p, "a") as f:
         f.write("42\n7 word\n")  # one-word sentences draw noise contexts; a hashed token
     dev = torch.device("cuda", 0)
-    kw = dict(batch_size=256, window=3, negatives=5, min_count=2, sample=sample, seed=99)
+    kw = dict(batch_size=batch, window=3, negatives=5, min_count=2, sample=sample, seed=99,
+              mode=mode)
     dsrc = FileCorpusSource(p, resident="hbm", device=dev, **kw)
     hsrc = FileCorpusSource(p, resident="host", pin=False, **kw)
     assert dsrc.resident == "hbm" and dsrc.graph_capturable
     keys = torch.empty(dsrc.n_keys, dtype=torch.int64, device=dev)
     hk = torch.empty(hsrc.n_keys, dtype=torch.int64)
+    win = mode == "window"
+    meta = torch.empty(dsrc.run_len, dtype=torch.int32, device=dev) if win else None
+    hm = torch.empty(hsrc.run_len, dtype=torch.int32) if win else None
     step_dev = torch.zeros(1, dtype=torch.int64, device=dev)
     for step in (0, 1, 5):
-        hsrc.generate(step, 0, 1, hk)
-        dsrc.generate(step, 0, 1, keys)
+        hsrc.generate(step, 0, 1, hk, meta=hm)
+        dsrc.generate(step, 0, 1, keys, meta=meta)
         torch.cuda.synchronize()
         assert torch.equal(keys.cpu(), hk), step
+        if win:
+            assert torch.equal(meta.cpu(), hm), step
+            if sample:
+                assert (hm < 0).any()  # some tokens sub-sampled away
         step_dev.fill_(step + 1)
-        dsrc.generate(0, 0, 1, keys, step_dev=step_dev.data_ptr(), step_delta=-1)
+        dsrc.generate(0, 0, 1, keys, step_dev=step_dev.data_ptr(), step_delta=-1, meta=meta)
         torch.cuda.synchronize()
         assert torch.equal(keys.cpu(), hk), step
+        if win:
+            assert torch.equal(meta.cpu(), hm), step
     hsrc.close()
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("resident", ["hbm", "host"])
-def test_word2vec_trains_from_corpus_file(tmp_path, resident):
+@pytest.mark.parametrize("resident,mode", [("hbm", "window"), ("host", "window"),
+                                           ("hbm", "pairs"), ("host", "pairs")])
+def test_word2vec_trains_from_corpus_file(tmp_path, resident, mode):
     from swiftsnails_amd.models.word2vec import Word2VecWorker, make_w2v_table_args
     from swiftsnails_amd.ops.table import HbmTable
     from swiftsnails_amd.parallel.engine import PSEngine
@@ -247,7 +325,8 @@ def test_word2vec_trains_from_corpus_file(tmp_path, resident):
     subprocess.check_call([sys.executable, os.path.join(ROOT, "tools", "gen_word2vec_data.py"), p,
                            "--lines", "5000", "--zipf", "1.3", "--vocab", "2000"])
     dev = torch.device("cuda", 0)
-    src = FileCorpusSource(p, batch_size=1024, window=2, negatives=5, resident=resident)
+    src = FileCorpusSource(p, batch_size=1024, window=2, negatives=5, resident=resident,
+                           mode=mode)
     assert src.resident == resident
     opt, init = make_w2v_table_args(32)
     table = HbmTable(capacity=16384, dim=32, optimizer=opt, init=init, device=dev)

@@ -2,14 +2,14 @@
 colocated and split server/worker roles), checked against a single-table
 oracle that applies each round's merged gradients source-rank by source-rank.
 """
-import os
-import socket
 
 import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
+
+from _mp import collect, file_init, init_gloo
 
 DIM = 3
 ROUNDS = 4
@@ -47,11 +47,8 @@ def _oracle(world, workers, opt_kind):
     return t.to_dict(with_state=True), pulled
 
 
-def _run_rank(rank, world, port, servers, workers, opt_kind, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _run_rank(rank, world, init, servers, workers, opt_kind, q):
+    init_gloo(init, rank, world)
     try:
         from swiftsnails_amd.ops.host_table import HostTable
         from swiftsnails_amd.ops.optim import InitConfig, Optimizer
@@ -81,14 +78,6 @@ def _run_rank(rank, world, port, servers, workers, opt_kind, q):
         dist.destroy_process_group()
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
 @pytest.mark.parametrize("world,servers,workers,opt", [
     (2, [0, 1], [0, 1], "adagrad"),
     (3, [0, 1, 2], [0, 1, 2], "sgd"),
@@ -100,12 +89,12 @@ def _free_port():
 def test_engine_multiprocess_gloo(world, servers, workers, opt):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_run_rank, args=(r, world, port, servers, workers, opt, q))
+    init = file_init()
+    procs = [ctx.Process(target=_run_rank, args=(r, world, init, servers, workers, opt, q))
              for r in range(world)]
     for p in procs:
         p.start()
-    res = [q.get(timeout=240) for _ in range(world)]
+    res = collect(q, procs, world, 240)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0

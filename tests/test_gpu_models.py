@@ -60,6 +60,125 @@ def test_w2v_sgns_tile_matches_reference(dev, D, bf16):
     np.testing.assert_allclose(loss.sum().item(), tot, rtol=1e-4 if not bf16 else 3e-3)
 
 
+@pytest.mark.parametrize("D,W,B", [(32, 2, 128), (64, 5, 150), (128, 5, 256), (128, 15, 100)])
+def test_w2v_window_tile_matches_reference(dev, D, W, B):
+    """Windowed skip-gram tile (k_w2v_win_bf16) vs the fp64 reference on the
+    same band of valid pairs: every run position its own row, so each row's
+    gradient (summed over the tiles whose window covers it) is checked;
+    random sentence tags, reduced windows and masked positions; a partial
+    last tile (B = 150, 100)."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.models.word2vec import sgns_window_reference, window_pairs_reference
+
+    S, T = 64, 64
+    tiles = (B + T - 1) // T
+    R = B + 2 * W
+    rng = np.random.default_rng(D + W)
+    tags = np.cumsum(rng.random(R) < 0.08)  # sentences of ~12 tokens
+    bs = rng.integers(1, W + 1, R)
+    meta = ((tags << 4) | bs).astype(np.int32)
+    meta[rng.random(R) < 0.1] = -1
+    nrows = B + R + tiles * S
+    U = (rng.standard_normal((nrows, D)) * 0.3).astype(np.float32)
+    inv = np.arange(nrows, dtype=np.int32)
+    g = torch.zeros((nrows, D), device=dev)
+    loss, pairs = torch.zeros(256 * 32, device=dev), torch.zeros(256 * 32, device=dev)
+    tu, ti, tm = (torch.from_numpy(U).to(dev), torch.from_numpy(inv).to(dev),
+                  torch.from_numpy(meta).to(dev))
+    p = ti.data_ptr()
+    npp = 5 / S
+    hip().w2v_win(p, p + B * 4, p + (B + R) * 4, tm.data_ptr(), B, W, D, npp, tu.data_ptr(),
+                  g.data_ptr(), loss.data_ptr(), pairs.data_ptr(),
+                  torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    G = g.cpu().numpy().astype(np.float64)
+    mask = window_pairs_reference(meta, B, W)
+    ref = np.zeros((nrows, D))
+    tot, npairs = 0.0, 0.0
+    for t in range(tiles):
+        c0, c1 = t * T, min(B, t * T + T)
+        q0, q1 = c0, min(R, c0 + T + 2 * W)
+        l, n, gV, gU, gN = sgns_window_reference(U[c0:c1], U[B + q0:B + q1],
+                                                 U[B + R + t * S:B + R + (t + 1) * S],
+                                                 mask[c0:c1, q0:q1], npp)
+        tot, npairs = tot + l, npairs + n
+        ref[c0:c1] += gV
+        ref[B + q0:B + q1] += gU
+        ref[B + R + t * S:B + R + (t + 1) * S] += gN
+    assert mask.sum() == npairs > 0
+    assert pairs.sum().item() == npairs
+    # bf16 rows (8 mantissa bits) in every GEMM, fp32 accumulation
+    np.testing.assert_allclose(G, ref, rtol=3e-2, atol=1e-2)
+    np.testing.assert_allclose(loss.sum().item(), tot, rtol=3e-3)
+    # centers without a valid pair and masked positions get no gradient
+    dead = ~mask.any(1)
+    assert not G[:B][dead].any()
+    assert not G[B:B + R][meta < 0].any()
+
+
+def test_w2v_stream_gen_window_layout(dev):
+    """Synthetic stream (k_w2v_stream_gen): centers are the run's middle
+    positions, sentence tags follow the position, reduced windows in [1, W],
+    and the runs of consecutive steps overlap consistently by 2W positions."""
+    from swiftsnails_amd.models.word2vec import OUT_BIT, W2VSynth
+
+    d = W2VSynth(batch_size=256, window=4, vocab=10000, sentence_len=10)
+    R, B, W = d.run_len, d.batch_size, d.window
+    out = []
+    for step in (0, 1):
+        keys = torch.empty(d.n_keys, dtype=torch.int64, device=dev)
+        meta = torch.empty(R, dtype=torch.int32, device=dev)
+        d.generate(step, 0, 1, keys, meta=meta)
+        torch.cuda.synchronize()
+        out.append((keys.cpu().numpy(), meta.cpu().numpy()))
+    (k0, m0), (k1, m1) = out
+    ob = 1 << OUT_BIT
+    for k, m, step in ((k0, m0, 0), (k1, m1, 1)):
+        run = k[B:B + R]
+        assert ((run & ob) != 0).all() and ((k[:B] & ob) == 0).all()
+        np.testing.assert_array_equal(k[:B], run[W:W + B] & ~ob)
+        assert (((k[B + R:] & ob) != 0)).all() and ((k[B + R:] & ~ob) < d.vocab).all()
+        g = step * B - W + np.arange(R)
+        valid = g >= 0
+        assert (m[~valid] == -1).all()
+        mv = m[valid].astype(np.int64)
+        np.testing.assert_array_equal(mv >> 4, g[valid] // d.sentence_len)
+        assert ((mv & 15) >= 1).all() and ((mv & 15) <= W).all()
+    # step 1's first 2W positions are step 0's last 2W
+    np.testing.assert_array_equal(k1[B:B + 2 * W], k0[B + B:B + B + 2 * W])
+    np.testing.assert_array_equal(m1[:2 * W], m0[B:B + 2 * W])
+
+
+@pytest.mark.parametrize("mode", ["window", "pairs"])
+def test_word2vec_modes_train(dev, mode):
+    """Both batch layouts train (loss per pair falls); the window layout
+    counts its pairs on the device (~B x (W + 1) minus sentence edges) and
+    carries B + 2W context keys instead of 2W per center."""
+    from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    data = W2VSynth(batch_size=2048, window=3, vocab=5000, noise=0.05, mode=mode)
+    opt, init = make_w2v_table_args(64, None)
+    table = HbmTable(64, 40000, optimizer=opt, init=init, device=dev)
+    eng = PSEngine(table, None, max_keys=data.n_keys, dim=64, device=dev)
+    w = Word2VecWorker(eng, data)
+    losses = []
+    for _ in range(40):
+        w.step()
+        losses.append(w.mean_loss())
+    table.check()
+    assert np.isfinite(losses).all()
+    assert np.mean(losses[-5:]) < 0.85 * np.mean(losses[:3]), losses
+    if mode == "window":
+        assert data.n_keys == 2048 + 2048 + 6 + 32 * 64
+        assert w.samples_per_step() == 2048
+        n = w.step_pairs()
+        assert 0.7 * 2048 * 4 < n <= 2048 * 6, n
+    else:
+        assert w.step_pairs() == 2048 * 6
+
+
 def test_w2v_sgns_duplicate_rows_accumulate(dev):
     """Repeated words (same unique row) must receive the SUM of their grads."""
     from swiftsnails_amd._native import hip
@@ -256,14 +375,15 @@ def _graph_worker(model, dev, **ek):
         eng = PSEngine(table, ek.pop("transport", None), max_keys=2048 * 16, dim=9, device=dev,
                        **ek)
         return FMWorker(eng, data), table
-    data = W2VSynth(batch_size=1024, window=3, vocab=5000, noise=0.05)
+    data = W2VSynth(batch_size=1024, window=3, vocab=5000, noise=0.05,
+                    mode="pairs" if model == "w2v_pairs" else "window")
     opt, init = make_w2v_table_args(64, None)
     table = HbmTable(64, 40000, optimizer=opt, init=init, device=dev)
     eng = PSEngine(table, ek.pop("transport", None), max_keys=data.n_keys, dim=64, device=dev, **ek)
     return Word2VecWorker(eng, data), table
 
 
-@pytest.mark.parametrize("model", ["lr", "fm", "w2v"])
+@pytest.mark.parametrize("model", ["lr", "fm", "w2v", "w2v_pairs"])
 def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
     """hipGraph replays (one graph per ring phase, device step counter for
     the generator) train exactly like eager steps: same per-step losses and
@@ -300,7 +420,7 @@ def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
     np.testing.assert_allclose(b, a, rtol=0, atol=2 * ta.opt.lr * n)
 
 
-@pytest.mark.parametrize("model", ["fm", "w2v"])
+@pytest.mark.parametrize("model", ["fm", "w2v", "w2v_pairs"])
 def test_hipgraph_pull_ahead_trains(dev, model):
     """Graph replays of the pull-ahead pipeline (rows of round i+1 pulled on
     the route stream while round i computes) keep training."""
@@ -323,7 +443,7 @@ def test_word2vec_context_reduce_matches_atomics(dev, monkeypatch):
     out = {}
     for mode in ("reduce", "atomic"):
         monkeypatch.setenv("SS_W2V_CTX", mode)  # (atomic is the default)
-        w, t = _graph_worker("w2v", dev)
+        w, t = _graph_worker("w2v_pairs", dev)
         assert w.ctx_reduce == (mode == "reduce")
         losses = [float(w.step().sum().item()) for _ in range(6)]
         torch.cuda.synchronize()

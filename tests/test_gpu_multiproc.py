@@ -7,7 +7,6 @@
   communicator's alltoallv (skipped if RCCL refuses duplicate devices).
 """
 import os
-import queue
 import socket
 
 import numpy as np
@@ -16,6 +15,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from _mp import collect, file_init, init_gloo
 from test_engine_cpu import DIM, ROUNDS, _grads_for, _keys_for, _oracle
 
 pytestmark = pytest.mark.gpu
@@ -29,11 +29,8 @@ def _free_port():
     return p
 
 
-def _run_rank(rank, world, port, servers, workers, opt_kind, transport, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+def _run_rank(rank, world, init, servers, workers, opt_kind, transport, q):
+    init_gloo(init, rank, world)
     try:
         from swiftsnails_amd.ops.optim import InitConfig, Optimizer
         from swiftsnails_amd.ops.table import HbmTable
@@ -73,20 +70,13 @@ def _run_rank(rank, world, port, servers, workers, opt_kind, transport, q):
 def _run(world, servers, workers, opt, transport):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
+    init = file_init()
     procs = [ctx.Process(target=_run_rank,
-                         args=(r, world, port, servers, workers, opt, transport, q))
+                         args=(r, world, init, servers, workers, opt, transport, q))
              for r in range(world)]
     for p in procs:
         p.start()
-    res = []
-    try:
-        for _ in range(world):
-            res.append(q.get(timeout=180))
-    except queue.Empty:
-        for p in procs:
-            p.kill()
-        raise
+    res = collect(q, procs, world, 180)
     for p in procs:
         p.join(60)
     if any(r[1] == "skip" for r in res):
@@ -121,12 +111,9 @@ def test_engine_gpu_rccl_same_device():
     _run(2, [0, 1], [0, 1], "adagrad", "rccl")
 
 
-def _run_lr_rank(rank, world, port, pull_ahead, grad_mode, q):
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+def _run_lr_rank(rank, world, init, pull_ahead, grad_mode, q):
     os.environ["SS_PULL_AHEAD"] = "1" if pull_ahead else "0"
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    init_gloo(init, rank, world)
     try:
         from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
         from swiftsnails_amd.parallel.engine import PSEngine
@@ -159,12 +146,12 @@ def test_lr_worker_world2_pull_ahead(grad_mode):
     out = {}
     for pa in (False, True):
         q = ctx.Queue()
-        port = _free_port()
-        procs = [ctx.Process(target=_run_lr_rank, args=(r, 2, port, pa, grad_mode, q))
+        init = file_init()
+        procs = [ctx.Process(target=_run_lr_rank, args=(r, 2, init, pa, grad_mode, q))
                  for r in range(2)]
         for p in procs:
             p.start()
-        res = [q.get(timeout=240) for _ in range(2)]
+        res = collect(q, procs, 2, 240)
         for p in procs:
             p.join(60)
             assert p.exitcode == 0

@@ -74,7 +74,7 @@ def build_rank(a, rank: int, world: int, servers, workers, tr, ct, pt, dev):
         cls = SparseLRWorker if a.model == "sparse_lr" else FMWorker
         w = cls(eng, data, rank=rank, world=world, active=work)
     else:
-        data = W2VSynth(batch_size=a.batch, window=a.window, vocab=a.vocab)
+        data = W2VSynth(batch_size=a.batch, window=a.window, vocab=a.vocab, mode=a.w2v_mode)
         opt, init = make_w2v_table_args(a.dim, None)
         table = (HbmTable(a.dim, int(2 * a.vocab / S / a.load) + 1024, optimizer=opt, init=init,
                           device=dev) if serve else None)
@@ -150,6 +150,7 @@ def main(argv=None):
     ap.add_argument("--vocab", type=int, default=1_000_000)
     ap.add_argument("--window", type=int, default=5)
     ap.add_argument("--dim", type=int, default=128)
+    ap.add_argument("--w2v-mode", default="window", choices=["window", "pairs"])
     ap.add_argument("--log-every", type=int, default=0)
     ap.add_argument("--timeout", type=float, default=1500)
     a = ap.parse_args(argv)
