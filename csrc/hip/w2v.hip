@@ -249,135 +249,140 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
   float* red = Gv + (POS ? kT * P : 0);                 // [kNW] loss partials
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const long long t0 = (long long)blockIdx.x * kT;
   __shared__ uint32_t rc[kT], rn[kS];
-  if (tid < kT) rc[tid] = (t0 + tid < B) ? inv_c[t0 + tid] : kInv;
-  else if (tid < kT + kS) rn[tid - kT] = inv_n[(long long)blockIdx.x * kS + (tid - kT)];
-  __syncthreads();
-  // rows -> bf16 tiles, 4 coordinates per thread (16-B loads, 8-B LDS stores)
-  for (int e = tid; e < kT * D / 4; e += kWG) {
-    const int r = e / (D / 4), d = 4 * (e - r * (D / 4));
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f), n = v;
-    if (rc[r] != kInv) v = *reinterpret_cast<const float4*>(uvals + (long long)rc[r] * D + d);
-    if (rn[r] != kInv) n = *reinterpret_cast<const float4*>(uvals + (long long)rn[r] * D + d);
-    const uint2 pv = make_uint2(f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
-                                f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
-    const uint2 pn = make_uint2(f2bf(n.x) | ((uint32_t)f2bf(n.y) << 16),
-                                f2bf(n.z) | ((uint32_t)f2bf(n.w) << 16));
-    *reinterpret_cast<uint2*>(Vb + r * PB + d) = pv;
-    *reinterpret_cast<uint2*>(Nb + r * PB + d) = pn;
-  }
-  if (POS)
-    for (int e = tid; e < kT * P; e += kWG) Gv[e] = 0.f;
-  __syncthreads();
-
+  const int ntiles = (B + kT - 1) / kT;
   float loss = 0.f;
-  const int r32 = lane & 31, h = lane >> 5;
-  // ---- S = V·Nᵀ: wave w < 4 owns quadrant (w>>1, w&1)
-  if (w < 4) {
-    const int i0 = (w >> 1) * 32, j0 = (w & 1) * 32;
-    f32x16 acc = {};
-#pragma unroll
-    for (int k0 = 0; k0 < D; k0 += 16) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Vb + (i0 + r32) * PB + k0 + 8 * h);
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(Nb + (j0 + r32) * PB + k0 + 8 * h);
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+  // a grid smaller than the tile count walks tiles (as in k_w2v_win_bf16)
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const long long t0 = (long long)tile * kT;
+    if (tid < kT) rc[tid] = (t0 + tid < B) ? inv_c[t0 + tid] : kInv;
+    else if (tid < kT + kS) rn[tid - kT] = inv_n[(long long)tile * kS + (tid - kT)];
+    __syncthreads();
+    // rows -> bf16 tiles, 4 coordinates per thread (16-B loads, 8-B LDS stores)
+    for (int e = tid; e < kT * D / 4; e += kWG) {
+      const int r = e / (D / 4), d = 4 * (e - r * (D / 4));
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f), n = v;
+      if (rc[r] != kInv) v = *reinterpret_cast<const float4*>(uvals + (long long)rc[r] * D + d);
+      if (rn[r] != kInv) n = *reinterpret_cast<const float4*>(uvals + (long long)rn[r] * D + d);
+      const uint2 pv = make_uint2(f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16),
+                                  f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+      const uint2 pn = make_uint2(f2bf(n.x) | ((uint32_t)f2bf(n.y) << 16),
+                                  f2bf(n.z) | ((uint32_t)f2bf(n.w) << 16));
+      *reinterpret_cast<uint2*>(Vb + r * PB + d) = pv;
+      *reinterpret_cast<uint2*>(Nb + r * PB + d) = pn;
     }
+    if (POS)
+      for (int e = tid; e < kT * P; e += kWG) Gv[e] = 0.f;
+    __syncthreads();
+
+    const int r32 = lane & 31, h = lane >> 5;
+    // ---- S = V·Nᵀ: wave w < 4 owns quadrant (w>>1, w&1)
+    if (w < 4) {
+      const int i0 = (w >> 1) * 32, j0 = (w & 1) * 32;
+      f32x16 acc = {};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = i0 + mrow(r, lane), col = j0 + r32;
-      const bool ok = rc[row] != kInv && rn[col] != kInv;
-      const float sc = acc[r];
-      Gb[row * GB + col] = f2bf(ok ? neg_scale * sigm(sc) : 0.f);
-      if (ok) loss += neg_scale * softplus(sc);
-    }
-  }
-  // ---- positive pairs (fp32): wave w owns centers [kT/kNW * w, +kT/kNW); the
-  // center row comes from global with the context rows (one round trip)
-  if (POS) {
-    constexpr int R = (D + 63) / 64;
-    constexpr int TW = kT / kNW;
-    for (int t = w * TW; t < w * TW + TW; ++t) {
-      if (rc[t] == kInv) continue;  // wave-uniform
-      const uint32_t xid = lane < C ? inv_x[(t0 + t) * (long long)C + lane] : kInv;
-      float u[kMaxC][R], v[R], gv[R];
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int d = lane + 64 * r;
-        v[r] = d < D ? uvals[(long long)rc[t] * D + d] : 0.f;
-        gv[r] = 0.f;
+      for (int k0 = 0; k0 < D; k0 += 16) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Vb + (i0 + r32) * PB + k0 + 8 * h);
+        const bf16x8 b = *reinterpret_cast<const bf16x8*>(Nb + (j0 + r32) * PB + k0 + 8 * h);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
       }
 #pragma unroll
-      for (int j = 0; j < kMaxC; ++j) {
-        const uint32_t x = __shfl(xid, j, 64);
+      for (int r = 0; r < 16; ++r) {
+        const int row = i0 + mrow(r, lane), col = j0 + r32;
+        const bool ok = rc[row] != kInv && rn[col] != kInv;
+        const float sc = acc[r];
+        Gb[row * GB + col] = f2bf(ok ? neg_scale * sigm(sc) : 0.f);
+        if (ok) loss += neg_scale * softplus(sc);
+      }
+    }
+    // ---- positive pairs (fp32): wave w owns centers [kT/kNW * w, +kT/kNW); the
+    // center row comes from global with the context rows (one round trip)
+    if (POS) {
+      constexpr int R = (D + 63) / 64;
+      constexpr int TW = kT / kNW;
+      for (int t = w * TW; t < w * TW + TW; ++t) {
+        if (rc[t] == kInv) continue;  // wave-uniform
+        const uint32_t xid = lane < C ? inv_x[(t0 + t) * (long long)C + lane] : kInv;
+        float u[kMaxC][R], v[R], gv[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int d = lane + 64 * r;
-          u[j][r] = (j < C && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
+          v[r] = d < D ? uvals[(long long)rc[t] * D + d] : 0.f;
+          gv[r] = 0.f;
         }
-      }
 #pragma unroll
-      for (int j = 0; j < kMaxC; ++j) {
-        const uint32_t x = __shfl(xid, j, 64);
-        if (j >= C || x == kInv) continue;  // wave-uniform
-        float part = 0.f;
+        for (int j = 0; j < kMaxC; ++j) {
+          const uint32_t x = __shfl(xid, j, 64);
 #pragma unroll
-        for (int r = 0; r < R; ++r) part += v[r] * u[j][r];
-        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-        const float g = sigm(part) - 1.f;
-        if (lane == 0) loss += softplus(-part);
-        float* gu = ugrad + (long long)x * D;
-#pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int d = lane + 64 * r;
-          if (d < D) {
-            atomicAdd(gu + d, g * v[r]);
-            gv[r] += g * u[j][r];
+          for (int r = 0; r < R; ++r) {
+            const int d = lane + 64 * r;
+            u[j][r] = (j < C && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
           }
         }
-      }
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int d = lane + 64 * r;
-        if (d < D) Gv[t * P + d] += gv[r];
-      }
-    }
-  }
-  __syncthreads();
-  // ---- gV = G·N (+ positive part) and gN = Gᵀ·V, K = 64 in 4 steps of 16.
-  // Row-major fragments (G's rows for gV's A) are one 16-B LDS read; the
-  // k-strided ones (N for gV's B, G and V for gN) are gathered per element.
-  constexpr int NT = 2 * (D / 32);
-  for (int tt = w; tt < 2 * NT; tt += kNW) {
-    const bool center = tt < NT;
-    const int q = center ? tt : tt - NT;
-    const int ti = q / (D / 32), tj = q % (D / 32);
-    f32x16 acc = {};
+        for (int j = 0; j < kMaxC; ++j) {
+          const uint32_t x = __shfl(xid, j, 64);
+          if (j >= C || x == kInv) continue;  // wave-uniform
+          float part = 0.f;
 #pragma unroll
-    for (int k0 = 0; k0 < 64; k0 += 16) {
-      bf16x8 a, b;
-      const int kb = k0 + 8 * h;
-      if (center) {  // A[i][k] = G[ti*32+i][k], B[k][j] = N[k][tj*32+j]
-        a = *reinterpret_cast<const bf16x8*>(Gb + (ti * 32 + r32) * GB + kb);
+          for (int r = 0; r < R; ++r) part += v[r] * u[j][r];
+          for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+          const float g = sigm(part) - 1.f;
+          if (lane == 0) loss += softplus(-part);
+          float* gu = ugrad + (long long)x * D;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) b[j] = (short)Nb[(kb + j) * PB + tj * 32 + r32];
-      } else {       // A[i][k] = G[k][ti*32+i], B[k][j] = V[k][tj*32+j]
+          for (int r = 0; r < R; ++r) {
+            const int d = lane + 64 * r;
+            if (d < D) {
+              atomicAdd(gu + d, g * v[r]);
+              gv[r] += g * u[j][r];
+            }
+          }
+        }
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          a[j] = (short)Gb[(kb + j) * GB + ti * 32 + r32];
-          b[j] = (short)Vb[(kb + j) * PB + tj * 32 + r32];
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          if (d < D) Gv[t * P + d] += gv[r];
         }
       }
-      acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
     }
+    __syncthreads();
+    // ---- gV = G·N (+ positive part) and gN = Gᵀ·V, K = 64 in 4 steps of 16.
+    // Row-major fragments (G's rows for gV's A) are one 16-B LDS read; the
+    // k-strided ones (N for gV's B, G and V for gN) are gathered per element.
+    constexpr int NT = 2 * (D / 32);
+    for (int tt = w; tt < 2 * NT; tt += kNW) {
+      const bool center = tt < NT;
+      const int q = center ? tt : tt - NT;
+      const int ti = q / (D / 32), tj = q % (D / 32);
+      f32x16 acc = {};
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
-      const uint32_t dst = center ? rc[row] : rn[row];
-      if (dst == kInv) continue;
-      const float v = acc[r] + (POS && center ? Gv[row * P + col] : 0.f);
-      atomicAdd(ugrad + (long long)dst * D + col, v);
+      for (int k0 = 0; k0 < 64; k0 += 16) {
+        bf16x8 a, b;
+        const int kb = k0 + 8 * h;
+        if (center) {  // A[i][k] = G[ti*32+i][k], B[k][j] = N[k][tj*32+j]
+          a = *reinterpret_cast<const bf16x8*>(Gb + (ti * 32 + r32) * GB + kb);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) b[j] = (short)Nb[(kb + j) * PB + tj * 32 + r32];
+        } else {       // A[i][k] = G[k][ti*32+i], B[k][j] = V[k][tj*32+j]
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            a[j] = (short)Gb[(kb + j) * GB + ti * 32 + r32];
+            b[j] = (short)Vb[(kb + j) * PB + tj * 32 + r32];
+          }
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
+        const uint32_t dst = center ? rc[row] : rn[row];
+        if (dst == kInv) continue;
+        const float v = acc[r] + (POS && center ? Gv[row * P + col] : 0.f);
+        atomicAdd(ugrad + (long long)dst * D + col, v);
+      }
     }
+    __syncthreads();  // the next tile overwrites the LDS tiles
   }
   for (int o = 32; o > 0; o >>= 1) loss += __shfl_down(loss, o, 64);
   if (lane == 0) red[w] = loss;
@@ -862,6 +867,26 @@ size_t w2v_smem_bytes(int D) {
   return sizeof(float) * ((size_t)3 * kT * P + (size_t)kT * (kS + 1) + kNW);
 }
 
+// Grid of the window tile kernel (k_w2v_win_bf16): half the CUs,
+// each workgroup walking tiles.  One workgroup per tile fills every CU with
+// an 80+ KB-LDS workgroup for the kernel's whole run, and the route stream's
+// dedup (53 KB LDS) of the next round then runs 5x slower beside it (11 -> 57
+// us).  Window layout, 16K centers: caps 256 / 192 / 160 / 128 / 96 / 64 gave
+// 0.143 / 0.124 / 0.121 / 0.123 / 0.128 / 0.148 ms/step.  SS_W2V_WIN_GRID
+// overrides (0: one workgroup per tile)
+static int w2v_tile_grid(int tiles) {
+  static const int cap = [] {
+    const char* e = std::getenv("SS_W2V_WIN_GRID");
+    if (e) return std::atoi(e);
+    int dev = 0, cus = 0;
+    check_hip(hipGetDevice(&dev), "hipGetDevice");
+    check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
+              "CU count");
+    return std::max(1, cus / 2);
+  }();
+  return cap > 0 ? std::min(tiles, cap) : tiles;
+}
+
 // Raise a kernel's dynamic-LDS limit once per process (a driver call per
 // launch costs host time on the small-batch path); thread-safe static init.
 template <auto Kernel>
@@ -889,6 +914,9 @@ static void launch_w2v_bf16(bool split, int tiles, const uint32_t* inv_c, const 
     smem_attr_once<k_w2v_sgns_bf16<D, false>>(sm);
   else
     smem_attr_once<k_w2v_sgns_bf16<D, true>>(sm);
+  // one workgroup per tile: the pairs tile is bound by its own ~84 MB of row
+  // atomics per 16K-center step and needs every CU (half the CUs, as the
+  // window tile uses: 0.272 -> 0.289 ms/step)
   hipLaunchKernelGGL(k, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, neg_scale, uvals,
                      ugrad, loss_sum);
 }
@@ -965,23 +993,7 @@ void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t
   if (B <= 0) return;
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_win: window must be in [1, 15]");
   const int tiles = (B + kT - 1) / kT;
-  // Default grid: half the CUs, each workgroup walking tiles.  One
-  // workgroup per tile fills every CU with an 85 KB-LDS workgroup for the
-  // kernel's whole run and the route stream's dedup (53 KB LDS) of the next
-  // round then runs 5x slower beside it (11 -> 57 us); with half the CUs
-  // left to it the step measured 0.143 -> 0.123 ms (1M vocab, dim 128, 16K
-  // centers; caps 192 / 128 / 64: 0.124 / 0.123 / 0.148).  SS_W2V_WIN_GRID
-  // overrides (0: one workgroup per tile)
-  static const int grid_cap = [] {
-    const char* e = std::getenv("SS_W2V_WIN_GRID");
-    if (e) return std::atoi(e);
-    int dev = 0, cus = 0;
-    check_hip(hipGetDevice(&dev), "hipGetDevice");
-    check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
-              "CU count");
-    return std::max(1, cus / 2);
-  }();
-  const int grid = grid_cap > 0 ? std::min(tiles, grid_cap) : tiles;
+  const int grid = w2v_tile_grid(tiles);
   switch (D) {
 #define SS_W2VW_CASE(DD)                                                                     \
   case DD:                                                                                   \
