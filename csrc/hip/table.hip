@@ -535,6 +535,50 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
   }
 }
 
+// K5 for narrow multi-coordinate rows (FM: 9 weights + 9 AdaGrad sums, 4
+// lanes per key): the row moves as 8-byte chunks staged through LDS.  The
+// per-coordinate form (apply_row) issues a 4-byte access per lane per array
+// and coordinate round — 6 loads and 6 stores per key for an FM row, each a
+// separate request to the same two or three sectors; here a key's row is 3
+// float2 loads and 3 stores (32 contiguous bytes per instruction per key),
+// regrouped into (w_j, s_j) pairs in LDS.
+static constexpr int kStageMaxW = 48;  // row floats staged per key (dim * (1 + state))
+template <int G>
+__global__ __launch_bounds__(256) void k_apply_st(DevTable t, const long long* __restrict__ slots,
+                                                  const float* __restrict__ grads, SegList sl,
+                                                  OptParams op) {
+  __shared__ float stage[256 / G][kStageMaxW + 1];
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x % G, grp = threadIdx.x / G;
+  const long long ngroups = (long long)gridDim.x * (256 / G);
+  const int dim = (int)t.dim, ns = opt_state_per_coord(op.kind);
+  const int W = dim * (1 + ns), nch = W / 2;  // W even (launch_apply checks)
+  float* st = stage[grp];
+  for (long long g = (long long)blockIdx.x * (256 / G) + grp; g < total; g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    const long long slot = slots[pos];
+    if (slot < 0) continue;  // the same for the G lanes of a group
+    float2* row = reinterpret_cast<float2*>(slot_row(t, slot));
+    for (int k = lg; k < nch; k += G) {
+      const float2 v = row[k];
+      st[2 * k] = v.x;
+      st[2 * k + 1] = v.y;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int j = lg; j < dim; j += G) {
+      float w = st[j], s1 = ns > 0 ? st[dim + j] : 0.f, s2 = ns > 1 ? st[2 * dim + j] : 0.f;
+      opt_update(op, w, s1, s2, grads[pos * (long long)dim + j]);
+      st[j] = w;
+      if (ns > 0) st[dim + j] = s1;
+      if (ns > 1) st[2 * dim + j] = s2;
+    }
+    __builtin_amdgcn_wave_barrier();
+    for (int k = lg; k < nch; k += G) row[k] = make_float2(st[2 * k], st[2 * k + 1]);
+    __builtin_amdgcn_wave_barrier();
+  }
+}
+
 // K5 over a bucketed dedup's rows in OCCURRENCE-SPACE layout (unique key l of
 // bucket b at row bstart[b] + l; see bdedup.hip): one workgroup per bucket
 template <int G>
@@ -758,6 +802,21 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
     const char* e = std::getenv("SS_APPLY_VEC");
     return e ? std::atoi(e) : 1;
   }();
+  // narrow multi-coordinate rows (FM): 8-byte chunks staged through LDS
+  // (k_apply_st); SS_APPLY_STAGE=0 keeps the per-coordinate form
+  static const int stage_env = [] {
+    const char* e = std::getenv("SS_APPLY_STAGE");
+    return e ? std::atoi(e) : 1;
+  }();
+  const int ns = opt_state_per_coord(op.kind);
+  const uint32_t W = t.dim * (uint32_t)(1 + ns);
+  if (stage_env && !snap && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
+      W % 2 == 0 && W == t.width && t.row_off % 8 == 0 && t.stride % 8 == 0) {
+    SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_st<kG>, dim3(grid_for(max_n, kG, 1 << 22)),
+                                        dim3(256), 0, st, t, slots, grads, sl, op));
+    check_launch("k_apply_st");
+    return;
+  }
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>,
                                       dim3(grid_for(max_n, kG, vec ? (1 << 22) : 16384)),
                                       dim3(256), 0, st, t, slots, grads, sl, op, vec,

@@ -90,8 +90,10 @@ def test_pull_duplicates_see_initialised_rows(dev, G, dim):
 
 
 @pytest.mark.parametrize("kind", ["sgd", "adagrad", "ftrl", "adam"])
-@pytest.mark.parametrize("dim", [1, 8, 33])
+@pytest.mark.parametrize("dim", [1, 5, 8, 9, 33])
 def test_apply_matches_reference(dev, kind, dim):
+    """K5 per optimizer vs the NumPy reference; dims 5-9 with state take the
+    LDS-staged 8-byte-chunk form (k_apply_st), 1 and 33 the others."""
     from swiftsnails_amd.ops.optim import InitConfig, Optimizer, apply_reference
     from swiftsnails_amd.ops.table import HbmTable
 
