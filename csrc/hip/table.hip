@@ -749,14 +749,14 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   // lane probes about once; measured 1.19 -> 1.13-1.17 ms/step vs 1 (the
   // kernel alone barely changes: smaller workgroups interleave better with
   // the route stream's kernels)
-  // (scalar rows only: FM / word2vec, whose pull runs on the lighter route
-  // stream, measured neutral)
+  // FM rows (G = 4): 2, 0.548-0.556 -> 0.541 ms/step (4: 0.544-0.551);
+  // word2vec rows (G = 64): 1 (2 and 4 neutral)
   static const int env_ny = [] {
     const char* e = std::getenv("SS_PULL_BK_Y");
     const int v = e ? std::atoi(e) : 0;
     return v < 0 ? 0 : (v > 16 ? 16 : v);
   }();
-  const int ny = env_ny ? env_ny : (G == 1 ? 4 : 1);
+  const int ny = env_ny ? env_ny : (G == 1 ? 4 : (G == 4 ? 2 : 1));
   // snapshot pulls on 16-byte [w | h | key] slots probe with one 16-byte
   // load per step (probe_slot16); SS_PULL_ONELOAD=0: key load, then row load
   static const bool oneload_env = [] {
