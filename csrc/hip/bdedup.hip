@@ -895,10 +895,13 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     return (v == 256 || v == 512 || v == 1024) ? v : def;
   };
   static const int ct = wg_env("SS_BD_CT", 1024);
-  // count: 1024 threads (at 256 chunks on the N>1 path: 1.032-1.036 ms/step
-  // vs 1.057-1.062 for 256 threads at 128 chunks; at 512 chunks both equal)
+  // count: 1024 threads on one GPU; 256 on the N>1 path, where it runs beside
+  // the server pull of the round before (k_pull_unique, capped at 4 WGs per
+  // CU): a 1024-thread workgroup needs 16 free wave slots on one CU at once
+  // and waited for them (26 us alone -> 310-385 us beside the pull); 256
+  // threads + the pull cap: 1.056-1.116 -> 1.035-1.067 ms/step on two boxes
   static const int cnt_env = wg_env("SS_BD_CNT", 0);
-  const int cnt = cnt_env ? cnt_env : 1024;
+  const int cnt = cnt_env ? cnt_env : (rs.nranks > 1 ? 256 : 1024);
   static const int cs = wg_env("SS_BD_CS", 1024);
 #define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \

@@ -16,6 +16,7 @@
 // and the G lanes sweep the row.  G=1 for sparse-LR rows (width 2 = 8 B),
 // G=16/64 for embedding rows (word2vec / FM), so a 64-wide wavefront always
 // has all lanes busy on HBM traffic.
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 
@@ -679,6 +680,20 @@ __global__ __launch_bounds__(256) void k_probe_hist(DevTable t, unsigned long lo
 }
 
 // ---------------------------------------------------------------- launchers
+// SS_PULL_GRID / SS_APPLY_GRID: cap (workgroups) on the general pull / the
+// apply (grid-stride loops), leaving CUs to the other streams' kernels.
+// `def_per_cu` > 0: default cap of that many 256-thread workgroups per CU
+static int env_grid_cap(const char* name, int def_per_cu = 0) {
+  const char* e = std::getenv(name);
+  const int v = e ? std::atoi(e) : -1;
+  if (v > 0) return v;
+  if (v == 0 || def_per_cu <= 0) return 1 << 22;
+  int dev = 0, cus = 0;
+  check_hip(hipGetDevice(&dev), "hipGetDevice");
+  check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
+  return std::max(1, cus * def_per_cu);
+}
+
 static inline int grid_for(long long groups, int G, int cap_blocks = 16384) {
   long long threads = groups * G;
   long long b = (threads + 255) / 256;
@@ -719,7 +734,11 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
   if (max_n <= 0) return;
   // one lane group per key (no grid-stride rounds: each is another serial
   // random probe for the lane)
-  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique<kG>, dim3(grid_for(max_n, kG, 1 << 22)),
+  // general pull (the N>1 server pull of the received segments): at most 4
+  // workgroups per CU, so the route stream's next dedup (count / scatter:
+  // few, large workgroups) is not starved beside it (see launch_bd_dedup)
+  static const int pull_cap = env_grid_cap("SS_PULL_GRID", 4);
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique<kG>, dim3(grid_for(max_n, kG, pull_cap)),
                                       dim3(256), 0, st, t, keys, sl, slots, out, ip, size_ctr,
                                       err));
   check_launch("k_pull_unique");
@@ -817,8 +836,9 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
     check_launch("k_apply_st");
     return;
   }
+  static const int apply_cap = env_grid_cap("SS_APPLY_GRID");
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>,
-                                      dim3(grid_for(max_n, kG, vec ? (1 << 22) : 16384)),
+                                      dim3(grid_for(max_n, kG, vec ? apply_cap : 16384)),
                                       dim3(256), 0, st, t, slots, grads, sl, op, vec,
                                       reinterpret_cast<const float2*>(snap)));
   check_launch("k_apply");

@@ -67,6 +67,12 @@ KNOBS: dict[str, Knob] = {
     "SS_PULL_ONELOAD": Knob("1", "csrc/hip/table.hip", "tuning",
                             "snapshot pull on 16-byte LR slots: one 16-byte load per probe step "
                             "(key + row) instead of a key load then a row load"),
+    "SS_PULL_GRID": Knob("4 x CUs", "csrc/hip/table.hip", "tuning",
+                         "workgroup cap of the general (N>1 server) pull, grid-stride beyond it "
+                         "(0: one group per key); with the N>1 count at 256 threads "
+                         "1.056-1.116 -> 1.035-1.067 ms/step"),
+    "SS_APPLY_GRID": Knob("0 (one group per key)", "csrc/hip/table.hip", "experiment",
+                          "workgroup cap of the apply, grid-stride beyond it"),
     "SS_APPLY_STAGE": Knob("1", "csrc/hip/table.hip", "tuning",
                            "narrow multi-coordinate rows (FM): K5 moves the row as 8-byte chunks "
                            "staged through LDS (k_apply_st)"),
@@ -78,7 +84,8 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_STAGE": Knob("0", "csrc/hip/bdedup.hip", "experiment",
                         "scatter stages keys in bucket order, dedup reads them coalesced "
                         "(0.949 -> 0.968 ms/step at 128 chunks, three A/B pairs)"),
-    "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "count workgroup size"),
+    "SS_BD_CNT": Knob("1024 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
+                      "count workgroup size"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
