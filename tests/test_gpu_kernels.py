@@ -833,3 +833,22 @@ def test_native_gpu_worker_pull_push(dev):
     assert a.keys() == b.keys()
     for k in a:
         np.testing.assert_allclose(a[k], b[k], rtol=1e-5, atol=1e-6)
+
+
+def test_stream_helpers_match_torch(dev):
+    """utils/streams.py: the explicit-device lookups and the stream switch
+    agree with torch's own view of the current stream, and restore it."""
+    from swiftsnails_amd.utils.streams import current, current_raw, use_stream
+
+    idx = dev.index or 0
+    base = torch.cuda.current_stream(dev)
+    assert current_raw(idx) == base.cuda_stream == current_raw()
+    assert current(idx) == base
+    s = torch.cuda.Stream(device=dev)
+    with use_stream(s):
+        assert torch.cuda.current_stream(dev) == s
+        assert current_raw(idx) == s.cuda_stream
+        x = torch.ones(1000, device=dev) * 2  # a torch op lands on s
+    assert torch.cuda.current_stream(dev) == base
+    s.synchronize()
+    assert float(x.sum().item()) == 2000.0
