@@ -62,10 +62,15 @@ class FMWorker(PipelinedWorker):
         lanes = 1 << max(0, (F - 1).bit_length())
         self.bucketed = (F <= 64 and lanes >= K and
                          all(getattr(dd, "mode", None) == "bucket" for dd in engine.dedupers))
+        # SS_FM_INV=1: the dedup also writes the inverse index (k_bd_inv, on
+        # the route stream) and the forward reads inv[j] instead of resolving
+        # luid[pos_of[j]] itself (one dependent random load fewer on the main
+        # stream)
+        self.use_inv = os.environ.get("SS_FM_INV", "0") != "0"
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False
-                dd.materialize_inv = False
+                dd.materialize_inv = self.use_inv
             self.gs = torch.empty(B, dtype=torch.float32, device=dev)
             self.gss = torch.empty(B * K, dtype=torch.float32, device=dev)
             # overflow-bucket list of the sorted reduce (buckets too large to
@@ -81,7 +86,8 @@ class FMWorker(PipelinedWorker):
         d = self.data
         if self.bucketed:
             h, o, dd = hip(), rnd.dd.owner, rnd.dd
-            h.fm_fwd_g(0, o.index_ptrs(dd.n), self.labels[slot].data_ptr(),
+            h.fm_fwd_g(rnd.inv.data_ptr() if self.use_inv else 0, o.index_ptrs(dd.n),
+                       self.labels[slot].data_ptr(),
                        d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                        self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
             # SS_FM_FUSE_APPLY=1 (one GPU): the sorted merge runs the optimizer
