@@ -67,6 +67,11 @@ class FMWorker(PipelinedWorker):
         # luid[pos_of[j]] itself (one dependent random load fewer on the main
         # stream).  Measured slower, 0.536 -> 0.552 ms/step: off
         self.use_inv = os.environ.get("SS_FM_INV", "0") != "0"
+        # SS_FM_PULL_GATE=1: the next round's pulled-ahead lookup starts after
+        # this round's forward (engine.gate_next_pull), so the forward's
+        # gathers run alone.  Measured slower, 0.537-0.539 -> 0.565-0.573
+        # ms/step (the lookup then crowds the merge and the update): off
+        self.pull_after_fwd = os.environ.get("SS_FM_PULL_GATE", "0") != "0"
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False
@@ -90,6 +95,8 @@ class FMWorker(PipelinedWorker):
                        self.labels[slot].data_ptr(),
                        d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                        self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
+            if self.pull_after_fwd:
+                self.engine.gate_next_pull(slot)
             # SS_FM_FUSE_APPLY=1 (one GPU): the sorted merge runs the optimizer
             # update itself, one thread per row.  Measured slower (0.62 ->
             # 1.04 ms/step): a thread's 18 dependent 4-byte accesses to a random

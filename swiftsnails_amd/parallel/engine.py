@@ -265,6 +265,9 @@ class PSEngine:
             self._ev_pull = [torch.cuda.Event() for _ in range(self.depth)]
             self._ev_free = [torch.cuda.Event() for _ in range(self.depth)]
             self._ev_grad = [torch.cuda.Event() for _ in range(self.depth)]
+            self._ev_gate = [torch.cuda.Event() for _ in range(self.depth)]
+        # gate_next_pull(): the next pulled-ahead round waits for this event
+        self._pull_gate = None
         # push on the pull stream (N>1 with a pull stream, SS_PUSH_STREAM=pull):
         # round i's gradient all-to-all-v and server apply are enqueued on the
         # pull stream right behind round i+1's pull (the worker calls
@@ -469,6 +472,7 @@ class PSEngine:
             if rs is not self.route_stream:
                 self._wait(rs, r.ready, r.tag)
             self._bound_staleness(rs, slot)
+            self._take_gate(rs)
             with use_stream(rs), self.trace("pull", rs):
                 own = dd.owner
                 if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
@@ -487,6 +491,7 @@ class PSEngine:
         if ps is not self.route_stream:
             self._wait(ps, r.ready, r.tag)
         self._bound_staleness(ps, slot)
+        self._take_gate(ps)
         with use_stream(ps), self.trace("pull", ps):
             self.pt.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
             self._server_pull(rcounts, slot)
@@ -499,6 +504,25 @@ class PSEngine:
                          a2a_bytes=8 * (sent + recv) + 4 * self.dim * (2 * sent + 2 * recv))
         return Round(dd, uv, slot, scounts=scounts, rcounts=rcounts,
                      stats={"sent": sent, "recv": recv}, ready=ev, tag=self.capture_tag)
+
+    def gate_next_pull(self, slot: int) -> None:
+        """Make the next ``pull_ahead_round`` wait for the work enqueued so
+        far on the current stream (a model calls this inside its compute, after
+        the kernels the lookup should not run beside).  Used by FM's
+        SS_FM_PULL_GATE experiment (lookup behind the forward, whose gathers
+        it slows 84 -> 215 us: the step measured slower, the lookup then
+        crowds the merge and the update)."""
+        if not self.gpu:
+            return
+        ev = self._ev_gate[slot]
+        ev.record(self.main_stream())
+        self._pull_gate = (ev, self.capture_tag)
+
+    def _take_gate(self, stream) -> None:
+        if self._pull_gate is not None:
+            ev, tag = self._pull_gate
+            self._pull_gate = None
+            self._wait(stream, ev, tag)
 
     def _bound_staleness(self, stream, slot: int) -> None:
         """Pull-ahead of round i+1 (ring slot ``slot``): wait until round

@@ -108,6 +108,9 @@ KNOBS: dict[str, Knob] = {
                          "store instead of add for keys seen once (reduce -6 us, step unchanged)"),
     "SS_LR_INV": Knob("0", "models/sparse_lr.py", "experiment",
                       "materialised inverse on the route stream (neutral)"),
+    "SS_FM_PULL_GATE": Knob("0", "models/fm.py", "experiment",
+                            "the next round's pulled-ahead lookup waits for this round's "
+                            "forward (0.537 -> 0.565 ms/step)"),
     "SS_FM_INV": Knob("0", "models/fm.py", "experiment",
                       "FM forward reads a materialised inverse index (k_bd_inv on the route "
                       "stream) instead of resolving luid[pos_of[j]] (0.536 -> 0.552 ms/step)"),
