@@ -177,8 +177,9 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
                                          const InitParams& ip, int* err, int lg,
                                          unsigned long long& ins,
                                          float2* __restrict__ snap = nullptr, int one16 = 0) {
-  if (G == 1 && snap && one16) {
-    // snapshot mode on 16-byte slots: one load per probe step (probe_slot16)
+  if (G == 1 && one16) {
+    // 16-byte [w | h | key] slots: one load per probe step (probe_slot16);
+    // with `snap` the (w, h) pair also goes to the snapshot
     bool b = false;
     float2 wh = make_float2(0.f, 0.f);
     const long long slot = key != kEmptyKey ? probe_slot16(t, key, &wh, &b) : -1;
@@ -197,7 +198,7 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
       if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
     }
     o[0] = wh.x;
-    snap[pos] = wh;
+    if (snap) snap[pos] = wh;
     ins += b;
     return;
   }
@@ -264,7 +265,8 @@ template <int G>
 __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t* __restrict__ keys,
                                                      SegList sl, long long* __restrict__ slots_out,
                                                      float* __restrict__ out, InitParams ip,
-                                                     unsigned long long* size_ctr, int* err) {
+                                                     unsigned long long* size_ctr, int* err,
+                                                     int one16) {
   const long long total = seg_total(sl);
   const int lg = threadIdx.x % G;
   const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
@@ -273,7 +275,7 @@ __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t*
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    pull_one<G>(t, keys[pos], pos, slots_out, out, ip, err, lg, ins);
+    pull_one<G>(t, keys[pos], pos, slots_out, out, ip, err, lg, ins, nullptr, one16);
   }
   ins = wave_sum_u64(ins);
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
@@ -732,15 +734,22 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
                         long long max_n, long long* slots, float* out, const InitParams& ip,
                         unsigned long long* size_ctr, int* err, int G, hipStream_t st) {
   if (max_n <= 0) return;
-  // one lane group per key (no grid-stride rounds: each is another serial
-  // random probe for the lane)
   // general pull (the N>1 server pull of the received segments): at most 4
-  // workgroups per CU, so the route stream's next dedup (count / scatter:
-  // few, large workgroups) is not starved beside it (see launch_bd_dedup)
+  // workgroups per CU, grid-stride beyond, so the route stream's next dedup
+  // (count / scatter: few, large workgroups) is not starved beside it (see
+  // launch_bd_dedup)
   static const int pull_cap = env_grid_cap("SS_PULL_GRID", 4);
+  // SS_PULL_ONELOAD_GEN=1: 16-byte LR slots probed with one load per step
+  // (key + row), as the snapshot pull does
+  static const int oneload_gen = [] {
+    const char* e = std::getenv("SS_PULL_ONELOAD_GEN");
+    return e ? std::atoi(e) : 0;
+  }();
+  const int one16 = oneload_gen && G == 1 && t.dim == 1 && t.stride == 16 && t.key_off == 8 &&
+                    t.row_off == 0;
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique<kG>, dim3(grid_for(max_n, kG, pull_cap)),
                                       dim3(256), 0, st, t, keys, sl, slots, out, ip, size_ctr,
-                                      err));
+                                      err, one16));
   check_launch("k_pull_unique");
 }
 

@@ -76,6 +76,9 @@ KNOBS: dict[str, Knob] = {
     "SS_APPLY_STAGE": Knob("1", "csrc/hip/table.hip", "tuning",
                            "narrow multi-coordinate rows (FM): K5 moves the row as 8-byte chunks "
                            "staged through LDS (k_apply_st)"),
+    "SS_PULL_ONELOAD_GEN": Knob("0", "csrc/hip/table.hip", "experiment",
+                                "general (N>1 server) pull on 16-byte LR slots: one 16-byte load "
+                                "per probe step (neutral: 1.081-1.085 vs 1.076-1.090 ms/step)"),
     "SS_APPLY_VEC": Knob("1", "csrc/hip/table.hip", "tuning",
                          "one lane group per key + 8-byte (w, h) accesses in k_apply"),
     "SS_BD_NCH": Knob("128 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
