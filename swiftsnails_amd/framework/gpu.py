@@ -315,6 +315,11 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     m = ctx.engine.metrics.counters
     if m:
         stats["rank0_engine"] = {k: int(v) for k, v in m.items()}
+    if getattr(w, "window_mode", False) and ctx.is_worker:
+        # word2vec sliding-window batches: samples are words (centers); the
+        # positive pairs per step depend on sentence edges and reduced windows
+        stats["pairs_last_step"] = w.step_pairs()
+        stats["pairs_per_s_est"] = stats["pairs_last_step"] * steps / el if el > 0 else 0.0
     if ctx.tracer.enabled:
         stats["trace"] = ctx.tracer.summary()
     if ctx.table is not None and str(cfg.get("table_stats", "1")) != "0":
