@@ -319,7 +319,8 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
         # word2vec sliding-window batches: samples are words (centers); the
         # positive pairs per step depend on sentence edges and reduced windows
         stats["rank0_pairs_last_step"] = w.step_pairs()
-        stats["rank0_pairs_per_s_est"] = stats["rank0_pairs_last_step"] * steps / el if el > 0 else 0.0
+        stats["rank0_pairs_per_s_est"] = (stats["rank0_pairs_last_step"] * steps / el
+                                          if el > 0 else 0.0)
     if ctx.tracer.enabled:
         stats["trace"] = ctx.tracer.summary()
     if ctx.table is not None and str(cfg.get("table_stats", "1")) != "0":
