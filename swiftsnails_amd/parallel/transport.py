@@ -35,8 +35,15 @@ class CountsHandle:
                  event=None, pinned: Optional[torch.Tensor] = None, world: int = 1):
         self._s, self._r, self.event, self.pinned, self.world = s, r, event, pinned, world
 
+    # SS_COUNTS_SPIN=1: poll the event instead of a blocking synchronize (the
+    # host's wake-up is on the N>1 critical cycle: route -> counts -> pull)
+    _spin = os.environ.get("SS_COUNTS_SPIN", "0") != "0"
+
     def wait(self) -> tuple[np.ndarray, np.ndarray]:
         if self._s is None:
+            if self._spin:
+                while not self.event.query():
+                    pass
             self.event.synchronize()
             p = self.pinned.numpy()
             self._s, self._r = p[:self.world].copy(), p[self.world:2 * self.world].copy()

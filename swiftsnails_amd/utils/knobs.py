@@ -139,6 +139,9 @@ KNOBS: dict[str, Knob] = {
                             "grid of the windowed word2vec tile kernel (workgroups walk tiles; "
                             "0: one per tile), leaving CUs to the route stream's dedup "
                             "(0.143 -> 0.123 ms/step)"),
+    "SS_COUNTS_SPIN": Knob("0", "parallel/transport.py", "experiment",
+                           "N>1: busy-poll the count exchange's event instead of a blocking "
+                           "synchronize (neutral on one GPU: 1.034-1.040 vs 1.036-1.054)"),
     "SS_PUSH_STREAM": Knob("main", "parallel/engine.py", "experiment",
                            "pull: N>1 gradient exchange + server apply on the pull stream "
                            "behind the next round's pull (1.049-1.053 -> 1.058-1.103 ms/step: "
