@@ -550,24 +550,25 @@ template <int G>
 __global__ __launch_bounds__(256) void k_apply_st(DevTable t, const long long* __restrict__ slots,
                                                   const float* __restrict__ grads, SegList sl,
                                                   OptParams op) {
-  __shared__ float stage[256 / G][kStageMaxW + 1];
+  // even row stride: the load/store phases move float2 pairs as one 8-byte
+  // LDS access (an odd stride split them into two 4-byte accesses); 52 floats
+  // = 20 mod 32 puts the 8 four-lane groups of a half-wave on disjoint 4-bank
+  // slots for the 4-byte update-phase accesses
+  __shared__ float2 stage2[256 / G][kStageMaxW / 2 + 2];
   const long long total = seg_total(sl);
   const int lg = threadIdx.x % G, grp = threadIdx.x / G;
   const long long ngroups = (long long)gridDim.x * (256 / G);
   const int dim = (int)t.dim, ns = opt_state_per_coord(op.kind);
   const int W = dim * (1 + ns), nch = W / 2;  // W even (launch_apply checks)
-  float* st = stage[grp];
+  float2* st2 = stage2[grp];
+  float* st = reinterpret_cast<float*>(st2);
   for (long long g = (long long)blockIdx.x * (256 / G) + grp; g < total; g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
     const long long slot = slots[pos];
     if (slot < 0) continue;  // the same for the G lanes of a group
     float2* row = reinterpret_cast<float2*>(slot_row(t, slot));
-    for (int k = lg; k < nch; k += G) {
-      const float2 v = row[k];
-      st[2 * k] = v.x;
-      st[2 * k + 1] = v.y;
-    }
+    for (int k = lg; k < nch; k += G) st2[k] = row[k];
     __builtin_amdgcn_wave_barrier();
     for (int j = lg; j < dim; j += G) {
       float w = st[j], s1 = ns > 0 ? st[dim + j] : 0.f, s2 = ns > 1 ? st[2 * dim + j] : 0.f;
@@ -577,7 +578,7 @@ __global__ __launch_bounds__(256) void k_apply_st(DevTable t, const long long* _
       if (ns > 1) st[2 * dim + j] = s2;
     }
     __builtin_amdgcn_wave_barrier();
-    for (int k = lg; k < nch; k += G) row[k] = make_float2(st[2 * k], st[2 * k + 1]);
+    for (int k = lg; k < nch; k += G) row[k] = st2[k];
     __builtin_amdgcn_wave_barrier();
   }
 }
