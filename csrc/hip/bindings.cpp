@@ -407,10 +407,26 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("w2v_win", [](uintptr_t inv_c, uintptr_t inv_w, uintptr_t inv_n, uintptr_t meta, int B,
                       int W, int D, float neg_per_pair, uintptr_t uvals, uintptr_t ugrad,
-                      uintptr_t loss, uintptr_t pairs, uintptr_t st) {
+                      uintptr_t loss, uintptr_t pairs, uintptr_t st, uintptr_t ograd,
+                      uintptr_t otail) {
     launch_w2v_win(P<const uint32_t>(inv_c), P<const uint32_t>(inv_w), P<const uint32_t>(inv_n),
                    P<const int32_t>(meta), B, W, D, neg_per_pair, P<const float>(uvals),
-                   P<float>(ugrad), P<float>(loss), P<float>(pairs), S(st));
+                   P<float>(ugrad), P<float>(loss), P<float>(pairs), S(st), P<float>(ograd),
+                   P<float>(otail));
+  }, py::arg("inv_c"), py::arg("inv_w"), py::arg("inv_n"), py::arg("meta"), py::arg("B"),
+     py::arg("W"), py::arg("D"), py::arg("neg_per_pair"), py::arg("uvals"), py::arg("ugrad"),
+     py::arg("loss"), py::arg("pairs"), py::arg("st"), py::arg("ograd") = 0,
+     py::arg("otail") = 0);
+  m.def("w2v_osort", [](int P_, uintptr_t bstart, uintptr_t unum, uintptr_t ubase, uintptr_t pj,
+                        uintptr_t luid, uintptr_t ord, uintptr_t items, uintptr_t st) {
+    launch_w2v_osort(P_, P<const uint32_t>(bstart), P<const uint32_t>(unum),
+                     P<const uint32_t>(ubase), P<const uint32_t>(pj), P<const uint32_t>(luid),
+                     P<uint32_t>(ord), P<uint32_t>(items), S(st));
+  });
+  m.def("w2v_oreduce", [](uintptr_t items, long long n, uintptr_t ord, uintptr_t ograd,
+                          uintptr_t otail, int B, int W, int D, uintptr_t ugrad, uintptr_t st) {
+    launch_w2v_oreduce(P<const uint32_t>(items), n, P<const uint32_t>(ord), P<const float>(ograd),
+                       P<const float>(otail), B, W, D, P<float>(ugrad), S(st));
   });
   m.def("w2v_stream_gen", [](uint64_t seed, long long base, int B, int W, int L, long long nneg,
                              long long V, float noise, uintptr_t keys, uintptr_t meta, uintptr_t st,

@@ -96,7 +96,12 @@ void launch_w2v_corpus_window(const uint64_t* tokens, const uint32_t* sent_of, l
 void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                     const int32_t* meta, int B, int W, int D, float neg_per_pair,
                     const float* uvals, float* ugrad, float* loss_sum, float* pair_sum,
-                    hipStream_t st);
+                    hipStream_t st, float* ograd = nullptr, float* otail = nullptr);
+void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const uint32_t* ubase,
+                      const uint32_t* pj, const uint32_t* luid, uint32_t* ord, uint32_t* items,
+                      hipStream_t st);
+void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
+                        const float* otail, int B, int W, int D, float* ugrad, hipStream_t st);
 void launch_w2v_stream_gen(uint64_t seed, long long base, int B, int W, int L, long long nneg,
                            long long V, float noise, uint64_t* keys, int32_t* meta,
                            hipStream_t st, const long long* step_dev, long long step_mul,

@@ -23,6 +23,7 @@
 //     128-B row segments (the full-rate atomic shape on MI355X).
 #include "ss_device.h"
 #include "ss_launch.h"
+#include "scan.h"
 #include "ss/w2v_window.h"
 
 #include <algorithm>
@@ -660,7 +661,8 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
     const uint32_t* __restrict__ inv_c, const uint32_t* __restrict__ inv_w,
     const uint32_t* __restrict__ inv_n, const int32_t* __restrict__ meta, int B, int W,
     float neg_per_pair, const float* __restrict__ uvals, float* __restrict__ ugrad,
-    float* __restrict__ loss_sum, float* __restrict__ pair_sum) {
+    float* __restrict__ loss_sum, float* __restrict__ pair_sum, int gmode,
+    float* __restrict__ ograd, float* __restrict__ otail) {
   using L = W2vWinSmem<D>;
   constexpr int PB = L::PB, GPB = L::GPB, GB = L::GB, TJ = D / 32;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
@@ -704,20 +706,30 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
       cwt[tid] = (float)n * neg_per_pair;
       npairs += (float)n;
     }
-    // rows -> bf16 tiles (V, U, N are consecutive rows of stride PB)
-    for (int e = tid; e < (kT + kWU + kS) * (D / 4); e += kWG) {
-      const int r = e / (D / 4), d = 4 * (e - r * (D / 4));
-      uint32_t id;
-      if (r < kT) {
-        const long long c = t0 + r;  // read inv_c directly: rc[] is written by this same phase
-        id = (c < B && mw[r + W] >= 0) ? inv_c[c] : kInv;
-      } else {
-        id = r < kT + kWU ? rw[r - kT] : rn[r - kT - kWU];
+    __syncthreads();
+    // rows -> bf16 tiles (V, U, N are consecutive rows of stride PB).  Every
+    // load of the thread is issued before the first LDS store (one memory
+    // round trip per tile instead of one per loop trip: the loop form
+    // serialised 14 dependent gathers per thread at D = 128).  A center row
+    // without pairs (rc = kInv) stays zero: its G+ and G- rows are zero.
+    {
+      constexpr int NE = (kT + kWU + kS) * (D / 4), PER = (NE + kWG - 1) / kWG;
+      float4 v[PER];
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = tid + i * kWG, r = e / (D / 4), d = 4 * (e - r * (D / 4));
+        const uint32_t id = e >= NE ? kInv : r < kT ? rc[r] : r < kT + kWU ? rw[r - kT] : rn[r - kT - kWU];
+        v[i] = id != kInv ? *reinterpret_cast<const float4*>(uvals + (long long)id * D + d)
+                          : make_float4(0.f, 0.f, 0.f, 0.f);
       }
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (id != kInv) v = *reinterpret_cast<const float4*>(uvals + (long long)id * D + d);
-      *reinterpret_cast<uint2*>(smem16 + r * PB + d) =
-          make_uint2(f2bf(v.x) | ((uint32_t)f2bf(v.y) << 16), f2bf(v.z) | ((uint32_t)f2bf(v.w) << 16));
+#pragma unroll
+      for (int i = 0; i < PER; ++i) {
+        const int e = tid + i * kWG, r = e / (D / 4), d = 4 * (e - r * (D / 4));
+        if (e < NE)
+          *reinterpret_cast<uint2*>(smem16 + r * PB + d) =
+              make_uint2(f2bf(v[i].x) | ((uint32_t)f2bf(v[i].y) << 16),
+                         f2bf(v[i].z) | ((uint32_t)f2bf(v[i].w) << 16));
+      }
     }
     __syncthreads();
 
@@ -798,9 +810,35 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
+        if (ograd) {
+          // occurrence rows, plain stores (k_w2v_oreduce sums them per key).
+          // Every row the tile covers is written (a row without pairs has a
+          // zero gradient).  Window row l >= 64 of a tile other than the
+          // last is also row l - 64 of the next tile: it goes to the tail
+          // buffer instead, so no occurrence row has two writers.
+          long long orow = -1;
+          if (kind == 0) {
+            if (t0 + row < B) orow = t0 + row;
+          } else if (kind == 1) {
+            const long long q = t0 + row;
+            if (row < kT + 2 * W && q < R) {
+              if (row < kT || tile == ntiles - 1)
+                orow = B + q;
+              else
+                otail[((long long)tile * 2 * W + (row - kT)) * D + col] = acc[r];
+            }
+          } else {
+            orow = B + R + (long long)tile * kS + row;
+          }
+          if (orow >= 0) ograd[orow * D + col] = acc[r];
+          continue;
+        }
         const uint32_t dst = kind == 0 ? rc[row] : (kind == 1 ? (uany[row] ? rw[row] : kInv) : rn[row]);
         if (dst == kInv) continue;  // lanes 0-31 / 32-63: one 128-B row segment each
-        atomicAdd(ugrad + (long long)dst * D + col, acc[r]);
+        if (gmode == 0)
+          atomicAdd(ugrad + (long long)dst * D + col, acc[r]);
+        else if (gmode == 1 || acc[r] == 1.2345e30f)  // measurement only: stores / no output
+          ugrad[(long long)dst * D + col] = acc[r];
       }
     }
     __syncthreads();  // the next tile overwrites the LDS tiles
@@ -817,6 +855,162 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
   if (w == 0 && pair_sum) {  // centers' pair counts live in wave 0 (tid < kT)
     for (int o = 32; o > 0; o >>= 1) npairs += __shfl_down(npairs, o, 64);
     if (lane == 0) ctr_addf(pair_sum, npairs);  // valid positive pairs
+  }
+}
+
+// ---- atomic-free gradient merge of the windowed tile (SS_W2V_GRAD=reduce)
+//
+// Measured: the tile's row atomics (~52K rows of 512 B per 16K-center step,
+// two 64-lane float atomics per row) took 71 of its 71 us standalone -> 32 us
+// with the same rows as plain stores; the per-CU atomic issue rate, not
+// memory, bounds them.  So the tile stores occurrence rows (ograd: one row per
+// key position, otail: the 2W window rows a tile shares with the next one)
+// and the rows are summed per unique key here.
+//
+// k_w2v_osort (route stream: depends on the key layout only, so it runs a
+// round ahead beside the dedup) groups each dedup bucket's occurrences by
+// unique key with a counting sort in LDS and cuts every key's list into items
+// of <= kOsCh occurrences, written into the bucket's own occurrence range of
+// `items` (a bucket has at most as many items as occurrences: no global scan).
+// k_w2v_oreduce (main stream) sums one item per wave, <= 8 rows in flight, and
+// stores the key's gradient row — or adds it with row atomics when a Zipf-head
+// key has several items (its row was zeroed by the dedup): a head key's
+// thousands of occurrences spread over many waves instead of serialising one.
+static constexpr int kOsT = 256;
+static constexpr int kOsMaxU = 4096;      // unique keys per dedup bucket (bdedup.hip kBdTS)
+static constexpr uint32_t kOsCh = 32;     // occurrences per reduce item
+
+__global__ __launch_bounds__(kOsT) void k_w2v_osort(const uint32_t* __restrict__ bstart,
+                                                    const uint32_t* __restrict__ unum,
+                                                    const uint32_t* __restrict__ ubase,
+                                                    const uint32_t* __restrict__ pj,
+                                                    const uint32_t* __restrict__ luid,
+                                                    uint32_t* __restrict__ ord,
+                                                    uint4* __restrict__ items) {
+  __shared__ uint32_t cnt[kOsMaxU];
+  __shared__ uint32_t ifirst[kOsMaxU];  // a single-occurrence key's item slot
+  __shared__ unsigned int wsum[kOsT / 64];
+  __shared__ unsigned int tot, toti;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], base = ubase[b];
+  const uint32_t nu = min(unum[b], (uint32_t)kOsMaxU);
+  for (uint32_t l = tid; l < nu; l += kOsT) cnt[l] = 0u;
+  __syncthreads();
+  for (uint32_t p = p0 + tid; p < p1; p += kOsT) {
+    const uint32_t l = luid[p];
+    if (l < nu) atomicAdd(&cnt[l], 1u);
+  }
+  __syncthreads();
+  constexpr int PT = kOsMaxU / kOsT;  // counts per thread, consecutive keys
+  uint32_t c[PT], sc = 0, si = 0;
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    const uint32_t l = (uint32_t)tid * PT + k;
+    c[k] = l < nu ? cnt[l] : 0u;
+    sc += c[k];
+    si += (c[k] + kOsCh - 1) / kOsCh;
+  }
+  uint32_t e = block_excl_scan<kOsT / 64>(sc, wsum, &tot);
+  uint32_t ei = block_excl_scan<kOsT / 64>(si, wsum, &toti);
+#pragma unroll
+  for (int k = 0; k < PT; ++k) {
+    const uint32_t l = (uint32_t)tid * PT + k;
+    if (l < nu) {
+      cnt[l] = e;  // placement cursor
+      ifirst[l] = (p0 + ei) | (c[k] == 1 ? 0x80000000u : 0u);
+      const uint32_t nit = (c[k] + kOsCh - 1) / kOsCh;
+      if (c[k] > 1)  // (a single-occurrence item is written at placement, below)
+        for (uint32_t m = 0; m < nit; ++m)
+          items[p0 + ei + m] = make_uint4(p0 + e + m * kOsCh, min(kOsCh, c[k] - m * kOsCh),
+                                          base + l, nit > 1 ? 1u : 0u);
+      ei += nit;
+    }
+    e += c[k];
+  }
+  for (uint32_t q = p0 + toti + tid; q < p1; q += kOsT) items[q] = make_uint4(0u, 0u, 0u, 0u);
+  __syncthreads();
+  for (uint32_t p = p0 + tid; p < p1; p += kOsT) {
+    const uint32_t l = luid[p];
+    if (l >= nu) continue;
+    const uint32_t j = pj[p];
+    ord[p0 + atomicAdd(&cnt[l], 1u)] = j;
+    // most keys occur once: their item carries the key position itself
+    // (flag 2), so the reduce skips the dependent `ord` load
+    if (ifirst[l] & 0x80000000u) items[ifirst[l] & 0x7FFFFFFFu] = make_uint4(j, 1u, base + l, 2u);
+  }
+}
+
+template <int V>
+struct OVec;  // V consecutive floats moved as one access
+template <>
+struct OVec<4> {
+  using T = float4;
+  __device__ static float get(const T& x, int v) { return v == 0 ? x.x : v == 1 ? x.y : v == 2 ? x.z : x.w; }
+};
+template <>
+struct OVec<2> {
+  using T = float2;
+  __device__ static float get(const T& x, int v) { return v == 0 ? x.x : x.y; }
+};
+template <>
+struct OVec<1> {
+  using T = float;
+  __device__ static float get(const T& x, int) { return x; }
+};
+
+template <int D>
+__global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ items, long long n,
+                                                     const uint32_t* __restrict__ ord,
+                                                     const float* __restrict__ ograd,
+                                                     const float* __restrict__ otail, int B,
+                                                     int W, int ntiles,
+                                                     float* __restrict__ ugrad) {
+  // one item per half-wave: 32 lanes x V floats cover a row (512 B at D =
+  // 128 as 16-B loads), two independent item chains per wave
+  constexpr int V = D / 32;
+  constexpr int QF = 8;  // rows in flight per half-wave
+  using VT = typename OVec<V>::T;
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const long long R = (long long)B + 2 * W;
+  const long long s = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  const uint4 it = s < n ? items[s] : make_uint4(0u, 0u, 0u, 0u);
+  if (it.y == 0) return;  // half-wave-uniform (the shuffles below stay inside a half)
+  // the tail copy of run position j (row l - 64 of the previous tile), or -1
+  auto tail_of = [&](long long j) -> long long {
+    if (j < B || j >= B + R) return -1;
+    const long long rq = j - B;
+    if (rq >= kT && rq % kT < 2 * W && rq / kT <= ntiles - 1) return (rq / kT - 1) * 2 * W + rq % kT;
+    return -1;
+  };
+  const uint32_t jl = (it.w & 2u) ? it.x : (hl < (int)it.y ? ord[it.x + hl] : 0u);
+  float acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) acc[v] = 0.f;
+  for (uint32_t k0 = 0; k0 < it.y; k0 += QF) {
+    VT x[QF], y[QF];
+#pragma unroll
+    for (int r = 0; r < QF; ++r) {
+      const uint32_t k = k0 + r;
+      const long long j = (long long)__shfl(jl, (int)(k < it.y ? k : 0), 32);
+      const long long tq = k < it.y ? tail_of(j) : -1;
+      x[r] = k < it.y ? *reinterpret_cast<const VT*>(ograd + j * D + hl * V) : VT{};
+      y[r] = tq >= 0 ? *reinterpret_cast<const VT*>(otail + tq * D + hl * V) : VT{};
+    }
+#pragma unroll
+    for (int r = 0; r < QF; ++r)
+#pragma unroll
+      for (int v = 0; v < V; ++v) acc[v] += OVec<V>::get(x[r], v) + OVec<V>::get(y[r], v);
+  }
+  float* g = ugrad + (long long)it.z * D + hl * V;
+  if (it.w & 1u) {
+#pragma unroll
+    for (int v = 0; v < V; ++v) atomicAdd(g + v, acc[v]);
+  } else {
+    VT o;
+    float* of = reinterpret_cast<float*>(&o);
+#pragma unroll
+    for (int v = 0; v < V; ++v) of[v] = acc[v];
+    *reinterpret_cast<VT*>(g) = o;
   }
 }
 
@@ -867,23 +1061,29 @@ size_t w2v_smem_bytes(int D) {
   return sizeof(float) * ((size_t)3 * kT * P + (size_t)kT * (kS + 1) + kNW);
 }
 
-// Grid of the window tile kernel (k_w2v_win_bf16): half the CUs,
-// each workgroup walking tiles.  One workgroup per tile fills every CU with
-// an 80+ KB-LDS workgroup for the kernel's whole run, and the route stream's
-// dedup (53 KB LDS) of the next round then runs 5x slower beside it (11 -> 57
-// us).  Window layout, 16K centers: caps 256 / 192 / 160 / 128 / 96 / 64 gave
-// 0.143 / 0.124 / 0.121 / 0.123 / 0.128 / 0.148 ms/step.  SS_W2V_WIN_GRID
-// overrides (0: one workgroup per tile)
-static int w2v_tile_grid(int tiles) {
-  static const int cap = [] {
+// Grid of the window tile kernel (k_w2v_win_bf16).  With the gradient rows as
+// float atomics: half the CUs, each workgroup walking tiles — one workgroup
+// per tile held every CU with an 80+ KB-LDS workgroup for the kernel's whole
+// (atomic-bound) run, and the route stream's dedup (53 KB LDS) of the next
+// round then ran 5x slower beside it (11 -> 57 us); 16K centers, caps 256 /
+// 192 / 160 / 128 / 96 / 64 gave 0.143 / 0.124 / 0.121 / 0.123 / 0.128 /
+// 0.148 ms/step.  With occurrence-row stores (the default) the tile takes 29
+// us and one workgroup per tile is faster (hipGraph replay, one box: 0.092 vs
+// 0.101-0.103 ms/step at half the CUs).  SS_W2V_WIN_GRID overrides (0: one
+// workgroup per tile)
+static int w2v_tile_grid(int tiles, bool atomics) {
+  static const int env = [] {
     const char* e = std::getenv("SS_W2V_WIN_GRID");
-    if (e) return std::atoi(e);
+    return e ? std::atoi(e) : -1;
+  }();
+  static const int half = [] {
     int dev = 0, cus = 0;
     check_hip(hipGetDevice(&dev), "hipGetDevice");
     check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev),
               "CU count");
     return std::max(1, cus / 2);
   }();
+  const int cap = env >= 0 ? env : (atomics ? half : 0);
   return cap > 0 ? std::min(tiles, cap) : tiles;
 }
 
@@ -986,21 +1186,62 @@ void launch_w2v_ctx_reduce(int P, const uint32_t* bstart, const uint32_t* unum,
   check_launch("k_w2v_ctx_reduce");
 }
 
+void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const uint32_t* ubase,
+                      const uint32_t* pj, const uint32_t* luid, uint32_t* ord, uint32_t* items,
+                      hipStream_t st) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(k_w2v_osort, dim3(P), dim3(kOsT), 0, st, bstart, unum, ubase, pj, luid, ord,
+                     reinterpret_cast<uint4*>(items));
+  check_launch("k_w2v_osort");
+}
+
+void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
+                        const float* otail, int B, int W, int D, float* ugrad, hipStream_t st) {
+  if (n <= 0) return;
+  if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_oreduce: window must be in [1, 15]");
+  const int ntiles = (B + kT - 1) / kT;
+  // an item per half-wave, no grid stride: the reduce is a chain of
+  // dependent loads per item (item -> rows -> store), so every chain of the
+  // call runs concurrently
+  const int grid = (int)((n + 7) / 8);
+  const uint4* it = reinterpret_cast<const uint4*>(items);
+  switch (D) {
+#define SS_W2VO_CASE(DD)                                                                      \
+  case DD:                                                                                    \
+    hipLaunchKernelGGL(k_w2v_oreduce<DD>, dim3(grid), dim3(256), 0, st, it, n, ord, ograd,    \
+                       otail, B, W, ntiles, ugrad);                                           \
+    break;
+    SS_W2VO_CASE(32)
+    SS_W2VO_CASE(64)
+    SS_W2VO_CASE(128)
+#undef SS_W2VO_CASE
+    default:
+      throw_error("w2v_oreduce: D must be 32, 64 or 128");
+  }
+  check_launch("k_w2v_oreduce");
+}
+
 void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                     const int32_t* meta, int B, int W, int D, float neg_per_pair,
                     const float* uvals, float* ugrad, float* loss_sum, float* pair_sum,
-                    hipStream_t st) {
+                    hipStream_t st, float* ograd, float* otail) {
   if (B <= 0) return;
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_win: window must be in [1, 15]");
   const int tiles = (B + kT - 1) / kT;
-  const int grid = w2v_tile_grid(tiles);
+  const int grid = w2v_tile_grid(tiles, ograd == nullptr);
+  // SS_W2V_WIN_GMODE (measurement only, wrong results): 1 = gradient rows as
+  // plain stores instead of atomics, 2 = no gradient output
+  static const int gmode = [] {
+    const char* e = std::getenv("SS_W2V_WIN_GMODE");
+    return e ? std::atoi(e) : 0;
+  }();
   switch (D) {
 #define SS_W2VW_CASE(DD)                                                                     \
   case DD:                                                                                   \
     smem_attr_once<k_w2v_win_bf16<DD>>(W2vWinSmem<DD>::bytes);                               \
     hipLaunchKernelGGL(k_w2v_win_bf16<DD>, dim3(grid), dim3(kWG), W2vWinSmem<DD>::bytes, st,  \
                        inv_c, inv_w, inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum,   \
-                       pair_sum);                                                            \
+                       pair_sum, gmode, ograd, otail);                                       \
     break;
     SS_W2VW_CASE(32)
     SS_W2VW_CASE(64)

@@ -12,6 +12,7 @@ non-worker contributes zero keys.
 """
 from __future__ import annotations
 
+import gc
 import os
 
 import torch
@@ -37,6 +38,10 @@ class PipelinedWorker:
         self._route_first = os.environ.get("SS_ROUTE_FIRST", "0") != "0"
 
     # -- subclass hooks
+    # optional ``(dd, slot, stream_ptr)`` hook run on the route stream right
+    # after the dedup (planning that depends on the key layout only)
+    _post_route = None
+
     def _produce(self, step: int, slot: int, stream) -> torch.Tensor:
         raise NotImplementedError
 
@@ -55,7 +60,7 @@ class PipelinedWorker:
         def produce(stream):
             return self._produce(step, slot, stream.cuda_stream if stream is not None else None)
 
-        return self.engine.route(produce=produce)
+        return self.engine.route(produce=produce, post=self._post_route)
 
     def _gen_kwargs(self, step: int) -> dict:
         """Generator arguments: inside a hipGraph capture the batch index is
@@ -98,6 +103,12 @@ class PipelinedWorker:
         # graphs 54 / 75 / 310
         per = 1 if os.environ.get("SS_GRAPH_STEPS", "") == "1" else eng.depth
         graphs, pool = [], None
+        # no garbage collection inside a capture: a collected object of an
+        # earlier worker (its pooled events, streams) would destroy HIP
+        # objects mid-capture, which aborts the process
+        gc_on = gc.isenabled()
+        gc.collect()
+        gc.disable()
         try:
             for p in range(eng.depth // per):
                 g = torch.cuda.CUDAGraph()
@@ -119,6 +130,8 @@ class PipelinedWorker:
                 graphs.append(g)
         finally:
             eng.capture_tag = None
+            if gc_on:
+                gc.enable()
         self._gper = per
         # the captures only recorded: the device is where it was before them,
         # and after `depth` steps the Python-side pipeline state is periodic

@@ -157,9 +157,33 @@ class Word2VecWorker(PipelinedWorker):
         # instead of 116, two workgroups per CU.  Measured 0.305 -> 0.278-0.282
         # ms/step (1M vocab, dim 128); SS_W2V_MFMA=f32 selects the fp32 tile
         self.mfma_bf16 = (os.environ.get("SS_W2V_MFMA", "bf16") == "bf16" and not self.ctx_reduce)
+        # window layout, SS_W2V_GRAD=reduce (default with the bucketed dedup):
+        # the tile stores one gradient row per key position and the rows are
+        # summed per unique key (w2v.hip k_w2v_osort on the route stream a
+        # round ahead, k_w2v_oreduce on the main stream) instead of leaving the
+        # tile as float row atomics
+        self.occ_reduce = (self.window_mode and engine.gpu and
+                           os.environ.get("SS_W2V_GRAD", "reduce") == "reduce" and
+                           all(getattr(d, "mode", None) == "bucket" for d in engine.dedupers))
+        if self.occ_reduce:
+            dev, n, D, W = engine.device, data.n_keys, engine.dim, data.window
+            self.ograd = torch.empty((n, D), dtype=torch.float32, device=dev)
+            self.otail = torch.empty((max(1, (data.tiles - 1) * 2 * W), D), dtype=torch.float32,
+                                     device=dev)
+            self.ord = [torch.empty(n, dtype=torch.int32, device=dev)
+                        for _ in range(engine.depth)]
+            self.items = [torch.empty((n, 4), dtype=torch.int32, device=dev)
+                          for _ in range(engine.depth)]
+            self._post_route = self._osort
 
     def _zero_acc(self) -> None:
         self._acc.zero_()
+
+    def _osort(self, dd, slot, st):
+        o = dd.owner
+        _, bstart, unum, ubase, P = o.bucket_view(dd.n)
+        hip().w2v_osort(P, bstart, unum, ubase, o.pj.data_ptr(), o.luid.data_ptr(),
+                        self.ord[slot].data_ptr(), self.items[slot].data_ptr(), st)
 
     def _produce(self, step, slot, stream):
         kw = self._gen_kwargs(step)
@@ -175,10 +199,15 @@ class Word2VecWorker(PipelinedWorker):
         ptr, es = inv.data_ptr(), inv.element_size()
         h = hip()
         if self.window_mode:
+            occ = self.occ_reduce
             h.w2v_win(ptr, ptr + B * es, ptr + (B + d.run_len) * es, self.meta[slot].data_ptr(),
                       B, d.window, self.engine.dim, d.neg_per_pair, rnd.uvals.data_ptr(),
                       rnd.ugrad.data_ptr(), self.loss_sum.data_ptr(), self.pair_sum.data_ptr(),
-                      st)
+                      st, self.ograd.data_ptr() if occ else 0, self.otail.data_ptr() if occ else 0)
+            if occ:
+                h.w2v_oreduce(self.items[slot].data_ptr(), d.n_keys, self.ord[slot].data_ptr(),
+                              self.ograd.data_ptr(), self.otail.data_ptr(), B, d.window,
+                              self.engine.dim, rnd.ugrad.data_ptr(), st)
             return
         h.w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
                    d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),

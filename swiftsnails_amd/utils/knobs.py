@@ -135,10 +135,17 @@ KNOBS: dict[str, Knob] = {
                            "one GPU with pull-ahead: the pulled-ahead round's table lookup on "
                            "its own stream, beside the next round's dedup (word2vec 0.128 -> "
                            "0.125 ms/step; FM 0.655 -> 0.685, so off there)"),
-    "SS_W2V_WIN_GRID": Knob("CUs / 2", "csrc/hip/w2v.hip", "tuning",
+    "SS_W2V_WIN_GRID": Knob("one per tile (atomic mode: CUs / 2)", "csrc/hip/w2v.hip", "tuning",
                             "grid of the windowed word2vec tile kernel (workgroups walk tiles; "
-                            "0: one per tile), leaving CUs to the route stream's dedup "
-                            "(0.143 -> 0.123 ms/step)"),
+                            "0: one per tile); half the CUs leaves CUs to the route stream's "
+                            "dedup when the tile is atomic-bound (0.143 -> 0.123 ms/step), one "
+                            "per tile is faster with occurrence-row stores (0.101 -> 0.092)"),
+    "SS_W2V_GRAD": Knob("reduce", "models/word2vec.py", "experiment",
+                        "window layout: tile gradients as occurrence rows summed per unique "
+                        "key (reduce) or as float row atomics from the tile (atomic)"),
+    "SS_W2V_WIN_GMODE": Knob("0", "csrc/hip/w2v.hip", "debug",
+                             "measurement only (wrong results): windowed word2vec tile's "
+                             "gradient rows as 1 = plain stores, 2 = not written"),
     "SS_COUNTS_SPIN": Knob("0", "parallel/transport.py", "experiment",
                            "N>1: busy-poll the count exchange's event instead of a blocking "
                            "synchronize (neutral on one GPU: 1.034-1.040 vs 1.036-1.054)"),

@@ -465,6 +465,43 @@ def test_word2vec_context_reduce_matches_atomics(dev, monkeypatch):
     np.testing.assert_allclose(b, a, rtol=5e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("D,B,W", [(128, 1000, 5), (32, 640, 2), (64, 4096, 15)])
+def test_word2vec_window_grad_reduce_matches_atomics(dev, monkeypatch, D, B, W):
+    """Window tile gradients as occurrence rows summed per unique key
+    (k_w2v_osort + k_w2v_oreduce: counting sort per dedup bucket, one wave per
+    <= 32-occurrence item, shared window rows through the tail buffer, Zipf
+    heads split over several items) == the tile's own row atomics.  Partial
+    last tile (B % 64 != 0), W from 2 to the maximum 15."""
+    from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    out = {}
+    for mode in ("reduce", "atomic"):
+        monkeypatch.setenv("SS_W2V_GRAD", mode)
+        data = W2VSynth(batch_size=B, window=W, vocab=3000, noise=0.05, mode="window")
+        opt, init = make_w2v_table_args(D, None)
+        t = HbmTable(D, 40000, optimizer=opt, init=init, device=dev)
+        eng = PSEngine(t, None, max_keys=data.n_keys, dim=D, device=dev)
+        w = Word2VecWorker(eng, data)
+        assert w.occ_reduce == (mode == "reduce")
+        losses = []
+        for _ in range(5):
+            w.step()
+            losses.append(w.mean_loss())
+        torch.cuda.synchronize()
+        t.check()
+        out[mode] = (losses, t.to_dict(with_state=True))
+    (lr, tr), (la, ta) = out["reduce"], out["atomic"]
+    np.testing.assert_allclose(lr, la, rtol=1e-4)
+    assert tr.keys() == ta.keys()
+    ks = list(tr.keys())
+    a, b = np.stack([ta[k] for k in ks]), np.stack([tr[k] for k in ks])
+    assert np.isclose(b, a, rtol=1e-3, atol=5e-4).mean() > 0.9999
+    np.testing.assert_allclose(b, a, rtol=5e-2, atol=2e-2)
+
+
 @pytest.mark.parametrize("model", ["lr", "fm", "w2v"])
 def test_general_path_rccl_world1_matches_loopback(dev, model, monkeypatch):
     """The N>1 engine path (send segments, count exchange with pinned D2H,
