@@ -101,7 +101,15 @@ class PipelinedWorker:
         # phase, joined at every step).  Measured, batch 1024 / 8192 / 65536:
         # eager 74 / 79 / 309 us, per-step graphs 68 / 92 / 318, ring-period
         # graphs 54 / 75 / 310
-        per = 1 if os.environ.get("SS_GRAPH_STEPS", "") == "1" else eng.depth
+        # default: one graph of 4 ring periods.  A replay joins every stream at
+        # its end, so the pipeline drains once per graph: word2vec (1M vocab,
+        # 16K centers) 4 / 8 / 16 / 32 steps per graph: 0.093 / 0.088 / 0.086 /
+        # 0.084 ms/step; sparse LR at batch 65536 unchanged (0.241 / 0.240).
+        # SS_GRAPH_STEPS=1 (a graph per step) or any multiple of the depth
+        per = 4 * eng.depth
+        env = os.environ.get("SS_GRAPH_STEPS", "")
+        if env.isdigit() and (int(env) == 1 or (int(env) > 0 and int(env) % eng.depth == 0)):
+            per = int(env)
         graphs, pool = [], None
         # no garbage collection inside a capture: a collected object of an
         # earlier worker (its pooled events, streams) would destroy HIP
@@ -110,7 +118,7 @@ class PipelinedWorker:
         gc.collect()
         gc.disable()
         try:
-            for p in range(eng.depth // per):
+            for p in range(max(1, eng.depth // per)):
                 g = torch.cuda.CUDAGraph()
                 with torch.cuda.graph(g, pool=pool):
                     eng.capture_tag = p + 1

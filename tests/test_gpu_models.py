@@ -395,15 +395,14 @@ def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
     here: with it, which of round i's updates round i+1 reads depends on
     timing (staleness 1), in eager mode as much as in graphs."""
     monkeypatch.setenv("SS_PULL_AHEAD", "0")
-    depth = int(os.environ.get("SS_ENGINE_DEPTH", "4"))
-    per = 1 if os.environ.get("SS_GRAPH_STEPS", "") == "1" else depth
-    n = 1 + 3 * per
-    wa, ta = _graph_worker(model, dev)
-    la = [float(wa.step().sum().item()) for _ in range(n)]
     wb, tb = _graph_worker(model, dev)
     lb = [float(wb.step().sum().item())]
     assert wb.enable_graph()
+    per = wb._gper  # steps per graph (SS_GRAPH_STEPS; default 4 ring periods)
+    n = 1 + 3 * per
     lb += [float(wb.step().sum().item()) for _ in range(n - 1)]
+    wa, ta = _graph_worker(model, dev)
+    la = [float(wa.step().sum().item()) for _ in range(n)]
     torch.cuda.synchronize()
     ta.check()
     tb.check()
