@@ -779,13 +779,15 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   // kernel alone barely changes: smaller workgroups interleave better with
   // the route stream's kernels)
   // FM rows (G = 4): 2, 0.548-0.556 -> 0.541 ms/step (4: 0.544-0.551);
-  // word2vec rows (G = 64): 1 (2 and 4 neutral)
+  // word2vec rows (G = 64): 2 — with the occurrence-row reduce and hipGraph
+  // replay, 1 / 2 / 4 / 8: 0.0840-0.0848 / 0.0829-0.0830 / 0.0837-0.0844 /
+  // 0.0858 ms/step (earlier, atomic-bound: 2 and 4 neutral)
   static const int env_ny = [] {
     const char* e = std::getenv("SS_PULL_BK_Y");
     const int v = e ? std::atoi(e) : 0;
     return v < 0 ? 0 : (v > 16 ? 16 : v);
   }();
-  const int ny = env_ny ? env_ny : (G == 1 ? 4 : (G == 4 ? 2 : 1));
+  const int ny = env_ny ? env_ny : (G == 1 ? 4 : 2);
   // snapshot pulls on 16-byte [w | h | key] slots probe with one 16-byte
   // load per step (probe_slot16); SS_PULL_ONELOAD=0: key load, then row load
   static const bool oneload_env = [] {

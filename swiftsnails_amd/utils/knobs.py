@@ -62,7 +62,7 @@ KNOBS: dict[str, Knob] = {
                             "cas, or claim (plain-store claim + verify; measured slower)"),
     "SS_TABLE_PREFILL": Knob("1", "ops/table.py", "tuning",
                              "zero-init tables pre-filled with the init row (insert = CAS only)"),
-    "SS_PULL_BK_Y": Knob("4 (G=1) / 2 (G=4) / 1", "csrc/hip/table.hip", "tuning",
+    "SS_PULL_BK_Y": Knob("4 (G=1) / 2", "csrc/hip/table.hip", "tuning",
                          "workgroups per dedup bucket in the bucketed pull"),
     "SS_PULL_ONELOAD": Knob("1", "csrc/hip/table.hip", "tuning",
                             "snapshot pull on 16-byte LR slots: one 16-byte load per probe step "
