@@ -656,8 +656,8 @@ struct W2vWinSmem {
       sizeof(unsigned short) * ((size_t)(kT + kWU + kS) * PB + (size_t)kT * GPB + (size_t)kT * GB);
 };
 
-template <int D>
-__global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
+template <int D, int NW>
+__global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
     const uint32_t* __restrict__ inv_c, const uint32_t* __restrict__ inv_w,
     const uint32_t* __restrict__ inv_n, const int32_t* __restrict__ meta, int B, int W,
     float neg_per_pair, const float* __restrict__ uvals, float* __restrict__ ugrad,
@@ -675,7 +675,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
   __shared__ int32_t mw[kWU];
   __shared__ int uany[kWU];
   __shared__ float cwt[kT];  // n_t * K / S
-  __shared__ float red[kNW];
+  __shared__ float red[NW];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const long long R = (long long)B + 2 * W;
@@ -713,18 +713,18 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
     // serialised 14 dependent gathers per thread at D = 128).  A center row
     // without pairs (rc = kInv) stays zero: its G+ and G- rows are zero.
     {
-      constexpr int NE = (kT + kWU + kS) * (D / 4), PER = (NE + kWG - 1) / kWG;
+      constexpr int NE = (kT + kWU + kS) * (D / 4), PER = (NE + (64 * NW) - 1) / (64 * NW);
       float4 v[PER];
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
-        const int e = tid + i * kWG, r = e / (D / 4), d = 4 * (e - r * (D / 4));
+        const int e = tid + i * (64 * NW), r = e / (D / 4), d = 4 * (e - r * (D / 4));
         const uint32_t id = e >= NE ? kInv : r < kT ? rc[r] : r < kT + kWU ? rw[r - kT] : rn[r - kT - kWU];
         v[i] = id != kInv ? *reinterpret_cast<const float4*>(uvals + (long long)id * D + d)
                           : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int i = 0; i < PER; ++i) {
-        const int e = tid + i * kWG, r = e / (D / 4), d = 4 * (e - r * (D / 4));
+        const int e = tid + i * (64 * NW), r = e / (D / 4), d = 4 * (e - r * (D / 4));
         if (e < NE)
           *reinterpret_cast<uint2*>(smem16 + r * PB + d) =
               make_uint2(f2bf(v[i].x) | ((uint32_t)f2bf(v[i].y) << 16),
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
 
     const int r32 = lane & 31, h = lane >> 5;
     // ---- scores: 6 tiles of S+ (2 x 3) and 4 of S- (2 x 2)
-    for (int k = w; k < 10; k += kNW) {
+    for (int k = w; k < 10; k += NW) {
       const bool pos = k < 6;
       const int ti = pos ? k / 3 : (k - 6) >> 1, tj = pos ? k % 3 : (k - 6) & 1;
       const unsigned short* Bm = pos ? Ub : Nb;
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
     }
     __syncthreads();
     // ---- gradients: gV (2 x TJ tiles), gU (3 x TJ), gN (2 x TJ)
-    for (int tt = w; tt < 7 * TJ; tt += kNW) {
+    for (int tt = w; tt < 7 * TJ; tt += NW) {
       const int kind = tt < 2 * TJ ? 0 : (tt < 5 * TJ ? 1 : 2);
       const int q = tt - (kind == 0 ? 0 : (kind == 1 ? 2 * TJ : 5 * TJ));
       const int ti = q / TJ, tj = q % TJ;
@@ -849,7 +849,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
   if (tid == 0 && loss_sum) {
     float tot = 0.f;
 #pragma unroll
-    for (int i = 0; i < kNW; ++i) tot += red[i];
+    for (int i = 0; i < NW; ++i) tot += red[i];
     ctr_addf(loss_sum, tot);
   }
   if (w == 0 && pair_sum) {  // centers' pair counts live in wave 0 (tid < kT)
@@ -1221,10 +1221,35 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
   check_launch("k_w2v_oreduce");
 }
 
+template <int D>
+static void launch_w2v_win_t(bool wide, int grid, hipStream_t st, const uint32_t* inv_c,
+                             const uint32_t* inv_w, const uint32_t* inv_n, const int32_t* meta,
+                             int B, int W, float neg_per_pair, const float* uvals, float* ugrad,
+                             float* loss_sum, float* pair_sum, int gmode, float* ograd,
+                             float* otail) {
+  const size_t sm = W2vWinSmem<D>::bytes;
+  if (wide) {
+    smem_attr_once<k_w2v_win_bf16<D, 16>>(sm);
+    hipLaunchKernelGGL((k_w2v_win_bf16<D, 16>), dim3(grid), dim3(1024), sm, st, inv_c, inv_w,
+                       inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum, pair_sum, gmode,
+                       ograd, otail);
+  } else {
+    smem_attr_once<k_w2v_win_bf16<D, 8>>(sm);
+    hipLaunchKernelGGL((k_w2v_win_bf16<D, 8>), dim3(grid), dim3(512), sm, st, inv_c, inv_w,
+                       inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum, pair_sum, gmode,
+                       ograd, otail);
+  }
+}
+
 void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                     const int32_t* meta, int B, int W, int D, float neg_per_pair,
                     const float* uvals, float* ugrad, float* loss_sum, float* pair_sum,
                     hipStream_t st, float* ograd, float* otail) {
+  // SS_W2V_WIN_WG: 512 (8 waves) or 1024 (16 waves) threads per tile
+  static const bool wide = [] {
+    const char* e = std::getenv("SS_W2V_WIN_WG");
+    return e && std::atoi(e) == 1024;
+  }();
   if (B <= 0) return;
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_win: window must be in [1, 15]");
   const int tiles = (B + kT - 1) / kT;
@@ -1238,10 +1263,8 @@ void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t
   switch (D) {
 #define SS_W2VW_CASE(DD)                                                                     \
   case DD:                                                                                   \
-    smem_attr_once<k_w2v_win_bf16<DD>>(W2vWinSmem<DD>::bytes);                               \
-    hipLaunchKernelGGL(k_w2v_win_bf16<DD>, dim3(grid), dim3(kWG), W2vWinSmem<DD>::bytes, st,  \
-                       inv_c, inv_w, inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum,   \
-                       pair_sum, gmode, ograd, otail);                                       \
+    launch_w2v_win_t<DD>(wide, grid, st, inv_c, inv_w, inv_n, meta, B, W, neg_per_pair, uvals,  \
+                         ugrad, loss_sum, pair_sum, gmode, ograd, otail);                    \
     break;
     SS_W2VW_CASE(32)
     SS_W2VW_CASE(64)

@@ -140,6 +140,10 @@ KNOBS: dict[str, Knob] = {
                             "0: one per tile); half the CUs leaves CUs to the route stream's "
                             "dedup when the tile is atomic-bound (0.143 -> 0.123 ms/step), one "
                             "per tile is faster with occurrence-row stores (0.101 -> 0.092)"),
+    "SS_W2V_WIN_WG": Knob("512", "csrc/hip/w2v.hip", "experiment",
+                          "1024: the window tile with 16 waves instead of 8 (standalone 29.6 -> "
+                          "23.1 us, but the step 0.083 -> 0.093 ms: the workgroup's registers "
+                          "fill its CU's SIMDs and nothing runs beside it)"),
     "SS_W2V_GRAD": Knob("reduce", "models/word2vec.py", "experiment",
                         "window layout: tile gradients as occurrence rows summed per unique "
                         "key (reduce) or as float row atomics from the tile (atomic)"),
