@@ -491,7 +491,9 @@ __global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ unum,
                                                     const uint32_t* __restrict__ luid,
                                                     const float* __restrict__ uvals,
-                                                    float* __restrict__ occ, int osi) {
+                                                    float* __restrict__ occ, int osi,
+                                                    const uint32_t* __restrict__ pj) {
+  // pj: write sample order instead, occ[pj[p]] (the forward then streams occ)
   __shared__ float sv[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
@@ -500,16 +502,17 @@ __global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__
   for (uint32_t l = threadIdx.x; l < nu; l += FT) sv[l] = uvals[base + l];
   __syncthreads();
   for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * FT) {
-    uint32_t l[4];
+    uint32_t l[4], q[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const uint32_t p = pb + r * FT;
       l[r] = p < p1 ? luid[p] : kBdInvalid;
+      q[r] = p < p1 ? (pj ? pj[p] : p) : 0u;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const uint32_t p = pb + r * FT;
-      if (p < p1) occ[p] = l[r] < nu ? sv[l[r]] : 0.f;
+      if (p < p1) occ[q[r]] = l[r] < nu ? sv[l[r]] : 0.f;
     }
   }
 }
@@ -952,11 +955,12 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
 }
 
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,
-                        const float* uvals, float* occ, int osi, hipStream_t st, int ndest) {
+                        const float* uvals, float* occ, int osi, hipStream_t st, int ndest,
+                        const uint32_t* pj) {
   if (n <= 0) return;
   const BdLayout L = bd_layout(n, nranks, ndest);
   hipLaunchKernelGGL(k_bd_fill_occ<512>, dim3(L.P), dim3(512), 0, st, scratch + L.bstart,
-                     scratch + L.ubase, scratch + L.unum, luid, uvals, occ, osi);
+                     scratch + L.ubase, scratch + L.unum, luid, uvals, occ, osi, pj);
   check_launch("k_bd_fill_occ");
 }
 

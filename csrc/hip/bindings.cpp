@@ -318,11 +318,13 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("uvals"), py::arg("g"), py::arg("per_sample"), py::arg("loss"), py::arg("pred"),
      py::arg("st"), py::arg("ix") = std::vector<uintptr_t>{}, py::arg("occ") = 0);
   m.def("bd_fill_occ", [](long long n, int nranks, uintptr_t scratch, uintptr_t luid,
-                          uintptr_t uvals, uintptr_t occ, int osi, uintptr_t st, int ndest) {
+                          uintptr_t uvals, uintptr_t occ, int osi, uintptr_t st, int ndest,
+                          uintptr_t pj) {
     launch_bd_fill_occ(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(luid),
-                       P<const float>(uvals), P<float>(occ), osi, S(st), ndest);
+                       P<const float>(uvals), P<float>(occ), osi, S(st), ndest,
+                       P<const uint32_t>(pj));
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("luid"), py::arg("uvals"),
-     py::arg("occ"), py::arg("osi"), py::arg("st"), py::arg("ndest") = 0);
+     py::arg("occ"), py::arg("osi"), py::arg("st"), py::arg("ndest") = 0, py::arg("pj") = 0);
   m.def("fm_fwd_g", [](uintptr_t inv, std::vector<uintptr_t> ix, uintptr_t labels, int B,
                        int F, int dim, uintptr_t uvals, uintptr_t gs, uintptr_t gss,
                        uintptr_t loss, uintptr_t pred, uintptr_t st) {

@@ -209,6 +209,7 @@ __device__ __forceinline__ float lr_param(long long j, const uint32_t* __restric
                                           const BdIndex& ix, const float* __restrict__ occ,
                                           const float* __restrict__ uvals) {
   if (occ) {
+    if (!ix.pos_of) return occ[j];  // filled in sample order (k_bd_fill_occ with pj)
     const uint32_t p = ix.pos_of[j];
     return p == kInvS ? 0.f : occ[p];
   }
@@ -347,8 +348,9 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
                      const float* labels, int B, int F, const float* uvals, float* gocc,
                      int per_sample, float* loss_sum, float* pred, hipStream_t st,
                      const float* occ) {
-  if (occ ? !ix.pos_of : (!inv && !(ix.pos_of && ix.luid && ix.bkt && ix.ubase)))
-    throw_error("lr_fwd_g: need inv, a complete BdIndex, or occ with pos_of");
+  if (!occ && !inv && !(ix.pos_of && ix.luid && ix.bkt && ix.ubase))
+    throw_error("lr_fwd_g: need inv, a complete BdIndex, or occ (bucket order with pos_of, "
+                "else sample order)");
   if (B <= 0) return;
   if (F < 1 || F > 256) throw_error("lr_fwd_g: F must be in [1,256]");
   // layout: one sample per lane group unless that leaves over a quarter of

@@ -164,7 +164,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
 // occ[p] = uvals[uid of occurrence position p] (scalar rows; 0 where none):
 // one workgroup per dedup bucket, for the LR forward's one-gather mode
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,
-                        const float* uvals, float* occ, int osi, hipStream_t st, int ndest);
+                        const float* uvals, float* occ, int osi, hipStream_t st, int ndest, const uint32_t* pj = nullptr);
 void launch_bd_unplace(long long n, int nranks, const uint32_t* scratch, const float* src,
                        float* dst, int dim, hipStream_t st, int ndest = 0);
 

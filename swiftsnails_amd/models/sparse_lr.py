@@ -113,6 +113,11 @@ class SparseLRWorker(PipelinedWorker):
         # array
         self.use_occ = (self.bucketed and not self.use_inv and
                         os.environ.get("SS_LR_OCC", "1") != "0")
+        # SS_LR_OCC=sample: the fill writes each parameter at its occurrence's
+        # own position (occ[pj[p]], scattered) and the forward streams occ[j].
+        # Measured slower, 0.858-0.862 -> 0.988 ms/step (three A/B pairs): the
+        # scattered 4-byte stores cost more than the forward's gather saves
+        self.occ_sample = self.use_occ and os.environ.get("SS_LR_OCC", "1") == "sample"
         self.occ = torch.empty(n, dtype=torch.float32, device=dev) if self.use_occ else None
         if self.bucketed:
             for dd in engine.dedupers:
@@ -132,12 +137,14 @@ class SparseLRWorker(PipelinedWorker):
                 self.use_occ, self.occ = False, None
             for dd in engine.dedupers:
                 dd.need_bkt = not self.use_occ
+                dd.need_pos = not self.occ_sample  # (sample order: nothing reads pos_of)
             # SS_PULL_FILL=1: the 1-GPU snapshot pull writes occ itself
             # (k_pull_fill_bk: one workgroup per bucket, weights staged in LDS).
             # Measured slower (0.94 vs 0.86 ms/step, three A/B pairs): one
             # workgroup per bucket serialises the probes the default pull
             # spreads over four
-            if self.use_occ and os.environ.get("SS_PULL_FILL", "0") != "0":
+            if (self.use_occ and not self.occ_sample and
+                    os.environ.get("SS_PULL_FILL", "0") != "0"):
                 engine.occ_buf = self.occ
         elif grad_mode == "segreduce":
             h = hip()
@@ -213,10 +220,11 @@ class SparseLRWorker(PipelinedWorker):
                            self.loss_sum.data_ptr(), 0, st)
             elif self.use_occ:
                 if not rnd.occ_filled:
-                    o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
+                    o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st, sample_order=self.occ_sample)
                 h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
                            rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
-                           self.loss_sum.data_ptr(), 0, st, o.index_ptrs(dd.n),
+                           self.loss_sum.data_ptr(), 0, st,
+                           [] if self.occ_sample else o.index_ptrs(dd.n),
                            occ=self.occ.data_ptr())
             elif self.bucketed:
                 h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,

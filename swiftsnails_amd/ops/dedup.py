@@ -84,6 +84,9 @@ class Deduper:
         # buffer (pull_buckets/push_buckets with osi, bd_unplace for N>1), and
         # no BdIndex (pos_of / bkt) is written
         self.osi = False
+        # need_pos=False: no consumer reads the j -> bucket-position map
+        # (pos_of), so the scatter skips writing it
+        self.need_pos = True
         # bucket mode: per unique key, whether it occurs once in the batch
         # (``usingle``, compact unique ids) — lets the LR reduce store instead
         # of accumulate with LDS atomics.  Allocated by track_singletons().
@@ -149,7 +152,7 @@ class Deduper:
             osi = self.osi
             self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
                             self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
-                            0 if osi else self.pos_of.data_ptr(),
+                            0 if (osi or not self.need_pos) else self.pos_of.data_ptr(),
                             0 if (osi or not self.need_bkt) else self.bkt.data_ptr(),
                             self.luid.data_ptr(),
                             self.bkeys.data_ptr(), self.ucount.data_ptr(),
@@ -197,15 +200,16 @@ class Deduper:
                          ndest=self.ndest)
 
     def fill_occ(self, n: int, uvals: torch.Tensor, occ: torch.Tensor, stream=None,
-                 osi: bool = False):
+                 osi: bool = False, sample_order: bool = False):
         """Scalar rows of the LAST call by occurrence position:
         ``occ[p] = uvals[uid]`` of the occurrence at bucket position p (0
-        where it has none), so a consumer reads ``occ[pos_of[j]]``."""
+        where it has none), so a consumer reads ``occ[pos_of[j]]``; with
+        ``sample_order`` at the occurrence's own position, ``occ[j]``."""
         if self.mode != "bucket":
             raise RuntimeError("fill_occ needs mode='bucket'")
         self.h.bd_fill_occ(n, self.nranks, self.scratch.data_ptr(), self.luid.data_ptr(),
                            uvals.data_ptr(), occ.data_ptr(), int(osi), _stream_ptr(stream),
-                           self.ndest)
+                           self.ndest, self.pj.data_ptr() if sample_order else 0)
 
     def unplace(self, n: int, src: torch.Tensor, dst: torch.Tensor, stream=None):
         """Rows of the LAST call from compact unique ids (``src``, the
