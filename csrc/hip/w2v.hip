@@ -735,7 +735,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
 
     const int r32 = lane & 31, h = lane >> 5;
     // ---- scores: 6 tiles of S+ (2 x 3) and 4 of S- (2 x 2)
-    for (int k = w; k < 10; k += NW) {
+    for (int k = w; k < (gmode >= 4 ? 0 : 10); k += NW) {  // (gmode 4: measurement, no scores)
       const bool pos = k < 6;
       const int ti = pos ? k / 3 : (k - 6) >> 1, tj = pos ? k % 3 : (k - 6) & 1;
       const unsigned short* Bm = pos ? Ub : Nb;
@@ -768,7 +768,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
     }
     __syncthreads();
     // ---- gradients: gV (2 x TJ tiles), gU (3 x TJ), gN (2 x TJ)
-    for (int tt = w; tt < 7 * TJ; tt += NW) {
+    for (int tt = w; tt < (gmode >= 3 ? 0 : 7 * TJ); tt += NW) {  // (gmode 3/4: no gradients)
       const int kind = tt < 2 * TJ ? 0 : (tt < 5 * TJ ? 1 : 2);
       const int q = tt - (kind == 0 ? 0 : (kind == 1 ? 2 * TJ : 5 * TJ));
       const int ti = q / TJ, tj = q % TJ;
@@ -1255,7 +1255,8 @@ void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t
   const int tiles = (B + kT - 1) / kT;
   const int grid = w2v_tile_grid(tiles, ograd == nullptr);
   // SS_W2V_WIN_GMODE (measurement only, wrong results): 1 = gradient rows as
-  // plain stores instead of atomics, 2 = no gradient output
+  // plain stores instead of atomics, 2 = no gradient output, 3 = no gradient
+  // GEMMs, 4 = row gathers only
   static const int gmode = [] {
     const char* e = std::getenv("SS_W2V_WIN_GMODE");
     return e ? std::atoi(e) : 0;

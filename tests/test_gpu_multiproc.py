@@ -209,3 +209,61 @@ def test_bench_script_world2_gloo_rehearsal():
     assert j["value"] > 0 and j["ms_per_step"] > 0
     assert j["config"]["global_batch"] == 2 * 4096
     assert j["config"]["parallelism"].startswith("ps2")
+
+
+def _run_w2v_rank(rank, world, init, grad, q):
+    os.environ["SS_PULL_AHEAD"] = "0"  # deterministic rounds: compare the two merges exactly
+    os.environ["SS_W2V_GRAD"] = grad
+    init_gloo(init, rank, world)
+    try:
+        from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
+        from swiftsnails_amd.ops.table import HbmTable
+        from swiftsnails_amd.parallel.engine import PSEngine
+        from swiftsnails_amd.parallel.transport import TorchDistTransport
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        data = W2VSynth(batch_size=1000, window=4, vocab=4000, noise=0.05, mode="window")
+        opt, init_cfg = make_w2v_table_args(64, None)
+        table = HbmTable(64, 20000, optimizer=opt, init=init_cfg, device=dev)
+        eng = PSEngine(table, TorchDistTransport(), max_keys=data.n_keys, dim=64, device=dev)
+        assert not eng.fast1
+        w = Word2VecWorker(eng, data, rank=rank, world=world)
+        assert w.occ_reduce == (grad == "reduce")
+        losses = []
+        for _ in range(12):
+            w.step()
+            losses.append(w.mean_loss())
+        torch.cuda.synchronize()
+        table.check()
+        q.put((rank, losses, table.to_dict(with_state=True)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_word2vec_window_world2_reduce_matches_atomics():
+    """N>1 engine path (two ranks on cuda:0, gloo data plane): the window
+    tile's per-key merge of occurrence rows (k_w2v_osort / k_w2v_oreduce over
+    the compact send layout) trains exactly like its row atomics."""
+    ctx = mp.get_context("spawn")
+    out = {}
+    for grad in ("reduce", "atomic"):
+        q = ctx.Queue()
+        init = file_init()
+        procs = [ctx.Process(target=_run_w2v_rank, args=(r, 2, init, grad, q)) for r in range(2)]
+        for p in procs:
+            p.start()
+        res = collect(q, procs, 2, 240)
+        for p in procs:
+            p.join(60)
+            assert p.exitcode == 0
+        out[grad] = {r: (l, t) for r, l, t in res}
+    for r in range(2):
+        (lr, tr), (la, ta) = out["reduce"][r], out["atomic"][r]
+        assert np.isfinite(lr).all() and np.mean(lr[-3:]) < np.mean(lr[:2])
+        np.testing.assert_allclose(lr, la, rtol=1e-4)
+        assert tr.keys() == ta.keys() and len(tr) > 0
+        ks = list(tr.keys())
+        a, b = np.stack([ta[k] for k in ks]), np.stack([tr[k] for k in ks])
+        assert np.isclose(b, a, rtol=1e-3, atol=5e-4).mean() > 0.9999
+        np.testing.assert_allclose(b, a, rtol=5e-2, atol=2e-2)
