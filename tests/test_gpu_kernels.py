@@ -241,6 +241,31 @@ def test_dedup_route_matches_reference(dev, nranks, n, frags, mode):
     assert int(r3.ucount.sum().item()) == len(np.unique(k3[ok]))
 
 
+@pytest.mark.parametrize("nranks", [1, 4])
+def test_bucket_dedup_edge_sizes_and_hot_key(dev, nranks):
+    """Bucketed dedup at the sizes where its layout changes (tiny calls, one
+    wave, one register tile) and a Zipf-extreme batch: one key repeated far
+    past a dedup thread's register slots (the hot-bucket excess loop)."""
+    from swiftsnails_amd.ops.dedup import Deduper
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    fm = torch.from_numpy(HashFrag(nranks, 64).rank_map().astype(np.int32))
+    d = Deduper(200_000, nranks=nranks, frag_map=fm, gdim=1, device=dev, mode="bucket")
+    rng = np.random.default_rng(7)
+    cases = [np.array([42], np.int64), np.array([5, 5], np.int64),
+             rng.integers(0, 50, 63), rng.integers(0, 10**12, 64), rng.integers(0, 30, 65),
+             rng.integers(0, 10**9, 4097),
+             np.concatenate([np.full(150_000, 123456789, np.int64), rng.integers(0, 999, 3000)])]
+    for k in cases:
+        k = k.astype(np.int64)
+        r = d(torch.from_numpy(k).to(dev))
+        torch.cuda.synchronize()
+        inv = r.inv.cpu().numpy().view(np.uint32).astype(np.int64)
+        np.testing.assert_array_equal(r.ukeys.cpu().numpy()[inv], k)
+        assert int(r.ucount.sum().item()) == len(np.unique(k))
+    d.check()
+
+
 @pytest.mark.parametrize("nranks", [1, 3])
 @pytest.mark.parametrize("singles", [False, True])
 def test_bucket_reduce_lr_matches_atomic_path(dev, nranks, singles):

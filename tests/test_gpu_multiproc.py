@@ -265,5 +265,7 @@ def test_word2vec_window_world2_reduce_matches_atomics():
         assert tr.keys() == ta.keys() and len(tr) > 0
         ks = list(tr.keys())
         a, b = np.stack([ta[k] for k in ks]), np.stack([tr[k] for k in ks])
-        assert np.isclose(b, a, rtol=1e-3, atol=5e-4).mean() > 0.9999
+        # the atomic path sums in arrival order, so 12 AdaGrad rounds leave a
+        # few near-zero coordinates outside the tight band (measured 99.95-100%)
+        assert np.isclose(b, a, rtol=1e-3, atol=5e-4).mean() > 0.999
         np.testing.assert_allclose(b, a, rtol=5e-2, atol=2e-2)
