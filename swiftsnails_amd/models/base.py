@@ -36,6 +36,11 @@ class PipelinedWorker:
         self._cap_base = 0
         # SS_ROUTE_FIRST=1: route round i+2 before pulling round i+1 (below)
         self._route_first = os.environ.get("SS_ROUTE_FIRST", "0") != "0"
+        # SS_ROUTE_EARLY=1: route round i+2 at the START of step i, before
+        # round i's compute and push are enqueued (experiment, below)
+        self._route_early = (os.environ.get("SS_ROUTE_EARLY", "0") != "0" and
+                             not self._route_first)
+        self._next2 = None
 
     # -- subclass hooks
     # optional ``(dd, slot, stream_ptr)`` hook run on the route stream right
@@ -185,6 +190,14 @@ class PipelinedWorker:
             self._cur = eng.pull_ahead_round(r)
             self._next = self._route(self.step_idx + 1)
         rnd = self._cur
+        if self._route_early and self._next2 is None and not getattr(eng, "push_on_pull", False):
+            # the route stream's kernels for round i+2 (its slot was released
+            # by round i+2-depth's push) get dispatched before round i's merge
+            # and apply fill the CUs.  Measured slower (1.103-1.106 ->
+            # 1.118-1.130 ms/step, N>1 path on one GPU with the N>1 route
+            # tuning, three A/B pairs): the earlier dedup competes with round
+            # i's main-stream chain, which is the longer one
+            self._next2 = self._route(self.step_idx + 2)
         eng.begin(rnd)
         self._zero_acc()
         if self.active:
@@ -207,6 +220,9 @@ class PipelinedWorker:
             nxt = self._route(self.step_idx + 2)
             self._cur = eng.pull_ahead_round(self._next)
             self._next = nxt
+        elif self._next2 is not None:
+            self._cur = eng.pull_ahead_round(self._next)
+            self._next, self._next2 = self._next2, None
         else:
             self._cur = eng.pull_ahead_round(self._next)
             self._next = self._route(self.step_idx + 2)

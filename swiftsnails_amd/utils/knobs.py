@@ -172,6 +172,10 @@ KNOBS: dict[str, Knob] = {
     "SS_ROUTE_FIRST": Knob("0", "models/base.py", "experiment",
                            "pull-ahead step: route round i+2 before waiting for round i+1's "
                            "counts (1.18 vs 1.16 ms/step, N>1 path on one GPU)"),
+    "SS_ROUTE_EARLY": Knob("0", "models/base.py", "experiment",
+                           "pull-ahead step: route round i+2 at the start of step i, before "
+                           "round i's merge and apply are enqueued (1.103-1.106 -> 1.118-1.130 "
+                           "ms/step, N>1 path on one GPU, three A/B pairs)"),
     "SS_PULL_FILL": Knob("0", "models/sparse_lr.py", "experiment",
                          "1 GPU LR: the snapshot pull writes the occurrence parameters itself "
                          "(k_pull_fill_bk; 0.86 -> 0.94 ms/step)"),
