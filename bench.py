@@ -148,9 +148,20 @@ def main(argv=None):
     # region; the data generator then reads its step from a device counter)
     graphed = False
     if a.graph == "on" or (a.graph == "auto" and world == 1):
+        # a replay runs a whole graph of `per` steps on the first step() of
+        # its period, so the timed region must start on a period boundary and
+        # span whole periods: per = the longest multiple of the ring depth (up
+        # to 4 periods) that divides --steps, else one graph per step
+        per = next((m * engine.depth for m in (4, 3, 2, 1) if a.steps % (m * engine.depth) == 0),
+                   1)
+        os.environ["SS_GRAPH_STEPS"] = str(per)
         graphed = worker.enable_graph()
-        for i in range(2 * engine.depth):  # warm every phase's graph
-            worker.step()
+        if graphed:
+            per = worker._gper
+            warm = per * max(1, -(-2 * engine.depth // per))  # whole periods, >= 2 ring periods
+            for i in range(warm):  # warm every graph
+                worker.step()
+            assert (worker.step_idx - worker._gbase) % per == 0 and a.steps % per == 0
     torch.cuda.synchronize()
     engine.check()
     first_loss = worker.mean_loss()
