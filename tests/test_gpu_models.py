@@ -662,3 +662,30 @@ def test_fm_trains_with_pull_ahead_staleness_bound(dev, monkeypatch, pull_stream
     table.check()
     assert np.isfinite(losses).all()
     assert np.mean(losses[-5:]) < min(0.66, np.mean(losses[5:10]) - 0.01), losses
+
+
+def _bench_1gpu(extra):
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py")] + extra, cwd=root,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+def test_bench_graph_mode_times_whole_periods():
+    """bench.py --graph on: the timed region runs exactly --steps steps.  With
+    12 timed steps the graph holds 12 steps (3 ring periods) and the warm-up
+    one graph, so the job runs warmup + 12 + 12 steps in all — the same
+    training as an eager run of warmup + 24 steps (identical final loss)."""
+    base = ["--batch", "4096", "--features", "2000000", "--warmup", "3"]
+    g = _bench_1gpu(base + ["--steps", "12", "--graph", "on"])
+    e = _bench_1gpu(base + ["--steps", "24"])
+    assert g["config"]["hipgraph"] is True and e["config"]["hipgraph"] is False
+    assert g["steps"] == 12 and g["ms_per_step"] > 0
+    assert g["config"]["loss_last"] == pytest.approx(e["config"]["loss_last"], rel=1e-4, abs=1e-5)
