@@ -288,6 +288,7 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     graphed = str(cfg.get("graph", "0")) not in ("0", "false", "") and w.enable_graph()
     torch.cuda.synchronize()
     ctx.barrier()
+    r0 = w.rounds_done()
     t0 = time.perf_counter()
     for i in range(steps):
         with ctx.tracer.range("step"):
@@ -303,13 +304,17 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     if ctx.world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     el = float(t.item())
+    # rounds the device ran in the timed region: with hipGraphs the last
+    # replay runs its whole graph, so this can exceed `steps`
+    done = max(steps, w.rounds_done() - r0)
     n = torch.tensor([w.samples_per_step()], dtype=torch.int64)
     if ctx.world > 1:
         dist.all_reduce(n)
     stats = {"model": cfg.get("model", "sparse_lr"), "world": ctx.world,
              "servers": len(ctx.servers), "workers": len(ctx.workers), "steps": steps,
-             "seconds": el, "ms_per_step": 1000 * el / max(1, steps),
-             "samples_per_s": int(n.item()) * steps / el if el > 0 else 0.0,
+             "seconds": el, "ms_per_step": 1000 * el / max(1, done),
+             "samples_per_s": int(n.item()) * done / el if el > 0 else 0.0,
+             "rounds_timed": done,
              "loss": w.mean_loss() if ctx.is_worker else None, "hipgraph": bool(graphed),
              "start_round": ctx.start_round}
     m = ctx.engine.metrics.counters
@@ -319,7 +324,7 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
         # word2vec sliding-window batches: samples are words (centers); the
         # positive pairs per step depend on sentence edges and reduced windows
         stats["rank0_pairs_last_step"] = w.step_pairs()
-        stats["rank0_pairs_per_s_est"] = (stats["rank0_pairs_last_step"] * steps / el
+        stats["rank0_pairs_per_s_est"] = (stats["rank0_pairs_last_step"] * done / el
                                           if el > 0 else 0.0)
     if ctx.tracer.enabled:
         stats["trace"] = ctx.tracer.summary()
