@@ -54,7 +54,7 @@ def test_cli_gpu_sparse_lr_backup_and_resume(tmp_path):
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
     assert r.returncode == 0, r.stderr[-3000:]
     stats = json.loads(r.stdout.strip().splitlines()[-1])
-    assert stats["samples_per_s"] > 0 and stats["steps"] == 10
+    assert stats["samples_per_s"] > 0 and stats["steps"] == 10 and stats["rounds_timed"] == 10
     assert (tmp_path / "param-5.shard0-of-1.bin").exists()
     assert (tmp_path / "param-10.shard0-of-1.bin").exists()
     txt = tmp_path / "final.shard0-of-1.txt"
@@ -116,3 +116,21 @@ def test_latest_checkpoint_picks_newest_complete_set(tmp_path):
         (tmp_path / name).write_bytes(b"x")
     assert ck.latest_checkpoint(str(tmp_path)) == (str(tmp_path / "param-10"), 10, 2)
     assert ck.latest_checkpoint(str(tmp_path / "missing")) is None
+
+
+@pytest.mark.gpu
+def test_cli_gpu_graph_replay_counts_rounds_run():
+    """With `graph: 1` a replay runs a whole graph (4 ring periods = 16 steps
+    by default), so 10 requested steps run 16 rounds and the stats divide by
+    the rounds the device ran."""
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    r = subprocess.run([sys.executable, "-m", "swiftsnails_amd.launch", "--config",
+                        os.path.join(ROOT, "configs", "sparse_lr_10m.conf"),
+                        "--set", "batch_size=4096", "--set", "num_features=1000000",
+                        "--set", "graph=1", "--steps", "10", "--warmup", "2"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    stats = json.loads(r.stdout.strip().splitlines()[-1])
+    assert stats["hipgraph"] is True and stats["steps"] == 10
+    assert stats["rounds_timed"] % 4 == 0 and stats["rounds_timed"] >= 10
+    assert stats["ms_per_step"] == pytest.approx(1000 * stats["seconds"] / stats["rounds_timed"])
