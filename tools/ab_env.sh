@@ -20,7 +20,8 @@ for rep in $(seq 1 "$REPS"); do
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])
 v = d.get("value", d.get("samples_per_s", 0.0))
-print(f"{sys.argv[2]:24s} {d['ms_per_step']:.4f} ms/step {v/1e6:7.1f} M/s loss {d.get('loss')}")
+loss = d.get("loss", d.get("config", {}).get("loss_last"))
+print(f"{sys.argv[2]:24s} {d['ms_per_step']:.4f} ms/step {v/1e6:7.1f} M/s loss {loss}")
 PY
   done
 done
