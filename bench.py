@@ -83,8 +83,9 @@ def main(argv=None):
     from swiftsnails_amd.parallel.transport import LoopbackTransport, RcclTransport
 
     ctrans = ptrans = None
+    comms = 0
     if world > 1:
-        from swiftsnails_amd.parallel.transport import default_gloo_ifname
+        from swiftsnails_amd.parallel.transport import default_gloo_ifname, rccl_comms_mode
 
         default_gloo_ifname()
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -94,31 +95,37 @@ def main(argv=None):
                 from swiftsnails_amd.parallel.transport import TorchDistTransport
 
                 transport = TorchDistTransport()
-            else:
-                # three native RCCL communicators, one per stream: data plane
-                # (main: gradients), count exchange (route), pulled-ahead round
-                # (pull: keys + rows)
+            elif rccl_comms_mode() == 1:
+                # one native RCCL communicator, every collective on its comm
+                # stream in program order (the conservative default)
                 transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
-                ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts")
-                ptrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_pull")
+                comms = 1
+            else:
+                # three communicators, one per engine stream: data plane
+                # (main: gradients), route (counts, bucket runs), pull (keys, rows)
+                transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data",
+                                          serial=False)
+                ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts",
+                                       serial=False)
+                ptrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_pull",
+                                       serial=False)
+                comms = 3
         except Exception as e:  # pragma: no cover - hardware dependent
             from swiftsnails_amd.parallel.transport import TorchDistTransport
 
             print(f"bench.py: native RCCL communicator failed ({e}); "
                   "falling back to torch.distributed(nccl=RCCL)", file=sys.stderr)
             transport = TorchDistTransport(dist.new_group(backend="nccl"))
+            ctrans = ptrans = None
+            comms = 0
     else:
         transport = LoopbackTransport()
         general = os.environ.get("SS_ENGINE_GENERAL", "0")
         if general == "rccl":
-            # the N>1 engine path on one GPU through three real (size-1) RCCL
-            # communicators: the multi-GPU call sequence, minus the peers
-            transport, ctrans, ptrans = (
-                RcclTransport(0, 1, dev, uid=RcclTransport.new_unique_id()) for _ in range(3))
-        elif general != "0":
-            # the N>1 engine path on one GPU: one loopback per stream, as the
-            # three RCCL communicators of a multi-GPU run
-            ctrans, ptrans = LoopbackTransport(), LoopbackTransport()
+            # the N>1 engine path on one GPU through a real (size-1) RCCL
+            # communicator: the multi-GPU call sequence, minus the peers
+            transport = RcclTransport(0, 1, dev, uid=RcclTransport.new_unique_id())
+            comms = 1
 
     data = CtrSynth(batch_size=a.batch, num_fields=a.fields, num_features=a.features,
                     tail_frac=a.tail)
@@ -132,7 +139,7 @@ def main(argv=None):
     from swiftsnails_amd.parallel.watchdog import FailureHandler, Watchdog
 
     failure = FailureHandler()
-    for t in (transport, ctrans, ptrans):
+    for t in {id(x): x for x in (transport, ctrans, ptrans) if x is not None}.values():
         if hasattr(t, "abort"):
             failure.add_hook(t.abort)
     wd = Watchdog(float(os.environ.get("SS_BENCH_ROUND_TIMEOUT", "300")), failure, name="bench")
@@ -187,6 +194,17 @@ def main(argv=None):
     keys_in_table = torch.tensor([table.size()], dtype=torch.int64)
     if world > 1:
         dist.all_reduce(keys_in_table)
+    # what the engine moved per step (this rank; host-known counts)
+    m = engine.metrics.counters
+    nsteps = max(1, engine.rounds)
+    a2a = int(m.get("a2a_bytes", 0) / nsteps)
+    srv_unique = int(m.get("server_unique", 0) / nsteps)
+    recv = int(m.get("unique_recv", 0) / nsteps)
+    if engine.fast1:
+        tlabel = "none (world 1: colocated worker + server, no exchange)"
+    else:
+        tlabel = transport.label
+    rccl_n = transport.nranks() if hasattr(transport, "nranks") else None
 
     samples = a.batch * world * a.steps
     value = samples / elapsed
@@ -210,10 +228,16 @@ def main(argv=None):
                 "model": f"sparse_lr_{a.features // 1_000_000}M_features",
                 "global_batch": a.batch * world,
                 "seq_len": a.fields,
-                "parallelism": (f"ps{world} (colocated worker+server shard per GPU, "
-                                f"{'RCCL' if a.transport == 'rccl' else 'gloo'} alltoallv"
-                                + (", pull-ahead staleness 1)" if getattr(engine, "pull_ahead", False)
-                                   else ")")),
+                "parallelism": f"ps{world}" + (" (colocated worker + server shard per GPU"
+                                                + (", pull-ahead staleness 1)"
+                                                   if getattr(engine, "pull_ahead", False)
+                                                   else ")")),
+                "transport": tlabel,
+                "comms": comms,
+                "rccl_nranks": rccl_n,
+                "a2a_bytes_per_step": a2a,
+                "unique_recv_per_step": recv,
+                "server_unique_keys_per_step": srv_unique,
                 "optimizer": a.optimizer,
                 "hipgraph": graphed,
                 "keys_per_step_per_gpu": a.batch * a.fields,

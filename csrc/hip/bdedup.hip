@@ -65,6 +65,11 @@ static constexpr int kBdMaxChunk = 8192;  // occurrences per count/scatter workg
 static constexpr int kBdChunkLanes = 1024;  // chunk granularity (any CT below divides it)
 static constexpr int kBdDT = 512;         // dedup workgroup size
 static constexpr int kBdTarget = 2048;  // target occurrences per bucket
+// N>1: a server merges bucket k of every source (server.hip), so a source's
+// bucket must stay small enough that N of them fit one server workgroup's
+// table after its sub-bucket split
+static constexpr int kBdTargetDist = 1024;
+static int bd_target(int nranks) { return nranks > 1 ? kBdTargetDist : kBdTarget; }
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
 static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
@@ -109,8 +114,9 @@ static BdLayout bd_layout(long long n, int nranks, int ndest) {
   ndest = bd_clamp_ndest(nranks, ndest);
   // ~2048 occurrences per bucket, but at least ~1024 buckets for small calls
   // (>= 4 workgroups per CU; a word2vec step of 196K keys got only 96 buckets)
-  long long target = std::min<long long>(kBdTarget, std::max<long long>(128, n / 1024));
-  if (n > (long long)kBdMaxBuckets * kBdTarget) target = (n + kBdMaxBuckets - 1) / kBdMaxBuckets;
+  const int tg = bd_target(nranks);
+  long long target = std::min<long long>(tg, std::max<long long>(128, n / 1024));
+  if (n > (long long)kBdMaxBuckets * tg) target = (n + kBdMaxBuckets - 1) / kBdMaxBuckets;
   // buckets per destination from the keys one destination receives (n /
   // ndest), not n / nranks: ranks that host no shard get empty buckets
   long long pd = (n + (long long)ndest * target - 1) / ((long long)ndest * target);
@@ -155,7 +161,8 @@ long long bd_scratch_words(long long n, int nranks, int ndest) {
   if (n < 1) n = 1;
   ndest = bd_clamp_ndest(nranks, ndest);
   // active buckets (those of receiving destinations), then all P = Pd * nranks
-  long long pact = std::max<long long>(1056, (n + kBdTarget - 1) / kBdTarget);
+  const int tg = bd_target(nranks);
+  long long pact = std::max<long long>(1056, (n + tg - 1) / tg);
   pact = std::min<long long>(pact, kBdMaxBuckets) + 2 * ndest;
   const long long pmax = ((pact + ndest - 1) / ndest + 1) * nranks;
   const long long waves = (n + 256ll * kBdMaxChunk - 1) / (256ll * kBdMaxChunk);
@@ -567,13 +574,14 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
   }
   __syncthreads();
   if (slots) {
-    // fused K5 (one GPU, scalar AdaGrad rows with a pull snapshot): the
-    // merged gradient goes straight into the optimizer update — the (w, h)
-    // the pull read (coalesced), one blind 8-byte store per key
+    // fused K5 (scalar AdaGrad rows): the merged gradient goes straight into
+    // the optimizer update — from the (w, h) the pull snapshot (coalesced,
+    // then one blind 8-byte store per key), or read from the row when no
+    // snapshot is valid (N>1 servers with pull-ahead: a read-modify-write)
     for (uint32_t l = threadIdx.x; l < nu; l += RT) {
       const long long slot = slots[base + l];
       if (slot < 0) continue;
-      float2 wh = snap[base + l];
+      float2 wh = snap ? snap[base + l] : *reinterpret_cast<const float2*>(slot_row(t, slot));
       float s2 = 0.f;
       opt_update(op, wh.x, wh.y, s2, acc[l]);
       *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
@@ -874,18 +882,25 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg, uint32_t* osi_inv, uint8_t* usingle, int ndest) {
+                     unsigned long long* dbg, uint32_t* osi_inv, uint8_t* usingle, int ndest,
+                     long long lay_n) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
-  if (n <= 0) {
+  // lay_n (N>1 engines): the bucket layout is that of a call of lay_n keys
+  // whatever this call's n, so every rank splits a destination's keys into
+  // the same Pd buckets (the servers merge bucket k of all sources); an empty
+  // call then still writes an all-empty layout
+  if (lay_n > 0 && lay_n < n) throw_error("bdedup: lay_n below the call's key count");
+  const long long ln = lay_n > 0 ? lay_n : n;
+  if (ln <= 0) {
     check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
     return;
   }
   if (ucap < n) throw_error("bdedup: per-destination capacity must be >= n");
   if ((unsigned long long)rs.nranks * (unsigned long long)ucap >= 0x7FFFFFFFull)
     throw_error("bdedup: nranks*ucap overflows 31-bit unique ids");
-  const BdLayout L = bd_layout(n, rs.nranks, ndest);
+  const BdLayout L = bd_layout(ln, rs.nranks, ndest);
   if ((long long)L.Pd * bd_clamp_ndest(rs.nranks, ndest) > kBdMaxBuckets + kMaxSeg ||
-      n > bd_max_keys())
+      ln > bd_max_keys())
     throw_error("bdedup: too many keys per call (max ~45M)");
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
@@ -983,9 +998,9 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   DevTable tv{};
   OptParams opv{};
   if (slots) {
-    if (!t || !op || !snap || osi || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
+    if (!t || !op || osi || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
         t->row_off % 8 != 0 || t->stride % 8 != 0)
-      throw_error("bd_reduce: fused apply needs scalar AdaGrad rows, a snapshot and compact ids");
+      throw_error("bd_reduce: fused apply needs scalar AdaGrad rows and compact ids");
     tv = *t;
     opv = *op;
   }
@@ -1007,6 +1022,37 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
                      S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
   check_launch("k_bd_reduce");
+}
+
+// explicit-layout forms (server.hip: the server's merge of received keys has
+// its own bucket arrays instead of a BdLayout scratch)
+void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, const uint32_t* unum,
+                        const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
+                        float* ugrad, const DevTable* t, const long long* slots,
+                        const float* snap, const OptParams* op, hipStream_t st) {
+  if (P <= 0) return;
+  DevTable tv{};
+  OptParams opv{};
+  if (slots) {
+    if (!t || !op || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
+        t->row_off % 8 != 0 || t->stride % 8 != 0)
+      throw_error("bd_reduce_p: fused apply needs scalar AdaGrad rows");
+    tv = *t;
+    opv = *op;
+  }
+  hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj, luid,
+                     gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
+                     reinterpret_cast<const float2*>(snap), opv);
+  check_launch("k_bd_reduce_p");
+}
+
+void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
+                          const uint32_t* unum, const uint32_t* luid, const float* uvals,
+                          float* occ, const uint32_t* pj, hipStream_t st) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(k_bd_fill_occ<512>, dim3(P), dim3(512), 0, st, bstart, ubase, unum, luid,
+                     uvals, occ, 0, pj);
+  check_launch("k_bd_fill_occ_p");
 }
 
 long long bd_fm_ovf_words(long long n) { return n / kFmOcc + 2; }

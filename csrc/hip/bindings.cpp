@@ -193,18 +193,19 @@ PYBIND11_MODULE(_ss_hip, m) {
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
                        uintptr_t st, uintptr_t dbg, uintptr_t osi_inv, uintptr_t usingle,
-                       int ndest) {
+                       int ndest, long long lay_n) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
                     P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
                     P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
                     P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg),
-                    P<uint32_t>(osi_inv), P<uint8_t>(usingle), ndest);
+                    P<uint32_t>(osi_inv), P<uint8_t>(usingle), ndest, lay_n);
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
-     py::arg("osi_inv") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0);
+     py::arg("osi_inv") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0,
+     py::arg("lay_n") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
@@ -325,6 +326,51 @@ PYBIND11_MODULE(_ss_hip, m) {
                        P<const uint32_t>(pj));
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("luid"), py::arg("uvals"),
      py::arg("occ"), py::arg("osi"), py::arg("st"), py::arg("ndest") = 0, py::arg("pj") = 0);
+  // server-side merge of a round's received keys (server.hip)
+  m.def("srv_sub_buckets", &srv_sub_buckets);
+  m.def("srv_dedup", [](uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum, long long cap, int nsrc,
+                        int Pd, int m, int me, uintptr_t cnt, uintptr_t bstart, uintptr_t pj,
+                        uintptr_t luid, uintptr_t bkeys, uintptr_t ubase, uintptr_t unum,
+                        uintptr_t ucount, uintptr_t err, uintptr_t st) {
+    launch_srv_dedup(P<const uint64_t>(rkeys), P<const uint32_t>(rbase), P<const uint32_t>(rnum),
+                     cap, nsrc, Pd, m, me, P<uint32_t>(cnt), P<uint32_t>(bstart), P<uint32_t>(pj),
+                     P<uint32_t>(luid), P<uint64_t>(bkeys), P<uint32_t>(ubase), P<uint32_t>(unum),
+                     P<unsigned long long>(ucount), P<uint32_t>(err), S(st));
+  });
+  m.def("srv_fill", [](int Pn, uintptr_t bstart, uintptr_t ubase, uintptr_t unum, uintptr_t pj,
+                       uintptr_t luid, uintptr_t rows, uintptr_t out, int D, uintptr_t st) {
+    if (D == 1)
+      launch_bd_fill_occ_p(Pn, P<const uint32_t>(bstart), P<const uint32_t>(ubase),
+                           P<const uint32_t>(unum), P<const uint32_t>(luid),
+                           P<const float>(rows), P<float>(out), P<const uint32_t>(pj), S(st));
+    else
+      launch_srv_fill_rows(Pn, P<const uint32_t>(bstart), P<const uint32_t>(ubase),
+                           P<const uint32_t>(pj), P<const uint32_t>(luid), P<const float>(rows),
+                           P<float>(out), D, S(st));
+  });
+  // merged gradients per distinct key; with a table (scalar AdaGrad rows) the
+  // update is fused: from the snapshot (blind store) or read from the row
+  m.def("srv_merge", [](int Pn, uintptr_t bstart, uintptr_t ubase, uintptr_t unum, uintptr_t pj,
+                        uintptr_t luid, uintptr_t grads, uintptr_t merged, int D,
+                        std::optional<DevTable> t, uintptr_t slots, uintptr_t snap,
+                        std::optional<OptParams> op, uintptr_t st) {
+    if (D == 1)
+      launch_bd_reduce_p(Pn, P<const uint32_t>(bstart), P<const uint32_t>(ubase),
+                         P<const uint32_t>(unum), P<const uint32_t>(pj), P<const uint32_t>(luid),
+                         P<const float>(grads), 1, P<float>(merged), t ? &*t : nullptr,
+                         P<const long long>(slots), P<const float>(snap), op ? &*op : nullptr,
+                         S(st));
+    else if (slots)
+      throw_error("srv_merge: a fused update needs scalar rows");
+    else
+      launch_srv_merge_rows(Pn, P<const uint32_t>(bstart), P<const uint32_t>(ubase),
+                            P<const uint32_t>(unum), P<const uint32_t>(pj),
+                            P<const uint32_t>(luid), P<const float>(grads), P<float>(merged), D,
+                            S(st));
+  }, py::arg("P"), py::arg("bstart"), py::arg("ubase"), py::arg("unum"), py::arg("pj"),
+     py::arg("luid"), py::arg("grads"), py::arg("merged"), py::arg("D"),
+     py::arg("t") = std::nullopt, py::arg("slots") = 0, py::arg("snap") = 0,
+     py::arg("op") = std::nullopt, py::arg("st") = 0);
   m.def("fm_fwd_g", [](uintptr_t inv, std::vector<uintptr_t> ix, uintptr_t labels, int B,
                        int F, int dim, uintptr_t uvals, uintptr_t gs, uintptr_t gss,
                        uintptr_t loss, uintptr_t pred, uintptr_t st) {
@@ -458,7 +504,11 @@ PYBIND11_MODULE(_ss_hip, m) {
       .def_static("unique_id", []() { return py::bytes(RcclComm::unique_id()); })
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("nranks", &RcclComm::nranks)
-      .def("alltoallv", &RcclComm::alltoallv, py::call_guard<py::gil_scoped_release>())
+      .def("alltoallv", &RcclComm::alltoallv, py::arg("send"), py::arg("scounts"),
+           py::arg("sdispls"), py::arg("recv"), py::arg("rcounts"), py::arg("rdispls"),
+           py::arg("elem_bytes"), py::arg("stream"), py::arg("send_cap") = -1,
+           py::arg("recv_cap") = -1, py::call_guard<py::gil_scoped_release>())
+      .def("comm_count", &RcclComm::comm_count)
       .def("alltoall", &RcclComm::alltoall, py::call_guard<py::gil_scoped_release>())
       .def("allreduce", &RcclComm::allreduce, py::call_guard<py::gil_scoped_release>())
       .def("broadcast", &RcclComm::broadcast, py::call_guard<py::gil_scoped_release>())

@@ -1,6 +1,8 @@
 // comm.cpp — RCCL communicator (see comm.h).
 #include "comm.h"
 
+#include "ss/a2a_schedule.h"
+
 #include <rccl/rccl.h>
 
 #include <cstring>
@@ -68,42 +70,46 @@ void RcclComm::abort() {
 void RcclComm::alltoallv(uintptr_t send, const std::vector<long long>& scounts,
                          const std::vector<long long>& sdispls, uintptr_t recv,
                          const std::vector<long long>& rcounts,
-                         const std::vector<long long>& rdispls, int elem_bytes, uintptr_t stream) {
-  if ((int)scounts.size() != nranks_ || (int)sdispls.size() != nranks_ ||
-      (int)rcounts.size() != nranks_ || (int)rdispls.size() != nranks_)
-    throw std::runtime_error("alltoallv: count/displ vectors must have nranks entries");
+                         const std::vector<long long>& rdispls, int elem_bytes, uintptr_t stream,
+                         long long send_cap, long long recv_cap) {
   if (!comm_) throw std::runtime_error("alltoallv on aborted communicator");
+  // the whole exchange is validated (sizes, ranges inside the buffers)
+  // before anything is enqueued: a bad count must not become a fault
+  const std::vector<A2aStep> plan = a2a_schedule(rank_, nranks_, scounts, sdispls, rcounts,
+                                                 rdispls, elem_bytes, send_cap, recv_cap);
   auto st = reinterpret_cast<hipStream_t>(stream);
   const char* sb = reinterpret_cast<const char*>(send);
   char* rb = reinterpret_cast<char*>(recv);
-  const size_t eb = (size_t)elem_bytes;
-  if (scounts[rank_] != rcounts[rank_])
-    throw std::runtime_error("alltoallv: self send/recv counts differ");
-  if (scounts[rank_] > 0)
-    check_hip_c(hipMemcpyAsync(rb + rdispls[rank_] * eb, sb + sdispls[rank_] * eb,
-                               scounts[rank_] * eb, hipMemcpyDeviceToDevice, st),
+  const A2aStep& self = plan[0];
+  if (self.send_bytes > 0)
+    check_hip_c(hipMemcpyAsync(rb + self.recv_off, sb + self.send_off, self.send_bytes,
+                               hipMemcpyDeviceToDevice, st),
                 "alltoallv self copy");
+  if (nranks_ == 1) return;
   check_nccl(ncclGroupStart(), "groupStart");
-  for (int k = 1; k < nranks_; ++k) {
-    // staggered peer order: rank r talks to r+k and r-k in step k, spreading
-    // the first-issued transfers over distinct xGMI links.
-    const int to = (rank_ + k) % nranks_;
-    const int from = (rank_ - k + nranks_) % nranks_;
-    if (scounts[to] > 0)
-      check_nccl(ncclSend(sb + sdispls[to] * eb, scounts[to] * eb, ncclUint8, to, comm_, st),
-                 "ncclSend");
-    if (rcounts[from] > 0)
-      check_nccl(ncclRecv(rb + rdispls[from] * eb, rcounts[from] * eb, ncclUint8, from, comm_, st),
+  for (size_t i = 1; i < plan.size(); ++i) {
+    const A2aStep& x = plan[i];
+    if (x.to >= 0)
+      check_nccl(ncclSend(sb + x.send_off, x.send_bytes, ncclUint8, x.to, comm_, st), "ncclSend");
+    if (x.from >= 0)
+      check_nccl(ncclRecv(rb + x.recv_off, x.recv_bytes, ncclUint8, x.from, comm_, st),
                  "ncclRecv");
   }
   check_nccl(ncclGroupEnd(), "groupEnd");
+}
+
+int RcclComm::comm_count() const {
+  if (!comm_) throw std::runtime_error("comm_count on aborted communicator");
+  int n = 0;
+  check_nccl(ncclCommCount(comm_, &n), "ncclCommCount");
+  return n;
 }
 
 void RcclComm::alltoall(uintptr_t send, uintptr_t recv, long long count, int elem_bytes,
                         uintptr_t stream) {
   std::vector<long long> c(nranks_, count), d(nranks_);
   for (int i = 0; i < nranks_; ++i) d[i] = (long long)i * count;
-  alltoallv(send, c, d, recv, c, d, elem_bytes, stream);
+  alltoallv(send, c, d, recv, c, d, elem_bytes, stream, -1, -1);
 }
 
 void RcclComm::allreduce(uintptr_t send, uintptr_t recv, long long count, int dtype, int op,

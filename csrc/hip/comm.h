@@ -40,7 +40,10 @@ class RcclComm {
   void alltoallv(uintptr_t send, const std::vector<long long>& scounts,
                  const std::vector<long long>& sdispls, uintptr_t recv,
                  const std::vector<long long>& rcounts, const std::vector<long long>& rdispls,
-                 int elem_bytes, uintptr_t stream);
+                 int elem_bytes, uintptr_t stream, long long send_cap = -1,
+                 long long recv_cap = -1);
+  // ranks of the communicator as RCCL reports them (ncclCommCount)
+  int comm_count() const;
   // Fixed-size alltoall: `count` elements of `elem_bytes` per peer.
   void alltoall(uintptr_t send, uintptr_t recv, long long count, int elem_bytes, uintptr_t stream);
   // dtype: 0=f32 1=f64 2=i32 3=i64 ; op: 0=sum 1=max 2=min

@@ -1,0 +1,336 @@
+// server.hip — a server's merge of the keys one round receives from all
+// source ranks (N>1): one table lookup and ONE optimizer update per distinct
+// key, whichever workers pushed it.
+//
+// Reference semantics: the server applies every push request as it arrives
+// (server/init.h:115-149, sparsetable.h:181-192) and the push access method
+// has a merge hook for duplicate gradients (merge_push_value,
+// sparse_access_method.h:39-40).  In a collective round all pushes of the
+// round arrive together, so the server merges them first — a key pushed by 8
+// workers costs one probe and one row update instead of 8 of each.
+//
+// Layout contract (bdedup.hip, N>1): every source splits the keys it sends to
+// destination d into the same Pd hash buckets (the layout of a lay_n-key
+// call), bucket (d, k) placed contiguously in its send segment.  With each
+// segment the source sends the per-bucket (ubase, unum) pairs, so bucket k's
+// keys from source s are the run
+//     rkeys[s*cap + (rbase[s][k] - me*cap) : ... + rnum[s][k]]
+// and server bucket k is the union of N runs.  N runs of ~1024 unique keys do
+// not fit one 4096-slot LDS table at N=8, so bucket k is further split into m
+// sub-buckets by an independent hash (the low word of dedup_hash; the sender
+// used the high word): server bucket b = k*m + t.
+//
+//   1 k_srv_count  per k: received keys per sub-bucket (m == 1: the run sums)
+//   2 k_srv_scan   exclusive scan -> bstart (server "occurrence" ranges)
+//   3 k_srv_dedup  per b: LDS hash dedup of the sub-bucket's received keys;
+//                  writes the received position of each (pj), its local id
+//                  (luid), the unique keys staged at bstart[b] (bkeys, what
+//                  the bucketed pull reads) and ubase/unum (compact ids)
+//
+// The outputs have the worker dedup's shape (bstart/ubase/unum/pj/luid), so
+// the server reuses the worker kernels: k_pull_unique_bk (lookup-or-init of
+// the distinct keys), k_bd_fill_occ with pj (response rows per received
+// position, dim 1), k_bd_reduce with F = 1 (gradient merge + fused AdaGrad,
+// dim 1).  Wider rows use k_srv_fill_rows / k_srv_merge_rows below.
+#include "ss_device.h"
+#include "ss_launch.h"
+#include "scan.h"
+
+namespace ss {
+
+static constexpr int kSrvTS = 4096;     // LDS hash slots per server bucket
+static constexpr int kSrvOcc = 8192;    // received keys per server bucket (LDS parking)
+static constexpr int kSrvDT = 512;      // dedup workgroup
+static constexpr uint32_t kSrvInv = 0xFFFFFFFFu;
+
+struct SrvRuns {
+  const uint64_t* rkeys;   // [nsrc * cap] received keys, segment s at s*cap
+  const uint32_t* rbase;   // [nsrc][Pd] the sources' bucket bases (their send layout)
+  const uint32_t* rnum;    // [nsrc][Pd] the sources' bucket sizes
+  long long cap;           // per-source segment capacity (== every source's ucap)
+  int nsrc, Pd, m, me;
+  __device__ __forceinline__ long long run_start(int s, int k) const {
+    return (long long)s * cap + ((long long)rbase[(long long)s * Pd + k] - (long long)me * cap);
+  }
+  __device__ __forceinline__ uint32_t run_len(int s, int k) const {
+    return rnum[(long long)s * Pd + k];
+  }
+};
+
+__device__ __forceinline__ uint32_t srv_sub(uint64_t key, int m) {
+  return m == 1 ? 0u : __umulhi((uint32_t)dedup_hash(key), (uint32_t)m);
+}
+
+// 1. received keys per server bucket
+__global__ __launch_bounds__(256) void k_srv_count(SrvRuns R, uint32_t* __restrict__ cnt) {
+  __shared__ unsigned int h[64];
+  const int k = blockIdx.x;
+  if (R.m == 1) {
+    // the run lengths are the counts: one lane per source
+    if (threadIdx.x < 64) {
+      unsigned int c = 0;
+      for (int s = threadIdx.x; s < R.nsrc; s += 64) c += R.run_len(s, k);
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (threadIdx.x == 0) cnt[k] = c;
+    }
+    return;
+  }
+  if (threadIdx.x < 64) h[threadIdx.x] = 0u;
+  __syncthreads();
+  for (int s = 0; s < R.nsrc; ++s) {
+    const long long a = R.run_start(s, k);
+    const uint32_t len = R.run_len(s, k);
+    for (uint32_t i = threadIdx.x; i < len; i += 256)
+      atomicAdd(&h[srv_sub(R.rkeys[a + i], R.m)], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x < (unsigned)R.m) cnt[(long long)k * R.m + threadIdx.x] = h[threadIdx.x];
+}
+
+// 2. bstart = exclusive scan of cnt (P entries; one workgroup), and the
+//    distinct-key counter the dedup reserves compact ids on starts at zero
+__global__ __launch_bounds__(1024) void k_srv_scan(const uint32_t* __restrict__ cnt, int P,
+                                                   uint32_t* __restrict__ bstart,
+                                                   unsigned long long* __restrict__ ucount) {
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned int tot;
+  const int per = (P + 1023) / 1024;
+  const int b0 = threadIdx.x * per;
+  unsigned int s = 0;
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < P) s += cnt[b0 + i];
+  unsigned int e = block_excl_scan<16>(s, wsum, &tot);
+  for (int i = 0; i < per; ++i)
+    if (b0 + i < P) {
+      bstart[b0 + i] = e;
+      e += cnt[b0 + i];
+    }
+  if (threadIdx.x == 0) {
+    bstart[P] = tot;
+    *ucount = 0ull;
+  }
+}
+
+// 3. one workgroup per server bucket b = k*m + t
+__global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t* __restrict__ bstart,
+                                                      uint32_t* __restrict__ pj,
+                                                      uint32_t* __restrict__ luid,
+                                                      uint64_t* __restrict__ bkeys,
+                                                      uint32_t* __restrict__ ubase,
+                                                      uint32_t* __restrict__ unum,
+                                                      unsigned long long* __restrict__ ucount,
+                                                      uint32_t* __restrict__ err) {
+  __shared__ unsigned long long tab[kSrvTS];
+  __shared__ unsigned int lid[kSrvTS];
+  __shared__ unsigned short park[kSrvOcc];
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned int tot, cur;
+  __shared__ int bad;
+  const int t = threadIdx.x, lane = t & 63;
+  const int b = blockIdx.x, k = b / R.m;
+  const uint32_t sub = (uint32_t)(b % R.m);
+  for (int s = t; s < kSrvTS; s += kSrvDT) tab[s] = kEmptyKey;
+  if (t == 0) {
+    cur = 0u;
+    bad = 0;
+  }
+  __syncthreads();
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+  auto insert = [&](uint64_t key) -> uint32_t {
+    // slot from the high word's low bits: the sender's bucket fixed the high
+    // word's top bits, the sub-bucket the low word's
+    uint32_t s = (uint32_t)(dedup_hash(key) >> 32) & (kSrvTS - 1);
+    for (int i = 0; i < kSrvTS; ++i) {
+      const unsigned long long v = tab[s];
+      if (v == key) return s;
+      if (v == kEmptyKey) {
+        const unsigned long long prev = atomicCAS(&tab[s], kEmptyKey, (unsigned long long)key);
+        if (prev == kEmptyKey || prev == key) return s;
+      }
+      s = (s + 1) & (kSrvTS - 1);
+    }
+    bad = 1;
+    return kSrvInv;
+  };
+  // every source's run of bucket k; the keys of sub-bucket `sub` get a
+  // position in [p0, p1) (wave-aggregated reservation) and an LDS slot
+  for (int s = 0; s < R.nsrc; ++s) {
+    const long long a = R.run_start(s, k);
+    const uint32_t len = R.run_len(s, k);
+    for (uint32_t i0 = 0; i0 < len; i0 += kSrvDT) {
+      const uint32_t i = i0 + t;
+      const uint64_t key = i < len ? R.rkeys[a + i] : kEmptyKey;
+      const bool mine = key != kEmptyKey && srv_sub(key, R.m) == sub;
+      const unsigned long long mask = __ballot(mine);
+      unsigned int wb = 0;
+      if (lane == 0 && mask) wb = atomicAdd(&cur, (unsigned int)__popcll(mask));
+      wb = __shfl(wb, 0, 64);
+      if (mine) {
+        const uint32_t q = wb + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
+        if (q < kSrvOcc && p0 + q < p1) {
+          pj[p0 + q] = (uint32_t)(a + i);
+          park[q] = (unsigned short)insert(key);
+        } else {
+          bad = 1;
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // compaction in slot order: thread t owns slots [kPerT*t, kPerT*(t+1))
+  constexpr int kPerT = kSrvTS / kSrvDT;
+  unsigned int occ = 0;
+#pragma unroll
+  for (int i = 0; i < kPerT; ++i) occ += tab[t * kPerT + i] != kEmptyKey;
+  unsigned int o = block_excl_scan<kSrvDT / 64>(occ, wsum, &tot);
+  __shared__ unsigned long long sbase;
+  if (t == 0) {
+    sbase = atomicAdd(ucount, (unsigned long long)tot);
+    ubase[b] = (uint32_t)sbase;
+    unum[b] = tot;
+    if (bad) atomicOr(err, 1u);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < kPerT; ++i) {
+    const int s = t * kPerT + i;
+    const unsigned long long v = tab[s];
+    if (v != kEmptyKey) {
+      lid[s] = o;
+      bkeys[p0 + o] = v;  // staged in the bucket's own range (k_pull_unique_bk reads it)
+      ++o;
+    }
+  }
+  __syncthreads();
+  const uint32_t n = min(cur, (uint32_t)kSrvOcc);
+  for (uint32_t q = t; q < n && p0 + q < p1; q += kSrvDT) {
+    const uint32_t sl = park[q] == 0xFFFFu ? kSrvInv : park[q];
+    luid[p0 + q] = sl == kSrvInv || sl >= (uint32_t)kSrvTS ? kSrvInv : lid[sl];
+  }
+}
+
+// response rows of width D > 1: out[pj[p]] = rows[ubase[b] + luid[p]]
+__global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restrict__ bstart,
+                                                       const uint32_t* __restrict__ ubase,
+                                                       const uint32_t* __restrict__ pj,
+                                                       const uint32_t* __restrict__ luid,
+                                                       const float* __restrict__ rows,
+                                                       float* __restrict__ out, int D) {
+  const int b = blockIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], base = ubase[b];
+  const long long tot = (long long)(p1 - p0) * D;
+  for (long long e = threadIdx.x; e < tot; e += 256) {
+    const uint32_t p = p0 + (uint32_t)(e / D);
+    const int c = (int)(e % D);
+    const uint32_t l = luid[p];
+    out[(long long)pj[p] * D + c] = l == kSrvInv ? 0.f : rows[((long long)base + l) * D + c];
+  }
+}
+
+// gradient merge of rows of width D: grads received at positions pj[p] are
+// summed per distinct key into merged[ubase[b] + l].  Per bucket the
+// positions are counting-sorted by local id in LDS, then each wave sums its
+// keys' rows (lanes over the row; no atomics)
+__global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restrict__ bstart,
+                                                        const uint32_t* __restrict__ ubase,
+                                                        const uint32_t* __restrict__ unum,
+                                                        const uint32_t* __restrict__ pj,
+                                                        const uint32_t* __restrict__ luid,
+                                                        const float* __restrict__ grads,
+                                                        float* __restrict__ merged, int D) {
+  __shared__ unsigned int off[kSrvTS + 1];
+  __shared__ unsigned short ord[kSrvOcc];
+  __shared__ unsigned int wsum[16];
+  const int b = blockIdx.x, t = threadIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = min(unum[b], (uint32_t)kSrvTS);
+  const uint32_t base = ubase[b];
+  const uint32_t np = min(p1 - p0, (uint32_t)kSrvOcc);
+  for (uint32_t l = t; l <= (uint32_t)kSrvTS; l += 512) off[l] = 0u;
+  __syncthreads();
+  for (uint32_t q = t; q < np; q += 512) {
+    const uint32_t l = luid[p0 + q];
+    if (l < nu) atomicAdd(&off[l + 1], 1u);
+  }
+  __syncthreads();
+  // inclusive scan of off[1..nu] (kSrvTS / 512 = 8 entries per thread)
+  constexpr int kPer = kSrvTS / 512;
+  unsigned int v[kPer], s = 0;
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    v[i] = off[1 + t * kPer + i];
+    s += v[i];
+  }
+  unsigned int e = block_excl_scan<8>(s, wsum, nullptr);
+#pragma unroll
+  for (int i = 0; i < kPer; ++i) {
+    e += v[i];
+    off[1 + t * kPer + i] = e;
+  }
+  __syncthreads();
+  // placement: a second counter pass (cursor = off[l], advanced atomically)
+  __shared__ unsigned int cur[kSrvTS];
+  for (uint32_t l = t; l < (uint32_t)kSrvTS; l += 512) cur[l] = off[l];
+  __syncthreads();
+  for (uint32_t q = t; q < np; q += 512) {
+    const uint32_t l = luid[p0 + q];
+    if (l < nu) ord[atomicAdd(&cur[l], 1u)] = (unsigned short)q;
+  }
+  __syncthreads();
+  const int lane = t & 63, w = t >> 6;
+  for (uint32_t l = w; l < nu; l += 512 / 64) {
+    const uint32_t a = off[l], z = off[l + 1];
+    for (int c0 = 0; c0 < D; c0 += 64) {
+      const int c = c0 + lane;
+      float acc = 0.f;
+      if (c < D)
+        for (uint32_t i = a; i < z; ++i) acc += grads[(long long)pj[p0 + ord[i]] * D + c];
+      if (c < D) merged[((long long)base + l) * D + c] = acc;
+    }
+  }
+}
+
+// ------------------------------------------------------------- launchers
+int srv_sub_buckets(int nsrc) {
+  // N sources x ~1024 keys (<= ~1.25x that with hash imbalance) per bucket k,
+  // at most ~3000 distinct keys per 4096-slot table
+  const long long need = (long long)nsrc * 1280;
+  int m = (int)((need + 2999) / 3000);
+  return m < 1 ? 1 : (m > 64 ? 64 : m);
+}
+
+void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32_t* rnum,
+                      long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
+                      uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
+                      uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
+                      hipStream_t st) {
+  if (nsrc < 1 || Pd < 1 || m < 1 || m > 64) throw_error("srv_dedup: bad layout");
+  SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me};
+  const int P = Pd * m;
+  hipLaunchKernelGGL(k_srv_count, dim3(Pd), dim3(256), 0, st, R, cnt);
+  check_launch("k_srv_count");
+  hipLaunchKernelGGL(k_srv_scan, dim3(1), dim3(1024), 0, st, cnt, P, bstart, ucount);
+  check_launch("k_srv_scan");
+  hipLaunchKernelGGL(k_srv_dedup, dim3(P), dim3(kSrvDT), 0, st, R, bstart, pj, luid, bkeys,
+                     ubase, unum, ucount, err);
+  check_launch("k_srv_dedup");
+}
+
+void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
+                          const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
+                          int D, hipStream_t st) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(k_srv_fill_rows, dim3(P), dim3(256), 0, st, bstart, ubase, pj, luid, rows,
+                     out, D);
+  check_launch("k_srv_fill_rows");
+}
+
+void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
+                           const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
+                           const float* grads, float* merged, int D, hipStream_t st) {
+  if (P <= 0) return;
+  hipLaunchKernelGGL(k_srv_merge_rows, dim3(P), dim3(512), 0, st, bstart, ubase, unum, pj, luid,
+                     grads, merged, D);
+  check_launch("k_srv_merge_rows");
+}
+
+}  // namespace ss

@@ -154,7 +154,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                      unsigned long long* dbg = nullptr, uint32_t* osi_inv = nullptr,
-                     uint8_t* usingle = nullptr, int ndest = 0);
+                     uint8_t* usingle = nullptr, int ndest = 0, long long lay_n = 0);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi = 0,
@@ -175,6 +175,29 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
                          const long long* slots = nullptr, const OptParams* op = nullptr,
                          int ndest = 0);
 long long bd_fm_ovf_words(long long n);
+
+// explicit-layout forms of the bucket kernels (server-side merge)
+void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, const uint32_t* unum,
+                        const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
+                        float* ugrad, const DevTable* t, const long long* slots,
+                        const float* snap, const OptParams* op, hipStream_t st);
+void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
+                          const uint32_t* unum, const uint32_t* luid, const float* uvals,
+                          float* occ, const uint32_t* pj, hipStream_t st);
+
+// --- server.hip (N>1: merge of the keys a round receives from all sources)
+int srv_sub_buckets(int nsrc);
+void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32_t* rnum,
+                      long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
+                      uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
+                      uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
+                      hipStream_t st);
+void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
+                          const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
+                          int D, hipStream_t st);
+void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
+                           const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
+                           const float* grads, float* merged, int D, hipStream_t st);
 
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);

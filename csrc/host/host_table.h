@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstring>
 #include <thread>
+#include <unordered_map>
 #include <cstdio>
 #include <fstream>
 #include <memory>
@@ -231,13 +232,35 @@ class HostTable : NonCopyable {
   // Duplicate keys in one call are applied sequentially under the shard lock.
   void push(const uint64_t* keys, size_t n, const float* grads) {
     if (batch_fn_) {
-      std::vector<float> rows(n * (size_t)width_);
-      run_sharded(keys, n, [&](HostShard& sh, size_t i) {
-        const float* r = row_of(sh, keys[i]);
+      // the rule sees each key once: duplicates are merged (gradients summed,
+      // the reference's merge_push_value, sparse_access_method.h:39-40) —
+      // each copy would otherwise start from the same row and the last
+      // write-back would drop the others' updates
+      std::unordered_map<uint64_t, size_t> first;
+      first.reserve(n * 2);
+      std::vector<uint64_t> ukeys;
+      std::vector<float> ugrads;
+      ukeys.reserve(n);
+      ugrads.reserve(n * (size_t)dim_);
+      for (size_t i = 0; i < n; ++i) {
+        auto it = first.emplace(keys[i], ukeys.size());
+        const float* g = grads + i * (size_t)dim_;
+        if (it.second) {
+          ukeys.push_back(keys[i]);
+          ugrads.insert(ugrads.end(), g, g + dim_);
+        } else {
+          float* acc = ugrads.data() + it.first->second * (size_t)dim_;
+          for (int j = 0; j < dim_; ++j) acc[j] += g[j];
+        }
+      }
+      const size_t u = ukeys.size();
+      std::vector<float> rows(u * (size_t)width_);
+      run_sharded(ukeys.data(), u, [&](HostShard& sh, size_t i) {
+        const float* r = row_of(sh, ukeys[i]);
         std::copy(r, r + width_, rows.data() + i * width_);
       });
-      batch_fn_(keys, n, rows.data(), grads);
-      assign(keys, n, rows.data());
+      batch_fn_(ukeys.data(), u, rows.data(), ugrads.data());
+      assign(ukeys.data(), u, rows.data());
       return;
     }
     run_sharded(keys, n, [&](HostShard& sh, size_t i) {

@@ -13,6 +13,7 @@
 #include "dataio.h"
 #include "hashfrag.h"
 #include "host_table.h"
+#include "ss/a2a_schedule.h"
 #include "ss/hash.h"
 #include "string_util.h"
 #include "transfer.h"
@@ -45,6 +46,26 @@ PYBIND11_MODULE(_ss_host, m) {
     for (py::ssize_t i = 0; i < r.shape(0); ++i) o(i) = fmix64(r(i));
     return out;
   });
+
+  // ---- alltoallv peer schedule (the RCCL communicator's, csrc/hip/comm.cpp)
+  m.def("a2a_schedule",
+        [](int rank, int nranks, std::vector<long long> sc, std::vector<long long> sd,
+           std::vector<long long> rc, std::vector<long long> rd, int eb, long long send_cap,
+           long long recv_cap) {
+          py::list out;
+          try {
+            for (const A2aStep& x : a2a_schedule(rank, nranks, sc, sd, rc, rd, eb, send_cap,
+                                                 recv_cap))
+              out.append(py::make_tuple(x.k, x.to, x.send_off, x.send_bytes, x.from, x.recv_off,
+                                        x.recv_bytes));
+          } catch (const std::invalid_argument& e) {
+            throw py::value_error(e.what());
+          }
+          return out;
+        },
+        py::arg("rank"), py::arg("nranks"), py::arg("scounts"), py::arg("sdispls"),
+        py::arg("rcounts"), py::arg("rdispls"), py::arg("elem_bytes"), py::arg("send_cap") = -1,
+        py::arg("recv_cap") = -1);
 
   // ---- strings
   m.def("trim", &trim);

@@ -308,6 +308,12 @@ TEST(host_table_user_access_methods) {
   t.push(keys.data(), 1, g2.data());
   t.pull(keys.data(), 1, out.data());
   EXPECT(out[0] == 100.f);
+  // a key pushed twice in one call reaches the rule once, gradients summed
+  std::vector<uint64_t> kd = {10, 10};
+  std::vector<float> gd = {1.f, 0.f, 2.f, 0.f};
+  t.push(kd.data(), 2, gd.data());
+  t.pull(keys.data(), 1, out.data());
+  EXPECT(out[0] == 400.f);
   // pushing a key never pulled creates it with the user init first
   std::vector<uint64_t> k4 = {40};
   std::vector<float> g4 = {0.f, 0.f};

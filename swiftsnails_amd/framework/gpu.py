@@ -82,12 +82,16 @@ class PSContext:
             store = dist.distributed_c10d._get_default_store()
             kind = cfg.get("transport", "rccl")
             if kind == "rccl":
+                from ..parallel.transport import rccl_comms_mode
+
+                three = rccl_comms_mode() == 3
                 tr = RcclTransport(self.rank, self.world, self.device, store=store,
-                                   prefix="ss_data")
-                ct = RcclTransport(self.rank, self.world, self.device, store=store,
-                                   prefix="ss_counts")
-                pt = RcclTransport(self.rank, self.world, self.device, store=store,
-                                   prefix="ss_pull")
+                                   prefix="ss_data", serial=not three)
+                if three:
+                    ct = RcclTransport(self.rank, self.world, self.device, store=store,
+                                       prefix="ss_counts", serial=False)
+                    pt = RcclTransport(self.rank, self.world, self.device, store=store,
+                                       prefix="ss_pull", serial=False)
             else:
                 tr = TorchDistTransport()
         else:
@@ -107,7 +111,7 @@ class PSContext:
         self.engine.tracer = self.tracer  # per-phase ranges: route / pull / compute / push
         # failure detection (parallel/watchdog.py): round watchdog + heartbeats
         self.failure = FailureHandler(exit_process=str(cfg.get("watchdog_exit", "1")) != "0")
-        for t in (tr, ct, pt):
+        for t in [x for x in (tr, ct, pt) if x is not None]:
             if hasattr(t, "abort"):
                 self.failure.add_hook(t.abort)
         rt = float(cfg.get("round_timeout", 600) or 0)

@@ -34,13 +34,6 @@ class PipelinedWorker:
         self._gbase = 0
         self._gper = 1
         self._cap_base = 0
-        # SS_ROUTE_FIRST=1: route round i+2 before pulling round i+1 (below)
-        self._route_first = os.environ.get("SS_ROUTE_FIRST", "0") != "0"
-        # SS_ROUTE_EARLY=1: route round i+2 at the START of step i, before
-        # round i's compute and push are enqueued (experiment, below)
-        self._route_early = (os.environ.get("SS_ROUTE_EARLY", "0") != "0" and
-                             not self._route_first)
-        self._next2 = None
 
     # -- subclass hooks
     # optional ``(dd, slot, stream_ptr)`` hook run on the route stream right
@@ -182,50 +175,25 @@ class PipelinedWorker:
         return self.loss_sum
 
     def _step_pull_ahead(self) -> torch.Tensor:
-        """N>1: round i computes/pushes on the main stream while round i+1 is
-        pulled and round i+2 routed on the route stream (staleness 1)."""
+        """Round i computes/pushes on the main stream while round i+1 is
+        pulled and round i+2 routed on the side streams (staleness 1)."""
         eng = self.engine
         if self._cur is None:  # bootstrap the pipeline
             r = self._next if self._next is not None else self._route(self.step_idx)
             self._cur = eng.pull_ahead_round(r)
             self._next = self._route(self.step_idx + 1)
         rnd = self._cur
-        if self._route_early and self._next2 is None and not getattr(eng, "push_on_pull", False):
-            # the route stream's kernels for round i+2 (its slot was released
-            # by round i+2-depth's push) get dispatched before round i's merge
-            # and apply fill the CUs.  Measured slower (1.103-1.106 ->
-            # 1.118-1.130 ms/step, N>1 path on one GPU with the N>1 route
-            # tuning, three A/B pairs): the earlier dedup competes with round
-            # i's main-stream chain, which is the longer one
-            self._next2 = self._route(self.step_idx + 2)
         eng.begin(rnd)
         self._zero_acc()
         if self.active:
             with eng.trace("compute"):
                 self._compute(rnd, rnd.slot, eng.raw_stream())
-        if getattr(eng, "push_on_pull", False):
-            # push(i) goes on the pull stream behind pull(i+1) (engine.push_on_pull)
-            self._cur = eng.pull_ahead_round(self._next)
-            eng.push(rnd)
-            self._next = self._route(self.step_idx + 2)
-            self.step_idx += 1
-            return self.loss_sum
+        # round i+1's pull is enqueued before round i's push: with one comm
+        # stream (RCCL, SS_RCCL_COMMS=1) its exchanges then go ahead of round
+        # i's gradients instead of waiting behind round i's compute
+        self._cur = eng.pull_ahead_round(self._next)
         eng.push(rnd)
-        if self._route_first:
-            # route round i+2 before the host blocks on round i+1's counts
-            # (pull_ahead_round), so the route stream never idles while the
-            # host waits.  Measured slower (1.18 vs 1.16 ms/step, N>1 path on
-            # one GPU, three A/B pairs): round i+2's dedup then competes with
-            # round i+1's pull, which the next forward waits for
-            nxt = self._route(self.step_idx + 2)
-            self._cur = eng.pull_ahead_round(self._next)
-            self._next = nxt
-        elif self._next2 is not None:
-            self._cur = eng.pull_ahead_round(self._next)
-            self._next, self._next2 = self._next2, None
-        else:
-            self._cur = eng.pull_ahead_round(self._next)
-            self._next = self._route(self.step_idx + 2)
+        self._next = self._route(self.step_idx + 2)
         self.step_idx += 1
         return self.loss_sum
 

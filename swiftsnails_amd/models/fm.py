@@ -14,8 +14,6 @@ other beyond the lockstep collective round.
 """
 from __future__ import annotations
 
-import os
-
 from typing import Optional
 
 import numpy as np
@@ -62,20 +60,10 @@ class FMWorker(PipelinedWorker):
         lanes = 1 << max(0, (F - 1).bit_length())
         self.bucketed = (F <= 64 and lanes >= K and
                          all(getattr(dd, "mode", None) == "bucket" for dd in engine.dedupers))
-        # SS_FM_INV=1: the dedup also writes the inverse index (k_bd_inv, on
-        # the route stream) and the forward reads inv[j] instead of resolving
-        # luid[pos_of[j]] itself (one dependent random load fewer on the main
-        # stream).  Measured slower, 0.536 -> 0.552 ms/step: off
-        self.use_inv = os.environ.get("SS_FM_INV", "0") != "0"
-        # SS_FM_PULL_GATE=1: the next round's pulled-ahead lookup starts after
-        # this round's forward (engine.gate_next_pull), so the forward's
-        # gathers run alone.  Measured slower, 0.537-0.539 -> 0.565-0.573
-        # ms/step (the lookup then crowds the merge and the update): off
-        self.pull_after_fwd = os.environ.get("SS_FM_PULL_GATE", "0") != "0"
         if self.bucketed:
             for dd in engine.dedupers:
                 dd.zero_grad = False
-                dd.materialize_inv = self.use_inv
+                dd.materialize_inv = False  # the forward resolves luid[pos_of[j]] itself
             self.gs = torch.empty(B, dtype=torch.float32, device=dev)
             self.gss = torch.empty(B * K, dtype=torch.float32, device=dev)
             # overflow-bucket list of the sorted reduce (buckets too large to
@@ -91,24 +79,16 @@ class FMWorker(PipelinedWorker):
         d = self.data
         if self.bucketed:
             h, o, dd = hip(), rnd.dd.owner, rnd.dd
-            h.fm_fwd_g(rnd.inv.data_ptr() if self.use_inv else 0, o.index_ptrs(dd.n),
-                       self.labels[slot].data_ptr(),
+            h.fm_fwd_g(0, o.index_ptrs(dd.n), self.labels[slot].data_ptr(),
                        d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                        self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
-            if self.pull_after_fwd:
-                self.engine.gate_next_pull(slot)
-            # SS_FM_FUSE_APPLY=1 (one GPU): the sorted merge runs the optimizer
-            # update itself, one thread per row.  Measured slower (0.62 ->
-            # 1.04 ms/step): a thread's 18 dependent 4-byte accesses to a random
-            # 72-byte row vs k_apply's 4-lane groups, so off by default
-            fa = (self.engine.fuse_apply(rnd, snapshot=False)
-                  if os.environ.get("SS_FM_FUSE_APPLY", "0") == "1"
-                  and os.environ.get("SS_FM_REDUCE", "sorted") != "atomic" else None)
-            h.bd_reduce_fm(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
+            # the sorted per-bucket merge writes each unique row once; the
+            # update is a separate lane-group kernel (k_apply_st): fused into
+            # the merge, one thread per 72-byte row measured 0.62 -> 1.04 ms
+            h.bd_reduce_fm(dd.lay, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                            o.luid.data_ptr(), self.gs.data_ptr(), self.gss.data_ptr(),
                            d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
-                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr(), ndest=o.ndest,
-                           **(fa or {}))
+                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr(), ndest=o.ndest)
             return
         hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),

@@ -17,7 +17,6 @@ labels drawn from a hidden ground-truth sparse LR model so loss goes down.
 """
 from __future__ import annotations
 
-import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -80,72 +79,29 @@ class SparseLRWorker(PipelinedWorker):
                      if getattr(data, "has_values", False) else None)
         # grad_mode "segreduce": duplicate merge without global atomics.  With
         # the bucketed deduper (default) the dedup partition is the reduction
-        # plan: the forward writes per-occurrence g*x coalesced and one
-        # workgroup per bucket sums them in LDS and stores each unique row once
-        # (so the deduper need not zero the gradient rows).  With the hash
-        # deduper the separate bin plan of segreduce.hip is built on the route
-        # stream instead.  "atomic": one float atomicAdd per occurrence.
+        # plan: the forward writes per-sample gradients and one workgroup per
+        # bucket sums g*x over the bucket's occurrences in LDS and stores each
+        # unique row once (so the deduper need not zero the gradient rows).
+        # With the hash deduper the separate bin plan of segreduce.hip is
+        # built on the route stream instead.  "atomic": one float atomicAdd
+        # per occurrence.
         self.grad_mode = grad_mode
         self.bucketed = grad_mode == "segreduce" and all(
             getattr(dd, "mode", None) == "bucket" for dd in engine.dedupers)
         if grad_mode == "segreduce":
             # per-sample gradients (bucketed) or per-occurrence g*x (bin plan)
             self.gocc = torch.empty(B if self.bucketed else n, dtype=torch.float32, device=dev)
-        self.osi = False
-        # SS_LR_INV=1: the route stream materialises inv[j] (k_bd_inv) and the
-        # forward reads it coalesced, instead of resolving uid(j) through the
-        # dedup's bucket index on the main stream.  Measured neutral (forward
-        # 206 -> 123 us, k_bd_inv +109 us on the route stream): off
-        self.use_inv = self.bucketed and os.environ.get("SS_LR_INV", "0") == "1"
-        # SS_DATA_AHEAD=1: generate batch i+2 on a third (data) stream while
-        # the route stream dedups batch i+1, taking the generator off the
-        # route chain (eager steps only; a capture generates in-line).
-        # Measured neutral (0.971 vs 0.975 ms/step): the step is bound by the
-        # memory system both streams share, not by the route chain's order
-        self._data_ahead = os.environ.get("SS_DATA_AHEAD", "0") != "0"
-        self._data_stream = None
-        self._ahead = {}
-        # SS_LR_OCC=1 (bucketed, no materialised inverse): parameters are
-        # filled per dedup bucket into occurrence-position order
-        # (k_bd_fill_occ) and the forward reads one word per occurrence,
-        # occ[pos_of[j]], instead of the dependent gathers luid[pos_of[j]] ->
-        # uvals[ubase + luid]; the scatter then skips the bucket-of-occurrence
-        # array
-        self.use_occ = (self.bucketed and not self.use_inv and
-                        os.environ.get("SS_LR_OCC", "1") != "0")
-        # SS_LR_OCC=sample: the fill writes each parameter at its occurrence's
-        # own position (occ[pj[p]], scattered) and the forward streams occ[j].
-        # Measured slower, 0.858-0.862 -> 0.988 ms/step (three A/B pairs): the
-        # scattered 4-byte stores cost more than the forward's gather saves
-        self.occ_sample = self.use_occ and os.environ.get("SS_LR_OCC", "1") == "sample"
-        self.occ = torch.empty(n, dtype=torch.float32, device=dev) if self.use_occ else None
+        # bucketed: parameters are filled per dedup bucket into
+        # occurrence-position order (k_bd_fill_occ) and the forward reads one
+        # word per occurrence, occ[pos_of[j]], instead of the dependent
+        # gathers luid[pos_of[j]] -> uvals[ubase + luid] (0.941 -> 0.887
+        # ms/step); the scatter then skips the bucket-of-occurrence array
+        self.occ = torch.empty(n, dtype=torch.float32, device=dev) if self.bucketed else None
         if self.bucketed:
             for dd in engine.dedupers:
-                dd.zero_grad = False        # the LDS reduce stores every unique row
-                dd.materialize_inv = self.use_inv  # else the forward resolves uid(j) (BdIndex)
-                # SS_LR_SINGLE=1: the dedup flags keys seen once and the reduce
-                # stores their gradient instead of an LDS atomic add (measured:
-                # reduce 96 -> 90 us, step unchanged — off)
-                if os.environ.get("SS_LR_SINGLE", "0") != "0":
-                    dd.track_singletons()
-            # occurrence-space unique ids (SS_OSI=1, off by default: measured
-            # slower, see PSEngine.enable_osi): the dedup kernel writes inv[j]
-            # itself and the forward reads it coalesced instead of gathering
-            # luid[pos_of[j]]
-            self.osi = engine.enable_osi()
-            if self.osi:
-                self.use_occ, self.occ = False, None
-            for dd in engine.dedupers:
-                dd.need_bkt = not self.use_occ
-                dd.need_pos = not self.occ_sample  # (sample order: nothing reads pos_of)
-            # SS_PULL_FILL=1: the 1-GPU snapshot pull writes occ itself
-            # (k_pull_fill_bk: one workgroup per bucket, weights staged in LDS).
-            # Measured slower (0.94 vs 0.86 ms/step, three A/B pairs): one
-            # workgroup per bucket serialises the probes the default pull
-            # spreads over four
-            if (self.use_occ and not self.occ_sample and
-                    os.environ.get("SS_PULL_FILL", "0") != "0"):
-                engine.occ_buf = self.occ
+                dd.zero_grad = False         # the LDS reduce stores every unique row
+                dd.materialize_inv = False   # the forward resolves occurrences itself
+                dd.need_bkt = False
         elif grad_mode == "segreduce":
             h = hip()
             self.nbins = h.sr_nbins(n)
@@ -169,34 +125,9 @@ class SparseLRWorker(PipelinedWorker):
             return super()._route(step)
         eng = self.engine
         slot = eng._next_slot
-        produce = lambda stream: self._produce(step, slot, stream.cuda_stream)  # noqa: E731
-        if self._data_ahead and eng.gpu and eng.depth >= 3 and eng.capture_tag is None:
-            # the batch of `step` was generated one route earlier on the data
-            # stream (or is generated now if it was not); the batch of step+1
-            # goes on the data stream beside this route, into the next ring
-            # slot, whose last round was released >= 1 step ago
-            ev = self._ahead.pop((step, slot), None)
-            if ev is None:
-                ev = self._produce_ahead(step, slot)
-            self._ahead = {(step + 1, (slot + 1) % eng.depth):
-                           self._produce_ahead(step + 1, (slot + 1) % eng.depth)}
-            produce = lambda stream: (stream.wait_event(ev), self.keys[slot])[1]  # noqa: E731
-        return eng.route(produce=produce,
+        return eng.route(produce=lambda stream: self._produce(step, slot, stream.cuda_stream),
                          post=None if (self.bucketed or self.grad_mode != "segreduce")
                          else self._post)
-
-    def _produce_ahead(self, step, slot):
-        """Generate step's batch into ring slot `slot` on the data stream once
-        the slot's previous round has released it; returns the done event."""
-        eng = self.engine
-        if self._data_stream is None:
-            self._data_stream = torch.cuda.Stream(device=eng.device)
-        ds = self._data_stream
-        eng._wait(ds, eng._free[slot], eng._free_tag[slot])
-        self._produce(step, slot, ds.cuda_stream)
-        ev = torch.cuda.Event()
-        ev.record(ds)
-        return ev
 
     def _produce(self, step, slot, stream):
         if self.xval is not None:
@@ -212,44 +143,26 @@ class SparseLRWorker(PipelinedWorker):
         h = hip()
         dd = rnd.dd
         xp = self.xval[slot].data_ptr() if self.xval is not None else 0
-        if self.grad_mode == "segreduce":
+        if self.bucketed:
             o = dd.owner
-            if self.osi or self.use_inv:
-                h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
-                           d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
-                           self.loss_sum.data_ptr(), 0, st)
-            elif self.use_occ:
-                if not rnd.occ_filled:
-                    o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st, sample_order=self.occ_sample)
-                h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
-                           rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
-                           self.loss_sum.data_ptr(), 0, st,
-                           [] if self.occ_sample else o.index_ptrs(dd.n),
-                           occ=self.occ.data_ptr())
-            elif self.bucketed:
-                h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
-                           rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1,
-                           self.loss_sum.data_ptr(), 0, st, o.index_ptrs(dd.n))
-            else:
-                h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
-                           d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 0,
-                           self.loss_sum.data_ptr(), 0, st)
-            if self.bucketed:
-                # one GPU + osi: gradient rows in occurrence space (apply_bk);
-                # N>1: compact, the alltoallv layout
-                # one GPU: the merge kernel runs the AdaGrad update itself
-                # (engine.fuse_apply: pull snapshot still valid), push() then
-                # only does the bookkeeping
-                fa = self.engine.fuse_apply(rnd) if not self.osi else None
-                h.bd_reduce(dd.n, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
-                            o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
-                            rnd.ugrad.data_ptr(), st, int(self.osi and self.engine.fast1),
-                            o.usingle.data_ptr() if o.usingle is not None else 0,
-                            ndest=o.ndest, **(fa or {}))
-            else:
-                h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
-                            self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,
-                            dd.ucount.data_ptr(), dd.nranks, dd.ucap, rnd.ugrad.data_ptr(), st)
+            o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
+            h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
+                       rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1, self.loss_sum.data_ptr(),
+                       0, st, o.index_ptrs(dd.n), occ=self.occ.data_ptr())
+            # one GPU: the merge kernel runs the AdaGrad update itself
+            # (engine.fuse_apply: pull snapshot still valid), push() then only
+            # does the bookkeeping; N>1: compact rows in the alltoallv layout
+            fa = self.engine.fuse_apply(rnd)
+            h.bd_reduce(dd.lay, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
+                        o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
+                        rnd.ugrad.data_ptr(), st, 0, 0, ndest=o.ndest, **(fa or {}))
+        elif self.grad_mode == "segreduce":
+            h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
+                       d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 0,
+                       self.loss_sum.data_ptr(), 0, st)
+            h.sr_reduce(self.plan[slot].data_ptr(), self.gocc.data_ptr(),
+                        self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), dd.n,
+                        dd.ucount.data_ptr(), dd.nranks, dd.ucap, rnd.ugrad.data_ptr(), st)
         else:
             h.lr_fwd_bwd(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),

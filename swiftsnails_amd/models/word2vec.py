@@ -140,30 +140,18 @@ class Word2VecWorker(PipelinedWorker):
         self._acc = torch.zeros((2, self.loss_sum.numel()), dtype=torch.float32,
                                 device=engine.device)
         self.loss_sum, self.pair_sum = self._acc[0], self._acc[1]
-        # SS_W2V_CTX=reduce: context-row gradients as one scalar per (center,
-        # context) pair, summed per unique context key over the bucketed
-        # dedup's partition (k_w2v_ctx_reduce) instead of a row of float
-        # atomics per pair.  Measured slower (0.32 -> 0.81 ms/step): the sgns
-        # kernel drops 204 -> 105 us, but a Zipf-head context key puts
-        # thousands of row loads into one bucket's workgroup (587 us tail)
-        self.ctx_reduce = (not self.window_mode and
-                           os.environ.get("SS_W2V_CTX", "atomic") == "reduce" and
-                           all(getattr(d, "mode", None) == "bucket" for d in engine.dedupers))
-        self.gpos = (torch.empty(data.batch_size * data.contexts, dtype=torch.float32,
-                                 device=engine.device) if self.ctx_reduce else None)
         # the tile's negative-sample GEMMs on the bf16 MFMA (center / negative
         # rows and score gradients rounded to bf16, fp32 accumulate; positive
         # pairs, parameters and optimizer state stay fp32): 77 KB of LDS
         # instead of 116, two workgroups per CU.  Measured 0.305 -> 0.278-0.282
         # ms/step (1M vocab, dim 128); SS_W2V_MFMA=f32 selects the fp32 tile
-        self.mfma_bf16 = (os.environ.get("SS_W2V_MFMA", "bf16") == "bf16" and not self.ctx_reduce)
-        # window layout, SS_W2V_GRAD=reduce (default with the bucketed dedup):
-        # the tile stores one gradient row per key position and the rows are
-        # summed per unique key (w2v.hip k_w2v_osort on the route stream a
-        # round ahead, k_w2v_oreduce on the main stream) instead of leaving the
-        # tile as float row atomics
+        self.mfma_bf16 = os.environ.get("SS_W2V_MFMA", "bf16") == "bf16"
+        # window layout with the bucketed dedup: the tile stores one gradient
+        # row per key position and the rows are summed per unique key
+        # (w2v.hip k_w2v_osort on the route stream a round ahead,
+        # k_w2v_oreduce on the main stream) instead of float row atomics from
+        # the tile (0.101 -> 0.092 ms/step)
         self.occ_reduce = (self.window_mode and engine.gpu and
-                           os.environ.get("SS_W2V_GRAD", "reduce") == "reduce" and
                            all(getattr(d, "mode", None) == "bucket" for d in engine.dedupers))
         if self.occ_reduce:
             dev, n, D, W = engine.device, data.n_keys, engine.dim, data.window
@@ -211,14 +199,7 @@ class Word2VecWorker(PipelinedWorker):
             return
         h.w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
                    d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
-                   self.loss_sum.data_ptr(), st, self.gpos.data_ptr() if self.ctx_reduce else 0,
-                   int(self.mfma_bf16))
-        if self.ctx_reduce:
-            o = rnd.dd.owner
-            _, bstart, unum, ubase, P = o.bucket_view(rnd.dd.n)
-            h.w2v_ctx_reduce(P, bstart, unum, ubase, o.pj.data_ptr(), o.luid.data_ptr(), ptr,
-                             self.gpos.data_ptr(), B, C, self.engine.dim, rnd.uvals.data_ptr(),
-                             rnd.ugrad.data_ptr(), st)
+                   self.loss_sum.data_ptr(), st, 0, int(self.mfma_bf16))
 
     def samples_per_step(self) -> int:
         """Window layout: centers (words) per step, word2vec's "words/s"

@@ -52,6 +52,7 @@ class DedupResult:
     nranks: int
     n: int
     owner: object = None      # the Deduper (bucket mode: reduce plan lives there)
+    lay: int = 0              # bucket-layout size (>= n; N>1 engines: max_keys)
 
 
 class Deduper:
@@ -78,12 +79,10 @@ class Deduper:
         # bucket mode: False skips writing the contiguous send segment (ukeys)
         # when nothing reads it (the colocated 1-GPU engine pulls per bucket)
         self.need_ukeys = True
-        # bucket mode: occurrence-space unique ids.  ``inv[j]`` is then
-        # bstart[b] + l (unique key l of bucket b), written by the dedup kernel
-        # itself; rows indexed by it live at those positions of an n-row
-        # buffer (pull_buckets/push_buckets with osi, bd_unplace for N>1), and
-        # no BdIndex (pos_of / bkt) is written
-        self.osi = False
+        # bucket mode, N>1 engines: lay the buckets out as a call of lay_n
+        # keys whatever the call's n (every rank the same Pd buckets per
+        # destination: the servers merge bucket k of all sources, server.hip)
+        self.lay_n: Optional[int] = None
         # need_pos=False: no consumer reads the j -> bucket-position map
         # (pos_of), so the scatter skips writing it
         self.need_pos = True
@@ -149,22 +148,20 @@ class Deduper:
         ug = self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0
         if self.mode == "bucket":
             self._last_n = n
-            osi = self.osi
             self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
                             self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
-                            0 if (osi or not self.need_pos) else self.pos_of.data_ptr(),
-                            0 if (osi or not self.need_bkt) else self.bkt.data_ptr(),
+                            self.pos_of.data_ptr() if self.need_pos else 0,
+                            self.bkt.data_ptr() if self.need_bkt else 0,
                             self.luid.data_ptr(),
                             self.bkeys.data_ptr(), self.ucount.data_ptr(),
                             self.ukeys.data_ptr(), ug, self.gdim,
-                            self.inv.data_ptr() if (self.materialize_inv and not osi) else 0,
+                            self.inv.data_ptr() if self.materialize_inv else 0,
                             int(self.need_ukeys or bool(ug)), st,
-                            self.dbg.data_ptr() if self.dbg is not None else 0,
-                            self.inv.data_ptr() if osi else 0,
+                            self.dbg.data_ptr() if self.dbg is not None else 0, 0,
                             self.usingle.data_ptr() if self.usingle is not None else 0,
-                            self.ndest)
+                            self.ndest, self.lay_n or 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
-                               self.nranks, n, self)
+                               self.nranks, n, self, self._lay(n))
         # the scratch is all-EMPTY between calls: the finish kernel resets the
         # slots its winners claimed, so no per-round 0xFF memset is needed
         if self._dirty:
@@ -176,7 +173,23 @@ class Deduper:
                            self.ukeys.data_ptr(), ug, self.gdim,
                            self.blk_cnt.data_ptr(), self.inv.data_ptr(), st)
         return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
-                           self.nranks, n, self)
+                           self.nranks, n, self, n)
+
+    def _lay(self, n: int) -> int:
+        """Layout size of a call of n keys (what every bucket-layout helper
+        takes instead of n)."""
+        return max(int(self.lay_n or 0), int(n))
+
+    def run_tables(self, Pd: int):
+        """(ubase, unum) of the LAST call as int32 views of [nranks * Pd]:
+        destination d's bucket runs at [d*Pd, (d+1)*Pd) — what a source
+        sends each server with its keys (N>1, server.hip)."""
+        if self.mode != "bucket":
+            raise RuntimeError("run_tables needs mode='bucket'")
+        P, _, o_un, o_ub = self.h.bd_offsets(self._lay(self._last_n), self.nranks, self.ndest)
+        if P != Pd * self.nranks:
+            raise RuntimeError(f"run_tables: {P} buckets, expected {Pd} x {self.nranks}")
+        return self.scratch[o_ub:o_ub + P], self.scratch[o_un:o_un + P]
 
     def track_singletons(self) -> None:
         """Have the dedup flag the unique keys that occur once (bucket mode)."""
@@ -185,49 +198,37 @@ class Deduper:
                                        device=self.device)
 
     def reduce(self, n: int, gs: torch.Tensor, F: int, ugrad: torch.Tensor,
-                xval: Optional[torch.Tensor] = None, stream=None, osi: bool = False):
+               xval: Optional[torch.Tensor] = None, stream=None):
         """K7 for scalar rows, for the LAST call's partition (bucket mode):
         ugrad[uid] = sum over occurrences j of uid of gs[j // F] * xval[j]
-        (per-sample gradient times feature value; no zero-fill needed).
-        ``osi``: rows at occurrence-space ids, else at the compact ids."""
+        (per-sample gradient times feature value; no zero-fill needed)."""
         if self.mode != "bucket" or self.gdim != 1:
             raise RuntimeError("Deduper.reduce needs mode='bucket' and gdim=1")
-        self.h.bd_reduce(n, self.nranks, self.scratch.data_ptr(), self.pj.data_ptr(),
+        self.h.bd_reduce(self._lay(n), self.nranks, self.scratch.data_ptr(), self.pj.data_ptr(),
                          self.luid.data_ptr(), gs.data_ptr(),
                          xval.data_ptr() if xval is not None else 0, F, ugrad.data_ptr(),
-                         _stream_ptr(stream), int(osi),
+                         _stream_ptr(stream), 0,
                          self.usingle.data_ptr() if self.usingle is not None else 0,
                          ndest=self.ndest)
 
-    def fill_occ(self, n: int, uvals: torch.Tensor, occ: torch.Tensor, stream=None,
-                 osi: bool = False, sample_order: bool = False):
+    def fill_occ(self, n: int, uvals: torch.Tensor, occ: torch.Tensor, stream=None):
         """Scalar rows of the LAST call by occurrence position:
         ``occ[p] = uvals[uid]`` of the occurrence at bucket position p (0
-        where it has none), so a consumer reads ``occ[pos_of[j]]``; with
-        ``sample_order`` at the occurrence's own position, ``occ[j]``."""
+        where it has none), so a consumer reads ``occ[pos_of[j]]``."""
         if self.mode != "bucket":
             raise RuntimeError("fill_occ needs mode='bucket'")
-        self.h.bd_fill_occ(n, self.nranks, self.scratch.data_ptr(), self.luid.data_ptr(),
-                           uvals.data_ptr(), occ.data_ptr(), int(osi), _stream_ptr(stream),
-                           self.ndest, self.pj.data_ptr() if sample_order else 0)
-
-    def unplace(self, n: int, src: torch.Tensor, dst: torch.Tensor, stream=None):
-        """Rows of the LAST call from compact unique ids (``src``, the
-        alltoallv layout) to occurrence-space ids (``dst``, n rows)."""
-        if self.mode != "bucket":
-            raise RuntimeError("unplace needs mode='bucket'")
-        self.h.bd_unplace(n, self.nranks, self.scratch.data_ptr(), src.data_ptr(),
-                          dst.data_ptr(), src.shape[-1] if src.dim() > 1 else 1,
-                          _stream_ptr(stream), self.ndest)
+        self.h.bd_fill_occ(self._lay(n), self.nranks, self.scratch.data_ptr(),
+                           self.luid.data_ptr(), uvals.data_ptr(), occ.data_ptr(), 0,
+                           _stream_ptr(stream), self.ndest, 0)
 
     def index_ptrs(self, n: Optional[int] = None):
         """(pos_of, luid, bkt, ubase) device pointers of the last call: the
         kernels' BdIndex, uid(j) = ubase[bkt[j]] + luid[pos_of[j]]."""
-        if self.mode != "bucket" or self.osi:
-            raise RuntimeError("index_ptrs needs mode='bucket' without osi")
+        if self.mode != "bucket":
+            raise RuntimeError("index_ptrs needs mode='bucket'")
         n = self._last_n if n is None else n
-        ub = self.scratch.data_ptr() + 4 * self.h.bd_ubase_offset(max(1, n), self.nranks,
-                                                                  self.ndest)
+        ub = self.scratch.data_ptr() + 4 * self.h.bd_ubase_offset(max(1, self._lay(n)),
+                                                                  self.nranks, self.ndest)
         return [self.pos_of.data_ptr(), self.luid.data_ptr(), self.bkt.data_ptr(), ub]
 
     def bucket_view(self, n: Optional[int] = None):
@@ -237,7 +238,7 @@ class Deduper:
         if self.mode != "bucket":
             raise RuntimeError("bucket_view needs mode='bucket'")
         n = self._last_n if n is None else n
-        P, o_bs, o_un, o_ub = self.h.bd_offsets(max(1, n), self.nranks, self.ndest)
+        P, o_bs, o_un, o_ub = self.h.bd_offsets(max(1, self._lay(n)), self.nranks, self.ndest)
         b0 = self.scratch.data_ptr()
         return (self.bkeys.data_ptr(), b0 + 4 * o_bs, b0 + 4 * o_un, b0 + 4 * o_ub, P)
 
@@ -288,7 +289,8 @@ class CpuDeduper:
         ug = (torch.zeros((self.nranks * self.ucap, self.gdim), dtype=torch.float32)
               if self.with_grad else None)
         return DedupResult(torch.from_numpy(uk.view(np.int64)), torch.from_numpy(uc),
-                           torch.from_numpy(inv.astype(np.int32)), ug, self.ucap, self.nranks, n)
+                           torch.from_numpy(inv.astype(np.int32)), ug, self.ucap, self.nranks, n,
+                           None, n)
 
 
 def dedup_reference(keys, nranks: int = 1, frag_map: Optional[np.ndarray] = None,

@@ -20,6 +20,7 @@ from __future__ import annotations
 import contextlib
 import os
 import sys
+import threading
 from abc import ABC, abstractmethod
 from typing import Optional, Sequence
 
@@ -35,15 +36,8 @@ class CountsHandle:
                  event=None, pinned: Optional[torch.Tensor] = None, world: int = 1):
         self._s, self._r, self.event, self.pinned, self.world = s, r, event, pinned, world
 
-    # SS_COUNTS_SPIN=1: poll the event instead of a blocking synchronize (the
-    # host's wake-up is on the N>1 critical cycle: route -> counts -> pull)
-    _spin = os.environ.get("SS_COUNTS_SPIN", "0") != "0"
-
     def wait(self) -> tuple[np.ndarray, np.ndarray]:
         if self._s is None:
-            if self._spin:
-                while not self.event.query():
-                    pass
             self.event.synchronize()
             p = self.pinned.numpy()
             self._s, self._r = p[:self.world].copy(), p[self.world:2 * self.world].copy()
@@ -53,6 +47,7 @@ class CountsHandle:
 class Transport(ABC):
     rank: int = 0
     world: int = 1
+    label: str = "?"   # what actually carries the data (bench.py reports it)
 
     @abstractmethod
     def exchange_counts(self, send_counts: torch.Tensor) -> tuple[np.ndarray, np.ndarray]:
@@ -84,6 +79,8 @@ class Transport(ABC):
 
 
 class LoopbackTransport(Transport):
+    label = "loopback (world 1: device copies, no collective)"
+
     def __init__(self):
         self.rank, self.world = 0, 1
 
@@ -124,6 +121,8 @@ class TorchDistTransport(Transport):
         self.rank = dist.get_rank(group)
         self.world = dist.get_world_size(group)
         self.backend = dist.get_backend(group)
+        self.label = (f"torch.distributed {self.backend} all_to_all_single"
+                      + (" (host-staged)" if self.backend == "gloo" else ""))
 
     def _dev(self, t: torch.Tensor):
         return t if self.backend != "gloo" else t.cpu()
@@ -177,33 +176,58 @@ def default_gloo_ifname() -> None:
         os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
 
 
+_fd_lock = threading.Lock()
+_fd_depth = 0
+_fd_saved = -1
+
+
 @contextlib.contextmanager
 def _stdout_to_stderr():
     """Point fd 1 at fd 2 for the duration (native code writing to stdout).
     C stdio buffers are flushed before fd 1 is restored, so buffered native
-    output lands on stderr too."""
+    output lands on stderr too.  Reference-counted under a lock: nested or
+    concurrent users (in-process ranks building communicators on threads)
+    share one redirect, and only the outermost restores fd 1."""
     import ctypes
 
+    global _fd_depth, _fd_saved
     libc = ctypes.CDLL(None)
-    sys.stdout.flush()
-    saved = os.dup(1)
+    with _fd_lock:
+        if _fd_depth == 0:
+            sys.stdout.flush()
+            _fd_saved = os.dup(1)
+            os.dup2(2, 1)
+        _fd_depth += 1
     try:
-        os.dup2(2, 1)
         yield
     finally:
-        libc.fflush(None)
-        sys.stdout.flush()
-        os.dup2(saved, 1)
-        os.close(saved)
+        with _fd_lock:
+            _fd_depth -= 1
+            if _fd_depth == 0:
+                libc.fflush(None)
+                sys.stdout.flush()
+                os.dup2(_fd_saved, 1)
+                os.close(_fd_saved)
+                _fd_saved = -1
 
 
 class RcclTransport(Transport):
-    """Native RCCL communicator on a dedicated (or the current) HIP stream."""
+    """Native RCCL communicator over xGMI.
+
+    ``serial`` (SS_RCCL_COMMS=1, the default): every collective of this
+    communicator is enqueued on ONE dedicated comm stream, in host program
+    order — the caller's stream is joined to it before and after — so the
+    engine's route, pull and main streams can never have two operations of
+    the communicator in flight at once, and every rank issues the same
+    sequence on the same stream (no cross-rank ordering hazards).  With
+    SS_RCCL_COMMS=3 the engine uses three communicators, each on the stream
+    that calls it (more overlap; RCCL then relies on every rank enqueuing
+    them in the same order)."""
 
     _DT = {torch.float32: 0, torch.float64: 1, torch.int32: 2, torch.int64: 3}
 
     def __init__(self, rank: int, world: int, device: torch.device, store=None,
-                 uid: Optional[bytes] = None, prefix: str = "ss_rccl"):
+                 uid: Optional[bytes] = None, prefix: str = "ss_rccl", serial: bool = True):
         from .._native import hip
 
         h = hip()
@@ -223,8 +247,14 @@ class RcclTransport(Transport):
         # line)
         with _stdout_to_stderr():
             self.comm = h.RcclComm(rank, world, uid, self.device.index or 0)
+        self.serial = bool(serial)
+        self.stream = torch.cuda.Stream(device=self.device) if self.serial else None
+        self.label = f"RCCL grouped send/recv ({'1 comm stream' if self.serial else 'caller streams'})"
         self._pin = torch.empty(2 * world, dtype=torch.int64, pin_memory=True)
-        self._cnt_recv = torch.empty(world, dtype=torch.int64, device=self.device)
+
+    def nranks(self) -> int:
+        """Ranks of the communicator as RCCL reports them (ncclCommCount)."""
+        return int(self.comm.comm_count())
 
     @staticmethod
     def new_unique_id() -> bytes:
@@ -234,9 +264,18 @@ class RcclTransport(Transport):
         with _stdout_to_stderr():
             return hip().RcclComm.unique_id()
 
-    @staticmethod
-    def _st():
-        return torch.cuda.current_stream().cuda_stream
+    @contextlib.contextmanager
+    def _on(self, caller=None):
+        """The stream a collective goes on: the comm stream (serial), joined
+        to the caller's stream on both sides, or the caller's stream."""
+        cs = caller or torch.cuda.current_stream(self.device)
+        if not self.serial:
+            yield cs
+            return
+        self.stream.wait_stream(cs)
+        with torch.cuda.stream(self.stream):
+            yield self.stream
+        cs.wait_stream(self.stream)
 
     def abort(self) -> None:
         """ncclCommAbort: stuck collectives return; the communicator is dead
@@ -247,12 +286,11 @@ class RcclTransport(Transport):
         return self.exchange_counts_async(send_counts).wait()
 
     def exchange_counts_async(self, send_counts, pinned=None, stream=None):
-        """Counts all-to-all + D2H into pinned memory on `stream`; the host
-        only blocks in ``wait()`` (on an event), so the exchange overlaps with
-        whatever the other streams are running."""
-        st = stream or torch.cuda.current_stream()
+        """Counts all-to-all + D2H into pinned memory; the host only blocks
+        in ``wait()`` (on an event), so the exchange overlaps with whatever
+        the other streams are running."""
         pin = pinned if pinned is not None else self._pin
-        with torch.cuda.stream(st):
+        with self._on(stream) as st:
             s = send_counts.to(torch.int64).contiguous()
             recv = torch.empty(self.world, dtype=torch.int64, device=self.device)
             self.comm.alltoall(s.data_ptr(), recv.data_ptr(), 1, 8, st.cuda_stream)
@@ -264,22 +302,35 @@ class RcclTransport(Transport):
 
     def alltoallv(self, send, scounts, sdispls, recv, rcounts, rdispls, row_elems=1):
         eb = send.element_size() * row_elems
-        self.comm.alltoallv(send.data_ptr(), [int(x) for x in scounts],
-                            [int(x) for x in sdispls], recv.data_ptr(),
-                            [int(x) for x in rcounts], [int(x) for x in rdispls], eb, self._st())
+        with self._on() as st:
+            self.comm.alltoallv(send.data_ptr(), [int(x) for x in scounts],
+                                [int(x) for x in sdispls], recv.data_ptr(),
+                                [int(x) for x in rcounts], [int(x) for x in rdispls], eb,
+                                st.cuda_stream, send.numel() // row_elems,
+                                recv.numel() // row_elems)
 
     def allreduce_(self, t, op="sum"):
-        self.comm.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._DT[t.dtype],
-                            {"sum": 0, "max": 1, "min": 2}[op], self._st())
+        with self._on() as st:
+            self.comm.allreduce(t.data_ptr(), t.data_ptr(), t.numel(), self._DT[t.dtype],
+                                {"sum": 0, "max": 1, "min": 2}[op], st.cuda_stream)
         return t
 
     def barrier(self):
         x = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.allreduce_(x)
-        torch.cuda.current_stream().synchronize()
+        torch.cuda.current_stream(self.device).synchronize()
 
     def close(self):
         self.comm = None
+
+
+def rccl_comms_mode() -> int:
+    """SS_RCCL_COMMS: 1 (default) = one communicator on one comm stream; 3 =
+    data / count / pull communicators on the engine's three streams."""
+    v = os.environ.get("SS_RCCL_COMMS", "1")
+    if v not in ("1", "3"):
+        raise ValueError(f"SS_RCCL_COMMS={v!r}: 1 or 3")
+    return int(v)
 
 
 def make_transport(kind: str = "auto", device=None, store=None) -> Transport:

@@ -47,12 +47,6 @@ KNOBS: dict[str, Knob] = {
                             "1.018 ms/step for 3, four A/B pairs)"),
     "SS_PULL_AHEAD": Knob("1", "parallel/engine.py", "tuning",
                           "N>1 (and FM / word2vec at N=1): pull round i+1 while round i computes"),
-    "SS_PULL_SNAPSHOT": Knob("1", "parallel/engine.py", "tuning",
-                             "1 GPU, scalar AdaGrad: the pull snapshots (w, h) for a blind-store "
-                             "update (1.126 -> 1.085 ms/step)"),
-    "SS_FUSE_APPLY": Knob("1", "parallel/engine.py", "tuning",
-                          "1 GPU LR: AdaGrad update fused into the gradient merge "
-                          "(1.090 -> 0.985 ms/step)"),
     "SS_DEDUP": Knob("bucket", "ops/dedup.py", "tuning",
                      "bucket: LDS dedup per hash bucket; hash: global scratch table"),
     "SS_TABLE_G": Knob("auto", "ops/table.py", "tuning", "lanes per table row"),
@@ -92,41 +86,24 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
-    "SS_LR_OCC": Knob("1", "models/sparse_lr.py", "tuning",
-                      "LR forward reads occ[pos_of[j]] filled per dedup bucket (one gather "
-                      "per occurrence instead of two dependent ones); sample: the fill "
-                      "scatters occ[j] and the forward streams it (0.86 -> 0.99 ms/step)"),
     "SS_LR_FWD": Knob("auto", "csrc/hip/segreduce.hip", "tuning",
                       "LR forward layout: packed | group (auto by lane utilisation)"),
     "SS_FM_REDUCE": Knob("sorted", "csrc/hip/bdedup.hip, models/fm.py", "tuning",
                          "FM gradient merge: sorted lists, or atomic (LDS float atomics)"),
     "SS_W2V_MFMA": Knob("bf16", "models/word2vec.py", "tuning",
                         "word2vec tile: bf16 MFMA (77 KB LDS) or f32 (116 KB)"),
+    "SS_RCCL_COMMS": Knob("1", "parallel/transport.py, bench.py", "ops",
+                          "N>1 over RCCL: 1 = one communicator, every collective on one comm "
+                          "stream in program order (conservative); 3 = data / count / pull "
+                          "communicators on the engine's three streams"),
     # -- experiments (measured slower or neutral; kept for re-measurement)
     "SS_ENGINE_GENERAL": Knob("0", "parallel/engine.py, bench.py", "experiment",
                               "run a 1-GPU job through the N>1 path (1: loopback, rccl: size-1 "
                               "RCCL communicators)"),
-    "SS_OSI": Knob("0", "parallel/engine.py", "experiment",
-                   "occurrence-space unique ids (forward 192 -> 123 us, dedup 217 -> 350 us)"),
-    "SS_LR_SINGLE": Knob("0", "models/sparse_lr.py", "experiment",
-                         "store instead of add for keys seen once (reduce -6 us, step unchanged)"),
-    "SS_LR_INV": Knob("0", "models/sparse_lr.py", "experiment",
-                      "materialised inverse on the route stream (neutral)"),
-    "SS_FM_PULL_GATE": Knob("0", "models/fm.py", "experiment",
-                            "the next round's pulled-ahead lookup waits for this round's "
-                            "forward (0.537 -> 0.565 ms/step)"),
-    "SS_FM_INV": Knob("0", "models/fm.py", "experiment",
-                      "FM forward reads a materialised inverse index (k_bd_inv on the route "
-                      "stream) instead of resolving luid[pos_of[j]] (0.536 -> 0.552 ms/step)"),
-    "SS_FM_FUSE_APPLY": Knob("0", "models/fm.py", "experiment",
-                             "FM update fused into the sorted merge (0.62 -> 1.04 ms/step)"),
     "SS_FM_NC": Knob("auto", "csrc/hip/bdedup.hip", "experiment",
                      "FM atomic merge: factor columns per LDS pass"),
     "SS_FM_SPLIT": Knob("0", "csrc/hip/bdedup.hip", "experiment",
                         "FM atomic merge: column groups on separate workgroups"),
-    "SS_W2V_CTX": Knob("atomic", "models/word2vec.py", "experiment",
-                       "reduce: context gradients merged per key over the dedup buckets "
-                       "(0.32 -> 0.81 ms/step)"),
     "SS_STALENESS": Knob("1", "parallel/engine.py", "ops",
                          "pull-ahead bound: a round's pull waits until the push of the round "
                          "k+1 before it is applied (k = 1: staleness 1); ring: bounded by the "
@@ -145,40 +122,12 @@ KNOBS: dict[str, Knob] = {
                           "1024: the window tile with 16 waves instead of 8 (standalone 29.6 -> "
                           "23.1 us, but the step 0.083 -> 0.093 ms: the workgroup's registers "
                           "fill its CU's SIMDs and nothing runs beside it)"),
-    "SS_W2V_GRAD": Knob("reduce", "models/word2vec.py", "experiment",
-                        "window layout: tile gradients as occurrence rows summed per unique "
-                        "key (reduce) or as float row atomics from the tile (atomic)"),
     "SS_W2V_WIN_GMODE": Knob("0", "csrc/hip/w2v.hip", "debug",
                              "measurement only (wrong results): windowed word2vec tile's "
                              "gradient rows as 1 = plain stores, 2 = not written"),
-    "SS_COUNTS_SPIN": Knob("0", "parallel/transport.py", "experiment",
-                           "N>1: busy-poll the count exchange's event instead of a blocking "
-                           "synchronize (neutral on one GPU: 1.034-1.040 vs 1.036-1.054)"),
-    "SS_PUSH_STREAM": Knob("main", "parallel/engine.py", "experiment",
-                           "pull: N>1 gradient exchange + server apply on the pull stream "
-                           "behind the next round's pull (1.049-1.053 -> 1.058-1.103 ms/step: "
-                           "the route stream's dedup, sharing the chip, stays the chain)"),
     "SS_W2V_POS": Knob("fused", "csrc/hip/w2v.hip", "experiment",
                        "split: positive pairs in their own one-wave-per-center kernel "
                        "(0.307 -> 0.344 ms/step: atomic-rate bound, not occupancy bound)"),
-    "SS_ROUTE_CUS": Knob("0 (all)", "parallel/engine.py", "experiment",
-                         "route stream on a CU-masked stream of k CUs (measured 0.97 -> "
-                         "1.17-1.20 ms/step for k = 64..192 of 256)"),
-    "SS_DATA_AHEAD": Knob("0", "models/sparse_lr.py", "experiment",
-                          "generate batch i+2 on a third stream beside the route of i+1 "
-                          "(neutral: 0.971 vs 0.975 ms/step, three A/B pairs)"),
-    "SS_ROUTE_PRIORITY": Knob("0", "parallel/engine.py", "experiment",
-                              "high-priority route stream (no gain)"),
-    "SS_ROUTE_FIRST": Knob("0", "models/base.py", "experiment",
-                           "pull-ahead step: route round i+2 before waiting for round i+1's "
-                           "counts (1.18 vs 1.16 ms/step, N>1 path on one GPU)"),
-    "SS_ROUTE_EARLY": Knob("0", "models/base.py", "experiment",
-                           "pull-ahead step: route round i+2 at the start of step i, before "
-                           "round i's merge and apply are enqueued (1.103-1.106 -> 1.118-1.130 "
-                           "ms/step, N>1 path on one GPU, three A/B pairs)"),
-    "SS_PULL_FILL": Knob("0", "models/sparse_lr.py", "experiment",
-                         "1 GPU LR: the snapshot pull writes the occurrence parameters itself "
-                         "(k_pull_fill_bk; 0.86 -> 0.94 ms/step)"),
     "SS_GRAPH_STEPS": Knob("4 x depth", "models/base.py", "tuning",
                            "steps per hipGraph: 1, or a multiple of the ring depth (word2vec "
                            "4 / 8 / 16 / 32: 0.093 / 0.088 / 0.086 / 0.084 ms/step)"),

@@ -20,6 +20,7 @@ from typing import Optional
 
 import torch
 
+
 _roctx = None
 
 
@@ -88,13 +89,33 @@ class Tracer:
 
 
 class Metrics:
+    """Per-rank counters.  ``add`` takes host numbers; ``add_device`` takes
+    a device scalar tensor (a count a kernel wrote) and accumulates it on the
+    device, so the hot path never syncs — ``counters`` folds those in when
+    read (one sync)."""
+
     def __init__(self):
         self.t0 = time.perf_counter()
-        self.counters = defaultdict(float)
+        self._host = defaultdict(float)
+        self._dev: dict = {}
 
     def add(self, **kw):
         for k, v in kw.items():
-            self.counters[k] += v
+            self._host[k] += v
+
+    def add_device(self, **kw):
+        for k, v in kw.items():
+            acc = self._dev.get(k)
+            if acc is None:
+                acc = self._dev[k] = torch.zeros(1, dtype=torch.float64, device=v.device)
+            acc.add_(v.reshape(-1)[:1].to(torch.float64))
+
+    @property
+    def counters(self) -> dict:
+        out = defaultdict(float, self._host)
+        for k, acc in self._dev.items():
+            out[k] += float(acc.item())
+        return out
 
     def rates(self) -> dict:
         el = max(1e-9, time.perf_counter() - self.t0)

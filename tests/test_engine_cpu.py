@@ -1,6 +1,7 @@
 """Collective round engine on CPU: world 1 + multi-process gloo (world 2/3,
 colocated and split server/worker roles), checked against a single-table
-oracle that applies each round's merged gradients source-rank by source-rank.
+oracle that merges each round's gradients over ALL workers per key and
+applies one update per distinct key (the servers' cross-source merge).
 """
 
 import numpy as np
@@ -36,13 +37,14 @@ def _oracle(world, workers, opt_kind):
         for r in workers:
             k = _keys_for(r, rnd)
             pulled[(r, rnd)] = t.pull_keys(k).numpy()
-        for r in workers:  # rank order == engine's per-source apply order
-            k = _keys_for(r, rnd)
-            g = _grads_for(k, r, rnd)
-            u, inv = np.unique(k, return_inverse=True)
-            m = np.zeros((len(u), DIM), np.float32)
-            np.add.at(m, inv, g)
-            t.push_keys(u, m)
+        # one merged gradient per distinct key over every worker's push
+        ks = [_keys_for(r, rnd) for r in workers]
+        gs = [_grads_for(k, r, rnd) for k, r in zip(ks, workers)]
+        k = np.concatenate(ks)
+        u, inv = np.unique(k, return_inverse=True)
+        m = np.zeros((len(u), DIM), np.float64)
+        np.add.at(m, inv, np.concatenate(gs).astype(np.float64))
+        t.push_keys(u, m.astype(np.float32))
         t.next_round()
     return t.to_dict(with_state=True), pulled
 

@@ -341,72 +341,6 @@ def test_bucket_reduce_lr_matches_atomic_path(dev, nranks, singles):
     np.testing.assert_allclose(l_b.sum().item(), l_at.sum().item(), rtol=1e-5)
 
 
-@pytest.mark.parametrize("nranks", [1, 3])
-def test_bucket_dedup_occurrence_space_ids(dev, nranks):
-    """osi mode: the dedup kernel's own inverse indexes the staged unique keys
-    (bkeys[inv[j]] == keys[j]); unplace maps compact rows onto those ids; the
-    LDS reduce in occurrence space equals per-occurrence atomics."""
-    from swiftsnails_amd._native import hip
-    from swiftsnails_amd.ops.dedup import INVALID, Deduper
-    from swiftsnails_amd.parallel.router import HashFrag
-
-    h = hip()
-    B, F = 20000, 13
-    n = B * F
-    rng = np.random.default_rng(11 + nranks)
-    keys = (rng.zipf(1.3, n) % 300000).astype(np.int64)
-    keys[::97] = -1  # EMPTY: never reaches a bucket, inverse must be INVALID
-    fm = HashFrag(nranks, 64).rank_map()
-    d = Deduper(n, nranks=nranks, frag_map=torch.from_numpy(fm.astype(np.int32)), gdim=1,
-                device=dev, mode="bucket", zero_grad=False)
-    d.osi = True
-    d.inv.fill_(123)  # every entry must be rewritten
-    r = d(torch.from_numpy(keys).to(dev))
-    torch.cuda.synchronize()
-    d.check()
-    inv = r.inv.cpu().numpy().view(np.uint32).astype(np.int64)
-    bk = d.bkeys.cpu().numpy()
-    bad = keys == -1
-    assert (inv[bad] == INVALID).all()
-    ok = ~bad
-    np.testing.assert_array_equal(bk[inv[ok]], keys[ok])
-    # one id per distinct key
-    ids = {}
-    for k, i in zip(keys[ok][:50000].tolist(), inv[ok][:50000].tolist()):
-        assert ids.setdefault(k, i) == i
-    assert len(set(ids.values())) == len(ids)
-    assert int(r.ucount.sum()) == len(np.unique(keys[ok]))
-    # unplace: compact unique id ubase[b]+l -> occurrence-space id bstart[b]+l
-    P, o_bs, o_un, o_ub = h.bd_offsets(n, nranks, d.ndest)
-    sc = d.scratch.cpu().numpy().view(np.uint32).astype(np.int64)
-    bstart, unum, ubase = sc[o_bs:o_bs + P + 1], sc[o_un:o_un + P], sc[o_ub:o_ub + P]
-    U = nranks * d.ucap
-    src = torch.randn(U, device=dev)
-    dst = torch.full((n,), float("nan"), device=dev)
-    d.unplace(n, src, dst)
-    torch.cuda.synchronize()
-    s_np, d_np = src.cpu().numpy(), dst.cpu().numpy()
-    for b in range(0, P, 7):
-        np.testing.assert_array_equal(d_np[bstart[b]:bstart[b] + unum[b]],
-                                      s_np[ubase[b]:ubase[b] + unum[b]])
-    # reduce in occurrence space == per-occurrence atomics through the osi inverse
-    st = torch.cuda.current_stream().cuda_stream
-    uvals = torch.randn(n, device=dev) * 0.1
-    y = torch.from_numpy((rng.random(B) < 0.3).astype(np.float32)).to(dev)
-    g_at = torch.zeros(n, device=dev)
-    h.lr_fwd_bwd(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), g_at.data_ptr(),
-                 0, 0, st)
-    gs = torch.empty(B, device=dev)
-    h.lr_fwd_g(r.inv.data_ptr(), 0, y.data_ptr(), B, F, uvals.data_ptr(), gs.data_ptr(), 1,
-               0, 0, st)
-    g_b = torch.full((n,), float("nan"), device=dev)
-    d.reduce(n, gs, F, g_b, osi=True)
-    torch.cuda.synchronize()
-    live = np.concatenate([np.arange(bstart[b], bstart[b] + unum[b]) for b in range(P)])
-    np.testing.assert_allclose(g_b.cpu().numpy()[live], g_at.cpu().numpy()[live], rtol=1e-4,
-                               atol=1e-4)
-
-
 @pytest.mark.parametrize("F", [39, 7, 64, 100])  # lane-group layout (<=64) and LDS fallback
 def test_lr_fwd_bwd_matches_torch(dev, F):
     from swiftsnails_amd._native import hip
@@ -619,61 +553,36 @@ def test_probe_histogram_and_stats(dev):
     assert 0 <= st["probe_mean"] < 5
 
 
-def test_sparse_lr_osi_matches_compact_ids(dev, monkeypatch):
-    """The LR worker with occurrence-space ids (default) trains the same
-    model as with compact ids + BdIndex (SS_OSI=0), step for step."""
+@pytest.mark.parametrize("prefill", ["1", "0"])
+def test_sparse_lr_dist_path_matches_fast_path(dev, monkeypatch, prefill):
+    """One GPU through the N>1 engine path (SS_ENGINE_GENERAL=1: send
+    segments, bucket runs, the server's merge of received keys, the server's
+    snapshot pull and fused blind-store AdaGrad) trains the same model as the
+    1-GPU fast path (pull snapshot + AdaGrad fused into the worker's merge),
+    step for step, up to the float summation order."""
     from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
     from swiftsnails_amd.ops.optim import Optimizer
     from swiftsnails_amd.parallel.engine import PSEngine
 
+    monkeypatch.setenv("SS_TABLE_PREFILL", prefill)
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")  # the fast path's LR schedule (no staleness)
     out = {}
-    for osi in ("1", "0"):
-        monkeypatch.setenv("SS_OSI", osi)
+    for general in ("0", "1"):
+        monkeypatch.setenv("SS_ENGINE_GENERAL", general)
         data = CtrSynth(batch_size=4096, num_fields=13, num_features=300_000, tail_frac=0.2)
         table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
         eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
+        assert eng.fast1 == (general == "0")
         w = SparseLRWorker(eng, data)
-        assert w.osi == (osi == "1")
         losses = [float(w.step().sum().item()) for _ in range(12)]
         torch.cuda.synchronize()
-        table.check()
-        out[osi] = (losses, table.to_dict(with_state=True))
+        eng.check()
+        if general == "1":
+            assert eng.srv[0].snap_valid  # blind store from the server's snapshot
+            m = eng.metrics.counters
+            assert 0 < m["server_unique"] == m["unique_recv"]  # one source: no cross merges
+        out[general] = (losses, table.to_dict(with_state=True))
     (l1, t1), (l0, t0) = out["1"], out["0"]
-    np.testing.assert_allclose(l1, l0, rtol=1e-4)
-    assert t1.keys() == t0.keys()
-    ks = list(t1.keys())[:20000]
-    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
-                               rtol=1e-4, atol=1e-6)
-
-
-@pytest.mark.parametrize("env", [{"SS_PULL_FILL": "1"}, {"SS_LR_OCC": "0"}])
-def test_sparse_lr_occurrence_paths_agree(dev, monkeypatch, env):
-    """The LR forward's parameter paths train the same model: separate fill
-    kernel (default), pull fused with the occurrence fill (SS_PULL_FILL=1),
-    dependent gathers through the dedup index (SS_LR_OCC=0)."""
-    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
-    from swiftsnails_amd.ops.optim import Optimizer
-    from swiftsnails_amd.parallel.engine import PSEngine
-
-    out = {}
-    for name, e in (("default", {}), ("alt", env)):
-        for k in ("SS_PULL_FILL", "SS_LR_OCC"):
-            monkeypatch.delenv(k, raising=False)
-        for k, v in e.items():
-            monkeypatch.setenv(k, v)
-        data = CtrSynth(batch_size=4096, num_fields=13, num_features=300_000, tail_frac=0.2)
-        table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
-        eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
-        w = SparseLRWorker(eng, data)
-        if name == "default":
-            assert w.use_occ and eng.occ_buf is None
-        elif "SS_PULL_FILL" in e:
-            assert w.use_occ and eng.occ_buf is not None
-        losses = [float(w.step().sum().item()) for _ in range(12)]
-        torch.cuda.synchronize()
-        table.check()
-        out[name] = (losses, table.to_dict(with_state=True))
-    (l1, t1), (l0, t0) = out["default"], out["alt"]
     np.testing.assert_allclose(l1, l0, rtol=1e-4)
     assert t1.keys() == t0.keys()
     ks = list(t1.keys())[:20000]
@@ -712,41 +621,6 @@ def test_zero_init_prefilled_rows(dev, monkeypatch, prefill):
     np.testing.assert_allclose(row[:3], -0.5 / np.sqrt(1.1), rtol=1e-4)
 
 
-@pytest.mark.parametrize("prefill", ["1", "0"])
-def test_sparse_lr_pull_snapshot_matches_row_reads(dev, monkeypatch, prefill):
-    """Blind-write apply from the pull's (w, h) snapshot trains like the
-    read-modify-write apply (SS_PULL_SNAPSHOT=0), up to the float summation
-    order of the gradient merge (LDS atomics)."""
-    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
-    from swiftsnails_amd.ops.optim import Optimizer
-    from swiftsnails_amd.parallel.engine import PSEngine
-
-    monkeypatch.setenv("SS_TABLE_PREFILL", prefill)
-    out = {}
-    # (snapshot, fused merge+apply): default, snapshot with separate k_apply,
-    # plain read-modify-write apply
-    for snap, fuse in (("1", "1"), ("1", "0"), ("0", "1")):
-        monkeypatch.setenv("SS_PULL_SNAPSHOT", snap)
-        monkeypatch.setenv("SS_FUSE_APPLY", fuse)
-        data = CtrSynth(batch_size=4096, num_fields=13, num_features=300_000, tail_frac=0.2)
-        table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
-        eng = PSEngine(table, None, max_keys=4096 * 13, dim=1, device=dev)
-        assert eng.snapshot == (snap == "1")
-        w = SparseLRWorker(eng, data)
-        losses = [float(w.step().sum().item()) for _ in range(12)]
-        torch.cuda.synchronize()
-        table.check()
-        out[snap + fuse] = (losses, table.to_dict(with_state=True))
-    l0, t0 = out["01"]
-    ks = list(t0.keys())
-    for cfg in ("11", "10"):
-        l1, t1 = out[cfg]
-        np.testing.assert_allclose(l1, l0, rtol=1e-5)
-        assert t1.keys() == t0.keys()
-        np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
-                                   rtol=1e-4, atol=1e-6)
-
-
 def test_engine_snapshot_invalidated_by_interleaved_push(dev, monkeypatch):
     """pull A, pull B, push A, push B over overlapping keys: B's snapshot is
     stale after A's push, so B must re-read its rows (no lost update)."""
@@ -758,11 +632,11 @@ def test_engine_snapshot_invalidated_by_interleaved_push(dev, monkeypatch):
     kb = torch.arange(1501, 4501, dtype=torch.int64, device=dev)
     res = {}
     for snap in ("1", "0"):
-        monkeypatch.setenv("SS_PULL_SNAPSHOT", snap)
         t = HbmTable(1, 1 << 16, optimizer=Optimizer("adagrad", lr=0.5),
                      init=InitConfig("uniform", 0.1, 0.1, seed=3), device=dev)
         assert t.snapshot_ok
         eng = PSEngine(t, None, max_keys=4096, dim=1, device=dev)
+        eng.snapshot = snap == "1"  # "0": every apply reads its rows
         ra = eng.pull(ka)
         rb = eng.pull(kb)
         assert (ra.snap is not None) == (snap == "1")
@@ -877,3 +751,98 @@ def test_stream_helpers_match_torch(dev):
     assert torch.cuda.current_stream(dev) == base
     s.synchronize()
     assert float(x.sum().item()) == 2000.0
+
+
+@pytest.mark.parametrize("dim", [1, 3])
+def test_server_merge_matches_reference(dev, dim):
+    """server.hip on the keys three sources route to one server (real
+    bucketed dedups with the common N>1 layout, overlapping key sets): one
+    entry per distinct key, response rows per received position, and the
+    merged gradient of every distinct key — fused into the AdaGrad update for
+    scalar rows (read-modify-write, no snapshot), a merged row otherwise."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.ops.dedup import Deduper
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.router import HashFrag
+
+    h = hip()
+    N, me, n = 3, 1, 30000
+    fm = torch.from_numpy(HashFrag(N, 64).rank_map().astype(np.int32))
+    rng = np.random.default_rng(17)
+    pool = rng.choice(1 << 40, 40000, replace=False).astype(np.int64) + 1
+    ds = [Deduper(n, nranks=N, frag_map=fm, gdim=dim, device=dev) for _ in range(N)]
+    for d in ds:
+        d.lay_n = n
+    Pd = h.bd_buckets(n, N, ds[0].ndest) // N
+    m = h.srv_sub_buckets(N)
+    cap = n
+    rkeys = torch.full((N * cap,), -1, dtype=torch.int64, device=dev)
+    meta = torch.zeros(2 * N * Pd, dtype=torch.int32, device=dev)
+    recv = []
+    for s, d in enumerate(ds):
+        keys = torch.from_numpy(rng.choice(pool, n)).to(dev)  # duplicates within + across
+        r = d(keys)
+        c = int(r.ucount[me])
+        rkeys[s * cap:s * cap + c] = r.ukeys[me * cap:me * cap + c]
+        ub, un = d.run_tables(Pd)
+        meta[s * Pd:(s + 1) * Pd] = ub[me * Pd:(me + 1) * Pd]
+        meta[N * Pd + s * Pd:N * Pd + (s + 1) * Pd] = un[me * Pd:(me + 1) * Pd]
+        recv.append((s * cap, c))
+    P = Pd * m
+    rows = N * cap
+    i32 = dict(dtype=torch.int32, device=dev)
+    cnt, bstart = torch.empty(P, **i32), torch.empty(P + 1, **i32)
+    ubase, unum = torch.empty(P, **i32), torch.empty(P, **i32)
+    pj, luid = torch.empty(rows, **i32), torch.empty(rows, **i32)
+    bkeys = torch.empty(rows, dtype=torch.int64, device=dev)
+    uc = torch.zeros(1, dtype=torch.int64, device=dev)
+    err = torch.zeros(1, **i32)
+    st = torch.cuda.current_stream().cuda_stream
+    h.srv_dedup(rkeys.data_ptr(), meta.data_ptr(), meta.data_ptr() + 4 * N * Pd, cap, N, Pd, m,
+                me, cnt.data_ptr(), bstart.data_ptr(), pj.data_ptr(), luid.data_ptr(),
+                bkeys.data_ptr(), ubase.data_ptr(), unum.data_ptr(), uc.data_ptr(),
+                err.data_ptr(), st)
+    pos = np.concatenate([np.arange(a, a + c) for a, c in recv])
+    rk = rkeys.cpu().numpy()[pos]
+    distinct = np.unique(rk)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert int(uc.item()) == len(distinct) < len(pos)  # the sources overlap
+    assert int(bstart[P].item()) == len(pos)
+    t = HbmTable(dim, 1 << 18, optimizer=Optimizer("adagrad", lr=0.3),
+                 init=InitConfig("uniform", 0.2, 0.1, seed=5), device=dev)
+    svals = torch.empty((rows, dim), device=dev)
+    sslots = torch.empty(rows, dtype=torch.int64, device=dev)
+    t.pull_buckets((bkeys.data_ptr(), bstart.data_ptr(), unum.data_ptr(), ubase.data_ptr(), P),
+                   svals, sslots)
+    rvals = torch.full((rows, dim), float("nan"), device=dev)
+    h.srv_fill(P, bstart.data_ptr(), ubase.data_ptr(), unum.data_ptr(), pj.data_ptr(),
+               luid.data_ptr(), svals.data_ptr(), rvals.data_ptr(), dim, st)
+    torch.cuda.synchronize()
+    assert t.size() == len(distinct)
+    before = t.to_dict(with_state=True)
+    np.testing.assert_array_equal(rvals.cpu().numpy()[pos],
+                                  np.stack([before[int(k)][:dim] for k in rk]))
+    g = torch.randn((rows, dim), device=dev)
+    gn = g.cpu().numpy()
+    if dim == 1:
+        h.srv_merge(P, bstart.data_ptr(), ubase.data_ptr(), unum.data_ptr(), pj.data_ptr(),
+                    luid.data_ptr(), g.data_ptr(), 0, 1, t.dt, sslots.data_ptr(), 0,
+                    t.opt.native(), st)
+    else:
+        merged = torch.empty((rows, dim), device=dev)
+        h.srv_merge(P, bstart.data_ptr(), ubase.data_ptr(), unum.data_ptr(), pj.data_ptr(),
+                    luid.data_ptr(), g.data_ptr(), merged.data_ptr(), dim, st=st)
+        t.push_slots(sslots, merged, segs=t.dev_segs(uc), max_n=rows)
+    torch.cuda.synchronize()
+    after = t.to_dict(with_state=True)
+    acc = {}
+    for k, p in zip(rk.tolist(), pos.tolist()):
+        acc[k] = acc.get(k, 0.0) + gn[p].astype(np.float64)
+    for k in list(acc)[:3000]:
+        w0, h0 = before[k][:dim].astype(np.float64), before[k][dim:].astype(np.float64)
+        h1 = h0 + acc[k] ** 2
+        w1 = w0 - 0.3 * acc[k] / np.sqrt(h1 + 1e-8)
+        np.testing.assert_allclose(after[k][dim:], h1, rtol=2e-4, atol=1e-5)
+        np.testing.assert_allclose(after[k][:dim], w1, rtol=2e-4, atol=1e-5)

@@ -501,19 +501,22 @@ def test_word2vec_window_grad_reduce_matches_atomics(dev, monkeypatch, D, B, W):
     np.testing.assert_allclose(b, a, rtol=5e-2, atol=2e-2)
 
 
+@pytest.mark.parametrize("comms", [1, 3])
 @pytest.mark.parametrize("model", ["lr", "fm", "w2v"])
-def test_general_path_rccl_world1_matches_loopback(dev, model, monkeypatch):
+def test_general_path_rccl_world1_matches_loopback(dev, model, comms, monkeypatch):
     """The N>1 engine path (send segments, count exchange with pinned D2H,
-    server pull over received segments, per-source apply) on one GPU through
-    three real size-1 RCCL communicators trains exactly like the same path
-    over loopback transports: the multi-GPU RCCL call sequence, minus peers."""
+    bucket runs, the server's merge of received keys and merged update) on
+    one GPU through real size-1 RCCL communicators — one on its comm stream
+    (SS_RCCL_COMMS=1) or three on the engine's streams (3) — trains exactly
+    like the same path over loopback transports: the multi-GPU RCCL call
+    sequence, minus peers."""
     monkeypatch.setenv("SS_ENGINE_GENERAL", "1")
     monkeypatch.setenv("SS_PULL_AHEAD", "0")
     n = 12
     wa, ta = _graph_worker(model, dev)
     assert not wa.engine.fast1
     la = [float(wa.step().sum().item()) for _ in range(n)]
-    wb, tb = _graph_worker(model, dev, **_rccl1(dev))
+    wb, tb = _graph_worker(model, dev, **_rccl1(dev, comms))
     lb = [float(wb.step().sum().item()) for _ in range(n)]
     torch.cuda.synchronize()
     ta.check()
@@ -522,21 +525,28 @@ def test_general_path_rccl_world1_matches_loopback(dev, model, monkeypatch):
     assert ta.size() == tb.size()
 
 
-def _rccl1(dev):
+def _rccl1(dev, comms=1):
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.parallel.transport import RcclTransport
 
-    t, c, p = (RcclTransport(0, 1, dev, uid=hip().RcclComm.unique_id()) for _ in range(3))
+    if comms == 1:
+        t = RcclTransport(0, 1, dev, uid=hip().RcclComm.unique_id())
+        assert t.nranks() == 1
+        return {"transport": t}
+    t, c, p = (RcclTransport(0, 1, dev, uid=hip().RcclComm.unique_id(), serial=False)
+               for _ in range(3))
     return {"transport": t, "count_transport": c, "pull_transport": p}
 
 
+@pytest.mark.parametrize("comms", [1, 3])
 @pytest.mark.parametrize("model", ["lr", "fm", "w2v"])
-def test_general_path_rccl_world1_pull_ahead_trains(dev, model, monkeypatch):
+def test_general_path_rccl_world1_pull_ahead_trains(dev, model, comms, monkeypatch):
     """The production N>1 pipeline — pull-ahead of round i+1 on a third
-    stream with its own RCCL communicator while round i computes — on one
-    GPU through size-1 RCCL communicators: trains and keeps the table sane."""
+    stream while round i computes, the server's update a read-modify-write —
+    on one GPU through size-1 RCCL communicators: trains and keeps the table
+    sane."""
     monkeypatch.setenv("SS_ENGINE_GENERAL", "1")
-    w, t = _graph_worker(model, dev, **_rccl1(dev))
+    w, t = _graph_worker(model, dev, **_rccl1(dev, comms))
     assert w.engine.pull_ahead and w.engine.pull_stream is not None
     losses = [float(w.step().sum().item()) for _ in range(40)]
     torch.cuda.synchronize()
