@@ -53,8 +53,11 @@ def main(argv=None):
     ap.add_argument("--grad-mode", default="segreduce", choices=["segreduce", "atomic"])
     ap.add_argument("--dedup", default=None, choices=["bucket", "hash"],
                     help="batch dedup implementation (default: bucket)")
-    ap.add_argument("--transport", default="rccl", choices=["rccl", "gloo"],
-                    help="N>1 data plane; gloo is a host-staged rehearsal transport (tests)")
+    ap.add_argument("--transport", default="auto", choices=["auto", "xgmi", "rccl", "gloo"],
+                    help="N>1 data plane: xgmi (peer stores into IPC-mapped HBM mailboxes, "
+                         "device-side counts), rccl, or auto = xgmi, falling back to rccl if "
+                         "its start-up self-test fails; gloo is a host-staged rehearsal "
+                         "transport (tests)")
     # hipGraph replays: neutral at the default batch (GPU-bound), 74 -> 54
     # us/step at batch 1024 where host launch work bounds the step
     ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
@@ -95,6 +98,13 @@ def main(argv=None):
                 from swiftsnails_amd.parallel.transport import TorchDistTransport
 
                 transport = TorchDistTransport()
+            elif a.transport in ("auto", "xgmi"):
+                # the mailbox arena is laid out (and self-tested) when the
+                # engine is built, below
+                from swiftsnails_amd.parallel.transport import TorchDistTransport
+                from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+                transport = XgmiTransport(rank, world, dev, store, aux=TorchDistTransport())
             elif rccl_comms_mode() == 1:
                 # one native RCCL communicator, every collective on its comm
                 # stream in program order (the conservative default)
@@ -126,13 +136,27 @@ def main(argv=None):
             # communicator: the multi-GPU call sequence, minus the peers
             transport = RcclTransport(0, 1, dev, uid=RcclTransport.new_unique_id())
             comms = 1
+        elif general == "xgmi":
+            # ... or through a size-1 mailbox arena (puts to itself, waits)
+            from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+            transport = XgmiTransport(0, 1, dev, None)
 
     data = CtrSynth(batch_size=a.batch, num_fields=a.fields, num_features=a.features,
                     tail_frac=a.tail)
     opt = Optimizer(a.optimizer, lr=a.lr)
     table = make_lr_table(a.features, world, optimizer=opt, load=a.load, device=dev)
-    engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev,
-                      count_transport=ctrans, pull_transport=ptrans)
+    try:
+        engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev,
+                          count_transport=ctrans, pull_transport=ptrans)
+    except RuntimeError as e:
+        if not (world > 1 and a.transport == "auto" and "xgmi" in str(e)):
+            raise
+        # every rank failed the mailbox self-test together: RCCL instead
+        print(f"bench.py: {e}; falling back to RCCL", file=sys.stderr)
+        transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
+        comms = 1
+        engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev)
     worker = SparseLRWorker(engine, data, rank=rank, world=world, grad_mode=a.grad_mode)
 
     # a wedged collective ends the job (exit 3) instead of hanging the node

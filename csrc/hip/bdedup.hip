@@ -961,7 +961,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount, osi_inv, dbg,
                      place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, skeys);
   check_launch("k_bd_dedup");
-  if (inv) {
+  if (inv && n > 0) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");
     BdIndex ix{pos_of, luid, bkt, S + L.ubase};
     hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, n, inv);
@@ -1105,30 +1105,11 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
     check_launch("k_bd_reduce_fm_sorted");
     return;
   }
-  // SS_FM_NC: factor columns accumulated per pass (default: all that fit in
-  // LDS; 4 -> 80 KB, two workgroups per CU) — experiment knob
-  static const int nc = [] {
-    const char* e = std::getenv("SS_FM_NC");
-    return e ? std::atoi(e) : 0;
-  }();
-  static const bool split = [] {
-    const char* e = std::getenv("SS_FM_SPLIT");
-    return e && std::atoi(e) != 0;
-  }();
   switch (dim) {
 #define SS_BDFM_CASE(DD)                                                                       \
   case DD:                                                                                     \
-    if (nc == 4)                                                                               \
-      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 4>), dim3(L.P, split ? (DD + 2) / 4 : 1),        \
-                         dim3(1024), 0, st, S + L.bstart,                                      \
-                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, nullptr);   \
-    else if (nc == 2)                                                                          \
-      hipLaunchKernelGGL((k_bd_reduce_fm<DD, 2>), dim3(L.P, split ? DD / 2 : 1), dim3(1024), 0, \
-                         st, S + L.bstart,                                                     \
-                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, nullptr);   \
-    else                                                                                       \
-      hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,        \
-                         S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, nullptr);   \
+    hipLaunchKernelGGL(k_bd_reduce_fm<DD>, dim3(L.P), dim3(1024), 0, st, S + L.bstart,        \
+                       S + L.ubase, S + L.unum, pj, luid, gs, gss, F, uvals, ugrad, nullptr);   \
     break;
     SS_BDFM_CASE(2)
     SS_BDFM_CASE(5)

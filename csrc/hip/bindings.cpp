@@ -54,7 +54,10 @@ static BdIndex make_bdindex(const std::vector<uintptr_t>& v) {
                  P<const uint32_t>(v[3])};
 }
 
+void bind_xgmi(py::module_& m);  // xgmi.hip
+
 PYBIND11_MODULE(_ss_hip, m) {
+  bind_xgmi(m);
   m.doc() = "SwiftSnails-AMD gfx950 kernels + RCCL communicator";
 
   py::class_<DevTable>(m, "DevTable", py::module_local())

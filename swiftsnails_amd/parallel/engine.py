@@ -170,7 +170,18 @@ class PSEngine:
         frag_num = frag_num or max(1024, 8 * len(self.server_ranks))
         self.router = HashFrag(len(self.server_ranks), frag_num)
         self.frag_map = self.router.rank_map(self.server_ranks)
-        self.max_keys = int(max_keys)
+        # SS_ENGINE_GENERAL=1 (or rccl) runs a 1-GPU job through the N>1 code
+        # path: the per-rank cost of the multi-GPU pipeline without the network
+        self.fast1 = (self.gpu and self.world == 1 and
+                      os.environ.get("SS_ENGINE_GENERAL", "0") == "0")
+        self.dist = not self.fast1
+        # the xGMI mailbox transport (device-side counts) or a host-count one
+        from .xgmi import XgmiTransport
+
+        self.xg = self.t if isinstance(self.t, XgmiTransport) else None
+        # N>1 on GPU: segment strides a multiple of 64 rows (aligned peer stores)
+        self.max_keys = int(max_keys) if not (self.gpu and self.dist) else \
+            -(-int(max_keys) // 64) * 64
         # ring depth 4 by default: with one batch of lookahead, routing round
         # i+1 reuses the buffers of round i-3 (long pushed) instead of waiting
         # on round i-1's push; 4 measured 1.008 vs 1.018 ms/step for 3 (LR,
@@ -189,11 +200,6 @@ class PSEngine:
         # distinct keys the servers merged them into, alltoallv payload bytes
         self.metrics = Metrics()
         self.tracer = Tracer(enabled=False)
-        # SS_ENGINE_GENERAL=1 (or rccl) runs a 1-GPU job through the N>1 code
-        # path: the per-rank cost of the multi-GPU pipeline without the network
-        self.fast1 = (self.gpu and self.world == 1 and
-                      os.environ.get("SS_ENGINE_GENERAL", "0") == "0")
-        self.dist = not self.fast1
         fm = torch.from_numpy(self.frag_map.astype(np.int32))
         dd_cls = Deduper if self.gpu else CpuDeduper
         self.dedupers = [dd_cls(self.max_keys, nranks=self.world, frag_map=fm, gdim=self.dim,
@@ -274,12 +280,28 @@ class PSEngine:
             raise ValueError("PSEngine: max_keys differs across ranks (the N>1 bucket layout "
                              "is a function of it)")
         rows = N * cap
-        self.rkeys = torch.empty(rows, dtype=torch.int64, device=dev)
         self.rvals = torch.zeros((rows, d), dtype=torch.float32, device=dev)
-        self.rgrads = torch.empty((rows, d), dtype=torch.float32, device=dev)
-        # per slot: the received bucket runs ([N][Pd] bases, then sizes)
-        self.rmeta = [torch.zeros(2 * N * self.Pd, dtype=torch.int32, device=dev)
-                      for _ in range(self.depth)]
+        if self.xg:
+            # the receive buffers are the arena's mailboxes: keys + the bucket
+            # runs (bases, sizes) per source, rows back, gradients
+            Pd = self.Pd
+            self.xg.setup({"keys": (self.depth, [cap * 8, Pd * 4, Pd * 4]),
+                           "vals": (self.depth, [cap * 4 * d]),
+                           "grads": (self.depth, [cap * 4 * d])})
+            self.rkeys = [self.xg.region("keys", 0, q, torch.int64) for q in range(self.depth)]
+            self.rmeta = [(self.xg.region("keys", 1, q, torch.int32),
+                           self.xg.region("keys", 2, q, torch.int32)) for q in range(self.depth)]
+            self.uvals = [self.xg.region("vals", 0, q, torch.float32, d)
+                          for q in range(self.depth)]
+            self.rgrads = [self.xg.region("grads", 0, q, torch.float32, d)
+                           for q in range(self.depth)]
+        else:
+            self.rkeys = [torch.empty(rows, dtype=torch.int64, device=dev)] * self.depth
+            # per slot: the received bucket runs ([N][Pd] bases, then sizes)
+            meta = [torch.zeros(2 * N * self.Pd, dtype=torch.int32, device=dev)
+                    for _ in range(self.depth)]
+            self.rmeta = [(m[:N * self.Pd], m[N * self.Pd:]) for m in meta]
+            self.rgrads = [torch.empty((rows, d), dtype=torch.float32, device=dev)] * self.depth
         self.srv = None
         if self.table is not None:
             self.svals = torch.empty((rows, d), dtype=torch.float32, device=dev)
@@ -366,16 +388,22 @@ class PSEngine:
                 post(dd, slot, rs.cuda_stream)
             counts = None
             if self.dist:
-                counts = self.ct.exchange_counts_async(dd.ucount, pinned=self._pins[slot],
-                                                       stream=rs)
-                # the per-bucket runs of every destination's segment (fixed
-                # size: Pd bases + Pd sizes per peer)
+                # the keys with the per-bucket runs of every destination's
+                # segment (fixed size: Pd bases + Pd sizes per peer)
                 ub, un = dd.owner.run_tables(self.Pd)
-                m, Pd, N = self.rmeta[slot], self.Pd, self.world
-                fixed = [Pd] * N
+                Pd, N = self.Pd, self.world
                 dsp = [r * Pd for r in range(N)]
-                self.ct.alltoallv(ub, fixed, dsp, m[:N * Pd], fixed, dsp, 1)
-                self.ct.alltoallv(un, fixed, dsp, m[N * Pd:], fixed, dsp, 1)
+                if self.xg:
+                    self.xg.put("keys", slot, [(dd.ukeys, self.displs, dd.ucount, None),
+                                               (ub, dsp, None, Pd), (un, dsp, None, Pd)],
+                                stream=rs)
+                else:
+                    counts = self.ct.exchange_counts_async(dd.ucount, pinned=self._pins[slot],
+                                                           stream=rs)
+                    mb, mn = self.rmeta[slot]
+                    fixed = [Pd] * N
+                    self.ct.alltoallv(ub, fixed, dsp, mb, fixed, dsp, 1)
+                    self.ct.alltoallv(un, fixed, dsp, mn, fixed, dsp, 1)
             ev = self._ev_route[slot]
             ev.record(rs)
         return Routed(dd, slot, counts, ev, self.capture_tag)
@@ -389,8 +417,8 @@ class PSEngine:
             return
         h, S, N = _hip(), self.srv[slot], self.world
         st = stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
-        m = self.rmeta[slot]
-        h.srv_dedup(self.rkeys.data_ptr(), m.data_ptr(), m.data_ptr() + 4 * N * self.Pd,
+        mb, mn = self.rmeta[slot]
+        h.srv_dedup(self.rkeys[slot].data_ptr(), mb.data_ptr(), mn.data_ptr(),
                     self.max_keys, N, self.Pd, self.sub, self.rank, S.cnt.data_ptr(),
                     S.bstart.data_ptr(), S.pj.data_ptr(), S.luid.data_ptr(), S.bkeys.data_ptr(),
                     S.ubase.data_ptr(), S.unum.data_ptr(), S.ucount.data_ptr(),
@@ -418,12 +446,32 @@ class PSEngine:
         self.metrics.add(server_unique=int(uk.numel()))
         return (idx, uk, inv)
 
+    def _pull_xgmi(self, r: Routed, stream) -> Round:
+        """Keys in (put by every source at route time), server merge +
+        lookup, rows back over the mailboxes; nothing leaves the device."""
+        dd, slot, xg = r.dd, r.slot, self.xg
+        nb = 4 * self.Pd
+        xg.wait("keys", slot, stream, fixed_parts=[(1, nb), (2, nb)])
+        self._server_pull_gpu(slot, stream)
+        rc = xg.counts("keys", 0, slot)
+        xg.put("vals", slot, [(self.rvals, self.displs, rc, None, self.dim)], stream=stream)
+        xg.wait("vals", slot, stream)
+        with use_stream(stream):
+            sent, recv = dd.ucount.sum(), rc.sum()
+            self.metrics.add_device(unique_sent=sent, unique_recv=recv,
+                                    a2a_bytes=(8 + 8 * self.dim) * (sent + recv))
+        self.metrics.add(occurrences=dd.n)
+        return Round(dd, self.uvals[slot], slot)
+
     def _pull_exchange(self, r: Routed, uv: torch.Tensor, tr: Transport, stream):
         """Keys out, server merge + lookup, rows back (N>1; host counts)."""
+        if self.xg and self.gpu:
+            return self._pull_xgmi(r, stream)
         dd, slot = r.dd, r.slot
         scounts, rcounts = r.counts.wait()
         D = self.displs
-        tr.alltoallv(dd.ukeys, scounts, D, self.rkeys, rcounts, D, 1)
+        tr.alltoallv(dd.ukeys, scounts, D, self.rkeys[slot] if self.gpu else self.rkeys,
+                     rcounts, D, 1)
         server = None
         if self.gpu:
             self._server_pull_gpu(slot, stream)
@@ -535,7 +583,7 @@ class PSEngine:
             return
         h, S, st = _hip(), self.srv[slot], _stream()
         args = (self.Ps, S.bstart.data_ptr(), S.ubase.data_ptr(), S.unum.data_ptr(),
-                S.pj.data_ptr(), S.luid.data_ptr(), self.rgrads.data_ptr())
+                S.pj.data_ptr(), S.luid.data_ptr(), self.rgrads[slot].data_ptr())
         fused = (self.dim == 1 and tab.push_fn is None and tab.opt.kind == "adagrad" and
                  tab.width == 2 and tab.G == 1)
         if fused:
@@ -611,7 +659,14 @@ class PSEngine:
             tab.next_round()
         else:
             D = self.displs
-            self.t.alltoallv(g, rnd.scounts, D, self.rgrads, rnd.rcounts, D, self.dim)
+            if self.xg and self.gpu:
+                self.xg.put("grads", rnd.slot, [(g, D, rnd.dd.ucount, None, self.dim)],
+                            stream=self.main_stream())
+                self.xg.wait("grads", rnd.slot, self.main_stream())
+            else:
+                self.t.alltoallv(g, rnd.scounts, D,
+                                 self.rgrads[rnd.slot] if self.gpu else self.rgrads,
+                                 rnd.rcounts, D, self.dim)
             if self.gpu:
                 self._server_push_gpu(rnd.slot)
             else:
@@ -717,3 +772,5 @@ class PSEngine:
         chk = getattr(self.table, "check", None) if self.table is not None else None
         if chk is not None:
             chk()
+        if self.xg is not None:
+            self.xg.check()  # a peer that never arrived / a corrupt count

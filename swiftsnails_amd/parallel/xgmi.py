@@ -1,0 +1,223 @@
+"""xGMI peer-mailbox transport: the N>1 data plane with device-side counts.
+
+``RcclTransport`` moves a round's segments with grouped ncclSend/ncclRecv,
+which need the byte counts on the host — one D2H + host wait per round, and
+no hipGraph capture of an N>1 step.  This transport (``csrc/hip/xgmi.hip``)
+gives every rank an uncached HBM arena exported through an IPC handle and
+mapped by every peer: a ``put`` kernel stores this rank's segment for each
+peer straight into that peer's arena over xGMI, with the row count read from
+device memory and written into the receiver's header, then bumps a
+per-(channel, source) arrival counter there; a ``wait`` kernel on the
+consumer's stream spins until all sources have arrived.  The receiver's
+buffers ARE the arena: the server kernels read received keys and gradients
+in place, the worker reads pulled rows in place.
+
+The same code runs with every rank on ONE GPU (the IPC mappings are then the
+same device's memory), which is how the peer data path is exercised on a
+1-GPU box (tests/test_gpu_multiproc.py).  ``setup`` ends with a self-test —
+every rank puts a rank-stamped pattern to every peer and checks what
+arrived — so a fabric that cannot map or order peer stores fails at start-up
+(bench.py then falls back to RCCL), never mid-training.
+
+Control-plane collectives (barrier, the start-up agreement) go through
+``aux`` (a gloo ``TorchDistTransport``).  Reference parity:
+/root/reference/src/core/transfer/transfer.h:75-150 (send / receive loop).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+
+from .transport import Transport
+
+_ALIGN = 256
+_DT = {torch.int64: (0, 64), torch.int32: (0, 32), torch.float32: (2, 32)}
+
+
+def _al(x: int) -> int:
+    return (int(x) + _ALIGN - 1) // _ALIGN * _ALIGN
+
+
+class XgmiTransport(Transport):
+    label = "xGMI peer stores into IPC-mapped HBM mailboxes (device-side counts)"
+
+    def __init__(self, rank: int, world: int, device, store, aux: Optional[Transport] = None,
+                 prefix: str = "ss_xgmi", timeout_s: Optional[float] = None):
+        self.rank, self.world = int(rank), int(world)
+        self.device = torch.device(device)
+        self.store, self.prefix = store, prefix
+        self.aux = aux
+        self.timeout_s = float(timeout_s if timeout_s is not None else
+                               os.environ.get("SS_XGMI_TIMEOUT", "120"))
+        self.arena = None
+        self._ch: dict[str, int] = {}
+        self._layout: dict = {}
+        # blocks per peer of a put: enough to keep 7 links busy, not so many
+        # that small segments pay a launch tail
+        self.bpp = int(os.environ.get("SS_XGMI_BPP", "32"))
+
+    # ------------------------------------------------------------ set-up
+    def setup(self, channels: dict) -> None:
+        """Lay out and map the arena.  ``channels``: name -> (slots, parts),
+        parts a list of per-source segment sizes in bytes.  Collective: every
+        rank calls it with the same channels, in the same order."""
+        from .._native import hip
+
+        h = hip()
+        chans = dict(channels)
+        chans["_probe"] = (1, [4096])
+        off = h.xgmi_flag_bytes()
+        for name, (slots, parts) in chans.items():
+            if len(self._ch) >= 16:
+                raise ValueError("xgmi: at most 16 channels")
+            self._ch[name] = len(self._ch)
+            for slot in range(int(slots)):
+                for p, seg in enumerate(parts):
+                    # segments keep their exact size (source s at s * seg: the
+                    # consumers index [source][row]); regions start aligned
+                    hdr = _al(off)
+                    data = _al(hdr + 8 * self.world)
+                    self._layout[(name, p, slot)] = (hdr, data, int(seg))
+                    off = data + self.world * int(seg)
+        self.bytes = _al(off)
+        dev = self.device.index or 0
+        # a rank that cannot map its peers still takes part in the agreement
+        # of the self-test, so every rank raises together (and a caller can
+        # fall back to RCCL on all ranks)
+        err = None
+        try:
+            self.arena = h.XgmiArena(self.rank, self.world, dev, self.bytes)
+            handles = self._allgather_bytes(bytes(self.arena.ipc_handle()))
+            self.arena.open_peers(handles)
+            self._err = torch.utils.dlpack.from_dlpack(
+                h.dlpack_view(self.arena.err_ptr, [2], 0, 32, dev))
+        except Exception as e:  # pragma: no cover - hardware dependent
+            err = e
+            self._allgather_bytes(b"")  # the peers are waiting for a handle
+        self._selftest(err)
+
+    def _allgather_bytes(self, mine: bytes) -> list:
+        if self.world == 1:
+            return [mine]
+        self.store.set(f"{self.prefix}_h{self.rank}", mine)
+        out = []
+        for r in range(self.world):
+            k = f"{self.prefix}_h{r}"
+            self.store.wait([k])
+            out.append(bytes(self.store.get(k)))
+        return out
+
+    def _selftest(self, err: Optional[Exception] = None) -> None:
+        """Every rank puts (rank, peer)-stamped words to every peer; each
+        checks what arrived, and all ranks agree before the transport is
+        used (a failure raises on every rank)."""
+        N, me = self.world, self.rank
+        if err is not None:
+            flag = torch.zeros(1, dtype=torch.int64)
+            if self.aux is not None and N > 1:
+                self.aux.allreduce_(flag, "min")
+            raise RuntimeError(f"xgmi set-up failed on this rank: {err}")
+        src = torch.empty((N, 1024), dtype=torch.int32, device=self.device)
+        for d in range(N):
+            src[d] = me * 1000003 + d * 7919 + torch.arange(1024, dtype=torch.int32,
+                                                            device=self.device)
+        st = torch.cuda.current_stream(self.device)
+        self.put("_probe", 0, [(src, [d * 1024 for d in range(N)], None, 1024)], stream=st)
+        self.wait("_probe", 0, stream=st)
+        got = self.region("_probe", 0, 0, torch.int32).view(N, -1)[:, :1024].clone()
+        cnt = self.counts("_probe", 0, 0).clone()
+        st.synchronize()
+        exp = torch.stack([s * 1000003 + me * 7919 + torch.arange(1024, dtype=torch.int32)
+                           for s in range(N)])
+        ok = bool(torch.equal(got.cpu(), exp)) and bool((cnt.cpu() == 1024).all()) and \
+            int(self._err[0].item()) == 0
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        if self.aux is not None and N > 1:
+            self.aux.allreduce_(flag, "min")
+        if int(flag.item()) != 1:
+            raise RuntimeError(f"xgmi self-test failed on {'this rank' if not ok else 'a peer'}")
+
+    # ------------------------------------------------------------ data plane
+    def region(self, ch: str, part: int, slot: int, dtype=torch.float32,
+               cols: int = 1) -> torch.Tensor:
+        """The receive area of (channel, part, slot) as a tensor: source s's
+        segment at rows [s * seg_rows, ...)."""
+        from .._native import hip
+
+        hdr, data, seg = self._layout[(ch, part, slot)]
+        code, bits = _DT[dtype]
+        rows = self.world * seg // (bits // 8 * cols)
+        shape = [rows, cols] if cols > 1 else [rows]
+        return torch.utils.dlpack.from_dlpack(
+            hip().dlpack_view(self.arena.base + data, shape, code, bits,
+                              self.device.index or 0))
+
+    def counts(self, ch: str, part: int, slot: int) -> torch.Tensor:
+        """int64 [world]: rows each source put into (channel, part, slot)."""
+        from .._native import hip
+
+        hdr, _, _ = self._layout[(ch, part, slot)]
+        return torch.utils.dlpack.from_dlpack(
+            hip().dlpack_view(self.arena.base + hdr, [self.world], 0, 64,
+                              self.device.index or 0))
+
+    def seg_rows(self, ch: str, part: int, row_bytes: int) -> int:
+        return self._layout[(ch, part, 0)][2] // row_bytes
+
+    def put(self, ch: str, slot: int, parts: Sequence, stream=None) -> None:
+        """parts: (src tensor, per-destination row displacements, device
+        int64 [world] row counts or None, fixed row count, [row elems])."""
+        spec = []
+        for p, part in enumerate(parts):
+            src, displs, cnt, fixed = part[:4]
+            row_elems = part[4] if len(part) > 4 else 1
+            hdr, data, seg = self._layout[(ch, p, slot)]
+            rb = src.element_size() * row_elems
+            spec.append([src.data_ptr(), cnt.data_ptr() if cnt is not None else 0,
+                         int(fixed or 0), rb, hdr, data, seg] + [int(d) * rb for d in displs])
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.arena.put(self._ch[ch], spec, self.bpp, st.cuda_stream)
+
+    def wait(self, ch: str, slot: int, stream=None, fixed_parts: Sequence = ()) -> None:
+        """Block ``stream`` until every source's put of this channel's next
+        round has arrived.  ``fixed_parts``: (part, bytes) of fixed-size
+        parts read as zeros if a source never arrives."""
+        fx = []
+        for p, nb in fixed_parts:
+            _, data, seg = self._layout[(ch, p, slot)]
+            fx.append([data, seg, int(nb)])
+        st = stream if stream is not None else torch.cuda.current_stream(self.device)
+        self.arena.wait(self._ch[ch], fx, self.timeout_s, st.cuda_stream)
+
+    def check(self) -> None:
+        e = int(self._err[0].item())
+        if e & 1:
+            raise RuntimeError(f"xgmi: a peer did not arrive within {self.timeout_s} s")
+        if e & 2:
+            raise RuntimeError("xgmi: a put exceeded its segment (counts corrupt)")
+
+    # ------------------------------------------------------------ control plane
+    def exchange_counts(self, send_counts):
+        raise NotImplementedError("xgmi keeps counts on the device (use put / wait)")
+
+    def alltoallv(self, send, scounts, sdispls, recv, rcounts, rdispls, row_elems=1):
+        raise NotImplementedError("xgmi moves segments with put / wait")
+
+    def allreduce_(self, t: torch.Tensor, op: str = "sum") -> torch.Tensor:
+        if self.world == 1:
+            return t
+        if self.aux is None:
+            raise RuntimeError("xgmi: control-plane collectives need an aux transport")
+        return self.aux.allreduce_(t, op)
+
+    def barrier(self) -> None:
+        if self.aux is not None and self.world > 1:
+            self.aux.barrier()
+
+    def close(self) -> None:
+        if self.arena is not None:
+            torch.cuda.synchronize(self.device)
+        self.arena = None

@@ -96,14 +96,15 @@ KNOBS: dict[str, Knob] = {
                           "N>1 over RCCL: 1 = one communicator, every collective on one comm "
                           "stream in program order (conservative); 3 = data / count / pull "
                           "communicators on the engine's three streams"),
+    "SS_XGMI_TIMEOUT": Knob("120", "parallel/xgmi.py", "ops",
+                            "seconds a mailbox wait spins for a peer before it gives up (sticky "
+                            "error raised at the next check point)"),
+    "SS_XGMI_BPP": Knob("32", "parallel/xgmi.py", "tuning",
+                        "workgroups per peer of a mailbox put"),
     # -- experiments (measured slower or neutral; kept for re-measurement)
     "SS_ENGINE_GENERAL": Knob("0", "parallel/engine.py, bench.py", "experiment",
-                              "run a 1-GPU job through the N>1 path (1: loopback, rccl: size-1 "
-                              "RCCL communicators)"),
-    "SS_FM_NC": Knob("auto", "csrc/hip/bdedup.hip", "experiment",
-                     "FM atomic merge: factor columns per LDS pass"),
-    "SS_FM_SPLIT": Knob("0", "csrc/hip/bdedup.hip", "experiment",
-                        "FM atomic merge: column groups on separate workgroups"),
+                              "run a 1-GPU job through the N>1 path (1: loopback, rccl: a size-1 "
+                              "RCCL communicator, xgmi: a size-1 mailbox arena)"),
     "SS_STALENESS": Knob("1", "parallel/engine.py", "ops",
                          "pull-ahead bound: a round's pull waits until the push of the round "
                          "k+1 before it is applied (k = 1: staleness 1); ring: bounded by the "

@@ -438,39 +438,14 @@ def test_hipgraph_pull_ahead_trains(dev, model):
     assert np.mean(last[-5:]) < np.mean(first), (first, last[-5:])
 
 
-def test_word2vec_context_reduce_matches_atomics(dev, monkeypatch):
-    """Context-row gradients summed per unique key over the dedup buckets
-    (k_w2v_ctx_reduce) == one row of float atomics per (center, context)."""
-    monkeypatch.setenv("SS_PULL_AHEAD", "0")
-    monkeypatch.setenv("SS_W2V_MFMA", "f32")  # the context-reduce mode runs the fp32 tile
-    out = {}
-    for mode in ("reduce", "atomic"):
-        monkeypatch.setenv("SS_W2V_CTX", mode)  # (atomic is the default)
-        w, t = _graph_worker("w2v_pairs", dev)
-        assert w.ctx_reduce == (mode == "reduce")
-        losses = [float(w.step().sum().item()) for _ in range(6)]
-        torch.cuda.synchronize()
-        t.check()
-        out[mode] = (losses, t.to_dict(with_state=True))
-    (lr, tr), (la, ta) = out["reduce"], out["atomic"]
-    np.testing.assert_allclose(lr, la, rtol=1e-4)
-    assert tr.keys() == ta.keys()
-    ks = list(tr.keys())
-    # summation order differs (LDS vs memory-side atomics); AdaGrad divides by
-    # a still-small accumulator in the first steps: nearly all coordinates
-    # within a few 1e-4, every coordinate within a loose bound
-    a, b = np.stack([ta[k] for k in ks]), np.stack([tr[k] for k in ks])
-    assert np.isclose(b, a, rtol=1e-3, atol=5e-4).mean() > 0.9999
-    np.testing.assert_allclose(b, a, rtol=5e-2, atol=2e-2)
-
-
 @pytest.mark.parametrize("D,B,W", [(128, 1000, 5), (32, 640, 2), (64, 4096, 15)])
 def test_word2vec_window_grad_reduce_matches_atomics(dev, monkeypatch, D, B, W):
     """Window tile gradients as occurrence rows summed per unique key
     (k_w2v_osort + k_w2v_oreduce: counting sort per dedup bucket, one wave per
     <= 32-occurrence item, shared window rows through the tail buffer, Zipf
     heads split over several items) == the tile's own row atomics.  Partial
-    last tile (B % 64 != 0), W from 2 to the maximum 15."""
+    last tile (B % 64 != 0), W from 2 to the maximum 15.  (The atomic form
+    is what a non-bucketed dedup, SS_DEDUP=hash, runs.)"""
     from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
     from swiftsnails_amd.ops.table import HbmTable
     from swiftsnails_amd.parallel.engine import PSEngine
@@ -478,7 +453,7 @@ def test_word2vec_window_grad_reduce_matches_atomics(dev, monkeypatch, D, B, W):
     monkeypatch.setenv("SS_PULL_AHEAD", "0")
     out = {}
     for mode in ("reduce", "atomic"):
-        monkeypatch.setenv("SS_W2V_GRAD", mode)
+        monkeypatch.setenv("SS_DEDUP", "bucket" if mode == "reduce" else "hash")
         data = W2VSynth(batch_size=B, window=W, vocab=3000, noise=0.05, mode="window")
         opt, init = make_w2v_table_args(D, None)
         t = HbmTable(D, 40000, optimizer=opt, init=init, device=dev)
@@ -604,43 +579,6 @@ def test_fm_fused_update_matches_separate_apply(dev, dim):
     ks = list(a.keys())
     np.testing.assert_allclose(np.stack([b[k] for k in ks]), np.stack([a[k] for k in ks]),
                                rtol=1e-5, atol=1e-6)
-
-
-def test_fm_worker_fused_update_matches_separate_apply(dev, monkeypatch):
-    """The FM worker with the update fused into its gradient merge trains
-    like the separate k_apply (pull-ahead off: step-for-step comparable)."""
-    monkeypatch.setenv("SS_PULL_AHEAD", "0")
-    out = {}
-    for fuse in ("1", "0"):
-        monkeypatch.setenv("SS_FM_FUSE_APPLY", fuse)
-        w, t = _graph_worker("fm", dev)
-        losses = [float(w.step().sum().item()) for _ in range(10)]
-        torch.cuda.synchronize()
-        t.check()
-        out[fuse] = (losses, t.to_dict(with_state=True))
-    (l1, t1), (l0, t0) = out["1"], out["0"]
-    np.testing.assert_allclose(l1, l0, rtol=1e-4, atol=1e-3)
-    assert t1.keys() == t0.keys()
-    ks = list(t1.keys())[:5000]
-    # float summation order (LDS counting sort, atomics) over 10 training steps
-    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
-                               rtol=1e-3, atol=1e-3)
-
-
-def test_data_ahead_matches_inline(dev, monkeypatch):
-    """SS_DATA_AHEAD=1 (the batch of step i+2 generated on a third stream)
-    trains exactly like in-line generation on the route stream: the generator
-    is a pure function of the step, so the per-step losses agree."""
-    monkeypatch.setenv("SS_PULL_AHEAD", "0")
-    out = []
-    for ahead in ("0", "1"):
-        monkeypatch.setenv("SS_DATA_AHEAD", ahead)
-        w, t = _graph_worker("lr", dev)
-        assert w._data_ahead == (ahead == "1")
-        out.append([float(w.step().sum().item()) for _ in range(9)])
-        torch.cuda.synchronize()
-        t.check()
-    np.testing.assert_allclose(out[1], out[0], rtol=2e-4, atol=1e-3)
 
 
 @pytest.mark.parametrize("pull_stream", ["0", "1"])

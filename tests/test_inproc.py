@@ -144,18 +144,16 @@ def _rehearse(args):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("model,world,servers,workers,push_stream", [
-    ("sparse_lr", 8, "all", "all", "main"),  # the bench layout, small batch
-    ("word2vec", 4, "0-1", "2-3", "main"),   # BASELINE config 3 shape: servers + workers
-    ("fm", 4, "all", "all", "main"),
-    ("sparse_lr", 4, "all", "all", "pull"),  # SS_PUSH_STREAM=pull schedule
-    ("word2vec", 4, "0-1", "2-3", "pull"),
+@pytest.mark.parametrize("model,world,servers,workers", [
+    ("sparse_lr", 8, "all", "all"),  # the bench layout, small batch
+    ("word2vec", 4, "0-1", "2-3"),   # split servers + workers
+    ("word2vec", 4, "all", "all"),   # BASELINE config 3: 4 colocated ranks
+    ("fm", 4, "all", "all"),
 ])
-def test_rehearse_world_gpu(model, world, servers, workers, push_stream, monkeypatch):
+def test_rehearse_world_gpu(model, world, servers, workers, monkeypatch):
     """N rank threads on one GPU through the N>1 engine path with pull-ahead:
     no dedup overflow, every checked key on the shard the router names, loss
     goes down on every worker."""
-    monkeypatch.setenv("SS_PUSH_STREAM", push_stream)
     extra = (["--batch", "2048", "--vocab", "20000", "--dim", "64"] if model == "word2vec"
              else ["--batch", "4096", "--fields", "13", "--features", "2000000"])
     rc, out = _rehearse(["--world", str(world), "--model", model, "--servers", servers,

@@ -34,6 +34,8 @@ for s in ${STEPS//,/ }; do
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
     bench) run bench 600 python bench.py $BENCH_ARGS ;;
     general) run bench_general 600 env SS_ENGINE_GENERAL=rccl python bench.py $BENCH_ARGS ;;
+    general_xgmi) run bench_general_xgmi 600 env SS_ENGINE_GENERAL=xgmi python bench.py $BENCH_ARGS ;;
+    prof_general) run rocprof_general 600 env SS_ENGINE_GENERAL=rccl rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_general" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
     general_nopa) run bench_general_nopa 600 env SS_ENGINE_GENERAL=rccl SS_PULL_AHEAD=0 python bench.py $BENCH_ARGS ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
     *) run custom 600 bash -c "$s" ;;
