@@ -20,8 +20,9 @@
 // sub-buckets by an independent hash (the low word of dedup_hash; the sender
 // used the high word): server bucket b = k*m + t.
 //
-//   1 k_srv_count  per k: received keys per sub-bucket (m == 1: the run sums)
-//   2 k_srv_scan   exclusive scan -> bstart (server "occurrence" ranges)
+//   1 k_srv_count  per k: received keys per sub-bucket (m == 1: the run sums);
+//                  the last workgroup scans them -> bstart (server
+//                  "occurrence" ranges)
 //   3 k_srv_dedup  per b: LDS hash dedup of the sub-bucket's received keys;
 //                  writes the received position of each (pj), its local id
 //                  (luid), the unique keys staged at bstart[b] (bkeys, what
@@ -61,53 +62,66 @@ __device__ __forceinline__ uint32_t srv_sub(uint64_t key, int m) {
   return m == 1 ? 0u : __umulhi((uint32_t)dedup_hash(key), (uint32_t)m);
 }
 
-// 1. received keys per server bucket
-__global__ __launch_bounds__(256) void k_srv_count(SrvRuns R, uint32_t* __restrict__ cnt) {
-  __shared__ unsigned int h[64];
-  const int k = blockIdx.x;
-  if (R.m == 1) {
-    // the run lengths are the counts: one lane per source
-    if (threadIdx.x < 64) {
-      unsigned int c = 0;
-      for (int s = threadIdx.x; s < R.nsrc; s += 64) c += R.run_len(s, k);
-      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-      if (threadIdx.x == 0) cnt[k] = c;
-    }
-    return;
-  }
-  if (threadIdx.x < 64) h[threadIdx.x] = 0u;
-  __syncthreads();
-  for (int s = 0; s < R.nsrc; ++s) {
-    const long long a = R.run_start(s, k);
-    const uint32_t len = R.run_len(s, k);
-    for (uint32_t i = threadIdx.x; i < len; i += 256)
-      atomicAdd(&h[srv_sub(R.rkeys[a + i], R.m)], 1u);
-  }
-  __syncthreads();
-  if (threadIdx.x < (unsigned)R.m) cnt[(long long)k * R.m + threadIdx.x] = h[threadIdx.x];
-}
+// 1+2. received keys per server bucket, kSrvCntK buckets k per workgroup;
+//    the LAST workgroup to finish (arrival counter) scans the counts into
+//    bstart and zeroes the distinct-key counter — no separate
+//    single-workgroup launch.  (One workgroup per k measured 70 us: ~5000
+//    arrivals on one counter serialise at ~12 ns each.)
+static constexpr int kSrvCntK = 64;
 
-// 2. bstart = exclusive scan of cnt (P entries; one workgroup), and the
-//    distinct-key counter the dedup reserves compact ids on starts at zero
-__global__ __launch_bounds__(1024) void k_srv_scan(const uint32_t* __restrict__ cnt, int P,
+__global__ __launch_bounds__(256) void k_srv_count(SrvRuns R, uint32_t* __restrict__ cnt,
                                                    uint32_t* __restrict__ bstart,
-                                                   unsigned long long* __restrict__ ucount) {
+                                                   unsigned long long* __restrict__ ucount,
+                                                   unsigned int* __restrict__ ctr) {
+  __shared__ unsigned int h[kSrvCntK * 64];
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
-  const int per = (P + 1023) / 1024;
-  const int b0 = threadIdx.x * per;
-  unsigned int s = 0;
+  __shared__ bool last;
+  const int t = threadIdx.x;
+  const int k0 = blockIdx.x * kSrvCntK, k1 = min(R.Pd, k0 + kSrvCntK);
+  if (R.m == 1) {
+    // the run lengths are the counts: one thread per bucket
+    for (int k = k0 + t; k < k1; k += 256) {
+      unsigned int c = 0;
+      for (int s = 0; s < R.nsrc; ++s) c += R.run_len(s, k);
+      __hip_atomic_store(&cnt[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  } else {
+    for (int i = t; i < kSrvCntK * R.m; i += 256) h[i] = 0u;
+    __syncthreads();
+    for (int k = k0; k < k1; ++k)
+      for (int s = 0; s < R.nsrc; ++s) {
+        const long long a = R.run_start(s, k);
+        const uint32_t len = R.run_len(s, k);
+        for (uint32_t i = t; i < len; i += 256)
+          atomicAdd(&h[(k - k0) * R.m + srv_sub(R.rkeys[a + i], R.m)], 1u);
+      }
+    __syncthreads();
+    for (int i = t; i < (k1 - k0) * R.m; i += 256)
+      __hip_atomic_store(&cnt[(long long)k0 * R.m + i], h[i], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t == 0) last = atomicAdd(ctr, 1u) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;  // workgroup-uniform
+  const int P = R.Pd * R.m;
+  const int per = (P + 255) / 256;
+  const int b0 = t * per;
+  unsigned int sum = 0;
   for (int i = 0; i < per; ++i)
-    if (b0 + i < P) s += cnt[b0 + i];
-  unsigned int e = block_excl_scan<16>(s, wsum, &tot);
+    if (b0 + i < P) sum += __hip_atomic_load(&cnt[b0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  unsigned int e = block_excl_scan<4>(sum, wsum, &tot);
   for (int i = 0; i < per; ++i)
     if (b0 + i < P) {
       bstart[b0 + i] = e;
-      e += cnt[b0 + i];
+      e += __hip_atomic_load(&cnt[b0 + i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  if (threadIdx.x == 0) {
+  if (t == 0) {
     bstart[P] = tot;
     *ucount = 0ull;
+    *ctr = 0u;  // ready for the next call (stream-ordered)
   }
 }
 
@@ -306,10 +320,11 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
   if (nsrc < 1 || Pd < 1 || m < 1 || m > 64) throw_error("srv_dedup: bad layout");
   SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me};
   const int P = Pd * m;
-  hipLaunchKernelGGL(k_srv_count, dim3(Pd), dim3(256), 0, st, R, cnt);
+  // cnt has P + 1 words: the last is the count kernel's arrival counter
+  // (zeroed once at allocation, reset by the kernel)
+  hipLaunchKernelGGL(k_srv_count, dim3((Pd + kSrvCntK - 1) / kSrvCntK), dim3(256), 0, st, R, cnt,
+                     bstart, ucount, cnt + P);
   check_launch("k_srv_count");
-  hipLaunchKernelGGL(k_srv_scan, dim3(1), dim3(1024), 0, st, cnt, P, bstart, ucount);
-  check_launch("k_srv_scan");
   hipLaunchKernelGGL(k_srv_dedup, dim3(P), dim3(kSrvDT), 0, st, R, bstart, pj, luid, bkeys,
                      ubase, unum, ucount, err);
   check_launch("k_srv_dedup");

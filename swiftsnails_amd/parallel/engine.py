@@ -111,7 +111,7 @@ class _ServerSlot:
 
     def __init__(self, rows: int, P: int, dim: int, dev, snapshot: bool):
         u32 = torch.int32
-        self.cnt = torch.empty(P, dtype=u32, device=dev)
+        self.cnt = torch.zeros(P + 1, dtype=u32, device=dev)  # + the arrival counter
         self.bstart = torch.empty(P + 1, dtype=u32, device=dev)
         self.ubase = torch.empty(P, dtype=u32, device=dev)
         self.unum = torch.empty(P, dtype=u32, device=dev)

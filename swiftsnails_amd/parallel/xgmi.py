@@ -55,9 +55,10 @@ class XgmiTransport(Transport):
         self.arena = None
         self._ch: dict[str, int] = {}
         self._layout: dict = {}
-        # blocks per peer of a put: enough to keep 7 links busy, not so many
-        # that small segments pay a launch tail
-        self.bpp = int(os.environ.get("SS_XGMI_BPP", "32"))
+        # workgroups per peer of a put: a put is latency-bound per
+        # workgroup (16 B per lane per iteration), so a 42 MB segment needs
+        # ~100+ of them; 32 measured 211 us for the 1-GPU keys put
+        self.bpp = int(os.environ.get("SS_XGMI_BPP", "128"))
 
     # ------------------------------------------------------------ set-up
     def setup(self, channels: dict) -> None:

@@ -792,7 +792,7 @@ def test_server_merge_matches_reference(dev, dim):
     P = Pd * m
     rows = N * cap
     i32 = dict(dtype=torch.int32, device=dev)
-    cnt, bstart = torch.empty(P, **i32), torch.empty(P + 1, **i32)
+    cnt, bstart = torch.zeros(P + 1, **i32), torch.empty(P + 1, **i32)
     ubase, unum = torch.empty(P, **i32), torch.empty(P, **i32)
     pj, luid = torch.empty(rows, **i32), torch.empty(rows, **i32)
     bkeys = torch.empty(rows, dtype=torch.int64, device=dev)

@@ -28,7 +28,12 @@ run() {  # name timeout cmd...
   return 0
 }
 
-for s in ${STEPS//,/ }; do
+# steps separated by ';' (a custom step may contain spaces and commas)
+if [[ "$STEPS" == *";"* ]]; then IFS=';' read -ra STEP_LIST <<< "$STEPS"
+else IFS=',' read -ra STEP_LIST <<< "$STEPS"; fi
+n=0
+for s in "${STEP_LIST[@]}"; do
+  n=$((n + 1))
   case $s in
     smoke) run smoke 600 python -c "import __graft_entry__ as g; g.smoke()" ;;
     tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 240 --timeout-method thread ;;
@@ -36,9 +41,12 @@ for s in ${STEPS//,/ }; do
     general) run bench_general 600 env SS_ENGINE_GENERAL=rccl python bench.py $BENCH_ARGS ;;
     general_xgmi) run bench_general_xgmi 600 env SS_ENGINE_GENERAL=xgmi python bench.py $BENCH_ARGS ;;
     prof_general) run rocprof_general 600 env SS_ENGINE_GENERAL=rccl rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_general" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
+    prof_xgmi) run rocprof_xgmi 600 env SS_ENGINE_GENERAL=xgmi rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_xgmi" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
+    rehearse8) run rehearse8 900 python tools/rehearse_world.py --world 8 --steps 20 --warmup 4 ;;
+    general3) run bench_general3 600 env SS_ENGINE_GENERAL=rccl SS_RCCL_COMMS=3 python bench.py $BENCH_ARGS ;;
     general_nopa) run bench_general_nopa 600 env SS_ENGINE_GENERAL=rccl SS_PULL_AHEAD=0 python bench.py $BENCH_ARGS ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
-    *) run custom 600 bash -c "$s" ;;
+    *) run custom$n 600 bash -c "$s" ;;
   esac
 done
 echo "session done"
