@@ -80,8 +80,15 @@ class PSContext:
                 dist.init_process_group("gloo", rank=self.rank, world_size=self.world,
                                         timeout=datetime.timedelta(seconds=timeout))
             store = dist.distributed_c10d._get_default_store()
-            kind = cfg.get("transport", "rccl")
-            if kind == "rccl":
+            kind = cfg.get("transport", "auto")
+            if kind in ("auto", "xgmi"):
+                # device-side-count mailboxes over xGMI (parallel/xgmi.py),
+                # laid out and self-tested when the engine is built below
+                from ..parallel.xgmi import XgmiTransport
+
+                tr = XgmiTransport(self.rank, self.world, self.device, store,
+                                   aux=TorchDistTransport())
+            elif kind == "rccl":
                 from ..parallel.transport import rccl_comms_mode
 
                 three = rccl_comms_mode() == 3
@@ -99,10 +106,20 @@ class PSContext:
         self.transport = tr
         self.table = (HbmTable(dim, capacity, optimizer=optimizer, init=init, device=self.device)
                       if self.is_server else None)
-        self.engine = PSEngine(self.table, tr, max_keys=max_keys, dim=dim,
-                               frag_num=int(cfg.get("frag_num", 0) or 0),
-                               server_ranks=self.servers, device=self.device,
-                               count_transport=ct, pull_transport=pt)
+        ek = dict(max_keys=max_keys, dim=dim, frag_num=int(cfg.get("frag_num", 0) or 0),
+                  server_ranks=self.servers, device=self.device)
+        try:
+            self.engine = PSEngine(self.table, tr, count_transport=ct, pull_transport=pt, **ek)
+        except RuntimeError as e:
+            if not (self.world > 1 and cfg.get("transport", "auto") == "auto"
+                    and "xgmi" in str(e)):
+                raise
+            # every rank failed the mailbox self-test together: RCCL instead
+            log.warning("%s; falling back to RCCL", e)
+            tr = RcclTransport(self.rank, self.world, self.device, store=store,
+                               prefix="ss_data")
+            self.engine = PSEngine(self.table, tr, **ek)
+        self.transport = tr
         self.backup_period = int(cfg.get("param_backup_period", 0) or 0)
         self._last_backup = -1
         self.backup_root = cfg.get("param_backup_root", ".")
@@ -132,7 +149,7 @@ class PSContext:
         if resume == "latest":
             found = self._agree(ck.latest_checkpoint(self.backup_root), store)
             if found is not None:
-                self.resume(found[0], world=found[2])
+                self.resume(found[0], world=found[2], fmt=found[3])
                 self.start_round = found[1]
             else:
                 log.info("resume_from latest: no complete backup under %s", self.backup_root)
@@ -140,21 +157,22 @@ class PSContext:
             self.resume(resume)
             m = re.match(r".*param-(\d+)$", str(resume))
             self.start_round = int(m.group(1)) if m else 0
+        self._last_backup = self.start_round  # the resumed state is already on disk
 
     def _agree(self, found, store):
-        """Rank 0's choice of checkpoint ``(prefix, round, world)``, for every
-        rank (one filesystem view)."""
+        """Rank 0's choice of checkpoint ``(prefix, round, world, fmt)``, for
+        every rank (one filesystem view)."""
         if self.world == 1 or store is None:
             return found
         key = "ss_resume_latest"
-        enc = "" if found is None else f"{found[1]}:{found[2]}:{found[0]}"
+        enc = "" if found is None else f"{found[1]}:{found[2]}:{found[3]}:{found[0]}"
         if self.rank == 0:
             store.set(key, enc)
         v = store.get(key).decode() if self.rank != 0 else enc
         if not v:
             return None
-        rnd, w, prefix = v.split(":", 2)
-        return prefix, int(rnd), int(w)
+        rnd, w, fmt, prefix = v.split(":", 3)
+        return prefix, int(rnd), int(w), fmt
 
     # ------------------------------------------------------------ ckpt
     def _owner(self):
@@ -169,12 +187,13 @@ class PSContext:
         self.barrier()
         return p
 
-    def resume(self, prefix: str, world: Optional[int] = None) -> int:
+    def resume(self, prefix: str, world: Optional[int] = None, fmt: Optional[str] = None) -> int:
         """Load one complete shard set of ``prefix`` (``world``: the set
-        written by that many servers), re-routed to this job's shards."""
+        written by that many servers; ``fmt``: of that format), re-routed to
+        this job's shards."""
         n = 0
         if self.table is not None:
-            n = ck.load_sharded(self.table, prefix, owner_fn=self._owner(), world=world)
+            n = ck.load_sharded(self.table, prefix, owner_fn=self._owner(), world=world, fmt=fmt)
             log.info("rank %d resumed %d keys from %s", self.rank, n, prefix)
         self.barrier()
         return n
@@ -185,8 +204,11 @@ class PSContext:
         ``round_idx`` is the number of rounds the device has applied
         (``PipelinedWorker.rounds_done``, which runs ahead of the step count
         under hipGraph replays and then repeats): one backup per label."""
-        if (self.backup_period > 0 and round_idx > 0 and round_idx % self.backup_period == 0
-                and round_idx != self._last_backup):
+        # a backup whenever the applied rounds crossed a period boundary:
+        # under hipGraph replays rounds_done() advances a whole graph at a
+        # time, so an exact multiple of the period may never be seen
+        p = self.backup_period
+        if p > 0 and round_idx > 0 and round_idx // p > max(self._last_backup, 0) // p:
             self._last_backup = round_idx
             if self.watchdog:
                 self.watchdog.pause()
@@ -279,13 +301,29 @@ def build_worker(cfg: Config):
 
 def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
                  log_every: int = 0) -> dict:
-    """Train `steps` rounds (config num_iters) and return throughput stats."""
+    """Train and return throughput stats.
+
+    File data (a source with ``steps_per_pass``): ``num_iters`` is the number
+    of PASSES over each rank's own shard (the reference's num_iters,
+    SwiftWorker.h:77), so ranks with unequal shards have unequal step quotas;
+    a rank past its quota keeps serving empty rounds, and every
+    ``done_check_every`` rounds the ranks agree whether all are done
+    (PSEngine.all_done).  Synthetic data: ``num_iters`` (or ``steps``) rounds."""
     ctx, w = build_worker(cfg)
     # resumed job: continue the round count where the checkpoint was taken
     w.step_idx = ctx.start_round
-    steps = int(steps if steps is not None else cfg.get("num_iters", 100))
+    spp = getattr(getattr(w, "data", None), "steps_per_pass", None)
+    passes = None
+    if spp is not None and steps is None:
+        passes = int(cfg.get("num_iters", 1))
+        if w.active:
+            w.quota = ctx.start_round + passes * int(spp())
+        steps = None
+    else:
+        steps = int(steps if steps is not None else cfg.get("num_iters", 100))
+    every = max(1, int(cfg.get("done_check_every", 8) or 8))
     log_every = log_every or int(cfg.get("log_every", 0) or 0)
-    for _ in range(warmup):
+    for _ in range(warmup if passes is None else 0):
         w.step()
     # config `graph: 1`: replay the step as hipGraphs (1 GPU, synthetic data;
     # a no-op where unsupported — see PipelinedWorker.enable_graph)
@@ -294,13 +332,20 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     ctx.barrier()
     r0 = w.rounds_done()
     t0 = time.perf_counter()
-    for i in range(steps):
+    i = 0
+    while True:
+        if passes is None and i >= steps:
+            break
+        if passes is not None and i % every == 0 and ctx.engine.all_done(w.done):
+            break
         with ctx.tracer.range("step"):
             w.step()
+        i += 1
         ctx.round_done(w.step_idx)
         ctx.maybe_backup(w.rounds_done())
-        if log_every and (i + 1) % log_every == 0 and ctx.rank == 0:
-            log.warning("step %d loss %.5f", i + 1, w.mean_loss())
+        if log_every and i % log_every == 0 and ctx.rank == 0:
+            log.warning("step %d loss %.5f", i, w.mean_loss())
+    steps = i
     torch.cuda.synchronize()
     ctx.barrier()
     el = time.perf_counter() - t0
@@ -311,16 +356,21 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     # rounds the device ran in the timed region: with hipGraphs the last
     # replay runs its whole graph, so this can exceed `steps`
     done = max(steps, w.rounds_done() - r0)
-    n = torch.tensor([w.samples_per_step()], dtype=torch.int64)
+    # samples this rank trained in the timed rounds (a rank past its quota
+    # served empty rounds)
+    mine = done if w.quota is None else max(0, min(done, w.quota - r0))
+    n = torch.tensor([w.samples_per_step() * mine], dtype=torch.int64)
     if ctx.world > 1:
         dist.all_reduce(n)
     stats = {"model": cfg.get("model", "sparse_lr"), "world": ctx.world,
              "servers": len(ctx.servers), "workers": len(ctx.workers), "steps": steps,
              "seconds": el, "ms_per_step": 1000 * el / max(1, done),
-             "samples_per_s": int(n.item()) * done / el if el > 0 else 0.0,
+             "samples_per_s": int(n.item()) / el if el > 0 else 0.0,
+             "samples": int(n.item()),
              "rounds_timed": done,
              "loss": w.mean_loss() if ctx.is_worker else None, "hipgraph": bool(graphed),
-             "start_round": ctx.start_round}
+             "start_round": ctx.start_round, "passes": passes,
+             "rank0_quota": w.quota}
     m = ctx.engine.metrics.counters
     if m:
         stats["rank0_engine"] = {k: int(v) for k, v in m.items()}

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import gc
 import os
+from typing import Optional
 
 import torch
 
@@ -34,6 +35,14 @@ class PipelinedWorker:
         self._gbase = 0
         self._gper = 1
         self._cap_base = 0
+        # steps this worker has data for (absolute step index bound; None =
+        # unbounded, e.g. synthetic data): past it the rank routes empty key
+        # sets and skips the model kernels, but keeps entering every
+        # collective round as a server until all workers are done
+        # (PSEngine.all_done) — the reference's worker finishing on its own
+        # while the master waits for the rest (SwiftWorker.h:87-113,
+        # worker/terminate.h:37-51, master/terminate.h:44-62)
+        self.quota: Optional[int] = None
 
     # -- subclass hooks
     # optional ``(dd, slot, stream_ptr)`` hook run on the route stream right
@@ -50,9 +59,18 @@ class PipelinedWorker:
         raise NotImplementedError
 
     # -- driver
+    def has_data(self, step: int) -> bool:
+        """This rank trains on step ``step`` (a worker within its quota)."""
+        return self.active and (self.quota is None or step < self.quota)
+
+    @property
+    def done(self) -> bool:
+        """No data left for the next step (always true for a pure server)."""
+        return not self.has_data(self.step_idx)
+
     def _route(self, step: int):
         slot = self.engine._next_slot
-        if not self.active:
+        if not self.has_data(step):
             return self.engine.route(produce=lambda stream: self._empty)
 
         def produce(stream):
@@ -77,13 +95,21 @@ class PipelinedWorker:
         at its end, plus the device step counter the data generator reads.
         ``step()`` replays it every ``depth`` steps (the loss buffer then
         holds the loss of the graph's last step).  Replays remove the ~75 us
-        of host launch work per step that bounds small batches.  One GPU,
-        synthetic on-device data, and an optimizer without per-round host
-        state (not Adam) only; returns False otherwise.  Irreversible."""
+        of host launch work per step that bounds small batches.  One GPU, or
+        N>1 over the xGMI mailboxes (no host counts anywhere in a round);
+        synthetic on-device data, an optimizer without per-round host state
+        (not Adam) and no tensor-code update rule; returns False otherwise.
+        Irreversible."""
         eng = self.engine
         data = getattr(self, "data", None)
-        if (not eng.gpu or not eng.fast1 or not getattr(data, "graph_capturable", False)
-                or (eng.table is not None and eng.table.opt.kind == "adam")
+        tab = eng.table
+        if (not eng.gpu or not (eng.fast1 or getattr(eng, "xg", None) is not None)
+                or not getattr(data, "graph_capturable", False)
+                or (tab is not None and tab.opt.kind == "adam")
+                # a tensor-code update rule syncs the host (its row count)
+                or (tab is not None and getattr(tab, "push_fn", None) is not None)
+                # a quota decides per step on the host whether to route keys
+                or self.quota is not None
                 or os.environ.get("SS_GRAPH", "1") == "0"):
             return False
         if self._graphs is not None:
@@ -167,7 +193,7 @@ class PipelinedWorker:
         self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
         rnd = self.engine.pull(r)
         self._zero_acc()
-        if self.active:
+        if self.has_data(self.step_idx):
             with self.engine.trace("compute"):
                 self._compute(rnd, r.slot, self.engine.raw_stream())
         self.engine.push(rnd)
@@ -185,7 +211,7 @@ class PipelinedWorker:
         rnd = self._cur
         eng.begin(rnd)
         self._zero_acc()
-        if self.active:
+        if self.has_data(self.step_idx):
             with eng.trace("compute"):
                 self._compute(rnd, rnd.slot, eng.raw_stream())
         # round i+1's pull is enqueued before round i's push: with one comm

@@ -121,7 +121,7 @@ class SparseLRWorker(PipelinedWorker):
                       self.items[slot].data_ptr(), self.nitems[slot].data_ptr(), st)
 
     def _route(self, step: int):
-        if not self.active:
+        if not self.has_data(step):
             return super()._route(step)
         eng = self.engine
         slot = eng._next_slot

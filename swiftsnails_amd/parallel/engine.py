@@ -753,6 +753,19 @@ class PSEngine:
     def barrier(self):
         self.t.barrier()
 
+    def all_done(self, local_done: bool) -> bool:
+        """Collective termination check: True once every rank reports done.
+        Every rank calls it at the same rounds (syncs); a rank that finished
+        early keeps serving rounds with an empty key set until then — the
+        reference's master waiting for WORKER_FINISH_WORK from every worker
+        before telling the servers to stop (master/terminate.h:44-62)."""
+        if self.world == 1:
+            return bool(local_done)
+        dev = self.device if (self.gpu and not hasattr(self.t, "aux")) else "cpu"
+        flag = torch.tensor([1 if local_done else 0], dtype=torch.int64, device=dev)
+        self.t.allreduce_(flag, "min")
+        return int(flag.item()) == 1
+
     def check(self) -> None:
         """Raise on a sticky device-side error of this rank (syncs): a dedup
         bucket whose LDS table overflowed (its occurrences got no unique id,

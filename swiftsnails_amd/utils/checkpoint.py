@@ -309,34 +309,38 @@ def load_sharded(table, prefix: str, owner_fn=None, world: Optional[int] = None,
     return n
 
 
-def latest_checkpoint(root: str, stem: str = "param-") -> Optional[tuple[str, int, int]]:
-    """Newest COMPLETE periodic backup under `root`: ``(prefix, round,
-    world)`` of the highest ``<stem><round>`` with a shard set
-    ``.shard<r>-of-<W>`` present for every r < W.  A job that died while
-    writing a backup leaves an incomplete set, which is skipped; shard files
-    are renamed into place only once fully written (save_text /
+def latest_checkpoint(root: str, stem: str = "param-") -> Optional[tuple[str, int, int, str]]:
+    """Newest COMPLETE periodic backup under `root`: ``(prefix, round, world,
+    fmt)`` of the highest ``<stem><round>`` with a shard set
+    ``.shard<r>-of-<W>`` of one format present for every r < W.  A job that
+    died while writing a backup leaves an incomplete set, which is skipped;
+    shard files are renamed into place only once fully written (save_text /
     save_binary).  When one round holds complete sets of several world sizes
-    (a re-run at another size), the most recently written wins.  None if
-    there is none."""
+    or formats (a re-run at another size, or after ``checkpoint_format``
+    changed), the most recently written set wins, and its format is returned
+    so the load reads that set only.  None if there is none."""
     best = None
+    seen = set()
     for f in glob.glob(os.path.join(root, glob.escape(stem) + "*.shard*-of-*.*")):
         m = _shard_re().match(os.path.basename(f))
         if not m or not m.group(1).startswith(stem):
             continue
         rnd_s = m.group(1)[len(stem):]
-        if not rnd_s.isdigit():
+        if not rnd_s.isdigit() or m.group(1) in seen:
             continue
+        seen.add(m.group(1))
         prefix = os.path.join(root, m.group(1))
-        for w, by in shard_sets(prefix).items():
-            if not _complete(by, w):
-                continue
-            mtime = max(os.path.getmtime(p) for ps in by.values() for p in ps)
-            cand = (int(rnd_s), mtime, prefix, w)
-            if best is None or cand[:2] > best[:2]:
-                best = cand
+        for fmt in ("bin", "text"):
+            for w, by in shard_sets(prefix, fmt).items():
+                if not _complete(by, w):
+                    continue
+                mtime = max(os.path.getmtime(p) for ps in by.values() for p in ps)
+                cand = (int(rnd_s), mtime, prefix, w, fmt)
+                if best is None or cand[:2] > best[:2]:
+                    best = cand
     if best is None:
         return None
-    return best[2], best[0], best[3]
+    return best[2], best[0], best[3], best[4]
 
 
 def owner_filter(frag_rank_map: np.ndarray, rank: int):

@@ -171,6 +171,11 @@ class FileCtrSource:
     def rows(self) -> int:
         return self.ds.rows
 
+    def steps_per_pass(self) -> int:
+        """Steps of one pass over this rank's shard: every row once; the last
+        batch of a pass wraps into the shard's start (no partial batches)."""
+        return -(-self.ds.rows // self.batch_size)
+
     def _fill(self, step: int, buf):
         cursor = (step * self.batch_size) % self.ds.rows
         self.ds.fill(cursor, self.batch_size, self.num_fields, buf["keys"].data_ptr(),
@@ -285,6 +290,12 @@ class FileCorpusSource(W2VLayout):
     def graph_capturable(self) -> bool:
         return self.resident == "hbm"
 
+    def steps_per_pass(self) -> int:
+        """Steps of one pass over this rank's corpus shard: window mode walks
+        every token as a center once per pass; pairs mode draws as many
+        centers."""
+        return -(-self.corpus.size // self.batch_size)
+
     def _fill(self, step: int, buf):
         if self.mode == "window":
             self.corpus.fill_skipgram_window(self.seed, step, self.batch_size, self.window,
@@ -350,10 +361,22 @@ class _null:
         return False
 
 
+def rank_data_path(path: str, rank: int, world: int) -> tuple[str, int, int]:
+    """(file, shard, nshards) a rank reads: ``data_path`` with ``{rank}`` in
+    it names one file per rank (the reference's per-worker input split,
+    /root/reference/src/tools/run_worker.sh:4,13 — each worker trains on
+    its own data file), read whole; otherwise the rank takes the rank-th
+    contiguous 1/world of one shared file."""
+    if "{rank}" in path:
+        return path.replace("{rank}", str(rank)), 0, 1
+    return path, rank, world
+
+
 def make_ctr_source(cfg, rank: int = 0, world: int = 1, device=None):
     """Config keys: data_path, data_format (libsvm|ctr), batch_size, num_fields,
     data_resident (auto|hbm|host)."""
-    return FileCtrSource(cfg.get("data_path"), cfg.get("data_format", "libsvm"),
+    path, rank, world = rank_data_path(cfg.get("data_path"), rank, world)
+    return FileCtrSource(path, cfg.get("data_format", "libsvm"),
                          batch_size=int(cfg.get("batch_size", 65536)),
                          num_fields=int(cfg.get("num_fields", 0) or 0) or None,
                          rank=rank, world=world,
@@ -364,9 +387,11 @@ def make_ctr_source(cfg, rank: int = 0, world: int = 1, device=None):
 def make_corpus_source(cfg, rank: int = 0, world: int = 1, device=None):
     """Config keys: data_path, batch_size, window, negatives, min_count, sample,
     data_resident (auto|hbm|host), w2v_mode (window|pairs)."""
-    return FileCorpusSource(cfg.get("data_path"), batch_size=int(cfg.get("batch_size", 16384)),
+    path, shard, nshards = rank_data_path(cfg.get("data_path"), rank, world)
+    return FileCorpusSource(path, batch_size=int(cfg.get("batch_size", 16384)),
+                            seed=1234 + 7919 * (rank - shard),  # negatives differ per rank
                             window=int(cfg.get("window", 5)),
-                            negatives=int(cfg.get("negatives", 5)), rank=rank, world=world,
+                            negatives=int(cfg.get("negatives", 5)), rank=shard, world=nshards,
                             min_count=int(cfg.get("min_count", 1)),
                             sample=float(cfg.get("sample", 0.0)),
                             nthreads=int(cfg.get("data_threads", 8)),

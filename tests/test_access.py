@@ -289,3 +289,25 @@ def test_host_table_push_method_and_cluster_server():
     assert not errs, errs
     np.testing.assert_allclose(got["w"], [[-1, -1], [1, 0], [0, -1]])
     assert server.push_count == 2
+
+
+def test_host_table_tensor_rule_sees_duplicate_keys_once():
+    """A tensor-code update rule on the host table gets each key once per
+    push, with the gradients of its duplicates summed (no update dropped by
+    the last write-back winning)."""
+    from swiftsnails_amd.ops.host_table import HostTable
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+
+    t = HostTable(1, 2, Optimizer("sgd", lr=1.0), InitConfig("zero"))
+    seen = []
+
+    def rule(rows, g):
+        seen.append(rows.shape[0])
+        rows[:, 0] -= g[:, 0]
+        return rows
+
+    t.set_push_method(rule)
+    keys = np.array([5, 7, 5, 5, 9, 7], dtype=np.int64)
+    t.push_keys(keys, np.array([[1], [2], [3], [4], [5], [6]], dtype=np.float32))
+    assert seen == [3]
+    np.testing.assert_allclose(t.pull_keys(np.array([5, 7, 9])).numpy()[:, 0], [-8, -8, -5])

@@ -152,7 +152,7 @@ def test_text_save_is_atomic_and_crash_leaves_no_shard(tmp_path):
         ck.save_text(_CrashingTable(t), ck.shard_path(str(root / "param-9"), 1, 2, "text"))
     assert not (root / "param-9.shard1-of-2.txt").exists()
     assert not list(root.glob("*.tmp"))
-    assert ck.latest_checkpoint(str(root)) == (str(root / "param-5"), 5, 2)
+    assert ck.latest_checkpoint(str(root)) == (str(root / "param-5"), 5, 2, "text")
 
 
 def test_load_sharded_uses_one_set_only(tmp_path):
@@ -178,3 +178,67 @@ def test_load_sharded_uses_one_set_only(tmp_path):
     with pytest.raises(ValueError, match="fmt"):
         ck.select_shards(prefix, world=1)
     assert ck.select_shards(prefix, world=1, fmt="bin") == [ck.shard_path(prefix, 0, 1, "bin")]
+
+
+def test_latest_checkpoint_with_two_formats_in_one_round(tmp_path):
+    """A round holding complete .bin and .txt sets of the same world (the
+    checkpoint format changed between runs): the newest set is chosen with its
+    format, and loading it reads that set only (no 'pass fmt=' error)."""
+    import os
+    import time
+
+    from swiftsnails_amd.ops.host_table import HostTable
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.utils import checkpoint as ck
+
+    t = HostTable(2, 2, Optimizer("sgd", lr=1.0), InitConfig("zero"))
+    keys = np.arange(1, 41, dtype=np.int64)
+    t.push_keys(keys, np.ones((40, 2), np.float32))
+    root = tmp_path
+    for r in range(2):
+        ck.save_sharded(t, str(root / "param-4"), r, 2, fmt="bin")
+    old = time.time() - 100
+    for f in root.glob("param-4.*.bin"):
+        os.utime(f, (old, old))
+    for r in range(2):
+        ck.save_sharded(t, str(root / "param-4"), r, 2, fmt="text")
+    found = ck.latest_checkpoint(str(root))
+    assert found == (str(root / "param-4"), 4, 2, "text")
+    t2 = HostTable(2, 2, Optimizer("sgd", lr=1.0), InitConfig("zero"))
+    n = ck.load_sharded(t2, found[0], world=found[2], fmt=found[3])
+    assert n == 2 * 40  # both shards hold the whole (unsharded) table
+    np.testing.assert_allclose(t2.pull_keys(keys).numpy(), -np.ones((40, 2)))
+
+
+def test_backups_fire_when_rounds_cross_a_period():
+    """PSContext.maybe_backup with rounds that advance in jumps (hipGraph
+    replays of 16 steps): a backup whenever a period boundary was crossed,
+    labelled with the round reached, and none right after a resume."""
+    from swiftsnails_amd.framework.gpu import PSContext
+
+    class Stub:
+        backup_period = 10
+        _last_backup = -1
+        watchdog = None
+        backup_root = "/nonexistent"
+
+        def __init__(self):
+            self.saved = []
+
+            class E:
+                def check(self_):
+                    pass
+            self.engine = E()
+
+        def save(self, prefix, fmt=None):
+            self.saved.append(int(prefix.rsplit("-", 1)[1]))
+
+    s = Stub()
+    for r in (16, 32, 48, 64, 80, 96):
+        PSContext.maybe_backup(s, r)
+    assert s.saved == [16, 32, 48, 64, 80, 96]  # 10,20,30,... crossed each time
+    s2 = Stub()
+    s2._last_backup = 30  # resumed from param-30
+    for r in (31, 35, 39, 41, 45):
+        PSContext.maybe_backup(s2, r)
+    assert s2.saved == [41]

@@ -174,3 +174,76 @@ def test_rounds_done_under_graph_replays():
         w.step_idx = k
         got.append(w.rounds_done())
     assert got == [10, 14, 14, 14, 14, 18, 18, 18, 18]
+
+
+def _run_uneven_rank(rank, world, init, quotas, every, q):
+    init_gloo(init, rank, world)
+    try:
+        from swiftsnails_amd.ops.host_table import HostTable
+        from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+        from swiftsnails_amd.parallel.engine import PSEngine
+        from swiftsnails_amd.parallel.transport import TorchDistTransport
+
+        table = HostTable(DIM, 4, Optimizer("adagrad", lr=0.1), InitConfig("uniform", 0.2, 0.01))
+        eng = PSEngine(table, TorchDistTransport(), max_keys=300, dim=DIM, frag_num=64,
+                       device="cpu")
+        rnd = 0
+        while True:
+            if rnd % every == 0 and eng.all_done(rnd >= quotas[rank]):
+                break
+            k = _keys_for(rank, rnd) if rnd < quotas[rank] else np.zeros(0, np.int64)
+            r = eng.pull(torch.from_numpy(k))
+            if len(k):
+                eng.accumulate(r, torch.from_numpy(_grads_for(k, rank, rnd)))
+            eng.push(r)
+            rnd += 1
+        q.put((rank, rnd, table.to_dict(with_state=True)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_uneven_shards_collective_termination():
+    """Three workers with shards of 3, 7 and 2 rounds (SwiftWorker's own
+    pace): a finished worker keeps serving empty rounds; every 4 rounds the
+    ranks agree whether all are done (PSEngine.all_done); all stop at the
+    same round, and the tables match the oracle in which each round merges
+    only the workers that still had data."""
+    from swiftsnails_amd.ops.host_table import HostTable
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+
+    world, quotas, every = 3, [3, 7, 2], 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = file_init()
+    procs = [ctx.Process(target=_run_uneven_rank, args=(r, world, init, quotas, every, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = collect(q, procs, world, 240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    stops = {rnd for _, rnd, _ in res}
+    assert stops == {8}  # the first multiple of 4 at which all 7 rounds are done
+    merged = {}
+    for _, _, st in res:
+        merged.update(st)
+    t = HostTable(DIM, 4, Optimizer("adagrad", lr=0.1), InitConfig("uniform", 0.2, 0.01))
+    for rnd in range(8):
+        live = [r for r in range(world) if rnd < quotas[r]]
+        if not live:
+            t.next_round()
+            continue
+        ks = [_keys_for(r, rnd) for r in live]
+        gs = [_grads_for(k, r, rnd) for k, r in zip(ks, live)]
+        for k in ks:
+            t.pull_keys(k)
+        u, inv = np.unique(np.concatenate(ks), return_inverse=True)
+        m = np.zeros((len(u), DIM), np.float64)
+        np.add.at(m, inv, np.concatenate(gs).astype(np.float64))
+        t.push_keys(u, m.astype(np.float32))
+        t.next_round()
+    ref = t.to_dict(with_state=True)
+    assert set(merged) == set(ref)
+    for k in ref:
+        np.testing.assert_allclose(merged[k], ref[k], rtol=2e-5, atol=2e-6)

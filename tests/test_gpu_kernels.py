@@ -846,3 +846,37 @@ def test_server_merge_matches_reference(dev, dim):
         w1 = w0 - 0.3 * acc[k] / np.sqrt(h1 + 1e-8)
         np.testing.assert_allclose(after[k][dim:], h1, rtol=2e-4, atol=1e-5)
         np.testing.assert_allclose(after[k][:dim], w1, rtol=2e-4, atol=1e-5)
+
+
+def test_push_method_set_after_engine_on_lr_table(dev):
+    """A tensor-code update rule installed AFTER the engine was built on a
+    scalar-AdaGrad (LR-shaped) table: the pull takes no snapshot, the rule
+    runs, and hipGraph replay is refused (the rule syncs the host)."""
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    data = CtrSynth(batch_size=1024, num_fields=8, num_features=50_000)
+    t = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev)
+    eng = PSEngine(t, None, max_keys=1024 * 8, dim=1, device=dev)
+    assert eng.snapshot and t.snapshot_ok
+    calls = []
+
+    def rule(rows, g):
+        calls.append(rows.shape[0])
+        rows[:, 0] -= 0.5 * g[:, 0]
+        return rows
+
+    t.set_push_method(rule)
+    assert not t.snapshot_ok
+    keys = torch.arange(1, 201, dtype=torch.int64, device=dev)
+    r = eng.pull(keys)
+    assert r.snap is None
+    eng.accumulate(r, torch.ones(200, 1, device=dev))
+    eng.push(r)
+    torch.cuda.synchronize()
+    assert calls == [200]
+    v, _ = t.pull(keys, insert=False)
+    np.testing.assert_allclose(v.cpu().numpy()[:, 0], -0.5, rtol=1e-6)
+    w = SparseLRWorker(eng, data)
+    assert not w.enable_graph()

@@ -206,16 +206,20 @@ def _bench_torchrun(nproc, extra, env_extra=None):
     return json.loads(lines[0])
 
 
+@pytest.mark.parametrize("transport", ["auto", "rccl"])
 @pytest.mark.parametrize("world", [2, 4])  # N = 8 is the driver's scaling run
-def test_bench_script_multi_gpu_rccl(world):
+def test_bench_script_multi_gpu(world, transport):
     """The driver's scaling run in miniature: bench.py over `world` GPUs with
-    the native RCCL communicators (skipped on boxes with fewer GPUs)."""
+    the default xGMI mailboxes or the native RCCL communicator (skipped on
+    boxes with fewer GPUs)."""
     if torch.cuda.device_count() < world:
         pytest.skip(f"needs {world} GPUs")
     j = _bench_torchrun(world, ["--steps", "5", "--warmup", "2", "--batch", "16384",
-                                "--features", "10000000"])
+                                "--features", "10000000", "--transport", transport])
     assert j["n_gpus"] == world and j["value"] > 0
     assert j["config"]["parallelism"].startswith(f"ps{world}")
+    if transport == "rccl":
+        assert j["config"]["rccl_nranks"] == world
 
 
 def test_bench_script_world2_gloo_rehearsal():
@@ -282,3 +286,68 @@ def test_word2vec_window_world2_trains():
         assert np.isfinite(losses).all() and np.mean(losses[-3:]) < np.mean(losses[:2]), losses
         assert len(table) > 0 and not (keys & set(table))
         keys |= set(table)
+
+
+def test_bench_script_world2_xgmi_one_gpu():
+    """bench.py at N = 2 under torch.distributed.run with the DEFAULT data
+    plane (xGMI mailboxes, device-side counts), both ranks on cuda:0: the
+    driver's N>1 scaling path with a real peer — arena IPC mapping, the
+    start-up self-test, puts into the peer's mailboxes, waits on its arrival
+    counters, the servers' merge — and the one JSON line reporting what ran."""
+    j = _bench_torchrun(2, ["--steps", "6", "--warmup", "3", "--batch", "8192",
+                            "--features", "4000000"], {"SS_BENCH_DEVICE": "0"})
+    assert j["n_gpus"] == 2 and j["value"] > 0
+    c = j["config"]
+    assert c["transport"].startswith("xGMI"), c["transport"]
+    assert c["server_unique_keys_per_step"] > 0
+    assert c["server_unique_keys_per_step"] <= c["unique_recv_per_step"]
+    assert c["a2a_bytes_per_step"] > 0
+    assert c["loss_last"] < c["loss_first"]
+
+
+def test_uneven_file_shards_terminate_together(tmp_path):
+    """Two ranks on cuda:0 (xGMI mailboxes) training sparse LR on their OWN
+    files of different lengths (data_path with {rank}): num_iters = 2 passes
+    over each rank's file gives quotas of 2 x ceil(rows / B) steps; the rank
+    that finishes first serves empty rounds until both are done; the job
+    stops at the first agreed check round and dumps the final model."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    rng = np.random.default_rng(3)
+    rows = {0: 700, 1: 230}
+    for r, n in rows.items():
+        with open(tmp_path / f"d.{r}.txt", "w") as f:
+            for _ in range(n):
+                feats = sorted(set(rng.integers(1, 5000, size=6).tolist()))
+                f.write(f"{int(rng.random() < 0.3)} " + " ".join(f"{x}:1" for x in feats) + "\n")
+    out = tmp_path / "final"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "swiftsnails_amd.launch", "--config",
+           os.path.join(root, "configs", "sparse_lr_10m.conf"),
+           "--set", f"data_path={tmp_path}/d.{{rank}}.txt", "--set", "data_format=libsvm",
+           "--set", "batch_size=64", "--set", "num_fields=8", "--set", "num_iters=2",
+           "--set", "done_check_every=4", "--set", "table_capacity=100000",
+           "--set", f"param_output={out}", "--set", "param_output_format=text"]
+    env = dict(os.environ, GLOO_SOCKET_IFNAME="lo", SS_DEVICE="0", PYTHONPATH=root)
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    stats = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    quotas = {k: 2 * -(-n // 64) for k, n in rows.items()}  # 22 and 8 steps
+    assert stats["passes"] == 2 and stats["rank0_quota"] == quotas[0]
+    # the first multiple of done_check_every at which every rank is done
+    assert stats["steps"] == -(-max(quotas.values()) // 4) * 4
+    assert stats["samples"] == 64 * sum(quotas.values())
+    dumped = {}
+    for f in tmp_path.glob("final.shard*-of-2.txt"):
+        for ln in f.read_text().splitlines():
+            k, v = ln.split("\t")
+            dumped[int(k)] = v
+    feats = set()
+    for n in rows:
+        for ln in (tmp_path / f"d.{n}.txt").read_text().splitlines():
+            feats |= {int(t.split(":")[0]) for t in ln.split()[1:]}
+    assert set(dumped) == feats  # both ranks' keys, each on exactly one shard

@@ -114,7 +114,7 @@ def test_latest_checkpoint_picks_newest_complete_set(tmp_path):
                  "param-20.shard1-of-2.bin",  # incomplete: rank 0 never wrote
                  "param-7.shard0-of-1.bin.tmp", "other-30.shard0-of-1.bin"):
         (tmp_path / name).write_bytes(b"x")
-    assert ck.latest_checkpoint(str(tmp_path)) == (str(tmp_path / "param-10"), 10, 2)
+    assert ck.latest_checkpoint(str(tmp_path)) == (str(tmp_path / "param-10"), 10, 2, "text")
     assert ck.latest_checkpoint(str(tmp_path / "missing")) is None
 
 
