@@ -9,12 +9,20 @@
 #pragma once
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 
 #include "ss/hash.h"
 
 namespace ss {
 
-enum InitKind : int { kInitZero = 0, kInitUniform = 1, kInitNormal = 2 };
+// kInitConst: every parameter = scale.  kInitMarker: parameters get the
+// kInitMarkerBits NaN payload, so the host can find the keys a pull just
+// created and run a user's tensor-code initialiser on them
+// (HbmTable.set_init_method; the reference's PullAccessMethod::init_param,
+// sparse_access_method.h:10-28).
+enum InitKind : int { kInitZero = 0, kInitUniform = 1, kInitNormal = 2, kInitConst = 3,
+                      kInitMarker = 4 };
+static constexpr uint32_t kInitMarkerBits = 0x7FBADBADu;
 enum OptKind : int { kOptSGD = 0, kOptAdaGrad = 1, kOptFTRL = 2, kOptAdam = 3 };
 
 struct InitParams {
@@ -57,7 +65,14 @@ SS_HD int opt_state_width(int kind, int dim) {
 SS_HD float init_value(const InitParams& ip, uint64_t key, uint32_t j, uint32_t dim) {
   (void)dim;
   if (ip.kind == kInitZero) return 0.0f;
+  if (ip.kind == kInitMarker) {
+    const uint32_t b = kInitMarkerBits;
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+  }
   if (ip.zero_bit >= 0 && ((key >> ip.zero_bit) & 1ull)) return 0.0f;
+  if (ip.kind == kInitConst) return ip.scale;
   const uint64_t r =
       splitmix64(ip.seed ^ (key * 0x9E3779B97F4A7C15ull) ^ ((uint64_t)j << 48) ^ (uint64_t)j);
   if (ip.kind == kInitUniform) {

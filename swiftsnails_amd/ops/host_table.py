@@ -56,6 +56,8 @@ def set_table_push_method(native_table, fn) -> None:
 class HostTable:
     device = torch.device("cpu")
     push_fn = None
+    init_fn = None
+    pull_fn = None
 
     def __init__(self, dim: int, shard_num: int = 8, optimizer: Optional[Optimizer] = None,
                  init: Optional[InitConfig] = None, nthreads: int = 0):
@@ -74,14 +76,54 @@ class HostTable:
         self.push_fn = fn
         set_table_push_method(self._t, fn)
 
+    def set_init_method(self, fn) -> None:
+        """User initialiser, as ``HbmTable.set_init_method``: ``fn(keys) ->
+        rows [n, width]`` for keys a pull (or push) creates."""
+        self.init_fn = fn
+
+    def set_pull_method(self, fn) -> None:
+        """User pull transform, as ``HbmTable.set_pull_method``:
+        ``fn(keys, rows [n, width]) -> vals [n, dim]``."""
+        self.pull_fn = fn
+
+    @property
+    def custom_pull(self) -> bool:
+        return self.init_fn is not None or self.pull_fn is not None
+
+    def _create_missing(self, k: np.ndarray) -> None:
+        """Run the user initialiser on the keys of ``k`` not yet stored."""
+        if self.init_fn is None or len(k) == 0:
+            return
+        _, found = self._t.get_rows(k)
+        miss = np.unique(k[found == 0])
+        if len(miss):
+            rows = self.init_fn(torch.from_numpy(miss.view(np.int64)))
+            rows = np.ascontiguousarray(torch.as_tensor(rows, dtype=torch.float32).numpy())
+            if rows.shape != (len(miss), self.width):
+                raise ValueError(f"init method returned {rows.shape}, expected "
+                                 f"{(len(miss), self.width)}")
+            self._t.assign(miss, rows.reshape(-1))
+
     # same surface as HbmTable where it makes sense
     def pull_keys(self, keys) -> torch.Tensor:
-        return torch.from_numpy(self._t.pull(_u64(keys)))
+        k = _u64(keys)
+        self._create_missing(k)
+        vals = torch.from_numpy(self._t.pull(k))
+        if self.pull_fn is not None:
+            rows, _ = self._t.get_rows(k)
+            vals = torch.as_tensor(self.pull_fn(torch.from_numpy(k.view(np.int64)),
+                                                torch.from_numpy(rows)), dtype=torch.float32)
+            if vals.shape != (len(k), self.dim):
+                raise ValueError(f"pull method returned {tuple(vals.shape)}, expected "
+                                 f"{(len(k), self.dim)}")
+        return vals
 
     def push_keys(self, keys, grads):
         g = grads.detach().cpu().numpy() if isinstance(grads, torch.Tensor) else np.asarray(grads)
         self._t.set_opt(_host_opt(self.opt))
-        self._t.push(_u64(keys), np.ascontiguousarray(g, dtype=np.float32).reshape(-1))
+        k = _u64(keys)
+        self._create_missing(k)
+        self._t.push(k, np.ascontiguousarray(g, dtype=np.float32).reshape(-1))
 
     def next_round(self):
         self.opt.step += 1

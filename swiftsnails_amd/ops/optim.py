@@ -23,7 +23,10 @@ from dataclasses import dataclass, field
 import numpy as np
 
 OPT_KINDS = {"sgd": 0, "adagrad": 1, "ftrl": 2, "adam": 3}
-INIT_KINDS = {"zero": 0, "uniform": 1, "normal": 2}
+# compiled initialisers (ss/optim.h init_value); "marker" is internal: the
+# placeholder a tensor-code initialiser replaces (HbmTable.set_init_method)
+INIT_KINDS = {"zero": 0, "uniform": 1, "normal": 2, "const": 3, "marker": 4}
+INIT_MARKER_BITS = 0x7FBADBAD
 
 
 def state_width(kind: str, dim: int) -> int:

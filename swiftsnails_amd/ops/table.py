@@ -118,6 +118,10 @@ class HbmTable:
         self.version = 0
         # user-defined update rule (set_push_method), else the optimizer menu
         self.push_fn = None
+        # user-defined initialiser / pull transform (set_init_method,
+        # set_pull_method), else the compiled init menu and the identity
+        self.init_fn = None
+        self.pull_fn = None
         self._alloc(int(capacity))
         self._init_native = self.init_cfg.native()
 
@@ -205,13 +209,88 @@ class HbmTable:
             h.probe(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), self._init_native,
                     int(insert), self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, st)
             h.gather(self.dt, slots.data_ptr(), sl, n, out.data_ptr(), self.G, st)
+        if self.custom_pull and segs is None:
+            self.finish_pull(slots, out)
         return out, slots
 
     @property
     def snapshot_ok(self) -> bool:
         """Rows are (w, h) scalar AdaGrad pairs the pull can snapshot."""
         return (self.G == 1 and self.dim == 1 and self.width == 2 and self.push_fn is None and
+                not self.custom_pull and
                 self.opt.kind == "adagrad" and self.stride % 8 == 0 and self.row_off % 8 == 0)
+
+    # -- user-defined access methods (tensor code) ---------------------------
+    @property
+    def custom_pull(self) -> bool:
+        return self.init_fn is not None or self.pull_fn is not None
+
+    def set_init_method(self, fn) -> None:
+        """The reference's ``PullAccessMethod::init_param`` as tensor code
+        (/root/reference/src/core/parameter/sparse_access_method.h:10-28,
+        called by lookup-or-init, sparsetable.h:142-149): ``fn(keys) ->
+        rows`` gives the full rows [n, width] (parameters, then optimizer
+        state) of keys a pull creates.  The device insert writes a NaN marker
+        row; ``finish_pull`` finds the marked rows among a pull's and replaces
+        them.  ``None`` restores the compiled initialiser."""
+        self.init_fn = fn
+        self._init_native = (InitConfig("marker", state_init=self.init_cfg.state_init).native()
+                             if fn is not None else self.init_cfg.native())
+        self.version += 1
+
+    def set_pull_method(self, fn) -> None:
+        """The reference's ``PullAccessMethod::get_pull_value`` as tensor
+        code: ``fn(keys, rows) -> vals`` maps the stored rows [n, width] to the
+        values [n, dim] a pull returns (e.g. a weight derived from optimizer
+        state).  ``None`` returns the parameters as stored."""
+        self.pull_fn = fn
+        self.version += 1
+
+    def keys_view(self) -> torch.Tensor:
+        """[capacity] int64 view of every slot's key word (strided)."""
+        return self.storage.view(torch.int64).view(self.capacity, self.stride // 8)[
+            :, self.key_off // 8]
+
+    def finish_pull(self, slots: torch.Tensor, out: torch.Tensor, n=None) -> None:
+        """Apply the tensor-code initialiser / pull transform to the rows a
+        pull just produced: ``slots`` [n] (resolved slots, -1 = none), ``out``
+        [n, dim] (the pulled values, rewritten).  ``n``: a host count or a
+        device count tensor (synced).  On the current stream."""
+        if not self.custom_pull:
+            return
+        if n is None:
+            n = slots.numel()
+        elif isinstance(n, torch.Tensor):
+            n = int(n.reshape(-1).sum().item())
+        if n == 0:
+            return
+        s = slots.reshape(-1)[:n]
+        ok = s >= 0
+        s = s[ok]
+        rv = self.rows_view()
+        rows = rv[s]
+        keys = self.keys_view()[s]
+        if self.init_fn is not None:
+            from .optim import INIT_MARKER_BITS
+
+            new = rows[:, 0].view(torch.int32) == INIT_MARKER_BITS
+            if bool(new.any()):
+                r = torch.as_tensor(self.init_fn(keys[new]), dtype=torch.float32,
+                                    device=self.device)
+                if r.shape != (int(new.sum()), self.width):
+                    raise ValueError(f"init method returned {tuple(r.shape)}, expected "
+                                     f"{(int(new.sum()), self.width)}")
+                rv[s[new]] = r
+                rows[new] = r
+        vals = rows[:, :self.dim]
+        if self.pull_fn is not None:
+            vals = torch.as_tensor(self.pull_fn(keys, rows), dtype=torch.float32,
+                                   device=self.device)
+            if vals.shape != (s.numel(), self.dim):
+                raise ValueError(f"pull method returned {tuple(vals.shape)}, expected "
+                                 f"{(s.numel(), self.dim)}")
+        o = out.reshape(-1, self.dim)[:n]
+        o[ok] = vals
 
     # -- user-defined update rule -------------------------------------------
     def set_push_method(self, fn) -> None:
@@ -324,6 +403,8 @@ class HbmTable:
         """push by key: keys missing from the table are created first (the
         reference CHECK-fails instead, sparsetable.h:184)."""
         slots = self.lookup_slots(keys, insert=True, stream=stream)
+        if self.init_fn is not None:  # keys this push created: the user's rows first
+            self.finish_pull(slots, torch.empty((slots.numel(), self.dim), device=self.device))
         self.push_slots(slots, grads.reshape(-1, self.dim).contiguous(), stream=stream)
 
     def next_round(self):

@@ -428,6 +428,8 @@ class PSEngine:
         S.snap_valid = S.snap is not None and not self.pull_ahead and tab.snapshot_ok
         tab.pull_buckets(S.view(self.Ps), self.svals, S.slots, stream=st,
                          snap=S.snap if S.snap_valid else None)
+        if tab.custom_pull:  # user init / pull methods (tensor code; syncs)
+            tab.finish_pull(S.slots, self.svals, n=S.ucount)
         h.srv_fill(self.Ps, S.bstart.data_ptr(), S.ubase.data_ptr(), S.unum.data_ptr(),
                    S.pj.data_ptr(), S.luid.data_ptr(), self.svals.data_ptr(),
                    self.rvals.data_ptr(), self.dim, st)
@@ -507,6 +509,8 @@ class PSEngine:
         else:
             tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                      segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
+        if tab.custom_pull:  # user init / pull methods (tensor code; syncs)
+            tab.finish_pull(self.slots[slot], uv, n=dd.ucount)
         self.metrics.add(occurrences=dd.n)
         return Round(dd, uv, slot, slots=self.slots[slot], snap=snap,
                      snap_version=tab.version)
@@ -529,6 +533,8 @@ class PSEngine:
                 else:
                     tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],
                              segs=tab.dev_segs(dd.ucount), max_n=max(1, min(dd.n, dd.ucap)))
+                if tab.custom_pull:
+                    tab.finish_pull(self.slots[slot], uv, n=dd.ucount)
                 self.metrics.add(occurrences=dd.n)
                 rnd = Round(dd, uv, slot, slots=self.slots[slot])
             else:
@@ -734,6 +740,8 @@ class PSEngine:
             s = self.slots[r.slot]
             _hip().probe(tab.dt, dd.ukeys.data_ptr(), sl, n, s.data_ptr(), tab._init_native, 1,
                          tab.size_ctr.data_ptr(), tab.err.data_ptr(), tab.G, _stream())
+            if tab.init_fn is not None:  # keys this push created: the user's rows first
+                tab.finish_pull(s, self.uvals[r.slot], n=dd.ucount)
             if tab.push_fn is not None:
                 u = int(dd.ucount.sum())
                 tab.apply_custom(s[:u], dd.ugrad[:u])

@@ -247,3 +247,104 @@ def test_uneven_shards_collective_termination():
     assert set(merged) == set(ref)
     for k in ref:
         np.testing.assert_allclose(merged[k], ref[k], rtol=2e-5, atol=2e-6)
+
+
+def _init_rows(keys):
+    """user initialiser: w_j = key/1000 + j, AdaGrad state 0.5"""
+    k = keys.to(torch.float64)
+    w = torch.stack([k / 1000 + j for j in range(DIM)], 1)
+    return torch.cat([w, torch.full((len(keys), DIM), 0.5, dtype=torch.float64)], 1).float()
+
+
+def _pull_vals(keys, rows):
+    """user pull transform: parameters scaled by 1/sqrt(state)"""
+    return rows[:, :DIM] / rows[:, DIM:].sqrt()
+
+
+def _run_access_rank(rank, world, init, q):
+    init_gloo(init, rank, world)
+    try:
+        from swiftsnails_amd.ops.host_table import HostTable
+        from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+        from swiftsnails_amd.parallel.engine import PSEngine
+        from swiftsnails_amd.parallel.transport import TorchDistTransport
+
+        table = HostTable(DIM, 4, Optimizer("adagrad", lr=0.1), InitConfig("zero"))
+        table.set_init_method(_init_rows)
+        table.set_pull_method(_pull_vals)
+        eng = PSEngine(table, TorchDistTransport(), max_keys=300, dim=DIM, frag_num=64,
+                       device="cpu")
+        out = []
+        for rnd in range(3):
+            k = _keys_for(rank, rnd)
+            r = eng.pull(torch.from_numpy(k))
+            out.append((k, eng.gather(r).numpy().copy()))
+            eng.accumulate(r, torch.from_numpy(_grads_for(k, rank, rnd)))
+            eng.push(r)
+        q.put((rank, out, table.to_dict(with_state=True)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_user_init_and_pull_methods_world2():
+    """User access methods (the reference's PullAccessMethod::init_param and
+    get_pull_value as tensor code) on the servers of a 2-rank job: every key
+    is created with the user's rows, every pull returns the user's transform
+    of the stored row, and the merged AdaGrad updates apply to those rows."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = file_init()
+    procs = [ctx.Process(target=_run_access_rank, args=(r, 2, init, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = collect(q, procs, 2, 240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    state = {}
+    for _, _, st in res:
+        state.update(st)
+    check_access_results(res, state)
+
+
+def access_oracle(world=2, rounds=3):
+    """rows after `rounds` merged AdaGrad rounds (lr 0.1) of every rank's
+    keys from the user initialiser, and what each (rank, round) pulled"""
+    rows, pulled = {}, {}
+    for rnd in range(rounds):
+        for r in range(world):
+            k = _keys_for(r, rnd)
+            for x in k.tolist():
+                if x not in rows:
+                    rows[x] = _init_rows(torch.tensor([x])).numpy()[0].astype(np.float64)
+            pulled[(r, rnd)] = np.stack(
+                [rows[x][:DIM] / np.sqrt(rows[x][DIM:]) for x in k.tolist()])
+        acc = {}
+        for r in range(world):
+            k = _keys_for(r, rnd)
+            for x, g in zip(k.tolist(), _grads_for(k, r, rnd).astype(np.float64)):
+                acc[x] = acc.get(x, 0) + g
+        for x, g in acc.items():
+            rows[x][DIM:] += g * g
+            rows[x][:DIM] -= 0.1 * g / np.sqrt(rows[x][DIM:] + 1e-8)
+    return rows, pulled
+
+
+def check_access_results(res, state, world=2):
+    rows, pulled_ref = access_oracle(world)
+    for rank, out, _ in res:
+        for rnd, (k, vals) in enumerate(out):
+            np.testing.assert_allclose(vals, pulled_ref[(rank, rnd)], rtol=1e-4, atol=1e-5)
+    assert set(state) == set(rows)
+    for x, row in rows.items():
+        np.testing.assert_allclose(state[x], row, rtol=1e-4, atol=1e-5)
+
+
+def test_compiled_const_init():
+    from swiftsnails_amd.ops.host_table import HostTable
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+
+    t = HostTable(2, 2, Optimizer("adagrad"), InitConfig("const", scale=0.25, state_init=0.1))
+    v = t.pull_keys(np.array([3, 9], dtype=np.int64)).numpy()
+    np.testing.assert_allclose(v, 0.25)
+    np.testing.assert_allclose(t.to_dict(with_state=True)[3], [0.25, 0.25, 0.1, 0.1])

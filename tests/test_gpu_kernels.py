@@ -880,3 +880,42 @@ def test_push_method_set_after_engine_on_lr_table(dev):
     np.testing.assert_allclose(v.cpu().numpy()[:, 0], -0.5, rtol=1e-6)
     w = SparseLRWorker(eng, data)
     assert not w.enable_graph()
+
+
+def test_user_init_and_pull_methods_fast_path(dev):
+    """One GPU (fast path, bucketed pull): keys are created with the user's
+    rows, pulls return the user's transform, the compiled const init works,
+    and a push of never-pulled keys starts from the user's rows too."""
+    from test_engine_cpu import DIM, _grads_for, _init_rows, _keys_for, _pull_vals, access_oracle
+
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    t = HbmTable(DIM, 8192, Optimizer("adagrad", lr=0.1), InitConfig("zero"), device=dev)
+    t.set_init_method(lambda k: _init_rows(k.cpu()).to(dev))
+    t.set_pull_method(_pull_vals)
+    assert not t.snapshot_ok
+    eng = PSEngine(t, None, max_keys=300, dim=DIM, device=dev)
+    rows, pulled = access_oracle(world=1)  # one worker's stream
+    for rnd in range(3):
+        k = _keys_for(0, rnd)
+        r = eng.pull(torch.from_numpy(k).to(dev))
+        got = eng.gather(r, len(k)).cpu().numpy()
+        np.testing.assert_allclose(got, pulled[(0, rnd)], rtol=1e-4, atol=1e-5)
+        eng.accumulate(r, torch.from_numpy(_grads_for(k, 0, rnd)).to(dev))
+        eng.push(r)
+    torch.cuda.synchronize()
+    st = t.to_dict(with_state=True)
+    assert set(st) == set(rows)
+    for x, row in rows.items():
+        np.testing.assert_allclose(st[x], row, rtol=1e-4, atol=1e-5)
+    # a push creates keys with the user's rows before the update
+    t.push(torch.tensor([999_001], device=dev), torch.ones(1, DIM, device=dev))
+    row = t.to_dict(with_state=True)[999_001]
+    r0 = _init_rows(torch.tensor([999_001])).numpy()[0]
+    np.testing.assert_allclose(row[DIM:], r0[DIM:] + 1, rtol=1e-5)
+    # compiled constant initialiser
+    c = HbmTable(2, 1024, Optimizer("sgd"), InitConfig("const", scale=0.25), device=dev)
+    v, _ = c.pull(torch.tensor([5, 6], device=dev))
+    np.testing.assert_allclose(v.cpu().numpy(), 0.25)

@@ -351,3 +351,59 @@ def test_uneven_file_shards_terminate_together(tmp_path):
         for ln in (tmp_path / f"d.{n}.txt").read_text().splitlines():
             feats |= {int(t.split(":")[0]) for t in ln.split()[1:]}
     assert set(dumped) == feats  # both ranks' keys, each on exactly one shard
+
+
+def _run_access_rank_gpu(rank, world, init, q):
+    init_gloo(init, rank, world)
+    try:
+        from test_engine_cpu import _init_rows, _pull_vals
+
+        from swiftsnails_amd.ops.optim import InitConfig, Optimizer
+        from swiftsnails_amd.ops.table import HbmTable
+        from swiftsnails_amd.parallel.engine import PSEngine
+        from swiftsnails_amd.parallel.transport import TorchDistTransport
+        from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+        tr = XgmiTransport(rank, world, dev, dist.distributed_c10d._get_default_store(),
+                           aux=TorchDistTransport(), timeout_s=60)
+        table = HbmTable(DIM, 4096, Optimizer("adagrad", lr=0.1), InitConfig("zero"), device=dev)
+        table.set_init_method(lambda k: _init_rows(k.cpu()).to(dev))
+        table.set_pull_method(_pull_vals)
+        eng = PSEngine(table, tr, max_keys=300, dim=DIM, frag_num=64, device=dev)
+        out = []
+        for rnd in range(3):
+            from test_engine_cpu import _grads_for, _keys_for
+
+            k = _keys_for(rank, rnd)
+            r = eng.pull(torch.from_numpy(k).to(dev))
+            out.append((k, eng.gather(r, len(k)).cpu().numpy().copy()))
+            eng.accumulate(r, torch.from_numpy(_grads_for(k, rank, rnd)).to(dev))
+            eng.push(r)
+        torch.cuda.synchronize()
+        eng.check()
+        q.put((rank, out, table.to_dict(with_state=True)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_user_init_and_pull_methods_world2_gpu():
+    """User init / pull methods (tensor code) on HBM shards of a 2-process
+    job over the xGMI mailboxes: the same oracle as the CPU test."""
+    from test_engine_cpu import check_access_results
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    init = file_init()
+    procs = [ctx.Process(target=_run_access_rank_gpu, args=(r, 2, init, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = collect(q, procs, 2, 240)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    state = {}
+    for _, _, st in res:
+        state.update(st)
+    check_access_results(res, state)
