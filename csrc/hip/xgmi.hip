@@ -158,6 +158,30 @@ __global__ __launch_bounds__(64) void k_xwait(char* arena, XWait W,
   if (s == 0) waited[W.ch] = target;
 }
 
+// per-round exchange counters without a host sync and in one launch:
+// acc[0] += sum(sent), acc[1] += sum(recv), acc[2] += bytes_per_key * both
+__global__ __launch_bounds__(64) void k_xmetrics(const long long* sent, const long long* recv,
+                                                 int n, double bytes_per_key, double* acc) {
+  if (threadIdx.x != 0) return;
+  long long a = 0, b = 0;
+  for (int i = 0; i < n; ++i) {
+    a += sent[i];
+    b += recv[i];
+  }
+  acc[0] += (double)a;
+  acc[1] += (double)b;
+  acc[2] += bytes_per_key * (double)(a + b);
+}
+
+void launch_xmetrics(uintptr_t sent, uintptr_t recv, int n, double bytes_per_key, uintptr_t acc,
+                     uintptr_t st) {
+  hipLaunchKernelGGL(k_xmetrics, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(st),
+                     reinterpret_cast<const long long*>(sent),
+                     reinterpret_cast<const long long*>(recv), n, bytes_per_key,
+                     reinterpret_cast<double*>(acc));
+  check_launch("k_xmetrics");
+}
+
 // ---------------------------------------------------------------- host side
 class XgmiArena {
  public:
@@ -360,4 +384,6 @@ void bind_xgmi(py::module_& m) {
       .def("wait", &XgmiArena::wait, py::arg("ch"), py::arg("fixed"), py::arg("timeout_s"),
            py::arg("stream"));
   m.def("xgmi_flag_bytes", &ss::xgmi_flag_bytes);
+  m.def("xmetrics", &ss::launch_xmetrics, py::arg("sent"), py::arg("recv"), py::arg("n"),
+        py::arg("bytes_per_key"), py::arg("acc"), py::arg("st"));
 }

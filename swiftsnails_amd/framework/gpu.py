@@ -1,18 +1,23 @@
-"""MI355X collective mode: one process per GPU, HBM shards, RCCL rounds.
+"""MI355X collective mode: one process per GPU, HBM shards, collective rounds.
 
 This is the GPU-native counterpart of the reference's three roles
 (/root/reference/src/core/framework/Swift{Master,Server,Worker}.h):
 
-* master   -> rank 0 + the torch.distributed TCPStore: rendezvous,
-              RCCL unique-id broadcast, the role table, termination barrier
-              (replaces registration/route/hashfrag messages, S3-S5, S8);
+* master   -> rank 0 + the torch.distributed TCPStore: rendezvous, the
+              mailbox IPC handles / RCCL unique-id broadcast, the role table,
+              the termination agreement (replaces registration / route /
+              hashfrag messages, S3-S5, S8);
 * server   -> the ranks in ``server_ranks``: an ``HbmTable`` shard each;
 * worker   -> the ranks in ``worker_ranks``: a model worker each.
-Colocated (every rank both) is the default; "4 servers + 4 workers" is
-``server_ranks: 0,1,2,3`` / ``worker_ranks: 4,5,6,7``.
+Colocated (every rank both) is the default: "4 servers + 4 workers on 4
+GPUs" (BASELINE config 3) is 4 colocated ranks; split roles are
+``server_ranks`` / ``worker_ranks`` (e.g. 0,1,2,3 / 4,5,6,7 on 8 ranks).
 
-``PSContext`` owns the per-rank pieces (process group, two RCCL
-communicators, table, round engine) and the reference's periodic backup /
+Data plane (``transport``): ``auto`` (default) = the xGMI mailboxes
+(parallel/xgmi.py, device-side counts), falling back to RCCL if their
+start-up self-test fails on any rank; ``xgmi``; ``rccl``; ``gloo`` (host-
+staged, tests).  ``PSContext`` owns the per-rank pieces (process group,
+transport, table, round engine) and the reference's periodic backup /
 final dump behaviour (``param_backup_period``/``param_backup_root`` counted
 in rounds, ``param_output`` at the end), plus resume (``resume_from``), which
 the reference lacks.  ``run_training`` drives a model from a config.

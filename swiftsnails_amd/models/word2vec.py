@@ -1,7 +1,8 @@
 """word2vec skip-gram with (shared) negative sampling on the parameter server.
 
 BASELINE config 3: 1M-vocab synthetic corpus, 4 servers + 4 workers on 4
-MI355X.  The reference's word2vec app is absent from the snapshot (named by
+MI355X (4 colocated ranks: each GPU one server shard and one worker).  The
+reference's word2vec app is absent from the snapshot (named by
 /root/reference/src/tools/copy_exec.sh:4-9); its corpus generator
 (src/tools/gen-word2vec-data.py: lines of 6-15 random word ids) is mirrored by
 ``W2VSynth`` at scale, and the dense-vector math of utils/vec1.h (dot, scaled

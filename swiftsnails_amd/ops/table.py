@@ -132,8 +132,8 @@ class HbmTable:
         self.storage = torch.empty(cap * self.stride, dtype=torch.uint8, device=self.device)
         # key-independent init (zero): fill every row with the initial row up
         # front, so an insert is the key CAS alone (SS_TABLE_PREFILL=0: off)
-        self.prefilled = (self.init_cfg.kind == "zero" and
-                          os.environ.get("SS_TABLE_PREFILL", "1") != "0")
+        self.prefilled = (self.init_cfg.kind == "zero" and getattr(self, "init_fn", None) is None
+                          and os.environ.get("SS_TABLE_PREFILL", "1") != "0")
         if self.prefilled:
             self.storage.zero_()
             slots = self.storage.view(cap, self.stride)
@@ -147,8 +147,14 @@ class HbmTable:
         # sharded counter: 256 shards x 128 B (see ss_device.h ctr_add)
         self.size_ctr = torch.zeros(CTR_SHARDS * 16, dtype=torch.int64, device=self.device)
         self.err = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.dt = hip().DevTable(self.storage.data_ptr(), cap, self.stride, self.key_off, self.dim,
-                                 self.width, int(self.prefilled), self.row_off)
+        self._make_dt()
+
+    def _make_dt(self):
+        # a tensor-code initialiser needs the insert to write its marker row
+        # (the prefilled fast path writes nothing on insert)
+        self.dt = hip().DevTable(self.storage.data_ptr(), self.capacity, self.stride,
+                                 self.key_off, self.dim, self.width,
+                                 int(self.prefilled and self.init_fn is None), self.row_off)
 
     @staticmethod
     def plan(n_keys: int, dim: int, optimizer: Optional[Optimizer] = None,
@@ -233,9 +239,19 @@ class HbmTable:
         state) of keys a pull creates.  The device insert writes a NaN marker
         row; ``finish_pull`` finds the marked rows among a pull's and replaces
         them.  ``None`` restores the compiled initialiser."""
+        was = self.init_fn
         self.init_fn = fn
         self._init_native = (InitConfig("marker", state_init=self.init_cfg.state_init).native()
                              if fn is not None else self.init_cfg.native())
+        if fn is not None and was is None and self.prefilled:
+            # empty rows hold the prefilled initial row; a concurrent reader
+            # of a key being inserted must see the 0xFF "not written yet"
+            # pattern instead (table.hip fresh_or)
+            empty = self.keys_view() == EMPTY_I64
+            rv = self.rows_view()
+            rv[empty] = torch.tensor(-1, dtype=torch.int32, device=self.device).view(
+                torch.float32)
+        self._make_dt()
         self.version += 1
 
     def set_pull_method(self, fn) -> None:

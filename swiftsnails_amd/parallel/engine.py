@@ -433,7 +433,8 @@ class PSEngine:
         h.srv_fill(self.Ps, S.bstart.data_ptr(), S.ubase.data_ptr(), S.unum.data_ptr(),
                    S.pj.data_ptr(), S.luid.data_ptr(), self.svals.data_ptr(),
                    self.rvals.data_ptr(), self.dim, st)
-        self.metrics.add_device(server_unique=S.ucount)
+        sacc = self.metrics.device_block(("server_unique",), self.device)
+        sacc.add_(S.ucount)  # (one tiny kernel, no sync)
 
     def _server_pull_cpu(self, rcounts: np.ndarray):
         """Host server: distinct keys of all sources, looked up once."""
@@ -458,10 +459,9 @@ class PSEngine:
         rc = xg.counts("keys", 0, slot)
         xg.put("vals", slot, [(self.rvals, self.displs, rc, None, self.dim)], stream=stream)
         xg.wait("vals", slot, stream)
-        with use_stream(stream):
-            sent, recv = dd.ucount.sum(), rc.sum()
-            self.metrics.add_device(unique_sent=sent, unique_recv=recv,
-                                    a2a_bytes=(8 + 8 * self.dim) * (sent + recv))
+        acc = self.metrics.device_block(("unique_sent", "unique_recv", "a2a_bytes"), self.device)
+        _hip().xmetrics(dd.ucount.data_ptr(), rc.data_ptr(), self.world, 8.0 + 8.0 * self.dim,
+                        acc.data_ptr(), stream.cuda_stream)
         self.metrics.add(occurrences=dd.n)
         return Round(dd, self.uvals[slot], slot)
 

@@ -55,10 +55,10 @@ class XgmiTransport(Transport):
         self.arena = None
         self._ch: dict[str, int] = {}
         self._layout: dict = {}
-        # workgroups per peer of a put: a put is latency-bound per
-        # workgroup (16 B per lane per iteration), so a 42 MB segment needs
-        # ~100+ of them; 32 measured 211 us for the 1-GPU keys put
-        self.bpp = int(os.environ.get("SS_XGMI_BPP", "128"))
+        # workgroups per peer of a put (~1024 in all): a put is latency-bound
+        # per workgroup (16 B per lane per iteration); 32 per peer measured
+        # 211 us for the 42 MB keys put of a 1-rank arena
+        self.bpp = int(os.environ.get("SS_XGMI_BPP", "0")) or max(128, 1024 // self.world)
 
     # ------------------------------------------------------------ set-up
     def setup(self, channels: dict) -> None:

@@ -99,7 +99,7 @@ KNOBS: dict[str, Knob] = {
     "SS_XGMI_TIMEOUT": Knob("120", "parallel/xgmi.py", "ops",
                             "seconds a mailbox wait spins for a peer before it gives up (sticky "
                             "error raised at the next check point)"),
-    "SS_XGMI_BPP": Knob("128", "parallel/xgmi.py", "tuning",
+    "SS_XGMI_BPP": Knob("max(128, 1024 / world)", "parallel/xgmi.py", "tuning",
                         "workgroups per peer of a mailbox put"),
     # -- experiments (measured slower or neutral; kept for re-measurement)
     "SS_ENGINE_GENERAL": Knob("0", "parallel/engine.py, bench.py", "experiment",

@@ -103,6 +103,16 @@ class Metrics:
         for k, v in kw.items():
             self._host[k] += v
 
+    def device_block(self, names, device) -> torch.Tensor:
+        """A persistent float64 device vector whose entries accumulate the
+        counters ``names`` (a kernel adds into it; folded into ``counters``
+        when read)."""
+        key = tuple(names)
+        blk = self._dev.get(key)
+        if blk is None:
+            blk = self._dev[key] = torch.zeros(len(names), dtype=torch.float64, device=device)
+        return blk
+
     def add_device(self, **kw):
         for k, v in kw.items():
             acc = self._dev.get(k)
@@ -114,7 +124,11 @@ class Metrics:
     def counters(self) -> dict:
         out = defaultdict(float, self._host)
         for k, acc in self._dev.items():
-            out[k] += float(acc.item())
+            if isinstance(k, tuple):
+                for name, v in zip(k, acc.tolist()):
+                    out[name] += v
+            else:
+                out[k] += float(acc.item())
         return out
 
     def rates(self) -> dict:

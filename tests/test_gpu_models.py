@@ -637,3 +637,54 @@ def test_bench_graph_mode_times_whole_periods():
     assert g["config"]["hipgraph"] is True and e["config"]["hipgraph"] is False
     assert g["steps"] == 12 and g["ms_per_step"] > 0
     assert g["config"]["loss_last"] == pytest.approx(e["config"]["loss_last"], rel=1e-4, abs=1e-5)
+
+
+def _planted_corpus(path, clusters=20, words=40, sentences=6000, length=12, seed=5):
+    """Sentences of one cluster each: word ids c*1000 + i (i < words)."""
+    rng = np.random.default_rng(seed)
+    with open(path, "w") as f:
+        for _ in range(sentences):
+            c = int(rng.integers(clusters))
+            ids = c * 1000 + rng.integers(0, words, size=length)
+            f.write(" ".join(str(int(x)) for x in ids) + "\n")
+    return clusters, words
+
+
+@pytest.mark.parametrize("tile", ["bf16", "f32"])
+@pytest.mark.parametrize("mode", ["window", "pairs"])
+def test_word2vec_learns_planted_clusters(dev, tmp_path, monkeypatch, tile, mode):
+    """Embedding quality, not just a falling loss: on a corpus whose
+    sentences each draw from one of 20 word clusters, the learned input
+    vectors of words of the same cluster are far more similar (cosine) than
+    of words of different clusters — for both batch layouts and both MFMA
+    tile precisions of the shared-negative objective."""
+    from swiftsnails_amd.models.word2vec import Word2VecWorker, make_w2v_table_args
+    from swiftsnails_amd.ops.table import HbmTable
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.utils.dataio import FileCorpusSource
+
+    monkeypatch.setenv("SS_W2V_MFMA", tile)
+    C, M = _planted_corpus(tmp_path / "corpus.txt")
+    data = FileCorpusSource(str(tmp_path / "corpus.txt"), batch_size=2048, window=4,
+                            negatives=5, mode=mode, device=dev)
+    opt, init = make_w2v_table_args(64, None)
+    table = HbmTable(64, 1 << 14, optimizer=opt, init=init, device=dev)
+    eng = PSEngine(table, None, max_keys=data.n_keys, dim=64, device=dev)
+    w = Word2VecWorker(eng, data)
+    assert w.mfma_bf16 == (tile == "bf16")
+    for _ in range(3 * data.steps_per_pass()):  # 3 passes
+        w.step()
+    torch.cuda.synchronize()
+    table.check()
+    ids = torch.tensor([c * 1000 + i for c in range(C) for i in range(M)], device=dev)
+    v, _ = table.pull(ids, insert=False)
+    v = torch.nn.functional.normalize(v.double(), dim=1).cpu().numpy()
+    sim = v @ v.T
+    lab = np.repeat(np.arange(C), M)
+    same = lab[:, None] == lab[None, :]
+    off = ~np.eye(len(lab), dtype=bool)
+    within, across = sim[same & off].mean(), sim[~same].mean()
+    assert within - across > 0.4, (within, across)
+    # nearest neighbour of almost every word is in its own cluster
+    np.fill_diagonal(sim, -2)
+    assert (lab[sim.argmax(1)] == lab).mean() > 0.95

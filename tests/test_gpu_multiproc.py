@@ -331,7 +331,8 @@ def test_uneven_file_shards_terminate_together(tmp_path):
            "--set", f"data_path={tmp_path}/d.{{rank}}.txt", "--set", "data_format=libsvm",
            "--set", "batch_size=64", "--set", "num_fields=8", "--set", "num_iters=2",
            "--set", "done_check_every=4", "--set", "table_capacity=100000",
-           "--set", f"param_output={out}", "--set", "param_output_format=text"]
+           "--set", f"param_output={out}", "--set", "param_output_format=text",
+           "--set", "transport=xgmi"]
     env = dict(os.environ, GLOO_SOCKET_IFNAME="lo", SS_DEVICE="0", PYTHONPATH=root)
     r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]

@@ -44,6 +44,11 @@ for s in "${STEP_LIST[@]}"; do
     prof_xgmi) run rocprof_xgmi 600 env SS_ENGINE_GENERAL=xgmi rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_xgmi" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
     rehearse8) run rehearse8 900 python tools/rehearse_world.py --world 8 --steps 20 --warmup 4 ;;
     general3) run bench_general3 600 env SS_ENGINE_GENERAL=rccl SS_RCCL_COMMS=3 python bench.py $BENCH_ARGS ;;
+    graph_lr4k) run graph_lr4k 600 env SS_ENGINE_GENERAL=xgmi python bench.py --batch 4096 --steps 64 --warmup 16 --graph on ;;
+    eager_lr4k) run eager_lr4k 600 env SS_ENGINE_GENERAL=xgmi python bench.py --batch 4096 --steps 64 --warmup 16 ;;
+    fast_lr4k) run fast_lr4k 600 python bench.py --batch 4096 --steps 64 --warmup 16 --graph on ;;
+    graph_w2v) run graph_w2v 600 env SS_ENGINE_GENERAL=xgmi python -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 64 --warmup 16 ;;
+    fast_w2v) run fast_w2v 600 python -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 64 --warmup 16 ;;
     general_nopa) run bench_general_nopa 600 env SS_ENGINE_GENERAL=rccl SS_PULL_AHEAD=0 python bench.py $BENCH_ARGS ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
     *) run custom$n 600 bash -c "$s" ;;
