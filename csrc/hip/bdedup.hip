@@ -289,8 +289,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      uint32_t* __restrict__ pj,
                                                      uint32_t* __restrict__ pos_of,
                                                      uint32_t* __restrict__ bkt,
-                                                     uint32_t* __restrict__ osi_inv,
-                                                     uint64_t* __restrict__ skeys) {
+                                                     uint32_t* __restrict__ osi_inv) {
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
@@ -314,7 +313,6 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
           b = bd_bucket(k[e], rs, (uint32_t)Pd);
           pos = atomicAdd(&cur[b], 1u);
           pj[pos] = (uint32_t)j;
-          if (skeys) skeys[pos] = k[e];  // keys staged in bucket order for the dedup
         } else if (osi_inv) {
           osi_inv[j] = kBdInvalid;  // never reaches a bucket
         }
@@ -341,8 +339,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    unsigned long long* __restrict__ dbg,
                                                    uint64_t* __restrict__ ukeys,
                                                    float* __restrict__ ugrad, int gdim,
-                                                   uint8_t* __restrict__ usingle,
-                                                   const uint64_t* __restrict__ skeys) {
+                                                   uint8_t* __restrict__ usingle) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
   if (dbg && t == 0) dbg[(long long)b * 8 + (i)] = wall_clock64();
@@ -366,11 +363,11 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
     const uint32_t p = p0 + t + r * kBdDT;
-    // staged keys (skeys: this bucket's range of the bkeys buffer, written
-    // by the scatter; overwritten only by this workgroup's compaction below)
-    // are read coalesced; else gathered at keys[pj[p]]
-    jr[r] = p < p1 && (!skeys || osi_inv) ? pj[p] : 0u;
-    kk[r] = p < p1 ? (skeys ? skeys[p] : keys[jr[r]]) : kEmptyKey;
+    // keys gathered at keys[pj[p]] (staging them in bucket order in the
+    // scatter for a coalesced read here measured slower: 0.949 -> 0.968
+    // ms/step, the extra stores cost the scatter more than the gather saves)
+    jr[r] = p < p1 ? pj[p] : 0u;
+    kk[r] = p < p1 ? keys[jr[r]] : kEmptyKey;
   }
   __syncthreads();
   BD_STAMP(0)
@@ -406,7 +403,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
 #pragma unroll
     for (int r = 0; r < kBdRegs; ++r) {
       const uint32_t p = q + r * kBdDT;
-      k2[r] = p < p1 ? (skeys ? skeys[p] : keys[pj[p]]) : kEmptyKey;
+      k2[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
     }
 #pragma unroll
     for (int r = 0; r < kBdRegs; ++r) {
@@ -941,25 +938,15 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
 #undef SS_BD_CS_CASE
   }
   check_launch("k_bd_colscan");
-  // SS_BD_STAGE=1: the scatter also writes each key at its bucket position
-  // (into bkeys, which the dedup overwrites with unique keys only after it has
-  // read its bucket's occurrences), so the dedup reads keys coalesced instead
-  // of gathering keys[pj[p]].  Measured slower (0.968 vs 0.949 ms/step): the
-  // extra bucket-order stores cost the scatter more than the gather saves
-  static const bool stage = [] {
-    const char* e = std::getenv("SS_BD_STAGE");
-    return e && std::atoi(e) != 0;
-  }();
-  uint64_t* skeys = stage && bkeys ? bkeys : nullptr;
   SS_BD_CT_DISPATCH(ct, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pj,
-                    pos_of, bkt, osi_inv, skeys);
+                    pos_of, bkt, osi_inv);
 #undef SS_BD_CT_DISPATCH
   check_launch("k_bd_scatter");
   // place: unique keys straight into the per-destination send segments
   // (+ zeroed gradient rows), reserved with one atomic per bucket
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                      bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount, osi_inv, dbg,
-                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, skeys);
+                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle);
   check_launch("k_bd_dedup");
   if (inv && n > 0) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");

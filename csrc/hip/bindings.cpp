@@ -122,40 +122,20 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("pull_unique_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
                              uintptr_t ubase, int P_, uintptr_t slots, uintptr_t out,
                              const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
-                             uintptr_t st, int osi, uintptr_t snap) {
+                             uintptr_t st, uintptr_t snap) {
     launch_pull_unique_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
                           P<const uint32_t>(unum), P<const uint32_t>(ubase), P_,
                           P<long long>(slots), P<float>(out), ip, P<unsigned long long>(size_ctr),
-                          P<int>(err), G, osi, S(st), P<float>(snap));
+                          P<int>(err), G, S(st), P<float>(snap));
   }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
      py::arg("P"), py::arg("slots"), py::arg("out"), py::arg("ip"), py::arg("size_ctr"),
-     py::arg("err"), py::arg("G"), py::arg("st"), py::arg("osi") = 0, py::arg("snap") = 0);
-  m.def("pull_fill_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
-                           uintptr_t ubase, int P_, uintptr_t slots, uintptr_t out,
-                           const InitParams& ip, uintptr_t size_ctr, uintptr_t err, uintptr_t snap,
-                           uintptr_t luid, uintptr_t occ, uintptr_t st) {
-    launch_pull_fill_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
-                        P<const uint32_t>(unum), P<const uint32_t>(ubase), P_, P<long long>(slots),
-                        P<float>(out), ip, P<unsigned long long>(size_ctr), P<int>(err),
-                        P<float>(snap), P<const uint32_t>(luid), P<float>(occ), S(st));
-  });
-  m.def("pull_claim", [](const DevTable& t, uintptr_t keys, const SegList& sl, long long max_n,
-                         uintptr_t slots, uintptr_t out, const InitParams& ip, uintptr_t size_ctr,
-                         uintptr_t err, int G, uintptr_t st) {
-    launch_pull_claim(t, P<const uint64_t>(keys), sl, max_n, P<long long>(slots), P<float>(out),
-                      ip, P<unsigned long long>(size_ctr), P<int>(err), G, S(st));
-  });
+     py::arg("err"), py::arg("G"), py::arg("st"), py::arg("snap") = 0);
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
                     long long max_n, const OptParams& op, int G, uintptr_t st, uintptr_t snap) {
     launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st),
                  P<const float>(snap));
   }, py::arg("t"), py::arg("slots"), py::arg("grads"), py::arg("sl"), py::arg("max_n"),
      py::arg("op"), py::arg("G"), py::arg("st"), py::arg("snap") = 0);
-  m.def("apply_bk", [](const DevTable& t, uintptr_t slots, uintptr_t grads, uintptr_t bstart,
-                       uintptr_t unum, int P_, const OptParams& op, int G, uintptr_t st) {
-    launch_apply_bk(t, P<const long long>(slots), P<const float>(grads), P<const uint32_t>(bstart),
-                    P<const uint32_t>(unum), P_, op, G, S(st));
-  });
   m.def("assign", [](const DevTable& t, uintptr_t keys, uintptr_t rows, long long n,
                      uintptr_t size_ctr, uintptr_t err, int G, uintptr_t st) {
     launch_assign(t, P<const uint64_t>(keys), P<const float>(rows), n,
@@ -441,21 +421,13 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("w2v_sgns", [](uintptr_t inv_c, uintptr_t inv_x, uintptr_t inv_n, int B, int C, int D,
                        float neg_scale, uintptr_t uvals, uintptr_t ugrad, uintptr_t loss,
-                       uintptr_t st, uintptr_t gpos, int bf16) {
+                       uintptr_t st, int bf16) {
     launch_w2v_sgns(P<const uint32_t>(inv_c), P<const uint32_t>(inv_x), P<const uint32_t>(inv_n), B,
                     C, D, neg_scale, P<const float>(uvals), P<float>(ugrad), P<float>(loss), S(st),
-                    P<float>(gpos), bf16);
+                    bf16);
   }, py::arg("inv_c"), py::arg("inv_x"), py::arg("inv_n"), py::arg("B"), py::arg("C"),
      py::arg("D"), py::arg("neg_scale"), py::arg("uvals"), py::arg("ugrad"), py::arg("loss"),
-     py::arg("st"), py::arg("gpos") = 0, py::arg("bf16") = 0);
-  m.def("w2v_ctx_reduce", [](int P_, uintptr_t bstart, uintptr_t unum, uintptr_t ubase,
-                             uintptr_t pj, uintptr_t luid, uintptr_t inv_c, uintptr_t gpos, int B,
-                             int C, int D, uintptr_t uvals, uintptr_t ugrad, uintptr_t st) {
-    launch_w2v_ctx_reduce(P_, P<const uint32_t>(bstart), P<const uint32_t>(unum),
-                          P<const uint32_t>(ubase), P<const uint32_t>(pj), P<const uint32_t>(luid),
-                          P<const uint32_t>(inv_c), P<const float>(gpos), B, C, D,
-                          P<const float>(uvals), P<float>(ugrad), S(st));
-  });
+     py::arg("st"), py::arg("bf16") = 0);
   m.def("w2v_win", [](uintptr_t inv_c, uintptr_t inv_w, uintptr_t inv_n, uintptr_t meta, int B,
                       int W, int D, float neg_per_pair, uintptr_t uvals, uintptr_t ugrad,
                       uintptr_t loss, uintptr_t pairs, uintptr_t st, uintptr_t ograd,

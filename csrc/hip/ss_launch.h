@@ -32,20 +32,10 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, int osi, hipStream_t st, float* snap = nullptr);
-void launch_pull_fill_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
-                         const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
-                         float* out, const InitParams& ip, unsigned long long* size_ctr, int* err,
-                         float* snap, const uint32_t* luid, float* occ, hipStream_t st);
-void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
-                       long long max_n, long long* slots, float* out, const InitParams& ip,
-                       unsigned long long* size_ctr, int* err, int G, hipStream_t st);
+                           int* err, int G, hipStream_t st, float* snap = nullptr);
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
                   const float* snap = nullptr);
-void launch_apply_bk(const DevTable& t, const long long* slots, const float* grads,
-                     const uint32_t* bstart, const uint32_t* unum, int P, const OptParams& op,
-                     int G, hipStream_t st);
 void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, long long n,
                    unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,
@@ -203,11 +193,7 @@ void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
 size_t w2v_smem_bytes(int D);
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
-                     float* loss_sum, hipStream_t st, float* gpos = nullptr, int bf16 = 0);
-void launch_w2v_ctx_reduce(int P, const uint32_t* bstart, const uint32_t* unum,
-                           const uint32_t* ubase, const uint32_t* pj, const uint32_t* luid,
-                           const uint32_t* inv_c, const float* gpos, int B, int C, int D,
-                           const float* uvals, float* ugrad, hipStream_t st);
+                     float* loss_sum, hipStream_t st, int bf16 = 0);
 void launch_w2v_gen(uint64_t seed, long long base, int B, int C, int W, long long nneg,
                     long long V, float noise, uint64_t* keys, hipStream_t st,
                     const long long* step_dev = nullptr, long long step_mul = 0,

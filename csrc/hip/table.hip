@@ -265,8 +265,7 @@ template <int G>
 __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t* __restrict__ keys,
                                                      SegList sl, long long* __restrict__ slots_out,
                                                      float* __restrict__ out, InitParams ip,
-                                                     unsigned long long* size_ctr, int* err,
-                                                     int one16) {
+                                                     unsigned long long* size_ctr, int* err) {
   const long long total = seg_total(sl);
   const int lg = threadIdx.x % G;
   const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
@@ -275,7 +274,7 @@ __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t*
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    pull_one<G>(t, keys[pos], pos, slots_out, out, ip, err, lg, ins, nullptr, one16);
+    pull_one<G>(t, keys[pos], pos, slots_out, out, ip, err, lg, ins);
   }
   ins = wave_sum_u64(ins);
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
@@ -283,8 +282,7 @@ __global__ __launch_bounds__(256) void k_pull_unique(DevTable t, const uint64_t*
 
 // Same, straight from the bucketed dedup's per-bucket staging (bdedup.hip):
 // workgroup b pulls bucket b's unique keys bkeys[bstart[b] + l] to unique id
-// ubase[b] + l (or bstart[b] + l, osi) — the colocated 1-GPU path needs no
-// send-segment copy.
+// ubase[b] + l — the colocated 1-GPU path needs no send-segment copy.
 template <int G>
 __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64_t* __restrict__ bkeys,
                                                         const uint32_t* __restrict__ bstart,
@@ -293,12 +291,9 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
                                                         long long* __restrict__ slots_out,
                                                         float* __restrict__ out, InitParams ip,
                                                         unsigned long long* size_ctr, int* err,
-                                                        int osi, float2* __restrict__ snap,
-                                                        int one16) {
+                                                        float2* __restrict__ snap, int one16) {
   const int b = blockIdx.x, lg = threadIdx.x % G;
-  // osi: rows at occurrence-space ids bstart[b] + l (bdedup.hip), else at the
-  // compact unique ids ubase[b] + l
-  const uint32_t nu = unum[b], base = osi ? bstart[b] : ubase[b];
+  const uint32_t nu = unum[b], base = ubase[b];
   const uint64_t* src = bkeys + bstart[b];
   unsigned long long ins = 0;
   // gridDim.y workgroups share a bucket (fewer serial probes per lane)
@@ -309,163 +304,8 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
 }
 
-// Pull + occurrence fill fused (sparse LR, one GPU, snapshot pull on 16-byte
-// slots): one 1024-thread workgroup per dedup bucket probes the bucket's
-// unique keys (one 16-byte load per probe step), keeps the pulled weights in
-// LDS and then writes every occurrence's parameter in bucket-position order,
-// occ[p] = w[luid[p]] (k_bd_fill_occ's job) — no second pass over the rows
-// and no launch boundary between the two.
-static constexpr int kFillMax = 4096;  // unique keys per bucket (bdedup.hip kBdTS)
-
-__global__ __launch_bounds__(1024) void k_pull_fill_bk(
-    DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
-    const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
-    long long* __restrict__ slots_out, float* __restrict__ out, InitParams ip,
-    unsigned long long* size_ctr, int* err, float2* __restrict__ snap,
-    const uint32_t* __restrict__ luid, float* __restrict__ occ) {
-  __shared__ float sv[kFillMax];
-  const int b = blockIdx.x;
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
-  const uint32_t nu = min(unum[b], (uint32_t)kFillMax), base = ubase[b];
-  const uint64_t* src = bkeys + p0;
-  unsigned long long ins = 0;
-  for (uint32_t l = threadIdx.x; l < nu; l += 1024) {
-    pull_one<1>(t, src[l], (long long)base + l, slots_out, out, ip, err, 0, ins, snap, 1);
-    sv[l] = out[base + l];  // this lane's own store: visible to it
-  }
-  ins = wave_sum_u64(ins);
-  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
-  __syncthreads();
-  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 2 * 1024) {
-    uint32_t l[2];
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const uint32_t p = pb + r * 1024;
-      l[r] = p < p1 ? luid[p] : 0xFFFFFFFFu;
-    }
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const uint32_t p = pb + r * 1024;
-      if (p < p1) occ[p] = l[r] < nu ? sv[l[r]] : 0.f;
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------
-// CAS-free insert for key lists that are unique within the launch.
-//
-// Measured on MI355X: every device-scope atomic executes at the memory side
-// (the 8 XCD L2s are not coherent), so a 64-bit CAS per new key made the
-// fused pull_unique atomic-throughput bound (1.3M CAS ≈ 320 µs/step).  Here a
-// new key is claimed OPTIMISTICALLY with a plain 8-byte store into the first
-// empty slot of its probe sequence (pass 1); after the kernel boundary, pass 2
-// re-reads the slot: the key that is there owns it (an aligned 8-byte store is
-// single-copy atomic, so a slot holds exactly one of the racing keys), the
-// rare losers finish with the CAS probe (continuing at their slot).  Correct
-// because (a) keys are unique, so a loser's key is nowhere else in the table,
-// (b) slots only ever go EMPTY -> key, so a present key is always met before
-// the first empty slot of its sequence, and (c) pass 2 never plain-stores.
-static constexpr long long kPending = 1ll << 62;
-
-template <int G>
-__global__ __launch_bounds__(256) void k_pull_claim(DevTable t, const uint64_t* __restrict__ keys,
-                                                    SegList sl, long long* __restrict__ slots_out,
-                                                    float* __restrict__ out, int* err) {
-  const long long total = seg_total(sl);
-  const int lg = threadIdx.x % G;
-  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
-  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
-       g += ngroups) {
-    int seg;
-    const long long pos = seg_pos(sl, g, &seg);
-    const uint64_t key = keys[pos];
-    long long slot = -1;
-    if (lg == 0) {
-      if (key == kEmptyKey) {
-        atomicOr(err, 2);
-      } else {
-        uint64_t s = fastrange64(table_hash(key), t.cap);
-        for (uint64_t n = 0; n < t.cap; ++n) {
-          uint64_t* kp = slot_key(t, s);
-          const uint64_t k = *kp;
-          if (k == key) {
-            slot = (long long)s;
-            break;
-          }
-          if (k == kEmptyKey) {
-            *kp = key;  // optimistic claim, verified after the kernel boundary
-            slot = (long long)s | kPending;
-            break;
-          }
-          s = (s + 1 == t.cap) ? 0 : s + 1;
-        }
-        if (slot < 0) atomicOr(err, 1);
-      }
-      slots_out[pos] = slot;
-    }
-    if (G > 1) slot = __shfl(slot, 0, G);
-    if (slot >= 0 && !(slot & kPending)) {  // present: gather now
-      const float* row = slot_row(t, slot);
-      float* o = out + pos * (long long)t.dim;
-      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
-    }
-  }
-}
-
-template <int G>
-__global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t* __restrict__ keys,
-                                                     SegList sl, long long* __restrict__ slots_out,
-                                                     float* __restrict__ out, InitParams ip,
-                                                     unsigned long long* size_ctr, int* err) {
-  const long long total = seg_total(sl);
-  const int lg = threadIdx.x % G;
-  const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
-  unsigned long long ins = 0;
-  for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
-       g += ngroups) {
-    int seg;
-    const long long pos = seg_pos(sl, g, &seg);
-    long long slot = slots_out[pos];
-    if (slot < 0 || !(slot & kPending)) continue;  // group-uniform: same pos per group
-    const uint64_t key = keys[pos];
-    int inserted = 0;
-    if (lg == 0) {
-      slot &= ~kPending;
-      if (*slot_key(t, (uint64_t)slot) == key) {
-        inserted = 1;  // our optimistic claim stood
-      } else {
-        bool b = false;
-        slot = probe_slot(t, key, true, &b);  // lost the race: CAS from here on
-        inserted = b;
-        if (slot < 0) atomicOr(err, 1);
-      }
-      slots_out[pos] = slot;
-    }
-    if (G > 1) {
-      slot = __shfl(slot, 0, G);
-      inserted = __shfl(inserted, 0, G);
-    }
-    float* o = out + pos * (long long)t.dim;
-    if (slot < 0) {
-      for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
-      continue;
-    }
-    float* row = slot_row(t, slot);
-    if (inserted) {
-      for (uint32_t j = lg; j < t.width; j += G) {
-        const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
-        if (!t.prefilled) row[j] = v;
-        if (j < t.dim) o[j] = v;
-      }
-    } else {
-      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
-    }
-    ins += (lg == 0 && inserted);
-  }
-  ins = wave_sum_u64(ins);
-  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
-}
-
 // K5: fused optimizer update on resolved slots. Keys inside one launch must be
 // unique (the host launches one segment per source rank, in rank order, so
 // duplicate keys from different workers are applied sequentially — no lost
@@ -474,11 +314,10 @@ __global__ __launch_bounds__(256) void k_pull_verify(DevTable t, const uint64_t*
 template <int G>
 __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
                                           const float* __restrict__ gr, const OptParams& op,
-                                          int lg, bool vec = true,
-                                          const float2* __restrict__ snap = nullptr) {
+                                          int lg, const float2* __restrict__ snap = nullptr) {
   if (slot < 0) return;
   float* row = slot_row(t, slot);
-  if (G == 1 && t.dim == 1 && op.kind == kOptAdaGrad && vec &&
+  if (G == 1 && t.dim == 1 && op.kind == kOptAdaGrad &&
       t.row_off % 8 == 0 && t.stride % 8 == 0) {
     // scalar-row AdaGrad (sparse LR): the (w, h) pair as one 8-byte load and
     // one 8-byte store instead of two of each.  With a snapshot (the (w, h)
@@ -524,8 +363,7 @@ __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
 template <int G>
 __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __restrict__ slots,
                                                const float* __restrict__ grads, SegList sl,
-                                               OptParams op, int vec,
-                                               const float2* __restrict__ snap) {
+                                               OptParams op, const float2* __restrict__ snap) {
   const long long total = seg_total(sl);
   const int lg = threadIdx.x % G;
   const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
@@ -533,7 +371,7 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg, vec != 0,
+    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg,
                  snap ? snap + pos : nullptr);
   }
 }
@@ -580,22 +418,6 @@ __global__ __launch_bounds__(256) void k_apply_st(DevTable t, const long long* _
     __builtin_amdgcn_wave_barrier();
     for (int k = lg; k < nch; k += G) row[k] = st2[k];
     __builtin_amdgcn_wave_barrier();
-  }
-}
-
-// K5 over a bucketed dedup's rows in OCCURRENCE-SPACE layout (unique key l of
-// bucket b at row bstart[b] + l; see bdedup.hip): one workgroup per bucket
-template <int G>
-__global__ __launch_bounds__(256) void k_apply_bk(DevTable t, const long long* __restrict__ slots,
-                                                  const float* __restrict__ grads,
-                                                  const uint32_t* __restrict__ bstart,
-                                                  const uint32_t* __restrict__ unum,
-                                                  OptParams op) {
-  const int b = blockIdx.x, lg = threadIdx.x % G;
-  const uint32_t nu = unum[b], p0 = bstart[b];
-  for (uint32_t l = threadIdx.x / G; l < nu; l += 256 / G) {
-    const long long pos = (long long)p0 + l;
-    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg);
   }
 }
 
@@ -683,18 +505,13 @@ __global__ __launch_bounds__(256) void k_probe_hist(DevTable t, unsigned long lo
 }
 
 // ---------------------------------------------------------------- launchers
-// SS_PULL_GRID / SS_APPLY_GRID: cap (workgroups) on the general pull / the
-// apply (grid-stride loops), leaving CUs to the other streams' kernels.
-// `def_per_cu` > 0: default cap of that many 256-thread workgroups per CU
-static int env_grid_cap(const char* name, int def_per_cu = 0) {
-  const char* e = std::getenv(name);
-  const int v = e ? std::atoi(e) : -1;
-  if (v > 0) return v;
-  if (v == 0 || def_per_cu <= 0) return 1 << 22;
+// cap (workgroups) on the general pull's grid-stride loop: `per_cu`
+// 256-thread workgroups per CU, leaving CUs to the other streams' kernels
+static int grid_cap_per_cu(int per_cu) {
   int dev = 0, cus = 0;
   check_hip(hipGetDevice(&dev), "hipGetDevice");
   check_hip(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev), "CU count");
-  return std::max(1, cus * def_per_cu);
+  return std::max(1, cus * per_cu);
 }
 
 static inline int grid_for(long long groups, int G, int cap_blocks = 16384) {
@@ -739,42 +556,21 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
   // workgroups per CU, grid-stride beyond, so the route stream's next dedup
   // (count / scatter: few, large workgroups) is not starved beside it (see
   // launch_bd_dedup)
-  static const int pull_cap = env_grid_cap("SS_PULL_GRID", 4);
-  // SS_PULL_ONELOAD_GEN=1: 16-byte LR slots probed with one load per step
-  // (key + row), as the snapshot pull does
-  static const int oneload_gen = [] {
-    const char* e = std::getenv("SS_PULL_ONELOAD_GEN");
-    return e ? std::atoi(e) : 0;
-  }();
-  const int one16 = oneload_gen && G == 1 && t.dim == 1 && t.stride == 16 && t.key_off == 8 &&
-                    t.row_off == 0;
+  static const int pull_cap = grid_cap_per_cu(4);
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique<kG>, dim3(grid_for(max_n, kG, pull_cap)),
                                       dim3(256), 0, st, t, keys, sl, slots, out, ip, size_ctr,
-                                      err, one16));
+                                      err));
   check_launch("k_pull_unique");
-}
-
-void launch_pull_fill_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
-                         const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
-                         float* out, const InitParams& ip, unsigned long long* size_ctr, int* err,
-                         float* snap, const uint32_t* luid, float* occ, hipStream_t st) {
-  if (P <= 0) return;
-  if (!snap || !luid || !occ || !(t.dim == 1 && t.width == 2 && t.stride == 16 &&
-                                  t.key_off == 8 && t.row_off == 0))
-    throw std::invalid_argument("pull_fill_bk: snapshot pull of 16-byte scalar rows only");
-  hipLaunchKernelGGL(k_pull_fill_bk, dim3(P), dim3(1024), 0, st, t, bkeys, bstart, unum, ubase,
-                     slots, out, ip, size_ctr, err, reinterpret_cast<float2*>(snap), luid, occ);
-  check_launch("k_pull_fill_bk");
 }
 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, int osi, hipStream_t st, float* snap) {
+                           int* err, int G, hipStream_t st, float* snap) {
   if (P <= 0) return;
   if (snap && !(G == 1 && t.dim == 1 && t.width == 2 && t.row_off % 8 == 0 && t.stride % 8 == 0))
     throw std::invalid_argument("pull snapshot: scalar (w, h) rows with G = 1 only");
-  // workgroups per bucket (SS_PULL_BK_Y): 4 — one per ~265 unique keys, so a
+  // workgroups per bucket: 4 — one per ~265 unique keys, so a
   // lane probes about once; measured 1.19 -> 1.13-1.17 ms/step vs 1 (the
   // kernel alone barely changes: smaller workgroups interleave better with
   // the route stream's kernels)
@@ -782,76 +578,35 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   // word2vec rows (G = 64): 2 — with the occurrence-row reduce and hipGraph
   // replay, 1 / 2 / 4 / 8: 0.0840-0.0848 / 0.0829-0.0830 / 0.0837-0.0844 /
   // 0.0858 ms/step (earlier, atomic-bound: 2 and 4 neutral)
-  static const int env_ny = [] {
-    const char* e = std::getenv("SS_PULL_BK_Y");
-    const int v = e ? std::atoi(e) : 0;
-    return v < 0 ? 0 : (v > 16 ? 16 : v);
-  }();
-  const int ny = env_ny ? env_ny : (G == 1 ? 4 : 2);
+  const int ny = G == 1 ? 4 : 2;
   // snapshot pulls on 16-byte [w | h | key] slots probe with one 16-byte
-  // load per step (probe_slot16); SS_PULL_ONELOAD=0: key load, then row load
-  static const bool oneload_env = [] {
-    const char* e = std::getenv("SS_PULL_ONELOAD");
-    return !(e && std::atoi(e) == 0);
-  }();
-  const int one16 = oneload_env && snap && t.stride == 16 && t.key_off == 8 && t.row_off == 0;
+  // load per step (probe_slot16; key load then row load measured slower)
+  const int one16 = snap && t.stride == 16 && t.key_off == 8 && t.row_off == 0;
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique_bk<kG>, dim3(P, ny), dim3(256), 0, st, t,
                                       bkeys, bstart, unum, ubase, slots, out, ip, size_ctr, err,
-                                      osi, reinterpret_cast<float2*>(snap), one16));
+                                      reinterpret_cast<float2*>(snap), one16));
   check_launch("k_pull_unique_bk");
-}
-
-void launch_pull_claim(const DevTable& t, const uint64_t* keys, const SegList& sl,
-                       long long max_n, long long* slots, float* out, const InitParams& ip,
-                       unsigned long long* size_ctr, int* err, int G, hipStream_t st) {
-  if (max_n <= 0) return;
-  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_claim<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
-                                      st, t, keys, sl, slots, out, err));
-  check_launch("k_pull_claim");
-  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_verify<kG>, dim3(grid_for(max_n, kG)), dim3(256), 0,
-                                      st, t, keys, sl, slots, out, ip, size_ctr, err));
-  check_launch("k_pull_verify");
-}
-
-void launch_apply_bk(const DevTable& t, const long long* slots, const float* grads,
-                     const uint32_t* bstart, const uint32_t* unum, int P, const OptParams& op,
-                     int G, hipStream_t st) {
-  if (P <= 0) return;
-  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_bk<kG>, dim3(P), dim3(256), 0, st, t, slots, grads,
-                                      bstart, unum, op));
-  check_launch("k_apply_bk");
 }
 
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
                   const float* snap) {
   if (max_n <= 0) return;
-  // SS_APPLY_VEC=0: the previous form (experiment knob).  Default: one
-  // group per key (no grid-stride rounds: a second round is a second
-  // random-access latency chain for those lanes) and 8-byte (w, h) accesses
-  static const int vec = [] {
-    const char* e = std::getenv("SS_APPLY_VEC");
-    return e ? std::atoi(e) : 1;
-  }();
+  // one group per key (no grid-stride rounds: a second round is a second
+  // random-access latency chain for those lanes) and 8-byte (w, h) accesses;
   // narrow multi-coordinate rows (FM): 8-byte chunks staged through LDS
-  // (k_apply_st); SS_APPLY_STAGE=0 keeps the per-coordinate form
-  static const int stage_env = [] {
-    const char* e = std::getenv("SS_APPLY_STAGE");
-    return e ? std::atoi(e) : 1;
-  }();
+  // (k_apply_st)
   const int ns = opt_state_per_coord(op.kind);
   const uint32_t W = t.dim * (uint32_t)(1 + ns);
-  if (stage_env && !snap && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
+  if (!snap && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
       W % 2 == 0 && W == t.width && t.row_off % 8 == 0 && t.stride % 8 == 0) {
     SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_st<kG>, dim3(grid_for(max_n, kG, 1 << 22)),
                                         dim3(256), 0, st, t, slots, grads, sl, op));
     check_launch("k_apply_st");
     return;
   }
-  static const int apply_cap = env_grid_cap("SS_APPLY_GRID");
-  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>,
-                                      dim3(grid_for(max_n, kG, vec ? apply_cap : 16384)),
-                                      dim3(256), 0, st, t, slots, grads, sl, op, vec,
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>, dim3(grid_for(max_n, kG, 1 << 22)),
+                                      dim3(256), 0, st, t, slots, grads, sl, op,
                                       reinterpret_cast<const float2*>(snap)));
   check_launch("k_apply");
 }

@@ -59,8 +59,7 @@ __global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ i
                                                   const uint32_t* __restrict__ inv_n, int B, int C,
                                                   float neg_scale, const float* __restrict__ uvals,
                                                   float* __restrict__ ugrad,
-                                                  float* __restrict__ loss_sum,
-                                                  float* __restrict__ gpos) {
+                                                  float* __restrict__ loss_sum) {
   constexpr int P = D + 1;  // padded LDS row
   extern __shared__ __attribute__((aligned(16))) float smem[];
   float* Vs = smem;              // [T][P] center rows
@@ -140,22 +139,13 @@ __global__ __launch_bounds__(kWG) void k_w2v_sgns(const uint32_t* __restrict__ i
         for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
         const float g = sigm(part) - 1.f;  // d/ds softplus(-s)
         if (lane == 0) loss += softplus(-part);
-        if (gpos) {
-          // the context row's gradient g * v goes out as one scalar per pair;
-          // k_w2v_ctx_reduce sums g * v per unique context key (plain loads)
-          if (lane == 0) gpos[(t0 + t) * (long long)C + j] = g;
+        float* gu = ugrad + (long long)x * D;
 #pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (lane + 64 * r < D) gv[r] += g * u[j][r];
-        } else {
-          float* gu = ugrad + (long long)x * D;
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int d = lane + 64 * r;
-            if (d < D) {
-              atomicAdd(gu + d, g * v[r]);
-              gv[r] += g * u[j][r];
-            }
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          if (d < D) {
+            atomicAdd(gu + d, g * v[r]);
+            gv[r] += g * u[j][r];
           }
         }
       }
@@ -224,30 +214,28 @@ __device__ __forceinline__ unsigned short f2bf(float f) {
   return (unsigned short)(u >> 16);
 }
 
-// POS = false: the tile's negative part only (the positive pairs run in
-// k_w2v_pos, see there); the positive-grad tile is then not allocated.
-template <int D, bool POS = true>
+template <int D>
 struct W2vBf16Smem {
   static constexpr int PB = D + 8;    // bf16 row stride of the V / N tiles
   static constexpr int GB = kS + 8;   // bf16 row stride of the score-gradient tile
   static constexpr int P = D + 1;     // fp32 row stride of the positive-grad tile
   static constexpr size_t bytes = sizeof(unsigned short) * ((size_t)(kT + kS) * PB + (size_t)kT * GB) +
-                                  sizeof(float) * ((POS ? (size_t)kT * P : 0) + kNW);
+                                  sizeof(float) * ((size_t)kT * P + kNW);
 };
 
-template <int D, bool POS = true>
+template <int D>
 __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
     const uint32_t* __restrict__ inv_c, const uint32_t* __restrict__ inv_x,
     const uint32_t* __restrict__ inv_n, int B, int C, float neg_scale,
     const float* __restrict__ uvals, float* __restrict__ ugrad, float* __restrict__ loss_sum) {
-  using L = W2vBf16Smem<D, POS>;
+  using L = W2vBf16Smem<D>;
   constexpr int PB = L::PB, GB = L::GB, P = L::P;
   extern __shared__ __attribute__((aligned(16))) unsigned short smem16[];
   unsigned short* Vb = smem16;            // [T][PB] center rows (bf16)
   unsigned short* Nb = Vb + kT * PB;      // [S][PB] negative rows (bf16)
   unsigned short* Gb = Nb + kS * PB;      // [T][GB] score gradients (bf16)
   float* Gv = reinterpret_cast<float*>(Gb + kT * GB);  // [T][P] positive-part center grads
-  float* red = Gv + (POS ? kT * P : 0);                 // [kNW] loss partials
+  float* red = Gv + kT * P;                             // [kNW] loss partials
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   __shared__ uint32_t rc[kT], rn[kS];
@@ -272,8 +260,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
       *reinterpret_cast<uint2*>(Vb + r * PB + d) = pv;
       *reinterpret_cast<uint2*>(Nb + r * PB + d) = pn;
     }
-    if (POS)
-      for (int e = tid; e < kT * P; e += kWG) Gv[e] = 0.f;
+    for (int e = tid; e < kT * P; e += kWG) Gv[e] = 0.f;
     __syncthreads();
 
     const int r32 = lane & 31, h = lane >> 5;
@@ -298,7 +285,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
     }
     // ---- positive pairs (fp32): wave w owns centers [kT/kNW * w, +kT/kNW); the
     // center row comes from global with the context rows (one round trip)
-    if (POS) {
+    {
       constexpr int R = (D + 63) / 64;
       constexpr int TW = kT / kNW;
       for (int t = w * TW; t < w * TW + TW; ++t) {
@@ -379,7 +366,7 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
         const int row = ti * 32 + mrow(r, lane), col = tj * 32 + r32;
         const uint32_t dst = center ? rc[row] : rn[row];
         if (dst == kInv) continue;
-        const float v = acc[r] + (POS && center ? Gv[row * P + col] : 0.f);
+        const float v = acc[r] + (center ? Gv[row * P + col] : 0.f);
         atomicAdd(ugrad + (long long)dst * D + col, v);
       }
     }
@@ -397,191 +384,6 @@ __global__ __launch_bounds__(kWG, 4) void k_w2v_sgns_bf16(
 }
 
 // ---------------------------------------------------------------------------
-// Positive (center, context) pairs as their own kernel (SS_W2V_POS=split,
-// an experiment: measured slower, see w2v_pos_split): one wave per center.
-// Inside the tile kernel the pairs are a per-wave latency chain (8 centers
-// per wave, each an index load, then C context-row loads, then the row
-// atomics) and a 16K-center step is only 256 tiles, one 8-wave workgroup per
-// CU: 2 waves per SIMD to hide that chain.  Here the same work is 16K waves
-// of ~50 VGPRs (8 per SIMD resident), so the row gathers and the row atomics
-// of many centers are in flight at once.  The center row's gradient goes out
-// as its own row of atomics (the tile kernel then runs with POS = false).
-template <int D>
-__global__ __launch_bounds__(256) void k_w2v_pos(const uint32_t* __restrict__ inv_c,
-                                                 const uint32_t* __restrict__ inv_x, int B, int C,
-                                                 const float* __restrict__ uvals,
-                                                 float* __restrict__ ugrad,
-                                                 float* __restrict__ loss_sum) {
-  constexpr int R = (D + 63) / 64;
-  __shared__ float red[4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const long long t = (long long)blockIdx.x * 4 + w;
-  float loss = 0.f;
-  const uint32_t c = t < B ? inv_c[t] : kInv;
-  if (c != kInv) {  // wave-uniform
-    const uint32_t xid = lane < C ? inv_x[t * C + lane] : kInv;
-    float u[kMaxC][R], v[R], gv[R];
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int d = lane + 64 * r;
-      v[r] = d < D ? uvals[(long long)c * D + d] : 0.f;
-      gv[r] = 0.f;
-    }
-#pragma unroll
-    for (int j = 0; j < kMaxC; ++j) {
-      const uint32_t x = __shfl(xid, j, 64);
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int d = lane + 64 * r;
-        u[j][r] = (j < C && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < kMaxC; ++j) {
-      const uint32_t x = __shfl(xid, j, 64);
-      if (j >= C || x == kInv) continue;  // wave-uniform
-      float part = 0.f;
-#pragma unroll
-      for (int r = 0; r < R; ++r) part += v[r] * u[j][r];
-      for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-      const float g = sigm(part) - 1.f;  // d/ds softplus(-s)
-      if (lane == 0) loss += softplus(-part);
-      float* gu = ugrad + (long long)x * D;
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        const int d = lane + 64 * r;
-        if (d < D) {
-          atomicAdd(gu + d, g * v[r]);
-          gv[r] += g * u[j][r];
-        }
-      }
-    }
-    float* gc = ugrad + (long long)c * D;
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const int d = lane + 64 * r;
-      if (d < D) atomicAdd(gc + d, gv[r]);
-    }
-  }
-  if (lane == 0) red[w] = loss;
-  __syncthreads();
-  if (threadIdx.x == 0 && loss_sum) ctr_addf(loss_sum, red[0] + red[1] + red[2] + red[3]);
-}
-
-// SS_W2V_POS: "split" runs the positive pairs in k_w2v_pos and the tile
-// kernel on the negative part only; "fused" (default) keeps them in the tile
-// kernel.  Measured (1M vocab, dim 128, 16K centers): split 0.342-0.346
-// ms/step vs fused 0.307; k_w2v_pos alone takes 142-168 us, as long as the
-// whole fused tile kernel: the pairs are bound by the memory-side rate of
-// their ~92 MB of row atomics (~1.3 TB/s, MI355X_MICROARCH.md "Global float
-// atomics"), not by the tile kernel's occupancy
-static bool w2v_pos_split() {
-  static const bool v = [] {
-    const char* e = std::getenv("SS_W2V_POS");
-    return e && std::string(e) == "split";
-  }();
-  return v;
-}
-
-// Context-row gradients without global atomics (the sgns kernel's positive
-// pairs otherwise issue one 256-B row of float atomics per pair: 84 MB per
-// 16K-center step at the memory-side atomic rate, ~1.3 TB/s, which also
-// stalls every other stream's memory traffic).  One workgroup per bucket of
-// the bucketed dedup: its context occurrences p (key index j in [B, B+B*C))
-// add gpos[pair] * (center row of the pair) into LDS rows of the bucket's
-// unique keys, a window of kCW keys per pass; each row is then added to its
-// gradient row once (plain read-modify-write: the sgns kernel, whose atomics
-// cover the negative-sample part of the same rows, ran before on the stream).
-static constexpr int kCW = 64;  // unique keys per LDS window
-template <int D>
-__global__ __launch_bounds__(256) void k_w2v_ctx_reduce(const uint32_t* __restrict__ bstart,
-                                                        const uint32_t* __restrict__ unum,
-                                                        const uint32_t* __restrict__ ubase,
-                                                        const uint32_t* __restrict__ pj,
-                                                        const uint32_t* __restrict__ luid,
-                                                        const uint32_t* __restrict__ inv_c,
-                                                        const float* __restrict__ gpos, int B,
-                                                        int C, const float* __restrict__ uvals,
-                                                        float* __restrict__ ugrad) {
-  constexpr int R = (D + 63) / 64;
-  __shared__ float acc[kCW][D];
-  __shared__ uint32_t hit;
-  const int b = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b], base = ubase[b];
-  const long long jc0 = B, jc1 = (long long)B + (long long)B * C;
-  for (uint32_t l0 = 0; l0 < nu; l0 += kCW) {
-    for (int e = threadIdx.x; e < kCW * D; e += 256) (&acc[0][0])[e] = 0.f;
-    if (threadIdx.x == 0) hit = 0;
-    __syncthreads();
-    // wave w loads the metadata of 64 occurrences at once (lane i: p = pb + i),
-    // then walks the ones that hit this window, 4 rows in flight at a time;
-    // lanes sweep the row
-    for (uint32_t pb = p0 + 64 * w; pb < p1; pb += 256) {
-      const uint32_t p = pb + lane;
-      uint32_t l = kInv, c = kInv;
-      float g = 0.f;
-      if (p < p1) {
-        l = luid[p];
-        if (l != kInv && l >= l0 && l < l0 + kCW) {
-          const long long j = pj[p];
-          if (j >= jc0 && j < jc1) {  // a context occurrence (not a center / negative)
-            const long long pair = j - jc0;
-            c = inv_c[pair / C];
-            g = gpos[pair];
-          }
-        }
-      }
-      unsigned long long m = __ballot(c != kInv);
-      if (m && lane == 0) hit = 1;
-      while (m) {
-        int k[4];
-        int nk = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          k[q] = m ? __builtin_ctzll(m) : -1;
-          if (m) {
-            m &= m - 1;
-            ++nk;
-          }
-        }
-        float v[4][R];
-        uint32_t lk[4];
-        float gk[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int src = k[q] < 0 ? 0 : k[q];
-          const uint32_t cq = __shfl(c, src, 64);
-          lk[q] = __shfl(l, src, 64);
-          gk[q] = __shfl(g, src, 64);
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int d = lane + 64 * r;
-            v[q][r] = (q < nk && d < D) ? uvals[(size_t)cq * D + d] : 0.f;
-          }
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (q >= nk) break;  // wave-uniform
-#pragma unroll
-          for (int r = 0; r < R; ++r) {
-            const int d = lane + 64 * r;
-            if (d < D) atomicAdd(&acc[lk[q] - l0][d], gk[q] * v[q][r]);
-          }
-        }
-      }
-    }
-    __syncthreads();
-    if (hit) {
-      const uint32_t n = min((uint32_t)kCW, nu - l0);
-      for (uint32_t e = threadIdx.x; e < n * D; e += 256) {
-        const uint32_t l = e / D, d = e - l * D;
-        float* gr = ugrad + (size_t)(base + l0 + l) * D + d;
-        *gr += acc[l][d];
-      }
-    }
-    __syncthreads();
-  }
-}
 
 // log-uniform ("Zipf-like") word id in [0, V) from a 64-bit hash
 __device__ __forceinline__ uint64_t w2v_zipf(uint64_t r, long long V, double logV) {
@@ -656,12 +458,12 @@ struct W2vWinSmem {
       sizeof(unsigned short) * ((size_t)(kT + kWU + kS) * PB + (size_t)kT * GPB + (size_t)kT * GB);
 };
 
-template <int D, int NW>
-__global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
+template <int D>
+__global__ __launch_bounds__(kWG, 4) void k_w2v_win_bf16(
     const uint32_t* __restrict__ inv_c, const uint32_t* __restrict__ inv_w,
     const uint32_t* __restrict__ inv_n, const int32_t* __restrict__ meta, int B, int W,
     float neg_per_pair, const float* __restrict__ uvals, float* __restrict__ ugrad,
-    float* __restrict__ loss_sum, float* __restrict__ pair_sum, int gmode,
+    float* __restrict__ loss_sum, float* __restrict__ pair_sum,
     float* __restrict__ ograd, float* __restrict__ otail) {
   using L = W2vWinSmem<D>;
   constexpr int PB = L::PB, GPB = L::GPB, GB = L::GB, TJ = D / 32;
@@ -675,6 +477,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
   __shared__ int32_t mw[kWU];
   __shared__ int uany[kWU];
   __shared__ float cwt[kT];  // n_t * K / S
+  constexpr int NW = kNW;
   __shared__ float red[NW];
 
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -735,7 +538,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
 
     const int r32 = lane & 31, h = lane >> 5;
     // ---- scores: 6 tiles of S+ (2 x 3) and 4 of S- (2 x 2)
-    for (int k = w; k < (gmode >= 4 ? 0 : 10); k += NW) {  // (gmode 4: measurement, no scores)
+    for (int k = w; k < 10; k += NW) {
       const bool pos = k < 6;
       const int ti = pos ? k / 3 : (k - 6) >> 1, tj = pos ? k % 3 : (k - 6) & 1;
       const unsigned short* Bm = pos ? Ub : Nb;
@@ -768,7 +571,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
     }
     __syncthreads();
     // ---- gradients: gV (2 x TJ tiles), gU (3 x TJ), gN (2 x TJ)
-    for (int tt = w; tt < (gmode >= 3 ? 0 : 7 * TJ); tt += NW) {  // (gmode 3/4: no gradients)
+    for (int tt = w; tt < 7 * TJ; tt += NW) {
       const int kind = tt < 2 * TJ ? 0 : (tt < 5 * TJ ? 1 : 2);
       const int q = tt - (kind == 0 ? 0 : (kind == 1 ? 2 * TJ : 5 * TJ));
       const int ti = q / TJ, tj = q % TJ;
@@ -835,10 +638,7 @@ __global__ __launch_bounds__(64 * NW, 4) void k_w2v_win_bf16(
         }
         const uint32_t dst = kind == 0 ? rc[row] : (kind == 1 ? (uany[row] ? rw[row] : kInv) : rn[row]);
         if (dst == kInv) continue;  // lanes 0-31 / 32-63: one 128-B row segment each
-        if (gmode == 0)
-          atomicAdd(ugrad + (long long)dst * D + col, acc[r]);
-        else if (gmode == 1 || acc[r] == 1.2345e30f)  // measurement only: stores / no output
-          ugrad[(long long)dst * D + col] = acc[r];
+        atomicAdd(ugrad + (long long)dst * D + col, acc[r]);
       }
     }
     __syncthreads();  // the next tile overwrites the LDS tiles
@@ -1100,41 +900,32 @@ static void smem_attr_once(size_t bytes) {
 }
 
 template <int D>
-static void launch_w2v_bf16(bool split, int tiles, const uint32_t* inv_c, const uint32_t* inv_x,
+static void launch_w2v_bf16(int tiles, const uint32_t* inv_c, const uint32_t* inv_x,
                             const uint32_t* inv_n, int B, int C, float neg_scale,
                             const float* uvals, float* ugrad, float* loss_sum, hipStream_t st) {
-  if (split) {
-    hipLaunchKernelGGL(k_w2v_pos<D>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, inv_c, inv_x,
-                       B, C, uvals, ugrad, loss_sum);
-    check_launch("k_w2v_pos");
-  }
-  auto k = split ? k_w2v_sgns_bf16<D, false> : k_w2v_sgns_bf16<D, true>;
-  const size_t sm = split ? W2vBf16Smem<D, false>::bytes : W2vBf16Smem<D, true>::bytes;
-  if (split)
-    smem_attr_once<k_w2v_sgns_bf16<D, false>>(sm);
-  else
-    smem_attr_once<k_w2v_sgns_bf16<D, true>>(sm);
+  const size_t sm = W2vBf16Smem<D>::bytes;
+  smem_attr_once<k_w2v_sgns_bf16<D>>(sm);
   // one workgroup per tile: the pairs tile is bound by its own ~84 MB of row
   // atomics per 16K-center step and needs every CU (half the CUs, as the
-  // window tile uses: 0.272 -> 0.289 ms/step)
-  hipLaunchKernelGGL(k, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, neg_scale, uvals,
-                     ugrad, loss_sum);
+  // window tile uses: 0.272 -> 0.289 ms/step).  Positive pairs in their own
+  // one-wave-per-center kernel measured slower (0.307 -> 0.344 ms/step: the
+  // pairs are bound by the memory-side rate of their row atomics, not by the
+  // tile's occupancy)
+  hipLaunchKernelGGL(k_w2v_sgns_bf16<D>, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B,
+                     C, neg_scale, uvals, ugrad, loss_sum);
 }
 
 void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_t* inv_n, int B,
                      int C, int D, float neg_scale, const float* uvals, float* ugrad,
-                     float* loss_sum, hipStream_t st, float* gpos, int bf16) {
+                     float* loss_sum, hipStream_t st, int bf16) {
   if (B <= 0) return;
   if (C < 1 || C > kMaxC) throw_error("w2v_sgns: contexts per center must be in [1,16]");
   const int tiles = (B + kT - 1) / kT;
   if (bf16) {
-    if (gpos) throw_error("w2v_sgns: the bf16 tile has no context-reduce output");
-    // bf16: 1 = positive pairs as SS_W2V_POS says, 2 = split, 3 = fused
-    const bool split = bf16 == 2 ? true : bf16 == 3 ? false : w2v_pos_split();
     switch (D) {
 #define SS_W2VB_CASE(DD)                                                                     \
   case DD:                                                                                   \
-    launch_w2v_bf16<DD>(split, tiles, inv_c, inv_x, inv_n, B, C, neg_scale, uvals, ugrad,    \
+    launch_w2v_bf16<DD>(tiles, inv_c, inv_x, inv_n, B, C, neg_scale, uvals, ugrad,    \
                         loss_sum, st);                                                       \
     break;
       SS_W2VB_CASE(32)
@@ -1153,7 +944,7 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
   case DD:                                                                                  \
     smem_attr_once<k_w2v_sgns<DD>>(sm);                                                     \
     hipLaunchKernelGGL(k_w2v_sgns<DD>, dim3(tiles), dim3(kWG), sm, st, inv_c, inv_x, inv_n, B, C, \
-                       neg_scale, uvals, ugrad, loss_sum, gpos);                            \
+                       neg_scale, uvals, ugrad, loss_sum);                                  \
     break;
     SS_W2V_CASE(32)
     SS_W2V_CASE(64)
@@ -1163,27 +954,6 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
       throw_error("w2v_sgns: D must be 32, 64 or 128");
   }
   check_launch("k_w2v_sgns");
-}
-
-void launch_w2v_ctx_reduce(int P, const uint32_t* bstart, const uint32_t* unum,
-                           const uint32_t* ubase, const uint32_t* pj, const uint32_t* luid,
-                           const uint32_t* inv_c, const float* gpos, int B, int C, int D,
-                           const float* uvals, float* ugrad, hipStream_t st) {
-  if (P <= 0 || B <= 0) return;
-  switch (D) {
-#define SS_W2VR_CASE(DD)                                                                    \
-  case DD:                                                                                  \
-    hipLaunchKernelGGL(k_w2v_ctx_reduce<DD>, dim3(P), dim3(256), 0, st, bstart, unum, ubase, pj, \
-                       luid, inv_c, gpos, B, C, uvals, ugrad);                              \
-    break;
-    SS_W2VR_CASE(32)
-    SS_W2VR_CASE(64)
-    SS_W2VR_CASE(128)
-#undef SS_W2VR_CASE
-    default:
-      throw_error("w2v_ctx_reduce: D must be 32, 64 or 128");
-  }
-  check_launch("k_w2v_ctx_reduce");
 }
 
 void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const uint32_t* ubase,
@@ -1221,51 +991,24 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
   check_launch("k_w2v_oreduce");
 }
 
-template <int D>
-static void launch_w2v_win_t(bool wide, int grid, hipStream_t st, const uint32_t* inv_c,
-                             const uint32_t* inv_w, const uint32_t* inv_n, const int32_t* meta,
-                             int B, int W, float neg_per_pair, const float* uvals, float* ugrad,
-                             float* loss_sum, float* pair_sum, int gmode, float* ograd,
-                             float* otail) {
-  const size_t sm = W2vWinSmem<D>::bytes;
-  if (wide) {
-    smem_attr_once<k_w2v_win_bf16<D, 16>>(sm);
-    hipLaunchKernelGGL((k_w2v_win_bf16<D, 16>), dim3(grid), dim3(1024), sm, st, inv_c, inv_w,
-                       inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum, pair_sum, gmode,
-                       ograd, otail);
-  } else {
-    smem_attr_once<k_w2v_win_bf16<D, 8>>(sm);
-    hipLaunchKernelGGL((k_w2v_win_bf16<D, 8>), dim3(grid), dim3(512), sm, st, inv_c, inv_w,
-                       inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum, pair_sum, gmode,
-                       ograd, otail);
-  }
-}
-
 void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                     const int32_t* meta, int B, int W, int D, float neg_per_pair,
                     const float* uvals, float* ugrad, float* loss_sum, float* pair_sum,
                     hipStream_t st, float* ograd, float* otail) {
-  // SS_W2V_WIN_WG: 512 (8 waves) or 1024 (16 waves) threads per tile
-  static const bool wide = [] {
-    const char* e = std::getenv("SS_W2V_WIN_WG");
-    return e && std::atoi(e) == 1024;
-  }();
   if (B <= 0) return;
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_win: window must be in [1, 15]");
   const int tiles = (B + kT - 1) / kT;
   const int grid = w2v_tile_grid(tiles, ograd == nullptr);
-  // SS_W2V_WIN_GMODE (measurement only, wrong results): 1 = gradient rows as
-  // plain stores instead of atomics, 2 = no gradient output, 3 = no gradient
-  // GEMMs, 4 = row gathers only
-  static const int gmode = [] {
-    const char* e = std::getenv("SS_W2V_WIN_GMODE");
-    return e ? std::atoi(e) : 0;
-  }();
+  // 8 waves per tile: 16 (1024 threads) ran the tile alone 29.6 -> 23.1 us
+  // but the step 0.083 -> 0.093 ms (its registers fill the CU's SIMDs and
+  // nothing else runs beside it)
   switch (D) {
 #define SS_W2VW_CASE(DD)                                                                     \
   case DD:                                                                                   \
-    launch_w2v_win_t<DD>(wide, grid, st, inv_c, inv_w, inv_n, meta, B, W, neg_per_pair, uvals,  \
-                         ugrad, loss_sum, pair_sum, gmode, ograd, otail);                    \
+    smem_attr_once<k_w2v_win_bf16<DD>>(W2vWinSmem<DD>::bytes);                               \
+    hipLaunchKernelGGL(k_w2v_win_bf16<DD>, dim3(grid), dim3(512), W2vWinSmem<DD>::bytes, st,     \
+                       inv_c, inv_w, inv_n, meta, B, W, neg_per_pair, uvals, ugrad, loss_sum,  \
+                       pair_sum, ograd, otail);                                                \
     break;
     SS_W2VW_CASE(32)
     SS_W2VW_CASE(64)

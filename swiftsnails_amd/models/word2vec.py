@@ -200,7 +200,7 @@ class Word2VecWorker(PipelinedWorker):
             return
         h.w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
                    d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),
-                   self.loss_sum.data_ptr(), st, 0, int(self.mfma_bf16))
+                   self.loss_sum.data_ptr(), st, int(self.mfma_bf16))
 
     def samples_per_step(self) -> int:
         """Window layout: centers (words) per step, word2vec's "words/s"

@@ -108,11 +108,6 @@ class HbmTable:
         self.G = lane_group or int(os.environ.get("SS_TABLE_G", "0")) or \
             default_lane_group(self.width)
         self.max_load = max_load
-        # unique-key insert: "cas" = 64-bit CAS claim (default: measured
-        # 0.709 ms/step vs 0.756 for "claim" in the pipelined bench); "claim" =
-        # optimistic plain-store claim + verify pass, no device-scope atomics
-        # (its verify pass re-reads freshly claimed lines across XCDs).
-        self.insert_mode = os.environ.get("SS_TABLE_INSERT", "cas")
         # bumped by every row-modifying call: a pull snapshot (pull_buckets
         # snap=) is valid for a blind-write apply only while it is unchanged
         self.version = 0
@@ -206,11 +201,11 @@ class HbmTable:
         sl = segs if segs is not None else self._seg(keys.numel())
         # the CAS-insert fused kernel is also correct for duplicate keys (a
         # lane reading a row another lane is initialising substitutes the
-        # deterministic init value); the claim insert needs unique keys
-        if insert and (unique or self.insert_mode == "cas"):
-            fn = h.pull_unique if self.insert_mode == "cas" else h.pull_claim
-            fn(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), out.data_ptr(),
-               self._init_native, self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, st)
+        # deterministic init value)
+        if insert:
+            h.pull_unique(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), out.data_ptr(),
+                          self._init_native, self.size_ctr.data_ptr(), self.err.data_ptr(),
+                          self.G, st)
         else:
             h.probe(self.dt, keys.data_ptr(), sl, n, slots.data_ptr(), self._init_native,
                     int(insert), self.size_ctr.data_ptr(), self.err.data_ptr(), self.G, st)
@@ -353,39 +348,19 @@ class HbmTable:
             self.version += 1
 
     def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None,
-                     osi: bool = False, snap: Optional[torch.Tensor] = None,
-                     luid: Optional[torch.Tensor] = None, occ: Optional[torch.Tensor] = None):
+                     snap: Optional[torch.Tensor] = None):
         """Unique-key lookup-or-init + gather straight from a bucketed dedup
-        (``Deduper.bucket_view()``): rows land at their unique ids (compact,
-        or occurrence-space with ``osi``).  ``snap`` ([ucap, 2] float32,
+        (``Deduper.bucket_view()``): rows land at their compact unique ids.  ``snap`` ([ucap, 2] float32,
         ``snapshot_ok`` tables): also write each key's (w, h) there, for a
         ``push_slots(snap=)`` that needs no random row read."""
         bkeys, bstart, unum, ubase, P = view
         if snap is not None and not self.snapshot_ok:
             raise ValueError("pull snapshot needs scalar AdaGrad rows (dim 1, G 1)")
-        if occ is not None:
-            # fused with the occurrence fill (``Deduper.fill_occ``): occ[p] =
-            # the pulled weight of the occurrence at bucket position p
-            if snap is None or osi or luid is None or self.stride != 16:
-                raise ValueError("pull_buckets(occ=): snapshot pull of 16-byte rows, compact ids")
-            hip().pull_fill_bk(self.dt, bkeys, bstart, unum, ubase, P, slots.data_ptr(),
-                               out.data_ptr(), self._init_native, self.size_ctr.data_ptr(),
-                               self.err.data_ptr(), snap.data_ptr(), luid.data_ptr(),
-                               occ.data_ptr(), _stream_ptr(stream))
-            return out, slots
         hip().pull_unique_bk(self.dt, bkeys, bstart, unum, ubase, P, slots.data_ptr(),
                              out.data_ptr(), self._init_native, self.size_ctr.data_ptr(),
-                             self.err.data_ptr(), self.G, _stream_ptr(stream), int(osi),
+                             self.err.data_ptr(), self.G, _stream_ptr(stream),
                              0 if snap is None else snap.data_ptr())
         return out, slots
-
-    def push_buckets(self, view, slots: torch.Tensor, grads: torch.Tensor, stream=None):
-        """Optimizer update for a bucketed dedup's unique keys whose slots and
-        gradient rows sit at occurrence-space ids (``pull_buckets(osi=True)``)."""
-        _, bstart, unum, _, P = view
-        self.version += 1
-        hip().apply_bk(self.dt, slots.data_ptr(), grads.data_ptr(), bstart, unum, P,
-                       self.opt.native(), self.G, _stream_ptr(stream))
 
     def lookup_slots(self, keys: torch.Tensor, insert: bool = False, segs=None,
                      max_n: Optional[int] = None, stream=None) -> torch.Tensor:

@@ -235,7 +235,7 @@ class PSEngine:
                            for _ in range(self.depth)] if self.snapshot else None
             # the colocated pull reads the bucketed dedup's staging directly:
             # no contiguous send segment is needed
-            if table is not None and table.insert_mode == "cas":
+            if table is not None:
                 for dd in self.dedupers:
                     dd.need_ukeys = False
         elif self.gpu:
@@ -502,7 +502,7 @@ class PSEngine:
         tab = self.table
         snap = None
         own = dd.owner
-        if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
+        if getattr(own, "mode", None) == "bucket":
             if self.snapshot and tab.snapshot_ok:
                 snap = self._snaps[slot]
             tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], snap=snap)
@@ -528,7 +528,7 @@ class PSEngine:
             if self.fast1:
                 # one GPU: the pull waits for this round's dedup only
                 uv, tab, own = self.uvals[slot], self.table, dd.owner
-                if getattr(own, "mode", None) == "bucket" and tab.insert_mode == "cas":
+                if getattr(own, "mode", None) == "bucket":
                     tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], stream=ps)
                 else:
                     tab.pull(dd.ukeys, insert=True, unique=True, out=uv, slots=self.slots[slot],

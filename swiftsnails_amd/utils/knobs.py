@@ -52,35 +52,11 @@ KNOBS: dict[str, Knob] = {
     "SS_TABLE_G": Knob("auto", "ops/table.py", "tuning", "lanes per table row"),
     "SS_TABLE_LAYOUT": Knob("auto", "ops/table.py", "tuning",
                             "slot layout: rowfirst (width <= 2) / keyfirst"),
-    "SS_TABLE_INSERT": Knob("cas", "ops/table.py", "tuning",
-                            "cas, or claim (plain-store claim + verify; measured slower)"),
     "SS_TABLE_PREFILL": Knob("1", "ops/table.py", "tuning",
                              "zero-init tables pre-filled with the init row (insert = CAS only)"),
-    "SS_PULL_BK_Y": Knob("4 (G=1) / 2", "csrc/hip/table.hip", "tuning",
-                         "workgroups per dedup bucket in the bucketed pull"),
-    "SS_PULL_ONELOAD": Knob("1", "csrc/hip/table.hip", "tuning",
-                            "snapshot pull on 16-byte LR slots: one 16-byte load per probe step "
-                            "(key + row) instead of a key load then a row load"),
-    "SS_PULL_GRID": Knob("4 x CUs", "csrc/hip/table.hip", "tuning",
-                         "workgroup cap of the general (N>1 server) pull, grid-stride beyond it "
-                         "(0: one group per key); with the N>1 count at 256 threads "
-                         "1.056-1.116 -> 1.035-1.067 ms/step"),
-    "SS_APPLY_GRID": Knob("0 (one group per key)", "csrc/hip/table.hip", "experiment",
-                          "workgroup cap of the apply, grid-stride beyond it"),
-    "SS_APPLY_STAGE": Knob("1", "csrc/hip/table.hip", "tuning",
-                           "narrow multi-coordinate rows (FM): K5 moves the row as 8-byte chunks "
-                           "staged through LDS (k_apply_st)"),
-    "SS_PULL_ONELOAD_GEN": Knob("0", "csrc/hip/table.hip", "experiment",
-                                "general (N>1 server) pull on 16-byte LR slots: one 16-byte load "
-                                "per probe step (neutral: 1.081-1.085 vs 1.076-1.090 ms/step)"),
-    "SS_APPLY_VEC": Knob("1", "csrc/hip/table.hip", "tuning",
-                         "one lane group per key + 8-byte (w, h) accesses in k_apply"),
     "SS_BD_NCH": Knob("128 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
                       "max count/scatter chunks (1 GPU 512 -> 128: 0.93 -> 0.89 ms/step; "
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
-    "SS_BD_STAGE": Knob("0", "csrc/hip/bdedup.hip", "experiment",
-                        "scatter stages keys in bucket order, dedup reads them coalesced "
-                        "(0.949 -> 0.968 ms/step at 128 chunks, three A/B pairs)"),
     "SS_BD_CNT": Knob("1024 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
@@ -119,16 +95,6 @@ KNOBS: dict[str, Knob] = {
                             "0: one per tile); half the CUs leaves CUs to the route stream's "
                             "dedup when the tile is atomic-bound (0.143 -> 0.123 ms/step), one "
                             "per tile is faster with occurrence-row stores (0.101 -> 0.092)"),
-    "SS_W2V_WIN_WG": Knob("512", "csrc/hip/w2v.hip", "experiment",
-                          "1024: the window tile with 16 waves instead of 8 (standalone 29.6 -> "
-                          "23.1 us, but the step 0.083 -> 0.093 ms: the workgroup's registers "
-                          "fill its CU's SIMDs and nothing runs beside it)"),
-    "SS_W2V_WIN_GMODE": Knob("0", "csrc/hip/w2v.hip", "debug",
-                             "measurement only (wrong results): windowed word2vec tile's "
-                             "gradient rows as 1 = plain stores, 2 = not written"),
-    "SS_W2V_POS": Knob("fused", "csrc/hip/w2v.hip", "experiment",
-                       "split: positive pairs in their own one-wave-per-center kernel "
-                       "(0.307 -> 0.344 ms/step: atomic-rate bound, not occupancy bound)"),
     "SS_GRAPH_STEPS": Knob("4 x depth", "models/base.py", "tuning",
                            "steps per hipGraph: 1, or a multiple of the ring depth (word2vec "
                            "4 / 8 / 16 / 32: 0.093 / 0.088 / 0.086 / 0.084 ms/step)"),

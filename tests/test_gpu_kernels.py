@@ -509,17 +509,15 @@ def test_rccl_comm_world1(dev):
     np.testing.assert_array_equal(b.cpu().numpy()[5:9], [2, 3, 4, 5])
 
 
-@pytest.mark.parametrize("mode", ["claim", "cas"])
 @pytest.mark.parametrize("G,load", [(1, 0.9), (4, 0.5), (64, 0.95)])
-def test_pull_unique_insert_modes(dev, mode, G, load):
-    """Unique-key pull: optimistic claim+verify (and CAS) under heavy collisions."""
+def test_pull_unique_insert(dev, G, load):
+    """Unique-key pull (CAS insert) under heavy collisions."""
     from swiftsnails_amd.ops.optim import InitConfig, init_reference
     from swiftsnails_amd.ops.table import HbmTable
 
     init = InitConfig("uniform", 1.0, 0.0, seed=11)
     n = 20000
     t = HbmTable(2, int(n / load) + 1, init=init, device=dev, lane_group=G)
-    t.insert_mode = mode
     k = np.unique(_keys(n + 500, 12))[:n]
     rng = np.random.default_rng(13)
     # two overlapping rounds: half old keys, half new keys in round 2

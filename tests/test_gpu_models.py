@@ -17,12 +17,10 @@ def dev():
     return torch.device("cuda", 0)
 
 
-@pytest.mark.parametrize("D,bf16", [(32, 0), (64, 0), (128, 0), (32, 1), (64, 1), (128, 1),
-                                    (128, 2), (128, 3), (64, 2), (64, 3)])
+@pytest.mark.parametrize("D,bf16", [(32, 0), (64, 0), (128, 0), (32, 1), (64, 1), (128, 1)])
 def test_w2v_sgns_tile_matches_reference(dev, D, bf16):
     """fp32 tile: fp32-exact; bf16 tile (SS_W2V_MFMA=bf16): negative-sample
-    GEMMs from bf16-rounded rows, checked at bf16 tolerance.  bf16 = 2 / 3:
-    positive pairs in their own kernel (k_w2v_pos) / inside the tile."""
+    GEMMs from bf16-rounded rows, checked at bf16 tolerance."""
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.models.word2vec import sgns_reference
 
@@ -39,7 +37,7 @@ def test_w2v_sgns_tile_matches_reference(dev, D, bf16):
     neg_scale = 0.7
     hip().w2v_sgns(p, p + T * es, p + T * (1 + C) * es, T, C, D, neg_scale, tu.data_ptr(),
                    g.data_ptr(), loss.data_ptr(), torch.cuda.current_stream().cuda_stream,
-                   0, bf16)
+                   bf16)
     torch.cuda.synchronize()
     G = g.cpu().numpy()
     tot = 0.0
