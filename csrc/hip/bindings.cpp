@@ -440,6 +440,13 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("W"), py::arg("D"), py::arg("neg_per_pair"), py::arg("uvals"), py::arg("ugrad"),
      py::arg("loss"), py::arg("pairs"), py::arg("st"), py::arg("ograd") = 0,
      py::arg("otail") = 0);
+  m.def("w2v_pp", [](uintptr_t inv_c, uintptr_t inv_w, uintptr_t inv_n, uintptr_t meta, int B,
+                     int W, int K, int D, uintptr_t uvals, uintptr_t ograd, uintptr_t gpair,
+                     uintptr_t loss, uintptr_t pairs, uintptr_t st) {
+    launch_w2v_pp(P<const uint32_t>(inv_c), P<const uint32_t>(inv_w), P<const uint32_t>(inv_n),
+                  P<const int32_t>(meta), B, W, K, D, P<const float>(uvals), P<float>(ograd),
+                  P<float>(gpair), P<float>(loss), P<float>(pairs), S(st));
+  });
   m.def("w2v_osort", [](int P_, uintptr_t bstart, uintptr_t unum, uintptr_t ubase, uintptr_t pj,
                         uintptr_t luid, uintptr_t ord, uintptr_t items, uintptr_t st) {
     launch_w2v_osort(P_, P<const uint32_t>(bstart), P<const uint32_t>(unum),

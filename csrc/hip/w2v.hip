@@ -777,7 +777,7 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
   if (it.y == 0) return;  // half-wave-uniform (the shuffles below stay inside a half)
   // the tail copy of run position j (row l - 64 of the previous tile), or -1
   auto tail_of = [&](long long j) -> long long {
-    if (j < B || j >= B + R) return -1;
+    if (!otail || j < B || j >= B + R) return -1;
     const long long rq = j - B;
     if (rq >= kT && rq % kT < 2 * W && rq / kT <= ntiles - 1) return (rq / kT - 1) * 2 * W + rq % kT;
     return -1;
@@ -812,6 +812,162 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
     for (int v = 0; v < V; ++v) of[v] = acc[v];
     *reinterpret_cast<VT*>(g) = o;
   }
+}
+
+// ---- classic SGNS: K negatives drawn per positive pair (neg_mode per_pair)
+//
+// The shared-negative tile above trains each center against the 64 negatives
+// of its tile, weighted to K per pair; this is word2vec's own objective: every
+// (center t, context q) pair has its own K negatives (keys [B centers | run
+// positions | B x 2W x K negatives], negative (t, o, k) at B + R + (t*2W + o)*K
+// + k, o the offset slot of dq = o - W (o < W) or o - W + 1).  Dot products,
+// not GEMMs: each pair touches 1 + K rows once, so there is no tile to put on
+// the MFMA.  Gradients as occurrence rows with plain stores (summed per key by
+// k_w2v_oreduce, as the window tile's): k_w2v_pp (one wave per center) writes
+// the center row, the negative rows and the pair's scalar g+ = sig(v.u) - 1;
+// k_w2v_ppctx (one wave per run position) gathers g+ * v over the 2W centers
+// that pair with it.  Every occurrence row is written (zero when unused).
+static constexpr int kPpMaxK = 16;
+template <int D>
+__global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv_c,
+                                                const uint32_t* __restrict__ inv_w,
+                                                const uint32_t* __restrict__ inv_n,
+                                                const int32_t* __restrict__ meta, int B, int W,
+                                                int K, const float* __restrict__ uvals,
+                                                float* __restrict__ ograd,
+                                                float* __restrict__ gpair,
+                                                float* __restrict__ loss_sum,
+                                                float* __restrict__ pair_sum) {
+  constexpr int R = (D + 63) / 64;
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long t = (long long)blockIdx.x * 4 + w;
+  const long long Rn = (long long)B + 2 * W;
+  float loss = 0.f, npairs = 0.f;
+  if (t < B) {  // wave-uniform
+    const int32_t mc = meta[t + W];
+    float v[R], gv[R];
+    const uint32_t c = inv_c[t];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int d = lane + 64 * r;
+      v[r] = (d < D && c != kInv) ? uvals[(long long)c * D + d] : 0.f;
+      gv[r] = 0.f;
+    }
+    for (int o = 0; o < 2 * W; ++o) {
+      const int dq = o < W ? o - W : o - W + 1;
+      const long long q = t + W + dq;
+      const bool ok = c != kInv && w2v_pair_ok(mc, meta[q], dq);
+      const long long nb = (t * 2 * W + o) * (long long)K;
+      float* on = ograd + (B + Rn + nb) * (long long)D;
+      if (!ok) {  // the pair's occurrence rows still hold a (zero) gradient
+        for (int k = 0; k < K; ++k)
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (lane + 64 * r < D) on[(long long)k * D + lane + 64 * r] = 0.f;
+        if (lane == 0) gpair[t * 2 * W + o] = 0.f;
+        continue;
+      }
+      // every row of the pair in flight before the first use
+      const uint32_t xq = inv_w[q];
+      const uint32_t nk = lane < K ? inv_n[nb + lane] : kInv;
+      float u[R], n[kPpMaxK][R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        u[r] = (d < D && xq != kInv) ? uvals[(long long)xq * D + d] : 0.f;
+      }
+#pragma unroll
+      for (int k = 0; k < kPpMaxK; ++k) {
+        const uint32_t x = __shfl(nk, k, 64);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          n[k][r] = (k < K && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
+        }
+      }
+      float sp = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) sp += v[r] * u[r];
+      for (int m = 32; m > 0; m >>= 1) sp += __shfl_xor(sp, m, 64);
+      const float gp = sigm(sp) - 1.f;  // d/ds softplus(-s)
+      if (lane == 0) {
+        loss += softplus(-sp);
+        npairs += 1.f;
+        gpair[t * 2 * W + o] = gp;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) gv[r] += gp * u[r];
+#pragma unroll
+      for (int k = 0; k < kPpMaxK; ++k) {
+        if (k >= K) break;
+        float sn = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) sn += v[r] * n[k][r];
+        for (int m = 32; m > 0; m >>= 1) sn += __shfl_xor(sn, m, 64);
+        const float gn = sigm(sn);  // d/ds softplus(s)
+        if (lane == 0) loss += softplus(sn);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          gv[r] += gn * n[k][r];
+          if (d < D) on[(long long)k * D + d] = gn * v[r];
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (lane + 64 * r < D) ograd[t * D + lane + 64 * r] = gv[r];
+  }
+  if (lane == 0) {
+    red[0][w] = loss;
+    red[1][w] = npairs;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (loss_sum) ctr_addf(loss_sum, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    if (pair_sum) ctr_addf(pair_sum, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void k_w2v_ppctx(const uint32_t* __restrict__ inv_c,
+                                                   const float* __restrict__ gpair, int B, int W,
+                                                   const float* __restrict__ uvals,
+                                                   float* __restrict__ ograd) {
+  constexpr int R = (D + 63) / 64;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const long long Rn = (long long)B + 2 * W;
+  const long long q = (long long)blockIdx.x * 4 + w;  // run position
+  if (q >= Rn) return;  // wave-uniform
+  // lane o < 2W: the pair (center t = q - W - dq, q) of offset slot o, whose
+  // g+ k_w2v_pp stored (0 when the pair is not valid)
+  uint32_t cl = kInv;
+  float gl = 0.f;
+  if (lane < 2 * W) {
+    const int o = lane, dq = o < W ? o - W : o - W + 1;
+    const long long t = q - W - dq;
+    if (t >= 0 && t < B) {
+      gl = gpair[t * 2 * W + o];
+      if (gl != 0.f) cl = inv_c[t];
+    }
+  }
+  float acc[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) acc[r] = 0.f;
+  for (int o = 0; o < 2 * W; ++o) {
+    const uint32_t c = __shfl(cl, o, 64);
+    const float g = __shfl(gl, o, 64);
+    if (c == kInv) continue;  // wave-uniform
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int d = lane + 64 * r;
+      if (d < D) acc[r] += g * uvals[(long long)c * D + d];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r)
+    if (lane + 64 * r < D) ograd[(B + q) * D + lane + 64 * r] = acc[r];
 }
 
 // Synthetic token stream in the windowed layout: sentences of L tokens, each
@@ -1018,6 +1174,32 @@ void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t
       throw_error("w2v_win: D must be 32, 64 or 128");
   }
   check_launch("k_w2v_win_bf16");
+}
+
+void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
+                   const int32_t* meta, int B, int W, int K, int D, const float* uvals,
+                   float* ograd, float* gpair, float* loss_sum, float* pair_sum, hipStream_t st) {
+  if (B <= 0) return;
+  if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_pp: window must be in [1, 15]");
+  if (K < 1 || K > kPpMaxK) throw_error("w2v_pp: negatives per pair must be in [1, 16]");
+  const long long Rn = (long long)B + 2 * W;
+  switch (D) {
+#define SS_W2VP_CASE(DD)                                                                       \
+  case DD:                                                                                     \
+    hipLaunchKernelGGL(k_w2v_pp<DD>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, inv_c,    \
+                       inv_w, inv_n, meta, B, W, K, uvals, ograd, gpair, loss_sum, pair_sum);  \
+    check_launch("k_w2v_pp");                                                                  \
+    hipLaunchKernelGGL(k_w2v_ppctx<DD>, dim3((unsigned)((Rn + 3) / 4)), dim3(256), 0, st,       \
+                       inv_c, gpair, B, W, uvals, ograd);                                      \
+    check_launch("k_w2v_ppctx");                                                               \
+    break;
+    SS_W2VP_CASE(32)
+    SS_W2VP_CASE(64)
+    SS_W2VP_CASE(128)
+#undef SS_W2VP_CASE
+    default:
+      throw_error("w2v_pp: D must be 32, 64 or 128");
+  }
 }
 
 void launch_w2v_stream_gen(uint64_t seed, long long base, int B, int W, int L, long long nneg,

@@ -107,7 +107,17 @@ class PSContext:
             else:
                 tr = TorchDistTransport()
         else:
-            tr = LoopbackTransport()
+            # SS_ENGINE_GENERAL: a 1-GPU job through the N>1 engine path over a
+            # size-1 mailbox arena / RCCL communicator (as bench.py)
+            general = os.environ.get("SS_ENGINE_GENERAL", "0")
+            if general == "xgmi":
+                from ..parallel.xgmi import XgmiTransport
+
+                tr = XgmiTransport(0, 1, self.device, None)
+            elif general == "rccl":
+                tr = RcclTransport(0, 1, self.device, uid=RcclTransport.new_unique_id())
+            else:
+                tr = LoopbackTransport()
         self.transport = tr
         self.table = (HbmTable(dim, capacity, optimizer=optimizer, init=init, device=self.device)
                       if self.is_server else None)
@@ -293,7 +303,8 @@ def build_worker(cfg: Config):
                             vocab=int(float(cfg.get("vocab", 1e6))),
                             negatives=int(cfg.get("negatives", 5)),
                             mode=cfg.get("w2v_mode", "window"),
-                            sentence_len=int(cfg.get("sentence_len", 24)))
+                            sentence_len=int(cfg.get("sentence_len", 24)),
+                            neg_mode=cfg.get("neg_mode", "shared"))
         dim = int(cfg.get("dim", 128))
         opt, init = make_w2v_table_args(dim, opt)
         cap = int(cfg.get("table_capacity", 0) or 2 * data.vocab / nserv / load + 1024)
@@ -375,7 +386,14 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
              "rounds_timed": done,
              "loss": w.mean_loss() if ctx.is_worker else None, "hipgraph": bool(graphed),
              "start_round": ctx.start_round, "passes": passes,
-             "rank0_quota": w.quota}
+             "rank0_quota": w.quota,
+             "transport": getattr(ctx.transport, "label", type(ctx.transport).__name__)}
+    if cfg.get("model", "sparse_lr") == "word2vec" and ctx.is_worker:
+        d = w.data
+        stats["w2v"] = {"layout": d.mode, "neg_mode": getattr(d, "neg_mode", "shared"),
+                        "mfma": "bf16" if (d.mode == "window" and not w.per_pair)
+                        or w.mfma_bf16 else "fp32" if d.mode == "pairs" else "none (fp32 dots)",
+                        "negatives": d.negatives}
     m = ctx.engine.metrics.counters
     if m:
         stats["rank0_engine"] = {k: int(v) for k, v in m.items()}

@@ -41,7 +41,20 @@ class W2VLayout:
     run position (sentence tag, reduced window, mask); the contexts of a
     center are its run neighbours, as in word2vec's sliding window.
     ``mode="pairs"``: i.i.d. centers with 2W sampled contexts each, keys =
-    [B centers | B x 2W contexts | negatives]."""
+    [B centers | B x 2W contexts | negatives].
+
+    ``neg_mode="shared"`` (default): each 64-center tile trains against 64
+    shared negatives weighted to K per pair (GEMMs on the MFMA);
+    ``"per_pair"`` (window mode): word2vec's own objective, K negatives drawn
+    for every positive pair (B x 2W x K negative keys per step)."""
+
+    neg_mode = "shared"
+
+    @property
+    def n_neg(self) -> int:
+        if getattr(self, "neg_mode", "shared") == "per_pair":
+            return self.batch_size * self.contexts * self.negatives
+        return self.tiles * NEG_TILE
 
     @property
     def contexts(self) -> int:
@@ -58,8 +71,8 @@ class W2VLayout:
     @property
     def n_keys(self) -> int:
         if self.mode == "window":
-            return self.batch_size + self.run_len + self.tiles * NEG_TILE
-        return self.batch_size * (1 + self.contexts) + self.tiles * NEG_TILE
+            return self.batch_size + self.run_len + self.n_neg
+        return self.batch_size * (1 + self.contexts) + self.n_neg
 
     @property
     def neg_scale(self) -> float:
@@ -77,6 +90,10 @@ class W2VLayout:
             raise ValueError(f"word2vec batch mode must be window or pairs, not {self.mode!r}")
         if self.mode == "window" and not 1 <= self.window <= 15:
             raise ValueError("window mode: window must be in [1, 15]")
+        if self.neg_mode not in ("shared", "per_pair"):
+            raise ValueError(f"word2vec neg_mode must be shared or per_pair, not {self.neg_mode!r}")
+        if self.neg_mode == "per_pair" and (self.mode != "window" or not 1 <= self.negatives <= 16):
+            raise ValueError("per_pair negatives: window mode, 1..16 negatives per pair")
 
 
 @dataclass
@@ -89,6 +106,7 @@ class W2VSynth(W2VLayout):
     seed: int = 1234
     mode: str = "window"           # window | pairs (see W2VLayout)
     sentence_len: int = 24         # window mode: tokens per synthetic sentence
+    neg_mode: str = "shared"       # shared | per_pair (see W2VLayout)
 
     def __post_init__(self):
         self._check_mode()
@@ -104,12 +122,12 @@ class W2VSynth(W2VLayout):
             if meta is None or meta.numel() < self.run_len:
                 raise ValueError("window mode: generate() needs a meta buffer of run_len int32")
             hip().w2v_stream_gen(self.seed, base, B, self.window, self.sentence_len,
-                                 self.tiles * NEG_TILE, self.vocab, self.noise, keys.data_ptr(),
+                                 self.n_neg, self.vocab, self.noise, keys.data_ptr(),
                                  meta.data_ptr(), st, step_dev, world * B,
                                  (step_delta * world + rank) * B)
             return
         hip().w2v_gen(self.seed, base, B, self.contexts, self.window,
-                      self.tiles * NEG_TILE, self.vocab, self.noise, keys.data_ptr(), st,
+                      self.n_neg, self.vocab, self.noise, keys.data_ptr(), st,
                       step_dev, world * B, (step_delta * world + rank) * B)
 
 
@@ -154,11 +172,17 @@ class Word2VecWorker(PipelinedWorker):
         # the tile (0.101 -> 0.092 ms/step)
         self.occ_reduce = (self.window_mode and engine.gpu and
                            all(getattr(d, "mode", None) == "bucket" for d in engine.dedupers))
+        self.per_pair = getattr(data, "neg_mode", "shared") == "per_pair"
+        if self.per_pair and not self.occ_reduce:
+            raise ValueError("per_pair negatives need the bucketed dedup (SS_DEDUP=bucket)")
         if self.occ_reduce:
             dev, n, D, W = engine.device, data.n_keys, engine.dim, data.window
             self.ograd = torch.empty((n, D), dtype=torch.float32, device=dev)
             self.otail = torch.empty((max(1, (data.tiles - 1) * 2 * W), D), dtype=torch.float32,
                                      device=dev)
+            # per_pair: g+ of every (center, offset) pair (k_w2v_pp -> k_w2v_ppctx)
+            self.gpair = (torch.empty(data.batch_size * 2 * W, dtype=torch.float32, device=dev)
+                          if self.per_pair else None)
             self.ord = [torch.empty(n, dtype=torch.int32, device=dev)
                         for _ in range(engine.depth)]
             self.items = [torch.empty((n, 4), dtype=torch.int32, device=dev)
@@ -187,6 +211,15 @@ class Word2VecWorker(PipelinedWorker):
         B, C = d.batch_size, d.contexts
         ptr, es = inv.data_ptr(), inv.element_size()
         h = hip()
+        if self.per_pair:
+            h.w2v_pp(ptr, ptr + B * es, ptr + (B + d.run_len) * es, self.meta[slot].data_ptr(),
+                     B, d.window, d.negatives, self.engine.dim, rnd.uvals.data_ptr(),
+                     self.ograd.data_ptr(), self.gpair.data_ptr(), self.loss_sum.data_ptr(),
+                     self.pair_sum.data_ptr(), st)
+            h.w2v_oreduce(self.items[slot].data_ptr(), d.n_keys, self.ord[slot].data_ptr(),
+                          self.ograd.data_ptr(), 0, B, d.window, self.engine.dim,
+                          rnd.ugrad.data_ptr(), st)
+            return
         if self.window_mode:
             occ = self.occ_reduce
             h.w2v_win(ptr, ptr + B * es, ptr + (B + d.run_len) * es, self.meta[slot].data_ptr(),
@@ -253,6 +286,25 @@ def sgns_window_reference(V: np.ndarray, U: np.ndarray, N: np.ndarray, mask: np.
     Gn = cw * sig(Sn)
     loss = np.where(mask, sp(-Sp), 0.0).sum() + (cw * sp(Sn)).sum()
     return loss, n.sum(), Gp @ U + Gn @ N, Gp.T @ V, Gn.T @ V
+
+
+def sgns_pp_reference(V: np.ndarray, U: np.ndarray, N: np.ndarray, mask: np.ndarray):
+    """fp64 reference of per-pair negatives.  V [B,D] centers, U [B,2W,D]
+    context rows by offset slot, N [B,2W,K,D] each pair's negatives, mask
+    [B,2W] valid pairs.  Returns (loss, gV, gU, gN) (zero where not valid)."""
+    V, U, N = (a.astype(np.float64) for a in (V, U, N))
+    sig = lambda z: 1.0 / (1.0 + np.exp(-z))  # noqa: E731
+    sp = lambda z: np.maximum(z, 0) + np.log1p(np.exp(-np.abs(z)))  # noqa: E731
+    m = mask.astype(np.float64)
+    s_p = np.einsum("bd,bod->bo", V, U)
+    s_n = np.einsum("bd,bokd->bok", V, N)
+    gp = (sig(s_p) - 1.0) * m
+    gn = sig(s_n) * m[:, :, None]
+    loss = (sp(-s_p) * m).sum() + (sp(s_n) * m[:, :, None]).sum()
+    gV = np.einsum("bo,bod->bd", gp, U) + np.einsum("bok,bokd->bd", gn, N)
+    gU = gp[:, :, None] * V[:, None, :]
+    gN = gn[:, :, :, None] * V[:, None, None, :]
+    return loss, gV, gU, gN
 
 
 def sgns_reference(V: np.ndarray, X: np.ndarray, N: np.ndarray, neg_scale: float):

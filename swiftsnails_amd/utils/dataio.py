@@ -36,7 +36,6 @@ import torch
 
 from .._native import host
 
-NEG_TILE = 64
 TILE = 64
 
 
@@ -244,12 +243,13 @@ class FileCorpusSource(W2VLayout):
                  rank: int = 0, world: int = 1, min_count: int = 1, sample: float = 0.0,
                  seed: int = 1234, nthreads: int = 8, prefetch: int = 3,
                  pin: Optional[bool] = None, resident: Optional[str] = None, device=None,
-                 mode: str = "window"):
+                 mode: str = "window", neg_mode: str = "shared"):
         self.corpus = host().Corpus(path, nthreads, rank, world, min_count, sample)
         self.batch_size = int(batch_size)
         self.window = int(window)
         self.negatives = int(negatives)
         self.mode = mode
+        self.neg_mode = neg_mode
         self._check_mode()
         self.seed = int(seed) + 7919 * rank
         self.nthreads = nthreads
@@ -299,11 +299,11 @@ class FileCorpusSource(W2VLayout):
     def _fill(self, step: int, buf):
         if self.mode == "window":
             self.corpus.fill_skipgram_window(self.seed, step, self.batch_size, self.window,
-                                             self.tiles * NEG_TILE, buf["keys"].data_ptr(),
+                                             self.n_neg, buf["keys"].data_ptr(),
                                              buf["meta"].data_ptr())
             return
         self.corpus.fill_skipgram(self.seed, step, self.batch_size, self.contexts, self.window,
-                                  self.tiles * NEG_TILE, buf["keys"].data_ptr(), self.nthreads)
+                                  self.n_neg, buf["keys"].data_ptr(), self.nthreads)
 
     def generate(self, step: int, rank: int, world: int, keys: torch.Tensor, stream=None,
                  step_dev: int = 0, step_delta: int = 0, meta: Optional[torch.Tensor] = None):
@@ -325,7 +325,7 @@ class FileCorpusSource(W2VLayout):
                                         self.d_keep.data_ptr() if self.d_keep is not None else 0,
                                         self.d_tokens.numel(), self.seed, step, step_dev,
                                         step_delta, self.batch_size, self.window,
-                                        self.tiles * NEG_TILE, OUT_BIT, keys.data_ptr(),
+                                        self.n_neg, OUT_BIT, keys.data_ptr(),
                                         meta.data_ptr(), st)
                 return
             hip().w2v_corpus_batch(self.d_tokens.data_ptr(), self.d_soffs.data_ptr(),
@@ -334,7 +334,7 @@ class FileCorpusSource(W2VLayout):
                                    self.d_keep.data_ptr() if self.d_keep is not None else 0,
                                    self.d_tokens.numel(), self.seed, step, step_dev, step_delta,
                                    self.batch_size, self.contexts, self.window,
-                                   self.tiles * NEG_TILE, OUT_BIT, keys.data_ptr(), st)
+                                   self.n_neg, OUT_BIT, keys.data_ptr(), st)
             return
         if step_dev:
             raise RuntimeError("host-fed corpus batches cannot be replayed from a graph")
@@ -386,7 +386,7 @@ def make_ctr_source(cfg, rank: int = 0, world: int = 1, device=None):
 
 def make_corpus_source(cfg, rank: int = 0, world: int = 1, device=None):
     """Config keys: data_path, batch_size, window, negatives, min_count, sample,
-    data_resident (auto|hbm|host), w2v_mode (window|pairs)."""
+    data_resident (auto|hbm|host), w2v_mode (window|pairs), neg_mode (shared|per_pair)."""
     path, shard, nshards = rank_data_path(cfg.get("data_path"), rank, world)
     return FileCorpusSource(path, batch_size=int(cfg.get("batch_size", 16384)),
                             seed=1234 + 7919 * (rank - shard),  # negatives differ per rank
@@ -396,4 +396,5 @@ def make_corpus_source(cfg, rank: int = 0, world: int = 1, device=None):
                             sample=float(cfg.get("sample", 0.0)),
                             nthreads=int(cfg.get("data_threads", 8)),
                             resident=cfg.get("data_resident", "auto"), device=device,
-                            mode=cfg.get("w2v_mode", "window"))
+                            mode=cfg.get("w2v_mode", "window"),
+                            neg_mode=cfg.get("neg_mode", "shared"))

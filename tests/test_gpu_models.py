@@ -114,6 +114,56 @@ def test_w2v_window_tile_matches_reference(dev, D, W, B):
     assert not G[B:B + R][meta < 0].any()
 
 
+@pytest.mark.parametrize("D,W,K,B", [(32, 2, 3, 70), (64, 5, 5, 128), (128, 5, 5, 200),
+                                     (128, 15, 16, 40)])
+def test_w2v_per_pair_negatives_match_reference(dev, D, W, K, B):
+    """Classic SGNS (k_w2v_pp + k_w2v_ppctx): K negatives per positive pair,
+    gradients as occurrence rows.  Every key position its own row: the center
+    rows, the run-position rows (summed over the 2W centers that pair with
+    them) and every negative occurrence row vs the fp64 reference; rows of
+    invalid pairs and masked positions are written as zeros."""
+    from swiftsnails_amd._native import hip
+    from swiftsnails_amd.models.word2vec import sgns_pp_reference, window_pairs_reference
+
+    R = B + 2 * W
+    rng = np.random.default_rng(D + W + K)
+    tags = np.cumsum(rng.random(R) < 0.08)
+    bs = rng.integers(1, W + 1, R)
+    meta = ((tags << 4) | bs).astype(np.int32)
+    meta[rng.random(R) < 0.1] = -1
+    nneg = B * 2 * W * K
+    nrows = B + R + nneg
+    U = (rng.standard_normal((nrows, D)) * 0.3).astype(np.float32)
+    inv = np.arange(nrows, dtype=np.int32)
+    og = torch.full((nrows, D), float("nan"), device=dev)  # every row must be written
+    gp = torch.empty(B * 2 * W, device=dev)
+    loss, pairs = torch.zeros(256 * 32, device=dev), torch.zeros(256 * 32, device=dev)
+    tu, ti, tm = (torch.from_numpy(U).to(dev), torch.from_numpy(inv).to(dev),
+                  torch.from_numpy(meta).to(dev))
+    p = ti.data_ptr()
+    hip().w2v_pp(p, p + B * 4, p + (B + R) * 4, tm.data_ptr(), B, W, K, D, tu.data_ptr(),
+                 og.data_ptr(), gp.data_ptr(), loss.data_ptr(), pairs.data_ptr(),
+                 torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    G = og.cpu().numpy().astype(np.float64)
+    assert np.isfinite(G).all()
+    band = window_pairs_reference(meta, B, W)  # [B, R]
+    offs = [o - W if o < W else o - W + 1 for o in range(2 * W)]
+    qidx = np.arange(B)[:, None] + W + np.array(offs)[None, :]  # [B, 2W] run positions
+    mask = band[np.arange(B)[:, None], qidx]
+    V = U[:B]
+    Uc = U[B + qidx]
+    N = U[B + R:].reshape(B, 2 * W, K, D)
+    l, gV, gU, gN = sgns_pp_reference(V, Uc, N, mask)
+    ref = np.zeros((nrows, D))
+    ref[:B] = gV
+    np.add.at(ref, B + qidx.reshape(-1), gU.reshape(-1, D))
+    ref[B + R:] = gN.reshape(-1, D)
+    assert mask.sum() > 0 and pairs.sum().item() == mask.sum()
+    np.testing.assert_allclose(G, ref, rtol=2e-4, atol=2e-5)
+    np.testing.assert_allclose(loss.sum().item(), l, rtol=1e-4)
+
+
 def test_w2v_stream_gen_window_layout(dev):
     """Synthetic stream (k_w2v_stream_gen): centers are the run's middle
     positions, sentence tags follow the position, reduced windows in [1, W],
@@ -648,14 +698,17 @@ def _planted_corpus(path, clusters=20, words=40, sentences=6000, length=12, seed
     return clusters, words
 
 
-@pytest.mark.parametrize("tile", ["bf16", "f32"])
-@pytest.mark.parametrize("mode", ["window", "pairs"])
-def test_word2vec_learns_planted_clusters(dev, tmp_path, monkeypatch, tile, mode):
+@pytest.mark.parametrize("mode,neg_mode,tile", [("window", "shared", "bf16"),
+                                                ("pairs", "shared", "bf16"),
+                                                ("pairs", "shared", "f32"),
+                                                ("window", "per_pair", "f32")])
+def test_word2vec_learns_planted_clusters(dev, tmp_path, monkeypatch, mode, neg_mode, tile):
     """Embedding quality, not just a falling loss: on a corpus whose
     sentences each draw from one of 20 word clusters, the learned input
     vectors of words of the same cluster are far more similar (cosine) than
-    of words of different clusters — for both batch layouts and both MFMA
-    tile precisions of the shared-negative objective."""
+    of words of different clusters — for every objective variant: the
+    shared-negative tile (window layout: bf16 MFMA; pairs layout: bf16 and
+    fp32 MFMA) and per-pair negatives (classic SGNS, fp32 dot products)."""
     from swiftsnails_amd.models.word2vec import Word2VecWorker, make_w2v_table_args
     from swiftsnails_amd.ops.table import HbmTable
     from swiftsnails_amd.parallel.engine import PSEngine
@@ -664,12 +717,12 @@ def test_word2vec_learns_planted_clusters(dev, tmp_path, monkeypatch, tile, mode
     monkeypatch.setenv("SS_W2V_MFMA", tile)
     C, M = _planted_corpus(tmp_path / "corpus.txt")
     data = FileCorpusSource(str(tmp_path / "corpus.txt"), batch_size=2048, window=4,
-                            negatives=5, mode=mode, device=dev)
+                            negatives=5, mode=mode, neg_mode=neg_mode, device=dev)
     opt, init = make_w2v_table_args(64, None)
     table = HbmTable(64, 1 << 14, optimizer=opt, init=init, device=dev)
     eng = PSEngine(table, None, max_keys=data.n_keys, dim=64, device=dev)
     w = Word2VecWorker(eng, data)
-    assert w.mfma_bf16 == (tile == "bf16")
+    assert w.mfma_bf16 == (tile == "bf16") and w.per_pair == (neg_mode == "per_pair")
     for _ in range(3 * data.steps_per_pass()):  # 3 passes
         w.step()
     torch.cuda.synchronize()

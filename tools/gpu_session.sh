@@ -51,6 +51,10 @@ for s in "${STEP_LIST[@]}"; do
     fast_w2v) run fast_w2v 600 python -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 64 --warmup 16 ;;
     prof_w2v_x) run rocprof_w2v_x 600 env SS_ENGINE_GENERAL=xgmi rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_w2v_x" -o run -- python3 -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 32 --warmup 16 ;;
     prof_lr4k_x) run rocprof_lr4k_x 600 env SS_ENGINE_GENERAL=xgmi rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_lr4k_x" -o run -- python3 bench.py --batch 4096 --steps 32 --warmup 16 --graph on ;;
+    w2v_pp) run w2v_pp 600 python -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 64 --warmup 16 --set neg_mode=per_pair ;;
+    w2v_pairs_f32) run w2v_pairs_f32 600 env SS_W2V_MFMA=f32 python -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 64 --warmup 16 --set w2v_mode=pairs ;;
+    w2v_pairs_bf16) run w2v_pairs_bf16 600 python -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 64 --warmup 16 --set w2v_mode=pairs ;;
+    prof_w2v_pp) run rocprof_w2v_pp 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_w2v_pp" -o run -- python3 -m swiftsnails_amd.launch --config configs/word2vec_1m_4x4.conf --steps 32 --warmup 16 --set neg_mode=per_pair ;;
     general_nopa) run bench_general_nopa 600 env SS_ENGINE_GENERAL=rccl SS_PULL_AHEAD=0 python bench.py $BENCH_ARGS ;;
     prof) run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- python3 bench.py --steps 10 --warmup 3 ;;
     *) run custom$n 600 bash -c "$s" ;;
