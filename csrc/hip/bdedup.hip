@@ -289,7 +289,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      uint32_t* __restrict__ pj,
                                                      uint32_t* __restrict__ pos_of,
                                                      uint32_t* __restrict__ bkt,
-                                                     uint32_t* __restrict__ osi_inv) {
+                                                     uint4* __restrict__ rec) {
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
@@ -312,9 +312,14 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
         if (k[e] != kEmptyKey) {
           b = bd_bucket(k[e], rs, (uint32_t)Pd);
           pos = atomicAdd(&cur[b], 1u);
-          pj[pos] = (uint32_t)j;
-        } else if (osi_inv) {
-          osi_inv[j] = kBdInvalid;  // never reaches a bucket
+          // rec: the key travels with its sample index as ONE 16-byte store
+          // (a random store costs a write request whatever its width), so
+          // the dedup reads its bucket coalesced instead of gathering
+          // keys[pj[p]] (a 64-byte line per occurrence) and writes pj itself
+          if (rec)
+            rec[pos] = make_uint4((uint32_t)k[e], (uint32_t)(k[e] >> 32), (uint32_t)j, 0u);
+          else
+            pj[pos] = (uint32_t)j;
         }
         // the BdIndex (j -> bucket position, bucket) only for its consumers
         if (pos_of) pos_of[j] = pos;
@@ -326,7 +331,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
 
 // 5. one workgroup per bucket: LDS hash dedup -> bucket-local unique ids
 __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__ keys,
-                                                   const uint32_t* __restrict__ pj,
+                                                   uint32_t* __restrict__ pj,
                                                    const uint32_t* __restrict__ bstart,
                                                    uint32_t* __restrict__ luid,
                                                    uint64_t* __restrict__ bkeys,
@@ -335,7 +340,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    long long ucap,
                                                    uint32_t* __restrict__ ubase,
                                                    unsigned long long* __restrict__ ucount,
-                                                   uint32_t* __restrict__ osi_inv,
+                                                   const uint4* __restrict__ rec,
                                                    unsigned long long* __restrict__ dbg,
                                                    uint64_t* __restrict__ ukeys,
                                                    float* __restrict__ ugrad, int gdim,
@@ -358,16 +363,22 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   // the first kBdRegs occurrences of each thread keep their slot in
   // registers; a hot bucket's excess parks it in luid[] (rewritten below)
-  uint32_t slot[kBdRegs], jr[kBdRegs];
+  uint32_t slot[kBdRegs];
   uint64_t kk[kBdRegs];
+  // the bucket's (key, sample) records read coalesced (rec), pj written back
+  // for the consumers; else keys gathered at keys[pj[p]]
+  auto load = [&](uint32_t p) -> uint64_t {
+    if (rec) {
+      const uint4 v = rec[p];
+      pj[p] = v.z;
+      return (uint64_t)v.x | ((uint64_t)v.y << 32);
+    }
+    return keys[pj[p]];
+  };
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
     const uint32_t p = p0 + t + r * kBdDT;
-    // keys gathered at keys[pj[p]] (staging them in bucket order in the
-    // scatter for a coalesced read here measured slower: 0.949 -> 0.968
-    // ms/step, the extra stores cost the scatter more than the gather saves)
-    jr[r] = p < p1 ? pj[p] : 0u;
-    kk[r] = p < p1 ? keys[jr[r]] : kEmptyKey;
+    kk[r] = p < p1 ? load(p) : kEmptyKey;
   }
   __syncthreads();
   BD_STAMP(0)
@@ -403,7 +414,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
 #pragma unroll
     for (int r = 0; r < kBdRegs; ++r) {
       const uint32_t p = q + r * kBdDT;
-      k2[r] = p < p1 ? keys[pj[p]] : kEmptyKey;
+      k2[r] = p < p1 ? load(p) : kEmptyKey;
     }
 #pragma unroll
     for (int r = 0; r < kBdRegs; ++r) {
@@ -450,25 +461,14 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
       ugrad[ub * (unsigned long long)gdim + e] = 0.f;
   __syncthreads();
   BD_STAMP(2)
-  // osi_inv: the inverse index in OCCURRENCE-SPACE ids (unique key l of
-  // bucket b -> bstart[b] + l, known here without the global scan): one
-  // random 4-B store per occurrence, which the LR forward then reads
-  // coalesced instead of gathering luid[pos_of[j]] (a 64-B line per
-  // occurrence; stores move 32-B sectors, measured FETCH/WRITE_SIZE)
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
     const uint32_t p = p0 + t + r * kBdDT;
-    if (p < p1) {
-      const uint32_t l = slot[r] == kBdInvalid ? kBdInvalid : lid[slot[r]];
-      luid[p] = l;
-      if (osi_inv) osi_inv[jr[r]] = l == kBdInvalid ? kBdInvalid : p0 + l;
-    }
+    if (p < p1) luid[p] = slot[r] == kBdInvalid ? kBdInvalid : lid[slot[r]];
   }
   for (uint32_t p = p0 + t + kBdRegs * kBdDT; p < p1; p += kBdDT) {
     const uint32_t s = luid[p];
-    const uint32_t l = s == kBdInvalid ? kBdInvalid : lid[s];
-    luid[p] = l;
-    if (osi_inv) osi_inv[pj[p]] = l == kBdInvalid ? kBdInvalid : p0 + l;
+    luid[p] = s == kBdInvalid ? kBdInvalid : lid[s];
   }
   __syncthreads();
   BD_STAMP(3)
@@ -607,21 +607,20 @@ template <int DIM>
 __device__ __forceinline__ void fused_row_update(const DevTable& t, long long slot,
                                                  const float (&g)[DIM], const OptParams& op) {
   if (slot < 0) return;
-  float* row = slot_row(t, slot);
   const int ns = opt_state_per_coord(op.kind);
   float w[DIM], s1[DIM], s2[DIM];
 #pragma unroll
   for (int j = 0; j < DIM; ++j) {
-    w[j] = row[j];
-    s1[j] = ns > 0 ? row[DIM + j] : 0.f;
-    s2[j] = ns > 1 ? row[2 * DIM + j] : 0.f;
+    w[j] = row_ld(t, slot, j);
+    s1[j] = ns > 0 ? row_ld(t, slot, DIM + j) : 0.f;
+    s2[j] = ns > 1 ? row_ld(t, slot, 2 * DIM + j) : 0.f;
   }
 #pragma unroll
   for (int j = 0; j < DIM; ++j) {
     opt_update(op, w[j], s1[j], s2[j], g[j]);
-    row[j] = w[j];
-    if (ns > 0) row[DIM + j] = s1[j];
-    if (ns > 1) row[2 * DIM + j] = s2[j];
+    row_st(t, slot, j, w[j], true);
+    if (ns > 0) row_st(t, slot, DIM + j, s1[j], true);
+    if (ns > 1) row_st(t, slot, 2 * DIM + j, s2[j], true);
   }
 }
 
@@ -879,7 +878,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg, uint32_t* osi_inv, uint8_t* usingle, int ndest,
+                     unsigned long long* dbg, uint32_t* rec, uint8_t* usingle, int ndest,
                      long long lay_n) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   // lay_n (N>1 engines): the bucket layout is that of a call of lay_n keys
@@ -939,13 +938,14 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   }
   check_launch("k_bd_colscan");
   SS_BD_CT_DISPATCH(ct, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pj,
-                    pos_of, bkt, osi_inv);
+                    pos_of, bkt, reinterpret_cast<uint4*>(rec));
 #undef SS_BD_CT_DISPATCH
   check_launch("k_bd_scatter");
   // place: unique keys straight into the per-destination send segments
   // (+ zeroed gradient rows), reserved with one atomic per bucket
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
-                     bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount, osi_inv, dbg,
+                     bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
+                     reinterpret_cast<const uint4*>(rec), dbg,
                      place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle);
   check_launch("k_bd_dedup");
   if (inv && n > 0) {
@@ -985,7 +985,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   DevTable tv{};
   OptParams opv{};
   if (slots) {
-    if (!t || !op || osi || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
+    if (!t || !op || osi || t->bf16 || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
         t->row_off % 8 != 0 || t->stride % 8 != 0)
       throw_error("bd_reduce: fused apply needs scalar AdaGrad rows and compact ids");
     tv = *t;
@@ -1021,7 +1021,7 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
   DevTable tv{};
   OptParams opv{};
   if (slots) {
-    if (!t || !op || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
+    if (!t || !op || t->bf16 || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
         t->row_off % 8 != 0 || t->stride % 8 != 0)
       throw_error("bd_reduce_p: fused apply needs scalar AdaGrad rows");
     tv = *t;

@@ -62,11 +62,18 @@ PYBIND11_MODULE(_ss_hip, m) {
 
   py::class_<DevTable>(m, "DevTable", py::module_local())
       .def(py::init([](uintptr_t base, unsigned long long cap, uint32_t stride, uint32_t key_off,
-                       uint32_t dim, uint32_t width, uint32_t prefilled, uint32_t row_off) {
-             return DevTable{P<char>(base), cap, stride, key_off, dim, width, prefilled, row_off};
+                       uint32_t dim, uint32_t width, uint32_t prefilled, uint32_t row_off,
+                       uint32_t bf16) {
+             const uint32_t eb = bf16 ? 2u : 4u;
+             if (row_off + eb * width > stride || (key_off < row_off + eb * width && key_off + 8 > row_off))
+               throw std::invalid_argument("DevTable: row and key overlap inside the slot");
+             return DevTable{P<char>(base), cap, stride, key_off, dim, width, prefilled, row_off,
+                             bf16};
            }),
            py::arg("base"), py::arg("cap"), py::arg("stride"), py::arg("key_off"), py::arg("dim"),
-           py::arg("width"), py::arg("prefilled") = 0, py::arg("row_off") = 0)
+           py::arg("width"), py::arg("prefilled") = 0, py::arg("row_off") = 0,
+           py::arg("bf16") = 0)
+      .def_readonly("bf16", &DevTable::bf16)
       .def_readonly("row_off", &DevTable::row_off)
       .def_readonly("prefilled", &DevTable::prefilled)
       .def_readonly("cap", &DevTable::cap)
@@ -175,19 +182,19 @@ PYBIND11_MODULE(_ss_hip, m) {
                        long long ucap, uintptr_t scratch, uintptr_t pj, uintptr_t pos_of,
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
-                       uintptr_t st, uintptr_t dbg, uintptr_t osi_inv, uintptr_t usingle,
+                       uintptr_t st, uintptr_t dbg, uintptr_t rec, uintptr_t usingle,
                        int ndest, long long lay_n) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
                     P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
                     P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
                     P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg),
-                    P<uint32_t>(osi_inv), P<uint8_t>(usingle), ndest, lay_n);
+                    P<uint32_t>(rec), P<uint8_t>(usingle), ndest, lay_n);
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
-     py::arg("osi_inv") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0,
+     py::arg("rec") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0,
      py::arg("lay_n") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,

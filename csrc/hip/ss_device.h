@@ -49,6 +49,10 @@ struct DevTable {
   // second write to the freshly claimed line
   uint32_t prefilled;
   uint32_t row_off;   // byte offset of the row (params, then optimizer state)
+  // 1: compact rows — parameters and optimizer state stored as bf16 (half
+  // the bytes per slot: capacity for the 10B-key FM table), math in fp32;
+  // read / written through row_ld / row_st
+  uint32_t bf16;
 };
 
 __device__ __forceinline__ uint64_t* slot_key(const DevTable& t, uint64_t s) {
@@ -56,6 +60,55 @@ __device__ __forceinline__ uint64_t* slot_key(const DevTable& t, uint64_t s) {
 }
 __device__ __forceinline__ float* slot_row(const DevTable& t, uint64_t s) {
   return reinterpret_cast<float*>(t.base + s * (uint64_t)t.stride + t.row_off);
+}
+
+// coordinate j of slot s's row as fp32, either storage format.  A bf16 word
+// still holding the empty-slot fill (0xFFFF) reads as the fp32 fill
+// 0xFFFFFFFF, so "not written yet" (table.hip fresh_or) means the same.
+__device__ __forceinline__ float row_ld(const DevTable& t, uint64_t s, uint32_t j) {
+  const char* r = t.base + s * (uint64_t)t.stride + t.row_off;
+  if (t.bf16) {
+    const uint32_t u = reinterpret_cast<const unsigned short*>(r)[j];
+    return __uint_as_float(u == 0xFFFFu ? 0xFFFFFFFFu : (u << 16));
+  }
+  return reinterpret_cast<const float*>(r)[j];
+}
+
+// v as a compact row holds it (bf16 round to nearest even), else v: what a
+// pull returns for a row it just initialised equals what later pulls read
+__device__ __forceinline__ float row_round(const DevTable& t, float v) {
+  if (!t.bf16) return v;
+  uint32_t u = __float_as_uint(v);
+  if ((u & 0x7F800000u) != 0x7F800000u) u += 0x7FFFu + ((u >> 16) & 1u);
+  return __uint_as_float(u & 0xFFFF0000u);
+}
+
+// store v as coordinate j.  bf16: rounded stochastically when `sr` (an
+// optimizer step: round-to-nearest would drop every update below half an
+// ulp — 1/512 of the weight — so small steps would never move a weight),
+// else to nearest even; NaN / Inf keep their top bits (the init marker).
+__device__ __forceinline__ void row_st(const DevTable& t, uint64_t s, uint32_t j, float v,
+                                       bool sr = false) {
+  char* r = t.base + s * (uint64_t)t.stride + t.row_off;
+  if (!t.bf16) {
+    reinterpret_cast<float*>(r)[j] = v;
+    return;
+  }
+  uint32_t u = __float_as_uint(v);
+  if ((u & 0x7F800000u) != 0x7F800000u) {
+    if (sr) {
+      // data-dependent dither (slot, coordinate, value bits): no state, the
+      // same under hipGraph replay
+      uint32_t h = (uint32_t)s * 0x9E3779B1u ^ (j * 0x85EBCA77u) ^ u;
+      h ^= h >> 15;
+      h *= 0x2C1B3C6Du;
+      h ^= h >> 12;
+      u += h & 0xFFFFu;
+    } else {
+      u += 0x7FFFu + ((u >> 16) & 1u);
+    }
+  }
+  reinterpret_cast<unsigned short*>(r)[j] = (unsigned short)(u >> 16);
 }
 
 // A list of (offset, count) segments inside one buffer.  The collective

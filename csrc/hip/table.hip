@@ -58,11 +58,11 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v)
 }
 
 template <int G>
-__device__ __forceinline__ void init_row(const DevTable& t, const InitParams& ip, float* row,
+__device__ __forceinline__ void init_row(const DevTable& t, const InitParams& ip, long long slot,
                                          uint64_t key, int lg) {
   if (t.prefilled) return;
   for (uint32_t j = lg; j < t.width; j += G)
-    row[j] = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
+    row_st(t, slot, j, j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init);
 }
 
 // K3: lookup-or-init (insert=1) or lookup-only (insert=0). slots_out[pos] = slot | -1.
@@ -93,7 +93,7 @@ __global__ __launch_bounds__(256) void k_probe(DevTable t, const uint64_t* __res
       slot = __shfl(slot, 0, G);
       inserted = __shfl(inserted, 0, G);
     }
-    if (inserted) init_row<G>(t, ip, slot_row(t, slot), key, lg);
+    if (inserted) init_row<G>(t, ip, slot, key, lg);
     ins += (lg == 0 && inserted);
   }
   ins = wave_sum_u64(ins);
@@ -116,8 +116,7 @@ __global__ __launch_bounds__(256) void k_gather(DevTable t, const long long* __r
     if (slot < 0) {
       for (uint32_t j = lg; j < t.dim; j += G) o[j] = 0.f;
     } else {
-      const float* row = slot_row(t, slot);
-      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row[j];
+      for (uint32_t j = lg; j < t.dim; j += G) o[j] = row_ld(t, slot, j);
     }
   }
 }
@@ -233,12 +232,11 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
     o[0] = wh.x;
     snap[pos] = wh;
   } else {
-    float* row = slot_row(t, slot);
     if (inserted) {
       for (uint32_t j = lg; j < t.width; j += G) {
         const float v = j < t.dim ? init_value(ip, key, j, t.dim) : ip.state_init;
-        if (!t.prefilled) row[j] = v;
-        if (j < t.dim) o[j] = v;
+        if (!t.prefilled) row_st(t, slot, j, v);
+        if (j < t.dim) o[j] = row_round(t, v);
       }
     } else if (t.dim <= (uint32_t)G * kApplyRegs) {
       // every load before the first store: the compiler cannot prove `o` and
@@ -247,15 +245,16 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
 #pragma unroll
       for (int r = 0; r < kApplyRegs; ++r) {
         const uint32_t j = lg + r * G;
-        if (j < t.dim) v[r] = row[j];
+        if (j < t.dim) v[r] = row_ld(t, slot, j);
       }
 #pragma unroll
       for (int r = 0; r < kApplyRegs; ++r) {
         const uint32_t j = lg + r * G;
-        if (j < t.dim) o[j] = fresh_or(v[r], ip, key, j, t.dim);
+        if (j < t.dim) o[j] = row_round(t, fresh_or(v[r], ip, key, j, t.dim));
       }
     } else {
-      for (uint32_t j = lg; j < t.dim; j += G) o[j] = fresh_or(row[j], ip, key, j, t.dim);
+      for (uint32_t j = lg; j < t.dim; j += G)
+        o[j] = row_round(t, fresh_or(row_ld(t, slot, j), ip, key, j, t.dim));
     }
   }
   ins += (lg == 0 && inserted);
@@ -316,9 +315,9 @@ __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
                                           const float* __restrict__ gr, const OptParams& op,
                                           int lg, const float2* __restrict__ snap = nullptr) {
   if (slot < 0) return;
-  float* row = slot_row(t, slot);
-  if (G == 1 && t.dim == 1 && op.kind == kOptAdaGrad &&
+  if (G == 1 && t.dim == 1 && op.kind == kOptAdaGrad && !t.bf16 &&
       t.row_off % 8 == 0 && t.stride % 8 == 0) {
+    float* row = slot_row(t, slot);
     // scalar-row AdaGrad (sparse LR): the (w, h) pair as one 8-byte load and
     // one 8-byte store instead of two of each.  With a snapshot (the (w, h)
     // the pull read, valid when nothing else wrote the row in between) the
@@ -339,10 +338,10 @@ __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
     for (int r = 0; r < kApplyRegs; ++r) {
       const uint32_t j = lg + r * G;
       if (j < t.dim) {
-        w[r] = row[j];
+        w[r] = row_ld(t, slot, j);
         g[r] = gr[j];
-        s1[r] = ns > 0 ? row[t.dim + j] : 0.f;
-        s2[r] = ns > 1 ? row[2 * t.dim + j] : 0.f;
+        s1[r] = ns > 0 ? row_ld(t, slot, t.dim + j) : 0.f;
+        s2[r] = ns > 1 ? row_ld(t, slot, 2 * t.dim + j) : 0.f;
       }
     }
 #pragma unroll
@@ -350,12 +349,24 @@ __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
       const uint32_t j = lg + r * G;
       if (j < t.dim) {
         opt_update(op, w[r], s1[r], s2[r], g[r]);
-        row[j] = w[r];
-        if (ns > 0) row[t.dim + j] = s1[r];
-        if (ns > 1) row[2 * t.dim + j] = s2[r];
+        row_st(t, slot, j, w[r], true);
+        if (ns > 0) row_st(t, slot, t.dim + j, s1[r], true);
+        if (ns > 1) row_st(t, slot, 2 * t.dim + j, s2[r], true);
       }
     }
+  } else if (t.bf16) {
+    const int ns = opt_state_per_coord(op.kind);
+    for (uint32_t j = lg; j < t.dim; j += G) {
+      float w = row_ld(t, slot, j);
+      float s1 = ns > 0 ? row_ld(t, slot, t.dim + j) : 0.f;
+      float s2 = ns > 1 ? row_ld(t, slot, 2 * t.dim + j) : 0.f;
+      opt_update(op, w, s1, s2, gr[j]);
+      row_st(t, slot, j, w, true);
+      if (ns > 0) row_st(t, slot, t.dim + j, s1, true);
+      if (ns > 1) row_st(t, slot, 2 * t.dim + j, s2, true);
+    }
   } else {
+    float* row = slot_row(t, slot);
     for (uint32_t j = lg; j < t.dim; j += G) opt_apply(op, row, row + t.dim, t.dim, j, gr[j]);
   }
 }
@@ -446,9 +457,8 @@ __global__ __launch_bounds__(256) void k_assign(DevTable t, const uint64_t* __re
       inserted = __shfl(inserted, 0, G);
     }
     if (slot >= 0) {
-      float* row = slot_row(t, slot);
       const float* src = rows + g * (long long)t.width;
-      for (uint32_t j = lg; j < t.width; j += G) row[j] = src[j];
+      for (uint32_t j = lg; j < t.width; j += G) row_st(t, slot, j, src[j]);
     }
     ins += (lg == 0 && inserted);
   }
@@ -476,8 +486,7 @@ __global__ __launch_bounds__(256) void k_export(DevTable t, unsigned long long s
     if (occ) {
       const unsigned long long o = wbase + __popcll(mask & ((1ull << lane) - 1));
       keys_out[o] = key;
-      const float* row = slot_row(t, s0 + i);
-      for (uint32_t j = 0; j < t.width; ++j) rows_out[o * t.width + j] = row[j];
+      for (uint32_t j = 0; j < t.width; ++j) rows_out[o * t.width + j] = row_ld(t, s0 + i, j);
     }
   }
 }
@@ -568,7 +577,8 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
                            int* err, int G, hipStream_t st, float* snap) {
   if (P <= 0) return;
-  if (snap && !(G == 1 && t.dim == 1 && t.width == 2 && t.row_off % 8 == 0 && t.stride % 8 == 0))
+  if (snap && (t.bf16 || !(G == 1 && t.dim == 1 && t.width == 2 && t.row_off % 8 == 0 &&
+                           t.stride % 8 == 0)))
     throw std::invalid_argument("pull snapshot: scalar (w, h) rows with G = 1 only");
   // workgroups per bucket: 4 — one per ~265 unique keys, so a
   // lane probes about once; measured 1.19 -> 1.13-1.17 ms/step vs 1 (the
@@ -598,7 +608,8 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
   // (k_apply_st)
   const int ns = opt_state_per_coord(op.kind);
   const uint32_t W = t.dim * (uint32_t)(1 + ns);
-  if (!snap && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
+  if (snap && t.bf16) throw_error("apply: snapshot applies need fp32 rows");
+  if (!snap && !t.bf16 && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
       W % 2 == 0 && W == t.width && t.row_off % 8 == 0 && t.stride % 8 == 0) {
     SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_st<kG>, dim3(grid_for(max_n, kG, 1 << 22)),
                                         dim3(256), 0, st, t, slots, grads, sl, op));

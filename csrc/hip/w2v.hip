@@ -392,6 +392,19 @@ __device__ __forceinline__ uint64_t w2v_zipf(uint64_t r, long long V, double log
   return (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
 }
 
+// negative samples: word2vec's noise distribution, the unigram distribution
+// to the 3/4 — for the log-uniform corpus above P(k) ~ (k + 1)^-3/4, drawn by
+// inverting its continuous CDF ((x^(1/4) - 1) / ((V + 1)^(1/4) - 1) on
+// [1, V + 1)).  Flatter head than the corpus: the most frequent word is ~0.6%
+// of the draws at V = 1M instead of ~5%
+__device__ __forceinline__ uint64_t w2v_noise(uint64_t r, long long V) {
+  const double u = (double)(r >> 11) * (1.0 / 9007199254740992.0);
+  const double q = sqrt(sqrt((double)V + 1.0));
+  const double x = 1.0 + u * (q - 1.0);
+  long long v = (long long)((x * x) * (x * x)) - 1;
+  return (uint64_t)(v < 0 ? 0 : (v >= V ? V - 1 : v));
+}
+
 // Synthetic skip-gram batches. Centers are Zipf-like (log-uniform) over V
 // words; a context sits within +-W ids of its center (words with nearby ids
 // co-occur: learnable structure) except with probability `noise`; negatives
@@ -425,7 +438,10 @@ __global__ __launch_bounds__(256) void k_w2v_gen(uint64_t seed, long long base, 
     keys[i] = x | kOut;
   } else {
     const long long q = i - B - (long long)B * C;
-    keys[i] = zipf(splitmix64(seed ^ 0xBADC0DEull ^ ((uint64_t)(base + q) * 0xD1B54A32D192ED03ull))) | kOut;
+    // (base, q) hashed apart: a step's negatives never repeat another's,
+    // whatever their count per step
+    keys[i] = w2v_noise(splitmix64(seed ^ 0xBADC0DEull ^ splitmix64((uint64_t)base) ^
+                                   ((uint64_t)q * 0xD1B54A32D192ED03ull)), V) | kOut;
   }
 }
 
@@ -696,9 +712,23 @@ __global__ __launch_bounds__(kOsT) void k_w2v_osort(const uint32_t* __restrict__
   const uint32_t nu = min(unum[b], (uint32_t)kOsMaxU);
   for (uint32_t l = tid; l < nu; l += kOsT) cnt[l] = 0u;
   __syncthreads();
-  for (uint32_t p = p0 + tid; p < p1; p += kOsT) {
-    const uint32_t l = luid[p];
-    if (l < nu) atomicAdd(&cnt[l], 1u);
+  // loops with wave-uniform bounds: the hottest key of each wave's 64
+  // occurrences (lane-first match) takes one LDS atomic for all its lanes —
+  // a Zipf-head key (thousands of occurrences in one bucket: the negatives
+  // of a per-pair step) otherwise serialises its bucket's workgroup on one
+  // LDS word
+  const int lane = tid & 63;
+  for (uint32_t q = p0 + (tid & ~63u); q < p1; q += kOsT) {
+    const uint32_t p = q + lane;
+    const uint32_t l = p < p1 ? luid[p] : kInv;
+    const bool ok = l < nu;
+    const unsigned long long m = __ballot(ok);
+    if (!m) continue;  // wave-uniform
+    const int lead = __ffsll((long long)m) - 1;
+    const uint32_t lh = __shfl(l, lead, 64);
+    const unsigned long long same = __ballot(ok && l == lh);
+    if (lane == lead) atomicAdd(&cnt[lh], (uint32_t)__popcll(same));
+    else if (ok && l != lh) atomicAdd(&cnt[l], 1u);
   }
   __syncthreads();
   constexpr int PT = kOsMaxU / kOsT;  // counts per thread, consecutive keys
@@ -729,11 +759,23 @@ __global__ __launch_bounds__(kOsT) void k_w2v_osort(const uint32_t* __restrict__
   }
   for (uint32_t q = p0 + toti + tid; q < p1; q += kOsT) items[q] = make_uint4(0u, 0u, 0u, 0u);
   __syncthreads();
-  for (uint32_t p = p0 + tid; p < p1; p += kOsT) {
-    const uint32_t l = luid[p];
-    if (l >= nu) continue;
+  for (uint32_t q = p0 + (tid & ~63u); q < p1; q += kOsT) {
+    const uint32_t p = q + lane;
+    const uint32_t l = p < p1 ? luid[p] : kInv;
+    const bool ok = l < nu;
+    const unsigned long long m = __ballot(ok);
+    if (!m) continue;  // wave-uniform
+    const int lead = __ffsll((long long)m) - 1;
+    const uint32_t lh = __shfl(l, lead, 64);
+    const bool hot = ok && l == lh;
+    const unsigned long long same = __ballot(hot);
+    uint32_t o = 0;
+    if (lane == lead) o = atomicAdd(&cnt[lh], (uint32_t)__popcll(same));
+    o = __shfl(o, lead, 64) + (uint32_t)__popcll(same & ((1ull << lane) - 1ull));
+    if (ok && !hot) o = atomicAdd(&cnt[l], 1u);
+    if (!ok) continue;
     const uint32_t j = pj[p];
-    ord[p0 + atomicAdd(&cnt[l], 1u)] = j;
+    ord[p0 + o] = j;
     // most keys occur once: their item carries the key position itself
     // (flag 2), so the reduce skips the dependent `ord` load
     if (ifirst[l] & 0x80000000u) items[ifirst[l] & 0x7FFFFFFFu] = make_uint4(j, 1u, base + l, 2u);
@@ -1007,8 +1049,8 @@ __global__ __launch_bounds__(256) void k_w2v_stream_gen(
   } else if (i < R + nneg) {
     const long long q = i - R;
     keys[B + R + q] =
-        w2v_zipf(splitmix64(seed ^ 0xBADC0DEull ^ ((uint64_t)(base + q) * 0xD1B54A32D192ED03ull)), V,
-                 logV) | kOut;
+        w2v_noise(splitmix64(seed ^ 0xBADC0DEull ^ splitmix64((uint64_t)base) ^
+                             ((uint64_t)q * 0xD1B54A32D192ED03ull)), V) | kOut;
   }
 }
 

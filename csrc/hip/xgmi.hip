@@ -129,6 +129,14 @@ struct XWait {
   long long fix_data_off[kXMaxParts];
   long long fix_seg_bytes[kXMaxParts];
   long long fix_bytes[kXMaxParts];
+  // optional exchange counters, added once the wait is over (no launch of
+  // their own): acc[0..2] += sum(sent), sum(recv), bpk * both; xacc += *xval
+  const long long* m_sent;
+  const long long* m_recv;
+  double m_bpk;
+  double* m_acc;
+  const long long* m_xval;
+  double* m_xacc;
 };
 
 __global__ __launch_bounds__(64) void k_xwait(char* arena, XWait W,
@@ -158,31 +166,20 @@ __global__ __launch_bounds__(64) void k_xwait(char* arena, XWait W,
     }
   }
   __syncthreads();
-  if (s == 0) waited[W.ch] = target;
-}
-
-// per-round exchange counters without a host sync and in one launch:
-// acc[0] += sum(sent), acc[1] += sum(recv), acc[2] += bytes_per_key * both
-__global__ __launch_bounds__(64) void k_xmetrics(const long long* sent, const long long* recv,
-                                                 int n, double bytes_per_key, double* acc) {
-  if (threadIdx.x != 0) return;
-  long long a = 0, b = 0;
-  for (int i = 0; i < n; ++i) {
-    a += sent[i];
-    b += recv[i];
+  if (s == 0) {
+    waited[W.ch] = target;
+    if (W.m_acc) {
+      long long a = 0, b = 0;
+      for (int i = 0; i < W.nranks; ++i) {
+        a += W.m_sent[i];
+        b += W.m_recv[i];
+      }
+      W.m_acc[0] += (double)a;
+      W.m_acc[1] += (double)b;
+      W.m_acc[2] += W.m_bpk * (double)(a + b);
+    }
+    if (W.m_xacc) W.m_xacc[0] += (double)W.m_xval[0];
   }
-  acc[0] += (double)a;
-  acc[1] += (double)b;
-  acc[2] += bytes_per_key * (double)(a + b);
-}
-
-void launch_xmetrics(uintptr_t sent, uintptr_t recv, int n, double bytes_per_key, uintptr_t acc,
-                     uintptr_t st) {
-  hipLaunchKernelGGL(k_xmetrics, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(st),
-                     reinterpret_cast<const long long*>(sent),
-                     reinterpret_cast<const long long*>(recv), n, bytes_per_key,
-                     reinterpret_cast<double*>(acc));
-  check_launch("k_xmetrics");
 }
 
 // ---------------------------------------------------------------- host side
@@ -281,8 +278,10 @@ class XgmiArena {
   }
 
   // fixed: (data_off, seg_bytes, bytes) of the parts zeroed for a missing source
+  // metrics: () or (sent, recv, acc, xval, xacc) device pointers (0 = none),
+  // bpk: bytes per key of the exchange counter
   void wait(int ch, const std::vector<std::vector<long long>>& fixed, double timeout_s,
-            uintptr_t stream) {
+            uintptr_t stream, const std::vector<uintptr_t>& metrics, double bpk) {
     if (ch < 0 || ch >= kXMaxCh) throw_error("xgmi: bad channel");
     XWait W{};
     W.nranks = nranks_;
@@ -294,6 +293,17 @@ class XgmiArena {
       W.fix_data_off[q] = fixed[q][0];
       W.fix_seg_bytes[q] = fixed[q][1];
       W.fix_bytes[q] = fixed[q][2];
+    }
+    if (!metrics.empty()) {
+      if (metrics.size() != 5) throw_error("xgmi: metrics = (sent, recv, acc, xval, xacc)");
+      W.m_sent = reinterpret_cast<const long long*>(metrics[0]);
+      W.m_recv = reinterpret_cast<const long long*>(metrics[1]);
+      W.m_acc = reinterpret_cast<double*>(metrics[2]);
+      W.m_xval = reinterpret_cast<const long long*>(metrics[3]);
+      W.m_xacc = reinterpret_cast<double*>(metrics[4]);
+      W.m_bpk = bpk;
+      if ((W.m_acc && (!W.m_sent || !W.m_recv)) || (W.m_xacc && !W.m_xval))
+        throw_error("xgmi: metrics pointers incomplete");
     }
     unsigned long long* waited = local_ + kXMaxCh * kXMaxRanks;
     hipLaunchKernelGGL(k_xwait, dim3(1), dim3(64), 0, reinterpret_cast<hipStream_t>(stream),
@@ -385,8 +395,7 @@ void bind_xgmi(py::module_& m) {
       .def("put", &XgmiArena::put, py::arg("ch"), py::arg("parts"), py::arg("bpp"),
            py::arg("stream"))
       .def("wait", &XgmiArena::wait, py::arg("ch"), py::arg("fixed"), py::arg("timeout_s"),
-           py::arg("stream"));
+           py::arg("stream"), py::arg("metrics") = std::vector<uintptr_t>{},
+           py::arg("bpk") = 0.0);
   m.def("xgmi_flag_bytes", &ss::xgmi_flag_bytes);
-  m.def("xmetrics", &ss::launch_xmetrics, py::arg("sent"), py::arg("recv"), py::arg("n"),
-        py::arg("bytes_per_key"), py::arg("acc"), py::arg("st"));
 }

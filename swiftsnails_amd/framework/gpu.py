@@ -119,7 +119,8 @@ class PSContext:
             else:
                 tr = LoopbackTransport()
         self.transport = tr
-        self.table = (HbmTable(dim, capacity, optimizer=optimizer, init=init, device=self.device)
+        self.table = (HbmTable(dim, capacity, optimizer=optimizer, init=init, device=self.device,
+                               row_dtype=cfg.get("row_dtype", "fp32"))
                       if self.is_server else None)
         ek = dict(max_keys=max_keys, dim=dim, frag_num=int(cfg.get("frag_num", 0) or 0),
                   server_ranks=self.servers, device=self.device)

@@ -32,8 +32,12 @@ def fm_table_args(k: int, optimizer: Optional[Optimizer] = None):
     return opt, init
 
 
-def plan_fm_table(n_keys: int, k: int = 8, shards: int = 8, load: float = 0.7) -> dict:
-    p = HbmTable.plan(n_keys // shards, 1 + k, Optimizer("adagrad"), load)
+def plan_fm_table(n_keys: int, k: int = 8, shards: int = 8, load: float = 0.7,
+                  row_dtype: str = "fp32") -> dict:
+    """Per-shard table plan of the config-5 FM table; ``row_dtype="bf16"``
+    (compact rows) halves the row bytes: 10B keys at K = 16 are ~1.94 TB at
+    fp32 (past 8 x 288 GB with the slot keys) and fit as bf16 rows."""
+    p = HbmTable.plan(n_keys // shards, 1 + k, Optimizer("adagrad"), load, row_dtype)
     p["GB_per_shard"] = round(p["bytes"] / 1e9, 1)
     return p
 
@@ -96,6 +100,42 @@ class FMWorker(PipelinedWorker):
 
     def samples_per_step(self) -> int:
         return self.data.batch_size if self.active else 0
+
+    EVAL_STEP = 1 << 28  # held-out sample range of the synthetic generator
+
+    def evaluate(self, batches: int = 1) -> dict:
+        """Held-out metrics on fresh synthetic batches: AUC / log-loss of the
+        learned FM logits and the AUC of the planted ground-truth logits the
+        labels were drawn from (the Bayes-optimal reference).  Reads the table
+        without inserting (unseen keys contribute zero).  World 1."""
+        if self.world != 1 or self.engine.table is None:
+            raise NotImplementedError("evaluate() reads the local shard: world 1 only")
+        from ..models.ctr_data import truth_weight
+        from ..utils.metrics import auc, logloss
+
+        d, dev, D = self.data, self.engine.device, self.engine.dim
+        B, F = d.batch_size, d.num_fields
+        keys = torch.empty(B * F, dtype=torch.int64, device=dev)
+        labels = torch.empty(B, dtype=torch.float32, device=dev)
+        zs, zt, ys = [], [], []
+        torch.cuda.synchronize()
+        for b in range(batches):
+            d.generate(self.EVAL_STEP + b, 0, 1, keys, labels)
+            rows, _ = self.engine.table.pull(keys, insert=False)
+            zs.append(fm_logits(rows.view(B, F, D)).cpu().numpy())
+            k = keys.cpu().numpy().view(np.uint64)
+            zt.append(truth_weight(k, d.truth_scale).reshape(B, F).sum(1) + d.truth_bias)
+            ys.append(labels.cpu().numpy())
+        z, t, y = np.concatenate(zs), np.concatenate(zt), np.concatenate(ys)
+        return {"auc": auc(z, y), "logloss": logloss(z, y), "auc_truth": auc(t, y),
+                "logloss_truth": logloss(t, y), "samples": int(y.size)}
+
+
+def fm_logits(rows: torch.Tensor) -> torch.Tensor:
+    """FM logits of [B, F, 1 + K] rows: sum_i w_i + 1/2 sum_f [(sum_i v_if)^2
+    - sum_i v_if^2]."""
+    w, v = rows[..., 0], rows[..., 1:]
+    return w.sum(1) + 0.5 * (v.sum(1) ** 2 - (v * v).sum(1)).sum(-1)
 
 
 def fm_reference(rows: np.ndarray, labels: np.ndarray):

@@ -44,8 +44,10 @@ def _align(x: int, a: int) -> int:
     return (x + a - 1) // a * a
 
 
-def slot_layout(width: int, layout: Optional[str] = None) -> tuple[int, int, int]:
-    """(stride_bytes, key_offset_bytes, row_offset_bytes) of one slot.
+def slot_layout(width: int, layout: Optional[str] = None,
+                elem: int = 4) -> tuple[int, int, int]:
+    """(stride_bytes, key_offset_bytes, row_offset_bytes) of one slot;
+    ``elem``: bytes per row element (4 fp32, 2 compact bf16 rows).
 
     ``rowfirst``: [row | key] (scalar rows: LR's 16-byte [w, h, key] slot).
     ``keyfirst``: [key | row], so the key and the parameters a pull reads sit
@@ -54,14 +56,14 @@ def slot_layout(width: int, layout: Optional[str] = None) -> tuple[int, int, int
     layout = layout or os.environ.get("SS_TABLE_LAYOUT", "") or (
         "rowfirst" if width <= 2 else "keyfirst")
     if layout == "rowfirst":
-        key_off = _align(4 * width, 8)
+        key_off = _align(elem * width, 8)
         stride = key_off + 8
         if width >= 4:
             stride = _align(stride, 16)
         return stride, key_off, 0
     if layout not in ("keyfirst", "keyfirst_line"):
         raise ValueError(f"slot layout {layout!r}")
-    stride = _align(8 + 4 * width, 16 if width >= 2 else 8)
+    stride = _align(8 + elem * width, 16 if width >= 2 else 8)
     if layout == "keyfirst_line":
         stride = _align(stride, 64)
     return stride, 0, 8
@@ -83,6 +85,12 @@ def _stream_ptr(stream) -> int:
     return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
 
 
+def _i16(u: int) -> int:
+    """A 16-bit pattern as the signed value torch.int16 holds."""
+    u &= 0xFFFF
+    return u - 0x10000 if u >= 0x8000 else u
+
+
 class TableFullError(RuntimeError):
     pass
 
@@ -93,7 +101,7 @@ class HbmTable:
 
     def __init__(self, dim: int, capacity: int, optimizer: Optional[Optimizer] = None,
                  init: Optional[InitConfig] = None, device=None, lane_group: Optional[int] = None,
-                 max_load: float = 0.85):
+                 max_load: float = 0.85, row_dtype: str = "fp32"):
         if dim < 1:
             raise ValueError("dim must be >= 1")
         if capacity < 1:
@@ -104,7 +112,15 @@ class HbmTable:
         self.opt = optimizer or Optimizer()
         self.init_cfg = init or InitConfig()
         self.width = self.dim + self.opt.state_width(self.dim)
-        self.stride, self.key_off, self.row_off = slot_layout(self.width)
+        # "bf16": compact rows (parameters and optimizer state in bf16, fp32
+        # math, stochastically rounded updates): half the row bytes, for
+        # tables that do not fit at fp32 (the 10B-key FM table)
+        if row_dtype not in ("fp32", "bf16"):
+            raise ValueError(f"row_dtype must be fp32 or bf16, not {row_dtype!r}")
+        self.row_dtype = row_dtype
+        self.bf16 = row_dtype == "bf16"
+        self.elem = 2 if self.bf16 else 4
+        self.stride, self.key_off, self.row_off = slot_layout(self.width, elem=self.elem)
         self.G = lane_group or int(os.environ.get("SS_TABLE_G", "0")) or \
             default_lane_group(self.width)
         self.max_load = max_load
@@ -134,9 +150,7 @@ class HbmTable:
             slots = self.storage.view(cap, self.stride)
             slots[:, self.key_off:self.key_off + 8].fill_(255)  # every key word = EMPTY
             if self.width > self.dim and float(self.init_cfg.state_init) != 0.0:
-                rows = self.storage.view(torch.float32).view(cap, self.stride // 4)
-                r0 = self.row_off // 4
-                rows[:, r0 + self.dim:r0 + self.width].fill_(float(self.init_cfg.state_init))
+                self.rows_view()[:, self.dim:].fill_(float(self.init_cfg.state_init))
         else:
             self.storage.fill_(255)  # every key word = EMPTY (rows: the 0xFF sentinel)
         # sharded counter: 256 shards x 128 B (see ss_device.h ctr_add)
@@ -149,14 +163,15 @@ class HbmTable:
         # (the prefilled fast path writes nothing on insert)
         self.dt = hip().DevTable(self.storage.data_ptr(), self.capacity, self.stride,
                                  self.key_off, self.dim, self.width,
-                                 int(self.prefilled and self.init_fn is None), self.row_off)
+                                 int(self.prefilled and self.init_fn is None), self.row_off,
+                                 int(self.bf16))
 
     @staticmethod
     def plan(n_keys: int, dim: int, optimizer: Optional[Optimizer] = None,
-             load: float = 0.7) -> dict:
+             load: float = 0.7, row_dtype: str = "fp32") -> dict:
         opt = optimizer or Optimizer()
         width = dim + opt.state_width(dim)
-        stride, _, _ = slot_layout(width)
+        stride, _, _ = slot_layout(width, elem=2 if row_dtype == "bf16" else 4)
         cap = int(math.ceil(n_keys / load))
         return {"capacity": cap, "stride": stride, "bytes": cap * stride, "width": width}
 
@@ -218,6 +233,7 @@ class HbmTable:
     def snapshot_ok(self) -> bool:
         """Rows are (w, h) scalar AdaGrad pairs the pull can snapshot."""
         return (self.G == 1 and self.dim == 1 and self.width == 2 and self.push_fn is None and
+                not self.bf16 and
                 not self.custom_pull and
                 self.opt.kind == "adagrad" and self.stride % 8 == 0 and self.row_off % 8 == 0)
 
@@ -244,8 +260,9 @@ class HbmTable:
             # pattern instead (table.hip fresh_or)
             empty = self.keys_view() == EMPTY_I64
             rv = self.rows_view()
-            rv[empty] = torch.tensor(-1, dtype=torch.int32, device=self.device).view(
-                torch.float32)
+            fill = torch.tensor(-1, dtype=torch.int16 if self.bf16 else torch.int32,
+                                device=self.device).view(rv.dtype)
+            rv[empty] = fill
         self._make_dt()
         self.version += 1
 
@@ -279,12 +296,15 @@ class HbmTable:
         ok = s >= 0
         s = s[ok]
         rv = self.rows_view()
-        rows = rv[s]
+        rows = rv[s].to(torch.float32)
         keys = self.keys_view()[s]
         if self.init_fn is not None:
             from .optim import INIT_MARKER_BITS
 
-            new = rows[:, 0].view(torch.int32) == INIT_MARKER_BITS
+            if self.bf16:  # a compact row keeps the marker's top 16 bits
+                new = rows[:, 0].view(torch.int16) == _i16(INIT_MARKER_BITS >> 16)
+            else:
+                new = rows[:, 0].view(torch.int32) == INIT_MARKER_BITS
             if bool(new.any()):
                 r = torch.as_tensor(self.init_fn(keys[new]), dtype=torch.float32,
                                     device=self.device)
@@ -319,8 +339,9 @@ class HbmTable:
 
     def rows_view(self) -> torch.Tensor:
         """[capacity, width] float32 view of every slot's row (strided)."""
-        rows = self.storage.view(torch.float32).view(self.capacity, self.stride // 4)
-        r0 = self.row_off // 4
+        dt = torch.bfloat16 if self.bf16 else torch.float32
+        rows = self.storage.view(dt).view(self.capacity, self.stride // self.elem)
+        r0 = self.row_off // self.elem
         return rows[:, r0:r0 + self.width]
 
     def apply_custom(self, slots: torch.Tensor, grads: torch.Tensor, stream=None) -> None:
@@ -339,7 +360,7 @@ class HbmTable:
             if s.numel() == 0:
                 return
             rv = self.rows_view()
-            new = self.push_fn(rv[s].clone(), g.to(torch.float32))
+            new = self.push_fn(rv[s].to(torch.float32), g.to(torch.float32))
             new = torch.as_tensor(new, dtype=torch.float32, device=self.device)
             if new.shape != (s.numel(), self.width):
                 raise ValueError(f"push method returned {tuple(new.shape)}, "

@@ -433,8 +433,9 @@ class PSEngine:
         h.srv_fill(self.Ps, S.bstart.data_ptr(), S.ubase.data_ptr(), S.unum.data_ptr(),
                    S.pj.data_ptr(), S.luid.data_ptr(), self.svals.data_ptr(),
                    self.rvals.data_ptr(), self.dim, st)
-        sacc = self.metrics.device_block(("server_unique",), self.device)
-        sacc.add_(S.ucount)  # (one tiny kernel, no sync)
+        if not self.xg:  # (xgmi: counted by the vals wait, no launch of its own)
+            sacc = self.metrics.device_block(("server_unique",), self.device)
+            sacc.add_(S.ucount)  # (one tiny kernel, no sync)
 
     def _server_pull_cpu(self, rcounts: np.ndarray):
         """Host server: distinct keys of all sources, looked up once."""
@@ -458,10 +459,13 @@ class PSEngine:
         self._server_pull_gpu(slot, stream)
         rc = xg.counts("keys", 0, slot)
         xg.put("vals", slot, [(self.rvals, self.displs, rc, None, self.dim)], stream=stream)
-        xg.wait("vals", slot, stream)
         acc = self.metrics.device_block(("unique_sent", "unique_recv", "a2a_bytes"), self.device)
-        _hip().xmetrics(dd.ucount.data_ptr(), rc.data_ptr(), self.world, 8.0 + 8.0 * self.dim,
-                        acc.data_ptr(), stream.cuda_stream)
+        sx = None
+        if self.table is not None:
+            sx = self.metrics.device_block(("server_unique",), self.device)
+        xg.wait("vals", slot, stream,
+                metrics=(dd.ucount, rc, acc, self.srv[slot].ucount if sx is not None else None, sx),
+                bytes_per_key=8.0 + 8.0 * self.dim)
         self.metrics.add(occurrences=dd.n)
         return Round(dd, self.uvals[slot], slot)
 
@@ -591,7 +595,7 @@ class PSEngine:
         args = (self.Ps, S.bstart.data_ptr(), S.ubase.data_ptr(), S.unum.data_ptr(),
                 S.pj.data_ptr(), S.luid.data_ptr(), self.rgrads[slot].data_ptr())
         fused = (self.dim == 1 and tab.push_fn is None and tab.opt.kind == "adagrad" and
-                 tab.width == 2 and tab.G == 1)
+                 tab.width == 2 and tab.G == 1 and not getattr(tab, "bf16", False))
         if fused:
             h.srv_merge(*args, 0, 1, tab.dt, S.slots.data_ptr(),
                         S.snap.data_ptr() if S.snap_valid else 0, tab.opt.native(), st)

@@ -182,16 +182,21 @@ class XgmiTransport(Transport):
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         self.arena.put(self._ch[ch], spec, self.bpp, st.cuda_stream)
 
-    def wait(self, ch: str, slot: int, stream=None, fixed_parts: Sequence = ()) -> None:
+    def wait(self, ch: str, slot: int, stream=None, fixed_parts: Sequence = (),
+             metrics: Sequence = (), bytes_per_key: float = 0.0) -> None:
         """Block ``stream`` until every source's put of this channel's next
         round has arrived.  ``fixed_parts``: (part, bytes) of fixed-size
-        parts read as zeros if a source never arrives."""
+        parts read as zeros if a source never arrives.  ``metrics``: (sent
+        [world] i64, recv [world] i64, acc [3] f64, xval [1] i64, xacc [1]
+        f64) tensors or None, added on the device after the wait:
+        acc += (sum sent, sum recv, bytes_per_key * both), xacc += xval."""
         fx = []
         for p, nb in fixed_parts:
             _, data, seg = self._layout[(ch, p, slot)]
             fx.append([data, seg, int(nb)])
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
-        self.arena.wait(self._ch[ch], fx, self.timeout_s, st.cuda_stream)
+        mp = [t.data_ptr() if t is not None else 0 for t in metrics]
+        self.arena.wait(self._ch[ch], fx, self.timeout_s, st.cuda_stream, mp, float(bytes_per_key))
 
     def check(self) -> None:
         e = int(self._err[0].item())
