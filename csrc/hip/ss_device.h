@@ -97,9 +97,12 @@ __device__ __forceinline__ void row_st(const DevTable& t, uint64_t s, uint32_t j
   uint32_t u = __float_as_uint(v);
   if ((u & 0x7F800000u) != 0x7F800000u) {
     if (sr) {
-      // data-dependent dither (slot, coordinate, value bits): no state, the
-      // same under hipGraph replay
-      uint32_t h = (uint32_t)s * 0x9E3779B1u ^ (j * 0x85EBCA77u) ^ u;
+      // dither from (slot, coordinate, value bits, the wall clock): the
+      // clock makes a row that returns to the same value after an update
+      // that rounded away draw a fresh dither next time (value bits alone
+      // repeat the same rounding forever); no state, works under graph replay
+      uint32_t h = (uint32_t)s * 0x9E3779B1u ^ (j * 0x85EBCA77u) ^ u ^
+                   ((uint32_t)wall_clock64() * 0xC2B2AE35u);
       h ^= h >> 15;
       h *= 0x2C1B3C6Du;
       h ^= h >> 12;

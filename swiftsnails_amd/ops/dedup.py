@@ -130,8 +130,7 @@ class Deduper:
             self.luid = torch.empty(m, dtype=torch.int32, device=d)    # bucket-local ids
             self.bkeys = torch.empty(m, dtype=torch.int64, device=d)   # staged unique keys
             # (key, sample) records in bucket order, 16 B each (scatter -> dedup)
-            self.rec = (torch.empty((m, 4), dtype=torch.int32, device=d)
-                        if os.environ.get("SS_BD_REC", "1") != "0" else None)
+            self.rec = torch.empty((m, 4), dtype=torch.int32, device=d)
             self._last_n = 0
             # SS_BD_DEBUG=1: per-bucket phase timestamps of the dedup kernel
             self.dbg = (torch.zeros(8 * self.h.bd_buckets(m, self.nranks, self.ndest),
@@ -161,7 +160,7 @@ class Deduper:
                             self.inv.data_ptr() if self.materialize_inv else 0,
                             int(self.need_ukeys or bool(ug)), st,
                             self.dbg.data_ptr() if self.dbg is not None else 0,
-                            self.rec.data_ptr() if self.rec is not None else 0,
+                            self.rec.data_ptr(),
                             self.usingle.data_ptr() if self.usingle is not None else 0,
                             self.ndest, self.lay_n or 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,

