@@ -350,13 +350,14 @@ PYBIND11_MODULE(_ss_hip, m) {
                          P<const float>(grads), 1, P<float>(merged), t ? &*t : nullptr,
                          P<const long long>(slots), P<const float>(snap), op ? &*op : nullptr,
                          S(st));
-    else if (slots)
-      throw_error("srv_merge: a fused update needs scalar rows");
+    else if (snap)
+      throw_error("srv_merge: snapshot updates need scalar rows");
     else
       launch_srv_merge_rows(Pn, P<const uint32_t>(bstart), P<const uint32_t>(ubase),
                             P<const uint32_t>(unum), P<const uint32_t>(pj),
                             P<const uint32_t>(luid), P<const float>(grads), P<float>(merged), D,
-                            S(st));
+                            S(st), t ? &*t : nullptr, P<const long long>(slots),
+                            op ? &*op : nullptr);
   }, py::arg("P"), py::arg("bstart"), py::arg("ubase"), py::arg("unum"), py::arg("pj"),
      py::arg("luid"), py::arg("grads"), py::arg("merged"), py::arg("D"),
      py::arg("t") = std::nullopt, py::arg("slots") = 0, py::arg("snap") = 0,

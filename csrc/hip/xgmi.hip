@@ -41,6 +41,7 @@
 // after the engine's own event chain has consumed it (parallel/engine.py).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -250,7 +251,15 @@ class XgmiArena {
     P.me = rank_;
     P.ch = ch;
     P.nparts = (int)parts.size();
-    P.bpp = bpp < 1 ? 1 : bpp;
+    // blocks per peer: sized to the largest segment (~32 KB per block, 8 at
+    // least), capped by `bpp`.  Every block drains and arrives on one
+    // counter, and those device-scope adds serialise (~12 ns each): 1024
+    // blocks for a 1 MB segment cost 12+ us of arrivals alone
+    long long maxseg = 0;
+    for (const auto& v : parts)
+      if (v.size() > 6) maxseg = std::max(maxseg, v[6]);
+    const long long want = std::max(8ll, (maxseg + 32767) / 32768);
+    P.bpp = (int)std::max(1ll, std::min((long long)(bpp < 1 ? 1 : bpp), want));
     for (size_t q = 0; q < parts.size(); ++q) {
       const auto& v = parts[q];
       if ((int)v.size() != 7 + nranks_) throw_error("xgmi: malformed part");

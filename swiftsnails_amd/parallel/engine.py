@@ -599,6 +599,9 @@ class PSEngine:
         if fused:
             h.srv_merge(*args, 0, 1, tab.dt, S.slots.data_ptr(),
                         S.snap.data_ptr() if S.snap_valid else 0, tab.opt.native(), st)
+        elif self.dim > 1 and tab.push_fn is None:
+            # rows: the merged gradient row goes straight into the update
+            h.srv_merge(*args, 0, self.dim, tab.dt, S.slots.data_ptr(), 0, tab.opt.native(), st)
         else:
             h.srv_merge(*args, self.sgrad.data_ptr(), self.dim, st=st)
             if tab.push_fn is not None:

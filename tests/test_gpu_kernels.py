@@ -751,13 +751,14 @@ def test_stream_helpers_match_torch(dev):
     assert float(x.sum().item()) == 2000.0
 
 
-@pytest.mark.parametrize("dim", [1, 3])
-def test_server_merge_matches_reference(dev, dim):
+@pytest.mark.parametrize("dim,fused", [(1, True), (3, False), (3, True), (64, True)])
+def test_server_merge_matches_reference(dev, dim, fused):
     """server.hip on the keys three sources route to one server (real
     bucketed dedups with the common N>1 layout, overlapping key sets): one
     entry per distinct key, response rows per received position, and the
-    merged gradient of every distinct key — fused into the AdaGrad update for
-    scalar rows (read-modify-write, no snapshot), a merged row otherwise."""
+    merged gradient of every distinct key — fused into the AdaGrad update
+    (scalar rows: read-modify-write, no snapshot; wider rows: lane per
+    coordinate), or a merged row then the apply kernel."""
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.ops.dedup import Deduper
     from swiftsnails_amd.ops.optim import InitConfig, Optimizer
@@ -824,9 +825,9 @@ def test_server_merge_matches_reference(dev, dim):
                                   np.stack([before[int(k)][:dim] for k in rk]))
     g = torch.randn((rows, dim), device=dev)
     gn = g.cpu().numpy()
-    if dim == 1:
+    if fused:
         h.srv_merge(P, bstart.data_ptr(), ubase.data_ptr(), unum.data_ptr(), pj.data_ptr(),
-                    luid.data_ptr(), g.data_ptr(), 0, 1, t.dt, sslots.data_ptr(), 0,
+                    luid.data_ptr(), g.data_ptr(), 0, dim, t.dt, sslots.data_ptr(), 0,
                     t.opt.native(), st)
     else:
         merged = torch.empty((rows, dim), device=dev)
