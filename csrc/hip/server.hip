@@ -255,7 +255,7 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
                                                         const uint32_t* __restrict__ luid,
                                                         const float* __restrict__ grads,
                                                         float* __restrict__ merged, int D,
-                                                        DevTable t,
+                                                        DevTable tab,
                                                         const long long* __restrict__ slots,
                                                         OptParams op) {
   __shared__ unsigned int off[kSrvTS + 1];
@@ -310,13 +310,13 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
       if (!slots) {
         merged[((long long)base + l) * D + c] = acc;
       } else if (slot >= 0) {
-        float wv = row_ld(t, slot, c);
-        float s1 = ns > 0 ? row_ld(t, slot, D + c) : 0.f;
-        float s2 = ns > 1 ? row_ld(t, slot, 2 * D + c) : 0.f;
+        float wv = row_ld(tab, slot, c);
+        float s1 = ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
+        float s2 = ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
         opt_update(op, wv, s1, s2, acc);
-        row_st(t, slot, c, wv, true);
-        if (ns > 0) row_st(t, slot, D + c, s1, true);
-        if (ns > 1) row_st(t, slot, 2 * D + c, s2, true);
+        row_st(tab, slot, c, wv, true);
+        if (ns > 0) row_st(tab, slot, D + c, s1, true);
+        if (ns > 1) row_st(tab, slot, 2 * D + c, s2, true);
       }
     }
   }

@@ -312,7 +312,7 @@ class HbmTable:
                 if r.shape != (int(new.sum()), self.width):
                     raise ValueError(f"init method returned {tuple(r.shape)}, expected "
                                      f"{(int(new.sum()), self.width)}")
-                rv[s[new]] = r
+                rv[s[new]] = r.to(rv.dtype)
                 rows[new] = r
         vals = rows[:, :self.dim]
         if self.pull_fn is not None:
@@ -366,7 +366,7 @@ class HbmTable:
             if new.shape != (s.numel(), self.width):
                 raise ValueError(f"push method returned {tuple(new.shape)}, "
                                  f"expected {(s.numel(), self.width)}")
-            rv[s] = new
+            rv[s] = new.to(rv.dtype)
             self.version += 1
 
     def pull_buckets(self, view, out: torch.Tensor, slots: torch.Tensor, stream=None,
