@@ -55,9 +55,13 @@ static BdIndex make_bdindex(const std::vector<uintptr_t>& v) {
 }
 
 void bind_xgmi(py::module_& m);  // xgmi.hip
+namespace ss {
+void bind_round_engine(py::module_& m);  // round_engine.cpp
+}
 
 PYBIND11_MODULE(_ss_hip, m) {
   bind_xgmi(m);
+  ss::bind_round_engine(m);
   m.doc() = "SwiftSnails-AMD gfx950 kernels + RCCL communicator";
 
   py::class_<DevTable>(m, "DevTable", py::module_local())

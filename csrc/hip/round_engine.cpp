@@ -1,0 +1,346 @@
+// round_engine.cpp — the per-round launch sequences of the GPU round engine.
+//
+// parallel/engine.py decides WHAT a round does (which path, which hooks, the
+// snapshot bookkeeping); this class issues HOW — the stream waits, kernels,
+// xGMI puts / waits and event records of one stage — as ONE call per stage
+// (route end, pull, push) instead of ~4-10 Python-level calls each.  It owns
+// the ring's HIP events (route done, pull done, slot free) and their capture
+// tags: an event recorded in one hipGraph capture is only waited on inside
+// that capture (an earlier replay has completed anyway) — the same rule the
+// Python engine applied to torch events.
+//
+// Paths: the one-GPU path (colocated worker + shard, no exchange) and the
+// N>1 xGMI mailbox path (device-side counts; server merge of server.hip).
+// Host-count transports (RCCL, gloo, CPU) stay in parallel/engine_host.py.
+// Reference parity: the round replaces Transfer::send / the pull and push
+// access agents (/root/reference/src/core/transfer/transfer.h:75-150,
+// src/core/parameter/global_pull_access.h:40-120, global_push_access.h:36-149).
+#include <hip/hip_runtime.h>
+
+#include <array>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "ss_launch.h"
+#include "xgmi.h"
+
+namespace py = pybind11;
+
+namespace ss {
+
+namespace {
+template <typename T>
+T* Pt(uintptr_t p) { return reinterpret_cast<T*>(p); }
+hipStream_t St(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+}  // namespace
+
+// device buffers of one ring slot's server merge (engine._ServerSlot)
+struct SrvSlot {
+  uint32_t *cnt = nullptr, *bstart = nullptr, *ubase = nullptr, *unum = nullptr;
+  uint32_t *pj = nullptr, *luid = nullptr;
+  uint64_t* bkeys = nullptr;
+  long long* slots = nullptr;
+  float* snap = nullptr;
+  unsigned long long* ucount = nullptr;
+};
+
+// arena offsets of one (channel, part, slot) region
+struct XReg {
+  long long hdr = 0, data = 0, seg = 0;
+};
+
+class RoundEngine {
+ public:
+  enum Kind { kRoute = 0, kPull = 1, kFree = 2 };
+
+  RoundEngine(int depth, int device) : depth_(depth), device_(device) {
+    if (depth < 1 || depth > 16) throw std::invalid_argument("RoundEngine: depth 1..16");
+    check_hip(hipSetDevice(device), "hipSetDevice");
+    for (auto& k : ev_)
+      for (int s = 0; s < depth; ++s) {
+        hipEvent_t e;
+        check_hip(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+        k.push_back(e);
+      }
+    for (auto& t : tag_) t.assign(depth, -1);
+    srv_.resize(depth);
+    keys_.resize(depth);
+    vals_.resize(depth);
+    grads_.resize(depth);
+  }
+  ~RoundEngine() {
+    hipSetDevice(device_);
+    for (auto& k : ev_)
+      for (auto e : k) hipEventDestroy(e);
+  }
+  RoundEngine(const RoundEngine&) = delete;
+  RoundEngine& operator=(const RoundEngine&) = delete;
+
+  // -------------------------------------------------------------- events
+  // tag: the hipGraph capture the call runs in (0 = eager)
+  void record(int kind, int slot, uintptr_t stream, int tag) {
+    check_slot(slot);
+    check_hip(hipEventRecord(ev_.at(kind)[slot], St(stream)), "hipEventRecord");
+    tag_.at(kind)[slot] = tag;
+  }
+  void wait(int kind, int slot, uintptr_t stream, int tag) {
+    check_slot(slot);
+    if (tag_.at(kind)[slot] == tag)
+      check_hip(hipStreamWaitEvent(St(stream), ev_.at(kind)[slot], 0), "hipStreamWaitEvent");
+  }
+  bool recorded(int kind, int slot) const { return tag_.at(kind).at(slot) >= 0; }
+  void forget() {  // a new capture / a reset pipeline: nothing is waitable
+    for (auto& t : tag_) t.assign(depth_, -1);
+  }
+
+  // ---------------------------------------------------------- N>1 set-up
+  // regions: keys [depth][3 parts], vals [depth], grads [depth], each
+  // (hdr, data, seg); chans: the arena channel ids of keys / vals / grads
+  void set_xgmi(XgmiArena* arena, std::vector<int> chans, std::vector<std::vector<long long>> keys,
+                std::vector<std::vector<long long>> vals, std::vector<std::vector<long long>> grads,
+                int nranks, int rank, int Pd, int sub, long long cap, int dim, int bpp,
+                double timeout_s) {
+    if (!arena || chans.size() != 3) throw std::invalid_argument("set_xgmi: arena + 3 channels");
+    if ((int)keys.size() != depth_ || (int)vals.size() != depth_ || (int)grads.size() != depth_)
+      throw std::invalid_argument("set_xgmi: one region set per ring slot");
+    xg_ = arena;
+    ch_ = {chans[0], chans[1], chans[2]};
+    for (int s = 0; s < depth_; ++s) {
+      if (keys[s].size() != 9 || vals[s].size() != 3 || grads[s].size() != 3)
+        throw std::invalid_argument("set_xgmi: (hdr, data, seg) per part");
+      for (int p = 0; p < 3; ++p) keys_[s][p] = {keys[s][3 * p], keys[s][3 * p + 1], keys[s][3 * p + 2]};
+      vals_[s] = {vals[s][0], vals[s][1], vals[s][2]};
+      grads_[s] = {grads[s][0], grads[s][1], grads[s][2]};
+    }
+    nranks_ = nranks;
+    rank_ = rank;
+    Pd_ = Pd;
+    sub_ = sub;
+    cap_ = cap;
+    dim_ = dim;
+    bpp_ = bpp;
+    timeout_ = timeout_s;
+  }
+  void set_server_slot(int slot, std::vector<uintptr_t> p) {
+    check_slot(slot);
+    if (p.size() != 10) throw std::invalid_argument("set_server_slot: 10 pointers");
+    SrvSlot& S = srv_[slot];
+    S.cnt = Pt<uint32_t>(p[0]);
+    S.bstart = Pt<uint32_t>(p[1]);
+    S.ubase = Pt<uint32_t>(p[2]);
+    S.unum = Pt<uint32_t>(p[3]);
+    S.pj = Pt<uint32_t>(p[4]);
+    S.luid = Pt<uint32_t>(p[5]);
+    S.bkeys = Pt<uint64_t>(p[6]);
+    S.slots = Pt<long long>(p[7]);
+    S.snap = Pt<float>(p[8]);
+    S.ucount = Pt<unsigned long long>(p[9]);
+  }
+
+  // ------------------------------------------------------------ stage 1
+  // after the dedup on the route stream: N>1 — the keys + every destination's
+  // per-bucket runs into the peers' mailboxes; then the route event
+  void route_end(int slot, int tag, uintptr_t route, uintptr_t ukeys, uintptr_t ucount,
+                 uintptr_t runs_base, uintptr_t runs_num) {
+    check_slot(slot);
+    if (xg_) {
+      std::vector<std::vector<long long>> parts;
+      parts.push_back(part(ukeys, ucount, 0, 8, keys_[slot][0], cap_));
+      parts.push_back(part(runs_base, 0, Pd_, 4, keys_[slot][1], Pd_));
+      parts.push_back(part(runs_num, 0, Pd_, 4, keys_[slot][2], Pd_));
+      xg_->put(ch_[0], parts, bpp_, route);
+    }
+    record(kRoute, slot, route, tag);
+  }
+
+  // ------------------------------------------------------------ stage 2
+  // The pull's stream waits for the round's route (unless it IS the route
+  // stream) and, pulled ahead, for the push `prev` slots back (staleness
+  // bound; prev < 0: none).  One GPU: bucket pull of the dedup's unique keys
+  // (+ (w, h) snapshot).  Records the pull event when `ahead`.
+  void pull_fast(int slot, int tag, uintptr_t stream, bool wait_route, int prev, bool ahead,
+                 const DevTable& t, const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
+                 std::vector<uintptr_t> view, int P, uintptr_t uvals, uintptr_t slots,
+                 uintptr_t snap) {
+    pull_waits(slot, tag, stream, wait_route, prev);
+    if (view.size() != 4) throw std::invalid_argument("pull_fast: (bkeys, bstart, unum, ubase)");
+    launch_pull_unique_bk(t, Pt<const uint64_t>(view[0]), Pt<const uint32_t>(view[1]),
+                          Pt<const uint32_t>(view[2]), Pt<const uint32_t>(view[3]), P,
+                          Pt<long long>(slots), Pt<float>(uvals), ip,
+                          Pt<unsigned long long>(size_ctr), Pt<int>(err), G, St(stream),
+                          Pt<float>(snap));
+    if (ahead) record(kPull, slot, stream, tag);
+  }
+
+  // N>1 over the mailboxes: keys in (every source's put of this round),
+  // server merge (distinct keys across sources) + lookup, response rows per
+  // received position straight into the vals put, rows back; the exchange
+  // counters ride on the vals wait.  `table` false: a rank without a shard.
+  void pull_xgmi(int slot, int tag, uintptr_t stream, bool wait_route, int prev, bool ahead,
+                 bool table, const DevTable& t, const InitParams& ip, uintptr_t size_ctr,
+                 uintptr_t err, int G, uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum,
+                 uintptr_t srv_err, uintptr_t svals, uintptr_t rvals, bool snap, uintptr_t sent,
+                 std::vector<uintptr_t> metrics, bool custom_pull) {
+    check_xgmi();
+    pull_waits(slot, tag, stream, wait_route, prev);
+    // missing sources' fixed-size run tables read as empty
+    const long long nb = 4ll * Pd_;
+    xg_->wait(ch_[0], {{keys_[slot][1].data, keys_[slot][1].seg, nb},
+                        {keys_[slot][2].data, keys_[slot][2].seg, nb}},
+              timeout_, stream, {}, 0.0);
+    if (table) {
+      SrvSlot& S = srv_[slot];
+      launch_srv_dedup(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
+                       Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt,
+                       S.bstart, S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount,
+                       Pt<uint32_t>(srv_err), St(stream));
+      launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
+                            Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
+                            G, St(stream), snap ? S.snap : nullptr);
+      if (custom_pull) return;  // the caller finishes the pull (tensor-code hooks)
+      fill_and_return(slot, stream, svals, rvals, sent, metrics);
+    } else {
+      fill_and_return(slot, stream, 0, rvals, sent, metrics);
+    }
+    if (ahead) record(kPull, slot, stream, tag);
+  }
+  // the second half of pull_xgmi after a tensor-code pull hook ran
+  void pull_xgmi_finish(int slot, int tag, uintptr_t stream, bool ahead, uintptr_t svals,
+                        uintptr_t rvals, uintptr_t sent, std::vector<uintptr_t> metrics) {
+    check_xgmi();
+    fill_and_return(slot, stream, svals, rvals, sent, metrics);
+    if (ahead) record(kPull, slot, stream, tag);
+  }
+
+  // ------------------------------------------------------------ stage 3
+  // One GPU: the optimizer update at the pulled slots (compact unique ids,
+  // count on the device; `snap`: blind store from the pull's snapshot), then
+  // the slot-free event on the main stream.  `apply` false: the model's
+  // merge kernel already updated the rows (fuse_apply).
+  void push_fast(int slot, int tag, uintptr_t stream, bool apply, const DevTable& t,
+                 const OptParams& op, int G, uintptr_t slots, uintptr_t grads, uintptr_t ucount,
+                 long long max_n, uintptr_t snap) {
+    check_slot(slot);
+    if (apply) {
+      SegList sl{};
+      sl.nseg = 1;
+      sl.dev_count = Pt<const long long>(ucount);
+      launch_apply(t, Pt<const long long>(slots), Pt<const float>(grads), sl, max_n, op, G,
+                   St(stream), Pt<const float>(snap));
+    }
+    record(kFree, slot, stream, tag);
+  }
+
+  // N>1: gradient rows into the servers' mailboxes, wait for every source's,
+  // server merge + ONE update per distinct key (fused: scalar AdaGrad rows
+  // from the snapshot or the row; wider rows lane per coordinate), then the
+  // slot-free event.  `update` false: merged rows only (`merged`; the caller
+  // applies a tensor-code rule).
+  void push_xgmi(int slot, int tag, uintptr_t stream, uintptr_t grads, uintptr_t ucount,
+                 bool table, bool update, const DevTable& t, const OptParams& op, uintptr_t rgrads,
+                 bool scalar_fused, bool snap, uintptr_t merged, bool release) {
+    check_xgmi();
+    std::vector<std::vector<long long>> parts;
+    parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_));
+    xg_->put(ch_[2], parts, bpp_, stream);
+    xg_->wait(ch_[2], {}, timeout_, stream, {}, 0.0);
+    if (table) {
+      SrvSlot& S = srv_[slot];
+      const int Ps = Pd_ * sub_;
+      if (update && scalar_fused)
+        launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
+                           1, nullptr, &t, S.slots, snap ? S.snap : nullptr, &op, St(stream));
+      else if (update && dim_ > 1)
+        launch_srv_merge_rows(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid,
+                              Pt<const float>(rgrads), nullptr, dim_, St(stream), &t, S.slots,
+                              &op);
+      else if (dim_ == 1)
+        launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
+                           1, Pt<float>(merged), nullptr, nullptr, nullptr, nullptr, St(stream));
+      else
+        launch_srv_merge_rows(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid,
+                              Pt<const float>(rgrads), Pt<float>(merged), dim_, St(stream));
+    }
+    if (release) record(kFree, slot, stream, tag);
+  }
+
+ private:
+  void check_slot(int slot) const {
+    if (slot < 0 || slot >= depth_) throw std::out_of_range("RoundEngine: ring slot");
+  }
+  void check_xgmi() const {
+    if (!xg_) throw std::logic_error("RoundEngine: set_xgmi first");
+  }
+  void pull_waits(int slot, int tag, uintptr_t stream, bool wait_route, int prev) {
+    check_slot(slot);
+    if (wait_route) wait(kRoute, slot, stream, tag);
+    if (prev >= 0) wait(kFree, prev, stream, tag);
+  }
+  // one part of a put: (src, per-destination displacements, counts, fixed
+  // rows, row bytes) in the arena's layout (XgmiArena::put)
+  std::vector<long long> part(uintptr_t src, uintptr_t cnt, long long fixed, long long rb,
+                              const XReg& r, long long stride_rows) const {
+    std::vector<long long> v = {(long long)src, (long long)cnt, fixed, rb, r.hdr, r.data, r.seg};
+    for (int d = 0; d < nranks_; ++d) v.push_back((long long)d * stride_rows * rb);
+    return v;
+  }
+  void fill_and_return(int slot, uintptr_t stream, uintptr_t svals, uintptr_t rvals,
+                       uintptr_t sent, const std::vector<uintptr_t>& metrics) {
+    // the rows each source gets back = the keys it sent here (keys header)
+    const uintptr_t rc = xg_->base() + keys_[slot][0].hdr;
+    if (svals) {
+      SrvSlot& S = srv_[slot];
+      const int Ps = Pd_ * sub_;
+      if (dim_ == 1)
+        launch_bd_fill_occ_p(Ps, S.bstart, S.ubase, S.unum, S.luid, Pt<const float>(svals),
+                             Pt<float>(rvals), S.pj, St(stream));
+      else
+        launch_srv_fill_rows(Ps, S.bstart, S.ubase, S.pj, S.luid, Pt<const float>(svals),
+                             Pt<float>(rvals), dim_, St(stream));
+    }
+    std::vector<std::vector<long long>> parts;
+    parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_));
+    xg_->put(ch_[1], parts, bpp_, stream);
+    std::vector<uintptr_t> m = metrics;
+    if (!m.empty()) {
+      if (m.size() != 3) throw std::invalid_argument("pull_xgmi: metrics = (acc, xval, xacc)");
+      m = {sent, rc, metrics[0], metrics[1], metrics[2]};
+    }
+    xg_->wait(ch_[1], {}, timeout_, stream, m, 8.0 + 8.0 * dim_);
+  }
+
+  int depth_, device_;
+  std::array<std::vector<hipEvent_t>, 3> ev_;
+  std::array<std::vector<int>, 3> tag_;
+  std::vector<SrvSlot> srv_;
+  XgmiArena* xg_ = nullptr;
+  std::array<int, 3> ch_{};
+  std::vector<std::array<XReg, 3>> keys_;
+  std::vector<XReg> vals_, grads_;
+  int nranks_ = 1, rank_ = 0, Pd_ = 1, sub_ = 1, dim_ = 1, bpp_ = 128;
+  long long cap_ = 0;
+  double timeout_ = 120.0;
+};
+
+void bind_round_engine(py::module_& m) {
+  py::class_<RoundEngine>(m, "RoundEngine", py::module_local())
+      .def(py::init<int, int>(), py::arg("depth"), py::arg("device"))
+      .def("record", &RoundEngine::record)
+      .def("wait", &RoundEngine::wait)
+      .def("recorded", &RoundEngine::recorded)
+      .def("forget", &RoundEngine::forget)
+      .def("set_xgmi", &RoundEngine::set_xgmi)
+      .def("set_server_slot", &RoundEngine::set_server_slot)
+      .def("route_end", &RoundEngine::route_end)
+      .def("pull_fast", &RoundEngine::pull_fast)
+      .def("pull_xgmi", &RoundEngine::pull_xgmi)
+      .def("pull_xgmi_finish", &RoundEngine::pull_xgmi_finish)
+      .def("push_fast", &RoundEngine::push_fast)
+      .def("push_xgmi", &RoundEngine::push_xgmi);
+}
+
+}  // namespace ss

@@ -392,8 +392,8 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     if cfg.get("model", "sparse_lr") == "word2vec" and ctx.is_worker:
         d = w.data
         stats["w2v"] = {"layout": d.mode, "neg_mode": getattr(d, "neg_mode", "shared"),
-                        "mfma": "bf16" if (d.mode == "window" and not w.per_pair)
-                        or w.mfma_bf16 else "fp32" if d.mode == "pairs" else "none (fp32 dots)",
+                        "mfma": ("none (fp32 dot products)" if w.per_pair else
+                                 "bf16" if d.mode == "window" or w.mfma_bf16 else "fp32"),
                         "negatives": d.negatives}
     m = ctx.engine.metrics.counters
     if m:

@@ -165,6 +165,14 @@ class XgmiTransport(Transport):
             hip().dlpack_view(self.arena.base + hdr, [self.world], 0, 64,
                               self.device.index or 0))
 
+    def channel(self, ch: str) -> int:
+        """Arena channel id of ``ch`` (the C++ round engine addresses it)."""
+        return self._ch[ch]
+
+    def layout(self, ch: str, part: int, slot: int) -> tuple:
+        """(header offset, data offset, per-source segment bytes) in the arena."""
+        return self._layout[(ch, part, slot)]
+
     def seg_rows(self, ch: str, part: int, row_bytes: int) -> int:
         return self._layout[(ch, part, 0)][2] // row_bytes
 

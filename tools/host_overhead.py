@@ -8,6 +8,15 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def _transport(dev):
+    """SS_ENGINE_GENERAL=xgmi: the N>1 path through a size-1 mailbox arena."""
+    if os.environ.get("SS_ENGINE_GENERAL") == "xgmi":
+        from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+        return XgmiTransport(0, 1, dev, None)
+    return None
+
+
 def _worker(model, dev):
     from swiftsnails_amd.parallel.engine import PSEngine
 
@@ -16,7 +25,8 @@ def _worker(model, dev):
 
         data = CtrSynth()
         table = make_lr_table(data.num_features, device=dev)
-        eng = PSEngine(table, None, max_keys=data.batch_size * data.num_fields, dim=1, device=dev)
+        eng = PSEngine(table, _transport(dev), max_keys=data.batch_size * data.num_fields, dim=1,
+                       device=dev)
         return SparseLRWorker(eng, data)
     from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
     from swiftsnails_amd.ops.table import HbmTable
@@ -24,12 +34,12 @@ def _worker(model, dev):
     data = W2VSynth(mode="pairs" if model == "w2v_pairs" else "window")
     opt, init = make_w2v_table_args(128)
     table = HbmTable(128, int(2 * data.vocab / 0.5) + 1024, optimizer=opt, init=init, device=dev)
-    eng = PSEngine(table, None, max_keys=data.n_keys, dim=128, device=dev)
+    eng = PSEngine(table, _transport(dev), max_keys=data.n_keys, dim=128, device=dev)
     return Word2VecWorker(eng, data)
 
 
 def main():
-    """python tools/host_overhead.py [lr|w2v|w2v_pairs]"""
+    """python tools/host_overhead.py [lr|w2v|w2v_pairs]  (SS_ENGINE_GENERAL=xgmi: N>1 path)"""
     dev = torch.device("cuda", 0)
     w = _worker(sys.argv[1] if len(sys.argv) > 1 else "lr", dev)
     for _ in range(10):
