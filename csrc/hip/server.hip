@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
                                                        const uint32_t* __restrict__ pj,
                                                        const uint32_t* __restrict__ luid,
                                                        const float* __restrict__ rows,
-                                                       float* __restrict__ out, int D) {
+                                                       float* __restrict__ out, int D, XDst xd) {
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], base = ubase[b];
   const long long tot = (long long)(p1 - p0) * D;
@@ -237,8 +237,14 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
     const uint32_t p = p0 + (uint32_t)(e / D);
     const int c = (int)(e % D);
     const uint32_t l = luid[p];
-    out[(long long)pj[p] * D + c] = l == kSrvInv ? 0.f : rows[((long long)base + l) * D + c];
+    const float v = l == kSrvInv ? 0.f : rows[((long long)base + l) * D + c];
+    // xd: straight into the source's mailbox (see XDst)
+    if (xd.nsrc)
+      xd.row(pj[p], D)[c] = v;
+    else
+      out[(long long)pj[p] * D + c] = v;
   }
+  if (xd.nsrc) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // gradient merge of rows of width D: grads received at positions pj[p] are
@@ -351,10 +357,10 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
 
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
-                          int D, hipStream_t st) {
+                          int D, hipStream_t st, const XDst* xd) {
   if (P <= 0) return;
   hipLaunchKernelGGL(k_srv_fill_rows, dim3(P), dim3(256), 0, st, bstart, ubase, pj, luid, rows,
-                     out, D);
+                     out, D, xd ? *xd : XDst{});
   check_launch("k_srv_fill_rows");
 }
 

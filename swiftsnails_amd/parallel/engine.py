@@ -313,8 +313,11 @@ class PSEngine(HostRounds):
         return self.capture_tag or 0
 
     def _wait_ev(self, kind: int, obj, stream: int) -> None:
+        """``stream`` waits for the object's route / pull event if it was
+        recorded in the current capture (eager: eagerly); an event of an
+        earlier capture or of the eager priming has completed already."""
         if obj.ready:
-            self.native.wait(kind, obj.slot, stream, obj.tag)
+            self.native.wait(kind, obj.slot, stream, self._tag)
 
     def _release(self, slot: int) -> None:
         if self.gpu:
