@@ -493,10 +493,8 @@ __global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ luid,
                                                     const float* __restrict__ uvals,
                                                     float* __restrict__ occ, int osi,
-                                                    const uint32_t* __restrict__ pj,
-                                                    XDst xd) {
-  // pj: write sample order instead, occ[pj[p]] (the forward then streams occ);
-  // xd.nsrc: the server's response rows straight into the sources' mailboxes
+                                                    const uint32_t* __restrict__ pj) {
+  // pj: write sample order instead, occ[pj[p]] (the forward then streams occ)
   __shared__ float sv[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
@@ -515,18 +513,9 @@ __global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const uint32_t p = pb + r * FT;
-      if (p < p1) {
-        const float v = l[r] < nu ? sv[l[r]] : 0.f;
-        if (xd.nsrc)
-          *xd.row(q[r], 1) = v;
-        else
-          occ[q[r]] = v;
-      }
+      if (p < p1) occ[q[r]] = l[r] < nu ? sv[l[r]] : 0.f;
     }
   }
-  // remote (uncached) stores acknowledged before the block retires: the
-  // mailbox publish that follows on the stream orders after every one
-  if (xd.nsrc) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // K7 for scalar rows (sparse LR): one workgroup per bucket sums the gradients
@@ -971,7 +960,7 @@ void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const 
   if (n <= 0) return;
   const BdLayout L = bd_layout(n, nranks, ndest);
   hipLaunchKernelGGL(k_bd_fill_occ<512>, dim3(L.P), dim3(512), 0, st, scratch + L.bstart,
-                     scratch + L.ubase, scratch + L.unum, luid, uvals, occ, osi, pj, XDst{});
+                     scratch + L.ubase, scratch + L.unum, luid, uvals, occ, osi, pj);
   check_launch("k_bd_fill_occ");
 }
 
@@ -1044,10 +1033,10 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
 
 void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* unum, const uint32_t* luid, const float* uvals,
-                          float* occ, const uint32_t* pj, hipStream_t st, const XDst* xd) {
+                          float* occ, const uint32_t* pj, hipStream_t st) {
   if (P <= 0) return;
   hipLaunchKernelGGL(k_bd_fill_occ<512>, dim3(P), dim3(512), 0, st, bstart, ubase, unum, luid,
-                     uvals, occ, 0, pj, xd ? *xd : XDst{});
+                     uvals, occ, 0, pj);
   check_launch("k_bd_fill_occ_p");
 }
 

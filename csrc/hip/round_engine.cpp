@@ -292,27 +292,19 @@ class RoundEngine {
                        uintptr_t sent, const std::vector<uintptr_t>& metrics) {
     // the rows each source gets back = the keys it sent here (keys header)
     const uintptr_t rc = xg_->base() + keys_[slot][0].hdr;
-    // response rows straight into every source's mailbox (my segment of its
-    // vals region): no local buffer, no copying put — the put only writes
-    // the counts and publishes
-    XDst xd{};
-    xd.cap = cap_;
-    xd.nsrc = nranks_;
-    for (int s = 0; s < nranks_; ++s)
-      xd.base[s] = xg_->peer(s) + vals_[slot].data + (long long)rank_ * vals_[slot].seg;
     if (svals) {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
       if (dim_ == 1)
         launch_bd_fill_occ_p(Ps, S.bstart, S.ubase, S.unum, S.luid, Pt<const float>(svals),
-                             nullptr, S.pj, St(stream), &xd);
+                             Pt<float>(rvals), S.pj, St(stream));
       else
         launch_srv_fill_rows(Ps, S.bstart, S.ubase, S.pj, S.luid, Pt<const float>(svals),
-                             nullptr, dim_, St(stream), &xd);
+                             Pt<float>(rvals), dim_, St(stream));
     }
     std::vector<std::vector<long long>> parts;
     parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_));
-    xg_->put(ch_[1], parts, bpp_, stream, /*nocopy=*/true);
+    xg_->put(ch_[1], parts, bpp_, stream);
     std::vector<uintptr_t> m = metrics;
     if (!m.empty()) {
       if (m.size() != 3) throw std::invalid_argument("pull_xgmi: metrics = (acc, xval, xacc)");

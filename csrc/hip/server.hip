@@ -229,7 +229,7 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
                                                        const uint32_t* __restrict__ pj,
                                                        const uint32_t* __restrict__ luid,
                                                        const float* __restrict__ rows,
-                                                       float* __restrict__ out, int D, XDst xd) {
+                                                       float* __restrict__ out, int D) {
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], base = ubase[b];
   const long long tot = (long long)(p1 - p0) * D;
@@ -237,14 +237,8 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
     const uint32_t p = p0 + (uint32_t)(e / D);
     const int c = (int)(e % D);
     const uint32_t l = luid[p];
-    const float v = l == kSrvInv ? 0.f : rows[((long long)base + l) * D + c];
-    // xd: straight into the source's mailbox (see XDst)
-    if (xd.nsrc)
-      xd.row(pj[p], D)[c] = v;
-    else
-      out[(long long)pj[p] * D + c] = v;
+    out[(long long)pj[p] * D + c] = l == kSrvInv ? 0.f : rows[((long long)base + l) * D + c];
   }
-  if (xd.nsrc) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
 // gradient merge of rows of width D: grads received at positions pj[p] are
@@ -309,16 +303,19 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
     const long long slot = slots ? slots[(long long)base + l] : -1;
     for (int c0 = 0; c0 < D; c0 += 64) {
       const int c = c0 + lane;
+      // the row (and state) loads issued before the gradient sum: their
+      // latency overlaps the gathers instead of following them
+      const bool upd = slots && slot >= 0 && c < D;
+      float wv = upd ? row_ld(tab, slot, c) : 0.f;
+      float s1 = upd && ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
+      float s2 = upd && ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
       float acc = 0.f;
       if (c < D)
         for (uint32_t i = a; i < z; ++i) acc += grads[(long long)pj[p0 + ord[i]] * D + c];
       if (c >= D) continue;
       if (!slots) {
         merged[((long long)base + l) * D + c] = acc;
-      } else if (slot >= 0) {
-        float wv = row_ld(tab, slot, c);
-        float s1 = ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
-        float s2 = ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
+      } else if (upd) {
         opt_update(op, wv, s1, s2, acc);
         row_st(tab, slot, c, wv, true);
         if (ns > 0) row_st(tab, slot, D + c, s1, true);
@@ -357,10 +354,10 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
 
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
-                          int D, hipStream_t st, const XDst* xd) {
+                          int D, hipStream_t st) {
   if (P <= 0) return;
   hipLaunchKernelGGL(k_srv_fill_rows, dim3(P), dim3(256), 0, st, bstart, ubase, pj, luid, rows,
-                     out, D, xd ? *xd : XDst{});
+                     out, D);
   check_launch("k_srv_fill_rows");
 }
 

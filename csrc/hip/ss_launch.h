@@ -169,20 +169,6 @@ void launch_bd_reduce_fm(long long n, int nranks, const uint32_t* scratch, const
                          int ndest = 0);
 long long bd_fm_ovf_words(long long n);
 
-// Segmented output of the server's response rows (N>1 over the xGMI
-// mailboxes): received position q of source s = q / cap is written straight
-// into source s's mailbox, base[s] + (q - s * cap) * row_bytes, instead of a
-// local buffer a put then copies (nsrc 0: a plain local `out`)
-struct XDst {
-  char* base[16];
-  long long cap;
-  int nsrc;
-  __device__ __forceinline__ float* row(long long q, int D) const {
-    const long long s = q / cap;
-    return reinterpret_cast<float*>(base[s]) + (q - s * cap) * (long long)D;
-  }
-};
-
 // explicit-layout forms of the bucket kernels (server-side merge)
 void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, const uint32_t* unum,
                         const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
@@ -190,8 +176,7 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
                         const float* snap, const OptParams* op, hipStream_t st);
 void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* unum, const uint32_t* luid, const float* uvals,
-                          float* occ, const uint32_t* pj, hipStream_t st,
-                          const XDst* xd = nullptr);
+                          float* occ, const uint32_t* pj, hipStream_t st);
 
 // --- server.hip (N>1: merge of the keys a round receives from all sources)
 int srv_sub_buckets(int nsrc);
@@ -202,7 +187,7 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
                       hipStream_t st);
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
-                          int D, hipStream_t st, const XDst* xd = nullptr);
+                          int D, hipStream_t st);
 void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                            const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
                            const float* grads, float* merged, int D, hipStream_t st,

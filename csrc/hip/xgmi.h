@@ -28,7 +28,6 @@ struct XPart {
   long long hdr_off;                  // arena offset of this part's [nranks] count header
   long long data_off;                 // arena offset of its [nranks][seg_bytes] data
   long long seg_bytes;                // per-source segment capacity
-  int nocopy;                         // the producer stored the data itself: header + arrival only
 };
 
 struct XPut {
@@ -108,18 +107,12 @@ class XgmiArena {
     }
   }
   uintptr_t base() const { return reinterpret_cast<uintptr_t>(base_); }
-  char* peer(int r) const { return peers_.at(r); }
-  int nranks() const { return nranks_; }
-  int rank() const { return rank_; }
   long long bytes() const { return bytes_; }
   uintptr_t err_ptr() const { return reinterpret_cast<uintptr_t>(local_ + 2 * kXMaxCh * kXMaxRanks); }
 
   // parts: (src, sdispl bytes [nranks], cnt dev ptr or 0, cnt_fixed, row_bytes,
   //         hdr_off, data_off, seg_bytes)
-  // nocopy: the segments were stored into the peers' mailboxes by the
-  // producing kernel (XDst); write the counts and publish only
-  void put(int ch, const std::vector<std::vector<long long>>& parts, int bpp, uintptr_t stream,
-           bool nocopy = false) {
+  void put(int ch, const std::vector<std::vector<long long>>& parts, int bpp, uintptr_t stream) {
     if (ch < 0 || ch >= kXMaxCh) throw_error("xgmi: bad channel");
     if (parts.empty() || (int)parts.size() > kXMaxParts) throw_error("xgmi: 1..3 parts");
     XPut P{};
@@ -139,7 +132,7 @@ class XgmiArena {
     for (const auto& v : parts)
       if (v.size() > 6) maxseg = std::max(maxseg, v[6]);
     const long long want = std::max(8ll, (maxseg + 32767) / 32768);
-    P.bpp = nocopy ? 1 : (int)std::max(1ll, std::min((long long)(bpp < 1 ? 1 : bpp), want));
+    P.bpp = (int)std::max(1ll, std::min((long long)(bpp < 1 ? 1 : bpp), want));
     for (size_t q = 0; q < parts.size(); ++q) {
       const auto& v = parts[q];
       if ((int)v.size() != 7 + nranks_) throw_error("xgmi: malformed part");
@@ -151,7 +144,6 @@ class XgmiArena {
       x.hdr_off = v[4];
       x.data_off = v[5];
       x.seg_bytes = v[6];
-      x.nocopy = nocopy ? 1 : 0;
       if (x.row_bytes < 4 || x.row_bytes % 4) throw_error("xgmi: rows of whole 4-byte words");
       if (x.data_off + (long long)nranks_ * x.seg_bytes > bytes_ || x.hdr_off + 8ll * nranks_ > bytes_ ||
           x.hdr_off < kXFlagBytes || x.data_off < kXFlagBytes)

@@ -65,7 +65,6 @@ __global__ __launch_bounds__(kXPutThreads) void k_xput(XPut P, unsigned long lon
     if (b == 0 && t == 0)
       *reinterpret_cast<volatile long long*>(dst_arena + x.hdr_off + 8ll * P.me) = rows;
     const long long stride = (long long)P.bpp * kXPutThreads;
-    if (x.nocopy) continue;
     if ((((uintptr_t)s | (uintptr_t)o) & 15) == 0) {
       const long long n16 = bytes >> 4;
       const int4* s4 = reinterpret_cast<const int4*>(s);
@@ -222,7 +221,7 @@ void bind_xgmi(py::module_& m) {
       .def_property_readonly("bytes", &XgmiArena::bytes)
       .def_property_readonly("err_ptr", &XgmiArena::err_ptr)
       .def("put", &XgmiArena::put, py::arg("ch"), py::arg("parts"), py::arg("bpp"),
-           py::arg("stream"), py::arg("nocopy") = false)
+           py::arg("stream"))
       .def("wait", &XgmiArena::wait, py::arg("ch"), py::arg("fixed"), py::arg("timeout_s"),
            py::arg("stream"), py::arg("metrics") = std::vector<uintptr_t>{},
            py::arg("bpk") = 0.0);

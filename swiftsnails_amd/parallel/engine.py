@@ -478,7 +478,7 @@ class PSEngine(HostRounds):
         if tab is None or tab.push_fn is not None:
             return None
         if self.dim > 1:
-            return "rows"
+            return "rows" if os.environ.get("SS_SRV_FUSE_ROWS", "1") != "0" else None
         if (tab.opt.kind == "adagrad" and tab.width == 2 and tab.G == 1 and
                 not getattr(tab, "bf16", False)):
             return "scalar"
