@@ -236,10 +236,10 @@ class RoundEngine {
   }
 
   // N>1: gradient rows into the servers' mailboxes, wait for every source's,
-  // server merge + ONE update per distinct key (fused: scalar AdaGrad rows
-  // from the snapshot or the row; wider rows lane per coordinate), then the
-  // slot-free event.  `update` false: merged rows only (`merged`; the caller
-  // applies a tensor-code rule).
+  // server merge per distinct key — fused with the AdaGrad update for scalar
+  // rows (from the snapshot or the row), then the slot-free event; `update`
+  // false: merged rows only (`merged`), the caller applies them (the apply
+  // kernel, or a tensor-code rule) and releases the slot.
   void push_xgmi(int slot, int tag, uintptr_t stream, uintptr_t grads, uintptr_t ucount,
                  bool table, bool update, const DevTable& t, const OptParams& op, uintptr_t rgrads,
                  bool scalar_fused, bool snap, uintptr_t merged, bool release) {
@@ -254,10 +254,6 @@ class RoundEngine {
       if (update && scalar_fused)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
                            1, nullptr, &t, S.slots, snap ? S.snap : nullptr, &op, St(stream));
-      else if (update && dim_ > 1)
-        launch_srv_merge_rows(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid,
-                              Pt<const float>(rgrads), nullptr, dim_, St(stream), &t, S.slots,
-                              &op);
       else if (dim_ == 1)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
                            1, Pt<float>(merged), nullptr, nullptr, nullptr, nullptr, St(stream));

@@ -244,20 +244,14 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
 // gradient merge of rows of width D: grads received at positions pj[p] are
 // summed per distinct key into merged[ubase[b] + l].  Per bucket the
 // positions are counting-sorted by local id in LDS, then each wave sums its
-// keys' rows (lanes over the row; no atomics).  `slots` (fused K5): the
-// merged row goes straight into the optimizer update of the key's table row
-// (lane c updates coordinate c and its state) instead of to `merged` — one
-// kernel, no merged-row round trip, no separate apply launch
+// keys' rows (lanes over the row; no atomics)
 __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restrict__ bstart,
                                                         const uint32_t* __restrict__ ubase,
                                                         const uint32_t* __restrict__ unum,
                                                         const uint32_t* __restrict__ pj,
                                                         const uint32_t* __restrict__ luid,
                                                         const float* __restrict__ grads,
-                                                        float* __restrict__ merged, int D,
-                                                        DevTable tab,
-                                                        const long long* __restrict__ slots,
-                                                        OptParams op) {
+                                                        float* __restrict__ merged, int D) {
   __shared__ unsigned int off[kSrvTS + 1];
   __shared__ unsigned short ord[kSrvOcc];
   __shared__ unsigned int wsum[16];
@@ -297,30 +291,14 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
   }
   __syncthreads();
   const int lane = t & 63, w = t >> 6;
-  const int ns = opt_state_per_coord(op.kind);
   for (uint32_t l = w; l < nu; l += 512 / 64) {
     const uint32_t a = off[l], z = off[l + 1];
-    const long long slot = slots ? slots[(long long)base + l] : -1;
     for (int c0 = 0; c0 < D; c0 += 64) {
       const int c = c0 + lane;
-      // the row (and state) loads issued before the gradient sum: their
-      // latency overlaps the gathers instead of following them
-      const bool upd = slots && slot >= 0 && c < D;
-      float wv = upd ? row_ld(tab, slot, c) : 0.f;
-      float s1 = upd && ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
-      float s2 = upd && ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
       float acc = 0.f;
       if (c < D)
         for (uint32_t i = a; i < z; ++i) acc += grads[(long long)pj[p0 + ord[i]] * D + c];
-      if (c >= D) continue;
-      if (!slots) {
-        merged[((long long)base + l) * D + c] = acc;
-      } else if (upd) {
-        opt_update(op, wv, s1, s2, acc);
-        row_st(tab, slot, c, wv, true);
-        if (ns > 0) row_st(tab, slot, D + c, s1, true);
-        if (ns > 1) row_st(tab, slot, 2 * D + c, s2, true);
-      }
+      if (c < D) merged[((long long)base + l) * D + c] = acc;
     }
   }
 }
@@ -363,14 +341,10 @@ void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
 
 void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                            const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
-                           const float* grads, float* merged, int D, hipStream_t st,
-                           const DevTable* t, const long long* slots, const OptParams* op) {
+                           const float* grads, float* merged, int D, hipStream_t st) {
   if (P <= 0) return;
-  if (slots && (!t || !op || (int)t->dim != D ||
-                (int)t->width != D * (1 + opt_state_per_coord(op->kind))))
-    throw_error("srv_merge_rows: a fused update needs the table of these rows");
   hipLaunchKernelGGL(k_srv_merge_rows, dim3(P), dim3(512), 0, st, bstart, ubase, unum, pj, luid,
-                     grads, merged, D, t ? *t : DevTable{}, slots, op ? *op : OptParams{});
+                     grads, merged, D);
   check_launch("k_srv_merge_rows");
 }
 

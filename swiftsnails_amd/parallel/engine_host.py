@@ -123,9 +123,6 @@ class HostRounds:
         if kind == "scalar":
             h.srv_merge(*args, 0, 1, tab.dt, S.slots.data_ptr(),
                         S.snap.data_ptr() if S.snap_valid else 0, tab.opt.native(), st)
-        elif kind == "rows":
-            # rows: the merged gradient row goes straight into the update
-            h.srv_merge(*args, 0, self.dim, tab.dt, S.slots.data_ptr(), 0, tab.opt.native(), st)
         else:
             h.srv_merge(*args, self.sgrad.data_ptr(), self.dim, st=st)
             self._apply_merged(slot)

@@ -95,9 +95,6 @@ KNOBS: dict[str, Knob] = {
                             "0: one per tile); half the CUs leaves CUs to the route stream's "
                             "dedup when the tile is atomic-bound (0.143 -> 0.123 ms/step), one "
                             "per tile is faster with occurrence-row stores (0.101 -> 0.092)"),
-    "SS_SRV_FUSE_ROWS": Knob("1", "parallel/engine.py", "experiment",
-                             "N>1 server, rows wider than 1: merge + optimizer update in one "
-                             "kernel (0: merged rows, then the apply kernel)"),
     "SS_GRAPH_STEPS": Knob("4 x depth", "models/base.py", "tuning",
                            "steps per hipGraph: 1, or a multiple of the ring depth (word2vec "
                            "4 / 8 / 16 / 32: 0.093 / 0.088 / 0.086 / 0.084 ms/step)"),
