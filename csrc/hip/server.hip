@@ -290,11 +290,15 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
     if (l < nu) ord[atomicAdd(&cur[l], 1u)] = (unsigned short)q;
   }
   __syncthreads();
-  const int lane = t & 63, w = t >> 6;
-  for (uint32_t l = w; l < nu; l += 512 / 64) {
+  // a group of G lanes per key, G the row width rounded up to a power of two
+  // (one key per wave left 55 of 64 lanes idle on FM's 9-wide rows)
+  const int G = D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16 : D <= 32 ? 32 : 64;
+  const int lane = t & 63, lg = lane % G;
+  const uint32_t per = 512 / G;  // keys in flight per workgroup
+  for (uint32_t l = (uint32_t)(t / G); l < nu; l += per) {
     const uint32_t a = off[l], z = off[l + 1];
-    for (int c0 = 0; c0 < D; c0 += 64) {
-      const int c = c0 + lane;
+    for (int c0 = 0; c0 < D; c0 += G) {
+      const int c = c0 + lg;
       float acc = 0.f;
       if (c < D)
         for (uint32_t i = a; i < z; ++i) acc += grads[(long long)pj[p0 + ord[i]] * D + c];
