@@ -342,8 +342,8 @@ PYBIND11_MODULE(_ss_hip, m) {
                            P<const uint32_t>(pj), P<const uint32_t>(luid), P<const float>(rows),
                            P<float>(out), D, S(st));
   });
-  // merged gradients per distinct key; with a table (scalar AdaGrad rows) the
-  // update is fused: from the snapshot (blind store) or read from the row
+  // merged gradients per distinct key; with a table the update is fused
+  // (scalar rows: from the snapshot (blind store) or read from the row)
   m.def("srv_merge", [](int Pn, uintptr_t bstart, uintptr_t ubase, uintptr_t unum, uintptr_t pj,
                         uintptr_t luid, uintptr_t grads, uintptr_t merged, int D,
                         std::optional<DevTable> t, uintptr_t slots, uintptr_t snap,
@@ -354,15 +354,12 @@ PYBIND11_MODULE(_ss_hip, m) {
                          P<const float>(grads), 1, P<float>(merged), t ? &*t : nullptr,
                          P<const long long>(slots), P<const float>(snap), op ? &*op : nullptr,
                          S(st));
-    else if (slots)
-      // (fusing the update into the row merge measured slower: FM's 9-wide
-      // rows left 55 of 64 lanes idle, 1.00 -> 1.22 ms/step; word2vec neutral)
-      throw_error("srv_merge: a fused update needs scalar rows");
     else
       launch_srv_merge_rows(Pn, P<const uint32_t>(bstart), P<const uint32_t>(ubase),
                             P<const uint32_t>(unum), P<const uint32_t>(pj),
                             P<const uint32_t>(luid), P<const float>(grads), P<float>(merged), D,
-                            S(st));
+                            S(st), t ? &*t : nullptr, P<const long long>(slots),
+                            op ? &*op : nullptr);
   }, py::arg("P"), py::arg("bstart"), py::arg("ubase"), py::arg("unum"), py::arg("pj"),
      py::arg("luid"), py::arg("grads"), py::arg("merged"), py::arg("D"),
      py::arg("t") = std::nullopt, py::arg("slots") = 0, py::arg("snap") = 0,

@@ -237,7 +237,8 @@ class RoundEngine {
 
   // N>1: gradient rows into the servers' mailboxes, wait for every source's,
   // server merge per distinct key — fused with the AdaGrad update for scalar
-  // rows (from the snapshot or the row), then the slot-free event; `update`
+  // rows (from the snapshot or the row) or into the row update (wider
+  // rows), then the slot-free event; `update`
   // false: merged rows only (`merged`), the caller applies them (the apply
   // kernel, or a tensor-code rule) and releases the slot.
   void push_xgmi(int slot, int tag, uintptr_t stream, uintptr_t grads, uintptr_t ucount,
@@ -257,6 +258,10 @@ class RoundEngine {
       else if (dim_ == 1)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
                            1, Pt<float>(merged), nullptr, nullptr, nullptr, nullptr, St(stream));
+      else if (update)
+        launch_srv_merge_rows(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid,
+                              Pt<const float>(rgrads), nullptr, dim_, St(stream), &t, S.slots,
+                              &op);
       else
         launch_srv_merge_rows(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid,
                               Pt<const float>(rgrads), Pt<float>(merged), dim_, St(stream));

@@ -244,14 +244,19 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
 // gradient merge of rows of width D: grads received at positions pj[p] are
 // summed per distinct key into merged[ubase[b] + l].  Per bucket the
 // positions are counting-sorted by local id in LDS, then each wave sums its
-// keys' rows (lanes over the row; no atomics)
+// keys' rows (lanes over the row; no atomics).  `slots`: the merged row goes
+// straight into the optimizer update of the key's table row (lane c updates
+// coordinate c and its state) — no merged-row round trip, no apply launch
 __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restrict__ bstart,
                                                         const uint32_t* __restrict__ ubase,
                                                         const uint32_t* __restrict__ unum,
                                                         const uint32_t* __restrict__ pj,
                                                         const uint32_t* __restrict__ luid,
                                                         const float* __restrict__ grads,
-                                                        float* __restrict__ merged, int D) {
+                                                        float* __restrict__ merged, int D,
+                                                        DevTable tab,
+                                                        const long long* __restrict__ slots,
+                                                        OptParams op) {
   __shared__ unsigned int off[kSrvTS + 1];
   __shared__ unsigned short ord[kSrvOcc];
   __shared__ unsigned int wsum[16];
@@ -295,14 +300,29 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
   const int G = D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16 : D <= 32 ? 32 : 64;
   const int lane = t & 63, lg = lane % G;
   const uint32_t per = 512 / G;  // keys in flight per workgroup
+  const int ns = opt_state_per_coord(op.kind);
   for (uint32_t l = (uint32_t)(t / G); l < nu; l += per) {
     const uint32_t a = off[l], z = off[l + 1];
+    const long long slot = slots ? slots[(long long)base + l] : -1;
     for (int c0 = 0; c0 < D; c0 += G) {
       const int c = c0 + lg;
+      if (c >= D) continue;
+      // fused update: the row (and state) loads go out before the gradient
+      // sum, their latency overlaps the gathers instead of following them
+      const bool upd = slots && slot >= 0;
+      float wv = upd ? row_ld(tab, slot, c) : 0.f;
+      float s1 = upd && ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
+      float s2 = upd && ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
       float acc = 0.f;
-      if (c < D)
-        for (uint32_t i = a; i < z; ++i) acc += grads[(long long)pj[p0 + ord[i]] * D + c];
-      if (c < D) merged[((long long)base + l) * D + c] = acc;
+      for (uint32_t i = a; i < z; ++i) acc += grads[(long long)pj[p0 + ord[i]] * D + c];
+      if (!slots) {
+        merged[((long long)base + l) * D + c] = acc;
+      } else if (upd) {
+        opt_update(op, wv, s1, s2, acc);
+        row_st(tab, slot, c, wv, true);
+        if (ns > 0) row_st(tab, slot, D + c, s1, true);
+        if (ns > 1) row_st(tab, slot, 2 * D + c, s2, true);
+      }
     }
   }
 }
@@ -345,10 +365,15 @@ void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
 
 void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                            const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
-                           const float* grads, float* merged, int D, hipStream_t st) {
+                           const float* grads, float* merged, int D, hipStream_t st,
+                           const DevTable* t, const long long* slots, const OptParams* op) {
   if (P <= 0) return;
+  if (slots && (!t || !op || (int)t->dim != D ||
+                (int)t->width != D * (1 + opt_state_per_coord(op->kind))))
+    throw_error("srv_merge_rows: a fused update needs the table of these rows");
+  if (!slots && !merged) throw_error("srv_merge_rows: merged rows or a fused update");
   hipLaunchKernelGGL(k_srv_merge_rows, dim3(P), dim3(512), 0, st, bstart, ubase, unum, pj, luid,
-                     grads, merged, D);
+                     grads, merged, D, t ? *t : DevTable{}, slots, op ? *op : OptParams{});
   check_launch("k_srv_merge_rows");
 }
 

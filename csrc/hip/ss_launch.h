@@ -190,7 +190,9 @@ void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           int D, hipStream_t st);
 void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                            const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
-                           const float* grads, float* merged, int D, hipStream_t st);
+                           const float* grads, float* merged, int D, hipStream_t st,
+                           const DevTable* t = nullptr, const long long* slots = nullptr,
+                           const OptParams* op = nullptr);
 
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);

@@ -471,13 +471,15 @@ class PSEngine(HostRounds):
 
     # ------------------------------------------------------------ stage 3
     def _server_update_kind(self) -> Optional[str]:
-        """How the server merge applies the update: fused for scalar AdaGrad
-        rows ("scalar"); None: merged rows first, then the apply kernel (wider
-        rows: fusing the update into the row merge measured slower, FM
-        1.00 -> 1.22 ms/step on the N>1 path) or a tensor-code rule."""
+        """How the server merge applies the update: fused into the merge for
+        scalar AdaGrad rows ("scalar") and for wider rows ("rows": lane c of
+        a key's lane group updates coordinate c); None: merged rows first,
+        then the apply kernel (other scalar rules) or a tensor-code rule."""
         tab = self.table
-        if tab is None or tab.push_fn is not None or self.dim > 1:
+        if tab is None or tab.push_fn is not None:
             return None
+        if self.dim > 1:
+            return "rows"
         if (tab.opt.kind == "adagrad" and tab.width == 2 and tab.G == 1 and
                 not getattr(tab, "bf16", False)):
             return "scalar"

@@ -120,9 +120,10 @@ class HostRounds:
         args = (self.Ps, S.bstart.data_ptr(), S.ubase.data_ptr(), S.unum.data_ptr(),
                 S.pj.data_ptr(), S.luid.data_ptr(), self.rgrads[slot].data_ptr())
         kind = self._server_update_kind()
-        if kind == "scalar":
-            h.srv_merge(*args, 0, 1, tab.dt, S.slots.data_ptr(),
-                        S.snap.data_ptr() if S.snap_valid else 0, tab.opt.native(), st)
+        if kind is not None:
+            h.srv_merge(*args, 0, self.dim, tab.dt, S.slots.data_ptr(),
+                        S.snap.data_ptr() if S.snap_valid and kind == "scalar" else 0,
+                        tab.opt.native(), st)
         else:
             h.srv_merge(*args, self.sgrad.data_ptr(), self.dim, st=st)
             self._apply_merged(slot)

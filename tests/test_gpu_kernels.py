@@ -751,14 +751,15 @@ def test_stream_helpers_match_torch(dev):
     assert float(x.sum().item()) == 2000.0
 
 
-@pytest.mark.parametrize("dim,fused", [(1, True), (3, False), (64, False)])
+@pytest.mark.parametrize("dim,fused", [(1, True), (3, False), (64, False), (9, True),
+                                       (128, True)])
 def test_server_merge_matches_reference(dev, dim, fused):
     """server.hip on the keys three sources route to one server (real
     bucketed dedups with the common N>1 layout, overlapping key sets): one
     entry per distinct key, response rows per received position, and the
-    merged gradient of every distinct key — fused into the AdaGrad update for
-    scalar rows (read-modify-write, no snapshot), else a merged row then the
-    apply kernel."""
+    merged gradient of every distinct key — fused into the AdaGrad update
+    (scalar rows: read-modify-write, no snapshot; wider rows: a lane group per
+    key), else a merged row then the apply kernel."""
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.ops.dedup import Deduper
     from swiftsnails_amd.ops.optim import InitConfig, Optimizer
