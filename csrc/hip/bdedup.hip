@@ -74,6 +74,7 @@ static int bd_target(int nranks) { return nranks > 1 ? kBdTargetDist : kBdTarget
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
 static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
+static constexpr int kBdMaxSub = 64;    // server sub-buckets per bucket (srv_sub_buckets)
 
 __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs, uint32_t Pd) {
   const uint32_t d = rs.dest_of(key);
@@ -344,7 +345,8 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    unsigned long long* __restrict__ dbg,
                                                    uint64_t* __restrict__ ukeys,
                                                    float* __restrict__ ugrad, int gdim,
-                                                   uint8_t* __restrict__ usingle) {
+                                                   uint8_t* __restrict__ usingle, int msub,
+                                                   uint32_t* __restrict__ usub) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
   if (dbg && t == 0) dbg[(long long)b * 8 + (i)] = wall_clock64();
@@ -354,8 +356,10 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
   __shared__ int bad;
+  __shared__ unsigned int hsub[kBdMaxSub];  // msub > 1: keys per server sub-bucket, then offsets
   const int t = threadIdx.x, b = blockIdx.x;
   if (t == 0) bad = 0;
+  if (t < kBdMaxSub) hsub[t] = 0u;
   for (int s = t; s < kBdTS; s += kBdDT) {
     tab[s] = kEmptyKey;
     dupf[s] = 0;
@@ -421,12 +425,38 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   }
   __syncthreads();
   BD_STAMP(1)
-  // compaction in slot order: thread t owns slots [kPerT*t, kPerT*(t+1))
+  // compaction in slot order: thread t owns slots [kPerT*t, kPerT*(t+1));
+  // msub > 1 (N>1 xGMI rounds): grouped by the server's sub-bucket first, so
+  // a server sub-bucket's keys from this bucket are one contiguous range
+  // (offsets in usub) and the server reads exactly its keys — no re-read of
+  // the whole run per sub-bucket, no hashing pass to count them
   constexpr int kPerT = kBdTS / kBdDT;
-  unsigned int occ = 0;
+  unsigned int o = 0;
+  uint8_t sb[kPerT];
+  uint16_t rk[kPerT];
+  if (msub > 1) {
 #pragma unroll
-  for (int k = 0; k < kPerT; ++k) occ += tab[t * kPerT + k] != kEmptyKey;
-  unsigned int o = block_excl_scan<kBdDT / 64>(occ, wsum, &tot);
+    for (int k = 0; k < kPerT; ++k) {
+      const unsigned long long v = tab[t * kPerT + k];
+      sb[k] = v != kEmptyKey ? (uint8_t)srv_sub(v, msub) : 0;
+      rk[k] = v != kEmptyKey ? (uint16_t)atomicAdd(&hsub[sb[k]], 1u) : 0;
+    }
+    __syncthreads();
+    if (t == 0) {
+      unsigned int e = 0;
+      for (int i = 0; i < msub; ++i) {
+        const unsigned int c = hsub[i];
+        hsub[i] = e;
+        e += c;
+      }
+      tot = e;
+    }
+  } else {
+    unsigned int occ = 0;
+#pragma unroll
+    for (int k = 0; k < kPerT; ++k) occ += tab[t * kPerT + k] != kEmptyKey;
+    o = block_excl_scan<kBdDT / 64>(occ, wsum, &tot);
+  }
   // the bucket's unique ids: one device-scope add per bucket reserves them in
   // its destination's segment (ucount[d], zeroed by k_bd_count) — no scan
   // over the buckets, and the keys go straight to the alltoallv send layout
@@ -440,17 +470,18 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
     if (bad) atomicOr(err, 1u);
   }
   __syncthreads();
+  if (msub > 1 && usub && t < msub) usub[(long long)b * msub + t] = hsub[t];
   const unsigned long long ub = sbase;
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
     const int s = t * kPerT + k;
     const unsigned long long v = tab[s];
     if (v != kEmptyKey) {
-      lid[s] = o;
-      if (bkeys) bkeys[p0 + o] = v;  // staged in the bucket's own occurrence range
-      if (ukeys) ukeys[ub + o] = v;
-      if (usingle) usingle[ub + o] = dupf[s] ? 0 : 1;  // one occurrence in the batch
-      ++o;
+      const unsigned int q = msub > 1 ? hsub[sb[k]] + rk[k] : o++;
+      lid[s] = q;
+      if (bkeys) bkeys[p0 + q] = v;  // staged in the bucket's own occurrence range
+      if (ukeys) ukeys[ub + q] = v;
+      if (usingle) usingle[ub + q] = dupf[s] ? 0 : 1;  // one occurrence in the batch
     }
   }
   if (ugrad)  // zeroed gradient rows for consumers that scatter-add into them
@@ -876,8 +907,10 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                      unsigned long long* dbg, uint32_t* rec, uint8_t* usingle, int ndest,
-                     long long lay_n) {
+                     long long lay_n, int msub, uint32_t* usub) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
+  if (msub < 1 || msub > kBdMaxSub || (msub > 1 && !usub))
+    throw_error("bdedup: server sub-buckets 1..64 (and their offset table)");
   // lay_n (N>1 engines): the bucket layout is that of a call of lay_n keys
   // whatever this call's n, so every rank splits a destination's keys into
   // the same Pd buckets (the servers merge bucket k of all sources); an empty
@@ -944,7 +977,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                      bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
                      reinterpret_cast<const uint4*>(rec), dbg,
-                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle);
+                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub);
   check_launch("k_bd_dedup");
   if (inv && n > 0) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");

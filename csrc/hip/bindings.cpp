@@ -187,19 +187,20 @@ PYBIND11_MODULE(_ss_hip, m) {
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
                        uintptr_t st, uintptr_t dbg, uintptr_t rec, uintptr_t usingle,
-                       int ndest, long long lay_n) {
+                       int ndest, long long lay_n, int msub, uintptr_t usub) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
     launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
                     P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
                     P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
                     P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg),
-                    P<uint32_t>(rec), P<uint8_t>(usingle), ndest, lay_n);
+                    P<uint32_t>(rec), P<uint8_t>(usingle), ndest, lay_n, msub,
+                    P<uint32_t>(usub));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
      py::arg("rec") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0,
-     py::arg("lay_n") = 0);
+     py::arg("lay_n") = 0, py::arg("msub") = 1, py::arg("usub") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
@@ -325,12 +326,16 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("srv_dedup", [](uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum, long long cap, int nsrc,
                         int Pd, int m, int me, uintptr_t cnt, uintptr_t bstart, uintptr_t pj,
                         uintptr_t luid, uintptr_t bkeys, uintptr_t ubase, uintptr_t unum,
-                        uintptr_t ucount, uintptr_t err, uintptr_t st) {
+                        uintptr_t ucount, uintptr_t err, uintptr_t st, uintptr_t roff) {
     launch_srv_dedup(P<const uint64_t>(rkeys), P<const uint32_t>(rbase), P<const uint32_t>(rnum),
                      cap, nsrc, Pd, m, me, P<uint32_t>(cnt), P<uint32_t>(bstart), P<uint32_t>(pj),
                      P<uint32_t>(luid), P<uint64_t>(bkeys), P<uint32_t>(ubase), P<uint32_t>(unum),
-                     P<unsigned long long>(ucount), P<uint32_t>(err), S(st));
-  });
+                     P<unsigned long long>(ucount), P<uint32_t>(err), S(st),
+                     P<const uint32_t>(roff));
+  }, py::arg("rkeys"), py::arg("rbase"), py::arg("rnum"), py::arg("cap"), py::arg("nsrc"),
+     py::arg("Pd"), py::arg("m"), py::arg("me"), py::arg("cnt"), py::arg("bstart"), py::arg("pj"),
+     py::arg("luid"), py::arg("bkeys"), py::arg("ubase"), py::arg("unum"), py::arg("ucount"),
+     py::arg("err"), py::arg("st"), py::arg("roff") = 0);
   m.def("srv_fill", [](int Pn, uintptr_t bstart, uintptr_t ubase, uintptr_t unum, uintptr_t pj,
                        uintptr_t luid, uintptr_t rows, uintptr_t out, int D, uintptr_t st) {
     if (D == 1)

@@ -98,8 +98,9 @@ class RoundEngine {
   }
 
   // ---------------------------------------------------------- N>1 set-up
-  // regions: keys [depth][3 parts], vals [depth], grads [depth], each
-  // (hdr, data, seg); chans: the arena channel ids of keys / vals / grads
+  // regions: keys [depth][3 parts, or 4 with the sub-bucket offsets of a
+  // server split (sub > 1)], vals [depth], grads [depth], each (hdr, data,
+  // seg); chans: the arena channel ids of keys / vals / grads
   void set_xgmi(XgmiArena* arena, std::vector<int> chans, std::vector<std::vector<long long>> keys,
                 std::vector<std::vector<long long>> vals, std::vector<std::vector<long long>> grads,
                 int nranks, int rank, int Pd, int sub, long long cap, int dim, int bpp,
@@ -109,10 +110,12 @@ class RoundEngine {
       throw std::invalid_argument("set_xgmi: one region set per ring slot");
     xg_ = arena;
     ch_ = {chans[0], chans[1], chans[2]};
+    nkp_ = sub > 1 ? 4 : 3;
     for (int s = 0; s < depth_; ++s) {
-      if (keys[s].size() != 9 || vals[s].size() != 3 || grads[s].size() != 3)
+      if ((int)keys[s].size() != 3 * nkp_ || vals[s].size() != 3 || grads[s].size() != 3)
         throw std::invalid_argument("set_xgmi: (hdr, data, seg) per part");
-      for (int p = 0; p < 3; ++p) keys_[s][p] = {keys[s][3 * p], keys[s][3 * p + 1], keys[s][3 * p + 2]};
+      for (int p = 0; p < nkp_; ++p)
+        keys_[s][p] = {keys[s][3 * p], keys[s][3 * p + 1], keys[s][3 * p + 2]};
       vals_[s] = {vals[s][0], vals[s][1], vals[s][2]};
       grads_[s] = {grads[s][0], grads[s][1], grads[s][2]};
     }
@@ -143,15 +146,21 @@ class RoundEngine {
 
   // ------------------------------------------------------------ stage 1
   // after the dedup on the route stream: N>1 — the keys + every destination's
-  // per-bucket runs into the peers' mailboxes; then the route event
+  // per-bucket runs (+ their sub-bucket offsets) into the peers' mailboxes;
+  // then the route event
   void route_end(int slot, int tag, uintptr_t route, uintptr_t ukeys, uintptr_t ucount,
-                 uintptr_t runs_base, uintptr_t runs_num) {
+                 uintptr_t runs_base, uintptr_t runs_num, uintptr_t runs_sub) {
     check_slot(slot);
     if (xg_) {
       std::vector<std::vector<long long>> parts;
       parts.push_back(part(ukeys, ucount, 0, 8, keys_[slot][0], cap_));
       parts.push_back(part(runs_base, 0, Pd_, 4, keys_[slot][1], Pd_));
       parts.push_back(part(runs_num, 0, Pd_, 4, keys_[slot][2], Pd_));
+      if (nkp_ == 4) {
+        if (!runs_sub) throw std::invalid_argument("route_end: the sub-bucket offsets");
+        parts.push_back(part(runs_sub, 0, (long long)Pd_ * sub_, 4, keys_[slot][3],
+                             (long long)Pd_ * sub_));
+      }
       xg_->put(ch_[0], parts, bpp_, route);
     }
     record(kRoute, slot, route, tag);
@@ -189,15 +198,18 @@ class RoundEngine {
     pull_waits(slot, tag, stream, wait_route, prev);
     // missing sources' fixed-size run tables read as empty
     const long long nb = 4ll * Pd_;
-    xg_->wait(ch_[0], {{keys_[slot][1].data, keys_[slot][1].seg, nb},
-                        {keys_[slot][2].data, keys_[slot][2].seg, nb}},
-              timeout_, stream, {}, 0.0);
+    std::vector<std::vector<long long>> fixed = {{keys_[slot][1].data, keys_[slot][1].seg, nb},
+                                                 {keys_[slot][2].data, keys_[slot][2].seg, nb}};
+    if (nkp_ == 4) fixed.push_back({keys_[slot][3].data, keys_[slot][3].seg, nb * sub_});
+    xg_->wait(ch_[0], fixed, timeout_, stream, {}, 0.0);
     if (table) {
       SrvSlot& S = srv_[slot];
+      const uint32_t* roff =
+          nkp_ == 4 ? Pt<const uint32_t>(xg_->base() + keys_[slot][3].data) : nullptr;
       launch_srv_dedup(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
                        Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt,
                        S.bstart, S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount,
-                       Pt<uint32_t>(srv_err), St(stream));
+                       Pt<uint32_t>(srv_err), St(stream), roff);
       launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
                             Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
                             G, St(stream), snap ? S.snap : nullptr);
@@ -320,7 +332,8 @@ class RoundEngine {
   std::vector<SrvSlot> srv_;
   XgmiArena* xg_ = nullptr;
   std::array<int, 3> ch_{};
-  std::vector<std::array<XReg, 3>> keys_;
+  std::vector<std::array<XReg, 4>> keys_;
+  int nkp_ = 3;  // parts of the keys channel
   std::vector<XReg> vals_, grads_;
   int nranks_ = 1, rank_ = 0, Pd_ = 1, sub_ = 1, dim_ = 1, bpp_ = 128;
   long long cap_ = 0;

@@ -50,17 +50,30 @@ struct SrvRuns {
   const uint32_t* rnum;    // [nsrc][Pd] the sources' bucket sizes
   long long cap;           // per-source segment capacity (== every source's ucap)
   int nsrc, Pd, m, me;
+  // [nsrc][Pd][m] or null: where sub-bucket t starts in source s's run k (the
+  // sender grouped each run by sub-bucket, bdedup.hip msub)
+  const uint32_t* roff;
   __device__ __forceinline__ long long run_start(int s, int k) const {
     return (long long)s * cap + ((long long)rbase[(long long)s * Pd + k] - (long long)me * cap);
   }
   __device__ __forceinline__ uint32_t run_len(int s, int k) const {
     return rnum[(long long)s * Pd + k];
   }
+  // the part of run (s, k) a server bucket k*m + t reads: the sub-bucket's
+  // range when the sender grouped it, else the whole run (filtered by hash)
+  __device__ __forceinline__ void part(int s, int k, int t, long long* a, uint32_t* len) const {
+    *a = run_start(s, k);
+    const uint32_t n = run_len(s, k);
+    if (m == 1 || !roff) {
+      *len = n;
+      return;
+    }
+    const uint32_t* o = roff + ((long long)s * Pd + k) * m;
+    const uint32_t lo = min(o[t], n), hi = t + 1 < m ? min(o[t + 1], n) : n;
+    *a += lo;
+    *len = hi > lo ? hi - lo : 0u;
+  }
 };
-
-__device__ __forceinline__ uint32_t srv_sub(uint64_t key, int m) {
-  return m == 1 ? 0u : __umulhi((uint32_t)dedup_hash(key), (uint32_t)m);
-}
 
 // 1+2. received keys per server bucket, kSrvCntK buckets k per workgroup;
 //    the LAST workgroup to finish (arrival counter) scans the counts into
@@ -79,12 +92,17 @@ __global__ __launch_bounds__(256) void k_srv_count(SrvRuns R, uint32_t* __restri
   __shared__ bool last;
   const int t = threadIdx.x;
   const int k0 = blockIdx.x * kSrvCntK, k1 = min(R.Pd, k0 + kSrvCntK);
-  if (R.m == 1) {
-    // the run lengths are the counts: one thread per bucket
-    for (int k = k0 + t; k < k1; k += 256) {
+  if (R.m == 1 || R.roff) {
+    // the run (or sub-range) lengths are the counts: one thread per bucket
+    for (int b = k0 * R.m + t; b < k1 * R.m; b += 256) {
       unsigned int c = 0;
-      for (int s = 0; s < R.nsrc; ++s) c += R.run_len(s, k);
-      __hip_atomic_store(&cnt[k], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int s = 0; s < R.nsrc; ++s) {
+        long long a;
+        uint32_t len;
+        R.part(s, b / R.m, b % R.m, &a, &len);
+        c += len;
+      }
+      __hip_atomic_store(&cnt[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   } else {
     for (int i = t; i < kSrvCntK * R.m; i += 256) h[i] = 0u;
@@ -168,13 +186,15 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   };
   // every source's run of bucket k; the keys of sub-bucket `sub` get a
   // position in [p0, p1) (wave-aggregated reservation) and an LDS slot
+  const bool exact = R.m == 1 || R.roff;  // every key read is this sub-bucket's
   for (int s = 0; s < R.nsrc; ++s) {
-    const long long a = R.run_start(s, k);
-    const uint32_t len = R.run_len(s, k);
+    long long a;
+    uint32_t len;
+    R.part(s, k, (int)sub, &a, &len);
     for (uint32_t i0 = 0; i0 < len; i0 += kSrvDT) {
       const uint32_t i = i0 + t;
       const uint64_t key = i < len ? R.rkeys[a + i] : kEmptyKey;
-      const bool mine = key != kEmptyKey && srv_sub(key, R.m) == sub;
+      const bool mine = key != kEmptyKey && (exact || srv_sub(key, R.m) == sub);
       const unsigned long long mask = __ballot(mine);
       unsigned int wb = 0;
       if (lane == 0 && mask) wb = atomicAdd(&cur, (unsigned int)__popcll(mask));
@@ -340,9 +360,9 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
                       long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
                       uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
                       uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
-                      hipStream_t st) {
+                      hipStream_t st, const uint32_t* roff) {
   if (nsrc < 1 || Pd < 1 || m < 1 || m > 64) throw_error("srv_dedup: bad layout");
-  SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me};
+  SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me, roff};
   const int P = Pd * m;
   // cnt has P + 1 words: the last is the count kernel's arrival counter
   // (zeroed once at allocation, reset by the kernel)

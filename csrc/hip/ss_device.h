@@ -139,4 +139,11 @@ __device__ __forceinline__ long long seg_pos(const SegList& sl, long long g, int
   return sl.off[s] + (g - sl.prefix[s]);
 }
 
+// N>1 server sub-bucket of a key (server.hip): the top bits of dedup_hash's
+// low word.  The sender's bucket took the high word's top bits and its LDS
+// slot the low word's low bits, so the three are independent.
+__device__ __forceinline__ uint32_t srv_sub(uint64_t key, int m) {
+  return m <= 1 ? 0u : __umulhi((uint32_t)dedup_hash(key), (uint32_t)m);
+}
+
 }  // namespace ss

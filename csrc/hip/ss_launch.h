@@ -147,7 +147,8 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
                      uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                      float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                      unsigned long long* dbg = nullptr, uint32_t* rec = nullptr,
-                     uint8_t* usingle = nullptr, int ndest = 0, long long lay_n = 0);
+                     uint8_t* usingle = nullptr, int ndest = 0, long long lay_n = 0,
+                     int msub = 1, uint32_t* usub = nullptr);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi = 0,
@@ -184,7 +185,7 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
                       long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
                       uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
                       uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
-                      hipStream_t st);
+                      hipStream_t st, const uint32_t* roff = nullptr);
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
                           int D, hipStream_t st);

@@ -15,7 +15,7 @@ namespace ss {
 
 static constexpr int kXMaxRanks = 16;
 static constexpr int kXMaxCh = 16;
-static constexpr int kXMaxParts = 3;
+static constexpr int kXMaxParts = 4;
 static constexpr long long kXFlagBytes = (long long)kXMaxCh * kXMaxRanks * 128;
 static constexpr int kXPutThreads = 256;
 

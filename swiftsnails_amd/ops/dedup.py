@@ -90,6 +90,10 @@ class Deduper:
         # (``usingle``, compact unique ids) — lets the LR reduce store instead
         # of accumulate with LDS atomics.  Allocated by track_singletons().
         self.usingle = None
+        # bucket mode, N>1 xGMI engines: each bucket's unique keys grouped by
+        # the server's sub-bucket (msub > 1), with the offsets in ``usub``
+        # ([P][msub], sent with the keys: the server reads its exact ranges)
+        self.msub, self.usub = 1, None
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -162,7 +166,8 @@ class Deduper:
                             self.dbg.data_ptr() if self.dbg is not None else 0,
                             self.rec.data_ptr(),
                             self.usingle.data_ptr() if self.usingle is not None else 0,
-                            self.ndest, self.lay_n or 0)
+                            self.ndest, self.lay_n or 0, self.msub,
+                            self.usub.data_ptr() if self.usub is not None else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self, self._lay(n))
         # the scratch is all-EMPTY between calls: the finish kernel resets the
@@ -193,6 +198,26 @@ class Deduper:
         if P != Pd * self.nranks:
             raise RuntimeError(f"run_tables: {P} buckets, expected {Pd} x {self.nranks}")
         return self.scratch[o_ub:o_ub + P], self.scratch[o_un:o_un + P]
+
+    def split_for_servers(self, m: int) -> None:
+        """Group each bucket's unique keys by the servers' sub-bucket (one
+        of ``m``, server.hip) and record the groups' offsets (bucket mode,
+        N>1 engines with a fixed ``lay_n``)."""
+        if m <= 1:
+            self.msub, self.usub = 1, None
+            return
+        if self.mode != "bucket" or not self.lay_n:
+            raise RuntimeError("split_for_servers needs mode='bucket' and lay_n")
+        P = self.h.bd_buckets(self.lay_n, self.nranks, self.ndest)
+        self.msub = int(m)
+        self.usub = torch.zeros(P * self.msub, dtype=torch.int32, device=self.device)
+
+    def sub_table(self, Pd: int) -> torch.Tensor:
+        """int32 [nranks * Pd * msub]: destination d's sub-bucket offsets at
+        [d*Pd*msub, (d+1)*Pd*msub) (after split_for_servers)."""
+        if self.usub is None or self.usub.numel() != self.nranks * Pd * self.msub:
+            raise RuntimeError("sub_table: split_for_servers(m) with this layout first")
+        return self.usub
 
     def track_singletons(self) -> None:
         """Have the dedup flag the unique keys that occur once (bucket mode)."""

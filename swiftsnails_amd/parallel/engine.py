@@ -236,6 +236,11 @@ class PSEngine(HostRounds):
         self.Pd = h.bd_buckets(cap, N, self.dedupers[0].ndest) // N
         self.sub = h.srv_sub_buckets(N)
         self.Ps = self.Pd * self.sub
+        # sub > 1: every source groups its runs by the servers' sub-bucket
+        # and sends the offsets with them (the server reads exact ranges)
+        for dd in self.dedupers:
+            dd.split_for_servers(self.sub)
+        Psub = self.Pd * self.sub if self.sub > 1 else 0
         # every rank's max_keys must agree (it fixes Pd)
         mk = torch.tensor([cap, -cap], dtype=torch.int64, device=dev)
         self._agree(mk)
@@ -248,11 +253,13 @@ class PSEngine(HostRounds):
             # the receive buffers are the arena's mailboxes: keys + the bucket
             # runs (bases, sizes) per source, rows back, gradients
             Pd, xg = self.Pd, self.xg
-            xg.setup({"keys": (self.depth, [cap * 8, Pd * 4, Pd * 4]),
+            xg.setup({"keys": (self.depth, [cap * 8, Pd * 4, Pd * 4] + ([Psub * 4] if Psub else [])),
                       "vals": (self.depth, [cap * 4 * d]), "grads": (self.depth, [cap * 4 * d])})
             self.rkeys = [xg.region("keys", 0, q, torch.int64) for q in range(self.depth)]
             self.rmeta = [(xg.region("keys", 1, q, torch.int32),
                            xg.region("keys", 2, q, torch.int32)) for q in range(self.depth)]
+            self.rsub = [xg.region("keys", 3, q, torch.int32) if Psub else None
+                         for q in range(self.depth)]
             self.uvals = [xg.region("vals", 0, q, torch.float32, d) for q in range(self.depth)]
             self.rgrads = [xg.region("grads", 0, q, torch.float32, d) for q in range(self.depth)]
         else:
@@ -260,6 +267,8 @@ class PSEngine(HostRounds):
             meta = [torch.zeros(2 * N * self.Pd, dtype=torch.int32, device=dev)
                     for _ in range(self.depth)]
             self.rmeta = [(m[:N * self.Pd], m[N * self.Pd:]) for m in meta]
+            self.rsub = [torch.zeros(N * Psub, dtype=torch.int32, device=dev) if Psub else None
+                         for _ in range(self.depth)]
             self.rgrads = [torch.empty((rows, d), dtype=torch.float32, device=dev)] * self.depth
         self.srv = None
         if self.table is not None:
@@ -272,8 +281,8 @@ class PSEngine(HostRounds):
             D = self.depth
             self.native.set_xgmi(self.xg.arena, [self.xg.channel(c) for c in ("keys", "vals",
                                                                             "grads")],
-                                 [sum((list(self.xg.layout("keys", p, q)) for p in range(3)), [])
-                                  for q in range(D)],
+                                 [sum((list(self.xg.layout("keys", p, q))
+                                       for p in range(4 if Psub else 3)), []) for q in range(D)],
                                  [list(self.xg.layout("vals", 0, q)) for q in range(D)],
                                  [list(self.xg.layout("grads", 0, q)) for q in range(D)],
                                  N, self.rank, self.Pd, self.sub, cap, d, self.xg.bpp,
@@ -360,8 +369,9 @@ class PSEngine(HostRounds):
             counts = None
             if self.xg:
                 ub, un = dd.owner.run_tables(self.Pd)
+                us = dd.owner.sub_table(self.Pd).data_ptr() if dd.owner.msub > 1 else 0
                 self.native.route_end(slot, tag, rs.cuda_stream, dd.ukeys.data_ptr(),
-                                      dd.ucount.data_ptr(), ub.data_ptr(), un.data_ptr())
+                                      dd.ucount.data_ptr(), ub.data_ptr(), un.data_ptr(), us)
             else:
                 if self.dist:
                     counts = self._route_counts(dd, slot, rs)

@@ -42,6 +42,10 @@ class HostRounds:
         fixed = [Pd] * N
         self.ct.alltoallv(ub, fixed, dsp, mb, fixed, dsp, 1)
         self.ct.alltoallv(un, fixed, dsp, mn, fixed, dsp, 1)
+        if self.rsub[slot] is not None:  # sub-bucket offsets of the runs
+            m = self.Pd * self.sub
+            fm, dm = [m] * N, [r * m for r in range(N)]
+            self.ct.alltoallv(dd.owner.sub_table(Pd), fm, dm, self.rsub[slot], fm, dm, 1)
         return counts
 
     # ------------------------------------------------------------ stage 2
@@ -58,7 +62,8 @@ class HostRounds:
                     self.max_keys, N, self.Pd, self.sub, self.rank, S.cnt.data_ptr(),
                     S.bstart.data_ptr(), S.pj.data_ptr(), S.luid.data_ptr(), S.bkeys.data_ptr(),
                     S.ubase.data_ptr(), S.unum.data_ptr(), S.ucount.data_ptr(),
-                    self.srv_err.data_ptr(), st)
+                    self.srv_err.data_ptr(), st,
+                    self.rsub[slot].data_ptr() if self.rsub[slot] is not None else 0)
         # a snapshot is exact when no update lands between this pull and the
         # round's push: the pull and push alternate (no pull-ahead)
         S.snap_valid = S.snap is not None and not self.pull_ahead and tab.snapshot_ok

@@ -1,0 +1,88 @@
+#!/usr/bin/env python3
+"""Kernel profile of an N-rank bench.py job with every rank on ONE GPU.
+
+Spawns N rank processes (child processes, never exec) of ``bench.py`` with
+the torch.distributed env set by hand, all on device 0 (SS_BENCH_DEVICE), each
+wrapped in its own ``rocprofv3 --kernel-trace --stats`` (output
+``<out>/rank<r>/run_kernel_stats.csv``).  The ranks time-share the GPU, so
+kernel durations carry the other ranks' contention; what the profile shows is
+the per-rank kernel work at the N-rank shapes (server buckets for N sources,
+sub-bucket splits, per-destination segments) — the work an N-GPU job's rank
+does — which a 1-rank run through the N>1 path cannot show.
+
+    python tools/prof_world.py --world 8 --out gpurun_out/profw8 -- --steps 10 --warmup 3 \
+        --transport xgmi --batch 131072
+"""
+from __future__ import annotations
+
+import argparse
+import os
+import socket
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=8)
+    ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "profw"))
+    ap.add_argument("--timeout", type=float, default=400.0)
+    ap.add_argument("--no-prof", action="store_true", help="run the ranks without rocprofv3")
+    ap.add_argument("bench_args", nargs=argparse.REMAINDER)
+    a = ap.parse_args()
+    if not 1 <= a.world <= 12:
+        raise SystemExit("prof_world: 1..12 ranks on one GPU")
+    args = [x for x in a.bench_args if x != "--"]
+    port = free_port()
+    procs = []
+    for r in range(a.world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.world),
+                   LOCAL_WORLD_SIZE=str(a.world), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port), SS_BENCH_DEVICE="0", TMPDIR="/tmp")
+        bench = ["python3", os.path.join(ROOT, "bench.py"), "--gpus", str(a.world)] + args
+        if a.no_prof:
+            cmd = bench
+        else:
+            d = os.path.join(a.out, f"rank{r}")
+            os.makedirs(d, exist_ok=True)
+            cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", d,
+                   "-o", "run", "--"] + bench
+        os.makedirs(a.out, exist_ok=True)
+        log = open(os.path.join(a.out, f"rank{r}.log"), "w")
+        procs.append((subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT,
+                                       cwd=ROOT, start_new_session=True), log))
+    t0, rc = time.time(), 0
+    for p, log in procs:
+        left = max(1.0, a.timeout - (time.time() - t0))
+        try:
+            c = p.wait(timeout=left)
+        except subprocess.TimeoutExpired:
+            c = 124
+            for q, _ in procs:  # the job is wedged: end every rank's process group
+                try:
+                    os.killpg(q.pid, 9)
+                except ProcessLookupError:
+                    pass
+        log.close()
+        rc = rc or c
+    with open(os.path.join(a.out, "rank0.log")) as f:
+        for line in f:
+            if line.startswith("{"):
+                print(line.strip())
+    print(f"prof_world: world {a.world} rc={rc} ({time.time() - t0:.0f} s)")
+    return rc
+
+
+if __name__ == "__main__":
+    sys.exit(main())
