@@ -124,6 +124,7 @@ def test_engine_gpu_rccl_same_device():
     (3, [0, 1, 2], [0, 1, 2], "sgd"),
     (2, [1], [0], "adagrad"),
     (4, [0, 1], [2, 3], "ftrl"),
+    (8, list(range(8)), list(range(8)), "adagrad"),  # 4 server sub-buckets per bucket
 ])
 def test_engine_gpu_xgmi_peers(world, servers, workers, opt):
     """The xGMI mailbox data plane with real peers: N processes on cuda:0
