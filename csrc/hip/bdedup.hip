@@ -358,13 +358,17 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   __shared__ int bad;
   __shared__ unsigned int hsub[kBdMaxSub];  // msub > 1: keys per server sub-bucket, then offsets
   const int t = threadIdx.x, b = blockIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+  // the hash table sized to the bucket (load <= 1/2 of its occurrences, 64
+  // slots at least): small buckets (word2vec's ~200 occurrences, split-role
+  // layouts) do not pay for initialising and compacting all 4096 slots
+  const uint32_t ts = lds_table_size(p1 - p0, kBdTS);
   if (t == 0) bad = 0;
   if (t < kBdMaxSub) hsub[t] = 0u;
-  for (int s = t; s < kBdTS; s += kBdDT) {
+  for (uint32_t s = t; s < ts; s += kBdDT) {
     tab[s] = kEmptyKey;
     dupf[s] = 0;
   }
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   // the first kBdRegs occurrences of each thread keep their slot in
   // registers; a hot bucket's excess parks it in luid[] (rewritten below)
   uint32_t slot[kBdRegs];
@@ -386,8 +390,8 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   // dupf[s]: the key of slot s occurs more than once in the bucket (set by
   // every occurrence but the inserting one: a plain, idempotent LDS store)
   auto insert = [&](uint64_t key) -> uint32_t {
-    uint32_t s = (uint32_t)dedup_hash(key) & (kBdTS - 1);
-    for (int k = 0; k < kBdTS; ++k) {
+    uint32_t s = (uint32_t)dedup_hash(key) & (ts - 1);
+    for (uint32_t k = 0; k < ts; ++k) {
       const unsigned long long v = tab[s];
       if (v == key) {
         dupf[s] = 1;
@@ -401,7 +405,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
           return s;
         }
       }
-      s = (s + 1) & (kBdTS - 1);
+      s = (s + 1) & (ts - 1);
     }
     bad = 1;
     return kBdInvalid;
@@ -425,19 +429,25 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   }
   __syncthreads();
   BD_STAMP(1)
-  // compaction in slot order: thread t owns slots [kPerT*t, kPerT*(t+1));
+  // compaction in slot order: thread t owns slots [per*t, per*(t+1));
   // msub > 1 (N>1 xGMI rounds): grouped by the server's sub-bucket first, so
   // a server sub-bucket's keys from this bucket are one contiguous range
   // (offsets in usub) and the server reads exactly its keys — no re-read of
   // the whole run per sub-bucket, no hashing pass to count them
   constexpr int kPerT = kBdTS / kBdDT;
+  const uint32_t per = ts >= (uint32_t)kBdDT ? ts / kBdDT : 1u;
+  // slot k of this thread's run (kEmptyKey past the table)
+  auto own = [&](int k) -> unsigned long long {
+    const uint32_t s = (uint32_t)t * per + (uint32_t)k;
+    return (uint32_t)k < per && s < ts ? tab[s] : kEmptyKey;
+  };
   unsigned int o = 0;
   uint8_t sb[kPerT];
   uint16_t rk[kPerT];
   if (msub > 1) {
 #pragma unroll
     for (int k = 0; k < kPerT; ++k) {
-      const unsigned long long v = tab[t * kPerT + k];
+      const unsigned long long v = own(k);
       sb[k] = v != kEmptyKey ? (uint8_t)srv_sub(v, msub) : 0;
       rk[k] = v != kEmptyKey ? (uint16_t)atomicAdd(&hsub[sb[k]], 1u) : 0;
     }
@@ -454,7 +464,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   } else {
     unsigned int occ = 0;
 #pragma unroll
-    for (int k = 0; k < kPerT; ++k) occ += tab[t * kPerT + k] != kEmptyKey;
+    for (int k = 0; k < kPerT; ++k) occ += own(k) != kEmptyKey;
     o = block_excl_scan<kBdDT / 64>(occ, wsum, &tot);
   }
   // the bucket's unique ids: one device-scope add per bucket reserves them in
@@ -474,8 +484,8 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   const unsigned long long ub = sbase;
 #pragma unroll
   for (int k = 0; k < kPerT; ++k) {
-    const int s = t * kPerT + k;
-    const unsigned long long v = tab[s];
+    const uint32_t s = (uint32_t)t * per + (uint32_t)k;
+    const unsigned long long v = own(k);
     if (v != kEmptyKey) {
       const unsigned int q = msub > 1 ? hsub[sb[k]] + rk[k] : o++;
       lid[s] = q;

@@ -161,25 +161,28 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   const int t = threadIdx.x, lane = t & 63;
   const int b = blockIdx.x, k = b / R.m;
   const uint32_t sub = (uint32_t)(b % R.m);
-  for (int s = t; s < kSrvTS; s += kSrvDT) tab[s] = kEmptyKey;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+  // the table sized to the bucket's received keys (load <= 1/2): small
+  // buckets (word2vec) skip initialising and compacting 4096 slots
+  const uint32_t ts = lds_table_size(p1 - p0, kSrvTS);
+  for (uint32_t s = t; s < ts; s += kSrvDT) tab[s] = kEmptyKey;
   if (t == 0) {
     cur = 0u;
     bad = 0;
   }
   __syncthreads();
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
   auto insert = [&](uint64_t key) -> uint32_t {
     // slot from the high word's low bits: the sender's bucket fixed the high
     // word's top bits, the sub-bucket the low word's
-    uint32_t s = (uint32_t)(dedup_hash(key) >> 32) & (kSrvTS - 1);
-    for (int i = 0; i < kSrvTS; ++i) {
+    uint32_t s = (uint32_t)(dedup_hash(key) >> 32) & (ts - 1);
+    for (uint32_t i = 0; i < ts; ++i) {
       const unsigned long long v = tab[s];
       if (v == key) return s;
       if (v == kEmptyKey) {
         const unsigned long long prev = atomicCAS(&tab[s], kEmptyKey, (unsigned long long)key);
         if (prev == kEmptyKey || prev == key) return s;
       }
-      s = (s + 1) & (kSrvTS - 1);
+      s = (s + 1) & (ts - 1);
     }
     bad = 1;
     return kSrvInv;
@@ -211,11 +214,16 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
     }
   }
   __syncthreads();
-  // compaction in slot order: thread t owns slots [kPerT*t, kPerT*(t+1))
+  // compaction in slot order: thread t owns slots [per*t, per*(t+1))
   constexpr int kPerT = kSrvTS / kSrvDT;
+  const uint32_t per = ts >= (uint32_t)kSrvDT ? ts / kSrvDT : 1u;
+  auto own = [&](int i) -> unsigned long long {
+    const uint32_t s = (uint32_t)t * per + (uint32_t)i;
+    return (uint32_t)i < per && s < ts ? tab[s] : kEmptyKey;
+  };
   unsigned int occ = 0;
 #pragma unroll
-  for (int i = 0; i < kPerT; ++i) occ += tab[t * kPerT + i] != kEmptyKey;
+  for (int i = 0; i < kPerT; ++i) occ += own(i) != kEmptyKey;
   unsigned int o = block_excl_scan<kSrvDT / 64>(occ, wsum, &tot);
   __shared__ unsigned long long sbase;
   if (t == 0) {
@@ -227,8 +235,8 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   __syncthreads();
 #pragma unroll
   for (int i = 0; i < kPerT; ++i) {
-    const int s = t * kPerT + i;
-    const unsigned long long v = tab[s];
+    const uint32_t s = (uint32_t)t * per + (uint32_t)i;
+    const unsigned long long v = own(i);
     if (v != kEmptyKey) {
       lid[s] = o;
       bkeys[p0 + o] = v;  // staged in the bucket's own range (k_pull_unique_bk reads it)
@@ -239,34 +247,50 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   const uint32_t n = min(cur, (uint32_t)kSrvOcc);
   for (uint32_t q = t; q < n && p0 + q < p1; q += kSrvDT) {
     const uint32_t sl = park[q] == 0xFFFFu ? kSrvInv : park[q];
-    luid[p0 + q] = sl == kSrvInv || sl >= (uint32_t)kSrvTS ? kSrvInv : lid[sl];
+    luid[p0 + q] = sl == kSrvInv || sl >= ts ? kSrvInv : lid[sl];
   }
 }
 
-// response rows of width D > 1: out[pj[p]] = rows[ubase[b] + luid[p]]
+// lanes per row for rows of n 16-byte chunks: the next power of two, <= 64
+__device__ __forceinline__ int srv_group(int n) {
+  return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : n <= 8 ? 8 : n <= 16 ? 16 : n <= 32 ? 32 : 64;
+}
+
+// response rows of width D > 1: out[pj[p]] = rows[ubase[b] + luid[p]].  A
+// group of lanes per received row moving it as 16-byte chunks (D % 4 == 0;
+// word2vec's 512-byte rows: one 32-lane group each), 4-byte words otherwise
 __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restrict__ bstart,
                                                        const uint32_t* __restrict__ ubase,
                                                        const uint32_t* __restrict__ pj,
                                                        const uint32_t* __restrict__ luid,
                                                        const float* __restrict__ rows,
                                                        float* __restrict__ out, int D) {
-  const int b = blockIdx.x;
+  const int b = blockIdx.x, t = threadIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], base = ubase[b];
-  const long long tot = (long long)(p1 - p0) * D;
-  for (long long e = threadIdx.x; e < tot; e += 256) {
-    const uint32_t p = p0 + (uint32_t)(e / D);
-    const int c = (int)(e % D);
+  const bool vec = (D & 3) == 0;
+  const int W = vec ? D >> 2 : D;  // chunks per row
+  const int G = srv_group(W), lg = t % G, ng = 256 / G;
+  for (uint32_t p = p0 + t / G; p < p1; p += ng) {
     const uint32_t l = luid[p];
-    out[(long long)pj[p] * D + c] = l == kSrvInv ? 0.f : rows[((long long)base + l) * D + c];
+    const long long o = (long long)pj[p] * W, r = ((long long)base + l) * W;
+    if (vec) {
+      float4* dst = reinterpret_cast<float4*>(out) + o;
+      const float4* src = reinterpret_cast<const float4*>(rows) + r;
+      for (int c = lg; c < W; c += G) dst[c] = l == kSrvInv ? make_float4(0.f, 0.f, 0.f, 0.f) : src[c];
+    } else {
+      for (int c = lg; c < W; c += G) out[o + c] = l == kSrvInv ? 0.f : rows[r + c];
+    }
   }
 }
 
 // gradient merge of rows of width D: grads received at positions pj[p] are
 // summed per distinct key into merged[ubase[b] + l].  Per bucket the
-// positions are counting-sorted by local id in LDS, then each wave sums its
-// keys' rows (lanes over the row; no atomics).  `slots`: the merged row goes
-// straight into the optimizer update of the key's table row (lane c updates
-// coordinate c and its state) — no merged-row round trip, no apply launch
+// positions are counting-sorted by local id in LDS (tables sized by the
+// bucket's distinct keys, not the 4096-slot maximum: word2vec buckets hold
+// ~30), then a lane group per key sums its rows (16-byte chunks when D % 4
+// == 0; no atomics).  `slots`: the merged row goes straight into the
+// optimizer update of the key's table row (each lane updates its
+// coordinates and their state) — no merged-row round trip, no apply launch
 __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restrict__ bstart,
                                                         const uint32_t* __restrict__ ubase,
                                                         const uint32_t* __restrict__ unum,
@@ -278,70 +302,95 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
                                                         const long long* __restrict__ slots,
                                                         OptParams op) {
   __shared__ unsigned int off[kSrvTS + 1];
+  __shared__ unsigned int cur[kSrvTS];
   __shared__ unsigned short ord[kSrvOcc];
   __shared__ unsigned int wsum[16];
   const int b = blockIdx.x, t = threadIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = min(unum[b], (uint32_t)kSrvTS);
   const uint32_t base = ubase[b];
   const uint32_t np = min(p1 - p0, (uint32_t)kSrvOcc);
-  for (uint32_t l = t; l <= (uint32_t)kSrvTS; l += 512) off[l] = 0u;
+  if (nu == 0) return;  // workgroup-uniform
+  for (uint32_t l = t; l <= nu; l += 512) off[l] = 0u;
   __syncthreads();
   for (uint32_t q = t; q < np; q += 512) {
     const uint32_t l = luid[p0 + q];
     if (l < nu) atomicAdd(&off[l + 1], 1u);
   }
   __syncthreads();
-  // inclusive scan of off[1..nu] (kSrvTS / 512 = 8 entries per thread)
-  constexpr int kPer = kSrvTS / 512;
-  unsigned int v[kPer], s = 0;
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    v[i] = off[1 + t * kPer + i];
-    s += v[i];
+  // inclusive scan of off[1..nu]: thread t owns `per` consecutive entries
+  const uint32_t per = (nu + 511) / 512;  // <= kSrvTS / 512
+  unsigned int sum = 0;
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t l = 1 + t * per + i;
+    if (l <= nu) sum += off[l];
   }
-  unsigned int e = block_excl_scan<8>(s, wsum, nullptr);
-#pragma unroll
-  for (int i = 0; i < kPer; ++i) {
-    e += v[i];
-    off[1 + t * kPer + i] = e;
+  unsigned int e = block_excl_scan<8>(sum, wsum, nullptr);
+  for (uint32_t i = 0; i < per; ++i) {
+    const uint32_t l = 1 + t * per + i;
+    if (l <= nu) {
+      e += off[l];
+      off[l] = e;
+    }
   }
   __syncthreads();
   // placement: a second counter pass (cursor = off[l], advanced atomically)
-  __shared__ unsigned int cur[kSrvTS];
-  for (uint32_t l = t; l < (uint32_t)kSrvTS; l += 512) cur[l] = off[l];
+  for (uint32_t l = t; l < nu; l += 512) cur[l] = off[l];
   __syncthreads();
   for (uint32_t q = t; q < np; q += 512) {
     const uint32_t l = luid[p0 + q];
     if (l < nu) ord[atomicAdd(&cur[l], 1u)] = (unsigned short)q;
   }
   __syncthreads();
-  // a group of G lanes per key, G the row width rounded up to a power of two
-  // (one key per wave left 55 of 64 lanes idle on FM's 9-wide rows)
-  const int G = D <= 4 ? 4 : D <= 8 ? 8 : D <= 16 ? 16 : D <= 32 ? 32 : 64;
-  const int lane = t & 63, lg = lane % G;
-  const uint32_t per = 512 / G;  // keys in flight per workgroup
   const int ns = opt_state_per_coord(op.kind);
-  for (uint32_t l = (uint32_t)(t / G); l < nu; l += per) {
+  const bool vec = (D & 3) == 0;
+  const int V = vec ? 4 : 1;          // coordinates per lane and chunk
+  const int W = D / V;                // chunks per row
+  const int G = srv_group(W), lg = t % G;
+  const uint32_t kpp = 512 / G;       // keys in flight per workgroup
+  for (uint32_t l = (uint32_t)(t / G); l < nu; l += kpp) {
     const uint32_t a = off[l], z = off[l + 1];
     const long long slot = slots ? slots[(long long)base + l] : -1;
-    for (int c0 = 0; c0 < D; c0 += G) {
-      const int c = c0 + lg;
-      if (c >= D) continue;
+    const bool upd = slots && slot >= 0;
+    for (int c0 = lg; c0 < W; c0 += G) {
       // fused update: the row (and state) loads go out before the gradient
       // sum, their latency overlaps the gathers instead of following them
-      const bool upd = slots && slot >= 0;
-      float wv = upd ? row_ld(tab, slot, c) : 0.f;
-      float s1 = upd && ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
-      float s2 = upd && ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
-      float acc = 0.f;
-      for (uint32_t i = a; i < z; ++i) acc += grads[(long long)pj[p0 + ord[i]] * D + c];
+      float wv[4], s1[4], s2[4], acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 * V + i;
+        const bool on = upd && i < V;
+        wv[i] = on ? row_ld(tab, slot, c) : 0.f;
+        s1[i] = on && ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
+        s2[i] = on && ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
+      }
+      for (uint32_t i = a; i < z; ++i) {
+        const long long r = (long long)pj[p0 + ord[i]] * W + c0;
+        if (vec) {
+          const float4 g = reinterpret_cast<const float4*>(grads)[r];
+          acc[0] += g.x;
+          acc[1] += g.y;
+          acc[2] += g.z;
+          acc[3] += g.w;
+        } else {
+          acc[0] += grads[r];
+        }
+      }
       if (!slots) {
-        merged[((long long)base + l) * D + c] = acc;
+        const long long o = ((long long)base + l) * W + c0;
+        if (vec)
+          reinterpret_cast<float4*>(merged)[o] = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        else
+          merged[o] = acc[0];
       } else if (upd) {
-        opt_update(op, wv, s1, s2, acc);
-        row_st(tab, slot, c, wv, true);
-        if (ns > 0) row_st(tab, slot, D + c, s1, true);
-        if (ns > 1) row_st(tab, slot, 2 * D + c, s2, true);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          if (i >= V) break;
+          const int c = c0 * V + i;
+          opt_update(op, wv[i], s1[i], s2[i], acc[i]);
+          row_st(tab, slot, c, wv[i], true);
+          if (ns > 0) row_st(tab, slot, D + c, s1[i], true);
+          if (ns > 1) row_st(tab, slot, 2 * D + c, s2[i], true);
+        }
       }
     }
   }

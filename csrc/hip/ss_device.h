@@ -139,6 +139,14 @@ __device__ __forceinline__ long long seg_pos(const SegList& sl, long long g, int
   return sl.off[s] + (g - sl.prefix[s]);
 }
 
+// slots of a per-workgroup LDS hash table for up to n distinct keys: the
+// power of two >= 2n (load <= 1/2), at least 64, at most cap
+__device__ __forceinline__ uint32_t lds_table_size(uint32_t n, uint32_t cap) {
+  uint32_t ts = 64;
+  while (ts < 2 * n && ts < cap) ts <<= 1;
+  return ts;
+}
+
 // N>1 server sub-bucket of a key (server.hip): the top bits of dedup_hash's
 // low word.  The sender's bucket took the high word's top bits and its LDS
 // slot the low word's low bits, so the three are independent.
