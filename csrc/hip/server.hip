@@ -18,11 +18,13 @@
 // and server bucket k is the union of N runs.  N runs of ~1024 unique keys do
 // not fit one 4096-slot LDS table at N=8, so bucket k is further split into m
 // sub-buckets by an independent hash (the low word of dedup_hash; the sender
-// used the high word): server bucket b = k*m + t.
+// used the high word): server bucket b = k*m + t.  The sender grouped each
+// run by sub-bucket and sent the groups' offsets (bdedup.hip msub), so
+// sub-bucket t's keys from source s are one exact range of its run.
 //
-//   1 k_srv_count  per k: received keys per sub-bucket (m == 1: the run sums);
-//                  the last workgroup scans them -> bstart (server
-//                  "occurrence" ranges)
+//   1 k_srv_count  per b: received keys = the sum of its ranges' lengths (no
+//                  key is read); the last workgroup scans them -> bstart
+//                  (server "occurrence" ranges)
 //   3 k_srv_dedup  per b: LDS hash dedup of the sub-bucket's received keys;
 //                  writes the received position of each (pj), its local id
 //                  (luid), the unique keys staged at bstart[b] (bkeys, what
@@ -42,6 +44,8 @@ namespace ss {
 static constexpr int kSrvTS = 4096;     // LDS hash slots per server bucket
 static constexpr int kSrvOcc = 8192;    // received keys per server bucket (LDS parking)
 static constexpr int kSrvDT = 512;      // dedup workgroup
+static constexpr int kSrvRegs = 8;      // received keys per dedup thread in flight
+static constexpr int kSrvMaxSrc = 64;   // sources of a round
 static constexpr uint32_t kSrvInv = 0xFFFFFFFFu;
 
 struct SrvRuns {
@@ -50,8 +54,8 @@ struct SrvRuns {
   const uint32_t* rnum;    // [nsrc][Pd] the sources' bucket sizes
   long long cap;           // per-source segment capacity (== every source's ucap)
   int nsrc, Pd, m, me;
-  // [nsrc][Pd][m] or null: where sub-bucket t starts in source s's run k (the
-  // sender grouped each run by sub-bucket, bdedup.hip msub)
+  // [nsrc][Pd][m] (m > 1): where sub-bucket t starts in source s's run k
+  // (the sender grouped each run by sub-bucket, bdedup.hip msub)
   const uint32_t* roff;
   __device__ __forceinline__ long long run_start(int s, int k) const {
     return (long long)s * cap + ((long long)rbase[(long long)s * Pd + k] - (long long)me * cap);
@@ -59,12 +63,12 @@ struct SrvRuns {
   __device__ __forceinline__ uint32_t run_len(int s, int k) const {
     return rnum[(long long)s * Pd + k];
   }
-  // the part of run (s, k) a server bucket k*m + t reads: the sub-bucket's
-  // range when the sender grouped it, else the whole run (filtered by hash)
+  // the part of run (s, k) server bucket k*m + t reads: the whole run (m ==
+  // 1) or the sub-bucket's range (the sender grouped the run)
   __device__ __forceinline__ void part(int s, int k, int t, long long* a, uint32_t* len) const {
     *a = run_start(s, k);
     const uint32_t n = run_len(s, k);
-    if (m == 1 || !roff) {
+    if (m == 1) {
       *len = n;
       return;
     }
@@ -86,38 +90,21 @@ __global__ __launch_bounds__(256) void k_srv_count(SrvRuns R, uint32_t* __restri
                                                    uint32_t* __restrict__ bstart,
                                                    unsigned long long* __restrict__ ucount,
                                                    unsigned int* __restrict__ ctr) {
-  __shared__ unsigned int h[kSrvCntK * 64];
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
   __shared__ bool last;
   const int t = threadIdx.x;
   const int k0 = blockIdx.x * kSrvCntK, k1 = min(R.Pd, k0 + kSrvCntK);
-  if (R.m == 1 || R.roff) {
-    // the run (or sub-range) lengths are the counts: one thread per bucket
-    for (int b = k0 * R.m + t; b < k1 * R.m; b += 256) {
-      unsigned int c = 0;
-      for (int s = 0; s < R.nsrc; ++s) {
-        long long a;
-        uint32_t len;
-        R.part(s, b / R.m, b % R.m, &a, &len);
-        c += len;
-      }
-      __hip_atomic_store(&cnt[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the run (or sub-range) lengths are the counts: one thread per bucket
+  for (int b = k0 * R.m + t; b < k1 * R.m; b += 256) {
+    unsigned int c = 0;
+    for (int s = 0; s < R.nsrc; ++s) {
+      long long a;
+      uint32_t len;
+      R.part(s, b / R.m, b % R.m, &a, &len);
+      c += len;
     }
-  } else {
-    for (int i = t; i < kSrvCntK * R.m; i += 256) h[i] = 0u;
-    __syncthreads();
-    for (int k = k0; k < k1; ++k)
-      for (int s = 0; s < R.nsrc; ++s) {
-        const long long a = R.run_start(s, k);
-        const uint32_t len = R.run_len(s, k);
-        for (uint32_t i = t; i < len; i += 256)
-          atomicAdd(&h[(k - k0) * R.m + srv_sub(R.rkeys[a + i], R.m)], 1u);
-      }
-    __syncthreads();
-    for (int i = t; i < (k1 - k0) * R.m; i += 256)
-      __hip_atomic_store(&cnt[(long long)k0 * R.m + i], h[i], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&cnt[b], c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -156,9 +143,11 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   __shared__ unsigned int lid[kSrvTS];
   __shared__ unsigned short park[kSrvOcc];
   __shared__ unsigned int wsum[16];
-  __shared__ unsigned int tot, cur;
+  __shared__ long long sa[kSrvMaxSrc];      // where each source's part starts
+  __shared__ unsigned int so[kSrvMaxSrc + 1];  // its first flat index
+  __shared__ unsigned int tot;
   __shared__ int bad;
-  const int t = threadIdx.x, lane = t & 63;
+  const int t = threadIdx.x;
   const int b = blockIdx.x, k = b / R.m;
   const uint32_t sub = (uint32_t)(b % R.m);
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
@@ -166,9 +155,18 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   // buckets (word2vec) skip initialising and compacting 4096 slots
   const uint32_t ts = lds_table_size(p1 - p0, kSrvTS);
   for (uint32_t s = t; s < ts; s += kSrvDT) tab[s] = kEmptyKey;
+  if (t < R.nsrc) {  // every source's part, looked up in parallel
+    long long a;
+    uint32_t len;
+    R.part(t, k, (int)sub, &a, &len);
+    sa[t] = a;
+    so[t + 1] = len;
+  }
+  __syncthreads();
   if (t == 0) {
-    cur = 0u;
-    bad = 0;
+    so[0] = 0u;
+    for (int s = 0; s < R.nsrc; ++s) so[s + 1] += so[s];
+    bad = so[R.nsrc] != p1 - p0 || p1 - p0 > (uint32_t)kSrvOcc;
   }
   __syncthreads();
   auto insert = [&](uint64_t key) -> uint32_t {
@@ -187,30 +185,28 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
     bad = 1;
     return kSrvInv;
   };
-  // every source's run of bucket k; the keys of sub-bucket `sub` get a
-  // position in [p0, p1) (wave-aggregated reservation) and an LDS slot
-  const bool exact = R.m == 1 || R.roff;  // every key read is this sub-bucket's
-  for (int s = 0; s < R.nsrc; ++s) {
-    long long a;
-    uint32_t len;
-    R.part(s, k, (int)sub, &a, &len);
-    for (uint32_t i0 = 0; i0 < len; i0 += kSrvDT) {
-      const uint32_t i = i0 + t;
-      const uint64_t key = i < len ? R.rkeys[a + i] : kEmptyKey;
-      const bool mine = key != kEmptyKey && (exact || srv_sub(key, R.m) == sub);
-      const unsigned long long mask = __ballot(mine);
-      unsigned int wb = 0;
-      if (lane == 0 && mask) wb = atomicAdd(&cur, (unsigned int)__popcll(mask));
-      wb = __shfl(wb, 0, 64);
-      if (mine) {
-        const uint32_t q = wb + (uint32_t)__popcll(mask & ((1ull << lane) - 1));
-        if (q < kSrvOcc && p0 + q < p1) {
-          pj[p0 + q] = (uint32_t)(a + i);
-          park[q] = (unsigned short)insert(key);
-        } else {
-          bad = 1;
-        }
+  // the sources' parts as one flat list [0, n): position p0 + f holds flat
+  // key f.  kSrvRegs keys per thread are loaded before any is inserted (one
+  // load latency per round instead of one per source)
+  const uint32_t n = min(min(so[R.nsrc], p1 - p0), (uint32_t)kSrvOcc);
+  for (uint32_t f0 = 0; f0 < n; f0 += kSrvDT * kSrvRegs) {
+    uint64_t kk[kSrvRegs];
+#pragma unroll
+    for (int r = 0; r < kSrvRegs; ++r) {
+      const uint32_t f = f0 + (uint32_t)(r * kSrvDT + t);
+      kk[r] = kEmptyKey;
+      if (f < n) {
+        int s = 0;
+        while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
+        const long long pos = sa[s] + (f - so[s]);
+        kk[r] = R.rkeys[pos];
+        pj[p0 + f] = (uint32_t)pos;
       }
+    }
+#pragma unroll
+    for (int r = 0; r < kSrvRegs; ++r) {
+      const uint32_t f = f0 + (uint32_t)(r * kSrvDT + t);
+      if (f < n) park[f] = (unsigned short)insert(kk[r]);
     }
   }
   __syncthreads();
@@ -244,8 +240,7 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
     }
   }
   __syncthreads();
-  const uint32_t n = min(cur, (uint32_t)kSrvOcc);
-  for (uint32_t q = t; q < n && p0 + q < p1; q += kSrvDT) {
+  for (uint32_t q = t; q < n; q += kSrvDT) {
     const uint32_t sl = park[q] == 0xFFFFu ? kSrvInv : park[q];
     luid[p0 + q] = sl == kSrvInv || sl >= ts ? kSrvInv : lid[sl];
   }
@@ -410,7 +405,8 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
                       uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
                       uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
                       hipStream_t st, const uint32_t* roff) {
-  if (nsrc < 1 || Pd < 1 || m < 1 || m > 64) throw_error("srv_dedup: bad layout");
+  if (nsrc < 1 || nsrc > kSrvMaxSrc || Pd < 1 || m < 1 || m > 64) throw_error("srv_dedup: bad layout");
+  if (m > 1 && !roff) throw_error("srv_dedup: sub-buckets need the senders' offsets (msub)");
   SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me, roff};
   const int P = Pd * m;
   // cnt has P + 1 words: the last is the count kernel's arrival counter

@@ -751,19 +751,17 @@ def test_stream_helpers_match_torch(dev):
     assert float(x.sum().item()) == 2000.0
 
 
-@pytest.mark.parametrize("dim,fused,split", [(1, True, False), (3, False, False),
-                                             (64, False, False), (9, True, False),
-                                             (128, True, False), (1, True, True),
-                                             (9, True, True)])
-def test_server_merge_matches_reference(dev, dim, fused, split):
+@pytest.mark.parametrize("dim,fused", [(1, True), (3, False), (64, False), (9, True),
+                                       (128, True)])
+def test_server_merge_matches_reference(dev, dim, fused):
     """server.hip on the keys three sources route to one server (real
     bucketed dedups with the common N>1 layout, overlapping key sets): one
     entry per distinct key, response rows per received position, and the
     merged gradient of every distinct key — fused into the AdaGrad update
     (scalar rows: read-modify-write, no snapshot; wider rows: a lane group per
-    key), else a merged row then the apply kernel.  ``split``: the sources
-    group each run by the server's sub-bucket and send the offsets (the
-    xGMI path), so the server reads exact ranges instead of filtering."""
+    key), else a merged row then the apply kernel.  N = 3 splits a server
+    bucket in m = 2: the sources group each run by sub-bucket and send the
+    offsets, the server reads exact ranges."""
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.ops.dedup import Deduper
     from swiftsnails_amd.ops.optim import InitConfig, Optimizer
@@ -781,9 +779,8 @@ def test_server_merge_matches_reference(dev, dim, fused, split):
     Pd = h.bd_buckets(n, N, ds[0].ndest) // N
     m = h.srv_sub_buckets(N)
     assert m > 1
-    if split:
-        for d in ds:
-            d.split_for_servers(m)
+    for d in ds:
+        d.split_for_servers(m)
     roff = torch.zeros(N * Pd * m, dtype=torch.int32, device=dev)
     cap = n
     rkeys = torch.full((N * cap,), -1, dtype=torch.int64, device=dev)
@@ -797,8 +794,7 @@ def test_server_merge_matches_reference(dev, dim, fused, split):
         ub, un = d.run_tables(Pd)
         meta[s * Pd:(s + 1) * Pd] = ub[me * Pd:(me + 1) * Pd]
         meta[N * Pd + s * Pd:N * Pd + (s + 1) * Pd] = un[me * Pd:(me + 1) * Pd]
-        if split:
-            roff[s * Pd * m:(s + 1) * Pd * m] = d.sub_table(Pd)[me * Pd * m:(me + 1) * Pd * m]
+        roff[s * Pd * m:(s + 1) * Pd * m] = d.sub_table(Pd)[me * Pd * m:(me + 1) * Pd * m]
         recv.append((s * cap, c))
     P = Pd * m
     rows = N * cap
@@ -813,7 +809,7 @@ def test_server_merge_matches_reference(dev, dim, fused, split):
     h.srv_dedup(rkeys.data_ptr(), meta.data_ptr(), meta.data_ptr() + 4 * N * Pd, cap, N, Pd, m,
                 me, cnt.data_ptr(), bstart.data_ptr(), pj.data_ptr(), luid.data_ptr(),
                 bkeys.data_ptr(), ubase.data_ptr(), unum.data_ptr(), uc.data_ptr(),
-                err.data_ptr(), st, roff.data_ptr() if split else 0)
+                err.data_ptr(), st, roff.data_ptr())
     pos = np.concatenate([np.arange(a, a + c) for a, c in recv])
     rk = rkeys.cpu().numpy()[pos]
     distinct = np.unique(rk)
