@@ -10,6 +10,7 @@
 #include <vector>
 
 #include "ss_launch.h"
+#include "xdirect.h"
 
 namespace ss {
 
@@ -17,6 +18,10 @@ static constexpr int kXMaxRanks = 16;
 static constexpr int kXMaxCh = 16;
 static constexpr int kXMaxParts = 4;
 static constexpr long long kXFlagBytes = (long long)kXMaxCh * kXMaxRanks * 128;
+static_assert(kXMaxRanks == kXDirectMaxRanks, "one peer table size");
+// local counters: put arrivals [ch][dest], waits [ch], error word(s),
+// direct-put arrivals [ch][dest]
+static constexpr long long kXLocalWords = 3ll * kXMaxCh * kXMaxRanks + 8;
 static constexpr int kXPutThreads = 256;
 
 struct XPart {
@@ -69,10 +74,8 @@ class XgmiArena {
               "xgmi arena (uncached)");
     base_ = static_cast<char*>(p);
     check_hip(hipMemset(base_, 0, (size_t)kXFlagBytes), "xgmi flags");
-    check_hip(hipMalloc(&local_, sizeof(unsigned long long) * (2 * kXMaxCh * kXMaxRanks + 8)),
-              "xgmi counters");
-    check_hip(hipMemset(local_, 0, sizeof(unsigned long long) * (2 * kXMaxCh * kXMaxRanks + 8)),
-              "xgmi counters");
+    check_hip(hipMalloc(&local_, sizeof(unsigned long long) * kXLocalWords), "xgmi counters");
+    check_hip(hipMemset(local_, 0, sizeof(unsigned long long) * kXLocalWords), "xgmi counters");
     peers_.assign(nranks, nullptr);
     peers_[rank] = base_;
   }
@@ -155,6 +158,38 @@ class XgmiArena {
     unsigned long long* arrive = local_ + (long long)ch * kXMaxRanks;
     launch_xput(P, arrive, reinterpret_cast<unsigned int*>(err_ptr()),
                 reinterpret_cast<hipStream_t>(stream));
+  }
+
+  // descriptor of a producer kernel storing its rows straight into the peers'
+  // region (hdr_off, data_off, seg_bytes) of channel ch (xdirect.h): `cnt`
+  // rows per destination (device), each destination's rows written by
+  // `blocks_per_dest` workgroups, row r of destination d at r (ucap rows per
+  // destination in the producer's own layout)
+  XDirect direct(int ch, long long hdr_off, long long data_off, long long seg_bytes,
+                 long long ucap, int row_bytes, uintptr_t cnt, int blocks_per_dest) const {
+    if (ch < 0 || ch >= kXMaxCh) throw_error("xgmi: bad channel");
+    if (blocks_per_dest < 1 || row_bytes < 4 || !cnt) throw_error("xgmi: bad direct put");
+    if (data_off + (long long)nranks_ * seg_bytes > bytes_ || hdr_off + 8ll * nranks_ > bytes_ ||
+        hdr_off < kXFlagBytes || data_off < kXFlagBytes)
+      throw_error("xgmi: direct region outside the arena");
+    XDirect X{};
+    for (int r = 0; r < nranks_; ++r) {
+      if (!peers_[r]) throw_error("xgmi: peer arenas not open");
+      X.peer[r] = peers_[r];
+    }
+    X.data_off = data_off;
+    X.seg_bytes = seg_bytes;
+    X.hdr_off = hdr_off;
+    X.flag_off = ((long long)ch * kXMaxRanks + rank_) * 128;  // xgmi.hip xflag
+    X.ucap = ucap;
+    X.cnt = reinterpret_cast<const unsigned long long*>(cnt);
+    X.arrive = local_ + 2ll * kXMaxCh * kXMaxRanks + 8 + (long long)ch * kXMaxRanks;
+    X.err = reinterpret_cast<unsigned int*>(err_ptr());
+    X.me = rank_;
+    X.nranks = nranks_;
+    X.blocks_per_dest = blocks_per_dest;
+    X.row_bytes = row_bytes;
+    return X;
   }
 
   // fixed: (data_off, seg_bytes, bytes) of the parts zeroed for a missing source
