@@ -636,7 +636,7 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (threadIdx.x == 0) xd_arrive(xd, d);
+    if (threadIdx.x == 0) xd_arrive(xd, d, b - d * xd.blocks_per_dest);
     return;
   }
   for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];

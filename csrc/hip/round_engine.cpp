@@ -236,8 +236,9 @@ class RoundEngine {
     check_xgmi();
     check_slot(slot);
     const XReg& r = grads_[slot];
-    return xg_->direct(ch_[2], r.hdr, r.data, r.seg, cap_, 4 * dim_, ucount, blocks);
+    return xg_->direct(ch_[2], {{r.data, r.seg}}, r.hdr, cap_, 4 * dim_, ucount, blocks);
   }
+
 
   // ------------------------------------------------------------ stage 3
   // One GPU: the optimizer update at the pulled slots (compact unique ids,

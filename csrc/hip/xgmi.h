@@ -21,7 +21,8 @@ static constexpr long long kXFlagBytes = (long long)kXMaxCh * kXMaxRanks * 128;
 static_assert(kXMaxRanks == kXDirectMaxRanks, "one peer table size");
 // local counters: put arrivals [ch][dest], waits [ch], error word(s),
 // direct-put arrivals [ch][dest]
-static constexpr long long kXLocalWords = 3ll * kXMaxCh * kXMaxRanks + 8;
+static constexpr long long kXLocalWords =
+    2ll * kXMaxCh * kXMaxRanks + 8 + (long long)kXMaxCh * kXMaxRanks * kXDirectDestWords;
 static constexpr int kXPutThreads = 256;
 
 struct XPart {
@@ -160,33 +161,42 @@ class XgmiArena {
                 reinterpret_cast<hipStream_t>(stream));
   }
 
-  // descriptor of a producer kernel storing its rows straight into the peers'
-  // region (hdr_off, data_off, seg_bytes) of channel ch (xdirect.h): `cnt`
-  // rows per destination (device), each destination's rows written by
+  // descriptor of a producer kernel storing its segments straight into the
+  // peers' regions of channel ch (xdirect.h): parts = (data_off, seg_bytes)
+  // each, hdr_off part 0's row-count header; `cnt` part-0 rows per
+  // destination (device), each destination's stores made by
   // `blocks_per_dest` workgroups, row r of destination d at r (ucap rows per
   // destination in the producer's own layout)
-  XDirect direct(int ch, long long hdr_off, long long data_off, long long seg_bytes,
+  XDirect direct(int ch, const std::vector<std::vector<long long>>& parts, long long hdr_off,
                  long long ucap, int row_bytes, uintptr_t cnt, int blocks_per_dest) const {
     if (ch < 0 || ch >= kXMaxCh) throw_error("xgmi: bad channel");
     if (blocks_per_dest < 1 || row_bytes < 4 || !cnt) throw_error("xgmi: bad direct put");
-    if (data_off + (long long)nranks_ * seg_bytes > bytes_ || hdr_off + 8ll * nranks_ > bytes_ ||
-        hdr_off < kXFlagBytes || data_off < kXFlagBytes)
-      throw_error("xgmi: direct region outside the arena");
+    if (parts.empty() || (int)parts.size() > kXDirectMaxParts) throw_error("xgmi: 1..4 parts");
+    if (hdr_off < kXFlagBytes || hdr_off + 8ll * nranks_ > bytes_)
+      throw_error("xgmi: direct header outside the arena");
     XDirect X{};
+    for (size_t p = 0; p < parts.size(); ++p) {
+      if (parts[p].size() != 2) throw_error("xgmi: direct part = (data_off, seg_bytes)");
+      const long long off = parts[p][0], seg = parts[p][1];
+      if (off < kXFlagBytes || off + (long long)nranks_ * seg > bytes_)
+        throw_error("xgmi: direct region outside the arena");
+      X.data_off[p] = off;
+      X.seg_bytes[p] = seg;
+    }
     for (int r = 0; r < nranks_; ++r) {
       if (!peers_[r]) throw_error("xgmi: peer arenas not open");
       X.peer[r] = peers_[r];
     }
-    X.data_off = data_off;
-    X.seg_bytes = seg_bytes;
     X.hdr_off = hdr_off;
     X.flag_off = ((long long)ch * kXMaxRanks + rank_) * 128;  // xgmi.hip xflag
     X.ucap = ucap;
     X.cnt = reinterpret_cast<const unsigned long long*>(cnt);
-    X.arrive = local_ + 2ll * kXMaxCh * kXMaxRanks + 8 + (long long)ch * kXMaxRanks;
+    X.arrive = local_ + 2ll * kXMaxCh * kXMaxRanks + 8 +
+               (long long)ch * kXMaxRanks * kXDirectDestWords;
     X.err = reinterpret_cast<unsigned int*>(err_ptr());
     X.me = rank_;
     X.nranks = nranks_;
+    X.nparts = (int)parts.size();
     X.blocks_per_dest = blocks_per_dest;
     X.row_bytes = row_bytes;
     return X;
