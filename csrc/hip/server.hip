@@ -282,8 +282,8 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
 // summed per distinct key into merged[ubase[b] + l].  Per bucket the
 // positions are counting-sorted by local id in LDS (tables sized by the
 // bucket's distinct keys, not the 4096-slot maximum: word2vec buckets hold
-// ~30), then a lane group per key sums its rows (16-byte chunks when D % 4
-// == 0; no atomics).  `slots`: the merged row goes straight into the
+// ~30), then a lane group per key sums its rows (lane-consecutive words; no
+// atomics).  `slots`: the merged row goes straight into the
 // optimizer update of the key's table row (each lane updates its
 // coordinates and their state) — no merged-row round trip, no apply launch
 __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restrict__ bstart,
@@ -305,82 +305,87 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
   const uint32_t base = ubase[b];
   const uint32_t np = min(p1 - p0, (uint32_t)kSrvOcc);
   if (nu == 0) return;  // workgroup-uniform
-  for (uint32_t l = t; l <= nu; l += 512) off[l] = 0u;
-  __syncthreads();
-  for (uint32_t q = t; q < np; q += 512) {
-    const uint32_t l = luid[p0 + q];
-    if (l < nu) atomicAdd(&off[l + 1], 1u);
-  }
-  __syncthreads();
-  // inclusive scan of off[1..nu]: thread t owns `per` consecutive entries
-  const uint32_t per = (nu + 511) / 512;  // <= kSrvTS / 512
-  unsigned int sum = 0;
-  for (uint32_t i = 0; i < per; ++i) {
-    const uint32_t l = 1 + t * per + i;
-    if (l <= nu) sum += off[l];
-  }
-  unsigned int e = block_excl_scan<8>(sum, wsum, nullptr);
-  for (uint32_t i = 0; i < per; ++i) {
-    const uint32_t l = 1 + t * per + i;
-    if (l <= nu) {
-      e += off[l];
-      off[l] = e;
+  if (np == nu) {
+    // every distinct key received once (one source, or no overlap between
+    // the sources in this bucket): key l's position is the q with luid = l,
+    // no counting sort
+    for (uint32_t l = t; l <= nu; l += 512) off[l] = l;
+    for (uint32_t q = t; q < np; q += 512) {
+      const uint32_t l = luid[p0 + q];
+      if (l < nu) ord[l] = (unsigned short)q;
     }
+    __syncthreads();
+  } else {
+    for (uint32_t l = t; l <= nu; l += 512) off[l] = 0u;
+    __syncthreads();
+    for (uint32_t q = t; q < np; q += 512) {
+      const uint32_t l = luid[p0 + q];
+      if (l < nu) atomicAdd(&off[l + 1], 1u);
+    }
+    __syncthreads();
+    // inclusive scan of off[1..nu]: thread t owns `per` consecutive entries
+    const uint32_t per = (nu + 511) / 512;  // <= kSrvTS / 512
+    unsigned int sum = 0;
+    for (uint32_t i = 0; i < per; ++i) {
+      const uint32_t l = 1 + t * per + i;
+      if (l <= nu) sum += off[l];
+    }
+    unsigned int e = block_excl_scan<8>(sum, wsum, nullptr);
+    for (uint32_t i = 0; i < per; ++i) {
+      const uint32_t l = 1 + t * per + i;
+      if (l <= nu) {
+        e += off[l];
+        off[l] = e;
+      }
+    }
+    __syncthreads();
+    // placement: a second counter pass (cursor = off[l], advanced atomically)
+    for (uint32_t l = t; l < nu; l += 512) cur[l] = off[l];
+    __syncthreads();
+    for (uint32_t q = t; q < np; q += 512) {
+      const uint32_t l = luid[p0 + q];
+      if (l < nu) ord[atomicAdd(&cur[l], 1u)] = (unsigned short)q;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  // placement: a second counter pass (cursor = off[l], advanced atomically)
-  for (uint32_t l = t; l < nu; l += 512) cur[l] = off[l];
-  __syncthreads();
-  for (uint32_t q = t; q < np; q += 512) {
-    const uint32_t l = luid[p0 + q];
-    if (l < nu) ord[atomicAdd(&cur[l], 1u)] = (unsigned short)q;
-  }
-  __syncthreads();
   const int ns = opt_state_per_coord(op.kind);
-  const bool vec = (D & 3) == 0;
-  const int V = vec ? 4 : 1;          // coordinates per lane and chunk
-  const int W = D / V;                // chunks per row
-  const int G = srv_group(W), lg = t % G;
+  // a group of G lanes per key; lane lg owns coordinates lg + i*G, so every
+  // load / store instruction of the group covers G consecutive words (the
+  // table row and the gradient rows alike; 16-byte chunks per lane left each
+  // instruction a strided 512-byte span)
+  const int G = srv_group((D + 3) / 4), lg = t % G;
   const uint32_t kpp = 512 / G;       // keys in flight per workgroup
   for (uint32_t l = (uint32_t)(t / G); l < nu; l += kpp) {
     const uint32_t a = off[l], z = off[l + 1];
     const long long slot = slots ? slots[(long long)base + l] : -1;
     const bool upd = slots && slot >= 0;
-    for (int c0 = lg; c0 < W; c0 += G) {
+    for (int c0 = 0; c0 < D; c0 += 4 * G) {
       // fused update: the row (and state) loads go out before the gradient
       // sum, their latency overlaps the gathers instead of following them
       float wv[4], s1[4], s2[4], acc[4] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int c = c0 * V + i;
-        const bool on = upd && i < V;
+        const int c = c0 + lg + i * G;
+        const bool on = upd && c < D;
         wv[i] = on ? row_ld(tab, slot, c) : 0.f;
         s1[i] = on && ns > 0 ? row_ld(tab, slot, D + c) : 0.f;
         s2[i] = on && ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
       }
-      for (uint32_t i = a; i < z; ++i) {
-        const long long r = (long long)pj[p0 + ord[i]] * W + c0;
-        if (vec) {
-          const float4 g = reinterpret_cast<const float4*>(grads)[r];
-          acc[0] += g.x;
-          acc[1] += g.y;
-          acc[2] += g.z;
-          acc[3] += g.w;
-        } else {
-          acc[0] += grads[r];
-        }
-      }
-      if (!slots) {
-        const long long o = ((long long)base + l) * W + c0;
-        if (vec)
-          reinterpret_cast<float4*>(merged)[o] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-        else
-          merged[o] = acc[0];
-      } else if (upd) {
+      for (uint32_t q = a; q < z; ++q) {
+        const float* g = grads + (long long)pj[p0 + ord[q]] * D;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          if (i >= V) break;
-          const int c = c0 * V + i;
+          const int c = c0 + lg + i * G;
+          if (c < D) acc[i] += g[c];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 + lg + i * G;
+        if (c >= D) continue;
+        if (!slots) {
+          merged[((long long)base + l) * D + c] = acc[i];
+        } else if (upd) {
           opt_update(op, wv[i], s1[i], s2[i], acc[i]);
           row_st(tab, slot, c, wv[i], true);
           if (ns > 0) row_st(tab, slot, D + c, s1[i], true);
