@@ -65,6 +65,12 @@ def main(argv=None):
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
+    # SS_BENCH_TRACE_AFTER=S: dump every thread's Python stack to stderr after
+    # S seconds (a wedged rank shows where it waits)
+    if os.environ.get("SS_BENCH_TRACE_AFTER"):
+        import faulthandler
+
+        faulthandler.dump_traceback_later(float(os.environ["SS_BENCH_TRACE_AFTER"]), exit=False)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -98,18 +98,26 @@ class RoundEngine {
   }
 
   // ---------------------------------------------------------- N>1 set-up
-  // regions: keys [depth][3 parts, or 4 with the sub-bucket offsets of a
-  // server split (sub > 1)], vals [depth], grads [depth], each (hdr, data,
-  // seg); chans: the arena channel ids of keys / vals / grads
-  void set_xgmi(XgmiArena* arena, std::vector<int> chans, std::vector<std::vector<long long>> keys,
+  // arenas: per ring slot the (keys, vals, grads) mailbox arenas (one IPC
+  // allocation each, channel 0 inside; parallel/xgmi.py); regions: keys
+  // [depth][3 parts, or 4 with the sub-bucket offsets of a server split (sub
+  // > 1)], vals [depth], grads [depth], each (hdr, data, seg) in its arena
+  void set_xgmi(std::vector<std::vector<XgmiArena*>> arenas,
+                std::vector<std::vector<long long>> keys,
                 std::vector<std::vector<long long>> vals, std::vector<std::vector<long long>> grads,
                 int nranks, int rank, int Pd, int sub, long long cap, int dim, int bpp,
                 double timeout_s) {
-    if (!arena || chans.size() != 3) throw std::invalid_argument("set_xgmi: arena + 3 channels");
-    if ((int)keys.size() != depth_ || (int)vals.size() != depth_ || (int)grads.size() != depth_)
-      throw std::invalid_argument("set_xgmi: one region set per ring slot");
-    xg_ = arena;
-    ch_ = {chans[0], chans[1], chans[2]};
+    if ((int)arenas.size() != depth_ || (int)keys.size() != depth_ || (int)vals.size() != depth_ ||
+        (int)grads.size() != depth_)
+      throw std::invalid_argument("set_xgmi: one arena and region set per ring slot");
+    ar_.assign(depth_, {nullptr, nullptr, nullptr});
+    for (int s = 0; s < depth_; ++s) {
+      if (arenas[s].size() != 3) throw std::invalid_argument("set_xgmi: (keys, vals, grads) arenas");
+      for (int c = 0; c < 3; ++c) {
+        if (!arenas[s][c]) throw std::invalid_argument("set_xgmi: null arena");
+        ar_[s][c] = arenas[s][c];
+      }
+    }
     nkp_ = sub > 1 ? 4 : 3;
     for (int s = 0; s < depth_; ++s) {
       if ((int)keys[s].size() != 3 * nkp_ || vals[s].size() != 3 || grads[s].size() != 3)
@@ -151,7 +159,7 @@ class RoundEngine {
   void route_end(int slot, int tag, uintptr_t route, uintptr_t ukeys, uintptr_t ucount,
                  uintptr_t runs_base, uintptr_t runs_num, uintptr_t runs_sub) {
     check_slot(slot);
-    if (xg_) {
+    if (!ar_.empty()) {
       std::vector<std::vector<long long>> parts;
       parts.push_back(part(ukeys, ucount, 0, 8, keys_[slot][0], cap_));
       parts.push_back(part(runs_base, 0, Pd_, 4, keys_[slot][1], Pd_));
@@ -161,7 +169,7 @@ class RoundEngine {
         parts.push_back(part(runs_sub, 0, (long long)Pd_ * sub_, 4, keys_[slot][3],
                              (long long)Pd_ * sub_));
       }
-      xg_->put(ch_[0], parts, bpp_, route);
+      ar_[slot][0]->put(0, parts, bpp_, route);
     }
     record(kRoute, slot, route, tag);
   }
@@ -201,11 +209,11 @@ class RoundEngine {
     std::vector<std::vector<long long>> fixed = {{keys_[slot][1].data, keys_[slot][1].seg, nb},
                                                  {keys_[slot][2].data, keys_[slot][2].seg, nb}};
     if (nkp_ == 4) fixed.push_back({keys_[slot][3].data, keys_[slot][3].seg, nb * sub_});
-    xg_->wait(ch_[0], fixed, timeout_, stream, {}, 0.0);
+    ar_[slot][0]->wait(0, fixed, timeout_, stream, {}, 0.0);
     if (table) {
       SrvSlot& S = srv_[slot];
       const uint32_t* roff =
-          nkp_ == 4 ? Pt<const uint32_t>(xg_->base() + keys_[slot][3].data) : nullptr;
+          nkp_ == 4 ? Pt<const uint32_t>(ar_[slot][0]->base() + keys_[slot][3].data) : nullptr;
       launch_srv_dedup(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
                        Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt,
                        S.bstart, S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount,
@@ -236,7 +244,7 @@ class RoundEngine {
     check_xgmi();
     check_slot(slot);
     const XReg& r = grads_[slot];
-    return xg_->direct(ch_[2], {{r.data, r.seg}}, r.hdr, cap_, 4 * dim_, ucount, blocks);
+    return ar_[slot][2]->direct(0, {{r.data, r.seg}}, r.hdr, cap_, 4 * dim_, ucount, blocks);
   }
 
 
@@ -272,9 +280,9 @@ class RoundEngine {
     if (put) {  // else the model's merge kernel stored the rows (grads_direct)
       std::vector<std::vector<long long>> parts;
       parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_));
-      xg_->put(ch_[2], parts, bpp_, stream);
+      ar_[slot][2]->put(0, parts, bpp_, stream);
     }
-    xg_->wait(ch_[2], {}, timeout_, stream, {}, 0.0);
+    ar_[slot][2]->wait(0, {}, timeout_, stream, {}, 0.0);
     if (table) {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
@@ -300,7 +308,7 @@ class RoundEngine {
     if (slot < 0 || slot >= depth_) throw std::out_of_range("RoundEngine: ring slot");
   }
   void check_xgmi() const {
-    if (!xg_) throw std::logic_error("RoundEngine: set_xgmi first");
+    if (ar_.empty()) throw std::logic_error("RoundEngine: set_xgmi first");
   }
   void pull_waits(int slot, int tag, uintptr_t stream, bool wait_route, int prev) {
     check_slot(slot);
@@ -318,7 +326,7 @@ class RoundEngine {
   void fill_and_return(int slot, uintptr_t stream, uintptr_t svals, uintptr_t rvals,
                        uintptr_t sent, const std::vector<uintptr_t>& metrics) {
     // the rows each source gets back = the keys it sent here (keys header)
-    const uintptr_t rc = xg_->base() + keys_[slot][0].hdr;
+    const uintptr_t rc = ar_[slot][0]->base() + keys_[slot][0].hdr;
     if (svals) {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
@@ -331,21 +339,20 @@ class RoundEngine {
     }
     std::vector<std::vector<long long>> parts;
     parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_));
-    xg_->put(ch_[1], parts, bpp_, stream);
+    ar_[slot][1]->put(0, parts, bpp_, stream);
     std::vector<uintptr_t> m = metrics;
     if (!m.empty()) {
       if (m.size() != 3) throw std::invalid_argument("pull_xgmi: metrics = (acc, xval, xacc)");
       m = {sent, rc, metrics[0], metrics[1], metrics[2]};
     }
-    xg_->wait(ch_[1], {}, timeout_, stream, m, 8.0 + 8.0 * dim_);
+    ar_[slot][1]->wait(0, {}, timeout_, stream, m, 8.0 + 8.0 * dim_);
   }
 
   int depth_, device_;
   std::array<std::vector<hipEvent_t>, 3> ev_;
   std::array<std::vector<int>, 3> tag_;
   std::vector<SrvSlot> srv_;
-  XgmiArena* xg_ = nullptr;
-  std::array<int, 3> ch_{};
+  std::vector<std::array<XgmiArena*, 3>> ar_;  // per slot: keys, vals, grads
   std::vector<std::array<XReg, 4>> keys_;
   int nkp_ = 3;  // parts of the keys channel
   std::vector<XReg> vals_, grads_;

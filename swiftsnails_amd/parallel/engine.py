@@ -213,11 +213,16 @@ class PSEngine(HostRounds):
             self.rkeys = torch.empty(N * cap, dtype=torch.int64)
             self.rvals = torch.zeros((N * cap, d), dtype=torch.float32)
             self.rgrads = torch.empty((N * cap, d), dtype=torch.float32)
-        # pull-ahead (N>1 on GPU): round i+1's pull runs on the pull stream
-        # while round i computes — bounded staleness 1; needs ring
-        # depth >= 3 (rounds i, i+1, i+2 in flight)
+        # pull-ahead: round i+1's pull runs on the pull stream while round i
+        # computes — bounded staleness 1; needs ring depth >= 3
+        # (rounds i, i+1, i+2 in flight).  Models opt in (FM, word2vec:
+        # enable_pull_ahead); sparse LR runs synchronous rounds at every N:
+        # measured faster with the servers' snapshot (blind-store) update
+        # than pulled ahead with a read-modify-write (one GPU through the N>1
+        # path 1.106 vs 1.12 ms; 2 / 4 xGMI ranks sharing one GPU -5 %), and
+        # no staleness.  SS_PULL_AHEAD=1 turns it on for every model at N>1
         if self.gpu and self.dist and self.depth >= 3 and \
-                os.environ.get("SS_PULL_AHEAD", "1") != "0":
+                os.environ.get("SS_PULL_AHEAD", "auto") == "1":
             self.pull_ahead = True
             self.pull_stream = torch.cuda.Stream(device=self.device)
         # a pulled-ahead round misses at most this many rounds' updates
@@ -280,8 +285,8 @@ class PSEngine(HostRounds):
             self.srv = [_ServerSlot(rows, self.Ps, dev, snap_ok) for _ in range(self.depth)]
         if self.xg:
             D = self.depth
-            self.native.set_xgmi(self.xg.arena, [self.xg.channel(c) for c in ("keys", "vals",
-                                                                            "grads")],
+            self.native.set_xgmi([[self.xg.arena_of(c, q) for c in ("keys", "vals", "grads")]
+                                  for q in range(D)],
                                  [sum((list(self.xg.layout("keys", p, q))
                                        for p in range(4 if Psub else 3)), []) for q in range(D)],
                                  [list(self.xg.layout("vals", 0, q)) for q in range(D)],
@@ -467,7 +472,7 @@ class PSEngine(HostRounds):
         hold up the next dedup (word2vec 0.128 -> 0.125 ms/step), not when
         the main stream is the longer one (FM 0.655 -> 0.685)."""
         if on and self.gpu and self.depth >= 3 and \
-                os.environ.get("SS_PULL_AHEAD", "1") != "0":
+                os.environ.get("SS_PULL_AHEAD", "auto") != "0":
             self.pull_ahead = True
             want = os.environ.get("SS_PULL_STREAM", "1" if pull_stream else "0") != "0"
             if self.fast1 and self.pull_stream is None and want:

@@ -26,6 +26,8 @@ KNOBS: dict[str, Knob] = {
     "SS_DEVICE": Knob("LOCAL_RANK", "framework/gpu.py", "ops",
                       "pin every rank to one device (multi-rank rehearsal on one GPU, gloo)"),
     "SS_BENCH_DEVICE": Knob("LOCAL_RANK", "bench.py", "ops", "same, for bench.py"),
+    "SS_BENCH_TRACE_AFTER": Knob("unset", "bench.py", "ops",
+                                 "dump every thread's Python stack to stderr after S seconds"),
     "SS_BENCH_ROUND_TIMEOUT": Knob("300", "bench.py", "ops",
                                    "seconds without a finished step before the bench aborts"),
     "SS_FAULT": Knob("", "parallel/watchdog.py", "ops",
@@ -45,8 +47,9 @@ KNOBS: dict[str, Knob] = {
     "SS_ENGINE_DEPTH": Knob("4", "parallel/engine.py", "tuning",
                             "route-buffer ring depth (>= 3 for pull-ahead; 4 measured 1.008 vs "
                             "1.018 ms/step for 3, four A/B pairs)"),
-    "SS_PULL_AHEAD": Knob("1", "parallel/engine.py", "tuning",
-                          "N>1 (and FM / word2vec at N=1): pull round i+1 while round i computes"),
+    "SS_PULL_AHEAD": Knob("auto", "parallel/engine.py", "tuning",
+                          "pull round i+1 while round i computes: auto = the models that opt "
+                          "in (FM, word2vec), 1 = every model at N>1, 0 = none"),
     "SS_DEDUP": Knob("bucket", "ops/dedup.py", "tuning",
                      "bucket: LDS dedup per hash bucket; hash: global scratch table"),
     "SS_TABLE_G": Knob("auto", "ops/table.py", "tuning", "lanes per table row"),

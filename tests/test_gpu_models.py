@@ -569,6 +569,7 @@ def test_general_path_rccl_world1_pull_ahead_trains(dev, model, comms, monkeypat
     on one GPU through size-1 RCCL communicators: trains and keeps the table
     sane."""
     monkeypatch.setenv("SS_ENGINE_GENERAL", "1")
+    monkeypatch.setenv("SS_PULL_AHEAD", "1")  # LR runs synchronous rounds by default
     w, t = _graph_worker(model, dev, **_rccl1(dev, comms))
     assert w.engine.pull_ahead and w.engine.pull_stream is not None
     losses = [float(w.step().sum().item()) for _ in range(40)]
