@@ -97,3 +97,20 @@ def test_schedule_rejects_malformed_exchanges():
         h.a2a_schedule(0, 2, [2, 2], [0, 2], [1, 3], [0, 1], 4)
     with pytest.raises(ValueError, match="rank"):
         h.a2a_schedule(2, 2, *ok, 4)
+
+
+def test_xgmi_arenas_stay_below_the_ipc_limit():
+    """Importing an uncached allocation of 2 GB or more through
+    hipIpcOpenMemHandle never returned on the MI355X boxes, so the mailbox
+    transport gives every (channel, ring slot) its own allocation and
+    refuses one of 2 GiB or more before allocating anything.  The bench's
+    largest mailbox, one round of keys from 8 sources of a 262144 x 39
+    batch, is 0.65 GB."""
+    import torch
+
+    from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+    t = XgmiTransport(0, 8, torch.device("cuda", 0), None)
+    with pytest.raises(ValueError, match="2 GiB"):
+        t.setup({"keys": (4, [10_223_616 * 8 * 4])})
+    assert 8 * 10_223_616 * 8 < (2 << 30)
