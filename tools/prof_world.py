@@ -12,6 +12,8 @@ does — which a 1-rank run through the N>1 path cannot show.
 
     python tools/prof_world.py --world 8 --out gpurun_out/profw8 -- --steps 10 --warmup 3 \
         --transport xgmi --batch 131072
+    python tools/prof_world.py --world 4 --no-prof --launch -- \
+        --config configs/word2vec_1m_4x4.conf --steps 64 --warmup 16   # the config launcher
 """
 from __future__ import annotations
 
@@ -39,6 +41,8 @@ def main() -> int:
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "profw"))
     ap.add_argument("--timeout", type=float, default=400.0)
     ap.add_argument("--no-prof", action="store_true", help="run the ranks without rocprofv3")
+    ap.add_argument("--launch", action="store_true",
+                    help="run python -m swiftsnails_amd.launch (config jobs) instead of bench.py")
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
     a = ap.parse_args()
     if not 1 <= a.world <= 12:
@@ -49,8 +53,9 @@ def main() -> int:
     for r in range(a.world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(a.world),
                    LOCAL_WORLD_SIZE=str(a.world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), SS_BENCH_DEVICE="0", TMPDIR="/tmp")
-        bench = ["python3", os.path.join(ROOT, "bench.py"), "--gpus", str(a.world)] + args
+                   MASTER_PORT=str(port), SS_BENCH_DEVICE="0", SS_DEVICE="0", TMPDIR="/tmp")
+        bench = (["python3", "-m", "swiftsnails_amd.launch"] + args if a.launch else
+                 ["python3", os.path.join(ROOT, "bench.py"), "--gpus", str(a.world)] + args)
         if a.no_prof:
             cmd = bench
         else:
