@@ -155,7 +155,7 @@ def main(argv=None):
     try:
         engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev,
                           count_transport=ctrans, pull_transport=ptrans)
-    except RuntimeError as e:
+    except (RuntimeError, ValueError) as e:
         if not (world > 1 and a.transport == "auto" and "xgmi" in str(e)):
             raise
         # every rank failed the mailbox self-test together: RCCL instead
