@@ -574,8 +574,7 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     float* __restrict__ ugrad, int osi,
                                                     const uint8_t* __restrict__ usingle,
                                                     DevTable t, const long long* __restrict__ slots,
-                                                    const float2* __restrict__ snap, OptParams op,
-                                                    XDirect xd) {
+                                                    const float2* __restrict__ snap, OptParams op) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
@@ -622,21 +621,6 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
       opt_update(op, wh.x, wh.y, s2, acc[l]);
       *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
     }
-    return;
-  }
-  if (xd.nranks > 0) {
-    // N>1 xGMI: the merged rows go straight into the destination's mailbox
-    // (this bucket's run of its segment), then the workgroup arrives; the
-    // last of the destination's Pd buckets publishes the segment
-    const int d = b / xd.blocks_per_dest;
-    const long long r0 = (long long)base - (long long)d * xd.ucap;
-    for (uint32_t l = threadIdx.x; l < nu; l += RT) {
-      float* o = reinterpret_cast<float*>(xd_row(xd, d, r0 + l));
-      if (o) *o = acc[l];
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) xd_arrive(xd, d, b - d * xd.blocks_per_dest);
     return;
   }
   for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];
@@ -1036,11 +1020,8 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi, const uint8_t* usingle,
                       const DevTable* t, const long long* slots, const float* snap,
-                      const OptParams* op, int ndest, const XDirect* xd) {
-  if (n <= 0) {
-    if (xd) throw_error("bd_reduce: a direct put must run (its receivers wait for it)");
-    return;
-  }
+                      const OptParams* op, int ndest) {
+  if (n <= 0) return;
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
   DevTable tv{};
   OptParams opv{};
@@ -1053,12 +1034,6 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   }
   const float2* sn = reinterpret_cast<const float2*>(snap);
   const BdLayout L = bd_layout(n, nranks, ndest);
-  XDirect xdv{};
-  if (xd) {
-    if (slots || osi || xd->nranks != nranks || xd->blocks_per_dest != L.Pd || xd->row_bytes != 4)
-      throw_error("bd_reduce: a direct put needs compact scalar rows in this layout");
-    xdv = *xd;
-  }
   const uint32_t* S = scratch;
   // workgroup size (SS_BD_RT experiment knob): measured 1024 >= 512 >= 256
   static const int rt = [] {
@@ -1067,15 +1042,13 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   }();
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       xdv);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       xdv);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
-                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv, xdv);
+                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
   check_launch("k_bd_reduce");
 }
 
@@ -1097,7 +1070,7 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
   }
   hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj, luid,
                      gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
-                     reinterpret_cast<const float2*>(snap), opv, XDirect{});
+                     reinterpret_cast<const float2*>(snap), opv);
   check_launch("k_bd_reduce_p");
 }
 

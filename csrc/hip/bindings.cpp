@@ -93,11 +93,6 @@ PYBIND11_MODULE(_ss_hip, m) {
            py::arg("kind") = 0, py::arg("scale") = 0.f, py::arg("state_init") = 0.f,
            py::arg("seed") = 0, py::arg("zero_bit") = -1);
 
-  // opaque: a producer kernel's direct stores into the peers' mailboxes
-  // (xdirect.h), made by RoundEngine.grads_direct
-  py::class_<XDirect>(m, "XDirect", py::module_local())
-      .def_readonly("nranks", &XDirect::nranks)
-      .def_readonly("blocks_per_dest", &XDirect::blocks_per_dest);
   py::class_<OptParams>(m, "OptParams", py::module_local())
       .def(py::init([](int kind, float lr, float l1, float l2, float eps, float beta1, float beta2,
                        float bc1, float bc2, float alpha, float beta, float grad_scale,
@@ -209,18 +204,16 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
-                        uintptr_t snap, std::optional<OptParams> op, int ndest,
-                        std::optional<XDirect> xd) {
+                        uintptr_t snap, std::optional<OptParams> op, int ndest) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                      P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
                      P<float>(ugrad), S(st), osi, P<const uint8_t>(usingle),
                      t ? &*t : nullptr, P<const long long>(slots), P<const float>(snap),
-                     op ? &*op : nullptr, ndest, xd ? &*xd : nullptr);
+                     op ? &*op : nullptr, ndest);
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("xval"), py::arg("F"), py::arg("ugrad"), py::arg("st"),
      py::arg("osi") = 0, py::arg("usingle") = 0, py::arg("t") = py::none(), py::arg("slots") = 0,
-     py::arg("snap") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0,
-     py::arg("xd") = py::none());
+     py::arg("snap") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0);
   m.def("bd_unplace", [](long long n, int nranks, uintptr_t scratch, uintptr_t src, uintptr_t dst,
                          int dim, uintptr_t st, int ndest) {
     launch_bd_unplace(n, nranks, P<const uint32_t>(scratch), P<const float>(src), P<float>(dst),

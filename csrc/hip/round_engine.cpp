@@ -236,16 +236,6 @@ class RoundEngine {
     if (ahead) record(kPull, slot, stream, tag);
   }
 
-  // the gradient rows of ring slot `slot` stored by the model's merge kernel
-  // straight into the servers' mailboxes (xdirect.h): `ucount` rows per
-  // destination, each destination's rows from `blocks` workgroups (its
-  // buckets); push_xgmi(..., put=false) then only waits
-  XDirect grads_direct(int slot, uintptr_t ucount, int blocks) const {
-    check_xgmi();
-    check_slot(slot);
-    const XReg& r = grads_[slot];
-    return ar_[slot][2]->direct(0, {{r.data, r.seg}}, r.hdr, cap_, 4 * dim_, ucount, blocks);
-  }
 
 
   // ------------------------------------------------------------ stage 3
@@ -275,13 +265,11 @@ class RoundEngine {
   // kernel, or a tensor-code rule) and releases the slot.
   void push_xgmi(int slot, int tag, uintptr_t stream, uintptr_t grads, uintptr_t ucount,
                  bool table, bool update, const DevTable& t, const OptParams& op, uintptr_t rgrads,
-                 bool scalar_fused, bool snap, uintptr_t merged, bool release, bool put) {
+                 bool scalar_fused, bool snap, uintptr_t merged, bool release) {
     check_xgmi();
-    if (put) {  // else the model's merge kernel stored the rows (grads_direct)
-      std::vector<std::vector<long long>> parts;
-      parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_));
-      ar_[slot][2]->put(0, parts, bpp_, stream);
-    }
+    std::vector<std::vector<long long>> parts;
+    parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_));
+    ar_[slot][2]->put(0, parts, bpp_, stream);
     ar_[slot][2]->wait(0, {}, timeout_, stream, {}, 0.0);
     if (table) {
       SrvSlot& S = srv_[slot];
@@ -375,8 +363,7 @@ void bind_round_engine(py::module_& m) {
       .def("pull_xgmi", &RoundEngine::pull_xgmi)
       .def("pull_xgmi_finish", &RoundEngine::pull_xgmi_finish)
       .def("push_fast", &RoundEngine::push_fast)
-      .def("push_xgmi", &RoundEngine::push_xgmi)
-      .def("grads_direct", &RoundEngine::grads_direct);
+      .def("push_xgmi", &RoundEngine::push_xgmi);
 }
 
 }  // namespace ss

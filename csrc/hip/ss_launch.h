@@ -9,7 +9,6 @@
 #include <vector>
 #include "bdindex.h"
 #include "ss_device.h"
-#include "xdirect.h"
 
 namespace ss {
 
@@ -155,8 +154,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       float* ugrad, hipStream_t st, int osi = 0,
                       const uint8_t* usingle = nullptr, const DevTable* t = nullptr,
                       const long long* slots = nullptr, const float* snap = nullptr,
-                      const OptParams* op = nullptr, int ndest = 0,
-                      const XDirect* xd = nullptr);
+                      const OptParams* op = nullptr, int ndest = 0);
 // occ[p] = uvals[uid of occurrence position p] (scalar rows; 0 where none):
 // one workgroup per dedup bucket, for the LR forward's one-gather mode
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,

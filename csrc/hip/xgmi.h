@@ -10,7 +10,6 @@
 #include <vector>
 
 #include "ss_launch.h"
-#include "xdirect.h"
 
 namespace ss {
 
@@ -18,11 +17,8 @@ static constexpr int kXMaxRanks = 16;
 static constexpr int kXMaxCh = 16;
 static constexpr int kXMaxParts = 4;
 static constexpr long long kXFlagBytes = (long long)kXMaxCh * kXMaxRanks * 128;
-static_assert(kXMaxRanks == kXDirectMaxRanks, "one peer table size");
-// local counters: put arrivals [ch][dest], waits [ch], error word(s),
-// direct-put arrivals [ch][dest]
-static constexpr long long kXLocalWords =
-    2ll * kXMaxCh * kXMaxRanks + 8 + (long long)kXMaxCh * kXMaxRanks * kXDirectDestWords;
+// local counters: put arrivals [ch][dest], waits [ch], error word(s)
+static constexpr long long kXLocalWords = 2ll * kXMaxCh * kXMaxRanks + 8;
 static constexpr int kXPutThreads = 256;
 
 struct XPart {
@@ -159,47 +155,6 @@ class XgmiArena {
     unsigned long long* arrive = local_ + (long long)ch * kXMaxRanks;
     launch_xput(P, arrive, reinterpret_cast<unsigned int*>(err_ptr()),
                 reinterpret_cast<hipStream_t>(stream));
-  }
-
-  // descriptor of a producer kernel storing its segments straight into the
-  // peers' regions of channel ch (xdirect.h): parts = (data_off, seg_bytes)
-  // each, hdr_off part 0's row-count header; `cnt` part-0 rows per
-  // destination (device), each destination's stores made by
-  // `blocks_per_dest` workgroups, row r of destination d at r (ucap rows per
-  // destination in the producer's own layout)
-  XDirect direct(int ch, const std::vector<std::vector<long long>>& parts, long long hdr_off,
-                 long long ucap, int row_bytes, uintptr_t cnt, int blocks_per_dest) const {
-    if (ch < 0 || ch >= kXMaxCh) throw_error("xgmi: bad channel");
-    if (blocks_per_dest < 1 || row_bytes < 4 || !cnt) throw_error("xgmi: bad direct put");
-    if (parts.empty() || (int)parts.size() > kXDirectMaxParts) throw_error("xgmi: 1..4 parts");
-    if (hdr_off < kXFlagBytes || hdr_off + 8ll * nranks_ > bytes_)
-      throw_error("xgmi: direct header outside the arena");
-    XDirect X{};
-    for (size_t p = 0; p < parts.size(); ++p) {
-      if (parts[p].size() != 2) throw_error("xgmi: direct part = (data_off, seg_bytes)");
-      const long long off = parts[p][0], seg = parts[p][1];
-      if (off < kXFlagBytes || off + (long long)nranks_ * seg > bytes_)
-        throw_error("xgmi: direct region outside the arena");
-      X.data_off[p] = off;
-      X.seg_bytes[p] = seg;
-    }
-    for (int r = 0; r < nranks_; ++r) {
-      if (!peers_[r]) throw_error("xgmi: peer arenas not open");
-      X.peer[r] = peers_[r];
-    }
-    X.hdr_off = hdr_off;
-    X.flag_off = ((long long)ch * kXMaxRanks + rank_) * 128;  // xgmi.hip xflag
-    X.ucap = ucap;
-    X.cnt = reinterpret_cast<const unsigned long long*>(cnt);
-    X.arrive = local_ + 2ll * kXMaxCh * kXMaxRanks + 8 +
-               (long long)ch * kXMaxRanks * kXDirectDestWords;
-    X.err = reinterpret_cast<unsigned int*>(err_ptr());
-    X.me = rank_;
-    X.nranks = nranks_;
-    X.nparts = (int)parts.size();
-    X.blocks_per_dest = blocks_per_dest;
-    X.row_bytes = row_bytes;
-    return X;
   }
 
   // fixed: (data_off, seg_bytes, bytes) of the parts zeroed for a missing source

@@ -151,10 +151,8 @@ class SparseLRWorker(PipelinedWorker):
                        0, st, o.index_ptrs(dd.n), occ=self.occ.data_ptr())
             # one GPU: the merge kernel runs the AdaGrad update itself
             # (engine.fuse_apply: pull snapshot still valid), push() then only
-            # does the bookkeeping; N>1 over xGMI: it stores the merged rows
-            # straight into the servers' mailboxes (engine.fuse_put); else
-            # compact rows in the alltoallv layout
-            fa = self.engine.fuse_apply(rnd) or self.engine.fuse_put(rnd)
+            # does the bookkeeping; N>1: compact rows in the send layout
+            fa = self.engine.fuse_apply(rnd)
             h.bd_reduce(dd.lay, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                         o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
                         rnd.ugrad.data_ptr(), st, 0, 0, ndest=o.ndest, **(fa or {}))

@@ -72,7 +72,6 @@ class Round:
     snap: Optional[torch.Tensor] = None   # world-1: (w, h) rows as pulled (blind apply)
     snap_version: int = -1                # table.version the snapshot is valid for
     applied: bool = False                 # the model's kernel already ran K5 (fuse_apply)
-    direct: bool = False                  # the model's kernel stored the grads in the mailboxes
     server: Optional[object] = None       # CPU N>1: (unique keys, inverse) of the server merge
 
     @property
@@ -519,17 +518,6 @@ class PSEngine(HostRounds):
             args["snap"] = rnd.snap.data_ptr()
         return args
 
-    def fuse_put(self, rnd: Round) -> Optional[dict]:
-        """Arguments that let a model's scalar gradient-merge kernel store its
-        merged rows straight into the servers' mailboxes (``bd_reduce(...,
-        **args)``; xdirect.h) instead of the local send segment + the put
-        kernel, or None.  N>1 over xGMI; marks the round's put done."""
-        if not (self.xg and self.gpu and self.dim == 1 and not rnd.direct and rnd.dd.n > 0
-                and getattr(rnd.dd.owner, "mode", None) == "bucket"):
-            return None
-        rnd.direct = True
-        return {"xd": self.native.grads_direct(rnd.slot, rnd.dd.ucount.data_ptr(), self.Pd)}
-
     def push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
         with self.trace("push"):
             self._push(rnd, grads)
@@ -563,8 +551,7 @@ class PSEngine(HostRounds):
                                   tab.dt if S else self._nodt, tab.opt.native() if S else self._noop,
                                   self.rgrads[slot].data_ptr(), kind == "scalar",
                                   bool(S and S.snap_valid),
-                                  self.sgrad.data_ptr() if merged_only else 0, not merged_only,
-                                  not rnd.direct)
+                                  self.sgrad.data_ptr() if merged_only else 0, not merged_only)
             if merged_only:
                 self._apply_merged(slot)
                 self._release(slot)

@@ -189,73 +189,6 @@ def test_lr_worker_world2_pull_ahead(grad_mode):
     assert abs(ahead_last - sync_last) < 0.03, (sync_last, ahead_last)
 
 
-def _run_lr_xgmi_rank(rank, world, init, q):
-    # synchronous rounds: with pull-ahead, whether round i+1's lookup sees
-    # round i's update is a race by design (staleness 1), so losses of two
-    # runs are only comparable without it
-    os.environ["SS_PULL_AHEAD"] = "0"
-    init_gloo(init, rank, world)
-    try:
-        from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
-        from swiftsnails_amd.parallel.engine import PSEngine
-        from swiftsnails_amd.parallel.transport import TorchDistTransport
-        from swiftsnails_amd.parallel.xgmi import XgmiTransport
-
-        dev = torch.device("cuda", 0)
-        torch.cuda.set_device(dev)
-        store = dist.distributed_c10d._get_default_store()
-        out = {}
-        for direct in (True, False):
-            tr = XgmiTransport(rank, world, dev, store, aux=TorchDistTransport(),
-                               prefix=f"ss_xgmi_{int(direct)}", timeout_s=60)
-            data = CtrSynth(batch_size=2048, num_fields=13, num_features=200_000, tail_frac=0.1)
-            table = make_lr_table(data.num_features, world, device=dev)
-            eng = PSEngine(table, tr, max_keys=2048 * 13, dim=1, device=dev)
-            used = []
-            if direct:
-                fp = eng.fuse_put
-                eng.fuse_put = lambda rnd: used.append(1) or fp(rnd)
-            else:
-                eng.fuse_put = lambda rnd: None
-            w = SparseLRWorker(eng, data, rank=rank, world=world)
-            losses = []
-            for _ in range(12):
-                w.step()
-                losses.append(w.mean_loss())
-            torch.cuda.synchronize()
-            eng.check()
-            out[direct] = (losses, table.to_dict(with_state=True), len(used))
-            dist.barrier()  # no peer still stores into this rank's arena
-            tr.close()
-        q.put((rank, out))
-    finally:
-        dist.destroy_process_group()
-
-
-def test_lr_xgmi_direct_grads_match_put():
-    """The LR merge kernel storing its gradient rows straight into the servers'
-    mailboxes (xdirect.h) delivers what the put kernel delivers: same losses,
-    same final shards (3 ranks on cuda:0, 2 server sub-buckets)."""
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    init = file_init()
-    procs = [ctx.Process(target=_run_lr_xgmi_rank, args=(r, 3, init, q)) for r in range(3)]
-    for p in procs:
-        p.start()
-    res = collect(q, procs, 3, 240)
-    for p in procs:
-        p.join(60)
-        assert p.exitcode == 0
-    for rank, out in res:
-        (ld, td, nd), (lp, tp, np_) = out[True], out[False]
-        assert nd == 12 and np_ == 0
-        np.testing.assert_allclose(ld, lp, rtol=1e-5)
-        assert set(td) == set(tp) and len(td) > 0
-        a = np.stack([td[k] for k in sorted(td)])
-        b = np.stack([tp[k] for k in sorted(tp)])
-        np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-6)
-
-
 def _bench_torchrun(nproc, extra, env_extra=None):
     import json
     import subprocess
