@@ -626,8 +626,10 @@ def test_fm_fused_update_matches_separate_apply(dev, dim):
     a, b = tabs[0].to_dict(with_state=True), tabs[1].to_dict(with_state=True)
     assert a.keys() == b.keys() and len(a) == u
     ks = list(a.keys())
+    # rtol 3e-5: the hot key's 32000 occurrences are summed with LDS float
+    # atomics in either order (one coordinate measured 1.05e-5 apart)
     np.testing.assert_allclose(np.stack([b[k] for k in ks]), np.stack([a[k] for k in ks]),
-                               rtol=1e-5, atol=1e-6)
+                               rtol=3e-5, atol=1e-6)
 
 
 @pytest.mark.parametrize("pull_stream", ["0", "1"])
