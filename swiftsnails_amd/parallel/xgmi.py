@@ -3,9 +3,10 @@
 ``RcclTransport`` moves a round's segments with grouped ncclSend/ncclRecv,
 which need the byte counts on the host — one D2H + host wait per round, and
 no hipGraph capture of an N>1 step.  This transport (``csrc/hip/xgmi.hip``)
-gives every rank an uncached HBM arena exported through an IPC handle and
-mapped by every peer: a ``put`` kernel stores this rank's segment for each
-peer straight into that peer's arena over xGMI, with the row count read from
+gives every rank uncached HBM arenas — one per (channel, ring slot), each
+below 2 GiB, the largest IPC import that returns — exported through IPC
+handles and mapped by every peer: a ``put`` kernel stores this rank's segment
+for each peer straight into that peer's arena over xGMI, with the row count read from
 device memory and written into the receiver's header, then bumps a
 per-(channel, source) arrival counter there; a ``wait`` kernel on the
 consumer's stream spins until all sources have arrived.  The receiver's
