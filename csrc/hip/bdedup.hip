@@ -82,22 +82,23 @@ __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs,
   return d * Pd + __umulhi(h, Pd);
 }
 
-// upper bound on count/scatter chunks (SS_BD_NCH knob; default by path).
-// One rank (the 1-GPU step): 128 — a chunk of the bench batch (10.2M keys)
-// is 80K keys, looped in 8192-key register tiles, so each (chunk, bucket) run
-// of positions is ~16 long and the scatter's partial-line stores merge in L2,
-// and the route stream holds fewer CUs beside the main stream.  Measured
-// (bench, A/B pairs): 512 -> 0.928-0.932 ms/step, 256 -> 0.914, 128 ->
-// 0.886-0.899, 96 -> 0.888-0.894, 64 -> 0.90-0.916.  N>1 ranks: 256 (the
-// route stream is the N>1 step's critical chain and its count kernel must not
-// starve beside the pull and apply streams): 128 -> 1.057-1.062 ms/step,
-// 256 -> 1.032-1.036, 512 -> 1.046-1.049 (N>1 engine path on one GPU).
+// upper bound on count/scatter chunks (SS_BD_NCH knob): 128 — a chunk of the
+// bench batch (10.2M keys) is 80K keys, looped in 8192-key register tiles, so
+// each (chunk, bucket) run of positions is ~16 long and the scatter's
+// partial-line stores merge in L2, and the route stream holds fewer CUs beside
+// the main stream.  Measured (bench, A/B pairs): 512 -> 0.928-0.932 ms/step,
+// 256 -> 0.914, 128 -> 0.886-0.899, 96 -> 0.888-0.894, 64 -> 0.90-0.916.  The
+// N>1 path used 256 while its rounds pulled ahead (the route stream was its
+// critical chain); with synchronous rounds 128 measured as good or better: the
+// 1-rank N>1 path 1.065-1.105 vs 1.094-1.131 ms, 8 ranks on one GPU 8.48 vs
+// 8.41-8.84 ms per 8-rank step.
 static long long bd_max_chunks(int nranks) {
+  (void)nranks;
   static const long long env = [] {
     const char* e = std::getenv("SS_BD_NCH");
     return e ? std::atoll(e) : 0ll;
   }();
-  const long long x = env ? env : (nranks > 1 ? 256 : 128);
+  const long long x = env ? env : 128;
   return x < 64 ? 64 : x;
 }
 
@@ -950,13 +951,12 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     return (v == 256 || v == 512 || v == 1024) ? v : def;
   };
   static const int ct = wg_env("SS_BD_CT", 1024);
-  // count: 1024 threads on one GPU; 256 on the N>1 path, where it runs beside
-  // the server pull of the round before (k_pull_unique, capped at 4 WGs per
-  // CU): a 1024-thread workgroup needs 16 free wave slots on one CU at once
-  // and waited for them (26 us alone -> 310-385 us beside the pull); 256
-  // threads + the pull cap: 1.056-1.116 -> 1.035-1.067 ms/step on two boxes
-  static const int cnt_env = wg_env("SS_BD_CNT", 0);
-  const int cnt = cnt_env ? cnt_env : (rs.nranks > 1 ? 256 : 1024);
+  // count: 1024 threads.  (256 on the N>1 path paid while its rounds pulled
+  // ahead — the count then ran beside the server pull and waited for 16 free
+  // wave slots on one CU; with synchronous rounds 1024 measured better: 8
+  // ranks on one GPU 8.66-8.74 vs 8.71-9.26 ms per 8-rank step, the 1-rank
+  // N>1 path 1.076-1.103 vs 1.109-1.169 ms)
+  static const int cnt = wg_env("SS_BD_CNT", 1024);
   static const int cs = wg_env("SS_BD_CS", 1024);
 #define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \

@@ -57,10 +57,10 @@ KNOBS: dict[str, Knob] = {
                             "slot layout: rowfirst (width <= 2) / keyfirst"),
     "SS_TABLE_PREFILL": Knob("1", "ops/table.py", "tuning",
                              "zero-init tables pre-filled with the init row (insert = CAS only)"),
-    "SS_BD_NCH": Knob("128 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
+    "SS_BD_NCH": Knob("128", "csrc/hip/bdedup.hip", "tuning",
                       "max count/scatter chunks (1 GPU 512 -> 128: 0.93 -> 0.89 ms/step; "
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
-    "SS_BD_CNT": Knob("1024 (1 rank) / 256 (N>1)", "csrc/hip/bdedup.hip", "tuning",
+    "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
