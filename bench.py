@@ -62,6 +62,12 @@ def main(argv=None):
     # us/step at batch 1024 where host launch work bounds the step
     ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
                     help="replay the step as hipGraphs (1 GPU; auto = on for N=1)")
+    # zero: the usual sparse-LR start (prefilled table, an insert is the key
+    # CAS alone); uniform: random (u - 0.5) * scale weights drawn per key on
+    # insert (measured ~2 % slower: every insert writes its row)
+    ap.add_argument("--init", default="zero", choices=["zero", "uniform"],
+                    help="weight initialiser of the table")
+    ap.add_argument("--init-scale", type=float, default=0.01)
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -86,83 +92,36 @@ def main(argv=None):
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
 
-    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, make_lr_table
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, lr_init, make_lr_table
     from swiftsnails_amd.ops.optim import Optimizer
     from swiftsnails_amd.parallel.engine import PSEngine
-    from swiftsnails_amd.parallel.transport import LoopbackTransport, RcclTransport
 
-    ctrans = ptrans = None
-    comms = 0
+    store = None
     if world > 1:
-        from swiftsnails_amd.parallel.transport import default_gloo_ifname, rccl_comms_mode
+        from swiftsnails_amd.parallel.transport import default_gloo_ifname
 
         default_gloo_ifname()
         dist.init_process_group("gloo", rank=rank, world_size=world)
         store = dist.distributed_c10d._get_default_store()
-        try:
-            if a.transport == "gloo":
-                from swiftsnails_amd.parallel.transport import TorchDistTransport
-
-                transport = TorchDistTransport()
-            elif a.transport in ("auto", "xgmi"):
-                # the mailbox arena is laid out (and self-tested) when the
-                # engine is built, below
-                from swiftsnails_amd.parallel.transport import TorchDistTransport
-                from swiftsnails_amd.parallel.xgmi import XgmiTransport
-
-                transport = XgmiTransport(rank, world, dev, store, aux=TorchDistTransport())
-            elif rccl_comms_mode() == 1:
-                # one native RCCL communicator, every collective on its comm
-                # stream in program order (the conservative default)
-                transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
-                comms = 1
-            else:
-                # three communicators, one per engine stream: data plane
-                # (main: gradients), route (counts, bucket runs), pull (keys, rows)
-                transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data",
-                                          serial=False)
-                ctrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_counts",
-                                       serial=False)
-                ptrans = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_pull",
-                                       serial=False)
-                comms = 3
-        except Exception as e:  # pragma: no cover - hardware dependent
-            from swiftsnails_amd.parallel.transport import TorchDistTransport
-
-            print(f"bench.py: native RCCL communicator failed ({e}); "
-                  "falling back to torch.distributed(nccl=RCCL)", file=sys.stderr)
-            transport = TorchDistTransport(dist.new_group(backend="nccl"))
-            ctrans = ptrans = None
-            comms = 0
-    else:
-        transport = LoopbackTransport()
-        general = os.environ.get("SS_ENGINE_GENERAL", "0")
-        if general == "rccl":
-            # the N>1 engine path on one GPU through a real (size-1) RCCL
-            # communicator: the multi-GPU call sequence, minus the peers
-            transport = RcclTransport(0, 1, dev, uid=RcclTransport.new_unique_id())
-            comms = 1
-        elif general == "xgmi":
-            # ... or through a size-1 mailbox arena (puts to itself, waits)
-            from swiftsnails_amd.parallel.xgmi import XgmiTransport
-
-            transport = XgmiTransport(0, 1, dev, None)
 
     data = CtrSynth(batch_size=a.batch, num_fields=a.fields, num_features=a.features,
                     tail_frac=a.tail)
     opt = Optimizer(a.optimizer, lr=a.lr)
-    table = make_lr_table(a.features, world, optimizer=opt, load=a.load, device=dev)
-    try:
-        engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev,
-                          count_transport=ctrans, pull_transport=ptrans)
-    except (RuntimeError, ValueError) as e:
-        if not (world > 1 and a.transport == "auto" and "xgmi" in str(e)):
-            raise
-        # every rank failed the mailbox self-test together: RCCL instead
-        print(f"bench.py: {e}; falling back to RCCL", file=sys.stderr)
-        transport = RcclTransport(rank, world, dev, store=store, prefix="ss_rccl_data")
-        comms = 1
-        engine = PSEngine(table, transport, max_keys=a.batch * a.fields, dim=1, device=dev)
+    table = make_lr_table(a.features, world, optimizer=opt, load=a.load, device=dev,
+                          init=lr_init(a.init, a.init_scale))
+
+    # data plane: xGMI mailboxes (fence-free, then fenced publish; each tier
+    # must pass the start-up litmus on every rank) -> RCCL (parallel/select.py)
+    from swiftsnails_amd.parallel.select import build_engine
+
+    def make_engine(tr, ct, pt):
+        return PSEngine(table, tr, max_keys=a.batch * a.fields, dim=1, device=dev,
+                        count_transport=ct, pull_transport=pt)
+
+    engine, (transport, ctrans, ptrans), plane = build_engine(
+        a.transport, rank, world, dev, store, make_engine,
+        log=lambda m: print(f"bench.py: {m}", file=sys.stderr))
+    comms = plane.comms
     worker = SparseLRWorker(engine, data, rank=rank, world=world, grad_mode=a.grad_mode)
 
     # a wedged collective ends the job (exit 3) instead of hanging the node
@@ -233,7 +192,7 @@ def main(argv=None):
     if engine.fast1:
         tlabel = "none (world 1: colocated worker + server, no exchange)"
     else:
-        tlabel = transport.label
+        tlabel = plane.transport
     rccl_n = transport.nranks() if hasattr(transport, "nranks") else None
 
     samples = a.batch * world * a.steps
@@ -253,7 +212,9 @@ def main(argv=None):
                             if BASELINE_SAMPLES_PER_SEC else None),
             "dtype": "fp32",
             "data": (f"synthetic (on-device CTR generator, {a.fields} fields, Zipf ids over "
-                     f"{a.features / 1e9:g}B features; random-init (zero) weights)"),
+                     f"{a.features / 1e9:g}B features; "
+                     + ("zero-initialised weights" if a.init == "zero" else
+                        f"random-initialised weights, uniform (u-0.5)*{a.init_scale:g}") + ")"),
             "config": {
                 "model": f"sparse_lr_{a.features // 1_000_000}M_features",
                 "global_batch": a.batch * world,
@@ -263,6 +224,12 @@ def main(argv=None):
                                                    if getattr(engine, "pull_ahead", False)
                                                    else ")")),
                 "transport": tlabel,
+                "plane": plane.plane if not engine.fast1 else "none",
+                "xgmi_tier": plane.xgmi_tier,
+                "fell_back": plane.fell_back,
+                **({"fallback_reason": plane.fallback_reason[:300]} if plane.fell_back else {}),
+                "devices": plane.devices,
+                "init": a.init,
                 "comms": comms,
                 "rccl_nranks": rccl_n,
                 "a2a_bytes_per_step": a2a,

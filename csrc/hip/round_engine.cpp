@@ -136,6 +136,9 @@ class RoundEngine {
     bpp_ = bpp;
     timeout_ = timeout_s;
   }
+  // drop the arena pointers (the transport is closing): later N>1 stage
+  // calls fail in check_xgmi instead of launching against freed arenas
+  void clear_xgmi() { ar_.clear(); }
   void set_server_slot(int slot, std::vector<uintptr_t> p) {
     check_slot(slot);
     if (p.size() != 10) throw std::invalid_argument("set_server_slot: 10 pointers");
@@ -356,7 +359,9 @@ void bind_round_engine(py::module_& m) {
       .def("wait", &RoundEngine::wait)
       .def("recorded", &RoundEngine::recorded)
       .def("forget", &RoundEngine::forget)
-      .def("set_xgmi", &RoundEngine::set_xgmi)
+      // the engine keeps raw arena pointers: keep the arenas alive with it
+      .def("set_xgmi", &RoundEngine::set_xgmi, py::keep_alive<1, 2>())
+      .def("clear_xgmi", &RoundEngine::clear_xgmi)
       .def("set_server_slot", &RoundEngine::set_server_slot)
       .def("route_end", &RoundEngine::route_end)
       .def("pull_fast", &RoundEngine::pull_fast)

@@ -37,7 +37,6 @@ import torch.distributed as dist
 from ..ops.optim import InitConfig, Optimizer
 from ..ops.table import HbmTable
 from ..parallel.engine import PSEngine
-from ..parallel.transport import LoopbackTransport, RcclTransport, TorchDistTransport
 from ..parallel.watchdog import FailureHandler, FaultInjector, Heartbeat, Watchdog
 from ..utils import checkpoint as ck
 from ..utils.config import Config
@@ -72,7 +71,6 @@ class PSContext:
         self.workers = _ranks(cfg.get("worker_ranks"), self.world)
         self.is_server = self.rank in self.servers
         self.is_worker = self.rank in self.workers
-        ct = pt = None
         store = None
         if self.world > 1:
             from ..parallel.transport import default_gloo_ifname
@@ -85,56 +83,22 @@ class PSContext:
                 dist.init_process_group("gloo", rank=self.rank, world_size=self.world,
                                         timeout=datetime.timedelta(seconds=timeout))
             store = dist.distributed_c10d._get_default_store()
-            kind = cfg.get("transport", "auto")
-            if kind in ("auto", "xgmi"):
-                # device-side-count mailboxes over xGMI (parallel/xgmi.py),
-                # laid out and self-tested when the engine is built below
-                from ..parallel.xgmi import XgmiTransport
-
-                tr = XgmiTransport(self.rank, self.world, self.device, store,
-                                   aux=TorchDistTransport())
-            elif kind == "rccl":
-                from ..parallel.transport import rccl_comms_mode
-
-                three = rccl_comms_mode() == 3
-                tr = RcclTransport(self.rank, self.world, self.device, store=store,
-                                   prefix="ss_data", serial=not three)
-                if three:
-                    ct = RcclTransport(self.rank, self.world, self.device, store=store,
-                                       prefix="ss_counts", serial=False)
-                    pt = RcclTransport(self.rank, self.world, self.device, store=store,
-                                       prefix="ss_pull", serial=False)
-            else:
-                tr = TorchDistTransport()
-        else:
-            # SS_ENGINE_GENERAL: a 1-GPU job through the N>1 engine path over a
-            # size-1 mailbox arena / RCCL communicator (as bench.py)
-            general = os.environ.get("SS_ENGINE_GENERAL", "0")
-            if general == "xgmi":
-                from ..parallel.xgmi import XgmiTransport
-
-                tr = XgmiTransport(0, 1, self.device, None)
-            elif general == "rccl":
-                tr = RcclTransport(0, 1, self.device, uid=RcclTransport.new_unique_id())
-            else:
-                tr = LoopbackTransport()
-        self.transport = tr
         self.table = (HbmTable(dim, capacity, optimizer=optimizer, init=init, device=self.device,
                                row_dtype=cfg.get("row_dtype", "fp32"))
                       if self.is_server else None)
         ek = dict(max_keys=max_keys, dim=dim, frag_num=int(cfg.get("frag_num", 0) or 0),
                   server_ranks=self.servers, device=self.device)
-        try:
-            self.engine = PSEngine(self.table, tr, count_transport=ct, pull_transport=pt, **ek)
-        except RuntimeError as e:
-            if not (self.world > 1 and cfg.get("transport", "auto") == "auto"
-                    and "xgmi" in str(e)):
-                raise
-            # every rank failed the mailbox self-test together: RCCL instead
-            log.warning("%s; falling back to RCCL", e)
-            tr = RcclTransport(self.rank, self.world, self.device, store=store,
-                               prefix="ss_data")
-            self.engine = PSEngine(self.table, tr, **ek)
+        # data plane (parallel/select.py): auto = xGMI mailboxes (drain, then
+        # fenced publish, each litmus-tested on every rank) falling back to
+        # RCCL; xgmi; rccl; gloo (host-staged, tests).  World 1: loopback, or
+        # SS_ENGINE_GENERAL=xgmi|rccl (the N>1 path through a size-1 plane)
+        from ..parallel.select import build_engine
+
+        self.engine, (tr, ct, pt), self.plane = build_engine(
+            cfg.get("transport", "auto"), self.rank, self.world, self.device, store,
+            lambda tr, ct, pt: PSEngine(self.table, tr, count_transport=ct, pull_transport=pt,
+                                        **ek),
+            log=log.warning)
         self.transport = tr
         self.backup_period = int(cfg.get("param_backup_period", 0) or 0)
         self._last_backup = -1
@@ -238,6 +202,7 @@ class PSContext:
         """Per-round progress mark for the watchdog (+ fault injection point)."""
         if self.watchdog:
             self.watchdog.beat(round_idx)
+        self.engine.poll()  # a timed-out / out-of-order mailbox round raises now
         self.fault.maybe(round_idx)
 
     def barrier(self):
@@ -388,7 +353,9 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
              "loss": w.mean_loss() if ctx.is_worker else None, "hipgraph": bool(graphed),
              "start_round": ctx.start_round, "passes": passes,
              "rank0_quota": w.quota,
-             "transport": getattr(ctx.transport, "label", type(ctx.transport).__name__)}
+             "transport": getattr(ctx.transport, "label", type(ctx.transport).__name__),
+             "plane": ctx.plane.plane, "xgmi_tier": ctx.plane.xgmi_tier,
+             "fell_back": ctx.plane.fell_back, "devices": ctx.plane.devices}
     if cfg.get("model", "sparse_lr") == "word2vec" and ctx.is_worker:
         d = w.data
         stats["w2v"] = {"layout": d.mode, "neg_mode": getattr(d, "neg_mode", "shared"),

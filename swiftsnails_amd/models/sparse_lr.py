@@ -202,9 +202,20 @@ class SparseLRWorker(PipelinedWorker):
                 "logloss_truth": logloss(t, y), "samples": int(y.size)}
 
 
+def lr_init(kind: str = "zero", scale: float = 0.01) -> InitConfig:
+    """Weight initialiser of a sparse-LR table: ``zero`` (the usual LR start;
+    the table is prefilled, an insert is the key CAS alone) or ``uniform``
+    (random (u - 0.5) * scale per key, drawn from a key-seeded hash when the
+    key is inserted — the word2vec convention of vec1.h:223-226)."""
+    if kind not in ("zero", "uniform"):
+        raise ValueError("sparse LR init: zero or uniform")
+    return InitConfig("zero") if kind == "zero" else InitConfig("uniform", scale)
+
+
 def make_lr_table(num_features: int, world: int = 1, optimizer: Optional[Optimizer] = None,
-                  load: float = 0.7, device=None, capacity: Optional[int] = None) -> HbmTable:
+                  load: float = 0.7, device=None, capacity: Optional[int] = None,
+                  init: Optional[InitConfig] = None) -> HbmTable:
     """Shard sized for the whole feature space split over `world` servers."""
     opt = optimizer or Optimizer("adagrad", lr=0.05, eps=1e-8)
     cap = capacity or int(num_features / world / load) + 1024
-    return HbmTable(1, cap, optimizer=opt, init=InitConfig("zero"), device=device)
+    return HbmTable(1, cap, optimizer=opt, init=init or InitConfig("zero"), device=device)

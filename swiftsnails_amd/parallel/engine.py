@@ -292,6 +292,8 @@ class PSEngine(HostRounds):
                                  [list(self.xg.layout("grads", 0, q)) for q in range(D)],
                                  N, self.rank, self.Pd, self.sub, cap, d, self.xg.bpp,
                                  self.xg.timeout_s)
+            # a closed transport frees its arenas: the engine forgets them first
+            self.xg._close_hooks.append(self.native.clear_xgmi)
             for q in range(D):
                 if self.srv is not None:
                     self.native.set_server_slot(q, self.srv[q].ptrs())
@@ -576,12 +578,20 @@ class PSEngine(HostRounds):
         keeps serving rounds with an empty key set until then — the
         reference's master waiting for every worker's WORKER_FINISH_WORK
         before stopping the servers (master/terminate.h:44-62)."""
+        self.poll()
         if self.world == 1:
             return bool(local_done)
         dev = self.device if (self.gpu and not hasattr(self.t, "aux")) else "cpu"
         flag = torch.tensor([1 if local_done else 0], dtype=torch.int64, device=dev)
         self.t.allreduce_(flag, "min")
         return int(flag.item()) == 1
+
+    def poll(self) -> None:
+        """Cheap per-round health check, no device sync: raises if a mailbox
+        wait has timed out or seen a stale round tag (host-mapped error
+        words of the xGMI transport)."""
+        if self.xg is not None:
+            self.xg.poll_error()
 
     def check(self) -> None:
         """Raise on a sticky device-side error (syncs): an overflowed dedup

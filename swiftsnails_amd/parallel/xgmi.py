@@ -15,10 +15,26 @@ in place, the worker reads pulled rows in place.
 
 The same code runs with every rank on ONE GPU (the IPC mappings are then the
 same device's memory), which is how the peer data path is exercised on a
-1-GPU box (tests/test_gpu_multiproc.py).  ``setup`` ends with a self-test —
-every rank puts a rank-stamped pattern to every peer and checks what
-arrived — so a fabric that cannot map or order peer stores fails at start-up
-(bench.py then falls back to RCCL), never mid-training.
+1-GPU box (tests/test_gpu_multiproc.py).
+
+Fail-safe start-up (``setup``): the arenas are mapped, then a message-passing
+LITMUS runs on the real arenas — every (channel, slot) arena, full-size
+segments of every part, the production put geometry, ``2 x depth`` rounds
+reusing the slots, each round's words stamped with (round, source,
+destination, channel, part) and checked word by word by the receiver — once
+per publish tier, in order:
+
+  ``drain``  — fence-free (drained uncached stores, relaxed flag add);
+  ``fenced`` — one system-scope release per put block towards arenas on
+               another device, one system-scope acquire after each wait.
+
+The first tier that passes on EVERY rank is used (``tier``); if none does,
+``setup`` raises and the caller falls back to RCCL (``select.build_engine``).
+``SS_XGMI_FORCE_TIER=fenced|rccl`` makes the earlier tiers fail on purpose
+(proves each fallback step end to end); ``SS_XGMI_VERIFY=1`` keeps checking
+at run time: every put block writes a round tag after its payload, every
+wait checks them, and a stale tag (a flag that overtook its data) sets a
+sticky error that ``poll_error`` sees without a device sync.
 
 Control-plane collectives (barrier, the start-up agreement) go through
 ``aux`` (a gloo ``TorchDistTransport``).  Reference parity:
@@ -64,6 +80,16 @@ class XgmiTransport(Transport):
         # per workgroup (16 B per lane per iteration); 32 per peer measured
         # 211 us for the 42 MB keys put of a 1-rank arena
         self.bpp = int(os.environ.get("SS_XGMI_BPP", "0")) or max(128, 1024 // self.world)
+        self.verify = os.environ.get("SS_XGMI_VERIFY", "0") not in ("0", "")
+        self.force_tier = os.environ.get("SS_XGMI_FORCE_TIER", "").strip().lower()
+        if self.force_tier not in ("", "drain", "fenced", "rccl"):
+            raise ValueError("SS_XGMI_FORCE_TIER: drain, fenced or rccl")
+        self.tier: Optional[str] = None
+        self.litmus_log: list = []   # (tier, passed, seconds, reason)
+        self.remote_mask = 0
+        self.devices = 1             # distinct devices among the ranks
+        self._channels: dict = {}
+        self._close_hooks: list = []  # engines holding arena pointers (clear_xgmi)
 
     # ------------------------------------------------------------ set-up
     def setup(self, channels: dict) -> None:
@@ -83,10 +109,11 @@ class XgmiTransport(Transport):
         h = hip()
         chans = dict(channels)
         chans["_probe"] = (1, [4096])
+        self._channels = chans
         sizes = {}
         for name, (slots, parts) in chans.items():
             for slot in range(int(slots)):
-                off = h.xgmi_flag_bytes()
+                off = h.xgmi_head_bytes()
                 for p, seg in enumerate(parts):
                     # segments keep their exact size (source s at s * seg: the
                     # consumers index [source][row]); regions start aligned
@@ -95,7 +122,9 @@ class XgmiTransport(Transport):
                     self._layout[(name, p, slot)] = (hdr, data, int(seg))
                     off = data + self.world * int(seg)
                 if _al(off) >= _MAX_ARENA:
-                    raise ValueError(f"xgmi: the {name} mailbox of one round needs "
+                    # a RuntimeError like every other set-up failure: callers
+                    # fall back to RCCL on it
+                    raise RuntimeError(f"xgmi: the {name} mailbox of one round needs "
                                      f"{_al(off) / 2**30:.2f} GiB (< 2 GiB per IPC allocation)")
                 sizes[(name, slot)] = _al(off)
         self.bytes = sum(sizes.values())
@@ -117,9 +146,133 @@ class XgmiTransport(Transport):
         if err is None:
             self._errs = [torch.utils.dlpack.from_dlpack(h.dlpack_view(a.err_ptr, [2], 0, 32, dev))
                           for a in self.arenas.values()]
-        self._selftest(err)
+        self._peer_devices(h, dev)
+        self._select_tier(err)
 
-    def _allgather_bytes(self, mine: bytes, tag: int = 0) -> list:
+    # ------------------------------------------------------------ tiers
+    TIERS = ("drain", "fenced")
+
+    def _peer_devices(self, h, dev: int) -> None:
+        """Which ranks' arenas live on another device (the fenced tier
+        releases only towards those), and how many distinct devices the job
+        spans.  SS_XGMI_FENCE_ALL=1 treats every peer as remote (tests of
+        the fenced tier with all ranks on one GPU)."""
+        try:
+            mine = h.device_pci_id(dev).encode()
+        except Exception:  # pragma: no cover - hardware dependent
+            mine = f"dev{dev}".encode()
+        ids = self._allgather_bytes(mine, "pci")
+        self.devices = len(set(ids))
+        fence_all = os.environ.get("SS_XGMI_FENCE_ALL", "0") not in ("0", "")
+        self.remote_mask = sum(1 << r for r, x in enumerate(ids)
+                               if r != self.rank and (fence_all or x != mine))
+
+    def _set_tier(self, tier: str) -> None:
+        t = self.TIERS.index(tier)
+        for a in self.arenas.values():
+            a.set_tier(t, self.remote_mask, self.verify)
+
+    def _select_tier(self, err: Optional[Exception]) -> None:
+        """Run the litmus per tier; keep the first that passes on every rank
+        (all ranks see the same agreed results, so all pick the same tier or
+        all raise)."""
+        import time
+
+        if err is not None:
+            self._agree_ok(False)
+            raise RuntimeError(f"xgmi set-up failed on this rank: {err}")
+        reasons = []
+        for tier in self.TIERS:
+            self._set_tier(tier)
+            forced = self.force_tier == "rccl" or (self.force_tier == "fenced" and tier == "drain")
+            t0 = time.perf_counter()
+            ok, why = self._litmus(fail=forced)
+            ok = self._agree_ok(ok)
+            dt = time.perf_counter() - t0
+            self.litmus_log.append((tier, ok, round(dt, 3), "" if ok else (why or "a peer failed")))
+            if ok:
+                self.tier = tier
+                return
+            reasons.append(f"{tier}: {why or 'a peer failed'}")
+            if why == "timeout":
+                break  # the arrival counters are no longer in step: no retry
+        raise RuntimeError("xgmi litmus failed on every tier (" + "; ".join(reasons) + ")")
+
+    def _agree_ok(self, ok: bool) -> bool:
+        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+        if self.aux is not None and self.world > 1:
+            self.aux.allreduce_(flag, "min")
+        return int(flag.item()) == 1
+
+    @staticmethod
+    def _seed(rnd: int, src: int, dst: int, ch: int, part: int) -> int:
+        x = (rnd * 0x9E3779B1 + src * 0x85EBCA77 + dst * 0xC2B2AE3D + ch * 0x27D4EB2F +
+             part * 0x165667B1 + 0x5BD1E995)
+        return x & 0xFFFFFFFF
+
+    def _litmus(self, fail: bool = False):
+        """Message-passing litmus on the real arenas (see the module doc).
+        Returns (passed on this rank, reason)."""
+        from .._native import hip
+
+        h = hip()
+        N, me, dev = self.world, self.rank, self.device
+        st = torch.cuda.current_stream(dev)
+        names = sorted(self._channels)
+        rounds = max(2, 2 * max(int(sl) for sl, _ in self._channels.values()))
+        bad = torch.zeros(1, dtype=torch.int32, device=dev)
+        cnt_bad = torch.zeros(1, dtype=torch.int64, device=dev)
+        srcs = {}
+        for ci, name in enumerate(names):
+            for p, seg in enumerate(self._channels[name][1]):
+                if int(seg) % 4:
+                    return False, f"segment of {name}/{p} not whole words"
+                srcs[(name, p)] = torch.empty(N * int(seg) // 4, dtype=torch.int32, device=dev)
+        try:
+            for rnd in range(rounds):
+                for ci, name in enumerate(names):
+                    slots, parts = self._channels[name]
+                    slot = rnd % int(slots)
+                    spec = []
+                    for p, seg in enumerate(parts):
+                        w = int(seg) // 4
+                        src = srcs[(name, p)]
+                        for d in range(N):
+                            h.xgmi_pattern(src.data_ptr() + 4 * d * w, w,
+                                           self._seed(rnd, me, d, ci, p), st.cuda_stream)
+                        full = torch.full((N,), w, dtype=torch.int64, device=dev)
+                        spec.append((src, [d * w for d in range(N)], full, None))
+                        srcs[(name, p, "cnt")] = full  # alive until the put ran
+                    self.put(name, slot, spec, stream=st)
+                    self.wait(name, slot, stream=st)
+                    for p, seg in enumerate(parts):
+                        w = int(seg) // 4
+                        got = self.region(name, p, slot, torch.int32)
+                        for s_ in range(N):
+                            h.xgmi_check(got.data_ptr() + 4 * s_ * w, w,
+                                         self._seed(rnd, s_, me, ci, p), bad.data_ptr(),
+                                         st.cuda_stream)
+                        cnt_bad += (self.counts(name, p, slot) != w).sum()
+                # no rank rewrites a slot before every receiver checked it
+                st.synchronize()
+                if self.aux is not None and N > 1:
+                    self.aux.barrier()
+            st.synchronize()
+        except Exception as e:  # pragma: no cover - hardware dependent
+            return False, f"exception: {e}"
+        errs = [int(e[0].item()) for e in self._errs]
+        if any(e & 1 for e in errs):
+            return False, "timeout"
+        if any(e for e in errs):
+            return False, f"error word {max(errs)}"
+        nb, nc = int(bad.item()), int(cnt_bad.item())
+        if nb or nc:
+            return False, f"{nb} words and {nc} counts wrong"
+        if fail:
+            return False, "forced (SS_XGMI_FORCE_TIER)"
+        return True, ""
+
+    def _allgather_bytes(self, mine: bytes, tag=0) -> list:
         if self.world == 1:
             return [mine]
         self.store.set(f"{self.prefix}_h{tag}_{self.rank}", mine)
@@ -159,36 +312,6 @@ class XgmiTransport(Transport):
             if self.world > 1:
                 self.store.set(key, b"1")
         return err
-
-    def _selftest(self, err: Optional[Exception] = None) -> None:
-        """Every rank puts (rank, peer)-stamped words to every peer; each
-        checks what arrived, and all ranks agree before the transport is
-        used (a failure raises on every rank)."""
-        N, me = self.world, self.rank
-        if err is not None:
-            flag = torch.zeros(1, dtype=torch.int64)
-            if self.aux is not None and N > 1:
-                self.aux.allreduce_(flag, "min")
-            raise RuntimeError(f"xgmi set-up failed on this rank: {err}")
-        src = torch.empty((N, 1024), dtype=torch.int32, device=self.device)
-        for d in range(N):
-            src[d] = me * 1000003 + d * 7919 + torch.arange(1024, dtype=torch.int32,
-                                                            device=self.device)
-        st = torch.cuda.current_stream(self.device)
-        self.put("_probe", 0, [(src, [d * 1024 for d in range(N)], None, 1024)], stream=st)
-        self.wait("_probe", 0, stream=st)
-        got = self.region("_probe", 0, 0, torch.int32).view(N, -1)[:, :1024].clone()
-        cnt = self.counts("_probe", 0, 0).clone()
-        st.synchronize()
-        exp = torch.stack([s * 1000003 + me * 7919 + torch.arange(1024, dtype=torch.int32)
-                           for s in range(N)])
-        ok = bool(torch.equal(got.cpu(), exp)) and bool((cnt.cpu() == 1024).all()) and \
-            all(int(e[0].item()) == 0 for e in self._errs)
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
-        if self.aux is not None and N > 1:
-            self.aux.allreduce_(flag, "min")
-        if int(flag.item()) != 1:
-            raise RuntimeError(f"xgmi self-test failed on {'this rank' if not ok else 'a peer'}")
 
     # ------------------------------------------------------------ data plane
     def arena_of(self, ch: str, slot: int):
@@ -265,6 +388,30 @@ class XgmiTransport(Transport):
                 raise RuntimeError(f"xgmi: a peer did not arrive within {self.timeout_s} s")
             if v & 2:
                 raise RuntimeError("xgmi: a put exceeded its segment (counts corrupt)")
+            if v & 4:
+                raise RuntimeError("xgmi: a round tag was stale when its flag arrived "
+                                   f"(publish ordering failed on tier {self.tier})")
+
+    def poll_error(self) -> None:
+        """Raise if a wait kernel has flagged an error (timeout, stale round
+        tag): reads the host-mapped error words, no device sync — cheap
+        enough for every round (engine.all_done, the bench loop)."""
+        v = 0
+        for a in self.arenas.values():
+            v |= int(a.host_err())
+        if v & 1:
+            raise RuntimeError(f"xgmi: a peer did not arrive within {self.timeout_s} s "
+                               "(SS_XGMI_TIMEOUT)")
+        if v & 4:
+            raise RuntimeError("xgmi: a round tag was stale when its flag arrived "
+                               f"(publish ordering failed on tier {self.tier})")
+
+    def describe(self) -> dict:
+        """What the start-up chose: tier, litmus results, distinct devices."""
+        return {"xgmi_tier": self.tier, "devices": self.devices,
+                "xgmi_verify": bool(self.verify),
+                "litmus": [{"tier": t, "passed": ok, "s": dt, **({"why": w} if w else {})}
+                           for t, ok, dt, w in self.litmus_log]}
 
     # ------------------------------------------------------------ control plane
     def exchange_counts(self, send_counts):
@@ -287,4 +434,8 @@ class XgmiTransport(Transport):
     def close(self) -> None:
         if self.arenas:
             torch.cuda.synchronize(self.device)
+        for f in getattr(self, "_close_hooks", []):
+            f()
+        self._close_hooks = []
+        self._errs = []
         self.arenas = {}

@@ -80,6 +80,16 @@ KNOBS: dict[str, Knob] = {
                             "error raised at the next check point)"),
     "SS_XGMI_BPP": Knob("max(128, 1024 / world)", "parallel/xgmi.py", "tuning",
                         "workgroups per peer of a mailbox put"),
+    "SS_XGMI_VERIFY": Knob("0", "parallel/xgmi.py, csrc/hip/xgmi.hip", "ops",
+                           "1: every put block writes a round tag after its payload, every "
+                           "wait checks all tags (a flag that overtook its data raises at the "
+                           "next round's poll)"),
+    "SS_XGMI_FORCE_TIER": Knob("(none)", "parallel/xgmi.py", "ops",
+                               "fenced: fail the drain tier's litmus on purpose; rccl: fail both "
+                               "xGMI tiers (proves each step of the fallback chain)"),
+    "SS_XGMI_FENCE_ALL": Knob("0", "parallel/xgmi.py", "ops",
+                              "1: the fenced tier releases towards every peer, also peers on "
+                              "the same device (tests of the tier with all ranks on one GPU)"),
     # -- experiments (measured slower or neutral; kept for re-measurement)
     "SS_ENGINE_GENERAL": Knob("0", "parallel/engine.py, bench.py", "experiment",
                               "run a 1-GPU job through the N>1 path (1: loopback, rccl: a size-1 "

@@ -111,6 +111,32 @@ def test_xgmi_arenas_stay_below_the_ipc_limit():
     from swiftsnails_amd.parallel.xgmi import XgmiTransport
 
     t = XgmiTransport(0, 8, torch.device("cuda", 0), None)
-    with pytest.raises(ValueError, match="2 GiB"):
+    with pytest.raises(RuntimeError, match="2 GiB"):
         t.setup({"keys": (4, [10_223_616 * 8 * 4])})
     assert 8 * 10_223_616 * 8 < (2 << 30)
+
+
+def test_auto_plane_falls_back_when_the_mailbox_layout_is_refused(monkeypatch):
+    """transport=auto: a mailbox set-up failure (here the 2 GiB IPC limit)
+    closes the xGMI transport and builds the engine on the fallback plane,
+    and the PlaneInfo says so (bench.py / the launcher report it)."""
+    from swiftsnails_amd.parallel import select
+    from swiftsnails_amd.parallel.transport import LoopbackTransport
+    from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+    monkeypatch.setenv("SS_ENGINE_GENERAL", "xgmi")
+    monkeypatch.setattr(select, "_rccl_fallback", lambda *a: LoopbackTransport())
+    built = []
+
+    def make_engine(tr, ct, pt):
+        built.append(tr)
+        if isinstance(tr, XgmiTransport):
+            tr.setup({"keys": (4, [10_223_616 * 8 * 4 * 8])})
+        return "engine"
+
+    eng, (tr, ct, pt), info = select.build_engine("auto", 0, 1, "cpu", None, make_engine)
+    assert eng == "engine" and isinstance(tr, LoopbackTransport)
+    assert isinstance(built[0], XgmiTransport) and built[0].arenas == {}
+    assert info.fell_back and "2 GiB" in info.fallback_reason and info.plane == "loopback"
+    with pytest.raises(RuntimeError, match="2 GiB"):  # transport=xgmi: no fallback
+        select.build_engine("xgmi", 0, 1, "cpu", None, make_engine)

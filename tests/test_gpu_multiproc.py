@@ -29,7 +29,8 @@ def _free_port():
     return p
 
 
-def _run_rank(rank, world, init, servers, workers, opt_kind, transport, q):
+def _run_rank(rank, world, init, servers, workers, opt_kind, transport, q, env=None):
+    os.environ.update(env or {})
     init_gloo(init, rank, world)
     try:
         from swiftsnails_amd.ops.optim import InitConfig, Optimizer
@@ -67,20 +68,23 @@ def _run_rank(rank, world, init, servers, workers, opt_kind, transport, q):
             eng.push(r)
         torch.cuda.synchronize()
         eng.check()
+        eng.poll()
         if hasattr(tr, "check"):
             tr.check()
         state = table.to_dict(with_state=True) if table is not None else {}
+        if hasattr(tr, "describe"):
+            pulled["_plane"] = tr.describe()
         q.put((rank, pulled, state))
     finally:
         dist.destroy_process_group()
 
 
-def _run(world, servers, workers, opt, transport):
+def _run(world, servers, workers, opt, transport, env=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     init = file_init()
     procs = [ctx.Process(target=_run_rank,
-                         args=(r, world, init, servers, workers, opt, transport, q))
+                         args=(r, world, init, servers, workers, opt, transport, q, env))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -94,10 +98,11 @@ def _run(world, servers, workers, opt, transport):
         pytest.skip("RCCL refused 2 ranks on one GPU: " + str([r[2] for r in res if r[1] == "skip"]))
     for p in procs:
         assert p.exitcode == 0
-    merged, pulled = {}, {}
+    merged, pulled, planes = {}, {}, []
     for rank, pl, st in res:
         assert not (set(st) & set(merged))
         merged.update(st)
+        planes.append(pl.pop("_plane", None))
         pulled.update(pl)
     ref_state, ref_pulled = _oracle(world, workers, opt)
     assert set(merged) == set(ref_state)
@@ -105,6 +110,7 @@ def _run(world, servers, workers, opt, transport):
         np.testing.assert_allclose(merged[k], ref_state[k], rtol=3e-5, atol=3e-6)
     for key, v in ref_pulled.items():
         np.testing.assert_allclose(pulled[key], v, rtol=3e-5, atol=3e-6)
+    return planes
 
 
 @pytest.mark.parametrize("world,servers,workers,opt", [
@@ -219,8 +225,11 @@ def test_bench_script_multi_gpu(world, transport):
                                 "--features", "10000000", "--transport", transport])
     assert j["n_gpus"] == world and j["value"] > 0
     assert j["config"]["parallelism"].startswith(f"ps{world}")
+    assert j["config"]["devices"] == world
     if transport == "rccl":
-        assert j["config"]["rccl_nranks"] == world
+        assert j["config"]["rccl_nranks"] == world and j["config"]["plane"] == "rccl"
+    else:  # auto: the mailboxes ran (no silent fallback to RCCL)
+        assert j["config"]["plane"] == "xgmi" and not j["config"]["fell_back"], j["config"]
 
 
 def test_bench_script_world2_gloo_rehearsal():
@@ -300,6 +309,8 @@ def test_bench_script_world2_xgmi_one_gpu():
     assert j["n_gpus"] == 2 and j["value"] > 0
     c = j["config"]
     assert c["transport"].startswith("xGMI"), c["transport"]
+    assert c["plane"] == "xgmi" and c["xgmi_tier"] == "drain" and not c["fell_back"]
+    assert c["devices"] == 1
     assert c["server_unique_keys_per_step"] > 0
     assert c["server_unique_keys_per_step"] <= c["unique_recv_per_step"]
     assert c["a2a_bytes_per_step"] > 0
