@@ -68,6 +68,8 @@ def main(argv=None):
     ap.add_argument("--init", default="zero", choices=["zero", "uniform"],
                     help="weight initialiser of the table")
     ap.add_argument("--init-scale", type=float, default=0.01)
+    ap.add_argument("--cal-steps", type=int, default=6,
+                    help="N>1: timed steps per mode of the pull-ahead calibration (0: off)")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -137,9 +139,17 @@ def main(argv=None):
         if world > 1:
             dist.barrier()
 
+    # SS_FAULT=delay:<rank>:<ms>: a straggler rank (sleeps every step)
+    from swiftsnails_amd.parallel.watchdog import FaultInjector
+
+    fault = FaultInjector(rank=rank)
     for i in range(a.warmup):
+        fault.maybe(i)
         worker.step()
         wd.beat(i)
+    # N>1 (SS_PULL_AHEAD=auto): time synchronous vs pulled-ahead rounds on
+    # the live world and keep the faster (untimed; reported as "calibration")
+    cal = worker.calibrate_pull_ahead(a.cal_steps) if a.cal_steps > 0 else {}
     # hipGraph replays of the whole step (captured here, outside the timed
     # region; the data generator then reads its step from a device counter)
     graphed = False
@@ -166,6 +176,7 @@ def main(argv=None):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
+        fault.maybe(a.warmup + i)
         worker.step()
         wd.beat(i)  # one attribute store: no measurable cost
     torch.cuda.synchronize()
@@ -220,9 +231,12 @@ def main(argv=None):
                 "global_batch": a.batch * world,
                 "seq_len": a.fields,
                 "parallelism": f"ps{world}" + (" (colocated worker + server shard per GPU"
-                                                + (", pull-ahead staleness 1)"
+                                                + (f", pull-ahead staleness {engine.lookahead})"
                                                    if getattr(engine, "pull_ahead", False)
                                                    else ")")),
+                "pull_ahead": bool(getattr(engine, "pull_ahead", False)),
+                "staleness": engine.lookahead if getattr(engine, "pull_ahead", False) else 0,
+                **({"calibration": cal} if cal else {}),
                 "transport": tlabel,
                 "plane": plane.plane if not engine.fast1 else "none",
                 "xgmi_tier": plane.xgmi_tier,

@@ -244,6 +244,21 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
     const uint32_t sl = park[q] == 0xFFFFu ? kSrvInv : park[q];
     luid[p0 + q] = sl == kSrvInv || sl >= ts ? kSrvInv : lid[sl];
   }
+  // an overflowed bucket (error flagged above): the positions past the LDS
+  // parking area still get an in-range pj and no local id, so the fill and
+  // merge kernels (which walk [p0, p1)) write zero rows to real positions and
+  // skip the gradients instead of reading / writing through unset entries
+  const uint32_t nall = p1 - p0, nflat = so[R.nsrc];
+  for (uint32_t f = n + t; f < nall; f += kSrvDT) {
+    uint32_t pos = 0u;
+    if (f < nflat) {
+      int s = 0;
+      while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
+      pos = (uint32_t)(sa[s] + (f - so[s]));
+    }
+    pj[p0 + f] = pos;
+    luid[p0 + f] = kSrvInv;
+  }
 }
 
 // lanes per row for rows of n 16-byte chunks: the next power of two, <= 64

@@ -307,6 +307,12 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     log_every = log_every or int(cfg.get("log_every", 0) or 0)
     for _ in range(warmup if passes is None else 0):
         w.step()
+    # N>1, SS_PULL_AHEAD=auto: keep whichever of synchronous / pulled-ahead
+    # rounds runs faster on this world (synthetic data only: the calibration
+    # steps consume batches)
+    cal = {}
+    if passes is None and warmup > 0 and int(cfg.get("calibrate_steps", 6) or 0) > 0 and w.active:
+        cal = w.calibrate_pull_ahead(int(cfg.get("calibrate_steps", 6)))
     # config `graph: 1`: replay the step as hipGraphs (1 GPU, synthetic data;
     # a no-op where unsupported — see PipelinedWorker.enable_graph)
     graphed = str(cfg.get("graph", "0")) not in ("0", "false", "") and w.enable_graph()
@@ -354,6 +360,8 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
              "start_round": ctx.start_round, "passes": passes,
              "rank0_quota": w.quota,
              "transport": getattr(ctx.transport, "label", type(ctx.transport).__name__),
+             "pull_ahead": bool(getattr(ctx.engine, "pull_ahead", False)),
+             "calibration": cal,
              "plane": ctx.plane.plane, "xgmi_tier": ctx.plane.xgmi_tier,
              "fell_back": ctx.plane.fell_back, "devices": ctx.plane.devices}
     if cfg.get("model", "sparse_lr") == "word2vec" and ctx.is_worker:

@@ -12,8 +12,10 @@ non-worker contributes zero keys.
 """
 from __future__ import annotations
 
+import collections
 import gc
 import os
+import time
 from typing import Optional
 
 import torch
@@ -27,7 +29,9 @@ class PipelinedWorker:
         self.loss_sum = loss_buffer(engine.device)
         self.step_idx = 0
         self._next = None
-        self._cur = None
+        # pull-ahead: rounds pulled ahead of the one computing (round i at
+        # the head, up to i + lookahead - 1), oldest first
+        self._pulled: collections.deque = collections.deque()
         self._empty = torch.empty(0, dtype=torch.int64, device=engine.device)
         # hipGraph mode (enable_graph): one captured graph per ring phase
         self._graphs = None
@@ -118,7 +122,7 @@ class PipelinedWorker:
             self.step()  # prime the lookahead pipeline eagerly
         torch.cuda.synchronize()
         self._gstep = torch.full((1,), self.step_idx, dtype=torch.int64, device=eng.device)
-        saved = (self.step_idx, self._next, self._cur, eng._next_slot, eng.rounds)
+        saved = (self.step_idx, self._next, list(self._pulled), eng._next_slot, eng.rounds)
         # steps per graph: `depth` (default: one graph holding a whole ring
         # period, steps inside it overlap across their boundaries; a replay
         # advances `depth` steps) or 1 (SS_GRAPH_STEPS=1: one graph per ring
@@ -167,7 +171,8 @@ class PipelinedWorker:
         self._gper = per
         # the captures only recorded: the device is where it was before them,
         # and after `depth` steps the Python-side pipeline state is periodic
-        self.step_idx, self._next, self._cur, eng._next_slot, eng.rounds = saved
+        self.step_idx, self._next, pulled, eng._next_slot, eng.rounds = saved
+        self._pulled = collections.deque(pulled)
         self._graphs, self._gbase = graphs, self.step_idx
         return True
 
@@ -187,7 +192,8 @@ class PipelinedWorker:
 
     def _step_eager(self) -> torch.Tensor:
         eng = self.engine
-        if getattr(eng, "pull_ahead", False):
+        # pull-ahead, or draining it after it was switched off
+        if getattr(eng, "pull_ahead", False) or self._pulled:
             return self._step_pull_ahead()
         r = self._next if self._next is not None else self._route(self.step_idx)
         self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
@@ -201,29 +207,90 @@ class PipelinedWorker:
         return self.loss_sum
 
     def _step_pull_ahead(self) -> torch.Tensor:
-        """Round i computes/pushes on the main stream while round i+1 is
-        pulled and round i+2 routed on the side streams (staleness 1)."""
+        """Round i computes/pushes on the main stream while rounds i+1 ..
+        i+L are pulled (L = engine.lookahead, the staleness bound) and round
+        i+L+1 routed on the side streams.  Switched off, the pipeline drains:
+        the pulled rounds compute and push without new pulls, then the
+        synchronous pipeline continues from the routed round i+L."""
         eng = self.engine
-        if self._cur is None:  # bootstrap the pipeline
+        ahead = bool(eng.pull_ahead)
+        if ahead and not self._pulled:  # (re)start: rounds i .. i+L-1 pulled, i+L routed
+            L = max(1, int(getattr(eng, "lookahead", 1)))
             r = self._next if self._next is not None else self._route(self.step_idx)
-            self._cur = eng.pull_ahead_round(r)
-            self._next = self._route(self.step_idx + 1)
-        rnd = self._cur
+            self._pulled.append(eng.pull_ahead_round(r))
+            for j in range(1, L):
+                self._pulled.append(eng.pull_ahead_round(self._route(self.step_idx + j)))
+            self._next = self._route(self.step_idx + L)
+        rnd = self._pulled.popleft()
         eng.begin(rnd)
         self._zero_acc()
         if self.has_data(self.step_idx):
             with eng.trace("compute"):
                 self._compute(rnd, rnd.slot, eng.raw_stream())
-        # round i+1's pull is enqueued before round i's push: with one comm
+        # round i+L's pull is enqueued before round i's push: with one comm
         # stream (RCCL, SS_RCCL_COMMS=1) its exchanges then go ahead of round
         # i's gradients instead of waiting behind round i's compute.  (Issuing
         # route i+2 and pull i+1 before round i's compute measured no better:
         # word2vec one GPU 0.097 -> 0.111 ms/step, N>1 path 0.171 -> 0.167)
-        self._cur = eng.pull_ahead_round(self._next)
+        if ahead:
+            self._pulled.append(eng.pull_ahead_round(self._next))
         eng.push(rnd)
-        self._next = self._route(self.step_idx + 2)
+        if ahead:
+            self._next = self._route(self.step_idx + 1 + len(self._pulled))
         self.step_idx += 1
         return self.loss_sum
+
+    def set_pull_ahead(self, on: bool) -> bool:
+        """Switch between pulled-ahead (bounded staleness) and synchronous
+        rounds between steps.  Off: the rounds already pulled drain over the
+        next steps (they still train).  Returns the engine's mode."""
+        eng = self.engine
+        if on:
+            return eng.enable_pull_ahead(True, force=True)
+        eng.enable_pull_ahead(False)
+        return False
+
+    def drain(self) -> None:
+        """Run steps until no pulled-ahead round is outstanding (the engine
+        then is in a synchronous state)."""
+        while self._pulled and not self.engine.pull_ahead:
+            self.step()
+
+    def calibrate_pull_ahead(self, steps: int = 6) -> dict:
+        """SS_PULL_AHEAD=auto at N>1: time ``steps`` synchronous and ``steps``
+        pulled-ahead steps on the live world (max over ranks) and keep the
+        faster mode.  On one GPU shared by all ranks there is no cross-device
+        wait to hide and the synchronous snapshot update wins; across real
+        xGMI links the keys -> rows chain of the next round can hide behind
+        this round's compute.  Returns the choice and both timings (ms per
+        step), {} where it does not apply (one-GPU path, host-count
+        transports without a pull stream, SS_PULL_AHEAD=0/1, SS_STALENESS=0)."""
+        eng = self.engine
+        if not (getattr(eng, "gpu", False) and getattr(eng, "dist", False) and eng.depth >= 3
+                and os.environ.get("SS_PULL_AHEAD", "auto") == "auto"
+                and getattr(eng, "lookahead", 1) > 0 and self._graphs is None
+                and os.environ.get("SS_STALENESS", "1") != "0"):
+            return {}
+        times = {}
+        for mode in (False, True):
+            self.set_pull_ahead(mode)
+            self.drain()
+            for _ in range(2):  # settle: the (re)started pipeline
+                self.step()
+            torch.cuda.synchronize(eng.device)
+            eng.barrier()
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                self.step()
+            torch.cuda.synchronize(eng.device)
+            eng.barrier()
+            times[mode] = eng.max_over_ranks(time.perf_counter() - t0) / steps
+        best = times[True] < times[False]
+        self.set_pull_ahead(best)
+        self.drain()
+        return {"pull_ahead": best, "staleness": eng.lookahead if best else 0,
+                "sync_ms": round(1e3 * times[False], 4), "ahead_ms": round(1e3 * times[True], 4),
+                "steps_per_mode": steps + 2}
 
     def rounds_done(self) -> int:
         """Rounds whose pushes have been enqueued on the device.  Eagerly
@@ -239,3 +306,51 @@ class PipelinedWorker:
     def mean_loss(self) -> float:
         n = self.samples_per_step()
         return float(self.loss_sum.sum().item()) / n if n else 0.0
+
+
+EVAL_STEP = 1 << 28  # held-out sample range of the synthetic CTR generators
+
+
+def evaluate_ctr(worker, batches: int, logits) -> dict:
+    """Held-out metrics of a CTR model (sparse LR, FM) on fresh synthetic
+    batches: AUC / log-loss of the learned logits and of the planted
+    ground-truth logits the labels were drawn from (the Bayes-optimal
+    reference).  Reads the table without inserting (unseen keys read zero).
+    World > 1: a COLLECTIVE — every rank calls it; each worker rank scores
+    its own held-out samples through ``PSEngine.lookup`` (the read-only pull
+    from every shard) and the metrics are over all ranks' samples.
+    ``logits(rows [B*F, D], B, F)`` -> [B] tensor."""
+    import numpy as np
+
+    from ..models.ctr_data import truth_weight
+    from ..utils.metrics import auc, logloss
+
+    eng, d = worker.engine, worker.data
+    dev = eng.device
+    B, F = d.batch_size, d.num_fields
+    keys = torch.empty(B * F, dtype=torch.int64, device=dev)
+    labels = torch.empty(B, dtype=torch.float32, device=dev)
+    empty = torch.empty(0, dtype=torch.int64, device=dev)
+    zs, zt, ys = [], [], []
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)  # the route stream may still be producing
+    for b in range(batches):
+        if not worker.active:
+            eng.lookup(empty)  # a pure server still answers the round
+            continue
+        d.generate(EVAL_STEP + b, worker.rank, worker.world, keys, labels)
+        rows = eng.lookup(keys)
+        zs.append(logits(rows, B, F).float().cpu().numpy())
+        k = keys.cpu().numpy().view(np.uint64)
+        zt.append(truth_weight(k, d.truth_scale).reshape(B, F).sum(1) + d.truth_bias)
+        ys.append(labels.cpu().numpy())
+    cat = (lambda xs: np.concatenate(xs) if xs else np.zeros(0))  # noqa: E731
+    z, t, y = cat(zs), cat(zt), cat(ys)
+    if worker.world > 1:
+        import torch.distributed as dist
+
+        parts = [None] * worker.world
+        dist.all_gather_object(parts, (z, t, y))
+        z, t, y = (np.concatenate([p[i] for p in parts]) for i in range(3))
+    return {"auc": auc(z, y), "logloss": logloss(z, y), "auc_truth": auc(t, y),
+            "logloss_truth": logloss(t, y), "samples": int(y.size)}

@@ -22,7 +22,7 @@ import torch
 from .._native import hip
 from ..ops.optim import InitConfig, Optimizer
 from ..ops.table import HbmTable
-from .base import PipelinedWorker
+from .base import PipelinedWorker, evaluate_ctr
 from .sparse_lr import CtrSynth
 
 
@@ -101,34 +101,12 @@ class FMWorker(PipelinedWorker):
     def samples_per_step(self) -> int:
         return self.data.batch_size if self.active else 0
 
-    EVAL_STEP = 1 << 28  # held-out sample range of the synthetic generator
-
     def evaluate(self, batches: int = 1) -> dict:
-        """Held-out metrics on fresh synthetic batches: AUC / log-loss of the
-        learned FM logits and the AUC of the planted ground-truth logits the
-        labels were drawn from (the Bayes-optimal reference).  Reads the table
-        without inserting (unseen keys contribute zero).  World 1."""
-        if self.world != 1 or self.engine.table is None:
-            raise NotImplementedError("evaluate() reads the local shard: world 1 only")
-        from ..models.ctr_data import truth_weight
-        from ..utils.metrics import auc, logloss
-
-        d, dev, D = self.data, self.engine.device, self.engine.dim
-        B, F = d.batch_size, d.num_fields
-        keys = torch.empty(B * F, dtype=torch.int64, device=dev)
-        labels = torch.empty(B, dtype=torch.float32, device=dev)
-        zs, zt, ys = [], [], []
-        torch.cuda.synchronize()
-        for b in range(batches):
-            d.generate(self.EVAL_STEP + b, 0, 1, keys, labels)
-            rows, _ = self.engine.table.pull(keys, insert=False)
-            zs.append(fm_logits(rows.view(B, F, D)).cpu().numpy())
-            k = keys.cpu().numpy().view(np.uint64)
-            zt.append(truth_weight(k, d.truth_scale).reshape(B, F).sum(1) + d.truth_bias)
-            ys.append(labels.cpu().numpy())
-        z, t, y = np.concatenate(zs), np.concatenate(zt), np.concatenate(ys)
-        return {"auc": auc(z, y), "logloss": logloss(z, y), "auc_truth": auc(t, y),
-                "logloss_truth": logloss(t, y), "samples": int(y.size)}
+        """Held-out AUC / log-loss of the FM logits vs the planted ground
+        truth (models/base.py evaluate_ctr; unseen keys contribute zero).
+        World > 1: collective, over every shard (read-only pull)."""
+        D = self.engine.dim
+        return evaluate_ctr(self, batches, lambda rows, B, F: fm_logits(rows.view(B, F, D)))
 
 
 def fm_logits(rows: torch.Tensor) -> torch.Tensor:

@@ -26,7 +26,7 @@ import torch
 from .._native import hip
 from ..ops.optim import InitConfig, Optimizer
 from ..ops.table import HbmTable
-from .base import PipelinedWorker
+from .base import PipelinedWorker, evaluate_ctr
 
 
 @dataclass
@@ -171,35 +171,11 @@ class SparseLRWorker(PipelinedWorker):
     def samples_per_step(self) -> int:
         return self.data.batch_size if self.active else 0
 
-    EVAL_STEP = 1 << 28  # held-out sample range of the synthetic generator
-
     def evaluate(self, batches: int = 1) -> dict:
-        """Held-out metrics of the current model on fresh synthetic batches:
-        AUC and log-loss of the learned logits, and the AUC of the planted
-        ground-truth logits (the Bayes-optimal reference).  Reads the table
-        without inserting.  One rank (world 1): a sharded model is evaluated
-        by routing through the engine, which this pipelined worker owns."""
-        if self.world != 1 or self.engine.table is None:
-            raise NotImplementedError("evaluate() reads the local shard: world 1 only")
-        from ..models.ctr_data import truth_weight
-        from ..utils.metrics import auc, logloss
-
-        d, dev = self.data, self.engine.device
-        B, F = d.batch_size, d.num_fields
-        keys = torch.empty(B * F, dtype=torch.int64, device=dev)
-        labels = torch.empty(B, dtype=torch.float32, device=dev)
-        zs, zt, ys = [], [], []
-        torch.cuda.synchronize()  # the route stream may still be producing
-        for b in range(batches):
-            d.generate(self.EVAL_STEP + b, 0, 1, keys, labels)
-            vals, _ = self.engine.table.pull(keys, insert=False)
-            zs.append(vals.view(B, F).sum(1).cpu().numpy())
-            k = keys.cpu().numpy().view(np.uint64)
-            zt.append(truth_weight(k, d.truth_scale).reshape(B, F).sum(1) + d.truth_bias)
-            ys.append(labels.cpu().numpy())
-        z, t, y = np.concatenate(zs), np.concatenate(zt), np.concatenate(ys)
-        return {"auc": auc(z, y), "logloss": logloss(z, y), "auc_truth": auc(t, y),
-                "logloss_truth": logloss(t, y), "samples": int(y.size)}
+        """Held-out AUC / log-loss of the current model vs the planted
+        ground truth (models/base.py evaluate_ctr).  World > 1: collective,
+        over every shard through the engine's read-only pull."""
+        return evaluate_ctr(self, batches, lambda rows, B, F: rows.view(B, F).sum(1))
 
 
 def lr_init(kind: str = "zero", scale: float = 0.01) -> InitConfig:

@@ -212,22 +212,28 @@ class PSEngine(HostRounds):
             self.rkeys = torch.empty(N * cap, dtype=torch.int64)
             self.rvals = torch.zeros((N * cap, d), dtype=torch.float32)
             self.rgrads = torch.empty((N * cap, d), dtype=torch.float32)
-        # pull-ahead: round i+1's pull runs on the pull stream while round i
-        # computes — bounded staleness 1; needs ring depth >= 3
-        # (rounds i, i+1, i+2 in flight).  Models opt in (FM, word2vec:
-        # enable_pull_ahead); sparse LR runs synchronous rounds at every N:
-        # measured faster with the servers' snapshot (blind-store) update
-        # than pulled ahead with a read-modify-write (one GPU through the N>1
-        # path 1.106 vs 1.12 ms; 2 / 4 xGMI ranks sharing one GPU -5 %), and
-        # no staleness.  SS_PULL_AHEAD=1 turns it on for every model at N>1
-        if self.gpu and self.dist and self.depth >= 3 and \
+        # pull-ahead (SURVEY X3 bounded staleness): rounds i+1 .. i+L are
+        # pulled on the pull stream while round i computes, L = SS_STALENESS
+        # (default 1; at most depth - 2: rounds i .. i+L pulled or pulling and
+        # i+L+1 routing fill the ring); a pulled-ahead round misses at most
+        # L rounds' updates (its pull waits for the push L+1 rounds back).
+        # SS_STALENESS=ring: one round ahead, bounded by the ring depth only;
+        # SS_STALENESS=0: synchronous rounds always.  Models opt in (FM,
+        # word2vec: enable_pull_ahead); sparse LR runs synchronous rounds
+        # (the servers' snapshot blind-store update) unless the bench /
+        # launcher calibration (SS_PULL_AHEAD=auto, PipelinedWorker.
+        # calibrate_pull_ahead) measures pull-ahead faster on the live world.
+        # SS_PULL_AHEAD=1 / 0 forces it on / off for every model at N>1
+        st_env = os.environ.get("SS_STALENESS", "1")
+        ring = st_env == "ring"
+        k = 1 if ring else max(0, int(st_env))
+        self.lookahead = max(1, min(k, self.depth - 2)) if k > 0 else 0
+        self.staleness = 0 if ring else self.lookahead  # bound the pull waits for
+        if self.dist and self.depth >= 3 and self.lookahead > 0 and \
                 os.environ.get("SS_PULL_AHEAD", "auto") == "1":
             self.pull_ahead = True
-            self.pull_stream = torch.cuda.Stream(device=self.device)
-        # a pulled-ahead round misses at most this many rounds' updates
-        # (SS_STALENESS=ring: only the ring depth bounds it)
-        st_env = os.environ.get("SS_STALENESS", "1")
-        self.staleness = 0 if st_env == "ring" else max(1, int(st_env))
+            if self.gpu:
+                self.pull_stream = torch.cuda.Stream(device=self.device)
 
     # ------------------------------------------------------------ N>1 (GPU)
     def _init_dist_gpu(self) -> None:
@@ -321,8 +327,9 @@ class PSEngine(HostRounds):
         return current(self._dix)
 
     def raw_stream(self) -> int:
-        """hipStream_t of the caller's current stream on this engine's device."""
-        return current_raw(self._dix)
+        """hipStream_t of the caller's current stream on this engine's device
+        (0 on the CPU engine)."""
+        return current_raw(self._dix) if self.gpu else 0
 
     @property
     def _tag(self) -> int:
@@ -397,7 +404,11 @@ class PSEngine(HostRounds):
     def pull_ahead_round(self, r: Routed) -> Round:
         """Stage 2 on the pull (or route) stream (pull-ahead): the Round's
         rows are ready at its pull event; ``begin(rnd)`` makes the main
-        stream wait for them."""
+        stream wait for them.  The CPU engine pulls right away (the same
+        collective order: round i+L's pull before round i's push)."""
+        if not self.gpu:
+            with self.trace("pull"):
+                return self._pull_stage(r, self.uvals[r.slot], None, ahead=True)
         ps = self.pull_stream or self.route_stream
         st = ps.cuda_stream
         if ps is not self.route_stream:
@@ -466,21 +477,37 @@ class PSEngine(HostRounds):
         self.metrics.add(occurrences=dd.n)
         return Round(dd, self.uvals[slot], slot, ready=ahead, tag=self._tag)
 
-    def enable_pull_ahead(self, on: bool = True, pull_stream: bool = False) -> bool:
-        """Opt into pull-ahead (staleness 1) where supported.  ``pull_stream``
-        (one GPU; SS_PULL_STREAM=0/1 overrides): the lookup on its own stream
-        instead of behind the dedup on the route stream — pays when it would
-        hold up the next dedup (word2vec 0.128 -> 0.125 ms/step), not when
-        the main stream is the longer one (FM 0.655 -> 0.685)."""
-        if on and self.gpu and self.depth >= 3 and \
-                os.environ.get("SS_PULL_AHEAD", "auto") != "0":
+    def enable_pull_ahead(self, on: bool = True, pull_stream: bool = False,
+                          force: bool = False) -> bool:
+        """Opt into pull-ahead (staleness ``lookahead``) where supported.
+        ``pull_stream`` (one GPU; SS_PULL_STREAM=0/1 overrides): the lookup
+        on its own stream instead of behind the dedup on the route stream —
+        pays when it would hold up the next dedup (word2vec 0.128 -> 0.125
+        ms/step), not when the main stream is the longer one (FM 0.655 ->
+        0.685).  N>1 always pulls on its own stream.  ``force``: the
+        calibration's switch (ignores SS_PULL_AHEAD=auto's model default).
+        Switching off takes effect for the next pull; rounds already pulled
+        drain (PipelinedWorker.set_pull_ahead)."""
+        env = os.environ.get("SS_PULL_AHEAD", "auto")
+        if on and (self.gpu or self.dist) and self.depth >= 3 and self.lookahead > 0 and \
+                (env != "0" or force):
             self.pull_ahead = True
             want = os.environ.get("SS_PULL_STREAM", "1" if pull_stream else "0") != "0"
-            if self.fast1 and self.pull_stream is None and want:
+            if self.gpu and self.pull_stream is None and (self.dist or want):
                 self.pull_stream = torch.cuda.Stream(device=self.device)
         elif not on:
             self.pull_ahead = False
         return self.pull_ahead
+
+    def max_over_ranks(self, value: float) -> float:
+        """max of a host float over the ranks (control plane; syncs)."""
+        if self.world == 1:
+            return float(value)
+        dev = self.device if (self.gpu and not hasattr(self.t, "aux")) else "cpu"
+        t = torch.tensor([value], dtype=torch.float32 if dev != "cpu" else torch.float64,
+                         device=dev)
+        self.t.allreduce_(t, "max")
+        return float(t.item())
 
     def begin(self, rnd: Round) -> None:
         if self.gpu:
@@ -567,6 +594,55 @@ class PSEngine(HostRounds):
             self._release(slot)
         rnd.pushed = True
         self.rounds += 1
+
+    # ------------------------------------------------------------ read-only
+    def lookup(self, keys: torch.Tensor) -> torch.Tensor:
+        """Collective READ-ONLY pull: rows [n, dim] of ``keys`` (in order)
+        from whichever shard owns each key; a key no shard holds reads as
+        zeros and is NOT inserted, and nothing is pushed — the reference's
+        pull_with_barrier of any key from every server by any worker
+        (/root/reference/src/core/parameter/global_pull_access.h:40-55), for
+        evaluating a sharded model.  Every rank calls it together (a rank
+        without keys passes an empty tensor).  It runs on the gloo control
+        plane (host-staged): an evaluation path, not a training one."""
+        keys = keys.reshape(-1)
+        if self.world == 1:
+            return self._read_rows(keys.to(self.device)).to(keys.device)
+        import torch.distributed as dist
+
+        from .router import route_keys_np
+
+        N = self.world
+        u, inv = torch.unique(keys.cpu(), return_inverse=True)
+        dest = route_keys_np(u.numpy().view(np.uint64), self.frag_map) if len(u) else \
+            np.zeros(0, np.int64)
+        order = torch.from_numpy(np.argsort(dest, kind="stable"))
+        scount = torch.from_numpy(np.bincount(dest, minlength=N).astype(np.int64))
+        rcount = torch.empty(N, dtype=torch.int64)
+        dist.all_to_all_single(rcount, scount)
+        sk = u[order].contiguous()
+        rk = torch.empty(int(rcount.sum()), dtype=torch.int64)
+        dist.all_to_all_single(rk, sk, rcount.tolist(), scount.tolist())
+        rows = (self._read_rows(rk.to(self.device)).cpu().contiguous() if self.table is not None
+                else torch.zeros((len(rk), self.dim), dtype=torch.float32))
+        back = torch.empty((len(sk), self.dim), dtype=torch.float32)
+        dist.all_to_all_single(back.view(-1), rows.view(-1), [c * self.dim for c in scount.tolist()],
+                               [c * self.dim for c in rcount.tolist()])
+        out_u = torch.empty_like(back)
+        out_u[order] = back
+        return out_u[inv].to(keys.device)
+
+    def _read_rows(self, keys: torch.Tensor) -> torch.Tensor:
+        tab = self.table
+        if len(keys) == 0:
+            return torch.zeros((0, self.dim), dtype=torch.float32, device=keys.device)
+        if self.gpu:
+            torch.cuda.synchronize(self.device)  # every enqueued update applied
+            return tab.pull(keys, insert=False)[0]
+        rows, found = tab._t.get_rows(keys.numpy().view(np.uint64))
+        r = torch.from_numpy(np.ascontiguousarray(rows[:, :self.dim]))
+        r[torch.from_numpy(found == 0)] = 0.0
+        return r
 
     # ------------------------------------------------------------ control
     def barrier(self):

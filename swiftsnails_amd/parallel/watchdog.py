@@ -169,7 +169,9 @@ class Heartbeat:
 
 
 class FaultInjector:
-    """``SS_FAULT=kind[:rank=R][:step=S][:secs=T]``; kind in hang, crash, slow."""
+    """``SS_FAULT=kind[:rank=R][:step=S][:secs=T][:ms=M]``; kind in hang,
+    crash, slow (once, at step S) and delay (a straggler: rank R's host loop
+    sleeps M ms in EVERY step from S on; ``delay:<rank>:<ms>`` also parses)."""
 
     def __init__(self, spec: Optional[str] = None, rank: int = 0):
         spec = spec if spec is not None else os.environ.get("SS_FAULT", "")
@@ -180,8 +182,15 @@ class FaultInjector:
             return
         parts = spec.split(":")
         self.kind = parts[0]
-        if self.kind not in ("hang", "crash", "slow"):
+        if self.kind not in ("hang", "crash", "slow", "delay"):
             raise ValueError(f"SS_FAULT kind {self.kind!r}")
+        if self.kind == "delay":
+            self.secs = 0.001
+            pos = [p for p in parts[1:] if "=" not in p]
+            if pos:  # delay:<rank>:<ms>
+                self.rank = int(pos[0])
+                if len(pos) > 1:
+                    self.secs = float(pos[1]) / 1e3
         for p in parts[1:]:
             k, _, v = p.partition("=")
             if k == "rank":
@@ -190,10 +199,17 @@ class FaultInjector:
                 self.step = int(v)
             elif k == "secs":
                 self.secs = float(v)
+            elif k == "ms":
+                self.secs = float(v) / 1e3
 
     def maybe(self, step: int) -> None:
-        if self.kind is None or step != self.step or (self.rank is not None and
-                                                      self.rank != self.me):
+        if self.kind is None or (self.rank is not None and self.rank != self.me):
+            return
+        if self.kind == "delay":
+            if step >= self.step:
+                time.sleep(self.secs)
+            return
+        if step != self.step:
             return
         log.error("SS_FAULT: injecting %s on rank %d at step %d", self.kind, self.me, step)
         if self.kind == "crash":

@@ -992,3 +992,46 @@ def test_compact_bf16_rows(dev, G):
     v, _ = t16.pull(newk, unique=True)
     torch.cuda.synchronize()
     assert torch.all(v == 0.25)
+
+
+def test_server_bucket_overflow_keeps_fill_in_bounds(dev):
+    """A server bucket with more received keys than its LDS parking area
+    (8192) sets the sticky error, and every position past it still gets an
+    in-range pj and no local id: the fill writes zero rows to those real
+    positions and nothing anywhere else (unset pj entries)."""
+    from swiftsnails_amd._native import hip
+
+    h = hip()
+    n, nd = 10000, 100
+    rng = np.random.default_rng(5)
+    keys = torch.from_numpy(rng.choice(np.arange(1, nd + 1, dtype=np.int64), n)).to(dev)
+    rbase = torch.zeros(1, dtype=torch.int32, device=dev)
+    rnum = torch.full((1,), n, dtype=torch.int32, device=dev)
+    i32 = dict(dtype=torch.int32, device=dev)
+    cnt, bstart = torch.zeros(2, **i32), torch.empty(2, **i32)
+    ubase, unum = torch.empty(1, **i32), torch.empty(1, **i32)
+    rows = n + 64
+    pj = torch.full((rows,), -7, **i32)
+    luid = torch.full((rows,), -7, **i32)
+    bkeys = torch.empty(rows, dtype=torch.int64, device=dev)
+    uc = torch.zeros(1, dtype=torch.int64, device=dev)
+    err = torch.zeros(1, **i32)
+    st = torch.cuda.current_stream().cuda_stream
+    h.srv_dedup(keys.data_ptr(), rbase.data_ptr(), rnum.data_ptr(), rows, 1, 1, 1, 0,
+                cnt.data_ptr(), bstart.data_ptr(), pj.data_ptr(), luid.data_ptr(),
+                bkeys.data_ptr(), ubase.data_ptr(), unum.data_ptr(), uc.data_ptr(),
+                err.data_ptr(), st)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 1
+    pjn, ln = pj.cpu().numpy(), luid.cpu().numpy()
+    np.testing.assert_array_equal(pjn[:n], np.arange(n))
+    assert (ln[8192:n] == -1).all() and (ln[:8192] >= 0).all()
+    assert (pjn[n:] == -7).all() and (ln[n:] == -7).all()  # nothing past the bucket
+    svals = torch.arange(rows, dtype=torch.float32, device=dev) + 1.0
+    out = torch.full((rows,), float("nan"), device=dev)
+    h.srv_fill(1, bstart.data_ptr(), ubase.data_ptr(), unum.data_ptr(), pj.data_ptr(),
+               luid.data_ptr(), svals.data_ptr(), out.data_ptr(), 1, st)
+    torch.cuda.synchronize()
+    o = out.cpu().numpy()
+    assert (o[8192:n] == 0).all() and (o[:8192] > 0).all()
+    assert np.isnan(o[n:]).all()

@@ -76,6 +76,24 @@ def test_fault_injector_spec():
         FaultInjector("explode")
 
 
+def test_fault_injector_delay_every_step():
+    """delay: a straggler rank sleeps in every step from `step` on."""
+    from swiftsnails_amd.parallel.watchdog import FaultInjector
+
+    for spec in ("delay:1:30", "delay:rank=1:ms=30"):
+        f = FaultInjector(spec, rank=1)
+        assert f.kind == "delay" and f.rank == 1 and abs(f.secs - 0.03) < 1e-9
+        t0 = time.time()
+        for i in range(4):
+            f.maybe(i)
+        assert time.time() - t0 >= 0.12
+    t0 = time.time()
+    FaultInjector("delay:0:500", rank=1).maybe(3)  # other rank: no-op
+    g = FaultInjector("delay:rank=1:ms=500:step=5", rank=1)
+    g.maybe(4)  # before its first step
+    assert time.time() - t0 < 0.25
+
+
 _WORKER = textwrap.dedent("""
     import os, sys, datetime
     sys.path.insert(0, %(root)r)
