@@ -76,6 +76,27 @@ static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in 
 static constexpr int kBdMaxBuckets = 16384;
 static constexpr int kBdMaxSub = 64;    // server sub-buckets per bucket (srv_sub_buckets)
 
+// (key, sample) record of the scatter -> dedup hand-off: 16 bytes (uint4, one
+// dwordx4) or 12 (three dwords, one dwordx3 store / load: 25 % fewer bytes
+// of the route stream's largest array; SS_BD_REC=12|16)
+struct alignas(4) BdRec3 {
+  uint32_t x, y, z;
+};
+template <int RW>
+struct BdRecT {
+  using T = uint4;
+  static __device__ __forceinline__ T make(uint64_t k, uint32_t j) {
+    return make_uint4((uint32_t)k, (uint32_t)(k >> 32), j, 0u);
+  }
+};
+template <>
+struct BdRecT<3> {
+  using T = BdRec3;
+  static __device__ __forceinline__ T make(uint64_t k, uint32_t j) {
+    return BdRec3{(uint32_t)k, (uint32_t)(k >> 32), j};
+  }
+};
+
 __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs, uint32_t Pd) {
   const uint32_t d = rs.dest_of(key);
   const uint32_t h = (uint32_t)(dedup_hash(key) >> 32);
@@ -284,7 +305,7 @@ __global__ __launch_bounds__(CS) void k_bd_colscan(uint32_t* __restrict__ hist, 
 }
 
 // 4. bucket-ordered occurrence list (dynamic LDS: P words)
-template <int CT>
+template <int CT, int RW>
 __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ keys, long long n,
                                                      RouteSpec rs, int Pd, int P, int chunk,
                                                      const uint32_t* __restrict__ hist,
@@ -292,7 +313,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      uint32_t* __restrict__ pj,
                                                      uint32_t* __restrict__ pos_of,
                                                      uint32_t* __restrict__ bkt,
-                                                     uint4* __restrict__ rec) {
+                                                     typename BdRecT<RW>::T* __restrict__ rec) {
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
   const uint32_t* row = hist + (long long)c * P;
@@ -321,7 +342,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
           // (a 64-byte line per occurrence) and writes pj itself.  Measured
           // standalone: scatter 119 -> 163 us, dedup 213 -> 123 us; N>1
           // engine path 1.211 -> 1.169 ms/step, one GPU neutral
-          rec[pos] = make_uint4((uint32_t)k[e], (uint32_t)(k[e] >> 32), (uint32_t)j, 0u);
+          rec[pos] = BdRecT<RW>::make(k[e], (uint32_t)j);
         }
         // the BdIndex (j -> bucket position, bucket) only for its consumers
         if (pos_of) pos_of[j] = pos;
@@ -332,6 +353,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
 }
 
 // 5. one workgroup per bucket: LDS hash dedup -> bucket-local unique ids
+template <int RW>
 __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__ keys,
                                                    uint32_t* __restrict__ pj,
                                                    const uint32_t* __restrict__ bstart,
@@ -342,7 +364,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    long long ucap,
                                                    uint32_t* __restrict__ ubase,
                                                    unsigned long long* __restrict__ ucount,
-                                                   const uint4* __restrict__ rec,
+                                                   const typename BdRecT<RW>::T* __restrict__ rec,
                                                    unsigned long long* __restrict__ dbg,
                                                    uint64_t* __restrict__ ukeys,
                                                    float* __restrict__ ugrad, int gdim,
@@ -377,7 +399,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   // the bucket's (key, sample) records read coalesced, pj written back for
   // the consumers
   auto load = [&](uint32_t p) -> uint64_t {
-    const uint4 v = rec[p];
+    const typename BdRecT<RW>::T v = rec[p];
     pj[p] = v.z;
     return (uint64_t)v.x | ((uint64_t)v.y << 32);
   };
@@ -958,11 +980,22 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   // N>1 path 1.076-1.103 vs 1.109-1.169 ms)
   static const int cnt = wg_env("SS_BD_CNT", 1024);
   static const int cs = wg_env("SS_BD_CS", 1024);
+  // record width (SS_BD_REC): 16 or 12 bytes
+  static const int rw = [] {
+    const char* e = std::getenv("SS_BD_REC");
+    return e && std::atoi(e) == 12 ? 3 : 4;
+  }();
 #define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \
     case 256: hipLaunchKernelGGL(KERNEL<256>, dim3(L.nch), dim3(256), lds, st, __VA_ARGS__); break; \
     case 512: hipLaunchKernelGGL(KERNEL<512>, dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
     default: hipLaunchKernelGGL(KERNEL<1024>, dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
+  }
+#define SS_BD_CT_DISPATCH2(ct, RW, KERNEL, ...)                                                  \
+  switch (ct) {                                                                               \
+    case 256: hipLaunchKernelGGL((KERNEL<256, RW>), dim3(L.nch), dim3(256), lds, st, __VA_ARGS__); break; \
+    case 512: hipLaunchKernelGGL((KERNEL<512, RW>), dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL((KERNEL<1024, RW>), dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
   }
   SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, ucount);
   check_launch("k_bd_count");
@@ -978,16 +1011,27 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
 #undef SS_BD_CS_CASE
   }
   check_launch("k_bd_colscan");
-  SS_BD_CT_DISPATCH(ct, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pj,
-                    pos_of, bkt, reinterpret_cast<uint4*>(rec));
+  if (rw == 3)
+    SS_BD_CT_DISPATCH2(ct, 3, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
+                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<BdRec3*>(rec))
+  else
+    SS_BD_CT_DISPATCH2(ct, 4, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
+                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<uint4*>(rec))
 #undef SS_BD_CT_DISPATCH
+#undef SS_BD_CT_DISPATCH2
   check_launch("k_bd_scatter");
   // place: unique keys straight into the per-destination send segments
   // (+ zeroed gradient rows), reserved with one atomic per bucket
-  hipLaunchKernelGGL(k_bd_dedup, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
-                     bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
-                     reinterpret_cast<const uint4*>(rec), dbg,
-                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub);
+  if (rw == 3)
+    hipLaunchKernelGGL(k_bd_dedup<3>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
+                       bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
+                       reinterpret_cast<const BdRec3*>(rec), dbg,
+                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub);
+  else
+    hipLaunchKernelGGL(k_bd_dedup<4>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
+                       bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
+                       reinterpret_cast<const uint4*>(rec), dbg,
+                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub);
   check_launch("k_bd_dedup");
   if (inv && n > 0) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");

@@ -457,10 +457,10 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("otail") = 0);
   m.def("w2v_pp", [](uintptr_t inv_c, uintptr_t inv_w, uintptr_t inv_n, uintptr_t meta, int B,
                      int W, int K, int D, uintptr_t uvals, uintptr_t ograd, uintptr_t gpair,
-                     uintptr_t loss, uintptr_t pairs, uintptr_t st) {
+                     uintptr_t loss, uintptr_t pairs, uintptr_t st, uintptr_t gnc) {
     launch_w2v_pp(P<const uint32_t>(inv_c), P<const uint32_t>(inv_w), P<const uint32_t>(inv_n),
                   P<const int32_t>(meta), B, W, K, D, P<const float>(uvals), P<float>(ograd),
-                  P<float>(gpair), P<float>(loss), P<float>(pairs), S(st));
+                  P<float>(gpair), P<float>(loss), P<float>(pairs), S(st), P<float>(gnc));
   });
   m.def("w2v_osort", [](int P_, uintptr_t bstart, uintptr_t unum, uintptr_t ubase, uintptr_t pj,
                         uintptr_t luid, uintptr_t ord, uintptr_t items, uintptr_t st) {
@@ -469,10 +469,14 @@ PYBIND11_MODULE(_ss_hip, m) {
                      P<uint32_t>(ord), P<uint32_t>(items), S(st));
   });
   m.def("w2v_oreduce", [](uintptr_t items, long long n, uintptr_t ord, uintptr_t ograd,
-                          uintptr_t otail, int B, int W, int D, uintptr_t ugrad, uintptr_t st) {
+                          uintptr_t otail, int B, int W, int D, uintptr_t ugrad, uintptr_t st,
+                          uintptr_t gnc, long long negbase, uintptr_t uvals) {
     launch_w2v_oreduce(P<const uint32_t>(items), n, P<const uint32_t>(ord), P<const float>(ograd),
-                       P<const float>(otail), B, W, D, P<float>(ugrad), S(st));
-  });
+                       P<const float>(otail), B, W, D, P<float>(ugrad), S(st),
+                       P<const float>(gnc), negbase, P<const float>(uvals));
+  }, py::arg("items"), py::arg("n"), py::arg("ord"), py::arg("ograd"), py::arg("otail"),
+     py::arg("B"), py::arg("W"), py::arg("D"), py::arg("ugrad"), py::arg("st"),
+     py::arg("gnc") = 0, py::arg("negbase") = 0, py::arg("uvals") = 0);
   m.def("w2v_stream_gen", [](uint64_t seed, long long base, int B, int W, int L, long long nneg,
                              long long V, float noise, uintptr_t keys, uintptr_t meta, uintptr_t st,
                              uintptr_t step_dev, long long step_mul, long long step_add) {

@@ -92,9 +92,12 @@ void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const
                       hipStream_t st);
 void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                    const int32_t* meta, int B, int W, int K, int D, const float* uvals,
-                   float* ograd, float* gpair, float* loss_sum, float* pair_sum, hipStream_t st);
+                   float* ograd, float* gpair, float* loss_sum, float* pair_sum, hipStream_t st,
+                   float* gnc);
 void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
-                        const float* otail, int B, int W, int D, float* ugrad, hipStream_t st);
+                        const float* otail, int B, int W, int D, float* ugrad, hipStream_t st,
+                        const float* gnc = nullptr, long long negbase = 0,
+                        const float* uvals = nullptr);
 void launch_w2v_stream_gen(uint64_t seed, long long base, int B, int W, int L, long long nneg,
                            long long V, float noise, uint64_t* keys, int32_t* meta,
                            hipStream_t st, const long long* step_dev, long long step_mul,

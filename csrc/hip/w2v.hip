@@ -800,13 +800,20 @@ struct OVec<1> {
   __device__ static float get(const T& x, int) { return x; }
 };
 
+// `gnc` (per-pair negatives): occurrence j >= `negbase` is the negative row
+// gn * v_c, stored by k_w2v_pp as the pair (gn, c) — 8 bytes instead of a
+// D-float row — and expanded here from the center row uvals[c] (the step's
+// center rows: a few MB, cache-resident)
 template <int D>
 __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ items, long long n,
                                                      const uint32_t* __restrict__ ord,
                                                      const float* __restrict__ ograd,
                                                      const float* __restrict__ otail, int B,
                                                      int W, int ntiles,
-                                                     float* __restrict__ ugrad) {
+                                                     float* __restrict__ ugrad,
+                                                     const float2* __restrict__ gnc,
+                                                     long long negbase,
+                                                     const float* __restrict__ uvals) {
   // one item per half-wave: 32 lanes x V floats cover a row (512 B at D =
   // 128 as 16-B loads), two independent item chains per wave
   constexpr int V = D / 32;
@@ -830,10 +837,21 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
   for (uint32_t k0 = 0; k0 < it.y; k0 += QF) {
     VT x[QF], y[QF];
+    float sc[QF];
 #pragma unroll
     for (int r = 0; r < QF; ++r) {
       const uint32_t k = k0 + r;
       const long long j = (long long)__shfl(jl, (int)(k < it.y ? k : 0), 32);
+      sc[r] = 1.f;
+      if (gnc && j >= negbase) {  // a scaled center row (per-pair negative)
+        const float2 e = k < it.y ? gnc[j - negbase] : make_float2(0.f, 0.f);
+        const uint32_t c = __float_as_uint(e.y);
+        const bool on = k < it.y && c != kInv && e.x != 0.f;
+        sc[r] = e.x;
+        x[r] = on ? *reinterpret_cast<const VT*>(uvals + (long long)c * D + hl * V) : VT{};
+        y[r] = VT{};
+        continue;
+      }
       const long long tq = k < it.y ? tail_of(j) : -1;
       x[r] = k < it.y ? *reinterpret_cast<const VT*>(ograd + j * D + hl * V) : VT{};
       y[r] = tq >= 0 ? *reinterpret_cast<const VT*>(otail + tq * D + hl * V) : VT{};
@@ -841,7 +859,7 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
 #pragma unroll
     for (int r = 0; r < QF; ++r)
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] += OVec<V>::get(x[r], v) + OVec<V>::get(y[r], v);
+      for (int v = 0; v < V; ++v) acc[v] += sc[r] * OVec<V>::get(x[r], v) + OVec<V>::get(y[r], v);
   }
   float* g = ugrad + (long long)it.z * D + hl * V;
   if (it.w & 1u) {
@@ -864,11 +882,14 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
 // positions | B x 2W x K negatives], negative (t, o, k) at B + R + (t*2W + o)*K
 // + k, o the offset slot of dq = o - W (o < W) or o - W + 1).  Dot products,
 // not GEMMs: each pair touches 1 + K rows once, so there is no tile to put on
-// the MFMA.  Gradients as occurrence rows with plain stores (summed per key by
-// k_w2v_oreduce, as the window tile's): k_w2v_pp (one wave per center) writes
-// the center row, the negative rows and the pair's scalar g+ = sig(v.u) - 1;
-// k_w2v_ppctx (one wave per run position) gathers g+ * v over the 2W centers
-// that pair with it.  Every occurrence row is written (zero when unused).
+// the MFMA.  Gradients as occurrence rows summed per key by k_w2v_oreduce (as
+// the window tile's): k_w2v_pp (one wave per center) writes the center row,
+// the pair's scalar g+ = sig(v.u) - 1, and for each negative only the pair
+// (gn, center id) — the negative's gradient row is gn * v_center, which the
+// reduce expands from the (cache-resident) center row: 8 bytes per negative
+// occurrence instead of a D-float row (819K x 512 B = 420 MB of stores and as
+// many loads per config-3 step); k_w2v_ppctx (one wave per run position)
+// gathers g+ * v over the 2W centers that pair with it.
 static constexpr int kPpMaxK = 16;
 template <int D>
 __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv_c,
@@ -879,7 +900,8 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
                                                 float* __restrict__ ograd,
                                                 float* __restrict__ gpair,
                                                 float* __restrict__ loss_sum,
-                                                float* __restrict__ pair_sum) {
+                                                float* __restrict__ pair_sum,
+                                                float2* __restrict__ gnc) {
   constexpr int R = (D + 63) / 64;
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -901,12 +923,8 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
       const long long q = t + W + dq;
       const bool ok = c != kInv && w2v_pair_ok(mc, meta[q], dq);
       const long long nb = (t * 2 * W + o) * (long long)K;
-      float* on = ograd + (B + Rn + nb) * (long long)D;
-      if (!ok) {  // the pair's occurrence rows still hold a (zero) gradient
-        for (int k = 0; k < K; ++k)
-#pragma unroll
-          for (int r = 0; r < R; ++r)
-            if (lane + 64 * r < D) on[(long long)k * D + lane + 64 * r] = 0.f;
+      if (!ok) {  // the pair's negatives still get a (zero) gradient entry
+        if (lane < K) gnc[nb + lane] = make_float2(0.f, __uint_as_float(kInv));
         if (lane == 0) gpair[t * 2 * W + o] = 0.f;
         continue;
       }
@@ -940,6 +958,7 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) gv[r] += gp * u[r];
+      float gk = 0.f;  // lane k < K: negative k's gn
 #pragma unroll
       for (int k = 0; k < kPpMaxK; ++k) {
         if (k >= K) break;
@@ -949,13 +968,11 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
         for (int m = 32; m > 0; m >>= 1) sn += __shfl_xor(sn, m, 64);
         const float gn = sigm(sn);  // d/ds softplus(s)
         if (lane == 0) loss += softplus(sn);
+        if (lane == k) gk = gn;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-          const int d = lane + 64 * r;
-          gv[r] += gn * n[k][r];
-          if (d < D) on[(long long)k * D + d] = gn * v[r];
-        }
+        for (int r = 0; r < R; ++r) gv[r] += gn * n[k][r];
       }
+      if (lane < K) gnc[nb + lane] = make_float2(gk, __uint_as_float(c));
     }
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -1164,7 +1181,9 @@ void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const
 }
 
 void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
-                        const float* otail, int B, int W, int D, float* ugrad, hipStream_t st) {
+                        const float* otail, int B, int W, int D, float* ugrad, hipStream_t st,
+                        const float* gnc, long long negbase, const float* uvals) {
+  if (gnc && !uvals) throw_error("w2v_oreduce: scaled negative rows need the center rows");
   if (n <= 0) return;
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_oreduce: window must be in [1, 15]");
   const int ntiles = (B + kT - 1) / kT;
@@ -1177,7 +1196,8 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
 #define SS_W2VO_CASE(DD)                                                                      \
   case DD:                                                                                    \
     hipLaunchKernelGGL(k_w2v_oreduce<DD>, dim3(grid), dim3(256), 0, st, it, n, ord, ograd,    \
-                       otail, B, W, ntiles, ugrad);                                           \
+                       otail, B, W, ntiles, ugrad, reinterpret_cast<const float2*>(gnc),       \
+                       negbase, uvals);                                                        \
     break;
     SS_W2VO_CASE(32)
     SS_W2VO_CASE(64)
@@ -1220,8 +1240,10 @@ void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t
 
 void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                    const int32_t* meta, int B, int W, int K, int D, const float* uvals,
-                   float* ograd, float* gpair, float* loss_sum, float* pair_sum, hipStream_t st) {
+                   float* ograd, float* gpair, float* loss_sum, float* pair_sum, hipStream_t st,
+                   float* gnc) {
   if (B <= 0) return;
+  if (!gnc) throw_error("w2v_pp: the (gn, center) buffer of the negatives is required");
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_pp: window must be in [1, 15]");
   if (K < 1 || K > kPpMaxK) throw_error("w2v_pp: negatives per pair must be in [1, 16]");
   const long long Rn = (long long)B + 2 * W;
@@ -1229,7 +1251,8 @@ void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t*
 #define SS_W2VP_CASE(DD)                                                                       \
   case DD:                                                                                     \
     hipLaunchKernelGGL(k_w2v_pp<DD>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, inv_c,    \
-                       inv_w, inv_n, meta, B, W, K, uvals, ograd, gpair, loss_sum, pair_sum);  \
+                       inv_w, inv_n, meta, B, W, K, uvals, ograd, gpair, loss_sum, pair_sum,   \
+                       reinterpret_cast<float2*>(gnc));                                        \
     check_launch("k_w2v_pp");                                                                  \
     hipLaunchKernelGGL(k_w2v_ppctx<DD>, dim3((unsigned)((Rn + 3) / 4)), dim3(256), 0, st,       \
                        inv_c, gpair, B, W, uvals, ograd);                                      \

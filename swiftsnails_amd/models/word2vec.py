@@ -177,7 +177,12 @@ class Word2VecWorker(PipelinedWorker):
             raise ValueError("per_pair negatives need the bucketed dedup (SS_DEDUP=bucket)")
         if self.occ_reduce:
             dev, n, D, W = engine.device, data.n_keys, engine.dim, data.window
-            self.ograd = torch.empty((n, D), dtype=torch.float32, device=dev)
+            # per_pair: the negatives' gradient rows are (gn, center) pairs
+            # (gnc below), so occurrence rows cover centers + run positions only
+            rows = data.batch_size + data.run_len if self.per_pair else n
+            self.ograd = torch.empty((rows, D), dtype=torch.float32, device=dev)
+            self.gnc = (torch.empty((max(1, n - rows), 2), dtype=torch.float32, device=dev)
+                        if self.per_pair else None)
             self.otail = torch.empty((max(1, (data.tiles - 1) * 2 * W), D), dtype=torch.float32,
                                      device=dev)
             # per_pair: g+ of every (center, offset) pair (k_w2v_pp -> k_w2v_ppctx)
@@ -215,10 +220,11 @@ class Word2VecWorker(PipelinedWorker):
             h.w2v_pp(ptr, ptr + B * es, ptr + (B + d.run_len) * es, self.meta[slot].data_ptr(),
                      B, d.window, d.negatives, self.engine.dim, rnd.uvals.data_ptr(),
                      self.ograd.data_ptr(), self.gpair.data_ptr(), self.loss_sum.data_ptr(),
-                     self.pair_sum.data_ptr(), st)
+                     self.pair_sum.data_ptr(), st, self.gnc.data_ptr())
             h.w2v_oreduce(self.items[slot].data_ptr(), d.n_keys, self.ord[slot].data_ptr(),
                           self.ograd.data_ptr(), 0, B, d.window, self.engine.dim,
-                          rnd.ugrad.data_ptr(), st)
+                          rnd.ugrad.data_ptr(), st, gnc=self.gnc.data_ptr(),
+                          negbase=B + d.run_len, uvals=rnd.uvals.data_ptr())
             return
         if self.window_mode:
             occ = self.occ_reduce

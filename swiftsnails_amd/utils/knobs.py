@@ -31,7 +31,8 @@ KNOBS: dict[str, Knob] = {
     "SS_BENCH_ROUND_TIMEOUT": Knob("300", "bench.py", "ops",
                                    "seconds without a finished step before the bench aborts"),
     "SS_FAULT": Knob("", "parallel/watchdog.py", "ops",
-                     "fault injection: hang|crash|slow:rank=R:step=S"),
+                     "fault injection: hang|crash|slow:rank=R:step=S (once), "
+                     "delay:<rank>:<ms> (a straggler: sleeps every step)"),
     "SS_LOG_LEVEL": Knob("WARNING", "utils/logging.py, csrc/host/common.h", "ops",
                          "log level (Python and the native runtime)"),
     "SS_LOCAL_IP": Knob("auto", "csrc/host/transfer.h", "ops",
@@ -48,8 +49,10 @@ KNOBS: dict[str, Knob] = {
                             "route-buffer ring depth (>= 3 for pull-ahead; 4 measured 1.008 vs "
                             "1.018 ms/step for 3, four A/B pairs)"),
     "SS_PULL_AHEAD": Knob("auto", "parallel/engine.py", "tuning",
-                          "pull round i+1 while round i computes: auto = the models that opt "
-                          "in (FM, word2vec), 1 = every model at N>1, 0 = none"),
+                          "pull rounds i+1..i+k while round i computes: auto = the models that "
+                          "opt in (FM, word2vec), and at N>1 the bench / launcher calibration "
+                          "times synchronous vs pulled-ahead steps on the live world and keeps "
+                          "the faster; 1 = every model at N>1, 0 = none"),
     "SS_DEDUP": Knob("bucket", "ops/dedup.py", "tuning",
                      "bucket: LDS dedup per hash bucket; hash: global scratch table"),
     "SS_TABLE_G": Knob("auto", "ops/table.py", "tuning", "lanes per table row"),
@@ -62,6 +65,9 @@ KNOBS: dict[str, Knob] = {
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
     "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
+    "SS_BD_REC": Knob("16", "csrc/hip/bdedup.hip", "tuning",
+                      "bytes of the scatter -> dedup (key, sample) record: 16 (dwordx4) or 12 "
+                      "(dwordx3)"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
@@ -95,8 +101,9 @@ KNOBS: dict[str, Knob] = {
                               "run a 1-GPU job through the N>1 path (1: loopback, rccl: a size-1 "
                               "RCCL communicator, xgmi: a size-1 mailbox arena)"),
     "SS_STALENESS": Knob("1", "parallel/engine.py", "ops",
-                         "pull-ahead bound: a round's pull waits until the push of the round "
-                         "k+1 before it is applied (k = 1: staleness 1); ring: bounded by the "
+                         "pull-ahead depth and bound k (<= ring depth - 2): rounds i+1..i+k "
+                         "are pulled while round i computes, each pull waits for the push k+1 "
+                         "rounds back; 0: synchronous rounds; ring: one ahead, bounded by the "
                          "route-ring depth only (FM 0.655 -> 0.620 ms/step, word2vec 0.125 -> "
                          "0.118; N>1 LR path unchanged)"),
     "SS_PULL_STREAM": Knob("model (word2vec 1, FM 0)", "parallel/engine.py", "tuning",

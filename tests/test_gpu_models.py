@@ -118,10 +118,10 @@ def test_w2v_window_tile_matches_reference(dev, D, W, B):
                                      (128, 15, 16, 40)])
 def test_w2v_per_pair_negatives_match_reference(dev, D, W, K, B):
     """Classic SGNS (k_w2v_pp + k_w2v_ppctx): K negatives per positive pair,
-    gradients as occurrence rows.  Every key position its own row: the center
-    rows, the run-position rows (summed over the 2W centers that pair with
-    them) and every negative occurrence row vs the fp64 reference; rows of
-    invalid pairs and masked positions are written as zeros."""
+    gradients as occurrence rows.  The center rows and the run-position rows
+    (summed over the 2W centers that pair with them) as rows, every negative
+    occurrence as its (gn, center) pair — its row is gn * v_center — vs the
+    fp64 reference; invalid pairs and masked positions get zero gradients."""
     from swiftsnails_amd._native import hip
     from swiftsnails_amd.models.word2vec import sgns_pp_reference, window_pairs_reference
 
@@ -135,7 +135,8 @@ def test_w2v_per_pair_negatives_match_reference(dev, D, W, K, B):
     nrows = B + R + nneg
     U = (rng.standard_normal((nrows, D)) * 0.3).astype(np.float32)
     inv = np.arange(nrows, dtype=np.int32)
-    og = torch.full((nrows, D), float("nan"), device=dev)  # every row must be written
+    og = torch.full((B + R, D), float("nan"), device=dev)  # every row must be written
+    gnc = torch.full((nneg, 2), float("nan"), device=dev)
     gp = torch.empty(B * 2 * W, device=dev)
     loss, pairs = torch.zeros(256 * 32, device=dev), torch.zeros(256 * 32, device=dev)
     tu, ti, tm = (torch.from_numpy(U).to(dev), torch.from_numpy(inv).to(dev),
@@ -143,9 +144,16 @@ def test_w2v_per_pair_negatives_match_reference(dev, D, W, K, B):
     p = ti.data_ptr()
     hip().w2v_pp(p, p + B * 4, p + (B + R) * 4, tm.data_ptr(), B, W, K, D, tu.data_ptr(),
                  og.data_ptr(), gp.data_ptr(), loss.data_ptr(), pairs.data_ptr(),
-                 torch.cuda.current_stream().cuda_stream)
+                 torch.cuda.current_stream().cuda_stream, gnc.data_ptr())
     torch.cuda.synchronize()
-    G = og.cpu().numpy().astype(np.float64)
+    gn = gnc.cpu().numpy()
+    cen = gn[:, 1].copy().view(np.uint32)
+    assert np.isfinite(gn[:, 0]).all()
+    live = cen != 0xFFFFFFFF
+    assert (gn[~live, 0] == 0).all()
+    Gneg = np.zeros((nneg, D))
+    Gneg[live] = gn[live, 0:1].astype(np.float64) * U[cen[live].astype(np.int64)]
+    G = np.concatenate([og.cpu().numpy().astype(np.float64), Gneg])
     assert np.isfinite(G).all()
     band = window_pairs_reference(meta, B, W)  # [B, R]
     offs = [o - W if o < W else o - W + 1 for o in range(2 * W)]
