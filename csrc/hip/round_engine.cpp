@@ -18,7 +18,6 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
-#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -218,18 +217,6 @@ class RoundEngine {
       SrvSlot& S = srv_[slot];
       const uint32_t* roff =
           nkp_ == 4 ? Pt<const uint32_t>(ar_[slot][0]->base() + keys_[slot][3].data) : nullptr;
-      if (dim_ == 1 && G == 1 && !custom_pull && fused_pull() && srv_pull1_ok(t)) {
-        // scalar rows: dedup + lookup + response rows in one kernel (server.hip)
-        launch_srv_pull1(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
-                         Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt,
-                         S.bstart, S.pj, S.luid, S.ubase, S.unum, S.ucount,
-                         Pt<uint32_t>(srv_err), St(stream), roff, t, ip, S.slots,
-                         snap ? S.snap : nullptr, Pt<float>(rvals),
-                         Pt<unsigned long long>(size_ctr), Pt<int>(err));
-        fill_and_return(slot, stream, 0, rvals, sent, metrics);
-        if (ahead) record(kPull, slot, stream, tag);
-        return;
-      }
       launch_srv_dedup(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
                        Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt,
                        S.bstart, S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount,
@@ -308,15 +295,6 @@ class RoundEngine {
   }
 
  private:
-  // SS_SRV_FUSED=0: the server pull of scalar rows as three kernels (dedup,
-  // lookup, fill) instead of k_srv_pull1 (A/B)
-  static bool fused_pull() {
-    static const bool on = [] {
-      const char* e = std::getenv("SS_SRV_FUSED");
-      return !(e && e[0] == '0');
-    }();
-    return on;
-  }
   void check_slot(int slot) const {
     if (slot < 0 || slot >= depth_) throw std::out_of_range("RoundEngine: ring slot");
   }

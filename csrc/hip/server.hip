@@ -38,7 +38,6 @@
 #include "ss_device.h"
 #include "ss_launch.h"
 #include "scan.h"
-#include "table_probe.h"
 
 namespace ss {
 
@@ -262,180 +261,6 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   }
 }
 
-// 3' (scalar rows: sparse LR).  k_srv_dedup + k_pull_unique_bk + the response
-// fill in ONE workgroup per server bucket: the LDS dedup of the bucket's
-// received keys (as k_srv_dedup), then each distinct key's table lookup-or-
-// insert straight from the LDS table (its (w, h) row to slots / the pull
-// snapshot, w kept in LDS by local id), then every received position's
-// response row written from LDS.  Against the three kernels it saves the
-// staged key list (bkeys: a write and a read of 8 B per distinct key), the
-// per-key value array between the lookup and the fill (a write and a read),
-// the fill's re-read of luid, and two launches.  16-byte [w | h | key] slots
-// (probe_slot16: one load per probe step).
-__global__ __launch_bounds__(kSrvDT) void k_srv_pull1(
-    SrvRuns R, const uint32_t* __restrict__ bstart, uint32_t* __restrict__ pj,
-    uint32_t* __restrict__ luid, uint32_t* __restrict__ ubase, uint32_t* __restrict__ unum,
-    unsigned long long* __restrict__ ucount, uint32_t* __restrict__ err, DevTable tab,
-    InitParams ip, long long* __restrict__ slots, float2* __restrict__ snap,
-    float* __restrict__ rvals, unsigned long long* __restrict__ size_ctr, int* __restrict__ terr) {
-  __shared__ unsigned long long tab_[kSrvTS];
-  __shared__ unsigned int lid[kSrvTS];
-  __shared__ float val[kSrvTS];
-  __shared__ unsigned short park[kSrvOcc];
-  __shared__ unsigned int wsum[16];
-  __shared__ long long sa[kSrvMaxSrc];
-  __shared__ unsigned int so[kSrvMaxSrc + 1];
-  __shared__ unsigned int tot;
-  __shared__ int bad;
-  __shared__ unsigned long long sbase;
-  const int t = threadIdx.x;
-  const int b = blockIdx.x, k = b / R.m;
-  const uint32_t sub = (uint32_t)(b % R.m);
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
-  const uint32_t ts = lds_table_size(p1 - p0, kSrvTS);
-  for (uint32_t s = t; s < ts; s += kSrvDT) tab_[s] = kEmptyKey;
-  if (t < R.nsrc) {
-    long long a;
-    uint32_t len;
-    R.part(t, k, (int)sub, &a, &len);
-    sa[t] = a;
-    so[t + 1] = len;
-  }
-  __syncthreads();
-  if (t == 0) {
-    so[0] = 0u;
-    for (int s = 0; s < R.nsrc; ++s) so[s + 1] += so[s];
-    bad = so[R.nsrc] != p1 - p0 || p1 - p0 > (uint32_t)kSrvOcc;
-  }
-  __syncthreads();
-  auto insert = [&](uint64_t key) -> uint32_t {
-    uint32_t s = (uint32_t)(dedup_hash(key) >> 32) & (ts - 1);
-    for (uint32_t i = 0; i < ts; ++i) {
-      const unsigned long long v = tab_[s];
-      if (v == key) return s;
-      if (v == kEmptyKey) {
-        const unsigned long long prev = atomicCAS(&tab_[s], kEmptyKey, (unsigned long long)key);
-        if (prev == kEmptyKey || prev == key) return s;
-      }
-      s = (s + 1) & (ts - 1);
-    }
-    bad = 1;
-    return kSrvInv;
-  };
-  const uint32_t n = min(min(so[R.nsrc], p1 - p0), (uint32_t)kSrvOcc);
-  for (uint32_t f0 = 0; f0 < n; f0 += kSrvDT * kSrvRegs) {
-    uint64_t kk[kSrvRegs];
-#pragma unroll
-    for (int r = 0; r < kSrvRegs; ++r) {
-      const uint32_t f = f0 + (uint32_t)(r * kSrvDT + t);
-      kk[r] = kEmptyKey;
-      if (f < n) {
-        int s = 0;
-        while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
-        const long long pos = sa[s] + (f - so[s]);
-        kk[r] = R.rkeys[pos];
-        pj[p0 + f] = (uint32_t)pos;
-      }
-    }
-#pragma unroll
-    for (int r = 0; r < kSrvRegs; ++r) {
-      const uint32_t f = f0 + (uint32_t)(r * kSrvDT + t);
-      if (f < n) park[f] = (unsigned short)insert(kk[r]);
-    }
-  }
-  __syncthreads();
-  constexpr int kPerT = kSrvTS / kSrvDT;
-  const uint32_t per = ts >= (uint32_t)kSrvDT ? ts / kSrvDT : 1u;
-  auto own = [&](int i) -> unsigned long long {
-    const uint32_t s = (uint32_t)t * per + (uint32_t)i;
-    return (uint32_t)i < per && s < ts ? tab_[s] : kEmptyKey;
-  };
-  unsigned int occ = 0;
-#pragma unroll
-  for (int i = 0; i < kPerT; ++i) occ += own(i) != kEmptyKey;
-  unsigned int o = block_excl_scan<kSrvDT / 64>(occ, wsum, &tot);
-  if (t == 0) {
-    sbase = atomicAdd(ucount, (unsigned long long)tot);
-    ubase[b] = (uint32_t)sbase;
-    unum[b] = tot;
-    if (bad) atomicOr(err, 1u);
-  }
-  __syncthreads();
-  const uint32_t base = (uint32_t)sbase;
-  // the lookups: every owned key's first probe load goes out before any is
-  // resolved (one random-access latency per thread instead of one per key)
-  uint64_t key[kPerT];
-  uint64_t hs[kPerT];
-  uint4 first[kPerT];
-  uint32_t q0 = o;
-#pragma unroll
-  for (int i = 0; i < kPerT; ++i) {
-    key[i] = own(i);
-    hs[i] = key[i] != kEmptyKey ? fastrange64(table_hash(key[i]), tab.cap) : 0;
-    if (key[i] != kEmptyKey) first[i] = *reinterpret_cast<const uint4*>(tab.base + hs[i] * 16);
-  }
-  unsigned long long ins = 0;
-#pragma unroll
-  for (int i = 0; i < kPerT; ++i) {
-    if (key[i] == kEmptyKey) continue;
-    const uint32_t s = (uint32_t)t * per + (uint32_t)i;
-    const uint32_t q = q0++;
-    lid[s] = q;
-    // the first probe step from the batched load, the rest (collisions,
-    // claims) as probe_slot16 does
-    long long slot = -1;
-    bool claimed = false;
-    float2 wh = make_float2(0.f, 0.f);
-    const uint64_t fk = ((uint64_t)first[i].w << 32) | first[i].z;
-    if (fk == key[i]) {
-      slot = (long long)hs[i];
-      wh = make_float2(__uint_as_float(first[i].x), __uint_as_float(first[i].y));
-    } else {
-      slot = probe_slot16(tab, key[i], &wh, &claimed);
-    }
-    if (slot < 0) {
-      atomicOr(terr, 1);
-      val[q] = 0.f;
-      slots[base + q] = -1;
-      continue;
-    }
-    if (claimed) {
-      wh = make_float2(init_value(ip, key[i], 0, 1), ip.state_init);
-      if (!tab.prefilled) *reinterpret_cast<float2*>(slot_row(tab, slot)) = wh;
-      ++ins;
-    } else {
-      wh.x = fresh_or(wh.x, ip, key[i], 0, 1);
-      if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
-    }
-    val[q] = wh.x;
-    slots[base + q] = slot;
-    if (snap) snap[base + q] = wh;
-  }
-  ins = wave_sum_u64(ins);
-  if ((t & 63) == 0 && ins) ctr_add(size_ctr, ins);
-  __syncthreads();
-  // local ids of the received positions and their response rows
-  for (uint32_t q = t; q < n; q += kSrvDT) {
-    const uint32_t sl = park[q] == 0xFFFFu ? kSrvInv : park[q];
-    const uint32_t l = sl == kSrvInv || sl >= ts ? kSrvInv : lid[sl];
-    luid[p0 + q] = l;
-    rvals[pj[p0 + q]] = l == kSrvInv ? 0.f : val[l];
-  }
-  // an overflowed bucket: positions past the parking area (see k_srv_dedup)
-  const uint32_t nall = p1 - p0, nflat = so[R.nsrc];
-  for (uint32_t f = n + t; f < nall; f += kSrvDT) {
-    uint32_t pos = 0u;
-    if (f < nflat) {
-      int s = 0;
-      while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
-      pos = (uint32_t)(sa[s] + (f - so[s]));
-    }
-    pj[p0 + f] = pos;
-    luid[p0 + f] = kSrvInv;
-    rvals[pos] = 0.f;
-  }
-}
-
 // lanes per row for rows of n 16-byte chunks: the next power of two, <= 64
 __device__ __forceinline__ int srv_group(int n) {
   return n <= 1 ? 1 : n <= 2 ? 2 : n <= 4 ? 4 : n <= 8 ? 8 : n <= 16 ? 16 : n <= 32 ? 32 : 64;
@@ -612,32 +437,6 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
   hipLaunchKernelGGL(k_srv_dedup, dim3(P), dim3(kSrvDT), 0, st, R, bstart, pj, luid, bkeys,
                      ubase, unum, ucount, err);
   check_launch("k_srv_dedup");
-}
-
-void launch_srv_pull1(const uint64_t* rkeys, const uint32_t* rbase, const uint32_t* rnum,
-                      long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
-                      uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint32_t* ubase,
-                      uint32_t* unum, unsigned long long* ucount, uint32_t* err, hipStream_t st,
-                      const uint32_t* roff, const DevTable& t, const InitParams& ip,
-                      long long* slots, float* snap, float* rvals, unsigned long long* size_ctr,
-                      int* terr) {
-  if (nsrc < 1 || nsrc > kSrvMaxSrc || Pd < 1 || m < 1 || m > 64) throw_error("srv_pull1: bad layout");
-  if (m > 1 && !roff) throw_error("srv_pull1: sub-buckets need the senders' offsets (msub)");
-  if (!srv_pull1_ok(t)) throw_error("srv_pull1: 16-byte [w | h | key] scalar rows only");
-  SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me, roff};
-  const int P = Pd * m;
-  hipLaunchKernelGGL(k_srv_count, dim3((Pd + kSrvCntK - 1) / kSrvCntK), dim3(256), 0, st, R, cnt,
-                     bstart, ucount, cnt + P);
-  check_launch("k_srv_count");
-  hipLaunchKernelGGL(k_srv_pull1, dim3(P), dim3(kSrvDT), 0, st, R, bstart, pj, luid, ubase, unum,
-                     ucount, err, t, ip, slots, reinterpret_cast<float2*>(snap), rvals, size_ctr,
-                     terr);
-  check_launch("k_srv_pull1");
-}
-
-bool srv_pull1_ok(const DevTable& t) {
-  return !t.bf16 && t.dim == 1 && t.width == 2 && t.stride == 16 && t.key_off == 8 &&
-         t.row_off == 0;
 }
 
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,

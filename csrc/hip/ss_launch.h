@@ -189,15 +189,6 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
                       uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
                       uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
                       hipStream_t st, const uint32_t* roff = nullptr);
-// fused N>1 server pull of scalar rows (dedup + lookup + response fill)
-bool srv_pull1_ok(const DevTable& t);
-void launch_srv_pull1(const uint64_t* rkeys, const uint32_t* rbase, const uint32_t* rnum,
-                      long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
-                      uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint32_t* ubase,
-                      uint32_t* unum, unsigned long long* ucount, uint32_t* err, hipStream_t st,
-                      const uint32_t* roff, const DevTable& t, const InitParams& ip,
-                      long long* slots, float* snap, float* rvals, unsigned long long* size_ctr,
-                      int* terr);
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
                           int D, hipStream_t st);

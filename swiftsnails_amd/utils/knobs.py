@@ -68,9 +68,6 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_REC": Knob("16", "csrc/hip/bdedup.hip", "tuning",
                       "bytes of the scatter -> dedup (key, sample) record: 16 (dwordx4) or 12 "
                       "(dwordx3)"),
-    "SS_SRV_FUSED": Knob("1", "csrc/hip/round_engine.cpp", "tuning",
-                         "N>1 server pull of scalar rows: one kernel (dedup + lookup + response "
-                         "fill, k_srv_pull1); 0: the three kernels"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
