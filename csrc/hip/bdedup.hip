@@ -70,15 +70,26 @@ static constexpr int kBdTarget = 2048;  // target occurrences per bucket
 // bucket must stay small enough that N of them fit one server workgroup's
 // table after its sub-bucket split
 static constexpr int kBdTargetDist = 1024;
-static int bd_target(int nranks) { return nranks > 1 ? kBdTargetDist : kBdTarget; }
+// SS_BD_TARGET (one rank): occurrences per bucket, 1024..3584 (A/B: larger
+// buckets make each (chunk, bucket) run of the scatter longer — fewer partial
+// lines — at the price of a fuller LDS table in the dedup)
+static int bd_target(int nranks) {
+  static const int one = [] {
+    const char* e = std::getenv("SS_BD_TARGET");
+    const int v = e ? std::atoi(e) : kBdTarget;
+    return v < 1024 ? 1024 : (v > 3584 ? 3584 : v);
+  }();
+  return nranks > 1 ? kBdTargetDist : one;
+}
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
 static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
 static constexpr int kBdMaxSub = 64;    // server sub-buckets per bucket (srv_sub_buckets)
 
-// (key, sample) record of the scatter -> dedup hand-off: 16 bytes (uint4, one
-// dwordx4) or 12 (three dwords, one dwordx3 store / load: 25 % fewer bytes
-// of the route stream's largest array; SS_BD_REC=12|16)
+// (key, sample) record of the scatter -> dedup hand-off: 12 bytes (three
+// dwords, one dwordx3 store / load) or 16 (uint4, one dwordx4; SS_BD_REC=16).
+// 12: 25 % fewer bytes of the route stream's largest array; the bench step
+// 0.850-0.854 -> 0.836-0.841 ms (three interleaved A/B pairs on one box)
 struct alignas(4) BdRec3 {
   uint32_t x, y, z;
 };
@@ -983,7 +994,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   // record width (SS_BD_REC): 16 or 12 bytes
   static const int rw = [] {
     const char* e = std::getenv("SS_BD_REC");
-    return e && std::atoi(e) == 12 ? 3 : 4;
+    return e && std::atoi(e) == 16 ? 4 : 3;
   }();
 #define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \

@@ -155,9 +155,11 @@ class PSEngine(HostRounds):
         frag_num = frag_num or max(1024, 8 * len(self.server_ranks))
         self.router = HashFrag(len(self.server_ranks), frag_num)
         self.frag_map = self.router.rank_map(self.server_ranks)
-        # SS_ENGINE_GENERAL=1|rccl|xgmi runs a 1-GPU job through the N>1 path
-        self.fast1 = (self.gpu and self.world == 1 and
-                      os.environ.get("SS_ENGINE_GENERAL", "0") == "0")
+        # SS_ENGINE_GENERAL=1|rccl|xgmi runs a 1-GPU job through the N>1 path;
+        # so does a 1-rank engine handed an N>1 data plane (a size-1 mailbox
+        # arena or communicator)
+        self.fast1 = (self.gpu and self.world == 1 and isinstance(self.t, LoopbackTransport)
+                      and os.environ.get("SS_ENGINE_GENERAL", "0") == "0")
         self.dist = not self.fast1
         from .xgmi import XgmiTransport
 

@@ -65,9 +65,11 @@ KNOBS: dict[str, Knob] = {
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
     "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
-    "SS_BD_REC": Knob("16", "csrc/hip/bdedup.hip", "tuning",
-                      "bytes of the scatter -> dedup (key, sample) record: 16 (dwordx4) or 12 "
-                      "(dwordx3)"),
+    "SS_BD_REC": Knob("12", "csrc/hip/bdedup.hip", "tuning",
+                      "bytes of the scatter -> dedup (key, sample) record: 12 (dwordx3) or 16 "
+                      "(dwordx4); 12 measured 0.836-0.841 vs 0.850-0.854 ms/step (3 A/B pairs)"),
+    "SS_BD_TARGET": Knob("2048", "csrc/hip/bdedup.hip", "tuning",
+                         "one rank: target occurrences per dedup bucket (1024..3584)"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
