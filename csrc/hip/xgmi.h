@@ -95,6 +95,7 @@ void launch_xwait(char* arena, const XWait& W, unsigned long long* waited, unsig
 // litmus patterns: word i of a segment = mix(seed, i); check counts mismatches
 void launch_xpattern(int* dst, long long words, unsigned seed, hipStream_t st);
 void launch_xcheck(const int* src, long long words, unsigned seed, int* bad, hipStream_t st);
+void launch_spin(double us, hipStream_t st);
 
 // put workgroups per peer for segments of at most `maxseg` bytes: ~32 KB per
 // block, 8 at least, capped by `cap`.  Every block drains and arrives on one

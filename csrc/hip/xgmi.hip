@@ -227,6 +227,19 @@ __global__ __launch_bounds__(256) void k_xcheck(const int* src, long long words,
   if (n) atomicAdd(bad, n);
 }
 
+// one wave busy for `ticks` of the 100 MHz wall clock: a slow device on
+// demand (SS_FAULT=gpudelay: a straggler whose GPU work takes longer)
+__global__ __launch_bounds__(64) void k_spin(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+void launch_spin(double us, hipStream_t st) {
+  if (us <= 0) return;
+  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, st, (long long)(us * 100.0));
+  check_launch("k_spin");
+}
+
 void launch_xput(const XPut& P, unsigned long long* arrive, unsigned int* err, hipStream_t st) {
   hipLaunchKernelGGL(k_xput, dim3(P.bpp, P.nranks), dim3(kXPutThreads), 0, st, P, arrive, err);
   check_launch("k_xput");
@@ -345,6 +358,9 @@ void bind_xgmi(py::module_& m) {
                          uintptr_t st) {
     ss::launch_xcheck(reinterpret_cast<const int*>(src), words, seed, reinterpret_cast<int*>(bad),
                       reinterpret_cast<hipStream_t>(st));
+  });
+  m.def("spin_us", [](double us, uintptr_t st) {
+    ss::launch_spin(us, reinterpret_cast<hipStream_t>(st));
   });
   m.def("device_pci_id", [](int device) {
     char buf[64] = {0};

@@ -169,9 +169,12 @@ class Heartbeat:
 
 
 class FaultInjector:
-    """``SS_FAULT=kind[:rank=R][:step=S][:secs=T][:ms=M]``; kind in hang,
-    crash, slow (once, at step S) and delay (a straggler: rank R's host loop
-    sleeps M ms in EVERY step from S on; ``delay:<rank>:<ms>`` also parses)."""
+    """``SS_FAULT=kind[:rank=R][:step=S][:secs=T][:ms=M][:p=P]``; kind in
+    hang, crash, slow (once, at step S), delay (a straggler: rank R's host
+    loop sleeps M ms in every step from S on, or in a fraction P of them;
+    ``delay:<rank>:<ms>`` also parses) and gpudelay (the same as device work:
+    a kernel that keeps one wave busy for M ms on the rank's current stream —
+    a slow or contended GPU rather than a slow host)."""
 
     def __init__(self, spec: Optional[str] = None, rank: int = 0):
         spec = spec if spec is not None else os.environ.get("SS_FAULT", "")
@@ -182,9 +185,10 @@ class FaultInjector:
             return
         parts = spec.split(":")
         self.kind = parts[0]
-        if self.kind not in ("hang", "crash", "slow", "delay"):
+        self.p = 1.0
+        if self.kind not in ("hang", "crash", "slow", "delay", "gpudelay"):
             raise ValueError(f"SS_FAULT kind {self.kind!r}")
-        if self.kind == "delay":
+        if self.kind in ("delay", "gpudelay"):
             self.secs = 0.001
             pos = [p for p in parts[1:] if "=" not in p]
             if pos:  # delay:<rank>:<ms>
@@ -201,13 +205,26 @@ class FaultInjector:
                 self.secs = float(v)
             elif k == "ms":
                 self.secs = float(v) / 1e3
+            elif k == "p":
+                self.p = float(v)
 
     def maybe(self, step: int) -> None:
         if self.kind is None or (self.rank is not None and self.rank != self.me):
             return
-        if self.kind == "delay":
-            if step >= self.step:
+        if self.kind in ("delay", "gpudelay"):
+            # a fraction p of the steps, chosen by a hash of the step (the
+            # same steps on every run)
+            if step < self.step or (self.p < 1.0 and
+                                    ((step * 2654435761) % 1000003) / 1000003.0 >= self.p):
+                return
+            if self.kind == "delay":
                 time.sleep(self.secs)
+            else:
+                import torch
+
+                from .._native import hip
+
+                hip().spin_us(self.secs * 1e6, torch.cuda.current_stream().cuda_stream)
             return
         if step != self.step:
             return

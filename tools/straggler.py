@@ -31,6 +31,10 @@ def main() -> int:
     ap.add_argument("--world", type=int, default=4)
     ap.add_argument("--delays", default="0,2,5,10", help="ms per step on rank 1")
     ap.add_argument("--staleness", default="0,1,2")
+    ap.add_argument("--kind", default="delay", choices=["delay", "gpudelay"],
+                    help="delay: rank 1's host loop sleeps; gpudelay: a kernel keeps its GPU "
+                         "busy (a slow device)")
+    ap.add_argument("--p", type=float, default=1.0, help="fraction of steps delayed (jitter)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "straggler"))
     ap.add_argument("--timeout", type=float, default=300.0)
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
@@ -42,7 +46,7 @@ def main() -> int:
         for d in [float(x) for x in a.delays.split(",")]:
             env = dict(os.environ, SS_STALENESS=str(k), SS_PULL_AHEAD="1" if k else "0")
             if d > 0:
-                env["SS_FAULT"] = f"delay:1:{d:g}"
+                env["SS_FAULT"] = f"{a.kind}:rank=1:ms={d:g}" + (f":p={a.p:g}" if a.p < 1 else "")
             out = os.path.join(a.out, f"k{k}_d{d:g}")
             cmd = [sys.executable, os.path.join(ROOT, "tools", "prof_world.py"), "--world",
                    str(a.world), "--no-prof", "--out", out, "--timeout", str(a.timeout), "--",
@@ -56,13 +60,13 @@ def main() -> int:
                       file=sys.stderr)
                 return 1
             j = json.loads(js[-1])
-            row = {"staleness": k, "delay_ms": d, "ms_per_step": j["ms_per_step"],
+            row = {"kind": a.kind, "p": a.p, "staleness": k, "delay_ms": d, "ms_per_step": j["ms_per_step"],
                    "pull_ahead": j["config"].get("pull_ahead"), "loss_last":
                    j["config"]["loss_last"], "wall_s": round(time.time() - t0, 1)}
             rows.append(row)
             print(json.dumps(row), flush=True)
     base = {r["staleness"]: r["ms_per_step"] for r in rows if r["delay_ms"] == 0}
-    with open(os.path.join(a.out, "straggler.jsonl"), "w") as f:
+    with open(os.path.join(a.out, f"straggler_{a.kind}_p{a.p:g}.jsonl"), "w") as f:
         for r in rows:
             f.write(json.dumps(r) + "\n")
     print(f"\n| staleness | delay (ms/step on rank 1) | ms/step | added vs no delay | "
@@ -70,7 +74,7 @@ def main() -> int:
     print("|---|---|---|---|---|")
     for r in rows:
         add = r["ms_per_step"] - base.get(r["staleness"], r["ms_per_step"])
-        ab = 1.0 - add / r["delay_ms"] if r["delay_ms"] > 0 else float("nan")
+        ab = 1.0 - add / (r["delay_ms"] * a.p) if r["delay_ms"] > 0 else float("nan")
         print(f"| {r['staleness']} | {r['delay_ms']:g} | {r['ms_per_step']:.3f} | {add:+.3f} | "
               f"{ab:.0%} |")
     return 0
