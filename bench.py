@@ -243,6 +243,7 @@ def main(argv=None):
                 "fell_back": plane.fell_back,
                 **({"fallback_reason": plane.fallback_reason[:300]} if plane.fell_back else {}),
                 "devices": plane.devices,
+                **({"litmus": plane.litmus} if plane.litmus else {}),
                 "init": a.init,
                 "comms": comms,
                 "rccl_nranks": rccl_n,

@@ -286,6 +286,9 @@ class PipelinedWorker:
             eng.barrier()
             times[mode] = eng.max_over_ranks(time.perf_counter() - t0) / steps
         best = times[True] < times[False]
+        pick = os.environ.get("SS_CAL_PICK", "")  # debug: force the outcome
+        if pick in ("sync", "ahead"):
+            best = pick == "ahead"
         self.set_pull_ahead(best)
         self.drain()
         return {"pull_ahead": best, "staleness": eng.lookahead if best else 0,

@@ -37,6 +37,9 @@ KNOBS: dict[str, Knob] = {
                          "log level (Python and the native runtime)"),
     "SS_LOCAL_IP": Knob("auto", "csrc/host/transfer.h", "ops",
                         "address the host-mode roles advertise"),
+    "SS_CAL_PICK": Knob("", "models/base.py", "debug",
+                        "sync|ahead: force the pull-ahead calibration's outcome (it still "
+                        "measures both)"),
     "SS_GRAPH": Knob("1", "models/base.py", "ops",
                      "0: enable_graph() declines (replay is requested by config `graph` or "
                      "bench --graph)"),

@@ -72,7 +72,8 @@ def test_stale_round_tag_is_detected():
         del os.environ["SS_XGMI_VERIFY"]
 
 
-def _bench(env, extra=(), nproc=1):
+def _bench(env, extra=(), nproc=1, shape=("--steps", "4", "--warmup", "2", "--batch", "4096",
+                                          "--features", "2000000")):
     e = dict(os.environ, GLOO_SOCKET_IFNAME="lo", **env)
     if nproc == 1:
         cmd = [sys.executable, os.path.join(ROOT, "bench.py")]
@@ -82,8 +83,7 @@ def _bench(env, extra=(), nproc=1):
                "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
                "--gpus", str(nproc)]
         e["SS_BENCH_DEVICE"] = "0"
-    cmd += ["--steps", "4", "--warmup", "2", "--batch", "4096", "--features", "2000000",
-            *extra]
+    cmd += [*shape, *extra]
     r = subprocess.run(cmd, cwd=ROOT, env=e, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -116,7 +116,9 @@ def test_bench_world2_fenced_verified():
     """bench.py at N = 2 (both ranks on cuda:0) on the fenced tier with round
     tags verified every wait: the driver's N>1 path on the defensive tier."""
     j, _ = _bench({"SS_XGMI_FORCE_TIER": "fenced", "SS_XGMI_FENCE_ALL": "1",
-                   "SS_XGMI_VERIFY": "1"}, nproc=2)
+                   "SS_XGMI_VERIFY": "1"}, nproc=2,
+                  shape=("--steps", "6", "--warmup", "3", "--batch", "8192", "--features",
+                         "4000000", "--cal-steps", "0"))
     c = j["config"]
     assert c["plane"] == "xgmi" and c["xgmi_tier"] == "fenced" and not c["fell_back"]
     assert c["devices"] == 1 and j["n_gpus"] == 2
