@@ -891,6 +891,13 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
 // many loads per config-3 step); k_w2v_ppctx (one wave per run position)
 // gathers g+ * v over the 2W centers that pair with it.
 static constexpr int kPpMaxK = 16;
+static constexpr int kPpIdx = 8;  // negative indices per lane: 2W * K <= 64 * 8
+// One wave per center; the 2W pairs run as a two-stage pipeline: every
+// index of the center (contexts, pair validity, all 2W x K negatives) is
+// loaded up front, one lane each, and pair o+1's 1 + K rows are in flight
+// while pair o computes — one row-load latency per pair instead of an
+// index load followed by a row load (measured: the per-pair chain, not
+// bandwidth, bounded the kernel).
 template <int D>
 __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv_c,
                                                 const uint32_t* __restrict__ inv_w,
@@ -906,32 +913,42 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
   __shared__ float red[2][4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long long t = (long long)blockIdx.x * 4 + w;
-  const long long Rn = (long long)B + 2 * W;
   float loss = 0.f, npairs = 0.f;
   if (t < B) {  // wave-uniform
-    const int32_t mc = meta[t + W];
-    float v[R], gv[R];
+    const int P2 = 2 * W;
     const uint32_t c = inv_c[t];
+    // lane o < 2W: pair o's context row id (kInv: the pair is not valid)
+    uint32_t xl = kInv;
+    if (lane < P2) {
+      const int dq = lane < W ? lane - W : lane - W + 1;
+      const long long q = t + W + dq;
+      if (c != kInv && w2v_pair_ok(meta[t + W], meta[q], dq)) xl = inv_w[q];
+    }
+    // every negative index of the center: (pair o, k) at o * K + k, lane-strided
+    uint32_t ni[kPpIdx];
+    const long long nb0 = t * (long long)P2 * K;
+#pragma unroll
+    for (int i = 0; i < kPpIdx; ++i) {
+      const int e = i * 64 + lane;
+      ni[i] = e < P2 * K ? inv_n[nb0 + e] : kInv;
+    }
+    float v[R], gv[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const int d = lane + 64 * r;
       v[r] = (d < D && c != kInv) ? uvals[(long long)c * D + d] : 0.f;
       gv[r] = 0.f;
     }
-    for (int o = 0; o < 2 * W; ++o) {
-      const int dq = o < W ? o - W : o - W + 1;
-      const long long q = t + W + dq;
-      const bool ok = c != kInv && w2v_pair_ok(mc, meta[q], dq);
-      const long long nb = (t * 2 * W + o) * (long long)K;
-      if (!ok) {  // the pair's negatives still get a (zero) gradient entry
-        if (lane < K) gnc[nb + lane] = make_float2(0.f, __uint_as_float(kInv));
-        if (lane == 0) gpair[t * 2 * W + o] = 0.f;
-        continue;
-      }
-      // every row of the pair in flight before the first use
-      const uint32_t xq = inv_w[q];
-      const uint32_t nk = lane < K ? inv_n[nb + lane] : kInv;
-      float u[R], n[kPpMaxK][R];
+    auto nidx = [&](int e) -> uint32_t {  // negative e of the center (wave-uniform e)
+      uint32_t x = kInv;
+#pragma unroll
+      for (int i = 0; i < kPpIdx; ++i)
+        if (e / 64 == i) x = __shfl(ni[i], e % 64, 64);
+      return x;
+    };
+    // rows of pair o into (u, n); nothing when the pair is not valid
+    auto issue = [&](int o, float (&u)[R], float (&n)[kPpMaxK][R]) {
+      const uint32_t xq = __shfl(xl, o, 64);
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const int d = lane + 64 * r;
@@ -939,12 +956,20 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
       }
 #pragma unroll
       for (int k = 0; k < kPpMaxK; ++k) {
-        const uint32_t x = __shfl(nk, k, 64);
+        const uint32_t x = (k < K && xq != kInv) ? nidx(o * K + k) : kInv;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
           const int d = lane + 64 * r;
-          n[k][r] = (k < K && x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
+          n[k][r] = (x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
         }
+      }
+    };
+    auto compute = [&](int o, const float (&u)[R], const float (&n)[kPpMaxK][R]) {
+      const long long nb = (t * P2 + o) * (long long)K;
+      if (__shfl(xl, o, 64) == kInv) {  // the pair's negatives get a zero entry
+        if (lane < K) gnc[nb + lane] = make_float2(0.f, __uint_as_float(kInv));
+        if (lane == 0) gpair[t * P2 + o] = 0.f;
+        return;
       }
       float sp = 0.f;
 #pragma unroll
@@ -954,7 +979,7 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
       if (lane == 0) {
         loss += softplus(-sp);
         npairs += 1.f;
-        gpair[t * 2 * W + o] = gp;
+        gpair[t * P2 + o] = gp;
       }
 #pragma unroll
       for (int r = 0; r < R; ++r) gv[r] += gp * u[r];
@@ -973,6 +998,16 @@ __global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv
         for (int r = 0; r < R; ++r) gv[r] += gn * n[k][r];
       }
       if (lane < K) gnc[nb + lane] = make_float2(gk, __uint_as_float(c));
+    };
+    float ua[R], na[kPpMaxK][R], ub[R], nbuf[kPpMaxK][R];
+    issue(0, ua, na);
+    for (int o = 0; o < P2; o += 2) {
+      if (o + 1 < P2) issue(o + 1, ub, nbuf);
+      compute(o, ua, na);
+      if (o + 1 < P2) {
+        if (o + 2 < P2) issue(o + 2, ua, na);
+        compute(o + 1, ub, nbuf);
+      }
     }
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -1246,6 +1281,7 @@ void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t*
   if (!gnc) throw_error("w2v_pp: the (gn, center) buffer of the negatives is required");
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_pp: window must be in [1, 15]");
   if (K < 1 || K > kPpMaxK) throw_error("w2v_pp: negatives per pair must be in [1, 16]");
+  if (2 * W * K > 64 * kPpIdx) throw_error("w2v_pp: 2W x K must be <= 512");
   const long long Rn = (long long)B + 2 * W;
   switch (D) {
 #define SS_W2VP_CASE(DD)                                                                       \
