@@ -838,23 +838,37 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
   for (uint32_t k0 = 0; k0 < it.y; k0 += QF) {
     VT x[QF], y[QF];
     float sc[QF];
+    long long jj[QF];
+    float2 e[QF];
+    // three phases, so every load of a phase is in flight together: the
+    // occurrence ids, then (per-pair negatives) their (gn, center) pairs,
+    // then the rows
 #pragma unroll
     for (int r = 0; r < QF; ++r) {
       const uint32_t k = k0 + r;
-      const long long j = (long long)__shfl(jl, (int)(k < it.y ? k : 0), 32);
+      const long long jv = (long long)__shfl(jl, (int)(k < it.y ? k : 0), 32);
+      jj[r] = k < it.y ? jv : -1;
+    }
+#pragma unroll
+    for (int r = 0; r < QF; ++r)
+      e[r] = (gnc && jj[r] >= negbase) ? gnc[jj[r] - negbase] : make_float2(1.f, 0.f);
+#pragma unroll
+    for (int r = 0; r < QF; ++r) {
+      const long long j = jj[r];
       sc[r] = 1.f;
-      if (gnc && j >= negbase) {  // a scaled center row (per-pair negative)
-        const float2 e = k < it.y ? gnc[j - negbase] : make_float2(0.f, 0.f);
-        const uint32_t c = __float_as_uint(e.y);
-        const bool on = k < it.y && c != kInv && e.x != 0.f;
-        sc[r] = e.x;
-        x[r] = on ? *reinterpret_cast<const VT*>(uvals + (long long)c * D + hl * V) : VT{};
-        y[r] = VT{};
-        continue;
+      y[r] = VT{};
+      if (j < 0) {
+        x[r] = VT{};
+      } else if (gnc && j >= negbase) {  // a scaled center row (per-pair negative)
+        const uint32_t c = __float_as_uint(e[r].y);
+        sc[r] = e[r].x;
+        x[r] = (c != kInv && e[r].x != 0.f)
+                   ? *reinterpret_cast<const VT*>(uvals + (long long)c * D + hl * V) : VT{};
+      } else {
+        const long long tq = tail_of(j);
+        x[r] = *reinterpret_cast<const VT*>(ograd + j * D + hl * V);
+        if (tq >= 0) y[r] = *reinterpret_cast<const VT*>(otail + tq * D + hl * V);
       }
-      const long long tq = k < it.y ? tail_of(j) : -1;
-      x[r] = k < it.y ? *reinterpret_cast<const VT*>(ograd + j * D + hl * V) : VT{};
-      y[r] = tq >= 0 ? *reinterpret_cast<const VT*>(otail + tq * D + hl * V) : VT{};
     }
 #pragma unroll
     for (int r = 0; r < QF; ++r)

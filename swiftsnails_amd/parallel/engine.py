@@ -234,8 +234,19 @@ class PSEngine(HostRounds):
         if self.dist and self.depth >= 3 and self.lookahead > 0 and \
                 os.environ.get("SS_PULL_AHEAD", "auto") == "1":
             self.pull_ahead = True
-            if self.gpu:
+            if self.gpu and not self.shared_device:
                 self.pull_stream = torch.cuda.Stream(device=self.device)
+
+    @property
+    def shared_device(self) -> bool:
+        """Several ranks of this job run on this rank's GPU (one-GPU
+        rehearsals of an N-rank job).  Their processes' streams then share
+        the device's hardware queues: 8 processes x 3 streams measured
+        2.5x slower than x 2 (HWS oversubscription; GPU_MAX_HW_QUEUES=2
+        restores it), so a pulled-ahead round then runs on the route stream
+        instead of a third stream of its own."""
+        xg = getattr(self, "xg", None)
+        return bool(xg is not None and getattr(xg, "devices", self.world) < self.world)
 
     # ------------------------------------------------------------ N>1 (GPU)
     def _init_dist_gpu(self) -> None:
@@ -495,7 +506,8 @@ class PSEngine(HostRounds):
                 (env != "0" or force):
             self.pull_ahead = True
             want = os.environ.get("SS_PULL_STREAM", "1" if pull_stream else "0") != "0"
-            if self.gpu and self.pull_stream is None and (self.dist or want):
+            if self.gpu and self.pull_stream is None and (self.dist or want) and \
+                    not self.shared_device:
                 self.pull_stream = torch.cuda.Stream(device=self.device)
         elif not on:
             self.pull_ahead = False
