@@ -568,7 +568,8 @@ __global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ luid,
                                                     const float* __restrict__ uvals,
                                                     float* __restrict__ occ, int osi,
-                                                    const uint32_t* __restrict__ pj) {
+                                                    const uint32_t* __restrict__ pj,
+                                                    SelfSeg self) {
   // pj: write sample order instead, occ[pj[p]] (the forward then streams occ)
   __shared__ float sv[kBdTS];
   const int b = blockIdx.x;
@@ -588,7 +589,7 @@ __global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const uint32_t p = pb + r * FT;
-      if (p < p1) occ[q[r]] = l[r] < nu ? sv[l[r]] : 0.f;
+      if (p < p1) self.pick(occ, (long long)q[r])[q[r]] = l[r] < nu ? sv[l[r]] : 0.f;
     }
   }
 }
@@ -608,7 +609,8 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     float* __restrict__ ugrad, int osi,
                                                     const uint8_t* __restrict__ usingle,
                                                     DevTable t, const long long* __restrict__ slots,
-                                                    const float2* __restrict__ snap, OptParams op) {
+                                                    const float2* __restrict__ snap, OptParams op,
+                                                    SelfSeg self) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
@@ -627,7 +629,7 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     }
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
-      g[r] = l[r] != kBdInvalid ? gs[j[r] / (uint32_t)F] : 0.f;
+      g[r] = l[r] != kBdInvalid ? self.pick(gs, (long long)j[r])[j[r] / (uint32_t)F] : 0.f;
       if (xval && l[r] != kBdInvalid) g[r] *= xval[j[r]];
     }
     // keys occurring once in the batch (usingle, from the dedup): a plain
@@ -1058,7 +1060,7 @@ void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const 
   if (n <= 0) return;
   const BdLayout L = bd_layout(n, nranks, ndest);
   hipLaunchKernelGGL(k_bd_fill_occ<512>, dim3(L.P), dim3(512), 0, st, scratch + L.bstart,
-                     scratch + L.ubase, scratch + L.unum, luid, uvals, occ, osi, pj);
+                     scratch + L.ubase, scratch + L.unum, luid, uvals, occ, osi, pj, SelfSeg{});
   check_launch("k_bd_fill_occ");
 }
 
@@ -1097,13 +1099,16 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   }();
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
+                       SelfSeg{});
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
+                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
+                       SelfSeg{});
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
-                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv);
+                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
+                       SelfSeg{});
   check_launch("k_bd_reduce");
 }
 
@@ -1112,7 +1117,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
 void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, const uint32_t* unum,
                         const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
                         float* ugrad, const DevTable* t, const long long* slots,
-                        const float* snap, const OptParams* op, hipStream_t st) {
+                        const float* snap, const OptParams* op, hipStream_t st, SelfSeg self) {
   if (P <= 0) return;
   DevTable tv{};
   OptParams opv{};
@@ -1125,16 +1130,16 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
   }
   hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj, luid,
                      gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
-                     reinterpret_cast<const float2*>(snap), opv);
+                     reinterpret_cast<const float2*>(snap), opv, self);
   check_launch("k_bd_reduce_p");
 }
 
 void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* unum, const uint32_t* luid, const float* uvals,
-                          float* occ, const uint32_t* pj, hipStream_t st) {
+                          float* occ, const uint32_t* pj, hipStream_t st, SelfSeg self) {
   if (P <= 0) return;
   hipLaunchKernelGGL(k_bd_fill_occ<512>, dim3(P), dim3(512), 0, st, bstart, ubase, unum, luid,
-                     uvals, occ, 0, pj);
+                     uvals, occ, 0, pj, self);
   check_launch("k_bd_fill_occ_p");
 }
 

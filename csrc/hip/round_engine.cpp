@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -71,6 +72,7 @@ class RoundEngine {
     keys_.resize(depth);
     vals_.resize(depth);
     grads_.resize(depth);
+    self_keys_.assign(depth, 0);
   }
   ~RoundEngine() {
     hipSetDevice(device_);
@@ -164,7 +166,8 @@ class RoundEngine {
     check_slot(slot);
     if (!ar_.empty()) {
       std::vector<std::vector<long long>> parts;
-      parts.push_back(part(ukeys, ucount, 0, 8, keys_[slot][0], cap_));
+      parts.push_back(part(ukeys, ucount, 0, 8, keys_[slot][0], cap_, self_bypass()));
+      self_keys_[slot] = ukeys;  // the server reads this rank's own keys here
       parts.push_back(part(runs_base, 0, Pd_, 4, keys_[slot][1], Pd_));
       parts.push_back(part(runs_num, 0, Pd_, 4, keys_[slot][2], Pd_));
       if (nkp_ == 4) {
@@ -220,7 +223,7 @@ class RoundEngine {
       launch_srv_dedup(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
                        Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt,
                        S.bstart, S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount,
-                       Pt<uint32_t>(srv_err), St(stream), roff);
+                       Pt<uint32_t>(srv_err), St(stream), roff, self_seg(self_keys_[slot]));
       launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
                             Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
                             G, St(stream), snap ? S.snap : nullptr);
@@ -271,25 +274,28 @@ class RoundEngine {
                  bool scalar_fused, bool snap, uintptr_t merged, bool release) {
     check_xgmi();
     std::vector<std::vector<long long>> parts;
-    parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_));
+    parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_, self_bypass()));
     ar_[slot][2]->put(0, parts, bpp_, stream);
     ar_[slot][2]->wait(0, {}, timeout_, stream, {}, 0.0);
     if (table) {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
+      const SelfSeg sg = self_seg(grads);  // this rank's own gradient rows, in place
       if (update && scalar_fused)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
-                           1, nullptr, &t, S.slots, snap ? S.snap : nullptr, &op, St(stream));
+                           1, nullptr, &t, S.slots, snap ? S.snap : nullptr, &op, St(stream), sg);
       else if (dim_ == 1)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
-                           1, Pt<float>(merged), nullptr, nullptr, nullptr, nullptr, St(stream));
+                           1, Pt<float>(merged), nullptr, nullptr, nullptr, nullptr, St(stream),
+                           sg);
       else if (update)
         launch_srv_merge_rows(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid,
                               Pt<const float>(rgrads), nullptr, dim_, St(stream), &t, S.slots,
-                              &op);
+                              &op, sg);
       else
         launch_srv_merge_rows(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid,
-                              Pt<const float>(rgrads), Pt<float>(merged), dim_, St(stream));
+                              Pt<const float>(rgrads), Pt<float>(merged), dim_, St(stream),
+                              nullptr, nullptr, nullptr, sg);
     }
     if (release) record(kFree, slot, stream, tag);
   }
@@ -309,27 +315,50 @@ class RoundEngine {
   // one part of a put: (src, per-destination displacements, counts, fixed
   // rows, row bytes) in the arena's layout (XgmiArena::put)
   std::vector<long long> part(uintptr_t src, uintptr_t cnt, long long fixed, long long rb,
-                              const XReg& r, long long stride_rows) const {
+                              const XReg& r, long long stride_rows, bool skip_self = false) const {
     std::vector<long long> v = {(long long)src, (long long)cnt, fixed, rb, r.hdr, r.data, r.seg};
     for (int d = 0; d < nranks_; ++d) v.push_back((long long)d * stride_rows * rb);
+    v.push_back(skip_self ? 1 : 0);
     return v;
+  }
+  // this rank's own segment of a (cap-row) exchange, read in place from `ptr`
+  SelfSeg self_seg(uintptr_t ptr) const {
+    SelfSeg s;
+    if (!self_bypass()) return s;
+    s.ptr = reinterpret_cast<char*>(ptr);
+    s.lo = (long long)rank_ * cap_;
+    s.hi = s.lo + cap_;
+    return s;
+  }
+  // SS_XGMI_SELF=0: copy the rank's own segments into its arena like the
+  // peers' (the put kernel's self-copy; A/B)
+  static bool self_bypass() {
+    static const bool on = [] {
+      const char* e = std::getenv("SS_XGMI_SELF");
+      return !(e && e[0] == '0');
+    }();
+    return on;
   }
   void fill_and_return(int slot, uintptr_t stream, uintptr_t svals, uintptr_t rvals,
                        uintptr_t sent, const std::vector<uintptr_t>& metrics) {
     // the rows each source gets back = the keys it sent here (keys header)
     const uintptr_t rc = ar_[slot][0]->base() + keys_[slot][0].hdr;
+    // the rows for this rank's own keys go straight into its vals arena (the
+    // worker reads them there), the peers' into the response buffer the put
+    // sends
+    const SelfSeg sv = self_seg(ar_[slot][1]->base() + vals_[slot].data);
     if (svals) {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
       if (dim_ == 1)
         launch_bd_fill_occ_p(Ps, S.bstart, S.ubase, S.unum, S.luid, Pt<const float>(svals),
-                             Pt<float>(rvals), S.pj, St(stream));
+                             Pt<float>(rvals), S.pj, St(stream), sv);
       else
         launch_srv_fill_rows(Ps, S.bstart, S.ubase, S.pj, S.luid, Pt<const float>(svals),
-                             Pt<float>(rvals), dim_, St(stream));
+                             Pt<float>(rvals), dim_, St(stream), sv);
     }
     std::vector<std::vector<long long>> parts;
-    parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_));
+    parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_, sv.ptr != nullptr && svals));
     ar_[slot][1]->put(0, parts, bpp_, stream);
     std::vector<uintptr_t> m = metrics;
     if (!m.empty()) {
@@ -347,6 +376,7 @@ class RoundEngine {
   std::vector<std::array<XReg, 4>> keys_;
   int nkp_ = 3;  // parts of the keys channel
   std::vector<XReg> vals_, grads_;
+  std::vector<uintptr_t> self_keys_;  // per slot: this rank's send layout of its keys
   int nranks_ = 1, rank_ = 0, Pd_ = 1, sub_ = 1, dim_ = 1, bpp_ = 128;
   long long cap_ = 0;
   double timeout_ = 120.0;

@@ -57,6 +57,7 @@ struct SrvRuns {
   // [nsrc][Pd][m] (m > 1): where sub-bucket t starts in source s's run k
   // (the sender grouped each run by sub-bucket, bdedup.hip msub)
   const uint32_t* roff;
+  SelfSeg self;            // this rank's own keys: the sender's send buffer, not the arena
   __device__ __forceinline__ long long run_start(int s, int k) const {
     return (long long)s * cap + ((long long)rbase[(long long)s * Pd + k] - (long long)me * cap);
   }
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
         int s = 0;
         while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
         const long long pos = sa[s] + (f - so[s]);
-        kk[r] = R.rkeys[pos];
+        kk[r] = R.self.pick(R.rkeys, pos)[pos];
         pj[p0 + f] = (uint32_t)pos;
       }
     }
@@ -274,7 +275,8 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
                                                        const uint32_t* __restrict__ pj,
                                                        const uint32_t* __restrict__ luid,
                                                        const float* __restrict__ rows,
-                                                       float* __restrict__ out, int D) {
+                                                       float* __restrict__ out, int D,
+                                                       SelfSeg self) {
   const int b = blockIdx.x, t = threadIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], base = ubase[b];
   const bool vec = (D & 3) == 0;
@@ -283,12 +285,13 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
   for (uint32_t p = p0 + t / G; p < p1; p += ng) {
     const uint32_t l = luid[p];
     const long long o = (long long)pj[p] * W, r = ((long long)base + l) * W;
+    float* outp = self.pick(out, (long long)pj[p]);
     if (vec) {
-      float4* dst = reinterpret_cast<float4*>(out) + o;
+      float4* dst = reinterpret_cast<float4*>(outp) + o;
       const float4* src = reinterpret_cast<const float4*>(rows) + r;
       for (int c = lg; c < W; c += G) dst[c] = l == kSrvInv ? make_float4(0.f, 0.f, 0.f, 0.f) : src[c];
     } else {
-      for (int c = lg; c < W; c += G) out[o + c] = l == kSrvInv ? 0.f : rows[r + c];
+      for (int c = lg; c < W; c += G) outp[o + c] = l == kSrvInv ? 0.f : rows[r + c];
     }
   }
 }
@@ -310,7 +313,7 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
                                                         float* __restrict__ merged, int D,
                                                         DevTable tab,
                                                         const long long* __restrict__ slots,
-                                                        OptParams op) {
+                                                        OptParams op, SelfSeg self) {
   __shared__ unsigned int off[kSrvTS + 1];
   __shared__ unsigned int cur[kSrvTS];
   __shared__ unsigned short ord[kSrvOcc];
@@ -387,7 +390,8 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
         s2[i] = on && ns > 1 ? row_ld(tab, slot, 2 * D + c) : 0.f;
       }
       for (uint32_t q = a; q < z; ++q) {
-        const float* g = grads + (long long)pj[p0 + ord[q]] * D;
+        const long long gp = pj[p0 + ord[q]];
+        const float* g = self.pick(grads, gp) + gp * D;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const int c = c0 + lg + i * G;
@@ -424,10 +428,10 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
                       long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
                       uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
                       uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
-                      hipStream_t st, const uint32_t* roff) {
+                      hipStream_t st, const uint32_t* roff, SelfSeg self) {
   if (nsrc < 1 || nsrc > kSrvMaxSrc || Pd < 1 || m < 1 || m > 64) throw_error("srv_dedup: bad layout");
   if (m > 1 && !roff) throw_error("srv_dedup: sub-buckets need the senders' offsets (msub)");
-  SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me, roff};
+  SrvRuns R{rkeys, rbase, rnum, cap, nsrc, Pd, m, me, roff, self};
   const int P = Pd * m;
   // cnt has P + 1 words: the last is the count kernel's arrival counter
   // (zeroed once at allocation, reset by the kernel)
@@ -441,24 +445,25 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
 
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
-                          int D, hipStream_t st) {
+                          int D, hipStream_t st, SelfSeg self) {
   if (P <= 0) return;
   hipLaunchKernelGGL(k_srv_fill_rows, dim3(P), dim3(256), 0, st, bstart, ubase, pj, luid, rows,
-                     out, D);
+                     out, D, self);
   check_launch("k_srv_fill_rows");
 }
 
 void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                            const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
                            const float* grads, float* merged, int D, hipStream_t st,
-                           const DevTable* t, const long long* slots, const OptParams* op) {
+                           const DevTable* t, const long long* slots, const OptParams* op,
+                           SelfSeg self) {
   if (P <= 0) return;
   if (slots && (!t || !op || (int)t->dim != D ||
                 (int)t->width != D * (1 + opt_state_per_coord(op->kind))))
     throw_error("srv_merge_rows: a fused update needs the table of these rows");
   if (!slots && !merged) throw_error("srv_merge_rows: merged rows or a fused update");
   hipLaunchKernelGGL(k_srv_merge_rows, dim3(P), dim3(512), 0, st, bstart, ubase, unum, pj, luid,
-                     grads, merged, D, t ? *t : DevTable{}, slots, op ? *op : OptParams{});
+                     grads, merged, D, t ? *t : DevTable{}, slots, op ? *op : OptParams{}, self);
   check_launch("k_srv_merge_rows");
 }
 

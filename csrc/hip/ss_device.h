@@ -139,6 +139,19 @@ __device__ __forceinline__ long long seg_pos(const SegList& sl, long long g, int
   return sl.off[s] + (g - sl.prefix[s]);
 }
 
+// N>1 rounds: a rank's own segment of a mailbox exchange is not copied into
+// its arena — the positions [lo, hi) (source / destination == this rank, in
+// rows) are read from / written to the local buffer the put would have copied
+// (the same row index), every other position from / to the arena
+struct SelfSeg {
+  char* ptr = nullptr;
+  long long lo = 0, hi = 0;
+  template <typename T>
+  __host__ __device__ __forceinline__ T* pick(T* arena, long long pos) const {
+    return (ptr && pos >= lo && pos < hi) ? reinterpret_cast<T*>(ptr) : arena;
+  }
+};
+
 // slots of a per-workgroup LDS hash table for up to n distinct keys: the
 // power of two >= 2n (load <= 1/2), at least 64, at most cap
 __device__ __forceinline__ uint32_t lds_table_size(uint32_t n, uint32_t cap) {

@@ -177,10 +177,11 @@ long long bd_fm_ovf_words(long long n);
 void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, const uint32_t* unum,
                         const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
                         float* ugrad, const DevTable* t, const long long* slots,
-                        const float* snap, const OptParams* op, hipStream_t st);
+                        const float* snap, const OptParams* op, hipStream_t st,
+                        SelfSeg self = {});
 void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* unum, const uint32_t* luid, const float* uvals,
-                          float* occ, const uint32_t* pj, hipStream_t st);
+                          float* occ, const uint32_t* pj, hipStream_t st, SelfSeg self = {});
 
 // --- server.hip (N>1: merge of the keys a round receives from all sources)
 int srv_sub_buckets(int nsrc);
@@ -188,15 +189,15 @@ void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32
                       long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
                       uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,
                       uint32_t* ubase, uint32_t* unum, unsigned long long* ucount, uint32_t* err,
-                      hipStream_t st, const uint32_t* roff = nullptr);
+                      hipStream_t st, const uint32_t* roff = nullptr, SelfSeg self = {});
 void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
-                          int D, hipStream_t st);
+                          int D, hipStream_t st, SelfSeg self = {});
 void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                            const uint32_t* unum, const uint32_t* pj, const uint32_t* luid,
                            const float* grads, float* merged, int D, hipStream_t st,
                            const DevTable* t = nullptr, const long long* slots = nullptr,
-                           const OptParams* op = nullptr);
+                           const OptParams* op = nullptr, SelfSeg self = {});
 
 // --- w2v.hip
 size_t w2v_smem_bytes(int D);

@@ -56,6 +56,8 @@ struct XPart {
   long long hdr_off;                  // arena offset of this part's [nranks] count header
   long long data_off;                 // arena offset of its [nranks][seg_bytes] data
   long long seg_bytes;                // per-source segment capacity
+  int skip_self;                      // this rank's own segment is read in place by its
+                                      // consumer (SelfSeg): header and arrival only
 };
 
 struct XPut {
@@ -179,8 +181,8 @@ class XgmiArena {
     verify_ = verify;
   }
 
-  // parts: (src, sdispl bytes [nranks], cnt dev ptr or 0, cnt_fixed, row_bytes,
-  //         hdr_off, data_off, seg_bytes)
+  // parts: (src, cnt dev ptr or 0, cnt_fixed, row_bytes, hdr_off, data_off,
+  //         seg_bytes, sdispl bytes [nranks] [, skip_self])
   void put(int ch, const std::vector<std::vector<long long>>& parts, int bpp, uintptr_t stream) {
     if (ch < 0 || ch >= kXMaxCh) throw_error("xgmi: bad channel");
     if (parts.empty() || (int)parts.size() > kXMaxParts) throw_error("xgmi: 1..4 parts");
@@ -204,7 +206,8 @@ class XgmiArena {
     P.ticket = local_ + kXTicketOff + ch;
     for (size_t q = 0; q < parts.size(); ++q) {
       const auto& v = parts[q];
-      if ((int)v.size() != 7 + nranks_) throw_error("xgmi: malformed part");
+      if ((int)v.size() != 7 + nranks_ && (int)v.size() != 8 + nranks_)
+        throw_error("xgmi: malformed part");
       XPart& x = P.part[q];
       x.src = reinterpret_cast<const char*>(v[0]);
       x.cnt = reinterpret_cast<const long long*>(v[1]);
@@ -220,6 +223,7 @@ class XgmiArena {
       if (!x.cnt && x.cnt_fixed * x.row_bytes > x.seg_bytes)
         throw_error("xgmi: fixed part larger than its segment");
       for (int r = 0; r < nranks_; ++r) x.sdispl[r] = v[7 + r];
+      x.skip_self = (int)v.size() == 8 + nranks_ ? (int)v[7 + nranks_] : 0;
     }
     // every rank puts to (ch, this arena layout) with the same geometry, so
     // the receiver's tag check uses the block count of its own put

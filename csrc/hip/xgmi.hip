@@ -87,6 +87,7 @@ __global__ __launch_bounds__(kXPutThreads) void k_xput(XPut P, unsigned long lon
     char* o = dst_arena + x.data_off + (long long)P.me * x.seg_bytes;
     if (b == 0 && t == 0)
       *reinterpret_cast<volatile long long*>(dst_arena + x.hdr_off + 8ll * P.me) = rows;
+    if (x.skip_self && d == P.me) continue;  // consumed in place (SelfSeg)
     const long long stride = (long long)P.bpp * kXPutThreads;
     if ((((uintptr_t)s | (uintptr_t)o) & 15) == 0) {
       const long long n16 = bytes >> 4;

@@ -91,6 +91,10 @@ KNOBS: dict[str, Knob] = {
                             "error raised at the next check point)"),
     "SS_XGMI_BPP": Knob("max(128, 1024 / world)", "parallel/xgmi.py", "tuning",
                         "workgroups per peer of a mailbox put"),
+    "SS_XGMI_SELF": Knob("1", "csrc/hip/round_engine.cpp", "tuning",
+                         "1: a rank's own segment of the keys / rows / gradients exchange is read "
+                         "in place by its consumer instead of copied into its own arena by the "
+                         "put (1/N of the put bytes; all of them at N = 1); 0: copied"),
     "SS_XGMI_VERIFY": Knob("0", "parallel/xgmi.py, csrc/hip/xgmi.hip", "ops",
                            "1: every put block writes a round tag after its payload, every "
                            "wait checks all tags (a flag that overtook its data raises at the "
