@@ -178,31 +178,36 @@ class XgmiTransport(Transport):
         all raise)."""
         import time
 
-        if err is not None:
-            self._agree_ok(False)
-            raise RuntimeError(f"xgmi set-up failed on this rank: {err}")
+        # every rank agrees on the set-up first: a rank that could not map
+        # its peers must not leave the others in a litmus it never joins
+        ok, _ = self._agree_ok(err is None)
+        if not ok:
+            raise RuntimeError(f"xgmi set-up failed on {'this rank' if err else 'a peer'}"
+                               + (f": {err}" if err else ""))
         reasons = []
         for tier in self.TIERS:
             self._set_tier(tier)
             forced = self.force_tier == "rccl" or (self.force_tier == "fenced" and tier == "drain")
             t0 = time.perf_counter()
             ok, why = self._litmus(fail=forced)
-            ok = self._agree_ok(ok)
+            # agreed collectively: passed on every rank; timed out on any
+            ok, timed_out = self._agree_ok(ok, why == "timeout")
             dt = time.perf_counter() - t0
             self.litmus_log.append((tier, ok, round(dt, 3), "" if ok else (why or "a peer failed")))
             if ok:
                 self.tier = tier
                 return
             reasons.append(f"{tier}: {why or 'a peer failed'}")
-            if why == "timeout":
+            if timed_out:
                 break  # the arrival counters are no longer in step: no retry
         raise RuntimeError("xgmi litmus failed on every tier (" + "; ".join(reasons) + ")")
 
-    def _agree_ok(self, ok: bool) -> bool:
-        flag = torch.tensor([1 if ok else 0], dtype=torch.int64)
+    def _agree_ok(self, ok: bool, timed_out: bool = False):
+        """(every rank ok, any rank timed out), the same on every rank."""
+        flag = torch.tensor([1 if ok else 0, 0 if timed_out else 1], dtype=torch.int64)
         if self.aux is not None and self.world > 1:
             self.aux.allreduce_(flag, "min")
-        return int(flag.item()) == 1
+        return int(flag[0].item()) == 1, int(flag[1].item()) == 0
 
     @staticmethod
     def _seed(rnd: int, src: int, dst: int, ch: int, part: int) -> int:
@@ -212,57 +217,43 @@ class XgmiTransport(Transport):
 
     def _litmus(self, fail: bool = False):
         """Message-passing litmus on the real arenas (see the module doc).
-        Returns (passed on this rank, reason)."""
+        Returns (passed on this rank, reason).  A rank whose GPU work fails
+        keeps taking every round's barrier (its peers' waits on it time out)
+        so the ranks never diverge in their collectives."""
         from .._native import hip
 
         h = hip()
-        N, me, dev = self.world, self.rank, self.device
+        N, dev = self.world, self.device
         st = torch.cuda.current_stream(dev)
         names = sorted(self._channels)
         rounds = max(2, 2 * max(int(sl) for sl, _ in self._channels.values()))
-        bad = torch.zeros(1, dtype=torch.int32, device=dev)
-        cnt_bad = torch.zeros(1, dtype=torch.int64, device=dev)
-        srcs = {}
-        for ci, name in enumerate(names):
-            for p, seg in enumerate(self._channels[name][1]):
-                if int(seg) % 4:
-                    return False, f"segment of {name}/{p} not whole words"
-                srcs[(name, p)] = torch.empty(N * int(seg) // 4, dtype=torch.int32, device=dev)
+        failed, srcs = None, {}
         try:
-            for rnd in range(rounds):
-                for ci, name in enumerate(names):
-                    slots, parts = self._channels[name]
-                    slot = rnd % int(slots)
-                    spec = []
-                    for p, seg in enumerate(parts):
-                        w = int(seg) // 4
-                        src = srcs[(name, p)]
-                        for d in range(N):
-                            h.xgmi_pattern(src.data_ptr() + 4 * d * w, w,
-                                           self._seed(rnd, me, d, ci, p), st.cuda_stream)
-                        full = torch.full((N,), w, dtype=torch.int64, device=dev)
-                        spec.append((src, [d * w for d in range(N)], full, None))
-                        srcs[(name, p, "cnt")] = full  # alive until the put ran
-                    self.put(name, slot, spec, stream=st)
-                    self.wait(name, slot, stream=st)
-                    for p, seg in enumerate(parts):
-                        w = int(seg) // 4
-                        got = self.region(name, p, slot, torch.int32)
-                        for s_ in range(N):
-                            h.xgmi_check(got.data_ptr() + 4 * s_ * w, w,
-                                         self._seed(rnd, s_, me, ci, p), bad.data_ptr(),
-                                         st.cuda_stream)
-                        cnt_bad += (self.counts(name, p, slot) != w).sum()
-                # no rank rewrites a slot before every receiver checked it
-                st.synchronize()
-                if self.aux is not None and N > 1:
-                    self.aux.barrier()
-            st.synchronize()
+            bad = torch.zeros(1, dtype=torch.int32, device=dev)
+            cnt_bad = torch.zeros(1, dtype=torch.int64, device=dev)
+            for name in names:
+                for p, seg in enumerate(self._channels[name][1]):
+                    if int(seg) % 4:
+                        raise ValueError(f"segment of {name}/{p} not whole words")
+                    srcs[(name, p)] = torch.empty(N * int(seg) // 4, dtype=torch.int32,
+                                                  device=dev)
         except Exception as e:  # pragma: no cover - hardware dependent
-            return False, f"exception: {e}"
+            failed = f"exception: {e}"
+        for rnd in range(rounds):
+            if failed is None:
+                try:
+                    self._litmus_round(h, rnd, names, srcs, bad, cnt_bad, st)
+                    st.synchronize()
+                except Exception as e:  # pragma: no cover - hardware dependent
+                    failed = f"exception: {e}"
+            # no rank rewrites a slot before every receiver checked it
+            if self.aux is not None and N > 1:
+                self.aux.barrier()
         errs = [int(e[0].item()) for e in self._errs]
         if any(e & 1 for e in errs):
             return False, "timeout"
+        if failed is not None:
+            return False, failed
         if any(e for e in errs):
             return False, f"error word {max(errs)}"
         nb, nc = int(bad.item()), int(cnt_bad.item())
@@ -271,6 +262,37 @@ class XgmiTransport(Transport):
         if fail:
             return False, "forced (SS_XGMI_FORCE_TIER)"
         return True, ""
+
+    def _litmus_round(self, h, rnd: int, names, srcs, bad, cnt_bad, st) -> None:
+        """One litmus round: every channel's slot rnd % slots, full-size
+        segments stamped (round, source, destination, channel, part), put,
+        waited for, every received word checked."""
+        N, me, dev = self.world, self.rank, self.device
+        tmo = min(self.timeout_s, float(os.environ.get("SS_XGMI_LITMUS_TIMEOUT", "30")))
+        for ci, name in enumerate(names):
+            slots, parts = self._channels[name]
+            slot = rnd % int(slots)
+            spec = []
+            for p, seg in enumerate(parts):
+                w = int(seg) // 4
+                src = srcs[(name, p)]
+                for d in range(N):
+                    h.xgmi_pattern(src.data_ptr() + 4 * d * w, w,
+                                   self._seed(rnd, me, d, ci, p), st.cuda_stream)
+                full = torch.full((N,), w, dtype=torch.int64, device=dev)
+                spec.append((src, [d * w for d in range(N)], full, None))
+                srcs[(name, p, "cnt")] = full  # alive until the put ran
+            self.put(name, slot, spec, stream=st)
+            # at start-up every rank is ready: a peer that has not arrived
+            # within the litmus timeout is not coming
+            self.wait(name, slot, stream=st, timeout_s=tmo)
+            for p, seg in enumerate(parts):
+                w = int(seg) // 4
+                got = self.region(name, p, slot, torch.int32)
+                for s_ in range(N):
+                    h.xgmi_check(got.data_ptr() + 4 * s_ * w, w, self._seed(rnd, s_, me, ci, p),
+                                 bad.data_ptr(), st.cuda_stream)
+                cnt_bad += (self.counts(name, p, slot) != w).sum()
 
     def _allgather_bytes(self, mine: bytes, tag=0) -> list:
         if self.world == 1:
@@ -365,7 +387,8 @@ class XgmiTransport(Transport):
         self.arenas[(ch, slot)].put(0, spec, self.bpp, st.cuda_stream)
 
     def wait(self, ch: str, slot: int, stream=None, fixed_parts: Sequence = (),
-             metrics: Sequence = (), bytes_per_key: float = 0.0) -> None:
+             metrics: Sequence = (), bytes_per_key: float = 0.0,
+             timeout_s: Optional[float] = None) -> None:
         """Block ``stream`` until every source's put of this (channel, slot)'s
         next round has arrived.  ``fixed_parts``: (part, bytes) of fixed-size
         parts read as zeros if a source never arrives.  ``metrics``: (sent
@@ -378,8 +401,8 @@ class XgmiTransport(Transport):
             fx.append([data, seg, int(nb)])
         st = stream if stream is not None else torch.cuda.current_stream(self.device)
         mp = [t.data_ptr() if t is not None else 0 for t in metrics]
-        self.arenas[(ch, slot)].wait(0, fx, self.timeout_s, st.cuda_stream, mp,
-                                     float(bytes_per_key))
+        self.arenas[(ch, slot)].wait(0, fx, self.timeout_s if timeout_s is None else timeout_s,
+                                     st.cuda_stream, mp, float(bytes_per_key))
 
     def check(self) -> None:
         for e in self._errs:

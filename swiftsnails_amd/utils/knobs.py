@@ -95,6 +95,9 @@ KNOBS: dict[str, Knob] = {
                          "1: a rank's own segment of the keys / rows / gradients exchange is read "
                          "in place by its consumer instead of copied into its own arena by the "
                          "put (1/N of the put bytes; all of them at N = 1); 0: copied"),
+    "SS_XGMI_LITMUS_TIMEOUT": Knob("30", "parallel/xgmi.py", "ops",
+                                   "seconds a start-up litmus wait spins before the tier counts "
+                                   "as failed (timeout: no further xGMI tier, RCCL)"),
     "SS_XGMI_VERIFY": Knob("0", "parallel/xgmi.py, csrc/hip/xgmi.hip", "ops",
                            "1: every put block writes a round tag after its payload, every "
                            "wait checks all tags (a flag that overtook its data raises at the "
