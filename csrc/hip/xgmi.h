@@ -68,6 +68,8 @@ struct XPut {
   int verify;                         // write the round tag of each block (SS_XGMI_VERIFY)
   unsigned long long* sent;           // [ch] rounds put (verify mode)
   unsigned long long* ticket;         // [ch] blocks of this put done (verify mode)
+  int self_lite;                      // every large part skips d == me: block 0 alone
+                                      // serves this rank's own segment and publishes it
   XPart part[kXMaxParts];
 };
 
@@ -204,6 +206,7 @@ class XgmiArena {
     P.verify = verify_;
     P.sent = local_ + kXSentOff + ch;
     P.ticket = local_ + kXTicketOff + ch;
+    long long self_bytes = 0;  // what d == me still copies (parts not skipped)
     for (size_t q = 0; q < parts.size(); ++q) {
       const auto& v = parts[q];
       if ((int)v.size() != 7 + nranks_ && (int)v.size() != 8 + nranks_)
@@ -224,7 +227,12 @@ class XgmiArena {
         throw_error("xgmi: fixed part larger than its segment");
       for (int r = 0; r < nranks_; ++r) x.sdispl[r] = v[7 + r];
       x.skip_self = (int)v.size() == 8 + nranks_ ? (int)v[7 + nranks_] : 0;
+      if (!x.skip_self) self_bytes += x.seg_bytes;
     }
+    // the own segment's leftovers (bucket-run tables) are small: one block,
+    // no arrival counting (the verify tags of the other blocks then stay
+    // unwritten, so verify mode keeps the full grid)
+    P.self_lite = !verify_ && self_bytes <= (256ll << 10);
     // every rank puts to (ch, this arena layout) with the same geometry, so
     // the receiver's tag check uses the block count of its own put
     put_bpp_[ch] = P.bpp;

@@ -69,6 +69,11 @@ __global__ __launch_bounds__(kXPutThreads) void k_xput(XPut P, unsigned long lon
                                                        unsigned int* err) {
   const int d = blockIdx.y, b = blockIdx.x, t = threadIdx.x;
   char* dst_arena = P.peer[d];
+  // this rank's own segment, consumed in place (SelfSeg): block 0 writes the
+  // headers and the small parts and publishes; the other blocks have nothing
+  // to do and do not arrive
+  const bool lite = P.self_lite && d == P.me;
+  if (lite && b > 0) return;
   // verify mode: this put's round = rounds put so far + 1 (the counter only
   // moves after every block of the put has read it: ticket below)
   const unsigned round =
@@ -88,7 +93,7 @@ __global__ __launch_bounds__(kXPutThreads) void k_xput(XPut P, unsigned long lon
     if (b == 0 && t == 0)
       *reinterpret_cast<volatile long long*>(dst_arena + x.hdr_off + 8ll * P.me) = rows;
     if (x.skip_self && d == P.me) continue;  // consumed in place (SelfSeg)
-    const long long stride = (long long)P.bpp * kXPutThreads;
+    const long long stride = lite ? (long long)kXPutThreads : (long long)P.bpp * kXPutThreads;
     if ((((uintptr_t)s | (uintptr_t)o) & 15) == 0) {
       const long long n16 = bytes >> 4;
       const int4* s4 = reinterpret_cast<const int4*>(s);
@@ -105,6 +110,12 @@ __global__ __launch_bounds__(kXPutThreads) void k_xput(XPut P, unsigned long lon
   // drain this block's (uncached) stores to the fabric, then arrive
   xdrain();
   __syncthreads();
+  if (lite) {  // the only block of the own segment: publish it directly
+    if (t == 0)
+      __hip_atomic_fetch_add(xflag(dst_arena, P.ch, P.me), 1ull, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   if (t == 0) {
     const bool fence = P.fenced && ((P.remote >> d) & 1u);
     if (P.verify) {
