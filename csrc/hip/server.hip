@@ -282,7 +282,8 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
   const bool vec = (D & 3) == 0;
   const int W = vec ? D >> 2 : D;  // chunks per row
   const int G = srv_group(W), lg = t % G, ng = 256 / G;
-  for (uint32_t p = p0 + t / G; p < p1; p += ng) {
+  // gridDim.y workgroups share a bucket (few, large buckets: word2vec)
+  for (uint32_t p = p0 + blockIdx.y * ng + t / G; p < p1; p += gridDim.y * ng) {
     const uint32_t l = luid[p];
     const long long o = (long long)pj[p] * W, r = ((long long)base + l) * W;
     float* outp = self.pick(out, (long long)pj[p]);
@@ -373,7 +374,9 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
   // instruction a strided 512-byte span)
   const int G = srv_group((D + 3) / 4), lg = t % G;
   const uint32_t kpp = 512 / G;       // keys in flight per workgroup
-  for (uint32_t l = (uint32_t)(t / G); l < nu; l += kpp) {
+  // gridDim.y workgroups share a bucket (each sorted the bucket's positions
+  // above; few, large buckets: word2vec at one rank has ~50)
+  for (uint32_t l = blockIdx.y * kpp + (uint32_t)(t / G); l < nu; l += gridDim.y * kpp) {
     const uint32_t a = off[l], z = off[l + 1];
     const long long slot = slots ? slots[(long long)base + l] : -1;
     const bool upd = slots && slot >= 0;
@@ -416,6 +419,13 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
 }
 
 // ------------------------------------------------------------- launchers
+// workgroups per server bucket of the wide-row fill / merge: enough for ~1024
+// workgroups in all (word2vec's ~50 buckets of ~500 keys left 200 CUs idle)
+static int srv_share(int P) {
+  const int y = 1024 / (P < 1 ? 1 : P);
+  return y < 1 ? 1 : (y > 8 ? 8 : y);
+}
+
 int srv_sub_buckets(int nsrc) {
   // N sources x ~1024 keys (<= ~1.25x that with hash imbalance) per bucket k,
   // at most ~3000 distinct keys per 4096-slot table
@@ -447,8 +457,8 @@ void launch_srv_fill_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* pj, const uint32_t* luid, const float* rows, float* out,
                           int D, hipStream_t st, SelfSeg self) {
   if (P <= 0) return;
-  hipLaunchKernelGGL(k_srv_fill_rows, dim3(P), dim3(256), 0, st, bstart, ubase, pj, luid, rows,
-                     out, D, self);
+  hipLaunchKernelGGL(k_srv_fill_rows, dim3(P, srv_share(P)), dim3(256), 0, st, bstart, ubase, pj,
+                     luid, rows, out, D, self);
   check_launch("k_srv_fill_rows");
 }
 
@@ -462,7 +472,8 @@ void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                 (int)t->width != D * (1 + opt_state_per_coord(op->kind))))
     throw_error("srv_merge_rows: a fused update needs the table of these rows");
   if (!slots && !merged) throw_error("srv_merge_rows: merged rows or a fused update");
-  hipLaunchKernelGGL(k_srv_merge_rows, dim3(P), dim3(512), 0, st, bstart, ubase, unum, pj, luid,
+  hipLaunchKernelGGL(k_srv_merge_rows, dim3(P, srv_share(P)), dim3(512), 0, st, bstart, ubase,
+                     unum, pj, luid,
                      grads, merged, D, t ? *t : DevTable{}, slots, op ? *op : OptParams{}, self);
   check_launch("k_srv_merge_rows");
 }
