@@ -803,8 +803,9 @@ struct OVec<1> {
 // `gnc` (per-pair negatives): occurrence j >= `negbase` is the negative row
 // gn * v_c, stored by k_w2v_pp as the pair (gn, c) — 8 bytes instead of a
 // D-float row — and expanded here from the center row uvals[c] (the step's
-// center rows: a few MB, cache-resident)
-template <int D>
+// center rows: a few MB, cache-resident).  SC: the per-pair form; the window
+// tile's reduce (no scaled rows) keeps its one-phase loop.
+template <int D, bool SC>
 __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ items, long long n,
                                                      const uint32_t* __restrict__ ord,
                                                      const float* __restrict__ ograd,
@@ -837,12 +838,26 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
   for (uint32_t k0 = 0; k0 < it.y; k0 += QF) {
     VT x[QF], y[QF];
+    if constexpr (!SC) {
+#pragma unroll
+      for (int r = 0; r < QF; ++r) {
+        const uint32_t k = k0 + r;
+        const long long j = (long long)__shfl(jl, (int)(k < it.y ? k : 0), 32);
+        const long long tq = k < it.y ? tail_of(j) : -1;
+        x[r] = k < it.y ? *reinterpret_cast<const VT*>(ograd + j * D + hl * V) : VT{};
+        y[r] = tq >= 0 ? *reinterpret_cast<const VT*>(otail + tq * D + hl * V) : VT{};
+      }
+#pragma unroll
+      for (int r = 0; r < QF; ++r)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[v] += OVec<V>::get(x[r], v) + OVec<V>::get(y[r], v);
+      continue;
+    }
     float sc[QF];
     long long jj[QF];
     float2 e[QF];
     // three phases, so every load of a phase is in flight together: the
-    // occurrence ids, then (per-pair negatives) their (gn, center) pairs,
-    // then the rows
+    // occurrence ids, then the negatives' (gn, center) pairs, then the rows
 #pragma unroll
     for (int r = 0; r < QF; ++r) {
       const uint32_t k = k0 + r;
@@ -851,7 +866,7 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
     }
 #pragma unroll
     for (int r = 0; r < QF; ++r)
-      e[r] = (gnc && jj[r] >= negbase) ? gnc[jj[r] - negbase] : make_float2(1.f, 0.f);
+      e[r] = jj[r] >= negbase ? gnc[jj[r] - negbase] : make_float2(1.f, 0.f);
 #pragma unroll
     for (int r = 0; r < QF; ++r) {
       const long long j = jj[r];
@@ -859,21 +874,19 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
       y[r] = VT{};
       if (j < 0) {
         x[r] = VT{};
-      } else if (gnc && j >= negbase) {  // a scaled center row (per-pair negative)
+      } else if (j >= negbase) {  // a scaled center row (per-pair negative)
         const uint32_t c = __float_as_uint(e[r].y);
         sc[r] = e[r].x;
         x[r] = (c != kInv && e[r].x != 0.f)
                    ? *reinterpret_cast<const VT*>(uvals + (long long)c * D + hl * V) : VT{};
       } else {
-        const long long tq = tail_of(j);
         x[r] = *reinterpret_cast<const VT*>(ograd + j * D + hl * V);
-        if (tq >= 0) y[r] = *reinterpret_cast<const VT*>(otail + tq * D + hl * V);
       }
     }
 #pragma unroll
     for (int r = 0; r < QF; ++r)
 #pragma unroll
-      for (int v = 0; v < V; ++v) acc[v] += sc[r] * OVec<V>::get(x[r], v) + OVec<V>::get(y[r], v);
+      for (int v = 0; v < V; ++v) acc[v] += sc[r] * OVec<V>::get(x[r], v);
   }
   float* g = ugrad + (long long)it.z * D + hl * V;
   if (it.w & 1u) {
@@ -1244,9 +1257,13 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
   switch (D) {
 #define SS_W2VO_CASE(DD)                                                                      \
   case DD:                                                                                    \
-    hipLaunchKernelGGL(k_w2v_oreduce<DD>, dim3(grid), dim3(256), 0, st, it, n, ord, ograd,    \
-                       otail, B, W, ntiles, ugrad, reinterpret_cast<const float2*>(gnc),       \
-                       negbase, uvals);                                                        \
+    if (gnc)                                                                                  \
+      hipLaunchKernelGGL((k_w2v_oreduce<DD, true>), dim3(grid), dim3(256), 0, st, it, n, ord,  \
+                         ograd, otail, B, W, ntiles, ugrad,                                    \
+                         reinterpret_cast<const float2*>(gnc), negbase, uvals);                \
+    else                                                                                      \
+      hipLaunchKernelGGL((k_w2v_oreduce<DD, false>), dim3(grid), dim3(256), 0, st, it, n, ord, \
+                         ograd, otail, B, W, ntiles, ugrad, nullptr, 0ll, nullptr);            \
     break;
     SS_W2VO_CASE(32)
     SS_W2VO_CASE(64)
