@@ -233,6 +233,7 @@ class XgmiArena {
     // no arrival counting (the verify tags of the other blocks then stay
     // unwritten, so verify mode keeps the full grid)
     P.self_lite = !verify_ && self_bytes <= (256ll << 10);
+    if (P.self_lite && nranks_ == 1) P.bpp = 1;  // nothing but the own segment: one block
     // every rank puts to (ch, this arena layout) with the same geometry, so
     // the receiver's tag check uses the block count of its own put
     put_bpp_[ch] = P.bpp;
