@@ -2,13 +2,27 @@
 """Summarise a rocprofv3 kernel_stats.csv: top kernels by total time, per step.
 
     python tools/kstats.py gpurun_out/prof/run_kernel_stats.csv [steps]
+    python tools/kstats.py gpurun_out/prof/run_results.db [steps]
 """
 import csv
 import sys
 
 
+def _rows(path):
+    """kernel_stats.csv rows, or the same aggregated from a rocprofv3 rocpd
+    database (``run_results.db``, the default output format)."""
+    if not path.endswith(".db"):
+        return list(csv.DictReader(open(path)))
+    import sqlite3
+
+    c = sqlite3.connect(path)
+    q = "select name, count(*), sum(duration), avg(duration) from kernels group by name"
+    return [{"Name": n, "Calls": str(k), "TotalDurationNs": str(t), "AverageNs": str(a)}
+            for n, k, t, a in c.execute(q)]
+
+
 def main(path, steps=None):
-    rows = list(csv.DictReader(open(path)))
+    rows = _rows(path)
     rows.sort(key=lambda r: -float(r["TotalDurationNs"]))
     tot = sum(float(r["TotalDurationNs"]) for r in rows)
     print(f"{'kernel':64s} {'calls':>6} {'avg us':>8} {'total ms':>9} {'%':>5}"
