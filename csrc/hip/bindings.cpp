@@ -470,13 +470,16 @@ PYBIND11_MODULE(_ss_hip, m) {
   });
   m.def("w2v_oreduce", [](uintptr_t items, long long n, uintptr_t ord, uintptr_t ograd,
                           uintptr_t otail, int B, int W, int D, uintptr_t ugrad, uintptr_t st,
-                          uintptr_t gnc, long long negbase, uintptr_t uvals) {
+                          uintptr_t gnc, long long negbase, uintptr_t uvals, uintptr_t acc,
+                          uintptr_t acc_out, int acc_n) {
     launch_w2v_oreduce(P<const uint32_t>(items), n, P<const uint32_t>(ord), P<const float>(ograd),
                        P<const float>(otail), B, W, D, P<float>(ugrad), S(st),
-                       P<const float>(gnc), negbase, P<const float>(uvals));
+                       P<const float>(gnc), negbase, P<const float>(uvals), P<float>(acc),
+                       P<float>(acc_out), acc_n);
   }, py::arg("items"), py::arg("n"), py::arg("ord"), py::arg("ograd"), py::arg("otail"),
      py::arg("B"), py::arg("W"), py::arg("D"), py::arg("ugrad"), py::arg("st"),
-     py::arg("gnc") = 0, py::arg("negbase") = 0, py::arg("uvals") = 0);
+     py::arg("gnc") = 0, py::arg("negbase") = 0, py::arg("uvals") = 0, py::arg("acc") = 0,
+     py::arg("acc_out") = 0, py::arg("acc_n") = 0);
   m.def("w2v_stream_gen", [](uint64_t seed, long long base, int B, int W, int L, long long nneg,
                              long long V, float noise, uintptr_t keys, uintptr_t meta, uintptr_t st,
                              uintptr_t step_dev, long long step_mul, long long step_add) {

@@ -97,7 +97,8 @@ void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t*
 void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
                         const float* otail, int B, int W, int D, float* ugrad, hipStream_t st,
                         const float* gnc = nullptr, long long negbase = 0,
-                        const float* uvals = nullptr);
+                        const float* uvals = nullptr, float* acc = nullptr,
+                        float* acc_out = nullptr, int acc_n = 0);
 void launch_w2v_stream_gen(uint64_t seed, long long base, int B, int W, int L, long long nneg,
                            long long V, float noise, uint64_t* keys, int32_t* meta,
                            hipStream_t st, const long long* step_dev, long long step_mul,

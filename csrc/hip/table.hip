@@ -304,6 +304,75 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
 }
 
 
+// k_pull_unique_bk for wide fp32 rows (word2vec, D = 32 / 64 / 128): 8 lanes
+// per key, each moving D/32 16-byte vectors of the row (a D = 128 row is 32
+// float4s: 8 lanes x 4), so a wave has 8 keys' probe -> row chains in flight
+// instead of one (a 64-lane group per key left the pull latency-bound: 439K
+// distinct 512-B rows of a per-pair step read + written at ~1.3 TB/s).
+static constexpr int kPvL = 8;
+template <int D>
+__global__ __launch_bounds__(256) void k_pull_rows_bk(DevTable t, const uint64_t* __restrict__ bkeys,
+                                                      const uint32_t* __restrict__ bstart,
+                                                      const uint32_t* __restrict__ unum,
+                                                      const uint32_t* __restrict__ ubase,
+                                                      long long* __restrict__ slots_out,
+                                                      float* __restrict__ out, InitParams ip,
+                                                      unsigned long long* size_ctr, int* err) {
+  constexpr int NV = D / (4 * kPvL);  // float4s per lane
+  static_assert(NV >= 1 && D % (4 * kPvL) == 0, "D must be a multiple of 32");
+  const int b = blockIdx.x, lg = threadIdx.x & (kPvL - 1);
+  const uint32_t nu = unum[b], base = ubase[b];
+  const uint64_t* src = bkeys + bstart[b];
+  unsigned long long ins = 0;
+  // block-uniform trip count: every shuffle below runs with the whole wave
+  for (uint32_t l0 = blockIdx.y * (256 / kPvL); l0 < nu; l0 += gridDim.y * (256 / kPvL)) {
+    const uint32_t l = l0 + threadIdx.x / kPvL;
+    const bool act = l < nu;  // uniform inside a lane group
+    const uint64_t key = act ? src[l] : kEmptyKey;
+    long long slot = -1;
+    int inserted = 0;
+    if (act && lg == 0) {
+      bool bb = false;
+      if (key != kEmptyKey) slot = probe_slot(t, key, true, &bb);
+      inserted = bb;
+      if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
+      if (slots_out) slots_out[(long long)base + l] = slot;
+    }
+    slot = __shfl(slot, 0, kPvL);
+    inserted = __shfl(inserted, 0, kPvL);
+    if (!act) continue;
+    float4* o = reinterpret_cast<float4*>(out + ((long long)base + l) * D);
+    if (slot < 0) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) o[lg + k * kPvL] = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (inserted) {
+      for (uint32_t j = lg; j < t.width; j += kPvL) {
+        const float v = j < (uint32_t)D ? init_value(ip, key, j, D) : ip.state_init;
+        if (!t.prefilled) row_st(t, slot, j, v);
+        if (j < (uint32_t)D) out[((long long)base + l) * D + j] = v;
+      }
+      ins += (lg == 0);
+    } else {
+      const float4* r = reinterpret_cast<const float4*>(slot_row(t, slot));
+      float4 v[NV];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] = r[lg + k * kPvL];
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        const uint32_t j = 4u * (lg + k * kPvL);
+        v[k].x = fresh_or(v[k].x, ip, key, j, D);
+        v[k].y = fresh_or(v[k].y, ip, key, j + 1, D);
+        v[k].z = fresh_or(v[k].z, ip, key, j + 2, D);
+        v[k].w = fresh_or(v[k].w, ip, key, j + 3, D);
+        o[lg + k * kPvL] = v[k];
+      }
+    }
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
+}
+
+
 // ---------------------------------------------------------------------------
 // K5: fused optimizer update on resolved slots. Keys inside one launch must be
 // unique (the host launches one segment per source rank, in rank order, so
@@ -384,6 +453,51 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
     const long long pos = seg_pos(sl, g, &seg);
     apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg,
                  snap ? snap + pos : nullptr);
+  }
+}
+
+// K5 for wide fp32 rows (word2vec, D = 32 / 64 / 128): 8 lanes per key,
+// parameters, optimizer state and gradient moved as 16-byte vectors (the
+// 64-lane group per key kept one key's load -> update -> store chain per
+// wave in flight).
+template <int D>
+__global__ __launch_bounds__(256) void k_apply_rows(DevTable t, const long long* __restrict__ slots,
+                                                    const float* __restrict__ grads, SegList sl,
+                                                    OptParams op) {
+  constexpr int NV = D / (4 * kPvL), Q = D / 4;  // float4s per lane / per array
+  const long long total = seg_total(sl);
+  const int lg = threadIdx.x & (kPvL - 1);
+  const long long ngroups = (long long)gridDim.x * (256 / kPvL);
+  const int ns = opt_state_per_coord(op.kind);
+  for (long long g = (long long)blockIdx.x * (256 / kPvL) + threadIdx.x / kPvL; g < total;
+       g += ngroups) {
+    int seg;
+    const long long pos = seg_pos(sl, g, &seg);
+    const long long slot = slots[pos];
+    if (slot < 0) continue;  // the same for the 8 lanes of a key
+    float4* row = reinterpret_cast<float4*>(slot_row(t, slot));
+    const float4* gr = reinterpret_cast<const float4*>(grads + pos * D);
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 w[NV], s1[NV], s2[NV], gv[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int q = lg + k * kPvL;
+      w[k] = row[q];
+      gv[k] = gr[q];
+      s1[k] = ns > 0 ? row[Q + q] : z;
+      s2[k] = ns > 1 ? row[2 * Q + q] : z;
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      opt_update(op, w[k].x, s1[k].x, s2[k].x, gv[k].x);
+      opt_update(op, w[k].y, s1[k].y, s2[k].y, gv[k].y);
+      opt_update(op, w[k].z, s1[k].z, s2[k].z, gv[k].z);
+      opt_update(op, w[k].w, s1[k].w, s2[k].w, gv[k].w);
+      const int q = lg + k * kPvL;
+      row[q] = w[k];
+      if (ns > 0) row[Q + q] = s1[k];
+      if (ns > 1) row[2 * Q + q] = s2[k];
+    }
   }
 }
 
@@ -540,6 +654,19 @@ static inline int grid_for(long long groups, int G, int cap_blocks = 16384) {
     default: throw_error("unsupported lane-group size");    \
   }
 
+// the 8-lane / 16-byte forms for wide fp32 rows (SS_PULL_VEC=0: the lane-group forms)
+static bool pull_vec_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("SS_PULL_VEC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+static bool wide_rows(const DevTable& t) {
+  return !t.bf16 && (t.dim == 32 || t.dim == 64 || t.dim == 128) && t.row_off % 16 == 0 &&
+         t.stride % 16 == 0;
+}
+
 void launch_probe(const DevTable& t, const uint64_t* keys, const SegList& sl, long long max_n,
                   long long* slots, const InitParams& ip, int insert,
                   unsigned long long* size_ctr, int* err, int G, hipStream_t st) {
@@ -589,6 +716,19 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   // replay, 1 / 2 / 4 / 8: 0.0840-0.0848 / 0.0829-0.0830 / 0.0837-0.0844 /
   // 0.0858 ms/step (earlier, atomic-bound: 2 and 4 neutral)
   const int ny = G == 1 ? 4 : 2;
+  // wide fp32 rows: 8 lanes per key, 16-byte row accesses (k_pull_rows_bk)
+  if (!snap && pull_vec_on() && wide_rows(t) && reinterpret_cast<uintptr_t>(out) % 16 == 0) {
+    switch (t.dim) {
+      case 32: hipLaunchKernelGGL(k_pull_rows_bk<32>, dim3(P, ny), dim3(256), 0, st, t, bkeys,
+                                  bstart, unum, ubase, slots, out, ip, size_ctr, err); break;
+      case 64: hipLaunchKernelGGL(k_pull_rows_bk<64>, dim3(P, ny), dim3(256), 0, st, t, bkeys,
+                                  bstart, unum, ubase, slots, out, ip, size_ctr, err); break;
+      default: hipLaunchKernelGGL(k_pull_rows_bk<128>, dim3(P, ny), dim3(256), 0, st, t, bkeys,
+                                  bstart, unum, ubase, slots, out, ip, size_ctr, err); break;
+    }
+    check_launch("k_pull_rows_bk");
+    return;
+  }
   // snapshot pulls on 16-byte [w | h | key] slots probe with one 16-byte
   // load per step (probe_slot16; key load then row load measured slower)
   const int one16 = snap && t.stride == 16 && t.key_off == 8 && t.row_off == 0;
@@ -609,6 +749,20 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
   const int ns = opt_state_per_coord(op.kind);
   const uint32_t W = t.dim * (uint32_t)(1 + ns);
   if (snap && t.bf16) throw_error("apply: snapshot applies need fp32 rows");
+  if (!snap && pull_vec_on() && wide_rows(t) && W == t.width &&
+      reinterpret_cast<uintptr_t>(grads) % 16 == 0) {
+    const long long grid = grid_for(max_n, kPvL, 1 << 22);
+    switch (t.dim) {
+      case 32: hipLaunchKernelGGL(k_apply_rows<32>, dim3(grid), dim3(256), 0, st, t, slots, grads,
+                                  sl, op); break;
+      case 64: hipLaunchKernelGGL(k_apply_rows<64>, dim3(grid), dim3(256), 0, st, t, slots, grads,
+                                  sl, op); break;
+      default: hipLaunchKernelGGL(k_apply_rows<128>, dim3(grid), dim3(256), 0, st, t, slots,
+                                  grads, sl, op); break;
+    }
+    check_launch("k_apply_rows");
+    return;
+  }
   if (!snap && !t.bf16 && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
       W % 2 == 0 && W == t.width && t.row_off % 8 == 0 && t.stride % 8 == 0) {
     SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_st<kG>, dim3(grid_for(max_n, kG, 1 << 22)),

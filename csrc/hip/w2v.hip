@@ -814,7 +814,17 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
                                                      float* __restrict__ ugrad,
                                                      const float2* __restrict__ gnc,
                                                      long long negbase,
-                                                     const float* __restrict__ uvals) {
+                                                     const float* __restrict__ uvals,
+                                                     float* __restrict__ lacc,
+                                                     float* __restrict__ lacc_out, int lacc_n) {
+  // the step's loss / pair accumulators (the tile kernel's, ordered before
+  // this launch on the stream) move to acc_out and are left zero for the next
+  // step's tile: no zero-fill launch per step
+  if (lacc)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < lacc_n; i += gridDim.x * 256) {
+      lacc_out[i] = lacc[i];
+      lacc[i] = 0.f;
+    }
   // one item per half-wave: 32 lanes x V floats cover a row (512 B at D =
   // 128 as 16-B loads), two independent item chains per wave
   constexpr int V = D / 32;
@@ -1244,15 +1254,17 @@ void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const
 
 void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
                         const float* otail, int B, int W, int D, float* ugrad, hipStream_t st,
-                        const float* gnc, long long negbase, const float* uvals) {
+                        const float* gnc, long long negbase, const float* uvals, float* acc,
+                        float* acc_out, int acc_n) {
   if (gnc && !uvals) throw_error("w2v_oreduce: scaled negative rows need the center rows");
-  if (n <= 0) return;
+  if (acc && (!acc_out || acc_n <= 0)) throw_error("w2v_oreduce: accumulator hand-off needs acc_out");
+  if (n <= 0 && !acc) return;
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_oreduce: window must be in [1, 15]");
   const int ntiles = (B + kT - 1) / kT;
   // an item per half-wave, no grid stride: the reduce is a chain of
   // dependent loads per item (item -> rows -> store), so every chain of the
   // call runs concurrently
-  const int grid = (int)((n + 7) / 8);
+  const int grid = (int)std::max<long long>((n + 7) / 8, acc ? 64 : 1);
   const uint4* it = reinterpret_cast<const uint4*>(items);
   switch (D) {
 #define SS_W2VO_CASE(DD)                                                                      \
@@ -1260,10 +1272,12 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
     if (gnc)                                                                                  \
       hipLaunchKernelGGL((k_w2v_oreduce<DD, true>), dim3(grid), dim3(256), 0, st, it, n, ord,  \
                          ograd, otail, B, W, ntiles, ugrad,                                    \
-                         reinterpret_cast<const float2*>(gnc), negbase, uvals);                \
+                         reinterpret_cast<const float2*>(gnc), negbase, uvals, acc, acc_out,   \
+                         acc_n);                                                               \
     else                                                                                      \
       hipLaunchKernelGGL((k_w2v_oreduce<DD, false>), dim3(grid), dim3(256), 0, st, it, n, ord, \
-                         ograd, otail, B, W, ntiles, ugrad, nullptr, 0ll, nullptr);            \
+                         ograd, otail, B, W, ntiles, ugrad, nullptr, 0ll, nullptr, acc,        \
+                         acc_out, acc_n);                                                      \
     break;
     SS_W2VO_CASE(32)
     SS_W2VO_CASE(64)

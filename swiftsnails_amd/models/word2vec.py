@@ -155,9 +155,13 @@ class Word2VecWorker(PipelinedWorker):
         self.meta = ([torch.empty(data.run_len, dtype=torch.int32, device=engine.device)
                       for _ in range(engine.depth)] if self.window_mode else None)
         # window layout: positive pairs of the last step (sharded counter),
-        # beside the loss in one buffer: one zero-fill per step for both
+        # beside the loss in one buffer: one zero-fill per step for both.
+        # With the occurrence reduce the kernels add into _acc and
+        # k_w2v_oreduce moves it to _out (loss_sum / pair_sum) and leaves it
+        # zero: no fill launch per step
         self._acc = torch.zeros((2, self.loss_sum.numel()), dtype=torch.float32,
                                 device=engine.device)
+        self._out = self._acc
         self.loss_sum, self.pair_sum = self._acc[0], self._acc[1]
         # the tile's negative-sample GEMMs on the bf16 MFMA (center / negative
         # rows and score gradients rounded to bf16, fp32 accumulate; positive
@@ -193,9 +197,17 @@ class Word2VecWorker(PipelinedWorker):
             self.items = [torch.empty((n, 4), dtype=torch.int32, device=dev)
                           for _ in range(engine.depth)]
             self._post_route = self._osort
+            self._out = torch.zeros_like(self._acc)
+            self.loss_sum, self.pair_sum = self._out[0], self._out[1]
 
     def _zero_acc(self) -> None:
-        self._acc.zero_()
+        if self._out is self._acc:
+            self._acc.zero_()
+
+    def _handoff(self) -> dict:
+        """k_w2v_oreduce's accumulator hand-off (_acc -> _out, _acc zeroed)."""
+        return {"acc": self._acc.data_ptr(), "acc_out": self._out.data_ptr(),
+                "acc_n": self._acc.numel()}
 
     def _osort(self, dd, slot, st):
         o = dd.owner
@@ -219,23 +231,23 @@ class Word2VecWorker(PipelinedWorker):
         if self.per_pair:
             h.w2v_pp(ptr, ptr + B * es, ptr + (B + d.run_len) * es, self.meta[slot].data_ptr(),
                      B, d.window, d.negatives, self.engine.dim, rnd.uvals.data_ptr(),
-                     self.ograd.data_ptr(), self.gpair.data_ptr(), self.loss_sum.data_ptr(),
-                     self.pair_sum.data_ptr(), st, self.gnc.data_ptr())
+                     self.ograd.data_ptr(), self.gpair.data_ptr(), self._acc[0].data_ptr(),
+                     self._acc[1].data_ptr(), st, self.gnc.data_ptr())
             h.w2v_oreduce(self.items[slot].data_ptr(), d.n_keys, self.ord[slot].data_ptr(),
                           self.ograd.data_ptr(), 0, B, d.window, self.engine.dim,
                           rnd.ugrad.data_ptr(), st, gnc=self.gnc.data_ptr(),
-                          negbase=B + d.run_len, uvals=rnd.uvals.data_ptr())
+                          negbase=B + d.run_len, uvals=rnd.uvals.data_ptr(), **self._handoff())
             return
         if self.window_mode:
             occ = self.occ_reduce
             h.w2v_win(ptr, ptr + B * es, ptr + (B + d.run_len) * es, self.meta[slot].data_ptr(),
                       B, d.window, self.engine.dim, d.neg_per_pair, rnd.uvals.data_ptr(),
-                      rnd.ugrad.data_ptr(), self.loss_sum.data_ptr(), self.pair_sum.data_ptr(),
+                      rnd.ugrad.data_ptr(), self._acc[0].data_ptr(), self._acc[1].data_ptr(),
                       st, self.ograd.data_ptr() if occ else 0, self.otail.data_ptr() if occ else 0)
             if occ:
                 h.w2v_oreduce(self.items[slot].data_ptr(), d.n_keys, self.ord[slot].data_ptr(),
                               self.ograd.data_ptr(), self.otail.data_ptr(), B, d.window,
-                              self.engine.dim, rnd.ugrad.data_ptr(), st)
+                              self.engine.dim, rnd.ugrad.data_ptr(), st, **self._handoff())
             return
         h.w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
                    d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),

@@ -66,7 +66,11 @@ def slot_layout(width: int, layout: Optional[str] = None,
     stride = _align(8 + elem * width, 16 if width >= 2 else 8)
     if layout == "keyfirst_line":
         stride = _align(stride, 64)
-    return stride, 0, 8
+    # a row of whole 16-byte vectors starts 16-byte aligned (the stride's
+    # padding moves in front of it: [key | pad | row], same stride), so wide
+    # rows move as float4s (table.hip k_pull_rows_bk)
+    row_off = 16 if (elem * width) % 16 == 0 and stride >= 16 + elem * width else 8
+    return stride, 0, row_off
 
 
 def default_lane_group(width: int) -> int:

@@ -89,11 +89,55 @@ def test_pull_duplicates_see_initialised_rows(dev, G, dim):
         assert first.setdefault(key, sl) == sl
 
 
+@pytest.mark.parametrize("dim", [32, 64, 128])
+@pytest.mark.parametrize("init_kind", ["uniform", "zero"])
+def test_pull_wide_rows_from_buckets(dev, dim, init_kind):
+    """Bucketed unique pull of wide fp32 rows (k_pull_rows_bk: 8 lanes per
+    key, 16-byte row vectors; the rows start 16-byte aligned in the slot):
+    new keys read their initial row, existing keys their stored row, slots
+    agree with a probe, and partial last lane groups of a bucket are inert."""
+    from swiftsnails_amd.ops.optim import InitConfig, Optimizer, init_reference
+    from swiftsnails_amd.ops.table import HbmTable
+
+    init = InitConfig(init_kind, scale=0.5, seed=7)
+    t = HbmTable(dim, 1 << 14, optimizer=Optimizer("adagrad", lr=0.2), init=init, device=dev)
+    assert t.row_off % 16 == 0 and t.stride % 16 == 0
+    k = np.unique(_keys(3001, 9))
+    kt = torch.from_numpy(k).to(dev)
+    old = kt[::3].contiguous()
+    t.pull(old, unique=True)
+    g = torch.randn((old.numel(), dim), device=dev)
+    t.push(old, g)  # the existing rows differ from their initial value
+    torch.cuda.synchronize()
+    before = t.to_dict(with_state=True)
+    # buckets of uneven sizes (1 .. 70 keys: partial 8-lane groups and rounds)
+    sizes, n = [], len(k)
+    rng = np.random.default_rng(5)
+    while sum(sizes) < n:
+        sizes.append(int(min(rng.integers(1, 71), n - sum(sizes))))
+    bstart = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int32)
+    bs = torch.from_numpy(bstart).to(dev)
+    un = torch.from_numpy(np.asarray(sizes, np.int32)).to(dev)
+    out = torch.full((n, dim), float("nan"), device=dev)
+    slots = torch.empty(n, dtype=torch.int64, device=dev)
+    t.pull_buckets((kt.data_ptr(), bs.data_ptr(), un.data_ptr(), bs.data_ptr(), len(sizes)),
+                   out, slots)
+    torch.cuda.synchronize()
+    t.check()
+    assert t.size() == n
+    ref = init_reference(init, k, dim, t.width)[:, :dim]
+    for i in range(0, n, 3):
+        ref[i] = before[int(k.view(np.uint64)[i])][:dim]
+    np.testing.assert_array_equal(out.cpu().numpy(), ref)
+    np.testing.assert_array_equal(slots.cpu().numpy(), t.lookup_slots(kt).cpu().numpy())
+
+
 @pytest.mark.parametrize("kind", ["sgd", "adagrad", "ftrl", "adam"])
-@pytest.mark.parametrize("dim", [1, 5, 8, 9, 33])
+@pytest.mark.parametrize("dim", [1, 5, 8, 9, 33, 32, 128])
 def test_apply_matches_reference(dev, kind, dim):
     """K5 per optimizer vs the NumPy reference; dims 5-9 with state take the
-    LDS-staged 8-byte-chunk form (k_apply_st), 1 and 33 the others."""
+    LDS-staged 8-byte-chunk form (k_apply_st), 32 / 128 the 16-byte-vector
+    form (k_apply_rows), 1 and 33 the others."""
     from swiftsnails_amd.ops.optim import InitConfig, Optimizer, apply_reference
     from swiftsnails_amd.ops.table import HbmTable
 

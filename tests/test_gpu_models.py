@@ -499,7 +499,9 @@ def test_word2vec_window_grad_reduce_matches_atomics(dev, monkeypatch, D, B, W):
     """Window tile gradients as occurrence rows summed per unique key
     (k_w2v_osort + k_w2v_oreduce: counting sort per dedup bucket, one wave per
     <= 32-occurrence item, shared window rows through the tail buffer, Zipf
-    heads split over several items) == the tile's own row atomics.  Partial
+    heads split over several items) == the tile's own row atomics; the
+    per-step loss moved out of the zeroed accumulator by the reduce == the
+    zero-filled one.  Partial
     last tile (B % 64 != 0), W from 2 to the maximum 15.  (The atomic form
     is what a non-bucketed dedup, SS_DEDUP=hash, runs.)"""
     from swiftsnails_amd.models.word2vec import W2VSynth, Word2VecWorker, make_w2v_table_args
@@ -522,6 +524,8 @@ def test_word2vec_window_grad_reduce_matches_atomics(dev, monkeypatch, D, B, W):
             losses.append(w.mean_loss())
         torch.cuda.synchronize()
         t.check()
+        if mode == "reduce":  # k_w2v_oreduce handed the accumulators off and zeroed them
+            assert w._out is not w._acc and float(w._acc.abs().sum()) == 0.0
         out[mode] = (losses, t.to_dict(with_state=True))
     (lr, tr), (la, ta) = out["reduce"], out["atomic"]
     np.testing.assert_allclose(lr, la, rtol=1e-4)
