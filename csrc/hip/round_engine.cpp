@@ -73,6 +73,7 @@ class RoundEngine {
     vals_.resize(depth);
     grads_.resize(depth);
     self_keys_.assign(depth, 0);
+    srv_done_.assign(depth, 0);
   }
   ~RoundEngine() {
     hipSetDevice(device_);
@@ -161,9 +162,19 @@ class RoundEngine {
   // after the dedup on the route stream: N>1 — the keys + every destination's
   // per-bucket runs (+ their sub-bucket offsets) into the peers' mailboxes;
   // then the route event
+  //
+  // `srv_ahead` (N>1): the server half that depends on the keys alone —
+  // every source's keys in (the keys wait) and the merge of the sources'
+  // runs into distinct keys (k_srv_count / k_srv_dedup) — runs here on the
+  // route stream too, a round ahead beside the main stream's compute, instead
+  // of at the head of the pull; the table lookup stays in the pull (it must
+  // see the previous round's update).  `table`: this rank hosts a shard.
   void route_end(int slot, int tag, uintptr_t route, uintptr_t ukeys, uintptr_t ucount,
-                 uintptr_t runs_base, uintptr_t runs_num, uintptr_t runs_sub) {
+                 uintptr_t runs_base, uintptr_t runs_num, uintptr_t runs_sub, bool srv_ahead,
+                 bool table, uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum,
+                 uintptr_t srv_err) {
     check_slot(slot);
+    srv_done_[slot] = false;
     if (!ar_.empty()) {
       std::vector<std::vector<long long>> parts;
       parts.push_back(part(ukeys, ucount, 0, 8, keys_[slot][0], cap_, self_bypass()));
@@ -176,6 +187,10 @@ class RoundEngine {
                              (long long)Pd_ * sub_));
       }
       ar_[slot][0]->put(0, parts, bpp_, route);
+      if (srv_ahead) {
+        keys_in(slot, route, table, rkeys, rbase, rnum, srv_err);
+        srv_done_[slot] = true;
+      }
     }
     record(kRoute, slot, route, tag);
   }
@@ -210,20 +225,11 @@ class RoundEngine {
                  std::vector<uintptr_t> metrics, bool custom_pull) {
     check_xgmi();
     pull_waits(slot, tag, stream, wait_route, prev);
-    // missing sources' fixed-size run tables read as empty
-    const long long nb = 4ll * Pd_;
-    std::vector<std::vector<long long>> fixed = {{keys_[slot][1].data, keys_[slot][1].seg, nb},
-                                                 {keys_[slot][2].data, keys_[slot][2].seg, nb}};
-    if (nkp_ == 4) fixed.push_back({keys_[slot][3].data, keys_[slot][3].seg, nb * sub_});
-    ar_[slot][0]->wait(0, fixed, timeout_, stream, {}, 0.0);
+    // the keys in and the server's distinct-key merge, unless the route ran them
+    if (!srv_done_[slot]) keys_in(slot, stream, table, rkeys, rbase, rnum, srv_err);
+    srv_done_[slot] = false;
     if (table) {
       SrvSlot& S = srv_[slot];
-      const uint32_t* roff =
-          nkp_ == 4 ? Pt<const uint32_t>(ar_[slot][0]->base() + keys_[slot][3].data) : nullptr;
-      launch_srv_dedup(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
-                       Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt,
-                       S.bstart, S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount,
-                       Pt<uint32_t>(srv_err), St(stream), roff, self_seg(self_keys_[slot]));
       launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
                             Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
                             G, St(stream), snap ? S.snap : nullptr);
@@ -321,6 +327,24 @@ class RoundEngine {
     v.push_back(skip_self ? 1 : 0);
     return v;
   }
+  // every source's keys of the round in (missing sources' fixed-size run
+  // tables read as empty), then — a shard — their merge into distinct keys
+  void keys_in(int slot, uintptr_t stream, bool table, uintptr_t rkeys, uintptr_t rbase,
+               uintptr_t rnum, uintptr_t srv_err) {
+    const long long nb = 4ll * Pd_;
+    std::vector<std::vector<long long>> fixed = {{keys_[slot][1].data, keys_[slot][1].seg, nb},
+                                                 {keys_[slot][2].data, keys_[slot][2].seg, nb}};
+    if (nkp_ == 4) fixed.push_back({keys_[slot][3].data, keys_[slot][3].seg, nb * sub_});
+    ar_[slot][0]->wait(0, fixed, timeout_, stream, {}, 0.0);
+    if (!table) return;
+    SrvSlot& S = srv_[slot];
+    const uint32_t* roff =
+        nkp_ == 4 ? Pt<const uint32_t>(ar_[slot][0]->base() + keys_[slot][3].data) : nullptr;
+    launch_srv_dedup(Pt<const uint64_t>(rkeys), Pt<const uint32_t>(rbase),
+                     Pt<const uint32_t>(rnum), cap_, nranks_, Pd_, sub_, rank_, S.cnt, S.bstart,
+                     S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount, Pt<uint32_t>(srv_err),
+                     St(stream), roff, self_seg(self_keys_[slot]));
+  }
   // this rank's own segment of a (cap-row) exchange, read in place from `ptr`
   SelfSeg self_seg(uintptr_t ptr) const {
     SelfSeg s;
@@ -377,6 +401,7 @@ class RoundEngine {
   int nkp_ = 3;  // parts of the keys channel
   std::vector<XReg> vals_, grads_;
   std::vector<uintptr_t> self_keys_;  // per slot: this rank's send layout of its keys
+  std::vector<char> srv_done_;        // per slot: the route ran keys_in (srv_ahead)
   int nranks_ = 1, rank_ = 0, Pd_ = 1, sub_ = 1, dim_ = 1, bpp_ = 128;
   long long cap_ = 0;
   double timeout_ = 120.0;

@@ -295,6 +295,7 @@ class PSEngine(HostRounds):
                          for _ in range(self.depth)]
             self.rgrads = [torch.empty((rows, d), dtype=torch.float32, device=dev)] * self.depth
         self.srv = None
+        self.srv_ahead = os.environ.get("SS_SRV_AHEAD", "1") != "0"
         if self.table is not None:
             self.svals = torch.empty((rows, d), dtype=torch.float32, device=dev)
             self.sgrad = torch.empty((rows, d), dtype=torch.float32, device=dev)
@@ -397,8 +398,15 @@ class PSEngine(HostRounds):
             if self.xg:
                 ub, un = dd.owner.run_tables(self.Pd)
                 us = dd.owner.sub_table(self.Pd).data_ptr() if dd.owner.msub > 1 else 0
+                # the keys in + the server's distinct-key merge on the route
+                # stream, a round ahead (SS_SRV_AHEAD=0: at the head of the pull)
+                tab = self.table is not None
                 self.native.route_end(slot, tag, rs.cuda_stream, dd.ukeys.data_ptr(),
-                                      dd.ucount.data_ptr(), ub.data_ptr(), un.data_ptr(), us)
+                                      dd.ucount.data_ptr(), ub.data_ptr(), un.data_ptr(), us,
+                                      self.srv_ahead, tab, self.rkeys[slot].data_ptr(),
+                                      self.rmeta[slot][0].data_ptr(),
+                                      self.rmeta[slot][1].data_ptr(),
+                                      self.srv_err.data_ptr() if tab else 0)
             else:
                 if self.dist:
                     counts = self._route_counts(dd, slot, rs)
