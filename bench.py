@@ -8,7 +8,9 @@ Each rank is a colocated worker + server shard (one process per GPU):
   * its table shard holds 1/N of the 1B-feature space (AdaGrad, 16-byte slots);
   * its worker trains on its own synthetic CTR stream (B samples x 39 fields
     per step, generated on-device inside the timed step);
-  * pull/push rounds route keys over RCCL alltoallv (xGMI) for N > 1.
+  * for N > 1 pull/push rounds exchange keys, rows and gradients as peer
+    stores into xGMI-mapped HBM mailboxes (device-side counts; a start-up
+    litmus picks the publish tier, RCCL all-to-all-v is the fallback).
 
 Weak scaling: the per-GPU batch is fixed, the global batch is N*B.
 
