@@ -331,6 +331,17 @@ __global__ __launch_bounds__(256) void k_pull_rows_bk(DevTable t, const uint64_t
     const uint64_t key = act ? src[l] : kEmptyKey;
     long long slot = -1;
     int inserted = 0;
+    // the row of the key's home slot, loaded beside the probe's first key
+    // load (most keys sit in their home slot): found there, the row is
+    // already in registers — one round trip instead of key, then row
+    const bool live = act && key != kEmptyKey;
+    const uint64_t home = live ? fastrange64(table_hash(key), t.cap) : 0;
+    float4 v[NV];
+    if (live) {
+      const float4* r0 = reinterpret_cast<const float4*>(slot_row(t, home));
+#pragma unroll
+      for (int k = 0; k < NV; ++k) v[k] = r0[lg + k * kPvL];
+    }
     if (act && lg == 0) {
       bool bb = false;
       if (key != kEmptyKey) slot = probe_slot(t, key, true, &bb);
@@ -353,10 +364,11 @@ __global__ __launch_bounds__(256) void k_pull_rows_bk(DevTable t, const uint64_t
       }
       ins += (lg == 0);
     } else {
-      const float4* r = reinterpret_cast<const float4*>(slot_row(t, slot));
-      float4 v[NV];
+      if ((uint64_t)slot != home) {  // displaced by the probe: the row again
+        const float4* r = reinterpret_cast<const float4*>(slot_row(t, slot));
 #pragma unroll
-      for (int k = 0; k < NV; ++k) v[k] = r[lg + k * kPvL];
+        for (int k = 0; k < NV; ++k) v[k] = r[lg + k * kPvL];
+      }
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         const uint32_t j = 4u * (lg + k * kPvL);
@@ -365,6 +377,86 @@ __global__ __launch_bounds__(256) void k_pull_rows_bk(DevTable t, const uint64_t
         v[k].z = fresh_or(v[k].z, ip, key, j + 2, D);
         v[k].w = fresh_or(v[k].w, ip, key, j + 3, D);
         o[lg + k * kPvL] = v[k];
+      }
+    }
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
+}
+
+
+// k_pull_unique_bk for narrow fp32 rows whose key and parameters share a
+// slot's first 64 bytes ([key | params | state], FM's 9 parameters at bytes
+// 8..44 of an 80-byte slot): 4 lanes per key, each probe step one 16-byte
+// load per lane, so the step that finds the key has already read the row —
+// one dependent round trip per key instead of two (key, then row).
+static constexpr int kPnL = 4;
+__global__ __launch_bounds__(256) void k_pull_narrow_bk(DevTable t, const uint64_t* __restrict__ bkeys,
+                                                        const uint32_t* __restrict__ bstart,
+                                                        const uint32_t* __restrict__ unum,
+                                                        const uint32_t* __restrict__ ubase,
+                                                        long long* __restrict__ slots_out,
+                                                        float* __restrict__ out, InitParams ip,
+                                                        unsigned long long* size_ctr, int* err) {
+  const int b = blockIdx.x, lg = threadIdx.x & (kPnL - 1);
+  const uint32_t nu = unum[b], base = ubase[b], D = t.dim;
+  const uint64_t* src = bkeys + bstart[b];
+  unsigned long long ins = 0;
+  // block-uniform trip count: the shuffles below run with the whole wave
+  for (uint32_t l0 = blockIdx.y * (256 / kPnL); l0 < nu; l0 += gridDim.y * (256 / kPnL)) {
+    const uint32_t l = l0 + threadIdx.x / kPnL;
+    const bool act = l < nu;  // uniform inside a lane group
+    const uint64_t key = act ? src[l] : kEmptyKey;
+    long long slot = -1;
+    bool inserted = false;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (act && key != kEmptyKey) {
+      uint64_t s = fastrange64(table_hash(key), t.cap);
+      for (uint64_t n = 0; n < t.cap; ++n) {  // group-uniform trip count
+        v = *reinterpret_cast<const uint4*>(t.base + s * (uint64_t)t.stride + 16 * lg);
+        const uint64_t k = ((uint64_t)__shfl(v.y, 0, kPnL) << 32) | __shfl(v.x, 0, kPnL);
+        if (k == key) {
+          slot = (long long)s;
+          break;
+        }
+        if (k == kEmptyKey) {
+          unsigned long long prev = 0;
+          if (lg == 0)
+            prev = atomicCAS(reinterpret_cast<unsigned long long*>(slot_key(t, s)), kEmptyKey, key);
+          prev = __shfl(prev, 0, kPnL);
+          if (prev == kEmptyKey || prev == key) {  // claimed (or a duplicate of this key did)
+            slot = (long long)s;
+            inserted = prev == kEmptyKey;
+            break;
+          }
+        }
+        s = (s + 1 == t.cap) ? 0 : s + 1;
+      }
+    }
+    if (!act) continue;
+    if (lg == 0) {
+      if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
+      if (slots_out) slots_out[(long long)base + l] = slot;
+    }
+    float* o = out + ((long long)base + l) * D;
+    if (slot < 0) {
+      for (uint32_t j = lg; j < D; j += kPnL) o[j] = 0.f;
+    } else if (inserted) {
+      for (uint32_t j = lg; j < t.width; j += kPnL) {
+        const float x = j < D ? init_value(ip, key, j, D) : ip.state_init;
+        if (!t.prefilled) row_st(t, (uint64_t)slot, j, x);
+        if (j < D) o[j] = x;
+      }
+      ins += (lg == 0);
+    } else {
+      // this lane holds slot bytes [16 lg, 16 lg + 16): parameter j is at 8 + 4 j
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int byte = 16 * lg + 4 * c;
+        if (byte < 8) continue;
+        const uint32_t j = (uint32_t)(byte - 8) >> 2;
+        if (j < D) o[j] = fresh_or(__uint_as_float(w[c]), ip, key, j, D);
       }
     }
   }
@@ -727,6 +819,14 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
                                   bstart, unum, ubase, slots, out, ip, size_ctr, err); break;
     }
     check_launch("k_pull_rows_bk");
+    return;
+  }
+  // narrow fp32 rows with key + parameters in the slot's first 64 bytes (FM)
+  if (!snap && pull_vec_on() && !t.bf16 && t.key_off == 0 && t.row_off == 8 &&
+      t.stride % 16 == 0 && t.stride >= 64 && t.dim >= 2 && 8 + 4 * t.dim <= 64) {
+    hipLaunchKernelGGL(k_pull_narrow_bk, dim3(P, ny), dim3(256), 0, st, t, bkeys, bstart, unum,
+                       ubase, slots, out, ip, size_ctr, err);
+    check_launch("k_pull_narrow_bk");
     return;
   }
   // snapshot pulls on 16-byte [w | h | key] slots probe with one 16-byte

@@ -398,12 +398,17 @@ class PSEngine(HostRounds):
             if self.xg:
                 ub, un = dd.owner.run_tables(self.Pd)
                 us = dd.owner.sub_table(self.Pd).data_ptr() if dd.owner.msub > 1 else 0
-                # the keys in + the server's distinct-key merge on the route
-                # stream, a round ahead (SS_SRV_AHEAD=0: at the head of the pull)
+                # synchronous rounds: the keys in + the server's distinct-key
+                # merge on the route stream, a round ahead, off the main
+                # stream's chain (SS_SRV_AHEAD=0: at the head of the pull).
+                # Pulled-ahead rounds keep them in the pull, already off the
+                # main stream (on the route stream they lengthened its chain:
+                # word2vec N>1 0.107 -> 0.117 ms/step)
                 tab = self.table is not None
+                ahead = self.srv_ahead and not self.pull_ahead
                 self.native.route_end(slot, tag, rs.cuda_stream, dd.ukeys.data_ptr(),
                                       dd.ucount.data_ptr(), ub.data_ptr(), un.data_ptr(), us,
-                                      self.srv_ahead, tab, self.rkeys[slot].data_ptr(),
+                                      ahead, tab, self.rkeys[slot].data_ptr(),
                                       self.rmeta[slot][0].data_ptr(),
                                       self.rmeta[slot][1].data_ptr(),
                                       self.srv_err.data_ptr() if tab else 0)

@@ -72,9 +72,10 @@ KNOBS: dict[str, Knob] = {
                       "bytes of the scatter -> dedup (key, sample) record: 12 (dwordx3) or 16 "
                       "(dwordx4); 12 measured 0.836-0.841 vs 0.850-0.854 ms/step (3 A/B pairs)"),
     "SS_SRV_AHEAD": Knob("1", "swiftsnails_amd/parallel/engine.py", "tuning",
-                         "N>1 xGMI path: wait for the round's keys and merge them into the "
-                         "server's distinct keys on the route stream, a round ahead (0: at the "
-                         "head of the pull)"),
+                         "N>1 xGMI path, synchronous rounds: wait for the round's keys and "
+                         "merge them into the server's distinct keys on the route stream, a "
+                         "round ahead (0: at the head of the pull; pulled-ahead rounds always "
+                         "keep them in the pull)"),
     "SS_PULL_VEC": Knob("1", "csrc/hip/table.hip", "tuning",
                         "wide fp32 rows (dim 32/64/128): pull and apply with 8 lanes per key "
                         "and 16-byte row vectors (0: one lane group per key)"),

@@ -89,19 +89,24 @@ def test_pull_duplicates_see_initialised_rows(dev, G, dim):
         assert first.setdefault(key, sl) == sl
 
 
-@pytest.mark.parametrize("dim", [32, 64, 128])
+@pytest.mark.parametrize("cap", [1 << 14, 4200])
+@pytest.mark.parametrize("dim", [9, 32, 64, 128])
 @pytest.mark.parametrize("init_kind", ["uniform", "zero"])
-def test_pull_wide_rows_from_buckets(dev, dim, init_kind):
+def test_pull_wide_rows_from_buckets(dev, dim, init_kind, cap):
     """Bucketed unique pull of wide fp32 rows (k_pull_rows_bk: 8 lanes per
-    key, 16-byte row vectors; the rows start 16-byte aligned in the slot):
-    new keys read their initial row, existing keys their stored row, slots
-    agree with a probe, and partial last lane groups of a bucket are inert."""
+    key, 16-byte row vectors; the rows start 16-byte aligned in the slot) and
+    of FM's narrow rows (dim 9, k_pull_narrow_bk: key + parameters read by
+    the probe's own 16-byte loads): new keys read their initial row, existing
+    keys their stored row, slots agree with a probe, and partial last lane
+    groups of a bucket are inert.  Capacity 4200 for 3001 keys: long probe
+    runs (keys away from their home slot, where the row read beside the
+    first key load must be repeated)."""
     from swiftsnails_amd.ops.optim import InitConfig, Optimizer, init_reference
     from swiftsnails_amd.ops.table import HbmTable
 
     init = InitConfig(init_kind, scale=0.5, seed=7)
-    t = HbmTable(dim, 1 << 14, optimizer=Optimizer("adagrad", lr=0.2), init=init, device=dev)
-    assert t.row_off % 16 == 0 and t.stride % 16 == 0
+    t = HbmTable(dim, cap, optimizer=Optimizer("adagrad", lr=0.2), init=init, device=dev)
+    assert t.stride % 16 == 0 and (t.row_off % 16 == 0 or 8 + 4 * dim <= 64)
     k = np.unique(_keys(3001, 9))
     kt = torch.from_numpy(k).to(dev)
     old = kt[::3].contiguous()
