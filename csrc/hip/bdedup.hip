@@ -89,7 +89,10 @@ static constexpr int kBdMaxSub = 64;    // server sub-buckets per bucket (srv_su
 // (key, sample) record of the scatter -> dedup hand-off: 12 bytes (three
 // dwords, one dwordx3 store / load) or 16 (uint4, one dwordx4; SS_BD_REC=16).
 // 12: 25 % fewer bytes of the route stream's largest array; the bench step
-// 0.850-0.854 -> 0.836-0.841 ms (three interleaved A/B pairs on one box)
+// 0.850-0.854 -> 0.836-0.841 ms (three interleaved A/B pairs on one box).
+// A call whose keys all fit 32 bits (ids of a <= 4G-feature space: the
+// count kernel ORs the high words, the column scan publishes the verdict)
+// moves 8-byte (key, sample) records instead (SS_BD_REC=12 keeps 12).
 struct alignas(4) BdRec3 {
   uint32_t x, y, z;
 };
@@ -137,7 +140,7 @@ static long long bd_max_chunks(int nranks) {
 // ---- layout of the int scratch (u32 words), a function of (n, nranks) only
 struct BdLayout {
   int P, Pd, nch, chunk;
-  long long hist, btot, bstart, ubase, unum, ctr, total;
+  long long hist, btot, bstart, ubase, unum, ctr, wacc, wfin, total;
 };
 
 static int bd_clamp_ndest(int nranks, int ndest) {
@@ -174,8 +177,10 @@ static BdLayout bd_layout(long long n, int nranks, int ndest) {
   // words 0, 1: sticky error flag and the colscan arrival counter, at fixed
   // positions for any n (the scratch is sized for the largest call and
   // zeroed once; every other word is rewritten by each call)
-  long long o = 2;
+  long long o = 4;
   L.ctr = 1;
+  L.wacc = 2;  // count: some key of this call has high bits (atomicOr)
+  L.wfin = 3;  // colscan's last workgroup: the call's value (wacc reset to 0)
   L.hist = o; o += (long long)L.P * L.nch;
   L.btot = o; o += L.P;
   L.bstart = o; o += L.P + 1;
@@ -204,7 +209,7 @@ long long bd_scratch_words(long long n, int nranks, int ndest) {
   long long nchmax = std::min<long long>(256 * waves, bd_max_chunks(nranks));
   nchmax = std::min<long long>(nchmax, (n + kBdChunkLanes - 1) / kBdChunkLanes);
   nchmax = std::max<long long>(nchmax, 1);
-  const long long bound = 2 + pmax * nchmax + 4 * pmax + 1;
+  const long long bound = 4 + pmax * nchmax + 4 * pmax + 1;
   return std::max(bound, bd_layout(n, nranks, ndest).total);
 }
 int bd_buckets(long long n, int nranks, int ndest) {
@@ -224,8 +229,11 @@ template <int CT>
 __global__ __launch_bounds__(CT) void k_bd_count(const uint64_t* __restrict__ keys, long long n,
                                                     RouteSpec rs, int Pd, int P, int chunk,
                                                     uint32_t* __restrict__ hist,
-                                                    unsigned long long* __restrict__ ucount) {
+                                                    unsigned long long* __restrict__ ucount,
+                                                    uint32_t* __restrict__ wacc) {
   extern __shared__ unsigned int h[];
+  __shared__ unsigned int hiw;
+  if (threadIdx.x == 0) hiw = 0u;
   // the dedup's per-destination unique counters start from zero (stream order)
   if (blockIdx.x == 0 && threadIdx.x < (unsigned)rs.nranks) ucount[threadIdx.x] = 0ull;
   for (int b = threadIdx.x; b < P; b += CT) h[b] = 0u;
@@ -241,11 +249,17 @@ __global__ __launch_bounds__(CT) void k_bd_count(const uint64_t* __restrict__ ke
       const long long j = base + e * CT;
       k[e] = (e < per && j < n) ? keys[j] : kEmptyKey;
     }
+    uint32_t hi = 0u;
 #pragma unroll
     for (int e = 0; e < (kBdMaxChunk / CT); ++e)
-      if (k[e] != kEmptyKey) atomicAdd(&h[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
+      if (k[e] != kEmptyKey) {
+        atomicAdd(&h[bd_bucket(k[e], rs, (uint32_t)Pd)], 1u);
+        hi |= (uint32_t)(k[e] >> 32);
+      }
+    if (__ballot(hi != 0u) && (threadIdx.x & 63) == 0) hiw = 1u;  // benign race: all store 1
   }
   __syncthreads();
+  if (threadIdx.x == 0 && hiw && wacc) atomicOr(wacc, 1u);
   uint32_t* row = hist + (long long)blockIdx.x * P;
   for (int b = threadIdx.x; b < P; b += CT) row[b] = h[b];
 }
@@ -261,7 +275,9 @@ template <int CS>
 __global__ __launch_bounds__(CS) void k_bd_colscan(uint32_t* __restrict__ hist, int nch, int P,
                                                    uint32_t* __restrict__ btot,
                                                    uint32_t* __restrict__ bstart,
-                                                   unsigned int* __restrict__ ctr) {
+                                                   unsigned int* __restrict__ ctr,
+                                                   uint32_t* __restrict__ wacc,
+                                                   uint32_t* __restrict__ wfin) {
   constexpr int NS = CS / 64;  // chunk segments per column
   __shared__ unsigned int ss[NS][64];
   __shared__ unsigned int wsum[16];
@@ -312,6 +328,9 @@ __global__ __launch_bounds__(CS) void k_bd_colscan(uint32_t* __restrict__ hist, 
   if (threadIdx.x == 0) {
     bstart[P] = tot;
     *ctr = 0u;  // ready for the next call (stream-ordered)
+    // the record width of this call (kernel-ordered after the count)
+    *wfin = wacc ? *wacc : 1u;
+    if (wacc) *wacc = 0u;
   }
 }
 
@@ -324,9 +343,13 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      uint32_t* __restrict__ pj,
                                                      uint32_t* __restrict__ pos_of,
                                                      uint32_t* __restrict__ bkt,
-                                                     typename BdRecT<RW>::T* __restrict__ rec) {
+                                                     typename BdRecT<RW>::T* __restrict__ rec,
+                                                     const uint32_t* __restrict__ wfin) {
   extern __shared__ unsigned int cur[];
   const int c = blockIdx.x;
+  // keys of 32 bits: 8-byte (key, sample) records (RW 3 only)
+  const bool narrow = RW == 3 && wfin && *wfin == 0u;
+  uint2* rec2 = reinterpret_cast<uint2*>(rec);
   const uint32_t* row = hist + (long long)c * P;
   for (int b = threadIdx.x; b < P; b += CT) cur[b] = bstart[b] + row[b];
   for (int t0 = 0; t0 < chunk; t0 += kBdMaxChunk) {
@@ -353,7 +376,8 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
           // (a 64-byte line per occurrence) and writes pj itself.  Measured
           // standalone: scatter 119 -> 163 us, dedup 213 -> 123 us; N>1
           // engine path 1.211 -> 1.169 ms/step, one GPU neutral
-          rec[pos] = BdRecT<RW>::make(k[e], (uint32_t)j);
+          if (narrow) rec2[pos] = make_uint2((uint32_t)k[e], (uint32_t)j);
+          else rec[pos] = BdRecT<RW>::make(k[e], (uint32_t)j);
         }
         // the BdIndex (j -> bucket position, bucket) only for its consumers
         if (pos_of) pos_of[j] = pos;
@@ -380,7 +404,8 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    uint64_t* __restrict__ ukeys,
                                                    float* __restrict__ ugrad, int gdim,
                                                    uint8_t* __restrict__ usingle, int msub,
-                                                   uint32_t* __restrict__ usub) {
+                                                   uint32_t* __restrict__ usub,
+                                                   const uint32_t* __restrict__ wfin) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
   if (dbg && t == 0) dbg[(long long)b * 8 + (i)] = wall_clock64();
@@ -409,7 +434,14 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   uint64_t kk[kBdRegs];
   // the bucket's (key, sample) records read coalesced, pj written back for
   // the consumers
+  const bool narrow = RW == 3 && wfin && *wfin == 0u;  // 8-byte records (32-bit keys)
+  const uint2* rec2 = reinterpret_cast<const uint2*>(rec);
   auto load = [&](uint32_t p) -> uint64_t {
+    if (narrow) {
+      const uint2 v = rec2[p];
+      pj[p] = v.y;
+      return (uint64_t)v.x;
+    }
     const typename BdRecT<RW>::T v = rec[p];
     pj[p] = v.z;
     return (uint64_t)v.x | ((uint64_t)v.y << 32);
@@ -993,11 +1025,18 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   // N>1 path 1.076-1.103 vs 1.109-1.169 ms)
   static const int cnt = wg_env("SS_BD_CNT", 1024);
   static const int cs = wg_env("SS_BD_CS", 1024);
-  // record width (SS_BD_REC): 16 or 12 bytes
+  // record width (SS_BD_REC): 16, 12, or auto (default: 8 bytes when every
+  // key of the call fits 32 bits, else 12)
   static const int rw = [] {
     const char* e = std::getenv("SS_BD_REC");
     return e && std::atoi(e) == 16 ? 4 : 3;
   }();
+  static const bool narrow_ok = [] {
+    const char* e = std::getenv("SS_BD_REC");
+    return !(e && (std::atoi(e) == 12 || std::atoi(e) == 16));
+  }();
+  uint32_t* wacc = narrow_ok ? S + L.wacc : nullptr;
+  uint32_t* wfin = S + L.wfin;
 #define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \
     case 256: hipLaunchKernelGGL(KERNEL<256>, dim3(L.nch), dim3(256), lds, st, __VA_ARGS__); break; \
@@ -1010,13 +1049,13 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     case 512: hipLaunchKernelGGL((KERNEL<512, RW>), dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
     default: hipLaunchKernelGGL((KERNEL<1024, RW>), dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
   }
-  SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, ucount);
+  SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, ucount, wacc);
   check_launch("k_bd_count");
   switch (cs) {
 #define SS_BD_CS_CASE(CS)                                                                      \
   case CS:                                                                                     \
     hipLaunchKernelGGL(k_bd_colscan<CS>, dim3((L.P + 63) / 64), dim3(CS), 0, st, S + L.hist,   \
-                       L.nch, L.P, S + L.btot, S + L.bstart, S + L.ctr);                       \
+                       L.nch, L.P, S + L.btot, S + L.bstart, S + L.ctr, wacc, wfin);           \
     break;
     SS_BD_CS_CASE(256)
     SS_BD_CS_CASE(512)
@@ -1026,10 +1065,10 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   check_launch("k_bd_colscan");
   if (rw == 3)
     SS_BD_CT_DISPATCH2(ct, 3, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
-                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<BdRec3*>(rec))
+                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<BdRec3*>(rec), wfin)
   else
     SS_BD_CT_DISPATCH2(ct, 4, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
-                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<uint4*>(rec))
+                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<uint4*>(rec), nullptr)
 #undef SS_BD_CT_DISPATCH
 #undef SS_BD_CT_DISPATCH2
   check_launch("k_bd_scatter");
@@ -1039,12 +1078,14 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     hipLaunchKernelGGL(k_bd_dedup<3>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                        bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
                        reinterpret_cast<const BdRec3*>(rec), dbg,
-                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub);
+                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub,
+                       wfin);
   else
     hipLaunchKernelGGL(k_bd_dedup<4>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                        bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
                        reinterpret_cast<const uint4*>(rec), dbg,
-                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub);
+                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub,
+                       nullptr);
   check_launch("k_bd_dedup");
   if (inv && n > 0) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");
