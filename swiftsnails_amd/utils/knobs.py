@@ -68,9 +68,10 @@ KNOBS: dict[str, Knob] = {
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
     "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
-    "SS_BD_REC": Knob("12", "csrc/hip/bdedup.hip", "tuning",
-                      "bytes of the scatter -> dedup (key, sample) record: 12 (dwordx3) or 16 "
-                      "(dwordx4); 12 measured 0.836-0.841 vs 0.850-0.854 ms/step (3 A/B pairs)"),
+    "SS_BD_REC": Knob("auto", "csrc/hip/bdedup.hip", "tuning",
+                      "bytes of the scatter -> dedup (key, sample) record: auto = 8 when every "
+                      "key of the call fits 32 bits, else 12 (dwordx3); 12 or 16 (dwordx4) "
+                      "fixed; 12 measured 0.836-0.841 vs 0.850-0.854 ms/step for 16 (3 A/B pairs)"),
     "SS_SRV_AHEAD": Knob("1", "swiftsnails_amd/parallel/engine.py", "tuning",
                          "N>1 xGMI path, synchronous rounds: wait for the round's keys and "
                          "merge them into the server's distinct keys on the route stream, a "

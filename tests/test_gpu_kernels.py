@@ -1,4 +1,6 @@
 """HIP kernel numerics vs fp32 host references (run on MI355X: -m gpu)."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -305,6 +307,7 @@ def test_bucket_dedup_edge_sizes_and_hot_key(dev, nranks):
              rng.integers(0, 50, 63), rng.integers(0, 10**12, 64), rng.integers(0, 30, 65),
              rng.integers(0, 10**9, 4097),
              np.concatenate([np.full(150_000, 123456789, np.int64), rng.integers(0, 999, 3000)])]
+    cases.append(np.concatenate([rng.integers(0, 1 << 32, 5000), [(1 << 32) + 7]]))
     for k in cases:
         k = k.astype(np.int64)
         r = d(torch.from_numpy(k).to(dev))
@@ -312,6 +315,10 @@ def test_bucket_dedup_edge_sizes_and_hot_key(dev, nranks):
         inv = r.inv.cpu().numpy().view(np.uint32).astype(np.int64)
         np.testing.assert_array_equal(r.ukeys.cpu().numpy()[inv], k)
         assert int(r.ucount.sum().item()) == len(np.unique(k))
+        # scratch word 3: this call's record width (0: 8-byte records, every
+        # key fits 32 bits; the next call decides afresh)
+        if os.environ.get("SS_BD_REC") is None:
+            assert int(d.scratch[3].item()) == int(bool((k >> 32).any()))
     d.check()
 
 
