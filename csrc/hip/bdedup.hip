@@ -642,7 +642,8 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     const uint8_t* __restrict__ usingle,
                                                     DevTable t, const long long* __restrict__ slots,
                                                     const float2* __restrict__ snap, OptParams op,
-                                                    SelfSeg self) {
+                                                    SelfSeg self,
+                                                    const int* __restrict__ slots32 = nullptr) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
@@ -676,13 +677,14 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     }
   }
   __syncthreads();
-  if (slots) {
+  if (slots || slots32) {
     // fused K5 (scalar AdaGrad rows): the merged gradient goes straight into
     // the optimizer update — from the (w, h) the pull snapshot (coalesced,
     // then one blind 8-byte store per key), or read from the row when no
-    // snapshot is valid (N>1 servers with pull-ahead: a read-modify-write)
+    // snapshot is valid (N>1 servers with pull-ahead: a read-modify-write).
+    // slots32: the pull stored 4-byte slot indices (tables under 2^31 slots)
     for (uint32_t l = threadIdx.x; l < nu; l += RT) {
-      const long long slot = slots[base + l];
+      const long long slot = slots32 ? (long long)slots32[base + l] : slots[base + l];
       if (slot < 0) continue;
       float2 wh = snap ? snap[base + l] : *reinterpret_cast<const float2*>(slot_row(t, slot));
       float s2 = 0.f;
@@ -1118,12 +1120,15 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi, const uint8_t* usingle,
                       const DevTable* t, const long long* slots, const float* snap,
-                      const OptParams* op, int ndest) {
+                      const OptParams* op, int ndest, int slot32) {
   if (n <= 0) return;
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
+  // slot32: `slots` holds 4-byte indices (k_pull_unique_bk's slot32 form)
+  const int* s32 = slot32 ? reinterpret_cast<const int*>(slots) : nullptr;
+  if (slot32) slots = nullptr;
   DevTable tv{};
   OptParams opv{};
-  if (slots) {
+  if (slots || s32) {
     if (!t || !op || osi || t->bf16 || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
         t->row_off % 8 != 0 || t->stride % 8 != 0)
       throw_error("bd_reduce: fused apply needs scalar AdaGrad rows and compact ids");
@@ -1141,15 +1146,15 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
                        S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{});
+                       SelfSeg{}, s32);
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
                        S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{});
+                       SelfSeg{}, s32);
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
                      S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{});
+                       SelfSeg{}, s32);
   check_launch("k_bd_reduce");
 }
 

@@ -133,14 +133,14 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("pull_unique_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
                              uintptr_t ubase, int P_, uintptr_t slots, uintptr_t out,
                              const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
-                             uintptr_t st, uintptr_t snap) {
+                             uintptr_t st, uintptr_t snap, int slot32) {
     launch_pull_unique_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
                           P<const uint32_t>(unum), P<const uint32_t>(ubase), P_,
                           P<long long>(slots), P<float>(out), ip, P<unsigned long long>(size_ctr),
-                          P<int>(err), G, S(st), P<float>(snap));
+                          P<int>(err), G, S(st), P<float>(snap), slot32);
   }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
      py::arg("P"), py::arg("slots"), py::arg("out"), py::arg("ip"), py::arg("size_ctr"),
-     py::arg("err"), py::arg("G"), py::arg("st"), py::arg("snap") = 0);
+     py::arg("err"), py::arg("G"), py::arg("st"), py::arg("snap") = 0, py::arg("slot32") = 0);
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
                     long long max_n, const OptParams& op, int G, uintptr_t st, uintptr_t snap) {
     launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st),
@@ -204,16 +204,17 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
-                        uintptr_t snap, std::optional<OptParams> op, int ndest) {
+                        uintptr_t snap, std::optional<OptParams> op, int ndest, int slot32) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                      P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
                      P<float>(ugrad), S(st), osi, P<const uint8_t>(usingle),
                      t ? &*t : nullptr, P<const long long>(slots), P<const float>(snap),
-                     op ? &*op : nullptr, ndest);
+                     op ? &*op : nullptr, ndest, slot32);
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("xval"), py::arg("F"), py::arg("ugrad"), py::arg("st"),
      py::arg("osi") = 0, py::arg("usingle") = 0, py::arg("t") = py::none(), py::arg("slots") = 0,
-     py::arg("snap") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0);
+     py::arg("snap") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0,
+     py::arg("slot32") = 0);
   m.def("bd_unplace", [](long long n, int nranks, uintptr_t scratch, uintptr_t src, uintptr_t dst,
                          int dim, uintptr_t st, int ndest) {
     launch_bd_unplace(n, nranks, P<const uint32_t>(scratch), P<const float>(src), P<float>(dst),

@@ -32,7 +32,8 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, hipStream_t st, float* snap = nullptr);
+                           int* err, int G, hipStream_t st, float* snap = nullptr,
+                           int slot32 = 0);
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
                   const float* snap = nullptr);
@@ -158,7 +159,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       float* ugrad, hipStream_t st, int osi = 0,
                       const uint8_t* usingle = nullptr, const DevTable* t = nullptr,
                       const long long* slots = nullptr, const float* snap = nullptr,
-                      const OptParams* op = nullptr, int ndest = 0);
+                      const OptParams* op = nullptr, int ndest = 0, int slot32 = 0);
 // occ[p] = uvals[uid of occurrence position p] (scalar rows; 0 where none):
 // one workgroup per dedup bucket, for the LR forward's one-gather mode
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,

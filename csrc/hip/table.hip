@@ -178,12 +178,16 @@ __device__ __forceinline__ void pull_one(const DevTable& t, uint64_t key, long l
                                          float2* __restrict__ snap = nullptr, int one16 = 0) {
   if (G == 1 && one16) {
     // 16-byte [w | h | key] slots: one load per probe step (probe_slot16);
-    // with `snap` the (w, h) pair also goes to the snapshot
+    // with `snap` the (w, h) pair also goes to the snapshot.  one16 == 2:
+    // the slot indices are stored as 4 bytes (a table under 2^31 slots)
     bool b = false;
     float2 wh = make_float2(0.f, 0.f);
     const long long slot = key != kEmptyKey ? probe_slot16(t, key, &wh, &b) : -1;
     if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);
-    if (slots_out) slots_out[pos] = slot;
+    if (slots_out) {
+      if (one16 == 2) reinterpret_cast<int*>(slots_out)[pos] = (int)slot;
+      else slots_out[pos] = slot;
+    }
     float* o = out + pos * (long long)t.dim;
     if (slot < 0) {
       o[0] = 0.f;
@@ -784,7 +788,7 @@ void launch_pull_unique(const DevTable& t, const uint64_t* keys, const SegList& 
 void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                            const uint32_t* unum, const uint32_t* ubase, int P, long long* slots,
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
-                           int* err, int G, hipStream_t st, float* snap) {
+                           int* err, int G, hipStream_t st, float* snap, int slot32) {
   if (P <= 0) return;
   if (snap && (t.bf16 || !(G == 1 && t.dim == 1 && t.width == 2 && t.row_off % 8 == 0 &&
                            t.stride % 8 == 0)))
@@ -821,7 +825,12 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   }
   // snapshot pulls on 16-byte [w | h | key] slots probe with one 16-byte
   // load per step (probe_slot16; key load then row load measured slower)
-  const int one16 = snap && t.stride == 16 && t.key_off == 8 && t.row_off == 0;
+  int one16 = snap && t.stride == 16 && t.key_off == 8 && t.row_off == 0;
+  if (slot32) {
+    if (!one16 || G != 1 || t.cap >= (1ull << 31))
+      throw std::invalid_argument("pull: 4-byte slots need snapshot 16-byte slots, cap < 2^31");
+    one16 = 2;
+  }
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_pull_unique_bk<kG>, dim3(P, ny), dim3(256), 0, st, t,
                                       bkeys, bstart, unum, ubase, slots, out, ip, size_ctr, err,
                                       reinterpret_cast<float2*>(snap), one16));

@@ -72,6 +72,7 @@ class Round:
     snap: Optional[torch.Tensor] = None   # world-1: (w, h) rows as pulled (blind apply)
     snap_version: int = -1                # table.version the snapshot is valid for
     applied: bool = False                 # the model's kernel already ran K5 (fuse_apply)
+    slot32: bool = False                  # world-1: `slots` holds 4-byte indices (first half)
     server: Optional[object] = None       # CPU N>1: (unique keys, inverse) of the server merge
 
     @property
@@ -199,10 +200,16 @@ class PSEngine(HostRounds):
             self._pins = [torch.zeros(2 * N, dtype=torch.int64, pin_memory=True)
                           for _ in range(self.depth)]
         if self.fast1:
-            self.slots = [torch.empty(cap, dtype=torch.int64, device=dev)
-                          for _ in range(self.depth)]
             # pull snapshots for the blind-write apply (scalar AdaGrad rows)
             self.snapshot = bool(getattr(table, "snapshot_ok", False))
+            # ... whose slot indices the pull stores as 4 bytes when the shard
+            # has fewer than 2^31 slots (the fused merge reads them back):
+            # 42 MB less traffic per step at the bench shape (SS_SLOT32=0: 8)
+            self.slot32 = bool(self.snapshot and table.stride == 16 and table.G == 1 and
+                               table.capacity < (1 << 31) and
+                               os.environ.get("SS_SLOT32", "1") != "0")
+            self.slots = [torch.empty(cap, dtype=torch.int64, device=dev)
+                          for _ in range(self.depth)]
             self._snaps = [torch.empty((cap, 2), dtype=torch.float32, device=dev)
                            for _ in range(self.depth)] if self.snapshot else None
             if table is not None:  # the pull reads the dedup's staging: no send segment
@@ -459,13 +466,15 @@ class PSEngine(HostRounds):
             snap = (self._snaps[slot] if (not ahead and self.snapshot and tab.snapshot_ok)
                     else None)
             native = getattr(own, "mode", None) == "bucket" and not tab.custom_pull
+            s32 = False
             if native:
                 v = own.bucket_view(dd.n)
+                s32 = self.slot32 and snap is not None
                 self.native.pull_fast(slot, self._tag, st, False, -1, ahead, tab.dt,
                                       tab._init_native, tab.size_ctr.data_ptr(),
                                       tab.err.data_ptr(), tab.G, list(v[:4]), v[4], uv.data_ptr(),
                                       self.slots[slot].data_ptr(),
-                                      snap.data_ptr() if snap is not None else 0)
+                                      snap.data_ptr() if snap is not None else 0, int(s32))
             elif getattr(own, "mode", None) == "bucket":
                 tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], stream=st, snap=snap)
             else:
@@ -475,7 +484,8 @@ class PSEngine(HostRounds):
                 tab.finish_pull(self.slots[slot], uv, n=dd.ucount)
             self.metrics.add(occurrences=dd.n)
             return Round(dd, uv, slot, slots=self.slots[slot], snap=snap,
-                         snap_version=tab.version, ready=native and ahead, tag=self._tag)
+                         snap_version=tab.version, ready=native and ahead, tag=self._tag,
+                         slot32=native and s32)
         if not (self.xg and self.gpu):
             return self._pull_counts(r, uv, self.pt if ahead else self.t, st)
         # N>1 over the mailboxes: one call (keys wait, server merge + lookup,
@@ -569,7 +579,8 @@ class PSEngine(HostRounds):
             return None
         rnd.applied = True
         tab.version += 1
-        args = {"t": tab.dt, "slots": rnd.slots.data_ptr(), "op": tab.opt.native()}
+        args = {"t": tab.dt, "slots": rnd.slots.data_ptr(), "op": tab.opt.native(),
+                "slot32": int(rnd.slot32)}
         if snapshot:
             args["snap"] = rnd.snap.data_ptr()
         return args
@@ -592,8 +603,11 @@ class PSEngine(HostRounds):
                                     rnd.snap_version == tab.version) else None
                 if apply:
                     tab.version += 1
+                sl = rnd.slots
+                if apply and rnd.slot32:  # the apply kernel reads 8-byte slots
+                    sl = sl.view(torch.int32)[:sl.numel()].to(torch.int64)
                 self.native.push_fast(slot, self._tag, self.raw_stream(), apply, tab.dt,
-                                      tab.opt.native(), tab.G, rnd.slots.data_ptr(), g.data_ptr(),
+                                      tab.opt.native(), tab.G, sl.data_ptr(), g.data_ptr(),
                                       rnd.dd.ucount.data_ptr(),
                                       max(1, min(rnd.dd.n, rnd.dd.ucap)),
                                       snap.data_ptr() if snap is not None else 0)

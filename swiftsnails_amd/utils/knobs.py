@@ -72,6 +72,9 @@ KNOBS: dict[str, Knob] = {
                       "bytes of the scatter -> dedup (key, sample) record: auto = 8 when every "
                       "key of the call fits 32 bits, else 12 (dwordx3); 12 or 16 (dwordx4) "
                       "fixed; 12 measured 0.836-0.841 vs 0.850-0.854 ms/step for 16 (3 A/B pairs)"),
+    "SS_SLOT32": Knob("1", "swiftsnails_amd/parallel/engine.py", "tuning",
+                      "one GPU, scalar (w, h) snapshot rows, shard under 2^31 slots: the pull "
+                      "stores 4-byte slot indices for the fused merge + update (0: 8 bytes)"),
     "SS_SRV_AHEAD": Knob("1", "swiftsnails_amd/parallel/engine.py", "tuning",
                          "N>1 xGMI path, synchronous rounds: wait for the round's keys and "
                          "merge them into the server's distinct keys on the route stream, a "

@@ -443,6 +443,28 @@ def _graph_worker(model, dev, **ek):
     return Word2VecWorker(eng, data), table
 
 
+def test_lr_slot32_matches_slot64(dev, monkeypatch):
+    """One-GPU sparse LR with the pull storing 4-byte slot indices for the
+    fused merge + AdaGrad update (default, shards under 2^31 slots) trains
+    exactly like 8-byte slots: same per-step losses, same table."""
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    out = {}
+    for s32 in ("1", "0"):
+        monkeypatch.setenv("SS_SLOT32", s32)
+        w, t = _graph_worker("lr", dev)
+        assert w.engine.slot32 == (s32 == "1")
+        losses = [float(w.step().sum().item()) for _ in range(6)]
+        torch.cuda.synchronize()
+        t.check()
+        out[s32] = (losses, t.to_dict(with_state=True))
+    (l1, d1), (l0, d0) = out["1"], out["0"]
+    np.testing.assert_allclose(l1, l0, rtol=1e-5, atol=1e-6)
+    assert d1.keys() == d0.keys()
+    ks = list(d0.keys())
+    np.testing.assert_allclose(np.stack([d1[k] for k in ks]), np.stack([d0[k] for k in ks]),
+                               rtol=1e-5, atol=1e-6)
+
+
 @pytest.mark.parametrize("model", ["lr", "fm", "w2v", "w2v_pairs"])
 def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
     """hipGraph replays (one graph per ring phase, device step counter for
