@@ -1163,11 +1163,14 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
 void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, const uint32_t* unum,
                         const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
                         float* ugrad, const DevTable* t, const long long* slots,
-                        const float* snap, const OptParams* op, hipStream_t st, SelfSeg self) {
+                        const float* snap, const OptParams* op, hipStream_t st, SelfSeg self,
+                        int slot32) {
   if (P <= 0) return;
   DevTable tv{};
   OptParams opv{};
-  if (slots) {
+  const int* s32 = slot32 ? reinterpret_cast<const int*>(slots) : nullptr;
+  if (slot32) slots = nullptr;
+  if (slots || s32) {
     if (!t || !op || t->bf16 || op->kind != kOptAdaGrad || t->dim != 1 || t->width != 2 ||
         t->row_off % 8 != 0 || t->stride % 8 != 0)
       throw_error("bd_reduce_p: fused apply needs scalar AdaGrad rows");
@@ -1176,7 +1179,7 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
   }
   hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj, luid,
                      gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
-                     reinterpret_cast<const float2*>(snap), opv, self);
+                     reinterpret_cast<const float2*>(snap), opv, self, s32);
   check_launch("k_bd_reduce_p");
 }
 

@@ -74,6 +74,7 @@ class RoundEngine {
     grads_.resize(depth);
     self_keys_.assign(depth, 0);
     srv_done_.assign(depth, 0);
+    srv_s32_.assign(depth, 0);
   }
   ~RoundEngine() {
     hipSetDevice(device_);
@@ -230,9 +231,13 @@ class RoundEngine {
     srv_done_[slot] = false;
     if (table) {
       SrvSlot& S = srv_[slot];
+      // snapshot pulls of 16-byte scalar slots in a shard under 2^31 slots
+      // store 4-byte slot indices; the push's fused merge reads them back
+      srv_s32_[slot] = snap && G == 1 && t.stride == 16 && t.key_off == 8 && t.row_off == 0 &&
+                       t.cap < (1ull << 31) && slot32_on();
       launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
                             Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
-                            G, St(stream), snap ? S.snap : nullptr);
+                            G, St(stream), snap ? S.snap : nullptr, srv_s32_[slot]);
       if (custom_pull) return;  // the caller finishes the pull (tensor-code hooks)
       fill_and_return(slot, stream, svals, rvals, sent, metrics);
     } else {
@@ -287,9 +292,12 @@ class RoundEngine {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
       const SelfSeg sg = self_seg(grads);  // this rank's own gradient rows, in place
+      if (srv_s32_[slot] && !(update && scalar_fused && snap))
+        throw std::logic_error("push_xgmi: a 4-byte-slot pull needs the fused snapshot merge");
       if (update && scalar_fused)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
-                           1, nullptr, &t, S.slots, snap ? S.snap : nullptr, &op, St(stream), sg);
+                           1, nullptr, &t, S.slots, snap ? S.snap : nullptr, &op, St(stream), sg,
+                           srv_s32_[slot]);
       else if (dim_ == 1)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
                            1, Pt<float>(merged), nullptr, nullptr, nullptr, nullptr, St(stream),
@@ -402,6 +410,14 @@ class RoundEngine {
   std::vector<XReg> vals_, grads_;
   std::vector<uintptr_t> self_keys_;  // per slot: this rank's send layout of its keys
   std::vector<char> srv_done_;        // per slot: the route ran keys_in (srv_ahead)
+  std::vector<char> srv_s32_;         // per slot: the server pull stored 4-byte slots
+  static bool slot32_on() {           // SS_SLOT32=0: 8-byte slot indices
+    static const bool on = [] {
+      const char* e = std::getenv("SS_SLOT32");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   int nranks_ = 1, rank_ = 0, Pd_ = 1, sub_ = 1, dim_ = 1, bpp_ = 128;
   long long cap_ = 0;
   double timeout_ = 120.0;

@@ -180,7 +180,7 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
                         const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
                         float* ugrad, const DevTable* t, const long long* slots,
                         const float* snap, const OptParams* op, hipStream_t st,
-                        SelfSeg self = {});
+                        SelfSeg self = {}, int slot32 = 0);
 void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* unum, const uint32_t* luid, const float* uvals,
                           float* occ, const uint32_t* pj, hipStream_t st, SelfSeg self = {});
