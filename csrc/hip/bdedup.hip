@@ -643,9 +643,19 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     DevTable t, const long long* __restrict__ slots,
                                                     const float2* __restrict__ snap, OptParams op,
                                                     SelfSeg self,
-                                                    const int* __restrict__ slots32 = nullptr) {
+                                                    const int* __restrict__ slots32 = nullptr,
+                                                    float* __restrict__ lacc = nullptr,
+                                                    float* __restrict__ lacc_out = nullptr,
+                                                    int lacc_n = 0) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
+  // the step's loss accumulator (added by the forward, ordered before this
+  // launch) moves to lacc_out and is left zero: no zero-fill launch per step
+  if (lacc)
+    for (int i = b * RT + threadIdx.x; i < lacc_n; i += gridDim.x * RT) {
+      lacc_out[i] = lacc[i];
+      lacc[i] = 0.f;
+    }
   const uint32_t p0 = bstart[b], p1 = bstart[b + 1], nu = unum[b];
   const uint32_t base = osi ? p0 : ubase[b];  // rows in occurrence space or compact
   for (uint32_t l = threadIdx.x; l < nu; l += RT) acc[l] = 0.f;
@@ -1120,8 +1130,10 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi, const uint8_t* usingle,
                       const DevTable* t, const long long* slots, const float* snap,
-                      const OptParams* op, int ndest, int slot32) {
+                      const OptParams* op, int ndest, int slot32, float* lacc, float* lacc_out,
+                      int lacc_n) {
   if (n <= 0) return;
+  if (lacc && (!lacc_out || lacc_n <= 0)) throw_error("bd_reduce: loss hand-off needs its output");
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
   // slot32: `slots` holds 4-byte indices (k_pull_unique_bk's slot32 form)
   const int* s32 = slot32 ? reinterpret_cast<const int*>(slots) : nullptr;
@@ -1146,15 +1158,15 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
                        S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32);
+                       SelfSeg{}, s32, lacc, lacc_out, lacc_n);
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
                        S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32);
+                       SelfSeg{}, s32, lacc, lacc_out, lacc_n);
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
                      S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32);
+                       SelfSeg{}, s32, lacc, lacc_out, lacc_n);
   check_launch("k_bd_reduce");
 }
 

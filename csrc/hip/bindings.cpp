@@ -204,17 +204,18 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
-                        uintptr_t snap, std::optional<OptParams> op, int ndest, int slot32) {
+                        uintptr_t snap, std::optional<OptParams> op, int ndest, int slot32,
+                        uintptr_t acc, uintptr_t acc_out, int acc_n) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                      P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
                      P<float>(ugrad), S(st), osi, P<const uint8_t>(usingle),
                      t ? &*t : nullptr, P<const long long>(slots), P<const float>(snap),
-                     op ? &*op : nullptr, ndest, slot32);
+                     op ? &*op : nullptr, ndest, slot32, P<float>(acc), P<float>(acc_out), acc_n);
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("xval"), py::arg("F"), py::arg("ugrad"), py::arg("st"),
      py::arg("osi") = 0, py::arg("usingle") = 0, py::arg("t") = py::none(), py::arg("slots") = 0,
      py::arg("snap") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0,
-     py::arg("slot32") = 0);
+     py::arg("slot32") = 0, py::arg("acc") = 0, py::arg("acc_out") = 0, py::arg("acc_n") = 0);
   m.def("bd_unplace", [](long long n, int nranks, uintptr_t scratch, uintptr_t src, uintptr_t dst,
                          int dim, uintptr_t st, int ndest) {
     launch_bd_unplace(n, nranks, P<const uint32_t>(scratch), P<const float>(src), P<float>(dst),

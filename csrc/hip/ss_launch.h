@@ -159,7 +159,8 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       float* ugrad, hipStream_t st, int osi = 0,
                       const uint8_t* usingle = nullptr, const DevTable* t = nullptr,
                       const long long* slots = nullptr, const float* snap = nullptr,
-                      const OptParams* op = nullptr, int ndest = 0, int slot32 = 0);
+                      const OptParams* op = nullptr, int ndest = 0, int slot32 = 0,
+                      float* lacc = nullptr, float* lacc_out = nullptr, int lacc_n = 0);
 // occ[p] = uvals[uid of occurrence position p] (scalar rows; 0 where none):
 // one workgroup per dedup bucket, for the LR forward's one-gather mode
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,

@@ -98,6 +98,9 @@ class SparseLRWorker(PipelinedWorker):
         # ms/step); the scatter then skips the bucket-of-occurrence array
         self.occ = torch.empty(n, dtype=torch.float32, device=dev) if self.bucketed else None
         if self.bucketed:
+            # the forward adds the loss into _acc; the merge moves it to
+            # loss_sum and leaves _acc zero (see _compute)
+            self._acc = torch.zeros_like(self.loss_sum)
             for dd in engine.dedupers:
                 dd.zero_grad = False         # the LDS reduce stores every unique row
                 dd.materialize_inv = False   # the forward resolves occurrences itself
@@ -114,6 +117,10 @@ class SparseLRWorker(PipelinedWorker):
                           for _ in range(engine.depth)]
             self.nitems = [torch.zeros(1, dtype=torch.int32, device=dev)
                            for _ in range(engine.depth)]
+
+    def _zero_acc(self) -> None:
+        if not self.bucketed:
+            self.loss_sum.zero_()
 
     def _post(self, dd, slot, st):
         hip().sr_plan(dd.inv.data_ptr(), dd.n, dd.ucount.data_ptr(), dd.nranks, dd.ucap,
@@ -147,15 +154,18 @@ class SparseLRWorker(PipelinedWorker):
             o = dd.owner
             o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
             h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
-                       rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1, self.loss_sum.data_ptr(),
+                       rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1, self._acc.data_ptr(),
                        0, st, o.index_ptrs(dd.n), occ=self.occ.data_ptr())
             # one GPU: the merge kernel runs the AdaGrad update itself
             # (engine.fuse_apply: pull snapshot still valid), push() then only
             # does the bookkeeping; N>1: compact rows in the send layout
             fa = self.engine.fuse_apply(rnd)
+            # the merge also moves the step's loss out of the forward's
+            # accumulator and zeroes it (no zero-fill launch per step)
             h.bd_reduce(dd.lay, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                         o.luid.data_ptr(), self.gocc.data_ptr(), xp, d.num_fields,
-                        rnd.ugrad.data_ptr(), st, 0, 0, ndest=o.ndest, **(fa or {}))
+                        rnd.ugrad.data_ptr(), st, 0, 0, ndest=o.ndest, acc=self._acc.data_ptr(),
+                        acc_out=self.loss_sum.data_ptr(), acc_n=self._acc.numel(), **(fa or {}))
         elif self.grad_mode == "segreduce":
             h.lr_fwd_g(rnd.inv.data_ptr(), xp, self.labels[slot].data_ptr(), d.batch_size,
                        d.num_fields, rnd.uvals.data_ptr(), self.gocc.data_ptr(), 0,

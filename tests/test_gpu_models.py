@@ -453,6 +453,12 @@ def test_lr_slot32_matches_slot64(dev, monkeypatch):
         monkeypatch.setenv("SS_SLOT32", s32)
         w, t = _graph_worker("lr", dev)
         assert w.engine.slot32 == (s32 == "1")
+        w.step()
+        # zero-initialised weights: every logit 0, the first step's loss is
+        # ln 2 per sample — moved out of the forward's accumulator by the
+        # merge kernel, which leaves the accumulator zero
+        assert abs(w.mean_loss() - np.log(2.0)) < 1e-4
+        assert float(w._acc.abs().sum()) == 0.0
         losses = [float(w.step().sum().item()) for _ in range(6)]
         torch.cuda.synchronize()
         t.check()
