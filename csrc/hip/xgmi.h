@@ -233,13 +233,12 @@ class XgmiArena {
     // no arrival counting (the verify tags of the other blocks then stay
     // unwritten, so verify mode keeps the full grid)
     P.self_lite = !verify_ && self_bytes <= (256ll << 10);
-    if (nranks_ == 1 && !verify_) {
-      // nothing but the own segment: a block per 8 KB of what it still copies
-      // (one block for 40 KB of bucket-run tables took 16 us), arrivals
-      // counted only when there are several
-      P.bpp = (int)std::min<long long>(32, std::max<long long>(1, (self_bytes + 8191) / 8192));
-      P.self_lite = P.bpp == 1;
-    }
+    // nothing but the own segment: one block.  (Sizing this grid by the bytes
+    // left to copy made the block count differ between the start-up litmus
+    // and the production puts of a channel; the arrival counter publishes on
+    // every bpp-th arrival, so a put of another geometry could publish before
+    // its last block had drained — the grid of a channel must not change.)
+    if (P.self_lite && nranks_ == 1) P.bpp = 1;
     // every rank puts to (ch, this arena layout) with the same geometry, so
     // the receiver's tag check uses the block count of its own put
     put_bpp_[ch] = P.bpp;
