@@ -239,6 +239,13 @@ class XgmiArena {
     // every bpp-th arrival, so a put of another geometry could publish before
     // its last block had drained — the grid of a channel must not change.)
     if (P.self_lite && nranks_ == 1) P.bpp = 1;
+    // the arrival counters (every destination but a lite own segment) publish
+    // on each bpp-th arrival: one geometry per channel for the arena's life
+    if (nranks_ > 1 || !P.self_lite) {
+      if (!arrive_bpp_[ch]) arrive_bpp_[ch] = P.bpp;
+      else if (arrive_bpp_[ch] != P.bpp)
+        throw_error("xgmi: a channel's put grid changed (its arrival counter would publish early)");
+    }
     // every rank puts to (ch, this arena layout) with the same geometry, so
     // the receiver's tag check uses the block count of its own put
     put_bpp_[ch] = P.bpp;
@@ -296,6 +303,7 @@ class XgmiArena {
   unsigned remote_ = 0;
   bool verify_ = false;
   int put_bpp_[kXMaxCh] = {};
+  int arrive_bpp_[kXMaxCh] = {};  // the block count the channel's arrival counters count in
 };
 
 long long xgmi_head_bytes();
