@@ -304,11 +304,7 @@ __global__ __launch_bounds__(256) void k_srv_fill_rows(const uint32_t* __restric
 // ~30), then a lane group per key sums its rows (lane-consecutive words; no
 // atomics).  `slots`: the merged row goes straight into the
 // optimizer update of the key's table row (each lane updates its
-// coordinates and their state) — no merged-row round trip, no apply launch.
-// VD = 32 / 64 / 128 (fp32 rows starting 16-byte aligned in the slot): 8
-// lanes per key moving row, state and gradients as float4s (table.hip's
-// k_apply_rows form: 8 keys per wave in flight instead of two)
-template <int VD>
+// coordinates and their state) — no merged-row round trip, no apply launch
 __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restrict__ bstart,
                                                         const uint32_t* __restrict__ ubase,
                                                         const uint32_t* __restrict__ unum,
@@ -372,54 +368,6 @@ __global__ __launch_bounds__(512) void k_srv_merge_rows(const uint32_t* __restri
     __syncthreads();
   }
   const int ns = opt_state_per_coord(op.kind);
-  if constexpr (VD > 0) {
-    constexpr int NV = VD / 32, Q = VD / 4;  // float4s per lane / per row array
-    const int lg = t & 7;
-    const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (uint32_t l = blockIdx.y * 64 + (uint32_t)(t >> 3); l < nu; l += gridDim.y * 64) {
-      const uint32_t a = off[l], z = off[l + 1];
-      const long long slot = slots ? slots[(long long)base + l] : -1;
-      const bool upd = slots && slot >= 0;
-      float4 w[NV], s1[NV], s2[NV], acc[NV];
-      float4* row = upd ? reinterpret_cast<float4*>(slot_row(tab, slot)) : nullptr;
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const int c = lg + 8 * k;
-        acc[k] = z4;
-        w[k] = upd ? row[c] : z4;
-        s1[k] = upd && ns > 0 ? row[Q + c] : z4;
-        s2[k] = upd && ns > 1 ? row[2 * Q + c] : z4;
-      }
-      for (uint32_t q = a; q < z; ++q) {
-        const long long gp = pj[p0 + ord[q]];
-        const float4* g = reinterpret_cast<const float4*>(self.pick(grads, gp) + gp * VD);
-#pragma unroll
-        for (int k = 0; k < NV; ++k) {
-          const float4 v = g[lg + 8 * k];
-          acc[k].x += v.x;
-          acc[k].y += v.y;
-          acc[k].z += v.z;
-          acc[k].w += v.w;
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < NV; ++k) {
-        const int c = lg + 8 * k;
-        if (!slots) {
-          reinterpret_cast<float4*>(merged)[((long long)base + l) * Q + c] = acc[k];
-        } else if (upd) {
-          opt_update(op, w[k].x, s1[k].x, s2[k].x, acc[k].x);
-          opt_update(op, w[k].y, s1[k].y, s2[k].y, acc[k].y);
-          opt_update(op, w[k].z, s1[k].z, s2[k].z, acc[k].z);
-          opt_update(op, w[k].w, s1[k].w, s2[k].w, acc[k].w);
-          row[c] = w[k];
-          if (ns > 0) row[Q + c] = s1[k];
-          if (ns > 1) row[2 * Q + c] = s2[k];
-        }
-      }
-    }
-    return;
-  }
   // a group of G lanes per key; lane lg owns coordinates lg + i*G, so every
   // load / store instruction of the group covers G consecutive words (the
   // table row and the gradient rows alike; 16-byte chunks per lane left each
@@ -524,26 +472,9 @@ void launch_srv_merge_rows(int P, const uint32_t* bstart, const uint32_t* ubase,
                 (int)t->width != D * (1 + opt_state_per_coord(op->kind))))
     throw_error("srv_merge_rows: a fused update needs the table of these rows");
   if (!slots && !merged) throw_error("srv_merge_rows: merged rows or a fused update");
-  // fp32 rows of 32 / 64 / 128 starting 16-byte aligned: the 8-lane float4 form
-  static const bool vec_on = [] {
-    const char* e = std::getenv("SS_PULL_VEC");
-    return !(e && e[0] == '0');
-  }();
-  const auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  const bool vec = vec_on && (D == 32 || D == 64 || D == 128) && a16(grads) &&
-                   a16(self.ptr) && (slots ? (!t->bf16 && t->row_off % 16 == 0 &&
-                                              t->stride % 16 == 0)
-                                           : a16(merged));
-  const DevTable tv = t ? *t : DevTable{};
-  const OptParams ov = op ? *op : OptParams{};
-#define SS_SRV_MERGE(VD)                                                                       \
-  hipLaunchKernelGGL(k_srv_merge_rows<VD>, dim3(P, srv_share(P)), dim3(512), 0, st, bstart,     \
-                     ubase, unum, pj, luid, grads, merged, D, tv, slots, ov, self)
-  if (vec && D == 32) SS_SRV_MERGE(32);
-  else if (vec && D == 64) SS_SRV_MERGE(64);
-  else if (vec && D == 128) SS_SRV_MERGE(128);
-  else SS_SRV_MERGE(0);
-#undef SS_SRV_MERGE
+  hipLaunchKernelGGL(k_srv_merge_rows, dim3(P, srv_share(P)), dim3(512), 0, st, bstart, ubase,
+                     unum, pj, luid,
+                     grads, merged, D, t ? *t : DevTable{}, slots, op ? *op : OptParams{}, self);
   check_launch("k_srv_merge_rows");
 }
 
