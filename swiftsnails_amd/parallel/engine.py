@@ -25,7 +25,9 @@ ring's events).  Host-count transports (RCCL, gloo, the CPU engine that
 tests the multi-rank logic) are the ``HostRounds`` mixin
 (``engine_host.py``).  Split roles (S servers + W workers) fall out of the
 same code: non-server ranks own no table, non-worker ranks route an empty
-key set, every rank enters every round.
+key set, every rank enters every round.  The N>1 device set-up
+(``engine_dist.py``) and the read-only lookup / control calls
+(``engine_ctl.py``) are mixins of PSEngine.
 """
 from __future__ import annotations
 
@@ -40,6 +42,8 @@ import torch
 from ..ops.dedup import CpuDeduper, DedupResult, Deduper
 from ..utils.streams import current, current_raw, use_stream
 from ..utils.tracing import Metrics, Tracer
+from .engine_ctl import EngineControl
+from .engine_dist import DeviceSetup, _ServerSlot  # noqa: F401 (re-export)
 from .engine_host import HostRounds
 from .router import HashFrag
 from .transport import CountsHandle, LoopbackTransport, Transport
@@ -90,35 +94,8 @@ def _hip():
     return hip()
 
 
-class _ServerSlot:
-    """Device buffers of one ring slot's server-side merge (N>1, GPU)."""
 
-    def __init__(self, rows: int, P: int, dev, snapshot: bool):
-        u32 = torch.int32
-        self.cnt = torch.zeros(P + 1, dtype=u32, device=dev)  # + the arrival counter
-        self.bstart = torch.empty(P + 1, dtype=u32, device=dev)
-        self.ubase = torch.empty(P, dtype=u32, device=dev)
-        self.unum = torch.empty(P, dtype=u32, device=dev)
-        self.ucount = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.pj = torch.empty(rows, dtype=u32, device=dev)
-        self.luid = torch.empty(rows, dtype=u32, device=dev)
-        self.bkeys = torch.empty(rows, dtype=torch.int64, device=dev)
-        self.slots = torch.empty(rows, dtype=torch.int64, device=dev)
-        self.snap = torch.empty((rows, 2), dtype=torch.float32, device=dev) if snapshot else None
-        self.snap_valid = False
-
-    def view(self, P: int):
-        return (self.bkeys.data_ptr(), self.bstart.data_ptr(), self.unum.data_ptr(),
-                self.ubase.data_ptr(), P)
-
-    def ptrs(self):
-        t = (self.cnt, self.bstart, self.ubase, self.unum, self.pj, self.luid, self.bkeys,
-             self.slots)
-        return [x.data_ptr() for x in t] + [self.snap.data_ptr() if self.snap is not None else 0,
-                                            self.ucount.data_ptr()]
-
-
-class PSEngine(HostRounds):
+class PSEngine(HostRounds, DeviceSetup, EngineControl):
     """Worker+server round engine for one rank.
 
     table           : this rank's shard (``HbmTable``/``HostTable``) or None when not a server
@@ -254,87 +231,6 @@ class PSEngine(HostRounds):
         instead of a third stream of its own."""
         xg = getattr(self, "xg", None)
         return bool(xg is not None and getattr(xg, "devices", self.world) < self.world)
-
-    # ------------------------------------------------------------ N>1 (GPU)
-    def _init_dist_gpu(self) -> None:
-        """Receive buffers and server-merge slots of the N>1 device path.
-        Every rank lays its buckets out as a call of ``max_keys`` keys (the
-        common layout the servers merge) and sends each destination its
-        per-bucket runs with the keys."""
-        N, cap, d, dev, h = self.world, self.max_keys, self.dim, self.device, _hip()
-        for dd in self.dedupers:
-            dd.lay_n = cap
-        self.Pd = h.bd_buckets(cap, N, self.dedupers[0].ndest) // N
-        self.sub = h.srv_sub_buckets(N)
-        self.Ps = self.Pd * self.sub
-        # sub > 1: every source groups its runs by the servers' sub-bucket
-        # and sends the offsets with them (the server reads exact ranges)
-        for dd in self.dedupers:
-            dd.split_for_servers(self.sub)
-        Psub = self.Pd * self.sub if self.sub > 1 else 0
-        # every rank's max_keys must agree (it fixes Pd)
-        mk = torch.tensor([cap, -cap], dtype=torch.int64, device=dev)
-        self._agree(mk)
-        if int(mk[0]) != cap or int(-mk[1]) != cap:
-            raise ValueError("PSEngine: max_keys differs across ranks (the N>1 bucket layout "
-                             "is a function of it)")
-        rows = N * cap
-        self.rvals = torch.zeros((rows, d), dtype=torch.float32, device=dev)
-        if self.xg:
-            # the receive buffers are the arena's mailboxes: keys + the bucket
-            # runs (bases, sizes) per source, rows back, gradients
-            Pd, xg = self.Pd, self.xg
-            xg.setup({"keys": (self.depth, [cap * 8, Pd * 4, Pd * 4] + ([Psub * 4] if Psub else [])),
-                      "vals": (self.depth, [cap * 4 * d]), "grads": (self.depth, [cap * 4 * d])})
-            self.rkeys = [xg.region("keys", 0, q, torch.int64) for q in range(self.depth)]
-            self.rmeta = [(xg.region("keys", 1, q, torch.int32),
-                           xg.region("keys", 2, q, torch.int32)) for q in range(self.depth)]
-            self.rsub = [xg.region("keys", 3, q, torch.int32) if Psub else None
-                         for q in range(self.depth)]
-            self.uvals = [xg.region("vals", 0, q, torch.float32, d) for q in range(self.depth)]
-            self.rgrads = [xg.region("grads", 0, q, torch.float32, d) for q in range(self.depth)]
-        else:
-            self.rkeys = [torch.empty(rows, dtype=torch.int64, device=dev)] * self.depth
-            meta = [torch.zeros(2 * N * self.Pd, dtype=torch.int32, device=dev)
-                    for _ in range(self.depth)]
-            self.rmeta = [(m[:N * self.Pd], m[N * self.Pd:]) for m in meta]
-            self.rsub = [torch.zeros(N * Psub, dtype=torch.int32, device=dev) if Psub else None
-                         for _ in range(self.depth)]
-            self.rgrads = [torch.empty((rows, d), dtype=torch.float32, device=dev)] * self.depth
-        self.srv = None
-        self.srv_ahead = os.environ.get("SS_SRV_AHEAD", "1") != "0"
-        if self.table is not None:
-            self.svals = torch.empty((rows, d), dtype=torch.float32, device=dev)
-            self.sgrad = torch.empty((rows, d), dtype=torch.float32, device=dev)
-            self.srv_err = torch.zeros(1, dtype=torch.int32, device=dev)
-            snap_ok = bool(getattr(self.table, "snapshot_ok", False))
-            self.srv = [_ServerSlot(rows, self.Ps, dev, snap_ok) for _ in range(self.depth)]
-        if self.xg:
-            D = self.depth
-            self.native.set_xgmi([[self.xg.arena_of(c, q) for c in ("keys", "vals", "grads")]
-                                  for q in range(D)],
-                                 [sum((list(self.xg.layout("keys", p, q))
-                                       for p in range(4 if Psub else 3)), []) for q in range(D)],
-                                 [list(self.xg.layout("vals", 0, q)) for q in range(D)],
-                                 [list(self.xg.layout("grads", 0, q)) for q in range(D)],
-                                 N, self.rank, self.Pd, self.sub, cap, d, self.xg.bpp,
-                                 self.xg.timeout_s)
-            # a closed transport frees its arenas: the engine forgets them first
-            self.xg._close_hooks.append(self.native.clear_xgmi)
-            for q in range(D):
-                if self.srv is not None:
-                    self.native.set_server_slot(q, self.srv[q].ptrs())
-            self._nodt = h.DevTable(0, 1, 16, 8, 1, 2)  # a rank without a shard
-            self._noop = h.OptParams()
-            self._noip = h.InitParams()
-
-    def _agree(self, t: torch.Tensor) -> None:
-        """min-all-reduce of a small int64 tensor over the data transport."""
-        if self.world == 1:
-            return
-        self.t.allreduce_(t, "min")
-        if self.gpu:
-            torch.cuda.current_stream(self.device).synchronize()
 
     @staticmethod
     def slot_bytes(world: int, max_keys: int, dim: int) -> int:
@@ -536,16 +432,6 @@ class PSEngine(HostRounds):
             self.pull_ahead = False
         return self.pull_ahead
 
-    def max_over_ranks(self, value: float) -> float:
-        """max of a host float over the ranks (control plane; syncs)."""
-        if self.world == 1:
-            return float(value)
-        dev = self.device if (self.gpu and not hasattr(self.t, "aux")) else "cpu"
-        t = torch.tensor([value], dtype=torch.float32 if dev != "cpu" else torch.float64,
-                         device=dev)
-        self.t.allreduce_(t, "max")
-        return float(t.item())
-
     def begin(self, rnd: Round) -> None:
         if self.gpu:
             self._wait_ev(PULL, rnd, self.raw_stream())
@@ -635,97 +521,3 @@ class PSEngine(HostRounds):
             self._release(slot)
         rnd.pushed = True
         self.rounds += 1
-
-    # ------------------------------------------------------------ read-only
-    def lookup(self, keys: torch.Tensor) -> torch.Tensor:
-        """Collective READ-ONLY pull: rows [n, dim] of ``keys`` (in order)
-        from whichever shard owns each key; a key no shard holds reads as
-        zeros and is NOT inserted, and nothing is pushed — the reference's
-        pull_with_barrier of any key from every server by any worker
-        (/root/reference/src/core/parameter/global_pull_access.h:40-55), for
-        evaluating a sharded model.  Every rank calls it together (a rank
-        without keys passes an empty tensor).  It runs on the gloo control
-        plane (host-staged): an evaluation path, not a training one."""
-        keys = keys.reshape(-1)
-        if self.world == 1:
-            return self._read_rows(keys.to(self.device)).to(keys.device)
-        import torch.distributed as dist
-
-        from .router import route_keys_np
-
-        N = self.world
-        u, inv = torch.unique(keys.cpu(), return_inverse=True)
-        dest = route_keys_np(u.numpy().view(np.uint64), self.frag_map) if len(u) else \
-            np.zeros(0, np.int64)
-        order = torch.from_numpy(np.argsort(dest, kind="stable"))
-        scount = torch.from_numpy(np.bincount(dest, minlength=N).astype(np.int64))
-        rcount = torch.empty(N, dtype=torch.int64)
-        dist.all_to_all_single(rcount, scount)
-        sk = u[order].contiguous()
-        rk = torch.empty(int(rcount.sum()), dtype=torch.int64)
-        dist.all_to_all_single(rk, sk, rcount.tolist(), scount.tolist())
-        rows = (self._read_rows(rk.to(self.device)).cpu().contiguous() if self.table is not None
-                else torch.zeros((len(rk), self.dim), dtype=torch.float32))
-        back = torch.empty((len(sk), self.dim), dtype=torch.float32)
-        dist.all_to_all_single(back.view(-1), rows.view(-1), [c * self.dim for c in scount.tolist()],
-                               [c * self.dim for c in rcount.tolist()])
-        out_u = torch.empty_like(back)
-        out_u[order] = back
-        return out_u[inv].to(keys.device)
-
-    def _read_rows(self, keys: torch.Tensor) -> torch.Tensor:
-        tab = self.table
-        if len(keys) == 0:
-            return torch.zeros((0, self.dim), dtype=torch.float32, device=keys.device)
-        if self.gpu:
-            torch.cuda.synchronize(self.device)  # every enqueued update applied
-            return tab.pull(keys, insert=False)[0]
-        rows, found = tab._t.get_rows(keys.numpy().view(np.uint64))
-        r = torch.from_numpy(np.ascontiguousarray(rows[:, :self.dim]))
-        r[torch.from_numpy(found == 0)] = 0.0
-        return r
-
-    # ------------------------------------------------------------ control
-    def barrier(self):
-        self.t.barrier()
-
-    def all_done(self, local_done: bool) -> bool:
-        """Collective termination: True once every rank reports done (every
-        rank calls it at the same rounds; syncs).  A rank that finished early
-        keeps serving rounds with an empty key set until then — the
-        reference's master waiting for every worker's WORKER_FINISH_WORK
-        before stopping the servers (master/terminate.h:44-62)."""
-        self.poll()
-        if self.world == 1:
-            return bool(local_done)
-        dev = self.device if (self.gpu and not hasattr(self.t, "aux")) else "cpu"
-        flag = torch.tensor([1 if local_done else 0], dtype=torch.int64, device=dev)
-        self.t.allreduce_(flag, "min")
-        return int(flag.item()) == 1
-
-    def poll(self) -> None:
-        """Cheap per-round health check, no device sync: raises if a mailbox
-        wait has timed out or seen a stale round tag (host-mapped error
-        words of the xGMI transport)."""
-        if self.xg is not None:
-            self.xg.poll_error()
-
-    def check(self) -> None:
-        """Raise on a sticky device-side error (syncs): an overflowed dedup
-        or server-merge bucket, a full / misused table, a mailbox peer that
-        never arrived.  Called at the end of bench.py, every periodic backup
-        and PSContext.finish."""
-        for d in self.dedupers:
-            chk = getattr(d, "check", None)
-            if chk is not None:
-                chk()
-        if getattr(self, "srv", None) is not None and int(self.srv_err.item()) != 0:
-            from ..ops.dedup import DedupOverflowError
-
-            raise DedupOverflowError("server merge: a bucket of received keys overflowed its "
-                                     "LDS table")
-        chk = getattr(self.table, "check", None) if self.table is not None else None
-        if chk is not None:
-            chk()
-        if self.xg is not None:
-            self.xg.check()

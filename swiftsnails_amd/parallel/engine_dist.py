@@ -1,0 +1,129 @@
+"""N>1 device set-up of the round engine (parallel/engine.py): the receive
+buffers, the server-merge slots and the xGMI mailbox layout handed to the C++
+RoundEngine.  Split out of PSEngine as a mixin; see engine.py for the round
+itself."""
+from __future__ import annotations
+
+import os
+
+import torch
+
+
+def _hip():
+    from .._native import hip
+
+    return hip()
+
+
+class _ServerSlot:
+    """Device buffers of one ring slot's server-side merge (N>1, GPU)."""
+
+    def __init__(self, rows: int, P: int, dev, snapshot: bool):
+        u32 = torch.int32
+        self.cnt = torch.zeros(P + 1, dtype=u32, device=dev)  # + the arrival counter
+        self.bstart = torch.empty(P + 1, dtype=u32, device=dev)
+        self.ubase = torch.empty(P, dtype=u32, device=dev)
+        self.unum = torch.empty(P, dtype=u32, device=dev)
+        self.ucount = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.pj = torch.empty(rows, dtype=u32, device=dev)
+        self.luid = torch.empty(rows, dtype=u32, device=dev)
+        self.bkeys = torch.empty(rows, dtype=torch.int64, device=dev)
+        self.slots = torch.empty(rows, dtype=torch.int64, device=dev)
+        self.snap = torch.empty((rows, 2), dtype=torch.float32, device=dev) if snapshot else None
+        self.snap_valid = False
+
+    def view(self, P: int):
+        return (self.bkeys.data_ptr(), self.bstart.data_ptr(), self.unum.data_ptr(),
+                self.ubase.data_ptr(), P)
+
+    def ptrs(self):
+        t = (self.cnt, self.bstart, self.ubase, self.unum, self.pj, self.luid, self.bkeys,
+             self.slots)
+        return [x.data_ptr() for x in t] + [self.snap.data_ptr() if self.snap is not None else 0,
+                                            self.ucount.data_ptr()]
+
+
+class DeviceSetup:
+    """PSEngine mixin: the N>1 GPU buffers (``_init_dist_gpu``) and the
+    collective agreement on a small int64 tensor (``_agree``)."""
+
+    # ------------------------------------------------------------ N>1 (GPU)
+    def _init_dist_gpu(self) -> None:
+        """Receive buffers and server-merge slots of the N>1 device path.
+        Every rank lays its buckets out as a call of ``max_keys`` keys (the
+        common layout the servers merge) and sends each destination its
+        per-bucket runs with the keys."""
+        N, cap, d, dev, h = self.world, self.max_keys, self.dim, self.device, _hip()
+        for dd in self.dedupers:
+            dd.lay_n = cap
+        self.Pd = h.bd_buckets(cap, N, self.dedupers[0].ndest) // N
+        self.sub = h.srv_sub_buckets(N)
+        self.Ps = self.Pd * self.sub
+        # sub > 1: every source groups its runs by the servers' sub-bucket
+        # and sends the offsets with them (the server reads exact ranges)
+        for dd in self.dedupers:
+            dd.split_for_servers(self.sub)
+        Psub = self.Pd * self.sub if self.sub > 1 else 0
+        # every rank's max_keys must agree (it fixes Pd)
+        mk = torch.tensor([cap, -cap], dtype=torch.int64, device=dev)
+        self._agree(mk)
+        if int(mk[0]) != cap or int(-mk[1]) != cap:
+            raise ValueError("PSEngine: max_keys differs across ranks (the N>1 bucket layout "
+                             "is a function of it)")
+        rows = N * cap
+        self.rvals = torch.zeros((rows, d), dtype=torch.float32, device=dev)
+        if self.xg:
+            # the receive buffers are the arena's mailboxes: keys + the bucket
+            # runs (bases, sizes) per source, rows back, gradients
+            Pd, xg = self.Pd, self.xg
+            xg.setup({"keys": (self.depth, [cap * 8, Pd * 4, Pd * 4] + ([Psub * 4] if Psub else [])),
+                      "vals": (self.depth, [cap * 4 * d]), "grads": (self.depth, [cap * 4 * d])})
+            self.rkeys = [xg.region("keys", 0, q, torch.int64) for q in range(self.depth)]
+            self.rmeta = [(xg.region("keys", 1, q, torch.int32),
+                           xg.region("keys", 2, q, torch.int32)) for q in range(self.depth)]
+            self.rsub = [xg.region("keys", 3, q, torch.int32) if Psub else None
+                         for q in range(self.depth)]
+            self.uvals = [xg.region("vals", 0, q, torch.float32, d) for q in range(self.depth)]
+            self.rgrads = [xg.region("grads", 0, q, torch.float32, d) for q in range(self.depth)]
+        else:
+            self.rkeys = [torch.empty(rows, dtype=torch.int64, device=dev)] * self.depth
+            meta = [torch.zeros(2 * N * self.Pd, dtype=torch.int32, device=dev)
+                    for _ in range(self.depth)]
+            self.rmeta = [(m[:N * self.Pd], m[N * self.Pd:]) for m in meta]
+            self.rsub = [torch.zeros(N * Psub, dtype=torch.int32, device=dev) if Psub else None
+                         for _ in range(self.depth)]
+            self.rgrads = [torch.empty((rows, d), dtype=torch.float32, device=dev)] * self.depth
+        self.srv = None
+        self.srv_ahead = os.environ.get("SS_SRV_AHEAD", "1") != "0"
+        if self.table is not None:
+            self.svals = torch.empty((rows, d), dtype=torch.float32, device=dev)
+            self.sgrad = torch.empty((rows, d), dtype=torch.float32, device=dev)
+            self.srv_err = torch.zeros(1, dtype=torch.int32, device=dev)
+            snap_ok = bool(getattr(self.table, "snapshot_ok", False))
+            self.srv = [_ServerSlot(rows, self.Ps, dev, snap_ok) for _ in range(self.depth)]
+        if self.xg:
+            D = self.depth
+            self.native.set_xgmi([[self.xg.arena_of(c, q) for c in ("keys", "vals", "grads")]
+                                  for q in range(D)],
+                                 [sum((list(self.xg.layout("keys", p, q))
+                                       for p in range(4 if Psub else 3)), []) for q in range(D)],
+                                 [list(self.xg.layout("vals", 0, q)) for q in range(D)],
+                                 [list(self.xg.layout("grads", 0, q)) for q in range(D)],
+                                 N, self.rank, self.Pd, self.sub, cap, d, self.xg.bpp,
+                                 self.xg.timeout_s)
+            # a closed transport frees its arenas: the engine forgets them first
+            self.xg._close_hooks.append(self.native.clear_xgmi)
+            for q in range(D):
+                if self.srv is not None:
+                    self.native.set_server_slot(q, self.srv[q].ptrs())
+            self._nodt = h.DevTable(0, 1, 16, 8, 1, 2)  # a rank without a shard
+            self._noop = h.OptParams()
+            self._noip = h.InitParams()
+
+    def _agree(self, t: torch.Tensor) -> None:
+        """min-all-reduce of a small int64 tensor over the data transport."""
+        if self.world == 1:
+            return
+        self.t.allreduce_(t, "min")
+        if self.gpu:
+            torch.cuda.current_stream(self.device).synchronize()
