@@ -120,6 +120,15 @@ class PipelinedWorker:
             return True
         if self._next is None:
             self.step()  # prime the lookahead pipeline eagerly
+        # N>1: a captured pull runs the keys wait and the server merge unless
+        # its round's route ran them (synchronous rounds, PSEngine.route,
+        # srv_ahead); the round routed last before the capture must have been
+        # routed the way the captured routes are, or the graph's first pull bakes in a second keys wait for
+        # its slot and every later replay waits for a round that never comes
+        # (word2vec, 4 xGMI ranks: calibrated pulled-ahead, then synchronous
+        # rounds, then the capture).  One eager step routes it in this mode.
+        if getattr(eng, "xg", None) is not None and not eng.last_route_matches():
+            self.step()
         torch.cuda.synchronize()
         self._gstep = torch.full((1,), self.step_idx, dtype=torch.int64, device=eng.device)
         saved = (self.step_idx, self._next, list(self._pulled), eng._next_slot, eng.rounds)

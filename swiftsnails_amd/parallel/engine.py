@@ -221,6 +221,14 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             if self.gpu and not self.shared_device:
                 self.pull_stream = torch.cuda.Stream(device=self.device)
 
+    def last_route_matches(self) -> bool:
+        """The last routed round ran the keys-in as a route issued now would
+        (N>1 xGMI: on the route stream for synchronous rounds with
+        SS_SRV_AHEAD, else in the pull); a hipGraph capture must start from
+        such a round (PipelinedWorker.enable_graph)."""
+        last = getattr(self, "_route_srv", None)
+        return last is None or last == (getattr(self, "srv_ahead", False) and not self.pull_ahead)
+
     @property
     def shared_device(self) -> bool:
         """Several ranks of this job run on this rank's GPU (one-GPU
@@ -309,6 +317,7 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                 # word2vec N>1 0.107 -> 0.117 ms/step)
                 tab = self.table is not None
                 ahead = self.srv_ahead and not self.pull_ahead
+                self._route_srv = ahead
                 self.native.route_end(slot, tag, rs.cuda_stream, dd.ukeys.data_ptr(),
                                       dd.ucount.data_ptr(), ub.data_ptr(), un.data_ptr(), us,
                                       ahead, tab, self.rkeys[slot].data_ptr(),

@@ -95,6 +95,7 @@ class DeviceSetup:
             self.rgrads = [torch.empty((rows, d), dtype=torch.float32, device=dev)] * self.depth
         self.srv = None
         self.srv_ahead = os.environ.get("SS_SRV_AHEAD", "1") != "0"
+        self._route_srv = None  # how the last route ran the keys-in (srv_ahead)
         if self.table is not None:
             self.svals = torch.empty((rows, d), dtype=torch.float32, device=dev)
             self.sgrad = torch.empty((rows, d), dtype=torch.float32, device=dev)

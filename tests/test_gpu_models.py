@@ -443,6 +443,33 @@ def _graph_worker(model, dev, **ek):
     return Word2VecWorker(eng, data), table
 
 
+def test_graph_capture_after_mode_switch_xgmi(dev, monkeypatch):
+    """N>1 path (a size-1 xGMI arena): pulled-ahead rounds, then synchronous
+    ones (the launcher calibration's last switch), then the hipGraph capture.
+    Synchronous rounds run the keys wait + server merge in their routes; the
+    capture must start from a round routed that way (enable_graph settles one
+    eager step), else every replay's first pull waits a second time on its
+    slot's keys and the job hangs (here: a mailbox timeout)."""
+    monkeypatch.setenv("SS_XGMI_TIMEOUT", "20")
+    monkeypatch.setenv("SS_PULL_AHEAD", "auto")
+    from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+    w, t = _graph_worker("w2v", dev, transport=XgmiTransport(0, 1, dev, None))
+    assert w.set_pull_ahead(True)
+    for _ in range(3):
+        w.step()
+    w.set_pull_ahead(False)
+    w.drain()
+    assert w.enable_graph()
+    assert w.engine.last_route_matches()
+    for _ in range(3 * w._gper):
+        w.step()
+    torch.cuda.synchronize()
+    w.engine.check()
+    t.check()
+    assert np.isfinite(w.mean_loss())
+
+
 def test_lr_slot32_matches_slot64(dev, monkeypatch):
     """One-GPU sparse LR with the pull storing 4-byte slot indices for the
     fused merge + AdaGrad update (default, shards under 2^31 slots) trains
