@@ -64,14 +64,20 @@ def main(argv=None):
     # us/step at batch 1024 where host launch work bounds the step
     ap.add_argument("--graph", default="off", choices=["auto", "on", "off"],
                     help="replay the step as hipGraphs (1 GPU; auto = on for N=1)")
-    # zero: the usual sparse-LR start (prefilled table, an insert is the key
-    # CAS alone); uniform: random (u - 0.5) * scale weights drawn per key on
-    # insert (measured ~2 % slower: every insert writes its row)
-    ap.add_argument("--init", default="zero", choices=["zero", "uniform"],
+    # uniform (default, BASELINE.json: random-init weights): (u - 0.5) * scale
+    # per key, drawn from a key-seeded hash when the key is inserted.  With
+    # claimed pulls (one GPU, region tables) a new key's row is written once,
+    # by the fused merge's [w | h | key] store, whatever the initialiser, so
+    # random init costs nothing over zero init; zero: the usual LR start
+    ap.add_argument("--init", default="uniform", choices=["zero", "uniform"],
                     help="weight initialiser of the table")
     ap.add_argument("--init-scale", type=float, default=0.01)
-    ap.add_argument("--cal-steps", type=int, default=6,
-                    help="N>1: timed steps per mode of the pull-ahead calibration (0: off)")
+    ap.add_argument("--cal-steps", type=int, default=10,
+                    help="N>1: timed steps per window and mode of the pull-ahead calibration "
+                         "(0: off); pulled-ahead rounds are kept only if they win by >= 3%% in "
+                         "every window")
+    ap.add_argument("--cal-windows", type=int, default=2,
+                    help="N>1: alternating (synchronous, pulled-ahead) calibration windows")
     ap.add_argument("--verbose", action="store_true")
     a = ap.parse_args(argv)
 
@@ -151,7 +157,8 @@ def main(argv=None):
         wd.beat(i)
     # N>1 (SS_PULL_AHEAD=auto): time synchronous vs pulled-ahead rounds on
     # the live world and keep the faster (untimed; reported as "calibration")
-    cal = worker.calibrate_pull_ahead(a.cal_steps) if a.cal_steps > 0 else {}
+    cal = (worker.calibrate_pull_ahead(a.cal_steps, a.cal_windows)
+           if a.cal_steps > 0 else {})
     # hipGraph replays of the whole step (captured here, outside the timed
     # region; the data generator then reads its step from a device counter)
     graphed = False

@@ -113,6 +113,12 @@ struct BdRecT<3> {
 
 __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs, uint32_t Pd) {
   const uint32_t d = rs.dest_of(key);
+  if (rs.rbits) {
+    // region tables: bucket floor(region * Pd / R) — every region inside ONE
+    // bucket (the bucket's pull owns its inserts, k_pull_claim_bk)
+    const uint64_t region = table_hash(key) >> (64 - rs.rbits);
+    return d * Pd + (uint32_t)((region * (uint64_t)Pd) >> rs.rbits);
+  }
   const uint32_t h = (uint32_t)(dedup_hash(key) >> 32);
   return d * Pd + __umulhi(h, Pd);
 }
@@ -646,7 +652,8 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     const int* __restrict__ slots32 = nullptr,
                                                     float* __restrict__ lacc = nullptr,
                                                     float* __restrict__ lacc_out = nullptr,
-                                                    int lacc_n = 0) {
+                                                    int lacc_n = 0,
+                                                    const uint64_t* __restrict__ bkeys = nullptr) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   // the step's loss accumulator (added by the forward, ordered before this
@@ -693,13 +700,24 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     // then one blind 8-byte store per key), or read from the row when no
     // snapshot is valid (N>1 servers with pull-ahead: a read-modify-write).
     // slots32: the pull stored 4-byte slot indices (tables under 2^31 slots)
+    // bkeys (claimed pulls, k_pull_claim_bk): the slot of a new key holds
+    // nothing yet — store the whole [w | h | key] slot in one 16-byte store
+    // (the key of a found key is rewritten unchanged), the bucket's unique
+    // keys read coalesced from the dedup's staging
     for (uint32_t l = threadIdx.x; l < nu; l += RT) {
       const long long slot = slots32 ? (long long)slots32[base + l] : slots[base + l];
       if (slot < 0) continue;
       float2 wh = snap ? snap[base + l] : *reinterpret_cast<const float2*>(slot_row(t, slot));
       float s2 = 0.f;
       opt_update(op, wh.x, wh.y, s2, acc[l]);
-      *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
+      if (bkeys) {
+        const uint64_t key = bkeys[p0 + l];
+        *reinterpret_cast<uint4*>(t.base + (uint64_t)slot * 16) =
+            make_uint4(__float_as_uint(wh.x), __float_as_uint(wh.y), (uint32_t)key,
+                       (uint32_t)(key >> 32));
+      } else {
+        *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
+      }
     }
     return;
   }
@@ -992,13 +1010,14 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
 }
 
 // ------------------------------------------------------------- launchers
-void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
-                     uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
-                     uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
-                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg, uint32_t* rec, uint8_t* usingle, int ndest,
-                     long long lay_n, int msub, uint32_t* usub) {
+int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
+                    uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
+                    uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
+                    float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
+                    unsigned long long* dbg, uint32_t* rec, uint8_t* usingle, int ndest,
+                    long long lay_n, int msub, uint32_t* usub) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
+  if (rs.rbits < 0 || rs.rbits > 20) throw_error("bdedup: region bits 0..20");
   if (msub < 1 || msub > kBdMaxSub || (msub > 1 && !usub))
     throw_error("bdedup: server sub-buckets 1..64 (and their offset table)");
   // lay_n (N>1 engines): the bucket layout is that of a call of lay_n keys
@@ -1009,7 +1028,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   const long long ln = lay_n > 0 ? lay_n : n;
   if (ln <= 0) {
     check_hip(hipMemsetAsync(ucount, 0, sizeof(unsigned long long) * rs.nranks, st), "ucount");
-    return;
+    return 0;
   }
   if (ucap < n) throw_error("bdedup: per-destination capacity must be >= n");
   if ((unsigned long long)rs.nranks * (unsigned long long)ucap >= 0x7FFFFFFFull)
@@ -1019,6 +1038,10 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
   if ((long long)L.Pd * bd_clamp_ndest(rs.nranks, ndest) > kBdMaxBuckets + kMaxSeg ||
       ln > bd_max_keys())
     throw_error("bdedup: too many keys per call (max ~45M)");
+  // region buckets (one rank): only when every bucket gets >= 4 regions, so
+  // the floor(region * Pd / R) split keeps buckets within ~25% of the target
+  // (a region's keys cannot be split over buckets); else dedup-hash buckets
+  if (rs.rbits && (rs.nranks != 1 || 4ll * L.Pd > (1ll << rs.rbits))) rs.rbits = 0;
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
   // workgroup sizes (256/512/1024): count (SS_BD_CNT), column scan
@@ -1105,6 +1128,7 @@ void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long 
     hipLaunchKernelGGL(k_bd_inv, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, ix, n, inv);
     check_launch("k_bd_inv");
   }
+  return rs.rbits;  // the region bits the buckets follow (0: dedup-hash buckets)
 }
 
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,
@@ -1131,7 +1155,7 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
                       float* ugrad, hipStream_t st, int osi, const uint8_t* usingle,
                       const DevTable* t, const long long* slots, const float* snap,
                       const OptParams* op, int ndest, int slot32, float* lacc, float* lacc_out,
-                      int lacc_n) {
+                      int lacc_n, const uint64_t* bkeys) {
   if (n <= 0) return;
   if (lacc && (!lacc_out || lacc_n <= 0)) throw_error("bd_reduce: loss hand-off needs its output");
   if (F < 1) throw_error("bd_reduce: F must be >= 1");
@@ -1147,6 +1171,8 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
     tv = *t;
     opv = *op;
   }
+  if (bkeys && (!(slots || s32) || !snap || t->stride != 16 || t->key_off != 8 || t->row_off != 0))
+    throw_error("bd_reduce: slot stores with keys need a snapshot merge into 16-byte [w|h|key] slots");
   const float2* sn = reinterpret_cast<const float2*>(snap);
   const BdLayout L = bd_layout(n, nranks, ndest);
   const uint32_t* S = scratch;
@@ -1158,15 +1184,15 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
                        S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32, lacc, lacc_out, lacc_n);
+                       SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
   else if (rt == 512)
     hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
                        S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32, lacc, lacc_out, lacc_n);
+                       SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
   else
     hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
                      S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32, lacc, lacc_out, lacc_n);
+                       SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
   check_launch("k_bd_reduce");
 }
 

@@ -67,16 +67,21 @@ PYBIND11_MODULE(_ss_hip, m) {
   py::class_<DevTable>(m, "DevTable", py::module_local())
       .def(py::init([](uintptr_t base, unsigned long long cap, uint32_t stride, uint32_t key_off,
                        uint32_t dim, uint32_t width, uint32_t prefilled, uint32_t row_off,
-                       uint32_t bf16) {
+                       uint32_t bf16, uint32_t rbits) {
              const uint32_t eb = bf16 ? 2u : 4u;
              if (row_off + eb * width > stride || (key_off < row_off + eb * width && key_off + 8 > row_off))
                throw std::invalid_argument("DevTable: row and key overlap inside the slot");
+             // region tables: 2^rbits equal regions of >= 64 slots
+             if (rbits > 20 || (rbits && (cap % (1ull << rbits) != 0 || (cap >> rbits) < 64)))
+               throw std::invalid_argument("DevTable: rbits needs cap = rlen * 2^rbits, rlen >= 64");
              return DevTable{P<char>(base), cap, stride, key_off, dim, width, prefilled, row_off,
-                             bf16};
+                             bf16, rbits, rbits ? (cap >> rbits) : cap};
            }),
            py::arg("base"), py::arg("cap"), py::arg("stride"), py::arg("key_off"), py::arg("dim"),
            py::arg("width"), py::arg("prefilled") = 0, py::arg("row_off") = 0,
-           py::arg("bf16") = 0)
+           py::arg("bf16") = 0, py::arg("rbits") = 0)
+      .def_readonly("rbits", &DevTable::rbits)
+      .def_readonly("rlen", &DevTable::rlen)
       .def_readonly("bf16", &DevTable::bf16)
       .def_readonly("row_off", &DevTable::row_off)
       .def_readonly("prefilled", &DevTable::prefilled)
@@ -141,6 +146,22 @@ PYBIND11_MODULE(_ss_hip, m) {
   }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
      py::arg("P"), py::arg("slots"), py::arg("out"), py::arg("ip"), py::arg("size_ctr"),
      py::arg("err"), py::arg("G"), py::arg("st"), py::arg("snap") = 0, py::arg("slot32") = 0);
+  m.def("pull_claim_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
+                            uintptr_t ubase, int P_, uintptr_t slots32, uintptr_t out,
+                            uintptr_t snap, const InitParams& ip, uintptr_t size_ctr,
+                            uintptr_t err, uintptr_t st) {
+    launch_pull_claim_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
+                         P<const uint32_t>(unum), P<const uint32_t>(ubase), P_, P<int>(slots32),
+                         P<float>(out), P<float>(snap), ip, P<unsigned long long>(size_ctr),
+                         P<int>(err), S(st));
+  });
+  m.def("commit_claims", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
+                            uintptr_t ubase, int P_, uintptr_t slots32, uintptr_t snap,
+                            uintptr_t st) {
+    launch_commit_claims(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
+                         P<const uint32_t>(unum), P<const uint32_t>(ubase), P_,
+                         P<const int>(slots32), P<const float>(snap), S(st));
+  });
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
                     long long max_n, const OptParams& op, int G, uintptr_t st, uintptr_t snap) {
     launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st),
@@ -187,35 +208,37 @@ PYBIND11_MODULE(_ss_hip, m) {
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
                        uintptr_t st, uintptr_t dbg, uintptr_t rec, uintptr_t usingle,
-                       int ndest, long long lay_n, int msub, uintptr_t usub) {
-    RouteSpec rs{P<const int>(frag_map), frag_num, nranks};
-    launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch), P<uint32_t>(pj),
-                    P<uint32_t>(pos_of), P<uint32_t>(bkt), P<uint32_t>(luid), P<uint64_t>(bkeys),
-                    P<unsigned long long>(ucount), P<uint64_t>(ukeys), P<float>(ugrad), gdim,
-                    P<uint32_t>(inv), place, S(st), P<unsigned long long>(dbg),
-                    P<uint32_t>(rec), P<uint8_t>(usingle), ndest, lay_n, msub,
-                    P<uint32_t>(usub));
+                       int ndest, long long lay_n, int msub, uintptr_t usub, int rbits) {
+    RouteSpec rs{P<const int>(frag_map), frag_num, nranks, rbits};
+    return launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch),
+                           P<uint32_t>(pj), P<uint32_t>(pos_of), P<uint32_t>(bkt),
+                           P<uint32_t>(luid), P<uint64_t>(bkeys), P<unsigned long long>(ucount),
+                           P<uint64_t>(ukeys), P<float>(ugrad), gdim, P<uint32_t>(inv), place,
+                           S(st), P<unsigned long long>(dbg), P<uint32_t>(rec),
+                           P<uint8_t>(usingle), ndest, lay_n, msub, P<uint32_t>(usub));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
      py::arg("rec") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0,
-     py::arg("lay_n") = 0, py::arg("msub") = 1, py::arg("usub") = 0);
+     py::arg("lay_n") = 0, py::arg("msub") = 1, py::arg("usub") = 0, py::arg("rbits") = 0);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
                         uintptr_t snap, std::optional<OptParams> op, int ndest, int slot32,
-                        uintptr_t acc, uintptr_t acc_out, int acc_n) {
+                        uintptr_t acc, uintptr_t acc_out, int acc_n, uintptr_t bkeys) {
     launch_bd_reduce(n, nranks, P<const uint32_t>(scratch), P<const uint32_t>(pj),
                      P<const uint32_t>(luid), P<const float>(gs), P<const float>(xval), F,
                      P<float>(ugrad), S(st), osi, P<const uint8_t>(usingle),
                      t ? &*t : nullptr, P<const long long>(slots), P<const float>(snap),
-                     op ? &*op : nullptr, ndest, slot32, P<float>(acc), P<float>(acc_out), acc_n);
+                     op ? &*op : nullptr, ndest, slot32, P<float>(acc), P<float>(acc_out), acc_n,
+                     P<const uint64_t>(bkeys));
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("pj"), py::arg("luid"),
      py::arg("gs"), py::arg("xval"), py::arg("F"), py::arg("ugrad"), py::arg("st"),
      py::arg("osi") = 0, py::arg("usingle") = 0, py::arg("t") = py::none(), py::arg("slots") = 0,
      py::arg("snap") = 0, py::arg("op") = py::none(), py::arg("ndest") = 0,
-     py::arg("slot32") = 0, py::arg("acc") = 0, py::arg("acc_out") = 0, py::arg("acc_n") = 0);
+     py::arg("slot32") = 0, py::arg("acc") = 0, py::arg("acc_out") = 0, py::arg("acc_n") = 0,
+     py::arg("bkeys") = 0);
   m.def("bd_unplace", [](long long n, int nranks, uintptr_t scratch, uintptr_t src, uintptr_t dst,
                          int dim, uintptr_t st, int ndest) {
     launch_bd_unplace(n, nranks, P<const uint32_t>(scratch), P<const float>(src), P<float>(dst),

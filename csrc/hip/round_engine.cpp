@@ -204,14 +204,22 @@ class RoundEngine {
   void pull_fast(int slot, int tag, uintptr_t stream, bool wait_route, int prev, bool ahead,
                  const DevTable& t, const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
                  std::vector<uintptr_t> view, int P, uintptr_t uvals, uintptr_t slots,
-                 uintptr_t snap, int slot32) {
+                 uintptr_t snap, int slot32, bool claim) {
     pull_waits(slot, tag, stream, wait_route, prev);
     if (view.size() != 4) throw std::invalid_argument("pull_fast: (bkeys, bstart, unum, ubase)");
-    launch_pull_unique_bk(t, Pt<const uint64_t>(view[0]), Pt<const uint32_t>(view[1]),
-                          Pt<const uint32_t>(view[2]), Pt<const uint32_t>(view[3]), P,
-                          Pt<long long>(slots), Pt<float>(uvals), ip,
-                          Pt<unsigned long long>(size_ctr), Pt<int>(err), G, St(stream),
-                          Pt<float>(snap), slot32);
+    // claim: region-aligned buckets of a region table — LDS-claimed inserts,
+    // the fused merge stores the slots (k_pull_claim_bk)
+    if (claim)
+      launch_pull_claim_bk(t, Pt<const uint64_t>(view[0]), Pt<const uint32_t>(view[1]),
+                           Pt<const uint32_t>(view[2]), Pt<const uint32_t>(view[3]), P,
+                           Pt<int>(slots), Pt<float>(uvals), Pt<float>(snap), ip,
+                           Pt<unsigned long long>(size_ctr), Pt<int>(err), St(stream));
+    else
+      launch_pull_unique_bk(t, Pt<const uint64_t>(view[0]), Pt<const uint32_t>(view[1]),
+                            Pt<const uint32_t>(view[2]), Pt<const uint32_t>(view[3]), P,
+                            Pt<long long>(slots), Pt<float>(uvals), ip,
+                            Pt<unsigned long long>(size_ctr), Pt<int>(err), G, St(stream),
+                            Pt<float>(snap), slot32);
     if (ahead) record(kPull, slot, stream, tag);
   }
 

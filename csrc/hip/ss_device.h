@@ -14,6 +14,15 @@
 //     initialises the row. Readers of a freshly inserted row are always in a
 //     later kernel (stream order = the happens-before edge), so no per-slot
 //     ready flag or spin is needed.
+//   * region tables (rbits > 0, scalar LR shards): the slots form R = 2^rbits
+//     equal regions and a key probes only inside the region of its hash's top
+//     rbits bits (home slot, then linear, wrapping at the region's end).  The
+//     1-GPU dedup buckets whole regions (bd_bucket with RouteSpec.rbits), so
+//     ONE workgroup owns every insert into a region during a pull: it claims
+//     empty slots in LDS instead of with a device-scope CAS, and the fused
+//     merge + update stores [w | h | key] in one 16-byte store (table.hip
+//     k_pull_claim_bk, bdedup.hip k_bd_reduce) — no atomic, no second write
+//     to the claimed line.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
@@ -53,7 +62,35 @@ struct DevTable {
   // the bytes per slot: capacity for the 10B-key FM table), math in fp32;
   // read / written through row_ld / row_st
   uint32_t bf16;
+  // region tables: log2 of the region count (0: one region, the whole
+  // table) and slots per region (cap = rlen << rbits)
+  uint32_t rbits;
+  uint64_t rlen;
 };
+
+// The probe sequence of a key: home slot fastrange(table_hash, cap), then
+// linear inside [lo, hi) — the key's region (the whole table when rbits is
+// 0).  fastrange keeps the home inside the region of the hash's top bits:
+// floor(floor(h * cap / 2^64) / rlen) == floor(h * 2^rbits / 2^64) for
+// cap == rlen * 2^rbits.
+struct ProbeSeq {
+  uint64_t s, lo, hi;
+  __device__ __forceinline__ void next() { s = (s + 1 == hi) ? lo : s + 1; }
+  __device__ __forceinline__ uint64_t len() const { return hi - lo; }
+};
+__device__ __forceinline__ ProbeSeq probe_seq(const DevTable& t, uint64_t key) {
+  const uint64_t h = table_hash(key);
+  ProbeSeq p;
+  p.s = fastrange64(h, t.cap);
+  if (t.rbits) {
+    p.lo = (h >> (64 - t.rbits)) * t.rlen;
+    p.hi = p.lo + t.rlen;
+  } else {
+    p.lo = 0;
+    p.hi = t.cap;
+  }
+  return p;
+}
 
 __device__ __forceinline__ uint64_t* slot_key(const DevTable& t, uint64_t s) {
   return reinterpret_cast<uint64_t*>(t.base + s * (uint64_t)t.stride + t.key_off);

@@ -34,6 +34,17 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
                            float* out, const InitParams& ip, unsigned long long* size_ctr,
                            int* err, int G, hipStream_t st, float* snap = nullptr,
                            int slot32 = 0);
+// region tables, region-aligned buckets (launch_bd_dedup returned rbits):
+// one workgroup per bucket claims new keys' slots in LDS (no device atomic,
+// nothing written to the table); the fused merge stores [w | h | key]
+// (launch_bd_reduce with bkeys) or launch_commit_claims writes them
+void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                          const uint32_t* unum, const uint32_t* ubase, int P, int* slots32,
+                          float* out, float* snap, const InitParams& ip,
+                          unsigned long long* size_ctr, int* err, hipStream_t st);
+void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                          const uint32_t* unum, const uint32_t* ubase, int P, const int* slots32,
+                          const float* snap, hipStream_t st);
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
                   const float* snap = nullptr);
@@ -48,6 +59,10 @@ struct RouteSpec {
   const int* frag_map;  // frag -> destination rank (device)
   int frag_num;
   int nranks;
+  // > 0: the bucketed dedup buckets whole regions of a region table with
+  // 2^rbits regions (ss_device.h), so a bucket's pull owns its regions'
+  // inserts (k_pull_claim_bk); 0: buckets by dedup_hash
+  int rbits = 0;
   // fragment of a key = fmix64(key) % frag_num (reference hashfrag.h:48-53);
   // a 64-bit modulo is a long software sequence on the GPU, so power-of-two
   // fragment counts (the default 1024) take the mask instead — same result
@@ -147,20 +162,23 @@ long long bd_scratch_words(long long n, int nranks, int ndest = 0);
 long long bd_ubase_offset(long long n, int nranks, int ndest = 0);
 std::vector<long long> bd_offsets(long long n, int nranks, int ndest = 0);
 int bd_buckets(long long n, int nranks, int ndest = 0);
-void launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
-                     uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
-                     uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
-                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
-                     unsigned long long* dbg = nullptr, uint32_t* rec = nullptr,
-                     uint8_t* usingle = nullptr, int ndest = 0, long long lay_n = 0,
-                     int msub = 1, uint32_t* usub = nullptr);
+// returns the region bits the call's buckets follow (rs.rbits if the layout
+// allows region buckets — one rank, >= 4 regions per bucket — else 0)
+int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
+                    uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
+                    uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
+                    float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
+                    unsigned long long* dbg = nullptr, uint32_t* rec = nullptr,
+                    uint8_t* usingle = nullptr, int ndest = 0, long long lay_n = 0,
+                    int msub = 1, uint32_t* usub = nullptr);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi = 0,
                       const uint8_t* usingle = nullptr, const DevTable* t = nullptr,
                       const long long* slots = nullptr, const float* snap = nullptr,
                       const OptParams* op = nullptr, int ndest = 0, int slot32 = 0,
-                      float* lacc = nullptr, float* lacc_out = nullptr, int lacc_n = 0);
+                      float* lacc = nullptr, float* lacc_out = nullptr, int lacc_n = 0,
+                      const uint64_t* bkeys = nullptr);
 // occ[p] = uvals[uid of occurrence position p] (scalar rows; 0 where none):
 // one workgroup per dedup bucket, for the LR forward's one-gather mode
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,

@@ -30,8 +30,9 @@ static constexpr int kApplyRegs = 4;  // row coordinates per lane held in regist
 
 __device__ __forceinline__ long long probe_slot(const DevTable& t, uint64_t key, bool insert,
                                                 bool* inserted) {
-  uint64_t s = fastrange64(table_hash(key), t.cap);
-  for (uint64_t n = 0; n < t.cap; ++n) {
+  ProbeSeq ps = probe_seq(t, key);
+  for (uint64_t n = 0, len = ps.len(); n < len; ++n, ps.next()) {
+    const uint64_t s = ps.s;
     uint64_t* kp = slot_key(t, s);
     // A slot's key only ever changes EMPTY -> key inside a launch, so a stale
     // plain load can only read EMPTY; the CAS below then returns the truth.
@@ -47,7 +48,6 @@ __device__ __forceinline__ long long probe_slot(const DevTable& t, uint64_t key,
       }
       if (prev == key) return (long long)s;
     }
-    s = (s + 1 == t.cap) ? 0 : s + 1;
   }
   return -1;
 }
@@ -144,8 +144,9 @@ __device__ __forceinline__ float fresh_or(float v, const InitParams& ip, uint64_
 // claimed an EMPTY slot (the row then is the prefilled / initial row).
 __device__ __forceinline__ long long probe_slot16(const DevTable& t, uint64_t key, float2* wh,
                                                   bool* inserted) {
-  uint64_t s = fastrange64(table_hash(key), t.cap);
-  for (uint64_t n = 0; n < t.cap; ++n) {
+  ProbeSeq ps = probe_seq(t, key);
+  for (uint64_t n = 0, len = ps.len(); n < len; ++n, ps.next()) {
+    const uint64_t s = ps.s;
     const uint4 v = *reinterpret_cast<const uint4*>(t.base + s * 16);
     const uint64_t k = ((uint64_t)v.w << 32) | v.z;
     if (k == key) {
@@ -165,7 +166,6 @@ __device__ __forceinline__ long long probe_slot16(const DevTable& t, uint64_t ke
         return (long long)s;
       }
     }
-    s = (s + 1 == t.cap) ? 0 : s + 1;
   }
   return -1;
 }
@@ -308,6 +308,112 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
 }
 
 
+// K3 of the one-GPU headline on a REGION table (ss_device.h): one workgroup
+// per region-aligned dedup bucket, so the workgroup is the only inserter
+// into its regions during this launch.  A key is probed with 16-byte
+// [w | h | key] loads; an EMPTY slot is claimed in an LDS set of slot
+// indices instead of with a device-scope CAS (those run at the memory side:
+// 3.3M new keys per bench step cost more than the probes), and NOTHING is
+// written to the table: the pull returns the initial (w, h) of a new key as
+// its snapshot, and the fused merge + AdaGrad update stores the whole slot
+// [w | h | key] with one 16-byte store (k_bd_reduce with bkeys) — which also
+// makes a random initialiser free (the row is written once either way).
+// Until that store a claimed slot still reads EMPTY: every consumer of the
+// table is stream-ordered after it (PSEngine defers only synchronous
+// one-GPU rounds; launch_commit_claims is the fallback writer).
+static constexpr int kClaimT = 1024;  // threads per bucket workgroup
+static constexpr int kClaimTS = 8192;  // LDS claim slots (>= 2x the <= 4096 keys of a bucket)
+__device__ __forceinline__ bool lds_claim(uint32_t* cl, uint32_t s) {
+  uint32_t i = (s * 0x9E3779B1u) >> (32 - 13);  // 13 = log2(kClaimTS)
+  for (int k = 0; k < kClaimTS; ++k) {
+    const uint32_t v = cl[i];
+    if (v == s) return false;
+    if (v == 0xFFFFFFFFu) {
+      const uint32_t prev = atomicCAS(&cl[i], 0xFFFFFFFFu, s);
+      if (prev == 0xFFFFFFFFu) return true;
+      if (prev == s) return false;
+    }
+    i = (i + 1) & (kClaimTS - 1);
+  }
+  return false;  // unreachable: at most 4096 claims per workgroup
+}
+static_assert(kClaimTS == 1 << 13, "lds_claim hashes to 13 bits");
+
+__global__ __launch_bounds__(kClaimT) void k_pull_claim_bk(
+    DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
+    const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
+    int* __restrict__ slots32, float* __restrict__ out, float2* __restrict__ snap, InitParams ip,
+    unsigned long long* size_ctr, int* err) {
+  __shared__ uint32_t cl[kClaimTS];
+  for (int i = threadIdx.x; i < kClaimTS; i += kClaimT) cl[i] = 0xFFFFFFFFu;
+  __syncthreads();
+  const int b = blockIdx.x;
+  const uint32_t nu = unum[b], base = ubase[b];
+  const uint64_t* src = bkeys + bstart[b];
+  unsigned long long ins = 0;
+  for (uint32_t l = threadIdx.x; l < nu; l += kClaimT) {
+    const uint64_t key = src[l];
+    long long slot = -1;
+    bool inserted = false;
+    float2 wh = make_float2(0.f, 0.f);
+    if (key != kEmptyKey) {
+      ProbeSeq ps = probe_seq(t, key);
+      for (uint64_t n = 0, len = ps.len(); n < len; ++n, ps.next()) {
+        const uint4 v = *reinterpret_cast<const uint4*>(t.base + ps.s * 16);
+        const uint64_t k = ((uint64_t)v.w << 32) | v.z;
+        if (k == key) {
+          slot = (long long)ps.s;
+          wh = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
+          break;
+        }
+        if (k == kEmptyKey && lds_claim(cl, (uint32_t)ps.s)) {
+          slot = (long long)ps.s;
+          inserted = true;
+          break;
+        }
+      }
+    }
+    if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);  // 1: the key's region is full
+    const long long pos = (long long)base + l;
+    slots32[pos] = (int)slot;
+    if (inserted) {
+      wh = make_float2(init_value(ip, key, 0, 1), ip.state_init);
+    } else if (slot >= 0) {
+      // a row written by an older CAS-path insert of a non-prefilled table
+      wh.x = fresh_or(wh.x, ip, key, 0, 1);
+      if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
+    }
+    out[pos] = wh.x;
+    snap[pos] = wh;
+    ins += inserted;
+  }
+  ins = wave_sum_u64(ins);
+  if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
+}
+
+// The fallback writer of a claimed pull whose fused merge did not run (a
+// snapshot invalidated between pull and push): every claimed slot still
+// EMPTY gets its key and the snapshot's (initial) row.
+__global__ __launch_bounds__(256) void k_commit_claims(
+    DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
+    const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
+    const int* __restrict__ slots32, const float2* __restrict__ snap) {
+  const int b = blockIdx.x;
+  const uint32_t nu = unum[b], base = ubase[b];
+  const uint64_t* src = bkeys + bstart[b];
+  for (uint32_t l = threadIdx.x; l < nu; l += 256) {
+    const int s = slots32[base + l];
+    if (s < 0) continue;
+    const uint64_t key = src[l];
+    if (*slot_key(t, (uint64_t)s) != kEmptyKey) continue;
+    const float2 wh = snap[base + l];
+    *reinterpret_cast<uint4*>(t.base + (uint64_t)s * 16) =
+        make_uint4(__float_as_uint(wh.x), __float_as_uint(wh.y), (uint32_t)key,
+                   (uint32_t)(key >> 32));
+  }
+}
+
+
 // k_pull_unique_bk for wide fp32 rows (word2vec, D = 32 / 64 / 128): 8 lanes
 // per key, each moving D/32 16-byte vectors of the row (a D = 128 row is 32
 // float4s: 8 lanes x 4), so a wave has 8 keys' probe -> row chains in flight
@@ -405,8 +511,9 @@ __global__ __launch_bounds__(256) void k_pull_narrow_bk(DevTable t, const uint64
     bool inserted = false;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (act && key != kEmptyKey) {
-      uint64_t s = fastrange64(table_hash(key), t.cap);
-      for (uint64_t n = 0; n < t.cap; ++n) {  // group-uniform trip count
+      ProbeSeq ps = probe_seq(t, key);
+      for (uint64_t n = 0, len = ps.len(); n < len; ++n, ps.next()) {  // group-uniform trip count
+        const uint64_t s = ps.s;
         v = *reinterpret_cast<const uint4*>(t.base + s * (uint64_t)t.stride + 16 * lg);
         const uint64_t k = ((uint64_t)__shfl(v.y, 0, kPnL) << 32) | __shfl(v.x, 0, kPnL);
         if (k == key) {
@@ -424,7 +531,6 @@ __global__ __launch_bounds__(256) void k_pull_narrow_bk(DevTable t, const uint64
             break;
           }
         }
-        s = (s + 1 == t.cap) ? 0 : s + 1;
       }
     }
     if (!act) continue;
@@ -704,8 +810,9 @@ __global__ __launch_bounds__(256) void k_probe_hist(DevTable t, unsigned long lo
        s += stride) {
     const uint64_t key = *slot_key(t, s);
     if (key == kEmptyKey) continue;
-    const uint64_t home = fastrange64(table_hash(key), t.cap);
-    const uint64_t d = s >= home ? s - home : s + t.cap - home;
+    const ProbeSeq ps = probe_seq(t, key);  // home slot and the key's region
+    const uint64_t home = ps.s;
+    const uint64_t d = s >= home ? s - home : s + ps.len() - home;
     atomicAdd(&h[d < (uint64_t)nbins - 1 ? (int)d : nbins - 1], 1u);
   }
   __syncthreads();
@@ -835,6 +942,35 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
                                       bkeys, bstart, unum, ubase, slots, out, ip, size_ctr, err,
                                       reinterpret_cast<float2*>(snap), one16));
   check_launch("k_pull_unique_bk");
+}
+
+static void check_claim_table(const DevTable& t) {
+  if (!t.rbits || t.bf16 || t.stride != 16 || t.key_off != 8 || t.row_off != 0 || t.dim != 1 ||
+      t.width != 2 || t.cap >= (1ull << 31))
+    throw std::invalid_argument(
+        "claimed pulls: a region table of 16-byte [w|h|key] slots under 2^31 slots");
+}
+
+void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                          const uint32_t* unum, const uint32_t* ubase, int P, int* slots32,
+                          float* out, float* snap, const InitParams& ip,
+                          unsigned long long* size_ctr, int* err, hipStream_t st) {
+  if (P <= 0) return;
+  check_claim_table(t);
+  if (!slots32 || !out || !snap) throw std::invalid_argument("claimed pull: slots, rows, snapshot");
+  hipLaunchKernelGGL(k_pull_claim_bk, dim3(P), dim3(kClaimT), 0, st, t, bkeys, bstart, unum, ubase,
+                     slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err);
+  check_launch("k_pull_claim_bk");
+}
+
+void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                          const uint32_t* unum, const uint32_t* ubase, int P, const int* slots32,
+                          const float* snap, hipStream_t st) {
+  if (P <= 0) return;
+  check_claim_table(t);
+  hipLaunchKernelGGL(k_commit_claims, dim3(P), dim3(256), 0, st, t, bkeys, bstart, unum, ubase,
+                     slots32, reinterpret_cast<const float2*>(snap));
+  check_launch("k_commit_claims");
 }
 
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,

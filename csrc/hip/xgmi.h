@@ -173,6 +173,16 @@ class XgmiArena {
   long long bytes() const { return bytes_; }
   uintptr_t err_ptr() const { return reinterpret_cast<uintptr_t>(local_ + kXErrOff); }
   unsigned host_err() const { return *host_err_; }
+  // clear the sticky device and host-mapped error words (between start-up
+  // litmus tiers: a failed tier's bits must not fail the next one).  Waits
+  // for the device first, so no wait kernel of the earlier tier still writes.
+  void reset_err() {
+    check_hip(hipSetDevice(device_), "hipSetDevice");
+    check_hip(hipDeviceSynchronize(), "xgmi reset_err (sync)");
+    check_hip(hipMemset(local_ + kXErrOff, 0, sizeof(unsigned long long)), "xgmi reset_err");
+    check_hip(hipDeviceSynchronize(), "xgmi reset_err (sync)");
+    *host_err_ = 0u;
+  }
   int tier() const { return tier_; }
   // tier (XTier), the destinations a fenced put releases to (bit d: rank d's
   // arena is on another device), round-tag verification

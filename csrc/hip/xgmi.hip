@@ -355,6 +355,7 @@ void bind_xgmi(py::module_& m) {
       .def_property_readonly("err_ptr", &XgmiArena::err_ptr)
       .def_property_readonly("tier", &XgmiArena::tier)
       .def("host_err", &XgmiArena::host_err)
+      .def("reset_err", &XgmiArena::reset_err)
       .def("set_tier", &XgmiArena::set_tier, py::arg("tier"), py::arg("remote"),
            py::arg("verify"))
       .def("put", &XgmiArena::put, py::arg("ch"), py::arg("parts"), py::arg("bpp"),

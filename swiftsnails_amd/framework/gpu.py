@@ -311,8 +311,10 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     # rounds runs faster on this world (synthetic data only: the calibration
     # steps consume batches)
     cal = {}
-    if passes is None and warmup > 0 and int(cfg.get("calibrate_steps", 6) or 0) > 0 and w.active:
-        cal = w.calibrate_pull_ahead(int(cfg.get("calibrate_steps", 6)))
+    # a collective (rounds, barriers, an all-reduce): every rank calls it,
+    # pure servers too (they step with empty key sets)
+    if passes is None and warmup > 0 and int(cfg.get("calibrate_steps", 10) or 0) > 0:
+        cal = w.calibrate_pull_ahead(int(cfg.get("calibrate_steps", 10)))
     # config `graph: 1`: replay the step as hipGraphs (1 GPU, synthetic data;
     # a no-op where unsupported — see PipelinedWorker.enable_graph)
     graphed = str(cfg.get("graph", "0")) not in ("0", "false", "") and w.enable_graph()

@@ -118,6 +118,10 @@ class PipelinedWorker:
             return False
         if self._graphs is not None:
             return True
+        # a pipeline switched to synchronous rounds but not drained still
+        # holds pulled-ahead rounds: a capture would record drain steps, not
+        # the periodic synchronous step
+        self.drain()
         if self._next is None:
             self.step()  # prime the lookahead pipeline eagerly
         # N>1: a captured pull runs the keys wait and the server merge unless
@@ -207,10 +211,14 @@ class PipelinedWorker:
         r = self._next if self._next is not None else self._route(self.step_idx)
         self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
         rnd = self.engine.pull(r)
-        self._zero_acc()
         if self.has_data(self.step_idx):
+            self._zero_acc()
             with self.engine.trace("compute"):
                 self._compute(rnd, r.slot, self.engine.raw_stream())
+        else:
+            # no compute: a model whose merge kernel moves the loss (sparse
+            # LR, word2vec) would otherwise report the previous step's loss
+            self.loss_sum.zero_()
         self.engine.push(rnd)
         self.step_idx += 1
         return self.loss_sum
@@ -232,10 +240,12 @@ class PipelinedWorker:
             self._next = self._route(self.step_idx + L)
         rnd = self._pulled.popleft()
         eng.begin(rnd)
-        self._zero_acc()
         if self.has_data(self.step_idx):
+            self._zero_acc()
             with eng.trace("compute"):
                 self._compute(rnd, rnd.slot, eng.raw_stream())
+        else:
+            self.loss_sum.zero_()
         # round i+L's pull is enqueued before round i's push: with one comm
         # stream (RCCL, SS_RCCL_COMMS=1) its exchanges then go ahead of round
         # i's gradients instead of waiting behind round i's compute.  (Issuing
@@ -265,44 +275,62 @@ class PipelinedWorker:
         while self._pulled and not self.engine.pull_ahead:
             self.step()
 
-    def calibrate_pull_ahead(self, steps: int = 6) -> dict:
-        """SS_PULL_AHEAD=auto at N>1: time ``steps`` synchronous and ``steps``
-        pulled-ahead steps on the live world (max over ranks) and keep the
-        faster mode.  On one GPU shared by all ranks there is no cross-device
-        wait to hide and the synchronous snapshot update wins; across real
-        xGMI links the keys -> rows chain of the next round can hide behind
-        this round's compute.  Returns the choice and both timings (ms per
-        step), {} where it does not apply (one-GPU path, host-count
-        transports without a pull stream, SS_PULL_AHEAD=0/1, SS_STALENESS=0)."""
+    def calibrate_pull_ahead(self, steps: int = 10, windows: int = 2,
+                             margin: float = 0.03) -> dict:
+        """SS_PULL_AHEAD=auto at N>1: time synchronous and pulled-ahead steps
+        on the live world and keep pulled-ahead rounds only if they win
+        clearly.  ``windows`` alternating (synchronous, pulled-ahead) windows
+        of ``steps`` timed steps each (max over ranks); pulled-ahead rounds are
+        chosen only if they beat the synchronous window next to them by at
+        least ``margin`` in EVERY window, else rounds stay synchronous (no
+        staleness).  A single short window let box noise flip the choice (the
+        two modes overlap within a few percent on one GPU), which changes both
+        the speed and the staleness semantics of a run.  On one GPU shared by
+        all ranks there is no cross-device wait to hide and the synchronous
+        snapshot update wins; across real xGMI links the keys -> rows chain of
+        the next round can hide behind this round's compute.  Returns the
+        choice, the per-window timings (ms per step, slowest rank) and the
+        per-window spread over ranks, {} where it does not apply (one-GPU path,
+        host-count transports without a pull stream, SS_PULL_AHEAD=0/1,
+        SS_STALENESS=0).  A collective: every rank calls it."""
         eng = self.engine
         if not (getattr(eng, "gpu", False) and getattr(eng, "dist", False) and eng.depth >= 3
                 and os.environ.get("SS_PULL_AHEAD", "auto") == "auto"
                 and getattr(eng, "lookahead", 1) > 0 and self._graphs is None
                 and os.environ.get("SS_STALENESS", "1") != "0"):
             return {}
-        times = {}
-        for mode in (False, True):
-            self.set_pull_ahead(mode)
-            self.drain()
-            for _ in range(2):  # settle: the (re)started pipeline
-                self.step()
-            torch.cuda.synchronize(eng.device)
-            eng.barrier()
-            t0 = time.perf_counter()
-            for _ in range(steps):
-                self.step()
-            torch.cuda.synchronize(eng.device)
-            eng.barrier()
-            times[mode] = eng.max_over_ranks(time.perf_counter() - t0) / steps
-        best = times[True] < times[False]
+        steps, windows = max(1, int(steps)), max(1, int(windows))
+        times = {False: [], True: []}
+        spread = {False: [], True: []}
+        for _ in range(windows):
+            for mode in (False, True):
+                self.set_pull_ahead(mode)
+                self.drain()
+                for _ in range(2):  # settle: the (re)started pipeline
+                    self.step()
+                torch.cuda.synchronize(eng.device)
+                eng.barrier()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    self.step()
+                torch.cuda.synchronize(eng.device)
+                el = time.perf_counter() - t0
+                eng.barrier()
+                hi = eng.max_over_ranks(el) / steps
+                lo = -eng.max_over_ranks(-el) / steps
+                times[mode].append(hi)
+                spread[mode].append(hi - lo)
+        best = all(a <= (1.0 - margin) * s for s, a in zip(times[False], times[True]))
         pick = os.environ.get("SS_CAL_PICK", "")  # debug: force the outcome
         if pick in ("sync", "ahead"):
             best = pick == "ahead"
         self.set_pull_ahead(best)
         self.drain()
+        ms = lambda xs: [round(1e3 * x, 4) for x in xs]  # noqa: E731
         return {"pull_ahead": best, "staleness": eng.lookahead if best else 0,
-                "sync_ms": round(1e3 * times[False], 4), "ahead_ms": round(1e3 * times[True], 4),
-                "steps_per_mode": steps + 2}
+                "sync_ms": ms(times[False]), "ahead_ms": ms(times[True]),
+                "rank_spread_ms": {"sync": ms(spread[False]), "ahead": ms(spread[True])},
+                "windows": windows, "steps_per_window": steps, "margin": margin}
 
     def rounds_done(self) -> int:
         """Rounds whose pushes have been enqueued on the device.  Eagerly

@@ -101,6 +101,10 @@ class SparseLRWorker(PipelinedWorker):
             # the forward adds the loss into _acc; the merge moves it to
             # loss_sum and leaves _acc zero (see _compute)
             self._acc = torch.zeros_like(self.loss_sum)
+            # every pulled round is pushed through the fused snapshot merge:
+            # the one-GPU engine may claim new keys' slots in the pull and let
+            # the merge store them (PSEngine.claim, table.hip k_pull_claim_bk)
+            engine.claim_rounds = True
             for dd in engine.dedupers:
                 dd.zero_grad = False         # the LDS reduce stores every unique row
                 dd.materialize_inv = False   # the forward resolves occurrences itself

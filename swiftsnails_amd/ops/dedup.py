@@ -53,6 +53,7 @@ class DedupResult:
     n: int
     owner: object = None      # the Deduper (bucket mode: reduce plan lives there)
     lay: int = 0              # bucket-layout size (>= n; N>1 engines: max_keys)
+    rbits: int = 0            # > 0: buckets hold whole regions of a 2^rbits-region table
 
 
 class Deduper:
@@ -94,6 +95,10 @@ class Deduper:
         # the server's sub-bucket (msub > 1), with the offsets in ``usub``
         # ([P][msub], sent with the keys: the server reads its exact ranges)
         self.msub, self.usub = 1, None
+        # bucket mode, one rank: bucket whole regions of a region table with
+        # 2^rbits regions (ops/table.py _region_bits) when the call's layout
+        # allows it (the kernel reports the bits it used: DedupResult.rbits)
+        self.rbits = 0
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -154,7 +159,7 @@ class Deduper:
         ug = self.ugrad.data_ptr() if (self.ugrad is not None and self.zero_grad) else 0
         if self.mode == "bucket":
             self._last_n = n
-            self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
+            used = self.h.bd_dedup(keys.data_ptr(), n, self.frag_map.data_ptr(), self.frag_map.numel(),
                             self.nranks, self.ucap, self.scratch.data_ptr(), self.pj.data_ptr(),
                             self.pos_of.data_ptr() if self.need_pos else 0,
                             self.bkt.data_ptr() if self.need_bkt else 0,
@@ -167,9 +172,10 @@ class Deduper:
                             self.rec.data_ptr(),
                             self.usingle.data_ptr() if self.usingle is not None else 0,
                             self.ndest, self.lay_n or 0, self.msub,
-                            self.usub.data_ptr() if self.usub is not None else 0)
+                            self.usub.data_ptr() if self.usub is not None else 0,
+                            self.rbits)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
-                               self.nranks, n, self, self._lay(n))
+                               self.nranks, n, self, self._lay(n), int(used or 0))
         # the scratch is all-EMPTY between calls: the finish kernel resets the
         # slots its winners claimed, so no per-round 0xFF memset is needed
         if self._dirty:

@@ -141,7 +141,26 @@ class HbmTable:
         self._init_native = self.init_cfg.native()
 
     # -- storage ------------------------------------------------------------
+    def _region_bits(self, cap: int) -> int:
+        """Region count (log2) of a new allocation of ``cap`` slots: scalar
+        16-byte [w | h | key] rows (sparse LR) are split into 2^rbits equal
+        regions of >= 1024 slots (at most 2^16), inside which each key probes
+        (ss_device.h ProbeSeq): the one-GPU engine then buckets whole regions
+        per dedup workgroup and inserts without device atomics
+        (table.hip k_pull_claim_bk).  0: one region (SS_TABLE_REGIONS=0, other
+        layouts, tables under 64K slots)."""
+        if (os.environ.get("SS_TABLE_REGIONS", "1") == "0" or self.bf16 or self.width != 2
+                or self.dim != 1 or (self.stride, self.key_off, self.row_off) != (16, 8, 0)
+                or cap >= (1 << 31) - (1 << 16)):
+            return 0
+        rb = min(16, max(0, (cap // 1024).bit_length() - 1))
+        return rb if rb >= 6 else 0
+
     def _alloc(self, cap: int):
+        self.rbits = self._region_bits(cap)
+        if self.rbits:  # whole regions: capacity rounded up to a multiple of 2^rbits
+            R = 1 << self.rbits
+            cap = -(-cap // R) * R
         self.capacity = cap
         self.version += 1
         self.storage = torch.empty(cap * self.stride, dtype=torch.uint8, device=self.device)
@@ -168,7 +187,7 @@ class HbmTable:
         self.dt = hip().DevTable(self.storage.data_ptr(), self.capacity, self.stride,
                                  self.key_off, self.dim, self.width,
                                  int(self.prefilled and self.init_fn is None), self.row_off,
-                                 int(self.bf16))
+                                 int(self.bf16), self.rbits)
 
     @staticmethod
     def plan(n_keys: int, dim: int, optimizer: Optional[Optimizer] = None,

@@ -77,6 +77,7 @@ class Round:
     snap_version: int = -1                # table.version the snapshot is valid for
     applied: bool = False                 # the model's kernel already ran K5 (fuse_apply)
     slot32: bool = False                  # world-1: `slots` holds 4-byte indices (first half)
+    deferred: bool = False                # world-1 claimed pull: new keys' slots not written yet
     server: Optional[object] = None       # CPU N>1: (unique keys, inverse) of the server merge
 
     @property
@@ -176,6 +177,16 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             self.native = _hip().RoundEngine(self.depth, self._dix)
             self._pins = [torch.zeros(2 * N, dtype=torch.int64, pin_memory=True)
                           for _ in range(self.depth)]
+        # claimed pulls whose slots no kernel has written yet (pulled, merge not
+        # issued): a further pull first commits them (pull A, pull B, push A,
+        # push B must not claim a slot twice), and the ring slot of the last
+        # claimed round, whose push a pull off the main stream waits for
+        self._claimed: list = []
+        self._deferred_slot: Optional[int] = None
+        self.claim = False
+        # set by a caller whose every pulled round is pushed through the
+        # fused snapshot merge (SparseLRWorker): only its pulls claim
+        self.claim_rounds = False
         if self.fast1:
             # pull snapshots for the blind-write apply (scalar AdaGrad rows)
             self.snapshot = bool(getattr(table, "snapshot_ok", False))
@@ -192,6 +203,16 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             if table is not None:  # the pull reads the dedup's staging: no send segment
                 for dd in self.dedupers:
                     dd.need_ukeys = False
+            # claimed pulls (region tables, table.hip k_pull_claim_bk): the
+            # dedup buckets whole table regions, the bucket's pull claims new
+            # keys' slots in LDS (no device-scope CAS, nothing written), and
+            # the fused merge stores [w | h | key] per slot (SS_CLAIM=0: off)
+            self.claim = bool(self.slot32 and getattr(table, "rbits", 0) and
+                              os.environ.get("SS_CLAIM", "1") != "0")
+            if self.claim:
+                for dd in self.dedupers:
+                    if getattr(dd, "mode", None) == "bucket":
+                        dd.rbits = table.rbits
         elif self.gpu:
             self._init_dist_gpu()
         else:
@@ -351,6 +372,14 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         st = ps.cuda_stream
         if ps is not self.route_stream:
             self._wait_ev(ROUTE, r, st)
+        if self._claimed:  # committed on the main stream, after their pulls
+            self._commit_claimed(self.raw_stream())
+            ps.wait_stream(self.main_stream())
+        if self._deferred_slot is not None:
+            # the table holds the last claimed pull's new keys only after that
+            # round's push: a pull off the main stream waits for it
+            self.native.wait(FREE, self._deferred_slot, st, self._tag)
+            self._deferred_slot = None
         # staleness bound: round i+1 waits for round i-1's push (k slots back)
         k = self.staleness
         if 0 < k < self.depth - 1:
@@ -367,19 +396,26 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         a returned Round with ``ready`` set has its pull event recorded."""
         dd, slot, tab = r.dd, r.slot, self.table
         if self.fast1:
+            self._commit_claimed(st)
             own = dd.owner
             snap = (self._snaps[slot] if (not ahead and self.snapshot and tab.snapshot_ok)
                     else None)
             native = getattr(own, "mode", None) == "bucket" and not tab.custom_pull
-            s32 = False
+            s32 = claim = False
             if native:
                 v = own.bucket_view(dd.n)
                 s32 = self.slot32 and snap is not None
+                # a claimed pull: synchronous rounds only (the table is written
+                # by this round's merge, before the next pull on this stream)
+                claim = bool(s32 and self.claim and self.claim_rounds and dd.rbits and
+                             dd.rbits == tab.rbits)
                 self.native.pull_fast(slot, self._tag, st, False, -1, ahead, tab.dt,
                                       tab._init_native, tab.size_ctr.data_ptr(),
                                       tab.err.data_ptr(), tab.G, list(v[:4]), v[4], uv.data_ptr(),
                                       self.slots[slot].data_ptr(),
-                                      snap.data_ptr() if snap is not None else 0, int(s32))
+                                      snap.data_ptr() if snap is not None else 0, int(s32), claim)
+                if claim:
+                    self._deferred_slot = slot
             elif getattr(own, "mode", None) == "bucket":
                 tab.pull_buckets(own.bucket_view(dd.n), uv, self.slots[slot], stream=st, snap=snap)
             else:
@@ -388,9 +424,12 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             if tab.custom_pull:  # user init / pull methods (tensor code; syncs)
                 tab.finish_pull(self.slots[slot], uv, n=dd.ucount)
             self.metrics.add(occurrences=dd.n)
-            return Round(dd, uv, slot, slots=self.slots[slot], snap=snap,
-                         snap_version=tab.version, ready=native and ahead, tag=self._tag,
-                         slot32=native and s32)
+            rnd = Round(dd, uv, slot, slots=self.slots[slot], snap=snap,
+                        snap_version=tab.version, ready=native and ahead, tag=self._tag,
+                        slot32=native and s32, deferred=claim)
+            if claim:
+                self._claimed.append(rnd)
+            return rnd
         if not (self.xg and self.gpu):
             return self._pull_counts(r, uv, self.pt if ahead else self.t, st)
         # N>1 over the mailboxes: one call (keys wait, server merge + lookup,
@@ -472,13 +511,36 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             return None
         if snapshot and not (rnd.snap is not None and rnd.snap_version == tab.version):
             return None
+        if rnd.deferred and not snapshot:
+            return None  # a claimed pull is committed by the snapshot merge only
         rnd.applied = True
         tab.version += 1
         args = {"t": tab.dt, "slots": rnd.slots.data_ptr(), "op": tab.opt.native(),
                 "slot32": int(rnd.slot32)}
         if snapshot:
             args["snap"] = rnd.snap.data_ptr()
+        if rnd.deferred:  # the merge stores whole [w | h | key] slots
+            args["bkeys"] = rnd.dd.owner.bkeys.data_ptr()
+            self._claimed = [x for x in self._claimed if x is not rnd]
+            rnd.deferred = False
         return args
+
+    def _commit(self, rnd: Round, stream: Optional[int] = None) -> None:
+        """Write the keys (and the initial rows, i.e. its snapshot) of a
+        claimed pull that no fused merge committed — its snapshot went stale
+        before the push, or another pull comes first (k_commit_claims)."""
+        if not rnd.deferred:
+            return
+        v = rnd.dd.owner.bucket_view(rnd.dd.n)
+        _hip().commit_claims(self.table.dt, v[0], v[1], v[2], v[3], v[4], rnd.slots.data_ptr(),
+                             rnd.snap.data_ptr(),
+                             self.raw_stream() if stream is None else stream)
+        rnd.deferred = False
+        self._claimed = [x for x in self._claimed if x is not rnd]
+
+    def _commit_claimed(self, stream) -> None:
+        for rnd in list(self._claimed):
+            self._commit(rnd, stream)
 
     def push(self, rnd: Round, grads: Optional[torch.Tensor] = None) -> None:
         with self.trace("push"):
@@ -488,9 +550,14 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         g = rnd.ugrad if grads is None else grads
         tab, slot = self.table, rnd.slot
         if self.fast1:
+            if not rnd.applied:
+                self._commit(rnd)
             if not rnd.applied and tab.push_fn is not None:
                 n = int(rnd.dd.ucount.sum())  # a tensor rule: host-sized (syncs)
-                tab.apply_custom(rnd.slots[:n], g[:n])
+                sl = rnd.slots
+                if rnd.slot32:  # the pull stored 4-byte slot indices
+                    sl = sl.view(torch.int32)[:sl.numel()].to(torch.int64)
+                tab.apply_custom(sl[:n], g[:n])
                 self._release(slot)
             else:
                 apply = not rnd.applied

@@ -61,6 +61,8 @@ class EngineControl:
         if len(keys) == 0:
             return torch.zeros((0, self.dim), dtype=torch.float32, device=keys.device)
         if self.gpu:
+            if getattr(self, "_claimed", None):  # a claimed pull not pushed yet
+                self._commit_claimed(self.raw_stream())
             torch.cuda.synchronize(self.device)  # every enqueued update applied
             return tab.pull(keys, insert=False)[0]
         rows, found = tab._t.get_rows(keys.numpy().view(np.uint64))

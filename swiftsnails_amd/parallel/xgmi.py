@@ -186,6 +186,11 @@ class XgmiTransport(Transport):
                                + (f": {err}" if err else ""))
         reasons = []
         for tier in self.TIERS:
+            # a failed earlier tier's sticky error bits (a stale round tag, a
+            # corrupt count) must not fail this tier's litmus or the first
+            # training round: clear the device and host-mapped error words
+            # once that tier's work has drained (reset_err synchronises)
+            self.reset_errors()
             self._set_tier(tier)
             forced = self.force_tier == "rccl" or (self.force_tier == "fenced" and tier == "drain")
             t0 = time.perf_counter()
@@ -201,6 +206,12 @@ class XgmiTransport(Transport):
             if timed_out:
                 break  # the arrival counters are no longer in step: no retry
         raise RuntimeError("xgmi litmus failed on every tier (" + "; ".join(reasons) + ")")
+
+    def reset_errors(self) -> None:
+        """Clear every arena's sticky device and host-mapped error words
+        (waits for the device)."""
+        for a in self.arenas.values():
+            a.reset_err()
 
     def _agree_ok(self, ok: bool, timed_out: bool = False):
         """(every rank ok, any rank timed out), the same on every rank."""

@@ -63,6 +63,13 @@ KNOBS: dict[str, Knob] = {
                             "slot layout: rowfirst (width <= 2) / keyfirst"),
     "SS_TABLE_PREFILL": Knob("1", "ops/table.py", "tuning",
                              "zero-init tables pre-filled with the init row (insert = CAS only)"),
+    "SS_TABLE_REGIONS": Knob("1", "ops/table.py", "tuning",
+                             "scalar 16-byte LR slots: split the shard into 2^k probe regions "
+                             "(>= 1024 slots each) so one dedup bucket owns its regions' inserts "
+                             "(0: one region, every insert a device CAS)"),
+    "SS_CLAIM": Knob("1", "parallel/engine.py", "tuning",
+                     "one GPU, region tables, synchronous rounds: the pull claims new keys' "
+                     "slots in LDS and the fused merge stores [w | h | key] (0: CAS inserts)"),
     "SS_BD_NCH": Knob("128", "csrc/hip/bdedup.hip", "tuning",
                       "max count/scatter chunks (1 GPU 512 -> 128: 0.93 -> 0.89 ms/step; "
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),

@@ -72,6 +72,48 @@ def test_stale_round_tag_is_detected():
         del os.environ["SS_XGMI_VERIFY"]
 
 
+def test_failed_tier_error_bits_do_not_fail_next_tier(monkeypatch):
+    """A drain-tier litmus that fails with sticky error bits set (what a stale
+    round tag under SS_XGMI_VERIFY=1 leaves behind) must not fail the fenced
+    tier's litmus, nor the first rounds after it: the error words are cleared
+    before each tier."""
+    monkeypatch.setenv("SS_XGMI_VERIFY", "1")
+    from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+    orig = XgmiTransport._litmus
+
+    def litmus(self, fail=False):
+        ok, why = orig(self, fail)
+        if self.tier is None and not getattr(self, "_poisoned", False):
+            self._poisoned = True  # the drain tier: a stale tag seen by the waits
+            torch.cuda.synchronize()
+            for e in self._errs:
+                e.fill_(4)
+            torch.cuda.synchronize()
+            return False, "stale round tag (injected)"
+        return ok, why
+
+    monkeypatch.setattr(XgmiTransport, "_litmus", litmus)
+    dev = torch.device("cuda", 0)
+    tr = XgmiTransport(0, 1, dev, None, timeout_s=10)
+    tr.setup({"c": (2, [4096])})
+    assert tr.tier == "fenced"
+    assert [x[1] for x in tr.litmus_log] == [False, True]
+    tr.poll_error()
+    tr.check()
+    src = torch.arange(1024, dtype=torch.int32, device=dev)
+    st = torch.cuda.current_stream(dev)
+    for r in range(4):
+        tr.put("c", r % 2, [(src, [0], None, 1024)], stream=st)
+        tr.wait("c", r % 2, stream=st)
+    st.synchronize()
+    tr.poll_error()
+    tr.check()
+    got = tr.region("c", 0, 1, torch.int32)[:1024]
+    assert torch.equal(got, src)
+    tr.close()
+
+
 def _bench(env, extra=(), nproc=1, shape=("--steps", "4", "--warmup", "2", "--batch", "4096",
                                           "--features", "2000000")):
     e = dict(os.environ, GLOO_SOCKET_IFNAME="lo", **env)
