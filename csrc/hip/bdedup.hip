@@ -411,7 +411,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    float* __restrict__ ugrad, int gdim,
                                                    uint8_t* __restrict__ usingle, int msub,
                                                    uint32_t* __restrict__ usub,
-                                                   const uint32_t* __restrict__ wfin) {
+                                                   const uint32_t* __restrict__ wfin, int rbits) {
   // dbg (optional): per bucket wall-clock stamps of the phases (profiling)
 #define BD_STAMP(i) \
   if (dbg && t == 0) dbg[(long long)b * 8 + (i)] = wall_clock64();
@@ -516,11 +516,23 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   unsigned int o = 0;
   uint8_t sb[kPerT];
   uint16_t rk[kPerT];
+  // the server's sub-bucket of a key: region buckets (rbits) split each
+  // bucket's regions further, floor(region * Pd * msub / R) - k * msub, so a
+  // server sub-bucket is whole regions of the server's table too (its pull
+  // claims inserts, table.hip k_pull_claim_bk); else a dedup_hash split
+  auto sub_of = [&](uint64_t v) -> uint32_t {
+    if (rbits) {
+      const uint64_t region = table_hash(v) >> (64 - rbits);
+      const uint32_t f = (uint32_t)((region * (uint64_t)Pd * (uint64_t)msub) >> rbits);
+      return f - (uint32_t)(b % Pd) * (uint32_t)msub;
+    }
+    return srv_sub(v, msub);
+  };
   if (msub > 1) {
 #pragma unroll
     for (int k = 0; k < kPerT; ++k) {
       const unsigned long long v = own(k);
-      sb[k] = v != kEmptyKey ? (uint8_t)srv_sub(v, msub) : 0;
+      sb[k] = v != kEmptyKey ? (uint8_t)sub_of(v) : 0;
       rk[k] = v != kEmptyKey ? (uint16_t)atomicAdd(&hsub[sb[k]], 1u) : 0;
     }
     __syncthreads();
@@ -1038,10 +1050,12 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   if ((long long)L.Pd * bd_clamp_ndest(rs.nranks, ndest) > kBdMaxBuckets + kMaxSeg ||
       ln > bd_max_keys())
     throw_error("bdedup: too many keys per call (max ~45M)");
-  // region buckets (one rank): only when every bucket gets >= 4 regions, so
-  // the floor(region * Pd / R) split keeps buckets within ~25% of the target
-  // (a region's keys cannot be split over buckets); else dedup-hash buckets
-  if (rs.rbits && (rs.nranks != 1 || 4ll * L.Pd > (1ll << rs.rbits))) rs.rbits = 0;
+  // region buckets: only when every (server sub-)bucket gets >= 4 regions,
+  // so the floor(region * Pd * msub / R) split keeps buckets within ~25% of
+  // the target (a region's keys cannot be split over buckets); else
+  // dedup-hash buckets.  A function of the layout only: every rank of an
+  // N>1 job decides the same
+  if (rs.rbits && 4ll * L.Pd * msub > (1ll << rs.rbits)) rs.rbits = 0;
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
   // workgroup sizes (256/512/1024): count (SS_BD_CNT), column scan
@@ -1114,13 +1128,13 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
                        bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
                        reinterpret_cast<const BdRec3*>(rec), dbg,
                        place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub,
-                       wfin);
+                       wfin, rs.rbits);
   else
     hipLaunchKernelGGL(k_bd_dedup<4>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
                        bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
                        reinterpret_cast<const uint4*>(rec), dbg,
                        place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub,
-                       nullptr);
+                       nullptr, rs.rbits);
   check_launch("k_bd_dedup");
   if (inv && n > 0) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");
@@ -1202,7 +1216,7 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
                         const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
                         float* ugrad, const DevTable* t, const long long* slots,
                         const float* snap, const OptParams* op, hipStream_t st, SelfSeg self,
-                        int slot32) {
+                        int slot32, const uint64_t* bkeys) {
   if (P <= 0) return;
   DevTable tv{};
   OptParams opv{};
@@ -1215,9 +1229,12 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
     tv = *t;
     opv = *op;
   }
+  if (bkeys && (!(slots || s32) || !snap || t->stride != 16 || t->key_off != 8 || t->row_off != 0))
+    throw_error("bd_reduce_p: slot stores with keys need a snapshot merge into [w|h|key] slots");
   hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj, luid,
                      gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
-                     reinterpret_cast<const float2*>(snap), opv, self, s32);
+                     reinterpret_cast<const float2*>(snap), opv, self, s32, nullptr, nullptr, 0,
+                     bkeys);
   check_launch("k_bd_reduce_p");
 }
 

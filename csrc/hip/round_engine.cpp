@@ -75,6 +75,7 @@ class RoundEngine {
     self_keys_.assign(depth, 0);
     srv_done_.assign(depth, 0);
     srv_s32_.assign(depth, 0);
+    srv_claim_.assign(depth, 0);
   }
   ~RoundEngine() {
     hipSetDevice(device_);
@@ -231,7 +232,8 @@ class RoundEngine {
                  bool table, const DevTable& t, const InitParams& ip, uintptr_t size_ctr,
                  uintptr_t err, int G, uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum,
                  uintptr_t srv_err, uintptr_t svals, uintptr_t rvals, bool snap, uintptr_t sent,
-                 std::vector<uintptr_t> metrics, bool custom_pull) {
+                 std::vector<uintptr_t> metrics, bool custom_pull, bool claim,
+                 bool insert) {
     check_xgmi();
     pull_waits(slot, tag, stream, wait_route, prev);
     // the keys in and the server's distinct-key merge, unless the route ran them
@@ -243,9 +245,24 @@ class RoundEngine {
       // store 4-byte slot indices; the push's fused merge reads them back
       srv_s32_[slot] = snap && G == 1 && t.stride == 16 && t.key_off == 8 && t.row_off == 0 &&
                        t.cap < (1ull << 31) && slot32_on();
-      launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
-                            Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
-                            G, St(stream), snap ? S.snap : nullptr, srv_s32_[slot]);
+      // claim: every server sub-bucket is whole regions of this shard (the
+      // senders' region buckets): LDS-claimed inserts, the push's fused merge
+      // stores [w | h | key] (synchronous snapshot rounds only)
+      srv_claim_[slot] = claim && srv_s32_[slot];
+      if (!insert) {  // read-only (PSEngine.lookup): nothing inserted, zeros if absent
+        if (snap || claim || custom_pull)
+          throw std::invalid_argument("pull_xgmi: a read-only lookup takes no snapshot / claim / hook");
+        srv_s32_[slot] = srv_claim_[slot] = 0;
+        launch_lookup_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, Pt<float>(svals), G,
+                         St(stream));
+      } else if (srv_claim_[slot])
+        launch_pull_claim_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_,
+                             reinterpret_cast<int*>(S.slots), Pt<float>(svals), S.snap, ip,
+                             Pt<unsigned long long>(size_ctr), Pt<int>(err), St(stream));
+      else
+        launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
+                              Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
+                              G, St(stream), snap ? S.snap : nullptr, srv_s32_[slot]);
       if (custom_pull) return;  // the caller finishes the pull (tensor-code hooks)
       fill_and_return(slot, stream, svals, rvals, sent, metrics);
     } else {
@@ -302,10 +319,12 @@ class RoundEngine {
       const SelfSeg sg = self_seg(grads);  // this rank's own gradient rows, in place
       if (srv_s32_[slot] && !(update && scalar_fused && snap))
         throw std::logic_error("push_xgmi: a 4-byte-slot pull needs the fused snapshot merge");
+      if (srv_claim_[slot] && !(update && scalar_fused && snap))
+        throw std::logic_error("push_xgmi: a claimed pull needs the fused snapshot merge");
       if (update && scalar_fused)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
                            1, nullptr, &t, S.slots, snap ? S.snap : nullptr, &op, St(stream), sg,
-                           srv_s32_[slot]);
+                           srv_s32_[slot], srv_claim_[slot] ? S.bkeys : nullptr);
       else if (dim_ == 1)
         launch_bd_reduce_p(Ps, S.bstart, S.ubase, S.unum, S.pj, S.luid, Pt<const float>(rgrads),
                            1, Pt<float>(merged), nullptr, nullptr, nullptr, nullptr, St(stream),
@@ -419,6 +438,7 @@ class RoundEngine {
   std::vector<uintptr_t> self_keys_;  // per slot: this rank's send layout of its keys
   std::vector<char> srv_done_;        // per slot: the route ran keys_in (srv_ahead)
   std::vector<char> srv_s32_;         // per slot: the server pull stored 4-byte slots
+  std::vector<char> srv_claim_;       // per slot: ... and claimed its inserts (no CAS)
   static bool slot32_on() {           // SS_SLOT32=0: 8-byte slot indices
     static const bool on = [] {
       const char* e = std::getenv("SS_SLOT32");

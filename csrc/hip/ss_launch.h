@@ -42,6 +42,10 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
                           const uint32_t* unum, const uint32_t* ubase, int P, int* slots32,
                           float* out, float* snap, const InitParams& ip,
                           unsigned long long* size_ctr, int* err, hipStream_t st);
+// read-only lookup of a bucket view's unique keys (no insert; zeros if absent)
+void launch_lookup_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                      const uint32_t* unum, const uint32_t* ubase, int P, float* out, int G,
+                      hipStream_t st);
 void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                           const uint32_t* unum, const uint32_t* ubase, int P, const int* slots32,
                           const float* snap, hipStream_t st);
@@ -199,7 +203,7 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
                         const uint32_t* pj, const uint32_t* luid, const float* gs, int F,
                         float* ugrad, const DevTable* t, const long long* slots,
                         const float* snap, const OptParams* op, hipStream_t st,
-                        SelfSeg self = {}, int slot32 = 0);
+                        SelfSeg self = {}, int slot32 = 0, const uint64_t* bkeys = nullptr);
 void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
                           const uint32_t* unum, const uint32_t* luid, const float* uvals,
                           float* occ, const uint32_t* pj, hipStream_t st, SelfSeg self = {});

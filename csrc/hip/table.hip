@@ -565,6 +565,33 @@ __global__ __launch_bounds__(256) void k_pull_narrow_bk(DevTable t, const uint64
 }
 
 
+// Read-only lookup of a bucket view's unique keys (the N>1 collective
+// lookup, PSEngine.lookup: a server answers any worker's keys without
+// inserting): out[(ubase[b] + l) * dim + j] = the row of bkeys[bstart[b] + l],
+// zeros for a key this shard does not hold.  G lanes per key.
+template <int G>
+__global__ __launch_bounds__(256) void k_lookup_bk(DevTable t, const uint64_t* __restrict__ bkeys,
+                                                   const uint32_t* __restrict__ bstart,
+                                                   const uint32_t* __restrict__ unum,
+                                                   const uint32_t* __restrict__ ubase,
+                                                   float* __restrict__ out) {
+  const int b = blockIdx.x, lg = threadIdx.x % G;
+  const uint32_t nu = unum[b], base = ubase[b];
+  const uint64_t* src = bkeys + bstart[b];
+  for (uint32_t l = blockIdx.y * (256 / G) + threadIdx.x / G; l < nu;
+       l += gridDim.y * (256 / G)) {  // uniform inside a lane group
+    const uint64_t key = src[l];
+    long long slot = -1;
+    if (lg == 0 && key != kEmptyKey) {
+      bool unused = false;
+      slot = probe_slot(t, key, false, &unused);
+    }
+    if (G > 1) slot = __shfl(slot, 0, G);
+    float* o = out + ((long long)base + l) * (long long)t.dim;
+    for (uint32_t j = lg; j < t.dim; j += G) o[j] = slot < 0 ? 0.f : row_ld(t, slot, j);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K5: fused optimizer update on resolved slots. Keys inside one launch must be
 // unique (the host launches one segment per source rank, in rank order, so
@@ -942,6 +969,15 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
                                       bkeys, bstart, unum, ubase, slots, out, ip, size_ctr, err,
                                       reinterpret_cast<float2*>(snap), one16));
   check_launch("k_pull_unique_bk");
+}
+
+void launch_lookup_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
+                      const uint32_t* unum, const uint32_t* ubase, int P, float* out, int G,
+                      hipStream_t st) {
+  if (P <= 0) return;
+  SS_DISPATCH_G(G, hipLaunchKernelGGL(k_lookup_bk<kG>, dim3(P, 2), dim3(256), 0, st, t, bkeys,
+                                      bstart, unum, ubase, out));
+  check_launch("k_lookup_bk");
 }
 
 static void check_claim_table(const DevTable& t) {

@@ -182,6 +182,7 @@ class PipelinedWorker:
             if gc_on:
                 gc.enable()
         self._gper = per
+        eng.graphed = True  # replays hold ring slots across calls (PSEngine.lookup)
         # the captures only recorded: the device is where it was before them,
         # and after `depth` steps the Python-side pipeline state is periodic
         self.step_idx, self._next, pulled, eng._next_slot, eng.rounds = saved

@@ -174,7 +174,9 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self.native = None
         if self.gpu:
             self.route_stream = torch.cuda.Stream(device=dev)
-            self.native = _hip().RoundEngine(self.depth, self._dix)
+            # + one slot past the ring: the N>1 read-only lookup's round
+            # (PSEngine.lookup) never touches a ring slot the pipeline holds
+            self.native = _hip().RoundEngine(self.depth + 1, self._dix)
             self._pins = [torch.zeros(2 * N, dtype=torch.int64, pin_memory=True)
                           for _ in range(self.depth)]
         # claimed pulls whose slots no kernel has written yet (pulled, merge not
@@ -441,6 +443,12 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         sx = self.metrics.device_block(("server_unique",), self.device) if S is not None else None
         m = [acc.data_ptr(), S.ucount.data_ptr() if S else 0, sx.data_ptr() if S else 0]
         custom = S is not None and tab.custom_pull
+        # a claimed server pull (sync snapshot rounds, region buckets): its
+        # merge in this round's push stores the new keys' slots
+        claim = bool(S is not None and S.snap_valid and not custom and self.claim and
+                     self.claim_rounds and dd.rbits and dd.rbits == tab.rbits)
+        if claim:
+            self._deferred_slot = slot
         svals = self.svals.data_ptr() if S is not None else 0
         self.native.pull_xgmi(slot, self._tag, st, False, -1, ahead and not custom, S is not None,
                               tab.dt if S else self._nodt, tab._init_native if S else self._noip,
@@ -449,7 +457,7 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                               self.rmeta[slot][0].data_ptr(), self.rmeta[slot][1].data_ptr(),
                               self.srv_err.data_ptr() if S else 0, svals,
                               self.rvals.data_ptr(), bool(S and S.snap_valid),
-                              dd.ucount.data_ptr(), m, custom)
+                              dd.ucount.data_ptr(), m, custom, claim, True)
         if custom:
             tab.finish_pull(S.slots, self.svals, n=S.ucount)
             self.native.pull_xgmi_finish(slot, self._tag, st, ahead, svals, self.rvals.data_ptr(),

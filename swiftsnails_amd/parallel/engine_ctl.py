@@ -32,6 +32,10 @@ class EngineControl:
         keys = keys.reshape(-1)
         if self.world == 1:
             return self._read_rows(keys.to(self.device)).to(keys.device)
+        if self.gpu and getattr(self, "lookup_slot", None) is not None and \
+                not getattr(self, "graphed", False) and \
+                not (self.table is not None and self.table.custom_pull):
+            return self._lookup_xgmi(keys)
         import torch.distributed as dist
 
         from .router import route_keys_np
@@ -55,6 +59,63 @@ class EngineControl:
         out_u = torch.empty_like(back)
         out_u[order] = back
         return out_u[inv].to(keys.device)
+
+    def _lookup_xgmi(self, keys: torch.Tensor) -> torch.Tensor:
+        """The collective read-only lookup on the device (N>1 over the xGMI
+        mailboxes): the same round as a training pull — dedup + route into
+        per-server bucket runs, keys into the servers' mailboxes, every
+        server's merge of the sources' keys — but the servers LOOK UP their
+        distinct keys without inserting (table.hip k_lookup_bk, zeros for
+        absent keys) and nothing is pushed; rows come back through the vals
+        mailboxes and are gathered into occurrence order.  It runs on the
+        reserved slot past the route ring, so a pipeline holding ring slots
+        (routed / pulled-ahead rounds) is not disturbed.  Batches of up to
+        ``max_keys`` keys per rank per round; longer key lists take several
+        rounds (every rank the same number: agreed first)."""
+        from .engine import FREE, _hip
+
+        h = _hip()
+        n = int(keys.numel())
+        cap = self.max_keys
+        nr = torch.tensor([-(-n // cap)], dtype=torch.int64)
+        self.t.allreduce_(nr, "max")  # control plane (gloo): every rank the same rounds
+        rounds = int(nr.item())
+        q, tab, dd = self.lookup_slot, self.table, self._lk_dd
+        dd.materialize_inv, dd.need_bkt, dd.need_pos = True, True, True
+        out = torch.empty((n, self.dim), dtype=torch.float32, device=self.device)
+        kd = keys.to(self.device, torch.int64)
+        st = self.raw_stream()
+        if getattr(self, "_claimed", None):
+            self._commit_claimed(st)
+        S = self.srv[q] if self.srv is not None else None
+        for i in range(rounds):
+            part = kd[i * cap:(i + 1) * cap]
+            m = int(part.numel())
+            self.native.wait(FREE, q, st, 0)  # the previous lookup round is done
+            r = dd(part, stream=st)
+            ub, un = dd.run_tables(self.Pd)
+            us = dd.sub_table(self.Pd).data_ptr() if dd.msub > 1 else 0
+            self.native.route_end(q, 0, st, r.ukeys.data_ptr(), r.ucount.data_ptr(),
+                                  ub.data_ptr(), un.data_ptr(), us, False, tab is not None,
+                                  self.rkeys[q].data_ptr(), self.rmeta[q][0].data_ptr(),
+                                  self.rmeta[q][1].data_ptr(),
+                                  self.srv_err.data_ptr() if tab is not None else 0)
+            self.native.pull_xgmi(q, 0, st, False, -1, False, S is not None,
+                                  tab.dt if S else self._nodt,
+                                  tab._init_native if S else self._noip,
+                                  tab.size_ctr.data_ptr() if S else 0,
+                                  tab.err.data_ptr() if S else 0, tab.G if S else 1,
+                                  self.rkeys[q].data_ptr(), self.rmeta[q][0].data_ptr(),
+                                  self.rmeta[q][1].data_ptr(),
+                                  self.srv_err.data_ptr() if S else 0,
+                                  self.svals.data_ptr() if S else 0, self.rvals.data_ptr(),
+                                  False, r.ucount.data_ptr(), [], False, False, False)
+            if m:
+                h.gather_rows(self.uvals[q].data_ptr(), r.inv.data_ptr(), m, self.dim,
+                              out[i * cap:i * cap + m].data_ptr(), st)
+            self.native.record(FREE, q, st, 0)
+        self.metrics.add(lookup_keys=n)
+        return out.to(keys.device)
 
     def _read_rows(self, keys: torch.Tensor) -> torch.Tensor:
         tab = self.table

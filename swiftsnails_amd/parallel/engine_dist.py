@@ -72,19 +72,31 @@ class DeviceSetup:
                              "is a function of it)")
         rows = N * cap
         self.rvals = torch.zeros((rows, d), dtype=torch.float32, device=dev)
+        # xGMI: one slot past the ring (index `depth`) for the read-only
+        # lookup's rounds (PSEngine.lookup), with its own deduper
+        NS = self.depth + (1 if self.xg else 0)
+        self.lookup_slot = self.depth if self.xg else None
         if self.xg:
+            from ..ops.dedup import Deduper
+
+            lk = Deduper(self.max_keys, nranks=N, frag_map=self.dedupers[0].frag_map.cpu(),
+                         gdim=d, device=dev)
+            lk.lay_n = cap
+            lk.split_for_servers(self.sub)
+            lk.need_ukeys = True
+            self._lk_dd = lk
             # the receive buffers are the arena's mailboxes: keys + the bucket
             # runs (bases, sizes) per source, rows back, gradients
             Pd, xg = self.Pd, self.xg
-            xg.setup({"keys": (self.depth, [cap * 8, Pd * 4, Pd * 4] + ([Psub * 4] if Psub else [])),
-                      "vals": (self.depth, [cap * 4 * d]), "grads": (self.depth, [cap * 4 * d])})
-            self.rkeys = [xg.region("keys", 0, q, torch.int64) for q in range(self.depth)]
+            xg.setup({"keys": (NS, [cap * 8, Pd * 4, Pd * 4] + ([Psub * 4] if Psub else [])),
+                      "vals": (NS, [cap * 4 * d]), "grads": (NS, [cap * 4 * d])})
+            self.rkeys = [xg.region("keys", 0, q, torch.int64) for q in range(NS)]
             self.rmeta = [(xg.region("keys", 1, q, torch.int32),
-                           xg.region("keys", 2, q, torch.int32)) for q in range(self.depth)]
+                           xg.region("keys", 2, q, torch.int32)) for q in range(NS)]
             self.rsub = [xg.region("keys", 3, q, torch.int32) if Psub else None
-                         for q in range(self.depth)]
-            self.uvals = [xg.region("vals", 0, q, torch.float32, d) for q in range(self.depth)]
-            self.rgrads = [xg.region("grads", 0, q, torch.float32, d) for q in range(self.depth)]
+                         for q in range(NS)]
+            self.uvals = [xg.region("vals", 0, q, torch.float32, d) for q in range(NS)]
+            self.rgrads = [xg.region("grads", 0, q, torch.float32, d) for q in range(NS)]
         else:
             self.rkeys = [torch.empty(rows, dtype=torch.int64, device=dev)] * self.depth
             meta = [torch.zeros(2 * N * self.Pd, dtype=torch.int32, device=dev)
@@ -93,6 +105,20 @@ class DeviceSetup:
             self.rsub = [torch.zeros(N * Psub, dtype=torch.int32, device=dev) if Psub else None
                          for _ in range(self.depth)]
             self.rgrads = [torch.empty((rows, d), dtype=torch.float32, device=dev)] * self.depth
+        # region buckets (claimed server pulls, table.hip k_pull_claim_bk):
+        # every shard has the same region count (same capacity), agreed with
+        # the worker-only ranks, whose buckets must follow the same regions
+        own = getattr(self.table, "rbits", 0) if self.table is not None else None
+        rb = torch.tensor([99 if own is None else own, 1 if own is None else -own],
+                          dtype=torch.int64, device=dev)
+        self._agree(rb)
+        lo, hi = int(rb[0]), -int(rb[1])
+        self.srv_rbits = lo if (lo == hi and 0 < lo < 99 and
+                                os.environ.get("SS_CLAIM", "1") != "0") else 0
+        self.claim = bool(self.srv_rbits and self.xg)
+        if self.claim:
+            for dd in self.dedupers:
+                dd.rbits = self.srv_rbits
         self.srv = None
         self.srv_ahead = os.environ.get("SS_SRV_AHEAD", "1") != "0"
         self._route_srv = None  # how the last route ran the keys-in (srv_ahead)
@@ -101,9 +127,10 @@ class DeviceSetup:
             self.sgrad = torch.empty((rows, d), dtype=torch.float32, device=dev)
             self.srv_err = torch.zeros(1, dtype=torch.int32, device=dev)
             snap_ok = bool(getattr(self.table, "snapshot_ok", False))
-            self.srv = [_ServerSlot(rows, self.Ps, dev, snap_ok) for _ in range(self.depth)]
+            self.srv = [_ServerSlot(rows, self.Ps, dev, snap_ok and q < self.depth)
+                        for q in range(NS)]
         if self.xg:
-            D = self.depth
+            D = NS
             self.native.set_xgmi([[self.xg.arena_of(c, q) for c in ("keys", "vals", "grads")]
                                   for q in range(D)],
                                  [sum((list(self.xg.layout("keys", p, q))

@@ -208,3 +208,43 @@ def test_interleaved_claimed_pulls(dev, monkeypatch):
     for k in res["0"]:
         np.testing.assert_array_equal(res["1"][k], res["0"][k])
     np.testing.assert_allclose(res["1"][20000 * 7919][1], 6.1, rtol=1e-6)
+
+
+def test_sparse_lr_xgmi_path_claimed_matches_cas(dev, monkeypatch):
+    """The N>1 engine path (a size-1 xGMI mailbox arena: keys + bucket runs
+    in, the server's merge of the sources' keys, rows back, gradients, the
+    server's fused merge) with claimed server pulls — the senders' buckets
+    and the server's sub-buckets follow the shard's regions — trains the
+    same model as with CAS inserts."""
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, lr_init, make_lr_table
+    from swiftsnails_amd.ops.optim import Optimizer
+    from swiftsnails_amd.parallel.engine import PSEngine
+    from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    out = {}
+    for claim in ("1", "0"):
+        monkeypatch.setenv("SS_CLAIM", claim)
+        data = CtrSynth(batch_size=4096, num_fields=13, num_features=2_000_000, tail_frac=0.3)
+        table = make_lr_table(data.num_features, 1, Optimizer("adagrad", lr=0.1), device=dev,
+                              capacity=1 << 22, init=lr_init("uniform", 0.01))
+        tr = XgmiTransport(0, 1, dev, None, timeout_s=30)
+        eng = PSEngine(table, tr, max_keys=4096 * 13, dim=1, device=dev)
+        assert not eng.fast1 and eng.xg is not None
+        assert eng.claim == (claim == "1") and eng.srv_rbits == (12 if claim == "1" else 0)
+        w = SparseLRWorker(eng, data)
+        losses, used = [], 0
+        for _ in range(10):
+            losses.append(float(w.step().sum().item()))
+            used += eng._deferred_slot is not None
+        torch.cuda.synchronize()
+        eng.check()
+        assert (used > 0) == (claim == "1")
+        out[claim] = (losses, table.to_dict(with_state=True))
+        tr.close()
+    (l1, t1), (l0, t0) = out["1"], out["0"]
+    np.testing.assert_allclose(l1, l0, rtol=1e-4)
+    assert t1.keys() == t0.keys()
+    ks = list(t1.keys())
+    np.testing.assert_allclose(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]),
+                               rtol=1e-4, atol=1e-6)

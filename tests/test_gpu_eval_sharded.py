@@ -6,11 +6,15 @@ rank r of N the samples [(step*N + r) * B/N, ...)) — then evaluated on the
 same held-out samples through the collective read-only pull
 (PSEngine.lookup: every shard answers, nothing is inserted).  The servers'
 merged push (one AdaGrad step on the sum of the workers' gradients per key)
-makes a round at world N the same update as world 1's step, so the held-out
-AUC must agree within 0.005."""
+makes a round at world N the same update as world 1's step, so with
+synchronous rounds the held-out AUC must agree within 0.005.  With
+pulled-ahead rounds (bounded staleness 1 or 2: what the start-up calibration
+may pick on a multi-GPU node) a round misses up to that many rounds' updates;
+the held-out AUC must stay within 0.01 of world 1.  At N > 1 the evaluation's
+read-only pull runs on the device (the xGMI round on the slot past the ring,
+PSEngine._lookup_xgmi), and it leaves every table's size unchanged."""
 import os
 
-import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -38,11 +42,14 @@ def _train_eval(rank, world, dev, transport):
     before = table.size()
     ev = w.evaluate(batches=2)
     assert table.size() == before  # read-only: nothing inserted
+    if world > 1:  # the device lookup ran, not the gloo fallback
+        assert eng.metrics.counters.get("lookup_keys", 0) == 2 * (B // world) * F
+    ev["pull_ahead"] = bool(eng.pull_ahead)
     return ev, before
 
 
-def _rank(rank, world, init, q):
-    os.environ["SS_PULL_AHEAD"] = "0"
+def _rank(rank, world, init, q, env):
+    os.environ.update(env)
     init_gloo(init, rank, world)
     try:
         from swiftsnails_amd.parallel.transport import TorchDistTransport
@@ -58,11 +65,11 @@ def _rank(rank, world, init, q):
         dist.destroy_process_group()
 
 
-def _world(world):
+def _world(world, env):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     init = file_init()
-    procs = [ctx.Process(target=_rank, args=(r, world, init, q)) for r in range(world)]
+    procs = [ctx.Process(target=_rank, args=(r, world, init, q, env)) for r in range(world)]
     for p in procs:
         p.start()
     res = collect(q, procs, world, 240)
@@ -75,15 +82,38 @@ def _world(world):
     return evs[0], sum(n for _, _, n in res)
 
 
-def test_sharded_eval_matches_world1():
+_REF = {}
+
+
+def _ref():
+    """World 1 (the one-GPU path, synchronous), trained once per session."""
     from swiftsnails_amd.parallel.transport import LoopbackTransport
 
-    dev = torch.device("cuda", 0)
-    ref, n1 = _train_eval(0, 1, dev, LoopbackTransport())
+    if not _REF:
+        old = os.environ.get("SS_PULL_AHEAD")
+        os.environ["SS_PULL_AHEAD"] = "0"
+        try:
+            _REF["ref"] = _train_eval(0, 1, torch.device("cuda", 0), LoopbackTransport())
+        finally:
+            if old is None:
+                del os.environ["SS_PULL_AHEAD"]
+            else:
+                os.environ["SS_PULL_AHEAD"] = old
+    return _REF["ref"]
+
+
+@pytest.mark.parametrize("mode,env,bound", [
+    ("sync", {"SS_PULL_AHEAD": "0"}, 0.005),
+    ("staleness1", {"SS_PULL_AHEAD": "1", "SS_STALENESS": "1"}, 0.01),
+    ("staleness2", {"SS_PULL_AHEAD": "1", "SS_STALENESS": "2"}, 0.01),
+])
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_eval_matches_world1(world, mode, env, bound):
+    ref, n1 = _ref()
     assert ref["auc"] > 0.6 and ref["samples"] == 2 * B
-    for world in (2, 4):
-        ev, n = _world(world)
-        assert ev["samples"] == 2 * B
-        assert n == n1  # the same keys trained, each on exactly one shard
-        assert abs(ev["auc"] - ref["auc"]) < 0.005, (world, ev, ref)
-        assert abs(ev["auc_truth"] - ref["auc_truth"]) < 1e-9
+    ev, n = _world(world, env)
+    assert ev["samples"] == 2 * B
+    assert ev["pull_ahead"] == (mode != "sync")
+    assert n == n1  # the same keys trained, each on exactly one shard
+    assert abs(ev["auc"] - ref["auc"]) < bound, (world, mode, ev, ref)
+    assert abs(ev["auc_truth"] - ref["auc_truth"]) < 1e-9

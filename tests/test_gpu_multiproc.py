@@ -420,3 +420,34 @@ def test_user_init_and_pull_methods_world2_gpu():
     for _, _, st in res:
         state.update(st)
     check_access_results(res, state)
+
+
+def test_split_roles_calibration_world3():
+    """Split roles (rank 0 serves only, ranks 1-2 only train) through the
+    launcher with warmup > 0 under SS_PULL_AHEAD=auto: the pull-ahead
+    calibration is a collective (rounds, barriers, an all-reduce), so the
+    server-only rank must take part in it — it used to skip it and the
+    workers' calibration rounds waited for it forever.  All
+    three ranks on cuda:0 over the xGMI mailboxes."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=3",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           "-m", "swiftsnails_amd.launch", "--config",
+           os.path.join(root, "configs", "sparse_lr_10m.conf"),
+           "--steps", "6", "--warmup", "3",
+           "--set", "batch_size=2048", "--set", "num_fields=13", "--set", "num_features=2000000",
+           "--set", "server_ranks=0", "--set", "worker_ranks=1,2", "--set", "calibrate_steps=3",
+           "--set", "transport=xgmi", "--set", "round_timeout=120"]
+    env = dict(os.environ, GLOO_SOCKET_IFNAME="lo", SS_DEVICE="0", PYTHONPATH=root,
+               SS_PULL_AHEAD="auto", SS_XGMI_TIMEOUT="60")
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    stats = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    cal = stats.get("calibration") or {}
+    assert cal, stats  # the calibration ran (on every rank: it returned)
+    assert len(cal["sync_ms"]) == cal["windows"] == 2
+    assert stats["steps"] == 6
