@@ -56,7 +56,9 @@ struct XReg {
 
 class RoundEngine {
  public:
-  enum Kind { kRoute = 0, kPull = 1, kFree = 2 };
+  // kGput: this rank's gradients of the slot are put (the main stream's last
+  // use of the slot when the server half runs on its own stream)
+  enum Kind { kRoute = 0, kPull = 1, kFree = 2, kGput = 3 };
 
   RoundEngine(int depth, int device) : depth_(depth), device_(device) {
     if (depth < 1 || depth > 16) throw std::invalid_argument("RoundEngine: depth 1..16");
@@ -233,11 +235,22 @@ class RoundEngine {
                  uintptr_t err, int G, uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum,
                  uintptr_t srv_err, uintptr_t svals, uintptr_t rvals, bool snap, uintptr_t sent,
                  std::vector<uintptr_t> metrics, bool custom_pull, bool claim,
-                 bool insert) {
+                 bool insert, uintptr_t srv_stream) {
     check_xgmi();
     pull_waits(slot, tag, stream, wait_route, prev);
+    // the server half (keys in, merge, lookup, response rows out) on the
+    // server stream when the rank has one: a slow compute on the worker's
+    // stream no longer holds up the rows every peer waits for.  It follows
+    // the round's route (this rank's own keys are read in place) and, in
+    // issue order on its stream, the server updates of earlier rounds
+    const uintptr_t ss = srv_stream ? srv_stream : stream;
+    if (ss != stream) {
+      if (custom_pull) throw std::invalid_argument("pull_xgmi: tensor-code pull hooks run on the caller's stream");
+      wait(kRoute, slot, ss, tag);
+      if (prev >= 0) wait(kFree, prev, ss, tag);
+    }
     // the keys in and the server's distinct-key merge, unless the route ran them
-    if (!srv_done_[slot]) keys_in(slot, stream, table, rkeys, rbase, rnum, srv_err);
+    if (!srv_done_[slot]) keys_in(slot, ss, table, rkeys, rbase, rnum, srv_err);
     srv_done_[slot] = false;
     if (table) {
       SrvSlot& S = srv_[slot];
@@ -254,27 +267,29 @@ class RoundEngine {
           throw std::invalid_argument("pull_xgmi: a read-only lookup takes no snapshot / claim / hook");
         srv_s32_[slot] = srv_claim_[slot] = 0;
         launch_lookup_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, Pt<float>(svals), G,
-                         St(stream));
+                         St(ss));
       } else if (srv_claim_[slot])
         launch_pull_claim_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_,
                              reinterpret_cast<int*>(S.slots), Pt<float>(svals), S.snap, ip,
-                             Pt<unsigned long long>(size_ctr), Pt<int>(err), St(stream));
+                             Pt<unsigned long long>(size_ctr), Pt<int>(err), St(ss));
       else
         launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
                               Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
-                              G, St(stream), snap ? S.snap : nullptr, srv_s32_[slot]);
+                              G, St(ss), snap ? S.snap : nullptr, srv_s32_[slot]);
       if (custom_pull) return;  // the caller finishes the pull (tensor-code hooks)
-      fill_and_return(slot, stream, svals, rvals, sent, metrics);
+      fill_and_put(slot, ss, svals, rvals);
     } else {
-      fill_and_return(slot, stream, 0, rvals, sent, metrics);
+      fill_and_put(slot, ss, 0, rvals);
     }
+    rows_wait(slot, stream, sent, metrics);
     if (ahead) record(kPull, slot, stream, tag);
   }
   // the second half of pull_xgmi after a tensor-code pull hook ran
   void pull_xgmi_finish(int slot, int tag, uintptr_t stream, bool ahead, uintptr_t svals,
                         uintptr_t rvals, uintptr_t sent, std::vector<uintptr_t> metrics) {
     check_xgmi();
-    fill_and_return(slot, stream, svals, rvals, sent, metrics);
+    fill_and_put(slot, stream, svals, rvals);
+    rows_wait(slot, stream, sent, metrics);
     if (ahead) record(kPull, slot, stream, tag);
   }
 
@@ -307,11 +322,21 @@ class RoundEngine {
   // kernel, or a tensor-code rule) and releases the slot.
   void push_xgmi(int slot, int tag, uintptr_t stream, uintptr_t grads, uintptr_t ucount,
                  bool table, bool update, const DevTable& t, const OptParams& op, uintptr_t rgrads,
-                 bool scalar_fused, bool snap, uintptr_t merged, bool release) {
+                 bool scalar_fused, bool snap, uintptr_t merged, bool release,
+                 uintptr_t srv_stream) {
     check_xgmi();
     std::vector<std::vector<long long>> parts;
     parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_, self_bypass()));
     ar_[slot][2]->put(0, parts, bpp_, stream);
+    // the server half (gradients in, merge + update, slot free) on the server
+    // stream: it follows this put (the worker's last use of the slot)
+    const uintptr_t ss = srv_stream ? srv_stream : stream;
+    if (ss != stream) {
+      if (!(update && release)) throw std::invalid_argument("push_xgmi: the server stream runs fused updates only");
+      record(kGput, slot, stream, tag);
+      wait(kGput, slot, ss, tag);
+    }
+    stream = ss;
     ar_[slot][2]->wait(0, {}, timeout_, stream, {}, 0.0);
     if (table) {
       SrvSlot& S = srv_[slot];
@@ -398,8 +423,9 @@ class RoundEngine {
     }();
     return on;
   }
-  void fill_and_return(int slot, uintptr_t stream, uintptr_t svals, uintptr_t rvals,
-                       uintptr_t sent, const std::vector<uintptr_t>& metrics) {
+  // response rows of this round's received keys (per received position)
+  // into the vals put, to every source
+  void fill_and_put(int slot, uintptr_t stream, uintptr_t svals, uintptr_t rvals) {
     // the rows each source gets back = the keys it sent here (keys header)
     const uintptr_t rc = ar_[slot][0]->base() + keys_[slot][0].hdr;
     // the rows for this rank's own keys go straight into its vals arena (the
@@ -419,6 +445,10 @@ class RoundEngine {
     std::vector<std::vector<long long>> parts;
     parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_, sv.ptr != nullptr && svals));
     ar_[slot][1]->put(0, parts, bpp_, stream);
+  }
+  // wait for every server's rows of this round (+ the exchange counters)
+  void rows_wait(int slot, uintptr_t stream, uintptr_t sent, const std::vector<uintptr_t>& metrics) {
+    const uintptr_t rc = ar_[slot][0]->base() + keys_[slot][0].hdr;
     std::vector<uintptr_t> m = metrics;
     if (!m.empty()) {
       if (m.size() != 3) throw std::invalid_argument("pull_xgmi: metrics = (acc, xval, xacc)");
@@ -428,8 +458,8 @@ class RoundEngine {
   }
 
   int depth_, device_;
-  std::array<std::vector<hipEvent_t>, 3> ev_;
-  std::array<std::vector<int>, 3> tag_;
+  std::array<std::vector<hipEvent_t>, 4> ev_;
+  std::array<std::vector<int>, 4> tag_;
   std::vector<SrvSlot> srv_;
   std::vector<std::array<XgmiArena*, 3>> ar_;  // per slot: keys, vals, grads
   std::vector<std::array<XReg, 4>> keys_;

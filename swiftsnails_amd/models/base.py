@@ -165,7 +165,8 @@ class PipelinedWorker:
                     eng.capture_tag = p + 1
                     # fork the route stream into the capture at the start (no
                     # ordering: its work overlaps the whole step)
-                    side = [x for x in (eng.route_stream, eng.pull_stream) if x is not None]
+                    side = [x for x in (eng.route_stream, eng.pull_stream,
+                                        getattr(eng, "server_stream", None)) if x is not None]
                     for x in side:
                         x.wait_stream(torch.cuda.current_stream())
                     self._cap_base = self.step_idx  # what the counter holds at replay

@@ -450,6 +450,7 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         if claim:
             self._deferred_slot = slot
         svals = self.svals.data_ptr() if S is not None else 0
+        ss = self._srv_stream(custom)
         self.native.pull_xgmi(slot, self._tag, st, False, -1, ahead and not custom, S is not None,
                               tab.dt if S else self._nodt, tab._init_native if S else self._noip,
                               tab.size_ctr.data_ptr() if S else 0, tab.err.data_ptr() if S else 0,
@@ -457,7 +458,7 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                               self.rmeta[slot][0].data_ptr(), self.rmeta[slot][1].data_ptr(),
                               self.srv_err.data_ptr() if S else 0, svals,
                               self.rvals.data_ptr(), bool(S and S.snap_valid),
-                              dd.ucount.data_ptr(), m, custom, claim, True)
+                              dd.ucount.data_ptr(), m, custom, claim, True, ss)
         if custom:
             tab.finish_pull(S.slots, self.svals, n=S.ucount)
             self.native.pull_xgmi_finish(slot, self._tag, st, ahead, svals, self.rvals.data_ptr(),
@@ -507,6 +508,21 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                 not getattr(tab, "bf16", False)):
             return "scalar"
         return None
+
+    def _srv_stream(self, host_side: bool) -> int:
+        """hipStream_t of the server stream for this stage, 0 for none.  A
+        stage with tensor-code hooks (a user pull method, a merged-rows push
+        the caller applies) runs on the caller's stream; the server stream is
+        then retired for good (the main stream first waits for it), so no
+        server update can reorder against a lookup."""
+        ss = getattr(self, "server_stream", None)
+        if ss is None:
+            return 0
+        if host_side:
+            torch.cuda.current_stream(self.device).wait_stream(ss)
+            self.server_stream = None
+            return 0
+        return ss.cuda_stream
 
     def fuse_apply(self, rnd: Round, snapshot: bool = True) -> Optional[dict]:
         """Arguments that let a model's gradient-merge kernel run the optimizer
@@ -586,12 +602,14 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             kind = self._server_update_kind()
             S = self.srv[slot] if self.srv is not None else None
             merged_only = S is not None and kind is None
+            ss = self._srv_stream(merged_only)
             self.native.push_xgmi(slot, self._tag, self.raw_stream(), g.data_ptr(),
                                   rnd.dd.ucount.data_ptr(), S is not None, kind is not None,
                                   tab.dt if S else self._nodt, tab.opt.native() if S else self._noop,
                                   self.rgrads[slot].data_ptr(), kind == "scalar",
                                   bool(S and S.snap_valid),
-                                  self.sgrad.data_ptr() if merged_only else 0, not merged_only)
+                                  self.sgrad.data_ptr() if merged_only else 0, not merged_only,
+                                  ss)
             if merged_only:
                 self._apply_merged(slot)
                 self._release(slot)

@@ -87,6 +87,10 @@ class EngineControl:
         st = self.raw_stream()
         if getattr(self, "_claimed", None):
             self._commit_claimed(st)
+        ss = getattr(self, "server_stream", None)
+        main = torch.cuda.current_stream(self.device)
+        if ss is not None:  # every enqueued server update before the lookup
+            main.wait_stream(ss)
         S = self.srv[q] if self.srv is not None else None
         for i in range(rounds):
             part = kd[i * cap:(i + 1) * cap]
@@ -109,11 +113,13 @@ class EngineControl:
                                   self.rmeta[q][1].data_ptr(),
                                   self.srv_err.data_ptr() if S else 0,
                                   self.svals.data_ptr() if S else 0, self.rvals.data_ptr(),
-                                  False, r.ucount.data_ptr(), [], False, False, False)
+                                  False, r.ucount.data_ptr(), [], False, False, False, 0)
             if m:
                 h.gather_rows(self.uvals[q].data_ptr(), r.inv.data_ptr(), m, self.dim,
                               out[i * cap:i * cap + m].data_ptr(), st)
             self.native.record(FREE, q, st, 0)
+        if ss is not None:  # later server updates after the lookup read the rows
+            ss.wait_stream(main)
         self.metrics.add(lookup_keys=n)
         return out.to(keys.device)
 

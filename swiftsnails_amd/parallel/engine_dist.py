@@ -119,6 +119,15 @@ class DeviceSetup:
         if self.claim:
             for dd in self.dedupers:
                 dd.rbits = self.srv_rbits
+        # the server half of every round (keys in, merge, lookup, rows out;
+        # gradients in, merge + update) on its own highest-priority stream: a
+        # slow compute on this rank's main stream does not hold up the rows
+        # every peer waits for (SS_SERVER_STREAM=0: on the main stream)
+        self.server_stream = None
+        if self.table is not None and self.xg is not None and \
+                os.environ.get("SS_SERVER_STREAM", "1") != "0":
+            lo_prio, hi_prio = torch.cuda.Stream.priority_range()
+            self.server_stream = torch.cuda.Stream(device=dev, priority=min(lo_prio, hi_prio))
         self.srv = None
         self.srv_ahead = os.environ.get("SS_SRV_AHEAD", "1") != "0"
         self._route_srv = None  # how the last route ran the keys-in (srv_ahead)

@@ -67,6 +67,10 @@ KNOBS: dict[str, Knob] = {
                              "scalar 16-byte LR slots: split the shard into 2^k probe regions "
                              "(>= 1024 slots each) so one dedup bucket owns its regions' inserts "
                              "(0: one region, every insert a device CAS)"),
+    "SS_SERVER_STREAM": Knob("1", "parallel/engine_dist.py", "tuning",
+                             "N>1 over xGMI: the server half of each round (keys in, merge, "
+                             "lookup, rows out; gradients in, merge + update) on its own "
+                             "highest-priority stream (0: on the main stream)"),
     "SS_CLAIM": Knob("1", "parallel/engine.py", "tuning",
                      "one GPU, region tables, synchronous rounds: the pull claims new keys' "
                      "slots in LDS and the fused merge stores [w | h | key] (0: CAS inserts)"),

@@ -41,6 +41,11 @@ def main() -> int:
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "profw"))
     ap.add_argument("--timeout", type=float, default=400.0)
     ap.add_argument("--no-prof", action="store_true", help="run the ranks without rocprofv3")
+    ap.add_argument("--pmc", default="",
+                    help="counter pass instead of the kernel stats: rocprofv3 --pmc <counters> "
+                         "(space-separated, one pass; <= 8 SQ / 4 TCC / 4 TCP per pass)")
+    ap.add_argument("--prof-ranks", default="all",
+                    help="ranks run under rocprofv3 (comma list or 'all'); the others run bare")
     ap.add_argument("--launch", action="store_true",
                     help="run python -m swiftsnails_amd.launch (config jobs) instead of bench.py")
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
@@ -56,13 +61,16 @@ def main() -> int:
                    MASTER_PORT=str(port), SS_BENCH_DEVICE="0", SS_DEVICE="0", TMPDIR="/tmp")
         bench = (["python3", "-m", "swiftsnails_amd.launch"] + args if a.launch else
                  ["python3", os.path.join(ROOT, "bench.py"), "--gpus", str(a.world)] + args)
-        if a.no_prof:
+        profiled = a.prof_ranks == "all" or str(r) in a.prof_ranks.split(",")
+        if a.no_prof or not profiled:
             cmd = bench
         else:
             d = os.path.join(a.out, f"rank{r}")
             os.makedirs(d, exist_ok=True)
-            cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", d,
-                   "-o", "run", "--"] + bench
+            what = (["--pmc"] + a.pmc.split() + ["--kernel-trace"] if a.pmc else
+                    ["--kernel-trace", "--stats"])
+            cmd = ["rocprofv3"] + what + ["--output-format", "csv", "-d", d, "-o", "run",
+                                          "--"] + bench
         os.makedirs(a.out, exist_ok=True)
         log = open(os.path.join(a.out, f"rank{r}.log"), "w")
         procs.append((subprocess.Popen(cmd, env=env, stdout=log, stderr=subprocess.STDOUT,
