@@ -149,12 +149,15 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("pull_claim_bk", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
                             uintptr_t ubase, int P_, uintptr_t slots32, uintptr_t out,
                             uintptr_t snap, const InitParams& ip, uintptr_t size_ctr,
-                            uintptr_t err, uintptr_t st) {
+                            uintptr_t err, uintptr_t st, uintptr_t luid, uintptr_t occ) {
     launch_pull_claim_bk(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
                          P<const uint32_t>(unum), P<const uint32_t>(ubase), P_, P<int>(slots32),
                          P<float>(out), P<float>(snap), ip, P<unsigned long long>(size_ctr),
-                         P<int>(err), S(st));
-  });
+                         P<int>(err), S(st), P<const uint32_t>(luid), P<float>(occ));
+  }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
+     py::arg("P"), py::arg("slots32"), py::arg("out"), py::arg("snap"), py::arg("ip"),
+     py::arg("size_ctr"), py::arg("err"), py::arg("st"), py::arg("luid") = 0,
+     py::arg("occ") = 0);
   m.def("commit_claims", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
                             uintptr_t ubase, int P_, uintptr_t slots32, uintptr_t snap,
                             uintptr_t st) {

@@ -207,7 +207,7 @@ class RoundEngine {
   void pull_fast(int slot, int tag, uintptr_t stream, bool wait_route, int prev, bool ahead,
                  const DevTable& t, const InitParams& ip, uintptr_t size_ctr, uintptr_t err, int G,
                  std::vector<uintptr_t> view, int P, uintptr_t uvals, uintptr_t slots,
-                 uintptr_t snap, int slot32, bool claim) {
+                 uintptr_t snap, int slot32, bool claim, uintptr_t luid, uintptr_t occ) {
     pull_waits(slot, tag, stream, wait_route, prev);
     if (view.size() != 4) throw std::invalid_argument("pull_fast: (bkeys, bstart, unum, ubase)");
     // claim: region-aligned buckets of a region table — LDS-claimed inserts,
@@ -215,8 +215,9 @@ class RoundEngine {
     if (claim)
       launch_pull_claim_bk(t, Pt<const uint64_t>(view[0]), Pt<const uint32_t>(view[1]),
                            Pt<const uint32_t>(view[2]), Pt<const uint32_t>(view[3]), P,
-                           Pt<int>(slots), Pt<float>(uvals), Pt<float>(snap), ip,
-                           Pt<unsigned long long>(size_ctr), Pt<int>(err), St(stream));
+                           Pt<int>(slots), occ ? nullptr : Pt<float>(uvals), Pt<float>(snap), ip,
+                           Pt<unsigned long long>(size_ctr), Pt<int>(err), St(stream),
+                           Pt<const uint32_t>(luid), Pt<float>(occ));
     else
       launch_pull_unique_bk(t, Pt<const uint64_t>(view[0]), Pt<const uint32_t>(view[1]),
                             Pt<const uint32_t>(view[2]), Pt<const uint32_t>(view[3]), P,

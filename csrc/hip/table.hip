@@ -339,12 +339,19 @@ __device__ __forceinline__ bool lds_claim(uint32_t* cl, uint32_t s) {
 }
 static_assert(kClaimTS == 1 << 13, "lds_claim hashes to 13 bits");
 
+// luid / occ (optional, the LR forward's one-gather mode): the bucket's
+// parameters also go to occ[p] = w(luid[p]) for its occurrence positions p
+// (k_bd_fill_occ fused: the rows staged in LDS, no uvals round trip); `out`
+// may then be null.
+static constexpr int kClaimMaxU = 4096;  // unique keys of a bucket (the dedup's LDS table)
 __global__ __launch_bounds__(kClaimT) void k_pull_claim_bk(
     DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
     const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
     int* __restrict__ slots32, float* __restrict__ out, float2* __restrict__ snap, InitParams ip,
-    unsigned long long* size_ctr, int* err) {
+    unsigned long long* size_ctr, int* err, const uint32_t* __restrict__ luid,
+    float* __restrict__ occ) {
   __shared__ uint32_t cl[kClaimTS];
+  __shared__ float sv[kClaimMaxU];
   for (int i = threadIdx.x; i < kClaimTS; i += kClaimT) cl[i] = 0xFFFFFFFFu;
   __syncthreads();
   const int b = blockIdx.x;
@@ -383,12 +390,31 @@ __global__ __launch_bounds__(kClaimT) void k_pull_claim_bk(
       wh.x = fresh_or(wh.x, ip, key, 0, 1);
       if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
     }
-    out[pos] = wh.x;
+    if (out) out[pos] = wh.x;
+    if (occ && l < (uint32_t)kClaimMaxU) sv[l] = wh.x;
     snap[pos] = wh;
     ins += inserted;
   }
   ins = wave_sum_u64(ins);
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
+  if (occ) {  // workgroup-uniform
+    __syncthreads();
+    const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+    const uint32_t nv = min(nu, (uint32_t)kClaimMaxU);
+    for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * kClaimT) {
+      uint32_t lu[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t p = pb + r * kClaimT;
+        lu[r] = p < p1 ? luid[p] : 0xFFFFFFFFu;
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const uint32_t p = pb + r * kClaimT;
+        if (p < p1) occ[p] = lu[r] < nv ? sv[lu[r]] : 0.f;
+      }
+    }
+  }
 }
 
 // The fallback writer of a claimed pull whose fused merge did not run (a
@@ -990,12 +1016,14 @@ static void check_claim_table(const DevTable& t) {
 void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                           const uint32_t* unum, const uint32_t* ubase, int P, int* slots32,
                           float* out, float* snap, const InitParams& ip,
-                          unsigned long long* size_ctr, int* err, hipStream_t st) {
+                          unsigned long long* size_ctr, int* err, hipStream_t st,
+                          const uint32_t* luid, float* occ) {
   if (P <= 0) return;
   check_claim_table(t);
-  if (!slots32 || !out || !snap) throw std::invalid_argument("claimed pull: slots, rows, snapshot");
+  if (!slots32 || !(out || occ) || !snap || (occ && !luid))
+    throw std::invalid_argument("claimed pull: slots, rows (or occurrence rows + luid), snapshot");
   hipLaunchKernelGGL(k_pull_claim_bk, dim3(P), dim3(kClaimT), 0, st, t, bkeys, bstart, unum, ubase,
-                     slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err);
+                     slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err, luid, occ);
   check_launch("k_pull_claim_bk");
 }
 

@@ -105,6 +105,7 @@ class SparseLRWorker(PipelinedWorker):
             # the one-GPU engine may claim new keys' slots in the pull and let
             # the merge store them (PSEngine.claim, table.hip k_pull_claim_bk)
             engine.claim_rounds = True
+            engine.claim_occ = self.occ  # ... and the claimed pull fills it (no fill_occ)
             for dd in engine.dedupers:
                 dd.zero_grad = False         # the LDS reduce stores every unique row
                 dd.materialize_inv = False   # the forward resolves occurrences itself
@@ -156,7 +157,8 @@ class SparseLRWorker(PipelinedWorker):
         xp = self.xval[slot].data_ptr() if self.xval is not None else 0
         if self.bucketed:
             o = dd.owner
-            o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
+            if not rnd.occ_filled:
+                o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)
             h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
                        rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1, self._acc.data_ptr(),
                        0, st, o.index_ptrs(dd.n), occ=self.occ.data_ptr())

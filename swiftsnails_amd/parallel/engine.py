@@ -78,6 +78,7 @@ class Round:
     applied: bool = False                 # the model's kernel already ran K5 (fuse_apply)
     slot32: bool = False                  # world-1: `slots` holds 4-byte indices (first half)
     deferred: bool = False                # world-1 claimed pull: new keys' slots not written yet
+    occ_filled: bool = False              # world-1 claimed pull also filled claim_occ
     server: Optional[object] = None       # CPU N>1: (unique keys, inverse) of the server merge
 
     @property
@@ -187,8 +188,11 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self._deferred_slot: Optional[int] = None
         self.claim = False
         # set by a caller whose every pulled round is pushed through the
-        # fused snapshot merge (SparseLRWorker): only its pulls claim
+        # fused snapshot merge (SparseLRWorker): only its pulls claim; and
+        # its occurrence-position parameter buffer, which a claimed pull
+        # fills itself (k_bd_fill_occ fused into k_pull_claim_bk)
         self.claim_rounds = False
+        self.claim_occ: Optional[torch.Tensor] = None
         if self.fast1:
             # pull snapshots for the blind-write apply (scalar AdaGrad rows)
             self.snapshot = bool(getattr(table, "snapshot_ok", False))
@@ -411,11 +415,14 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                 # by this round's merge, before the next pull on this stream)
                 claim = bool(s32 and self.claim and self.claim_rounds and dd.rbits and
                              dd.rbits == tab.rbits)
+                occ = self.claim_occ if claim else None
                 self.native.pull_fast(slot, self._tag, st, False, -1, ahead, tab.dt,
                                       tab._init_native, tab.size_ctr.data_ptr(),
                                       tab.err.data_ptr(), tab.G, list(v[:4]), v[4], uv.data_ptr(),
                                       self.slots[slot].data_ptr(),
-                                      snap.data_ptr() if snap is not None else 0, int(s32), claim)
+                                      snap.data_ptr() if snap is not None else 0, int(s32), claim,
+                                      own.luid.data_ptr() if occ is not None else 0,
+                                      occ.data_ptr() if occ is not None else 0)
                 if claim:
                     self._deferred_slot = slot
             elif getattr(own, "mode", None) == "bucket":
@@ -428,7 +435,8 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             self.metrics.add(occurrences=dd.n)
             rnd = Round(dd, uv, slot, slots=self.slots[slot], snap=snap,
                         snap_version=tab.version, ready=native and ahead, tag=self._tag,
-                        slot32=native and s32, deferred=claim)
+                        slot32=native and s32, deferred=claim,
+                        occ_filled=bool(claim and self.claim_occ is not None))
             if claim:
                 self._claimed.append(rnd)
             return rnd

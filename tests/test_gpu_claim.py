@@ -126,6 +126,23 @@ def test_claim_pull_then_commit(dev, init):
     np.testing.assert_array_equal(s_old.cpu().numpy(), sl[~is_new])
     keys_view = t.keys_view().cpu().numpy()
     assert (keys_view[sl[is_new]] == -1).all()  # claimed slots still EMPTY
+    # the fused occurrence fill (the LR forward's one-gather mode): the same
+    # pull again (it wrote nothing) with occ[p] = w(luid[p]) and no uvals
+    occ_t = torch.full((len(occ),), -5.0, device=dev)
+    snap2 = torch.zeros_like(snap)
+    ctr2 = torch.zeros_like(t.size_ctr)  # its insert count goes elsewhere
+    h.pull_claim_bk(t.dt, bk, bs, un, ub, P, slots.data_ptr(), 0, snap2.data_ptr(),
+                    t._init_native, ctr2.data_ptr(), t.err.data_ptr(),
+                    torch.cuda.current_stream().cuda_stream, dd.luid.data_ptr(), occ_t.data_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(snap2, snap) and int(ctr2.sum()) == int(is_new.sum())
+    luid = dd.luid.cpu().numpy().view(np.uint32)
+    on = out.cpu().numpy()
+    want = np.zeros(len(occ), dtype=np.float32)
+    for b in range(P):
+        p0, p1 = bstart[b], bstart[b + 1]
+        want[p0:p1] = on[ub0[b] + luid[p0:p1].astype(np.int64)]
+    np.testing.assert_array_equal(occ_t.cpu().numpy(), want)
     h.commit_claims(t.dt, bk, bs, un, ub, P, slots.data_ptr(), snap.data_ptr(),
                     torch.cuda.current_stream().cuda_stream)
     vals, s2 = t.pull(torch.from_numpy(uk).to(dev), insert=False)
