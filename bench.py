@@ -101,6 +101,11 @@ def main(argv=None):
     dev_idx = int(os.environ.get("SS_BENCH_DEVICE", local_rank))
     torch.cuda.set_device(dev_idx)
     dev = torch.device("cuda", dev_idx)
+    # SS_MAIN_PRIO=1: the step's main stream (pull, model kernels, push) at
+    # the highest stream priority, above the route stream's dedup
+    if os.environ.get("SS_MAIN_PRIO", "0") != "0":
+        lo, hi = torch.cuda.Stream.priority_range()
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=min(lo, hi)))
 
     from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, lr_init, make_lr_table
     from swiftsnails_amd.ops.optim import Optimizer

@@ -375,6 +375,29 @@ void bind_xgmi(py::module_& m) {
   m.def("spin_us", [](double us, uintptr_t st) {
     ss::launch_spin(us, reinterpret_cast<hipStream_t>(st));
   });
+  // a stream whose kernels run on `ncus` of the device's CUs only (spread
+  // evenly over the CU ids, so every XCD keeps some): the route stream's
+  // dedup kernels then leave the other CUs to the main stream's
+  // latency-bound table kernels (SS_ROUTE_CUS).  `priority`: the stream's
+  // priority (hipStreamCreateWithPriority semantics; 0 = default).  Never
+  // destroyed: it lives as long as the engine that wraps it.
+  m.def("cu_stream", [](int device, int ncus, int invert) {
+    ss::check_hip(hipSetDevice(device), "hipSetDevice");
+    int total = 0;
+    ss::check_hip(hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device),
+                  "CU count");
+    if (ncus < 1 || ncus > total) throw std::invalid_argument("cu_stream: 1..CU count CUs");
+    std::vector<uint32_t> mask((total + 31) / 32, invert ? 0xFFFFFFFFu : 0u);
+    for (int k = 0; k < ncus; ++k) {
+      const int cu = (int)((long long)k * total / ncus);
+      if (invert) mask[cu / 32] &= ~(1u << (cu % 32));
+      else mask[cu / 32] |= 1u << (cu % 32);
+    }
+    hipStream_t st = nullptr;
+    ss::check_hip(hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()),
+                  "hipExtStreamCreateWithCUMask");
+    return reinterpret_cast<uintptr_t>(st);
+  }, py::arg("device"), py::arg("ncus"), py::arg("invert") = 0);
   m.def("device_pci_id", [](int device) {
     char buf[64] = {0};
     ss::check_hip(hipDeviceGetPCIBusId(buf, sizeof(buf), device), "hipDeviceGetPCIBusId");

@@ -174,7 +174,7 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self._dix = (self.device.index or 0) if self.gpu else -1
         self.native = None
         if self.gpu:
-            self.route_stream = torch.cuda.Stream(device=dev)
+            self.route_stream = self._make_route_stream(dev)
             # + one slot past the ring: the N>1 read-only lookup's round
             # (PSEngine.lookup) never touches a ring slot the pipeline holds
             self.native = _hip().RoundEngine(self.depth + 1, self._dix)
@@ -247,6 +247,16 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             self.pull_ahead = True
             if self.gpu and not self.shared_device:
                 self.pull_stream = torch.cuda.Stream(device=self.device)
+
+    def _make_route_stream(self, dev) -> torch.cuda.Stream:
+        """The route stream; SS_ROUTE_CUS=n: restricted to n of the device's
+        CUs (a CU-masked HIP stream), so the dedup's large workgroups leave
+        the remaining CUs to the main stream's latency-bound table kernels."""
+        n = int(os.environ.get("SS_ROUTE_CUS", "0") or 0)
+        if n <= 0:
+            return torch.cuda.Stream(device=dev)
+        ptr = _hip().cu_stream(dev.index or 0, n, 0)
+        return torch.cuda.ExternalStream(ptr, device=dev)
 
     def last_route_matches(self) -> bool:
         """The last routed round ran the keys-in as a route issued now would

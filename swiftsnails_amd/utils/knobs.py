@@ -71,6 +71,11 @@ KNOBS: dict[str, Knob] = {
                              "N>1 over xGMI: the server half of each round (keys in, merge, "
                              "lookup, rows out; gradients in, merge + update) on its own "
                              "highest-priority stream (0: on the main stream)"),
+    "SS_MAIN_PRIO": Knob("0", "bench.py", "experiment",
+                         "1: bench.py runs the step's main stream at the highest stream priority"),
+    "SS_ROUTE_CUS": Knob("0", "parallel/engine.py", "experiment",
+                         "n > 0: the route stream runs on n of the device's CUs (CU-masked "
+                         "stream), leaving the rest to the main stream"),
     "SS_CLAIM": Knob("1", "parallel/engine.py", "tuning",
                      "one GPU, region tables, synchronous rounds: the pull claims new keys' "
                      "slots in LDS and the fused merge stores [w | h | key] (0: CAS inserts)"),
