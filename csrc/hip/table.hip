@@ -344,7 +344,8 @@ static_assert(kClaimTS == 1 << 13, "lds_claim hashes to 13 bits");
 // (k_bd_fill_occ fused: the rows staged in LDS, no uvals round trip); `out`
 // may then be null.
 static constexpr int kClaimMaxU = 4096;  // unique keys of a bucket (the dedup's LDS table)
-__global__ __launch_bounds__(kClaimT) void k_pull_claim_bk(
+template <int CT>
+__global__ __launch_bounds__(CT) void k_pull_claim_bk(
     DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
     const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
     int* __restrict__ slots32, float* __restrict__ out, float2* __restrict__ snap, InitParams ip,
@@ -352,13 +353,13 @@ __global__ __launch_bounds__(kClaimT) void k_pull_claim_bk(
     float* __restrict__ occ) {
   __shared__ uint32_t cl[kClaimTS];
   __shared__ float sv[kClaimMaxU];
-  for (int i = threadIdx.x; i < kClaimTS; i += kClaimT) cl[i] = 0xFFFFFFFFu;
+  for (int i = threadIdx.x; i < kClaimTS; i += CT) cl[i] = 0xFFFFFFFFu;
   __syncthreads();
   const int b = blockIdx.x;
   const uint32_t nu = unum[b], base = ubase[b];
   const uint64_t* src = bkeys + bstart[b];
   unsigned long long ins = 0;
-  for (uint32_t l = threadIdx.x; l < nu; l += kClaimT) {
+  for (uint32_t l = threadIdx.x; l < nu; l += CT) {
     const uint64_t key = src[l];
     long long slot = -1;
     bool inserted = false;
@@ -401,16 +402,16 @@ __global__ __launch_bounds__(kClaimT) void k_pull_claim_bk(
     __syncthreads();
     const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
     const uint32_t nv = min(nu, (uint32_t)kClaimMaxU);
-    for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * kClaimT) {
+    for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * CT) {
       uint32_t lu[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint32_t p = pb + r * kClaimT;
+        const uint32_t p = pb + r * CT;
         lu[r] = p < p1 ? luid[p] : 0xFFFFFFFFu;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const uint32_t p = pb + r * kClaimT;
+        const uint32_t p = pb + r * CT;
         if (p < p1) occ[p] = lu[r] < nv ? sv[lu[r]] : 0.f;
       }
     }
@@ -1022,8 +1023,20 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
   check_claim_table(t);
   if (!slots32 || !(out || occ) || !snap || (occ && !luid))
     throw std::invalid_argument("claimed pull: slots, rows (or occurrence rows + luid), snapshot");
-  hipLaunchKernelGGL(k_pull_claim_bk, dim3(P), dim3(kClaimT), 0, st, t, bkeys, bstart, unum, ubase,
-                     slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err, luid, occ);
+  // workgroup size (SS_CLAIM_T: 256 / 512 / 1024): one workgroup per bucket
+  static const int ct = [] {
+    const char* e = std::getenv("SS_CLAIM_T");
+    const int v = e ? std::atoi(e) : kClaimT;
+    return (v == 256 || v == 512) ? v : 1024;
+  }();
+#define SS_CLAIM_LAUNCH(CT)                                                                     \
+  hipLaunchKernelGGL(k_pull_claim_bk<CT>, dim3(P), dim3(CT), 0, st, t, bkeys, bstart, unum,     \
+                     ubase, slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err, luid, \
+                     occ)
+  if (ct == 256) SS_CLAIM_LAUNCH(256);
+  else if (ct == 512) SS_CLAIM_LAUNCH(512);
+  else SS_CLAIM_LAUNCH(1024);
+#undef SS_CLAIM_LAUNCH
   check_launch("k_pull_claim_bk");
 }
 
