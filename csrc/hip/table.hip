@@ -321,7 +321,10 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
 // Until that store a claimed slot still reads EMPTY: every consumer of the
 // table is stream-ordered after it (PSEngine defers only synchronous
 // one-GPU rounds; launch_commit_claims is the fallback writer).
-static constexpr int kClaimT = 1024;  // threads per bucket workgroup
+// threads per bucket workgroup (SS_CLAIM_T): 256 measured 0.795-0.798 ms
+// per bench step against 0.832-0.835 (512) and 0.843-0.844 (1024) on one
+// box — small workgroups interleave with the route stream's kernels
+static constexpr int kClaimT = 256;
 static constexpr int kClaimTS = 8192;  // LDS claim slots (>= 2x the <= 4096 keys of a bucket)
 __device__ __forceinline__ bool lds_claim(uint32_t* cl, uint32_t s) {
   uint32_t i = (s * 0x9E3779B1u) >> (32 - 13);  // 13 = log2(kClaimTS)
@@ -1027,13 +1030,15 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
   static const int ct = [] {
     const char* e = std::getenv("SS_CLAIM_T");
     const int v = e ? std::atoi(e) : kClaimT;
-    return (v == 256 || v == 512) ? v : 1024;
+    return (v == 64 || v == 128 || v == 512 || v == 1024) ? v : 256;
   }();
 #define SS_CLAIM_LAUNCH(CT)                                                                     \
   hipLaunchKernelGGL(k_pull_claim_bk<CT>, dim3(P), dim3(CT), 0, st, t, bkeys, bstart, unum,     \
                      ubase, slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err, luid, \
                      occ)
   if (ct == 256) SS_CLAIM_LAUNCH(256);
+  else if (ct == 64) SS_CLAIM_LAUNCH(64);
+  else if (ct == 128) SS_CLAIM_LAUNCH(128);
   else if (ct == 512) SS_CLAIM_LAUNCH(512);
   else SS_CLAIM_LAUNCH(1024);
 #undef SS_CLAIM_LAUNCH

@@ -122,6 +122,13 @@ class PipelinedWorker:
         # holds pulled-ahead rounds: a capture would record drain steps, not
         # the periodic synchronous step
         self.drain()
+        # replays run the server half of a round on the main stream (a
+        # capture that forked the server stream ended in a crash inside
+        # hipStreamEndCapture on the N>1 xGMI path)
+        ss = getattr(eng, "server_stream", None)
+        if ss is not None:
+            torch.cuda.current_stream(eng.device).wait_stream(ss)
+            eng.server_stream = None
         if self._next is None:
             self.step()  # prime the lookahead pipeline eagerly
         # N>1: a captured pull runs the keys wait and the server merge unless
@@ -165,8 +172,7 @@ class PipelinedWorker:
                     eng.capture_tag = p + 1
                     # fork the route stream into the capture at the start (no
                     # ordering: its work overlaps the whole step)
-                    side = [x for x in (eng.route_stream, eng.pull_stream,
-                                        getattr(eng, "server_stream", None)) if x is not None]
+                    side = [x for x in (eng.route_stream, eng.pull_stream) if x is not None]
                     for x in side:
                         x.wait_stream(torch.cuda.current_stream())
                     self._cap_base = self.step_idx  # what the counter holds at replay

@@ -76,8 +76,9 @@ KNOBS: dict[str, Knob] = {
     "SS_ROUTE_CUS": Knob("0", "parallel/engine.py", "experiment",
                          "n > 0: the route stream runs on n of the device's CUs (CU-masked "
                          "stream), leaving the rest to the main stream"),
-    "SS_CLAIM_T": Knob("1024", "csrc/hip/table.hip", "tuning",
-                       "claimed pull: threads per bucket workgroup (256 / 512 / 1024)"),
+    "SS_CLAIM_T": Knob("256", "csrc/hip/table.hip", "tuning",
+                       "claimed pull: threads per bucket workgroup (256 / 512 / 1024: 0.795 / "
+                       "0.833 / 0.843 ms per bench step on one box)"),
     "SS_CLAIM": Knob("1", "parallel/engine.py", "tuning",
                      "one GPU, region tables, synchronous rounds: the pull claims new keys' "
                      "slots in LDS and the fused merge stores [w | h | key] (0: CAS inserts)"),
