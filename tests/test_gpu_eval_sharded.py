@@ -114,6 +114,8 @@ def test_sharded_eval_matches_world1(world, mode, env, bound):
     ev, n = _world(world, env)
     assert ev["samples"] == 2 * B
     assert ev["pull_ahead"] == (mode != "sync")
-    assert n == n1  # the same keys trained, each on exactly one shard
+    # the same keys trained, each on exactly one shard; pulled-ahead rounds
+    # have also inserted the keys of the rounds pulled past the last step
+    assert n == n1 if mode == "sync" else n1 <= n < 1.1 * n1
     assert abs(ev["auc"] - ref["auc"]) < bound, (world, mode, ev, ref)
     assert abs(ev["auc_truth"] - ref["auc_truth"]) < 1e-9
