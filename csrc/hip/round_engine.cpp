@@ -324,7 +324,7 @@ class RoundEngine {
   void push_xgmi(int slot, int tag, uintptr_t stream, uintptr_t grads, uintptr_t ucount,
                  bool table, bool update, const DevTable& t, const OptParams& op, uintptr_t rgrads,
                  bool scalar_fused, bool snap, uintptr_t merged, bool release,
-                 uintptr_t srv_stream) {
+                 uintptr_t srv_stream, uintptr_t gstage) {
     check_xgmi();
     std::vector<std::vector<long long>> parts;
     parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_, self_bypass()));
@@ -343,6 +343,15 @@ class RoundEngine {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
       const SelfSeg sg = self_seg(grads);  // this rank's own gradient rows, in place
+      // the peers' gradient rows streamed out of the uncached mailbox into a
+      // cached buffer first: the merge gathers them per received position
+      if (gstage && nranks_ > 1) {
+        launch_xstage(Pt<const char>(rgrads),
+                      Pt<const long long>(ar_[slot][2]->base() + grads_[slot].hdr), nranks_,
+                      grads_[slot].seg, 4 * dim_, sg.ptr ? rank_ : -1, Pt<char>(gstage),
+                      St(stream));
+        rgrads = gstage;
+      }
       if (srv_s32_[slot] && !(update && scalar_fused && snap))
         throw std::logic_error("push_xgmi: a 4-byte-slot pull needs the fused snapshot merge");
       if (srv_claim_[slot] && !(update && scalar_fused && snap))

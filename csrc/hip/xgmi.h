@@ -98,6 +98,9 @@ void launch_xwait(char* arena, const XWait& W, unsigned long long* waited, unsig
                   hipStream_t st);
 // litmus patterns: word i of a segment = mix(seed, i); check counts mismatches
 void launch_xpattern(int* dst, long long words, unsigned seed, hipStream_t st);
+// received rows out of the uncached mailbox into a cached buffer (k_xstage)
+void launch_xstage(const char* src, const long long* cnt, int nsrc, long long seg_bytes,
+                   int row_bytes, int skip, char* dst, hipStream_t st);
 void launch_xcheck(const int* src, long long words, unsigned seed, int* bad, hipStream_t st);
 void launch_spin(double us, hipStream_t st);
 

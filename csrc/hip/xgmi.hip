@@ -224,6 +224,39 @@ __device__ __forceinline__ int xpattern_word(unsigned seed, long long i) {
   return (int)x;
 }
 
+// Received segments out of the (uncached) mailbox into a cached buffer at
+// the same offsets: source s's first cnt[s] rows of row_bytes each, at byte
+// s * seg_bytes, streamed with 16-byte accesses (every source but `skip`, the
+// rank's own segment, which its consumer reads in place).  The server's
+// gradient merge then gathers per received position from L2 / MALL instead
+// of one uncached memory transaction per 4-byte gather.
+__global__ __launch_bounds__(256) void k_xstage(const char* __restrict__ src,
+                                                const long long* __restrict__ cnt,
+                                                long long seg_bytes, int row_bytes, int skip,
+                                                char* __restrict__ dst) {
+  const int s = blockIdx.y;
+  if (s == skip) return;  // block-uniform
+  const long long n = cnt[s] * (long long)row_bytes;
+  const long long nv = n / 16;
+  const uint4* sv = reinterpret_cast<const uint4*>(src + s * seg_bytes);
+  uint4* dv = reinterpret_cast<uint4*>(dst + s * seg_bytes);
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < nv;
+       i += (long long)gridDim.x * 256)
+    dv[i] = sv[i];
+  const long long tail = n - nv * 16;  // whole 4-byte words (row_bytes % 4 == 0)
+  if (blockIdx.x == 0 && threadIdx.x < tail / 4)
+    reinterpret_cast<uint32_t*>(dst + s * seg_bytes + nv * 16)[threadIdx.x] =
+        reinterpret_cast<const uint32_t*>(src + s * seg_bytes + nv * 16)[threadIdx.x];
+}
+
+void launch_xstage(const char* src, const long long* cnt, int nsrc, long long seg_bytes,
+                   int row_bytes, int skip, char* dst, hipStream_t st) {
+  if (nsrc < 1 || row_bytes % 4 || seg_bytes % 16) throw_error("xstage: layout");
+  hipLaunchKernelGGL(k_xstage, dim3(128, nsrc), dim3(256), 0, st, src, cnt, seg_bytes, row_bytes,
+                     skip, dst);
+  check_launch("k_xstage");
+}
+
 __global__ __launch_bounds__(256) void k_xpattern(int* dst, long long words, unsigned seed) {
   for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < words;
        i += (long long)gridDim.x * 256)

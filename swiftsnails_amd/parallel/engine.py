@@ -627,7 +627,9 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                                   self.rgrads[slot].data_ptr(), kind == "scalar",
                                   bool(S and S.snap_valid),
                                   self.sgrad.data_ptr() if merged_only else 0, not merged_only,
-                                  ss)
+                                  ss, self.gstage.data_ptr()
+                                  if S is not None and getattr(self, "gstage", None) is not None
+                                  else 0)
             if merged_only:
                 self._apply_merged(slot)
                 self._release(slot)

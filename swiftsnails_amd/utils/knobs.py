@@ -67,10 +67,11 @@ KNOBS: dict[str, Knob] = {
                              "scalar 16-byte LR slots: split the shard into 2^k probe regions "
                              "(>= 1024 slots each) so one dedup bucket owns its regions' inserts "
                              "(0: one region, every insert a device CAS)"),
-    "SS_SERVER_STREAM": Knob("1", "parallel/engine_dist.py", "tuning",
+    "SS_SERVER_STREAM": Knob("auto", "parallel/engine_dist.py", "tuning",
                              "N>1 over xGMI: the server half of each round (keys in, merge, "
                              "lookup, rows out; gradients in, merge + update) on its own "
-                             "highest-priority stream (0: on the main stream)"),
+                             "highest-priority stream; auto = when every rank has its own "
+                             "device, 1 = always, 0 = on the main stream"),
     "SS_MAIN_PRIO": Knob("0", "bench.py", "experiment",
                          "1: bench.py runs the step's main stream at the highest stream priority"),
     "SS_ROUTE_CUS": Knob("0", "parallel/engine.py", "experiment",
@@ -79,6 +80,10 @@ KNOBS: dict[str, Knob] = {
     "SS_CLAIM_T": Knob("256", "csrc/hip/table.hip", "tuning",
                        "claimed pull: threads per bucket workgroup (256 / 512 / 1024: 0.795 / "
                        "0.833 / 0.843 ms per bench step on one box)"),
+    "SS_SRV_STAGE": Knob("1", "parallel/engine_dist.py", "tuning",
+                         "N>1 xGMI servers: stream the peers' gradient rows out of the uncached "
+                         "mailbox into a cached buffer before the merge gathers them (0: gather "
+                         "from the mailbox)"),
     "SS_CLAIM": Knob("1", "parallel/engine.py", "tuning",
                      "one GPU, region tables, synchronous rounds: the pull claims new keys' "
                      "slots in LDS and the fused merge stores [w | h | key] (0: CAS inserts)"),

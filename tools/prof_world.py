@@ -46,6 +46,8 @@ def main() -> int:
                          "(space-separated, one pass; <= 8 SQ / 4 TCC / 4 TCP per pass)")
     ap.add_argument("--prof-ranks", default="all",
                     help="ranks run under rocprofv3 (comma list or 'all'); the others run bare")
+    ap.add_argument("--script", default="",
+                    help="run this python script (repo-relative) per rank instead of bench.py")
     ap.add_argument("--launch", action="store_true",
                     help="run python -m swiftsnails_amd.launch (config jobs) instead of bench.py")
     ap.add_argument("bench_args", nargs=argparse.REMAINDER)
@@ -60,6 +62,7 @@ def main() -> int:
                    LOCAL_WORLD_SIZE=str(a.world), MASTER_ADDR="127.0.0.1",
                    MASTER_PORT=str(port), SS_BENCH_DEVICE="0", SS_DEVICE="0", TMPDIR="/tmp")
         bench = (["python3", "-m", "swiftsnails_amd.launch"] + args if a.launch else
+                 ["python3", os.path.join(ROOT, a.script)] + args if a.script else
                  ["python3", os.path.join(ROOT, "bench.py"), "--gpus", str(a.world)] + args)
         profiled = a.prof_ranks == "all" or str(r) in a.prof_ranks.split(",")
         if a.no_prof or not profiled:
