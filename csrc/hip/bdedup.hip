@@ -65,7 +65,11 @@ static constexpr uint32_t kBdInvalid = 0xFFFFFFFFu;
 static constexpr int kBdMaxChunk = 8192;  // occurrences per count/scatter workgroup
 static constexpr int kBdChunkLanes = 1024;  // chunk granularity (any CT below divides it)
 static constexpr int kBdDT = 512;         // dedup workgroup size
-static constexpr int kBdTarget = 2048;  // target occurrences per bucket
+// target occurrences per bucket (one rank; SS_BD_TARGET): 3584 measured
+// 0.774-0.785 ms per bench step against 0.790-0.791 (3072) and 0.801-0.806
+// (2048) with claimed pulls — longer (chunk, bucket) runs in the scatter,
+// fewer and fuller claimed-pull workgroups
+static constexpr int kBdTarget = 3584;
 // N>1: a server merges bucket k of every source (server.hip), so a source's
 // bucket must stay small enough that N of them fit one server workgroup's
 // table after its sub-bucket split

@@ -148,12 +148,18 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self.max_keys = int(max_keys) if not (self.gpu and self.dist) else \
             -(-int(max_keys) // 64) * 64
         # ring depth 4 (measured 1.008 vs 1.018 ms/step for 3, LR on one
-        # GPU); 3 when a fourth slot would take more than 1/8 of the device
+        # GPU); 3 when a fourth slot would take more than 1/8 of the device.
+        # One GPU: 8 — the route stream then runs further ahead of the main
+        # stream (bench 0.774-0.780 vs 0.785-0.794 ms/step with 3584-key
+        # buckets); N>1 keeps 4 (every slot is a set of IPC-mapped mailboxes)
         if depth is None and os.environ.get("SS_ENGINE_DEPTH") is None:
-            depth = 4
-            if self.gpu and 4 * self.slot_bytes(self.world, max_keys, dim) > \
-                    torch.cuda.mem_get_info(self.device)[1] // 8:
-                depth = 3
+            fast = (self.gpu and self.world == 1 and isinstance(self.t, LoopbackTransport)
+                    and os.environ.get("SS_ENGINE_GENERAL", "0") == "0")
+            depth = 8 if fast else 4
+            budget = torch.cuda.mem_get_info(self.device)[1] // 8 if self.gpu else 0
+            while self.gpu and depth > 3 and \
+                    depth * self.slot_bytes(self.world, max_keys, dim) > budget:
+                depth = 4 if depth > 4 else 3
         self.depth = max(1, int(depth if depth is not None else
                                 os.environ.get("SS_ENGINE_DEPTH", "4")))
         # observability: occurrences routed, unique keys exchanged,

@@ -48,9 +48,9 @@ KNOBS: dict[str, Knob] = {
     "SS_NO_AUTOBUILD": Knob("0", "_native.py", "build",
                             "1: never build on import; a missing extension is an error"),
     # -- engine / table (defaults are the measured best)
-    "SS_ENGINE_DEPTH": Knob("4", "parallel/engine.py", "tuning",
-                            "route-buffer ring depth (>= 3 for pull-ahead; 4 measured 1.008 vs "
-                            "1.018 ms/step for 3, four A/B pairs)"),
+    "SS_ENGINE_DEPTH": Knob("8 one GPU, 4 N>1", "parallel/engine.py", "tuning",
+                            "route-buffer ring depth (>= 3 for pull-ahead; one GPU 8 vs 4: "
+                            "0.791-0.797 vs 0.802-0.806 ms/step; 4 vs 3: 1.008 vs 1.018)"),
     "SS_PULL_AHEAD": Knob("auto", "parallel/engine.py", "tuning",
                           "pull rounds i+1..i+k while round i computes: auto = the models that "
                           "opt in (FM, word2vec), and at N>1 the bench / launcher calibration "
@@ -107,8 +107,9 @@ KNOBS: dict[str, Knob] = {
     "SS_PULL_VEC": Knob("1", "csrc/hip/table.hip", "tuning",
                         "wide fp32 rows (dim 32/64/128): pull and apply with 8 lanes per key "
                         "and 16-byte row vectors (0: one lane group per key)"),
-    "SS_BD_TARGET": Knob("2048", "csrc/hip/bdedup.hip", "tuning",
-                         "one rank: target occurrences per dedup bucket (1024..3584)"),
+    "SS_BD_TARGET": Knob("3584", "csrc/hip/bdedup.hip", "tuning",
+                         "one rank: target occurrences per dedup bucket (1024..3584; 3584 / 3072 "
+                         "/ 2048: 0.774-0.785 / 0.790 / 0.801-0.806 ms per bench step)"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
