@@ -746,14 +746,15 @@ def _bench_1gpu(extra):
 
 def test_bench_graph_mode_times_whole_periods():
     """bench.py --graph on: the timed region runs exactly --steps steps.  With
-    12 timed steps the graph holds 12 steps (3 ring periods) and the warm-up
-    one graph, so the job runs warmup + 12 + 12 steps in all — the same
-    training as an eager run of warmup + 24 steps (identical final loss)."""
+    16 timed steps the graph holds 16 steps (2 ring periods of the one-GPU
+    8-slot ring, or 4 of a 4-slot one) and the warm-up one graph, so the job
+    runs warmup + 16 + 16 steps in all — the same training as an eager run of
+    warmup + 32 steps (identical final loss)."""
     base = ["--batch", "4096", "--features", "2000000", "--warmup", "3"]
-    g = _bench_1gpu(base + ["--steps", "12", "--graph", "on"])
-    e = _bench_1gpu(base + ["--steps", "24"])
+    g = _bench_1gpu(base + ["--steps", "16", "--graph", "on"])
+    e = _bench_1gpu(base + ["--steps", "32"])
     assert g["config"]["hipgraph"] is True and e["config"]["hipgraph"] is False
-    assert g["steps"] == 12 and g["ms_per_step"] > 0
+    assert g["steps"] == 16 and g["ms_per_step"] > 0
     assert g["config"]["loss_last"] == pytest.approx(e["config"]["loss_last"], rel=1e-4, abs=1e-5)
 
 
