@@ -149,13 +149,14 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             -(-int(max_keys) // 64) * 64
         # ring depth 4 (measured 1.008 vs 1.018 ms/step for 3, LR on one
         # GPU); 3 when a fourth slot would take more than 1/8 of the device.
-        # One GPU: 8 — the route stream then runs further ahead of the main
-        # stream (bench 0.774-0.780 vs 0.785-0.794 ms/step with 3584-key
-        # buckets); N>1 keeps 4 (every slot is a set of IPC-mapped mailboxes)
+        # One GPU, scalar LR rows: 8 — the route stream then runs further
+        # ahead of the main stream (bench 0.774-0.780 vs 0.785-0.794 ms/step
+        # with 3584-key buckets; word2vec 0.089 vs 0.091, FM unchanged: 4);
+        # N>1 keeps 4 (every slot is a set of IPC-mapped mailboxes)
         if depth is None and os.environ.get("SS_ENGINE_DEPTH") is None:
             fast = (self.gpu and self.world == 1 and isinstance(self.t, LoopbackTransport)
                     and os.environ.get("SS_ENGINE_GENERAL", "0") == "0")
-            depth = 8 if fast else 4
+            depth = 8 if fast and getattr(table, "snapshot_ok", False) else 4
             budget = torch.cuda.mem_get_info(self.device)[1] // 8 if self.gpu else 0
             while self.gpu and depth > 3 and \
                     depth * self.slot_bytes(self.world, max_keys, dim) > budget:
