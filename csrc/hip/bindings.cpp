@@ -166,11 +166,12 @@ PYBIND11_MODULE(_ss_hip, m) {
                          P<const int>(slots32), P<const float>(snap), S(st));
   });
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
-                    long long max_n, const OptParams& op, int G, uintptr_t st, uintptr_t snap) {
+                    long long max_n, const OptParams& op, int G, uintptr_t st, uintptr_t snap,
+                    uintptr_t only) {
     launch_apply(t, P<const long long>(slots), P<const float>(grads), sl, max_n, op, G, S(st),
-                 P<const float>(snap));
+                 P<const float>(snap), P<const uint8_t>(only));
   }, py::arg("t"), py::arg("slots"), py::arg("grads"), py::arg("sl"), py::arg("max_n"),
-     py::arg("op"), py::arg("G"), py::arg("st"), py::arg("snap") = 0);
+     py::arg("op"), py::arg("G"), py::arg("st"), py::arg("snap") = 0, py::arg("only") = 0);
   m.def("assign", [](const DevTable& t, uintptr_t keys, uintptr_t rows, long long n,
                      uintptr_t size_ctr, uintptr_t err, int G, uintptr_t st) {
     launch_assign(t, P<const uint64_t>(keys), P<const float>(rows), n,
@@ -491,23 +492,28 @@ PYBIND11_MODULE(_ss_hip, m) {
                   P<float>(gpair), P<float>(loss), P<float>(pairs), S(st), P<float>(gnc));
   });
   m.def("w2v_osort", [](int P_, uintptr_t bstart, uintptr_t unum, uintptr_t ubase, uintptr_t pj,
-                        uintptr_t luid, uintptr_t ord, uintptr_t items, uintptr_t st) {
+                        uintptr_t luid, uintptr_t ord, uintptr_t items, uintptr_t st,
+                        uintptr_t uhot) {
     launch_w2v_osort(P_, P<const uint32_t>(bstart), P<const uint32_t>(unum),
                      P<const uint32_t>(ubase), P<const uint32_t>(pj), P<const uint32_t>(luid),
-                     P<uint32_t>(ord), P<uint32_t>(items), S(st));
-  });
+                     P<uint32_t>(ord), P<uint32_t>(items), S(st), P<uint8_t>(uhot));
+  }, py::arg("P"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"), py::arg("pj"),
+     py::arg("luid"), py::arg("ord"), py::arg("items"), py::arg("st"), py::arg("uhot") = 0);
   m.def("w2v_oreduce", [](uintptr_t items, long long n, uintptr_t ord, uintptr_t ograd,
                           uintptr_t otail, int B, int W, int D, uintptr_t ugrad, uintptr_t st,
                           uintptr_t gnc, long long negbase, uintptr_t uvals, uintptr_t acc,
-                          uintptr_t acc_out, int acc_n) {
+                          uintptr_t acc_out, int acc_n, std::optional<DevTable> t,
+                          uintptr_t slots, std::optional<OptParams> op) {
     launch_w2v_oreduce(P<const uint32_t>(items), n, P<const uint32_t>(ord), P<const float>(ograd),
                        P<const float>(otail), B, W, D, P<float>(ugrad), S(st),
                        P<const float>(gnc), negbase, P<const float>(uvals), P<float>(acc),
-                       P<float>(acc_out), acc_n);
+                       P<float>(acc_out), acc_n, t ? &*t : nullptr, P<const long long>(slots),
+                       op ? &*op : nullptr);
   }, py::arg("items"), py::arg("n"), py::arg("ord"), py::arg("ograd"), py::arg("otail"),
      py::arg("B"), py::arg("W"), py::arg("D"), py::arg("ugrad"), py::arg("st"),
      py::arg("gnc") = 0, py::arg("negbase") = 0, py::arg("uvals") = 0, py::arg("acc") = 0,
-     py::arg("acc_out") = 0, py::arg("acc_n") = 0);
+     py::arg("acc_out") = 0, py::arg("acc_n") = 0, py::arg("t") = py::none(),
+     py::arg("slots") = 0, py::arg("op") = py::none());
   m.def("w2v_stream_gen", [](uint64_t seed, long long base, int B, int W, int L, long long nneg,
                              long long V, float noise, uintptr_t keys, uintptr_t meta, uintptr_t st,
                              uintptr_t step_dev, long long step_mul, long long step_add) {

@@ -50,9 +50,10 @@ void launch_lookup_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* 
 void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                           const uint32_t* unum, const uint32_t* ubase, int P, const int* slots32,
                           const float* snap, hipStream_t st);
+// only (optional): apply only at positions with only[pos] != 0 (wide rows)
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
-                  const float* snap = nullptr);
+                  const float* snap = nullptr, const uint8_t* only = nullptr);
 void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, long long n,
                    unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,
@@ -110,7 +111,7 @@ void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t
                     hipStream_t st, float* ograd = nullptr, float* otail = nullptr);
 void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const uint32_t* ubase,
                       const uint32_t* pj, const uint32_t* luid, uint32_t* ord, uint32_t* items,
-                      hipStream_t st);
+                      hipStream_t st, uint8_t* uhot = nullptr);
 void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                    const int32_t* meta, int B, int W, int K, int D, const float* uvals,
                    float* ograd, float* gpair, float* loss_sum, float* pair_sum, hipStream_t st,
@@ -119,7 +120,8 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
                         const float* otail, int B, int W, int D, float* ugrad, hipStream_t st,
                         const float* gnc = nullptr, long long negbase = 0,
                         const float* uvals = nullptr, float* acc = nullptr,
-                        float* acc_out = nullptr, int acc_n = 0);
+                        float* acc_out = nullptr, int acc_n = 0, const DevTable* tab = nullptr,
+                        const long long* slots = nullptr, const OptParams* op = nullptr);
 void launch_w2v_stream_gen(uint64_t seed, long long base, int B, int W, int L, long long nneg,
                            long long V, float noise, uint64_t* keys, int32_t* meta,
                            hipStream_t st, const long long* step_dev, long long step_mul,

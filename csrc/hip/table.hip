@@ -712,7 +712,8 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
 template <int D>
 __global__ __launch_bounds__(256) void k_apply_rows(DevTable t, const long long* __restrict__ slots,
                                                     const float* __restrict__ grads, SegList sl,
-                                                    OptParams op) {
+                                                    OptParams op,
+                                                    const uint8_t* __restrict__ only) {
   constexpr int NV = D / (4 * kPvL), Q = D / 4;  // float4s per lane / per array
   const long long total = seg_total(sl);
   const int lg = threadIdx.x & (kPvL - 1);
@@ -722,8 +723,9 @@ __global__ __launch_bounds__(256) void k_apply_rows(DevTable t, const long long*
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
+    if (only && !only[pos]) continue;  // the same for the 8 lanes of a key
     const long long slot = slots[pos];
-    if (slot < 0) continue;  // the same for the 8 lanes of a key
+    if (slot < 0) continue;
     float4* row = reinterpret_cast<float4*>(slot_row(t, slot));
     const float4* gr = reinterpret_cast<const float4*>(grads + pos * D);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1057,7 +1059,7 @@ void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32
 
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
-                  const float* snap) {
+                  const float* snap, const uint8_t* only) {
   if (max_n <= 0) return;
   // one group per key (no grid-stride rounds: a second round is a second
   // random-access latency chain for those lanes) and 8-byte (w, h) accesses;
@@ -1071,15 +1073,16 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
     const long long grid = grid_for(max_n, kPvL, 1 << 22);
     switch (t.dim) {
       case 32: hipLaunchKernelGGL(k_apply_rows<32>, dim3(grid), dim3(256), 0, st, t, slots, grads,
-                                  sl, op); break;
+                                  sl, op, only); break;
       case 64: hipLaunchKernelGGL(k_apply_rows<64>, dim3(grid), dim3(256), 0, st, t, slots, grads,
-                                  sl, op); break;
+                                  sl, op, only); break;
       default: hipLaunchKernelGGL(k_apply_rows<128>, dim3(grid), dim3(256), 0, st, t, slots,
-                                  grads, sl, op); break;
+                                  grads, sl, op, only); break;
     }
     check_launch("k_apply_rows");
     return;
   }
+  if (only) throw_error("apply: the `only` mask is for wide fp32 rows");
   if (!snap && !t.bf16 && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
       W % 2 == 0 && W == t.width && t.row_off % 8 == 0 && t.stride % 8 == 0) {
     SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_st<kG>, dim3(grid_for(max_n, kG, 1 << 22)),

@@ -702,7 +702,8 @@ __global__ __launch_bounds__(kOsT) void k_w2v_osort(const uint32_t* __restrict__
                                                     const uint32_t* __restrict__ pj,
                                                     const uint32_t* __restrict__ luid,
                                                     uint32_t* __restrict__ ord,
-                                                    uint4* __restrict__ items) {
+                                                    uint4* __restrict__ items,
+                                                    uint8_t* __restrict__ uhot) {
   __shared__ uint32_t cnt[kOsMaxU];
   __shared__ uint32_t ifirst[kOsMaxU];  // a single-occurrence key's item slot
   __shared__ unsigned int wsum[kOsT / 64];
@@ -749,6 +750,9 @@ __global__ __launch_bounds__(kOsT) void k_w2v_osort(const uint32_t* __restrict__
       cnt[l] = e;  // placement cursor
       ifirst[l] = (p0 + ei) | (c[k] == 1 ? 0x80000000u : 0u);
       const uint32_t nit = (c[k] + kOsCh - 1) / kOsCh;
+      // uhot: the key's row sums over several items (row atomics into ugrad):
+      // its optimizer update runs after the reduce (launch_apply `only`)
+      if (uhot) uhot[base + l] = nit > 1 ? 1 : 0;
       if (c[k] > 1)  // (a single-occurrence item is written at placement, below)
         for (uint32_t m = 0; m < nit; ++m)
           items[p0 + ei + m] = make_uint4(p0 + e + m * kOsCh, min(kOsCh, c[k] - m * kOsCh),
@@ -816,7 +820,10 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
                                                      long long negbase,
                                                      const float* __restrict__ uvals,
                                                      float* __restrict__ lacc,
-                                                     float* __restrict__ lacc_out, int lacc_n) {
+                                                     float* __restrict__ lacc_out, int lacc_n,
+                                                     DevTable tab,
+                                                     const long long* __restrict__ slots,
+                                                     OptParams op) {
   // the step's loss / pair accumulators (the tile kernel's, ordered before
   // this launch on the stream) move to acc_out and are left zero for the next
   // step's tile: no zero-fill launch per step
@@ -897,6 +904,29 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
     for (int r = 0; r < QF; ++r)
 #pragma unroll
       for (int v = 0; v < V; ++v) acc[v] += sc[r] * OVec<V>::get(x[r], v);
+  }
+  if (slots && !(it.w & 1u)) {
+    // fused K5 (one GPU): this item is the key's whole gradient row — the
+    // optimizer update of its table row right here (parameters, then the
+    // state, V consecutive floats per lane) instead of a ugrad row that the
+    // apply kernel reads back; keys summed over several items (row atomics
+    // below) are updated by the apply kernel afterwards (launch_apply only)
+    const long long slot = slots[it.z];
+    if (slot < 0) return;  // half-wave-uniform
+    const int ns = opt_state_per_coord(op.kind);
+    float* row = slot_row(tab, slot) + hl * V;
+    VT w = *reinterpret_cast<const VT*>(row);
+    VT s1 = ns > 0 ? *reinterpret_cast<const VT*>(row + D) : VT{};
+    VT s2 = ns > 1 ? *reinterpret_cast<const VT*>(row + 2 * D) : VT{};
+    float* wf = reinterpret_cast<float*>(&w);
+    float* s1f = reinterpret_cast<float*>(&s1);
+    float* s2f = reinterpret_cast<float*>(&s2);
+#pragma unroll
+    for (int v = 0; v < V; ++v) opt_update(op, wf[v], s1f[v], s2f[v], acc[v]);
+    *reinterpret_cast<VT*>(row) = w;
+    if (ns > 0) *reinterpret_cast<VT*>(row + D) = s1;
+    if (ns > 1) *reinterpret_cast<VT*>(row + 2 * D) = s2;
+    return;
   }
   float* g = ugrad + (long long)it.z * D + hl * V;
   if (it.w & 1u) {
@@ -1245,18 +1275,29 @@ void launch_w2v_sgns(const uint32_t* inv_c, const uint32_t* inv_x, const uint32_
 
 void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const uint32_t* ubase,
                       const uint32_t* pj, const uint32_t* luid, uint32_t* ord, uint32_t* items,
-                      hipStream_t st) {
+                      hipStream_t st, uint8_t* uhot) {
   if (P <= 0) return;
   hipLaunchKernelGGL(k_w2v_osort, dim3(P), dim3(kOsT), 0, st, bstart, unum, ubase, pj, luid, ord,
-                     reinterpret_cast<uint4*>(items));
+                     reinterpret_cast<uint4*>(items), uhot);
   check_launch("k_w2v_osort");
 }
 
 void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
                         const float* otail, int B, int W, int D, float* ugrad, hipStream_t st,
                         const float* gnc, long long negbase, const float* uvals, float* acc,
-                        float* acc_out, int acc_n) {
+                        float* acc_out, int acc_n, const DevTable* tab, const long long* slots,
+                        const OptParams* op) {
   if (gnc && !uvals) throw_error("w2v_oreduce: scaled negative rows need the center rows");
+  DevTable tv{};
+  OptParams opv{};
+  if (slots) {
+    const int ns = op ? opt_state_per_coord(op->kind) : 0;
+    if (!tab || !op || tab->bf16 || (int)tab->dim != D || (int)tab->width != D * (1 + ns) ||
+        tab->row_off % 16 != 0 || tab->stride % 16 != 0)
+      throw_error("w2v_oreduce: a fused update needs fp32 rows of this D (16-byte aligned)");
+    tv = *tab;
+    opv = *op;
+  }
   if (acc && (!acc_out || acc_n <= 0)) throw_error("w2v_oreduce: accumulator hand-off needs acc_out");
   if (n <= 0 && !acc) return;
   if (W < 1 || W > kW2vMaxWindow) throw_error("w2v_oreduce: window must be in [1, 15]");
@@ -1273,11 +1314,11 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
       hipLaunchKernelGGL((k_w2v_oreduce<DD, true>), dim3(grid), dim3(256), 0, st, it, n, ord,  \
                          ograd, otail, B, W, ntiles, ugrad,                                    \
                          reinterpret_cast<const float2*>(gnc), negbase, uvals, acc, acc_out,   \
-                         acc_n);                                                               \
+                         acc_n, tv, slots, opv);                                               \
     else                                                                                      \
       hipLaunchKernelGGL((k_w2v_oreduce<DD, false>), dim3(grid), dim3(256), 0, st, it, n, ord, \
                          ograd, otail, B, W, ntiles, ugrad, nullptr, 0ll, nullptr, acc,        \
-                         acc_out, acc_n);                                                      \
+                         acc_out, acc_n, tv, slots, opv);                                      \
     break;
     SS_W2VO_CASE(32)
     SS_W2VO_CASE(64)

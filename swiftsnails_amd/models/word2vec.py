@@ -194,6 +194,14 @@ class Word2VecWorker(PipelinedWorker):
                           if self.per_pair else None)
             self.ord = [torch.empty(n, dtype=torch.int32, device=dev)
                         for _ in range(engine.depth)]
+            # one GPU: the reduce runs the optimizer update of every key whose
+            # gradient row is one item (k_w2v_oreduce with the table), and
+            # the apply kernel then only the keys it summed over several
+            # items (uhot, written by k_w2v_osort); SS_W2V_FUSE=0: off
+            self.fuse = engine.fast1 and os.environ.get("SS_W2V_FUSE", "1") != "0"
+            self.uhot = ([torch.zeros(engine.max_keys * engine.world, dtype=torch.uint8,
+                                      device=dev) for _ in range(engine.depth)]
+                         if self.fuse else None)
             self.items = [torch.empty((n, 4), dtype=torch.int32, device=dev)
                           for _ in range(engine.depth)]
             self._post_route = self._osort
@@ -213,7 +221,8 @@ class Word2VecWorker(PipelinedWorker):
         o = dd.owner
         _, bstart, unum, ubase, P = o.bucket_view(dd.n)
         hip().w2v_osort(P, bstart, unum, ubase, o.pj.data_ptr(), o.luid.data_ptr(),
-                        self.ord[slot].data_ptr(), self.items[slot].data_ptr(), st)
+                        self.ord[slot].data_ptr(), self.items[slot].data_ptr(), st,
+                        self.uhot[slot].data_ptr() if self.uhot is not None else 0)
 
     def _produce(self, step, slot, stream):
         kw = self._gen_kwargs(step)
@@ -221,6 +230,26 @@ class Word2VecWorker(PipelinedWorker):
             kw["meta"] = self.meta[slot]
         self.data.generate(step, self.rank, self.world, self.keys[slot], stream=stream, **kw)
         return self.keys[slot]
+
+    def _fused(self, rnd):
+        """Table arguments of a reduce that runs the optimizer update itself
+        (one GPU), or {} (PSEngine.fuse_apply declined: the push applies)."""
+        if self.uhot is None:
+            return {}
+        fa = self.engine.fuse_apply(rnd, snapshot=False)
+        return {"t": fa["t"], "slots": fa["slots"], "op": fa["op"]} if fa else {}
+
+    def _apply_hot(self, rnd, fa, slot, st):
+        """The update of the keys the fused reduce summed over several items
+        (their gradient rows are complete after it): the apply kernel over
+        the round's unique keys, masked to those."""
+        if not fa:
+            return
+        tab = self.engine.table
+        sl = hip().SegList.from_device(rnd.dd.ucount.data_ptr())
+        hip().apply(tab.dt, rnd.slots.data_ptr(), rnd.ugrad.data_ptr(), sl,
+                    max(1, min(rnd.dd.n, rnd.dd.ucap)), fa["op"], tab.G, st, 0,
+                    self.uhot[slot].data_ptr())
 
     def _compute(self, rnd, slot, st):
         d = self.data
@@ -233,10 +262,13 @@ class Word2VecWorker(PipelinedWorker):
                      B, d.window, d.negatives, self.engine.dim, rnd.uvals.data_ptr(),
                      self.ograd.data_ptr(), self.gpair.data_ptr(), self._acc[0].data_ptr(),
                      self._acc[1].data_ptr(), st, self.gnc.data_ptr())
+            fa = self._fused(rnd)
             h.w2v_oreduce(self.items[slot].data_ptr(), d.n_keys, self.ord[slot].data_ptr(),
                           self.ograd.data_ptr(), 0, B, d.window, self.engine.dim,
                           rnd.ugrad.data_ptr(), st, gnc=self.gnc.data_ptr(),
-                          negbase=B + d.run_len, uvals=rnd.uvals.data_ptr(), **self._handoff())
+                          negbase=B + d.run_len, uvals=rnd.uvals.data_ptr(), **self._handoff(),
+                          **fa)
+            self._apply_hot(rnd, fa, slot, st)
             return
         if self.window_mode:
             occ = self.occ_reduce
@@ -245,9 +277,11 @@ class Word2VecWorker(PipelinedWorker):
                       rnd.ugrad.data_ptr(), self._acc[0].data_ptr(), self._acc[1].data_ptr(),
                       st, self.ograd.data_ptr() if occ else 0, self.otail.data_ptr() if occ else 0)
             if occ:
+                fa = self._fused(rnd)
                 h.w2v_oreduce(self.items[slot].data_ptr(), d.n_keys, self.ord[slot].data_ptr(),
                               self.ograd.data_ptr(), self.otail.data_ptr(), B, d.window,
-                              self.engine.dim, rnd.ugrad.data_ptr(), st, **self._handoff())
+                              self.engine.dim, rnd.ugrad.data_ptr(), st, **self._handoff(), **fa)
+                self._apply_hot(rnd, fa, slot, st)
             return
         h.w2v_sgns(ptr, ptr + B * es, ptr + B * (1 + C) * es, B, C, self.engine.dim,
                    d.neg_scale, rnd.uvals.data_ptr(), rnd.ugrad.data_ptr(),

@@ -84,6 +84,10 @@ KNOBS: dict[str, Knob] = {
                          "N>1 xGMI servers: stream the peers' gradient rows out of the uncached "
                          "mailbox into a cached buffer before the merge gathers them (0: gather "
                          "from the mailbox)"),
+    "SS_W2V_FUSE": Knob("1", "models/word2vec.py", "tuning",
+                        "one GPU: the word2vec occurrence-row reduce runs the optimizer update "
+                        "of single-item keys itself; the apply kernel only the rest (0: reduce, "
+                        "then apply every key)"),
     "SS_CLAIM": Knob("1", "parallel/engine.py", "tuning",
                      "one GPU, region tables, synchronous rounds: the pull claims new keys' "
                      "slots in LDS and the fused merge stores [w | h | key] (0: CAS inserts)"),
