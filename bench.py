@@ -96,6 +96,8 @@ def main(argv=None):
             return 2
     if a.dedup:
         os.environ["SS_DEDUP"] = a.dedup
+    if a.graph == "on":  # replays run the server half on the main stream (framework/gpu.py)
+        os.environ.setdefault("SS_SERVER_STREAM", "0")
     # SS_BENCH_DEVICE pins every rank to one device: a multi-rank rehearsal
     # of this script on a 1-GPU box (with --transport gloo)
     dev_idx = int(os.environ.get("SS_BENCH_DEVICE", local_rank))

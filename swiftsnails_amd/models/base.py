@@ -288,10 +288,13 @@ class PipelinedWorker:
         """SS_PULL_AHEAD=auto at N>1: time synchronous and pulled-ahead steps
         on the live world and keep pulled-ahead rounds only if they win
         clearly.  ``windows`` alternating (synchronous, pulled-ahead) windows
-        of ``steps`` timed steps each (max over ranks); pulled-ahead rounds are
-        chosen only if they beat the synchronous window next to them by at
-        least ``margin`` in EVERY window, else rounds stay synchronous (no
-        staleness).  A single short window let box noise flip the choice (the
+        of ``steps`` timed steps each (max over ranks); the mode the model
+        runs by default (synchronous for sparse LR, pulled ahead for word2vec
+        and FM, which opt in) is kept unless the other beats the window next
+        to it by at least ``margin`` in EVERY window.  Eager windows understate
+        pulled-ahead rounds under hipGraph replay (word2vec at N>1: 0.105
+        ahead vs 0.135 ms sync replayed), so a model that pulls ahead keeps
+        doing so unless synchronous rounds win clearly.  A single short window let box noise flip the choice (the
         two modes overlap within a few percent on one GPU), which changes both
         the speed and the staleness semantics of a run.  On one GPU shared by
         all ranks there is no cross-device wait to hide and the synchronous
@@ -308,6 +311,9 @@ class PipelinedWorker:
                 and os.environ.get("SS_STALENESS", "1") != "0"):
             return {}
         steps, windows = max(1, int(steps)), max(1, int(windows))
+        # the model's own mode (pulled ahead for word2vec / FM, synchronous
+        # for sparse LR) is kept unless the other wins clearly in every window
+        default = bool(eng.pull_ahead)
         times = {False: [], True: []}
         spread = {False: [], True: []}
         for _ in range(windows):
@@ -328,14 +334,18 @@ class PipelinedWorker:
                 lo = -eng.max_over_ranks(-el) / steps
                 times[mode].append(hi)
                 spread[mode].append(hi - lo)
-        best = all(a <= (1.0 - margin) * s for s, a in zip(times[False], times[True]))
+        if default:
+            best = not all(s <= (1.0 - margin) * a for s, a in zip(times[False], times[True]))
+        else:
+            best = all(a <= (1.0 - margin) * s for s, a in zip(times[False], times[True]))
         pick = os.environ.get("SS_CAL_PICK", "")  # debug: force the outcome
         if pick in ("sync", "ahead"):
             best = pick == "ahead"
         self.set_pull_ahead(best)
         self.drain()
         ms = lambda xs: [round(1e3 * x, 4) for x in xs]  # noqa: E731
-        return {"pull_ahead": best, "staleness": eng.lookahead if best else 0,
+        return {"pull_ahead": best, "default": default,
+                "staleness": eng.lookahead if best else 0,
                 "sync_ms": ms(times[False]), "ahead_ms": ms(times[True]),
                 "rank_spread_ms": {"sync": ms(spread[False]), "ahead": ms(spread[True])},
                 "windows": windows, "steps_per_window": steps, "margin": margin}
