@@ -127,6 +127,16 @@ __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs,
   return d * Pd + __umulhi(h, Pd);
 }
 
+// SS_BD_XCD=1: the scatter's chunks in XCD-aware order (measured neutral:
+// bench 0.779-0.784 vs 0.784-0.786 ms, the same WRITE_SIZE)
+static int bd_xcd() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_BD_XCD");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 // upper bound on count/scatter chunks (SS_BD_NCH knob): 128 — a chunk of the
 // bench batch (10.2M keys) is 80K keys, looped in 8192-key register tiles, so
 // each (chunk, bucket) run of positions is ~16 long and the scatter's
@@ -354,9 +364,18 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      uint32_t* __restrict__ pos_of,
                                                      uint32_t* __restrict__ bkt,
                                                      typename BdRecT<RW>::T* __restrict__ rec,
-                                                     const uint32_t* __restrict__ wfin) {
+                                                     const uint32_t* __restrict__ wfin,
+                                                     int xcd) {
   extern __shared__ unsigned int cur[];
-  const int c = blockIdx.x;
+  // XCD-aware chunk order (xcd != 0): blocks b and b + 8 share an XCD, so
+  // they get ADJACENT chunks — a bucket's runs are laid out chunk after chunk,
+  // and the line two neighbouring runs share is then written by one L2 and
+  // merged there instead of leaving two partial lines for the fabric
+  int c = blockIdx.x;
+  if (xcd) {
+    const int g = (int)gridDim.x, x = c & 7;
+    c = x * (g >> 3) + min(x, g & 7) + (c >> 3);
+  }
   // keys of 32 bits: 8-byte (key, sample) records (RW 3 only)
   const bool narrow = RW == 3 && wfin && *wfin == 0u;
   uint2* rec2 = reinterpret_cast<uint2*>(rec);
@@ -394,6 +413,117 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
         if (bkt) bkt[j] = b;
       }
     }
+  }
+}
+
+// 4'. the same bucket-ordered list, written through LDS (12- and 8-byte
+// records; SS_BD_SORT=0: the kernel above).  One random 8-byte store per key
+// left a partial 32-byte sector per record: the scatter wrote 288 MB per
+// bench step for 82 MB of records + 41 MB of pos_of (WRITE_SIZE), and the L2
+// does not merge a (chunk, bucket) run's stores across tiles (the same bytes
+// at 32, 64 and 128 chunks).  Here each tile of KT * 1024 keys is counting-
+// sorted by bucket in LDS (tile histogram, scan over the P buckets, staged
+// SoA records), then written out in bucket order: consecutive lanes store
+// consecutive positions of a bucket's run, so one store instruction covers
+// whole sectors of the runs it touches.  LDS: (2P + 1) words + 14 bytes per
+// tile key (the launcher picks KT so the workgroup fits).
+template <int KT>
+__global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restrict__ keys,
+                                                       long long n, RouteSpec rs, int Pd, int P,
+                                                       int chunk,
+                                                       const uint32_t* __restrict__ hist,
+                                                       const uint32_t* __restrict__ bstart,
+                                                       uint32_t* __restrict__ pos_of,
+                                                       uint32_t* __restrict__ bkt,
+                                                       uint32_t* __restrict__ rec,
+                                                       const uint32_t* __restrict__ wfin,
+                                                       int xcd) {
+  constexpr int CT = 1024, T = KT * CT;
+  extern __shared__ unsigned int sm[];
+  unsigned int* cur = sm;           // [P] the chunk's cursor per bucket
+  unsigned int* toff = sm + P;      // [P + 1] tile counts, then tile offsets
+  uint32_t* sx = toff + P + 1;      // [T] staged records, SoA: key low, key high, sample
+  uint32_t* sy = sx + T;
+  uint32_t* sz = sy + T;
+  uint16_t* sb = reinterpret_cast<uint16_t*>(sz + T);  // [T] bucket of each staged record
+  __shared__ unsigned int wsum[16];
+  __shared__ unsigned int tot;
+  const int t = threadIdx.x;
+  int c = blockIdx.x;
+  if (xcd) {
+    const int g = (int)gridDim.x, x = c & 7;
+    c = x * (g >> 3) + min(x, g & 7) + (c >> 3);
+  }
+  const bool narrow = wfin && *wfin == 0u;
+  const uint32_t* row = hist + (long long)c * P;
+  for (int b = t; b < P; b += CT) cur[b] = bstart[b] + row[b];
+  const int per = (P + CT - 1) / CT;  // scan: buckets per thread
+  const int b0 = t * per, b1 = min(P, b0 + per);
+  for (int t0 = 0; t0 < chunk; t0 += T) {
+    for (int b = t; b < P; b += CT) toff[b] = 0u;
+    __syncthreads();
+    const long long base = (long long)c * chunk + t0 + t;
+    const int kt = min(chunk - t0, T) / CT;
+    uint64_t k[KT];
+    uint32_t bb[KT], rr[KT];
+#pragma unroll
+    for (int e = 0; e < KT; ++e) {
+      const long long j = base + (long long)e * CT;
+      k[e] = (e < kt && j < n) ? keys[j] : kEmptyKey;
+    }
+#pragma unroll
+    for (int e = 0; e < KT; ++e)
+      if (k[e] != kEmptyKey) {
+        bb[e] = bd_bucket(k[e], rs, (uint32_t)Pd);
+        rr[e] = atomicAdd(&toff[bb[e]], 1u);
+      }
+    __syncthreads();
+    unsigned int sum = 0;
+    for (int b = b0; b < b1; ++b) sum += toff[b];
+    unsigned int o = block_excl_scan_1024(sum, wsum, &tot);
+    for (int b = b0; b < b1; ++b) {
+      const unsigned int v = toff[b];
+      toff[b] = o;
+      o += v;
+    }
+    if (t == 0) toff[P] = tot;
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < KT; ++e) {
+      const long long j = base + (long long)e * CT;
+      if (e < kt && j < n) {
+        uint32_t pos = kBdInvalid, b = kBdInvalid;
+        if (k[e] != kEmptyKey) {
+          b = bb[e];
+          const uint32_t i = toff[b] + rr[e];
+          sx[i] = (uint32_t)k[e];
+          sy[i] = (uint32_t)(k[e] >> 32);
+          sz[i] = (uint32_t)j;
+          sb[i] = (uint16_t)b;
+          pos = cur[b] + rr[e];
+        }
+        if (pos_of) pos_of[j] = pos;
+        if (bkt) bkt[j] = b;
+      }
+    }
+    __syncthreads();
+    const unsigned int nt = tot;
+    if (narrow) {
+      uint2* r2 = reinterpret_cast<uint2*>(rec);
+      for (unsigned int i = t; i < nt; i += CT) {
+        const uint32_t b = sb[i];
+        r2[cur[b] + (i - toff[b])] = make_uint2(sx[i], sz[i]);
+      }
+    } else {
+      BdRec3* r3 = reinterpret_cast<BdRec3*>(rec);
+      for (unsigned int i = t; i < nt; i += CT) {
+        const uint32_t b = sb[i];
+        r3[cur[b] + (i - toff[b])] = BdRec3{sx[i], sy[i], sz[i]};
+      }
+    }
+    __syncthreads();
+    for (int b = t; b < P; b += CT) cur[b] += toff[b + 1] - toff[b];
+    __syncthreads();
   }
 }
 
@@ -1116,12 +1246,43 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
 #undef SS_BD_CS_CASE
   }
   check_launch("k_bd_colscan");
-  if (rw == 3)
+  // the LDS-sorted scatter (12- / 8-byte records): the largest tile whose
+  // workgroup fits the LDS (a P of up to ~16K buckets takes 2048-key tiles)
+  static const bool sorted = [] {
+    const char* e = std::getenv("SS_BD_SORT");
+    return !(e && e[0] == '0');
+  }();
+  auto s_lds = [&](int kt) { return sizeof(unsigned int) * (2 * (size_t)L.P + 1) + (size_t)kt * 1024 * 14; };
+  const size_t kLdsMax = 160 * 1024 - 256;
+  const int skt = s_lds(8) <= kLdsMax ? 8 : s_lds(4) <= kLdsMax ? 4 : s_lds(2) <= kLdsMax ? 2 : 0;
+  if (rw == 3 && sorted && skt) {
+    if (L.chunk % 1024) throw_error("bdedup: chunk not a multiple of 1024");
+    switch (skt) {
+#define SS_BD_S_CASE(KT)                                                                          \
+  case KT: {                                                                                      \
+    static const bool attr = (check_hip(hipFuncSetAttribute((const void*)k_bd_scatter_s<KT>,       \
+                                                            hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                                            (int)kLdsMax),                        \
+                                        "k_bd_scatter_s LDS"),                                    \
+                              true);                                                              \
+    (void)attr;                                                                                   \
+    hipLaunchKernelGGL(k_bd_scatter_s<KT>, dim3(L.nch), dim3(1024), s_lds(KT), st, keys, n, rs,  \
+                       L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pos_of, bkt, rec, wfin,      \
+                       bd_xcd());                                                                 \
+  } break;
+      SS_BD_S_CASE(8)
+      SS_BD_S_CASE(4)
+      SS_BD_S_CASE(2)
+#undef SS_BD_S_CASE
+    }
+  } else if (rw == 3)
     SS_BD_CT_DISPATCH2(ct, 3, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
-                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<BdRec3*>(rec), wfin)
+                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<BdRec3*>(rec), wfin,
+                       bd_xcd())
   else
     SS_BD_CT_DISPATCH2(ct, 4, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
-                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<uint4*>(rec), nullptr)
+                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<uint4*>(rec), nullptr,
+                       bd_xcd())
 #undef SS_BD_CT_DISPATCH
 #undef SS_BD_CT_DISPATCH2
   check_launch("k_bd_scatter");

@@ -94,6 +94,12 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_NCH": Knob("128", "csrc/hip/bdedup.hip", "tuning",
                       "max count/scatter chunks (1 GPU 512 -> 128: 0.93 -> 0.89 ms/step; "
                       "N>1 path 128 / 256 / 512: 1.06 / 1.03 / 1.05)"),
+    "SS_BD_XCD": Knob("0", "csrc/hip/bdedup.hip", "tuning",
+                      "1: scatter chunks in XCD-aware order (blocks b, b+8 share an XCD and get "
+                      "adjacent chunks; measured neutral)"),
+    "SS_BD_SORT": Knob("1", "csrc/hip/bdedup.hip", "tuning",
+                       "route scatter through an LDS counting sort per tile, stored in bucket "
+                       "order (0: one random store per key)"),
     "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
     "SS_BD_REC": Knob("auto", "csrc/hip/bdedup.hip", "tuning",

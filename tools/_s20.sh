@@ -1,0 +1,18 @@
+# LDS-sorted route scatter: dedup/claim/kernel tests, A/B bench (SS_BD_SORT 1 vs 0),
+# serial kernel stats + WRITE_SIZE for both
+set -u
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/s20; mkdir -p $O
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_claim.py -m gpu > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for r in 1 2 3; do
+  for x in 1 0; do
+    SS_BD_SORT=$x timeout -k 10 200 python bench.py --steps 50 --warmup 10 > $O/b_${x}_$r.json 2>$O/b_${x}_$r.err || exit $?
+    python -c "import json; d=json.loads(open('$O/b_${x}_$r.json').read().splitlines()[-1]); print('sort=$x', d['ms_per_step'], d['config']['loss_last'])"
+  done
+done
+cd /tmp
+for x in 1 0; do
+  SS_BD_SORT=$x HIP_LAUNCH_BLOCKING=1 timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $O/ser_$x -o run -- python3 $R/bench.py --steps 25 --warmup 2 > $O/ser_$x.log 2>&1 || exit $?
+  SS_BD_SORT=$x timeout -s KILL 90 rocprofv3 --kernel-trace --stats --pmc WRITE_SIZE TCC_EA0_WRREQ_sum --output-format csv -d $O/pmc_$x -o run -- python3 $R/bench.py --steps 4 --warmup 2 > $O/pmc_$x.log 2>&1 || exit $?
+done
