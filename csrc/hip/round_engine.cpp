@@ -303,14 +303,14 @@ class RoundEngine {
   // merge kernel already updated the rows (fuse_apply).
   void push_fast(int slot, int tag, uintptr_t stream, bool apply, const DevTable& t,
                  const OptParams& op, int G, uintptr_t slots, uintptr_t grads, uintptr_t ucount,
-                 long long max_n, uintptr_t snap) {
+                 long long max_n, uintptr_t snap, int slot32) {
     check_slot(slot);
     if (apply) {
       SegList sl{};
       sl.nseg = 1;
       sl.dev_count = Pt<const long long>(ucount);
       launch_apply(t, Pt<const long long>(slots), Pt<const float>(grads), sl, max_n, op, G,
-                   St(stream), Pt<const float>(snap));
+                   St(stream), Pt<const float>(snap), nullptr, slot32);
     }
     record(kFree, slot, stream, tag);
   }

@@ -50,10 +50,11 @@ void launch_lookup_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* 
 void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                           const uint32_t* unum, const uint32_t* ubase, int P, const int* slots32,
                           const float* snap, hipStream_t st);
-// only (optional): apply only at positions with only[pos] != 0 (wide rows)
+// only (optional): apply only at positions with only[pos] != 0 (wide rows);
+// slot32: `slots` holds 4-byte slot indices (a snapshot pull of scalar rows)
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
-                  const float* snap = nullptr, const uint8_t* only = nullptr);
+                  const float* snap = nullptr, const uint8_t* only = nullptr, int slot32 = 0);
 void launch_assign(const DevTable& t, const uint64_t* keys, const float* rows, long long n,
                    unsigned long long* size_ctr, int* err, int G, hipStream_t st);
 void launch_export(const DevTable& t, unsigned long long s0, long long n, uint64_t* keys_out,

@@ -692,15 +692,17 @@ __device__ __forceinline__ void apply_row(const DevTable& t, long long slot,
 template <int G>
 __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __restrict__ slots,
                                                const float* __restrict__ grads, SegList sl,
-                                               OptParams op, const float2* __restrict__ snap) {
+                                               OptParams op, const float2* __restrict__ snap,
+                                               int slot32) {
   const long long total = seg_total(sl);
+  const int* s32 = reinterpret_cast<const int*>(slots);
   const int lg = threadIdx.x % G;
   const long long ngroups = (long long)gridDim.x * (blockDim.x / G);
   for (long long g = (long long)blockIdx.x * (blockDim.x / G) + threadIdx.x / G; g < total;
        g += ngroups) {
     int seg;
     const long long pos = seg_pos(sl, g, &seg);
-    apply_row<G>(t, slots[pos], grads + pos * (long long)t.dim, op, lg,
+    apply_row<G>(t, slot32 ? (long long)s32[pos] : slots[pos], grads + pos * (long long)t.dim, op, lg,
                  snap ? snap + pos : nullptr);
   }
 }
@@ -1059,8 +1061,10 @@ void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32
 
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,
                   const SegList& sl, long long max_n, const OptParams& op, int G, hipStream_t st,
-                  const float* snap, const uint8_t* only) {
+                  const float* snap, const uint8_t* only, int slot32) {
   if (max_n <= 0) return;
+  if (slot32 && (t.dim != 1 || G != 1))
+    throw_error("apply: 4-byte slot indices are for scalar rows");
   // one group per key (no grid-stride rounds: a second round is a second
   // random-access latency chain for those lanes) and 8-byte (w, h) accesses;
   // narrow multi-coordinate rows (FM): 8-byte chunks staged through LDS
@@ -1092,7 +1096,7 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
   }
   SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply<kG>, dim3(grid_for(max_n, kG, 1 << 22)),
                                       dim3(256), 0, st, t, slots, grads, sl, op,
-                                      reinterpret_cast<const float2*>(snap)));
+                                      reinterpret_cast<const float2*>(snap), slot32));
   check_launch("k_apply");
 }
 

@@ -614,14 +614,13 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                                     rnd.snap_version == tab.version) else None
                 if apply:
                     tab.version += 1
-                sl = rnd.slots
-                if apply and rnd.slot32:  # the apply kernel reads 8-byte slots
-                    sl = sl.view(torch.int32)[:sl.numel()].to(torch.int64)
+                # a 4-byte-slot pull: the apply kernel reads them as such
                 self.native.push_fast(slot, self._tag, self.raw_stream(), apply, tab.dt,
-                                      tab.opt.native(), tab.G, sl.data_ptr(), g.data_ptr(),
+                                      tab.opt.native(), tab.G, rnd.slots.data_ptr(), g.data_ptr(),
                                       rnd.dd.ucount.data_ptr(),
                                       max(1, min(rnd.dd.n, rnd.dd.ucap)),
-                                      snap.data_ptr() if snap is not None else 0)
+                                      snap.data_ptr() if snap is not None else 0,
+                                      int(bool(rnd.slot32)))
             tab.next_round()
         elif self.xg and self.gpu:
             kind = self._server_update_kind()

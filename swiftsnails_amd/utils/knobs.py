@@ -80,10 +80,10 @@ KNOBS: dict[str, Knob] = {
     "SS_CLAIM_T": Knob("256", "csrc/hip/table.hip", "tuning",
                        "claimed pull: threads per bucket workgroup (256 / 512 / 1024: 0.795 / "
                        "0.833 / 0.843 ms per bench step on one box)"),
-    "SS_SRV_STAGE": Knob("1", "parallel/engine_dist.py", "tuning",
-                         "N>1 xGMI servers: stream the peers' gradient rows out of the uncached "
-                         "mailbox into a cached buffer before the merge gathers them (0: gather "
-                         "from the mailbox)"),
+    "SS_SRV_STAGE": Knob("0", "parallel/engine_dist.py", "tuning",
+                         "1: N>1 xGMI servers stream the peers' gradient rows out of the "
+                         "uncached mailbox into a cached buffer before the merge gathers them "
+                         "(measured neutral at 4 / 8 ranks on one GPU)"),
     "SS_W2V_FUSE": Knob("1", "models/word2vec.py", "tuning",
                         "one GPU: the word2vec occurrence-row reduce runs the optimizer update "
                         "of single-item keys itself; the apply kernel only the rest (0: reduce, "

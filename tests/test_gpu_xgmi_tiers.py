@@ -40,6 +40,14 @@ def test_tier_litmus_and_engine_oracle(world, tier):
             assert "forced" in lit[0]["why"]
 
 
+def test_server_gradient_staging_oracle():
+    """SS_SRV_STAGE=1 (off by default: measured neutral): the servers stream
+    the peers' gradient rows out of the mailbox into a cached buffer
+    (k_xstage) before the merge; the rounds still reproduce the oracle."""
+    planes = _run(4, list(range(4)), list(range(4)), "adagrad", "xgmi", {"SS_SRV_STAGE": "1"})
+    assert all(p["xgmi_tier"] in ("drain", "fenced") for p in planes)
+
+
 def test_stale_round_tag_is_detected():
     """A tag overwritten between a put and its wait (what a flag overtaking
     its data looks like) sets the sticky error, and poll_error raises
