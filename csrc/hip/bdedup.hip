@@ -421,12 +421,14 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
 // left a partial 32-byte sector per record: the scatter wrote 288 MB per
 // bench step for 82 MB of records + 41 MB of pos_of (WRITE_SIZE), and the L2
 // does not merge a (chunk, bucket) run's stores across tiles (the same bytes
-// at 32, 64 and 128 chunks).  Here each tile of KT * 1024 keys is counting-
-// sorted by bucket in LDS (tile histogram, scan over the P buckets, staged
-// SoA records), then written out in bucket order: consecutive lanes store
-// consecutive positions of a bucket's run, so one store instruction covers
-// whole sectors of the runs it touches.  LDS: (2P + 1) words + 14 bytes per
-// tile key (the launcher picks KT so the workgroup fits).
+// at 32, 64 and 128 chunks).  Here each tile is counting-sorted by bucket in
+// LDS (tile histogram, scan over the P buckets, staged SoA records) and
+// written out in bucket order: consecutive lanes store consecutive positions
+// of a bucket's run, so one store instruction covers whole sectors of the
+// runs it touches.  The longer a tile, the longer each (tile, bucket) run:
+// KT keys per thread for 8-byte records (two staged words per key; the
+// write-out re-hashes the key for its bucket instead of staging it), KT / 2
+// for 12-byte ones.  LDS: (2P + 1) words + 2 * KT * 1024 words.
 template <int KT>
 __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restrict__ keys,
                                                        long long n, RouteSpec rs, int Pd, int P,
@@ -438,14 +440,11 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
                                                        uint32_t* __restrict__ rec,
                                                        const uint32_t* __restrict__ wfin,
                                                        int xcd) {
-  constexpr int CT = 1024, T = KT * CT;
+  constexpr int CT = 1024;
   extern __shared__ unsigned int sm[];
   unsigned int* cur = sm;           // [P] the chunk's cursor per bucket
   unsigned int* toff = sm + P;      // [P + 1] tile counts, then tile offsets
-  uint32_t* sx = toff + P + 1;      // [T] staged records, SoA: key low, key high, sample
-  uint32_t* sy = sx + T;
-  uint32_t* sz = sy + T;
-  uint16_t* sb = reinterpret_cast<uint16_t*>(sz + T);  // [T] bucket of each staged record
+  uint32_t* stage = toff + P + 1;   // [2 * KT * CT] staged records, SoA
   __shared__ unsigned int wsum[16];
   __shared__ unsigned int tot;
   const int t = threadIdx.x;
@@ -455,6 +454,11 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
     c = x * (g >> 3) + min(x, g & 7) + (c >> 3);
   }
   const bool narrow = wfin && *wfin == 0u;
+  // 8-byte records: (key, sample) in two arrays of T; 12-byte: three of T
+  const int T = narrow ? KT * CT : (KT / 2) * CT;
+  uint32_t* sx = stage;
+  uint32_t* sy = stage + T;                  // key high words (12-byte records)
+  uint32_t* sz = stage + (narrow ? T : 2 * T);
   const uint32_t* row = hist + (long long)c * P;
   for (int b = t; b < P; b += CT) cur[b] = bstart[b] + row[b];
   const int per = (P + CT - 1) / CT;  // scan: buckets per thread
@@ -465,7 +469,7 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
     const long long base = (long long)c * chunk + t0 + t;
     const int kt = min(chunk - t0, T) / CT;
     uint64_t k[KT];
-    uint32_t bb[KT], rr[KT];
+    uint32_t br[KT];  // bucket << 16 | rank within the tile's bucket (P, T <= 65536)
 #pragma unroll
     for (int e = 0; e < KT; ++e) {
       const long long j = base + (long long)e * CT;
@@ -474,8 +478,8 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
 #pragma unroll
     for (int e = 0; e < KT; ++e)
       if (k[e] != kEmptyKey) {
-        bb[e] = bd_bucket(k[e], rs, (uint32_t)Pd);
-        rr[e] = atomicAdd(&toff[bb[e]], 1u);
+        const uint32_t b = bd_bucket(k[e], rs, (uint32_t)Pd);
+        br[e] = b << 16 | atomicAdd(&toff[b], 1u);
       }
     __syncthreads();
     unsigned int sum = 0;
@@ -494,13 +498,13 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
       if (e < kt && j < n) {
         uint32_t pos = kBdInvalid, b = kBdInvalid;
         if (k[e] != kEmptyKey) {
-          b = bb[e];
-          const uint32_t i = toff[b] + rr[e];
+          b = br[e] >> 16;
+          const uint32_t r = br[e] & 0xFFFFu;
+          const uint32_t i = toff[b] + r;
           sx[i] = (uint32_t)k[e];
-          sy[i] = (uint32_t)(k[e] >> 32);
+          if (!narrow) sy[i] = (uint32_t)(k[e] >> 32);
           sz[i] = (uint32_t)j;
-          sb[i] = (uint16_t)b;
-          pos = cur[b] + rr[e];
+          pos = cur[b] + r;
         }
         if (pos_of) pos_of[j] = pos;
         if (bkt) bkt[j] = b;
@@ -511,14 +515,16 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
     if (narrow) {
       uint2* r2 = reinterpret_cast<uint2*>(rec);
       for (unsigned int i = t; i < nt; i += CT) {
-        const uint32_t b = sb[i];
-        r2[cur[b] + (i - toff[b])] = make_uint2(sx[i], sz[i]);
+        const uint32_t key = sx[i];
+        const uint32_t b = bd_bucket((uint64_t)key, rs, (uint32_t)Pd);
+        r2[cur[b] + (i - toff[b])] = make_uint2(key, sz[i]);
       }
     } else {
       BdRec3* r3 = reinterpret_cast<BdRec3*>(rec);
       for (unsigned int i = t; i < nt; i += CT) {
-        const uint32_t b = sb[i];
-        r3[cur[b] + (i - toff[b])] = BdRec3{sx[i], sy[i], sz[i]};
+        const uint32_t x = sx[i], y = sy[i];
+        const uint32_t b = bd_bucket((uint64_t)x | ((uint64_t)y << 32), rs, (uint32_t)Pd);
+        r3[cur[b] + (i - toff[b])] = BdRec3{x, y, sz[i]};
       }
     }
     __syncthreads();
@@ -1252,10 +1258,17 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     const char* e = std::getenv("SS_BD_SORT");
     return !(e && e[0] == '0');
   }();
-  auto s_lds = [&](int kt) { return sizeof(unsigned int) * (2 * (size_t)L.P + 1) + (size_t)kt * 1024 * 14; };
+  auto s_lds = [&](int kt) { return sizeof(unsigned int) * (2 * (size_t)L.P + 1 + 2 * (size_t)kt * 1024); };
   const size_t kLdsMax = 160 * 1024 - 256;
-  const int skt = s_lds(8) <= kLdsMax ? 8 : s_lds(4) <= kLdsMax ? 4 : s_lds(2) <= kLdsMax ? 2 : 0;
-  if (rw == 3 && sorted && skt) {
+  // SS_BD_SKT: the largest keys-per-thread tile to try (16 measured best)
+  static const int skt_max = [] {
+    const char* e = std::getenv("SS_BD_SKT");
+    return e ? std::atoi(e) : 16;
+  }();
+  int skt = 0;
+  for (int kt = 16; kt >= 2 && !skt; kt /= 2)
+    if (kt <= skt_max && s_lds(kt) <= kLdsMax) skt = kt;
+  if (rw == 3 && sorted && skt && L.P < 65536) {
     if (L.chunk % 1024) throw_error("bdedup: chunk not a multiple of 1024");
     switch (skt) {
 #define SS_BD_S_CASE(KT)                                                                          \
@@ -1270,6 +1283,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
                        L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pos_of, bkt, rec, wfin,      \
                        bd_xcd());                                                                 \
   } break;
+      SS_BD_S_CASE(16)
       SS_BD_S_CASE(8)
       SS_BD_S_CASE(4)
       SS_BD_S_CASE(2)

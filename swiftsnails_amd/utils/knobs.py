@@ -97,6 +97,9 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_XCD": Knob("0", "csrc/hip/bdedup.hip", "tuning",
                       "1: scatter chunks in XCD-aware order (blocks b, b+8 share an XCD and get "
                       "adjacent chunks; measured neutral)"),
+    "SS_BD_SKT": Knob("16", "csrc/hip/bdedup.hip", "tuning",
+                      "sorted scatter: largest keys per thread per LDS tile (16 / 8 / 4 / 2; "
+                      "halved for 12-byte records and when the bucket table needs the LDS)"),
     "SS_BD_SORT": Knob("1", "csrc/hip/bdedup.hip", "tuning",
                        "route scatter through an LDS counting sort per tile, stored in bucket "
                        "order (0: one random store per key)"),
