@@ -40,3 +40,33 @@ def collect(q, procs, n: int, timeout: float) -> list:
             raise RuntimeError(f"rank process exit codes {[p.exitcode for p in procs]}"
                                if dead else f"no result within {timeout} s")
     return out
+
+
+def _child_main(fn, args, q):
+    try:
+        fn(*args)
+        q.put(("ok", ""))
+    except BaseException:  # noqa: BLE001 - the parent re-raises it
+        import traceback
+
+        q.put(("fail", traceback.format_exc()))
+
+
+def in_child(fn, *args, timeout: float = 240.0) -> None:
+    """Run ``fn(*args)`` (a module-level test body) in a spawned process and
+    re-raise its failure here.  The hipGraph tests run this way: a graph
+    replay in a process that had already run many other GPU tests (engines,
+    streams and graphs created and torn down) segfaulted inside
+    hipGraphLaunch, depending on which tests ran before — never in a fresh
+    process, and never in the single-model processes bench.py and the
+    launcher run."""
+    import torch.multiprocessing as mp
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_child_main, args=(fn, args, q))
+    p.start()
+    res = collect(q, [p], 1, timeout)[0]
+    p.join(60)
+    if res[0] != "ok":
+        raise AssertionError("in the child process:\n" + res[1])

@@ -5,6 +5,7 @@ import os
 import numpy as np
 import pytest
 import torch
+from _mp import in_child
 
 pytestmark = pytest.mark.gpu
 
@@ -443,17 +444,23 @@ def _graph_worker(model, dev, **ek):
     return Word2VecWorker(eng, data), table
 
 
-def test_graph_capture_after_mode_switch_xgmi(dev, monkeypatch):
+def test_graph_capture_after_mode_switch_xgmi(dev):
     """N>1 path (a size-1 xGMI arena): pulled-ahead rounds, then synchronous
     ones (the launcher calibration's last switch), then the hipGraph capture.
     Synchronous rounds run the keys wait + server merge in their routes; the
     capture must start from a round routed that way (enable_graph settles one
     eager step), else every replay's first pull waits a second time on its
-    slot's keys and the job hangs (here: a mailbox timeout)."""
-    monkeypatch.setenv("SS_XGMI_TIMEOUT", "20")
-    monkeypatch.setenv("SS_PULL_AHEAD", "auto")
+    slot's keys and the job hangs (here: a mailbox timeout).  (Graph tests run
+    in a child process: tests/_mp.py in_child.)"""
+    in_child(_graph_after_mode_switch_body, dev)
+
+
+def _graph_after_mode_switch_body(dev):
+    os.environ["SS_XGMI_TIMEOUT"] = "20"
+    os.environ["SS_PULL_AHEAD"] = "auto"
     from swiftsnails_amd.parallel.xgmi import XgmiTransport
 
+    torch.cuda.set_device(dev)
     w, t = _graph_worker("w2v", dev, transport=XgmiTransport(0, 1, dev, None))
     assert w.set_pull_ahead(True)
     for _ in range(3):
@@ -499,13 +506,19 @@ def test_lr_slot32_matches_slot64(dev, monkeypatch):
 
 
 @pytest.mark.parametrize("model", ["lr", "fm", "w2v", "w2v_pairs"])
-def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
+def test_hipgraph_replay_matches_eager(dev, model):
     """hipGraph replays (one graph per ring phase, device step counter for
     the generator) train exactly like eager steps: same per-step losses and
     the same table (up to float-atomic summation order).  Pull-ahead is off
     here: with it, which of round i's updates round i+1 reads depends on
-    timing (staleness 1), in eager mode as much as in graphs."""
-    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    timing (staleness 1), in eager mode as much as in graphs.  (In a child
+    process: tests/_mp.py in_child.)"""
+    in_child(_replay_matches_eager_body, dev, model)
+
+
+def _replay_matches_eager_body(dev, model):
+    os.environ["SS_PULL_AHEAD"] = "0"
+    torch.cuda.set_device(dev)
     wb, tb = _graph_worker(model, dev)
     lb = [float(wb.step().sum().item())]
     assert wb.enable_graph()
@@ -537,7 +550,13 @@ def test_hipgraph_replay_matches_eager(dev, model, monkeypatch):
 @pytest.mark.parametrize("model", ["fm", "w2v", "w2v_pairs"])
 def test_hipgraph_pull_ahead_trains(dev, model):
     """Graph replays of the pull-ahead pipeline (rows of round i+1 pulled on
-    the route stream while round i computes) keep training."""
+    the route stream while round i computes) keep training.  (In a child
+    process: tests/_mp.py in_child.)"""
+    in_child(_pull_ahead_trains_body, dev, model)
+
+
+def _pull_ahead_trains_body(dev, model):
+    torch.cuda.set_device(dev)
     w, t = _graph_worker(model, dev)
     assert w.engine.pull_ahead
     first = [float(w.step().sum().item()) for _ in range(3)]
