@@ -269,11 +269,24 @@ class RoundEngine {
         srv_s32_[slot] = srv_claim_[slot] = 0;
         launch_lookup_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, Pt<float>(svals), G,
                          St(ss));
-      } else if (srv_claim_[slot])
+      } else if (srv_claim_[slot]) {
+        // scalar rows: the response fill (rows per received position) fused
+        // into the claimed pull — the bucket's rows are staged in its LDS
+        // (SS_SRV_FILL_FUSED=0: the separate fill kernel)
+        const bool fused = dim_ == 1 && !custom_pull && srv_fill_fused();
         launch_pull_claim_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_,
-                             reinterpret_cast<int*>(S.slots), Pt<float>(svals), S.snap, ip,
-                             Pt<unsigned long long>(size_ctr), Pt<int>(err), St(ss));
-      else
+                             reinterpret_cast<int*>(S.slots), fused ? nullptr : Pt<float>(svals),
+                             S.snap, ip, Pt<unsigned long long>(size_ctr), Pt<int>(err), St(ss),
+                             fused ? S.luid : nullptr, fused ? Pt<float>(rvals) : nullptr,
+                             fused ? S.pj : nullptr,
+                             fused ? self_seg(ar_[slot][1]->base() + vals_[slot].data) : SelfSeg{});
+        if (fused) {
+          fill_and_put(slot, ss, 0, rvals, true);
+          rows_wait(slot, stream, sent, metrics);
+          if (ahead) record(kPull, slot, stream, tag);
+          return;
+        }
+      } else
         launch_pull_unique_bk(t, S.bkeys, S.bstart, S.unum, S.ubase, Pd_ * sub_, S.slots,
                               Pt<float>(svals), ip, Pt<unsigned long long>(size_ctr), Pt<int>(err),
                               G, St(ss), snap ? S.snap : nullptr, srv_s32_[slot]);
@@ -435,7 +448,9 @@ class RoundEngine {
   }
   // response rows of this round's received keys (per received position)
   // into the vals put, to every source
-  void fill_and_put(int slot, uintptr_t stream, uintptr_t svals, uintptr_t rvals) {
+  // filled: the rows are in place already (the claimed pull's fused fill)
+  void fill_and_put(int slot, uintptr_t stream, uintptr_t svals, uintptr_t rvals,
+                    bool filled = false) {
     // the rows each source gets back = the keys it sent here (keys header)
     const uintptr_t rc = ar_[slot][0]->base() + keys_[slot][0].hdr;
     // the rows for this rank's own keys go straight into its vals arena (the
@@ -453,7 +468,8 @@ class RoundEngine {
                              Pt<float>(rvals), dim_, St(stream), sv);
     }
     std::vector<std::vector<long long>> parts;
-    parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_, sv.ptr != nullptr && svals));
+    parts.push_back(part(rvals, rc, 0, 4ll * dim_, vals_[slot], cap_,
+                         sv.ptr != nullptr && (svals || filled)));
     ar_[slot][1]->put(0, parts, bpp_, stream);
   }
   // wait for every server's rows of this round (+ the exchange counters)
@@ -479,6 +495,13 @@ class RoundEngine {
   std::vector<char> srv_done_;        // per slot: the route ran keys_in (srv_ahead)
   std::vector<char> srv_s32_;         // per slot: the server pull stored 4-byte slots
   std::vector<char> srv_claim_;       // per slot: ... and claimed its inserts (no CAS)
+  static bool srv_fill_fused() {  // SS_SRV_FILL_FUSED=0: a separate server fill kernel
+    static const bool on = [] {
+      const char* e = std::getenv("SS_SRV_FILL_FUSED");
+      return !(e && e[0] == '0');
+    }();
+    return on;
+  }
   static bool slot32_on() {           // SS_SLOT32=0: 8-byte slot indices
     static const bool on = [] {
       const char* e = std::getenv("SS_SLOT32");

@@ -42,7 +42,8 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
                           const uint32_t* unum, const uint32_t* ubase, int P, int* slots32,
                           float* out, float* snap, const InitParams& ip,
                           unsigned long long* size_ctr, int* err, hipStream_t st,
-                          const uint32_t* luid = nullptr, float* occ = nullptr);
+                          const uint32_t* luid = nullptr, float* occ = nullptr,
+                          const uint32_t* pj = nullptr, SelfSeg self = SelfSeg{});
 // read-only lookup of a bucket view's unique keys (no insert; zeros if absent)
 void launch_lookup_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                       const uint32_t* unum, const uint32_t* ubase, int P, float* out, int G,

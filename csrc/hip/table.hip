@@ -353,7 +353,7 @@ __global__ __launch_bounds__(CT) void k_pull_claim_bk(
     const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
     int* __restrict__ slots32, float* __restrict__ out, float2* __restrict__ snap, InitParams ip,
     unsigned long long* size_ctr, int* err, const uint32_t* __restrict__ luid,
-    float* __restrict__ occ) {
+    float* __restrict__ occ, const uint32_t* __restrict__ pj, SelfSeg self) {
   __shared__ uint32_t cl[kClaimTS];
   __shared__ float sv[kClaimMaxU];
   for (int i = threadIdx.x; i < kClaimTS; i += CT) cl[i] = 0xFFFFFFFFu;
@@ -405,17 +405,21 @@ __global__ __launch_bounds__(CT) void k_pull_claim_bk(
     __syncthreads();
     const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
     const uint32_t nv = min(nu, (uint32_t)kClaimMaxU);
+    // pj (an N>1 server's fill, k_bd_fill_occ_p fused): the row goes to the
+    // received position pj[p] of the response, this rank's own positions
+    // straight into its vals arena (self)
     for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 4 * CT) {
-      uint32_t lu[4];
+      uint32_t lu[4], q[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint32_t p = pb + r * CT;
         lu[r] = p < p1 ? luid[p] : 0xFFFFFFFFu;
+        q[r] = p < p1 ? (pj ? pj[p] : p) : 0u;
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const uint32_t p = pb + r * CT;
-        if (p < p1) occ[p] = lu[r] < nv ? sv[lu[r]] : 0.f;
+        if (p < p1) self.pick(occ, (long long)q[r])[q[r]] = lu[r] < nv ? sv[lu[r]] : 0.f;
       }
     }
   }
@@ -1025,7 +1029,8 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
                           const uint32_t* unum, const uint32_t* ubase, int P, int* slots32,
                           float* out, float* snap, const InitParams& ip,
                           unsigned long long* size_ctr, int* err, hipStream_t st,
-                          const uint32_t* luid, float* occ) {
+                          const uint32_t* luid, float* occ, const uint32_t* pj,
+                          SelfSeg self) {
   if (P <= 0) return;
   check_claim_table(t);
   if (!slots32 || !(out || occ) || !snap || (occ && !luid))
@@ -1039,7 +1044,7 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
 #define SS_CLAIM_LAUNCH(CT)                                                                     \
   hipLaunchKernelGGL(k_pull_claim_bk<CT>, dim3(P), dim3(CT), 0, st, t, bkeys, bstart, unum,     \
                      ubase, slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err, luid, \
-                     occ)
+                     occ, pj, self)
   if (ct == 256) SS_CLAIM_LAUNCH(256);
   else if (ct == 64) SS_CLAIM_LAUNCH(64);
   else if (ct == 128) SS_CLAIM_LAUNCH(128);

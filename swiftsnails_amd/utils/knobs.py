@@ -80,6 +80,9 @@ KNOBS: dict[str, Knob] = {
     "SS_CLAIM_T": Knob("256", "csrc/hip/table.hip", "tuning",
                        "claimed pull: threads per bucket workgroup (256 / 512 / 1024: 0.795 / "
                        "0.833 / 0.843 ms per bench step on one box)"),
+    "SS_SRV_FILL_FUSED": Knob("1", "csrc/hip/round_engine.cpp", "tuning",
+                              "N>1 servers, claimed scalar pulls: the response fill (rows per "
+                              "received position) fused into the pull (0: separate kernel)"),
     "SS_SRV_STAGE": Knob("0", "parallel/engine_dist.py", "tuning",
                          "1: N>1 xGMI servers stream the peers' gradient rows out of the "
                          "uncached mailbox into a cached buffer before the merge gathers them "
