@@ -133,7 +133,9 @@ def main(argv=None):
 
     def make_engine(tr, ct, pt):
         return PSEngine(table, tr, max_keys=a.batch * a.fields, dim=1, device=dev,
-                        count_transport=ct, pull_transport=pt)
+                        count_transport=ct, pull_transport=pt,
+                        exchange=os.environ.get("SS_XCHG", "unique")
+                        if a.grad_mode == "segreduce" else "unique")
 
     engine, (transport, ctrans, ptrans), plane = build_engine(
         a.transport, rank, world, dev, store, make_engine,

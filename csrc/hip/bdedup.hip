@@ -77,14 +77,25 @@ static constexpr int kBdTargetDist = 1024;
 // SS_BD_TARGET (one rank): occurrences per bucket, 1024..3584 (A/B: larger
 // buckets make each (chunk, bucket) run of the scatter longer — fewer partial
 // lines — at the price of a fuller LDS table in the dedup)
+// N>1 record exchange (bd_set_record_layout): the sources ship every
+// occurrence, not their unique keys, so server bucket k is the union of N
+// runs of records and must hold about one one-rank bucket: 3584 / N records
+// per source bucket (the bucket-count cap raises it at N = 8, ~620 at the
+// bench shape: ~5000 records, ~2000 distinct keys per server bucket)
+static int g_bd_records = 0;
 static int bd_target(int nranks) {
   static const int one = [] {
     const char* e = std::getenv("SS_BD_TARGET");
     const int v = e ? std::atoi(e) : kBdTarget;
     return v < 1024 ? 1024 : (v > 3584 ? 3584 : v);
   }();
+  if (nranks > 1 && g_bd_records) return std::max(256, kBdTarget / nranks);
   return nranks > 1 ? kBdTargetDist : one;
 }
+// every N>1 deduper of the process lays its buckets out for the record
+// exchange (on) or the unique-key exchange (off); set before the dedupers'
+// scratch is sized — the layout is what every rank and server agree on
+void bd_set_record_layout(int on) { g_bd_records = on ? 1 : 0; }
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
 static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
@@ -291,13 +302,30 @@ __global__ __launch_bounds__(CT) void k_bd_count(const uint64_t* __restrict__ ke
 //    launch.  CS = workgroup size (small workgroups are not starved by the
 //    other stream's kernels: 1024-thread ones waited ~200 us for a CU with 16
 //    free wave slots beside the pull)
+// Record exchange (`gap` > 0, RecLay): destination d's buckets are placed
+// from d * gap (its send segment in the mailbox layout) instead of after
+// destination d-1's, the last workgroup writes the per-destination record
+// counts and the run tables the servers read (ubase = the gapped bucket
+// starts, unum = the bucket sizes), and the scatter's positions are then
+// send-segment positions: the rows come back to exactly those positions.
+static constexpr int kRecMaxDest = 64;  // destinations of a record-exchange layout
+struct RecLay {
+  long long gap;                 // 0: contiguous buckets
+  int Pd;                        // buckets per destination
+  unsigned long long* ucount;    // [nranks] records per destination
+  uint32_t* ubase;               // [P] run bases (gapped bucket starts)
+  uint32_t* unum;                // [P] run lengths
+  uint32_t* err;                 // sticky flag: a destination got more than gap
+};
+
 template <int CS>
 __global__ __launch_bounds__(CS) void k_bd_colscan(uint32_t* __restrict__ hist, int nch, int P,
                                                    uint32_t* __restrict__ btot,
                                                    uint32_t* __restrict__ bstart,
                                                    unsigned int* __restrict__ ctr,
                                                    uint32_t* __restrict__ wacc,
-                                                   uint32_t* __restrict__ wfin) {
+                                                   uint32_t* __restrict__ wfin,
+                                                   RecLay rl = RecLay{}) {
   constexpr int NS = CS / 64;  // chunk segments per column
   __shared__ unsigned int ss[NS][64];
   __shared__ unsigned int wsum[16];
@@ -339,12 +367,43 @@ __global__ __launch_bounds__(CS) void k_bd_colscan(uint32_t* __restrict__ hist, 
   for (int k = 0; k < per; ++k)
     if (b0 + k < P)
       sum += __hip_atomic_load(&btot[b0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  unsigned int e = block_excl_scan<NS>(sum, wsum, &tot);
-  for (int k = 0; k < per; ++k)
-    if (b0 + k < P) {
-      bstart[b0 + k] = e;
-      e += __hip_atomic_load(&btot[b0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned int e0 = block_excl_scan<NS>(sum, wsum, &tot);
+  unsigned int e = e0;
+  if (!rl.gap) {
+    for (int k = 0; k < per; ++k)
+      if (b0 + k < P) {
+        bstart[b0 + k] = e;
+        e += __hip_atomic_load(&btot[b0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+  } else {
+    // record exchange: E_d (the contiguous start of destination d's first
+    // bucket) in LDS, then every bucket rebased to d * gap
+    __shared__ unsigned int ed[kRecMaxDest + 1];
+    const int nd = P / rl.Pd;
+    for (int k = 0; k < per; ++k)
+      if (b0 + k < P) {
+        if ((b0 + k) % rl.Pd == 0) ed[(b0 + k) / rl.Pd] = e;
+        e += __hip_atomic_load(&btot[b0 + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    if (threadIdx.x == 0) ed[nd] = tot;
+    __syncthreads();
+    e = e0;
+    for (int k = 0; k < per; ++k)
+      if (b0 + k < P) {
+        const int b = b0 + k, d = b / rl.Pd;
+        const uint32_t c = __hip_atomic_load(&btot[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint32_t s = (uint32_t)((long long)d * rl.gap + (e - ed[d]));
+        bstart[b] = s;
+        rl.ubase[b] = s;
+        rl.unum[b] = c;
+        e += c;
+      }
+    for (int d = threadIdx.x; d < nd; d += CS) {
+      const unsigned int c = ed[d + 1] - ed[d];
+      rl.ucount[d] = c;
+      if ((long long)c > rl.gap) atomicOr(rl.err, 1u);
     }
+  }
   if (threadIdx.x == 0) {
     bstart[P] = tot;
     *ctr = 0u;  // ready for the next call (stream-ordered)
@@ -365,7 +424,8 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      uint32_t* __restrict__ bkt,
                                                      typename BdRecT<RW>::T* __restrict__ rec,
                                                      const uint32_t* __restrict__ wfin,
-                                                     int xcd) {
+                                                     int xcd, uint64_t* __restrict__ skeys = nullptr,
+                                                     uint32_t* __restrict__ spj = nullptr) {
   extern __shared__ unsigned int cur[];
   // XCD-aware chunk order (xcd != 0): blocks b and b + 8 share an XCD, so
   // they get ADJACENT chunks — a bucket's runs are laid out chunk after chunk,
@@ -405,8 +465,16 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
           // (a 64-byte line per occurrence) and writes pj itself.  Measured
           // standalone: scatter 119 -> 163 us, dedup 213 -> 123 us; N>1
           // engine path 1.211 -> 1.169 ms/step, one GPU neutral
-          if (narrow) rec2[pos] = make_uint2((uint32_t)k[e], (uint32_t)j);
-          else rec[pos] = BdRecT<RW>::make(k[e], (uint32_t)j);
+          // record exchange: the key and its occurrence in two arrays at
+          // send-segment positions (the keys are the send segment)
+          if (skeys) {
+            skeys[pos] = k[e];
+            spj[pos] = (uint32_t)j;
+          } else if (narrow) {
+            rec2[pos] = make_uint2((uint32_t)k[e], (uint32_t)j);
+          } else {
+            rec[pos] = BdRecT<RW>::make(k[e], (uint32_t)j);
+          }
         }
         // the BdIndex (j -> bucket position, bucket) only for its consumers
         if (pos_of) pos_of[j] = pos;
@@ -439,7 +507,8 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
                                                        uint32_t* __restrict__ bkt,
                                                        uint32_t* __restrict__ rec,
                                                        const uint32_t* __restrict__ wfin,
-                                                       int xcd) {
+                                                       int xcd, uint64_t* __restrict__ skeys = nullptr,
+                                                       uint32_t* __restrict__ spj = nullptr) {
   constexpr int CT = 1024;
   extern __shared__ unsigned int sm[];
   unsigned int* cur = sm;           // [P] the chunk's cursor per bucket
@@ -517,14 +586,26 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
       for (unsigned int i = t; i < nt; i += CT) {
         const uint32_t key = sx[i];
         const uint32_t b = bd_bucket((uint64_t)key, rs, (uint32_t)Pd);
-        r2[cur[b] + (i - toff[b])] = make_uint2(key, sz[i]);
+        const uint32_t q = cur[b] + (i - toff[b]);
+        if (skeys) {
+          skeys[q] = key;
+          spj[q] = sz[i];
+        } else {
+          r2[q] = make_uint2(key, sz[i]);
+        }
       }
     } else {
       BdRec3* r3 = reinterpret_cast<BdRec3*>(rec);
       for (unsigned int i = t; i < nt; i += CT) {
         const uint32_t x = sx[i], y = sy[i];
         const uint32_t b = bd_bucket((uint64_t)x | ((uint64_t)y << 32), rs, (uint32_t)Pd);
-        r3[cur[b] + (i - toff[b])] = BdRec3{x, y, sz[i]};
+        const uint32_t q = cur[b] + (i - toff[b]);
+        if (skeys) {
+          skeys[q] = (uint64_t)x | ((uint64_t)y << 32);
+          spj[q] = sz[i];
+        } else {
+          r3[q] = BdRec3{x, y, sz[i]};
+        }
       }
     }
     __syncthreads();
@@ -1167,8 +1248,14 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
                     uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                     unsigned long long* dbg, uint32_t* rec, uint8_t* usingle, int ndest,
-                    long long lay_n, int msub, uint32_t* usub) {
+                    long long lay_n, int msub, uint32_t* usub, uint32_t* spj) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
+  // spj (record exchange): no dedup — count, column scan into send-segment
+  // positions (d * ucap + ...) with the run tables and per-destination
+  // counts, then the scatter writes every occurrence's key into ukeys and its
+  // index into spj at that position (the servers dedup what they receive)
+  if (spj && (!ukeys || !ucount || rs.nranks > kRecMaxDest || msub != 1 || !pos_of))
+    throw_error("bdedup: the record exchange needs ukeys, ucount, pos_of, <= 64 ranks, no sub-buckets");
   if (rs.rbits < 0 || rs.rbits > 20) throw_error("bdedup: region bits 0..20");
   if (msub < 1 || msub > kBdMaxSub || (msub > 1 && !usub))
     throw_error("bdedup: server sub-buckets 1..64 (and their offset table)");
@@ -1239,12 +1326,14 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     default: hipLaunchKernelGGL((KERNEL<1024, RW>), dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
   }
   SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, ucount, wacc);
+  RecLay rl{};
+  if (spj) rl = RecLay{ucap, L.Pd, ucount, S + L.ubase, S + L.unum, S};
   check_launch("k_bd_count");
   switch (cs) {
 #define SS_BD_CS_CASE(CS)                                                                      \
   case CS:                                                                                     \
     hipLaunchKernelGGL(k_bd_colscan<CS>, dim3((L.P + 63) / 64), dim3(CS), 0, st, S + L.hist,   \
-                       L.nch, L.P, S + L.btot, S + L.bstart, S + L.ctr, wacc, wfin);           \
+                       L.nch, L.P, S + L.btot, S + L.bstart, S + L.ctr, wacc, wfin, rl);       \
     break;
     SS_BD_CS_CASE(256)
     SS_BD_CS_CASE(512)
@@ -1281,7 +1370,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     (void)attr;                                                                                   \
     hipLaunchKernelGGL(k_bd_scatter_s<KT>, dim3(L.nch), dim3(1024), s_lds(KT), st, keys, n, rs,  \
                        L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pos_of, bkt, rec, wfin,      \
-                       bd_xcd());                                                                 \
+                       bd_xcd(), spj ? ukeys : nullptr, spj);                                     \
   } break;
       SS_BD_S_CASE(16)
       SS_BD_S_CASE(8)
@@ -1292,14 +1381,15 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   } else if (rw == 3)
     SS_BD_CT_DISPATCH2(ct, 3, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
                        S + L.bstart, pj, pos_of, bkt, reinterpret_cast<BdRec3*>(rec), wfin,
-                       bd_xcd())
+                       bd_xcd(), spj ? ukeys : nullptr, spj)
   else
     SS_BD_CT_DISPATCH2(ct, 4, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
                        S + L.bstart, pj, pos_of, bkt, reinterpret_cast<uint4*>(rec), nullptr,
-                       bd_xcd())
+                       bd_xcd(), spj ? ukeys : nullptr, spj)
 #undef SS_BD_CT_DISPATCH
 #undef SS_BD_CT_DISPATCH2
   check_launch("k_bd_scatter");
+  if (spj) return rs.rbits;  // record exchange: the servers dedup
   // place: unique keys straight into the per-destination send segments
   // (+ zeroed gradient rows), reserved with one atomic per bucket
   if (rw == 3)
@@ -1322,6 +1412,118 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     check_launch("k_bd_inv");
   }
   return rs.rbits;  // the region bits the buckets follow (0: dedup-hash buckets)
+}
+
+// ---- record exchange, worker side (N>1 scalar rows; bd_set_record_layout)
+//
+// The rows of a step come back at the send-segment positions of its
+// occurrences, so the forward reads occ[pos_of[j]] from the rows mailbox (or
+// a cached copy, k_rec_copy); its per-sample gradient then goes out per
+// occurrence: grec[p] = gs[spj[p] / F] * x[spj[p]] at the same positions.
+// The servers merge them per distinct key with the update fused (server.hip):
+// no worker dedup, no worker merge.  The destinations' ranges
+// [d * gap, d * gap + ucount[d]) are walked as one flat list.
+__device__ __forceinline__ void rec_ranges(const unsigned long long* __restrict__ ucount, int nd,
+                                           long long gap, long long* cs) {
+  if (threadIdx.x == 0) {
+    long long a = 0;
+    for (int d = 0; d < nd; ++d) {
+      cs[d] = a;
+      a += (long long)min(ucount[d], (unsigned long long)gap);
+    }
+    cs[nd] = a;
+  }
+  __syncthreads();
+}
+__device__ __forceinline__ long long rec_pos(const long long* cs, int nd, long long gap,
+                                             long long f) {
+  int d = 0;
+  while (d + 1 < nd && f >= cs[d + 1]) ++d;
+  return (long long)d * gap + (f - cs[d]);
+}
+
+__global__ __launch_bounds__(256) void k_rec_grad(const unsigned long long* __restrict__ ucount,
+                                                  int nd, long long gap,
+                                                  const uint32_t* __restrict__ spj,
+                                                  const float* __restrict__ gs,
+                                                  const float* __restrict__ xval, int F,
+                                                  float* __restrict__ grec,
+                                                  float* __restrict__ lacc,
+                                                  float* __restrict__ lacc_out, int lacc_n) {
+  __shared__ long long cs[kRecMaxDest + 1];
+  // the step's loss accumulator (the forward's, stream-ordered before this
+  // launch) moves to lacc_out and is left zero, as k_bd_reduce does
+  if (lacc)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < lacc_n; i += gridDim.x * 256) {
+      lacc_out[i] = lacc[i];
+      lacc[i] = 0.f;
+    }
+  rec_ranges(ucount, nd, gap, cs);
+  const long long tot = cs[nd], stride = (long long)gridDim.x * 256 * 4;
+  for (long long f0 = (long long)blockIdx.x * 1024 + threadIdx.x; f0 < tot; f0 += stride) {
+    long long p[4];
+    uint32_t j[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long f = f0 + r * 256;
+      p[r] = f < tot ? rec_pos(cs, nd, gap, f) : -1;
+      j[r] = p[r] >= 0 ? spj[p[r]] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (p[r] < 0) continue;
+      float g = gs[j[r] / (uint32_t)F];
+      if (xval) g *= xval[j[r]];
+      grec[p[r]] = g;
+    }
+  }
+}
+
+// the rows of the step's occurrences out of the (uncached) rows mailbox into
+// a cached array with the same positions (SS_REC_OCC=copy)
+__global__ __launch_bounds__(256) void k_rec_copy(const unsigned long long* __restrict__ ucount,
+                                                  int nd, long long gap,
+                                                  const float* __restrict__ src,
+                                                  float* __restrict__ dst) {
+  __shared__ long long cs[kRecMaxDest + 1];
+  rec_ranges(ucount, nd, gap, cs);
+  const long long tot = cs[nd], stride = (long long)gridDim.x * 256 * 4;
+  for (long long f0 = (long long)blockIdx.x * 1024 + threadIdx.x; f0 < tot; f0 += stride) {
+    long long p[4];
+    float v[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const long long f = f0 + r * 256;
+      p[r] = f < tot ? rec_pos(cs, nd, gap, f) : -1;
+      v[r] = p[r] >= 0 ? src[p[r]] : 0.f;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (p[r] >= 0) dst[p[r]] = v[r];
+  }
+}
+
+static int rec_grid(long long cap, int nd) {
+  const long long work = (cap * nd + 1023) / 1024;  // the ranges' upper bound
+  return (int)std::max<long long>(1, std::min<long long>(work, 2048));
+}
+
+void launch_rec_grad(const unsigned long long* ucount, int nd, long long gap, const uint32_t* spj,
+                     const float* gs, const float* xval, int F, float* grec, hipStream_t st,
+                     float* lacc, float* lacc_out, int lacc_n) {
+  if (nd < 1 || nd > kRecMaxDest || gap < 1 || F < 1) throw_error("rec_grad: bad layout");
+  if (lacc && (!lacc_out || lacc_n <= 0)) throw_error("rec_grad: loss hand-off needs its output");
+  hipLaunchKernelGGL(k_rec_grad, dim3(rec_grid(gap, nd)), dim3(256), 0, st, ucount, nd, gap, spj,
+                     gs, xval, F, grec, lacc, lacc_out, lacc_n);
+  check_launch("k_rec_grad");
+}
+
+void launch_rec_copy(const unsigned long long* ucount, int nd, long long gap, const float* src,
+                     float* dst, hipStream_t st) {
+  if (nd < 1 || nd > kRecMaxDest || gap < 1) throw_error("rec_copy: bad layout");
+  hipLaunchKernelGGL(k_rec_copy, dim3(rec_grid(gap, nd)), dim3(256), 0, st, ucount, nd, gap, src,
+                     dst);
+  check_launch("k_rec_copy");
 }
 
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,

@@ -212,20 +212,39 @@ PYBIND11_MODULE(_ss_hip, m) {
                        uintptr_t bkt, uintptr_t luid, uintptr_t bkeys, uintptr_t ucount,
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
                        uintptr_t st, uintptr_t dbg, uintptr_t rec, uintptr_t usingle,
-                       int ndest, long long lay_n, int msub, uintptr_t usub, int rbits) {
+                       int ndest, long long lay_n, int msub, uintptr_t usub, int rbits,
+                       uintptr_t spj) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks, rbits};
     return launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch),
                            P<uint32_t>(pj), P<uint32_t>(pos_of), P<uint32_t>(bkt),
                            P<uint32_t>(luid), P<uint64_t>(bkeys), P<unsigned long long>(ucount),
                            P<uint64_t>(ukeys), P<float>(ugrad), gdim, P<uint32_t>(inv), place,
                            S(st), P<unsigned long long>(dbg), P<uint32_t>(rec),
-                           P<uint8_t>(usingle), ndest, lay_n, msub, P<uint32_t>(usub));
+                           P<uint8_t>(usingle), ndest, lay_n, msub, P<uint32_t>(usub),
+                           P<uint32_t>(spj));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
      py::arg("rec") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0,
-     py::arg("lay_n") = 0, py::arg("msub") = 1, py::arg("usub") = 0, py::arg("rbits") = 0);
+     py::arg("lay_n") = 0, py::arg("msub") = 1, py::arg("usub") = 0, py::arg("rbits") = 0,
+     py::arg("spj") = 0);
+  m.def("bd_set_record_layout", &bd_set_record_layout, py::arg("on"));
+  m.def("rec_grad", [](uintptr_t ucount, int nd, long long gap, uintptr_t spj, uintptr_t gs,
+                       uintptr_t xval, int F, uintptr_t grec, uintptr_t st, uintptr_t acc,
+                       uintptr_t acc_out, int acc_n) {
+    launch_rec_grad(P<const unsigned long long>(ucount), nd, gap, P<const uint32_t>(spj),
+                    P<const float>(gs), P<const float>(xval), F, P<float>(grec), S(st),
+                    P<float>(acc), P<float>(acc_out), acc_n);
+  }, py::arg("ucount"), py::arg("nd"), py::arg("gap"), py::arg("spj"), py::arg("gs"),
+     py::arg("xval"), py::arg("F"), py::arg("grec"), py::arg("st"), py::arg("acc") = 0,
+     py::arg("acc_out") = 0, py::arg("acc_n") = 0);
+  m.def("rec_copy", [](uintptr_t ucount, int nd, long long gap, uintptr_t src, uintptr_t dst,
+                       uintptr_t st) {
+    launch_rec_copy(P<const unsigned long long>(ucount), nd, gap, P<const float>(src),
+                    P<float>(dst), S(st));
+  }, py::arg("ucount"), py::arg("nd"), py::arg("gap"), py::arg("src"), py::arg("dst"),
+     py::arg("st"));
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,

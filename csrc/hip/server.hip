@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   if (t == 0) {
     so[0] = 0u;
     for (int s = 0; s < R.nsrc; ++s) so[s + 1] += so[s];
-    bad = so[R.nsrc] != p1 - p0 || p1 - p0 > (uint32_t)kSrvOcc;
+    bad = so[R.nsrc] != p1 - p0;
   }
   __syncthreads();
   auto insert = [&](uint64_t key) -> uint32_t {
@@ -186,20 +186,27 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
     bad = 1;
     return kSrvInv;
   };
-  // the sources' parts as one flat list [0, n): position p0 + f holds flat
-  // key f.  kSrvRegs keys per thread are loaded before any is inserted (one
-  // load latency per round instead of one per source)
-  const uint32_t n = min(min(so[R.nsrc], p1 - p0), (uint32_t)kSrvOcc);
-  for (uint32_t f0 = 0; f0 < n; f0 += kSrvDT * kSrvRegs) {
+  // the sources' parts as one flat list [0, nall): position p0 + f holds
+  // flat key f.  kSrvRegs keys per thread are loaded before any is inserted
+  // (one load latency per round instead of one per source).  The first
+  // kSrvOcc keys park their LDS slot; the rest (a Zipf-head bucket of the
+  // record exchange, whose sources ship every occurrence) probe the table
+  // again after the compaction
+  const uint32_t nall = min(so[R.nsrc], p1 - p0);
+  const uint32_t n = min(nall, (uint32_t)kSrvOcc);
+  auto flat_pos = [&](uint32_t f) -> long long {
+    int s = 0;
+    while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
+    return sa[s] + (f - so[s]);
+  };
+  for (uint32_t f0 = 0; f0 < nall; f0 += kSrvDT * kSrvRegs) {
     uint64_t kk[kSrvRegs];
 #pragma unroll
     for (int r = 0; r < kSrvRegs; ++r) {
       const uint32_t f = f0 + (uint32_t)(r * kSrvDT + t);
       kk[r] = kEmptyKey;
-      if (f < n) {
-        int s = 0;
-        while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
-        const long long pos = sa[s] + (f - so[s]);
+      if (f < nall) {
+        const long long pos = flat_pos(f);
         kk[r] = R.self.pick(R.rkeys, pos)[pos];
         pj[p0 + f] = (uint32_t)pos;
       }
@@ -207,7 +214,10 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
 #pragma unroll
     for (int r = 0; r < kSrvRegs; ++r) {
       const uint32_t f = f0 + (uint32_t)(r * kSrvDT + t);
-      if (f < n) park[f] = (unsigned short)insert(kk[r]);
+      if (f < nall) {
+        const uint32_t sl = insert(kk[r]);
+        if (f < n) park[f] = (unsigned short)sl;
+      }
     }
   }
   __syncthreads();
@@ -245,19 +255,30 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
     const uint32_t sl = park[q] == 0xFFFFu ? kSrvInv : park[q];
     luid[p0 + q] = sl == kSrvInv || sl >= ts ? kSrvInv : lid[sl];
   }
-  // an overflowed bucket (error flagged above): the positions past the LDS
-  // parking area still get an in-range pj and no local id, so the fill and
-  // merge kernels (which walk [p0, p1)) write zero rows to real positions and
-  // skip the gradients instead of reading / writing through unset entries
-  const uint32_t nall = p1 - p0, nflat = so[R.nsrc];
+  // keys past the parking area: their slot by a read-only probe of the
+  // compacted table (every key of the bucket was inserted above)
   for (uint32_t f = n + t; f < nall; f += kSrvDT) {
-    uint32_t pos = 0u;
-    if (f < nflat) {
-      int s = 0;
-      while (s + 1 < R.nsrc && f >= so[s + 1]) ++s;
-      pos = (uint32_t)(sa[s] + (f - so[s]));
+    const long long pos = flat_pos(f);
+    const uint64_t key = R.self.pick(R.rkeys, pos)[pos];
+    uint32_t sl = (uint32_t)(dedup_hash(key) >> 32) & (ts - 1), id = kSrvInv;
+    for (uint32_t i = 0; i < ts; ++i) {
+      const unsigned long long v = tab[sl];
+      if (v == key) {
+        id = lid[sl];
+        break;
+      }
+      if (v == kEmptyKey) break;
+      sl = (sl + 1) & (ts - 1);
     }
-    pj[p0 + f] = pos;
+    luid[p0 + f] = id;
+  }
+  // a bucket whose counts disagree with its runs (error flagged above): the
+  // positions past the sources' runs still get an in-range pj and no local
+  // id, so the fill and merge kernels (which walk [p0, p1)) write zero rows
+  // to real positions and skip the gradients instead of reading / writing
+  // through unset entries
+  for (uint32_t f = nall + t; f < p1 - p0; f += kSrvDT) {
+    pj[p0 + f] = 0u;
     luid[p0 + f] = kSrvInv;
   }
 }

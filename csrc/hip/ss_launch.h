@@ -179,7 +179,13 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                     unsigned long long* dbg = nullptr, uint32_t* rec = nullptr,
                     uint8_t* usingle = nullptr, int ndest = 0, long long lay_n = 0,
-                    int msub = 1, uint32_t* usub = nullptr);
+                    int msub = 1, uint32_t* usub = nullptr, uint32_t* spj = nullptr);
+void bd_set_record_layout(int on);
+void launch_rec_grad(const unsigned long long* ucount, int nd, long long gap, const uint32_t* spj,
+                     const float* gs, const float* xval, int F, float* grec, hipStream_t st,
+                     float* lacc = nullptr, float* lacc_out = nullptr, int lacc_n = 0);
+void launch_rec_copy(const unsigned long long* ucount, int nd, long long gap, const float* src,
+                     float* dst, hipStream_t st);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi = 0,

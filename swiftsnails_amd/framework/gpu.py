@@ -57,7 +57,7 @@ def _ranks(spec, world: int) -> list[int]:
 
 class PSContext:
     def __init__(self, cfg: Config, dim: int, optimizer: Optimizer, init: InitConfig,
-                 max_keys: int, capacity: int):
+                 max_keys: int, capacity: int, exchange: str = "unique"):
         self.cfg = cfg
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
@@ -87,7 +87,7 @@ class PSContext:
                                row_dtype=cfg.get("row_dtype", "fp32"))
                       if self.is_server else None)
         ek = dict(max_keys=max_keys, dim=dim, frag_num=int(cfg.get("frag_num", 0) or 0),
-                  server_ranks=self.servers, device=self.device)
+                  server_ranks=self.servers, device=self.device, exchange=exchange)
         # data plane (parallel/select.py): auto = xGMI mailboxes (drain, then
         # fenced publish, each litmus-tested on every rank) falling back to
         # RCCL; xgmi; rccl; gloo (host-staged, tests).  World 1: loopback, or
@@ -261,7 +261,11 @@ def build_worker(cfg: Config):
         dim = 1 if model == "sparse_lr" else int(cfg.get("dim", 9))
         init = InitConfig("zero") if model == "sparse_lr" else fm_table_args(dim - 1, opt)[1]
         cap = int(cfg.get("table_capacity", 0) or data.num_features / nserv / load + 1024)
-        ctx = PSContext(cfg, dim, opt, init, data.batch_size * data.num_fields, cap)
+        # sparse LR may ship every occurrence at N>1 (exchange: records /
+        # SS_XCHG=records; PSEngine), else each source's unique keys
+        xch = str(cfg.get("exchange", os.environ.get("SS_XCHG", "unique")))
+        ctx = PSContext(cfg, dim, opt, init, data.batch_size * data.num_fields, cap,
+                        exchange=xch if model == "sparse_lr" else "unique")
         cls = SparseLRWorker if model == "sparse_lr" else FMWorker
         w = cls(ctx.engine, data, rank=ctx.rank, world=world, active=ctx.is_worker)
     elif model == "word2vec":

@@ -17,6 +17,8 @@ labels drawn from a hidden ground-truth sparse LR model so loss goes down.
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 from typing import Optional
 
@@ -122,6 +124,14 @@ class SparseLRWorker(PipelinedWorker):
                           for _ in range(engine.depth)]
             self.nitems = [torch.zeros(1, dtype=torch.int32, device=dev)
                            for _ in range(engine.depth)]
+        if getattr(engine, "records", False) and not self.bucketed:
+            raise ValueError("the record exchange needs the bucketed segreduce merge "
+                             "(SS_DEDUP=bucket, grad_mode segreduce)")
+        # N>1 record exchange (PSEngine exchange="records"): the forward reads
+        # the rows mailbox in place, or a cached copy of it (SS_REC_OCC=copy)
+        self.rocc = (torch.empty(engine.world * engine.max_keys, dtype=torch.float32, device=dev)
+                     if self.bucketed and getattr(engine, "records", False) and
+                     os.environ.get("SS_REC_OCC", "arena") == "copy" else None)
 
     def _zero_acc(self) -> None:
         if not self.bucketed:
@@ -155,7 +165,25 @@ class SparseLRWorker(PipelinedWorker):
         h = hip()
         dd = rnd.dd
         xp = self.xval[slot].data_ptr() if self.xval is not None else 0
-        if self.bucketed:
+        if self.bucketed and self.engine.records:
+            # N>1 record exchange: the rows came back per occurrence at its
+            # send-segment position (the forward reads occ[pos_of[j]] there),
+            # the gradients go out the same way — no worker merge; the
+            # servers merge per distinct key with the AdaGrad update fused
+            o, eng = dd.owner, self.engine
+            occ = rnd.uvals
+            if self.rocc is not None:  # SS_REC_OCC=copy: out of the mailbox first
+                h.rec_copy(dd.ucount.data_ptr(), eng.world, o.ucap, rnd.uvals.data_ptr(),
+                           self.rocc.data_ptr(), st)
+                occ = self.rocc
+            h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
+                       rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1, self._acc.data_ptr(),
+                       0, st, o.index_ptrs(dd.n), occ=occ.data_ptr())
+            h.rec_grad(dd.ucount.data_ptr(), eng.world, o.ucap, o.spj.data_ptr(),
+                       self.gocc.data_ptr(), xp, d.num_fields, rnd.ugrad.data_ptr(), st,
+                       acc=self._acc.data_ptr(), acc_out=self.loss_sum.data_ptr(),
+                       acc_n=self._acc.numel())
+        elif self.bucketed:
             o = dd.owner
             if not rnd.occ_filled:
                 o.fill_occ(dd.n, rnd.uvals, self.occ, stream=st)

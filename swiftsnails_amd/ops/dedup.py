@@ -99,6 +99,11 @@ class Deduper:
         # 2^rbits regions (ops/table.py _region_bits) when the call's layout
         # allows it (the kernel reports the bits it used: DedupResult.rbits)
         self.rbits = 0
+        # bucket mode, N>1 record exchange (enable_records): no dedup — every
+        # occurrence's key goes into ukeys at its send-segment position
+        # (destination d from d * ucap), its occurrence index into ``spj``;
+        # pos_of maps j to that position (the rows come back there)
+        self.spj = None
 
         self.h = hip()
         self.device = torch.device(device) if device is not None else torch.device(
@@ -173,7 +178,7 @@ class Deduper:
                             self.usingle.data_ptr() if self.usingle is not None else 0,
                             self.ndest, self.lay_n or 0, self.msub,
                             self.usub.data_ptr() if self.usub is not None else 0,
-                            self.rbits)
+                            self.rbits, self.spj.data_ptr() if self.spj is not None else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self, self._lay(n), int(used or 0))
         # the scratch is all-EMPTY between calls: the finish kernel resets the
@@ -224,6 +229,21 @@ class Deduper:
         if self.usub is None or self.usub.numel() != self.nranks * Pd * self.msub:
             raise RuntimeError("sub_table: split_for_servers(m) with this layout first")
         return self.usub
+
+    def enable_records(self) -> None:
+        """Route every occurrence instead of the unique keys (bucket mode,
+        N>1 engines with a fixed ``lay_n``, no sub-buckets): ukeys holds the
+        occurrences' keys at their send-segment positions, ``spj`` their
+        occurrence indices, ``ucount`` the records per destination, and the
+        run tables the records per bucket (the servers dedup them)."""
+        if self.mode != "bucket" or not self.lay_n or self.msub != 1:
+            raise RuntimeError("enable_records needs mode='bucket', lay_n and no sub-buckets")
+        if self.spj is None:
+            self.spj = torch.empty(self.nranks * self.ucap, dtype=torch.int32,
+                                   device=self.device)
+        self.need_pos = True
+        self.need_bkt = False
+        self.materialize_inv = False
 
     def track_singletons(self) -> None:
         """Have the dedup flag the unique keys that occur once (bucket mode)."""

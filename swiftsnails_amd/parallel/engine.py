@@ -111,12 +111,23 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
     depth           : route-buffer ring depth
 
     A ``Round`` aliases engine-owned buffers of its ring slot: it is valid
-    until that slot is routed again (``depth`` routes later)."""
+    until that slot is routed again (``depth`` routes later).
+
+    exchange        : what an N>1 xGMI round ships for dim-1 rows —
+                      ``"unique"`` (each source's unique keys; per-unique
+                      rows and gradients, the worker merges its occurrences)
+                      or ``"records"`` (every occurrence: no worker dedup or
+                      merge, the servers dedup and merge what they receive;
+                      ``Round.uvals`` / ``ugrad`` are then per occurrence at
+                      its send-segment position).  Records halve the
+                      per-rank kernel work at N <= 4 but double the link
+                      bytes (docs/PERFORMANCE.md): not the default."""
 
     def __init__(self, table, transport: Optional[Transport], max_keys: int, dim: int,
                  frag_num: int = 0, server_ranks: Optional[Sequence[int]] = None, device=None,
                  count_transport: Optional[Transport] = None, depth: Optional[int] = None,
-                 pull_transport: Optional[Transport] = None, zero_grad: bool = True):
+                 pull_transport: Optional[Transport] = None, zero_grad: bool = True,
+                 exchange: str = "unique"):
         self.t = transport or LoopbackTransport()
         self.ct = count_transport or self.t
         self.pt = pull_transport or self.ct
@@ -144,6 +155,17 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         from .xgmi import XgmiTransport
 
         self.xg = self.t if isinstance(self.t, XgmiTransport) else None
+        # record exchange (N>1 over the mailboxes, scalar rows): chosen by the
+        # caller for a model whose compute handles per-occurrence rows
+        # (SparseLRWorker; bench.py / the launcher pass SS_XCHG).  Every N>1
+        # deduper of the process takes its bucket layout: set before any is
+        # sized
+        if exchange not in ("unique", "records"):
+            raise ValueError(f"exchange must be unique or records, not {exchange!r}")
+        self.records = bool(exchange == "records" and self.gpu and self.dist and
+                            self.xg is not None and int(dim) == 1)
+        if self.gpu and self.dist:
+            _hip().bd_set_record_layout(int(self.records))
         # N>1 on GPU: segment strides a multiple of 64 rows (aligned peer stores)
         self.max_keys = int(max_keys) if not (self.gpu and self.dist) else \
             -(-int(max_keys) // 64) * 64

@@ -57,12 +57,16 @@ class DeviceSetup:
         for dd in self.dedupers:
             dd.lay_n = cap
         self.Pd = h.bd_buckets(cap, N, self.dedupers[0].ndest) // N
-        self.sub = h.srv_sub_buckets(N)
+        # record exchange: a server bucket is N runs of records sized for one
+        # LDS table together (bdedup.hip bd_target), no sub-buckets
+        self.sub = 1 if self.records else h.srv_sub_buckets(N)
         self.Ps = self.Pd * self.sub
         # sub > 1: every source groups its runs by the servers' sub-bucket
         # and sends the offsets with them (the server reads exact ranges)
         for dd in self.dedupers:
             dd.split_for_servers(self.sub)
+            if self.records:
+                dd.enable_records()
         Psub = self.Pd * self.sub if self.sub > 1 else 0
         # every rank's max_keys must agree (it fixes Pd)
         mk = torch.tensor([cap, -cap], dtype=torch.int64, device=dev)

@@ -33,7 +33,9 @@ def _train_eval(rank, world, dev, transport):
 
     data = CtrSynth(batch_size=B // world, num_fields=F, num_features=FEATS, tail_frac=0.05)
     table = make_lr_table(FEATS, world, device=dev)
-    eng = PSEngine(table, transport, max_keys=(B // world) * F, dim=1, device=dev)
+    eng = PSEngine(table, transport, max_keys=(B // world) * F, dim=1, device=dev,
+                   exchange=os.environ.get("SS_TEST_XCHG", "unique"))
+    assert eng.records == (world > 1 and os.environ.get("SS_TEST_XCHG") == "records")
     w = SparseLRWorker(eng, data, rank=rank, world=world)
     for _ in range(STEPS):
         w.step()
@@ -106,6 +108,10 @@ def _ref():
     ("sync", {"SS_PULL_AHEAD": "0"}, 0.005),
     ("staleness1", {"SS_PULL_AHEAD": "1", "SS_STALENESS": "1"}, 0.01),
     ("staleness2", {"SS_PULL_AHEAD": "1", "SS_STALENESS": "2"}, 0.01),
+    # the record exchange (every occurrence shipped, servers dedup + merge)
+    ("sync", {"SS_PULL_AHEAD": "0", "SS_TEST_XCHG": "records"}, 0.005),
+    ("staleness2", {"SS_PULL_AHEAD": "1", "SS_STALENESS": "2", "SS_TEST_XCHG": "records"},
+     0.01),
 ])
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_eval_matches_world1(world, mode, env, bound):

@@ -477,6 +477,44 @@ def _graph_after_mode_switch_body(dev):
     assert np.isfinite(w.mean_loss())
 
 
+@pytest.mark.parametrize("occ", ["arena", "copy"])
+def test_record_exchange_world1_matches_unique(dev, monkeypatch, occ):
+    """The record exchange (every occurrence shipped; the server dedups what
+    it receives, fills a row per occurrence and merges the per-occurrence
+    gradients with the AdaGrad update fused — no worker dedup or merge)
+    through a size-1 xGMI arena trains like the unique-key exchange on the
+    same path: the same keys, the same losses and parameters up to float
+    summation order (SS_REC_OCC: the forward reads the rows mailbox or a
+    cached copy).  Graph tests run in a child process (tests/_mp.py)."""
+    in_child(_record_exchange_body, dev, occ)
+
+
+def _record_exchange_body(dev, occ):
+    os.environ["SS_ENGINE_GENERAL"] = "xgmi"
+    os.environ["SS_PULL_AHEAD"] = "0"
+    os.environ["SS_REC_OCC"] = occ
+    os.environ["SS_XGMI_TIMEOUT"] = "30"
+    from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+    torch.cuda.set_device(dev)
+    out = {}
+    for ex in ("unique", "records"):
+        w, t = _graph_worker("lr", dev, transport=XgmiTransport(0, 1, dev, None), exchange=ex)
+        assert w.engine.records == (ex == "records")
+        assert (w.rocc is not None) == (ex == "records" and occ == "copy")
+        losses = [float(w.step().sum().item()) for _ in range(12)]
+        torch.cuda.synchronize()
+        w.engine.check()
+        t.check()
+        out[ex] = (losses, t.to_dict(with_state=True))
+    (lu, tu), (lr_, tr) = out["unique"], out["records"]
+    np.testing.assert_allclose(lr_, lu, rtol=1e-4, atol=1e-5)
+    assert tr.keys() == tu.keys()
+    ks = list(tu.keys())
+    a, b = np.stack([tu[k] for k in ks]), np.stack([tr[k] for k in ks])
+    np.testing.assert_allclose(b, a, rtol=1e-3, atol=1e-5)
+
+
 def test_lr_slot32_matches_slot64(dev, monkeypatch):
     """One-GPU sparse LR with the pull storing 4-byte slot indices for the
     fused merge + AdaGrad update (default, shards under 2^31 slots) trains

@@ -1,0 +1,20 @@
+# N>1 record exchange (SS_XCHG records vs unique): GPU tests, 1-rank N>1 path, 4 and 8 ranks on one GPU
+set -u
+export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/s36; mkdir -p $O
+timeout -k 10 900 python -u -m pytest -x -q --timeout 200 --timeout-method thread -p no:cacheprovider tests/test_gpu_kernels.py::test_server_bucket_past_parking_area "tests/test_gpu_models.py::test_record_exchange_world1_matches_unique" tests/test_gpu_eval_sharded.py -m gpu > $O/pytest.log 2>&1 || { grep -E "Error|error|FAILED|^E " $O/pytest.log | head -40; tail -5 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+for r in 1 2; do
+  for x in records unique; do
+    SS_XCHG=$x SS_ENGINE_GENERAL=xgmi timeout -k 10 200 python bench.py --steps 50 --warmup 10 --cal-steps 0 > $O/x_${x}_$r.json 2>$O/x_${x}_$r.err || { tail -20 $O/x_${x}_$r.err; exit 1; }
+    python -c "import json; d=json.loads(open('$O/x_${x}_$r.json').read().splitlines()[-1]); print('$x xgmi1', d['ms_per_step'], d['config']['loss_last'])"
+  done
+done
+SS_REC_OCC=copy SS_ENGINE_GENERAL=xgmi timeout -k 10 200 python bench.py --steps 50 --warmup 10 --cal-steps 0 > $O/x_copy.json 2>$O/x_copy.err || { tail -20 $O/x_copy.err; exit 1; }
+python -c "import json; d=json.loads(open('$O/x_copy.json').read().splitlines()[-1]); print('records+copy xgmi1', d['ms_per_step'], d['config']['loss_last'])"
+for w in 4 8; do
+  for x in records unique; do
+    SS_XCHG=$x timeout -k 10 400 python tools/prof_world.py --world $w --no-prof --out $O/w${w}_$x --timeout 300 -- --transport xgmi --cal-steps 0 > $O/w${w}_$x.log 2>&1 || { tail -20 $O/w${w}_$x.log; exit 1; }
+    python -c "import json; d=json.loads([l for l in open('$O/w${w}_$x/rank0.log') if l.startswith('{')][-1]); print('$x world$w', d['ms_per_step'], d['config']['loss_last'])"
+  done
+done
