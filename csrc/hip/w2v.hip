@@ -958,15 +958,146 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
 // many loads per config-3 step); k_w2v_ppctx (one wave per run position)
 // gathers g+ * v over the 2W centers that pair with it.
 static constexpr int kPpMaxK = 16;
+// One wave per center; its 2W pairs run as an S-stage pipeline: pairs o+1 ..
+// o+S-1 have their 1 + K rows in flight while pair o computes (the per-pair
+// row-load chain, not bandwidth, bounds the kernel).  KT: the compile-time
+// bound of K (5, word2vec's default), so the row stages take S x (1 + KT) x
+// D/64 registers — at KT = 5, S = 3: two pairs in flight at 5+ waves per
+// SIMD, against one pair at 122 VGPRs (4 waves) when every stage was sized
+// for 16 negatives (k_w2v_pp16 below, any K).  The wave's center, its
+// pairs' context ids and its negatives' ids are wave-uniform: scalar loads,
+// no lane shuffles.
+template <int D, int KT, int S>
+__global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv_c,
+                                                const uint32_t* __restrict__ inv_w,
+                                                const uint32_t* __restrict__ inv_n,
+                                                const int32_t* __restrict__ meta, int B, int W,
+                                                int K, const float* __restrict__ uvals,
+                                                float* __restrict__ ograd,
+                                                float* __restrict__ gpair,
+                                                float* __restrict__ loss_sum,
+                                                float* __restrict__ pair_sum,
+                                                float2* __restrict__ gnc) {
+  constexpr int R = (D + 63) / 64;
+  __shared__ float red[2][4];
+  const int lane = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const long long t = (long long)blockIdx.x * 4 + w;
+  float loss = 0.f, npairs = 0.f;
+  if (t < B) {  // wave-uniform
+    const int P2 = 2 * W;
+    const uint32_t c = inv_c[t];
+    const int32_t mt = meta[t + W];
+    const long long nb0 = t * (long long)P2 * K;
+    // pair o's context row id (kInv: not a valid pair); uniform
+    auto ctx = [&](int o) -> uint32_t {
+      const int dq = o < W ? o - W : o - W + 1;
+      const long long q = t + W + dq;
+      return (c != kInv && w2v_pair_ok(mt, meta[q], dq)) ? inv_w[q] : kInv;
+    };
+    float v[R], gv[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const int d = lane + 64 * r;
+      v[r] = (d < D && c != kInv) ? uvals[(long long)c * D + d] : 0.f;
+      gv[r] = 0.f;
+    }
+    // rows of pair o into (u, n); nothing when the pair is not valid
+    auto issue = [&](int o, uint32_t xq, float (&u)[R], float (&n)[KT][R]) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int d = lane + 64 * r;
+        u[r] = (d < D && xq != kInv) ? uvals[(long long)xq * D + d] : 0.f;
+      }
+      const long long nb = nb0 + (long long)o * K;
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        const uint32_t x = (k < K && xq != kInv) ? inv_n[nb + k] : kInv;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const int d = lane + 64 * r;
+          n[k][r] = (x != kInv && d < D) ? uvals[(long long)x * D + d] : 0.f;
+        }
+      }
+    };
+    auto compute = [&](int o, uint32_t xq, const float (&u)[R], const float (&n)[KT][R]) {
+      const long long nb = (t * P2 + o) * (long long)K;
+      if (xq == kInv) {  // the pair's negatives get a zero entry
+        if (lane < K) gnc[nb + lane] = make_float2(0.f, __uint_as_float(kInv));
+        if (lane == 0) gpair[t * P2 + o] = 0.f;
+        return;
+      }
+      float sp = 0.f;
+#pragma unroll
+      for (int r = 0; r < R; ++r) sp += v[r] * u[r];
+      for (int m = 32; m > 0; m >>= 1) sp += __shfl_xor(sp, m, 64);
+      const float gp = sigm(sp) - 1.f;  // d/ds softplus(-s)
+      if (lane == 0) {
+        loss += softplus(-sp);
+        npairs += 1.f;
+        gpair[t * P2 + o] = gp;
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) gv[r] += gp * u[r];
+      float gk = 0.f;  // lane k < K: negative k's gn
+#pragma unroll
+      for (int k = 0; k < KT; ++k) {
+        if (k >= K) break;
+        float sn = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) sn += v[r] * n[k][r];
+        for (int m = 32; m > 0; m >>= 1) sn += __shfl_xor(sn, m, 64);
+        const float gn = sigm(sn);  // d/ds softplus(s)
+        if (lane == 0) loss += softplus(sn);
+        if (lane == k) gk = gn;
+#pragma unroll
+        for (int r = 0; r < R; ++r) gv[r] += gn * n[k][r];
+      }
+      if (lane < K) gnc[nb + lane] = make_float2(gk, __uint_as_float(c));
+    };
+    float u[S][R], n[S][KT][R];
+    uint32_t xs[S];
+#pragma unroll
+    for (int q = 0; q < S - 1; ++q)
+      if (q < P2) {
+        xs[q] = ctx(q);
+        issue(q, xs[q], u[q], n[q]);
+      }
+    for (int o0 = 0; o0 < P2; o0 += S) {
+#pragma unroll
+      for (int q = 0; q < S; ++q) {
+        const int o = o0 + q, oi = o + S - 1;
+        if (oi < P2) {  // pair oi into the stage pair o - 1 freed
+          xs[(q + S - 1) % S] = ctx(oi);
+          issue(oi, xs[(q + S - 1) % S], u[(q + S - 1) % S], n[(q + S - 1) % S]);
+        }
+        if (o < P2) compute(o, xs[q], u[q], n[q]);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+      if (lane + 64 * r < D) ograd[t * D + lane + 64 * r] = gv[r];
+  }
+  if (lane == 0) {
+    red[0][w] = loss;
+    red[1][w] = npairs;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (loss_sum) ctr_addf(loss_sum, red[0][0] + red[0][1] + red[0][2] + red[0][3]);
+    if (pair_sum) ctr_addf(pair_sum, red[1][0] + red[1][1] + red[1][2] + red[1][3]);
+  }
+}
+
 static constexpr int kPpIdx = 8;  // negative indices per lane: 2W * K <= 64 * 8
-// One wave per center; the 2W pairs run as a two-stage pipeline: every
+// Any K <= 16 (k_w2v_pp16): one wave per center; the 2W pairs run as a two-stage pipeline: every
 // index of the center (contexts, pair validity, all 2W x K negatives) is
 // loaded up front, one lane each, and pair o+1's 1 + K rows are in flight
 // while pair o computes — one row-load latency per pair instead of an
 // index load followed by a row load (measured: the per-pair chain, not
 // bandwidth, bounded the kernel).
 template <int D>
-__global__ __launch_bounds__(256) void k_w2v_pp(const uint32_t* __restrict__ inv_c,
+__global__ __launch_bounds__(256) void k_w2v_pp16(const uint32_t* __restrict__ inv_c,
                                                 const uint32_t* __restrict__ inv_w,
                                                 const uint32_t* __restrict__ inv_n,
                                                 const int32_t* __restrict__ meta, int B, int W,
@@ -1359,6 +1490,17 @@ void launch_w2v_win(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t
   check_launch("k_w2v_win_bf16");
 }
 
+// SS_W2V_PP_STAGES: pipeline stages of the K <= 5 kernel, 3 (default) or 4;
+// 2: the K <= 16 kernel for every K.  Measured (1M vocab, dim 128, K = 5,
+// serialised): 110.5 / 122.6 / 171 us; step 0.542 / 0.551 / 0.607-0.610 ms
+static int pp_stages() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_W2V_PP_STAGES");
+    return e ? std::atoi(e) : 3;
+  }();
+  return v;
+}
+
 void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t* inv_n,
                    const int32_t* meta, int B, int W, int K, int D, const float* uvals,
                    float* ograd, float* gpair, float* loss_sum, float* pair_sum, hipStream_t st,
@@ -1372,9 +1514,18 @@ void launch_w2v_pp(const uint32_t* inv_c, const uint32_t* inv_w, const uint32_t*
   switch (D) {
 #define SS_W2VP_CASE(DD)                                                                       \
   case DD:                                                                                     \
-    hipLaunchKernelGGL(k_w2v_pp<DD>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st, inv_c,    \
-                       inv_w, inv_n, meta, B, W, K, uvals, ograd, gpair, loss_sum, pair_sum,   \
-                       reinterpret_cast<float2*>(gnc));                                        \
+    if (K <= 5 && pp_stages() == 3)                                                            \
+      hipLaunchKernelGGL((k_w2v_pp<DD, 5, 3>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,  \
+                         inv_c, inv_w, inv_n, meta, B, W, K, uvals, ograd, gpair, loss_sum,     \
+                         pair_sum, reinterpret_cast<float2*>(gnc));                             \
+    else if (K <= 5 && pp_stages() > 3)                                                        \
+      hipLaunchKernelGGL((k_w2v_pp<DD, 5, 4>), dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,  \
+                         inv_c, inv_w, inv_n, meta, B, W, K, uvals, ograd, gpair, loss_sum,     \
+                         pair_sum, reinterpret_cast<float2*>(gnc));                             \
+    else                                                                                       \
+      hipLaunchKernelGGL(k_w2v_pp16<DD>, dim3((unsigned)((B + 3) / 4)), dim3(256), 0, st,       \
+                         inv_c, inv_w, inv_n, meta, B, W, K, uvals, ograd, gpair, loss_sum,     \
+                         pair_sum, reinterpret_cast<float2*>(gnc));                             \
     check_launch("k_w2v_pp");                                                                  \
     hipLaunchKernelGGL(k_w2v_ppctx<DD>, dim3((unsigned)((Rn + 3) / 4)), dim3(256), 0, st,       \
                        inv_c, gpair, B, W, uvals, ograd);                                      \

@@ -114,10 +114,10 @@ class PSContext:
         rt = float(cfg.get("round_timeout", 600) or 0)
         self.watchdog = Watchdog(rt, self.failure) if rt > 0 else None
         self.heartbeat = None
-        if store is not None and float(cfg.get("peer_timeout", 120) or 0) > 0:
+        if store is not None and float(cfg.get("peer_timeout", 30) or 0) > 0:
             self.heartbeat = Heartbeat(store, self.rank, self.world, self.failure,
                                        interval=float(cfg.get("heartbeat_interval", 2.0)),
-                                       peer_timeout=float(cfg.get("peer_timeout", 120)))
+                                       peer_timeout=float(cfg.get("peer_timeout", 30)))
         self.fault = FaultInjector(rank=self.rank)
         # resume_from: a checkpoint prefix, or "latest" = the newest complete
         # periodic backup under param_backup_root (restart-after-failure:

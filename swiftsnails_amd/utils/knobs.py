@@ -140,6 +140,9 @@ KNOBS: dict[str, Knob] = {
                       "LR forward layout: packed | group (auto by lane utilisation)"),
     "SS_FM_REDUCE": Knob("sorted", "csrc/hip/bdedup.hip, models/fm.py", "tuning",
                          "FM gradient merge: sorted lists, or atomic (LDS float atomics)"),
+    "SS_W2V_PP_STAGES": Knob("3", "csrc/hip/w2v.hip", "tuning",
+                             "word2vec per-pair negatives (K <= 5): pipeline stages of the "
+                             "pair kernel (3 or 4); 2 = the any-K kernel"),
     "SS_W2V_MFMA": Knob("bf16", "models/word2vec.py", "tuning",
                         "word2vec tile: bf16 MFMA (77 KB LDS) or f32 (116 KB)"),
     "SS_RCCL_COMMS": Knob("1", "parallel/transport.py, bench.py", "ops",
