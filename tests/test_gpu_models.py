@@ -507,6 +507,14 @@ def _record_exchange_body(dev, occ):
         w.engine.check()
         t.check()
         out[ex] = (losses, t.to_dict(with_state=True))
+        if ex == "records" and occ == "arena":  # the record round captured as hipGraphs
+            assert w.enable_graph()
+            for _ in range(2 * w._gper):
+                w.step()
+            torch.cuda.synchronize()
+            w.engine.check()
+            t.check()
+            assert np.isfinite(w.mean_loss()) and 0 < w.mean_loss() < 0.7
     (lu, tu), (lr_, tr) = out["unique"], out["records"]
     np.testing.assert_allclose(lr_, lu, rtol=1e-4, atol=1e-5)
     assert tr.keys() == tu.keys()
