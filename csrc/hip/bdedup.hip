@@ -77,25 +77,25 @@ static constexpr int kBdTargetDist = 1024;
 // SS_BD_TARGET (one rank): occurrences per bucket, 1024..3584 (A/B: larger
 // buckets make each (chunk, bucket) run of the scatter longer — fewer partial
 // lines — at the price of a fuller LDS table in the dedup)
-// N>1 record exchange (bd_set_record_layout): the sources ship every
-// occurrence, not their unique keys, so server bucket k is the union of N
-// runs of records and must hold about one one-rank bucket: 3584 / N records
-// per source bucket (the bucket-count cap raises it at N = 8, ~620 at the
-// bench shape: ~5000 records, ~2000 distinct keys per server bucket)
-static int g_bd_records = 0;
-static int bd_target(int nranks) {
+// N>1 record exchange (the kBdRecLayout bit of the layout's ndest argument,
+// Deduper(record_layout=True)): the sources ship every occurrence, not their
+// unique keys, so server bucket k is the union of N runs of records and must
+// hold about one one-rank bucket: 3584 / N records per source bucket (the
+// bucket-count cap raises it at N = 8, ~620 at the bench shape: ~5000
+// records, ~2000 distinct keys per server bucket).  A property of the layout
+// (every call and helper of a deduper passes the same ndest), not of the
+// process: engines of either kind can coexist.
+static constexpr int kBdRecLayout = 1 << 16;
+static int bd_target(int nranks, bool rec) {
   static const int one = [] {
     const char* e = std::getenv("SS_BD_TARGET");
     const int v = e ? std::atoi(e) : kBdTarget;
     return v < 1024 ? 1024 : (v > 3584 ? 3584 : v);
   }();
-  if (nranks > 1 && g_bd_records) return std::max(256, kBdTarget / nranks);
+  if (nranks > 1 && rec) return std::max(256, kBdTarget / nranks);
   return nranks > 1 ? kBdTargetDist : one;
 }
-// every N>1 deduper of the process lays its buckets out for the record
-// exchange (on) or the unique-key exchange (off); set before the dedupers'
-// scratch is sized — the layout is what every rank and server agree on
-void bd_set_record_layout(int on) { g_bd_records = on ? 1 : 0; }
+int bd_record_layout_bit() { return kBdRecLayout; }
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
 static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
@@ -175,15 +175,17 @@ struct BdLayout {
 };
 
 static int bd_clamp_ndest(int nranks, int ndest) {
+  ndest &= ~kBdRecLayout;
   return ndest < 1 || ndest > nranks ? nranks : ndest;
 }
 
 static BdLayout bd_layout(long long n, int nranks, int ndest) {
   BdLayout L{};
+  const bool rec = (ndest & kBdRecLayout) != 0;
   ndest = bd_clamp_ndest(nranks, ndest);
   // ~2048 occurrences per bucket, but at least ~1024 buckets for small calls
   // (>= 4 workgroups per CU; a word2vec step of 196K keys got only 96 buckets)
-  const int tg = bd_target(nranks);
+  const int tg = bd_target(nranks, rec);
   long long target = std::min<long long>(tg, std::max<long long>(128, n / 1024));
   if (n > (long long)kBdMaxBuckets * tg) target = (n + kBdMaxBuckets - 1) / kBdMaxBuckets;
   // buckets per destination from the keys one destination receives (n /
@@ -230,9 +232,11 @@ long long bd_max_keys() { return (long long)kBdMaxBuckets * 2800; }
 // wave count), so bound P and nch over all m <= n instead of sizing for n
 long long bd_scratch_words(long long n, int nranks, int ndest) {
   if (n < 1) n = 1;
+  const int ndest_arg = ndest;
+  const bool rec = (ndest & kBdRecLayout) != 0;
   ndest = bd_clamp_ndest(nranks, ndest);
   // active buckets (those of receiving destinations), then all P = Pd * nranks
-  const int tg = bd_target(nranks);
+  const int tg = bd_target(nranks, rec);
   long long pact = std::max<long long>(1056, (n + tg - 1) / tg);
   pact = std::min<long long>(pact, kBdMaxBuckets) + 2 * ndest;
   const long long pmax = ((pact + ndest - 1) / ndest + 1) * nranks;
@@ -241,7 +245,7 @@ long long bd_scratch_words(long long n, int nranks, int ndest) {
   nchmax = std::min<long long>(nchmax, (n + kBdChunkLanes - 1) / kBdChunkLanes);
   nchmax = std::max<long long>(nchmax, 1);
   const long long bound = 4 + pmax * nchmax + 4 * pmax + 1;
-  return std::max(bound, bd_layout(n, nranks, ndest).total);
+  return std::max(bound, bd_layout(n, nranks, ndest_arg).total);
 }
 int bd_buckets(long long n, int nranks, int ndest) {
   return bd_layout(n < 1 ? 1 : n, nranks, ndest).P;
@@ -1254,8 +1258,10 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   // positions (d * ucap + ...) with the run tables and per-destination
   // counts, then the scatter writes every occurrence's key into ukeys and its
   // index into spj at that position (the servers dedup what they receive)
-  if (spj && (!ukeys || !ucount || rs.nranks > kRecMaxDest || msub != 1 || !pos_of))
-    throw_error("bdedup: the record exchange needs ukeys, ucount, pos_of, <= 64 ranks, no sub-buckets");
+  if (spj && (!ukeys || !ucount || rs.nranks > kRecMaxDest || msub != 1 || !pos_of ||
+              !(ndest & kBdRecLayout)))
+    throw_error("bdedup: the record exchange needs ukeys, ucount, pos_of, <= 64 ranks, no "
+                "sub-buckets and the record layout");
   if (rs.rbits < 0 || rs.rbits > 20) throw_error("bdedup: region bits 0..20");
   if (msub < 1 || msub > kBdMaxSub || (msub > 1 && !usub))
     throw_error("bdedup: server sub-buckets 1..64 (and their offset table)");

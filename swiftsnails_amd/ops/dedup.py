@@ -61,7 +61,7 @@ class Deduper:
 
     def __init__(self, max_n: int, nranks: int = 1, frag_map: Optional[torch.Tensor] = None,
                  gdim: int = 1, device=None, with_grad: bool = True, zero_grad: bool = True,
-                 mode: Optional[str] = None):
+                 mode: Optional[str] = None, record_layout: bool = False):
         from .._native import hip
 
         self.mode = mode or os.environ.get("SS_DEDUP", "bucket")
@@ -118,7 +118,13 @@ class Deduper:
         d = self.device
         if frag_map is None:
             frag_map = torch.zeros(1, dtype=torch.int32)
-        self.ndest = effective_ndest(frag_map, self.nranks)
+        # the layout argument every bucket helper takes: the destinations the
+        # buckets are sized for, plus (record_layout: N>1 record exchange,
+        # enable_records) the record-layout bit — smaller source buckets, so
+        # that N sources' records fill one server bucket (bdedup.hip)
+        self.record_layout = bool(record_layout)
+        self.ndest = effective_ndest(frag_map, self.nranks) | (
+            self.h.bd_record_layout_bit() if self.record_layout else 0)
         self.frag_map = frag_map.to(d, torch.int32).contiguous()
         m = max(1, self.max_n)
         if self.mode == "bucket" and m > self.h.bd_max_keys():
@@ -236,8 +242,9 @@ class Deduper:
         occurrences' keys at their send-segment positions, ``spj`` their
         occurrence indices, ``ucount`` the records per destination, and the
         run tables the records per bucket (the servers dedup them)."""
-        if self.mode != "bucket" or not self.lay_n or self.msub != 1:
-            raise RuntimeError("enable_records needs mode='bucket', lay_n and no sub-buckets")
+        if self.mode != "bucket" or not self.lay_n or self.msub != 1 or not self.record_layout:
+            raise RuntimeError("enable_records needs mode='bucket', lay_n, no sub-buckets and "
+                               "Deduper(record_layout=True)")
         if self.spj is None:
             self.spj = torch.empty(self.nranks * self.ucap, dtype=torch.int32,
                                    device=self.device)

@@ -157,15 +157,12 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self.xg = self.t if isinstance(self.t, XgmiTransport) else None
         # record exchange (N>1 over the mailboxes, scalar rows): chosen by the
         # caller for a model whose compute handles per-occurrence rows
-        # (SparseLRWorker; bench.py / the launcher pass SS_XCHG).  Every N>1
-        # deduper of the process takes its bucket layout: set before any is
-        # sized
+        # (SparseLRWorker; bench.py / the launcher pass SS_XCHG).  The
+        # engine's dedupers (and its lookup's) take the record bucket layout
         if exchange not in ("unique", "records"):
             raise ValueError(f"exchange must be unique or records, not {exchange!r}")
         self.records = bool(exchange == "records" and self.gpu and self.dist and
                             self.xg is not None and int(dim) == 1)
-        if self.gpu and self.dist:
-            _hip().bd_set_record_layout(int(self.records))
         # N>1 on GPU: segment strides a multiple of 64 rows (aligned peer stores)
         self.max_keys = int(max_keys) if not (self.gpu and self.dist) else \
             -(-int(max_keys) // 64) * 64
@@ -191,8 +188,10 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self.tracer = Tracer(enabled=False)
         fm = torch.from_numpy(self.frag_map.astype(np.int32))
         dd_cls = Deduper if self.gpu else CpuDeduper
+        rl = {"record_layout": True} if self.records else {}
         self.dedupers = [dd_cls(self.max_keys, nranks=self.world, frag_map=fm, gdim=self.dim,
-                                device=self.device, zero_grad=zero_grad) for _ in range(self.depth)]
+                                device=self.device, zero_grad=zero_grad, **rl)
+                         for _ in range(self.depth)]
         N, cap, d, dev = self.world, self.max_keys, self.dim, self.device
         self.uvals = [torch.empty((N * cap, d), dtype=torch.float32, device=dev)
                       for _ in range(self.depth)]

@@ -84,7 +84,7 @@ class DeviceSetup:
             from ..ops.dedup import Deduper
 
             lk = Deduper(self.max_keys, nranks=N, frag_map=self.dedupers[0].frag_map.cpu(),
-                         gdim=d, device=dev)
+                         gdim=d, device=dev, record_layout=self.records)
             lk.lay_n = cap
             lk.split_for_servers(self.sub)
             lk.need_ukeys = True
