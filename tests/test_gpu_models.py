@@ -834,17 +834,21 @@ def _planted_corpus(path, clusters=20, words=40, sentences=6000, length=12, seed
     return clusters, words
 
 
-@pytest.mark.parametrize("mode,neg_mode,tile", [("window", "shared", "bf16"),
-                                                ("pairs", "shared", "bf16"),
-                                                ("pairs", "shared", "f32"),
-                                                ("window", "per_pair", "f32")])
-def test_word2vec_learns_planted_clusters(dev, tmp_path, monkeypatch, mode, neg_mode, tile):
+@pytest.mark.parametrize("mode,neg_mode,tile,rows", [("window", "shared", "bf16", "fp32"),
+                                                     ("pairs", "shared", "bf16", "fp32"),
+                                                     ("pairs", "shared", "f32", "fp32"),
+                                                     ("window", "per_pair", "f32", "fp32"),
+                                                     ("window", "shared", "bf16", "bf16"),
+                                                     ("window", "per_pair", "f32", "bf16")])
+def test_word2vec_learns_planted_clusters(dev, tmp_path, monkeypatch, mode, neg_mode, tile, rows):
     """Embedding quality, not just a falling loss: on a corpus whose
     sentences each draw from one of 20 word clusters, the learned input
     vectors of words of the same cluster are far more similar (cosine) than
     of words of different clusters — for every objective variant: the
     shared-negative tile (window layout: bf16 MFMA; pairs layout: bf16 and
-    fp32 MFMA) and per-pair negatives (classic SGNS, fp32 dot products)."""
+    fp32 MFMA) and per-pair negatives (classic SGNS, fp32 dot products), on
+    fp32 rows and on compact bf16 rows (row_dtype: bf16, stochastic rounding;
+    the fused reduce + update is fp32-only, the apply kernel updates them)."""
     from swiftsnails_amd.models.word2vec import Word2VecWorker, make_w2v_table_args
     from swiftsnails_amd.ops.table import HbmTable
     from swiftsnails_amd.parallel.engine import PSEngine
@@ -855,10 +859,11 @@ def test_word2vec_learns_planted_clusters(dev, tmp_path, monkeypatch, mode, neg_
     data = FileCorpusSource(str(tmp_path / "corpus.txt"), batch_size=2048, window=4,
                             negatives=5, mode=mode, neg_mode=neg_mode, device=dev)
     opt, init = make_w2v_table_args(64, None)
-    table = HbmTable(64, 1 << 14, optimizer=opt, init=init, device=dev)
+    table = HbmTable(64, 1 << 14, optimizer=opt, init=init, device=dev, row_dtype=rows)
     eng = PSEngine(table, None, max_keys=data.n_keys, dim=64, device=dev)
     w = Word2VecWorker(eng, data)
     assert w.mfma_bf16 == (tile == "bf16") and w.per_pair == (neg_mode == "per_pair")
+    assert not (rows == "bf16" and getattr(w, "fuse", False))
     for _ in range(3 * data.steps_per_pass()):  # 3 passes
         w.step()
     torch.cuda.synchronize()
