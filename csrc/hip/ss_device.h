@@ -120,17 +120,12 @@ __device__ __forceinline__ float row_round(const DevTable& t, float v) {
   return __uint_as_float(u & 0xFFFF0000u);
 }
 
-// store v as coordinate j.  bf16: rounded stochastically when `sr` (an
-// optimizer step: round-to-nearest would drop every update below half an
-// ulp — 1/512 of the weight — so small steps would never move a weight),
-// else to nearest even; NaN / Inf keep their top bits (the init marker).
-__device__ __forceinline__ void row_st(const DevTable& t, uint64_t s, uint32_t j, float v,
-                                       bool sr = false) {
-  char* r = t.base + s * (uint64_t)t.stride + t.row_off;
-  if (!t.bf16) {
-    reinterpret_cast<float*>(r)[j] = v;
-    return;
-  }
+// v as the bf16 word a compact row stores for coordinate j of slot s:
+// rounded stochastically when `sr` (an optimizer step: round-to-nearest would
+// drop every update below half an ulp — 1/512 of the weight — so small steps
+// would never move a weight), else to nearest even; NaN / Inf keep their top
+// bits (the init marker)
+__device__ __forceinline__ unsigned short bf16_bits(uint64_t s, uint32_t j, float v, bool sr) {
   uint32_t u = __float_as_uint(v);
   if ((u & 0x7F800000u) != 0x7F800000u) {
     if (sr) {
@@ -148,7 +143,23 @@ __device__ __forceinline__ void row_st(const DevTable& t, uint64_t s, uint32_t j
       u += 0x7FFFu + ((u >> 16) & 1u);
     }
   }
-  reinterpret_cast<unsigned short*>(r)[j] = (unsigned short)(u >> 16);
+  return (unsigned short)(u >> 16);
+}
+// a stored bf16 word as fp32; the empty-slot fill (0xFFFF) reads as the fp32
+// fill 0xFFFFFFFF
+__device__ __forceinline__ float bf16_val(uint32_t u16) {
+  return __uint_as_float(u16 == 0xFFFFu ? 0xFFFFFFFFu : (u16 << 16));
+}
+
+// store v as coordinate j (bf16: bf16_bits, stochastic rounding when `sr`)
+__device__ __forceinline__ void row_st(const DevTable& t, uint64_t s, uint32_t j, float v,
+                                       bool sr = false) {
+  char* r = t.base + s * (uint64_t)t.stride + t.row_off;
+  if (!t.bf16) {
+    reinterpret_cast<float*>(r)[j] = v;
+    return;
+  }
+  reinterpret_cast<unsigned short*>(r)[j] = bf16_bits(s, j, v, sr);
 }
 
 // A list of (offset, count) segments inside one buffer.  The collective

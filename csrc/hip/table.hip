@@ -454,7 +454,32 @@ __global__ __launch_bounds__(256) void k_commit_claims(
 // instead of one (a 64-lane group per key left the pull latency-bound: 439K
 // distinct 512-B rows of a per-pair step read + written at ~1.3 TB/s).
 static constexpr int kPvL = 8;
-template <int D>
+// 4 consecutive coordinates of a wide row as one vector access: a float4
+// (fp32 rows) or 4 packed bf16 words (compact rows, one 8-byte access)
+template <bool B16>
+__device__ __forceinline__ float4 row4_ld(const char* row, int q) {
+  if constexpr (B16) {
+    const uint2 x = reinterpret_cast<const uint2*>(row)[q];
+    return make_float4(bf16_val(x.x & 0xFFFFu), bf16_val(x.x >> 16), bf16_val(x.y & 0xFFFFu),
+                       bf16_val(x.y >> 16));
+  } else {
+    return reinterpret_cast<const float4*>(row)[q];
+  }
+}
+// ... and stored: bf16 words rounded as row_st does (coordinate j0 + 0..3 of
+// slot s; `sr`: stochastically, for optimizer steps)
+template <bool B16>
+__device__ __forceinline__ void row4_st(char* row, int q, float4 v, uint64_t s, uint32_t j0,
+                                        bool sr) {
+  if constexpr (B16) {
+    const uint32_t a = bf16_bits(s, j0, v.x, sr), b = bf16_bits(s, j0 + 1, v.y, sr);
+    const uint32_t c = bf16_bits(s, j0 + 2, v.z, sr), d = bf16_bits(s, j0 + 3, v.w, sr);
+    reinterpret_cast<uint2*>(row)[q] = make_uint2(a | (b << 16), c | (d << 16));
+  } else {
+    reinterpret_cast<float4*>(row)[q] = v;
+  }
+}
+template <int D, bool B16>
 __global__ __launch_bounds__(256) void k_pull_rows_bk(DevTable t, const uint64_t* __restrict__ bkeys,
                                                       const uint32_t* __restrict__ bstart,
                                                       const uint32_t* __restrict__ unum,
@@ -493,23 +518,25 @@ __global__ __launch_bounds__(256) void k_pull_rows_bk(DevTable t, const uint64_t
       for (uint32_t j = lg; j < t.width; j += kPvL) {
         const float v = j < (uint32_t)D ? init_value(ip, key, j, D) : ip.state_init;
         if (!t.prefilled) row_st(t, slot, j, v);
-        if (j < (uint32_t)D) out[((long long)base + l) * D + j] = v;
+        // a compact row returns its initial value as stored (row_round)
+        if (j < (uint32_t)D) out[((long long)base + l) * D + j] = row_round(t, v);
       }
       ins += (lg == 0);
     } else {
       // (loading the home slot's row beside the probe's key load measured
       // neutral: 148 vs 152 us for the per-pair pull)
-      const float4* r = reinterpret_cast<const float4*>(slot_row(t, slot));
+      const char* r = reinterpret_cast<const char*>(slot_row(t, slot));
       float4 v[NV];
 #pragma unroll
-      for (int k = 0; k < NV; ++k) v[k] = r[lg + k * kPvL];
+      for (int k = 0; k < NV; ++k) v[k] = row4_ld<B16>(r, lg + k * kPvL);
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
         const uint32_t j = 4u * (lg + k * kPvL);
-        v[k].x = fresh_or(v[k].x, ip, key, j, D);
-        v[k].y = fresh_or(v[k].y, ip, key, j + 1, D);
-        v[k].z = fresh_or(v[k].z, ip, key, j + 2, D);
-        v[k].w = fresh_or(v[k].w, ip, key, j + 3, D);
+        // (row_round: a compact row's fresh value as it will be stored)
+        v[k].x = row_round(t, fresh_or(v[k].x, ip, key, j, D));
+        v[k].y = row_round(t, fresh_or(v[k].y, ip, key, j + 1, D));
+        v[k].z = row_round(t, fresh_or(v[k].z, ip, key, j + 2, D));
+        v[k].w = row_round(t, fresh_or(v[k].w, ip, key, j + 3, D));
         o[lg + k * kPvL] = v[k];
       }
     }
@@ -715,7 +742,7 @@ __global__ __launch_bounds__(256) void k_apply(DevTable t, const long long* __re
 // parameters, optimizer state and gradient moved as 16-byte vectors (the
 // 64-lane group per key kept one key's load -> update -> store chain per
 // wave in flight).
-template <int D>
+template <int D, bool B16>
 __global__ __launch_bounds__(256) void k_apply_rows(DevTable t, const long long* __restrict__ slots,
                                                     const float* __restrict__ grads, SegList sl,
                                                     OptParams op,
@@ -732,17 +759,17 @@ __global__ __launch_bounds__(256) void k_apply_rows(DevTable t, const long long*
     if (only && !only[pos]) continue;  // the same for the 8 lanes of a key
     const long long slot = slots[pos];
     if (slot < 0) continue;
-    float4* row = reinterpret_cast<float4*>(slot_row(t, slot));
+    char* row = reinterpret_cast<char*>(slot_row(t, slot));
     const float4* gr = reinterpret_cast<const float4*>(grads + pos * D);
     const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 w[NV], s1[NV], s2[NV], gv[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int q = lg + k * kPvL;
-      w[k] = row[q];
+      w[k] = row4_ld<B16>(row, q);
       gv[k] = gr[q];
-      s1[k] = ns > 0 ? row[Q + q] : z;
-      s2[k] = ns > 1 ? row[2 * Q + q] : z;
+      s1[k] = ns > 0 ? row4_ld<B16>(row, Q + q) : z;
+      s2[k] = ns > 1 ? row4_ld<B16>(row, 2 * Q + q) : z;
     }
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
@@ -751,9 +778,9 @@ __global__ __launch_bounds__(256) void k_apply_rows(DevTable t, const long long*
       opt_update(op, w[k].z, s1[k].z, s2[k].z, gv[k].z);
       opt_update(op, w[k].w, s1[k].w, s2[k].w, gv[k].w);
       const int q = lg + k * kPvL;
-      row[q] = w[k];
-      if (ns > 0) row[Q + q] = s1[k];
-      if (ns > 1) row[2 * Q + q] = s2[k];
+      row4_st<B16>(row, q, w[k], (uint64_t)slot, 4u * q, true);
+      if (ns > 0) row4_st<B16>(row, Q + q, s1[k], (uint64_t)slot, 4u * (Q + q), true);
+      if (ns > 1) row4_st<B16>(row, 2 * Q + q, s2[k], (uint64_t)slot, 4u * (2 * Q + q), true);
     }
   }
 }
@@ -920,9 +947,12 @@ static bool pull_vec_on() {
   }();
   return on;
 }
+// wide rows (word2vec): fp32 rows 16-byte aligned, or compact bf16 rows
+// 8-byte aligned (4 coordinates per 8-byte access)
 static bool wide_rows(const DevTable& t) {
-  return !t.bf16 && (t.dim == 32 || t.dim == 64 || t.dim == 128) && t.row_off % 16 == 0 &&
-         t.stride % 16 == 0;
+  const int al = t.bf16 ? 8 : 16;
+  return (t.dim == 32 || t.dim == 64 || t.dim == 128) && t.row_off % al == 0 &&
+         t.stride % al == 0;
 }
 
 void launch_probe(const DevTable& t, const uint64_t* keys, const SegList& sl, long long max_n,
@@ -976,14 +1006,15 @@ void launch_pull_unique_bk(const DevTable& t, const uint64_t* bkeys, const uint3
   const int ny = G == 1 ? 4 : 2;
   // wide fp32 rows: 8 lanes per key, 16-byte row accesses (k_pull_rows_bk)
   if (!snap && pull_vec_on() && wide_rows(t) && reinterpret_cast<uintptr_t>(out) % 16 == 0) {
+#define SS_PRB(DD, B)                                                                          \
+  hipLaunchKernelGGL((k_pull_rows_bk<DD, B>), dim3(P, ny), dim3(256), 0, st, t, bkeys, bstart,   \
+                     unum, ubase, slots, out, ip, size_ctr, err)
     switch (t.dim) {
-      case 32: hipLaunchKernelGGL(k_pull_rows_bk<32>, dim3(P, ny), dim3(256), 0, st, t, bkeys,
-                                  bstart, unum, ubase, slots, out, ip, size_ctr, err); break;
-      case 64: hipLaunchKernelGGL(k_pull_rows_bk<64>, dim3(P, ny), dim3(256), 0, st, t, bkeys,
-                                  bstart, unum, ubase, slots, out, ip, size_ctr, err); break;
-      default: hipLaunchKernelGGL(k_pull_rows_bk<128>, dim3(P, ny), dim3(256), 0, st, t, bkeys,
-                                  bstart, unum, ubase, slots, out, ip, size_ctr, err); break;
+      case 32: if (t.bf16) SS_PRB(32, true); else SS_PRB(32, false); break;
+      case 64: if (t.bf16) SS_PRB(64, true); else SS_PRB(64, false); break;
+      default: if (t.bf16) SS_PRB(128, true); else SS_PRB(128, false); break;
     }
+#undef SS_PRB
     check_launch("k_pull_rows_bk");
     return;
   }
@@ -1080,14 +1111,15 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
   if (!snap && pull_vec_on() && wide_rows(t) && W == t.width &&
       reinterpret_cast<uintptr_t>(grads) % 16 == 0) {
     const long long grid = grid_for(max_n, kPvL, 1 << 22);
+#define SS_ARB(DD, B)                                                                          \
+  hipLaunchKernelGGL((k_apply_rows<DD, B>), dim3(grid), dim3(256), 0, st, t, slots, grads, sl,   \
+                     op, only)
     switch (t.dim) {
-      case 32: hipLaunchKernelGGL(k_apply_rows<32>, dim3(grid), dim3(256), 0, st, t, slots, grads,
-                                  sl, op, only); break;
-      case 64: hipLaunchKernelGGL(k_apply_rows<64>, dim3(grid), dim3(256), 0, st, t, slots, grads,
-                                  sl, op, only); break;
-      default: hipLaunchKernelGGL(k_apply_rows<128>, dim3(grid), dim3(256), 0, st, t, slots,
-                                  grads, sl, op, only); break;
+      case 32: if (t.bf16) SS_ARB(32, true); else SS_ARB(32, false); break;
+      case 64: if (t.bf16) SS_ARB(64, true); else SS_ARB(64, false); break;
+      default: if (t.bf16) SS_ARB(128, true); else SS_ARB(128, false); break;
     }
+#undef SS_ARB
     check_launch("k_apply_rows");
     return;
   }

@@ -914,6 +914,28 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
     const long long slot = slots[it.z];
     if (slot < 0) return;  // half-wave-uniform
     const int ns = opt_state_per_coord(op.kind);
+    if (tab.bf16) {
+      // compact rows: V bf16 words per lane and array, updated in fp32 and
+      // stored with stochastic rounding (row_st's rule)
+      unsigned short* r16 = reinterpret_cast<unsigned short*>(slot_row(tab, slot));
+      float wf[V], s1f[V], s2f[V];
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int j = hl * V + v;
+        wf[v] = bf16_val(r16[j]);
+        s1f[v] = ns > 0 ? bf16_val(r16[D + j]) : 0.f;
+        s2f[v] = ns > 1 ? bf16_val(r16[2 * D + j]) : 0.f;
+      }
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        const int j = hl * V + v;
+        opt_update(op, wf[v], s1f[v], s2f[v], acc[v]);
+        r16[j] = bf16_bits((uint64_t)slot, j, wf[v], true);
+        if (ns > 0) r16[D + j] = bf16_bits((uint64_t)slot, D + j, s1f[v], true);
+        if (ns > 1) r16[2 * D + j] = bf16_bits((uint64_t)slot, 2 * D + j, s2f[v], true);
+      }
+      return;
+    }
     float* row = slot_row(tab, slot) + hl * V;
     VT w = *reinterpret_cast<const VT*>(row);
     VT s1 = ns > 0 ? *reinterpret_cast<const VT*>(row + D) : VT{};
@@ -1423,9 +1445,10 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
   OptParams opv{};
   if (slots) {
     const int ns = op ? opt_state_per_coord(op->kind) : 0;
-    if (!tab || !op || tab->bf16 || (int)tab->dim != D || (int)tab->width != D * (1 + ns) ||
-        tab->row_off % 16 != 0 || tab->stride % 16 != 0)
-      throw_error("w2v_oreduce: a fused update needs fp32 rows of this D (16-byte aligned)");
+    const int al = tab && tab->bf16 ? 8 : 16;
+    if (!tab || !op || (int)tab->dim != D || (int)tab->width != D * (1 + ns) ||
+        tab->row_off % al != 0 || tab->stride % al != 0)
+      throw_error("w2v_oreduce: a fused update needs aligned rows of this D");
     tv = *tab;
     opv = *op;
   }

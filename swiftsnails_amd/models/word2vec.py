@@ -198,10 +198,9 @@ class Word2VecWorker(PipelinedWorker):
             # gradient row is one item (k_w2v_oreduce with the table), and
             # the apply kernel then only the keys it summed over several
             # items (uhot, written by k_w2v_osort); SS_W2V_FUSE=0: off
-            # (compact bf16 rows: the apply kernel updates them, the fused
-            # reduce moves fp32 rows only)
-            self.fuse = (engine.fast1 and os.environ.get("SS_W2V_FUSE", "1") != "0" and
-                         not getattr(engine.table, "bf16", False))
+            # (compact bf16 rows too: updated in fp32, stored with stochastic
+            # rounding)
+            self.fuse = engine.fast1 and os.environ.get("SS_W2V_FUSE", "1") != "0"
             self.uhot = ([torch.zeros(engine.max_keys * engine.world, dtype=torch.uint8,
                                       device=dev) for _ in range(engine.depth)]
                          if self.fuse else None)

@@ -991,7 +991,7 @@ def _bf16_round(x: np.ndarray) -> np.ndarray:
     return u.astype(np.uint32).view(np.float32)
 
 
-@pytest.mark.parametrize("G", [1, 4, 16])
+@pytest.mark.parametrize("G", [1, 4, 16, 64])
 def test_compact_bf16_rows(dev, G):
     """Compact rows (row_dtype="bf16"): half the slot bytes; a pull returns
     the bf16-rounded initial row; AdaGrad pushes track an fp32 table to bf16
@@ -1001,7 +1001,9 @@ def test_compact_bf16_rows(dev, G):
     from swiftsnails_amd.ops.optim import InitConfig, Optimizer
     from swiftsnails_amd.ops.table import HbmTable
 
-    dim = {1: 1, 4: 9, 16: 32}[G]
+    # (dim 32 / 128: word2vec's wide rows — the vectorised apply moves 4
+    # bf16 words per 8-byte access, table.hip k_apply_rows<D, true>)
+    dim = {1: 1, 4: 9, 16: 32, 64: 128}[G]
     init = InitConfig("uniform", 0.5, 0.1, seed=3)
     mk = lambda dt: HbmTable(dim, 1 << 14, optimizer=Optimizer("adagrad", lr=0.05),  # noqa: E731
                              init=init, device=dev, lane_group=G, row_dtype=dt)

@@ -1,0 +1,39 @@
+"""The record exchange's bucket layout (bdedup.hip, the kBdRecLayout bit of a
+deduper's layout argument; host-side layout functions, no GPU): a source's
+bucket holds 3584 / N records so that server bucket k — the union of the N
+sources' bucket k — holds about one one-rank bucket (~3584 records, the
+one-GPU dedup's tuned size), up to the bucket-count cap; the unique-key layout
+is unchanged by the bit's existence, and the scratch is sized for the layout
+a deduper will actually use."""
+import pytest
+
+from swiftsnails_amd._native import hip
+
+N_BENCH = 262144 * 39
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_record_layout_server_bucket_size(world):
+    h = hip()
+    bit = h.bd_record_layout_bit()
+    P = h.bd_buckets(N_BENCH, world, world | bit)
+    assert P % world == 0
+    server_bucket = world * N_BENCH / P  # records of N sources per server bucket
+    if world <= 4:
+        assert 3400 < server_bucket < 3700, server_bucket
+    else:  # the 16K bucket cap: ~5000 records, ~2000 distinct keys at the bench shape
+        assert P <= 16384 + 64 and server_bucket < 6000, (P, server_bucket)
+    # the layout helpers all see the bit: offsets / scratch agree with the count
+    assert h.bd_offsets(N_BENCH, world, world | bit)[0] == P
+    assert h.bd_scratch_words(N_BENCH, world, world | bit) > P
+
+
+def test_unique_layout_unchanged_by_the_bit():
+    h = hip()
+    bit = h.bd_record_layout_bit()
+    # one rank: the same layout either way (no servers merging sources)
+    assert h.bd_buckets(N_BENCH, 1, 1 | bit) == h.bd_buckets(N_BENCH, 1, 1)
+    # N > 1 unique keys: ~1024 occurrences per source bucket (sub-bucket split at the server)
+    for world in (2, 4, 8):
+        P = h.bd_buckets(N_BENCH, world, world)
+        assert 900 < N_BENCH / P < 1100
