@@ -850,6 +850,10 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
     return -1;
   };
   const uint32_t jl = (it.w & 2u) ? it.x : (hl < (int)it.y ? ord[it.x + hl] : 0u);
+  // the fused update's slot index is loaded beside the first gathers (one
+  // dependent load off the item's chain; the row itself is read after them —
+  // holding it through the gathers cost an occupancy step)
+  const long long fslot = (slots && !(it.w & 1u)) ? slots[it.z] : -1;
   float acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
@@ -911,7 +915,7 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
     // state, V consecutive floats per lane) instead of a ugrad row that the
     // apply kernel reads back; keys summed over several items (row atomics
     // below) are updated by the apply kernel afterwards (launch_apply only)
-    const long long slot = slots[it.z];
+    const long long slot = fslot;
     if (slot < 0) return;  // half-wave-uniform
     const int ns = opt_state_per_coord(op.kind);
     if (tab.bf16) {
