@@ -823,7 +823,7 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
                                                      float* __restrict__ lacc_out, int lacc_n,
                                                      DevTable tab,
                                                      const long long* __restrict__ slots,
-                                                     OptParams op) {
+                                                     OptParams op, int early_slot) {
   // the step's loss / pair accumulators (the tile kernel's, ordered before
   // this launch on the stream) move to acc_out and are left zero for the next
   // step's tile: no zero-fill launch per step
@@ -853,7 +853,7 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
   // the fused update's slot index is loaded beside the first gathers (one
   // dependent load off the item's chain; the row itself is read after them —
   // holding it through the gathers cost an occupancy step)
-  const long long fslot = (slots && !(it.w & 1u)) ? slots[it.z] : -1;
+  const long long fslot = (early_slot && slots && !(it.w & 1u)) ? slots[it.z] : -1;
   float acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) acc[v] = 0.f;
@@ -915,7 +915,7 @@ __global__ __launch_bounds__(256) void k_w2v_oreduce(const uint4* __restrict__ i
     // state, V consecutive floats per lane) instead of a ugrad row that the
     // apply kernel reads back; keys summed over several items (row atomics
     // below) are updated by the apply kernel afterwards (launch_apply only)
-    const long long slot = fslot;
+    const long long slot = early_slot ? fslot : slots[it.z];
     if (slot < 0) return;  // half-wave-uniform
     const int ns = opt_state_per_coord(op.kind);
     if (tab.bf16) {
@@ -1439,6 +1439,16 @@ void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const
   check_launch("k_w2v_osort");
 }
 
+// SS_W2V_EARLY_SLOT=0: the fused update loads its slot index after the
+// occurrence gathers instead of beside the first (A/B)
+static int early_slot() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_W2V_EARLY_SLOT");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord, const float* ograd,
                         const float* otail, int B, int W, int D, float* ugrad, hipStream_t st,
                         const float* gnc, long long negbase, const float* uvals, float* acc,
@@ -1472,11 +1482,11 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
       hipLaunchKernelGGL((k_w2v_oreduce<DD, true>), dim3(grid), dim3(256), 0, st, it, n, ord,  \
                          ograd, otail, B, W, ntiles, ugrad,                                    \
                          reinterpret_cast<const float2*>(gnc), negbase, uvals, acc, acc_out,   \
-                         acc_n, tv, slots, opv);                                               \
+                         acc_n, tv, slots, opv, early_slot());                                 \
     else                                                                                      \
       hipLaunchKernelGGL((k_w2v_oreduce<DD, false>), dim3(grid), dim3(256), 0, st, it, n, ord, \
                          ograd, otail, B, W, ntiles, ugrad, nullptr, 0ll, nullptr, acc,        \
-                         acc_out, acc_n, tv, slots, opv);                                      \
+                         acc_out, acc_n, tv, slots, opv, early_slot());                        \
     break;
     SS_W2VO_CASE(32)
     SS_W2VO_CASE(64)

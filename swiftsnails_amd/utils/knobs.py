@@ -140,6 +140,9 @@ KNOBS: dict[str, Knob] = {
                       "LR forward layout: packed | group (auto by lane utilisation)"),
     "SS_FM_REDUCE": Knob("sorted", "csrc/hip/bdedup.hip, models/fm.py", "tuning",
                          "FM gradient merge: sorted lists, or atomic (LDS float atomics)"),
+    "SS_W2V_EARLY_SLOT": Knob("1", "csrc/hip/w2v.hip", "tuning",
+                              "word2vec occurrence reduce with the fused update: load the key's "
+                              "slot index beside the first gathers (1) or after them (0)"),
     "SS_W2V_PP_STAGES": Knob("3", "csrc/hip/w2v.hip", "tuning",
                              "word2vec per-pair negatives (K <= 5): pipeline stages of the "
                              "pair kernel (3 or 4); 2 = the any-K kernel"),
