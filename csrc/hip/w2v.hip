@@ -1439,6 +1439,159 @@ void launch_w2v_osort(int P, const uint32_t* bstart, const uint32_t* unum, const
   check_launch("k_w2v_osort");
 }
 
+// The per-pair form with TWO items per half-wave (SS_W2V_PP_ITEMS=2): most
+// items of a per-pair step are keys drawn once (a tail word's single
+// negative occurrence), whose chain — item, (gn, center), center row, slot,
+// parameter row, store — holds one row in flight per half-wave in the kernel
+// above.  Here each half-wave walks items s and s + nh (nh = half-waves in
+// the grid) in lock step, QF2 occurrences of each per round (2: 56 VGPRs at
+// D = 128, 8 waves per SIMD — twice the item chains in flight; 4: 78 VGPRs,
+// 6 waves, SS_W2V_PP_QF=4).
+template <int D, int QF2>
+__global__ __launch_bounds__(256) void k_w2v_oreduce_pp2(
+    const uint4* __restrict__ items, long long n, const uint32_t* __restrict__ ord,
+    const float* __restrict__ ograd, float* __restrict__ ugrad,
+    const float2* __restrict__ gnc, long long negbase, const float* __restrict__ uvals,
+    float* __restrict__ lacc, float* __restrict__ lacc_out, int lacc_n, DevTable tab,
+    const long long* __restrict__ slots, OptParams op) {
+  if (lacc)
+    for (int i = blockIdx.x * 256 + threadIdx.x; i < lacc_n; i += gridDim.x * 256) {
+      lacc_out[i] = lacc[i];
+      lacc[i] = 0.f;
+    }
+  constexpr int V = D / 32;
+  using VT = typename OVec<V>::T;
+  const int lane = threadIdx.x & 63, hl = lane & 31;
+  const long long nh = (long long)gridDim.x * 8;
+  const long long s0 = ((long long)blockIdx.x * 4 + (threadIdx.x >> 6)) * 2 + (lane >> 5);
+  uint4 it[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const long long s = s0 + u * nh;
+    it[u] = s < n ? items[s] : make_uint4(0u, 0u, 0u, 0u);
+  }
+  if (it[0].y == 0 && it[1].y == 0) return;  // half-wave-uniform
+  uint32_t jl[2];
+  long long fslot[2];
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    jl[u] = (it[u].w & 2u) ? it[u].x : (hl < (int)it[u].y ? ord[it[u].x + hl] : 0u);
+    fslot[u] = (slots && it[u].y && !(it[u].w & 1u)) ? slots[it[u].z] : -1;
+  }
+  float acc[2][V];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int v = 0; v < V; ++v) acc[u][v] = 0.f;
+  const uint32_t ymax = max(it[0].y, it[1].y);
+  for (uint32_t k0 = 0; k0 < ymax; k0 += QF2) {
+    long long jj[2][QF2];
+    float2 e[2][QF2];
+    VT x[2][QF2];
+    float sc[2][QF2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < QF2; ++r) {
+        const uint32_t k = k0 + r;
+        const long long jv = (long long)__shfl(jl[u], (int)(k < it[u].y ? k : 0), 32);
+        jj[u][r] = k < it[u].y ? jv : -1;
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < QF2; ++r)
+        e[u][r] = jj[u][r] >= negbase ? gnc[jj[u][r] - negbase] : make_float2(1.f, 0.f);
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < QF2; ++r) {
+        const long long j = jj[u][r];
+        sc[u][r] = 1.f;
+        if (j < 0) {
+          x[u][r] = VT{};
+        } else if (j >= negbase) {  // a scaled center row (per-pair negative)
+          const uint32_t c = __float_as_uint(e[u][r].y);
+          sc[u][r] = e[u][r].x;
+          x[u][r] = (c != kInv && e[u][r].x != 0.f)
+                        ? *reinterpret_cast<const VT*>(uvals + (long long)c * D + hl * V) : VT{};
+        } else {
+          x[u][r] = *reinterpret_cast<const VT*>(ograd + j * D + hl * V);
+        }
+      }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < QF2; ++r)
+#pragma unroll
+        for (int v = 0; v < V; ++v) acc[u][v] += sc[u][r] * OVec<V>::get(x[u][r], v);
+  }
+  const int ns = opt_state_per_coord(op.kind);
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    if (it[u].y == 0) continue;  // half-wave-uniform
+    if (slots && !(it[u].w & 1u)) {  // fused K5, as in k_w2v_oreduce
+      const long long slot = fslot[u];
+      if (slot < 0) continue;
+      if (tab.bf16) {
+        unsigned short* r16 = reinterpret_cast<unsigned short*>(slot_row(tab, slot));
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+          const int j = hl * V + v;
+          float w = bf16_val(r16[j]);
+          float a = ns > 0 ? bf16_val(r16[D + j]) : 0.f;
+          float b = ns > 1 ? bf16_val(r16[2 * D + j]) : 0.f;
+          opt_update(op, w, a, b, acc[u][v]);
+          r16[j] = bf16_bits((uint64_t)slot, j, w, true);
+          if (ns > 0) r16[D + j] = bf16_bits((uint64_t)slot, D + j, a, true);
+          if (ns > 1) r16[2 * D + j] = bf16_bits((uint64_t)slot, 2 * D + j, b, true);
+        }
+        continue;
+      }
+      float* row = slot_row(tab, slot) + hl * V;
+      VT w = *reinterpret_cast<const VT*>(row);
+      VT s1 = ns > 0 ? *reinterpret_cast<const VT*>(row + D) : VT{};
+      VT s2 = ns > 1 ? *reinterpret_cast<const VT*>(row + 2 * D) : VT{};
+      float* wf = reinterpret_cast<float*>(&w);
+      float* s1f = reinterpret_cast<float*>(&s1);
+      float* s2f = reinterpret_cast<float*>(&s2);
+#pragma unroll
+      for (int v = 0; v < V; ++v) opt_update(op, wf[v], s1f[v], s2f[v], acc[u][v]);
+      *reinterpret_cast<VT*>(row) = w;
+      if (ns > 0) *reinterpret_cast<VT*>(row + D) = s1;
+      if (ns > 1) *reinterpret_cast<VT*>(row + 2 * D) = s2;
+      continue;
+    }
+    float* g = ugrad + (long long)it[u].z * D + hl * V;
+    if (it[u].w & 1u) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) atomicAdd(g + v, acc[u][v]);
+    } else {
+      VT o;
+      float* of = reinterpret_cast<float*>(&o);
+#pragma unroll
+      for (int v = 0; v < V; ++v) of[v] = acc[u][v];
+      *reinterpret_cast<VT*>(g) = o;
+    }
+  }
+}
+
+static int pp_qf() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_W2V_PP_QF");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+// SS_W2V_PP_ITEMS: items per half-wave of the per-pair reduce, 1 or 2
+static int pp_items() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_W2V_PP_ITEMS");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
 // SS_W2V_EARLY_SLOT=0: the fused update loads its slot index after the
 // occurrence gathers instead of beside the first (A/B)
 static int early_slot() {
@@ -1475,6 +1628,31 @@ void launch_w2v_oreduce(const uint32_t* items, long long n, const uint32_t* ord,
   // call runs concurrently
   const int grid = (int)std::max<long long>((n + 7) / 8, acc ? 64 : 1);
   const uint4* it = reinterpret_cast<const uint4*>(items);
+  if (gnc && pp_items() == 2) {
+    // two items per half-wave: half the grid (s and s + nh per half-wave)
+    const int g2 = (int)std::max<long long>((n + 15) / 16, acc ? 64 : 1);
+    switch (D) {
+#define SS_W2VO2(DD)                                                                            \
+  case DD:                                                                                      \
+    if (pp_qf() == 4)                                                                           \
+      hipLaunchKernelGGL((k_w2v_oreduce_pp2<DD, 4>), dim3(g2), dim3(256), 0, st, it, n, ord,    \
+                         ograd, ugrad, reinterpret_cast<const float2*>(gnc), negbase, uvals,    \
+                         acc, acc_out, acc_n, tv, slots, opv);                                  \
+    else                                                                                        \
+      hipLaunchKernelGGL((k_w2v_oreduce_pp2<DD, 2>), dim3(g2), dim3(256), 0, st, it, n, ord,    \
+                         ograd, ugrad, reinterpret_cast<const float2*>(gnc), negbase, uvals,    \
+                         acc, acc_out, acc_n, tv, slots, opv);                                  \
+    break;
+      SS_W2VO2(32)
+      SS_W2VO2(64)
+      SS_W2VO2(128)
+#undef SS_W2VO2
+      default:
+        throw_error("w2v_oreduce: D must be 32, 64 or 128");
+    }
+    check_launch("k_w2v_oreduce_pp2");
+    return;
+  }
   switch (D) {
 #define SS_W2VO_CASE(DD)                                                                      \
   case DD:                                                                                    \

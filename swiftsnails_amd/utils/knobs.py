@@ -143,6 +143,12 @@ KNOBS: dict[str, Knob] = {
     "SS_W2V_EARLY_SLOT": Knob("1", "csrc/hip/w2v.hip", "tuning",
                               "word2vec occurrence reduce with the fused update: load the key's "
                               "slot index beside the first gathers (1) or after them (0)"),
+    "SS_W2V_PP_ITEMS": Knob("2", "csrc/hip/w2v.hip", "tuning",
+                            "word2vec per-pair occurrence reduce: items per half-wave (2: two "
+                            "independent item chains in lock step, 1: the one-item kernel)"),
+    "SS_W2V_PP_QF": Knob("2", "csrc/hip/w2v.hip", "tuning",
+                         "word2vec per-pair two-item reduce: occurrences per item and round "
+                         "(2 or 4)"),
     "SS_W2V_PP_STAGES": Knob("3", "csrc/hip/w2v.hip", "tuning",
                              "word2vec per-pair negatives (K <= 5): pipeline stages of the "
                              "pair kernel (3 or 4); 2 = the any-K kernel"),
