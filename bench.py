@@ -258,6 +258,10 @@ def main(argv=None):
                 "transport": tlabel,
                 "plane": plane.plane if not engine.fast1 else "none",
                 "xgmi_tier": plane.xgmi_tier,
+                # N>1 rounds: each source's unique keys, or every occurrence
+                # (SS_XCHG=records, PSEngine exchange=)
+                "exchange": None if engine.fast1 else
+                ("records" if getattr(engine, "records", False) else "unique"),
                 "fell_back": plane.fell_back,
                 **({"fallback_reason": plane.fallback_reason[:300]} if plane.fell_back else {}),
                 "devices": plane.devices,
