@@ -74,6 +74,17 @@ static constexpr int kBdTarget = 3584;
 // bucket must stay small enough that N of them fit one server workgroup's
 // table after its sub-bucket split
 static constexpr int kBdTargetDist = 1024;
+// SS_BD_TARGET_DIST: occurrences per source bucket of the N>1 unique-key
+// layout, 512..4096 (the servers' sub-bucket count follows it,
+// server.hip srv_sub_buckets)
+int bd_target_dist() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_BD_TARGET_DIST");
+    const int x = e ? std::atoi(e) : kBdTargetDist;
+    return x < 512 ? 512 : (x > 4096 ? 4096 : x);
+  }();
+  return v;
+}
 // SS_BD_TARGET (one rank): occurrences per bucket, 1024..3584 (A/B: larger
 // buckets make each (chunk, bucket) run of the scatter longer — fewer partial
 // lines — at the price of a fuller LDS table in the dedup)
@@ -93,7 +104,7 @@ static int bd_target(int nranks, bool rec) {
     return v < 1024 ? 1024 : (v > 3584 ? 3584 : v);
   }();
   if (nranks > 1 && rec) return std::max(256, kBdTarget / nranks);
-  return nranks > 1 ? kBdTargetDist : one;
+  return nranks > 1 ? bd_target_dist() : one;
 }
 int bd_record_layout_bit() { return kBdRecLayout; }
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket

@@ -448,9 +448,10 @@ static int srv_share(int P) {
 }
 
 int srv_sub_buckets(int nsrc) {
-  // N sources x ~1024 keys (<= ~1.25x that with hash imbalance) per bucket k,
-  // at most ~3000 distinct keys per 4096-slot table
-  const long long need = (long long)nsrc * 1280;
+  // N sources x ~bd_target_dist() keys (1024 by default; <= ~1.25x that with
+  // hash imbalance) per bucket k, at most ~3000 distinct keys per 4096-slot
+  // table
+  const long long need = (long long)nsrc * bd_target_dist() * 5 / 4;
   int m = (int)((need + 2999) / 3000);
   return m < 1 ? 1 : (m > 64 ? 64 : m);
 }
