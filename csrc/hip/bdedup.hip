@@ -70,10 +70,15 @@ static constexpr int kBdDT = 512;         // dedup workgroup size
 // (2048) with claimed pulls — longer (chunk, bucket) runs in the scatter,
 // fewer and fuller claimed-pull workgroups
 static constexpr int kBdTarget = 3584;
-// N>1: a server merges bucket k of every source (server.hip), so a source's
-// bucket must stay small enough that N of them fit one server workgroup's
-// table after its sub-bucket split
-static constexpr int kBdTargetDist = 1024;
+// N>1: a server merges bucket k of every source (server.hip); it splits the
+// union of the N sources' runs into sub-buckets that fit one workgroup's
+// table (the senders group each run by sub-bucket)
+// (3072: 4 / 8 bench ranks on one GPU 4.24 / 8.03 ms per step at 1024, 3.94 /
+// 7.19 at 2048, 3.72 / 6.98 at 3072 — bigger source buckets: longer scatter
+// runs, fuller dedup workgroups, a smaller count histogram; the servers split
+// them into proportionally more sub-buckets, so a server table holds the same;
+// profiles/raw/r5_bucket_target_dist.txt)
+static constexpr int kBdTargetDist = 3072;
 // SS_BD_TARGET_DIST: occurrences per source bucket of the N>1 unique-key
 // layout, 512..4096 (the servers' sub-bucket count follows it,
 // server.hip srv_sub_buckets)

@@ -230,6 +230,7 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("lay_n") = 0, py::arg("msub") = 1, py::arg("usub") = 0, py::arg("rbits") = 0,
      py::arg("spj") = 0);
   m.def("bd_record_layout_bit", &bd_record_layout_bit);
+  m.def("bd_target_dist", &bd_target_dist);
   m.def("rec_grad", [](uintptr_t ucount, int nd, long long gap, uintptr_t spj, uintptr_t gs,
                        uintptr_t xval, int F, uintptr_t grec, uintptr_t st, uintptr_t acc,
                        uintptr_t acc_out, int acc_n) {

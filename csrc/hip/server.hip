@@ -448,7 +448,7 @@ static int srv_share(int P) {
 }
 
 int srv_sub_buckets(int nsrc) {
-  // N sources x ~bd_target_dist() keys (1024 by default; <= ~1.25x that with
+  // N sources x ~bd_target_dist() keys (3072 by default; <= ~1.25x that with
   // hash imbalance) per bucket k, at most ~3000 distinct keys per 4096-slot
   // table
   const long long need = (long long)nsrc * bd_target_dist() * 5 / 4;

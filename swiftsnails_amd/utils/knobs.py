@@ -133,7 +133,7 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_TARGET": Knob("3584", "csrc/hip/bdedup.hip", "tuning",
                          "one rank: target occurrences per dedup bucket (1024..3584; 3584 / 3072 "
                          "/ 2048: 0.774-0.785 / 0.790 / 0.801-0.806 ms per bench step)"),
-    "SS_BD_TARGET_DIST": Knob("1024", "csrc/hip/bdedup.hip, csrc/hip/server.hip", "tuning",
+    "SS_BD_TARGET_DIST": Knob("3072", "csrc/hip/bdedup.hip, csrc/hip/server.hip", "tuning",
                               "N>1 unique-key layout: occurrences per source bucket (512..4096; "
                               "the servers' sub-bucket count follows)"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),

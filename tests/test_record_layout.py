@@ -33,7 +33,11 @@ def test_unique_layout_unchanged_by_the_bit():
     bit = h.bd_record_layout_bit()
     # one rank: the same layout either way (no servers merging sources)
     assert h.bd_buckets(N_BENCH, 1, 1 | bit) == h.bd_buckets(N_BENCH, 1, 1)
-    # N > 1 unique keys: ~1024 occurrences per source bucket (sub-bucket split at the server)
+    # N > 1 unique keys: ~3072 occurrences per source bucket (SS_BD_TARGET_DIST), split
+    # by the servers into sub-buckets of a table's size
+    tg = h.bd_target_dist()
     for world in (2, 4, 8):
         P = h.bd_buckets(N_BENCH, world, world)
-        assert 900 < N_BENCH / P < 1100
+        assert 0.9 * tg < N_BENCH / P < 1.1 * tg
+        m = h.srv_sub_buckets(world)
+        assert world * (N_BENCH / P) * 1.25 / m <= 3000  # <= ~3000 keys per server table
