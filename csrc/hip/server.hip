@@ -448,6 +448,9 @@ static int srv_share(int P) {
 }
 
 int srv_sub_buckets(int nsrc) {
+  // one source: its bucket's unique keys passed the worker dedup's own
+  // 4096-slot table, so they fit a server table as they are
+  if (nsrc <= 1) return 1;
   // N sources x ~bd_target_dist() keys (3072 by default; <= ~1.25x that with
   // hash imbalance) per bucket k, at most ~3000 distinct keys per 4096-slot
   // table
