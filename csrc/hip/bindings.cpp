@@ -371,7 +371,8 @@ PYBIND11_MODULE(_ss_hip, m) {
   }, py::arg("n"), py::arg("nranks"), py::arg("scratch"), py::arg("luid"), py::arg("uvals"),
      py::arg("occ"), py::arg("osi"), py::arg("st"), py::arg("ndest") = 0, py::arg("pj") = 0);
   // server-side merge of a round's received keys (server.hip)
-  m.def("srv_sub_buckets", &srv_sub_buckets);
+  m.def("srv_sub_buckets", &srv_sub_buckets, py::arg("nsrc"), py::arg("lay_n") = 0,
+        py::arg("ndest") = 0);
   m.def("srv_dedup", [](uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum, long long cap, int nsrc,
                         int Pd, int m, int me, uintptr_t cnt, uintptr_t bstart, uintptr_t pj,
                         uintptr_t luid, uintptr_t bkeys, uintptr_t ubase, uintptr_t unum,

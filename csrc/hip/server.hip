@@ -447,14 +447,28 @@ static int srv_share(int P) {
   return y < 1 ? 1 : (y > 8 ? 8 : y);
 }
 
-int srv_sub_buckets(int nsrc) {
+int srv_sub_buckets(int nsrc, long long lay_n, int ndest) {
+  // SS_SRV_SUB=m: a fixed count (A/B)
+  static const int fixed = [] {
+    const char* e = std::getenv("SS_SRV_SUB");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (fixed > 0) return fixed > 64 ? 64 : fixed;
   // one source: its bucket's unique keys passed the worker dedup's own
   // 4096-slot table, so they fit a server table as they are
   if (nsrc <= 1) return 1;
-  // N sources x ~bd_target_dist() keys (3072 by default; <= ~1.25x that with
-  // hash imbalance) per bucket k, at most ~3000 distinct keys per 4096-slot
-  // table
-  const long long need = (long long)nsrc * bd_target_dist() * 5 / 4;
+  // N sources x the layout's occurrences per source bucket (lay_n keys per
+  // call: ~bd_target_dist() for large calls, fewer for small ones such as
+  // word2vec's; <= ~1.25x that with hash imbalance, every occurrence counted
+  // as a distinct key) per bucket k, at most ~3000 distinct keys per
+  // 4096-slot table
+  long long per = bd_target_dist();
+  if (lay_n > 0) {
+    const int P = bd_buckets(lay_n, nsrc, ndest > 0 ? ndest : nsrc);
+    const int nd = ndest > 0 && ndest < nsrc ? ndest : nsrc;
+    per = (lay_n + (long long)(P / nsrc) * nd - 1) / ((long long)(P / nsrc) * nd);
+  }
+  const long long need = (long long)nsrc * per * 5 / 4;
   int m = (int)((need + 2999) / 3000);
   return m < 1 ? 1 : (m > 64 ? 64 : m);
 }

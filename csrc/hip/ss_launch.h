@@ -221,7 +221,7 @@ void launch_bd_fill_occ_p(int P, const uint32_t* bstart, const uint32_t* ubase,
                           float* occ, const uint32_t* pj, hipStream_t st, SelfSeg self = {});
 
 // --- server.hip (N>1: merge of the keys a round receives from all sources)
-int srv_sub_buckets(int nsrc);
+int srv_sub_buckets(int nsrc, long long lay_n = 0, int ndest = 0);
 void launch_srv_dedup(const uint64_t* rkeys, const uint32_t* rbase, const uint32_t* rnum,
                       long long cap, int nsrc, int Pd, int m, int me, uint32_t* cnt,
                       uint32_t* bstart, uint32_t* pj, uint32_t* luid, uint64_t* bkeys,

@@ -59,7 +59,8 @@ class DeviceSetup:
         self.Pd = h.bd_buckets(cap, N, self.dedupers[0].ndest) // N
         # record exchange: a server bucket is N runs of records sized for one
         # LDS table together (bdedup.hip bd_target), no sub-buckets
-        self.sub = 1 if self.records else h.srv_sub_buckets(N)
+        self.sub = 1 if self.records else h.srv_sub_buckets(
+            N, cap, self.dedupers[0].ndest & ~h.bd_record_layout_bit())
         self.Ps = self.Pd * self.sub
         # sub > 1: every source groups its runs by the servers' sub-bucket
         # and sends the offsets with them (the server reads exact ranges)

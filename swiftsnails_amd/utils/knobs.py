@@ -136,6 +136,9 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_TARGET_DIST": Knob("3072", "csrc/hip/bdedup.hip, csrc/hip/server.hip", "tuning",
                               "N>1 unique-key layout: occurrences per source bucket (512..4096; "
                               "the servers' sub-bucket count follows)"),
+    "SS_SRV_SUB": Knob("auto", "csrc/hip/server.hip", "tuning",
+                       "N>1 servers: sub-buckets per bucket (auto: from the sources' bucket "
+                       "size and count)"),
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
