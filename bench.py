@@ -168,6 +168,12 @@ def main(argv=None):
     # the live world and keep the faster (untimed; reported as "calibration")
     cal = (worker.calibrate_pull_ahead(a.cal_steps, a.cal_windows)
            if a.cal_steps > 0 else {})
+    # ... and the server stream (SS_SERVER_STREAM=auto, ranks with a device of
+    # their own): kept only if it costs <= 1 % on the live world
+    cal_ss = (worker.calibrate_server_stream(a.cal_steps, a.cal_windows)
+              if a.cal_steps > 0 else {})
+    if cal_ss:
+        cal = dict(cal, server_stream=cal_ss)
     # hipGraph replays of the whole step (captured here, outside the timed
     # region; the data generator then reads its step from a device counter)
     graphed = False
@@ -190,14 +196,22 @@ def main(argv=None):
     engine.check()
     first_loss = worker.mean_loss()
 
+    # a roctx range around exactly the timed steps (rocprofv3 --marker-trace):
+    # tools/kstats.py --range timed attributes a kernel to the steps iff it
+    # starts inside it, so start-up, litmus and calibration kernels never
+    # count as per-step work (two host calls; no device work)
+    from swiftsnails_amd.utils.tracing import Tracer
+
+    rx = Tracer(enabled=True)
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for i in range(a.steps):
-        fault.maybe(a.warmup + i)
-        worker.step()
-        wd.beat(i)  # one attribute store: no measurable cost
-    torch.cuda.synchronize()
+    with rx.range("timed"):
+        for i in range(a.steps):
+            fault.maybe(a.warmup + i)
+            worker.step()
+            wd.beat(i)  # one attribute store: no measurable cost
+        torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
 
@@ -267,6 +281,9 @@ def main(argv=None):
                 "devices": plane.devices,
                 **({"litmus": plane.litmus} if plane.litmus else {}),
                 "init": a.init,
+                # the round layout that produced this number (ring depth, server
+                # stream, N>1 bucket / sub-bucket layout, claimed server inserts)
+                "layout": engine.layout_info(),
                 "comms": comms,
                 "rccl_nranks": rccl_n,
                 "a2a_bytes_per_step": a2a,

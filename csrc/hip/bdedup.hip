@@ -112,6 +112,8 @@ static int bd_target(int nranks, bool rec) {
   return nranks > 1 ? bd_target_dist() : one;
 }
 int bd_record_layout_bit() { return kBdRecLayout; }
+// the occurrences-per-bucket target a layout of `nranks` ranks uses
+int bd_target_for(int nranks, bool records) { return bd_target(nranks, records); }
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
 static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in registers
 static constexpr int kBdMaxBuckets = 16384;
@@ -992,10 +994,48 @@ struct FmCols {
 // the DIM coordinates and their state stay in registers).  The model kernels
 // below call it instead of storing ugrad when the engine fuses the apply
 // (PSEngine.fuse_apply: one GPU, compact unique ids).
+// FM k = 8 rows in fp32 keyfirst slots (80 bytes: [key | w_0..w_8 | s_0..s_8]
+// with one state word per coordinate, AdaGrad / SGD-state layouts): the 72-byte
+// row moves as one 8-byte and four 16-byte accesses per thread, all five loads
+// in flight together, instead of 18 dependent-address 4-byte row_ld / row_st
+// (the one-thread-per-row update that measured 0.62 -> 1.04 ms per FM step)
+__device__ __forceinline__ bool fm9_vec_ok(const DevTable& t, const OptParams& op) {
+  return !t.bf16 && t.dim == 9 && t.stride == 80 && t.row_off == 8 &&
+         opt_state_per_coord(op.kind) == 1;
+}
+__device__ __forceinline__ void fm9_row_update(const DevTable& t, long long slot,
+                                               const float (&g)[9], const OptParams& op) {
+  float* row = slot_row(t, (uint64_t)slot);  // 8-byte aligned; row + 2 is 16-byte aligned
+  float r[18];
+  const float2 a = *reinterpret_cast<const float2*>(row);
+  const float4* q4 = reinterpret_cast<const float4*>(row + 2);
+  float4 q[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) q[i] = q4[i];
+  r[0] = a.x, r[1] = a.y;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    r[2 + 4 * i] = q[i].x, r[3 + 4 * i] = q[i].y, r[4 + 4 * i] = q[i].z, r[5 + 4 * i] = q[i].w;
+  float s2 = 0.f;
+#pragma unroll
+  for (int j = 0; j < 9; ++j) opt_update(op, r[j], r[9 + j], s2, g[j]);
+  *reinterpret_cast<float2*>(row) = make_float2(r[0], r[1]);
+  float4* o4 = reinterpret_cast<float4*>(row + 2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    o4[i] = make_float4(r[2 + 4 * i], r[3 + 4 * i], r[4 + 4 * i], r[5 + 4 * i]);
+}
+
 template <int DIM>
 __device__ __forceinline__ void fused_row_update(const DevTable& t, long long slot,
                                                  const float (&g)[DIM], const OptParams& op) {
   if (slot < 0) return;
+  if constexpr (DIM == 9) {
+    if (fm9_vec_ok(t, op)) {
+      fm9_row_update(t, slot, g, op);
+      return;
+    }
+  }
   const int ns = opt_state_per_coord(op.kind);
   float w[DIM], s1[DIM], s2[DIM];
 #pragma unroll
@@ -1305,6 +1345,17 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   // dedup-hash buckets.  A function of the layout only: every rank of an
   // N>1 job decides the same
   if (rs.rbits && 4ll * L.Pd * msub > (1ll << rs.rbits)) rs.rbits = 0;
+  // ... and only when the fullest bucket — ceil(R / Pd) whole regions of a
+  // destination's keys — still fits the dedup's 4096-slot LDS table with
+  // every key distinct (R / Pd just above 4 puts 5 regions, 1.25x the target,
+  // into some buckets: ~4480 occurrences at the one-rank target).  The hash
+  // buckets' sizes vary by ~2 %; 3800 leaves that margin
+  if (rs.rbits) {
+    const long long R = 1ll << rs.rbits;
+    const long long per_dest = (ln + bd_clamp_ndest(rs.nranks, ndest) - 1) /
+                               bd_clamp_ndest(rs.nranks, ndest);
+    if ((R + L.Pd - 1) / L.Pd * per_dest > 3800ll * R) rs.rbits = 0;
+  }
   uint32_t* S = scratch;
   const size_t lds = sizeof(unsigned int) * (size_t)L.P;
   // workgroup sizes (256/512/1024): count (SS_BD_CNT), column scan

@@ -231,6 +231,7 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("spj") = 0);
   m.def("bd_record_layout_bit", &bd_record_layout_bit);
   m.def("bd_target_dist", &bd_target_dist);
+  m.def("bd_target_for", &bd_target_for, py::arg("nranks"), py::arg("records") = false);
   m.def("rec_grad", [](uintptr_t ucount, int nd, long long gap, uintptr_t spj, uintptr_t gs,
                        uintptr_t xval, int F, uintptr_t grec, uintptr_t st, uintptr_t acc,
                        uintptr_t acc_out, int acc_n) {

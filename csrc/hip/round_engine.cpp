@@ -81,6 +81,9 @@ class RoundEngine {
   }
   ~RoundEngine() {
     hipSetDevice(device_);
+    // nothing enqueued may still record or wait these events (a graph
+    // replay, a stage of this engine on any stream)
+    hipDeviceSynchronize();
     for (auto& k : ev_)
       for (auto e : k) hipEventDestroy(e);
   }

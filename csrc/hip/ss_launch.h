@@ -182,6 +182,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
                     int msub = 1, uint32_t* usub = nullptr, uint32_t* spj = nullptr);
 int bd_record_layout_bit();
 int bd_target_dist();
+int bd_target_for(int nranks, bool records);
 void launch_rec_grad(const unsigned long long* ucount, int nd, long long gap, const uint32_t* spj,
                      const float* gs, const float* xval, int F, float* grec, hipStream_t st,
                      float* lacc = nullptr, float* lacc_out = nullptr, int lacc_n = 0);

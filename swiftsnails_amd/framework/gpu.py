@@ -324,6 +324,9 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
     # pure servers too (they step with empty key sets)
     if passes is None and warmup > 0 and int(cfg.get("calibrate_steps", 10) or 0) > 0:
         cal = w.calibrate_pull_ahead(int(cfg.get("calibrate_steps", 10)))
+        cal_ss = w.calibrate_server_stream(int(cfg.get("calibrate_steps", 10)))
+        if cal_ss:
+            cal = dict(cal, server_stream=cal_ss)
     # config `graph: 1`: replay the step as hipGraphs (1 GPU, synthetic data;
     # a no-op where unsupported — see PipelinedWorker.enable_graph)
     graphed = str(cfg.get("graph", "0")) not in ("0", "false", "") and w.enable_graph()
@@ -372,7 +375,7 @@ def run_training(cfg: Config, steps: Optional[int] = None, warmup: int = 0,
              "rank0_quota": w.quota,
              "transport": getattr(ctx.transport, "label", type(ctx.transport).__name__),
              "pull_ahead": bool(getattr(ctx.engine, "pull_ahead", False)),
-             "calibration": cal,
+             "calibration": cal, "layout": ctx.engine.layout_info(),
              "plane": ctx.plane.plane, "xgmi_tier": ctx.plane.xgmi_tier,
              "fell_back": ctx.plane.fell_back, "devices": ctx.plane.devices}
     if cfg.get("model", "sparse_lr") == "word2vec" and ctx.is_worker:

@@ -21,6 +21,37 @@ from typing import Optional
 import torch
 
 
+class _GraphSet(list):
+    """A worker's captured hipGraphs, owned so that they are destroyed BEFORE
+    what their nodes reference.  A captured step records and waits the round
+    engine's HIP events and launches kernels on its mailbox arenas; a graph
+    exec that outlived them (a worker collected by the cyclic GC, which
+    clears the objects of a cycle in no set order) left the HIP runtime with
+    dangling event nodes, and a later replay in the same process crashed
+    inside hipGraphLaunch.  The set keeps the engine alive and resets every
+    graph after the device drains — from ``close()``, or from its finaliser,
+    which the GC runs before it clears any object of the cycle (PEP 442) and
+    refcounting runs before the set's own references are dropped."""
+
+    def __init__(self, graphs, keep):
+        super().__init__(graphs)
+        self.keep = keep  # the engine: its RoundEngine events and arenas
+
+    def close(self) -> None:
+        if len(self):
+            torch.cuda.synchronize()
+            for g in self:
+                g.reset()
+            self.clear()
+        self.keep = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:  # noqa: BLE001 - interpreter shutdown
+            pass
+
+
 class PipelinedWorker:
     def __init__(self, engine, rank: int = 0, world: int = 1, active: bool = True):
         self.engine, self.rank, self.world, self.active = engine, rank, world, active
@@ -122,9 +153,12 @@ class PipelinedWorker:
         # holds pulled-ahead rounds: a capture would record drain steps, not
         # the periodic synchronous step
         self.drain()
-        # replays run the server half of a round on the main stream (a
-        # capture that forked the server stream ended in a crash inside
-        # hipStreamEndCapture on the N>1 xGMI path)
+        # replays run the server half of a round on the main stream: a
+        # capture that forks the server stream in (and joins it back at the
+        # end, like the route / pull streams) crashes inside
+        # hipStreamEndCapture on the N>1 xGMI path, at the top or the default
+        # stream priority alike (tools/exp/graph_server_stream.py); a server
+        # stream also made word2vec's N>1 replays 2x slower (0.28 vs 0.135 ms)
         ss = getattr(eng, "server_stream", None)
         if ss is not None:
             torch.cuda.current_stream(eng.device).wait_stream(ss)
@@ -194,8 +228,17 @@ class PipelinedWorker:
         # and after `depth` steps the Python-side pipeline state is periodic
         self.step_idx, self._next, pulled, eng._next_slot, eng.rounds = saved
         self._pulled = collections.deque(pulled)
-        self._graphs, self._gbase = graphs, self.step_idx
+        self._graphs, self._gbase = _GraphSet(graphs, eng), self.step_idx
         return True
+
+    def close(self) -> None:
+        """Drain the device and destroy the captured graphs (before the
+        engine's events and arenas go away).  The worker cannot replay
+        afterwards; eager steps still work."""
+        if self._graphs is not None:
+            self._graphs.close()
+            self._graphs = None
+            self.engine.graphed = False
 
     def _zero_acc(self) -> None:
         """Zero the per-step device accumulators (the loss) on the current stream."""
@@ -348,6 +391,49 @@ class PipelinedWorker:
                 "staleness": eng.lookahead if best else 0,
                 "sync_ms": ms(times[False]), "ahead_ms": ms(times[True]),
                 "rank_spread_ms": {"sync": ms(spread[False]), "ahead": ms(spread[True])},
+                "windows": windows, "steps_per_window": steps, "margin": margin}
+
+    def calibrate_server_stream(self, steps: int = 10, windows: int = 2,
+                                margin: float = 0.01) -> dict:
+        """SS_SERVER_STREAM=auto at N>1 with a device per rank: the server
+        half of every round on its own top-priority stream lets a peer's
+        rows leave while this rank's compute is slow (a straggler absorbs
+        43 % instead of 21 % of a device delay, profiles/
+        r5_n_gt_1_straggler_lookup.md) but costs an extra stream's hand-offs
+        when no rank straggles (one rank: 1.087 vs 1.064 ms).  Time
+        ``windows`` alternating (off, on) windows on the live world in the
+        current round mode and keep the stream only if it is within
+        ``margin`` of the step without it in EVERY window.  A collective.
+        Returns {} where it does not apply."""
+        eng = self.engine
+        if not (getattr(eng, "gpu", False) and getattr(eng, "dist", False)
+                and getattr(eng, "server_stream", None) is not None
+                and os.environ.get("SS_SERVER_STREAM", "auto") == "auto"
+                and self._graphs is None):
+            return {}
+        steps, windows = max(1, int(steps)), max(1, int(windows))
+        times = {False: [], True: []}
+        for _ in range(windows):
+            for on in (False, True):
+                eng.set_server_stream(on)
+                for _ in range(2):
+                    self.step()
+                torch.cuda.synchronize(eng.device)
+                eng.barrier()
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    self.step()
+                torch.cuda.synchronize(eng.device)
+                el = time.perf_counter() - t0
+                eng.barrier()
+                times[on].append(eng.max_over_ranks(el) / steps)
+        keep = all(a <= (1.0 + margin) * s for s, a in zip(times[False], times[True]))
+        pick = os.environ.get("SS_CAL_SERVER_STREAM", "")  # debug: force the outcome
+        if pick in ("0", "1"):
+            keep = pick == "1"
+        eng.set_server_stream(keep)
+        ms = lambda xs: [round(1e3 * x, 4) for x in xs]  # noqa: E731
+        return {"server_stream": keep, "off_ms": ms(times[False]), "on_ms": ms(times[True]),
                 "windows": windows, "steps_per_window": steps, "margin": margin}
 
     def rounds_done(self) -> int:

@@ -14,6 +14,7 @@ other beyond the lockstep collective round.
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import numpy as np
@@ -86,13 +87,23 @@ class FMWorker(PipelinedWorker):
             h.fm_fwd_g(0, o.index_ptrs(dd.n), self.labels[slot].data_ptr(),
                        d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                        self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
-            # the sorted per-bucket merge writes each unique row once; the
-            # update is a separate lane-group kernel (k_apply_st): fused into
-            # the merge, one thread per 72-byte row measured 0.62 -> 1.04 ms
+            # the sorted per-bucket merge sums each unique key's gradient row
+            # once; one GPU (SS_FM_FUSE=1): the AdaGrad update of that row is
+            # fused into it (the row moved as 8- + 16-byte vectors per thread,
+            # bdedup.hip fm9_row_update) instead of storing the gradient rows
+            # for a separate apply kernel (k_apply_st).  The scalar form of
+            # the fused update (18 dependent 4-byte accesses per row) measured
+            # 0.62 -> 1.04 ms; SS_FM_FUSE=0 keeps the separate apply
+            fa = (self.engine.fuse_apply(rnd, snapshot=False)
+                  if os.environ.get("SS_FM_FUSE", "1") != "0" else None)
+            kw = {}
+            if fa is not None:
+                assert not fa["slot32"]  # FM slots are never 4-byte (slot32: scalar rows)
+                kw = {"t": fa["t"], "slots": fa["slots"], "op": fa["op"]}
             h.bd_reduce_fm(dd.lay, dd.nranks, o.scratch.data_ptr(), o.pj.data_ptr(),
                            o.luid.data_ptr(), self.gs.data_ptr(), self.gss.data_ptr(),
                            d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
-                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr(), ndest=o.ndest)
+                           rnd.ugrad.data_ptr(), st, self.ovf.data_ptr(), ndest=o.ndest, **kw)
             return
         hip().fm_fwd_bwd(rnd.inv.data_ptr(), self.labels[slot].data_ptr(), d.batch_size,
                          d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),

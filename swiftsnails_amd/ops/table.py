@@ -478,6 +478,12 @@ class HbmTable:
     def check(self):
         e = int(self.err.item())
         if e & 1:
+            if self.rbits:  # keys probe only inside the region their hash names
+                raise TableFullError(
+                    f"table region full: a key's probe region ({self.capacity >> self.rbits} "
+                    f"slots, one of {1 << self.rbits}) has no empty slot; table size "
+                    f"{self.size()} of {self.capacity} (load {self.size() / self.capacity:.3f}) "
+                    "— the keys of that region were not inserted; size the shard for a lower load")
             raise TableFullError(f"table full: capacity {self.capacity}, size {self.size()}")
         if e & 2:
             raise ValueError("key 0xFFFFFFFFFFFFFFFF is reserved (empty-slot sentinel)")

@@ -19,6 +19,52 @@ class EngineControl:
         self.t.allreduce_(t, "max")
         return float(t.item())
 
+    def layout_info(self) -> dict:
+        """The round layout this rank runs (bench.py / the launcher put it in
+        their JSON, so a number says which layout produced it): ring depth,
+        the server stream, the N>1 bucket layout (occurrences per source
+        bucket, server sub-buckets), claimed server inserts and the region
+        bits they rely on."""
+        info = {"depth": int(self.depth), "fast1": bool(getattr(self, "fast1", False))}
+        if not (self.gpu and self.dist):
+            return info
+        from .engine import _hip
+
+        h = _hip()
+        info.update({
+            "server_stream": getattr(self, "server_stream", None) is not None,
+            # SS_BD_TARGET_DIST (the N>1 source-bucket target), and the target
+            # this layout actually uses (a one-rank layout takes SS_BD_TARGET)
+            "bd_target_dist": int(h.bd_target_dist()),
+            "bucket_target": int(h.bd_target_for(self.world, bool(getattr(self, "records", False)))),
+            "buckets_per_dest": int(getattr(self, "Pd", 0)),
+            "srv_sub_buckets": int(getattr(self, "sub", 1)),
+            "claim": bool(getattr(self, "claim", False)),
+            "srv_rbits": int(getattr(self, "srv_rbits", 0)),
+            "srv_ahead": bool(getattr(self, "srv_ahead", False)),
+            "shared_device": bool(self.shared_device),
+        })
+        return info
+
+    def set_server_stream(self, on: bool) -> bool:
+        """Run the server half of later rounds on the server stream (``on``)
+        or on the caller's streams.  Synchronises the device first, so no
+        round issued before the switch can reorder against one issued after
+        it (calibration only: PipelinedWorker.calibrate_server_stream).
+        Returns whether the server stream is in use."""
+        if not self.gpu:
+            return False
+        cur = getattr(self, "server_stream", None)
+        if on == (cur is not None):
+            return on
+        torch.cuda.synchronize(self.device)
+        if not on:
+            self._server_stream_off = cur
+            self.server_stream = None
+        else:
+            self.server_stream = getattr(self, "_server_stream_off", None)
+        return self.server_stream is not None
+
     # ------------------------------------------------------------ read-only
     def lookup(self, keys: torch.Tensor) -> torch.Tensor:
         """Collective READ-ONLY pull: rows [n, dim] of ``keys`` (in order)

@@ -71,7 +71,12 @@ KNOBS: dict[str, Knob] = {
                              "N>1 over xGMI: the server half of each round (keys in, merge, "
                              "lookup, rows out; gradients in, merge + update) on its own "
                              "highest-priority stream; auto = when every rank has its own "
-                             "device, 1 = always, 0 = on the main stream"),
+                             "device AND the bench / launcher calibration measures it within "
+                             "1 % of the step without it (PipelinedWorker."
+                             "calibrate_server_stream), 1 = always, 0 = on the main stream"),
+    "SS_CAL_SERVER_STREAM": Knob("", "models/base.py", "debug",
+                                 "0|1: force the server-stream calibration's outcome (it still "
+                                 "measures both)"),
     "SS_MAIN_PRIO": Knob("0", "bench.py", "experiment",
                          "1: bench.py runs the step's main stream at the highest stream priority"),
     "SS_ROUTE_CUS": Knob("0", "parallel/engine.py", "experiment",
@@ -144,6 +149,10 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
     "SS_LR_FWD": Knob("auto", "csrc/hip/segreduce.hip", "tuning",
                       "LR forward layout: packed | group (auto by lane utilisation)"),
+    "SS_FM_FUSE": Knob("1", "models/fm.py", "tuning",
+                       "one GPU: FM's AdaGrad update fused into the sorted gradient merge "
+                       "(rows as 8- + 16-byte vectors per thread; 0: gradient rows, then "
+                       "k_apply_st)"),
     "SS_FM_REDUCE": Knob("sorted", "csrc/hip/bdedup.hip, models/fm.py", "tuning",
                          "FM gradient merge: sorted lists, or atomic (LDS float atomics)"),
     "SS_W2V_EARLY_SLOT": Knob("1", "csrc/hip/w2v.hip", "tuning",

@@ -53,13 +53,22 @@ def _child_main(fn, args, q):
 
 
 def in_child(fn, *args, timeout: float = 240.0) -> None:
-    """Run ``fn(*args)`` (a module-level test body) in a spawned process and
-    re-raise its failure here.  The hipGraph tests run this way: a graph
-    replay in a process that had already run many other GPU tests (engines,
-    streams and graphs created and torn down) segfaulted inside
-    hipGraphLaunch, depending on which tests ran before — never in a fresh
-    process, and never in the single-model processes bench.py and the
-    launcher run."""
+    """Run ``fn(*args)`` (a module-level test body) — in this process, or
+    with SS_TEST_IN_CHILD=1 in a spawned one, re-raising its failure here.
+    The hipGraph tests used to need the child: a replay in a process that had
+    already run many other GPU tests segfaulted inside hipGraphLaunch.  The
+    cause was teardown order — a collected worker's graph execs outlived the
+    round engine's HIP events their nodes reference — and the graphs are now
+    owned so they are destroyed first (models/base.py _GraphSet), so the
+    graph tests run in the one pytest process again."""
+    if os.environ.get("SS_TEST_IN_CHILD", "0") != "1":
+        saved = dict(os.environ)  # the bodies set SS_* knobs for themselves
+        try:
+            fn(*args)
+        finally:
+            os.environ.clear()
+            os.environ.update(saved)
+        return
     import torch.multiprocessing as mp
 
     ctx = mp.get_context("spawn")

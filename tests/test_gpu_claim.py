@@ -273,3 +273,83 @@ def test_sparse_lr_xgmi_path_claimed_matches_cas(dev, monkeypatch):
     assert t1.keys() == t0.keys()
     ks = list(t1.keys())
     _rows_close(np.stack([t1[k] for k in ks]), np.stack([t0[k] for k in ks]))
+
+
+def test_region_full_fails_loudly_without_silent_loss(dev, monkeypatch):
+    """A region table driven towards full through the bench path (claimed
+    pulls, region-aligned buckets, the fused [w | h | key] merge store): a
+    key whose region has no empty slot left sets the sticky error, and the
+    engine's check raises a region-full error at that step.  Until then no
+    row is lost: after every step that passed its check the table holds
+    exactly the distinct keys pulled so far.  The first region fills only
+    near full load (keys probe only their own 1024-slot region)."""
+    from swiftsnails_amd.models.sparse_lr import CtrSynth, SparseLRWorker, lr_init, make_lr_table
+    from swiftsnails_amd.ops.table import TableFullError
+    from swiftsnails_amd.parallel.engine import PSEngine
+
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    # 1664 keys per call: <= 16 buckets, so each bucket gets >= 4 of the 64
+    # regions (the region-bucket rule of launch_bd_dedup) and pulls claim
+    B, F = 128, 13
+    data = CtrSynth(batch_size=B, num_fields=F, num_features=50_000_000, tail_frac=1.0)
+    table = make_lr_table(data.num_features, 1, load=0.5, device=dev, capacity=1 << 16,
+                          init=lr_init("uniform", 0.01))
+    assert table.rbits == 6 and table.capacity == 1 << 16  # 64 regions of 1024 slots
+    eng = PSEngine(table, None, max_keys=B * F, dim=1, device=dev)
+    w = SparseLRWorker(eng, data)
+    assert eng.claim and all(d.rbits == table.rbits for d in eng.dedupers)
+    k = torch.empty(B * F, dtype=torch.int64, device=dev)
+    y = torch.empty(B, dtype=torch.float32, device=dev)
+    seen = torch.empty(0, dtype=torch.int64, device=dev)
+    err = None
+    for step in range(100):
+        w.step()
+        torch.cuda.synchronize()
+        assert eng._deferred_slot is not None  # the pull claimed (bench path)
+        try:
+            eng.check()
+        except TableFullError as e:
+            err = e
+            break
+        data.generate(step, 0, 1, k, y)
+        seen = torch.unique(torch.cat([seen, k]))
+        assert table.size() == seen.numel(), step  # no silent row loss
+        keys = torch.cat([kk for kk, _ in table.export(to_host=False)])
+        assert keys.numel() == seen.numel() and torch.equal(torch.sort(keys)[0], seen)
+    assert err is not None, "the table never filled"
+    assert "region" in str(err), str(err)
+    # near full: the last clean step left the table above 85 % load
+    assert seen.numel() >= 0.85 * table.capacity, seen.numel() / table.capacity
+
+
+def test_region_buckets_fit_the_dedup_table_all_distinct(dev):
+    """Region buckets hold whole regions, floor or ceil of R / Pd of them:
+    with R / Pd just above 4 some buckets get 5 regions, 1.25x the target
+    occurrences (~4480 at the one-rank 3584).  All-distinct keys would then
+    overflow the dedup's 4096-slot LDS table — a run-ending error the hash
+    buckets (~2 % size spread) never hit.  The dedup takes region buckets
+    only when the fullest bucket fits with every key distinct, so this call
+    falls back to hash buckets and dedups cleanly; the bench shape (R / Pd
+    ~23) keeps its region buckets."""
+    from swiftsnails_amd.ops.dedup import Deduper
+
+    # 2^12 regions, ~950 buckets: R / Pd ~ 4.3
+    n = 3584 * 950
+    k = torch.from_numpy(_keys(int(n * 1.05), 11)[:n]).to(dev)
+    assert k.numel() == n
+    d = Deduper(n, nranks=1, device=dev, mode="bucket")
+    d.rbits = 12
+    r = d(k)
+    torch.cuda.synchronize()
+    d.check()  # no overflow
+    assert r.rbits == 0  # the layout declined region buckets
+    assert int(r.ucount[0]) == n
+    # the bench's call shape keeps them: 10.2M keys over 2^16 regions
+    n2 = 262144 * 39
+    k2 = torch.randint(0, 1 << 30, (n2,), dtype=torch.int64, device=dev)
+    d2 = Deduper(n2, nranks=1, device=dev, mode="bucket")
+    d2.rbits = 16
+    r2 = d2(k2)
+    torch.cuda.synchronize()
+    d2.check()
+    assert r2.rbits == 16

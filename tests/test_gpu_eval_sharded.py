@@ -15,6 +15,7 @@ read-only pull runs on the device (the xGMI round on the slot past the ring,
 PSEngine._lookup_xgmi), and it leaves every table's size unchanged."""
 import os
 
+import numpy as np
 import pytest
 import torch
 import torch.distributed as dist
@@ -47,7 +48,37 @@ def _train_eval(rank, world, dev, transport):
     if world > 1:  # the device lookup ran, not the gloo fallback
         assert eng.metrics.counters.get("lookup_keys", 0) == 2 * (B // world) * F
     ev["pull_ahead"] = bool(eng.pull_ahead)
-    return ev, before
+    # the shard's rows, and the rounds whose keys were pulled (inserted): the
+    # trained steps plus the rounds pulled ahead past the last one
+    keys, rows = _export(table)
+    return ev, before, keys, rows, w.step_idx + len(w._pulled)
+
+
+def _export(table):
+    ks, rs = [], []
+    for k, r in table.export():
+        ks.append(k.numpy())
+        rs.append(r.numpy())
+    keys = np.concatenate(ks) if ks else np.zeros(0, np.int64)
+    rows = np.concatenate(rs) if rs else np.zeros((0, 2), np.float32)
+    return keys, rows
+
+
+def _keys_of_rounds(world, rounds):
+    """Every distinct key the ranks of a world-``world`` job pull in rounds
+    0 .. rounds-1 (regenerated with the same device generator)."""
+    from swiftsnails_amd.models.sparse_lr import CtrSynth
+
+    dev = torch.device("cuda", 0)
+    data = CtrSynth(batch_size=B // world, num_fields=F, num_features=FEATS, tail_frac=0.05)
+    k = torch.empty((B // world) * F, dtype=torch.int64, device=dev)
+    y = torch.empty(B // world, dtype=torch.float32, device=dev)
+    out = []
+    for s in range(rounds):
+        for r in range(world):
+            data.generate(s, r, world, k, y)
+            out.append(torch.unique(k))
+    return torch.unique(torch.cat(out)).cpu().numpy()
 
 
 def _rank(rank, world, init, q, env):
@@ -61,8 +92,8 @@ def _rank(rank, world, init, q, env):
         torch.cuda.set_device(dev)
         tr = XgmiTransport(rank, world, dev, dist.distributed_c10d._get_default_store(),
                            aux=TorchDistTransport(), timeout_s=60)
-        ev, n = _train_eval(rank, world, dev, tr)
-        q.put((rank, ev, n))
+        ev, n, keys, rows, pulled = _train_eval(rank, world, dev, tr)
+        q.put((rank, ev, n, keys, rows, pulled))
     finally:
         dist.destroy_process_group()
 
@@ -78,10 +109,13 @@ def _world(world, env):
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
-    evs = [ev for _, ev, _ in res]
+    evs = [x[1] for x in res]
     for ev in evs[1:]:  # every rank reports the same global metrics
         assert ev == evs[0]
-    return evs[0], sum(n for _, _, n in res)
+    pulled = {x[5] for x in res}
+    assert len(pulled) == 1, pulled  # every rank pulled the same rounds
+    shards = [(x[3], x[4]) for x in sorted(res, key=lambda x: x[0])]
+    return evs[0], sum(x[2] for x in res), shards, pulled.pop()
 
 
 _REF = {}
@@ -115,13 +149,35 @@ def _ref():
 ])
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_eval_matches_world1(world, mode, env, bound):
-    ref, n1 = _ref()
+    ref, n1, *ref_rows, _ = _ref()
     assert ref["auc"] > 0.6 and ref["samples"] == 2 * B
-    ev, n = _world(world, env)
+    ev, n, shards, pulled = _world(world, env)
     assert ev["samples"] == 2 * B
     assert ev["pull_ahead"] == (mode != "sync")
-    # the same keys trained, each on exactly one shard; pulled-ahead rounds
-    # have also inserted the keys of the rounds pulled past the last step
-    assert n == n1 if mode == "sync" else n1 <= n < 1.1 * n1
+    # every exported key is unique within its shard and across shards (a
+    # duplicate claim — two pulls claiming slots for one new key before a
+    # commit — would store it twice), and the shards together hold exactly the
+    # distinct keys of the rounds pulled: the trained steps, plus with
+    # pulled-ahead rounds the ones pulled past the last step
+    keys = np.concatenate([k for k, _ in shards])
+    rows = np.concatenate([r for _, r in shards])
+    assert len(np.unique(keys)) == len(keys) == n
+    want = _keys_of_rounds(world, pulled)
+    assert pulled == STEPS if mode == "sync" else pulled > STEPS
+    assert np.array_equal(np.sort(keys), want)
+    if mode == "sync":
+        # synchronous world N is the same update as world 1 (one AdaGrad step
+        # per key on the sum of every source's gradient): the rows agree up
+        # to float summation order
+        assert n == n1
+        rk, rr = ref_rows
+        oa, ob = np.argsort(rk), np.argsort(keys)
+        assert np.array_equal(rk[oa], keys[ob])
+        a, b = rr[oa], rows[ob]
+        np.testing.assert_allclose(b[:, 1], a[:, 1], rtol=1e-4, atol=1e-7)  # AdaGrad sums
+        # a weight whose summed gradient is ~0 can take its first AdaGrad
+        # step (+-lr) with either sign depending on the summation order
+        assert np.isclose(b[:, 0], a[:, 0], rtol=1e-4, atol=1e-6).mean() >= 0.9995
+        np.testing.assert_allclose(b[:, 0], a[:, 0], rtol=0, atol=2 * 0.05 * STEPS)
     assert abs(ev["auc"] - ref["auc"]) < bound, (world, mode, ev, ref)
     assert abs(ev["auc_truth"] - ref["auc_truth"]) < 1e-9

@@ -477,6 +477,49 @@ def _graph_after_mode_switch_body(dev):
     assert np.isfinite(w.mean_loss())
 
 
+def test_graph_teardown_then_replay_same_process(dev, monkeypatch):
+    """The hipGraph teardown order: a worker with captured graphs
+    on the N>1 path (a size-1 xGMI arena: mailbox puts / waits and the round
+    engine's events in the graph) is dropped inside a reference cycle
+    without close(), and the cyclic GC collects it while a second worker's
+    graphs are replaying in the same process.  The graphs are reset before the engine's events and
+    arenas go away (models/base.py _GraphSet), so the replays go on and the
+    second worker trains; the first worker's graphs trained as well."""
+    import gc
+
+    monkeypatch.setenv("SS_XGMI_TIMEOUT", "20")
+    monkeypatch.setenv("SS_PULL_AHEAD", "0")
+    from swiftsnails_amd.parallel.xgmi import XgmiTransport
+
+    torch.cuda.set_device(dev)
+    a, ta = _graph_worker("lr", dev, transport=XgmiTransport(0, 1, dev, None))
+    first = [float(a.step().sum().item()) for _ in range(2)]
+    assert a.enable_graph()
+    for _ in range(3 * a._gper):
+        a.step()
+    torch.cuda.synchronize()
+    a.engine.check()
+    ta.check()
+    assert np.isfinite(a.mean_loss()) and a.mean_loss() < first[0]
+    a.cycle = a  # only the cyclic GC can free it now
+    del a, ta
+    b, tb = _graph_worker("lr", dev)
+    b.step()
+    assert b.enable_graph()
+    for i in range(4 * b._gper):
+        b.step()
+        if i == b._gper:
+            gc.collect()  # the first worker goes while these replays run
+    torch.cuda.synchronize()
+    tb.check()
+    b.engine.check()
+    assert np.isfinite(b.mean_loss()) and 0 < b.mean_loss() < 0.7
+    b.close()  # explicit teardown; eager steps still work afterwards
+    b.step()
+    torch.cuda.synchronize()
+    assert np.isfinite(b.mean_loss())
+
+
 @pytest.mark.parametrize("occ", ["arena", "copy"])
 def test_record_exchange_world1_matches_unique(dev, monkeypatch, occ):
     """The record exchange (every occurrence shipped; the server dedups what

@@ -157,6 +157,19 @@ def test_bench_fallback_chain(force, plane, tier, fell):
     c = j["config"]
     assert c["plane"] == plane and c["xgmi_tier"] == tier and c["fell_back"] is fell, c
     assert c["devices"] == 1 and j["value"] > 0 and np.isfinite(c["loss_last"])
+    # the number says which round layout produced it
+    lay = c["layout"]
+    for k in ("depth", "server_stream", "bd_target_dist", "srv_sub_buckets", "claim",
+              "srv_rbits", "buckets_per_dest"):
+        assert k in lay, lay
+    assert lay["depth"] >= 3 and lay["srv_sub_buckets"] >= 1 and lay["bd_target_dist"] > 0
+    if plane == "xgmi":
+        # one rank with a device of its own: the server stream exists and the
+        # calibration decided whether to keep it; the layout reports that
+        ss = c["calibration"]["server_stream"]
+        assert ss["server_stream"] == lay["server_stream"]
+        assert len(ss["off_ms"]) == len(ss["on_ms"]) == ss["windows"]
+        assert lay["claim"] and lay["srv_rbits"] > 0
     if fell:
         assert "litmus failed on every tier" in c["fallback_reason"]
         assert "falling back to RCCL" in err
