@@ -1275,6 +1275,11 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
 #pragma unroll
     for (int k = 0; k < K; ++k) ugrad[r + 1 + k] = a[k] - uvals[r + 1 + k] * g0;
   };
+  // fused FM k = 8 update with vector rows: the key's slot, its table row
+  // and its pulled v go out BEFORE the occurrence gathers, so the row's
+  // read latency overlaps the sum instead of following it
+  bool vec9 = false;
+  if constexpr (DIM == 9) vec9 = slots != nullptr && fm9_vec_ok(t, op);
   // short lists: a thread per unique key
   for (uint32_t l = tid; l < nu; l += 1024) {
     const uint32_t q0 = seg[l], q1 = seg[l + 1];
@@ -1282,6 +1287,38 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
     float g0 = 0.f, a[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) a[k] = 0.f;
+    if constexpr (DIM == 9) {
+      if (vec9) {
+        const long long slot = slots[base + l];
+        const size_t r = (size_t)(base + l) * DIM;
+        float v[K], row[18];
+#pragma unroll
+        for (int k = 0; k < K; ++k) v[k] = uvals[r + 1 + k];
+        float* rp = slot >= 0 ? slot_row(t, (uint64_t)slot) : nullptr;
+        if (rp) {
+          const float2 x = *reinterpret_cast<const float2*>(rp);
+          const float4* q4 = reinterpret_cast<const float4*>(rp + 2);
+          row[0] = x.x, row[1] = x.y;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float4 y = q4[i];
+            row[2 + 4 * i] = y.x, row[3 + 4 * i] = y.y, row[4 + 4 * i] = y.z, row[5 + 4 * i] = y.w;
+          }
+        }
+        accumulate(q0, q1, 1u, g0, a);
+        if (!rp) continue;
+        float s2 = 0.f;
+        opt_update(op, row[0], row[9], s2, g0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) opt_update(op, row[1 + k], row[10 + k], s2, a[k] - v[k] * g0);
+        *reinterpret_cast<float2*>(rp) = make_float2(row[0], row[1]);
+        float4* o4 = reinterpret_cast<float4*>(rp + 2);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          o4[i] = make_float4(row[2 + 4 * i], row[3 + 4 * i], row[4 + 4 * i], row[5 + 4 * i]);
+        continue;
+      }
+    }
     accumulate(q0, q1, 1u, g0, a);
     store_row(l, g0, a);
   }

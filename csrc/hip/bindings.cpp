@@ -158,13 +158,15 @@ PYBIND11_MODULE(_ss_hip, m) {
      py::arg("P"), py::arg("slots32"), py::arg("out"), py::arg("snap"), py::arg("ip"),
      py::arg("size_ctr"), py::arg("err"), py::arg("st"), py::arg("luid") = 0,
      py::arg("occ") = 0);
+  m.def("apply_masked_ok", &apply_masked_ok);
   m.def("commit_claims", [](const DevTable& t, uintptr_t bkeys, uintptr_t bstart, uintptr_t unum,
                             uintptr_t ubase, int P_, uintptr_t slots32, uintptr_t snap,
-                            uintptr_t st) {
+                            uintptr_t st, uintptr_t err) {
     launch_commit_claims(t, P<const uint64_t>(bkeys), P<const uint32_t>(bstart),
                          P<const uint32_t>(unum), P<const uint32_t>(ubase), P_,
-                         P<const int>(slots32), P<const float>(snap), S(st));
-  });
+                         P<const int>(slots32), P<const float>(snap), S(st), P<int>(err));
+  }, py::arg("t"), py::arg("bkeys"), py::arg("bstart"), py::arg("unum"), py::arg("ubase"),
+     py::arg("P"), py::arg("slots32"), py::arg("snap"), py::arg("st"), py::arg("err") = 0);
   m.def("apply", [](const DevTable& t, uintptr_t slots, uintptr_t grads, const SegList& sl,
                     long long max_n, const OptParams& op, int G, uintptr_t st, uintptr_t snap,
                     uintptr_t only) {

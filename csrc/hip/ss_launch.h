@@ -48,9 +48,10 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
 void launch_lookup_bk(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                       const uint32_t* unum, const uint32_t* ubase, int P, float* out, int G,
                       hipStream_t st);
+bool apply_masked_ok(const DevTable& t, const OptParams& op);
 void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                           const uint32_t* unum, const uint32_t* ubase, int P, const int* slots32,
-                          const float* snap, hipStream_t st);
+                          const float* snap, hipStream_t st, int* err = nullptr);
 // only (optional): apply only at positions with only[pos] != 0 (wide rows);
 // slot32: `slots` holds 4-byte slot indices (a snapshot pull of scalar rows)
 void launch_apply(const DevTable& t, const long long* slots, const float* grads,

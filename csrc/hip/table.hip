@@ -427,11 +427,15 @@ __global__ __launch_bounds__(CT) void k_pull_claim_bk(
 
 // The fallback writer of a claimed pull whose fused merge did not run (a
 // snapshot invalidated between pull and push): every claimed slot still
-// EMPTY gets its key and the snapshot's (initial) row.
+// EMPTY gets its key and the snapshot's (initial) row.  A claimed slot that
+// holds ANOTHER key by now was taken by an insert that bypassed the claim
+// bookkeeping (a direct table insert between the pull and its commit): the
+// round's slot indices then point at that key's row, so the sticky error bit
+// 4 fails the next check instead of letting the push update the wrong row.
 __global__ __launch_bounds__(256) void k_commit_claims(
     DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
     const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
-    const int* __restrict__ slots32, const float2* __restrict__ snap) {
+    const int* __restrict__ slots32, const float2* __restrict__ snap, int* __restrict__ err) {
   const int b = blockIdx.x;
   const uint32_t nu = unum[b], base = ubase[b];
   const uint64_t* src = bkeys + bstart[b];
@@ -439,7 +443,11 @@ __global__ __launch_bounds__(256) void k_commit_claims(
     const int s = slots32[base + l];
     if (s < 0) continue;
     const uint64_t key = src[l];
-    if (*slot_key(t, (uint64_t)s) != kEmptyKey) continue;
+    const uint64_t held = *slot_key(t, (uint64_t)s);
+    if (held != kEmptyKey) {
+      if (held != key && err) atomicOr(err, 4);
+      continue;
+    }
     const float2 wh = snap[base + l];
     *reinterpret_cast<uint4*>(t.base + (uint64_t)s * 16) =
         make_uint4(__float_as_uint(wh.x), __float_as_uint(wh.y), (uint32_t)key,
@@ -954,6 +962,11 @@ static bool wide_rows(const DevTable& t) {
   return (t.dim == 32 || t.dim == 64 || t.dim == 128) && t.row_off % al == 0 &&
          t.stride % al == 0;
 }
+// launch_apply takes an `only` mask for this table (the wide-row vector apply)
+bool apply_masked_ok(const DevTable& t, const OptParams& op) {
+  const uint32_t W = t.dim * (uint32_t)(1 + opt_state_per_coord(op.kind));
+  return pull_vec_on() && wide_rows(t) && W == t.width;
+}
 
 void launch_probe(const DevTable& t, const uint64_t* keys, const SegList& sl, long long max_n,
                   long long* slots, const InitParams& ip, int insert,
@@ -1087,11 +1100,11 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
 
 void launch_commit_claims(const DevTable& t, const uint64_t* bkeys, const uint32_t* bstart,
                           const uint32_t* unum, const uint32_t* ubase, int P, const int* slots32,
-                          const float* snap, hipStream_t st) {
+                          const float* snap, hipStream_t st, int* err) {
   if (P <= 0) return;
   check_claim_table(t);
   hipLaunchKernelGGL(k_commit_claims, dim3(P), dim3(256), 0, st, t, bkeys, bstart, unum, ubase,
-                     slots32, reinterpret_cast<const float2*>(snap));
+                     slots32, reinterpret_cast<const float2*>(snap), err);
   check_launch("k_commit_claims");
 }
 
@@ -1123,7 +1136,9 @@ void launch_apply(const DevTable& t, const long long* slots, const float* grads,
     check_launch("k_apply_rows");
     return;
   }
-  if (only) throw_error("apply: the `only` mask is for wide fp32 rows");
+  if (only)
+    throw_error("apply: the `only` mask needs the wide-row vector apply (dim 32 / 64 / 128, fp32 "
+                "or bf16 rows, SS_PULL_VEC=1)");
   if (!snap && !t.bf16 && G > 1 && G <= 16 && t.dim > 1 && W <= (uint32_t)kStageMaxW &&
       W % 2 == 0 && W == t.width && t.row_off % 8 == 0 && t.stride % 8 == 0) {
     SS_DISPATCH_G(G, hipLaunchKernelGGL(k_apply_st<kG>, dim3(grid_for(max_n, kG, 1 << 22)),

@@ -200,7 +200,12 @@ class Word2VecWorker(PipelinedWorker):
             # items (uhot, written by k_w2v_osort); SS_W2V_FUSE=0: off
             # (compact bf16 rows too: updated in fp32, stored with stochastic
             # rounding)
-            self.fuse = engine.fast1 and os.environ.get("SS_W2V_FUSE", "1") != "0"
+            # (the masked apply of the rest needs the wide-row vector apply:
+            # with SS_PULL_VEC=0 the fuse is off, not an error mid-round)
+            tab = engine.table
+            self.fuse = (engine.fast1 and os.environ.get("SS_W2V_FUSE", "1") != "0" and
+                         tab is not None and
+                         bool(hip().apply_masked_ok(tab.dt, tab.opt.native())))
             self.uhot = ([torch.zeros(engine.max_keys * engine.world, dtype=torch.uint8,
                                       device=dev) for _ in range(engine.depth)]
                          if self.fuse else None)

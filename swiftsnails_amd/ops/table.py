@@ -461,6 +461,24 @@ class HbmTable:
         hip().probe_hist(self.dt, hist.data_ptr(), nbins, _stream_ptr(None))
         return hist.cpu().numpy()
 
+    def region_occupancy(self) -> dict:
+        """Occupied slots per probe region of a region table (keys probe only
+        inside the region their hash names, so the fullest region, not the
+        table's load, is what fills first): max / mean / p99 / min over the
+        2^rbits regions and the fullest region's fill fraction.  Reads every
+        slot's key word (a device pass over the shard)."""
+        if not self.rbits:
+            return {}
+        R = 1 << self.rbits
+        rlen = self.capacity // R
+        kw = self.storage.view(torch.int64).view(self.capacity, self.stride // 8)[
+            :, self.key_off // 8]
+        occ = (kw != -1).view(R, rlen).sum(1, dtype=torch.int64).float()
+        q = torch.quantile(occ, torch.tensor([0.5, 0.99], device=occ.device))
+        return {"regions": R, "region_slots": rlen, "max": int(occ.max()),
+                "mean": float(occ.mean()), "p50": float(q[0]), "p99": float(q[1]),
+                "min": int(occ.min()), "max_fill": float(occ.max()) / rlen}
+
     def stats(self) -> dict:
         """Observability snapshot: size, load factor, mean/max probe length."""
         import numpy as np
@@ -487,6 +505,9 @@ class HbmTable:
             raise TableFullError(f"table full: capacity {self.capacity}, size {self.size()}")
         if e & 2:
             raise ValueError("key 0xFFFFFFFFFFFFFFFF is reserved (empty-slot sentinel)")
+        if e & 4:
+            raise RuntimeError("a claimed slot was taken by another key before its commit (a "
+                               "direct table insert between a claimed pull and its push)")
 
     def assign(self, keys: torch.Tensor, rows: torch.Tensor, stream=None):
         """Insert-or-overwrite full rows (params + optimizer state)."""

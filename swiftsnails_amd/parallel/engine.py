@@ -604,7 +604,8 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         v = rnd.dd.owner.bucket_view(rnd.dd.n)
         _hip().commit_claims(self.table.dt, v[0], v[1], v[2], v[3], v[4], rnd.slots.data_ptr(),
                              rnd.snap.data_ptr(),
-                             self.raw_stream() if stream is None else stream)
+                             self.raw_stream() if stream is None else stream,
+                             self.table.err.data_ptr())
         rnd.deferred = False
         self._claimed = [x for x in self._claimed if x is not rnd]
 

@@ -133,10 +133,13 @@ class EngineControl:
         st = self.raw_stream()
         if getattr(self, "_claimed", None):
             self._commit_claimed(st)
+        # every enqueued round first — server updates on the server stream and
+        # pulled-ahead server halves on the pull / route streams use the same
+        # svals / rvals buffers as this lookup's round (an evaluation path:
+        # a device sync is cheap next to it)
+        torch.cuda.synchronize(self.device)
         ss = getattr(self, "server_stream", None)
         main = torch.cuda.current_stream(self.device)
-        if ss is not None:  # every enqueued server update before the lookup
-            main.wait_stream(ss)
         S = self.srv[q] if self.srv is not None else None
         for i in range(rounds):
             part = kd[i * cap:(i + 1) * cap]

@@ -28,7 +28,11 @@ def _load_roctx():
     global _roctx
     if _roctx is not None:
         return _roctx or None
-    for name in ("libroctx64.so", "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"):
+    # the rocprofiler-sdk roctx first: rocprofv3 --marker-trace records its
+    # ranges; the legacy libroctx64 ranges do not reach rocprofv3
+    for name in ("librocprofiler-sdk-roctx.so.1", "librocprofiler-sdk-roctx.so",
+                 "/opt/rocm/lib/librocprofiler-sdk-roctx.so", "libroctx64.so",
+                 "libroctx64.so.4", "/opt/rocm/lib/libroctx64.so"):
         try:
             lib = ctypes.CDLL(name)
             lib.roctxRangePushA.argtypes = [ctypes.c_char_p]

@@ -333,12 +333,12 @@ def test_region_buckets_fit_the_dedup_table_all_distinct(dev):
     ~23) keeps its region buckets."""
     from swiftsnails_amd.ops.dedup import Deduper
 
-    # 2^12 regions, ~950 buckets: R / Pd ~ 4.3
-    n = 3584 * 950
+    # 2^13 regions, ~1905 buckets of the 3584 target: R / Pd ~ 4.3
+    n = 3584 * 1905
     k = torch.from_numpy(_keys(int(n * 1.05), 11)[:n]).to(dev)
     assert k.numel() == n
     d = Deduper(n, nranks=1, device=dev, mode="bucket")
-    d.rbits = 12
+    d.rbits = 13
     r = d(k)
     torch.cuda.synchronize()
     d.check()  # no overflow
