@@ -88,14 +88,17 @@ class FMWorker(PipelinedWorker):
                        d.batch_size, d.num_fields, self.engine.dim, rnd.uvals.data_ptr(),
                        self.gs.data_ptr(), self.gss.data_ptr(), self.loss_sum.data_ptr(), 0, st)
             # the sorted per-bucket merge sums each unique key's gradient row
-            # once; one GPU (SS_FM_FUSE=1): the AdaGrad update of that row is
-            # fused into it (the row moved as 8- + 16-byte vectors per thread,
-            # bdedup.hip fm9_row_update) instead of storing the gradient rows
-            # for a separate apply kernel (k_apply_st).  The scalar form of
-            # the fused update (18 dependent 4-byte accesses per row) measured
-            # 0.62 -> 1.04 ms; SS_FM_FUSE=0 keeps the separate apply
+            # once and stores it; the AdaGrad update is the separate lane-group
+            # apply (k_apply_st, ~140 us: the random read-modify-write floor
+            # of 1.35M 72-byte rows).  SS_FM_FUSE=1 fuses the update into the
+            # merge instead — the row moved as 8- + 16-byte vectors per thread,
+            # its loads issued before the occurrence gathers (bdedup.hip
+            # fm9_row_update): measured 0.570-0.573 vs 0.542-0.546 ms per step
+            # (two A/B pairs, round 6; the scalar fused form: 0.62 -> 1.04 ms),
+            # the extra row registers cost the merge's occupancy more than the
+            # gradient-row round trip it saves
             fa = (self.engine.fuse_apply(rnd, snapshot=False)
-                  if os.environ.get("SS_FM_FUSE", "1") != "0" else None)
+                  if os.environ.get("SS_FM_FUSE", "0") == "1" else None)
             kw = {}
             if fa is not None:
                 assert not fa["slot32"]  # FM slots are never 4-byte (slot32: scalar rows)

@@ -149,10 +149,10 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
     "SS_LR_FWD": Knob("auto", "csrc/hip/segreduce.hip", "tuning",
                       "LR forward layout: packed | group (auto by lane utilisation)"),
-    "SS_FM_FUSE": Knob("1", "models/fm.py", "tuning",
-                       "one GPU: FM's AdaGrad update fused into the sorted gradient merge "
-                       "(rows as 8- + 16-byte vectors per thread; 0: gradient rows, then "
-                       "k_apply_st)"),
+    "SS_FM_FUSE": Knob("0", "models/fm.py", "experiment",
+                       "1: one GPU, FM's AdaGrad update fused into the sorted gradient merge "
+                       "(rows as 8- + 16-byte vectors per thread; 0.570-0.573 vs 0.542-0.546 "
+                       "ms/step for the merge + k_apply_st default)"),
     "SS_FM_REDUCE": Knob("sorted", "csrc/hip/bdedup.hip, models/fm.py", "tuning",
                          "FM gradient merge: sorted lists, or atomic (LDS float atomics)"),
     "SS_W2V_EARLY_SLOT": Knob("1", "csrc/hip/w2v.hip", "tuning",
