@@ -891,7 +891,9 @@ __global__ __launch_bounds__(FT) void k_bd_fill_occ(const uint32_t* __restrict__
 // of its unique keys in LDS — per-occurrence g = gs[j / F] * x[j] gathered
 // from the per-sample gradient (L2-resident) — and stores each row once:
 // no zero-fill, no global atomics.
-template <int RT>
+// OCC: occurrences per thread in flight (all their loads issued before the
+// first LDS atomic), and unique rows per thread per pass of the fused update
+template <int RT, int OCC = 2>
 __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ bstart,
                                                     const uint32_t* __restrict__ ubase,
                                                     const uint32_t* __restrict__ unum,
@@ -922,25 +924,25 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
   const uint32_t base = osi ? p0 : ubase[b];  // rows in occurrence space or compact
   for (uint32_t l = threadIdx.x; l < nu; l += RT) acc[l] = 0.f;
   __syncthreads();
-  // two occurrences per thread in flight (loads before the LDS atomics)
-  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += 2 * RT) {
-    uint32_t l[2], j[2];
-    float g[2];
+  // OCC occurrences per thread in flight (loads before the LDS atomics)
+  for (uint32_t pb = p0 + threadIdx.x; pb < p1; pb += OCC * RT) {
+    uint32_t l[OCC], j[OCC];
+    float g[OCC];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < OCC; ++r) {
       const uint32_t p = pb + r * RT;
       l[r] = p < p1 ? luid[p] : kBdInvalid;  // bucket-local unique id
       j[r] = p < p1 ? pj[p] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < OCC; ++r) {
       g[r] = l[r] != kBdInvalid ? self.pick(gs, (long long)j[r])[j[r] / (uint32_t)F] : 0.f;
       if (xval && l[r] != kBdInvalid) g[r] *= xval[j[r]];
     }
     // keys occurring once in the batch (usingle, from the dedup): a plain
     // LDS store — LDS float atomics are this kernel's cost (~6 us per 1M)
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
+    for (int r = 0; r < OCC; ++r) {
       if (l[r] == kBdInvalid) continue;
       if (usingle && usingle[ubase[b] + l[r]])
         acc[l[r]] = g[r];
@@ -959,24 +961,47 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     // nothing yet — store the whole [w | h | key] slot in one 16-byte store
     // (the key of a found key is rewritten unchanged), the bucket's unique
     // keys read coalesced from the dedup's staging
-    for (uint32_t l = threadIdx.x; l < nu; l += RT) {
-      const long long slot = slots32 ? (long long)slots32[base + l] : slots[base + l];
-      if (slot < 0) continue;
-      float2 wh = snap ? snap[base + l] : *reinterpret_cast<const float2*>(slot_row(t, slot));
-      float s2 = 0.f;
-      opt_update(op, wh.x, wh.y, s2, acc[l]);
-      if (bkeys) {
-        const uint64_t key = bkeys[p0 + l];
-        *reinterpret_cast<uint4*>(t.base + (uint64_t)slot * 16) =
-            make_uint4(__float_as_uint(wh.x), __float_as_uint(wh.y), (uint32_t)key,
-                       (uint32_t)(key >> 32));
-      } else {
-        *reinterpret_cast<float2*>(slot_row(t, slot)) = wh;
+    // OCC rows per thread: every row's slot, snapshot and key loads in
+    // flight before the first store
+    for (uint32_t l0 = threadIdx.x; l0 < nu; l0 += OCC * RT) {
+      long long sl[OCC];
+      float2 wh[OCC];
+      uint64_t key[OCC];
+#pragma unroll
+      for (int r = 0; r < OCC; ++r) {
+        const uint32_t l = l0 + r * RT;
+        sl[r] = l < nu ? (slots32 ? (long long)slots32[base + l] : slots[base + l]) : -1;
+        if (snap && l < nu) wh[r] = snap[base + l];
+        key[r] = bkeys && l < nu ? bkeys[p0 + l] : 0ull;
+      }
+#pragma unroll
+      for (int r = 0; r < OCC; ++r) {
+        const uint32_t l = l0 + r * RT;
+        if (sl[r] < 0) continue;
+        if (!snap) wh[r] = *reinterpret_cast<const float2*>(slot_row(t, sl[r]));
+        float s2 = 0.f;
+        opt_update(op, wh[r].x, wh[r].y, s2, acc[l]);
+        if (bkeys) {
+          *reinterpret_cast<uint4*>(t.base + (uint64_t)sl[r] * 16) =
+              make_uint4(__float_as_uint(wh[r].x), __float_as_uint(wh[r].y), (uint32_t)key[r],
+                         (uint32_t)(key[r] >> 32));
+        } else {
+          *reinterpret_cast<float2*>(slot_row(t, sl[r])) = wh[r];
+        }
       }
     }
     return;
   }
   for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];
+}
+
+// SS_BD_ROCC: occurrences per thread in flight in k_bd_reduce (2 or 4)
+static int bd_rocc() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_BD_ROCC");
+    return e && std::atoi(e) == 2 ? 2 : 4;
+  }();
+  return v;
 }
 
 // K7 for FM rows [w | v_1..v_K]: per unique key u with occurrences in samples
@@ -1686,7 +1711,11 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
     const char* e = std::getenv("SS_BD_RT");
     return e ? std::atoi(e) : 1024;
   }();
-  if (rt == 1024)
+  if (rt == 1024 && bd_rocc() == 4)
+    hipLaunchKernelGGL((k_bd_reduce<1024, 4>), dim3(L.P), dim3(1024), 0, st, S + L.bstart,
+                       S + L.ubase, S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv,
+                       slots, sn, opv, SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
+  else if (rt == 1024)
     hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
                        S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
                        SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
@@ -1722,10 +1751,16 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
   }
   if (bkeys && (!(slots || s32) || !snap || t->stride != 16 || t->key_off != 8 || t->row_off != 0))
     throw_error("bd_reduce_p: slot stores with keys need a snapshot merge into [w|h|key] slots");
-  hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj, luid,
-                     gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
-                     reinterpret_cast<const float2*>(snap), opv, self, s32, nullptr, nullptr, 0,
-                     bkeys);
+  if (bd_rocc() == 4)
+    hipLaunchKernelGGL((k_bd_reduce<1024, 4>), dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj,
+                       luid, gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
+                       reinterpret_cast<const float2*>(snap), opv, self, s32, nullptr, nullptr, 0,
+                       bkeys);
+  else
+    hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj,
+                       luid, gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
+                       reinterpret_cast<const float2*>(snap), opv, self, s32, nullptr, nullptr, 0,
+                       bkeys);
   check_launch("k_bd_reduce_p");
 }
 

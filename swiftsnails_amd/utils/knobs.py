@@ -147,6 +147,9 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
+    "SS_BD_ROCC": Knob("4", "csrc/hip/bdedup.hip", "tuning",
+                       "k_bd_reduce: occurrences (and fused-update rows) per thread in flight, "
+                       "2 or 4"),
     "SS_LR_FWD": Knob("auto", "csrc/hip/segreduce.hip", "tuning",
                       "LR forward layout: packed | group (auto by lane utilisation)"),
     "SS_FM_FUSE": Knob("0", "models/fm.py", "experiment",
