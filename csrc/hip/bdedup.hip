@@ -21,10 +21,10 @@
 //              chunk-major ([nch][P], coalesced)
 //   2 colscan  per-bucket exclusive scan down the chunks + bucket totals; the
 //              last workgroup to finish scans those into bucket start offsets
-//   4 scatter  bucket-ordered (key, j) records, one 16-byte store each;
-//              pos_of[j] and the bucket bkt[j] (both coalesced)
-//   5 dedup    one workgroup per bucket: reads its records coalesced, writes
-//              the occurrence list pj[pos] = j; LDS hash insert + compaction;
+//   4 scatter  bucket-ordered keys and the occurrence list pj[pos] = j (two
+//              arrays); pos_of[j] and the bucket bkt[j] (both coalesced)
+//   5 dedup    one workgroup per bucket: reads its keys coalesced; LDS hash
+//              insert + compaction;
 //              bucket-local ids luid[pos], the bucket's keys (staged in its own
 //              occurrence range, and — N>1 — straight into the destination's
 //              send segment, + zeroed gradient rows) and its unique count;
@@ -119,30 +119,15 @@ static constexpr int kBdRegs = 8;       // occurrences per dedup thread kept in 
 static constexpr int kBdMaxBuckets = 16384;
 static constexpr int kBdMaxSub = 64;    // server sub-buckets per bucket (srv_sub_buckets)
 
-// (key, sample) record of the scatter -> dedup hand-off: 12 bytes (three
-// dwords, one dwordx3 store / load) or 16 (uint4, one dwordx4; SS_BD_REC=16).
-// 12: 25 % fewer bytes of the route stream's largest array; the bench step
-// 0.850-0.854 -> 0.836-0.841 ms (three interleaved A/B pairs on one box).
-// A call whose keys all fit 32 bits (ids of a <= 4G-feature space: the
-// count kernel ORs the high words, the column scan publishes the verdict)
-// moves 8-byte (key, sample) records instead (SS_BD_REC=12 keeps 12).
-struct alignas(4) BdRec3 {
-  uint32_t x, y, z;
-};
-template <int RW>
-struct BdRecT {
-  using T = uint4;
-  static __device__ __forceinline__ T make(uint64_t k, uint32_t j) {
-    return make_uint4((uint32_t)k, (uint32_t)(k >> 32), j, 0u);
-  }
-};
-template <>
-struct BdRecT<3> {
-  using T = BdRec3;
-  static __device__ __forceinline__ T make(uint64_t k, uint32_t j) {
-    return BdRec3{(uint32_t)k, (uint32_t)(k >> 32), j};
-  }
-};
+// The scatter -> dedup hand-off: the bucket-ordered keys (`rk`, the record
+// buffer) and the occurrence list pj[pos] = j as two arrays.  A call whose
+// keys all fit 32 bits (ids of a <= 4G-feature space: the count kernel ORs
+// the high words, the column scan publishes the verdict) stores 4-byte keys,
+// else 8-byte ones (SS_BD_REC=12 / 16: always 8).  Until round 6 key and j
+// travelled as one interleaved (key, j) record that the dedup read whole and
+// copied j out of into pj: 41 MB read + 41 MB written more per bench step
+// (8-byte records; 12 / 16 bytes for wide keys before that, round 4: 12-byte
+// records 0.850-0.854 -> 0.836-0.841 ms).
 
 __device__ __forceinline__ uint32_t bd_bucket(uint64_t key, const RouteSpec& rs, uint32_t Pd) {
   const uint32_t d = rs.dest_of(key);
@@ -444,7 +429,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      uint32_t* __restrict__ pj,
                                                      uint32_t* __restrict__ pos_of,
                                                      uint32_t* __restrict__ bkt,
-                                                     typename BdRecT<RW>::T* __restrict__ rec,
+                                                     void* __restrict__ rec,
                                                      const uint32_t* __restrict__ wfin,
                                                      int xcd, uint64_t* __restrict__ skeys = nullptr,
                                                      uint32_t* __restrict__ spj = nullptr) {
@@ -458,9 +443,10 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
     const int g = (int)gridDim.x, x = c & 7;
     c = x * (g >> 3) + min(x, g & 7) + (c >> 3);
   }
-  // keys of 32 bits: 8-byte (key, sample) records (RW 3 only)
+  // keys of 32 bits: 4-byte keys (RW 3 only)
   const bool narrow = RW == 3 && wfin && *wfin == 0u;
-  uint2* rec2 = reinterpret_cast<uint2*>(rec);
+  uint32_t* rk32 = reinterpret_cast<uint32_t*>(rec);
+  uint64_t* rk64 = reinterpret_cast<uint64_t*>(rec);
   const uint32_t* row = hist + (long long)c * P;
   for (int b = threadIdx.x; b < P; b += CT) cur[b] = bstart[b] + row[b];
   for (int t0 = 0; t0 < chunk; t0 += kBdMaxChunk) {
@@ -481,21 +467,22 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
         if (k[e] != kEmptyKey) {
           b = bd_bucket(k[e], rs, (uint32_t)Pd);
           pos = atomicAdd(&cur[b], 1u);
-          // the key travels with its sample index as ONE 16-byte record (a
-          // random store costs a write request whatever its width), so the
-          // dedup reads its bucket coalesced instead of gathering keys[pj[p]]
-          // (a 64-byte line per occurrence) and writes pj itself.  Measured
+          // the key travels to its bucket position beside its sample index,
+          // so the dedup reads its bucket's keys coalesced instead of
+          // gathering keys[pj[p]] (a 64-byte line per occurrence).  Measured
           // standalone: scatter 119 -> 163 us, dedup 213 -> 123 us; N>1
-          // engine path 1.211 -> 1.169 ms/step, one GPU neutral
-          // record exchange: the key and its occurrence in two arrays at
-          // send-segment positions (the keys are the send segment)
+          // engine path 1.211 -> 1.169 ms/step, one GPU neutral.
+          // record exchange: the key and its occurrence at send-segment
+          // positions (the keys are the send segment)
           if (skeys) {
             skeys[pos] = k[e];
             spj[pos] = (uint32_t)j;
-          } else if (narrow) {
-            rec2[pos] = make_uint2((uint32_t)k[e], (uint32_t)j);
           } else {
-            rec[pos] = BdRecT<RW>::make(k[e], (uint32_t)j);
+            if (narrow)
+              rk32[pos] = (uint32_t)k[e];
+            else
+              rk64[pos] = k[e];
+            pj[pos] = (uint32_t)j;
           }
         }
         // the BdIndex (j -> bucket position, bucket) only for its consumers
@@ -529,8 +516,9 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
                                                        uint32_t* __restrict__ bkt,
                                                        uint32_t* __restrict__ rec,
                                                        const uint32_t* __restrict__ wfin,
-                                                       int xcd, uint64_t* __restrict__ skeys = nullptr,
-                                                       uint32_t* __restrict__ spj = nullptr) {
+                                                       int xcd, uint64_t* __restrict__ skeys,
+                                                       uint32_t* __restrict__ spj,
+                                                       uint32_t* __restrict__ pj) {
   constexpr int CT = 1024;
   extern __shared__ unsigned int sm[];
   unsigned int* cur = sm;           // [P] the chunk's cursor per bucket
@@ -603,31 +591,29 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
     }
     __syncthreads();
     const unsigned int nt = tot;
+    // keys (4 or 8 bytes) and j into two arrays at the bucket positions
+    // (the record exchange: the send segment's keys and spj)
+    uint32_t* const qj = skeys ? spj : pj;
     if (narrow) {
-      uint2* r2 = reinterpret_cast<uint2*>(rec);
+      uint32_t* rk32 = reinterpret_cast<uint32_t*>(rec);
       for (unsigned int i = t; i < nt; i += CT) {
         const uint32_t key = sx[i];
         const uint32_t b = bd_bucket((uint64_t)key, rs, (uint32_t)Pd);
         const uint32_t q = cur[b] + (i - toff[b]);
-        if (skeys) {
+        if (skeys)
           skeys[q] = key;
-          spj[q] = sz[i];
-        } else {
-          r2[q] = make_uint2(key, sz[i]);
-        }
+        else
+          rk32[q] = key;
+        qj[q] = sz[i];
       }
     } else {
-      BdRec3* r3 = reinterpret_cast<BdRec3*>(rec);
+      uint64_t* rk64 = reinterpret_cast<uint64_t*>(rec);
       for (unsigned int i = t; i < nt; i += CT) {
-        const uint32_t x = sx[i], y = sy[i];
-        const uint32_t b = bd_bucket((uint64_t)x | ((uint64_t)y << 32), rs, (uint32_t)Pd);
+        const uint64_t key = (uint64_t)sx[i] | ((uint64_t)sy[i] << 32);
+        const uint32_t b = bd_bucket(key, rs, (uint32_t)Pd);
         const uint32_t q = cur[b] + (i - toff[b]);
-        if (skeys) {
-          skeys[q] = (uint64_t)x | ((uint64_t)y << 32);
-          spj[q] = sz[i];
-        } else {
-          r3[q] = BdRec3{x, y, sz[i]};
-        }
+        (skeys ? skeys : rk64)[q] = key;
+        qj[q] = sz[i];
       }
     }
     __syncthreads();
@@ -648,7 +634,7 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
                                                    long long ucap,
                                                    uint32_t* __restrict__ ubase,
                                                    unsigned long long* __restrict__ ucount,
-                                                   const typename BdRecT<RW>::T* __restrict__ rec,
+                                                   const void* __restrict__ rec,
                                                    unsigned long long* __restrict__ dbg,
                                                    uint64_t* __restrict__ ukeys,
                                                    float* __restrict__ ugrad, int gdim,
@@ -681,20 +667,11 @@ __global__ __launch_bounds__(kBdDT) void k_bd_dedup(const uint64_t* __restrict__
   // registers; a hot bucket's excess parks it in luid[] (rewritten below)
   uint32_t slot[kBdRegs];
   uint64_t kk[kBdRegs];
-  // the bucket's (key, sample) records read coalesced, pj written back for
-  // the consumers
-  const bool narrow = RW == 3 && wfin && *wfin == 0u;  // 8-byte records (32-bit keys)
-  const uint2* rec2 = reinterpret_cast<const uint2*>(rec);
-  auto load = [&](uint32_t p) -> uint64_t {
-    if (narrow) {
-      const uint2 v = rec2[p];
-      pj[p] = v.y;
-      return (uint64_t)v.x;
-    }
-    const typename BdRecT<RW>::T v = rec[p];
-    pj[p] = v.z;
-    return (uint64_t)v.x | ((uint64_t)v.y << 32);
-  };
+  // the bucket's keys read coalesced (the scatter wrote pj beside them)
+  const bool narrow = RW == 3 && wfin && *wfin == 0u;  // 4-byte keys
+  const uint32_t* rk32 = reinterpret_cast<const uint32_t*>(rec);
+  const uint64_t* rk64 = reinterpret_cast<const uint64_t*>(rec);
+  auto load = [&](uint32_t p) -> uint64_t { return narrow ? (uint64_t)rk32[p] : rk64[p]; };
 #pragma unroll
   for (int r = 0; r < kBdRegs; ++r) {
     const uint32_t p = p0 + t + r * kBdDT;
@@ -1396,7 +1373,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   if (ucap < n) throw_error("bdedup: per-destination capacity must be >= n");
   if ((unsigned long long)rs.nranks * (unsigned long long)ucap >= 0x7FFFFFFFull)
     throw_error("bdedup: nranks*ucap overflows 31-bit unique ids");
-  if (!rec) throw_error("bdedup: the (key, sample) record buffer is required");
+  if (!rec) throw_error("bdedup: the bucket-ordered key buffer is required");
   const BdLayout L = bd_layout(ln, rs.nranks, ndest);
   if ((long long)L.Pd * bd_clamp_ndest(rs.nranks, ndest) > kBdMaxBuckets + kMaxSeg ||
       ln > bd_max_keys())
@@ -1436,15 +1413,11 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   // N>1 path 1.076-1.103 vs 1.109-1.169 ms)
   static const int cnt = wg_env("SS_BD_CNT", 1024);
   static const int cs = wg_env("SS_BD_CS", 1024);
-  // record width (SS_BD_REC): 16, 12, or auto (default: 8 bytes when every
-  // key of the call fits 32 bits, else 12)
-  static const int rw = [] {
-    const char* e = std::getenv("SS_BD_REC");
-    return e && std::atoi(e) == 16 ? 4 : 3;
-  }();
+  // key width of the hand-off (SS_BD_REC): auto (default: 4 bytes when
+  // every key of the call fits 32 bits, else 8) or 8
   static const bool narrow_ok = [] {
     const char* e = std::getenv("SS_BD_REC");
-    return !(e && (std::atoi(e) == 12 || std::atoi(e) == 16));
+    return !(e && std::atoi(e) >= 8);
   }();
   uint32_t* wacc = narrow_ok ? S + L.wacc : nullptr;
   uint32_t* wfin = S + L.wfin;
@@ -1492,7 +1465,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   int skt = 0;
   for (int kt = 16; kt >= 2 && !skt; kt /= 2)
     if (kt <= skt_max && s_lds(kt) <= kLdsMax) skt = kt;
-  if (rw == 3 && sorted && skt && L.P < 65536) {
+  if (sorted && skt && L.P < 65536) {
     if (L.chunk % 1024) throw_error("bdedup: chunk not a multiple of 1024");
     switch (skt) {
 #define SS_BD_S_CASE(KT)                                                                          \
@@ -1505,7 +1478,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     (void)attr;                                                                                   \
     hipLaunchKernelGGL(k_bd_scatter_s<KT>, dim3(L.nch), dim3(1024), s_lds(KT), st, keys, n, rs,  \
                        L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pos_of, bkt, rec, wfin,      \
-                       bd_xcd(), spj ? ukeys : nullptr, spj);                                     \
+                       bd_xcd(), spj ? ukeys : nullptr, spj, pj);                                 \
   } break;
       SS_BD_S_CASE(16)
       SS_BD_S_CASE(8)
@@ -1513,13 +1486,9 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
       SS_BD_S_CASE(2)
 #undef SS_BD_S_CASE
     }
-  } else if (rw == 3)
+  } else
     SS_BD_CT_DISPATCH2(ct, 3, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
-                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<BdRec3*>(rec), wfin,
-                       bd_xcd(), spj ? ukeys : nullptr, spj)
-  else
-    SS_BD_CT_DISPATCH2(ct, 4, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
-                       S + L.bstart, pj, pos_of, bkt, reinterpret_cast<uint4*>(rec), nullptr,
+                       S + L.bstart, pj, pos_of, bkt, rec, wfin,
                        bd_xcd(), spj ? ukeys : nullptr, spj)
 #undef SS_BD_CT_DISPATCH
 #undef SS_BD_CT_DISPATCH2
@@ -1527,18 +1496,10 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   if (spj) return rs.rbits;  // record exchange: the servers dedup
   // place: unique keys straight into the per-destination send segments
   // (+ zeroed gradient rows), reserved with one atomic per bucket
-  if (rw == 3)
-    hipLaunchKernelGGL(k_bd_dedup<3>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
-                       bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
-                       reinterpret_cast<const BdRec3*>(rec), dbg,
-                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub,
-                       wfin, rs.rbits);
-  else
-    hipLaunchKernelGGL(k_bd_dedup<4>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
-                       bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount,
-                       reinterpret_cast<const uint4*>(rec), dbg,
-                       place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub,
-                       nullptr, rs.rbits);
+  hipLaunchKernelGGL(k_bd_dedup<3>, dim3(L.P), dim3(kBdDT), 0, st, keys, pj, S + L.bstart, luid,
+                     bkeys, S + L.unum, S, L.Pd, ucap, S + L.ubase, ucount, rec, dbg,
+                     place ? ukeys : nullptr, place ? ugrad : nullptr, gdim, usingle, msub, usub,
+                     wfin, rs.rbits);
   check_launch("k_bd_dedup");
   if (inv && n > 0) {
     if (!pos_of || !bkt) throw_error("bdedup: the compact inverse needs pos_of and bkt");

@@ -121,9 +121,8 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_CNT": Knob("1024", "csrc/hip/bdedup.hip", "tuning",
                       "count workgroup size"),
     "SS_BD_REC": Knob("auto", "csrc/hip/bdedup.hip", "tuning",
-                      "bytes of the scatter -> dedup (key, sample) record: auto = 8 when every "
-                      "key of the call fits 32 bits, else 12 (dwordx3); 12 or 16 (dwordx4) "
-                      "fixed; 12 measured 0.836-0.841 vs 0.850-0.854 ms/step for 16 (3 A/B pairs)"),
+                      "key bytes of the scatter -> dedup hand-off (keys and pj as two arrays): "
+                      "auto = 4 when every key of the call fits 32 bits, else 8; 8 fixed"),
     "SS_SLOT32": Knob("1", "swiftsnails_amd/parallel/engine.py", "tuning",
                       "one GPU, scalar (w, h) snapshot rows, shard under 2^31 slots: the pull "
                       "stores 4-byte slot indices for the fused merge + update (0: 8 bytes)"),
@@ -147,6 +146,9 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
+    "SS_CLAIM_KR": Knob("4", "csrc/hip/table.hip", "tuning",
+                        "claimed pull: keys per thread whose first probe loads are in flight "
+                        "together (1 / 4 / 8)"),
     "SS_BD_ROCC": Knob("4", "csrc/hip/bdedup.hip", "tuning",
                        "k_bd_reduce: occurrences (and fused-update rows) per thread in flight, "
                        "2 or 4"),
