@@ -972,13 +972,41 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
   for (uint32_t l = threadIdx.x; l < nu; l += RT) ugrad[base + l] = acc[l];
 }
 
-// SS_BD_ROCC: occurrences per thread in flight in k_bd_reduce (2 or 4)
+// SS_BD_ROCC: occurrences per thread in flight in k_bd_reduce (2, 4 or 8);
+// SS_BD_RT: its workgroup size (256, 512, 1024)
 static int bd_rocc() {
   static const int v = [] {
     const char* e = std::getenv("SS_BD_ROCC");
-    return e && std::atoi(e) == 2 ? 2 : 4;
+    const int x = e ? std::atoi(e) : 4;
+    return x == 2 || x == 8 ? x : 4;
   }();
   return v;
+}
+static int bd_rt() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_BD_RT");
+    const int x = e ? std::atoi(e) : 1024;
+    return x == 256 || x == 512 ? x : 1024;
+  }();
+  return v;
+}
+// one launch of k_bd_reduce over P buckets at the (SS_BD_RT, SS_BD_ROCC)
+// shape: (1024, 2 / 4), (512, 2 / 4 / 8), (256, 2); others fall back to (1024, 4)
+template <typename... A>
+static void bd_reduce_launch(int P, hipStream_t st, A... a) {
+  const int rt = bd_rt(), oc = bd_rocc();
+  if (rt == 512 && oc == 8)
+    hipLaunchKernelGGL((k_bd_reduce<512, 8>), dim3(P), dim3(512), 0, st, a...);
+  else if (rt == 512 && oc == 4)
+    hipLaunchKernelGGL((k_bd_reduce<512, 4>), dim3(P), dim3(512), 0, st, a...);
+  else if (rt == 512)
+    hipLaunchKernelGGL((k_bd_reduce<512, 2>), dim3(P), dim3(512), 0, st, a...);
+  else if (rt == 256)
+    hipLaunchKernelGGL((k_bd_reduce<256, 2>), dim3(P), dim3(256), 0, st, a...);
+  else if (oc == 2)
+    hipLaunchKernelGGL((k_bd_reduce<1024, 2>), dim3(P), dim3(1024), 0, st, a...);
+  else
+    hipLaunchKernelGGL((k_bd_reduce<1024, 4>), dim3(P), dim3(1024), 0, st, a...);
 }
 
 // K7 for FM rows [w | v_1..v_K]: per unique key u with occurrences in samples
@@ -1667,27 +1695,9 @@ void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const ui
   const float2* sn = reinterpret_cast<const float2*>(snap);
   const BdLayout L = bd_layout(n, nranks, ndest);
   const uint32_t* S = scratch;
-  // workgroup size (SS_BD_RT experiment knob): measured 1024 >= 512 >= 256
-  static const int rt = [] {
-    const char* e = std::getenv("SS_BD_RT");
-    return e ? std::atoi(e) : 1024;
-  }();
-  if (rt == 1024 && bd_rocc() == 4)
-    hipLaunchKernelGGL((k_bd_reduce<1024, 4>), dim3(L.P), dim3(1024), 0, st, S + L.bstart,
-                       S + L.ubase, S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv,
-                       slots, sn, opv, SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
-  else if (rt == 1024)
-    hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(L.P), dim3(1024), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
-  else if (rt == 512)
-    hipLaunchKernelGGL(k_bd_reduce<512>, dim3(L.P), dim3(512), 0, st, S + L.bstart, S + L.ubase,
-                       S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
-  else
-    hipLaunchKernelGGL(k_bd_reduce<256>, dim3(L.P), dim3(256), 0, st, S + L.bstart, S + L.ubase,
-                     S + L.unum, pj, luid, gs, xval, F, ugrad, osi, usingle, tv, slots, sn, opv,
-                       SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
+  // workgroup shape: SS_BD_RT / SS_BD_ROCC (bd_reduce_launch)
+  bd_reduce_launch(L.P, st, S + L.bstart, S + L.ubase, S + L.unum, pj, luid, gs, xval, F, ugrad,
+                   osi, usingle, tv, slots, sn, opv, SelfSeg{}, s32, lacc, lacc_out, lacc_n, bkeys);
   check_launch("k_bd_reduce");
 }
 
@@ -1712,16 +1722,10 @@ void launch_bd_reduce_p(int P, const uint32_t* bstart, const uint32_t* ubase, co
   }
   if (bkeys && (!(slots || s32) || !snap || t->stride != 16 || t->key_off != 8 || t->row_off != 0))
     throw_error("bd_reduce_p: slot stores with keys need a snapshot merge into [w|h|key] slots");
-  if (bd_rocc() == 4)
-    hipLaunchKernelGGL((k_bd_reduce<1024, 4>), dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj,
-                       luid, gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
-                       reinterpret_cast<const float2*>(snap), opv, self, s32, nullptr, nullptr, 0,
-                       bkeys);
-  else
-    hipLaunchKernelGGL(k_bd_reduce<1024>, dim3(P), dim3(1024), 0, st, bstart, ubase, unum, pj,
-                       luid, gs, nullptr, F, ugrad, 0, nullptr, tv, slots,
-                       reinterpret_cast<const float2*>(snap), opv, self, s32, nullptr, nullptr, 0,
-                       bkeys);
+  bd_reduce_launch(P, st, bstart, ubase, unum, pj, luid, gs, static_cast<const float*>(nullptr), F,
+                   ugrad, 0, static_cast<const uint8_t*>(nullptr), tv, slots,
+                   reinterpret_cast<const float2*>(snap), opv, self, s32,
+                   static_cast<float*>(nullptr), static_cast<float*>(nullptr), 0, bkeys);
   check_launch("k_bd_reduce_p");
 }
 

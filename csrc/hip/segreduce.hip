@@ -258,6 +258,67 @@ __global__ __launch_bounds__(256) void k_lr_fwd_g_lds(const uint32_t* __restrict
   if (active && !per_sample) gocc[j] = sg[ls] * x;
 }
 
+// k_lr_fwd_g_lds over R groups of spb samples per workgroup, for the
+// bucketed one-gather mode (occ + pos_of, per-sample gradients): every
+// thread issues its R pos_of loads, then its R occ gathers, before the first
+// LDS sum — R dependent-load chains in flight per thread instead of one, and
+// R x fewer 256-thread workgroups (43691 at the bench shape, each one chain
+// deep).  Needs R * spb <= 256 (the per-sample tail runs one sample per thread).
+template <int R>
+__global__ __launch_bounds__(256) void k_lr_fwd_occ(const uint32_t* __restrict__ pos_of,
+                                                    const float* __restrict__ xval,
+                                                    const float* __restrict__ labels, int B, int F,
+                                                    float* __restrict__ gs,
+                                                    float* __restrict__ loss_sum,
+                                                    float* __restrict__ pred,
+                                                    const float* __restrict__ occ) {
+  __shared__ float sval[R * 256];
+  __shared__ float sdot[256];
+  __shared__ float sloss[4];
+  const int spb = F >= 256 ? 1 : 256 / F;
+  const int t = threadIdx.x, ls = t / F;
+  const long long sb = (long long)blockIdx.x * spb * R;  // first sample of the workgroup
+  uint32_t p[R];
+  float x[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const long long s = sb + (long long)r * spb + ls;
+    const bool active = ls < spb && s < B;
+    const long long j = (sb + (long long)r * spb) * F + t;
+    p[r] = active ? pos_of[j] : kInvS;
+    x[r] = active ? (xval ? xval[j] : 1.f) : 0.f;
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) sval[r * 256 + t] = p[r] == kInvS ? 0.f : occ[p[r]] * x[r];
+  __syncthreads();
+  // R * spb sample sums, tps threads per sample (as packed_sample_sums)
+  const int ns = R * spb;
+  int tps = 8;
+  while (tps > 1 && tps * ns > 256) tps >>= 1;
+  const int gi = t / tps, k = t - gi * tps;
+  float z = 0.f;
+  if (gi < ns) {
+    const float* v = sval + (gi / spb) * 256 + (gi % spb) * F;
+    for (int f = k; f < F; f += tps) z += v[f];
+  }
+  for (int o = tps >> 1; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
+  if (gi < ns && k == 0) sdot[gi] = z;
+  __syncthreads();
+  float l = 0.f;
+  if (t < ns && sb + t < B) {  // group r's sample ls2 is sample sb + r * spb + ls2 = sb + t
+    const float zz = sdot[t];
+    const float y = labels[sb + t];
+    const float pr = 1.f / (1.f + __expf(-zz));
+    gs[sb + t] = pr - y;
+    if (pred) pred[sb + t] = pr;
+    l = fmaxf(zz, 0.f) + __logf(1.f + __expf(-fabsf(zz))) - y * zz;
+  }
+  for (int o = 32; o > 0; o >>= 1) l += __shfl_down(l, o, 64);
+  if ((t & 63) == 0) sloss[t >> 6] = l;
+  __syncthreads();
+  if (t == 0 && loss_sum) ctr_addf(loss_sum, sloss[0] + sloss[1] + sloss[2] + sloss[3]);
+}
+
 // Same contract, one sample per lane group (F <= 64, sample_group.h).
 __global__ __launch_bounds__(256) void k_lr_fwd_g(const uint32_t* __restrict__ inv,
                                                   BdIndex ix,
@@ -371,6 +432,24 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
     return;
   }
   const int spb = F >= 256 ? 1 : 256 / F;
+  // the one-gather mode with per-sample gradients: R sample groups per
+  // workgroup (SS_LR_FWD_R: 1 / 2 / 4)
+  static const int fr = [] {
+    const char* e = std::getenv("SS_LR_FWD_R");
+    const int v = e ? std::atoi(e) : 4;
+    return (v == 1 || v == 2) ? v : 4;
+  }();
+  if (occ && ix.pos_of && per_sample && fr > 1 && fr * spb <= 256) {
+    const int g = fr * spb;
+    if (fr == 4)
+      hipLaunchKernelGGL(k_lr_fwd_occ<4>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
+                         labels, B, F, gocc, loss_sum, pred, occ);
+    else
+      hipLaunchKernelGGL(k_lr_fwd_occ<2>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
+                         labels, B, F, gocc, loss_sum, pred, occ);
+    check_launch("k_lr_fwd_occ");
+    return;
+  }
   hipLaunchKernelGGL(k_lr_fwd_g_lds, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, ix, xval,
                      labels, B, F, uvals, gocc, per_sample, loss_sum, pred, occ);
   check_launch("k_lr_fwd_g_lds");

@@ -347,7 +347,13 @@ static_assert(kClaimTS == 1 << 13, "lds_claim hashes to 13 bits");
 // (k_bd_fill_occ fused: the rows staged in LDS, no uvals round trip); `out`
 // may then be null.
 static constexpr int kClaimMaxU = 4096;  // unique keys of a bucket (the dedup's LDS table)
-template <int CT>
+// KR: keys per thread whose first probe loads are in flight together (a
+// bucket's ~1800 unique keys over 256 threads are ~7 keys per thread; the
+// workgroup's 48 KB of LDS allows 3 per CU).  The first probe resolves
+// almost every key (mean probe length 0.48 at load 0.49,
+// profiles/r6_long_region.md); longer probes continue one load at a time.
+// KR = 1 (one key at a time) measured fastest: see launch_pull_claim_bk
+template <int CT, int KR>
 __global__ __launch_bounds__(CT) void k_pull_claim_bk(
     DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
     const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
@@ -362,42 +368,63 @@ __global__ __launch_bounds__(CT) void k_pull_claim_bk(
   const uint32_t nu = unum[b], base = ubase[b];
   const uint64_t* src = bkeys + bstart[b];
   unsigned long long ins = 0;
-  for (uint32_t l = threadIdx.x; l < nu; l += CT) {
-    const uint64_t key = src[l];
-    long long slot = -1;
-    bool inserted = false;
-    float2 wh = make_float2(0.f, 0.f);
-    if (key != kEmptyKey) {
-      ProbeSeq ps = probe_seq(t, key);
-      for (uint64_t n = 0, len = ps.len(); n < len; ++n, ps.next()) {
-        const uint4 v = *reinterpret_cast<const uint4*>(t.base + ps.s * 16);
-        const uint64_t k = ((uint64_t)v.w << 32) | v.z;
-        if (k == key) {
-          slot = (long long)ps.s;
-          wh = make_float2(__uint_as_float(v.x), __uint_as_float(v.y));
-          break;
-        }
-        if (k == kEmptyKey && lds_claim(cl, (uint32_t)ps.s)) {
-          slot = (long long)ps.s;
-          inserted = true;
-          break;
+  for (uint32_t l0 = threadIdx.x; l0 < nu; l0 += KR * CT) {
+    uint64_t key[KR], s0[KR];
+    uint4 v[KR];
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      const uint32_t l = l0 + r * CT;
+      key[r] = l < nu ? src[l] : kEmptyKey;
+    }
+#pragma unroll
+    for (int r = 0; r < KR; ++r)
+      if (key[r] != kEmptyKey) {
+        s0[r] = probe_seq(t, key[r]).s;
+        v[r] = *reinterpret_cast<const uint4*>(t.base + s0[r] * 16);
+      }
+#pragma unroll
+    for (int r = 0; r < KR; ++r) {
+      const uint32_t l = l0 + r * CT;
+      if (l >= nu) continue;
+      long long slot = -1;
+      bool inserted = false;
+      float2 wh = make_float2(0.f, 0.f);
+      if (key[r] != kEmptyKey) {
+        ProbeSeq ps = probe_seq(t, key[r]);
+        uint4 x = v[r];
+        for (uint64_t n = 0, len = ps.len(); n < len; ++n) {
+          if (n) {
+            ps.next();
+            x = *reinterpret_cast<const uint4*>(t.base + ps.s * 16);
+          }
+          const uint64_t k = ((uint64_t)x.w << 32) | x.z;
+          if (k == key[r]) {
+            slot = (long long)ps.s;
+            wh = make_float2(__uint_as_float(x.x), __uint_as_float(x.y));
+            break;
+          }
+          if (k == kEmptyKey && lds_claim(cl, (uint32_t)ps.s)) {
+            slot = (long long)ps.s;
+            inserted = true;
+            break;
+          }
         }
       }
+      if (slot < 0) atomicOr(err, key[r] == kEmptyKey ? 2 : 1);  // 1: the key's region is full
+      const long long pos = (long long)base + l;
+      slots32[pos] = (int)slot;
+      if (inserted) {
+        wh = make_float2(init_value(ip, key[r], 0, 1), ip.state_init);
+      } else if (slot >= 0) {
+        // a row written by an older CAS-path insert of a non-prefilled table
+        wh.x = fresh_or(wh.x, ip, key[r], 0, 1);
+        if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
+      }
+      if (out) out[pos] = wh.x;
+      if (occ && l < (uint32_t)kClaimMaxU) sv[l] = wh.x;
+      snap[pos] = wh;
+      ins += inserted;
     }
-    if (slot < 0) atomicOr(err, key == kEmptyKey ? 2 : 1);  // 1: the key's region is full
-    const long long pos = (long long)base + l;
-    slots32[pos] = (int)slot;
-    if (inserted) {
-      wh = make_float2(init_value(ip, key, 0, 1), ip.state_init);
-    } else if (slot >= 0) {
-      // a row written by an older CAS-path insert of a non-prefilled table
-      wh.x = fresh_or(wh.x, ip, key, 0, 1);
-      if (__float_as_uint(wh.y) == 0xFFFFFFFFu) wh.y = ip.state_init;
-    }
-    if (out) out[pos] = wh.x;
-    if (occ && l < (uint32_t)kClaimMaxU) sv[l] = wh.x;
-    snap[pos] = wh;
-    ins += inserted;
   }
   ins = wave_sum_u64(ins);
   if ((threadIdx.x & 63) == 0 && ins) ctr_add(size_ctr, ins);
@@ -1085,15 +1112,27 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
     const int v = e ? std::atoi(e) : kClaimT;
     return (v == 64 || v == 128 || v == 512 || v == 1024) ? v : 256;
   }();
-#define SS_CLAIM_LAUNCH(CT)                                                                     \
-  hipLaunchKernelGGL(k_pull_claim_bk<CT>, dim3(P), dim3(CT), 0, st, t, bkeys, bstart, unum,     \
+  // first-probe loads in flight per thread (SS_CLAIM_KR: 1 / 4 / 8; the
+  // 256-thread default workgroup only).  Measured slower with more in flight
+  // (bench 0.733-0.734 ms at 1, 0.737-0.739 at 4, 0.746-0.748 at 8; pull
+  // standalone 209 / 223 / 239 us, raw/r6_claim_kr_ab.txt): the pull is bound
+  // by the bytes of its random lines and streams, not by its load chains
+  static const int kr = [] {
+    const char* e = std::getenv("SS_CLAIM_KR");
+    const int v = e ? std::atoi(e) : 1;
+    return (v == 4 || v == 8) ? v : 1;
+  }();
+#define SS_CLAIM_LAUNCH(CT, KR)                                                                 \
+  hipLaunchKernelGGL((k_pull_claim_bk<CT, KR>), dim3(P), dim3(CT), 0, st, t, bkeys, bstart, unum, \
                      ubase, slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err, luid, \
                      occ, pj, self)
-  if (ct == 256) SS_CLAIM_LAUNCH(256);
-  else if (ct == 64) SS_CLAIM_LAUNCH(64);
-  else if (ct == 128) SS_CLAIM_LAUNCH(128);
-  else if (ct == 512) SS_CLAIM_LAUNCH(512);
-  else SS_CLAIM_LAUNCH(1024);
+  if (ct == 256 && kr == 4) SS_CLAIM_LAUNCH(256, 4);
+  else if (ct == 256 && kr == 8) SS_CLAIM_LAUNCH(256, 8);
+  else if (ct == 256) SS_CLAIM_LAUNCH(256, 1);
+  else if (ct == 64) SS_CLAIM_LAUNCH(64, 1);
+  else if (ct == 128) SS_CLAIM_LAUNCH(128, 1);
+  else if (ct == 512) SS_CLAIM_LAUNCH(512, 1);
+  else SS_CLAIM_LAUNCH(1024, 1);
 #undef SS_CLAIM_LAUNCH
   check_launch("k_pull_claim_bk");
 }

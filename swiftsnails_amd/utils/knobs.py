@@ -146,12 +146,15 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
-    "SS_CLAIM_KR": Knob("4", "csrc/hip/table.hip", "tuning",
+    "SS_CLAIM_KR": Knob("1", "csrc/hip/table.hip", "tuning",
                         "claimed pull: keys per thread whose first probe loads are in flight "
-                        "together (1 / 4 / 8)"),
+                        "together (1 / 4 / 8; 4 and 8 measured slower)"),
     "SS_BD_ROCC": Knob("4", "csrc/hip/bdedup.hip", "tuning",
                        "k_bd_reduce: occurrences (and fused-update rows) per thread in flight, "
                        "2 or 4"),
+    "SS_LR_FWD_R": Knob("4", "csrc/hip/segreduce.hip", "tuning",
+                        "packed LR forward (one-gather mode): sample groups per workgroup, "
+                        "their gathers in flight together (1 / 2 / 4)"),
     "SS_LR_FWD": Knob("auto", "csrc/hip/segreduce.hip", "tuning",
                       "LR forward layout: packed | group (auto by lane utilisation)"),
     "SS_FM_FUSE": Knob("0", "models/fm.py", "experiment",

@@ -428,6 +428,44 @@ def test_lr_fwd_bwd_matches_torch(dev, F):
     np.testing.assert_allclose(g.cpu().numpy(), ref_g.numpy(), rtol=1e-3, atol=1e-4)
 
 
+@pytest.mark.parametrize("F", [39, 13, 100])
+@pytest.mark.parametrize("with_x", [False, True])
+def test_lr_fwd_one_gather_matches_torch(dev, F, with_x):
+    """The bucketed forward's one-gather mode (occ[pos_of[j]], per-sample
+    gradient p - y): several sample groups per workgroup with their gathers
+    in flight together (k_lr_fwd_occ).  B is not a multiple of a workgroup's
+    samples, and some occurrences have no position (invalid keys: 0)."""
+    from swiftsnails_amd._native import hip
+
+    B, M = 3001, 40000
+    rng = np.random.default_rng(17 + F)
+    pos = rng.integers(0, M, size=B * F).astype(np.int64)
+    pos[::97] = 0xFFFFFFFF
+    x = rng.standard_normal(B * F).astype(np.float32)
+    y = (rng.random(B) < 0.3).astype(np.float32)
+    occ = (rng.standard_normal(M) * 0.2).astype(np.float32)
+    tpos = torch.from_numpy(pos.astype(np.uint32).view(np.int32)).to(dev)
+    tx, ty, tocc = (torch.from_numpy(a).to(dev) for a in (x, y, occ))
+    gs = torch.full((B,), float("nan"), device=dev)
+    loss = torch.zeros(256 * 32, device=dev)
+    pred = torch.empty(B, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    hip().lr_fwd_g(0, tx.data_ptr() if with_x else 0, ty.data_ptr(), B, F, 0, gs.data_ptr(), 1,
+                   loss.data_ptr(), pred.data_ptr(), st, [tpos.data_ptr(), 0, 0, 0],
+                   occ=tocc.data_ptr())
+    torch.cuda.synchronize()
+    valid = pos != 0xFFFFFFFF
+    w = np.where(valid, occ[np.where(valid, pos, 0)], 0.0).astype(np.float64)
+    xv = x.astype(np.float64) if with_x else np.ones(B * F)
+    z = torch.from_numpy((w * xv).reshape(B, F).sum(1))
+    p = torch.sigmoid(z)
+    Y = torch.from_numpy(y).double()
+    ref_loss = torch.nn.functional.binary_cross_entropy_with_logits(z, Y, reduction="sum")
+    np.testing.assert_allclose(pred.cpu().numpy(), p.numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(gs.cpu().numpy(), (p - Y).numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(loss.sum().item(), ref_loss.item(), rtol=1e-4)
+
+
 @pytest.mark.parametrize("nranks", [1, 3])
 def test_segreduce_lr_matches_atomic_path(dev, nranks):
     """Atomic-free bin-partition reduction == per-occurrence atomics (and torch)."""
