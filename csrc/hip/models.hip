@@ -87,6 +87,58 @@ __global__ __launch_bounds__(256) void k_gen_ctr(uint64_t seed, long long sample
     labels[s0 + t] = gen_ctr_label(seed, (uint64_t)(sample_base + s0 + t), sdot[t] + truth_bias);
 }
 
+// The same generator over R groups of spb samples per workgroup: each
+// thread draws its R keys (independent hash / exp chains, all in flight
+// together) before the per-sample sums, and R x fewer workgroups are
+// dispatched (43691 256-thread workgroups of one key per thread at the bench
+// shape).  Bit-identical keys and labels (models/ctr_data.py gen_ctr_np).
+template <int R>
+__global__ __launch_bounds__(256) void k_gen_ctr_r(uint64_t seed, long long sample_base, int B,
+                                                   int F, long long V, double logV,
+                                                   float tail_frac, float truth_scale,
+                                                   float truth_bias, uint64_t* __restrict__ keys,
+                                                   float* __restrict__ labels,
+                                                   const long long* __restrict__ step_dev,
+                                                   long long step_mul, long long step_add) {
+  if (step_dev) sample_base = *step_dev * step_mul + step_add;
+  __shared__ float sval[R * 256];
+  __shared__ float sdot[256];
+  const int spb = samples_per_block(F);
+  const int t = threadIdx.x;
+  const int ls = t / F, f = t - (t / F) * F;
+  const long long sb = (long long)blockIdx.x * spb * R;  // first sample of the workgroup
+  float wv[R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    const long long s = sb + (long long)r * spb + ls;
+    wv[r] = 0.f;
+    if (ls < spb && s < B) {
+      const uint64_t key = gen_ctr_key(seed, (uint64_t)(sample_base + s), f, V, logV, tail_frac);
+      keys[s * F + f] = key;
+      wv[r] = truth_weight(key, truth_scale);
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < R; ++r) sval[r * 256 + t] = wv[r];
+  __syncthreads();
+  // R * spb sample sums, tps threads per sample (as packed_sample_sums)
+  const int ns = R * spb;
+  int tps = 8;
+  while (tps > 1 && tps * ns > 256) tps >>= 1;
+  const int gi = t / tps, k = t - gi * tps;
+  float z = 0.f;
+  if (gi < ns) {
+    const float* v = sval + (gi / spb) * 256 + (gi % spb) * F;
+    for (int ff = k; ff < F; ff += tps) z += v[ff];
+  }
+  for (int o = tps >> 1; o > 0; o >>= 1) z += __shfl_xor(z, o, 64);
+  if (gi < ns && k == 0) sdot[gi] = z;
+  __syncthreads();
+  if (t < ns && sb + t < B)
+    labels[sb + t] =
+        gen_ctr_label(seed, (uint64_t)(sample_base + sb + t), sdot[t] + truth_bias);
+}
+
 // Fused LR forward/backward over B samples x F features (CTR-style fixed
 // field count).  inv[j] indexes the pulled unique-key value/gradient rows.
 __global__ __launch_bounds__(256) void k_lr_fwd_bwd_lds(const uint32_t* __restrict__ inv,
@@ -351,6 +403,25 @@ void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long lon
   if (F < 1 || F > 256) throw_error("gen_ctr: F must be in [1,256]");
   const double logV = log((double)vocab_per_field + 1.0);
   const int spb = samples_per_block(F);
+  // R sample groups per workgroup (SS_GEN_R: 1 / 2 / 4)
+  static const int gr = [] {
+    const char* e = std::getenv("SS_GEN_R");
+    const int v = e ? std::atoi(e) : 4;
+    return (v == 1 || v == 2) ? v : 4;
+  }();
+  if (gr > 1 && gr * spb <= 256) {
+    const int g = gr * spb, nb = (B + g - 1) / g;
+    if (gr == 4)
+      hipLaunchKernelGGL(k_gen_ctr_r<4>, dim3(nb), dim3(256), 0, st, seed, sample_base, B, F,
+                         vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels,
+                         step_dev, step_mul, step_add);
+    else
+      hipLaunchKernelGGL(k_gen_ctr_r<2>, dim3(nb), dim3(256), 0, st, seed, sample_base, B, F,
+                         vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels,
+                         step_dev, step_mul, step_add);
+    check_launch("k_gen_ctr_r");
+    return;
+  }
   const int blocks = (B + spb - 1) / spb;
   hipLaunchKernelGGL(k_gen_ctr, dim3(blocks), dim3(256), 0, st, seed, sample_base, B, F,
                      vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels,

@@ -325,10 +325,18 @@ __global__ __launch_bounds__(256) void k_pull_unique_bk(DevTable t, const uint64
 // per bench step against 0.832-0.835 (512) and 0.843-0.844 (1024) on one
 // box — small workgroups interleave with the route stream's kernels
 static constexpr int kClaimT = 256;
-static constexpr int kClaimTS = 8192;  // LDS claim slots (>= 2x the <= 4096 keys of a bucket)
+// LDS claim set of TS slot indices (a power of two >= the <= 4096 keys of a
+// bucket, so a claim always finds a free entry): 8192 keeps it at most half
+// full; 4096 (SS_CLAIM_TS=4096) halves its LDS — 32 instead of 48 KB per
+// workgroup, 5 instead of 3 workgroups per CU — at the price of longer LDS
+// probes in buckets with many new keys
+static constexpr int kClaimTS = 8192;
+template <int TS>
 __device__ __forceinline__ bool lds_claim(uint32_t* cl, uint32_t s) {
-  uint32_t i = (s * 0x9E3779B1u) >> (32 - 13);  // 13 = log2(kClaimTS)
-  for (int k = 0; k < kClaimTS; ++k) {
+  constexpr int kBits = TS == 8192 ? 13 : 12;
+  static_assert(TS == 1 << kBits, "claim set: 4096 or 8192 entries");
+  uint32_t i = (s * 0x9E3779B1u) >> (32 - kBits);
+  for (int k = 0; k < TS; ++k) {
     const uint32_t v = cl[i];
     if (v == s) return false;
     if (v == 0xFFFFFFFFu) {
@@ -336,11 +344,10 @@ __device__ __forceinline__ bool lds_claim(uint32_t* cl, uint32_t s) {
       if (prev == 0xFFFFFFFFu) return true;
       if (prev == s) return false;
     }
-    i = (i + 1) & (kClaimTS - 1);
+    i = (i + 1) & (TS - 1);
   }
-  return false;  // unreachable: at most 4096 claims per workgroup
+  return false;  // unreachable: at most 4096 distinct slots claimed per workgroup
 }
-static_assert(kClaimTS == 1 << 13, "lds_claim hashes to 13 bits");
 
 // luid / occ (optional, the LR forward's one-gather mode): the bucket's
 // parameters also go to occ[p] = w(luid[p]) for its occurrence positions p
@@ -353,16 +360,16 @@ static constexpr int kClaimMaxU = 4096;  // unique keys of a bucket (the dedup's
 // almost every key (mean probe length 0.48 at load 0.49,
 // profiles/r6_long_region.md); longer probes continue one load at a time.
 // KR = 1 (one key at a time) measured fastest: see launch_pull_claim_bk
-template <int CT, int KR>
+template <int CT, int KR, int TS = kClaimTS>
 __global__ __launch_bounds__(CT) void k_pull_claim_bk(
     DevTable t, const uint64_t* __restrict__ bkeys, const uint32_t* __restrict__ bstart,
     const uint32_t* __restrict__ unum, const uint32_t* __restrict__ ubase,
     int* __restrict__ slots32, float* __restrict__ out, float2* __restrict__ snap, InitParams ip,
     unsigned long long* size_ctr, int* err, const uint32_t* __restrict__ luid,
     float* __restrict__ occ, const uint32_t* __restrict__ pj, SelfSeg self) {
-  __shared__ uint32_t cl[kClaimTS];
+  __shared__ uint32_t cl[TS];
   __shared__ float sv[kClaimMaxU];
-  for (int i = threadIdx.x; i < kClaimTS; i += CT) cl[i] = 0xFFFFFFFFu;
+  for (int i = threadIdx.x; i < TS; i += CT) cl[i] = 0xFFFFFFFFu;
   __syncthreads();
   const int b = blockIdx.x;
   const uint32_t nu = unum[b], base = ubase[b];
@@ -403,7 +410,7 @@ __global__ __launch_bounds__(CT) void k_pull_claim_bk(
             wh = make_float2(__uint_as_float(x.x), __uint_as_float(x.y));
             break;
           }
-          if (k == kEmptyKey && lds_claim(cl, (uint32_t)ps.s)) {
+          if (k == kEmptyKey && lds_claim<TS>(cl, (uint32_t)ps.s)) {
             slot = (long long)ps.s;
             inserted = true;
             break;
@@ -1126,7 +1133,15 @@ void launch_pull_claim_bk(const DevTable& t, const uint64_t* bkeys, const uint32
   hipLaunchKernelGGL((k_pull_claim_bk<CT, KR>), dim3(P), dim3(CT), 0, st, t, bkeys, bstart, unum, \
                      ubase, slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr, err, luid, \
                      occ, pj, self)
-  if (ct == 256 && kr == 4) SS_CLAIM_LAUNCH(256, 4);
+  static const int cts = [] {
+    const char* e = std::getenv("SS_CLAIM_TS");
+    return e && std::atoi(e) == 4096 ? 4096 : kClaimTS;
+  }();
+  if (ct == 256 && kr == 1 && cts == 4096)
+    hipLaunchKernelGGL((k_pull_claim_bk<256, 1, 4096>), dim3(P), dim3(256), 0, st, t, bkeys, bstart,
+                       unum, ubase, slots32, out, reinterpret_cast<float2*>(snap), ip, size_ctr,
+                       err, luid, occ, pj, self);
+  else if (ct == 256 && kr == 4) SS_CLAIM_LAUNCH(256, 4);
   else if (ct == 256 && kr == 8) SS_CLAIM_LAUNCH(256, 8);
   else if (ct == 256) SS_CLAIM_LAUNCH(256, 1);
   else if (ct == 64) SS_CLAIM_LAUNCH(64, 1);

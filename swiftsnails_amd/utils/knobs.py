@@ -146,12 +146,17 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_CS": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "column-scan workgroup size"),
     "SS_BD_CT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "scatter workgroup size"),
     "SS_BD_RT": Knob("1024", "csrc/hip/bdedup.hip", "tuning", "reduce workgroup size"),
+    "SS_CLAIM_TS": Knob("8192", "csrc/hip/table.hip", "tuning",
+                        "claimed pull: LDS claim-set entries (8192, or 4096: 32 instead of "
+                        "48 KB of LDS per workgroup)"),
     "SS_CLAIM_KR": Knob("1", "csrc/hip/table.hip", "tuning",
                         "claimed pull: keys per thread whose first probe loads are in flight "
                         "together (1 / 4 / 8; 4 and 8 measured slower)"),
     "SS_BD_ROCC": Knob("4", "csrc/hip/bdedup.hip", "tuning",
                        "k_bd_reduce: occurrences (and fused-update rows) per thread in flight, "
                        "2 or 4"),
+    "SS_GEN_R": Knob("4", "csrc/hip/models.hip", "tuning",
+                     "synthetic CTR generator: sample groups per workgroup (1 / 2 / 4)"),
     "SS_LR_FWD_R": Knob("4", "csrc/hip/segreduce.hip", "tuning",
                         "packed LR forward (one-gather mode): sample groups per workgroup, "
                         "their gathers in flight together (1 / 2 / 4)"),
