@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void k_lr_fwd_occ(const uint32_t* __restrict__
     const long long s = sb + (long long)r * spb + ls;
     const bool active = ls < spb && s < B;
     const long long j = (sb + (long long)r * spb) * F + t;
-    p[r] = active ? pos_of[j] : kInvS;
+    p[r] = active ? (pos_of ? pos_of[j] : (uint32_t)j) : kInvS;  // null: occ in sample order
     x[r] = active ? (xval ? xval[j] : 1.f) : 0.f;
   }
 #pragma unroll
@@ -439,7 +439,7 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
     const int v = e ? std::atoi(e) : 4;
     return (v == 1 || v == 2) ? v : 4;
   }();
-  if (occ && ix.pos_of && per_sample && fr > 1 && fr * spb <= 256) {
+  if (occ && per_sample && fr > 1 && fr * spb <= 256) {
     const int g = fr * spb;
     if (fr == 4)
       hipLaunchKernelGGL(k_lr_fwd_occ<4>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
