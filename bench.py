@@ -131,23 +131,50 @@ def main(argv=None):
     # must pass the start-up litmus on every rank) -> RCCL (parallel/select.py)
     from swiftsnails_amd.parallel.select import build_engine
 
-    def make_engine(tr, ct, pt):
-        return PSEngine(table, tr, max_keys=a.batch * a.fields, dim=1, device=dev,
-                        count_transport=ct, pull_transport=pt,
-                        exchange=os.environ.get("SS_XCHG", "unique")
-                        if a.grad_mode == "segreduce" else "unique")
+    # N>1 exchange (SS_XCHG): unique (each source's unique keys; the worker
+    # merges its occurrences), records (every occurrence; the servers dedup
+    # and merge), or auto (default): both are built on the same table and
+    # timed on the live world after the warm-up, the faster kept — records
+    # do less kernel work per rank but ship twice the link bytes, so which
+    # wins depends on the links (models/base.py calibrate_exchange)
+    xchg = os.environ.get("SS_XCHG", "auto") if a.grad_mode == "segreduce" else "unique"
+    if xchg not in ("auto", "unique", "records"):
+        print(f"bench.py: SS_XCHG={xchg!r}: auto, unique or records", file=sys.stderr)
+        return 2
+
+    def make_engine_for(ex, streams_of=None):
+        def make(tr, ct, pt):
+            return PSEngine(table, tr, max_keys=a.batch * a.fields, dim=1, device=dev,
+                            count_transport=ct, pull_transport=pt, exchange=ex,
+                            streams_of=streams_of)
+        return make
 
     engine, (transport, ctrans, ptrans), plane = build_engine(
-        a.transport, rank, world, dev, store, make_engine,
+        a.transport, rank, world, dev, store,
+        make_engine_for("unique" if xchg == "auto" else xchg),
         log=lambda m: print(f"bench.py: {m}", file=sys.stderr))
     comms = plane.comms
     worker = SparseLRWorker(engine, data, rank=rank, world=world, grad_mode=a.grad_mode)
+    # the record-exchange candidate: only over the mailboxes (its own arenas)
+    alt = None
+    if xchg == "auto" and not engine.fast1 and plane.plane == "xgmi" and worker.bucketed \
+            and a.cal_steps > 0:
+        try:
+            e2, trs2, plane2 = build_engine("xgmi", rank, world, dev, store,
+                                            make_engine_for("records", engine),
+                                            prefix="ss_xgmi_rec")
+        except (RuntimeError, ValueError) as e:  # agreed collectively: every rank skips it
+            print(f"bench.py: record exchange unavailable ({e}); unique only", file=sys.stderr)
+        else:
+            alt = (e2, trs2, plane2, SparseLRWorker(e2, data, rank=rank, world=world,
+                                                    grad_mode=a.grad_mode))
 
     # a wedged collective ends the job (exit 3) instead of hanging the node
     from swiftsnails_amd.parallel.watchdog import FailureHandler, Watchdog
 
     failure = FailureHandler()
-    for t in {id(x): x for x in (transport, ctrans, ptrans) if x is not None}.values():
+    for t in {id(x): x for x in (transport, ctrans, ptrans) + (alt[1] if alt else ())
+              if x is not None}.values():
         if hasattr(t, "abort"):
             failure.add_hook(t.abort)
     wd = Watchdog(float(os.environ.get("SS_BENCH_ROUND_TIMEOUT", "300")), failure, name="bench")
@@ -164,10 +191,37 @@ def main(argv=None):
         fault.maybe(i)
         worker.step()
         wd.beat(i)
+    cal = {}
+    if alt is not None:
+        torch.cuda.synchronize()
+        e2, trs2, plane2, w2 = alt
+        for i in range(a.warmup):
+            w2.step()
+            wd.beat(i)
+        pick, cal_x = SparseLRWorker.calibrate_exchange(
+            {"unique": worker, "records": w2}, "unique", a.cal_steps, a.cal_windows)
+        cal["exchange"] = cal_x
+        # the loser's arenas go: every rank's rounds through them are done
+        # (synchronised + barrier in the calibration) before any rank frees
+        lose_w, lose_trs = (w2, trs2) if pick == "unique" else (worker, (transport, ctrans, ptrans))
+        if pick == "records":
+            engine, worker, plane = e2, w2, plane2
+            transport, ctrans, ptrans = trs2
+            comms = plane.comms
+        barrier()
+        lose_w.close()
+        for t in {id(x): x for x in lose_trs if x is not None}.values():
+            t.close()
+        del lose_w, lose_trs, alt, e2, w2, trs2
+        import gc
+
+        gc.collect()
+        torch.cuda.empty_cache()
+        barrier()
     # N>1 (SS_PULL_AHEAD=auto): time synchronous vs pulled-ahead rounds on
     # the live world and keep the faster (untimed; reported as "calibration")
-    cal = (worker.calibrate_pull_ahead(a.cal_steps, a.cal_windows)
-           if a.cal_steps > 0 else {})
+    if a.cal_steps > 0:
+        cal.update(worker.calibrate_pull_ahead(a.cal_steps, a.cal_windows))
     # ... and the server stream (SS_SERVER_STREAM=auto, ranks with a device of
     # their own): kept only if it costs <= 1 % on the live world
     cal_ss = (worker.calibrate_server_stream(a.cal_steps, a.cal_windows)

@@ -913,7 +913,7 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     }
 #pragma unroll
     for (int r = 0; r < OCC; ++r) {
-      g[r] = l[r] != kBdInvalid ? self.pick(gs, (long long)j[r])[j[r] / (uint32_t)F] : 0.f;
+      g[r] = l[r] != kBdInvalid ? self.grad(gs, j[r], (uint32_t)F) : 0.f;
       if (xval && l[r] != kBdInvalid) g[r] *= xval[j[r]];
     }
     // keys occurring once in the batch (usingle, from the dedup): a plain
@@ -1541,19 +1541,22 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
 // ---- record exchange, worker side (N>1 scalar rows; bd_set_record_layout)
 //
 // The rows of a step come back at the send-segment positions of its
-// occurrences, so the forward reads occ[pos_of[j]] from the rows mailbox (or
-// a cached copy, k_rec_copy); its per-sample gradient then goes out per
-// occurrence: grec[p] = gs[spj[p] / F] * x[spj[p]] at the same positions.
+// occurrences, so the forward reads occ[pos_of[j]] from the rows mailbox —
+// its own destination's rows from a cached buffer the server fill wrote
+// instead (SelfSeg) — and its per-sample gradient goes out per occurrence:
+// grec[p] = gs[spj[p] / F] * x[spj[p]] at the same positions, except for the
+// own destination, whose server merge reads gs through spj itself.
 // The servers merge them per distinct key with the update fused (server.hip):
 // no worker dedup, no worker merge.  The destinations' ranges
 // [d * gap, d * gap + ucount[d]) are walked as one flat list.
+// skip: a destination whose range is left out (-1: none)
 __device__ __forceinline__ void rec_ranges(const unsigned long long* __restrict__ ucount, int nd,
-                                           long long gap, long long* cs) {
+                                           long long gap, long long* cs, int skip = -1) {
   if (threadIdx.x == 0) {
     long long a = 0;
     for (int d = 0; d < nd; ++d) {
       cs[d] = a;
-      a += (long long)min(ucount[d], (unsigned long long)gap);
+      if (d != skip) a += (long long)min(ucount[d], (unsigned long long)gap);
     }
     cs[nd] = a;
   }
@@ -1573,7 +1576,8 @@ __global__ __launch_bounds__(256) void k_rec_grad(const unsigned long long* __re
                                                   const float* __restrict__ xval, int F,
                                                   float* __restrict__ grec,
                                                   float* __restrict__ lacc,
-                                                  float* __restrict__ lacc_out, int lacc_n) {
+                                                  float* __restrict__ lacc_out, int lacc_n,
+                                                  int skip) {
   __shared__ long long cs[kRecMaxDest + 1];
   // the step's loss accumulator (the forward's, stream-ordered before this
   // launch) moves to lacc_out and is left zero, as k_bd_reduce does
@@ -1582,7 +1586,9 @@ __global__ __launch_bounds__(256) void k_rec_grad(const unsigned long long* __re
       lacc_out[i] = lacc[i];
       lacc[i] = 0.f;
     }
-  rec_ranges(ucount, nd, gap, cs);
+  // skip: this rank's own destination, whose server merge reads the
+  // per-sample gradient through spj itself (SelfSeg::grad)
+  rec_ranges(ucount, nd, gap, cs, skip);
   const long long tot = cs[nd], stride = (long long)gridDim.x * 256 * 4;
   for (long long f0 = (long long)blockIdx.x * 1024 + threadIdx.x; f0 < tot; f0 += stride) {
     long long p[4];
@@ -1603,51 +1609,23 @@ __global__ __launch_bounds__(256) void k_rec_grad(const unsigned long long* __re
   }
 }
 
-// the rows of the step's occurrences out of the (uncached) rows mailbox into
-// a cached array with the same positions (SS_REC_OCC=copy)
-__global__ __launch_bounds__(256) void k_rec_copy(const unsigned long long* __restrict__ ucount,
-                                                  int nd, long long gap,
-                                                  const float* __restrict__ src,
-                                                  float* __restrict__ dst) {
-  __shared__ long long cs[kRecMaxDest + 1];
-  rec_ranges(ucount, nd, gap, cs);
-  const long long tot = cs[nd], stride = (long long)gridDim.x * 256 * 4;
-  for (long long f0 = (long long)blockIdx.x * 1024 + threadIdx.x; f0 < tot; f0 += stride) {
-    long long p[4];
-    float v[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const long long f = f0 + r * 256;
-      p[r] = f < tot ? rec_pos(cs, nd, gap, f) : -1;
-      v[r] = p[r] >= 0 ? src[p[r]] : 0.f;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (p[r] >= 0) dst[p[r]] = v[r];
-  }
-}
-
 static int rec_grid(long long cap, int nd) {
-  const long long work = (cap * nd + 1023) / 1024;  // the ranges' upper bound
+  const long long work = (cap * nd + 1023) / 1024;  // the ranges' upper bound (nd may be 0)
   return (int)std::max<long long>(1, std::min<long long>(work, 2048));
 }
 
 void launch_rec_grad(const unsigned long long* ucount, int nd, long long gap, const uint32_t* spj,
                      const float* gs, const float* xval, int F, float* grec, hipStream_t st,
-                     float* lacc, float* lacc_out, int lacc_n) {
+                     float* lacc, float* lacc_out, int lacc_n, int skip) {
   if (nd < 1 || nd > kRecMaxDest || gap < 1 || F < 1) throw_error("rec_grad: bad layout");
   if (lacc && (!lacc_out || lacc_n <= 0)) throw_error("rec_grad: loss hand-off needs its output");
-  hipLaunchKernelGGL(k_rec_grad, dim3(rec_grid(gap, nd)), dim3(256), 0, st, ucount, nd, gap, spj,
-                     gs, xval, F, grec, lacc, lacc_out, lacc_n);
+  if (skip >= nd) throw_error("rec_grad: skipped destination out of range");
+  // the grid covers the ranges walked: none at one rank with its own skipped
+  // (the launch then only hands the loss off)
+  const int grid = rec_grid(gap, skip >= 0 ? nd - 1 : nd);
+  hipLaunchKernelGGL(k_rec_grad, dim3(grid), dim3(256), 0, st, ucount, nd, gap, spj, gs, xval, F,
+                     grec, lacc, lacc_out, lacc_n, skip);
   check_launch("k_rec_grad");
-}
-
-void launch_rec_copy(const unsigned long long* ucount, int nd, long long gap, const float* src,
-                     float* dst, hipStream_t st) {
-  if (nd < 1 || nd > kRecMaxDest || gap < 1) throw_error("rec_copy: bad layout");
-  hipLaunchKernelGGL(k_rec_copy, dim3(rec_grid(gap, nd)), dim3(256), 0, st, ucount, nd, gap, src,
-                     dst);
-  check_launch("k_rec_copy");
 }
 
 void launch_bd_fill_occ(long long n, int nranks, const uint32_t* scratch, const uint32_t* luid,

@@ -236,19 +236,13 @@ PYBIND11_MODULE(_ss_hip, m) {
   m.def("bd_target_for", &bd_target_for, py::arg("nranks"), py::arg("records") = false);
   m.def("rec_grad", [](uintptr_t ucount, int nd, long long gap, uintptr_t spj, uintptr_t gs,
                        uintptr_t xval, int F, uintptr_t grec, uintptr_t st, uintptr_t acc,
-                       uintptr_t acc_out, int acc_n) {
+                       uintptr_t acc_out, int acc_n, int skip) {
     launch_rec_grad(P<const unsigned long long>(ucount), nd, gap, P<const uint32_t>(spj),
                     P<const float>(gs), P<const float>(xval), F, P<float>(grec), S(st),
-                    P<float>(acc), P<float>(acc_out), acc_n);
+                    P<float>(acc), P<float>(acc_out), acc_n, skip);
   }, py::arg("ucount"), py::arg("nd"), py::arg("gap"), py::arg("spj"), py::arg("gs"),
      py::arg("xval"), py::arg("F"), py::arg("grec"), py::arg("st"), py::arg("acc") = 0,
-     py::arg("acc_out") = 0, py::arg("acc_n") = 0);
-  m.def("rec_copy", [](uintptr_t ucount, int nd, long long gap, uintptr_t src, uintptr_t dst,
-                       uintptr_t st) {
-    launch_rec_copy(P<const unsigned long long>(ucount), nd, gap, P<const float>(src),
-                    P<float>(dst), S(st));
-  }, py::arg("ucount"), py::arg("nd"), py::arg("gap"), py::arg("src"), py::arg("dst"),
-     py::arg("st"));
+     py::arg("acc_out") = 0, py::arg("acc_n") = 0, py::arg("skip") = -1);
   m.def("bd_reduce", [](long long n, int nranks, uintptr_t scratch, uintptr_t pj, uintptr_t luid,
                         uintptr_t gs, uintptr_t xval, int F, uintptr_t ugrad, uintptr_t st,
                         int osi, uintptr_t usingle, std::optional<DevTable> t, uintptr_t slots,
@@ -358,13 +352,24 @@ PYBIND11_MODULE(_ss_hip, m) {
   // ix = (pos_of, luid, bkt, ubase) pointers of a bucketed dedup, or () with inv
   m.def("lr_fwd_g", [](uintptr_t inv, uintptr_t xval, uintptr_t labels, int B, int F,
                        uintptr_t uvals, uintptr_t g, int per_sample, uintptr_t loss,
-                       uintptr_t pred, uintptr_t st, std::vector<uintptr_t> ix, uintptr_t occ) {
+                       uintptr_t pred, uintptr_t st, std::vector<uintptr_t> ix, uintptr_t occ,
+                       uintptr_t own, long long own_lo, long long own_hi) {
+    // own: the cached buffer holding occ's positions [own_lo, own_hi) (the
+    // record exchange's own destination), indexed from own_lo
+    SelfSeg os{};
+    if (own) {
+      if (own_hi <= own_lo || own_lo < 0) throw std::invalid_argument("lr_fwd_g: own range");
+      os.ptr = reinterpret_cast<char*>(own) - own_lo * (long long)sizeof(float);
+      os.lo = own_lo;
+      os.hi = own_hi;
+    }
     launch_lr_fwd_g(P<const uint32_t>(inv), make_bdindex(ix), P<const float>(xval),
                     P<const float>(labels), B, F, P<const float>(uvals), P<float>(g), per_sample,
-                    P<float>(loss), P<float>(pred), S(st), P<const float>(occ));
+                    P<float>(loss), P<float>(pred), S(st), P<const float>(occ), os);
   }, py::arg("inv"), py::arg("xval"), py::arg("labels"), py::arg("B"), py::arg("F"),
      py::arg("uvals"), py::arg("g"), py::arg("per_sample"), py::arg("loss"), py::arg("pred"),
-     py::arg("st"), py::arg("ix") = std::vector<uintptr_t>{}, py::arg("occ") = 0);
+     py::arg("st"), py::arg("ix") = std::vector<uintptr_t>{}, py::arg("occ") = 0,
+     py::arg("own") = 0, py::arg("own_lo") = 0, py::arg("own_hi") = 0);
   m.def("bd_fill_occ", [](long long n, int nranks, uintptr_t scratch, uintptr_t luid,
                           uintptr_t uvals, uintptr_t occ, int osi, uintptr_t st, int ndest,
                           uintptr_t pj) {

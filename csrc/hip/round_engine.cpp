@@ -75,6 +75,7 @@ class RoundEngine {
     vals_.resize(depth);
     grads_.resize(depth);
     self_keys_.assign(depth, 0);
+    own_vals_.assign(depth, 0);
     srv_done_.assign(depth, 0);
     srv_s32_.assign(depth, 0);
     srv_claim_.assign(depth, 0);
@@ -239,9 +240,15 @@ class RoundEngine {
                  uintptr_t err, int G, uintptr_t rkeys, uintptr_t rbase, uintptr_t rnum,
                  uintptr_t srv_err, uintptr_t svals, uintptr_t rvals, bool snap, uintptr_t sent,
                  std::vector<uintptr_t> metrics, bool custom_pull, bool claim,
-                 bool insert, uintptr_t srv_stream) {
+                 bool insert, uintptr_t srv_stream, uintptr_t own_vals) {
     check_xgmi();
     pull_waits(slot, tag, stream, wait_route, prev);
+    // own_vals (record exchange): the rows of this rank's own records go to
+    // this cached buffer (cap rows) instead of its uncached vals arena — the
+    // forward gathers them per occurrence (SparseLRWorker, lr_fwd_g own=)
+    if (own_vals && !self_bypass())
+      throw std::invalid_argument("pull_xgmi: own rows need the own-segment bypass (SS_XGMI_SELF)");
+    own_vals_[slot] = own_vals;
     // the server half (keys in, merge, lookup, response rows out) on the
     // server stream when the rank has one: a slow compute on the worker's
     // stream no longer holds up the rows every peer waits for.  It follows
@@ -281,8 +288,7 @@ class RoundEngine {
                              reinterpret_cast<int*>(S.slots), fused ? nullptr : Pt<float>(svals),
                              S.snap, ip, Pt<unsigned long long>(size_ctr), Pt<int>(err), St(ss),
                              fused ? S.luid : nullptr, fused ? Pt<float>(rvals) : nullptr,
-                             fused ? S.pj : nullptr,
-                             fused ? self_seg(ar_[slot][1]->base() + vals_[slot].data) : SelfSeg{});
+                             fused ? S.pj : nullptr, fused ? vals_self(slot) : SelfSeg{});
         if (fused) {
           fill_and_put(slot, ss, 0, rvals, true);
           rows_wait(slot, stream, sent, metrics);
@@ -340,7 +346,13 @@ class RoundEngine {
   void push_xgmi(int slot, int tag, uintptr_t stream, uintptr_t grads, uintptr_t ucount,
                  bool table, bool update, const DevTable& t, const OptParams& op, uintptr_t rgrads,
                  bool scalar_fused, bool snap, uintptr_t merged, bool release,
-                 uintptr_t srv_stream, uintptr_t gstage) {
+                 uintptr_t srv_stream, uintptr_t gstage, std::vector<uintptr_t> own_grad) {
+    // own_grad (record exchange): (per-sample gradient, spj, F, feature
+    // values or 0) of this rank's own records, which k_rec_grad did not write
+    // out — the server merge reads gs[spj[p] / F] * x for its own positions
+    if (!own_grad.empty() && (own_grad.size() != 4 || !own_grad[0] || !own_grad[1] ||
+                              own_grad[2] < 1 || !self_bypass() || dim_ != 1))
+      throw std::invalid_argument("push_xgmi: own_grad = (gs, spj, F, xval), scalar rows, bypass on");
     check_xgmi();
     std::vector<std::vector<long long>> parts;
     parts.push_back(part(grads, ucount, 0, 4ll * dim_, grads_[slot], cap_, self_bypass()));
@@ -358,7 +370,15 @@ class RoundEngine {
     if (table) {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
-      const SelfSeg sg = self_seg(grads);  // this rank's own gradient rows, in place
+      SelfSeg sg = self_seg(grads);  // this rank's own gradient rows, in place
+      if (!own_grad.empty()) {
+        sg.ptr = reinterpret_cast<char*>(own_grad[0]);
+        sg.ind = Pt<const uint32_t>(own_grad[1]);
+        sg.F = (uint32_t)own_grad[2];
+        sg.xv = Pt<const float>(own_grad[3]);
+        if (gstage || !(update && scalar_fused))
+          throw std::invalid_argument("push_xgmi: own_grad needs the fused scalar merge, no staging");
+      }
       // the peers' gradient rows streamed out of the uncached mailbox into a
       // cached buffer first: the merge gathers them per received position
       if (gstage && nranks_ > 1) {
@@ -431,6 +451,14 @@ class RoundEngine {
                      S.pj, S.luid, S.bkeys, S.ubase, S.unum, S.ucount, Pt<uint32_t>(srv_err),
                      St(stream), roff, self_seg(self_keys_[slot]));
   }
+  // where the server's response rows for this rank's own keys go: its vals
+  // arena (same row index), or the record exchange's cached own-row buffer
+  SelfSeg vals_self(int slot) const {
+    if (!own_vals_[slot]) return self_seg(ar_[slot][1]->base() + vals_[slot].data);
+    SelfSeg s = self_seg(own_vals_[slot]);
+    s.ptr -= (long long)rank_ * cap_ * 4ll * dim_;  // row index rank*cap + i -> own_vals[i]
+    return s;
+  }
   // this rank's own segment of a (cap-row) exchange, read in place from `ptr`
   SelfSeg self_seg(uintptr_t ptr) const {
     SelfSeg s;
@@ -459,7 +487,7 @@ class RoundEngine {
     // the rows for this rank's own keys go straight into its vals arena (the
     // worker reads them there), the peers' into the response buffer the put
     // sends
-    const SelfSeg sv = self_seg(ar_[slot][1]->base() + vals_[slot].data);
+    const SelfSeg sv = vals_self(slot);
     if (svals) {
       SrvSlot& S = srv_[slot];
       const int Ps = Pd_ * sub_;
@@ -495,6 +523,7 @@ class RoundEngine {
   int nkp_ = 3;  // parts of the keys channel
   std::vector<XReg> vals_, grads_;
   std::vector<uintptr_t> self_keys_;  // per slot: this rank's send layout of its keys
+  std::vector<uintptr_t> own_vals_;   // per slot: own records' rows (0: the vals arena)
   std::vector<char> srv_done_;        // per slot: the route ran keys_in (srv_ahead)
   std::vector<char> srv_s32_;         // per slot: the server pull stored 4-byte slots
   std::vector<char> srv_claim_;       // per slot: ... and claimed its inserts (no CAS)

@@ -271,7 +271,8 @@ __global__ __launch_bounds__(256) void k_lr_fwd_occ(const uint32_t* __restrict__
                                                     float* __restrict__ gs,
                                                     float* __restrict__ loss_sum,
                                                     float* __restrict__ pred,
-                                                    const float* __restrict__ occ) {
+                                                    const float* __restrict__ occ,
+                                                    SelfSeg oself) {
   __shared__ float sval[R * 256];
   __shared__ float sdot[256];
   __shared__ float sloss[4];
@@ -289,7 +290,8 @@ __global__ __launch_bounds__(256) void k_lr_fwd_occ(const uint32_t* __restrict__
     x[r] = active ? (xval ? xval[j] : 1.f) : 0.f;
   }
 #pragma unroll
-  for (int r = 0; r < R; ++r) sval[r * 256 + t] = p[r] == kInvS ? 0.f : occ[p[r]] * x[r];
+  for (int r = 0; r < R; ++r)
+    sval[r * 256 + t] = p[r] == kInvS ? 0.f : oself.pick(occ, (long long)p[r])[p[r]] * x[r];
   __syncthreads();
   // R * spb sample sums, tps threads per sample (as packed_sample_sums)
   const int ns = R * spb;
@@ -408,7 +410,7 @@ void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
 void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
                      const float* labels, int B, int F, const float* uvals, float* gocc,
                      int per_sample, float* loss_sum, float* pred, hipStream_t st,
-                     const float* occ) {
+                     const float* occ, SelfSeg occ_self) {
   if (!occ && !inv && !(ix.pos_of && ix.luid && ix.bkt && ix.ubase))
     throw_error("lr_fwd_g: need inv, a complete BdIndex, or occ (bucket order with pos_of, "
                 "else sample order)");
@@ -424,7 +426,10 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
     return std::string(e) == "packed" ? 1 : (std::string(e) == "group" ? 2 : 0);
   }();
   const bool packed = force == 1 || (force == 0 && 4 * F < 3 * group_lanes(F));
-  if (F <= kGroupMaxF && !packed) {
+  // occ_self (positions read from a second buffer): the one-gather kernel only
+  if (occ_self.ptr && !(occ && per_sample))
+    throw_error("lr_fwd_g: an own-row buffer needs the one-gather per-sample form");
+  if (F <= kGroupMaxF && !packed && !occ_self.ptr) {
     const int L = group_lanes(F), spb = 256 / L;
     hipLaunchKernelGGL(k_lr_fwd_g, dim3((B + spb - 1) / spb), dim3(256), 0, st, inv, ix, xval,
                        labels, B, F, L, uvals, gocc, per_sample, loss_sum, pred, occ);
@@ -439,14 +444,18 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
     const int v = e ? std::atoi(e) : 4;
     return (v == 1 || v == 2) ? v : 4;
   }();
-  if (occ && per_sample && fr > 1 && fr * spb <= 256) {
-    const int g = fr * spb;
-    if (fr == 4)
+  if (occ && per_sample && ((fr > 1 && fr * spb <= 256) || occ_self.ptr)) {
+    const int r = fr * spb <= 256 ? fr : 1;
+    const int g = r * spb;
+    if (r == 4)
       hipLaunchKernelGGL(k_lr_fwd_occ<4>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
-                         labels, B, F, gocc, loss_sum, pred, occ);
-    else
+                         labels, B, F, gocc, loss_sum, pred, occ, occ_self);
+    else if (r == 2)
       hipLaunchKernelGGL(k_lr_fwd_occ<2>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
-                         labels, B, F, gocc, loss_sum, pred, occ);
+                         labels, B, F, gocc, loss_sum, pred, occ, occ_self);
+    else
+      hipLaunchKernelGGL(k_lr_fwd_occ<1>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
+                         labels, B, F, gocc, loss_sum, pred, occ, occ_self);
     check_launch("k_lr_fwd_occ");
     return;
   }

@@ -194,9 +194,30 @@ __device__ __forceinline__ long long seg_pos(const SegList& sl, long long g, int
 struct SelfSeg {
   char* ptr = nullptr;
   long long lo = 0, hi = 0;
+  // record exchange, own gradients (k_bd_reduce at the server): the rank's
+  // own records were never written out per occurrence — position p's
+  // gradient is ptr[ind[p] / F] (the worker's per-sample gradient) times
+  // xv[ind[p]] (file feature values; null: binary features), ind = the
+  // worker's spj (send position -> occurrence)
+  const uint32_t* ind = nullptr;
+  const float* xv = nullptr;
+  uint32_t F = 1;
   template <typename T>
   __host__ __device__ __forceinline__ T* pick(T* arena, long long pos) const {
     return (ptr && pos >= lo && pos < hi) ? reinterpret_cast<T*>(ptr) : arena;
+  }
+  __device__ __forceinline__ bool mine(long long pos) const {
+    return ptr && pos >= lo && pos < hi;
+  }
+  // the scalar gradient at received position j (arena rows are per position;
+  // the F of the arena's layout is `af`)
+  __device__ __forceinline__ float grad(const float* arena, uint32_t j, uint32_t af) const {
+    if (ind && mine(j)) {
+      const uint32_t q = ind[j];
+      const float g = reinterpret_cast<const float*>(ptr)[q / F];
+      return xv ? g * xv[q] : g;
+    }
+    return pick(arena, (long long)j)[j / af];
   }
 };
 

@@ -162,7 +162,7 @@ void launch_sr_reduce(const void* plan, const float* gocc, const void* items,
                       int nranks, long long ucap, float* ugrad, hipStream_t st);
 void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval, const float* labels, int B, int F, const float* uvals,
                      float* g, int per_sample, float* loss_sum, float* pred, hipStream_t st,
-                     const float* occ = nullptr);
+                     const float* occ = nullptr, SelfSeg occ_self = SelfSeg{});
 
 // --- bdedup.hip (bucketed dedup: partition by hash, LDS dedup per bucket)
 // ndest: destinations that receive keys (effective server count, <= nranks;
@@ -186,9 +186,8 @@ int bd_target_dist();
 int bd_target_for(int nranks, bool records);
 void launch_rec_grad(const unsigned long long* ucount, int nd, long long gap, const uint32_t* spj,
                      const float* gs, const float* xval, int F, float* grec, hipStream_t st,
-                     float* lacc = nullptr, float* lacc_out = nullptr, int lacc_n = 0);
-void launch_rec_copy(const unsigned long long* ucount, int nd, long long gap, const float* src,
-                     float* dst, hipStream_t st);
+                     float* lacc = nullptr, float* lacc_out = nullptr, int lacc_n = 0,
+                     int skip = -1);
 void launch_bd_reduce(long long n, int nranks, const uint32_t* scratch, const uint32_t* pj,
                       const uint32_t* luid, const float* gs, const float* xval, int F,
                       float* ugrad, hipStream_t st, int osi = 0,

@@ -263,7 +263,10 @@ def build_worker(cfg: Config):
         cap = int(cfg.get("table_capacity", 0) or data.num_features / nserv / load + 1024)
         # sparse LR may ship every occurrence at N>1 (exchange: records /
         # SS_XCHG=records; PSEngine), else each source's unique keys
+        # (SS_XCHG=auto, bench.py's start-up measurement of both, runs the
+        # unique exchange here)
         xch = str(cfg.get("exchange", os.environ.get("SS_XCHG", "unique")))
+        xch = "unique" if xch == "auto" else xch
         ctx = PSContext(cfg, dim, opt, init, data.batch_size * data.num_fields, cap,
                         exchange=xch if model == "sparse_lr" else "unique")
         cls = SparseLRWorker if model == "sparse_lr" else FMWorker

@@ -436,6 +436,65 @@ class PipelinedWorker:
         return {"server_stream": keep, "off_ms": ms(times[False]), "on_ms": ms(times[True]),
                 "windows": windows, "steps_per_window": steps, "margin": margin}
 
+    @staticmethod
+    def calibrate_exchange(cands: dict, default: str, steps: int = 10, windows: int = 2,
+                           margin: float = 0.03) -> tuple:
+        """Time workers that train the same model through different N>1
+        exchanges (``cands``: name -> worker, every worker's engine on the
+        same table, e.g. ``unique`` and ``records``) on the live world, in
+        ``windows`` alternating windows of ``steps`` timed steps (max over
+        ranks), and pick ``default`` unless another wins by ``margin`` in
+        EVERY window.  Which one is faster is a property of the machine: the
+        record exchange does less kernel work per rank (no worker dedup or
+        merge) but ships every occurrence, twice the unique exchange's link
+        bytes — on one GPU (no links) it wins at 1-2 ranks and loses at 4-8
+        (docs/PERFORMANCE.md), over real xGMI links only a measurement can
+        tell.  Between windows the device is synchronised and the ranks
+        barrier: the engines share the table, so one worker's rounds must be
+        applied before the other pulls.  Workers run synchronous rounds here.
+        A collective.  Returns (choice, report)."""
+        names = list(cands)
+        if default not in cands:
+            raise ValueError("calibrate_exchange: the default must be a candidate")
+        steps, windows = max(1, int(steps)), max(1, int(windows))
+        times = {n: [] for n in names}
+
+        def quiesce(eng):
+            torch.cuda.synchronize(eng.device)
+            eng.barrier()
+
+        for _ in range(windows):
+            for n in names:
+                w = cands[n]
+                eng = w.engine
+                if getattr(eng, "pull_ahead", False) or w._pulled or w._graphs is not None:
+                    raise RuntimeError("calibrate_exchange: synchronous eager rounds only")
+                quiesce(eng)
+                for _ in range(2):  # settle
+                    w.step()
+                quiesce(eng)
+                t0 = time.perf_counter()
+                for _ in range(steps):
+                    w.step()
+                torch.cuda.synchronize(eng.device)
+                el = time.perf_counter() - t0
+                eng.barrier()
+                times[n].append(eng.max_over_ranks(el) / steps)
+        best = default
+        for n in names:
+            if n != default and all(t <= (1.0 - margin) * d
+                                    for t, d in zip(times[n], times[default])):
+                if best == default or sum(times[n]) < sum(times[best]):
+                    best = n
+        pick = os.environ.get("SS_CAL_XCHG", "")  # debug: force the outcome
+        if pick in cands:
+            best = pick
+        quiesce(cands[best].engine)
+        ms = lambda xs: [round(1e3 * x, 4) for x in xs]  # noqa: E731
+        return best, {"exchange": best, "default": default,
+                      **{f"{n}_ms": ms(times[n]) for n in names},
+                      "windows": windows, "steps_per_window": steps, "margin": margin}
+
     def rounds_done(self) -> int:
         """Rounds whose pushes have been enqueued on the device.  Eagerly
         that is ``step_idx``; with hipGraphs a replay runs ``per`` steps on

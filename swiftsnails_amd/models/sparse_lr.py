@@ -128,10 +128,14 @@ class SparseLRWorker(PipelinedWorker):
             raise ValueError("the record exchange needs the bucketed segreduce merge "
                              "(SS_DEDUP=bucket, grad_mode segreduce)")
         # N>1 record exchange (PSEngine exchange="records"): the forward reads
-        # the rows mailbox in place, or a cached copy of it (SS_REC_OCC=copy)
-        self.rocc = (torch.empty(engine.world * engine.max_keys, dtype=torch.float32, device=dev)
-                     if self.bucketed and getattr(engine, "records", False) and
-                     os.environ.get("SS_REC_OCC", "arena") == "copy" else None)
+        # the rows mailbox in place, its own records' rows from the cached
+        # buffer its server filled (Round.own_vals), and the server merge reads
+        # those records' gradients from the per-sample gradient through spj —
+        # so that gradient is kept per ring slot (a server-stream merge of
+        # round i may still read it while round i+1 computes)
+        self.gring = ([torch.empty(B, dtype=torch.float32, device=dev)
+                       for _ in range(engine.depth)]
+                      if self.bucketed and getattr(engine, "own_vals", None) is not None else None)
 
     def _zero_acc(self) -> None:
         if not self.bucketed:
@@ -171,18 +175,22 @@ class SparseLRWorker(PipelinedWorker):
             # the gradients go out the same way — no worker merge; the
             # servers merge per distinct key with the AdaGrad update fused
             o, eng = dd.owner, self.engine
-            occ = rnd.uvals
-            if self.rocc is not None:  # SS_REC_OCC=copy: out of the mailbox first
-                h.rec_copy(dd.ucount.data_ptr(), eng.world, o.ucap, rnd.uvals.data_ptr(),
-                           self.rocc.data_ptr(), st)
-                occ = self.rocc
+            own = rnd.own_vals is not None and self.gring is not None
+            gs = self.gring[slot] if own else self.gocc
+            lo = eng.rank * o.ucap
             h.lr_fwd_g(0, xp, self.labels[slot].data_ptr(), d.batch_size, d.num_fields,
-                       rnd.uvals.data_ptr(), self.gocc.data_ptr(), 1, self._acc.data_ptr(),
-                       0, st, o.index_ptrs(dd.n), occ=occ.data_ptr())
+                       rnd.uvals.data_ptr(), gs.data_ptr(), 1, self._acc.data_ptr(),
+                       0, st, o.index_ptrs(dd.n), occ=rnd.uvals.data_ptr(),
+                       own=rnd.own_vals.data_ptr() if own else 0, own_lo=lo if own else 0,
+                       own_hi=lo + o.ucap if own else 0)
+            # the peers' records' gradients out per occurrence (own: skipped,
+            # the push hands the server merge (gs, spj, F, x) instead)
             h.rec_grad(dd.ucount.data_ptr(), eng.world, o.ucap, o.spj.data_ptr(),
-                       self.gocc.data_ptr(), xp, d.num_fields, rnd.ugrad.data_ptr(), st,
+                       gs.data_ptr(), xp, d.num_fields, rnd.ugrad.data_ptr(), st,
                        acc=self._acc.data_ptr(), acc_out=self.loss_sum.data_ptr(),
-                       acc_n=self._acc.numel())
+                       acc_n=self._acc.numel(), skip=eng.rank if own else -1)
+            if own:
+                rnd.own_grad = (gs.data_ptr(), o.spj.data_ptr(), d.num_fields, xp)
         elif self.bucketed:
             o = dd.owner
             if not rnd.occ_filled:

@@ -80,6 +80,11 @@ class Round:
     deferred: bool = False                # world-1 claimed pull: new keys' slots not written yet
     occ_filled: bool = False              # world-1 claimed pull also filled claim_occ
     server: Optional[object] = None       # CPU N>1: (unique keys, inverse) of the server merge
+    # record exchange: this rank's own records' rows (cached, cap rows; the
+    # rest stay in the vals arena) and, set by the model before the push,
+    # (gs, spj, F, xval) pointers its server merge reads their gradients from
+    own_vals: Optional[torch.Tensor] = None
+    own_grad: Optional[tuple] = None
 
     @property
     def inv(self) -> torch.Tensor:
@@ -120,14 +125,21 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                       merge, the servers dedup and merge what they receive;
                       ``Round.uvals`` / ``ugrad`` are then per occurrence at
                       its send-segment position).  Records halve the
-                      per-rank kernel work at N <= 4 but double the link
-                      bytes (docs/PERFORMANCE.md): not the default."""
+                      per-rank kernel work at N <= 2 but double the link
+                      bytes (docs/PERFORMANCE.md): not the default.
+    streams_of      : another engine of this rank whose route and server
+                      streams this one reuses (two candidate engines of one
+                      job that never run at the same time — bench.py's
+                      exchange calibration: a process gets GPU_MAX_HW_QUEUES
+                      = 4 hardware queues, and a fifth stream shares one with
+                      a busy stream, serialising what should overlap:
+                      records at one rank 0.98 vs 0.80 ms/step)"""
 
     def __init__(self, table, transport: Optional[Transport], max_keys: int, dim: int,
                  frag_num: int = 0, server_ranks: Optional[Sequence[int]] = None, device=None,
                  count_transport: Optional[Transport] = None, depth: Optional[int] = None,
                  pull_transport: Optional[Transport] = None, zero_grad: bool = True,
-                 exchange: str = "unique"):
+                 exchange: str = "unique", streams_of: Optional["PSEngine"] = None):
         self.t = transport or LoopbackTransport()
         self.ct = count_transport or self.t
         self.pt = pull_transport or self.ct
@@ -201,8 +213,10 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self.capture_tag: Optional[int] = None
         self._dix = (self.device.index or 0) if self.gpu else -1
         self.native = None
+        self._streams_of = streams_of
         if self.gpu:
-            self.route_stream = self._make_route_stream(dev)
+            self.route_stream = (streams_of.route_stream if streams_of is not None
+                                 else self._make_route_stream(dev))
             # + one slot past the ring: the N>1 read-only lookup's round
             # (PSEngine.lookup) never touches a ring slot the pipeline holds
             self.native = _hip().RoundEngine(self.depth + 1, self._dix)
@@ -253,6 +267,7 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             self.rkeys = torch.empty(N * cap, dtype=torch.int64)
             self.rvals = torch.zeros((N * cap, d), dtype=torch.float32)
             self.rgrads = torch.empty((N * cap, d), dtype=torch.float32)
+        self._streams_of = None  # the streams are taken; keep no reference to that engine
         # pull-ahead (SURVEY X3 bounded staleness): rounds i+1 .. i+L are
         # pulled on the pull stream while round i computes, L = SS_STALENESS
         # (default 1; at most depth - 2: rounds i .. i+L pulled or pulling and
@@ -497,6 +512,7 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
             self._deferred_slot = slot
         svals = self.svals.data_ptr() if S is not None else 0
         ss = self._srv_stream(custom)
+        ov = self.own_vals[slot] if getattr(self, "own_vals", None) is not None else None
         self.native.pull_xgmi(slot, self._tag, st, False, -1, ahead and not custom, S is not None,
                               tab.dt if S else self._nodt, tab._init_native if S else self._noip,
                               tab.size_ctr.data_ptr() if S else 0, tab.err.data_ptr() if S else 0,
@@ -504,13 +520,14 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                               self.rmeta[slot][0].data_ptr(), self.rmeta[slot][1].data_ptr(),
                               self.srv_err.data_ptr() if S else 0, svals,
                               self.rvals.data_ptr(), bool(S and S.snap_valid),
-                              dd.ucount.data_ptr(), m, custom, claim, True, ss)
+                              dd.ucount.data_ptr(), m, custom, claim, True, ss,
+                              ov.data_ptr() if ov is not None else 0)
         if custom:
             tab.finish_pull(S.slots, self.svals, n=S.ucount)
             self.native.pull_xgmi_finish(slot, self._tag, st, ahead, svals, self.rvals.data_ptr(),
                                          dd.ucount.data_ptr(), m)
         self.metrics.add(occurrences=dd.n)
-        return Round(dd, self.uvals[slot], slot, ready=ahead, tag=self._tag)
+        return Round(dd, self.uvals[slot], slot, ready=ahead, tag=self._tag, own_vals=ov)
 
     def enable_pull_ahead(self, on: bool = True, pull_stream: bool = False,
                           force: bool = False) -> bool:
@@ -657,7 +674,8 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
                                   self.sgrad.data_ptr() if merged_only else 0, not merged_only,
                                   ss, self.gstage.data_ptr()
                                   if S is not None and getattr(self, "gstage", None) is not None
-                                  else 0)
+                                  else 0, list(rnd.own_grad) if rnd.own_grad and S is not None
+                                  else [])
             if merged_only:
                 self._apply_merged(slot)
                 self._release(slot)

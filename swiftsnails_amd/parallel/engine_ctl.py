@@ -162,7 +162,7 @@ class EngineControl:
                                   self.rmeta[q][1].data_ptr(),
                                   self.srv_err.data_ptr() if S else 0,
                                   self.svals.data_ptr() if S else 0, self.rvals.data_ptr(),
-                                  False, r.ucount.data_ptr(), [], False, False, False, 0)
+                                  False, r.ucount.data_ptr(), [], False, False, False, 0, 0)
             if m:
                 h.gather_rows(self.uvals[q].data_ptr(), r.inv.data_ptr(), m, self.dim,
                               out[i * cap:i * cap + m].data_ptr(), st)

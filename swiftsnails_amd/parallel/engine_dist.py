@@ -136,8 +136,12 @@ class DeviceSetup:
         ss_env = os.environ.get("SS_SERVER_STREAM", "auto")
         if self.table is not None and self.xg is not None and \
                 (ss_env == "1" or (ss_env == "auto" and not self.shared_device)):
+            other = getattr(self, "_streams_of", None)
             lo_prio, hi_prio = torch.cuda.Stream.priority_range()
-            self.server_stream = torch.cuda.Stream(device=dev, priority=min(lo_prio, hi_prio))
+            self.server_stream = (
+                (getattr(other, "server_stream", None) or getattr(other, "_server_stream_off", None))
+                if other is not None else None) or \
+                torch.cuda.Stream(device=dev, priority=min(lo_prio, hi_prio))
         self.srv = None
         self.srv_ahead = os.environ.get("SS_SRV_AHEAD", "1") != "0"
         self._route_srv = None  # how the last route ran the keys-in (srv_ahead)
@@ -156,6 +160,19 @@ class DeviceSetup:
             snap_ok = bool(getattr(self.table, "snapshot_ok", False))
             self.srv = [_ServerSlot(rows, self.Ps, dev, snap_ok and q < self.depth)
                         for q in range(NS)]
+        # record exchange: the rows of this rank's own records are written by
+        # its own server into a cached buffer per ring slot (not the uncached
+        # vals arena, which only peers need), and their gradients are read by
+        # the server merge straight from the worker's per-sample gradient
+        # through spj — never written out per occurrence (SS_REC_OCC=arena:
+        # both through the arena, as the peers' records)
+        self.own_vals = None
+        if (self.records and self.table is not None and
+                self.server_ranks == list(range(N)) and
+                os.environ.get("SS_REC_OCC", "own") == "own" and
+                os.environ.get("SS_XGMI_SELF", "1") != "0"):
+            self.own_vals = [torch.empty((cap, d), dtype=torch.float32, device=dev)
+                             for _ in range(self.depth)]
         if self.xg:
             D = NS
             self.native.set_xgmi([[self.xg.arena_of(c, q) for c in ("keys", "vals", "grads")]

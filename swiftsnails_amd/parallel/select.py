@@ -79,11 +79,12 @@ def _plane_of(t) -> str:
     return type(t).__name__
 
 
-def make_transports(kind: str, rank: int, world: int, device, store):
+def make_transports(kind: str, rank: int, world: int, device, store, prefix: str = "ss_xgmi"):
     """(data transport, count transport, pull transport, native comms) for
     ``kind`` in auto | xgmi | rccl | gloo.  World 1: loopback, or with
     SS_ENGINE_GENERAL=xgmi|rccl a size-1 mailbox arena / communicator (the
-    N>1 engine path on one GPU)."""
+    N>1 engine path on one GPU).  ``prefix``: the mailboxes' store keys (a
+    second engine of the same job needs its own)."""
     from .transport import (LoopbackTransport, RcclTransport, TorchDistTransport,
                             rccl_comms_mode)
     from .xgmi import XgmiTransport
@@ -101,7 +102,8 @@ def make_transports(kind: str, rank: int, world: int, device, store):
     if kind in ("auto", "xgmi"):
         # the mailboxes are laid out, mapped and litmus-tested when the
         # engine is built (PSEngine -> XgmiTransport.setup)
-        return XgmiTransport(rank, world, dev, store, aux=TorchDistTransport()), None, None, 0
+        return (XgmiTransport(rank, world, dev, store, aux=TorchDistTransport(), prefix=prefix),
+                None, None, 0)
     if kind != "rccl":
         raise ValueError(f"transport {kind!r}: auto, xgmi, rccl or gloo")
     if rccl_comms_mode() == 1:
@@ -123,7 +125,8 @@ def _rccl_fallback(rank: int, world: int, device, store):
 
 
 def build_engine(kind: str, rank: int, world: int, device, store,
-                 make_engine: Callable, log: Optional[Callable[[str], None]] = None):
+                 make_engine: Callable, log: Optional[Callable[[str], None]] = None,
+                 prefix: str = "ss_xgmi"):
     """Build the round engine on the selected data plane, falling back from
     the xGMI mailboxes to RCCL when ``kind`` is auto.  ``make_engine(tr, ct,
     pt)`` builds a PSEngine (its construction lays out and litmus-tests the
@@ -131,7 +134,7 @@ def build_engine(kind: str, rank: int, world: int, device, store,
     the same branch (the litmus verdict is agreed collectively)."""
     from .xgmi import XgmiTransport
 
-    tr, ct, pt, comms = make_transports(kind, rank, world, device, store)
+    tr, ct, pt, comms = make_transports(kind, rank, world, device, store, prefix)
     fell, reason = False, ""
     litmus = []
     try:

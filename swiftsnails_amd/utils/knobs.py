@@ -88,13 +88,19 @@ KNOBS: dict[str, Knob] = {
     "SS_SRV_FILL_FUSED": Knob("1", "csrc/hip/round_engine.cpp", "tuning",
                               "N>1 servers, claimed scalar pulls: the response fill (rows per "
                               "received position) fused into the pull (0: separate kernel)"),
-    "SS_XCHG": Knob("unique", "bench.py, framework/gpu.py", "tuning",
+    "SS_XCHG": Knob("auto", "bench.py, framework/gpu.py", "tuning",
                     "sparse LR N>1 xGMI rounds: unique = each source's unique keys, merged "
                     "on the worker first; records = every occurrence shipped, the servers "
-                    "dedup and merge (less kernel work at N <= 4, twice the link bytes)"),
-    "SS_REC_OCC": Knob("arena", "models/sparse_lr.py", "tuning",
-                       "record exchange: the LR forward reads the rows mailbox in place "
-                       "(arena) or a cached copy of it (copy)"),
+                    "dedup and merge (less kernel work per rank at N <= 2, twice the link "
+                    "bytes); auto (bench.py) = both timed on the live world after the "
+                    "warm-up, the faster kept (the launcher runs unique)"),
+    "SS_CAL_XCHG": Knob("", "models/base.py", "debug",
+                        "debug: force calibrate_exchange's outcome (unique / records)"),
+    "SS_REC_OCC": Knob("own", "parallel/engine_dist.py", "tuning",
+                       "record exchange: own = this rank's own records' rows go to a cached "
+                       "buffer and their gradients are read by the server merge through spj "
+                       "(never written per occurrence); arena = both through the mailbox, "
+                       "like the peers' records"),
     "SS_SRV_STAGE": Knob("0", "parallel/engine_dist.py", "tuning",
                          "1: N>1 xGMI servers stream the peers' gradient rows out of the "
                          "uncached mailbox into a cached buffer before the merge gathers them "

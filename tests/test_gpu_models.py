@@ -520,15 +520,16 @@ def test_graph_teardown_then_replay_same_process(dev, monkeypatch):
     assert np.isfinite(b.mean_loss())
 
 
-@pytest.mark.parametrize("occ", ["arena", "copy"])
+@pytest.mark.parametrize("occ", ["own", "arena"])
 def test_record_exchange_world1_matches_unique(dev, monkeypatch, occ):
     """The record exchange (every occurrence shipped; the server dedups what
     it receives, fills a row per occurrence and merges the per-occurrence
     gradients with the AdaGrad update fused — no worker dedup or merge)
     through a size-1 xGMI arena trains like the unique-key exchange on the
     same path: the same keys, the same losses and parameters up to float
-    summation order (SS_REC_OCC: the forward reads the rows mailbox or a
-    cached copy).  Graph tests run in a child process (tests/_mp.py)."""
+    summation order (SS_REC_OCC: own = the own records' rows in a cached
+    buffer and their gradients read through spj by the server merge; arena =
+    through the mailbox).  Graph tests run in a child process (tests/_mp.py)."""
     in_child(_record_exchange_body, dev, occ)
 
 
@@ -544,13 +545,13 @@ def _record_exchange_body(dev, occ):
     for ex in ("unique", "records"):
         w, t = _graph_worker("lr", dev, transport=XgmiTransport(0, 1, dev, None), exchange=ex)
         assert w.engine.records == (ex == "records")
-        assert (w.rocc is not None) == (ex == "records" and occ == "copy")
+        assert (w.gring is not None) == (ex == "records" and occ == "own")
         losses = [float(w.step().sum().item()) for _ in range(12)]
         torch.cuda.synchronize()
         w.engine.check()
         t.check()
         out[ex] = (losses, t.to_dict(with_state=True))
-        if ex == "records" and occ == "arena":  # the record round captured as hipGraphs
+        if ex == "records":  # the record round captured as hipGraphs
             assert w.enable_graph()
             for _ in range(2 * w._gper):
                 w.step()

@@ -170,6 +170,10 @@ def test_bench_fallback_chain(force, plane, tier, fell):
         assert ss["server_stream"] == lay["server_stream"]
         assert len(ss["off_ms"]) == len(ss["on_ms"]) == ss["windows"]
         assert lay["claim"] and lay["srv_rbits"] > 0
+        # SS_XCHG=auto (default): both exchanges timed, the JSON names the pick
+        x = c["calibration"]["exchange"]
+        assert x["exchange"] == c["exchange"] and x["default"] == "unique"
+        assert len(x["unique_ms"]) == len(x["records_ms"]) == x["windows"]
     if fell:
         assert "litmus failed on every tier" in c["fallback_reason"]
         assert "falling back to RCCL" in err
@@ -185,5 +189,23 @@ def test_bench_world2_fenced_verified():
     c = j["config"]
     assert c["plane"] == "xgmi" and c["xgmi_tier"] == "fenced" and not c["fell_back"]
     assert c["devices"] == 1 and j["n_gpus"] == 2
+    assert c["loss_last"] < c["loss_first"]
+    assert np.isfinite(j["value"]) and j["value"] > 0
+
+
+@pytest.mark.parametrize("pick", ["records", "unique"])
+def test_bench_world2_exchange_calibration(pick):
+    """bench.py at N = 2 (both ranks on cuda:0) with SS_XCHG=auto: the unique
+    and the record exchange are built on one table, timed on the live world,
+    and the loser's engine and arenas are torn down on every rank before the
+    timed steps (SS_CAL_XCHG forces either outcome, so both teardowns run);
+    the survivor then trains on."""
+    j, _ = _bench({"SS_CAL_XCHG": pick}, nproc=2,
+                  shape=("--steps", "6", "--warmup", "3", "--batch", "8192", "--features",
+                         "4000000", "--cal-steps", "3", "--cal-windows", "1"))
+    c = j["config"]
+    assert c["plane"] == "xgmi" and c["exchange"] == pick
+    x = c["calibration"]["exchange"]
+    assert x["exchange"] == pick and len(x["unique_ms"]) == len(x["records_ms"]) == 1
     assert c["loss_last"] < c["loss_first"]
     assert np.isfinite(j["value"]) and j["value"] > 0
