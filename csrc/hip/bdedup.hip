@@ -887,7 +887,8 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
                                                     float* __restrict__ lacc = nullptr,
                                                     float* __restrict__ lacc_out = nullptr,
                                                     int lacc_n = 0,
-                                                    const uint64_t* __restrict__ bkeys = nullptr) {
+                                                    const uint64_t* __restrict__ bkeys = nullptr,
+                                                    int dbg = 0) {
   __shared__ float acc[kBdTS];
   const int b = blockIdx.x;
   // the step's loss accumulator (added by the forward, ordered before this
@@ -913,7 +914,7 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
     }
 #pragma unroll
     for (int r = 0; r < OCC; ++r) {
-      g[r] = l[r] != kBdInvalid ? self.grad(gs, j[r], (uint32_t)F) : 0.f;
+      g[r] = l[r] != kBdInvalid ? ((dbg & 2) ? 1.f : self.grad(gs, j[r], (uint32_t)F)) : 0.f;
       if (xval && l[r] != kBdInvalid) g[r] *= xval[j[r]];
     }
     // keys occurring once in the batch (usingle, from the dedup): a plain
@@ -921,7 +922,7 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
 #pragma unroll
     for (int r = 0; r < OCC; ++r) {
       if (l[r] == kBdInvalid) continue;
-      if (usingle && usingle[ubase[b] + l[r]])
+      if ((dbg & 1) || (usingle && !(dbg & 8) && usingle[ubase[b] + l[r]]))
         acc[l[r]] = g[r];
       else
         atomicAdd(&acc[l[r]], g[r]);
@@ -954,7 +955,7 @@ __global__ __launch_bounds__(RT) void k_bd_reduce(const uint32_t* __restrict__ b
 #pragma unroll
       for (int r = 0; r < OCC; ++r) {
         const uint32_t l = l0 + r * RT;
-        if (sl[r] < 0) continue;
+        if (sl[r] < 0 || (dbg & 4)) continue;
         if (!snap) wh[r] = *reinterpret_cast<const float2*>(slot_row(t, sl[r]));
         float s2 = 0.f;
         opt_update(op, wh[r].x, wh[r].y, s2, acc[l]);
@@ -992,21 +993,31 @@ static int bd_rt() {
 }
 // one launch of k_bd_reduce over P buckets at the (SS_BD_RT, SS_BD_ROCC)
 // shape: (1024, 2 / 4), (512, 2 / 4 / 8), (256, 2); others fall back to (1024, 4)
+// SS_BD_DBG (measurement only; wrong results): 1 = plain LDS stores for
+// every occurrence, 2 = no gradient gather, 4 = no table stores, 8 = atomics
+// for single-occurrence keys too
+static int bd_dbg() {
+  static const int v = [] {
+    const char* e = std::getenv("SS_BD_DBG");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
 template <typename... A>
 static void bd_reduce_launch(int P, hipStream_t st, A... a) {
-  const int rt = bd_rt(), oc = bd_rocc();
+  const int rt = bd_rt(), oc = bd_rocc(), dbg = bd_dbg();
   if (rt == 512 && oc == 8)
-    hipLaunchKernelGGL((k_bd_reduce<512, 8>), dim3(P), dim3(512), 0, st, a...);
+    hipLaunchKernelGGL((k_bd_reduce<512, 8>), dim3(P), dim3(512), 0, st, a..., dbg);
   else if (rt == 512 && oc == 4)
-    hipLaunchKernelGGL((k_bd_reduce<512, 4>), dim3(P), dim3(512), 0, st, a...);
+    hipLaunchKernelGGL((k_bd_reduce<512, 4>), dim3(P), dim3(512), 0, st, a..., dbg);
   else if (rt == 512)
-    hipLaunchKernelGGL((k_bd_reduce<512, 2>), dim3(P), dim3(512), 0, st, a...);
+    hipLaunchKernelGGL((k_bd_reduce<512, 2>), dim3(P), dim3(512), 0, st, a..., dbg);
   else if (rt == 256)
-    hipLaunchKernelGGL((k_bd_reduce<256, 2>), dim3(P), dim3(256), 0, st, a...);
+    hipLaunchKernelGGL((k_bd_reduce<256, 2>), dim3(P), dim3(256), 0, st, a..., dbg);
   else if (oc == 2)
-    hipLaunchKernelGGL((k_bd_reduce<1024, 2>), dim3(P), dim3(1024), 0, st, a...);
+    hipLaunchKernelGGL((k_bd_reduce<1024, 2>), dim3(P), dim3(1024), 0, st, a..., dbg);
   else
-    hipLaunchKernelGGL((k_bd_reduce<1024, 4>), dim3(P), dim3(1024), 0, st, a...);
+    hipLaunchKernelGGL((k_bd_reduce<1024, 4>), dim3(P), dim3(1024), 0, st, a..., dbg);
 }
 
 // K7 for FM rows [w | v_1..v_K]: per unique key u with occurrences in samples
