@@ -149,16 +149,32 @@ def main(argv=None):
                             streams_of=streams_of)
         return make
 
+    free0 = torch.cuda.mem_get_info(dev)[0]
     engine, (transport, ctrans, ptrans), plane = build_engine(
         a.transport, rank, world, dev, store,
         make_engine_for("unique" if xchg == "auto" else xchg),
         log=lambda m: print(f"bench.py: {m}", file=sys.stderr))
     comms = plane.comms
     worker = SparseLRWorker(engine, data, rank=rank, world=world, grad_mode=a.grad_mode)
-    # the record-exchange candidate: only over the mailboxes (its own arenas)
+    # the record-exchange candidate: only over the mailboxes (its own arenas),
+    # and only if every rank has room for a second engine of the first one's
+    # size (+ 25 %, + 2 GiB) — agreed before any rank builds it, since its
+    # set-up is collective (8 ranks sharing one GPU do not fit two engines)
     alt = None
-    if xchg == "auto" and not engine.fast1 and plane.plane == "xgmi" and worker.bucketed \
-            and a.cal_steps > 0:
+    want = (xchg == "auto" and not engine.fast1 and plane.plane == "xgmi" and worker.bucketed
+            and a.cal_steps > 0)
+    if want:
+        torch.cuda.synchronize(dev)
+        free1 = torch.cuda.mem_get_info(dev)[0]
+        fits = free1 > 1.25 * max(0, free0 - free1) + (2 << 30)
+        ok = torch.tensor([1 if fits else 0], dtype=torch.int64)
+        if world > 1:
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if not int(ok.item()):
+            want = False
+            print("bench.py: no room for the record-exchange candidate on some rank; unique only",
+                  file=sys.stderr)
+    if want:
         try:
             e2, trs2, plane2 = build_engine("xgmi", rank, world, dev, store,
                                             make_engine_for("records", engine),

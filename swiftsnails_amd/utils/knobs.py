@@ -96,7 +96,7 @@ KNOBS: dict[str, Knob] = {
                     "warm-up, the faster kept (the launcher runs unique)"),
     "SS_BD_CSUB": Knob("1", "csrc/hip/bdedup.hip", "tuning",
                        "2: the route count kernel runs two workgroups per scatter chunk (its own "
-                       "histogram row each; the column scan joins them)"),
+                       "histogram row each; the column scan joins them) — measured neutral"),
     "SS_BD_DBG": Knob("0", "csrc/hip/bdedup.hip", "debug",
                       "measurement only, wrong results: k_bd_reduce bits 1 = plain LDS stores, "
                       "2 = no gradient gather, 4 = no table stores, 8 = atomics for single keys"),
