@@ -16,6 +16,7 @@
 // A job whose litmus fails both tiers falls back to RCCL.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 
 #include <algorithm>
 #include <cstring>
@@ -122,8 +123,17 @@ class XgmiArena {
     if (bytes < kXHeadBytes) throw_error("xgmi: arena smaller than its flag and tag area");
     check_hip(hipSetDevice(device), "hipSetDevice");
     void* p = nullptr;
-    check_hip(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached),
-              "xgmi arena (uncached)");
+    // SS_XGMI_CACHED=1 (measurement only, one-rank arenas): an ordinary
+    // cached allocation — what the uncached mailbox costs its local readers
+    static const bool cached = [] {
+      const char* e = std::getenv("SS_XGMI_CACHED");
+      return e && e[0] == '1';
+    }();
+    if (cached && nranks == 1)
+      check_hip(hipMalloc(&p, (size_t)bytes), "xgmi arena (cached, one rank)");
+    else
+      check_hip(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached),
+                "xgmi arena (uncached)");
     base_ = static_cast<char*>(p);
     check_hip(hipMemset(base_, 0, (size_t)kXHeadBytes), "xgmi flags");
     check_hip(hipMalloc(&local_, sizeof(unsigned long long) * kXLocalWords), "xgmi counters");

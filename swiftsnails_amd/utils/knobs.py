@@ -100,6 +100,9 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_DBG": Knob("0", "csrc/hip/bdedup.hip", "debug",
                       "measurement only, wrong results: k_bd_reduce bits 1 = plain LDS stores, "
                       "2 = no gradient gather, 4 = no table stores, 8 = atomics for single keys"),
+    "SS_XGMI_CACHED": Knob("0", "csrc/hip/xgmi.h", "experiment",
+                           "1 (one-rank arenas only): the mailbox arenas as ordinary cached "
+                           "memory — measures what the uncached mailbox costs its local readers"),
     "SS_CAL_XCHG": Knob("", "models/base.py", "debug",
                         "debug: force calibrate_exchange's outcome (unique / records)"),
     "SS_REC_OCC": Knob("own", "parallel/engine_dist.py", "tuning",
