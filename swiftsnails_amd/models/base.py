@@ -459,8 +459,12 @@ class PipelinedWorker:
         steps, windows = max(1, int(steps)), max(1, int(windows))
         times = {n: [] for n in names}
 
+        def sync(eng):
+            if getattr(eng, "gpu", False):
+                torch.cuda.synchronize(eng.device)
+
         def quiesce(eng):
-            torch.cuda.synchronize(eng.device)
+            sync(eng)
             eng.barrier()
 
         for _ in range(windows):
@@ -476,7 +480,7 @@ class PipelinedWorker:
                 t0 = time.perf_counter()
                 for _ in range(steps):
                     w.step()
-                torch.cuda.synchronize(eng.device)
+                sync(eng)
                 el = time.perf_counter() - t0
                 eng.barrier()
                 times[n].append(eng.max_over_ranks(el) / steps)
