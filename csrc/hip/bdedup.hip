@@ -1653,7 +1653,10 @@ void launch_rec_grad(const unsigned long long* ucount, int nd, long long gap, co
   if (skip >= nd) throw_error("rec_grad: skipped destination out of range");
   // the grid covers the ranges walked: none at one rank with its own skipped
   // (the launch then only hands the loss off)
-  const int grid = rec_grid(gap, skip >= 0 ? nd - 1 : nd);
+  int grid = rec_grid(gap, skip >= 0 ? nd - 1 : nd);
+  // ... and at least one thread per accumulator word for the hand-off (one
+  // workgroup walking 8192 words took 16 us of dependent load -> store)
+  if (lacc) grid = std::max(grid, (lacc_n + 255) / 256);
   hipLaunchKernelGGL(k_rec_grad, dim3(grid), dim3(256), 0, st, ucount, nd, gap, spj, gs, xval, F,
                      grec, lacc, lacc_out, lacc_n, skip);
   check_launch("k_rec_grad");
