@@ -162,7 +162,7 @@ def main(argv=None):
     # set-up is collective (8 ranks sharing one GPU do not fit two engines)
     alt = None
     want = (xchg == "auto" and not engine.fast1 and plane.plane == "xgmi" and worker.bucketed
-            and a.cal_steps > 0)
+            and a.cal_steps > 0 and not engine.pull_ahead)  # (timed in synchronous rounds)
     if want:
         torch.cuda.synchronize(dev)
         free1 = torch.cuda.mem_get_info(dev)[0]
