@@ -286,9 +286,13 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
 
     t = torch.tensor([elapsed], dtype=torch.float64)
+    t_min = t.clone()
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t_min, op=dist.ReduceOp.MIN)
     elapsed = float(t.item())
+    # the fastest rank's own timed region (the reported step is the slowest's)
+    fastest_ms = 1000.0 * float(t_min.item()) / a.steps
     engine.check()  # table full / dedup overflow: fail instead of reporting
     last_loss = worker.mean_loss()
     # unique keys per step this rank routed (mean over the ring slots)
@@ -361,6 +365,7 @@ def main(argv=None):
                 "server_unique_keys_per_step": srv_unique,
                 "optimizer": a.optimizer,
                 "hipgraph": graphed,
+                "fastest_rank_ms_per_step": round(fastest_ms, 4),
                 "keys_per_step_per_gpu": a.batch * a.fields,
                 "unique_keys_per_step_per_gpu": uniq,
                 "table_keys": int(keys_in_table.item()),
