@@ -403,15 +403,19 @@ void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long lon
   if (F < 1 || F > 256) throw_error("gen_ctr: F must be in [1,256]");
   const double logV = log((double)vocab_per_field + 1.0);
   const int spb = samples_per_block(F);
-  // R sample groups per workgroup (SS_GEN_R: 1 / 2 / 4)
+  // R sample groups per workgroup (SS_GEN_R: 1 / 2 / 4 / 8)
   static const int gr = [] {
     const char* e = std::getenv("SS_GEN_R");
     const int v = e ? std::atoi(e) : 4;
-    return (v == 1 || v == 2) ? v : 4;
+    return (v == 1 || v == 2 || v == 8) ? v : 4;
   }();
   if (gr > 1 && gr * spb <= 256) {
     const int g = gr * spb, nb = (B + g - 1) / g;
-    if (gr == 4)
+    if (gr == 8)
+      hipLaunchKernelGGL(k_gen_ctr_r<8>, dim3(nb), dim3(256), 0, st, seed, sample_base, B, F,
+                         vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels,
+                         step_dev, step_mul, step_add);
+    else if (gr == 4)
       hipLaunchKernelGGL(k_gen_ctr_r<4>, dim3(nb), dim3(256), 0, st, seed, sample_base, B, F,
                          vocab_per_field, logV, tail_frac, truth_scale, truth_bias, keys, labels,
                          step_dev, step_mul, step_add);

@@ -442,12 +442,15 @@ void launch_lr_fwd_g(const uint32_t* inv, const BdIndex& ix, const float* xval,
   static const int fr = [] {
     const char* e = std::getenv("SS_LR_FWD_R");
     const int v = e ? std::atoi(e) : 4;
-    return (v == 1 || v == 2) ? v : 4;
+    return (v == 1 || v == 2 || v == 8) ? v : 4;
   }();
   if (occ && per_sample && ((fr > 1 && fr * spb <= 256) || occ_self.ptr)) {
     const int r = fr * spb <= 256 ? fr : 1;
     const int g = r * spb;
-    if (r == 4)
+    if (r == 8)
+      hipLaunchKernelGGL(k_lr_fwd_occ<8>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
+                         labels, B, F, gocc, loss_sum, pred, occ, occ_self);
+    else if (r == 4)
       hipLaunchKernelGGL(k_lr_fwd_occ<4>, dim3((B + g - 1) / g), dim3(256), 0, st, ix.pos_of, xval,
                          labels, B, F, gocc, loss_sum, pred, occ, occ_self);
     else if (r == 2)
