@@ -403,11 +403,12 @@ void launch_gen_ctr(uint64_t seed, long long sample_base, int B, int F, long lon
   if (F < 1 || F > 256) throw_error("gen_ctr: F must be in [1,256]");
   const double logV = log((double)vocab_per_field + 1.0);
   const int spb = samples_per_block(F);
-  // R sample groups per workgroup (SS_GEN_R: 1 / 2 / 4 / 8)
+  // R sample groups per workgroup (SS_GEN_R: 1 / 2 / 4 / 8); 8 measured
+  // 0.7227-0.7229 vs 0.7266-0.7278 ms per bench step (4), three A/B pairs
   static const int gr = [] {
     const char* e = std::getenv("SS_GEN_R");
-    const int v = e ? std::atoi(e) : 4;
-    return (v == 1 || v == 2 || v == 8) ? v : 4;
+    const int v = e ? std::atoi(e) : 8;
+    return (v == 1 || v == 2 || v == 4) ? v : 8;
   }();
   if (gr > 1 && gr * spb <= 256) {
     const int g = gr * spb, nb = (B + g - 1) / g;

@@ -170,11 +170,11 @@ KNOBS: dict[str, Knob] = {
     "SS_BD_ROCC": Knob("4", "csrc/hip/bdedup.hip", "tuning",
                        "k_bd_reduce: occurrences (and fused-update rows) per thread in flight, "
                        "2 or 4"),
-    "SS_GEN_R": Knob("4", "csrc/hip/models.hip", "tuning",
+    "SS_GEN_R": Knob("8", "csrc/hip/models.hip", "tuning",
                      "synthetic CTR generator: sample groups per workgroup (1 / 2 / 4 / 8)"),
     "SS_LR_FWD_R": Knob("4", "csrc/hip/segreduce.hip", "tuning",
                         "packed LR forward (one-gather mode): sample groups per workgroup, "
-                        "their gathers in flight together (1 / 2 / 4 / 8)"),
+                        "their gathers in flight together (1 / 2 / 4 / 8; 8 measured 4 % slower)"),
     "SS_LR_FWD": Knob("auto", "csrc/hip/segreduce.hip", "tuning",
                       "LR forward layout: packed | group (auto by lane utilisation)"),
     "SS_FM_FUSE": Knob("0", "models/fm.py", "experiment",
