@@ -94,6 +94,9 @@ KNOBS: dict[str, Knob] = {
                     "dedup and merge (less kernel work per rank at N <= 2, twice the link "
                     "bytes); auto (bench.py) = both timed on the live world after the "
                     "warm-up, the faster kept (the launcher runs unique)"),
+    "SS_ROUTE_AFTER_PULL": Knob("0", "models/base.py", "experiment",
+                                "1: one GPU, the next route waits for this round's pull (the "
+                                "pull runs without the route kernels beside it)"),
     "SS_BD_CSUB": Knob("1", "csrc/hip/bdedup.hip", "tuning",
                        "2: the route count kernel runs two workgroups per scatter chunk (its own "
                        "histogram row each; the column scan joins them) — measured neutral"),
