@@ -95,7 +95,7 @@ KNOBS: dict[str, Knob] = {
                     "bytes); auto (bench.py) = both timed on the live world after the "
                     "warm-up, the faster kept (the launcher runs unique)"),
     "SS_ROUTE_AFTER_PULL": Knob("0", "models/base.py", "experiment",
-                                "1: one GPU, the next route waits for this round's pull (the "
+                                "1: one GPU, the next route waits for this round's pull (measured 7 % slower; the "
                                 "pull runs without the route kernels beside it)"),
     "SS_BD_CSUB": Knob("1", "csrc/hip/bdedup.hip", "tuning",
                        "2: the route count kernel runs two workgroups per scatter chunk (its own "
