@@ -171,20 +171,9 @@ static long long bd_max_chunks(int nranks) {
   return x < 64 ? 64 : x;
 }
 
-// SS_BD_CSUB=2: the count kernel runs two workgroups per scatter chunk (the
-// scatter's 128 chunks fill half of the 256 CUs; the count has no reason to)
-static int bd_csub() {
-  static const int v = [] {
-    const char* e = std::getenv("SS_BD_CSUB");
-    return e && std::atoi(e) == 2 ? 2 : 1;
-  }();
-  return v;
-}
-
 // ---- layout of the int scratch (u32 words), a function of (n, nranks) only
 struct BdLayout {
   int P, Pd, nch, chunk;
-  int csub;  // count workgroups per scatter chunk (SS_BD_CSUB): hist has nch * csub rows
   long long hist, btot, bstart, ubase, unum, ctr, wacc, wfin, total;
 };
 
@@ -221,10 +210,6 @@ static BdLayout bd_layout(long long n, int nranks, int ndest) {
   L.chunk = (int)chunk;
   L.nch = (int)((n + L.chunk - 1) / L.chunk);
   if (L.nch < 1) L.nch = 1;
-  // the count over csub sub-chunks per chunk (its own histogram row each):
-  // the column scan turns row c * csub into chunk c's cursor — the chunk's
-  // keys are the sub-chunks' keys in order
-  L.csub = (bd_csub() == 2 && L.chunk % (2 * kBdChunkLanes) == 0) ? 2 : 1;
   // words 0, 1: sticky error flag and the colscan arrival counter, at fixed
   // positions for any n (the scratch is sized for the largest call and
   // zeroed once; every other word is rewritten by each call)
@@ -232,7 +217,7 @@ static BdLayout bd_layout(long long n, int nranks, int ndest) {
   L.ctr = 1;
   L.wacc = 2;  // count: some key of this call has high bits (atomicOr)
   L.wfin = 3;  // colscan's last workgroup: the call's value (wacc reset to 0)
-  L.hist = o; o += (long long)L.P * L.nch * L.csub;
+  L.hist = o; o += (long long)L.P * L.nch;
   L.btot = o; o += L.P;
   L.bstart = o; o += L.P + 1;
   L.ubase = o; o += L.P;
@@ -262,7 +247,7 @@ long long bd_scratch_words(long long n, int nranks, int ndest) {
   long long nchmax = std::min<long long>(256 * waves, bd_max_chunks(nranks));
   nchmax = std::min<long long>(nchmax, (n + kBdChunkLanes - 1) / kBdChunkLanes);
   nchmax = std::max<long long>(nchmax, 1);
-  const long long bound = 4 + pmax * nchmax * bd_csub() + 4 * pmax + 1;
+  const long long bound = 4 + pmax * nchmax + 4 * pmax + 1;
   return std::max(bound, bd_layout(n, nranks, ndest_arg).total);
 }
 int bd_buckets(long long n, int nranks, int ndest) {
@@ -447,10 +432,8 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
                                                      void* __restrict__ rec,
                                                      const uint32_t* __restrict__ wfin,
                                                      int xcd, uint64_t* __restrict__ skeys = nullptr,
-                                                     uint32_t* __restrict__ spj = nullptr,
-                                                     long long hstride = 0) {
+                                                     uint32_t* __restrict__ spj = nullptr) {
   extern __shared__ unsigned int cur[];
-  if (hstride == 0) hstride = P;
   // XCD-aware chunk order (xcd != 0): blocks b and b + 8 share an XCD, so
   // they get ADJACENT chunks — a bucket's runs are laid out chunk after chunk,
   // and the line two neighbouring runs share is then written by one L2 and
@@ -464,7 +447,7 @@ __global__ __launch_bounds__(CT) void k_bd_scatter(const uint64_t* __restrict__ 
   const bool narrow = RW == 3 && wfin && *wfin == 0u;
   uint32_t* rk32 = reinterpret_cast<uint32_t*>(rec);
   uint64_t* rk64 = reinterpret_cast<uint64_t*>(rec);
-  const uint32_t* row = hist + (long long)c * hstride;
+  const uint32_t* row = hist + (long long)c * P;
   for (int b = threadIdx.x; b < P; b += CT) cur[b] = bstart[b] + row[b];
   for (int t0 = 0; t0 < chunk; t0 += kBdMaxChunk) {
     const long long base = (long long)c * chunk + t0 + threadIdx.x;
@@ -535,8 +518,7 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
                                                        const uint32_t* __restrict__ wfin,
                                                        int xcd, uint64_t* __restrict__ skeys,
                                                        uint32_t* __restrict__ spj,
-                                                       uint32_t* __restrict__ pj,
-                                                       long long hstride) {
+                                                       uint32_t* __restrict__ pj) {
   constexpr int CT = 1024;
   extern __shared__ unsigned int sm[];
   unsigned int* cur = sm;           // [P] the chunk's cursor per bucket
@@ -556,7 +538,7 @@ __global__ __launch_bounds__(1024) void k_bd_scatter_s(const uint64_t* __restric
   uint32_t* sx = stage;
   uint32_t* sy = stage + T;                  // key high words (12-byte records)
   uint32_t* sz = stage + (narrow ? T : 2 * T);
-  const uint32_t* row = hist + (long long)c * hstride;  // chunk c = hist row c * csub
+  const uint32_t* row = hist + (long long)c * P;
   for (int b = t; b < P; b += CT) cur[b] = bstart[b] + row[b];
   const int per = (P + CT - 1) / CT;  // scan: buckets per thread
   const int b0 = t * per, b1 = min(P, b0 + per);
@@ -1480,9 +1462,9 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   uint32_t* wfin = S + L.wfin;
 #define SS_BD_CT_DISPATCH(ct, KERNEL, ...)                                                    \
   switch (ct) {                                                                               \
-    case 256: hipLaunchKernelGGL(KERNEL<256>, dim3(L.nch * L.csub), dim3(256), lds, st, __VA_ARGS__); break; \
-    case 512: hipLaunchKernelGGL(KERNEL<512>, dim3(L.nch * L.csub), dim3(512), lds, st, __VA_ARGS__); break; \
-    default: hipLaunchKernelGGL(KERNEL<1024>, dim3(L.nch * L.csub), dim3(1024), lds, st, __VA_ARGS__);     \
+    case 256: hipLaunchKernelGGL(KERNEL<256>, dim3(L.nch), dim3(256), lds, st, __VA_ARGS__); break; \
+    case 512: hipLaunchKernelGGL(KERNEL<512>, dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
+    default: hipLaunchKernelGGL(KERNEL<1024>, dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
   }
 #define SS_BD_CT_DISPATCH2(ct, RW, KERNEL, ...)                                                  \
   switch (ct) {                                                                               \
@@ -1490,8 +1472,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     case 512: hipLaunchKernelGGL((KERNEL<512, RW>), dim3(L.nch), dim3(512), lds, st, __VA_ARGS__); break; \
     default: hipLaunchKernelGGL((KERNEL<1024, RW>), dim3(L.nch), dim3(1024), lds, st, __VA_ARGS__);     \
   }
-  SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk / L.csub, S + L.hist, ucount,
-                    wacc);
+  SS_BD_CT_DISPATCH(cnt, k_bd_count, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist, ucount, wacc);
   RecLay rl{};
   if (spj) rl = RecLay{ucap, L.Pd, ucount, S + L.ubase, S + L.unum, S};
   check_launch("k_bd_count");
@@ -1499,7 +1480,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
 #define SS_BD_CS_CASE(CS)                                                                      \
   case CS:                                                                                     \
     hipLaunchKernelGGL(k_bd_colscan<CS>, dim3((L.P + 63) / 64), dim3(CS), 0, st, S + L.hist,   \
-                       L.nch * L.csub, L.P, S + L.btot, S + L.bstart, S + L.ctr, wacc, wfin, rl); \
+                       L.nch, L.P, S + L.btot, S + L.bstart, S + L.ctr, wacc, wfin, rl);       \
     break;
     SS_BD_CS_CASE(256)
     SS_BD_CS_CASE(512)
@@ -1536,8 +1517,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     (void)attr;                                                                                   \
     hipLaunchKernelGGL(k_bd_scatter_s<KT>, dim3(L.nch), dim3(1024), s_lds(KT), st, keys, n, rs,  \
                        L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pos_of, bkt, rec, wfin,      \
-                       bd_xcd(), spj ? ukeys : nullptr, spj, pj,                                  \
-                       (long long)L.P * L.csub);                                                  \
+                       bd_xcd(), spj ? ukeys : nullptr, spj, pj);                                 \
   } break;
       SS_BD_S_CASE(16)
       SS_BD_S_CASE(8)
@@ -1548,7 +1528,7 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   } else
     SS_BD_CT_DISPATCH2(ct, 3, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
                        S + L.bstart, pj, pos_of, bkt, rec, wfin,
-                       bd_xcd(), spj ? ukeys : nullptr, spj, (long long)L.P * L.csub)
+                       bd_xcd(), spj ? ukeys : nullptr, spj)
 #undef SS_BD_CT_DISPATCH
 #undef SS_BD_CT_DISPATCH2
   check_launch("k_bd_scatter");

@@ -20,8 +20,6 @@ from typing import Optional
 
 import torch
 
-_ROUTE_AFTER_PULL = os.environ.get("SS_ROUTE_AFTER_PULL", "0") == "1"
-
 
 class _GraphSet(list):
     """A worker's captured hipGraphs, owned so that they are destroyed BEFORE
@@ -262,19 +260,8 @@ class PipelinedWorker:
         if getattr(eng, "pull_ahead", False) or self._pulled:
             return self._step_pull_ahead()
         r = self._next if self._next is not None else self._route(self.step_idx)
-        if _ROUTE_AFTER_PULL and getattr(eng, "fast1", False):
-            # experiment (SS_ROUTE_AFTER_PULL=1): the next route starts only
-            # once this round's pull is done, so the pull runs without the
-            # route stream's kernels beside it and the route overlaps the
-            # forward + merge instead
-            rnd = self.engine.pull(r)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(eng.device))
-            eng.route_stream.wait_event(ev)
-            self._next = self._route(self.step_idx + 1)
-        else:
-            self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
-            rnd = self.engine.pull(r)
+        self._next = self._route(self.step_idx + 1)  # lookahead on the route stream
+        rnd = self.engine.pull(r)
         if self.has_data(self.step_idx):
             self._zero_acc()
             with self.engine.trace("compute"):

@@ -94,12 +94,6 @@ KNOBS: dict[str, Knob] = {
                     "dedup and merge (less kernel work per rank at N <= 2, twice the link "
                     "bytes); auto (bench.py) = both timed on the live world after the "
                     "warm-up, the faster kept (the launcher runs unique)"),
-    "SS_ROUTE_AFTER_PULL": Knob("0", "models/base.py", "experiment",
-                                "1: one GPU, the next route waits for this round's pull (measured 7 % slower; the "
-                                "pull runs without the route kernels beside it)"),
-    "SS_BD_CSUB": Knob("1", "csrc/hip/bdedup.hip", "tuning",
-                       "2: the route count kernel runs two workgroups per scatter chunk (its own "
-                       "histogram row each; the column scan joins them) — measured neutral"),
     "SS_BD_DBG": Knob("0", "csrc/hip/bdedup.hip", "debug",
                       "measurement only, wrong results: k_bd_reduce bits 1 = plain LDS stores, "
                       "2 = no gradient gather, 4 = no table stores, 8 = atomics for single keys"),
