@@ -102,6 +102,14 @@ int bd_target_dist() {
 // (every call and helper of a deduper passes the same ndest), not of the
 // process: engines of either kind can coexist.
 static constexpr int kBdRecLayout = 1 << 16;
+// ... with kBdRecGroup as well (N>1 grouped records, round 6): the record
+// placement but the unique layout's fuller source buckets (~3072
+// occurrences); a pass after the scatter (k_rec_group) groups each bucket's
+// records by the servers' sub-bucket, as the unique dedup groups its keys,
+// so a server reads exact ranges.  The small buckets above (3584 / N) made
+// the scatter's tile runs shorter than a sector at N >= 4 (P = 11K-16K
+// buckets, 8K- down to 2K-key tiles)
+static constexpr int kBdRecGroup = 1 << 17;
 static int bd_target(int nranks, bool rec) {
   static const int one = [] {
     const char* e = std::getenv("SS_BD_TARGET");
@@ -112,6 +120,7 @@ static int bd_target(int nranks, bool rec) {
   return nranks > 1 ? bd_target_dist() : one;
 }
 int bd_record_layout_bit() { return kBdRecLayout; }
+int bd_record_group_bit() { return kBdRecGroup; }
 // the occurrences-per-bucket target a layout of `nranks` ranks uses
 int bd_target_for(int nranks, bool records) { return bd_target(nranks, records); }
 static constexpr int kBdTS = 4096;      // LDS hash slots per bucket
@@ -178,13 +187,13 @@ struct BdLayout {
 };
 
 static int bd_clamp_ndest(int nranks, int ndest) {
-  ndest &= ~kBdRecLayout;
+  ndest &= ~(kBdRecLayout | kBdRecGroup);
   return ndest < 1 || ndest > nranks ? nranks : ndest;
 }
 
 static BdLayout bd_layout(long long n, int nranks, int ndest) {
   BdLayout L{};
-  const bool rec = (ndest & kBdRecLayout) != 0;
+  const bool rec = (ndest & kBdRecLayout) != 0 && !(ndest & kBdRecGroup);
   ndest = bd_clamp_ndest(nranks, ndest);
   // ~2048 occurrences per bucket, but at least ~1024 buckets for small calls
   // (>= 4 workgroups per CU; a word2vec step of 196K keys got only 96 buckets)
@@ -236,7 +245,7 @@ long long bd_max_keys() { return (long long)kBdMaxBuckets * 2800; }
 long long bd_scratch_words(long long n, int nranks, int ndest) {
   if (n < 1) n = 1;
   const int ndest_arg = ndest;
-  const bool rec = (ndest & kBdRecLayout) != 0;
+  const bool rec = (ndest & kBdRecLayout) != 0 && !(ndest & kBdRecGroup);
   ndest = bd_clamp_ndest(nranks, ndest);
   // active buckets (those of receiving destinations), then all P = Pd * nranks
   const int tg = bd_target(nranks, rec);
@@ -1380,22 +1389,40 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
   }
 }
 
+// grouped record layout: the per-bucket regroup after the scatter (defined
+// with the record-exchange kernels below)
+static constexpr int kRgT = 512;
+__global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__ bstart,
+                                                    const uint64_t* __restrict__ gkeys,
+                                                    const uint32_t* __restrict__ gspj,
+                                                    uint64_t* __restrict__ skeys,
+                                                    uint32_t* __restrict__ spj,
+                                                    uint32_t* __restrict__ pos_of,
+                                                    uint32_t* __restrict__ usub, int msub, int Pd,
+                                                    int rbits);
+
 // ------------------------------------------------------------- launchers
 int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long ucap,
                     uint32_t* scratch, uint32_t* pj, uint32_t* pos_of, uint32_t* bkt,
                     uint32_t* luid, uint64_t* bkeys, unsigned long long* ucount, uint64_t* ukeys,
                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                     unsigned long long* dbg, uint32_t* rec, uint8_t* usingle, int ndest,
-                    long long lay_n, int msub, uint32_t* usub, uint32_t* spj) {
+                    long long lay_n, int msub, uint32_t* usub, uint32_t* spj, uint64_t* gkeys,
+                    uint32_t* gspj) {
   if (rs.nranks < 1 || rs.nranks > kMaxSeg) throw_error("bdedup: bad nranks");
   // spj (record exchange): no dedup — count, column scan into send-segment
   // positions (d * ucap + ...) with the run tables and per-destination
   // counts, then the scatter writes every occurrence's key into ukeys and its
   // index into spj at that position (the servers dedup what they receive)
-  if (spj && (!ukeys || !ucount || rs.nranks > kRecMaxDest || msub != 1 || !pos_of ||
-              !(ndest & kBdRecLayout)))
-    throw_error("bdedup: the record exchange needs ukeys, ucount, pos_of, <= 64 ranks, no "
-                "sub-buckets and the record layout");
+  // grouped records (kBdRecGroup, msub > 1): the scatter writes into the
+  // staging (gkeys, gspj) and k_rec_group moves each bucket's run into the
+  // send segment grouped by the servers' sub-bucket
+  const bool grouped = spj && (ndest & kBdRecGroup) && msub > 1;
+  if (spj && (!ukeys || !ucount || rs.nranks > kRecMaxDest || !pos_of ||
+              !(ndest & kBdRecLayout) || (msub != 1 && !grouped) ||
+              (grouped && (!gkeys || !gspj || !usub))))
+    throw_error("bdedup: the record exchange needs ukeys, ucount, pos_of, <= 64 ranks and the "
+                "record layout; sub-buckets only grouped (with the staging and offsets)");
   if (rs.rbits < 0 || rs.rbits > 20) throw_error("bdedup: region bits 0..20");
   if (msub < 1 || msub > kBdMaxSub || (msub > 1 && !usub))
     throw_error("bdedup: server sub-buckets 1..64 (and their offset table)");
@@ -1517,7 +1544,8 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
     (void)attr;                                                                                   \
     hipLaunchKernelGGL(k_bd_scatter_s<KT>, dim3(L.nch), dim3(1024), s_lds(KT), st, keys, n, rs,  \
                        L.Pd, L.P, L.chunk, S + L.hist, S + L.bstart, pos_of, bkt, rec, wfin,      \
-                       bd_xcd(), spj ? ukeys : nullptr, spj, pj);                                 \
+                       bd_xcd(), spj ? (grouped ? gkeys : ukeys) : nullptr,                       \
+                       grouped ? gspj : spj, pj);                                                 \
   } break;
       SS_BD_S_CASE(16)
       SS_BD_S_CASE(8)
@@ -1528,10 +1556,15 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
   } else
     SS_BD_CT_DISPATCH2(ct, 3, k_bd_scatter, keys, n, rs, L.Pd, L.P, L.chunk, S + L.hist,
                        S + L.bstart, pj, pos_of, bkt, rec, wfin,
-                       bd_xcd(), spj ? ukeys : nullptr, spj)
+                       bd_xcd(), spj ? (grouped ? gkeys : ukeys) : nullptr, grouped ? gspj : spj)
 #undef SS_BD_CT_DISPATCH
 #undef SS_BD_CT_DISPATCH2
   check_launch("k_bd_scatter");
+  if (grouped) {
+    hipLaunchKernelGGL(k_rec_group, dim3(L.P), dim3(kRgT), 0, st, S + L.bstart, gkeys, gspj, ukeys,
+                       spj, pos_of, usub, msub, L.Pd, rs.rbits);
+    check_launch("k_rec_group");
+  }
   if (spj) return rs.rbits;  // record exchange: the servers dedup
   // place: unique keys straight into the per-destination send segments
   // (+ zeroed gradient rows), reserved with one atomic per bucket
@@ -1573,6 +1606,80 @@ __device__ __forceinline__ void rec_ranges(const unsigned long long* __restrict_
   }
   __syncthreads();
 }
+// grouped record layout (kBdRecGroup, N>1 with server sub-buckets): one
+// workgroup per bucket b moves its run [bstart[b], bstart[b+1]) from the
+// scatter's staging (gkeys, gspj: the same send-segment positions) into the
+// send segment grouped by the server's sub-bucket — the split the unique
+// dedup makes of its keys (region-based with region buckets, so a server
+// sub-bucket is whole regions and its pull can claim) — writing the groups'
+// offsets into usub and every record's final position into pos_of (the
+// scatter wrote the staging positions, and kBdInvalid for empty keys, first)
+__global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__ bstart,
+                                                    const uint64_t* __restrict__ gkeys,
+                                                    const uint32_t* __restrict__ gspj,
+                                                    uint64_t* __restrict__ skeys,
+                                                    uint32_t* __restrict__ spj,
+                                                    uint32_t* __restrict__ pos_of,
+                                                    uint32_t* __restrict__ usub, int msub, int Pd,
+                                                    int rbits) {
+  __shared__ unsigned int cnt[kBdMaxSub];
+  __shared__ unsigned int cur[kBdMaxSub];
+  const int t = threadIdx.x, b = blockIdx.x;
+  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+  if (t < msub) cnt[t] = 0u;
+  __syncthreads();
+  auto sub_of = [&](uint64_t v) -> uint32_t {
+    if (rbits) {
+      const uint64_t region = table_hash(v) >> (64 - rbits);
+      const uint32_t f = (uint32_t)((region * (uint64_t)Pd * (uint64_t)msub) >> rbits);
+      return f - (uint32_t)(b % Pd) * (uint32_t)msub;
+    }
+    return srv_sub(v, msub);
+  };
+  // pass 1: records per sub-bucket (4 per thread in flight)
+  for (uint32_t q0 = p0 + t; q0 < p1; q0 += 4 * kRgT) {
+    uint64_t k[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t p = q0 + r * kRgT;
+      k[r] = p < p1 ? gkeys[p] : kEmptyKey;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+      if (k[r] != kEmptyKey) atomicAdd(&cnt[min(sub_of(k[r]), (uint32_t)msub - 1)], 1u);
+  }
+  __syncthreads();
+  if (t == 0) {
+    unsigned int e = 0;
+    for (int i = 0; i < msub; ++i) {
+      cur[i] = e;
+      usub[(long long)b * msub + i] = e;
+      e += cnt[i];
+    }
+  }
+  __syncthreads();
+  // pass 2: every record to its group (the run is re-read from L2)
+  for (uint32_t q0 = p0 + t; q0 < p1; q0 += 4 * kRgT) {
+    uint64_t k[4];
+    uint32_t j[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const uint32_t p = q0 + r * kRgT;
+      k[r] = p < p1 ? gkeys[p] : kEmptyKey;
+      j[r] = p < p1 ? gspj[p] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      if (q0 + r * kRgT >= p1) continue;
+      const uint32_t g = k[r] != kEmptyKey ? min(sub_of(k[r]), (uint32_t)msub - 1) : 0u;
+      const uint32_t q = p0 + atomicAdd(&cur[g], 1u);
+      skeys[q] = k[r];
+      spj[q] = j[r];
+      pos_of[j[r]] = q;
+    }
+  }
+}
+
 __device__ __forceinline__ long long rec_pos(const long long* cs, int nd, long long gap,
                                              long long f) {
   int d = 0;

@@ -215,7 +215,7 @@ PYBIND11_MODULE(_ss_hip, m) {
                        uintptr_t ukeys, uintptr_t ugrad, int gdim, uintptr_t inv, int place,
                        uintptr_t st, uintptr_t dbg, uintptr_t rec, uintptr_t usingle,
                        int ndest, long long lay_n, int msub, uintptr_t usub, int rbits,
-                       uintptr_t spj) {
+                       uintptr_t spj, uintptr_t gkeys, uintptr_t gspj) {
     RouteSpec rs{P<const int>(frag_map), frag_num, nranks, rbits};
     return launch_bd_dedup(P<const uint64_t>(keys), n, rs, ucap, P<uint32_t>(scratch),
                            P<uint32_t>(pj), P<uint32_t>(pos_of), P<uint32_t>(bkt),
@@ -223,15 +223,16 @@ PYBIND11_MODULE(_ss_hip, m) {
                            P<uint64_t>(ukeys), P<float>(ugrad), gdim, P<uint32_t>(inv), place,
                            S(st), P<unsigned long long>(dbg), P<uint32_t>(rec),
                            P<uint8_t>(usingle), ndest, lay_n, msub, P<uint32_t>(usub),
-                           P<uint32_t>(spj));
+                           P<uint32_t>(spj), P<uint64_t>(gkeys), P<uint32_t>(gspj));
   }, py::arg("keys"), py::arg("n"), py::arg("frag_map"), py::arg("frag_num"), py::arg("nranks"),
      py::arg("ucap"), py::arg("scratch"), py::arg("pj"), py::arg("pos_of"), py::arg("bkt"),
      py::arg("luid"), py::arg("bkeys"), py::arg("ucount"), py::arg("ukeys"), py::arg("ugrad"),
      py::arg("gdim"), py::arg("inv"), py::arg("place"), py::arg("st"), py::arg("dbg") = 0,
      py::arg("rec") = 0, py::arg("usingle") = 0, py::arg("ndest") = 0,
      py::arg("lay_n") = 0, py::arg("msub") = 1, py::arg("usub") = 0, py::arg("rbits") = 0,
-     py::arg("spj") = 0);
+     py::arg("spj") = 0, py::arg("gkeys") = 0, py::arg("gspj") = 0);
   m.def("bd_record_layout_bit", &bd_record_layout_bit);
+  m.def("bd_record_group_bit", &bd_record_group_bit);
   m.def("bd_target_dist", &bd_target_dist);
   m.def("bd_target_for", &bd_target_for, py::arg("nranks"), py::arg("records") = false);
   m.def("rec_grad", [](uintptr_t ucount, int nd, long long gap, uintptr_t spj, uintptr_t gs,

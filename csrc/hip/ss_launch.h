@@ -180,8 +180,10 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
                     float* ugrad, int gdim, uint32_t* inv, int place, hipStream_t st,
                     unsigned long long* dbg = nullptr, uint32_t* rec = nullptr,
                     uint8_t* usingle = nullptr, int ndest = 0, long long lay_n = 0,
-                    int msub = 1, uint32_t* usub = nullptr, uint32_t* spj = nullptr);
+                    int msub = 1, uint32_t* usub = nullptr, uint32_t* spj = nullptr,
+                    uint64_t* gkeys = nullptr, uint32_t* gspj = nullptr);
 int bd_record_layout_bit();
+int bd_record_group_bit();
 int bd_target_dist();
 int bd_target_for(int nranks, bool records);
 void launch_rec_grad(const unsigned long long* ucount, int nd, long long gap, const uint32_t* spj,

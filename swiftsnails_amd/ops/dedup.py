@@ -61,7 +61,8 @@ class Deduper:
 
     def __init__(self, max_n: int, nranks: int = 1, frag_map: Optional[torch.Tensor] = None,
                  gdim: int = 1, device=None, with_grad: bool = True, zero_grad: bool = True,
-                 mode: Optional[str] = None, record_layout: bool = False):
+                 mode: Optional[str] = None, record_layout: bool = False,
+                 record_group: bool = False):
         from .._native import hip
 
         self.mode = mode or os.environ.get("SS_DEDUP", "bucket")
@@ -123,8 +124,14 @@ class Deduper:
         # enable_records) the record-layout bit — smaller source buckets, so
         # that N sources' records fill one server bucket (bdedup.hip)
         self.record_layout = bool(record_layout)
+        # ... record_group (N>1): the unique layout's fuller source buckets,
+        # each bucket's records then grouped by the servers' sub-bucket after
+        # the scatter (bdedup.hip k_rec_group; split_for_servers(m > 1))
+        self.record_group = bool(record_layout and record_group)
         self.ndest = effective_ndest(frag_map, self.nranks) | (
-            self.h.bd_record_layout_bit() if self.record_layout else 0)
+            self.h.bd_record_layout_bit() if self.record_layout else 0) | (
+            self.h.bd_record_group_bit() if self.record_group else 0)
+        self.gkeys = self.gspj = None  # grouped records: the scatter's staging
         self.frag_map = frag_map.to(d, torch.int32).contiguous()
         m = max(1, self.max_n)
         if self.mode == "bucket" and m > self.h.bd_max_keys():
@@ -184,7 +191,9 @@ class Deduper:
                             self.usingle.data_ptr() if self.usingle is not None else 0,
                             self.ndest, self.lay_n or 0, self.msub,
                             self.usub.data_ptr() if self.usub is not None else 0,
-                            self.rbits, self.spj.data_ptr() if self.spj is not None else 0)
+                            self.rbits, self.spj.data_ptr() if self.spj is not None else 0,
+                            self.gkeys.data_ptr() if self.gkeys is not None else 0,
+                            self.gspj.data_ptr() if self.gspj is not None else 0)
             return DedupResult(self.ukeys, self.ucount, self.inv[:n], self.ugrad, self.ucap,
                                self.nranks, n, self, self._lay(n), int(used or 0))
         # the scratch is all-EMPTY between calls: the finish kernel resets the
@@ -238,16 +247,23 @@ class Deduper:
 
     def enable_records(self) -> None:
         """Route every occurrence instead of the unique keys (bucket mode,
-        N>1 engines with a fixed ``lay_n``, no sub-buckets): ukeys holds the
+        N>1 engines with a fixed ``lay_n``; sub-buckets with record_group,
+        each bucket's records grouped by them): ukeys holds the
         occurrences' keys at their send-segment positions, ``spj`` their
         occurrence indices, ``ucount`` the records per destination, and the
         run tables the records per bucket (the servers dedup them)."""
-        if self.mode != "bucket" or not self.lay_n or self.msub != 1 or not self.record_layout:
-            raise RuntimeError("enable_records needs mode='bucket', lay_n, no sub-buckets and "
-                               "Deduper(record_layout=True)")
+        if self.mode != "bucket" or not self.lay_n or not self.record_layout or (
+                self.msub != 1 and not self.record_group):
+            raise RuntimeError("enable_records needs mode='bucket', lay_n and "
+                               "Deduper(record_layout=True); sub-buckets only with record_group")
         if self.spj is None:
             self.spj = torch.empty(self.nranks * self.ucap, dtype=torch.int32,
                                    device=self.device)
+        if self.msub > 1 and self.gkeys is None:
+            self.gkeys = torch.empty(self.nranks * self.ucap, dtype=torch.int64,
+                                     device=self.device)
+            self.gspj = torch.empty(self.nranks * self.ucap, dtype=torch.int32,
+                                    device=self.device)
         self.need_pos = True
         self.need_bkt = False
         self.materialize_inv = False

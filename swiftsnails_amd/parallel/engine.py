@@ -200,7 +200,12 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self.tracer = Tracer(enabled=False)
         fm = torch.from_numpy(self.frag_map.astype(np.int32))
         dd_cls = Deduper if self.gpu else CpuDeduper
-        rl = {"record_layout": True} if self.records else {}
+        # N>1 records: the unique layout's source buckets, grouped by the
+        # servers' sub-bucket after the scatter (SS_REC_GROUP=0: the small
+        # record buckets of round 5, 3584 / N records, no sub-buckets)
+        self.rec_group = bool(self.records and self.world > 1 and
+                              os.environ.get("SS_REC_GROUP", "1") != "0")
+        rl = {"record_layout": True, "record_group": self.rec_group} if self.records else {}
         self.dedupers = [dd_cls(self.max_keys, nranks=self.world, frag_map=fm, gdim=self.dim,
                                 device=self.device, zero_grad=zero_grad, **rl)
                          for _ in range(self.depth)]

@@ -36,7 +36,9 @@ class EngineControl:
             # SS_BD_TARGET_DIST (the N>1 source-bucket target), and the target
             # this layout actually uses (a one-rank layout takes SS_BD_TARGET)
             "bd_target_dist": int(h.bd_target_dist()),
-            "bucket_target": int(h.bd_target_for(self.world, bool(getattr(self, "records", False)))),
+            "bucket_target": int(h.bd_target_for(self.world, bool(getattr(self, "records", False))
+                                                 and not getattr(self, "rec_group", False))),
+            "record_group": bool(getattr(self, "rec_group", False)),
             "buckets_per_dest": int(getattr(self, "Pd", 0)),
             "srv_sub_buckets": int(getattr(self, "sub", 1)),
             "claim": bool(getattr(self, "claim", False)),

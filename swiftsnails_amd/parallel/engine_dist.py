@@ -58,9 +58,12 @@ class DeviceSetup:
             dd.lay_n = cap
         self.Pd = h.bd_buckets(cap, N, self.dedupers[0].ndest) // N
         # record exchange: a server bucket is N runs of records sized for one
-        # LDS table together (bdedup.hip bd_target), no sub-buckets
-        self.sub = 1 if self.records else h.srv_sub_buckets(
-            N, cap, self.dedupers[0].ndest & ~h.bd_record_layout_bit())
+        # LDS table together (bdedup.hip bd_target), no sub-buckets — or, with
+        # grouped records (rec_group), the unique layout's buckets and its
+        # sub-bucket split (the sender groups each run's records by it)
+        bits = h.bd_record_layout_bit() | h.bd_record_group_bit()
+        self.sub = 1 if (self.records and not self.rec_group) else h.srv_sub_buckets(
+            N, cap, self.dedupers[0].ndest & ~bits)
         self.Ps = self.Pd * self.sub
         # sub > 1: every source groups its runs by the servers' sub-bucket
         # and sends the offsets with them (the server reads exact ranges)
@@ -85,7 +88,8 @@ class DeviceSetup:
             from ..ops.dedup import Deduper
 
             lk = Deduper(self.max_keys, nranks=N, frag_map=self.dedupers[0].frag_map.cpu(),
-                         gdim=d, device=dev, record_layout=self.records)
+                         gdim=d, device=dev, record_layout=self.records,
+                         record_group=self.rec_group)
             lk.lay_n = cap
             lk.split_for_servers(self.sub)
             lk.need_ukeys = True

@@ -41,3 +41,22 @@ def test_unique_layout_unchanged_by_the_bit():
         assert 0.9 * tg < N_BENCH / P < 1.1 * tg
         m = h.srv_sub_buckets(world)
         assert world * (N_BENCH / P) * 1.25 / m <= 3000  # <= ~3000 keys per server table
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_grouped_record_layout_uses_the_unique_buckets(world):
+    """Grouped records (the kBdRecGroup bit beside kBdRecLayout, N > 1): the
+    record placement with the unique layout's ~3072-occurrence source buckets
+    (the servers split them into the unique layout's sub-buckets, each run's
+    records grouped by them after the scatter) — not the 3584 / N records
+    whose bucket count reaches the 16K cap at N = 8."""
+    h = hip()
+    bits = h.bd_record_layout_bit() | h.bd_record_group_bit()
+    P = h.bd_buckets(N_BENCH, world, world | bits)
+    assert P == h.bd_buckets(N_BENCH, world, world)
+    assert P < h.bd_buckets(N_BENCH, world, world | h.bd_record_layout_bit())
+    assert h.bd_offsets(N_BENCH, world, world | bits)[0] == P
+    assert h.bd_scratch_words(N_BENCH, world, world | bits) > P
+    # the servers' split of a grouped layout is the unique one's
+    m = h.srv_sub_buckets(world, N_BENCH, world)
+    assert m > 1 and world * (N_BENCH / P) * 1.25 / m <= 3000
