@@ -167,7 +167,7 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
   if (t == 0) {
     so[0] = 0u;
     for (int s = 0; s < R.nsrc; ++s) so[s + 1] += so[s];
-    bad = so[R.nsrc] != p1 - p0;
+    bad = so[R.nsrc] != p1 - p0 ? 2 : 0;  // 2: the runs disagree with the count
   }
   __syncthreads();
   auto insert = [&](uint64_t key) -> uint32_t {
@@ -183,7 +183,7 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
       }
       s = (s + 1) & (ts - 1);
     }
-    bad = 1;
+    atomicOr(&bad, 1);  // 1: the LDS table is full
     return kSrvInv;
   };
   // the sources' parts as one flat list [0, nall): position p0 + f holds
@@ -237,7 +237,7 @@ __global__ __launch_bounds__(kSrvDT) void k_srv_dedup(SrvRuns R, const uint32_t*
     sbase = atomicAdd(ucount, (unsigned long long)tot);
     ubase[b] = (uint32_t)sbase;
     unum[b] = tot;
-    if (bad) atomicOr(err, 1u);
+    if (bad) atomicOr(err, (uint32_t)bad);
   }
   __syncthreads();
 #pragma unroll

@@ -225,8 +225,21 @@ class EngineControl:
         if getattr(self, "srv", None) is not None and int(self.srv_err.item()) != 0:
             from ..ops.dedup import DedupOverflowError
 
-            raise DedupOverflowError("server merge: a bucket of received keys overflowed its "
-                                     "LDS table")
+            e = int(self.srv_err.item())
+            # the fullest server bucket of each ring slot (received keys,
+            # distinct keys) — what the sub-bucket split was sized against
+            sizes = []
+            for S in self.srv[:self.depth]:
+                bs = S.bstart.to(torch.int64)
+                if bs.numel() > 1:
+                    sizes.append((int((bs[1:] - bs[:-1]).max()), int(S.unum.max())))
+            raise DedupOverflowError(
+                "server merge: a bucket of received keys "
+                + ("overflowed its LDS table" if e & 1 else "")
+                + (" / " if e & 3 == 3 else "")
+                + ("disagreed with the sources' run tables" if e & 2 else "")
+                + f" (err {e}; {self.sub} sub-buckets per bucket; fullest bucket per slot "
+                f"(received, distinct): {sizes})")
         chk = getattr(self.table, "check", None) if self.table is not None else None
         if chk is not None:
             chk()
