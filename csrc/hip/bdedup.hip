@@ -1636,17 +1636,48 @@ __global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__
     }
     return srv_sub(v, msub);
   };
-  // pass 1: records per sub-bucket (4 per thread in flight)
-  for (uint32_t q0 = p0 + t; q0 < p1; q0 += 4 * kRgT) {
+  // a wave's lanes grouped by sub-bucket without same-address LDS atomics:
+  // a Zipf-hot key puts thousands of a bucket's records into one sub-bucket,
+  // and one returning LDS atomic per record on that counter serialised them
+  // (9 ms per call at 2 ranks).  Per distinct sub-bucket g of the wave (a
+  // leader lane's, found by ballot): one atomic adds the lanes that share it,
+  // each lane's rank among them is the popcount of the lower matching lanes
+  const int lane = (int)(threadIdx.x & 63);
+  auto wave_slot = [&](bool valid, uint32_t g, unsigned int* ctr, bool ret) -> uint32_t {
+    uint64_t todo = __ballot(valid);
+    uint32_t mine = 0u;
+    while (todo) {
+      const int leader = __ffsll((unsigned long long)todo) - 1;
+      const uint32_t gl = __shfl(g, leader, 64);
+      const uint64_t mask = __ballot(valid && g == gl);
+      uint32_t base = 0u;
+      if (lane == leader) {
+        const unsigned int c = (unsigned int)__popcll(mask);
+        base = ret ? atomicAdd(&ctr[gl], c) : (atomicAdd(&ctr[gl], c), 0u);
+      }
+      base = __shfl(base, leader, 64);
+      if (valid && g == gl)
+        mine = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+      todo &= ~mask;
+    }
+    return mine;
+  };
+  // pass 1: records per sub-bucket (4 per thread in flight); the loop is
+  // wave-uniform (every lane runs the ballots)
+  const uint32_t n = p1 - p0;
+  const uint32_t nr = (n + kRgT - 1) / kRgT;  // rounds of one record per thread
+  for (uint32_t r0 = 0; r0 < nr; r0 += 4) {
     uint64_t k[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t p = q0 + r * kRgT;
-      k[r] = p < p1 ? gkeys[p] : kEmptyKey;
+      const uint32_t p = p0 + (r0 + r) * kRgT + t;
+      k[r] = (r0 + r < nr && p < p1) ? gkeys[p] : kEmptyKey;
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r)
-      if (k[r] != kEmptyKey) atomicAdd(&cnt[min(sub_of(k[r]), (uint32_t)msub - 1)], 1u);
+    for (int r = 0; r < 4; ++r) {
+      const bool v = k[r] != kEmptyKey;
+      wave_slot(v, v ? min(sub_of(k[r]), (uint32_t)msub - 1) : 0u, cnt, false);
+    }
   }
   __syncthreads();
   if (t == 0) {
@@ -1659,23 +1690,26 @@ __global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__
   }
   __syncthreads();
   // pass 2: every record to its group (the run is re-read from L2)
-  for (uint32_t q0 = p0 + t; q0 < p1; q0 += 4 * kRgT) {
+  for (uint32_t r0 = 0; r0 < nr; r0 += 4) {
     uint64_t k[4];
     uint32_t j[4];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const uint32_t p = q0 + r * kRgT;
-      k[r] = p < p1 ? gkeys[p] : kEmptyKey;
-      j[r] = p < p1 ? gspj[p] : 0u;
+      const uint32_t p = p0 + (r0 + r) * kRgT + t;
+      const bool in = r0 + r < nr && p < p1;
+      k[r] = in ? gkeys[p] : kEmptyKey;
+      j[r] = in ? gspj[p] : kBdInvalid;
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      if (q0 + r * kRgT >= p1) continue;
-      const uint32_t g = k[r] != kEmptyKey ? min(sub_of(k[r]), (uint32_t)msub - 1) : 0u;
-      const uint32_t q = p0 + atomicAdd(&cur[g], 1u);
-      skeys[q] = k[r];
-      spj[q] = j[r];
-      pos_of[j[r]] = q;
+      const bool v = j[r] != kBdInvalid;
+      const uint32_t g = v && k[r] != kEmptyKey ? min(sub_of(k[r]), (uint32_t)msub - 1) : 0u;
+      const uint32_t q = p0 + wave_slot(v, g, cur, true);
+      if (v) {
+        skeys[q] = k[r];
+        spj[q] = j[r];
+        pos_of[j[r]] = q;
+      }
     }
   }
 }
