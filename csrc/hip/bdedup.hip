@@ -1392,7 +1392,8 @@ __global__ __launch_bounds__(1024) void k_bd_reduce_fm_sorted(
 // grouped record layout: the per-bucket regroup after the scatter (defined
 // with the record-exchange kernels below)
 static constexpr int kRgT = 512;
-__global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__ bstart,
+__global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__ rstart,
+                                                    const uint32_t* __restrict__ rnum,
                                                     const uint64_t* __restrict__ gkeys,
                                                     const uint32_t* __restrict__ gspj,
                                                     uint64_t* __restrict__ skeys,
@@ -1561,8 +1562,8 @@ int launch_bd_dedup(const uint64_t* keys, long long n, RouteSpec rs, long long u
 #undef SS_BD_CT_DISPATCH2
   check_launch("k_bd_scatter");
   if (grouped) {
-    hipLaunchKernelGGL(k_rec_group, dim3(L.P), dim3(kRgT), 0, st, S + L.bstart, gkeys, gspj, ukeys,
-                       spj, pos_of, usub, msub, L.Pd, rs.rbits);
+    hipLaunchKernelGGL(k_rec_group, dim3(L.P), dim3(kRgT), 0, st, S + L.ubase, S + L.unum, gkeys,
+                       gspj, ukeys, spj, pos_of, usub, msub, L.Pd, rs.rbits);
     check_launch("k_rec_group");
   }
   if (spj) return rs.rbits;  // record exchange: the servers dedup
@@ -1607,14 +1608,15 @@ __device__ __forceinline__ void rec_ranges(const unsigned long long* __restrict_
   __syncthreads();
 }
 // grouped record layout (kBdRecGroup, N>1 with server sub-buckets): one
-// workgroup per bucket b moves its run [bstart[b], bstart[b+1]) from the
+// workgroup per bucket b moves its run [ubase[b], ubase[b] + unum[b]) from the
 // scatter's staging (gkeys, gspj: the same send-segment positions) into the
 // send segment grouped by the server's sub-bucket — the split the unique
 // dedup makes of its keys (region-based with region buckets, so a server
 // sub-bucket is whole regions and its pull can claim) — writing the groups'
 // offsets into usub and every record's final position into pos_of (the
 // scatter wrote the staging positions, and kBdInvalid for empty keys, first)
-__global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__ bstart,
+__global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__ rstart,
+                                                    const uint32_t* __restrict__ rnum,
                                                     const uint64_t* __restrict__ gkeys,
                                                     const uint32_t* __restrict__ gspj,
                                                     uint64_t* __restrict__ skeys,
@@ -1625,7 +1627,11 @@ __global__ __launch_bounds__(kRgT) void k_rec_group(const uint32_t* __restrict__
   __shared__ unsigned int cnt[kBdMaxSub];
   __shared__ unsigned int cur[kBdMaxSub];
   const int t = threadIdx.x, b = blockIdx.x;
-  const uint32_t p0 = bstart[b], p1 = bstart[b + 1];
+  // the bucket's run from the run tables the column scan wrote: in the
+  // gapped record layout bstart[b + 1] of a destination's last bucket is the
+  // next destination's first, d * gap away — past the run, into staging the
+  // scatter never wrote
+  const uint32_t p0 = rstart[b], p1 = p0 + rnum[b];
   if (t < msub) cnt[t] = 0u;
   __syncthreads();
   auto sub_of = [&](uint64_t v) -> uint32_t {

@@ -146,6 +146,10 @@ def _ref():
     ("sync", {"SS_PULL_AHEAD": "0", "SS_TEST_XCHG": "records"}, 0.005),
     ("staleness2", {"SS_PULL_AHEAD": "1", "SS_STALENESS": "2", "SS_TEST_XCHG": "records"},
      0.01),
+    # grouped records: 3 server sub-buckets forced at this small shape, so
+    # every source bucket's records are grouped by them after the scatter
+    # (bdedup.hip k_rec_group) and the servers read exact ranges
+    ("sync", {"SS_PULL_AHEAD": "0", "SS_TEST_XCHG": "records", "SS_SRV_SUB": "3"}, 0.005),
 ])
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_eval_matches_world1(world, mode, env, bound):
