@@ -200,11 +200,15 @@ class PSEngine(HostRounds, DeviceSetup, EngineControl):
         self.tracer = Tracer(enabled=False)
         fm = torch.from_numpy(self.frag_map.astype(np.int32))
         dd_cls = Deduper if self.gpu else CpuDeduper
-        # N>1 records: the unique layout's source buckets, grouped by the
-        # servers' sub-bucket after the scatter (SS_REC_GROUP=0: the small
-        # record buckets of round 5, 3584 / N records, no sub-buckets)
+        # N>1 records, SS_REC_GROUP=1: the unique layout's source buckets,
+        # each bucket's records grouped by the servers' sub-bucket after the
+        # scatter (bdedup.hip k_rec_group).  Measured slower than the small
+        # record buckets (3584 / N records, no sub-buckets; default): 2 ranks
+        # on one GPU 2.18 vs 1.75 ms, 4 ranks 4.54 vs 3.96, 8 ranks 8.83 vs
+        # 8.86 (profiles/raw/r6_rec_group_ab.txt) — the regroup's per-record
+        # pos_of stores land in random order
         self.rec_group = bool(self.records and self.world > 1 and
-                              os.environ.get("SS_REC_GROUP", "1") != "0")
+                              os.environ.get("SS_REC_GROUP", "0") == "1")
         rl = {"record_layout": True, "record_group": self.rec_group} if self.records else {}
         self.dedupers = [dd_cls(self.max_keys, nranks=self.world, frag_map=fm, gdim=self.dim,
                                 device=self.device, zero_grad=zero_grad, **rl)

@@ -94,10 +94,10 @@ KNOBS: dict[str, Knob] = {
                     "dedup and merge (less kernel work per rank at N <= 2, twice the link "
                     "bytes); auto (bench.py) = both timed on the live world after the "
                     "warm-up, the faster kept (the launcher runs unique)"),
-    "SS_REC_GROUP": Knob("1", "parallel/engine.py", "tuning",
-                         "N>1 record exchange: the unique layout's source buckets with each "
-                         "bucket's records grouped by the servers' sub-bucket (0: round 5's "
-                         "3584 / N records per source bucket, no sub-buckets)"),
+    "SS_REC_GROUP": Knob("0", "parallel/engine.py", "tuning",
+                         "1: N>1 record exchange with the unique layout's source buckets, each "
+                         "bucket's records grouped by the servers' sub-bucket (measured slower "
+                         "than the default 3584 / N records per source bucket at 2 and 4 ranks)"),
     "SS_BD_DBG": Knob("0", "csrc/hip/bdedup.hip", "debug",
                       "measurement only, wrong results: k_bd_reduce bits 1 = plain LDS stores, "
                       "2 = no gradient gather, 4 = no table stores, 8 = atomics for single keys"),

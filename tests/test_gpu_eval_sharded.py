@@ -149,7 +149,8 @@ def _ref():
     # grouped records: 3 server sub-buckets forced at this small shape, so
     # every source bucket's records are grouped by them after the scatter
     # (bdedup.hip k_rec_group) and the servers read exact ranges
-    ("sync", {"SS_PULL_AHEAD": "0", "SS_TEST_XCHG": "records", "SS_SRV_SUB": "3"}, 0.005),
+    ("sync", {"SS_PULL_AHEAD": "0", "SS_TEST_XCHG": "records", "SS_REC_GROUP": "1",
+              "SS_SRV_SUB": "3"}, 0.005),
 ])
 @pytest.mark.parametrize("world", [2, 4])
 def test_sharded_eval_matches_world1(world, mode, env, bound):
