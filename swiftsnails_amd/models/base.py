@@ -14,11 +14,14 @@ from __future__ import annotations
 
 import collections
 import gc
+import logging
 import os
 import time
 from typing import Optional
 
 import torch
+
+log = logging.getLogger(__name__)
 
 
 class _GraphSet(list):
@@ -146,6 +149,19 @@ class PipelinedWorker:
                 # a quota decides per step on the host whether to route keys
                 or self.quota is not None
                 or os.environ.get("SS_GRAPH", "1") == "0"):
+            return False
+        # more than 4 ranks on one GPU: replays ran every round at ~21.4 ms
+        # (word2vec config 3, 8 processes colocated or split 4 + 4, one step
+        # or 16 per graph; eager 0.86-1.12 ms, 4 processes replay faster than
+        # eager: profiles/raw/r6_config3_split_roles.txt).  The constant
+        # 21.4 ms looks like a scheduler time slice: likely more processes'
+        # queues than the hardware keeps mapped, a replay's mailbox wait
+        # spinning until the peer's queue is mapped again (not profiled)
+        xg = getattr(eng, "xg", None)
+        if (xg is not None and eng.shared_device
+                and eng.world / max(1, getattr(xg, "devices", 1)) > 4
+                and os.environ.get("SS_GRAPH", "1") != "force"):
+            log.warning("hipGraph replay off: %d ranks share one GPU (eager rounds)", eng.world)
             return False
         if self._graphs is not None:
             return True

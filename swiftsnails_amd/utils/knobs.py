@@ -42,7 +42,8 @@ KNOBS: dict[str, Knob] = {
                         "measures both)"),
     "SS_GRAPH": Knob("1", "models/base.py", "ops",
                      "0: enable_graph() declines (replay is requested by config `graph` or "
-                     "bench --graph)"),
+                     "bench --graph); force: replay even with more than 4 ranks on one GPU "
+                     "(declined by default: ~21 ms per round measured)"),
     # -- build
     "SS_OFFLOAD_ARCH": Knob("gfx950", "_build.py", "build", "HIP offload target"),
     "SS_NO_AUTOBUILD": Knob("0", "_native.py", "build",

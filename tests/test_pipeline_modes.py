@@ -144,3 +144,31 @@ def test_pull_ahead_switches_mid_run_gloo(staleness):
     assert set(pulled) == set(ref_pulled)
     for key, v in ref_pulled.items():
         np.testing.assert_allclose(pulled[key], v, rtol=2e-5, atol=2e-6)
+
+
+def test_graph_declined_with_more_than_four_ranks_per_gpu(monkeypatch):
+    """enable_graph() keeps eager rounds when more than 4 ranks of an xGMI
+    job share one GPU (replays ran every round at ~21 ms there,
+    profiles/raw/r6_config3_split_roles.txt); SS_GRAPH=force overrides; ranks
+    on devices of their own are not affected."""
+    from types import SimpleNamespace
+
+    from swiftsnails_amd.models.base import PipelinedWorker
+
+    def worker(world, devices):
+        eng = SimpleNamespace(gpu=True, fast1=False, xg=SimpleNamespace(devices=devices),
+                              world=world, table=None, shared_device=devices < world)
+        w = object.__new__(PipelinedWorker)
+        w.engine, w.quota = eng, None
+        w.data = SimpleNamespace(graph_capturable=True)
+        w._graphs = ["captured"]  # past the guard, enable_graph returns True here
+        return w
+
+    monkeypatch.delenv("SS_GRAPH", raising=False)
+    assert not worker(8, 1).enable_graph()
+    assert not worker(5, 1).enable_graph()
+    assert worker(4, 1).enable_graph()
+    assert worker(8, 8).enable_graph()
+    assert worker(8, 2).enable_graph()  # 4 ranks per device
+    monkeypatch.setenv("SS_GRAPH", "force")
+    assert worker(8, 1).enable_graph()
