@@ -52,6 +52,7 @@
 // turn into an exception at the engine's check points.
 #include <algorithm>
 #include <cstdlib>
+#include <cstdio>
 #include <string>
 
 #include "bdindex.h"
@@ -1008,7 +1009,11 @@ static int bd_rt() {
 static int bd_dbg() {
   static const int v = [] {
     const char* e = std::getenv("SS_BD_DBG");
-    return e ? std::atoi(e) : 0;
+    const int d = e ? std::atoi(e) : 0;
+    if (d)
+      std::fprintf(stderr, "swiftsnails_amd: SS_BD_DBG=%d — k_bd_reduce runs a timing-only "
+                           "variant, training results are WRONG\n", d);
+    return d;
   }();
   return v;
 }
